@@ -1,0 +1,324 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident RX checksum + RSS throughput on MI355X.
+
+Metric (BASELINE.json): "Mpkt/s + GB/s device-resident RX checksum+RSS, 1518B
+batch; % HBM roofline".  Workload = BASELINE configs[1] (C2): 1 M x 1518 B
+Eth/IPv4/TCP frames per GPU (1 % corrupted), checksum verify + RSS with the
+40-B Microsoft key and a 128-entry 4-queue table (i % 4), tuple = parsed
+IPv4 4-tuple.  One step = one fused nicgpu_rx_offload launch over the whole
+resident batch.
+
+Multi-GPU (torchrun): one rank per GPU, each with its own 1 M-packet batch
+(weak scaling); the RSS key and table are RCCL-broadcast from rank 0 once
+before timing; no collective in the timed loop.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §5 for the roofline terms.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MS_KEY = bytes.fromhex("6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c6a42b73bbeac01fa")
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+PKT_LEN = 1518
+N_PER_GPU = 1 << 20
+DESC_BYTES = 8
+RESULT_BYTES = 8  # u16 csum + u16 queue + u32 hash
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(frames, desc, table, gpu_out, n_sample_mt, n_sample_1):
+    """Reference C++ path (oracle/_ref/libref.so: the reference's own
+    src/checksum.cpp + src/rss.cpp, compiled in the build container) or, if it
+    is absent, the oracle restatement, timed on this host's cores.  Also checks
+    the GPU outputs bit-exactly on the sample."""
+    import ctypes
+
+    from oracle import pyoracle as po
+
+    ref = po.ref_lib()
+    kind = "reference" if ref is not None else "port"
+    cores = min(16, os.cpu_count() or 1)
+    k = np.frombuffer(MS_KEY, np.uint8)
+    t = np.ascontiguousarray(table.astype(np.uint16))
+
+    def run(n, threads):
+        cs = np.zeros(n, np.uint16)
+        q = np.zeros(n, np.uint16)
+        d = np.ascontiguousarray(desc[:n])
+        t0 = time.perf_counter()
+        if ref is not None:
+            ref.ref_rx_batch(frames.ctypes.data, d.ctypes.data, n, 1, k.ctypes.data, k.size,
+                             t.ctypes.data, t.size, cs.ctypes.data, q.ctypes.data, threads)
+        else:
+            # the restatement is single-threaded; time it on one core
+            csum, _, qq, _, _ = po.rx_batch(frames, d, MS_KEY, t)
+            cs[:], q[:] = csum, qq
+        return time.perf_counter() - t0, cs, q
+
+    dt1, cs1, q1 = run(n_sample_1, 1)
+    if ref is not None:
+        dtm, csm, qm = run(n_sample_mt, cores)
+    else:
+        dtm, csm, qm, cores = dt1, cs1, q1, 1
+        n_sample_mt = n_sample_1
+    g_cs, g_q = gpu_out
+    ok = bool(np.array_equal(csm, g_cs[:n_sample_mt]) and np.array_equal(qm, g_q[:n_sample_mt])
+              and np.array_equal(cs1, g_cs[:n_sample_1]) and np.array_equal(q1, g_q[:n_sample_1]))
+    return {
+        "value": round(n_sample_mt / dtm / 1e6, 4),
+        "unit": "Mpkt/s",
+        "cores": cores,
+        "kind": kind,
+        "sample": f"first {n_sample_mt} of the C2 batch (1518 B TCP) on {cores} threads, one RssEngine per thread; "
+                  f"1 core: {round(n_sample_1 / dt1 / 1e6, 4)} Mpkt/s over {n_sample_1} packets",
+        "value_1core": round(n_sample_1 / dt1 / 1e6, 4),
+        "gbs": round(n_sample_mt * PKT_LEN / dtm / 1e9, 4),
+        "gpu_matches_cpu_on_sample": ok,
+        "cpu_model": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def load_traffic(path):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (see
+    profiles/README.md), or None."""
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--packets", type=int, default=N_PER_GPU, help="packets per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_c2.json"))
+    args = ap.parse_args()
+
+    import torch
+
+    import smart_nic_amd as sna
+    from smart_nic_amd import pktgen
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    n = args.packets
+    t0 = time.time()
+    frames, desc, corrupted = pktgen.make_batch(np.full(n, PKT_LEN), seed=42 + rank, proto=6, corrupt_frac=0.01)
+    log(f"[rank {rank}] generated {n} x {PKT_LEN} B in {time.time() - t0:.1f}s")
+    table = (np.arange(128) % 4).astype(np.uint16)
+
+    f_dev = torch.from_numpy(frames).to(dev)
+    d_dev = torch.from_numpy(desc.view(np.int64)).to(dev)
+    cs = torch.empty(n, dtype=torch.int16, device=dev)
+    hs = torch.empty(n, dtype=torch.int32, device=dev)
+    qs = torch.empty(n, dtype=torch.int16, device=dev)
+    hits = torch.zeros(128, dtype=torch.int64, device=dev)
+
+    # RSS key + table: rank 0's copy, RCCL-broadcast over xGMI to every rank.
+    key_dev = torch.tensor(list(MS_KEY), dtype=torch.uint8, device=dev)
+    tab_dev = torch.from_numpy(table.view(np.int16)).to(dev)
+    if dist is not None:
+        if rank != 0:
+            key_dev.zero_()
+            tab_dev.zero_()
+        dist.broadcast(key_dev, src=0)
+        dist.broadcast(tab_dev, src=0)
+    ctx = sna.RssContext(dev)
+    ctx.set_key_device(key_dev)
+    ctx.set_table_device(tab_dev)
+    torch.cuda.synchronize()
+
+    def step():
+        sna.rx_offload(ctx, f_dev, d_dev, sna.TUPLE_AUTO, 0, 0, cs, hs, qs, hits)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # per-launch HIP events on the launch stream (torch's current stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record()
+        step()
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t_wall = time.perf_counter() - t_start
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_avg_s = float(np.mean(kern_ms)) / 1e3
+    kern_med_s = float(np.median(kern_ms)) / 1e3
+
+    t_max = t_wall
+    if dist is not None:
+        tt = torch.tensor([t_wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+
+    # correctness of this run (cheap properties on every rank)
+    g_cs = cs.cpu().numpy().view(np.uint16)
+    g_h = hs.cpu().numpy().view(np.uint32)
+    g_q = qs.cpu().numpy().view(np.uint16)
+    status_ok = bool(np.array_equal(g_cs != 0, corrupted))
+    queue_ok = bool(np.array_equal(g_q, table[g_h % 128]))
+
+    total_pkts = n * world * args.steps
+    value = total_pkts / t_max / 1e6
+    alg_bytes = n * (PKT_LEN + DESC_BYTES + RESULT_BYTES)
+    achieved_gbs = alg_bytes / kern_avg_s / 1e9
+    frame_gbs = n * PKT_LEN / kern_avg_s / 1e9
+
+    out = None
+    if rank == 0:
+        traffic = load_traffic(args.traffic_json)
+        out = {
+            "metric": "Mpkt/s + GB/s device-resident RX checksum+RSS, 1518B batch; % HBM roofline",
+            "value": round(value, 3),
+            "unit": "Mpkt/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded Eth/IPv4/TCP frames, valid IPv4+TCP checksums, whole-frame balancing word, 1% corrupted)",
+            "config": {
+                "workload": "C2: 1M x 1518 B TCP per GPU, checksum verify + RSS (MS 40-B key, 128-entry table i%4, IPv4 4-tuple)",
+                "packets_per_gpu": n,
+                "packet_bytes": PKT_LEN,
+                "parallelism": f"replicas x{world} (packet shards, key/table RCCL broadcast)",
+            },
+            "gbs_frames": round(frame_gbs * world, 2),
+            "gbs_frames_per_gpu": round(frame_gbs, 2),
+            "kernel_us_avg": round(kern_avg_s * 1e6, 2),
+            "kernel_us_median": round(kern_med_s * 1e6, 2),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved_gbs, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "alg_bytes_per_launch": alg_bytes,
+            },
+            "checks": {"status_matches_corruption": status_ok, "queue_is_table_of_hash": queue_ok},
+        }
+    # end-to-end (host pinned -> H2D -> kernel -> D2H of results), rank 0 only
+    if rank == 0 and not args.no_e2e:
+        try:
+            out["e2e"] = e2e_rate(torch, sna, ctx, frames, desc, dev)
+        except Exception as e:  # report, never hide
+            out["e2e"] = {"error": repr(e)}
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(frames, desc, table, (g_cs, g_q),
+                                           n_sample_mt=min(n, 1 << 18), n_sample_1=min(n, 1 << 16))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def e2e_rate(torch, sna, ctx, frames, desc, dev, chunk_pkts=1 << 16, reps=3):
+    """Packets from pinned host memory through H2D copy, the kernel and D2H of
+    the results, chunked and double-buffered over two streams."""
+    n = desc.size
+    h_frames = torch.from_numpy(frames).pin_memory()
+    slot = PKT_LEN + (-PKT_LEN) % 16
+    nch = (n + chunk_pkts - 1) // chunk_pkts
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    bufs = []
+    for s in range(2):
+        bufs.append({
+            "f": torch.empty(chunk_pkts * slot + 64, dtype=torch.uint8, device=dev),
+            "d": torch.empty(chunk_pkts, dtype=torch.int64, device=dev),
+            "cs": torch.empty(chunk_pkts, dtype=torch.int16, device=dev),
+            "q": torch.empty(chunk_pkts, dtype=torch.int16, device=dev),
+            "h": torch.empty(chunk_pkts, dtype=torch.int32, device=dev),
+        })
+    # per-chunk descriptors rebased to the chunk buffer
+    d_local = desc.copy()
+    offs = (desc & np.uint64((1 << 40) - 1)).astype(np.int64)
+    h_desc = []
+    for c in range(nch):
+        a, b = c * chunk_pkts, min(n, (c + 1) * chunk_pkts)
+        base = offs[a]
+        dd = d_local[a:b] - np.uint64(base)
+        h_desc.append(torch.from_numpy(dd.view(np.int64)).pin_memory())
+    h_cs = torch.empty(n, dtype=torch.int16).pin_memory()
+    h_q = torch.empty(n, dtype=torch.int16).pin_memory()
+    h_h = torch.empty(n, dtype=torch.int32).pin_memory()
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for c in range(nch):
+            s = streams[c % 2]
+            B = bufs[c % 2]
+            a, b = c * chunk_pkts, min(n, (c + 1) * chunk_pkts)
+            fa, fb = int(offs[a]), int(offs[b - 1]) + slot
+            with torch.cuda.stream(s):
+                B["f"][: fb - fa].copy_(h_frames[fa:fb], non_blocking=True)
+                B["d"][: b - a].copy_(h_desc[c], non_blocking=True)
+                sna.rx_offload(ctx, B["f"], B["d"][: b - a], sna.TUPLE_AUTO, 0, 0,
+                               B["cs"], B["h"], B["q"], None, stream=s)
+                h_cs[a:b].copy_(B["cs"][: b - a], non_blocking=True)
+                h_q[a:b].copy_(B["q"][: b - a], non_blocking=True)
+                h_h[a:b].copy_(B["h"][: b - a], non_blocking=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return {"mpkts": round(n / best / 1e6, 2), "gbs_frames": round(n * PKT_LEN / best / 1e9, 2),
+            "chunk_packets": chunk_pkts, "streams": 2,
+            "note": "pinned host frames -> H2D -> kernel -> D2H(csum,queue,hash); PCIe-bound"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,130 @@
+/*
+ * nicgpu.h — C-ABI of the MI355X (gfx950) RX offload layer.
+ *
+ * This is the drop-in boundary under the nic:: C++20 API (include/nic/).
+ * Plain C: no HIP, torch or C++ types; device pointers are caller-owned; every
+ * launch takes an explicit stream (a hipStream_t passed as void*, NULL = the
+ * null stream) and is asynchronous; every entry point returns an int status
+ * (0 = ok, < 0 = error, see nicgpu_strerror).  Nothing here falls back to the
+ * CPU: a missing GPU or a HIP failure is an error.
+ *
+ * Reference interfaces replaced (file:line in rosslwheeler/smart_nic):
+ *   nicgpu_checksum_batch   <- nic::compute_checksum, include/nic/checksum.h:9,
+ *                              src/checksum.cpp:10-34 (one call per packet today)
+ *   nicgpu_rx_offload       <- the RX verify in QueuePair::handle_rx_segment,
+ *                              src/queue_pair.cpp:434-447, fused with
+ *                              nic::RssEngine::select_queue, include/nic/rss.h:35,
+ *                              src/rss.cpp:49-61 (+ RssStats, rss.h:18-21)
+ *   nicgpu_rss_set_key      <- nic::RssEngine::set_key, rss.h:29, rss.cpp:27-33
+ *   nicgpu_rss_set_table    <- nic::RssEngine::set_table, rss.h:30, rss.cpp:35-41
+ *   nicgpu_tso_checksum     <- QueuePair::build_segments + per-segment RX verify,
+ *                              src/queue_pair.cpp:212-278, 434-447
+ *
+ * Batch layout in HBM:
+ *   frames : byte buffer, 16-B aligned base.  Reads are 16-B granular: the
+ *            allocation must cover every 16-B chunk that holds a packet byte.
+ *   desc   : one uint64 per packet = offset (bits 0..39, any byte alignment)
+ *            | length (bits 40..63, must be <= NICGPU_MAX_PACKET; longer
+ *            descriptors give unspecified results).  NICGPU_DESC(off,len).
+ *   outputs: structure-of-arrays, any of them may be NULL.
+ */
+#ifndef NICGPU_H
+#define NICGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NICGPU_ABI_VERSION 1
+
+#define NICGPU_OK 0
+#define NICGPU_ERR_INVALID (-1)    /* bad argument (null ctx, bad mode, size limits) */
+#define NICGPU_ERR_HIP (-2)        /* a HIP runtime call failed */
+#define NICGPU_ERR_NO_DEVICE (-3)  /* no gfx950 device visible */
+#define NICGPU_ERR_NOMEM (-4)
+
+#define NICGPU_DESC_OFFSET_BITS 40
+/* Longest packet the kernels accept: 64 KiB - 1 (the TSO super-frame limit of
+ * an IPv4 total length).  Per-packet 32-bit partial sums stay exact below it. */
+#define NICGPU_MAX_PACKET 65535u
+#define NICGPU_DESC(off, len) \
+  ((uint64_t) (off) | ((uint64_t) (len) << NICGPU_DESC_OFFSET_BITS))
+
+/* Hash-input (tuple) selection — the reference has no parser; callers handed
+ * select_queue a 12-B src_ip|dst_ip|sport|dport string
+ * (tests/tutorial_lesson8_test.cpp:20-35).  AUTO parses Ethernet (+ up to two
+ * 0x8100/0x88A8 tags) -> IPv4 TCP/UDP 12 B, other IPv4 or fragments 8 B,
+ * IPv6 TCP/UDP 36 B, other IPv6 32 B, anything else 0 B (hash 0).
+ * RAW hashes frame bytes [raw_off, raw_off + raw_len) clipped to the frame,
+ * raw_off + raw_len <= NICGPU_RAW_MAX_END. */
+#define NICGPU_TUPLE_NONE 0
+#define NICGPU_TUPLE_AUTO 1
+#define NICGPU_TUPLE_RAW 2
+#define NICGPU_RAW_MAX_END 64
+#define NICGPU_MAX_TUPLE 64
+#define NICGPU_MAX_KEY 256    /* key bytes */
+#define NICGPU_MAX_TABLE 65536
+
+/* Library identity / device probe. */
+int nicgpu_abi_version(void);
+const char* nicgpu_strerror(int status);
+/* Number of visible gfx950 devices (>= 0) or a negative status. */
+int nicgpu_device_count(void);
+
+/* RSS context: the uploaded Toeplitz key (as a nibble lookup table of 32-bit
+ * key windows, built on the device) and indirection table, on one device.
+ * One context per stream/thread; contexts are not internally locked. */
+typedef struct nicgpu_rss_ctx nicgpu_rss_ctx;
+
+int nicgpu_rss_create(nicgpu_rss_ctx** out, int device);
+int nicgpu_rss_destroy(nicgpu_rss_ctx* ctx);
+
+/* Key bytes from host memory; len 0 selects the reference's 20-byte default
+ * key (src/rss.cpp:10-13, 27-33).  Enqueued on `stream`. */
+int nicgpu_rss_set_key(nicgpu_rss_ctx* ctx, const uint8_t* key, size_t len, void* stream);
+/* Key bytes already in device memory (e.g. after an RCCL broadcast). */
+int nicgpu_rss_set_key_device(nicgpu_rss_ctx* ctx, const uint8_t* key_dev, size_t len,
+                              void* stream);
+/* Indirection table; n 0 selects 128 zeros (src/rss.cpp:35-41). */
+int nicgpu_rss_set_table(nicgpu_rss_ctx* ctx, const uint16_t* table, size_t n, void* stream);
+int nicgpu_rss_set_table_device(nicgpu_rss_ctx* ctx, const uint16_t* table_dev, size_t n,
+                                void* stream);
+/* Current sizes (host-side mirror, no device sync). */
+int nicgpu_rss_info(const nicgpu_rss_ctx* ctx, size_t* key_len, size_t* table_n);
+
+/* Fused RX offload over a batch:
+ *   out_csum[i]  = compute_checksum(frame i)                 (u16)
+ *   out_hash[i]  = toeplitz(key, tuple(frame i))             (u32)
+ *   out_queue[i] = table[out_hash[i] % table_n]              (u16)
+ *   out_hits[j] += #packets with out_hash % table_n == j     (u64[table_n], accumulated)
+ * With tuple_mode NONE only out_csum is produced (ctx may be NULL).
+ * RX status per queue_pair.cpp:437-438 is (out_csum[i] == 0). */
+int nicgpu_rx_offload(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc,
+                      size_t n, int tuple_mode, uint32_t raw_off, uint32_t raw_len,
+                      uint16_t* out_csum, uint32_t* out_hash, uint16_t* out_queue,
+                      uint64_t* out_hits, void* stream);
+
+/* Checksum only (== rx_offload with NICGPU_TUPLE_NONE). */
+int nicgpu_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n,
+                          uint16_t* out_csum, void* stream);
+
+/* Per-segment checksums of TSO/GSO segmentation without materialising the
+ * segments: for frame i (desc[i]) with header length hdr_len[i] and mss[i],
+ * segment k = frame[0:H] || frame[H + k*mss : min(L, H + (k+1)*mss)], and
+ * out_csum[seg_base[i] + k] = compute_checksum(segment k).  Frames that the
+ * reference would not segment (H >= L, or L <= mss) yield one checksum of the
+ * whole frame.  The caller validates MSS/segment-count limits
+ * (queue_pair.cpp:225-270) and sizes seg_base (exclusive prefix of segment
+ * counts).  mss must be >= 1 for segmented frames. */
+int nicgpu_tso_checksum(const uint8_t* frames, const uint64_t* desc, const uint16_t* hdr_len,
+                        const uint16_t* mss, const uint32_t* seg_base, size_t n,
+                        uint16_t* out_csum, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NICGPU_H */

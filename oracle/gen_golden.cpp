@@ -1,0 +1,676 @@
+// gen_golden.cpp — writes tests/golden/ from the COMPILED REFERENCE.
+//
+// TEST INFRASTRUCTURE ONLY.  Built by oracle/Makefile (target `golden`) in the
+// container where /root/reference exists: it links the reference's own
+// src/checksum.cpp, src/rss.cpp and the QueuePair pipeline sources by path
+// (nothing is copied into this repo) and records what they compute.  The
+// outputs are plain data (JSON + little-endian .bin arrays); the GPU box only
+// ever sees those files.
+//
+// Expected values come from:
+//   nic::compute_checksum           src/checksum.cpp:10-34
+//   nic::RssEngine::hash/select     src/rss.cpp:43-61 (+ stats, :45, :56-58)
+//   nic::QueuePair::process_once    src/queue_pair.cpp:67-460 (statuses, TSO)
+// The tuple fed to select_queue is extracted with oracle_extract_tuple (the
+// build's own parser definition — the reference has none).
+
+#include <cassert>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "nic/checksum.h"
+#include "nic/dma_engine.h"
+#include "nic/queue_pair.h"
+#include "nic/rss.h"
+#include "nic/simple_host_memory.h"
+#include "nic/tx_rx.h"
+#include "oracle.h"
+
+using namespace nic;
+
+namespace {
+
+std::string g_out = "tests/golden";
+
+struct Rng {
+  std::uint64_t s;
+  std::uint64_t next() {  // splitmix64
+    std::uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  std::uint32_t u32() { return static_cast<std::uint32_t>(next() >> 32); }
+  std::uint32_t below(std::uint32_t n) { return static_cast<std::uint32_t>((next() >> 32) % n); }
+  std::uint8_t byte() { return static_cast<std::uint8_t>(next() >> 56); }
+};
+
+std::uint16_t ref_csum(const std::uint8_t* p, std::size_t n) {
+  return nic::compute_checksum(std::span<const std::byte>(reinterpret_cast<const std::byte*>(p), n));
+}
+
+std::string hex(const std::uint8_t* p, std::size_t n) {
+  static const char* d = "0123456789abcdef";
+  std::string s;
+  for (std::size_t i = 0; i < n; ++i) {
+    s += d[p[i] >> 4];
+    s += d[p[i] & 15];
+  }
+  return s;
+}
+
+template <class T>
+void write_bin(const std::string& name, const std::vector<T>& v) {
+  std::ofstream f(g_out + "/" + name, std::ios::binary);
+  f.write(reinterpret_cast<const char*>(v.data()), static_cast<std::streamsize>(v.size() * sizeof(T)));
+}
+
+template <class T>
+std::string json_arr(const std::vector<T>& v) {
+  std::ostringstream o;
+  o << "[";
+  for (std::size_t i = 0; i < v.size(); ++i) o << (i ? "," : "") << static_cast<std::uint64_t>(v[i]);
+  o << "]";
+  return o.str();
+}
+
+const std::vector<std::uint8_t> kMsKey = {
+    // tests/tutorial_lesson8_test.cpp:56-60 (the Microsoft RSS verification key)
+    0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
+    0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
+    0x80, 0x30, 0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa,
+};
+
+std::vector<std::uint8_t> default_key() {
+  std::vector<std::uint8_t> k(20);
+  oracle_default_key(k.data());
+  return k;
+}
+
+// ---------------------------------------------------------------- checksum --
+void gen_checksum() {
+  std::ostringstream js;
+  js << "{\n \"source\": \"nic::compute_checksum, src/checksum.cpp:10-34 (compiled reference)\",\n";
+  js << " \"cases\": [\n";
+  std::vector<std::vector<std::uint8_t>> cases = {
+      {},
+      {0xFF, 0xFF, 0xFF, 0xFF},  // tests/coverage_test.cpp:53-56 (asserts 0)
+      {0x01, 0x02, 0x03},        // coverage_test.cpp:60-62
+      {0xFF, 0xFF, 0xFF},        // coverage_test.cpp:64-66
+      {0xFF, 0xFF},              // tx_rx_test.cpp:855
+      {0x00, 0x00, 0x00, 0x00},
+      {0x00},
+      {0x80},
+      {0xFF},
+      {0x00, 0x01},
+      {0xFF, 0xFE},
+  };
+  // tests/tx_rx_test.cpp:103-110 make_payload(i & 0xFF) at the lengths the tests use.
+  for (std::size_t L : {1, 2, 3, 6, 8, 10, 12, 16, 63, 64, 65, 576, 1514, 1518, 9000, 9216}) {
+    std::vector<std::uint8_t> v(L);
+    for (std::size_t i = 0; i < L; ++i) v[i] = static_cast<std::uint8_t>(i & 0xFF);
+    cases.push_back(v);
+  }
+  // all-0xFF buffers: the sum is a multiple of 0xFFFF (checks the zero/0xFFFF corner)
+  for (std::size_t L : {2, 4, 6, 7, 130, 1518}) cases.emplace_back(L, 0xFF);
+  for (std::size_t i = 0; i < cases.size(); ++i) {
+    const auto& c = cases[i];
+    js << "  {\"hex\": \"" << hex(c.data(), c.size()) << "\", \"len\": " << c.size()
+       << ", \"csum\": " << ref_csum(c.data(), c.size()) << "}" << (i + 1 < cases.size() ? "," : "")
+       << "\n";
+  }
+  js << " ]\n}\n";
+  std::ofstream(g_out + "/checksum_kat.json") << js.str();
+
+  // Length/alignment sweep: every length 0..300, then random lengths up to 9216,
+  // placed at random (not only 16-B aligned) offsets with random gap bytes.
+  Rng r{1};
+  std::vector<std::uint8_t> frames;
+  std::vector<std::uint64_t> desc;
+  std::vector<std::uint16_t> csum;
+  std::vector<std::size_t> lens;
+  for (std::size_t L = 0; L <= 300; ++L) lens.push_back(L);
+  for (int i = 0; i < 64; ++i) lens.push_back(r.below(9217));
+  for (std::size_t L : {1518, 9000, 9216, 9215, 4095, 4096, 4097}) lens.push_back(L);
+  for (std::size_t L : lens) {
+    std::size_t gap = r.below(4) == 0 ? r.below(16) : (16 - frames.size() % 16) % 16;
+    for (std::size_t g = 0; g < gap; ++g) frames.push_back(r.byte());
+    std::uint64_t off = frames.size();
+    int pattern = static_cast<int>(r.below(4));
+    for (std::size_t i = 0; i < L; ++i) {
+      std::uint8_t b = pattern == 0 ? 0xFF : pattern == 1 ? static_cast<std::uint8_t>(i) : r.byte();
+      frames.push_back(b);
+    }
+    desc.push_back(off | (static_cast<std::uint64_t>(L) << 40));
+    csum.push_back(ref_csum(frames.data() + off, L));
+  }
+  for (int g = 0; g < 32; ++g) frames.push_back(r.byte());
+  while (frames.size() % 16) frames.push_back(0);
+  write_bin("checksum_sweep.frames.bin", frames);
+  write_bin("checksum_sweep.desc.bin", desc);
+  write_bin("checksum_sweep.csum.bin", csum);
+}
+
+// --------------------------------------------------------------------- RSS --
+struct RssCase {
+  std::vector<std::uint8_t> key;  // empty = engine default
+  std::vector<std::uint16_t> table;
+  std::vector<std::vector<std::uint8_t>> data;
+  std::string note;
+};
+
+std::vector<std::uint8_t> tuple12(std::uint32_t s, std::uint32_t d, std::uint16_t sp, std::uint16_t dp) {
+  return {static_cast<std::uint8_t>(s >> 24), static_cast<std::uint8_t>(s >> 16),
+          static_cast<std::uint8_t>(s >> 8),  static_cast<std::uint8_t>(s),
+          static_cast<std::uint8_t>(d >> 24), static_cast<std::uint8_t>(d >> 16),
+          static_cast<std::uint8_t>(d >> 8),  static_cast<std::uint8_t>(d),
+          static_cast<std::uint8_t>(sp >> 8), static_cast<std::uint8_t>(sp),
+          static_cast<std::uint8_t>(dp >> 8), static_cast<std::uint8_t>(dp)};
+}
+
+std::uint32_t ip(int a, int b, int c, int d) {
+  return (static_cast<std::uint32_t>(a) << 24) | (static_cast<std::uint32_t>(b) << 16) |
+         (static_cast<std::uint32_t>(c) << 8) | static_cast<std::uint32_t>(d);
+}
+
+void gen_rss() {
+  std::vector<RssCase> cases;
+  // tests/queue_manager_rss_test.cpp:263-285 / :287-313 / :34-50 (default 20-B key)
+  cases.push_back({{}, {0, 1, 2, 3}, {{0xAA, 0xBB, 0xCC, 0xDD}, {0x10, 0x20, 0x30, 0x40}, {0x01, 0x00, 0x00, 0x01}}, "queue_manager_rss_test.cpp:263-285"});
+  cases.push_back({{}, {0, 1}, {{0x00, 0x00, 0x00, 0x01}, {0xFF, 0xEE, 0xDD, 0xCC}, {0x12, 0x34, 0x56, 0x78}}, "queue_manager_rss_test.cpp:287-313"});
+  cases.push_back({{}, {2, 2, 2, 2}, {{0x01, 0x02, 0x03, 0x04}}, "queue_manager_rss_test.cpp:34-50"});
+  cases.push_back({{}, {}, {{}}, "queue_manager_rss_test.cpp:315-330 (empty data, default table)"});
+  // tests/tutorial_lesson8_test.cpp:94-160 (MS key, 8-entry table)
+  cases.push_back({kMsKey, {0, 1, 2, 3, 0, 1, 2, 3},
+                   {tuple12(0xC0A80164, 0xC0A80101, 8080, 80), tuple12(0xC0A80101, 0xC0A80164, 80, 8080)},
+                   "tutorial_lesson8_test.cpp:94-160"});
+  // docs/users_guide.md:2000-2020 (key = forty 0x6D)
+  cases.push_back({std::vector<std::uint8_t>(40, 0x6D), {0, 1, 2, 3},
+                   {tuple12(0xC0A80164, 0xC0A80101, 8080, 80)}, "users_guide.md:2000-2020"});
+  // Microsoft RSS verification suite, IPv4 rows (TCP 12-B tuple and IP-only 8-B tuple)
+  {
+    RssCase c{kMsKey, {0, 1, 2, 3}, {}, "Microsoft RSS verification suite (IPv4)"};
+    struct Row { std::uint32_t s, d; std::uint16_t sp, dp; };
+    Row rows[] = {{ip(66, 9, 149, 187), ip(161, 142, 100, 80), 2794, 1766},
+                  {ip(199, 92, 111, 2), ip(65, 69, 140, 83), 14230, 4739},
+                  {ip(24, 19, 198, 95), ip(12, 22, 207, 184), 12898, 38024},
+                  {ip(38, 27, 205, 30), ip(209, 142, 163, 6), 48228, 2217},
+                  {ip(153, 39, 163, 191), ip(202, 188, 127, 2), 44251, 1303}};
+    for (auto& w : rows) {
+      auto t = tuple12(w.s, w.d, w.sp, w.dp);
+      c.data.push_back(t);
+      c.data.emplace_back(t.begin(), t.begin() + 8);
+    }
+    cases.push_back(c);
+  }
+  // Key-wrap: 36-B inputs i*7+1 against the 20-B default key (wraps) and the MS key.
+  {
+    std::vector<std::uint8_t> d(36);
+    for (int i = 0; i < 36; ++i) d[i] = static_cast<std::uint8_t>(i * 7 + 1);
+    cases.push_back({{}, {0, 1, 2}, {d}, "key wrap, default 20-B key"});
+    cases.push_back({kMsKey, {0, 1, 2}, {d}, "36-B input, MS key"});
+  }
+  // Random data of many lengths x several keys (incl. short keys: 1, 4, 5 B) and table sizes.
+  {
+    Rng r{7};
+    std::vector<std::vector<std::uint8_t>> keys = {{}, kMsKey, {0xA5}, {1, 2, 3, 4}, {9, 8, 7, 6, 5}, std::vector<std::uint8_t>(52, 0x3C)};
+    for (std::size_t ki = 0; ki < keys.size(); ++ki) {
+      std::vector<std::uint16_t> table(1 + r.below(300));
+      for (auto& e : table) e = static_cast<std::uint16_t>(r.below(65536));
+      RssCase c{keys[ki], table, {}, "random data"};
+      for (int j = 0; j < 40; ++j) {
+        std::vector<std::uint8_t> d(r.below(65));
+        for (auto& b : d) b = r.byte();
+        c.data.push_back(d);
+      }
+      cases.push_back(c);
+    }
+  }
+
+  std::ostringstream js;
+  js << "{\n \"source\": \"nic::RssEngine::hash/select_queue/stats, src/rss.cpp:17-114 (compiled reference)\",\n";
+  js << " \"default_key\": \"" << hex(default_key().data(), 20) << "\",\n \"cases\": [\n";
+  for (std::size_t ci = 0; ci < cases.size(); ++ci) {
+    auto& c = cases[ci];
+    RssConfig cfg;
+    cfg.key = c.key;
+    cfg.table = c.table;
+    RssEngine eng{cfg};  // ctor applies ensure_defaults (rss.cpp:22-25, 96-108)
+    std::vector<std::uint32_t> hashes;
+    std::vector<std::uint16_t> queues;
+    std::vector<std::uint32_t> tidx;
+    for (auto& d : c.data) {
+      std::uint32_t h = eng.hash(std::span<const std::uint8_t>(d));
+      auto q = eng.select_queue(std::span<const std::uint8_t>(d));
+      hashes.push_back(h);
+      queues.push_back(*q);
+      tidx.push_back(static_cast<std::uint32_t>(h % eng.config().table.size()));
+    }
+    js << "  {\"note\": \"" << c.note << "\", \"key\": \"" << hex(eng.config().key.data(), eng.config().key.size())
+       << "\", \"table\": " << json_arr(eng.config().table) << ",\n   \"data\": [";
+    for (std::size_t j = 0; j < c.data.size(); ++j) js << (j ? "," : "") << "\"" << hex(c.data[j].data(), c.data[j].size()) << "\"";
+    js << "],\n   \"hash\": " << json_arr(hashes) << ", \"queue\": " << json_arr(queues)
+       << ", \"tidx\": " << json_arr(tidx) << ",\n   \"stats_hashes\": " << eng.stats().hashes
+       << ", \"stats_queue_hits\": " << json_arr(eng.stats().queue_hits) << "}"
+       << (ci + 1 < cases.size() ? "," : "") << "\n";
+  }
+  js << " ]\n}\n";
+  std::ofstream(g_out + "/rss_kat.json") << js.str();
+
+  // queue_hits guard (rss.cpp:56-58): set_table to a larger table after construction.
+  {
+    RssEngine eng;  // default: 128-entry table, queue_hits sized 128
+    std::vector<std::uint16_t> big(200);
+    for (std::size_t i = 0; i < big.size(); ++i) big[i] = static_cast<std::uint16_t>(i % 5);
+    eng.set_table(big);
+    Rng r{11};
+    std::vector<std::uint32_t> tidx;
+    std::ostringstream data;
+    for (int j = 0; j < 64; ++j) {
+      std::vector<std::uint8_t> d(12);
+      for (auto& b : d) b = r.byte();
+      auto q = eng.select_queue(std::span<const std::uint8_t>(d));
+      (void) q;
+      tidx.push_back(eng.hash(std::span<const std::uint8_t>(d)) % 200);
+      data << (j ? "," : "") << "\"" << hex(d.data(), d.size()) << "\"";
+    }
+    std::ofstream(g_out + "/rss_hits_guard.json")
+        << "{\"note\": \"set_table(200) after default ctor; queue_hits stays 128 (rss.cpp:56-58,107)\",\n"
+        << " \"table\": " << json_arr(big) << ",\n \"data\": [" << data.str() << "],\n \"tidx\": " << json_arr(tidx)
+        << ",\n \"stats_hashes\": " << eng.stats().hashes << ", \"stats_queue_hits\": " << json_arr(eng.stats().queue_hits) << "}\n";
+  }
+}
+
+// ------------------------------------------------------------ frame builder --
+// Eth/IPv4/TCP|UDP and IPv6 frames laid out as src/packet_generator.cpp:46-166;
+// IPv4 header checksum and L4 pseudo-header checksums as :200-305, 342-360.
+std::uint16_t inet_sum_be(const std::uint8_t* p, std::size_t n, std::uint32_t sum = 0) {
+  for (std::size_t i = 0; i < n; i += 2) {
+    std::uint32_t w = static_cast<std::uint32_t>(p[i]) << 8;
+    if (i + 1 < n) w |= p[i + 1];
+    sum += w;
+  }
+  while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
+  return static_cast<std::uint16_t>(sum);
+}
+
+struct FrameSpec {
+  int l3 = 4;          // 4, 6 or 0 (ARP)
+  int proto = 6;       // 6 TCP, 17 UDP, other
+  int vlan_tags = 0;   // 0..2
+  int ihl = 5;
+  bool frag = false;
+  std::size_t total = 64;  // frame length (may truncate headers)
+  bool balance = true;     // adjust src-MAC bytes 10..11 so compute_checksum(frame) == 0
+};
+
+std::vector<std::uint8_t> build_frame(Rng& r, const FrameSpec& s) {
+  std::vector<std::uint8_t> f;
+  auto put16 = [&](unsigned v) { f.push_back(static_cast<std::uint8_t>(v >> 8)); f.push_back(static_cast<std::uint8_t>(v)); };
+  for (int i = 0; i < 12; ++i) f.push_back(r.byte());  // dst + src MAC
+  unsigned et = s.l3 == 4 ? 0x0800 : s.l3 == 6 ? 0x86DD : 0x0806;
+  if (s.vlan_tags == 2) { put16(0x88A8); put16(r.below(4096)); put16(0x8100); put16(r.below(4096)); }
+  if (s.vlan_tags == 1) { put16(0x8100); put16(r.below(4096)); }
+  put16(et);
+  std::size_t l3 = f.size();
+  std::size_t l4 = l3;
+  if (s.l3 == 4) {
+    f.push_back(static_cast<std::uint8_t>(0x40 | s.ihl));
+    f.push_back(0);
+    put16(0);  // total length, patched below
+    put16(r.below(65536));
+    put16(s.frag ? (r.below(2) ? 0x2000 : (0x4000 | (1 + r.below(100)))) : 0x4000);
+    f.push_back(64);
+    f.push_back(static_cast<std::uint8_t>(s.proto));
+    put16(0);
+    for (int i = 0; i < 8; ++i) f.push_back(r.byte());
+    for (int i = 20; i < s.ihl * 4; ++i) f.push_back(1);  // NOP options
+    l4 = f.size();
+  } else if (s.l3 == 6) {
+    f.push_back(0x60); f.push_back(0); put16(r.below(65536));
+    put16(0);  // payload length
+    f.push_back(static_cast<std::uint8_t>(s.proto));
+    f.push_back(64);
+    for (int i = 0; i < 32; ++i) f.push_back(r.byte());
+    l4 = f.size();
+  } else {
+    for (int i = 0; i < 28; ++i) f.push_back(r.byte());  // ARP body
+    l4 = f.size();
+  }
+  if (s.l3 != 0) {
+    put16(1024 + r.below(64512));
+    put16(1 + r.below(65535));
+    if (s.proto == 6) {
+      for (int i = 0; i < 8; ++i) f.push_back(r.byte());
+      f.push_back(0x50); f.push_back(0x18); put16(r.below(65536)); put16(0); put16(0);
+    } else if (s.proto == 17) {
+      put16(0); put16(0);
+    }
+  }
+  while (f.size() < s.total) f.push_back(r.byte());
+  f.resize(s.total);
+  // Patch lengths and checksums when the headers are complete.
+  if (s.l3 == 4 && f.size() >= l3 + 20) {
+    std::size_t iplen = f.size() - l3;
+    f[l3 + 2] = static_cast<std::uint8_t>(iplen >> 8); f[l3 + 3] = static_cast<std::uint8_t>(iplen);
+    if (f.size() >= l3 + static_cast<std::size_t>(s.ihl) * 4) {
+      std::uint16_t c = static_cast<std::uint16_t>(~inet_sum_be(&f[l3], static_cast<std::size_t>(s.ihl) * 4));
+      f[l3 + 10] = static_cast<std::uint8_t>(c >> 8); f[l3 + 11] = static_cast<std::uint8_t>(c);
+    }
+  }
+  if (s.l3 == 6 && f.size() >= l3 + 40) {
+    std::size_t pl = f.size() - l3 - 40;
+    f[l3 + 4] = static_cast<std::uint8_t>(pl >> 8); f[l3 + 5] = static_cast<std::uint8_t>(pl);
+  }
+  bool l4full = (s.proto == 6 && f.size() >= l4 + 20) || (s.proto == 17 && f.size() >= l4 + 8);
+  if (s.l3 != 0 && l4full && !s.frag) {
+    std::size_t seglen = f.size() - l4;
+    if (s.proto == 17) { f[l4 + 4] = static_cast<std::uint8_t>(seglen >> 8); f[l4 + 5] = static_cast<std::uint8_t>(seglen); }
+    std::uint8_t ph[40];
+    std::size_t phl;
+    if (s.l3 == 4) {
+      std::memcpy(ph, &f[l3 + 12], 8); ph[8] = 0; ph[9] = static_cast<std::uint8_t>(s.proto);
+      ph[10] = static_cast<std::uint8_t>(seglen >> 8); ph[11] = static_cast<std::uint8_t>(seglen); phl = 12;
+    } else {
+      std::memcpy(ph, &f[l3 + 8], 32); ph[32] = 0; ph[33] = 0; ph[34] = static_cast<std::uint8_t>(seglen >> 8);
+      ph[35] = static_cast<std::uint8_t>(seglen); ph[36] = 0; ph[37] = 0; ph[38] = 0; ph[39] = static_cast<std::uint8_t>(s.proto); phl = 40;
+    }
+    std::size_t co = l4 + (s.proto == 6 ? 16 : 6);
+    std::uint32_t psum = inet_sum_be(ph, phl);
+    std::uint16_t c = static_cast<std::uint16_t>(~inet_sum_be(&f[l4], seglen, psum));
+    if (s.proto == 17 && c == 0) c = 0xFFFF;  // packet_generator.cpp:304
+    f[co] = static_cast<std::uint8_t>(c >> 8); f[co + 1] = static_cast<std::uint8_t>(c);
+  }
+  if (s.balance && f.size() >= 12) {
+    // Choose src-MAC bytes 10..11 so the whole-frame checksum (the RX verify of
+    // queue_pair.cpp:437-438) is 0: the ones'-complement sum must be 0xFFFF.
+    f[10] = 0; f[11] = 0;
+    std::uint16_t rest = inet_sum_be(f.data(), f.size());
+    std::uint16_t w = static_cast<std::uint16_t>(0xFFFF - rest);
+    if (w == 0) w = 0xFFFF;  // 0xFFFF + x == x in ones' complement, keeps the total 0xFFFF
+    if (rest == 0) w = 0xFFFF;
+    f[10] = static_cast<std::uint8_t>(w >> 8); f[11] = static_cast<std::uint8_t>(w);
+  }
+  return f;
+}
+
+FrameSpec random_spec(Rng& r) {
+  FrameSpec s;
+  int kind = static_cast<int>(r.below(14));
+  static const std::size_t sizes[] = {64, 64, 64, 64, 64, 64, 64, 576, 576, 576, 576, 1518};
+  s.total = r.below(5) == 0 ? 14 + r.below(1600) : sizes[r.below(12)];
+  if (r.below(40) == 0) s.total = 9000;
+  if (r.below(40) == 0) s.total = 9216;
+  switch (kind) {
+    case 0: s.proto = 6; break;
+    case 1: s.proto = 17; break;
+    case 2: s.vlan_tags = 1; s.proto = 6; break;
+    case 3: s.vlan_tags = 2; s.proto = 17; break;
+    case 4: s.ihl = 6 + static_cast<int>(r.below(10)); s.proto = 6; s.vlan_tags = static_cast<int>(r.below(3)); break;
+    case 5: s.frag = true; s.proto = 17; break;
+    case 6: s.proto = 1; break;
+    case 7: s.l3 = 6; s.proto = 6; break;
+    case 8: s.l3 = 6; s.proto = 17; s.vlan_tags = static_cast<int>(r.below(3)); break;
+    case 9: s.l3 = 6; s.proto = 58; break;
+    case 10: s.l3 = 0; break;
+    case 11: s.total = r.below(60); s.proto = r.below(2) ? 6 : 17; s.vlan_tags = static_cast<int>(r.below(2)); break;
+    default: s.total = s.total > 200 ? s.total : 200; break;  // plain TCP, bigger
+  }
+  s.balance = r.below(10) != 0;
+  return s;
+}
+
+// ----------------------------------------------------------------- RX mix --
+void gen_rx_mix() {
+  Rng r{42};
+  std::vector<std::uint8_t> frames;
+  std::vector<std::uint64_t> desc;
+  const int N = 3000;
+  for (int i = 0; i < N; ++i) {
+    FrameSpec s = random_spec(r);
+    auto f = build_frame(r, s);
+    std::size_t gap = r.below(8) == 0 ? r.below(16) : (16 - frames.size() % 16) % 16;
+    for (std::size_t g = 0; g < gap; ++g) frames.push_back(r.byte());
+    std::uint64_t off = frames.size();
+    frames.insert(frames.end(), f.begin(), f.end());
+    desc.push_back(off | (static_cast<std::uint64_t>(f.size()) << 40));
+  }
+  for (int g = 0; g < 32; ++g) frames.push_back(r.byte());
+  while (frames.size() % 16) frames.push_back(0);
+  write_bin("rx_mix.frames.bin", frames);
+  write_bin("rx_mix.desc.bin", desc);
+
+  std::vector<std::uint16_t> csum(N);
+  for (int i = 0; i < N; ++i) {
+    std::uint64_t off = desc[i] & ((1ull << 40) - 1);
+    csum[i] = ref_csum(frames.data() + off, static_cast<std::size_t>(desc[i] >> 40));
+  }
+  write_bin("rx_mix.csum.bin", csum);
+
+  struct Cfg { std::string name; std::vector<std::uint8_t> key; std::vector<std::uint16_t> table; int mode; int raw_off; int raw_len; };
+  std::vector<std::uint16_t> t4(128), t16(128), t7(7);
+  for (int i = 0; i < 128; ++i) { t4[i] = static_cast<std::uint16_t>(i % 4); t16[i] = static_cast<std::uint16_t>(i % 16); }
+  for (int i = 0; i < 7; ++i) t7[i] = static_cast<std::uint16_t>(100 + i);
+  std::vector<Cfg> cfgs = {
+      {"ms_q4", kMsKey, t4, ORACLE_TUPLE_AUTO, 0, 0},
+      {"ms_q16", kMsKey, t16, ORACLE_TUPLE_AUTO, 0, 0},
+      {"default_key_t7", {}, t7, ORACLE_TUPLE_AUTO, 0, 0},
+      {"default_engine", {}, {}, ORACLE_TUPLE_AUTO, 0, 0},
+      {"raw26x36_default_key", {}, {0, 1, 2, 3}, ORACLE_TUPLE_RAW, 26, 36},
+      {"raw0x64_ms", kMsKey, t16, ORACLE_TUPLE_RAW, 0, 64},
+      {"raw30x12_key52", std::vector<std::uint8_t>(52, 0x3C), t7, ORACLE_TUPLE_RAW, 30, 12},
+  };
+  std::ostringstream js;
+  js << "{\n \"source\": \"compute_checksum (src/checksum.cpp) + RssEngine::select_queue (src/rss.cpp) on oracle_extract_tuple\",\n";
+  js << " \"n\": " << N << ",\n \"configs\": [\n";
+  for (std::size_t ci = 0; ci < cfgs.size(); ++ci) {
+    auto& c = cfgs[ci];
+    RssConfig rc;
+    rc.key = c.key;
+    rc.table = c.table;
+    RssEngine eng{rc};
+    std::vector<std::uint32_t> hash(N), tidx(N);
+    std::vector<std::uint16_t> queue(N);
+    std::uint8_t tuple[64];
+    for (int i = 0; i < N; ++i) {
+      std::uint64_t off = desc[i] & ((1ull << 40) - 1);
+      std::size_t len = static_cast<std::size_t>(desc[i] >> 40);
+      std::size_t tl = oracle_extract_tuple(frames.data() + off, len, c.mode, static_cast<std::size_t>(c.raw_off),
+                                            static_cast<std::size_t>(c.raw_len), tuple);
+      std::span<const std::uint8_t> sp(tuple, tl);
+      auto q = eng.select_queue(sp);
+      queue[i] = *q;
+      RssEngine probe{eng.config()};
+      hash[i] = probe.hash(sp);
+      tidx[i] = static_cast<std::uint32_t>(hash[i] % eng.config().table.size());
+    }
+    write_bin("rx_mix." + c.name + ".hash.bin", hash);
+    write_bin("rx_mix." + c.name + ".queue.bin", queue);
+    write_bin("rx_mix." + c.name + ".tidx.bin", tidx);
+    js << "  {\"name\": \"" << c.name << "\", \"key\": \"" << hex(eng.config().key.data(), eng.config().key.size())
+       << "\", \"table\": " << json_arr(eng.config().table) << ", \"mode\": " << c.mode << ", \"raw_off\": " << c.raw_off
+       << ", \"raw_len\": " << c.raw_len << ",\n   \"stats_hashes\": " << eng.stats().hashes
+       << ", \"stats_queue_hits\": " << json_arr(eng.stats().queue_hits) << "}" << (ci + 1 < cfgs.size() ? "," : "") << "\n";
+  }
+  js << " ]\n}\n";
+  std::ofstream(g_out + "/rx_mix.json") << js.str();
+}
+
+// --------------------------------------------------------- QueuePair runs --
+struct PipeResult {
+  std::uint32_t tx_status = 0;
+  std::uint16_t tx_segments = 0;
+  std::vector<std::uint32_t> rx_status;
+  std::vector<std::uint8_t> rx_verified;
+  std::vector<std::uint16_t> seg_csum;  // compute_checksum of each delivered RX buffer
+  std::vector<std::uint32_t> seg_len;
+  std::uint64_t drops_checksum = 0;
+  std::uint64_t rx_packets = 0;
+};
+
+// One TX descriptor through QueuePair::process_once with `nrx` RX descriptors.
+PipeResult run_pipeline(const std::vector<std::uint8_t>& pkt, bool tso, std::uint16_t mss, std::uint16_t hdr,
+                        bool rx_csum, ChecksumMode mode, std::size_t nrx) {
+  const std::size_t slot = 9216 + 64;
+  HostMemoryConfig mc{.size_bytes = slot * (nrx + 2), .page_size = 4096, .iommu_enabled = false};
+  SimpleHostMemory mem{mc};
+  DMAEngine dma{mem};
+  QueuePairConfig qc{
+      .queue_id = 0,
+      .tx_ring = {.descriptor_size = sizeof(TxDescriptor), .ring_size = 4, .base_address = 0, .queue_id = 0, .host_backed = false},
+      .rx_ring = {.descriptor_size = sizeof(RxDescriptor), .ring_size = nrx + 1, .base_address = 0, .queue_id = 0, .host_backed = false},
+      .tx_completion = {.ring_size = 4, .queue_id = 0},
+      .rx_completion = {.ring_size = nrx + 1, .queue_id = 0},
+  };
+  QueuePair qp{qc, dma};
+  auto bytes = std::as_bytes(std::span<const std::uint8_t>(pkt));
+  assert(mem.write(0, bytes).ok());
+  TxDescriptor tx{.buffer_address = 0, .length = static_cast<std::uint32_t>(pkt.size()), .checksum = ChecksumMode::None,
+                  .descriptor_index = 1, .checksum_value = 0, .tso_enabled = tso, .mss = mss, .header_length = hdr};
+  std::vector<std::byte> tb(sizeof(TxDescriptor));
+  std::memcpy(tb.data(), &tx, sizeof(tx));
+  assert(qp.tx_ring().push_descriptor(tb).ok());
+  for (std::size_t i = 0; i < nrx; ++i) {
+    RxDescriptor rx{.buffer_address = slot * (i + 1), .buffer_length = static_cast<std::uint32_t>(slot), .checksum = mode,
+                    .descriptor_index = static_cast<std::uint16_t>(10 + i), .checksum_offload = rx_csum};
+    std::vector<std::byte> rb(sizeof(RxDescriptor));
+    std::memcpy(rb.data(), &rx, sizeof(rx));
+    assert(qp.rx_ring().push_descriptor(rb).ok());
+  }
+  qp.process_once();
+  PipeResult res;
+  auto tc = qp.tx_completion().poll_completion();
+  if (tc) { res.tx_status = tc->status; res.tx_segments = tc->segments_produced; }
+  std::size_t k = 0;
+  while (auto rc = qp.rx_completion().poll_completion()) {
+    res.rx_status.push_back(rc->status);
+    res.rx_verified.push_back(rc->checksum_verified ? 1 : 0);
+    ++k;
+  }
+  // Delivered segment bytes (only meaningful when every segment was delivered).
+  std::size_t H = (tso && mss > 0 && pkt.size() > mss) ? std::min<std::size_t>(hdr, pkt.size()) : pkt.size();
+  for (std::size_t i = 0; i < k; ++i) {
+    std::size_t seglen;
+    if (!(tso && mss > 0 && pkt.size() > mss) || H >= pkt.size()) seglen = pkt.size();
+    else seglen = H + std::min<std::size_t>(mss, pkt.size() - H - i * mss);
+    std::vector<std::byte> out(seglen);
+    assert(mem.read(slot * (i + 1), out).ok());
+    res.seg_csum.push_back(nic::compute_checksum(out));
+    res.seg_len.push_back(static_cast<std::uint32_t>(seglen));
+  }
+  res.drops_checksum = qp.stats().drops_checksum;
+  res.rx_packets = qp.stats().rx_packets;
+  return res;
+}
+
+void gen_c1() {
+  // C1: 64 x 64 B Eth/IPv4/UDP, RX checksum offload Layer4, RSS MS key + table {0,1,2,3}.
+  Rng r{64};
+  std::vector<std::uint8_t> frames;
+  std::vector<std::uint64_t> desc;
+  std::vector<std::uint16_t> csum, queue;
+  std::vector<std::uint32_t> hash, status;
+  RssConfig rc;
+  rc.key = kMsKey;
+  rc.table = {0, 1, 2, 3};
+  RssEngine eng{rc};
+  for (int i = 0; i < 64; ++i) {
+    FrameSpec s;
+    s.proto = 17;
+    s.total = 64;
+    s.balance = (i % 8) != 3;  // some frames fail the whole-frame verify
+    auto f = build_frame(r, s);
+    desc.push_back(frames.size() | (64ull << 40));
+    frames.insert(frames.end(), f.begin(), f.end());
+    csum.push_back(ref_csum(f.data(), f.size()));
+    std::uint8_t tuple[64];
+    std::size_t tl = oracle_extract_tuple(f.data(), f.size(), ORACLE_TUPLE_AUTO, 0, 0, tuple);
+    std::span<const std::uint8_t> sp(tuple, tl);
+    auto q = eng.select_queue(sp);
+    RssEngine probe{eng.config()};
+    hash.push_back(probe.hash(sp));
+    queue.push_back(*q);
+    auto pr = run_pipeline(f, false, 0, 0, true, ChecksumMode::Layer4, 1);
+    status.push_back(pr.rx_status.empty() ? 0xFFFFFFFFu : pr.rx_status[0]);
+  }
+  write_bin("c1_udp64.frames.bin", frames);
+  write_bin("c1_udp64.desc.bin", desc);
+  std::ofstream(g_out + "/c1_udp64.json")
+      << "{\"note\": \"C1: 64 x 64 B UDP; csum = compute_checksum, rx_status = QueuePair RX completion status "
+         "(queue_pair.cpp:434-447, Layer4 offload), queue = RssEngine::select_queue (MS key, table {0,1,2,3})\",\n"
+      << " \"key\": \"" << hex(kMsKey.data(), kMsKey.size()) << "\", \"table\": [0,1,2,3],\n"
+      << " \"csum\": " << json_arr(csum) << ",\n \"hash\": " << json_arr(hash) << ",\n \"queue\": " << json_arr(queue)
+      << ",\n \"rx_status\": " << json_arr(status) << ",\n \"stats_hashes\": " << eng.stats().hashes
+      << ", \"stats_queue_hits\": " << json_arr(eng.stats().queue_hits) << "}\n";
+}
+
+void gen_tso() {
+  Rng r{9000};
+  struct Case { std::size_t L; std::uint16_t H; std::uint16_t mss; bool tso; bool random_bytes; };
+  std::vector<Case> cs = {
+      {9000, 54, 1448, true, true},  {9000, 54, 1448, true, false}, {9000, 55, 1448, true, true},
+      {9000, 54, 1447, true, true},  {9000, 53, 1001, true, true},  {9000, 0, 1448, true, true},
+      {9000, 66, 8934, true, true},  {1518, 54, 1460, true, true},  {1518, 54, 100, true, true},
+      {4000, 54, 63, true, true},    {3000, 41, 17, true, true},    {200, 20, 5, true, true},
+      {12, 0, 6, true, false},       {10, 2, 3, true, false},       {100, 100, 10, true, true},
+      {100, 101, 10, true, true},    {9000, 54, 100, true, true},   {9000, 54, 9001, true, true},
+      {1518, 54, 1518, true, true},  {1518, 54, 0, true, true},     {700, 54, 1448, false, true},
+      {9000, 14, 140, true, true},   {9000, 54, 141, true, true},
+  };
+  std::ostringstream js;
+  js << "{\n \"source\": \"QueuePair::process_once TSO (src/queue_pair.cpp:195-460) + compute_checksum of each delivered RX segment\",\n \"cases\": [\n";
+  std::vector<std::uint8_t> frames;
+  for (std::size_t ci = 0; ci < cs.size(); ++ci) {
+    auto& c = cs[ci];
+    std::vector<std::uint8_t> pkt(c.L);
+    if (c.random_bytes) {
+      FrameSpec s; s.total = c.L; s.balance = false;
+      pkt = build_frame(r, s);
+    } else {
+      for (std::size_t i = 0; i < c.L; ++i) pkt[i] = static_cast<std::uint8_t>(i & 0xFF);
+    }
+    std::uint64_t off = frames.size();
+    frames.insert(frames.end(), pkt.begin(), pkt.end());
+    while (frames.size() % 16) frames.push_back(r.byte());
+    // Pass 1: no RX checksum offload -> every segment delivered; csum of each.
+    auto all = run_pipeline(pkt, c.tso, c.mss, c.H, false, ChecksumMode::None, 70);
+    // Pass 2: RX offload Layer4 -> statuses with the first-failure short-circuit.
+    auto ver = run_pipeline(pkt, c.tso, c.mss, c.H, true, ChecksumMode::Layer4, 70);
+    js << "  {\"off\": " << off << ", \"len\": " << c.L << ", \"hdr\": " << c.H << ", \"mss\": " << c.mss
+       << ", \"tso\": " << (c.tso ? 1 : 0) << ",\n   \"tx_status\": " << all.tx_status << ", \"tx_segments\": " << all.tx_segments
+       << ", \"seg_csum\": " << json_arr(all.seg_csum) << ", \"seg_len\": " << json_arr(all.seg_len)
+       << ",\n   \"verify_tx_status\": " << ver.tx_status << ", \"verify_tx_segments\": " << ver.tx_segments
+       << ", \"verify_rx_status\": " << json_arr(ver.rx_status) << ", \"verify_drops_checksum\": " << ver.drops_checksum
+       << ", \"verify_rx_packets\": " << ver.rx_packets << "}" << (ci + 1 < cs.size() ? "," : "") << "\n";
+  }
+  js << " ]\n}\n";
+  write_bin("tso.frames.bin", frames);
+  std::ofstream(g_out + "/tso.json") << js.str();
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc > 1) g_out = argv[1];
+  // Sanity: the reference reproduces the Microsoft verification vector.
+  {
+    RssConfig rc;
+    rc.key = kMsKey;
+    RssEngine e{rc};
+    auto t = tuple12(ip(66, 9, 149, 187), ip(161, 142, 100, 80), 2794, 1766);
+    if (e.hash(std::span<const std::uint8_t>(t)) != 0x51ccc178u) { std::fprintf(stderr, "MS vector mismatch\n"); return 1; }
+    if (e.hash(std::span<const std::uint8_t>(t.data(), 8)) != 0x323e8fc2u) { std::fprintf(stderr, "MS vector mismatch\n"); return 1; }
+  }
+  gen_checksum();
+  gen_rss();
+  gen_rx_mix();
+  gen_c1();
+  gen_tso();
+  std::printf("golden fixtures written to %s\n", g_out.c_str());
+  return 0;
+}

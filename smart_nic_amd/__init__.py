@@ -1,0 +1,223 @@
+"""smart_nic_amd — MI355X-native RX offload path of smart_nic (checksum + RSS).
+
+The product is native code: ``libnicgpu.so`` (HIP kernels for gfx950 behind the
+C-ABI of ``include/nicgpu.h``) and ``libnic_host.so`` (the C++20 ``nic::`` API,
+``include/nic/*.h``).  This Python package is glue for tests and ``bench.py``:
+it binds the C-ABI with ctypes and passes torch-allocated device memory to it.
+There is no CPU fallback — if the HIP library is missing or no gfx950 device
+is visible every call raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnicgpu.so")
+HOST_LIB_PATH = os.path.join(_HERE, "libnic_host.so")
+INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
+
+# include/nicgpu.h
+OK = 0
+ERR_INVALID = -1
+ERR_HIP = -2
+ERR_NO_DEVICE = -3
+ERR_NOMEM = -4
+TUPLE_NONE = 0
+TUPLE_AUTO = 1
+TUPLE_RAW = 2
+RAW_MAX_END = 64
+MAX_PACKET = 65535
+DESC_OFFSET_BITS = 40
+
+# Every symbol include/nicgpu.h declares (tests check the library exports them).
+ABI_SYMBOLS = (
+    "nicgpu_abi_version",
+    "nicgpu_strerror",
+    "nicgpu_device_count",
+    "nicgpu_rss_create",
+    "nicgpu_rss_destroy",
+    "nicgpu_rss_set_key",
+    "nicgpu_rss_set_key_device",
+    "nicgpu_rss_set_table",
+    "nicgpu_rss_set_table_device",
+    "nicgpu_rss_info",
+    "nicgpu_rx_offload",
+    "nicgpu_checksum_batch",
+    "nicgpu_tso_checksum",
+)
+
+_lib = None
+
+
+class NicGpuError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libnicgpu.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NicGpuError(
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(path)
+    vp, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
+    sig = {
+        "nicgpu_abi_version": (i32, []),
+        "nicgpu_strerror": (ctypes.c_char_p, [i32]),
+        "nicgpu_device_count": (i32, []),
+        "nicgpu_rss_create": (i32, [ctypes.POINTER(vp), i32]),
+        "nicgpu_rss_destroy": (i32, [vp]),
+        "nicgpu_rss_set_key": (i32, [vp, vp, sz, vp]),
+        "nicgpu_rss_set_key_device": (i32, [vp, vp, sz, vp]),
+        "nicgpu_rss_set_table": (i32, [vp, vp, sz, vp]),
+        "nicgpu_rss_set_table_device": (i32, [vp, vp, sz, vp]),
+        "nicgpu_rss_info": (i32, [vp, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
+        "nicgpu_rx_offload": (i32, [vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp]),
+        "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),
+        "nicgpu_tso_checksum": (i32, [vp, vp, vp, vp, vp, sz, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(status: int, what: str) -> None:
+    if status != OK:
+        msg = load_library().nicgpu_strerror(status).decode()
+        raise NicGpuError(f"{what} failed: {msg} ({status})")
+
+
+def _ptr(t):
+    """Device (or host) data pointer of a tensor, or None."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def device_count() -> int:
+    return load_library().nicgpu_device_count()
+
+
+def desc_pack(offsets, lengths):
+    """numpy: pack byte offsets and lengths into the uint64 descriptor format."""
+    import numpy as np
+
+    off = np.asarray(offsets, dtype=np.uint64)
+    ln = np.asarray(lengths, dtype=np.uint64)
+    return off | (ln << np.uint64(DESC_OFFSET_BITS))
+
+
+class RssContext:
+    """Owner of a ``nicgpu_rss_ctx`` (key LUT + indirection table on one GPU)."""
+
+    def __init__(self, device: int = 0):
+        import torch
+
+        self.lib = load_library()
+        self.device = device
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _check(self.lib.nicgpu_rss_create(ctypes.byref(h), device), "nicgpu_rss_create")
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self.lib.nicgpu_rss_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_key(self, key: bytes = b"", stream=None):
+        buf = (ctypes.c_uint8 * max(1, len(key))).from_buffer_copy(bytes(key) or b"\0")
+        _check(
+            self.lib.nicgpu_rss_set_key(self.handle, buf, len(key), _stream_ptr(stream)),
+            "nicgpu_rss_set_key",
+        )
+
+    def set_key_device(self, key_dev, stream=None):
+        _check(
+            self.lib.nicgpu_rss_set_key_device(
+                self.handle, _ptr(key_dev), key_dev.numel(), _stream_ptr(stream)
+            ),
+            "nicgpu_rss_set_key_device",
+        )
+
+    def set_table(self, table=(), stream=None):
+        import numpy as np
+
+        arr = np.ascontiguousarray(np.asarray(table, dtype=np.uint16))
+        _check(
+            self.lib.nicgpu_rss_set_table(
+                self.handle,
+                arr.ctypes.data_as(ctypes.c_void_p) if arr.size else None,
+                arr.size,
+                _stream_ptr(stream),
+            ),
+            "nicgpu_rss_set_table",
+        )
+
+    def set_table_device(self, table_dev, stream=None):
+        _check(
+            self.lib.nicgpu_rss_set_table_device(
+                self.handle, _ptr(table_dev), table_dev.numel(), _stream_ptr(stream)
+            ),
+            "nicgpu_rss_set_table_device",
+        )
+
+    def info(self):
+        k, t = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(self.lib.nicgpu_rss_info(self.handle, ctypes.byref(k), ctypes.byref(t)), "info")
+        return k.value, t.value
+
+
+def rx_offload(ctx, frames, desc, mode=TUPLE_AUTO, raw_off=0, raw_len=0, csum=None,
+               hash_out=None, queue=None, hits=None, stream=None):
+    """Launch the fused RX checksum + RSS kernel on torch device tensors."""
+    lib = load_library()
+    n = desc.numel()
+    _check(
+        lib.nicgpu_rx_offload(
+            ctx.handle if ctx is not None else None,
+            _ptr(frames), _ptr(desc), n, mode, raw_off, raw_len,
+            _ptr(csum), _ptr(hash_out), _ptr(queue), _ptr(hits), _stream_ptr(stream),
+        ),
+        "nicgpu_rx_offload",
+    )
+
+
+def checksum_batch(frames, desc, csum, stream=None):
+    lib = load_library()
+    _check(
+        lib.nicgpu_checksum_batch(_ptr(frames), _ptr(desc), desc.numel(), _ptr(csum),
+                                  _stream_ptr(stream)),
+        "nicgpu_checksum_batch",
+    )
+
+
+def tso_checksum(frames, desc, hdr_len, mss, seg_base, out, stream=None):
+    lib = load_library()
+    _check(
+        lib.nicgpu_tso_checksum(_ptr(frames), _ptr(desc), _ptr(hdr_len), _ptr(mss),
+                                _ptr(seg_base), desc.numel(), _ptr(out), _stream_ptr(stream)),
+        "nicgpu_tso_checksum",
+    )
