@@ -45,7 +45,6 @@ constexpr int kHdrBytes = kHdrChunks * 16;
 constexpr int kLutPos = 2 * NICGPU_MAX_TUPLE;  // nibble positions
 constexpr int kLutWords = kLutPos * 16;
 constexpr int kHistLds = 1024;     // tables up to this size histogram in LDS
-constexpr int kUnroll = 4;         // 16-B chunk loads in flight per lane
 constexpr uint64_t kOffMask = (1ull << NICGPU_DESC_OFFSET_BITS) - 1;
 
 const uint8_t kDefaultKey[20] = {0x6D, 0x5A, 0x56, 0x6B, 0x65, 0x4E, 0x67, 0x6E, 0x67, 0x55,
@@ -61,6 +60,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x118, 0xf, 0xf, true);  // row_shr:8
   v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x142, 0xa, 0xf, false); // row_bcast:15
   v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x143, 0xc, 0xf, false); // row_bcast:31
+  return v;
+}
+
+// Inclusive prefix max over the 64 lanes (same DPP pattern; 0 is the identity).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  v = max(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x111, 0xf, 0xf, true));
+  v = max(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x112, 0xf, 0xf, true));
+  v = max(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x114, 0xf, 0xf, true));
+  v = max(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x118, 0xf, 0xf, true));
+  v = max(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x142, 0xa, 0xf, false));
+  v = max(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x143, 0xc, 0xf, false));
   return v;
 }
 
@@ -144,59 +154,373 @@ struct RxParams {
   unsigned long long* out_hits;
 };
 
-struct RxShared {
-  uint4 hdr[kWavesPerBlock][kWave][kHdrChunks];  // 16 KiB: first 64 B (abs-aligned) per packet
-  uint4 pk[kWavesPerBlock][kWave];               // {delta lo, delta hi, end, info} per packet
-  uint32_t end[kWavesPerBlock][kWave];           // inclusive chunk-count prefix
-  uint32_t S[kWavesPerBlock][kWave];             // running prefix before the packet's first chunk
-  uint32_t E[kWavesPerBlock][kWave];             // running prefix after its last chunk
-  uint32_t lut[kLutWords];
-  uint32_t hist[kHistLds];
-};
+// Dynamic LDS layout (sized per launch by rx_lds_bytes):
+//   per wave: S[64] | E[64] | scratch | hdr[64][kHdrChunks] uint4 (only when hashing)
+//     scratch = general path: pk[64] uint4 {delta lo, delta hi, end, info} + marks[64 U]
+//               contiguous path: two slot windows of 64 U words (ping-pong)
+//   per block: lut[lut_words] | hist[hist_n]
+constexpr uint32_t kScratchOff = kWave * 4 * 2;
 
-// One byte of packet `l` at packet offset o: LDS when staged, else global.
-__device__ __forceinline__ uint32_t pkt_byte(const RxShared& sh, int w, int l, uint32_t lo,
-                                             const uint8_t* __restrict__ pkt, uint32_t o) {
+__host__ __device__ constexpr uint32_t rx_scratch_bytes(int unroll) {
+  return (uint32_t) (kWave * 16 + kWave * unroll * 4) > (uint32_t) (2 * kWave * unroll * 4)
+             ? (uint32_t) (kWave * 16 + kWave * unroll * 4)
+             : (uint32_t) (2 * kWave * unroll * 4);
+}
+
+__host__ __device__ constexpr uint32_t rx_hdr_off(int unroll) { return kScratchOff + rx_scratch_bytes(unroll); }
+
+__host__ __device__ constexpr uint32_t rx_wave_lds(bool rss, int unroll) {
+  return rx_hdr_off(unroll) + (rss ? kWave * kHdrChunks * 16 : 0);
+}
+
+__host__ __device__ inline uint32_t rx_lds_bytes(int wpb, int unroll, bool rss, uint32_t lut_words, uint32_t hist_n) {
+  return (uint32_t) wpb * rx_wave_lds(rss, unroll) + lut_words * 4u + hist_n * 4u;
+}
+
+// One byte of packet l at packet offset o: LDS when staged, else global.
+__device__ __forceinline__ uint32_t pkt_byte(const uint4* hdr_l, uint32_t lo, const uint8_t* __restrict__ pkt,
+                                             uint32_t o) {
   uint32_t a = lo + o;
-  if (a < (uint32_t) kHdrBytes) return reinterpret_cast<const uint8_t*>(&sh.hdr[w][l][0])[a];
+  if (a < (uint32_t) kHdrBytes) return reinterpret_cast<const uint8_t*>(hdr_l)[a];
   return pkt[o];
 }
 
-__device__ __forceinline__ uint32_t hash_bytes(uint32_t h, const RxShared& sh, int w, int l,
-                                               uint32_t lo, const uint8_t* __restrict__ pkt,
-                                               uint32_t src, uint32_t cnt, uint32_t pos) {
+__device__ __forceinline__ uint32_t hash_bytes(uint32_t h, const uint32_t* lut, const uint4* hdr_l, uint32_t lo,
+                                               const uint8_t* __restrict__ pkt, uint32_t src, uint32_t cnt,
+                                               uint32_t pos) {
   for (uint32_t i = 0; i < cnt; ++i) {
-    uint32_t b = pkt_byte(sh, w, l, lo, pkt, src + i);
+    uint32_t b = pkt_byte(hdr_l, lo, pkt, src + i);
     uint32_t p = 2 * (pos + i);
-    h ^= sh.lut[p * 16 + (b >> 4)] ^ sh.lut[(p + 1) * 16 + (b & 15)];
+    h ^= lut[p * 16 + (b >> 4)] ^ lut[(p + 1) * 16 + (b & 15)];
   }
   return h;
 }
 
-__global__ __launch_bounds__(kBlock) void rx_offload_kernel(RxParams P) {
-  __shared__ RxShared sh;
+// Tuple extraction + Toeplitz for one packet (oracle/oracle.c oracle_extract_tuple).
+__device__ __forceinline__ uint32_t rss_hash_packet(const RxParams& P, const uint32_t* lut, const uint4* hdr_l,
+                                                    uint32_t lo, const uint8_t* __restrict__ pkt, uint32_t len) {
+  uint32_t h = 0;
+  if (P.mode == NICGPU_TUPLE_RAW) {
+    uint32_t cnt = 0;
+    if (P.raw_off < len) {
+      uint32_t e = P.raw_off + P.raw_len;
+      cnt = (e > len ? len : e) - P.raw_off;
+    }
+    return hash_bytes(0u, lut, hdr_l, lo, pkt, P.raw_off, cnt, 0);
+  }
+  if (len < 14) return 0;
+  uint32_t l3 = 14;
+  uint32_t et = (pkt_byte(hdr_l, lo, pkt, 12) << 8) | pkt_byte(hdr_l, lo, pkt, 13);
+  for (int t = 0; t < 2 && (et == 0x8100u || et == 0x88A8u); ++t) {
+    if (len < l3 + 4) return 0;
+    et = (pkt_byte(hdr_l, lo, pkt, l3 + 2) << 8) | pkt_byte(hdr_l, lo, pkt, l3 + 3);
+    l3 += 4;
+  }
+  if (et == 0x0800u && len >= l3 + 20) {
+    uint32_t vihl = pkt_byte(hdr_l, lo, pkt, l3);
+    uint32_t ihl = (vihl & 15u) * 4u;
+    if ((vihl >> 4) == 4u && ihl >= 20u) {
+      h = hash_bytes(0u, lut, hdr_l, lo, pkt, l3 + 12, 8, 0);
+      uint32_t proto = pkt_byte(hdr_l, lo, pkt, l3 + 9);
+      uint32_t frag = ((pkt_byte(hdr_l, lo, pkt, l3 + 6) << 8) | pkt_byte(hdr_l, lo, pkt, l3 + 7)) & 0x3FFFu;
+      uint32_t l4 = l3 + ihl;
+      if ((proto == 6u || proto == 17u) && frag == 0u && l4 + 4u <= len)
+        h = hash_bytes(h, lut, hdr_l, lo, pkt, l4, 4, 8);
+    }
+  } else if (et == 0x86DDu && len >= l3 + 40) {
+    uint32_t vb = pkt_byte(hdr_l, lo, pkt, l3);
+    if ((vb >> 4) == 6u) {
+      h = hash_bytes(0u, lut, hdr_l, lo, pkt, l3 + 8, 32, 0);
+      uint32_t nh = pkt_byte(hdr_l, lo, pkt, l3 + 6);
+      if ((nh == 6u || nh == 17u) && l3 + 44u <= len) h = hash_bytes(h, lut, hdr_l, lo, pkt, l3 + 40, 4, 32);
+    }
+  }
+  return h;
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// A batch of U chunk loads per lane: chunk c = base + 64u + lane.
+template <int U>
+struct ChunkBatch {
+  u32x4 v[U];
+  uint32_t q[U];     // packet (lane) index within the tile
+  uint32_t meta[U];  // lo | hi<<4 | head<<9 | tail<<10 | valid<<11 | hdr slot (0..7)<<12
+};
+
+// chunk -> packet without a search: every non-empty packet whose first chunk
+// lies in this batch's window [base, base + 64U) writes its lane index, tagged
+// with the batch id, at its position in the wave's mark array; a lane's packet
+// is then the prefix-max of the valid marks up to its chunk (DPP), seeded with
+// the packet of the previous batch's last chunk (`carry`).  One LDS write and
+// one LDS read per batch instead of a chain of dependent reads.  The 16-B load
+// is issued unconditionally (lanes past the tile's end re-read its last chunk
+// and are zeroed later), so the loads carry no branches.
+template <int U, bool NT>
+__device__ __forceinline__ void plan_batch(ChunkBatch<U>& B, const uint4* __restrict__ pk, uint32_t* marks,
+                                           uint32_t base, uint32_t total, uint32_t lane, uint32_t my_start,
+                                           uint32_t my_nch, uint32_t tag, uint32_t& carry,
+                                           const uint8_t* __restrict__ frames) {
+  const uint32_t rel = my_start - base;
+  if (my_nch != 0u && my_start >= base && rel < (uint32_t) (kWave * U)) marks[rel] = (tag << 6) | lane;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t m = marks[u * kWave + lane];
+    const uint32_t cand = (m >> 6) == tag ? (m & 63u) : 0u;
+    uint32_t q = wave_incl_max(cand);
+    q = max(q, carry);
+    carry = (uint32_t) __builtin_amdgcn_readlane((int) q, 63);
+    const uint32_t c = base + (uint32_t) u * kWave + lane;
+    const uint4 e = pk[q];
+    const uint32_t endq = e.z, inf = e.w;
+    const uint32_t startq = endq - (inf >> 9);
+    const bool valid = c < total;
+    const bool head = c == startq;
+    const bool tail = c + 1 == endq;
+    const uint32_t lo = head ? (inf & 15u) : 0u;
+    const uint32_t hi = tail ? ((inf >> 4) & 31u) : 16u;
+    const uint32_t k = c - startq;
+    const uint32_t slot = k < (uint32_t) kHdrChunks ? k : 7u;
+    B.q[u] = q;
+    B.meta[u] = lo | (hi << 4) | ((uint32_t) head << 9) | ((uint32_t) tail << 10) | ((uint32_t) valid << 11) |
+                (slot << 12);
+    const uint32_t ce = valid ? c : total - 1u;
+    const int64_t dl = (int64_t) (((uint64_t) e.y << 32) | e.x);
+    const u32x4* p = reinterpret_cast<const u32x4*>(frames + (uint64_t) ((int64_t) ce + dl) * 16);
+    if constexpr (NT) B.v[u] = __builtin_nontemporal_load(p);
+    else B.v[u] = *p;
+  }
+}
+
+// Wave-uniform walker for tiles whose non-empty packets all span >= 64 chunks
+// (1 KiB+: C2's 1518 B, jumbo).  A 64-chunk step then holds at most two
+// packets — the tail of `qa` and the head of the next non-empty packet — so the
+// chunk -> packet map is one boundary lane index computed in scalar registers
+// (v_readlane of the packet lanes' descriptors, s_ff1 over the non-empty mask)
+// and a select per lane, instead of marks + a DPP max-scan + LDS reads.
+struct BigWalker {
+  uint64_t nonempty;  // ballot(nch > 0)
+  uint32_t qa;        // packet holding the walker's current chunk
+};
+
+__device__ __forceinline__ uint32_t next_nonempty(uint64_t nonempty, uint32_t q) {
+  const uint64_t m = q >= 63 ? 0ull : (nonempty & ~((2ull << q) - 1ull));
+  return m ? (uint32_t) __builtin_ctzll(m) : q;
+}
+
+template <int U, bool NT>
+__device__ __forceinline__ void plan_big(ChunkBatch<U>& B, BigWalker& W, uint32_t base, uint32_t total,
+                                         uint32_t lane, uint32_t v_end, uint32_t v_info, uint32_t v_dlo,
+                                         uint32_t v_dhi, const uint8_t* __restrict__ frames) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t sb = base + (uint32_t) u * kWave;
+    uint32_t qa = W.qa;
+    uint32_t ea = (uint32_t) __builtin_amdgcn_readlane((int) v_end, (int) qa);
+    while (ea <= sb && ea < total) {
+      qa = next_nonempty(W.nonempty, qa);
+      ea = (uint32_t) __builtin_amdgcn_readlane((int) v_end, (int) qa);
+    }
+    W.qa = qa;
+    const uint32_t infa = (uint32_t) __builtin_amdgcn_readlane((int) v_info, (int) qa);
+    const uint32_t dla = (uint32_t) __builtin_amdgcn_readlane((int) v_dlo, (int) qa);
+    const uint32_t dha = (uint32_t) __builtin_amdgcn_readlane((int) v_dhi, (int) qa);
+    uint32_t b = ea - sb;  // first lane of the next packet (>= 64: none in this step)
+    uint32_t qb = qa, eb = ea, infb = infa, dlb = dla, dhb = dha;
+    if (b < (uint32_t) kWave && ea < total) {
+      qb = next_nonempty(W.nonempty, qa);
+      eb = (uint32_t) __builtin_amdgcn_readlane((int) v_end, (int) qb);
+      infb = (uint32_t) __builtin_amdgcn_readlane((int) v_info, (int) qb);
+      dlb = (uint32_t) __builtin_amdgcn_readlane((int) v_dlo, (int) qb);
+      dhb = (uint32_t) __builtin_amdgcn_readlane((int) v_dhi, (int) qb);
+    } else {
+      b = (uint32_t) kWave;
+    }
+    const bool inA = lane < b;
+    const uint32_t c = sb + lane;
+    const uint32_t q = inA ? qa : qb;
+    const uint32_t endq = inA ? ea : eb;
+    const uint32_t inf = inA ? infa : infb;
+    const uint32_t startq = endq - (inf >> 9);
+    const bool valid = c < total;
+    const bool head = c == startq;
+    const bool tail = c + 1 == endq;
+    const uint32_t lo = head ? (inf & 15u) : 0u;
+    const uint32_t hi = tail ? ((inf >> 4) & 31u) : 16u;
+    const uint32_t k = c - startq;
+    const uint32_t slot = k < (uint32_t) kHdrChunks ? k : 7u;
+    B.q[u] = q;
+    B.meta[u] = lo | (hi << 4) | ((uint32_t) head << 9) | ((uint32_t) tail << 10) | ((uint32_t) valid << 11) |
+                (slot << 12);
+    const uint32_t ce = valid ? c : total - 1u;
+    const uint64_t dl = inA ? (((uint64_t) dha << 32) | dla) : (((uint64_t) dhb << 32) | dlb);
+    const u32x4* p = reinterpret_cast<const u32x4*>(frames + (uint64_t) ((int64_t) ce + (int64_t) dl) * 16);
+    if constexpr (NT) B.v[u] = __builtin_nontemporal_load(p);
+    else B.v[u] = *p;
+  }
+}
+
+// ---- contiguous tiles ----------------------------------------------------
+// When every non-empty packet of a tile starts in the 16-B chunk right after
+// the previous one's last chunk (a packed batch), chunk c of the tile lives at
+// absolute chunk D + c: loads need no chunk -> packet map at all.  The few
+// positions that need packet information — the first kHdrChunks chunks of a
+// packet (header staging, head mask) and its last chunk (tail mask, prefix
+// record) — are scattered by the packet lanes into a per-window slot array
+// (0 = nothing); chunk lanes read and clear their slot.
+//   slot: bit0 valid | q<<1 (6) | k<<7 (3: header chunk 0..3, 7 = none)
+//         | lo<<11 (4) | tail<<15 | hi<<16 (5)
+template <int U>
+struct ContigBatch {
+  u32x4 v[U];
+};
+
+template <int U>
+__device__ __forceinline__ void scatter_slots(uint32_t* slots, uint32_t base, uint32_t lane, uint32_t start,
+                                              uint32_t nch, uint32_t info) {
+  if (nch == 0u) return;
+  constexpr uint32_t W = (uint32_t) kWave * U;
+  const uint32_t rs = start - base;          // window-relative start (wraps when before the window)
+  const uint32_t re = start + nch - 1u - base;
+  const uint32_t lo = info & 15u, hi = (info >> 4) & 31u;
+  const uint32_t common = 1u | (lane << 1);
+#pragma unroll
+  for (uint32_t j = 0; j < (uint32_t) kHdrChunks; ++j) {
+    const uint32_t r = rs + j;
+    if (j < nch && r < W) {
+      uint32_t v = common | (j << 7) | (j == 0 ? (lo << 11) : 0u);
+      v |= (j + 1u == nch) ? ((1u << 15) | (hi << 16)) : (16u << 16);
+      slots[r] = v;
+    }
+  }
+  if (nch > (uint32_t) kHdrChunks && re < W) slots[re] = common | (7u << 7) | (1u << 15) | (hi << 16);
+}
+
+template <int U, bool NT>
+__device__ __forceinline__ void plan_contig(ContigBatch<U>& B, uint32_t* slots, uint32_t base, uint32_t total,
+                                            uint32_t lane, uint32_t start, uint32_t nch, uint32_t info,
+                                            const u32x4* __restrict__ tile16) {
+  scatter_slots<U>(slots, base, lane, start, nch, info);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t c = base + (uint32_t) u * kWave + lane;
+    const uint32_t ce = c < total ? c : total - 1u;
+    if constexpr (NT) B.v[u] = __builtin_nontemporal_load(tile16 + ce);
+    else B.v[u] = tile16[ce];
+  }
+}
+
+template <int U>
+__device__ __forceinline__ uint32_t process_contig(ContigBatch<U>& B, uint32_t* slots, uint32_t run, uint32_t* E,
+                                                   uint4* hdr, bool stage_hdr, uint32_t lane) {
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t sl = slots[u * kWave + lane];
+    u32x4 v = B.v[u];
+    if (sl != 0u) {
+      slots[u * kWave + lane] = 0u;
+      const int lo = (int) ((sl >> 11) & 15u), hi = (int) ((sl >> 16) & 31u);
+      if (lo != 0 || hi != 16) {
+        v.x &= dword_keep(lo, hi, 0);
+        v.y &= dword_keep(lo, hi, 1);
+        v.z &= dword_keep(lo, hi, 2);
+        v.w &= dword_keep(lo, hi, 3);
+      }
+    }
+    const uint32_t s = add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, 0u))));
+    const uint32_t incl = wave_incl_scan(s);
+    const uint32_t step_total = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
+    if (sl != 0u) {
+      const uint32_t q = (sl >> 1) & 63u, k = (sl >> 7) & 7u;
+      if (sl & (1u << 15)) E[q] = run + incl;
+      if (stage_hdr && k < (uint32_t) kHdrChunks) hdr[q * kHdrChunks + k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    run += step_total;
+  }
+  return run;
+}
+
+// Mask, sum, scan and record one batch.  `run` is the tile's running prefix.
+template <int U>
+__device__ __forceinline__ uint32_t process_batch(ChunkBatch<U>& B, uint32_t run, uint32_t* S, uint32_t* E,
+                                                  uint4* hdr, bool stage_hdr) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t m = B.meta[u];
+    const int lo = (int) (m & 15u), hi = (int) ((m >> 4) & 31u);
+    u32x4 v = B.v[u];
+    if (!(m & (1u << 11))) v = (u32x4){0u, 0u, 0u, 0u};
+    if (lo != 0 || hi != 16) {
+      v.x &= dword_keep(lo, hi, 0);
+      v.y &= dword_keep(lo, hi, 1);
+      v.z &= dword_keep(lo, hi, 2);
+      v.w &= dword_keep(lo, hi, 3);
+    }
+    const uint32_t s = add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, 0u))));
+    const uint32_t incl = wave_incl_scan(s);
+    const uint32_t step_total = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
+    if (m & (1u << 11)) {
+      const uint32_t q = B.q[u];
+      if (m & (1u << 9)) S[q] = run + incl - s;
+      if (m & (1u << 10)) E[q] = run + incl;
+      const uint32_t slot = m >> 12;
+      if (stage_hdr && slot < (uint32_t) kHdrChunks) hdr[q * kHdrChunks + slot] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    run += step_total;
+  }
+  return run;
+}
+
+template <int U, bool NT, int WPB, bool BIG, bool CONTIG>
+__global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
+  extern __shared__ uint4 lds_dyn[];
   const int w = threadIdx.x / kWave;
   const uint32_t lane = lane_id();
   const bool want_rss = P.mode != NICGPU_TUPLE_NONE;
   const bool hist_lds = P.out_hits != nullptr && P.table_n <= (uint32_t) kHistLds;
 
+  uint8_t* base_b = reinterpret_cast<uint8_t*>(lds_dyn);
+  uint8_t* wave_b = base_b + (uint32_t) w * rx_wave_lds(want_rss, U);
+  uint32_t* S = reinterpret_cast<uint32_t*>(wave_b);
+  uint32_t* E = S + kWave;
+  uint4* pk = reinterpret_cast<uint4*>(wave_b + kScratchOff);
+  uint32_t* marks = reinterpret_cast<uint32_t*>(wave_b + kScratchOff + kWave * 16);
+  uint32_t* slotsA = reinterpret_cast<uint32_t*>(wave_b + kScratchOff);
+  uint32_t* slotsB = slotsA + kWave * U;
+  uint4* hdr = reinterpret_cast<uint4*>(wave_b + rx_hdr_off(U));
+  // marks never match a live tag (tags start at 1; cleared slots read as 0)
+  for (uint32_t i = lane; i < (uint32_t) (kWave * U); i += kWave) marks[i] = 0xFFFFFFFFu;
+  uint32_t tag = 0;  // batch id (never reaches 0x3FFFFFF within a launch)
+  uint32_t* lut = reinterpret_cast<uint32_t*>(base_b + (uint32_t) WPB * rx_wave_lds(want_rss, U));
+  uint32_t* hist = lut + P.lut_words;
+
   if (want_rss) {
-    for (uint32_t i = threadIdx.x; i < P.lut_words; i += kBlock) sh.lut[i] = P.lut[i];
+    for (uint32_t i = threadIdx.x; i < P.lut_words; i += kWave * WPB) lut[i] = P.lut[i];
   }
   if (hist_lds) {
-    for (uint32_t i = threadIdx.x; i < P.table_n; i += kBlock) sh.hist[i] = 0;
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) hist[i] = 0;
   }
   __syncthreads();
 
   const uint64_t ntiles = (P.n + kWave - 1) / kWave;
-  const uint64_t wave_gid = (uint64_t) blockIdx.x * kWavesPerBlock + w;
-  const uint64_t nwaves = (uint64_t) gridDim.x * kWavesPerBlock;
+  const uint64_t nwaves = (uint64_t) gridDim.x * WPB;
+  uint64_t tile = (uint64_t) blockIdx.x * WPB + w;
+  // descriptor of this lane's packet in the current tile, prefetched one tile ahead
+  uint64_t d_next = 0;
+  if (tile < ntiles && tile * kWave + lane < P.n) d_next = P.desc[tile * kWave + lane];
 
-  for (uint64_t tile = wave_gid; tile < ntiles; tile += nwaves) {
+  for (; tile < ntiles; tile += nwaves) {
     const uint64_t p0 = tile * kWave;
     const uint64_t pid = p0 + lane;
     const bool have = pid < P.n;
-    const uint64_t d = have ? P.desc[pid] : 0;
+    const uint64_t d = d_next;
+    {
+      const uint64_t nt = tile + nwaves;
+      d_next = (nt < ntiles && nt * kWave + lane < P.n) ? P.desc[nt * kWave + lane] : 0;
+    }
     const uint64_t off = d & kOffMask;
     const uint32_t len = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
     const uint64_t first16 = off >> 4;
@@ -208,135 +532,112 @@ __global__ __launch_bounds__(kBlock) void rx_offload_kernel(RxParams P) {
     const uint32_t lo_first = (uint32_t) (off & 15);
     const uint32_t hi_last = len ? (uint32_t) (((off + len - 1) & 15) + 1) : 16u;
     const uint32_t info = lo_first | (hi_last << 4) | (nch << 9);
-    sh.end[w][lane] = end;
-    sh.pk[w][lane] = make_uint4((uint32_t) (uint64_t) delta, (uint32_t) ((uint64_t) delta >> 32), end, info);
-    __builtin_amdgcn_wave_barrier();
 
-    uint32_t run = 0;  // running chunk-sum prefix of the tile (wave-uniform)
-    for (uint32_t base = 0; base < total; base += kWave * kUnroll) {
-      uint4 data[kUnroll];
-      uint32_t q[kUnroll], c[kUnroll];
-      uint4 pk[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        c[u] = base + (uint32_t) u * kWave + lane;
-        uint32_t qq = 0;
-#pragma unroll
-        for (uint32_t s = 32; s >= 1; s >>= 1) {
-          if (sh.end[w][qq + s - 1] <= c[u]) qq += s;
-        }
-        q[u] = qq > 63 ? 63 : qq;
-        pk[u] = sh.pk[w][q[u]];
+    // Ping-pong pipeline: batch i+1's loads are in flight while batch i is
+    // reduced.  Every plan is unconditional (a batch past the tile's end just
+    // re-reads its last chunk) so the compiler can count the outstanding loads
+    // (s_waitcnt vmcnt(U)) instead of draining them (vmcnt(0)) at a merge.
+    constexpr uint32_t kStep = (uint32_t) kWave * U;
+    uint32_t run = 0, carry = 0;
+    const uint64_t nonempty = __ballot(nch != 0u);
+    const int first_ne = nonempty ? __builtin_ctzll(nonempty) : 0;
+    const uint32_t d_lo0 = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) (uint64_t) delta, first_ne);
+    const uint32_t d_hi0 = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) ((uint64_t) delta >> 32), first_ne);
+    const int64_t D = (int64_t) (((uint64_t) d_hi0 << 32) | d_lo0);
+    const bool contig = CONTIG && __ballot(nch != 0u && delta != D) == 0ull;
+    const bool big = !contig && BIG && __ballot(nch != 0u && nch < (uint32_t) kWave) == 0ull;
+    if (total != 0 && contig) {
+      for (uint32_t i = lane; i < (uint32_t) (2 * kWave * U); i += kWave) slotsA[i] = 0u;
+      __builtin_amdgcn_wave_barrier();
+      const u32x4* tile16 = reinterpret_cast<const u32x4*>(P.frames) + D;
+      ContigBatch<U> A, B;
+      uint32_t b0 = 0;
+      plan_contig<U, NT>(A, slotsA, b0, total, lane, start, nch, info, tile16);
+      for (;;) {
+        plan_contig<U, NT>(B, slotsB, b0 + kStep, total, lane, start, nch, info, tile16);
+        __builtin_amdgcn_sched_barrier(0);
+        run = process_contig<U>(A, slotsA, run, E, hdr, want_rss, lane);
+        if (b0 + kStep >= total) break;
+        plan_contig<U, NT>(A, slotsA, b0 + 2 * kStep, total, lane, start, nch, info, tile16);
+        __builtin_amdgcn_sched_barrier(0);
+        run = process_contig<U>(B, slotsB, run, E, hdr, want_rss, lane);
+        b0 += 2 * kStep;
+        if (b0 >= total) break;
       }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        if (c[u] < total) {
-          int64_t dl = (int64_t) (((uint64_t) pk[u].y << 32) | pk[u].x);
-          uint64_t a16 = (uint64_t) ((int64_t) c[u] + dl);
-          data[u] = *reinterpret_cast<const uint4*>(P.frames + a16 * 16);
-        } else {
-          data[u] = make_uint4(0, 0, 0, 0);
-        }
+    } else if (total != 0 && big) {
+      BigWalker W{__ballot(nch != 0u), 0u};
+      W.qa = (W.nonempty & 1ull) ? 0u : next_nonempty(W.nonempty, 0u);
+      const uint32_t dlo = (uint32_t) (uint64_t) delta, dhi = (uint32_t) ((uint64_t) delta >> 32);
+      ChunkBatch<U> A, B;
+      uint32_t b0 = 0;
+      plan_big<U, NT>(A, W, b0, total, lane, end, info, dlo, dhi, P.frames);
+      for (;;) {
+        plan_big<U, NT>(B, W, b0 + kStep, total, lane, end, info, dlo, dhi, P.frames);
+        __builtin_amdgcn_sched_barrier(0);
+        run = process_batch<U>(A, run, S, E, hdr, want_rss);
+        if (b0 + kStep >= total) break;
+        plan_big<U, NT>(A, W, b0 + 2 * kStep, total, lane, end, info, dlo, dhi, P.frames);
+        __builtin_amdgcn_sched_barrier(0);
+        run = process_batch<U>(B, run, S, E, hdr, want_rss);
+        b0 += 2 * kStep;
+        if (b0 >= total) break;
       }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const uint32_t endq = pk[u].z, inf = pk[u].w;
-        const uint32_t startq = endq - (inf >> 9);
-        const bool valid = c[u] < total;
-        const bool head = c[u] == startq;
-        const bool tail = c[u] + 1 == endq;
-        const int lo = head ? (int) (inf & 15u) : 0;
-        const int hi = tail ? (int) ((inf >> 4) & 31u) : 16;
-        uint4 v = data[u];
-        if (lo != 0 || hi != 16) {
-          v.x &= dword_keep(lo, hi, 0);
-          v.y &= dword_keep(lo, hi, 1);
-          v.z &= dword_keep(lo, hi, 2);
-          v.w &= dword_keep(lo, hi, 3);
-        }
-        const uint32_t s = chunk_sum(v);
-        const uint32_t incl = wave_incl_scan(s);
-        const uint32_t step_total = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
-        if (valid) {
-          const uint32_t k = c[u] - startq;
-          if (head) sh.S[w][q[u]] = run + incl - s;
-          if (tail) sh.E[w][q[u]] = run + incl;
-          if (want_rss && k < (uint32_t) kHdrChunks) sh.hdr[w][q[u]][k] = v;
-        }
-        run += step_total;
+    } else if (total != 0) {
+      pk[lane] = make_uint4((uint32_t) (uint64_t) delta, (uint32_t) ((uint64_t) delta >> 32), end, info);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      ChunkBatch<U> A, B;
+      uint32_t b0 = 0;
+      plan_batch<U, NT>(A, pk, marks, b0, total, lane, start, nch, ++tag, carry, P.frames);
+      for (;;) {
+        plan_batch<U, NT>(B, pk, marks, b0 + kStep, total, lane, start, nch, ++tag, carry, P.frames);
+        __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's wait
+        run = process_batch<U>(A, run, S, E, hdr, want_rss);
+        if (b0 + kStep >= total) break;
+        plan_batch<U, NT>(A, pk, marks, b0 + 2 * kStep, total, lane, start, nch, ++tag, carry, P.frames);
+        __builtin_amdgcn_sched_barrier(0);
+        run = process_batch<U>(B, run, S, E, hdr, want_rss);
+        b0 += 2 * kStep;
+        if (b0 >= total) break;
       }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 
+    // contiguous tiles record only tail prefixes: a packet starts where the
+    // nearest non-empty packet before it ended (0 at the tile start)
+    uint32_t e_prev = 0;
+    if (contig) {
+      const uint32_t pidx = wave_incl_max(nch ? lane + 1u : 0u);
+      const uint32_t prev = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) pidx, 0x138, 0xf, 0xf, false);  // wave_shr:1
+      e_prev = (lane != 0u && prev != 0u) ? E[prev - 1u] : 0u;
+    }
     if (have) {
-      const uint32_t sum = nch ? (sh.E[w][lane] - sh.S[w][lane]) : 0u;
+      const uint32_t sum = nch ? (E[lane] - (contig ? e_prev : S[lane])) : 0u;
       const uint32_t x = fold16(sum);
       // LE halfword sums at absolute positions == byte-swapped BE sum when the
       // packet starts at an even address (RFC 1071 byte-order independence).
       const uint32_t be = (off & 1) ? x : bswap16(x);
       if (P.out_csum) P.out_csum[pid] = (uint16_t) (~be & 0xFFFFu);
-
       if (want_rss) {
-        const uint8_t* pkt = P.frames + off;
-        uint32_t h = 0;
-        if (P.mode == NICGPU_TUPLE_RAW) {
-          uint32_t cnt = 0;
-          if (P.raw_off < len) {
-            uint32_t e = P.raw_off + P.raw_len;
-            cnt = (e > len ? len : e) - P.raw_off;
-          }
-          h = hash_bytes(0u, sh, w, (int) lane, lo_first, pkt, P.raw_off, cnt, 0);
-        } else if (len >= 14) {
-          uint32_t l3 = 14;
-          uint32_t et = (pkt_byte(sh, w, lane, lo_first, pkt, 12) << 8) | pkt_byte(sh, w, lane, lo_first, pkt, 13);
-          bool ok = true;
-          for (int t = 0; t < 2 && ok && (et == 0x8100u || et == 0x88A8u); ++t) {
-            if (len < l3 + 4) {
-              ok = false;
-            } else {
-              et = (pkt_byte(sh, w, lane, lo_first, pkt, l3 + 2) << 8) | pkt_byte(sh, w, lane, lo_first, pkt, l3 + 3);
-              l3 += 4;
-            }
-          }
-          if (ok && et == 0x0800u && len >= l3 + 20) {
-            uint32_t vihl = pkt_byte(sh, w, lane, lo_first, pkt, l3);
-            uint32_t ihl = (vihl & 15u) * 4u;
-            if ((vihl >> 4) == 4u && ihl >= 20u) {
-              h = hash_bytes(0u, sh, w, (int) lane, lo_first, pkt, l3 + 12, 8, 0);
-              uint32_t proto = pkt_byte(sh, w, lane, lo_first, pkt, l3 + 9);
-              uint32_t frag = ((pkt_byte(sh, w, lane, lo_first, pkt, l3 + 6) << 8) |
-                               pkt_byte(sh, w, lane, lo_first, pkt, l3 + 7)) & 0x3FFFu;
-              uint32_t l4 = l3 + ihl;
-              if ((proto == 6u || proto == 17u) && frag == 0u && l4 + 4u <= len)
-                h = hash_bytes(h, sh, w, (int) lane, lo_first, pkt, l4, 4, 8);
-            }
-          } else if (ok && et == 0x86DDu && len >= l3 + 40) {
-            uint32_t vb = pkt_byte(sh, w, lane, lo_first, pkt, l3);
-            if ((vb >> 4) == 6u) {
-              h = hash_bytes(0u, sh, w, (int) lane, lo_first, pkt, l3 + 8, 32, 0);
-              uint32_t nh = pkt_byte(sh, w, lane, lo_first, pkt, l3 + 6);
-              if ((nh == 6u || nh == 17u) && l3 + 44u <= len)
-                h = hash_bytes(h, sh, w, (int) lane, lo_first, pkt, l3 + 40, 4, 32);
-            }
-          }
-        }
+        const uint32_t h = rss_hash_packet(P, lut, hdr + lane * kHdrChunks, lo_first, P.frames + off, len);
         const uint32_t idx = h % P.table_n;
         if (P.out_hash) P.out_hash[pid] = h;
         if (P.out_queue) P.out_queue[pid] = P.table[idx];
         if (P.out_hits) {
-          if (hist_lds) atomicAdd(&sh.hist[idx], 1u);
+          if (hist_lds) atomicAdd(&hist[idx], 1u);
           else atomicAdd(&P.out_hits[idx], 1ull);
         }
       }
     }
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   }
 
   if (hist_lds) {
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < P.table_n; i += kBlock) {
-      uint32_t v = sh.hist[i];
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) {
+      uint32_t v = hist[i];
       if (v) atomicAdd(&P.out_hits[i], (unsigned long long) v);
     }
   }
@@ -438,12 +739,36 @@ __global__ __launch_bounds__(kBlock) void tso_checksum_kernel(TsoParams P) {
 }
 
 // ------------------------------------------------------------ host side --
+// Kernel variants: (loads in flight per lane U, nontemporal loads, waves per
+// block).  Variant 0 is the production choice (tools/tune_rx.py measures the
+// others against it on the GPU; DESIGN.md §4 records the result).
+struct RxVariant {
+  void (*kernel)(RxParams);
+  int unroll;
+  int wpb;
+  const char* name;
+};
+
+const RxVariant kRxVariants[] = {
+    {rx_offload_kernel<2, true, 4, false, true>, 2, 4, "u2_nt1_w4_c"},
+    {rx_offload_kernel<4, true, 4, false, true>, 4, 4, "u4_nt1_w4_c"},
+    {rx_offload_kernel<4, false, 4, false, true>, 4, 4, "u4_nt0_w4_c"},
+    {rx_offload_kernel<1, true, 8, false, true>, 1, 8, "u1_nt1_w8_c"},
+    {rx_offload_kernel<2, true, 4, false, false>, 2, 4, "u2_nt1_w4"},
+    {rx_offload_kernel<1, false, 8, false, false>, 1, 8, "u1_nt0_w8"},
+    {rx_offload_kernel<8, true, 2, false, true>, 8, 2, "u8_nt1_w2_c"},
+    {rx_offload_kernel<2, false, 8, false, true>, 2, 8, "u2_nt0_w8_c"},
+};
+constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
+
 struct DeviceInfo {
   bool init = false;
   int status = 0;
   int cus = 0;
-  int rx_blocks_per_cu = 0;
   int tso_blocks_per_cu = 0;
+  // occupancy cache per (variant, dynamic LDS bytes)
+  struct Occ { int variant; uint32_t lds; int blocks; };
+  std::vector<Occ> occ;
 };
 
 std::mutex g_mu;
@@ -461,11 +786,21 @@ const DeviceInfo& device_info(int dev) {
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) { di.status = NICGPU_ERR_NO_DEVICE; return di; }
   di.cus = prop.multiProcessorCount;
   int b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rx_offload_kernel, kBlock, 0) != hipSuccess || b < 1) b = 1;
-  di.rx_blocks_per_cu = b;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tso_checksum_kernel, kBlock, 0) != hipSuccess || b < 1) b = 1;
   di.tso_blocks_per_cu = b;
   return di;
+}
+
+int rx_blocks_per_cu(int dev, int variant, uint32_t lds) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceInfo& di = g_dev[dev & 63];
+  for (const auto& o : di.occ)
+    if (o.variant == variant && o.lds == lds) return o.blocks;
+  int b = 0;
+  const RxVariant& v = kRxVariants[variant];
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, v.kernel, kWave * v.wpb, lds) != hipSuccess || b < 1) b = 1;
+  di.occ.push_back({variant, lds, b});
+  return b;
 }
 
 int current_device_info(const DeviceInfo** out) {
@@ -517,6 +852,22 @@ int ensure_table(nicgpu_rss_ctx* ctx, size_t n) {
   if (hipMalloc(&ctx->d_table, n * sizeof(uint16_t)) != hipSuccess) return NICGPU_ERR_NOMEM;
   ctx->table_cap = n;
   return NICGPU_OK;
+}
+
+int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t stream) {
+  if (variant < 0 || variant >= kNumRxVariants) return NICGPU_ERR_INVALID;
+  const RxVariant& v = kRxVariants[variant];
+  const bool rss = P.mode != NICGPU_TUPLE_NONE;
+  const uint32_t hist_n = (P.out_hits && P.table_n <= (uint32_t) kHistLds) ? P.table_n : 0u;
+  const uint32_t lds = rx_lds_bytes(v.wpb, v.unroll, rss, rss ? P.lut_words : 0u, hist_n);
+  int dev = 0;
+  (void) hipGetDevice(&dev);
+  const uint64_t ntiles = (P.n + kWave - 1) / kWave;
+  const uint64_t want = (ntiles + v.wpb - 1) / (uint64_t) v.wpb;
+  const uint64_t cap = (uint64_t) di.cus * (uint64_t) rx_blocks_per_cu(dev, variant, lds);
+  const unsigned grid = (unsigned) (want < cap ? want : cap);
+  hipLaunchKernelGGL(v.kernel, dim3(grid), dim3(kWave * v.wpb), lds, stream, P);
+  return hip_status(hipGetLastError());
 }
 
 }  // namespace
@@ -644,9 +995,12 @@ int nicgpu_rss_info(const nicgpu_rss_ctx* ctx, size_t* key_len, size_t* table_n)
   return NICGPU_OK;
 }
 
-int nicgpu_rx_offload(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n,
-                      int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum,
-                      uint32_t* out_hash, uint16_t* out_queue, uint64_t* out_hits, void* stream) {
+}  // extern "C"
+
+namespace {
+int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n,
+                    int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum, uint32_t* out_hash,
+                    uint16_t* out_queue, uint64_t* out_hits, void* stream) {
   if (tuple_mode != NICGPU_TUPLE_NONE && tuple_mode != NICGPU_TUPLE_AUTO && tuple_mode != NICGPU_TUPLE_RAW)
     return NICGPU_ERR_INVALID;
   if (tuple_mode == NICGPU_TUPLE_RAW && (raw_off > NICGPU_RAW_MAX_END || raw_len > NICGPU_RAW_MAX_END ||
@@ -684,12 +1038,17 @@ int nicgpu_rx_offload(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const ui
     uint32_t max_tuple = tuple_mode == NICGPU_TUPLE_RAW ? raw_len : 36u;
     P.lut_words = 2u * max_tuple * 16u;
   }
-  const uint64_t ntiles = (n + kWave - 1) / kWave;
-  const uint64_t want = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  const uint64_t cap = (uint64_t) di->cus * (uint64_t) di->rx_blocks_per_cu;
-  const unsigned grid = (unsigned) (want < cap ? want : cap);
-  hipLaunchKernelGGL(rx_offload_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
-  return hip_status(hipGetLastError());
+  return launch_rx(P, *di, variant, static_cast<hipStream_t>(stream));
+}
+}  // namespace
+
+extern "C" {
+
+int nicgpu_rx_offload(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n,
+                      int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum,
+                      uint32_t* out_hash, uint16_t* out_queue, uint64_t* out_hits, void* stream) {
+  return rx_offload_impl(0, ctx, frames, desc, n, tuple_mode, raw_off, raw_len, out_csum, out_hash, out_queue,
+                         out_hits, stream);
 }
 
 int nicgpu_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n, uint16_t* out_csum, void* stream) {
@@ -714,3 +1073,114 @@ int nicgpu_tso_checksum(const uint8_t* frames, const uint64_t* desc, const uint1
 }
 
 }  // extern "C"
+
+#ifdef NICGPU_TUNING
+// ------------------------------------------------------------------------
+// Tuning-only entry points (built into libnicgpu_tune.so, never into the
+// product library): run any RX kernel variant, and a read-only streaming
+// kernel that measures this box's HBM read ceiling with the same access width.
+namespace {
+template <int U>
+__global__ __launch_bounds__(256) void stream_read_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                          uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+  uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = add_halves(v[u].w, add_halves(v[u].z, add_halves(v[u].y, add_halves(v[u].x, acc))));
+  }
+  for (; i < n16; i += stride) {
+    u32x4 v = p[i];
+    acc = add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, acc))));
+  }
+  if (acc == 0x12345678u) out[0] = acc;  // keep the loads live
+}
+
+// lane l of a wave reads the 32-B pair (2l, 2l+1) of each 2-KiB step
+__global__ __launch_bounds__(256) void stream_read_pairs_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                                uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wid = ((uint64_t) blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nw = ((uint64_t) gridDim.x * blockDim.x) >> 6;
+  for (uint64_t step = wid; step * 128 + 127 < n16; step += nw) {
+    const u32x4* q = p + step * 128 + 2 * lane;
+    u32x4 a = __builtin_nontemporal_load(q);
+    u32x4 b = __builtin_nontemporal_load(q + 1);
+    acc = add_halves(a.w, add_halves(a.z, add_halves(a.y, add_halves(a.x, acc))));
+    acc = add_halves(b.w, add_halves(b.z, add_halves(b.y, add_halves(b.x, acc))));
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// tile-per-wave streaming (the RX kernel's access pattern without its compute):
+// wave w streams region [t*R, (t+1)*R) for tiles t = w, w + nwaves, ...; each
+// step every lane loads 16 B (1 KiB per wave), U steps in flight.
+template <int U>
+__global__ __launch_bounds__(256) void stream_read_tiles_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                                uint64_t tile16, uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wid = ((uint64_t) blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nw = ((uint64_t) gridDim.x * blockDim.x) >> 6;
+  const uint64_t ntiles = n16 / tile16;
+  for (uint64_t t = wid; t < ntiles; t += nw) {
+    const u32x4* q = p + t * tile16 + lane;
+    for (uint64_t st = 0; st + 64 * U <= tile16; st += 64 * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = q[st + 64 * u];
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc = add_halves(v[u].w, add_halves(v[u].z, add_halves(v[u].y, add_halves(v[u].x, acc))));
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+}  // namespace
+
+extern "C" {
+int nicgpu_tune_stream_tiles(const uint8_t* buf, size_t bytes, size_t tile_bytes, int blocks_per_cu, int unroll,
+                             uint32_t* out, void* stream) {
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  const unsigned grid = (unsigned) (di->cus * (blocks_per_cu > 0 ? blocks_per_cu : 4));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const u32x4* p = reinterpret_cast<const u32x4*>(buf);
+  const uint64_t t16 = tile_bytes / 16;
+  if (unroll == 4) hipLaunchKernelGGL(stream_read_tiles_kernel<4>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  else if (unroll == 2) hipLaunchKernelGGL(stream_read_tiles_kernel<2>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  else hipLaunchKernelGGL(stream_read_tiles_kernel<1>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  return hip_status(hipGetLastError());
+}
+int nicgpu_tune_num_variants(void) { return kNumRxVariants; }
+const char* nicgpu_tune_variant_name(int v) { return (v >= 0 && v < kNumRxVariants) ? kRxVariants[v].name : ""; }
+int nicgpu_tune_rx_offload(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc,
+                           size_t n, int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum,
+                           uint32_t* out_hash, uint16_t* out_queue, uint64_t* out_hits, void* stream) {
+  return rx_offload_impl(variant, ctx, frames, desc, n, tuple_mode, raw_off, raw_len, out_csum, out_hash,
+                         out_queue, out_hits, stream);
+}
+// blocks_per_cu 0 = occupancy maximum; unroll in {1, 4, 8}
+int nicgpu_tune_stream_read(const uint8_t* buf, size_t bytes, int blocks_per_cu, int unroll, uint32_t* out,
+                            void* stream) {
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  const uint64_t n16 = bytes / 16;
+  const int bpc = blocks_per_cu > 0 ? blocks_per_cu : 8;
+  const unsigned grid = (unsigned) (di->cus * bpc);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const u32x4* p = reinterpret_cast<const u32x4*>(buf);
+  if (unroll == 2) hipLaunchKernelGGL(stream_read_pairs_kernel, dim3(grid), dim3(256), 0, s, p, n16, out);
+  else if (unroll == 8) hipLaunchKernelGGL(stream_read_kernel<8>, dim3(grid), dim3(256), 0, s, p, n16, out);
+  else if (unroll == 4) hipLaunchKernelGGL(stream_read_kernel<4>, dim3(grid), dim3(256), 0, s, p, n16, out);
+  else hipLaunchKernelGGL(stream_read_kernel<1>, dim3(grid), dim3(256), 0, s, p, n16, out);
+  return hip_status(hipGetLastError());
+}
+}  // extern "C"
+#endif  // NICGPU_TUNING

@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""A/B every RX kernel variant of libnicgpu_tune.so in ONE process, interleaved
+rounds (cdna_hip_programming.md §5.4 rule 24), on the bench workloads, plus the
+read-only streaming ceiling of this box.  Tuning infrastructure only.
+
+Prints a JSON summary (median per-launch µs, GB/s of algorithmic bytes, % of
+the 8 TB/s spec peak and of the measured read ceiling) and checks every variant
+bit-exactly against variant 0.
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+MS_KEY = bytes.fromhex("6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c6a42b73bbeac01fa")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--workloads", default="c2,imix,u64")
+    ap.add_argument("--variants", default="all")
+    args = ap.parse_args()
+
+    import torch
+
+    import smart_nic_amd as sna
+    from smart_nic_amd import pktgen
+
+    tl = ctypes.CDLL(os.path.join(ROOT, "smart_nic_amd", "libnicgpu_tune.so"))
+    vp, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
+    tl.nicgpu_tune_num_variants.restype = i32
+    tl.nicgpu_tune_variant_name.restype = ctypes.c_char_p
+    tl.nicgpu_tune_variant_name.argtypes = [i32]
+    tl.nicgpu_tune_rx_offload.restype = i32
+    tl.nicgpu_tune_rx_offload.argtypes = [i32, vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp]
+    tl.nicgpu_tune_stream_read.restype = i32
+    tl.nicgpu_tune_stream_read.argtypes = [vp, sz, i32, i32, vp, vp]
+    nv = tl.nicgpu_tune_num_variants()
+    names = [tl.nicgpu_tune_variant_name(i).decode() for i in range(nv)]
+    variants = list(range(nv)) if args.variants == "all" else [int(x) for x in args.variants.split(",")]
+
+    torch.cuda.set_device(0)
+    stream = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    # contexts must come from the tuning library (its own nicgpu_rss_ctx)
+    h = ctypes.c_void_p()
+    tl.nicgpu_rss_create.argtypes = [ctypes.POINTER(vp), i32]
+    tl.nicgpu_rss_set_key.argtypes = [vp, vp, sz, vp]
+    tl.nicgpu_rss_set_table.argtypes = [vp, vp, sz, vp]
+    assert tl.nicgpu_rss_create(ctypes.byref(h), 0) == 0
+    key = (ctypes.c_uint8 * 40).from_buffer_copy(MS_KEY)
+
+    out = {"variants": names, "workloads": {}}
+    rng = np.random.default_rng(0)
+    wls = []
+    for w in args.workloads.split(","):
+        if w == "c2":
+            wls.append(("c2_1518", np.full(1 << 20, 1518), 4, 6))
+        elif w == "imix":
+            wls.append(("c3_imix_16q", pktgen.imix_lengths(4 << 20, rng), 16, 17))
+        elif w == "u64":
+            wls.append(("u64", np.full(4 << 20, 64), 4, 17))
+        elif w == "jumbo":
+            wls.append(("jumbo_9000", np.full(160_000, 9000), 4, 6))
+
+    ceiling_buf = None
+    for name, lens, nq, proto in wls:
+        t0 = time.time()
+        frames, desc, _ = pktgen.make_batch(lens, seed=7, proto=proto, corrupt_frac=0.01)
+        print(f"# {name}: generated {desc.size} pkts in {time.time()-t0:.1f}s", file=sys.stderr, flush=True)
+        n = desc.size
+        table = (np.arange(128) % nq).astype(np.uint16)
+        assert tl.nicgpu_rss_set_key(h, key, 40, sp) == 0
+        assert tl.nicgpu_rss_set_table(h, table.ctypes.data, 128, sp) == 0
+        f = torch.from_numpy(frames).cuda()
+        d = torch.from_numpy(desc.view(np.int64)).cuda()
+        if ceiling_buf is None or f.numel() > ceiling_buf.numel():
+            ceiling_buf = f
+        cs = torch.empty(n, dtype=torch.int16, device="cuda")
+        hs = torch.empty(n, dtype=torch.int32, device="cuda")
+        qs = torch.empty(n, dtype=torch.int16, device="cuda")
+        hits = torch.zeros(128, dtype=torch.int64, device="cuda")
+        alg = int(lens.sum()) + 16 * n
+
+        def run(v, mode=sna.TUPLE_AUTO):
+            st = tl.nicgpu_tune_rx_offload(v, h, f.data_ptr(), d.data_ptr(), n, mode, 0, 0, cs.data_ptr(),
+                                           hs.data_ptr() if mode else None, qs.data_ptr() if mode else None,
+                                           hits.data_ptr() if mode else None, sp)
+            assert st == 0, st
+
+        # correctness vs variant 0
+        run(0)
+        torch.cuda.synchronize()
+        ref = (cs.clone(), hs.clone(), qs.clone())
+        for v in variants:
+            run(v)
+            torch.cuda.synchronize()
+            assert torch.equal(cs, ref[0]) and torch.equal(hs, ref[1]) and torch.equal(qs, ref[2]), names[v]
+        times = {v: [] for v in variants}
+        times_csum = {v: [] for v in variants}
+        for r in range(args.rounds):
+            for v in variants:
+                for mode, bucket in ((sna.TUPLE_AUTO, times), (sna.TUPLE_NONE, times_csum)):
+                    run(v, mode)
+                    e = [torch.cuda.Event(enable_timing=True) for _ in range(args.iters + 1)]
+                    e[0].record()
+                    for i in range(args.iters):
+                        run(v, mode)
+                        e[i + 1].record()
+                    torch.cuda.synchronize()
+                    bucket[v] += [e[i].elapsed_time(e[i + 1]) * 1e3 for i in range(args.iters)]
+        res = {}
+        for v in variants:
+            med = float(np.median(times[v]))
+            medc = float(np.median(times_csum[v]))
+            res[names[v]] = {
+                "us_median": round(med, 2), "us_min": round(float(np.min(times[v])), 2),
+                "alg_gbs": round(alg / med / 1e3, 1), "frac_spec": round(alg / med / 1e3 / 8000, 4),
+                "csum_only_us": round(medc, 2), "csum_only_gbs": round((int(lens.sum()) + 10 * n) / medc / 1e3, 1),
+                "mpkts": round(n / med, 1),
+            }
+        out["workloads"][name] = {"packets": n, "alg_bytes": alg, "results": res}
+        print(json.dumps({name: res}), file=sys.stderr, flush=True)
+        del f, d
+
+    # read-only streaming ceiling on the largest buffer
+    if ceiling_buf is not None:
+        nbytes = ceiling_buf.numel() // 16 * 16
+        sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ceil = {}
+        for unroll in (1, 2, 4, 8):
+            for bpc in (2, 4, 8):
+                ts = []
+                for _ in range(args.rounds * 2):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    assert tl.nicgpu_tune_stream_read(ceiling_buf.data_ptr(), nbytes, bpc, unroll, sink.data_ptr(), sp) == 0
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ts.append(e0.elapsed_time(e1) * 1e3)
+                med = float(np.median(ts))
+                ceil[f"u{unroll}_bpc{bpc}"] = round(nbytes / med / 1e3, 1)
+        tl.nicgpu_tune_stream_tiles.restype = i32
+        tl.nicgpu_tune_stream_tiles.argtypes = [vp, sz, sz, i32, i32, vp, vp]
+        tiles = {}
+        for tile_kb in (4, 24, 96, 384):
+            for unroll in (1, 2, 4):
+                for bpc in (4, 6, 8):
+                    ts = []
+                    for _ in range(args.rounds):
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        assert tl.nicgpu_tune_stream_tiles(ceiling_buf.data_ptr(), nbytes, tile_kb * 1024, bpc, unroll,
+                                                           sink.data_ptr(), sp) == 0
+                        e1.record()
+                        torch.cuda.synchronize()
+                        ts.append(e0.elapsed_time(e1) * 1e3)
+                    med = float(np.median(ts))
+                    used = nbytes // (tile_kb * 1024) * (tile_kb * 1024)
+                    tiles[f"t{tile_kb}k_u{unroll}_bpc{bpc}"] = round(used / med / 1e3, 1)
+        out["tile_stream_gbs"] = tiles
+        out["read_ceiling_gbs"] = ceil
+        best = max(ceil.values())
+        out["read_ceiling_best_gbs"] = best
+        for wl in out["workloads"].values():
+            for r in wl["results"].values():
+                r["frac_ceiling"] = round(r["alg_gbs"] / best, 4)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
