@@ -1,0 +1,83 @@
+// nic/rss.h — Toeplitz RSS engine of the smart_nic model.
+//
+// Drop-in for rosslwheeler/smart_nic include/nic/rss.h:13-48: the same
+// RssConfig / RssStats / RssEngine public surface and semantics
+// (src/rss.cpp:17-114) — 20-byte default key, 128-entry all-zero default
+// table, queue = table[hash % table.size()], Toeplitz windows taken at key bit
+// (bit + k) % key_bits (wraps for inputs longer than the key), stats counting
+// every hash() and select_queue() call, queue_hits indexed by table index and
+// sized only at construction / reset_stats().  Like the reference, the const
+// methods update mutable stats, so one engine must not be shared by threads.
+//
+// Added: select_queue_batch(), the same classification for every packet of a
+// device-resident batch in one GPU launch (fused with the RX checksum), with
+// the stats updated exactly as the equivalent sequence of select_queue calls.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <optional>
+#include <span>
+#include <vector>
+
+#include "nic/gpu_batch.h"
+
+namespace nic {
+
+struct RssConfig {
+  std::vector<std::uint8_t> key;     ///< Toeplitz key bytes
+  std::vector<std::uint16_t> table;  ///< indirection table: hash % size -> queue id
+};
+
+struct RssStats {
+  std::uint64_t hashes{0};
+  std::vector<std::uint64_t> queue_hits;  ///< hits per table index
+};
+
+namespace detail {
+struct RssGpuState;
+struct RssHostLut;
+}  // namespace detail
+
+class RssEngine {
+public:
+  RssEngine();
+  explicit RssEngine(RssConfig config);
+
+  void set_key(std::vector<std::uint8_t> key);
+  void set_table(std::vector<std::uint16_t> table);
+
+  [[nodiscard]] std::uint32_t hash(std::span<const std::uint8_t> data) const;
+
+  /// Queue for `data`; nullopt only for an empty table (never after construction).
+  [[nodiscard]] std::optional<std::uint16_t> select_queue(std::span<const std::uint8_t> data) const;
+
+  [[nodiscard]] const RssConfig& config() const noexcept { return config_; }
+  [[nodiscard]] const RssStats& stats() const noexcept { return stats_; }
+  void reset_stats() noexcept;
+
+  /// GPU batch (new): for every packet i of `batch`, extract the tuple per
+  /// `tuple`, then out.hash[i] = hash(tuple), out.queue[i] = table[hash % n],
+  /// and out.checksum[i] = compute_checksum(frame i) in the same pass.  Runs on
+  /// the current HIP device; stats are updated as if select_queue had been
+  /// called once per packet (hashes += count, queue_hits[idx] += hits for
+  /// idx < queue_hits.size()), which requires waiting for the launch: the call
+  /// is synchronous on `stream` unless update_stats is false.  Throws
+  /// nic::GpuError.
+  void select_queue_batch(const DevicePacketBatch& batch, const TupleSpec& tuple,
+                          const RxBatchOutputs& out, void* stream = nullptr,
+                          bool update_stats = true) const;
+
+private:
+  RssConfig config_;
+  mutable RssStats stats_;
+  mutable std::shared_ptr<detail::RssGpuState> gpu_;      // device key LUT + table (lazy)
+  mutable std::shared_ptr<const detail::RssHostLut> lut_;  // host byte LUT (lazy)
+
+  [[nodiscard]] std::uint32_t toeplitz_hash(std::span<const std::uint8_t> key,
+                                            std::span<const std::uint8_t> data) const;
+  void ensure_defaults();
+};
+
+}  // namespace nic

@@ -74,6 +74,17 @@ const char* nicgpu_strerror(int status);
 /* Number of visible gfx950 devices (>= 0) or a negative status. */
 int nicgpu_device_count(void);
 
+/* Minimal device-memory plumbing for host layers that must not include HIP
+ * headers (libnic_host.so).  Operate on the current HIP device. */
+int nicgpu_get_device(int* device);
+int nicgpu_set_device(int device);
+int nicgpu_malloc(void** dev_ptr, size_t bytes);
+int nicgpu_free(void* dev_ptr);
+int nicgpu_memset_async(void* dev_ptr, int value, size_t bytes, void* stream);
+/* Copies in any direction (hipMemcpyDefault), enqueued on `stream`. */
+int nicgpu_memcpy_async(void* dst, const void* src, size_t bytes, void* stream);
+int nicgpu_stream_synchronize(void* stream);
+
 /* RSS context: the uploaded Toeplitz key (as a nibble lookup table of 32-bit
  * key windows, built on the device) and indirection table, on one device.
  * One context per stream/thread; contexts are not internally locked. */

@@ -36,6 +36,13 @@ ABI_SYMBOLS = (
     "nicgpu_abi_version",
     "nicgpu_strerror",
     "nicgpu_device_count",
+    "nicgpu_get_device",
+    "nicgpu_set_device",
+    "nicgpu_malloc",
+    "nicgpu_free",
+    "nicgpu_memset_async",
+    "nicgpu_memcpy_async",
+    "nicgpu_stream_synchronize",
     "nicgpu_rss_create",
     "nicgpu_rss_destroy",
     "nicgpu_rss_set_key",

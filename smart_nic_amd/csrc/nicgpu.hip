@@ -898,6 +898,38 @@ int nicgpu_device_count(void) {
   return count;
 }
 
+int nicgpu_get_device(int* device) {
+  if (!device) return NICGPU_ERR_INVALID;
+  return hipGetDevice(device) == hipSuccess ? NICGPU_OK : NICGPU_ERR_NO_DEVICE;
+}
+
+int nicgpu_set_device(int device) { return hipSetDevice(device) == hipSuccess ? NICGPU_OK : NICGPU_ERR_NO_DEVICE; }
+
+int nicgpu_malloc(void** dev_ptr, size_t bytes) {
+  if (!dev_ptr) return NICGPU_ERR_INVALID;
+  *dev_ptr = nullptr;
+  if (bytes == 0) return NICGPU_OK;
+  return hipMalloc(dev_ptr, bytes) == hipSuccess ? NICGPU_OK : NICGPU_ERR_NOMEM;
+}
+
+int nicgpu_free(void* dev_ptr) { return (!dev_ptr || hipFree(dev_ptr) == hipSuccess) ? NICGPU_OK : NICGPU_ERR_HIP; }
+
+int nicgpu_memset_async(void* dev_ptr, int value, size_t bytes, void* stream) {
+  if (bytes == 0) return NICGPU_OK;
+  if (!dev_ptr) return NICGPU_ERR_INVALID;
+  return hip_status(hipMemsetAsync(dev_ptr, value, bytes, static_cast<hipStream_t>(stream)));
+}
+
+int nicgpu_memcpy_async(void* dst, const void* src, size_t bytes, void* stream) {
+  if (bytes == 0) return NICGPU_OK;
+  if (!dst || !src) return NICGPU_ERR_INVALID;
+  return hip_status(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, static_cast<hipStream_t>(stream)));
+}
+
+int nicgpu_stream_synchronize(void* stream) {
+  return hip_status(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+}
+
 int nicgpu_rss_create(nicgpu_rss_ctx** out, int device) {
   if (!out) return NICGPU_ERR_INVALID;
   *out = nullptr;

@@ -1,0 +1,154 @@
+// gpu_batch_test.cpp — the GPU batch entry points of the nic:: API against
+// the same API's per-packet calls (and therefore against the reference
+// semantics pinned by host_api_test).  Needs an MI355X.
+//
+// nic::compute_checksum_batch        vs nic::compute_checksum per frame
+// nic::RssEngine::select_queue_batch vs nic::RssEngine::select_queue per tuple,
+//                                       including RssStats after the batch.
+#undef NDEBUG
+#include <cassert>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "nic/checksum.h"
+#include "nic/rss.h"
+#include "nicgpu.h"
+#include "oracle.h"
+
+using namespace nic;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  explicit DevBuf(std::size_t n) { assert(nicgpu_malloc(&p, n ? n : 16) == NICGPU_OK); }
+  ~DevBuf() { nicgpu_free(p); }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+template <class T>
+void to_dev(const DevBuf& d, const std::vector<T>& v) {
+  assert(nicgpu_memcpy_async(d.p, v.data(), v.size() * sizeof(T), nullptr) == NICGPU_OK);
+  assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+}
+
+template <class T>
+std::vector<T> from_dev(const DevBuf& d, std::size_t n) {
+  std::vector<T> v(n);
+  assert(nicgpu_memcpy_async(v.data(), d.p, n * sizeof(T), nullptr) == NICGPU_OK);
+  assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+  return v;
+}
+
+// Eth/IPv4/TCP-ish frames with random fields, packed at random byte offsets.
+void make_batch(std::mt19937_64& rng, std::size_t n, std::vector<std::uint8_t>& frames, std::vector<std::uint64_t>& desc) {
+  frames.clear();
+  desc.clear();
+  for (std::size_t i = 0; i < n; ++i) {
+    std::size_t len = (rng() % 3 == 0) ? rng() % 60 : 54 + rng() % 1500;
+    if (rng() % 50 == 0) len = 0;
+    const std::size_t gap = (rng() % 4 == 0) ? rng() % 16 : (16 - frames.size() % 16) % 16;
+    for (std::size_t g = 0; g < gap; ++g) frames.push_back(static_cast<std::uint8_t>(rng()));
+    const std::size_t off = frames.size();
+    for (std::size_t b = 0; b < len; ++b) frames.push_back(static_cast<std::uint8_t>(rng()));
+    if (len >= 38 && rng() % 4 != 0) {
+      std::uint8_t* f = frames.data() + off;
+      f[12] = 0x08; f[13] = 0x00; f[14] = 0x45; f[20] = 0x40; f[21] = 0; f[23] = (rng() & 1) ? 6 : 17;
+    }
+    desc.push_back(NICGPU_DESC(off, len));
+  }
+  frames.resize(frames.size() + 64, 0);
+}
+
+void test_checksum_batch(std::mt19937_64& rng) {
+  std::vector<std::uint8_t> frames;
+  std::vector<std::uint64_t> desc;
+  make_batch(rng, 5000, frames, desc);
+  DevBuf f(frames.size()), d(desc.size() * 8), o(desc.size() * 2);
+  to_dev(f, frames);
+  to_dev(d, desc);
+  compute_checksum_batch(DevicePacketBatch{f.as<std::byte>(), d.as<std::uint64_t>(), desc.size()}, o.as<std::uint16_t>());
+  auto got = from_dev<std::uint16_t>(o, desc.size());
+  for (std::size_t i = 0; i < desc.size(); ++i) {
+    const std::size_t off = desc[i] & ((1ull << 40) - 1), len = desc[i] >> 40;
+    const auto* p = reinterpret_cast<const std::byte*>(frames.data() + off);
+    assert(got[i] == compute_checksum(std::span<const std::byte>(p, len)));
+  }
+}
+
+void test_select_queue_batch(std::mt19937_64& rng, const std::vector<std::uint8_t>& key, std::vector<std::uint16_t> table,
+                             TupleSpec tuple) {
+  std::vector<std::uint8_t> frames;
+  std::vector<std::uint64_t> desc;
+  make_batch(rng, 4000, frames, desc);
+  const std::size_t n = desc.size();
+  DevBuf f(frames.size()), d(n * 8), cs(n * 2), hs(n * 4), qs(n * 2);
+  to_dev(f, frames);
+  to_dev(d, desc);
+  RssEngine gpu_engine{RssConfig{key, table}};
+  RssEngine cpu_engine{RssConfig{key, table}};
+  const DevicePacketBatch batch{f.as<std::byte>(), d.as<std::uint64_t>(), n};
+  gpu_engine.select_queue_batch(batch, tuple, RxBatchOutputs{cs.as<std::uint16_t>(), hs.as<std::uint32_t>(), qs.as<std::uint16_t>()});
+  auto c = from_dev<std::uint16_t>(cs, n);
+  auto h = from_dev<std::uint32_t>(hs, n);
+  auto q = from_dev<std::uint16_t>(qs, n);
+  RssEngine probe{RssConfig{key, table}};
+  for (std::size_t i = 0; i < n; ++i) {
+    const std::size_t off = desc[i] & ((1ull << 40) - 1), len = desc[i] >> 40;
+    const std::uint8_t* p = frames.data() + off;
+    std::uint8_t t[64];
+    const std::size_t tl = oracle_extract_tuple(p, len, static_cast<int>(tuple.mode), tuple.raw_offset, tuple.raw_length, t);
+    const std::span<const std::uint8_t> sp(t, tl);
+    assert(c[i] == compute_checksum(std::span<const std::byte>(reinterpret_cast<const std::byte*>(p), len)));
+    assert(h[i] == probe.hash(sp));
+    assert(q[i] == *cpu_engine.select_queue(sp));
+  }
+  // stats identical to n sequential select_queue calls
+  assert(gpu_engine.stats().hashes == cpu_engine.stats().hashes);
+  assert(gpu_engine.stats().queue_hits == cpu_engine.stats().queue_hits);
+  // a second batch accumulates
+  gpu_engine.select_queue_batch(batch, tuple, RxBatchOutputs{nullptr, nullptr, qs.as<std::uint16_t>()});
+  assert(gpu_engine.stats().hashes == 2 * n);
+  // set_table invalidates the device table; queue_hits keeps its size
+  std::vector<std::uint16_t> t2(table.size() + 50, 7);
+  gpu_engine.set_table(t2);
+  gpu_engine.select_queue_batch(batch, tuple, RxBatchOutputs{nullptr, nullptr, qs.as<std::uint16_t>()});
+  auto q2 = from_dev<std::uint16_t>(qs, n);
+  for (auto v : q2) assert(v == 7);
+  assert(gpu_engine.stats().queue_hits.size() == table.size());
+}
+
+void test_errors() {
+  bool threw = false;
+  try {
+    compute_checksum_batch(DevicePacketBatch{reinterpret_cast<const std::byte*>(0x1), nullptr, 3}, nullptr);
+  } catch (const GpuError& e) {
+    threw = e.status() == NICGPU_ERR_INVALID;
+  }
+  assert(threw);
+}
+
+}  // namespace
+
+int main() {
+  assert(gpu_device_count() >= 1);
+  std::mt19937_64 rng(11);
+  test_checksum_batch(rng);
+  const std::vector<std::uint8_t> ms = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
+                                        0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
+                                        0x80, 0x30, 0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
+  std::vector<std::uint16_t> t16(128);
+  for (int i = 0; i < 128; ++i) t16[i] = static_cast<std::uint16_t>(i % 16);
+  test_select_queue_batch(rng, ms, t16, TupleSpec{TupleMode::Auto, 0, 0});
+  test_select_queue_batch(rng, {}, {}, TupleSpec{TupleMode::Auto, 0, 0});         // reference defaults
+  test_select_queue_batch(rng, {}, {0, 1, 2, 3, 4, 5, 6}, TupleSpec{TupleMode::Raw, 26, 36});  // key wrap
+  std::vector<std::uint16_t> big(3000);
+  for (std::size_t i = 0; i < big.size(); ++i) big[i] = static_cast<std::uint16_t>(i);
+  test_select_queue_batch(rng, ms, big, TupleSpec{TupleMode::Auto, 0, 0});        // table > LDS histogram
+  test_errors();
+  std::puts("gpu_batch_test: ok");
+  return 0;
+}
