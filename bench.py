@@ -157,13 +157,16 @@ def main():
 
     # RSS key + table: rank 0's copy, RCCL-broadcast over xGMI to every rank.
     key_dev = torch.tensor(list(MS_KEY), dtype=torch.uint8, device=dev)
-    tab_dev = torch.from_numpy(table.view(np.int16)).to(dev)
+    tab_dev = torch.from_numpy(table.astype(np.int32)).to(dev)
     if dist is not None:
+        from smart_nic_amd import dist as sdist
+
         if rank != 0:
             key_dev.zero_()
             tab_dev.zero_()
-        dist.broadcast(key_dev, src=0)
-        dist.broadcast(tab_dev, src=0)
+        key_dev, tab_dev = sdist.broadcast_rss_config(key_dev, tab_dev, dist)
+    else:
+        tab_dev = tab_dev.to(torch.int16)
     ctx = sna.RssContext(dev)
     ctx.set_key_device(key_dev)
     ctx.set_table_device(tab_dev)

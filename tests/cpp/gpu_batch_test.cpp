@@ -113,12 +113,14 @@ void test_select_queue_batch(std::mt19937_64& rng, const std::vector<std::uint8_
   gpu_engine.select_queue_batch(batch, tuple, RxBatchOutputs{nullptr, nullptr, qs.as<std::uint16_t>()});
   assert(gpu_engine.stats().hashes == 2 * n);
   // set_table invalidates the device table; queue_hits keeps its size
-  std::vector<std::uint16_t> t2(table.size() + 50, 7);
+  const std::size_t hits_size = gpu_engine.stats().queue_hits.size();
+  assert(hits_size == cpu_engine.config().table.size());
+  std::vector<std::uint16_t> t2(hits_size + 50, 7);
   gpu_engine.set_table(t2);
   gpu_engine.select_queue_batch(batch, tuple, RxBatchOutputs{nullptr, nullptr, qs.as<std::uint16_t>()});
   auto q2 = from_dev<std::uint16_t>(qs, n);
   for (auto v : q2) assert(v == 7);
-  assert(gpu_engine.stats().queue_hits.size() == table.size());
+  assert(gpu_engine.stats().queue_hits.size() == hits_size);
 }
 
 void test_errors() {
