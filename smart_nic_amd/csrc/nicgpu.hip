@@ -45,6 +45,7 @@ constexpr int kHdrBytes = kHdrChunks * 16;
 constexpr int kLutPos = 2 * NICGPU_MAX_TUPLE;  // nibble positions
 constexpr int kLutWords = kLutPos * 16;
 constexpr int kHistLds = 1024;     // tables up to this size histogram in LDS
+constexpr int kTableLds = 2048;    // tables up to this size are read from LDS
 constexpr uint64_t kOffMask = (1ull << NICGPU_DESC_OFFSET_BITS) - 1;
 
 const uint8_t kDefaultKey[20] = {0x6D, 0x5A, 0x56, 0x6B, 0x65, 0x4E, 0x67, 0x6E, 0x67, 0x55,
@@ -209,6 +210,29 @@ __device__ __forceinline__ uint32_t rss_hash_packet(const RxParams& P, const uin
     return hash_bytes(0u, lut, hdr_l, lo, pkt, P.raw_off, cnt, 0);
   }
   if (len < 14) return 0;
+  if (lo == 0u && len >= 38u) {
+    // Fast path: 16-B-aligned frame, Eth (no tag) / IPv4 IHL 5 / TCP|UDP, not a
+    // fragment — the first 48 bytes come from LDS in three 16-B reads and the
+    // fields are extracted at constant shifts.
+    const uint4 c0 = hdr_l[0], c1 = hdr_l[1], c2 = hdr_l[2];
+    const uint32_t w3 = c0.w;  // bytes 12..15: ethertype | ver/ihl | tos
+    const uint32_t w5 = c1.y;  // bytes 20..23: flags/frag | ttl | proto
+    const uint32_t proto = w5 >> 24;
+    if ((w3 & 0xFFFFFFu) == 0x450008u && (w5 & 0xFF3Fu) == 0u && (proto == 6u || proto == 17u)) {
+      // tuple = bytes 26..37: src ip 26..29, dst ip 30..33, ports 34..37
+      const uint32_t t0 = (c1.z >> 16) | (c1.w << 16);   // bytes 26..29
+      const uint32_t t1 = (c1.w >> 16) | (c2.x << 16);   // bytes 30..33
+      const uint32_t t2 = (c2.x >> 16) | (c2.y << 16);   // bytes 34..37
+      uint32_t hh = 0;
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        const uint32_t w = i < 4 ? t0 : (i < 8 ? t1 : t2);
+        const uint32_t b = (w >> (8 * (i & 3))) & 0xFFu;
+        hh ^= lut[(2 * i) * 16 + (b >> 4)] ^ lut[(2 * i + 1) * 16 + (b & 15u)];
+      }
+      return hh;
+    }
+  }
   uint32_t l3 = 14;
   uint32_t et = (pkt_byte(hdr_l, lo, pkt, 12) << 8) | pkt_byte(hdr_l, lo, pkt, 13);
   for (int t = 0; t < 2 && (et == 0x8100u || et == 0x88A8u); ++t) {
@@ -289,74 +313,6 @@ __device__ __forceinline__ void plan_batch(ChunkBatch<U>& B, const uint4* __rest
     const uint32_t ce = valid ? c : total - 1u;
     const int64_t dl = (int64_t) (((uint64_t) e.y << 32) | e.x);
     const u32x4* p = reinterpret_cast<const u32x4*>(frames + (uint64_t) ((int64_t) ce + dl) * 16);
-    if constexpr (NT) B.v[u] = __builtin_nontemporal_load(p);
-    else B.v[u] = *p;
-  }
-}
-
-// Wave-uniform walker for tiles whose non-empty packets all span >= 64 chunks
-// (1 KiB+: C2's 1518 B, jumbo).  A 64-chunk step then holds at most two
-// packets — the tail of `qa` and the head of the next non-empty packet — so the
-// chunk -> packet map is one boundary lane index computed in scalar registers
-// (v_readlane of the packet lanes' descriptors, s_ff1 over the non-empty mask)
-// and a select per lane, instead of marks + a DPP max-scan + LDS reads.
-struct BigWalker {
-  uint64_t nonempty;  // ballot(nch > 0)
-  uint32_t qa;        // packet holding the walker's current chunk
-};
-
-__device__ __forceinline__ uint32_t next_nonempty(uint64_t nonempty, uint32_t q) {
-  const uint64_t m = q >= 63 ? 0ull : (nonempty & ~((2ull << q) - 1ull));
-  return m ? (uint32_t) __builtin_ctzll(m) : q;
-}
-
-template <int U, bool NT>
-__device__ __forceinline__ void plan_big(ChunkBatch<U>& B, BigWalker& W, uint32_t base, uint32_t total,
-                                         uint32_t lane, uint32_t v_end, uint32_t v_info, uint32_t v_dlo,
-                                         uint32_t v_dhi, const uint8_t* __restrict__ frames) {
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const uint32_t sb = base + (uint32_t) u * kWave;
-    uint32_t qa = W.qa;
-    uint32_t ea = (uint32_t) __builtin_amdgcn_readlane((int) v_end, (int) qa);
-    while (ea <= sb && ea < total) {
-      qa = next_nonempty(W.nonempty, qa);
-      ea = (uint32_t) __builtin_amdgcn_readlane((int) v_end, (int) qa);
-    }
-    W.qa = qa;
-    const uint32_t infa = (uint32_t) __builtin_amdgcn_readlane((int) v_info, (int) qa);
-    const uint32_t dla = (uint32_t) __builtin_amdgcn_readlane((int) v_dlo, (int) qa);
-    const uint32_t dha = (uint32_t) __builtin_amdgcn_readlane((int) v_dhi, (int) qa);
-    uint32_t b = ea - sb;  // first lane of the next packet (>= 64: none in this step)
-    uint32_t qb = qa, eb = ea, infb = infa, dlb = dla, dhb = dha;
-    if (b < (uint32_t) kWave && ea < total) {
-      qb = next_nonempty(W.nonempty, qa);
-      eb = (uint32_t) __builtin_amdgcn_readlane((int) v_end, (int) qb);
-      infb = (uint32_t) __builtin_amdgcn_readlane((int) v_info, (int) qb);
-      dlb = (uint32_t) __builtin_amdgcn_readlane((int) v_dlo, (int) qb);
-      dhb = (uint32_t) __builtin_amdgcn_readlane((int) v_dhi, (int) qb);
-    } else {
-      b = (uint32_t) kWave;
-    }
-    const bool inA = lane < b;
-    const uint32_t c = sb + lane;
-    const uint32_t q = inA ? qa : qb;
-    const uint32_t endq = inA ? ea : eb;
-    const uint32_t inf = inA ? infa : infb;
-    const uint32_t startq = endq - (inf >> 9);
-    const bool valid = c < total;
-    const bool head = c == startq;
-    const bool tail = c + 1 == endq;
-    const uint32_t lo = head ? (inf & 15u) : 0u;
-    const uint32_t hi = tail ? ((inf >> 4) & 31u) : 16u;
-    const uint32_t k = c - startq;
-    const uint32_t slot = k < (uint32_t) kHdrChunks ? k : 7u;
-    B.q[u] = q;
-    B.meta[u] = lo | (hi << 4) | ((uint32_t) head << 9) | ((uint32_t) tail << 10) | ((uint32_t) valid << 11) |
-                (slot << 12);
-    const uint32_t ce = valid ? c : total - 1u;
-    const uint64_t dl = inA ? (((uint64_t) dha << 32) | dla) : (((uint64_t) dhb << 32) | dlb);
-    const u32x4* p = reinterpret_cast<const u32x4*>(frames + (uint64_t) ((int64_t) ce + (int64_t) dl) * 16);
     if constexpr (NT) B.v[u] = __builtin_nontemporal_load(p);
     else B.v[u] = *p;
   }
@@ -474,170 +430,205 @@ __device__ __forceinline__ uint32_t process_batch(ChunkBatch<U>& B, uint32_t run
   return run;
 }
 
-template <int U, bool NT, int WPB, bool BIG, bool CONTIG>
+// Per-lane view of one tile (lane = one packet).  `total` and `contig` are
+// wave-uniform.
+// (no padding bytes: struct copies with padding leave scratch allocas behind)
+struct Tile {
+  uint64_t id;
+  uint64_t off;
+  int64_t delta;  // first16 - start: chunk c of this packet is absolute chunk c + delta
+  int64_t D;      // common delta of a contiguous tile
+  uint32_t len, nch, start, end, info;
+  uint32_t total;
+  uint32_t contig;  // 0/1
+  uint32_t pad_;
+};
+static_assert(sizeof(Tile) == 64, "Tile must stay padding-free");
+
+template <bool CONTIG>
+__device__ __forceinline__ Tile make_tile(uint64_t id, uint64_t d) {
+  Tile t;
+  t.id = id;
+  t.off = d & kOffMask;
+  t.len = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
+  const uint64_t first16 = t.off >> 4;
+  t.nch = t.len ? (uint32_t) (((t.off + t.len - 1) >> 4) - first16 + 1) : 0u;
+  t.end = wave_incl_scan(t.nch);
+  t.total = (uint32_t) __builtin_amdgcn_readlane((int) t.end, 63);
+  t.start = t.end - t.nch;
+  t.delta = (int64_t) first16 - (int64_t) t.start;
+  const uint32_t lo_first = (uint32_t) (t.off & 15);
+  const uint32_t hi_last = t.len ? (uint32_t) (((t.off + t.len - 1) & 15) + 1) : 16u;
+  t.info = lo_first | (hi_last << 4) | (t.nch << 9);
+  const uint64_t nonempty = __ballot(t.nch != 0u);
+  const int first_ne = nonempty ? __builtin_ctzll(nonempty) : 0;
+  const uint32_t dl = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) (uint64_t) t.delta, first_ne);
+  const uint32_t dh = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) ((uint64_t) t.delta >> 32), first_ne);
+  t.D = (int64_t) (((uint64_t) dh << 32) | dl);
+  t.contig = (CONTIG && __ballot(t.nch != 0u && t.delta != t.D) == 0ull) ? 1u : 0u;
+  t.pad_ = 0;
+  return t;
+}
+
+struct RxLdsPtrs {
+  uint32_t* S;
+  uint32_t* E;
+  uint4* pk;
+  uint32_t* marks;
+  uint32_t* slotsA;
+  uint32_t* slotsB;
+  uint4* hdr;
+  uint32_t* lut;
+  uint32_t* hist;
+  uint16_t* table_s;
+  bool hist_lds, table_lds, want_rss;
+};
+
+// Checksum finish + tuple hash + queue of the tile's packets (one per lane).
+__device__ __forceinline__ void tile_epilogue(const RxParams& P, const RxLdsPtrs& L, const Tile& t, uint32_t lane) {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const uint64_t pid = t.id * kWave + lane;
+  // contiguous tiles record only tail prefixes: a packet starts where the
+  // nearest non-empty packet before it ended (0 at the tile start)
+  uint32_t base_prefix = 0;
+  if (t.contig) {
+    const uint32_t pidx = wave_incl_max(t.nch ? lane + 1u : 0u);
+    const uint32_t prev = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) pidx, 0x138, 0xf, 0xf, false);  // wave_shr:1
+    base_prefix = (lane != 0u && prev != 0u) ? L.E[prev - 1u] : 0u;
+  }
+  if (pid < P.n) {
+    const uint32_t sum = t.nch ? (L.E[lane] - (t.contig ? base_prefix : L.S[lane])) : 0u;
+    const uint32_t x = fold16(sum);
+    // LE halfword sums at absolute positions == byte-swapped BE sum when the
+    // packet starts at an even address (RFC 1071 byte-order independence).
+    const uint32_t be = (t.off & 1) ? x : bswap16(x);
+    if (P.out_csum) P.out_csum[pid] = (uint16_t) (~be & 0xFFFFu);
+    if (L.want_rss) {
+      const uint32_t h =
+          rss_hash_packet(P, L.lut, L.hdr + lane * kHdrChunks, (uint32_t) (t.off & 15), P.frames + t.off, t.len);
+      const uint32_t idx = h % P.table_n;
+      if (P.out_hash) P.out_hash[pid] = h;
+      if (P.out_queue) P.out_queue[pid] = L.table_lds ? L.table_s[idx] : P.table[idx];
+      if (P.out_hits) {
+        if (L.hist_lds) atomicAdd(&L.hist[idx], 1u);
+        else atomicAdd(&P.out_hits[idx], 1ull);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+
+// General tiles (packets not contiguous in chunk space): chunk -> packet by
+// marks + DPP prefix-max, ping-pong over the tile.
+template <int U, bool NT>
+__device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsPtrs& L, const Tile& t, uint32_t lane,
+                                                 uint32_t& tag) {
+  constexpr uint32_t kStep = (uint32_t) kWave * U;
+  L.pk[lane] = make_uint4((uint32_t) (uint64_t) t.delta, (uint32_t) ((uint64_t) t.delta >> 32), t.end, t.info);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  uint32_t run = 0, carry = 0;
+  ChunkBatch<U> A, B;
+  uint32_t b0 = 0;
+  plan_batch<U, NT>(A, L.pk, L.marks, b0, t.total, lane, t.start, t.nch, ++tag, carry, P.frames);
+  for (;;) {
+    plan_batch<U, NT>(B, L.pk, L.marks, b0 + kStep, t.total, lane, t.start, t.nch, ++tag, carry, P.frames);
+    __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's wait
+    run = process_batch<U>(A, run, L.S, L.E, L.hdr, L.want_rss);
+    if (b0 + kStep >= t.total) break;
+    plan_batch<U, NT>(A, L.pk, L.marks, b0 + 2 * kStep, t.total, lane, t.start, t.nch, ++tag, carry, P.frames);
+    __builtin_amdgcn_sched_barrier(0);
+    run = process_batch<U>(B, run, L.S, L.E, L.hdr, L.want_rss);
+    b0 += 2 * kStep;
+    if (b0 >= t.total) break;
+  }
+}
+
+template <int U, bool NT, int WPB, bool CONTIG>
 __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
   extern __shared__ uint4 lds_dyn[];
   const int w = threadIdx.x / kWave;
   const uint32_t lane = lane_id();
-  const bool want_rss = P.mode != NICGPU_TUPLE_NONE;
-  const bool hist_lds = P.out_hits != nullptr && P.table_n <= (uint32_t) kHistLds;
+  constexpr uint32_t kStep = (uint32_t) kWave * U;
 
+  RxLdsPtrs L;
+  L.want_rss = P.mode != NICGPU_TUPLE_NONE;
+  L.hist_lds = P.out_hits != nullptr && P.table_n <= (uint32_t) kHistLds;
+  L.table_lds = L.want_rss && P.table_n <= (uint32_t) kTableLds;
   uint8_t* base_b = reinterpret_cast<uint8_t*>(lds_dyn);
-  uint8_t* wave_b = base_b + (uint32_t) w * rx_wave_lds(want_rss, U);
-  uint32_t* S = reinterpret_cast<uint32_t*>(wave_b);
-  uint32_t* E = S + kWave;
-  uint4* pk = reinterpret_cast<uint4*>(wave_b + kScratchOff);
-  uint32_t* marks = reinterpret_cast<uint32_t*>(wave_b + kScratchOff + kWave * 16);
-  uint32_t* slotsA = reinterpret_cast<uint32_t*>(wave_b + kScratchOff);
-  uint32_t* slotsB = slotsA + kWave * U;
-  uint4* hdr = reinterpret_cast<uint4*>(wave_b + rx_hdr_off(U));
+  uint8_t* wave_b = base_b + (uint32_t) w * rx_wave_lds(L.want_rss, U);
+  L.S = reinterpret_cast<uint32_t*>(wave_b);
+  L.E = L.S + kWave;
+  L.pk = reinterpret_cast<uint4*>(wave_b + kScratchOff);
+  L.marks = reinterpret_cast<uint32_t*>(wave_b + kScratchOff + kWave * 16);
+  L.slotsA = reinterpret_cast<uint32_t*>(wave_b + kScratchOff);
+  L.slotsB = L.slotsA + kWave * U;
+  L.hdr = reinterpret_cast<uint4*>(wave_b + rx_hdr_off(U));
+  L.lut = reinterpret_cast<uint32_t*>(base_b + (uint32_t) WPB * rx_wave_lds(L.want_rss, U));
+  L.hist = L.lut + P.lut_words;
+  L.table_s = reinterpret_cast<uint16_t*>(L.hist + (L.hist_lds ? P.table_n : 0u));
   // marks never match a live tag (tags start at 1; cleared slots read as 0)
-  for (uint32_t i = lane; i < (uint32_t) (kWave * U); i += kWave) marks[i] = 0xFFFFFFFFu;
-  uint32_t tag = 0;  // batch id (never reaches 0x3FFFFFF within a launch)
-  uint32_t* lut = reinterpret_cast<uint32_t*>(base_b + (uint32_t) WPB * rx_wave_lds(want_rss, U));
-  uint32_t* hist = lut + P.lut_words;
+  for (uint32_t i = lane; i < (uint32_t) (kWave * U); i += kWave) L.marks[i] = 0xFFFFFFFFu;
+  uint32_t tag = 0;  // batch id of the general path (never reaches 0x3FFFFFF within a launch)
 
-  if (want_rss) {
-    for (uint32_t i = threadIdx.x; i < P.lut_words; i += kWave * WPB) lut[i] = P.lut[i];
+  if (L.want_rss) {
+    for (uint32_t i = threadIdx.x; i < P.lut_words; i += kWave * WPB) L.lut[i] = P.lut[i];
   }
-  if (hist_lds) {
-    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) hist[i] = 0;
+  if (L.hist_lds) {
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) L.hist[i] = 0;
+  }
+  if (L.table_lds) {
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) L.table_s[i] = P.table[i];
   }
   __syncthreads();
 
   const uint64_t ntiles = (P.n + kWave - 1) / kWave;
   const uint64_t nwaves = (uint64_t) gridDim.x * WPB;
-  uint64_t tile = (uint64_t) blockIdx.x * WPB + w;
-  // descriptor of this lane's packet in the current tile, prefetched one tile ahead
-  uint64_t d_next = 0;
-  if (tile < ntiles && tile * kWave + lane < P.n) d_next = P.desc[tile * kWave + lane];
+  auto desc_of = [&](uint64_t id) __attribute__((always_inline)) -> uint64_t {
+    return (id < ntiles && id * kWave + lane < P.n) ? P.desc[id * kWave + lane] : 0ull;
+  };
+  // descriptors are prefetched one tile ahead
+  uint64_t id0 = (uint64_t) blockIdx.x * WPB + w;
+  uint64_t d_next = desc_of(id0 + nwaves);
+  Tile cur = make_tile<CONTIG>(id0, desc_of(id0));
 
-  for (; tile < ntiles; tile += nwaves) {
-    const uint64_t p0 = tile * kWave;
-    const uint64_t pid = p0 + lane;
-    const bool have = pid < P.n;
-    const uint64_t d = d_next;
-    {
-      const uint64_t nt = tile + nwaves;
-      d_next = (nt < ntiles && nt * kWave + lane < P.n) ? P.desc[nt * kWave + lane] : 0;
-    }
-    const uint64_t off = d & kOffMask;
-    const uint32_t len = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
-    const uint64_t first16 = off >> 4;
-    const uint32_t nch = len ? (uint32_t) (((off + len - 1) >> 4) - first16 + 1) : 0u;
-    const uint32_t end = wave_incl_scan(nch);
-    const uint32_t total = (uint32_t) __builtin_amdgcn_readlane((int) end, 63);
-    const uint32_t start = end - nch;
-    const int64_t delta = (int64_t) first16 - (int64_t) start;
-    const uint32_t lo_first = (uint32_t) (off & 15);
-    const uint32_t hi_last = len ? (uint32_t) (((off + len - 1) & 15) + 1) : 16u;
-    const uint32_t info = lo_first | (hi_last << 4) | (nch << 9);
-
-    // Ping-pong pipeline: batch i+1's loads are in flight while batch i is
-    // reduced.  Every plan is unconditional (a batch past the tile's end just
-    // re-reads its last chunk) so the compiler can count the outstanding loads
-    // (s_waitcnt vmcnt(U)) instead of draining them (vmcnt(0)) at a merge.
-    constexpr uint32_t kStep = (uint32_t) kWave * U;
-    uint32_t run = 0, carry = 0;
-    const uint64_t nonempty = __ballot(nch != 0u);
-    const int first_ne = nonempty ? __builtin_ctzll(nonempty) : 0;
-    const uint32_t d_lo0 = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) (uint64_t) delta, first_ne);
-    const uint32_t d_hi0 = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) ((uint64_t) delta >> 32), first_ne);
-    const int64_t D = (int64_t) (((uint64_t) d_hi0 << 32) | d_lo0);
-    const bool contig = CONTIG && __ballot(nch != 0u && delta != D) == 0ull;
-    const bool big = !contig && BIG && __ballot(nch != 0u && nch < (uint32_t) kWave) == 0ull;
-    if (total != 0 && contig) {
-      for (uint32_t i = lane; i < (uint32_t) (2 * kWave * U); i += kWave) slotsA[i] = 0u;
+  while (cur.id < ntiles) {
+    if (cur.contig && cur.total != 0u) {
+      // Contiguous tile: chunk c is absolute chunk D + c.  Ping-pong: batch
+      // i+1's loads are in flight while batch i is reduced; every plan is
+      // unconditional (a batch past the end re-reads the last chunk) so the
+      // compiler keeps counted vmcnt waits instead of draining at merges.
+      for (uint32_t i = lane; i < (uint32_t) (2 * kWave * U); i += kWave) L.slotsA[i] = 0u;
       __builtin_amdgcn_wave_barrier();
-      const u32x4* tile16 = reinterpret_cast<const u32x4*>(P.frames) + D;
+      const u32x4* tile16 = reinterpret_cast<const u32x4*>(P.frames) + cur.D;
       ContigBatch<U> A, B;
-      uint32_t b0 = 0;
-      plan_contig<U, NT>(A, slotsA, b0, total, lane, start, nch, info, tile16);
+      uint32_t run = 0, b0 = 0;
+      plan_contig<U, NT>(A, L.slotsA, 0, cur.total, lane, cur.start, cur.nch, cur.info, tile16);
       for (;;) {
-        plan_contig<U, NT>(B, slotsB, b0 + kStep, total, lane, start, nch, info, tile16);
-        __builtin_amdgcn_sched_barrier(0);
-        run = process_contig<U>(A, slotsA, run, E, hdr, want_rss, lane);
-        if (b0 + kStep >= total) break;
-        plan_contig<U, NT>(A, slotsA, b0 + 2 * kStep, total, lane, start, nch, info, tile16);
-        __builtin_amdgcn_sched_barrier(0);
-        run = process_contig<U>(B, slotsB, run, E, hdr, want_rss, lane);
-        b0 += 2 * kStep;
-        if (b0 >= total) break;
-      }
-    } else if (total != 0 && big) {
-      BigWalker W{__ballot(nch != 0u), 0u};
-      W.qa = (W.nonempty & 1ull) ? 0u : next_nonempty(W.nonempty, 0u);
-      const uint32_t dlo = (uint32_t) (uint64_t) delta, dhi = (uint32_t) ((uint64_t) delta >> 32);
-      ChunkBatch<U> A, B;
-      uint32_t b0 = 0;
-      plan_big<U, NT>(A, W, b0, total, lane, end, info, dlo, dhi, P.frames);
-      for (;;) {
-        plan_big<U, NT>(B, W, b0 + kStep, total, lane, end, info, dlo, dhi, P.frames);
-        __builtin_amdgcn_sched_barrier(0);
-        run = process_batch<U>(A, run, S, E, hdr, want_rss);
-        if (b0 + kStep >= total) break;
-        plan_big<U, NT>(A, W, b0 + 2 * kStep, total, lane, end, info, dlo, dhi, P.frames);
-        __builtin_amdgcn_sched_barrier(0);
-        run = process_batch<U>(B, run, S, E, hdr, want_rss);
-        b0 += 2 * kStep;
-        if (b0 >= total) break;
-      }
-    } else if (total != 0) {
-      pk[lane] = make_uint4((uint32_t) (uint64_t) delta, (uint32_t) ((uint64_t) delta >> 32), end, info);
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      ChunkBatch<U> A, B;
-      uint32_t b0 = 0;
-      plan_batch<U, NT>(A, pk, marks, b0, total, lane, start, nch, ++tag, carry, P.frames);
-      for (;;) {
-        plan_batch<U, NT>(B, pk, marks, b0 + kStep, total, lane, start, nch, ++tag, carry, P.frames);
+        plan_contig<U, NT>(B, L.slotsB, b0 + kStep, cur.total, lane, cur.start, cur.nch, cur.info, tile16);
         __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's wait
-        run = process_batch<U>(A, run, S, E, hdr, want_rss);
-        if (b0 + kStep >= total) break;
-        plan_batch<U, NT>(A, pk, marks, b0 + 2 * kStep, total, lane, start, nch, ++tag, carry, P.frames);
+        run = process_contig<U>(A, L.slotsA, run, L.E, L.hdr, L.want_rss, lane);
+        if (b0 + kStep >= cur.total) break;
+        plan_contig<U, NT>(A, L.slotsA, b0 + 2 * kStep, cur.total, lane, cur.start, cur.nch, cur.info, tile16);
         __builtin_amdgcn_sched_barrier(0);
-        run = process_batch<U>(B, run, S, E, hdr, want_rss);
+        run = process_contig<U>(B, L.slotsB, run, L.E, L.hdr, L.want_rss, lane);
         b0 += 2 * kStep;
-        if (b0 >= total) break;
+        if (b0 >= cur.total) break;
       }
+    } else if (cur.total != 0u) {
+      run_general_tile<U, NT>(P, L, cur, lane, tag);
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-
-    // contiguous tiles record only tail prefixes: a packet starts where the
-    // nearest non-empty packet before it ended (0 at the tile start)
-    uint32_t e_prev = 0;
-    if (contig) {
-      const uint32_t pidx = wave_incl_max(nch ? lane + 1u : 0u);
-      const uint32_t prev = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) pidx, 0x138, 0xf, 0xf, false);  // wave_shr:1
-      e_prev = (lane != 0u && prev != 0u) ? E[prev - 1u] : 0u;
-    }
-    if (have) {
-      const uint32_t sum = nch ? (E[lane] - (contig ? e_prev : S[lane])) : 0u;
-      const uint32_t x = fold16(sum);
-      // LE halfword sums at absolute positions == byte-swapped BE sum when the
-      // packet starts at an even address (RFC 1071 byte-order independence).
-      const uint32_t be = (off & 1) ? x : bswap16(x);
-      if (P.out_csum) P.out_csum[pid] = (uint16_t) (~be & 0xFFFFu);
-      if (want_rss) {
-        const uint32_t h = rss_hash_packet(P, lut, hdr + lane * kHdrChunks, lo_first, P.frames + off, len);
-        const uint32_t idx = h % P.table_n;
-        if (P.out_hash) P.out_hash[pid] = h;
-        if (P.out_queue) P.out_queue[pid] = P.table[idx];
-        if (P.out_hits) {
-          if (hist_lds) atomicAdd(&hist[idx], 1u);
-          else atomicAdd(&P.out_hits[idx], 1ull);
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    tile_epilogue(P, L, cur, lane);
+    cur = make_tile<CONTIG>(cur.id + nwaves, d_next);
+    d_next = desc_of(cur.id + nwaves);
   }
 
-  if (hist_lds) {
+  if (L.hist_lds) {
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) {
-      uint32_t v = hist[i];
+      uint32_t v = L.hist[i];
       if (v) atomicAdd(&P.out_hits[i], (unsigned long long) v);
     }
   }
@@ -750,14 +741,14 @@ struct RxVariant {
 };
 
 const RxVariant kRxVariants[] = {
-    {rx_offload_kernel<2, true, 4, false, true>, 2, 4, "u2_nt1_w4_c"},
-    {rx_offload_kernel<4, true, 4, false, true>, 4, 4, "u4_nt1_w4_c"},
-    {rx_offload_kernel<4, false, 4, false, true>, 4, 4, "u4_nt0_w4_c"},
-    {rx_offload_kernel<1, true, 8, false, true>, 1, 8, "u1_nt1_w8_c"},
-    {rx_offload_kernel<2, true, 4, false, false>, 2, 4, "u2_nt1_w4"},
-    {rx_offload_kernel<1, false, 8, false, false>, 1, 8, "u1_nt0_w8"},
-    {rx_offload_kernel<8, true, 2, false, true>, 8, 2, "u8_nt1_w2_c"},
-    {rx_offload_kernel<2, false, 8, false, true>, 2, 8, "u2_nt0_w8_c"},
+    {rx_offload_kernel<2, true, 4, true>, 2, 4, "u2_nt1_w4_c"},
+    {rx_offload_kernel<3, true, 4, true>, 3, 4, "u3_nt1_w4_c"},
+    {rx_offload_kernel<4, true, 4, true>, 4, 4, "u4_nt1_w4_c"},
+    {rx_offload_kernel<2, true, 2, true>, 2, 2, "u2_nt1_w2_c"},
+    {rx_offload_kernel<2, true, 8, true>, 2, 8, "u2_nt1_w8_c"},
+    {rx_offload_kernel<2, true, 4, false>, 2, 4, "u2_nt1_w4"},
+    {rx_offload_kernel<1, false, 8, false>, 1, 8, "u1_nt0_w8"},
+    {rx_offload_kernel<2, false, 4, true>, 2, 4, "u2_nt0_w4_c"},
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
 
@@ -859,7 +850,8 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
   const RxVariant& v = kRxVariants[variant];
   const bool rss = P.mode != NICGPU_TUPLE_NONE;
   const uint32_t hist_n = (P.out_hits && P.table_n <= (uint32_t) kHistLds) ? P.table_n : 0u;
-  const uint32_t lds = rx_lds_bytes(v.wpb, v.unroll, rss, rss ? P.lut_words : 0u, hist_n);
+  const uint32_t table_words = (rss && P.table_n <= (uint32_t) kTableLds) ? (P.table_n + 1u) / 2u : 0u;
+  const uint32_t lds = rx_lds_bytes(v.wpb, v.unroll, rss, rss ? P.lut_words : 0u, hist_n) + table_words * 4u;
   int dev = 0;
   (void) hipGetDevice(&dev);
   const uint64_t ntiles = (P.n + kWave - 1) / kWave;
