@@ -174,6 +174,22 @@ __host__ __device__ constexpr uint32_t rx_wave_lds(bool rss, int unroll) {
   return rx_hdr_off(unroll) + (rss ? kWave * kHdrChunks * 16 : 0);
 }
 
+// block path: 2 slot windows + 2 x (U x WPB) step totals; general path: per-wave pk (rewritten every
+// tile, so it may overlay the slots) + per-wave tagged marks, which must never be overlaid (a stale
+// word matching a live tag would map chunks to the wrong packet)
+__host__ __device__ constexpr uint32_t rx_block_scratch_bytes(int unroll, int wpb) {
+  return ((uint32_t) (2 * kWave * wpb * unroll * 4 + 2 * unroll * wpb * 4) > (uint32_t) (wpb * kWave * 16)
+              ? (uint32_t) (2 * kWave * wpb * unroll * 4 + 2 * unroll * wpb * 4)
+              : (uint32_t) (wpb * kWave * 16)) +
+         (uint32_t) (wpb * kWave * unroll * 4);
+}
+
+__host__ __device__ inline uint32_t rx_block_lds_bytes(int wpb, int unroll, bool rss, uint32_t lut_words,
+                                                       uint32_t hist_n) {
+  return (uint32_t) (kWave * 8) + (rss ? (uint32_t) (kWave * kHdrChunks * 16) : 0u) +
+         rx_block_scratch_bytes(unroll, wpb) + lut_words * 4u + hist_n * 4u;
+}
+
 __host__ __device__ inline uint32_t rx_lds_bytes(int wpb, int unroll, bool rss, uint32_t lut_words, uint32_t hist_n) {
   return (uint32_t) wpb * rx_wave_lds(rss, unroll) + lut_words * 4u + hist_n * 4u;
 }
@@ -634,6 +650,203 @@ __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
   }
 }
 
+// --------------------------------------------------------------------------
+// Block-cooperative variant.  A block of WPB waves owns a tile of 64 packets
+// (all waves hold the same 64 descriptors).  Contiguous tiles are streamed by
+// the whole block: in a block step of WPB x 64 chunks, wave w reads KiB w, so
+// the waves of a block read adjacent memory (measured read ceiling of this
+// pattern 6.8-7.1 TB/s vs 6.0-6.4 TB/s for one tile per wave,
+// profiles/r01_tune_variants.json) and the grid has 4x fewer, 4x shorter
+// tiles in flight (a shorter tail).  Chunk sums are scanned per wave; the
+// per-wave step totals are exchanged through LDS once per batch (one
+// s_barrier) to form block-wide prefixes.  Packet sums are E - S recorded at
+// the packet's tail and head chunks.  Non-contiguous tiles are split into four
+// 16-packet quarters, one per wave, on the general (marks + prefix-max) path.
+template <int U>
+__device__ __forceinline__ void scatter_slots_win(uint32_t* slots, uint32_t win, uint32_t base, uint32_t lane,
+                                                  uint32_t start, uint32_t nch, uint32_t info) {
+  if (nch == 0u) return;
+  const uint32_t rs = start - base;
+  const uint32_t re = start + nch - 1u - base;
+  const uint32_t lo = info & 15u, hi = (info >> 4) & 31u;
+  const uint32_t common = 1u | (lane << 1);
+#pragma unroll
+  for (uint32_t j = 0; j < (uint32_t) kHdrChunks; ++j) {
+    const uint32_t r = rs + j;
+    if (j < nch && r < win) {
+      uint32_t v = common | (j << 7) | (j == 0 ? (lo << 11) : 0u);
+      v |= (j + 1u == nch) ? ((1u << 15) | (hi << 16)) : (16u << 16);
+      slots[r] = v;
+    }
+  }
+  if (nch > (uint32_t) kHdrChunks && re < win) slots[re] = common | (7u << 7) | (1u << 15) | (hi << 16);
+}
+
+template <int U, int WPB, bool NT>
+__device__ __forceinline__ void plan_block(ContigBatch<U>& B, uint32_t* slots, uint32_t base, uint32_t total,
+                                           uint32_t w, uint32_t lane, const Tile& t, const u32x4* __restrict__ tile16) {
+  constexpr uint32_t kS = (uint32_t) kWave * WPB;
+  if ((lane % WPB) == w) scatter_slots_win<U>(slots, kS * U, base, lane, t.start, t.nch, t.info);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t c = base + (uint32_t) u * kS + w * kWave + lane;
+    const uint32_t ce = c < total ? c : total - 1u;
+    if constexpr (NT) B.v[u] = __builtin_nontemporal_load(tile16 + ce);
+    else B.v[u] = tile16[ce];
+  }
+}
+
+template <int U, int WPB>
+__device__ __forceinline__ uint32_t process_block(ContigBatch<U>& B, uint32_t* slots, uint32_t* tot, uint32_t run,
+                                                  uint32_t* S, uint32_t* E, uint4* hdr, bool stage_hdr, uint32_t w,
+                                                  uint32_t lane) {
+  constexpr uint32_t kS = (uint32_t) kWave * WPB;
+  uint32_t sl[U], incl[U], sv[U];
+  u32x4 vv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t idx = (uint32_t) u * kS + w * kWave + lane;
+    sl[u] = slots[idx];
+    u32x4 v = B.v[u];
+    if (sl[u] != 0u) {
+      slots[idx] = 0u;
+      const int lo = (int) ((sl[u] >> 11) & 15u), hi = (int) ((sl[u] >> 16) & 31u);
+      if (lo != 0 || hi != 16) {
+        v.x &= dword_keep(lo, hi, 0);
+        v.y &= dword_keep(lo, hi, 1);
+        v.z &= dword_keep(lo, hi, 2);
+        v.w &= dword_keep(lo, hi, 3);
+      }
+    }
+    vv[u] = v;
+    sv[u] = add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, 0u))));
+    incl[u] = wave_incl_scan(sv[u]);
+    if (lane == 63u) tot[u * WPB + w] = incl[u];
+  }
+  __syncthreads();  // step totals of every wave (and the next window's slots) are visible
+  uint32_t tw[U * WPB];
+#pragma unroll
+  for (int i = 0; i < U * WPB; ++i) tw[i] = tot[i];
+  uint32_t pre = run;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    uint32_t before = 0;
+#pragma unroll
+    for (int j = 0; j < WPB; ++j) before += (j < (int) w) ? tw[u * WPB + j] : 0u;
+    const uint32_t base_pref = pre + before;
+    if (sl[u] != 0u) {
+      const uint32_t q = (sl[u] >> 1) & 63u, k = (sl[u] >> 7) & 7u;
+      if (k == 0u) S[q] = base_pref + incl[u] - sv[u];
+      if (sl[u] & (1u << 15)) E[q] = base_pref + incl[u];
+      if (stage_hdr && k < (uint32_t) kHdrChunks) hdr[q * kHdrChunks + k] = make_uint4(vv[u].x, vv[u].y, vv[u].z, vv[u].w);
+    }
+#pragma unroll
+    for (int j = 0; j < WPB; ++j) pre += tw[u * WPB + j];
+  }
+  return pre;
+}
+
+template <int U, bool NT, int WPB>
+__global__ __launch_bounds__(kWave * WPB) void rx_block_kernel(RxParams P) {
+  extern __shared__ uint4 lds_dyn[];
+  const uint32_t w = threadIdx.x / kWave;
+  const uint32_t lane = lane_id();
+  constexpr uint32_t kS = (uint32_t) kWave * WPB;
+  constexpr uint32_t kWin = kS * U;
+
+  RxLdsPtrs L;
+  L.want_rss = P.mode != NICGPU_TUPLE_NONE;
+  L.hist_lds = P.out_hits != nullptr && P.table_n <= (uint32_t) kHistLds;
+  L.table_lds = L.want_rss && P.table_n <= (uint32_t) kTableLds;
+  uint8_t* b = reinterpret_cast<uint8_t*>(lds_dyn);
+  L.S = reinterpret_cast<uint32_t*>(b);
+  L.E = L.S + kWave;
+  uint8_t* p = b + kWave * 8;
+  L.hdr = reinterpret_cast<uint4*>(p);
+  p += L.want_rss ? kWave * kHdrChunks * 16 : 0;
+  // scratch: block path = 2 slot windows + 2 x (U x WPB) step totals; general path = per-wave pk + marks
+  L.slotsA = reinterpret_cast<uint32_t*>(p);
+  L.slotsB = L.slotsA + kWin;
+  uint32_t* totA = L.slotsB + kWin;
+  uint32_t* totB = totA + U * WPB;
+  L.pk = reinterpret_cast<uint4*>(p + w * kWave * 16);
+  L.marks = reinterpret_cast<uint32_t*>(p + rx_block_scratch_bytes(U, WPB)) - (WPB - w) * kWave * U;
+  p += rx_block_scratch_bytes(U, WPB);
+  // marks never match a live tag (tags start at 1)
+  for (uint32_t i = lane; i < (uint32_t) (kWave * U); i += kWave) L.marks[i] = 0xFFFFFFFFu;
+  L.lut = reinterpret_cast<uint32_t*>(p);
+  L.hist = L.lut + P.lut_words;
+  L.table_s = reinterpret_cast<uint16_t*>(L.hist + (L.hist_lds ? P.table_n : 0u));
+  uint32_t tag = 0;
+
+  if (L.want_rss) {
+    for (uint32_t i = threadIdx.x; i < P.lut_words; i += kWave * WPB) L.lut[i] = P.lut[i];
+  }
+  if (L.hist_lds) {
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) L.hist[i] = 0;
+  }
+  if (L.table_lds) {
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) L.table_s[i] = P.table[i];
+  }
+
+  const uint64_t ntiles = (P.n + kWave - 1) / kWave;
+  auto desc_of = [&](uint64_t id) __attribute__((always_inline)) -> uint64_t {
+    return (id < ntiles && id * kWave + lane < P.n) ? P.desc[id * kWave + lane] : 0ull;
+  };
+  uint64_t d_cur = desc_of(blockIdx.x);
+  uint64_t d_next = desc_of(blockIdx.x + gridDim.x);
+
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const Tile t = make_tile<true>(tile, d_cur);
+    d_cur = d_next;
+    d_next = desc_of(tile + 2ull * gridDim.x);
+    __syncthreads();  // previous tile's epilogue is done with S/E/hdr/scratch
+    if (t.contig && t.total != 0u) {
+      for (uint32_t i = threadIdx.x; i < 2 * kWin; i += kWave * WPB) L.slotsA[i] = 0u;
+      __syncthreads();
+      const u32x4* tile16 = reinterpret_cast<const u32x4*>(P.frames) + t.D;
+      ContigBatch<U> A, B;
+      uint32_t run = 0, b0 = 0;
+      plan_block<U, WPB, NT>(A, L.slotsA, 0, t.total, w, lane, t, tile16);
+      __syncthreads();  // A's slots from every wave
+      for (;;) {
+        plan_block<U, WPB, NT>(B, L.slotsB, b0 + kWin, t.total, w, lane, t, tile16);
+        __builtin_amdgcn_sched_barrier(0);
+        run = process_block<U, WPB>(A, L.slotsA, totA, run, L.S, L.E, L.hdr, L.want_rss, w, lane);
+        if (b0 + kWin >= t.total) break;
+        plan_block<U, WPB, NT>(A, L.slotsA, b0 + 2 * kWin, t.total, w, lane, t, tile16);
+        __builtin_amdgcn_sched_barrier(0);
+        run = process_block<U, WPB>(B, L.slotsB, totB, run, L.S, L.E, L.hdr, L.want_rss, w, lane);
+        b0 += 2 * kWin;
+        if (b0 >= t.total) break;
+      }
+    } else if (t.total != 0u) {
+      // quarter q = w: packets [16w, 16w + 16) on the general path (others read as empty)
+      constexpr uint32_t kQ = (uint32_t) kWave / WPB;
+      const bool mine = (lane / kQ) == w;
+      const Tile m = make_tile<false>(tile, mine ? (t.off | ((uint64_t) t.len << NICGPU_DESC_OFFSET_BITS)) : 0ull);
+      if (m.total != 0u) run_general_tile<U, NT>(P, L, m, lane, tag);
+    }
+    __syncthreads();  // S/E/hdr of all 64 packets complete
+    {
+      constexpr uint32_t kQ = (uint32_t) kWave / WPB;
+      if ((lane / kQ) == w) {
+        Tile e = t;
+        e.contig = 0u;  // both paths record S at the head and E at the tail
+        tile_epilogue(P, L, e, lane);
+      }
+    }
+  }
+
+  if (L.hist_lds) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) {
+      uint32_t v = L.hist[i];
+      if (v) atomicAdd(&P.out_hits[i], (unsigned long long) v);
+    }
+  }
+}
+
 // ------------------------------------------------------------- TSO / GSO --
 // One wave per frame.  Each lane streams 16-B chunks of the payload region;
 // a chunk overlaps at most two segments (mss >= 16 in the fast path), so the
@@ -738,17 +951,18 @@ struct RxVariant {
   int unroll;
   int wpb;
   const char* name;
+  bool block = false;  // rx_block_kernel (block-cooperative) instead of rx_offload_kernel
 };
 
 const RxVariant kRxVariants[] = {
+    {rx_block_kernel<2, true, 4>, 2, 4, "blk_u2_nt1_w4", true},
     {rx_offload_kernel<2, true, 4, true>, 2, 4, "u2_nt1_w4_c"},
-    {rx_offload_kernel<3, true, 4, true>, 3, 4, "u3_nt1_w4_c"},
-    {rx_offload_kernel<4, true, 4, true>, 4, 4, "u4_nt1_w4_c"},
-    {rx_offload_kernel<2, true, 2, true>, 2, 2, "u2_nt1_w2_c"},
-    {rx_offload_kernel<2, true, 8, true>, 2, 8, "u2_nt1_w8_c"},
+    {rx_block_kernel<1, true, 4>, 1, 4, "blk_u1_nt1_w4", true},
+    {rx_block_kernel<4, true, 4>, 4, 4, "blk_u4_nt1_w4", true},
+    {rx_block_kernel<2, true, 8>, 2, 8, "blk_u2_nt1_w8", true},
+    {rx_block_kernel<2, false, 4>, 2, 4, "blk_u2_nt0_w4", true},
+    {rx_block_kernel<1, true, 8>, 1, 8, "blk_u1_nt1_w8", true},
     {rx_offload_kernel<2, true, 4, false>, 2, 4, "u2_nt1_w4"},
-    {rx_offload_kernel<1, false, 8, false>, 1, 8, "u1_nt0_w8"},
-    {rx_offload_kernel<2, false, 4, true>, 2, 4, "u2_nt0_w4_c"},
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
 
@@ -851,11 +1065,13 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
   const bool rss = P.mode != NICGPU_TUPLE_NONE;
   const uint32_t hist_n = (P.out_hits && P.table_n <= (uint32_t) kHistLds) ? P.table_n : 0u;
   const uint32_t table_words = (rss && P.table_n <= (uint32_t) kTableLds) ? (P.table_n + 1u) / 2u : 0u;
-  const uint32_t lds = rx_lds_bytes(v.wpb, v.unroll, rss, rss ? P.lut_words : 0u, hist_n) + table_words * 4u;
+  const uint32_t lds = (v.block ? rx_block_lds_bytes(v.wpb, v.unroll, rss, rss ? P.lut_words : 0u, hist_n)
+                                : rx_lds_bytes(v.wpb, v.unroll, rss, rss ? P.lut_words : 0u, hist_n)) +
+                       table_words * 4u;
   int dev = 0;
   (void) hipGetDevice(&dev);
   const uint64_t ntiles = (P.n + kWave - 1) / kWave;
-  const uint64_t want = (ntiles + v.wpb - 1) / (uint64_t) v.wpb;
+  const uint64_t want = v.block ? ntiles : (ntiles + v.wpb - 1) / (uint64_t) v.wpb;
   const uint64_t cap = (uint64_t) di.cus * (uint64_t) rx_blocks_per_cu(dev, variant, lds);
   const unsigned grid = (unsigned) (want < cap ? want : cap);
   hipLaunchKernelGGL(v.kernel, dim3(grid), dim3(kWave * v.wpb), lds, stream, P);
@@ -1157,7 +1373,28 @@ __global__ __launch_bounds__(256) void stream_read_tiles_kernel(const u32x4* __r
     for (uint64_t st = 0; st + 64 * U <= tile16; st += 64 * U) {
       u32x4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = q[st + 64 * u];
+      for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(q + st + 64 * u);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc = add_halves(v[u].w, add_halves(v[u].z, add_halves(v[u].y, add_halves(v[u].x, acc))));
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// block-cooperative tiles: the block's waves stream ONE tile together, wave w
+// reading KiB w of every (waves x 1 KiB) block step.
+template <int U>
+__global__ __launch_bounds__(256) void stream_read_btiles_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                                 uint64_t tile16, uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t ntiles = n16 / tile16;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const u32x4* q = p + t * tile16 + w * 64 + lane;
+    for (uint64_t st = 0; st + 256 * U <= tile16; st += 256 * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(q + st + 256 * u);
 #pragma unroll
       for (int u = 0; u < U; ++u) acc = add_halves(v[u].w, add_halves(v[u].z, add_halves(v[u].y, add_halves(v[u].x, acc))));
     }
@@ -1167,6 +1404,20 @@ __global__ __launch_bounds__(256) void stream_read_tiles_kernel(const u32x4* __r
 }  // namespace
 
 extern "C" {
+int nicgpu_tune_stream_btiles(const uint8_t* buf, size_t bytes, size_t tile_bytes, int blocks_per_cu, int unroll,
+                              uint32_t* out, void* stream) {
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  const unsigned grid = (unsigned) (di->cus * (blocks_per_cu > 0 ? blocks_per_cu : 4));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const u32x4* p = reinterpret_cast<const u32x4*>(buf);
+  const uint64_t t16 = tile_bytes / 16;
+  if (unroll == 4) hipLaunchKernelGGL(stream_read_btiles_kernel<4>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  else if (unroll == 2) hipLaunchKernelGGL(stream_read_btiles_kernel<2>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  else hipLaunchKernelGGL(stream_read_btiles_kernel<1>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  return hip_status(hipGetLastError());
+}
 int nicgpu_tune_stream_tiles(const uint8_t* buf, size_t bytes, size_t tile_bytes, int blocks_per_cu, int unroll,
                              uint32_t* out, void* stream) {
   const DeviceInfo* di = nullptr;

@@ -135,6 +135,38 @@ def main():
         print(json.dumps({name: res}), file=sys.stderr, flush=True)
         del f, d
 
+    # C5: 9000 B frames through TSO segmentation (H = 54, mss = 1448 -> 7 segments)
+    if "tso" in args.workloads.split(","):
+        import smart_nic_amd as sna_p
+
+        nf = 131072
+        frames, desc, _ = pktgen.make_batch(np.full(nf, 9000), seed=9, proto=6, corrupt_frac=0.0)
+        nseg = (9000 - 54 + 1447) // 1448
+        f = torch.from_numpy(frames).cuda()
+        d = torch.from_numpy(desc.view(np.int64)).cuda()
+        hdr = torch.full((nf,), 54, dtype=torch.int16, device="cuda")
+        mss = torch.full((nf,), 1448, dtype=torch.int16, device="cuda")
+        base = torch.arange(nf, dtype=torch.int32, device="cuda") * nseg
+        out_t = torch.empty(nf * nseg, dtype=torch.int16, device="cuda")
+        plib = sna_p.load_library()
+        ts = []
+        for r in range(args.rounds * args.iters):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            assert plib.nicgpu_tso_checksum(f.data_ptr(), d.data_ptr(), hdr.data_ptr(), mss.data_ptr(),
+                                            base.data_ptr(), nf, out_t.data_ptr(), sp) == 0
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        med = float(np.median(ts))
+        alg = nf * (9000 + 16) + nf * nseg * 2
+        out["workloads"]["c5_tso_9000"] = {"packets": nf, "segments": nf * nseg, "alg_bytes": alg, "results": {
+            "tso_checksum_kernel": {"us_median": round(med, 2), "alg_gbs": round(alg / med / 1e3, 1),
+                                    "frac_spec": round(alg / med / 1e3 / 8000, 4),
+                                    "msegs_per_s": round(nf * nseg / med, 1)}}}
+        print(json.dumps({"c5_tso_9000": out["workloads"]["c5_tso_9000"]}), file=sys.stderr, flush=True)
+        del f, d
+
     # read-only streaming ceiling on the largest buffer
     if ceiling_buf is not None:
         nbytes = ceiling_buf.numel() // 16 * 16
@@ -155,9 +187,9 @@ def main():
         tl.nicgpu_tune_stream_tiles.restype = i32
         tl.nicgpu_tune_stream_tiles.argtypes = [vp, sz, sz, i32, i32, vp, vp]
         tiles = {}
-        for tile_kb in (4, 24, 96, 384):
+        for tile_kb in (24, 96):
             for unroll in (1, 2, 4):
-                for bpc in (4, 6, 8):
+                for bpc in (4, 5, 8):
                     ts = []
                     for _ in range(args.rounds):
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -171,6 +203,25 @@ def main():
                     used = nbytes // (tile_kb * 1024) * (tile_kb * 1024)
                     tiles[f"t{tile_kb}k_u{unroll}_bpc{bpc}"] = round(used / med / 1e3, 1)
         out["tile_stream_gbs"] = tiles
+        tl.nicgpu_tune_stream_btiles.restype = i32
+        tl.nicgpu_tune_stream_btiles.argtypes = [vp, sz, sz, i32, i32, vp, vp]
+        btiles = {}
+        for tile_kb in (96, 384, 1536):
+            for unroll in (1, 2, 4):
+                for bpc in (2, 4, 5, 8):
+                    ts = []
+                    for _ in range(args.rounds):
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        assert tl.nicgpu_tune_stream_btiles(ceiling_buf.data_ptr(), nbytes, tile_kb * 1024, bpc, unroll,
+                                                            sink.data_ptr(), sp) == 0
+                        e1.record()
+                        torch.cuda.synchronize()
+                        ts.append(e0.elapsed_time(e1) * 1e3)
+                    med = float(np.median(ts))
+                    used = nbytes // (tile_kb * 1024) * (tile_kb * 1024)
+                    btiles[f"bt{tile_kb}k_u{unroll}_bpc{bpc}"] = round(used / med / 1e3, 1)
+        out["block_tile_stream_gbs"] = btiles
         out["read_ceiling_gbs"] = ceil
         best = max(ceil.values())
         out["read_ceiling_best_gbs"] = best
