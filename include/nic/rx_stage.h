@@ -1,0 +1,210 @@
+// nic/rx_stage.h — batched QueuePair RX stage on the GPU.
+//
+// The reference moves one TX descriptor at a time through
+// QueuePair::process_once (src/queue_pair.cpp:67-119) and its helpers
+// (validate_mtu :195-210, build_segments :212-278, process_segments :303-369,
+// handle_rx_segment :385-460).  BatchedQueuePair runs a whole batch of TX
+// descriptors against a batch of RX descriptors with the same observable
+// results:
+//   - every TX and RX CompletionEntry, in posting order, with identical fields;
+//   - QueuePairStats, counter by counter;
+//   - the bytes DMA-written into the RX buffers (TSO/GSO segments, VLAN
+//     insert/strip);
+//   - the same interrupt sequence (fire_tx_interrupt / fire_rx_interrupt),
+//     delivered to a callback instead of an InterruptDispatcher.
+// It adds RSS dispatch, which the reference lacks: every frame delivered with
+// RX status Success is hashed by an RssEngine and listed under its queue.
+//
+// Host memory is a device-resident image (DeviceHostMemory): host address a
+// is byte a of the image, and the bounds rule of SimpleHostMemory::translate_view
+// (simple_host_memory.cpp:85-93) decides DMA faults.  Descriptors arrive
+// already popped from their rings (DescriptorRing owns ring/doorbell state;
+// the stage starts where pop_descriptor ends).
+//
+// GPU work per batch: one checksum pass over the TX bytes (the per-piece
+// ones'-complement sums every TX/RX verify needs), one gather that
+// materialises the written segments into the RX buffers, and one RX offload
+// launch over the delivered frames (RSS).  The control flow between them —
+// ring consumption, first-failure aborts, statuses, stats — is sequential in
+// the reference and is resolved on the host from those sums, exactly.
+//
+// Not modelled: address translators / fault injectors of SimpleHostMemory
+// (only the plain bounds check), and aliasing between TX buffers and RX
+// buffers of the same batch (the reference would read bytes written by an
+// earlier segment of the batch; the stage reads every TX buffer first).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <span>
+#include <vector>
+
+#include "nic/gpu_batch.h"
+#include "nic/offload.h"
+#include "nic/rss.h"
+#include "nic/tx_rx.h"
+
+#if __has_include("nic/completion_queue.h")
+#include "nic/completion_queue.h"  // reference build: its CompletionEntry
+#else
+namespace nic {
+// Same members, order and defaults as include/nic/completion_queue.h:13-26.
+struct CompletionEntry {
+  std::uint16_t queue_id{0};
+  std::uint16_t descriptor_index{0};
+  std::uint32_t status{0};
+  bool checksum_offloaded{false};
+  bool checksum_verified{false};
+  bool tso_performed{false};
+  bool gso_performed{false};
+  bool vlan_inserted{false};
+  bool vlan_stripped{false};
+  bool gro_aggregated{false};
+  std::uint16_t segments_produced{1};
+  std::uint16_t vlan_tag{0};
+};
+static_assert(sizeof(CompletionEntry) == 20);
+}  // namespace nic
+#endif
+
+#if __has_include("nic/queue_pair.h")
+#include "nic/queue_pair.h"  // reference build: its QueuePairStats
+#else
+namespace nic {
+// Same members and order as include/nic/queue_pair.h:36-53.
+struct QueuePairStats {
+  std::uint64_t tx_packets{0};
+  std::uint64_t rx_packets{0};
+  std::uint64_t tx_bytes{0};
+  std::uint64_t rx_bytes{0};
+  std::uint64_t drops_checksum{0};
+  std::uint64_t drops_no_rx_desc{0};
+  std::uint64_t drops_buffer_small{0};
+  std::uint64_t drops_mtu_exceeded{0};
+  std::uint64_t drops_invalid_mss{0};
+  std::uint64_t drops_too_many_segments{0};
+  std::uint64_t tx_tso_segments{0};
+  std::uint64_t tx_gso_segments{0};
+  std::uint64_t tx_vlan_insertions{0};
+  std::uint64_t rx_vlan_strips{0};
+  std::uint64_t rx_checksum_verified{0};
+  std::uint64_t rx_gro_aggregated{0};
+};
+}  // namespace nic
+#endif
+
+namespace nic {
+
+/// Device-resident image of the host memory the DMA engine addresses.
+struct DeviceHostMemory {
+  std::byte* base{nullptr};  // device pointer; host address a <-> base[a]
+  std::size_t size{0};
+};
+
+struct BatchedQueuePairConfig {
+  std::uint16_t queue_id{0};
+  std::size_t max_mtu{kJumboMtu};   // QueuePairConfig::max_mtu (queue_pair.h:32)
+  bool enable_tx_interrupts{false};  // QueuePairConfig defaults (queue_pair.h:33-34)
+  bool enable_rx_interrupts{true};
+  /// Receives what InterruptDispatcher::on_completion would (queue_pair.cpp:371-383).
+  std::function<void(std::uint16_t queue_id, const CompletionEntry&)> on_interrupt{};
+  /// RSS over delivered frames; nullptr = no dispatch.  Not owned.
+  RssEngine* rss{nullptr};
+  TupleSpec tuple{};
+};
+
+struct RxBatchResult {
+  static constexpr std::uint16_t kNoQueue = 0xFFFF;
+  std::size_t tx_processed{0};  // TX descriptors consumed (all of them)
+  std::size_t rx_consumed{0};   // RX descriptors popped, in order from rx[0]
+  std::vector<CompletionEntry> tx_completions;  // posting order
+  std::vector<CompletionEntry> rx_completions;  // posting order
+  /// Per RX completion: RSS hash / queue of the delivered frame
+  /// (0 / kNoQueue unless status == Success and an RssEngine is configured).
+  std::vector<std::uint32_t> rx_hash;
+  std::vector<std::uint16_t> rx_queue;
+  /// queues[q] = indices into rx_completions dispatched to RSS queue q.
+  std::vector<std::vector<std::uint32_t>> queues;
+};
+
+/// QueuePair::process_once over a batch (src/queue_pair.cpp:67-460).
+class BatchedQueuePair {
+public:
+  explicit BatchedQueuePair(BatchedQueuePairConfig config);
+
+  /// Process every descriptor of `tx` in order against the RX descriptors `rx`
+  /// (the RX ring's contents, rx[0] first).  Synchronises `stream` (a
+  /// hipStream_t; nullptr = default stream) before returning.
+  RxBatchResult process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
+                              std::span<const RxDescriptor> rx, void* stream = nullptr);
+
+  [[nodiscard]] const QueuePairStats& stats() const noexcept { return stats_; }
+  void reset_stats() noexcept { stats_ = QueuePairStats{}; }
+  [[nodiscard]] const BatchedQueuePairConfig& config() const noexcept { return config_; }
+
+private:
+  BatchedQueuePairConfig config_;
+  QueuePairStats stats_{};
+};
+
+// Building blocks of process_batch, public so that the host logic can be
+// tested without a GPU (the piece sums then come from a CPU checker).
+namespace rx_stage_detail {
+
+/// A byte range of host memory whose ones'-complement sum the GPU computes.
+struct Piece {
+  std::uint64_t addr;
+  std::uint32_t len;  // <= NICGPU_MAX_PACKET
+};
+
+/// Which pieces make up the bytes each decision needs, per TX descriptor.
+//   kNoBytes    no decision reads the bytes (DMA read fault, or dropped before
+//               any checksum is needed)
+//   kPlain      the segment is the whole packet: pieces [0, min(4, L)) then
+//               [4, L) in runs of <= 65534 bytes
+//   kSegmented  H >= 4: [0, 4), [4, H), then chunk k = [H + k*mss, +len_k);
+//               H < 4:  [0, H), then per chunk [.., +min(4 - H, len_k)) and its rest
+// Segment sums are composed from pieces (first 4 bytes | the rest, so that a
+// VLAN strip of a segment's first 4 bytes, queue_pair.cpp:392-395, is exact).
+struct PacketPlan {
+  enum Kind : std::uint8_t { kNoBytes, kPlain, kSegmented };
+  Kind kind{kNoBytes};
+  std::uint32_t nseg{0};  // segments build_segments produces (kSegmented)
+  std::uint32_t first_piece{0};
+  std::uint32_t npieces{0};
+  std::uint32_t hdr_len{0};  // H (kSegmented)
+  std::uint32_t mss{0};      // (kSegmented)
+};
+
+struct Plan {
+  std::vector<PacketPlan> packets;
+  std::vector<Piece> pieces;
+};
+
+/// One DMA write: dst <- prefix (0 or 4 bytes) || [src_a, +len_a) || [src_b, +len_b).
+struct SegmentWrite {
+  std::uint64_t dst;
+  std::uint64_t src_a;
+  std::uint64_t src_b;
+  std::uint32_t len_a;
+  std::uint32_t len_b;
+  std::uint32_t prefix;      // bytes in memory order (little-endian word)
+  std::uint32_t prefix_len;  // 0 or 4
+};
+static_assert(sizeof(SegmentWrite) == 40);
+
+Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx);
+
+/// Sequential resolution of the batch, given piece_csum[i] =
+/// compute_checksum(bytes of plan.pieces[i]).  Appends completions to `out`,
+/// updates `stats`, fires interrupts, and lists the DMA writes to perform
+/// (write_of_rx[j] = index into writes of RX completion j, or -1).
+void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
+             std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
+             std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
+             std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx);
+
+}  // namespace rx_stage_detail
+
+}  // namespace nic

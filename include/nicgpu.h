@@ -134,6 +134,28 @@ int nicgpu_tso_checksum(const uint8_t* frames, const uint64_t* desc, const uint1
                         const uint16_t* mss, const uint32_t* seg_base, size_t n,
                         uint16_t* out_csum, void* stream);
 
+/* One DMA write of the batched QueuePair stage (nic/rx_stage.h):
+ *   mem[dst ..] <- prefix bytes (prefix_len 0 or 4; little-endian word, i.e.
+ *                  memory order) || mem[src_a, +len_a) || mem[src_b, +len_b).
+ * Replaces the per-segment DMAEngine::write of QueuePair::handle_rx_segment
+ * (src/queue_pair.cpp:416-426) after build_segments / VLAN insert-strip
+ * (:212-278, :324-331, :389-395).  40 bytes, naturally aligned. */
+typedef struct nicgpu_segment_write {
+  uint64_t dst;
+  uint64_t src_a;
+  uint64_t src_b;
+  uint32_t len_a;
+  uint32_t len_b;
+  uint32_t prefix;
+  uint32_t prefix_len;
+} nicgpu_segment_write;
+
+/* Perform n writes (device array) inside the memory image mem[0, mem_size).
+ * Destinations must not overlap each other or any source.  Entries reaching
+ * outside the image are skipped. */
+int nicgpu_segment_gather(uint8_t* mem, uint64_t mem_size, const nicgpu_segment_write* writes, size_t n,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

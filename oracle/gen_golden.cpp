@@ -653,6 +653,183 @@ void gen_tso() {
   std::ofstream(g_out + "/tso.json") << js.str();
 }
 
+
+// ------------------------------------------------- batched QueuePair runs --
+// Randomised multi-descriptor batches through the reference QueuePair
+// (queue_pair.cpp:67-460): every TX descriptor is processed by process_once in
+// ring order against a shared RX ring, as the batched RX stage
+// must reproduce.  Recorded: the initial host-memory image, the raw TX/RX
+// descriptor PODs, every TX and RX CompletionEntry in posting order, the
+// QueuePairStats, the RX descriptors consumed and an FNV-1a-64 of every RX
+// buffer region after the run (what the DMA writes left there).
+std::uint64_t fnv1a(const std::byte* p, std::size_t n) {
+  std::uint64_t h = 0xcbf29ce484222325ull;
+  for (std::size_t i = 0; i < n; ++i) { h ^= static_cast<std::uint8_t>(p[i]); h *= 0x100000001b3ull; }
+  return h;
+}
+
+std::string completion_json(const CompletionEntry& e) {
+  std::ostringstream o;
+  o << "[" << e.queue_id << "," << e.descriptor_index << "," << e.status << "," << int(e.checksum_offloaded) << ","
+    << int(e.checksum_verified) << "," << int(e.tso_performed) << "," << int(e.gso_performed) << ","
+    << int(e.vlan_inserted) << "," << int(e.vlan_stripped) << "," << int(e.gro_aggregated) << ","
+    << e.segments_produced << "," << e.vlan_tag << "]";
+  return o.str();
+}
+
+void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t ntx, std::size_t nrx, int flavour) {
+  Rng r{seed};
+  // TX region, then the RX buffers, then a guard tail; a few descriptors point
+  // past the end (DMA fault).
+  std::vector<TxDescriptor> txs;
+  std::vector<std::vector<std::uint8_t>> pkts;
+  std::size_t tx_end = 0;
+  std::vector<std::uint64_t> tx_addr;
+  for (std::size_t i = 0; i < ntx; ++i) {
+    std::size_t L;
+    const std::uint32_t pick = r.below(20);
+    if (flavour == 1) L = 9000;                       // C5-like TSO batch
+    else if (pick < 6) L = 64;
+    else if (pick < 9) L = 576;
+    else if (pick < 13) L = 1518;
+    else if (pick < 15) L = r.below(80);             // tiny / empty / sub-header
+    else if (pick < 17) L = 9000;
+    else if (pick < 18) L = 9001 + r.below(300);     // over max_mtu
+    else L = 64 + r.below(4000);
+    FrameSpec fs;
+    fs.total = L;
+    fs.proto = (r.below(2) == 0) ? 6 : 17;
+    fs.vlan_tags = (r.below(6) == 0) ? 1 : 0;
+    fs.balance = r.below(4) != 0;
+    std::vector<std::uint8_t> f = L >= 14 ? build_frame(r, fs) : std::vector<std::uint8_t>(L);
+    if (L < 14) for (auto& b : f) b = r.byte();
+    if (r.below(50) == 0) for (auto& b : f) b = 0;  // all-zero frame (checksum 0xFFFF)
+    const std::size_t gap = r.below(3) == 0 ? r.below(16) : 0;
+    tx_end += gap;
+    tx_addr.push_back(tx_end);
+    tx_end += L;
+    pkts.push_back(std::move(f));
+    TxDescriptor t{};
+    t.buffer_address = tx_addr.back();
+    t.length = static_cast<std::uint32_t>(L);
+    t.descriptor_index = static_cast<std::uint16_t>(i);
+    const std::uint32_t cm = r.below(6);
+    t.checksum = cm < 3 ? ChecksumMode::None : (cm < 5 ? ChecksumMode::Layer4 : ChecksumMode::Layer3);
+    t.checksum_offload = r.below(3) != 0;
+    const std::uint16_t good = ref_csum(pkts.back().data(), L);
+    t.checksum_value = r.below(5) == 0 ? static_cast<std::uint16_t>(good ^ (1u + r.below(0xFFFE))) : good;
+    const bool seg = flavour == 1 ? true : r.below(4) == 0;
+    if (seg) {
+      (r.below(2) ? t.tso_enabled : t.gso_enabled) = true;
+      if (r.below(6) == 0) { t.tso_enabled = true; t.gso_enabled = true; }
+      const std::uint32_t mp = r.below(12);
+      t.mss = mp == 0 ? 0 : (mp == 1 ? static_cast<std::uint16_t>(9001 + r.below(100))
+                                     : (mp == 2 ? static_cast<std::uint16_t>(1 + r.below(40))
+                                                : static_cast<std::uint16_t>(100 + r.below(1500))));
+      if (flavour == 1 && mp > 2) t.mss = r.below(3) == 0 ? 1447 : 1448;
+      const std::uint32_t hp = r.below(10);
+      t.header_length = hp == 0 ? 0 : (hp == 1 ? static_cast<std::uint16_t>(1 + r.below(5))
+                                               : (hp == 2 ? static_cast<std::uint16_t>(L + r.below(2))
+                                                          : static_cast<std::uint16_t>(54 + r.below(2))));
+    }
+    if (r.below(5) == 0) { t.vlan_insert = true; t.vlan_tag = static_cast<std::uint16_t>(r.u32()); }
+    txs.push_back(t);
+  }
+  tx_end = (tx_end + 63) & ~std::size_t{63};
+  std::vector<RxDescriptor> rxs;
+  std::size_t rx_at = tx_end;
+  for (std::size_t j = 0; j < nrx; ++j) {
+    RxDescriptor x{};
+    const std::uint32_t bp = r.below(10);
+    std::uint32_t blen = bp == 0 ? r.below(1600) : (bp == 1 ? 64 : (bp < 7 ? 1600 : 9216 + 8));
+    if (flavour == 1) blen = bp == 0 ? 1400 : 9216 + 8;
+    x.buffer_address = rx_at + r.below(4);
+    x.buffer_length = blen;
+    rx_at = x.buffer_address + blen + r.below(8);
+    x.descriptor_index = static_cast<std::uint16_t>(1000 + j);
+    x.checksum_offload = flavour == 1 ? r.below(4) == 0 : r.below(4) != 0;
+    const std::uint32_t cm = r.below(5);
+    x.checksum = cm == 0 ? ChecksumMode::None : (cm < 3 ? ChecksumMode::Layer4 : ChecksumMode::Layer3);
+    x.vlan_strip = r.below(3) == 0;
+    x.vlan_present = r.below(4) == 0;
+    x.vlan_tag = static_cast<std::uint16_t>(r.u32());
+    x.gro_enabled = r.below(5) == 0;
+    rxs.push_back(x);
+  }
+  const std::size_t mem_size = rx_at + 64;
+  // DMA faults: a few descriptors addressed past the end of host memory
+  // (past the end, or straddling it); RX fault addresses are distinct so no
+  // two DMA writes can land on the same bytes
+  for (std::size_t i = 0; i < ntx; ++i)
+    if (r.below(60) == 0) txs[i].buffer_address = r.below(2) ? mem_size + 1 + i : mem_size - txs[i].length / 2;
+  for (std::size_t j = 0; j < nrx; ++j)
+    if (r.below(80) == 0) rxs[j].buffer_address = mem_size + 1 + j;
+
+  HostMemoryConfig mc{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false};
+  SimpleHostMemory mem{mc};
+  std::vector<std::uint8_t> image(mem_size);
+  for (std::size_t a = 0; a < tx_end; ++a) image[a] = r.byte();  // RX region starts zeroed
+  for (std::size_t i = 0; i < ntx; ++i) std::memcpy(image.data() + tx_addr[i], pkts[i].data(), pkts[i].size());
+  assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(image))).ok());
+  DMAEngine dma{mem};
+  QueuePairConfig qc{
+      .queue_id = 5,
+      .tx_ring = {.descriptor_size = sizeof(TxDescriptor), .ring_size = ntx + 1, .base_address = 0, .queue_id = 5, .host_backed = false},
+      .rx_ring = {.descriptor_size = sizeof(RxDescriptor), .ring_size = nrx + 1, .base_address = 0, .queue_id = 5, .host_backed = false},
+      .tx_completion = {.ring_size = ntx + 1, .queue_id = 5},
+      .rx_completion = {.ring_size = 70 * ntx + 1, .queue_id = 5},
+  };
+  QueuePair qp{qc, dma};
+  for (auto& t : txs) {
+    std::vector<std::byte> b(sizeof(TxDescriptor));
+    std::memcpy(b.data(), &t, sizeof(t));
+    assert(qp.tx_ring().push_descriptor(b).ok());
+  }
+  for (auto& x : rxs) {
+    std::vector<std::byte> b(sizeof(RxDescriptor));
+    std::memcpy(b.data(), &x, sizeof(x));
+    assert(qp.rx_ring().push_descriptor(b).ok());
+  }
+  while (qp.process_once()) {
+  }
+  const std::size_t rx_consumed = nrx - qp.rx_ring().available();
+  std::ostringstream js;
+  js << "{\n \"source\": \"QueuePair::process_once over a batch (src/queue_pair.cpp:67-460)\",\n"
+     << " \"queue_id\": 5, \"max_mtu\": 9000, \"mem_size\": " << mem_size << ", \"ntx\": " << ntx << ", \"nrx\": " << nrx
+     << ", \"rx_consumed\": " << rx_consumed << ",\n \"tx_completions\": [";
+  bool first = true;
+  while (auto c = qp.tx_completion().poll_completion()) { js << (first ? "" : ",") << "\n  " << completion_json(*c); first = false; }
+  js << "],\n \"rx_completions\": [";
+  first = true;
+  while (auto c = qp.rx_completion().poll_completion()) { js << (first ? "" : ",") << "\n  " << completion_json(*c); first = false; }
+  const auto& st = qp.stats();
+  js << "],\n \"stats\": [" << st.tx_packets << "," << st.rx_packets << "," << st.tx_bytes << "," << st.rx_bytes << ","
+     << st.drops_checksum << "," << st.drops_no_rx_desc << "," << st.drops_buffer_small << "," << st.drops_mtu_exceeded
+     << "," << st.drops_invalid_mss << "," << st.drops_too_many_segments << "," << st.tx_tso_segments << ","
+     << st.tx_gso_segments << "," << st.tx_vlan_insertions << "," << st.rx_vlan_strips << "," << st.rx_checksum_verified
+     << "," << st.rx_gro_aggregated << "],\n \"rx_region_fnv\": [";
+  std::vector<std::byte> after(mem_size);
+  assert(mem.read(0, after).ok());
+  for (std::size_t j = 0; j < nrx; ++j) {
+    const std::size_t a = std::min<std::size_t>(rxs[j].buffer_address, mem_size);
+    const std::size_t n = std::min<std::size_t>(rxs[j].buffer_length, mem_size - a);
+    js << (j ? "," : "") << "\"" << std::hex << fnv1a(after.data() + a, n) << std::dec << "\"";
+  }
+  js << "],\n \"mem_fnv\": \"" << std::hex << fnv1a(after.data(), mem_size) << std::dec << "\"\n}\n";
+  std::ofstream(g_out + "/" + name + ".json") << js.str();
+  write_bin(name + ".mem.bin", image);
+  std::vector<std::uint8_t> tb(txs.size() * sizeof(TxDescriptor)), rb(rxs.size() * sizeof(RxDescriptor));
+  std::memcpy(tb.data(), txs.data(), tb.size());
+  std::memcpy(rb.data(), rxs.data(), rb.size());
+  write_bin(name + ".tx.bin", tb);
+  write_bin(name + ".rx.bin", rb);
+}
+
+void gen_qp_batch() {
+  gen_qp_batch_case("qp_mix_a", 101, 300, 180, 0);    // RX ring runs dry part-way
+  gen_qp_batch_case("qp_mix_b", 202, 400, 700, 0);    // ample RX descriptors
+  gen_qp_batch_case("qp_tso", 303, 40, 300, 1);       // 9000 B TSO/GSO, odd mss, tiny headers
+}
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -671,6 +848,7 @@ int main(int argc, char** argv) {
   gen_rx_mix();
   gen_c1();
   gen_tso();
+  gen_qp_batch();
   std::printf("golden fixtures written to %s\n", g_out.c_str());
   return 0;
 }

@@ -53,6 +53,7 @@ ABI_SYMBOLS = (
     "nicgpu_rx_offload",
     "nicgpu_checksum_batch",
     "nicgpu_tso_checksum",
+    "nicgpu_segment_gather",
 )
 
 _lib = None

@@ -1,0 +1,482 @@
+// rx_stage.cpp — nic::BatchedQueuePair: the reference's
+// QueuePair::process_once (src/queue_pair.cpp:67-460) over a batch.
+//
+// 1. make_plan: per TX descriptor, the byte pieces whose ones'-complement sums
+//    the TX verify (:105-116) and the RX verifies (:434-447) will need.
+// 2. GPU: nicgpu_checksum_batch over all pieces (one pass over the TX bytes).
+// 3. resolve: the reference's control flow, in order, from those sums.
+//    Piece sums compose exactly: fold(a + b) is 0 only when a and b are, and
+//    a piece placed at an odd offset contributes its byte-swapped sum.
+// 4. GPU: nicgpu_segment_gather writes the delivered segments (the DMA writes
+//    of :416-426) into the RX buffers.
+// 5. GPU: RssEngine::select_queue_batch over the frames delivered with
+//    Success -> per-queue dispatch lists.
+#include "nic/rx_stage.h"
+
+#include <algorithm>
+#include <cstring>
+#include <limits>
+#include <string>
+
+#include "nic/checksum.h"
+#include "nicgpu.h"
+
+namespace nic {
+namespace rx_stage_detail {
+namespace {
+
+constexpr std::uint32_t kRun = 65534;  // even, so every run starts at an even offset
+
+inline std::uint32_t add1c(std::uint32_t a, std::uint32_t b) {
+  const std::uint32_t x = a + b;
+  return (x & 0xFFFFu) + (x >> 16);
+}
+inline std::uint32_t swap16(std::uint32_t x) { return ((x & 0xFFu) << 8) | (x >> 8); }
+// Folded sum of a piece from its checksum (compute_checksum = ~fold(sum)).
+inline std::uint32_t piece_sum(std::span<const std::uint16_t> cs, std::uint32_t i) {
+  return static_cast<std::uint32_t>(~cs[i]) & 0xFFFFu;
+}
+inline std::uint32_t at_offset(std::uint32_t s, std::uint64_t off) { return (off & 1) ? swap16(s) : s; }
+
+bool dma_ok(std::size_t mem_size, std::uint64_t addr, std::uint64_t len) {
+  // SimpleHostMemory::translate_view bounds rule (simple_host_memory.cpp:85-93)
+  return addr <= mem_size && len <= mem_size - addr;
+}
+
+struct SegDecision {
+  bool segmented = false;  // build_segments produced chunks
+  bool invalid_mss = false;
+  bool too_many = false;
+  std::uint32_t nseg = 1;
+  std::uint32_t H = 0;
+};
+
+// build_segments (queue_pair.cpp:212-278) without the copies.
+SegDecision decide_segments(const TxDescriptor& t) {
+  SegDecision d;
+  const std::uint64_t L = t.length;
+  const bool enabled = (t.tso_enabled || t.gso_enabled) && t.mss > 0 && L > t.mss;
+  if (!enabled) return d;
+  if (t.mss < kMinMss || t.mss > kMaxMss) {
+    d.invalid_mss = true;
+    return d;
+  }
+  if (t.header_length > L) {
+    d.invalid_mss = true;
+    return d;
+  }
+  d.H = t.header_length;
+  if (d.H >= L) return d;  // degenerate: one unsegmented copy (:250-252)
+  const std::uint64_t n = (L - d.H + t.mss - 1) / t.mss;
+  if (n > kMaxTsoSegments) {
+    d.too_many = true;
+    return d;
+  }
+  d.segmented = true;
+  d.nseg = static_cast<std::uint32_t>(n);
+  return d;
+}
+
+inline bool tx_verify_needed(const TxDescriptor& t) { return !t.checksum_offload && t.checksum != ChecksumMode::None; }
+
+void push_runs(std::vector<Piece>& pieces, std::uint64_t addr, std::uint64_t len) {
+  for (std::uint64_t o = 0; o < len; o += kRun)
+    pieces.push_back(Piece{addr + o, static_cast<std::uint32_t>(std::min<std::uint64_t>(kRun, len - o))});
+}
+
+// Sums a resolve step needs, for one TX packet.
+struct PacketSums {
+  const PacketPlan* p;
+  std::span<const std::uint16_t> cs;
+  std::uint64_t L;
+
+  std::uint32_t s(std::uint32_t k) const { return piece_sum(cs, p->first_piece + k); }
+
+  std::uint32_t chunk_len(std::uint32_t k) const {
+    const std::uint64_t o = static_cast<std::uint64_t>(p->hdr_len) + static_cast<std::uint64_t>(k) * p->mss;
+    return static_cast<std::uint32_t>(std::min<std::uint64_t>(p->mss, L - o));
+  }
+  // whole packet, as compute_checksum(packet) sums it
+  std::uint32_t whole() const {
+    std::uint32_t acc = 0;
+    if (p->kind == PacketPlan::kPlain) {
+      for (std::uint32_t i = 0; i < p->npieces; ++i) acc = add1c(acc, s(i));  // all runs start at even offsets
+      return acc;
+    }
+    const std::uint32_t H = p->hdr_len;
+    if (H >= 4) {
+      acc = add1c(s(0), s(1));
+      for (std::uint32_t k = 0; k < p->nseg; ++k)
+        acc = add1c(acc, at_offset(s(2 + k), H + static_cast<std::uint64_t>(k) * p->mss));
+    } else {
+      acc = s(0);
+      for (std::uint32_t k = 0; k < p->nseg; ++k) {
+        const std::uint64_t o = H + static_cast<std::uint64_t>(k) * p->mss;
+        const std::uint32_t n0 = std::min<std::uint32_t>(4 - H, chunk_len(k));
+        acc = add1c(acc, at_offset(s(1 + 2 * k), o));
+        acc = add1c(acc, at_offset(s(2 + 2 * k), o + n0));
+      }
+    }
+    return acc;
+  }
+  // segment k: sum of its first 4 bytes and of the rest (rest placed at offset 4)
+  void segment(std::uint32_t k, std::uint32_t& first4, std::uint32_t& rest) const {
+    if (p->kind == PacketPlan::kPlain) {
+      first4 = s(0);
+      rest = 0;
+      for (std::uint32_t i = 1; i < p->npieces; ++i) rest = add1c(rest, s(i));
+      return;
+    }
+    const std::uint32_t H = p->hdr_len;
+    if (H >= 4) {
+      first4 = s(0);
+      rest = add1c(s(1), at_offset(s(2 + k), H - 4));
+    } else {
+      first4 = add1c(s(0), at_offset(s(1 + 2 * k), H));
+      rest = s(2 + 2 * k);
+    }
+  }
+};
+
+}  // namespace
+
+Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx) {
+  Plan plan;
+  plan.packets.resize(tx.size());
+  for (std::size_t i = 0; i < tx.size(); ++i) {
+    const TxDescriptor& t = tx[i];
+    PacketPlan& pp = plan.packets[i];
+    pp.first_piece = static_cast<std::uint32_t>(plan.pieces.size());
+    const std::uint64_t L = t.length;
+    if (!dma_ok(mem_size, t.buffer_address, L)) continue;  // read fault: no bytes
+    const bool verify = tx_verify_needed(t);
+    const bool mtu_drop = L > config.max_mtu;
+    const SegDecision d = decide_segments(t);
+    const bool dropped = mtu_drop || d.invalid_mss || d.too_many;
+    if (dropped && !verify) continue;
+    if (!d.segmented || dropped) {
+      pp.kind = PacketPlan::kPlain;
+      plan.pieces.push_back(Piece{t.buffer_address, static_cast<std::uint32_t>(std::min<std::uint64_t>(4, L))});
+      if (L > 4) push_runs(plan.pieces, t.buffer_address + 4, L - 4);
+    } else {
+      pp.kind = PacketPlan::kSegmented;
+      pp.nseg = d.nseg;
+      pp.hdr_len = d.H;
+      pp.mss = t.mss;
+      const std::uint64_t a = t.buffer_address;
+      if (d.H >= 4) {
+        plan.pieces.push_back(Piece{a, 4});
+        plan.pieces.push_back(Piece{a + 4, d.H - 4});
+        for (std::uint32_t k = 0; k < d.nseg; ++k) {
+          const std::uint64_t o = d.H + static_cast<std::uint64_t>(k) * t.mss;
+          plan.pieces.push_back(Piece{a + o, static_cast<std::uint32_t>(std::min<std::uint64_t>(t.mss, L - o))});
+        }
+      } else {
+        plan.pieces.push_back(Piece{a, d.H});
+        for (std::uint32_t k = 0; k < d.nseg; ++k) {
+          const std::uint64_t o = d.H + static_cast<std::uint64_t>(k) * t.mss;
+          const std::uint32_t len = static_cast<std::uint32_t>(std::min<std::uint64_t>(t.mss, L - o));
+          const std::uint32_t n0 = std::min<std::uint32_t>(4 - d.H, len);
+          plan.pieces.push_back(Piece{a + o, n0});
+          plan.pieces.push_back(Piece{a + o + n0, len - n0});
+        }
+      }
+    }
+    pp.npieces = static_cast<std::uint32_t>(plan.pieces.size()) - pp.first_piece;
+  }
+  return plan;
+}
+
+void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
+             std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
+             std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
+             std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx) {
+  const std::uint16_t qid = config.queue_id;
+  auto post_tx = [&](const CompletionEntry& e, bool fire) {
+    out.tx_completions.push_back(e);
+    if (fire && config.enable_tx_interrupts && config.on_interrupt) config.on_interrupt(qid, e);  // :371-376
+  };
+  auto post_rx = [&](const CompletionEntry& e, std::int64_t w) {
+    out.rx_completions.push_back(e);
+    write_of_rx.push_back(w);
+    if (config.enable_rx_interrupts && config.on_interrupt) config.on_interrupt(qid, e);  // :378-383
+  };
+  auto make_completion = [&](std::uint16_t idx, CompletionCode st) {  // :150-158
+    CompletionEntry e{};
+    e.queue_id = qid;
+    e.descriptor_index = idx;
+    e.status = static_cast<std::uint32_t>(st);
+    return e;
+  };
+  auto make_tx = [&](const TxDescriptor& t, CompletionCode st, std::size_t segs, bool tso, bool gso) {  // :160-177
+    CompletionEntry e = make_completion(t.descriptor_index, st);
+    e.checksum_offloaded = t.checksum_offload;
+    e.tso_performed = tso;
+    e.gso_performed = gso;
+    e.segments_produced = static_cast<std::uint16_t>(std::min<std::size_t>(segs, std::numeric_limits<std::uint16_t>::max()));
+    if (t.vlan_insert) {
+      e.vlan_inserted = true;
+      e.vlan_tag = t.vlan_tag;
+    }
+    return e;
+  };
+
+  std::size_t rc = 0;  // RX ring consumer position
+  for (std::size_t i = 0; i < tx.size(); ++i) {
+    const TxDescriptor& t = tx[i];
+    const PacketPlan& pp = plan.packets[i];
+    const PacketSums ps{&pp, piece_csum, t.length};
+    const std::uint64_t L = t.length;
+    // :75-83 no RX descriptor at all
+    if (rc == rx.size()) {
+      post_tx(make_tx(t, CompletionCode::NoDescriptor, 0, false, false), true);
+      stats.drops_no_rx_desc += 1;
+      continue;
+    }
+    // :86-92 DMA read
+    if (!dma_ok(mem_size, t.buffer_address, L)) {
+      post_tx(make_tx(t, CompletionCode::Fault, 0, false, false), true);
+      continue;
+    }
+    // :94-105 TX checksum verify
+    if (tx_verify_needed(t)) {
+      const std::uint16_t computed = static_cast<std::uint16_t>(~ps.whole() & 0xFFFFu);
+      if (computed != t.checksum_value) {
+        post_tx(make_tx(t, CompletionCode::ChecksumError, 0, false, false), true);
+        stats.drops_checksum += 1;
+        continue;
+      }
+    }
+    // :195-210 MTU
+    if (L > config.max_mtu) {
+      post_tx(make_tx(t, CompletionCode::MtuExceeded, 0, false, false), true);
+      stats.drops_mtu_exceeded += 1;
+      continue;
+    }
+    // :212-278 segmentation
+    const SegDecision d = decide_segments(t);
+    if (d.invalid_mss) {
+      post_tx(make_tx(t, CompletionCode::InvalidMss, 0, false, false), true);
+      stats.drops_invalid_mss += 1;
+      continue;
+    }
+    if (d.too_many) {
+      post_tx(make_tx(t, CompletionCode::TooManySegments, 0, false, false), true);
+      stats.drops_too_many_segments += 1;
+      continue;
+    }
+    const std::uint32_t total = d.nseg;
+    const bool tso = t.tso_enabled && total > 1;
+    const bool gso = t.gso_enabled && total > 1;
+    // :293-303 enough RX descriptors for every segment
+    if (rx.size() - rc < total) {
+      post_tx(make_tx(t, CompletionCode::NoDescriptor, 0, tso, gso), true);
+      stats.drops_no_rx_desc += 1;
+      continue;
+    }
+    bool aborted = false;
+    for (std::uint32_t k = 0; k < total; ++k) {
+      RxDescriptor x = rx[rc++];
+      if (t.vlan_insert) x.vlan_present = true;  // :320-322
+      // base segment = header || chunk k (or the whole packet)
+      std::uint64_t src_a = t.buffer_address, src_b = 0;
+      std::uint32_t len_a, len_b = 0;
+      if (d.segmented) {
+        len_a = d.H;
+        src_b = t.buffer_address + d.H + static_cast<std::uint64_t>(k) * t.mss;
+        len_b = ps.chunk_len(k);
+      } else {
+        len_a = static_cast<std::uint32_t>(L);
+      }
+      const std::uint64_t base_len = static_cast<std::uint64_t>(len_a) + len_b;
+      // :324-331 VLAN insert, :389-395 strip
+      std::uint64_t size = base_len + (t.vlan_insert ? 4 : 0);
+      const bool has_vlan = t.vlan_insert || x.vlan_present;
+      const bool strip = x.vlan_strip && has_vlan && size >= 4;
+      if (strip) size -= 4;
+      const bool prefix = t.vlan_insert && !strip;
+      const bool strip_base = strip && !t.vlan_insert;  // the base segment loses its first 4 bytes
+      // :397-414 buffer too small
+      if (x.buffer_length < size) {
+        post_tx(make_tx(t, CompletionCode::Success, total, tso, gso), false);
+        CompletionEntry e = make_completion(x.descriptor_index, CompletionCode::BufferTooSmall);
+        e.vlan_stripped = x.vlan_strip && has_vlan;
+        if (e.vlan_stripped) e.vlan_tag = t.vlan_insert ? t.vlan_tag : x.vlan_tag;
+        post_rx(e, -1);
+        stats.drops_buffer_small += 1;
+        aborted = true;
+        break;
+      }
+      // :416-426 DMA write
+      if (!dma_ok(mem_size, x.buffer_address, size)) {
+        post_tx(make_tx(t, CompletionCode::Fault, total, tso, gso), false);
+        post_rx(make_completion(x.descriptor_index, CompletionCode::Fault), -1);
+        aborted = true;
+        break;
+      }
+      SegmentWrite w{};
+      w.dst = x.buffer_address;
+      if (prefix) {
+        const std::uint32_t tag = t.vlan_tag;
+        w.prefix = 0x81u | (0x00u << 8) | (((tag >> 8) & 0xFFu) << 16) | ((tag & 0xFFu) << 24);
+        w.prefix_len = 4;
+      }
+      if (strip_base) {  // drop the first 4 bytes of header || chunk
+        const std::uint32_t from_a = std::min<std::uint32_t>(4, len_a);
+        src_a += from_a;
+        len_a -= from_a;
+        src_b += 4 - from_a;
+        len_b -= 4 - from_a;
+      }
+      w.src_a = src_a;
+      w.len_a = len_a;
+      w.src_b = src_b;
+      w.len_b = len_b;
+      writes.push_back(w);
+      const std::int64_t wi = static_cast<std::int64_t>(writes.size()) - 1;
+
+      CompletionEntry e = make_completion(x.descriptor_index, CompletionCode::Success);
+      e.gro_aggregated = x.gro_enabled;
+      if (e.gro_aggregated) stats.rx_gro_aggregated += 1;
+      // :434-447 RX checksum verify of the delivered bytes
+      if (x.checksum_offload && x.checksum != ChecksumMode::None) {
+        e.checksum_verified = true;
+        stats.rx_checksum_verified += 1;
+        std::uint32_t first4, rest;
+        ps.segment(k, first4, rest);
+        std::uint32_t sum;
+        if (strip_base) sum = rest;
+        else sum = add1c(first4, rest);
+        if (prefix) sum = add1c(add1c(0x8100u, t.vlan_tag), sum);
+        if ((~sum & 0xFFFFu) != 0) {
+          e.status = static_cast<std::uint32_t>(CompletionCode::ChecksumError);
+          post_rx(e, wi);
+          post_tx(make_tx(t, CompletionCode::Success, total, tso, gso), false);
+          stats.drops_checksum += 1;
+          aborted = true;
+          break;
+        }
+      }
+      e.vlan_stripped = x.vlan_strip && has_vlan;
+      if (e.vlan_stripped) {
+        e.vlan_tag = t.vlan_insert ? t.vlan_tag : x.vlan_tag;
+        stats.rx_vlan_strips += 1;
+      }
+      post_rx(e, wi);
+      stats.rx_packets += 1;
+      stats.rx_bytes += size;
+    }
+    if (aborted) continue;
+    // :280-301 finalize_tx_success
+    post_tx(make_tx(t, CompletionCode::Success, total, tso, gso), true);
+    stats.tx_packets += total;
+    stats.tx_bytes += L;
+    if (tso) stats.tx_tso_segments += total;
+    if (gso) stats.tx_gso_segments += total;
+    if (t.vlan_insert) stats.tx_vlan_insertions += total;
+  }
+  out.tx_processed = tx.size();
+  out.rx_consumed = rc;
+}
+
+}  // namespace rx_stage_detail
+
+namespace {
+
+void check(int st, const char* what) {
+  if (st != NICGPU_OK) throw GpuError(std::string(what) + ": " + nicgpu_strerror(st), st);
+}
+
+// Device scratch owned for the duration of one batch.
+struct DevScratch {
+  void* p = nullptr;
+  explicit DevScratch(std::size_t n) { check(nicgpu_malloc(&p, n ? n : 16), "nicgpu_malloc"); }
+  ~DevScratch() { nicgpu_free(p); }
+  DevScratch(const DevScratch&) = delete;
+  DevScratch& operator=(const DevScratch&) = delete;
+};
+
+}  // namespace
+
+BatchedQueuePair::BatchedQueuePair(BatchedQueuePairConfig config) : config_(std::move(config)) {}
+
+RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
+                                              std::span<const RxDescriptor> rx, void* stream) {
+  using namespace rx_stage_detail;
+  if (mem.base == nullptr && mem.size != 0) throw GpuError("process_batch: null host-memory image", NICGPU_ERR_INVALID);
+  const Plan plan = make_plan(config_, mem.size, tx);
+  const std::size_t np = plan.pieces.size();
+
+  // (2) piece sums on the GPU
+  std::vector<std::uint16_t> csum(np);
+  if (np) {
+    std::vector<std::uint64_t> desc(np);
+    for (std::size_t i = 0; i < np; ++i) desc[i] = NICGPU_DESC(plan.pieces[i].addr, plan.pieces[i].len);
+    DevScratch d_desc(np * 8), d_cs(np * 2);
+    check(nicgpu_memcpy_async(d_desc.p, desc.data(), np * 8, stream), "nicgpu_memcpy_async");
+    check(nicgpu_checksum_batch(reinterpret_cast<const std::uint8_t*>(mem.base), static_cast<const std::uint64_t*>(d_desc.p),
+                                np, static_cast<std::uint16_t*>(d_cs.p), stream),
+          "nicgpu_checksum_batch");
+    check(nicgpu_memcpy_async(csum.data(), d_cs.p, np * 2, stream), "nicgpu_memcpy_async");
+    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+  }
+
+  // (3) the reference's control flow
+  RxBatchResult out;
+  std::vector<SegmentWrite> writes;
+  std::vector<std::int64_t> write_of_rx;
+  QueuePairStats st = stats_;
+  resolve(config_, mem.size, plan, csum, tx, rx, st, out, writes, write_of_rx);
+
+  // (4) DMA writes of every segment that reached the RX buffer
+  if (!writes.empty()) {
+    DevScratch d_w(writes.size() * sizeof(SegmentWrite));
+    check(nicgpu_memcpy_async(d_w.p, writes.data(), writes.size() * sizeof(SegmentWrite), stream), "nicgpu_memcpy_async");
+    check(nicgpu_segment_gather(reinterpret_cast<std::uint8_t*>(mem.base), mem.size,
+                                static_cast<const nicgpu_segment_write*>(d_w.p), writes.size(), stream),
+          "nicgpu_segment_gather");
+    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+  }
+
+  // (5) RSS over frames delivered with Success
+  const std::size_t nrx = out.rx_completions.size();
+  out.rx_hash.assign(nrx, 0);
+  out.rx_queue.assign(nrx, RxBatchResult::kNoQueue);
+  if (config_.rss != nullptr) {
+    std::vector<std::uint32_t> which;
+    std::vector<std::uint64_t> desc;
+    for (std::size_t j = 0; j < nrx; ++j) {
+      if (out.rx_completions[j].status != static_cast<std::uint32_t>(CompletionCode::Success) || write_of_rx[j] < 0) continue;
+      const SegmentWrite& w = writes[static_cast<std::size_t>(write_of_rx[j])];
+      const std::uint64_t len = static_cast<std::uint64_t>(w.prefix_len) + w.len_a + w.len_b;
+      if (len > NICGPU_MAX_PACKET) throw GpuError("process_batch: delivered frame longer than NICGPU_MAX_PACKET", NICGPU_ERR_INVALID);
+      which.push_back(static_cast<std::uint32_t>(j));
+      desc.push_back(NICGPU_DESC(w.dst, len));
+    }
+    if (!which.empty()) {
+      const std::size_t m = which.size();
+      DevScratch d_desc(m * 8), d_h(m * 4), d_q(m * 2);
+      check(nicgpu_memcpy_async(d_desc.p, desc.data(), m * 8, stream), "nicgpu_memcpy_async");
+      config_.rss->select_queue_batch(
+          DevicePacketBatch{mem.base, static_cast<const std::uint64_t*>(d_desc.p), m}, config_.tuple,
+          RxBatchOutputs{nullptr, static_cast<std::uint32_t*>(d_h.p), static_cast<std::uint16_t*>(d_q.p)}, stream, true);
+      std::vector<std::uint32_t> h(m);
+      std::vector<std::uint16_t> q(m);
+      check(nicgpu_memcpy_async(h.data(), d_h.p, m * 4, stream), "nicgpu_memcpy_async");
+      check(nicgpu_memcpy_async(q.data(), d_q.p, m * 2, stream), "nicgpu_memcpy_async");
+      check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+      std::uint16_t qmax = 0;
+      for (std::size_t i = 0; i < m; ++i) {
+        out.rx_hash[which[i]] = h[i];
+        out.rx_queue[which[i]] = q[i];
+        qmax = std::max(qmax, q[i]);
+      }
+      out.queues.resize(static_cast<std::size_t>(qmax) + 1);
+      for (std::size_t i = 0; i < m; ++i) out.queues[q[i]].push_back(which[i]);
+    }
+  }
+  stats_ = st;
+  return out;
+}
+
+}  // namespace nic

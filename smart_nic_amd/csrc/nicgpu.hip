@@ -966,6 +966,79 @@ const RxVariant kRxVariants[] = {
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
 
+// ------------------------------------------------------ segment gather --
+// The DMA writes of the batched QueuePair stage (QueuePair::handle_rx_segment,
+// src/queue_pair.cpp:416-426): dst <- prefix (0/4 B, the inserted VLAN tag)
+// || [src_a, +len_a) || [src_b, +len_b), all inside one memory image.  One
+// wave per write.  Whole destination dwords are assembled from two aligned
+// source dwords with v_alignbyte (4 dwords = 16 B per lane per step, lanes
+// contiguous); the partial dwords at the ends of each part are written with
+// byte stores, so writes that share a dword never race.  Pure byte movement:
+// HBM-bound at 2 x bytes.
+struct GatherParams {
+  uint8_t* mem;
+  uint64_t mem_size;
+  const nicgpu_segment_write* w;
+  size_t n;
+};
+
+__device__ __forceinline__ uint32_t load_dword_clamped(const uint8_t* mem, uint64_t mem_size, uint64_t a) {
+  if (a + 4 <= mem_size) return *reinterpret_cast<const uint32_t*>(mem + a);
+  uint32_t v = 0;
+  for (uint32_t j = 0; j < 4; ++j)
+    if (a + j < mem_size) v |= (uint32_t) mem[a + j] << (8 * j);
+  return v;
+}
+
+// Wave-cooperative copy of [src, src+len) to [dst, dst+len), any alignment.
+__device__ void wave_copy(uint8_t* mem, uint64_t mem_size, uint64_t dst, uint64_t src, uint64_t len, uint32_t lane) {
+  if (len == 0) return;
+  const uint64_t d1 = dst + len;
+  const uint64_t A = (dst + 3) & ~3ull;  // first whole dword
+  const uint64_t B = d1 & ~3ull;          // end of the last whole dword
+  if (A >= B) {                           // no whole dword: bytes only
+    if (lane < len) mem[dst + lane] = mem[src + lane];
+    return;
+  }
+  const uint64_t head = A - dst, tail = d1 - B;
+  if (lane < head) mem[dst + lane] = mem[src + lane];
+  if (lane >= 8 && lane - 8 < tail) mem[B + (lane - 8)] = mem[src + (B - dst) + (lane - 8)];
+  const uint64_t nw = (B - A) >> 2;
+  const uint64_t s0 = src + head;  // source of dword A
+  const uint32_t sh = (uint32_t) (s0 & 3);
+  const uint64_t sa = s0 & ~3ull;
+  for (uint64_t i = (uint64_t) lane * 4; i < nw; i += 256) {
+    uint32_t v[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) v[j] = (i + j <= nw) ? load_dword_clamped(mem, mem_size, sa + 4 * (i + j)) : 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (i + j < nw) {
+        const uint32_t o = sh ? __builtin_amdgcn_alignbyte(v[j + 1], v[j], sh) : v[j];
+        *reinterpret_cast<uint32_t*>(mem + A + 4 * (i + j)) = o;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void segment_gather_kernel(GatherParams P) {
+  const uint32_t lane = lane_id();
+  const uint64_t wave = (uint64_t) blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+  const uint64_t nwaves = (uint64_t) gridDim.x * kWavesPerBlock;
+  for (uint64_t e = wave; e < P.n; e += nwaves) {
+    const nicgpu_segment_write w = P.w[e];
+    const uint64_t plen = w.prefix_len == 4 ? 4 : 0;
+    const uint64_t total = plen + w.len_a + w.len_b;
+    // entries outside the image are skipped (the host validated them)
+    if (w.prefix_len > 4 || w.dst > P.mem_size || total > P.mem_size - w.dst || w.src_a > P.mem_size ||
+        w.len_a > P.mem_size - w.src_a || w.src_b > P.mem_size || w.len_b > P.mem_size - w.src_b)
+      continue;
+    if (lane < plen) P.mem[w.dst + lane] = (uint8_t) (w.prefix >> (8 * lane));
+    wave_copy(P.mem, P.mem_size, w.dst + plen, w.src_a, w.len_a, lane);
+    wave_copy(P.mem, P.mem_size, w.dst + plen + w.len_a, w.src_b, w.len_b, lane);
+  }
+}
+
 struct DeviceInfo {
   bool init = false;
   int status = 0;
@@ -1309,6 +1382,21 @@ int nicgpu_tso_checksum(const uint8_t* frames, const uint64_t* desc, const uint1
   const uint64_t cap = (uint64_t) di->cus * (uint64_t) di->tso_blocks_per_cu * 2;
   const unsigned grid = (unsigned) (want < cap ? want : cap);
   hipLaunchKernelGGL(tso_checksum_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
+  return hip_status(hipGetLastError());
+}
+
+int nicgpu_segment_gather(uint8_t* mem, uint64_t mem_size, const nicgpu_segment_write* writes, size_t n,
+                          void* stream) {
+  if (n == 0) return NICGPU_OK;
+  if (!mem || !writes) return NICGPU_ERR_INVALID;
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  GatherParams P{mem, mem_size, writes, n};
+  const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint64_t cap = (uint64_t) di->cus * 8;
+  const unsigned grid = (unsigned) (want < cap ? want : cap);
+  hipLaunchKernelGGL(segment_gather_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
   return hip_status(hipGetLastError());
 }
 

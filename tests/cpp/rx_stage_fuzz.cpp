@@ -1,0 +1,222 @@
+// rx_stage_fuzz.cpp — randomised batches through the reference QueuePair
+// (src/queue_pair.cpp:67-460, compiled from /root/reference in this
+// container) and through nic::BatchedQueuePair's host logic
+// (rx_stage_detail::make_plan + resolve, piece sums from the oracle), in the
+// same process.  Compared per batch: every TX/RX CompletionEntry in posting
+// order, QueuePairStats, RX descriptors consumed, interrupts delivered (the
+// reference's InterruptDispatcher with a packet threshold of 1) and the whole
+// memory image after the DMA writes.
+//
+//   rx_stage_fuzz <first_seed> <count>
+#undef NDEBUG
+#include <cassert>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "nic/dma_engine.h"
+#include "nic/interrupt_dispatcher.h"
+#include "nic/queue_pair.h"
+#include "nic/rx_stage.h"
+#include "nic/simple_host_memory.h"
+#include "oracle.h"
+
+using namespace nic;
+
+namespace {
+
+struct Rng {
+  std::uint64_t s;
+  std::uint64_t next() {
+    std::uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  std::uint32_t below(std::uint32_t n) { return n ? static_cast<std::uint32_t>((next() >> 32) % n) : 0; }
+  std::uint8_t byte() { return static_cast<std::uint8_t>(next() >> 56); }
+};
+
+bool same(const CompletionEntry& a, const CompletionEntry& b) {
+  return a.queue_id == b.queue_id && a.descriptor_index == b.descriptor_index && a.status == b.status &&
+         a.checksum_offloaded == b.checksum_offloaded && a.checksum_verified == b.checksum_verified &&
+         a.tso_performed == b.tso_performed && a.gso_performed == b.gso_performed && a.vlan_inserted == b.vlan_inserted &&
+         a.vlan_stripped == b.vlan_stripped && a.gro_aggregated == b.gro_aggregated &&
+         a.segments_produced == b.segments_produced && a.vlan_tag == b.vlan_tag;
+}
+
+bool same(const QueuePairStats& a, const QueuePairStats& b) { return std::memcmp(&a, &b, sizeof(a)) == 0; }
+
+// Balance a buffer so that compute_checksum(buf) == 0 by adjusting the 16-bit
+// word at even offset `at` (needs at + 2 <= size).
+void balance(std::vector<std::uint8_t>& b, std::size_t at) {
+  b[at] = b[at + 1] = 0;
+  const std::uint16_t c = oracle_compute_checksum(b.data(), b.size());  // ~sum
+  b[at] = static_cast<std::uint8_t>(c >> 8);
+  b[at + 1] = static_cast<std::uint8_t>(c);
+}
+
+int run_case(std::uint64_t seed) {
+  Rng r{seed * 7919 + 1};
+  const std::size_t ntx = 1 + r.below(120);
+  const std::size_t nrx = r.below(220);
+  const std::size_t mtus[] = {9000, 1500, 3000, 65535};
+  const std::size_t max_mtu = mtus[r.below(4)];
+  std::vector<TxDescriptor> tx(ntx);
+  std::vector<std::vector<std::uint8_t>> pkts(ntx);
+  std::vector<std::uint64_t> addr(ntx);
+  std::size_t at = 0;
+  for (std::size_t i = 0; i < ntx; ++i) {
+    const std::uint32_t pick = r.below(16);
+    std::size_t L = pick < 4 ? r.below(70) : (pick < 9 ? 60 + r.below(1500) : (pick < 14 ? 9000 : 9000 + r.below(70000)));
+    auto& p = pkts[i];
+    p.resize(L);
+    const bool zero = r.below(40) == 0;
+    for (auto& b : p) b = zero ? 0 : r.byte();
+    if (L >= 16 && r.below(2)) balance(p, 10);
+    at += r.below(3) == 0 ? r.below(9) : 0;
+    addr[i] = at;
+    at += L;
+    TxDescriptor& t = tx[i];
+    t.buffer_address = addr[i];
+    t.length = static_cast<std::uint32_t>(L);
+    t.descriptor_index = static_cast<std::uint16_t>(r.below(65536));
+    t.checksum = static_cast<ChecksumMode>(r.below(3));
+    t.checksum_offload = r.below(2);
+    const std::uint16_t good = oracle_compute_checksum(p.data(), L);
+    t.checksum_value = r.below(4) == 0 ? static_cast<std::uint16_t>(r.below(65536)) : good;
+    if (r.below(3) == 0) {
+      t.tso_enabled = r.below(2);
+      t.gso_enabled = !t.tso_enabled || r.below(3) == 0;
+      const std::uint32_t mp = r.below(10);
+      t.mss = static_cast<std::uint16_t>(mp == 0 ? 0 : (mp == 1 ? 9001 + r.below(3) : (mp < 4 ? 1 + r.below(9) : 50 + r.below(2000))));
+      const std::uint32_t hp = r.below(8);
+      t.header_length = static_cast<std::uint16_t>(hp == 0 ? r.below(4) : (hp == 1 ? L + r.below(2) : (hp == 2 ? r.below(12) : 14 + r.below(60))));
+    }
+    if (r.below(4) == 0) {
+      t.vlan_insert = true;
+      t.vlan_tag = static_cast<std::uint16_t>(r.below(65536));
+    }
+  }
+  at = (at + 15) & ~std::size_t{15};
+  std::vector<RxDescriptor> rx(nrx);
+  for (std::size_t j = 0; j < nrx; ++j) {
+    RxDescriptor& x = rx[j];
+    const std::uint32_t bp = r.below(8);
+    x.buffer_length = bp == 0 ? r.below(200) : (bp < 4 ? 2000 : 9300);
+    x.buffer_address = at + r.below(5);
+    at = x.buffer_address + x.buffer_length + r.below(4);
+    x.descriptor_index = static_cast<std::uint16_t>(r.below(65536));
+    x.checksum = static_cast<ChecksumMode>(r.below(3));
+    x.checksum_offload = r.below(3) != 0;
+    x.vlan_strip = r.below(3) == 0;
+    x.vlan_present = r.below(3) == 0;
+    x.vlan_tag = static_cast<std::uint16_t>(r.below(65536));
+    x.gro_enabled = r.below(4) == 0;
+  }
+  const std::size_t mem_size = at + 32;
+  for (std::size_t i = 0; i < ntx; ++i)
+    if (r.below(40) == 0) tx[i].buffer_address = r.below(2) ? mem_size + 1 + i : mem_size - tx[i].length / 2;
+  for (std::size_t j = 0; j < nrx; ++j)
+    if (r.below(50) == 0) rx[j].buffer_address = mem_size + 1 + j;
+  std::vector<std::uint8_t> image(mem_size, 0);
+  for (std::size_t i = 0; i < ntx; ++i) std::memcpy(image.data() + addr[i], pkts[i].data(), pkts[i].size());
+  const bool tx_irq = r.below(2), rx_irq = r.below(4) != 0;
+  const std::uint16_t qid = static_cast<std::uint16_t>(r.below(8));
+
+  // ---- reference
+  SimpleHostMemory mem{HostMemoryConfig{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false}};
+  assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(image))).ok());
+  DMAEngine dma{mem};
+  std::size_t ref_irq = 0;
+  MsixTable table(8);
+  InterruptDispatcher disp{table, MsixMapping(8, 0), CoalesceConfig{1, 0},
+                           [&](std::uint16_t, std::uint32_t n) { ref_irq += n; }};
+  QueuePairConfig qc{
+      .queue_id = qid,
+      .tx_ring = {.descriptor_size = sizeof(TxDescriptor), .ring_size = ntx + 1, .base_address = 0, .queue_id = qid, .host_backed = false},
+      .rx_ring = {.descriptor_size = sizeof(RxDescriptor), .ring_size = nrx + 1, .base_address = 0, .queue_id = qid, .host_backed = false},
+      .tx_completion = {.ring_size = ntx + 1, .queue_id = qid},
+      .rx_completion = {.ring_size = 70 * ntx + 1, .queue_id = qid},
+      .interrupt_dispatcher = &disp,
+      .max_mtu = max_mtu,
+      .enable_tx_interrupts = tx_irq,
+      .enable_rx_interrupts = rx_irq,
+  };
+  QueuePair qp{qc, dma};
+  for (auto& t : tx) {
+    std::vector<std::byte> b(sizeof(TxDescriptor));
+    std::memcpy(b.data(), &t, sizeof(t));
+    assert(qp.tx_ring().push_descriptor(b).ok());
+  }
+  for (auto& x : rx) {
+    std::vector<std::byte> b(sizeof(RxDescriptor));
+    std::memcpy(b.data(), &x, sizeof(x));
+    assert(qp.rx_ring().push_descriptor(b).ok());
+  }
+  while (qp.process_once()) {
+  }
+  std::vector<CompletionEntry> ref_tx, ref_rx;
+  while (auto c = qp.tx_completion().poll_completion()) ref_tx.push_back(*c);
+  while (auto c = qp.rx_completion().poll_completion()) ref_rx.push_back(*c);
+  std::vector<std::byte> ref_after(mem_size);
+  assert(mem.read(0, ref_after).ok());
+
+  // ---- batched stage (host logic; sums from the oracle)
+  using namespace rx_stage_detail;
+  BatchedQueuePairConfig cfg;
+  cfg.queue_id = qid;
+  cfg.max_mtu = max_mtu;
+  cfg.enable_tx_interrupts = tx_irq;
+  cfg.enable_rx_interrupts = rx_irq;
+  std::size_t our_irq = 0;
+  cfg.on_interrupt = [&](std::uint16_t q, const CompletionEntry&) {
+    assert(q == qid);
+    ++our_irq;
+  };
+  const Plan plan = make_plan(cfg, mem_size, tx);
+  std::vector<std::uint16_t> cs(plan.pieces.size());
+  for (std::size_t i = 0; i < cs.size(); ++i) {
+    assert(plan.pieces[i].len <= 65535u);
+    cs[i] = oracle_compute_checksum(image.data() + plan.pieces[i].addr, plan.pieces[i].len);
+  }
+  RxBatchResult out;
+  QueuePairStats st{};
+  std::vector<SegmentWrite> writes;
+  std::vector<std::int64_t> wof;
+  resolve(cfg, mem_size, plan, cs, tx, rx, st, out, writes, wof);
+  std::vector<std::uint8_t> ours = image;
+  for (const auto& w : writes) {
+    std::uint64_t d = w.dst;
+    for (std::uint32_t j = 0; j < w.prefix_len; ++j) ours[d++] = static_cast<std::uint8_t>(w.prefix >> (8 * j));
+    std::memcpy(ours.data() + d, image.data() + w.src_a, w.len_a);
+    std::memcpy(ours.data() + d + w.len_a, image.data() + w.src_b, w.len_b);
+  }
+
+  bool ok = out.tx_completions.size() == ref_tx.size() && out.rx_completions.size() == ref_rx.size();
+  for (std::size_t i = 0; ok && i < ref_tx.size(); ++i) ok = same(out.tx_completions[i], ref_tx[i]);
+  for (std::size_t i = 0; ok && i < ref_rx.size(); ++i) ok = same(out.rx_completions[i], ref_rx[i]);
+  ok = ok && same(st, qp.stats());
+  ok = ok && out.rx_consumed == nrx - qp.rx_ring().available();
+  ok = ok && our_irq == ref_irq;
+  ok = ok && std::memcmp(ours.data(), ref_after.data(), mem_size) == 0;
+  if (!ok) {
+    std::fprintf(stderr, "seed %llu: mismatch (tx %zu/%zu rx %zu/%zu irq %zu/%zu)\n", (unsigned long long) seed,
+                 out.tx_completions.size(), ref_tx.size(), out.rx_completions.size(), ref_rx.size(), our_irq, ref_irq);
+    return 1;
+  }
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const std::uint64_t first = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
+  const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 200;
+  int bad = 0;
+  for (std::uint64_t s = first; s < first + count; ++s) bad += run_case(s);
+  if (bad) return 1;
+  std::printf("rx_stage_fuzz: ok (%llu batches)\n", (unsigned long long) count);
+  return 0;
+}

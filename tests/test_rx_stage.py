@@ -1,0 +1,89 @@
+"""Batched QueuePair RX stage (nic::BatchedQueuePair) against
+batches run through the reference QueuePair::process_once
+(tests/golden/qp_*.json; oracle/gen_golden.cpp, src/queue_pair.cpp:67-460).
+
+cpu: the stage's host logic (plan + resolve) with piece checksums from the
+     oracle and the DMA writes applied on a host copy — completions, stats and
+     the RX buffer bytes must equal the reference's.
+gpu: the product path end to end (GPU piece sums, GPU gather of the segments,
+     GPU RSS of the delivered frames), same comparison plus RSS dispatch.
+"""
+
+import json
+import os
+import subprocess
+
+import pytest
+
+from test_host_cpp import _build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+CASES = ["qp_mix_a", "qp_mix_b", "qp_tso"]
+
+
+def _flatten(name, out_dir):
+    d = json.load(open(os.path.join(GOLDEN, name + ".json")))
+    lines = [f'{d["queue_id"]} {d["max_mtu"]} {d["mem_size"]} {d["ntx"]} {d["nrx"]} {d["rx_consumed"]}']
+    for key in ("tx_completions", "rx_completions"):
+        lines.append(str(len(d[key])))
+        lines += [" ".join(str(x) for x in c) for c in d[key]]
+    lines.append(" ".join(str(x) for x in d["stats"]))
+    lines.append(" ".join(d["rx_region_fnv"]))
+    lines.append(d["mem_fnv"])
+    path = os.path.join(out_dir, name + ".expect.txt")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return path
+
+
+def _run(exe, mode, name, tmp_path):
+    exp = _flatten(name, str(tmp_path))
+    args = [exe, mode, exp] + [os.path.join(GOLDEN, f"{name}.{k}.bin") for k in ("mem", "tx", "rx")]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert f"rx_stage_test {mode}: ok" in r.stdout
+
+
+def test_fixture_coverage():
+    """The fixtures exercise every TX and RX status the reference posts."""
+    tx_st, rx_st = set(), set()
+    for n in CASES:
+        d = json.load(open(os.path.join(GOLDEN, n + ".json")))
+        tx_st |= {c[2] for c in d["tx_completions"]}
+        rx_st |= {c[2] for c in d["rx_completions"]}
+        assert d["rx_consumed"] <= d["nrx"]
+    assert tx_st == {0, 2, 3, 4, 5, 6, 7}  # Success, ChecksumError, NoDescriptor, Fault, Mtu, InvalidMss, TooMany
+    assert rx_st == {0, 1, 2, 4}  # Success, BufferTooSmall, ChecksumError, Fault
+
+
+def test_rx_stage_host_logic(tmp_path):
+    exe = _build(tmp_path, "rx_stage_test")
+    for n in CASES:
+        _run(exe, "cpu", n, tmp_path)
+
+
+@pytest.mark.gpu
+def test_rx_stage_gpu(tmp_path):
+    exe = _build(tmp_path, "rx_stage_test")
+    for n in CASES:
+        _run(exe, "gpu", n, tmp_path)
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="needs /root/reference (build container)")
+def test_rx_stage_fuzz_vs_reference_queue_pair():
+    """2000 random batches: the reference QueuePair (compiled in place from
+    /root/reference, this build's nic/ headers first) vs the stage's host logic
+    in one process — completions, stats, interrupts, memory image."""
+    import test_dropin_link as dl
+
+    objs = dl._objects()
+    exe = os.path.join(dl.OUT, "rx_stage_fuzz")
+    r = subprocess.run(["g++", "-std=c++20", "-O2", "-UNDEBUG", f"-I{ROOT}/include", f"-I{dl.REF}/include",
+                        f"-I{ROOT}/oracle", os.path.join(ROOT, "tests", "cpp", "rx_stage_fuzz.cpp"), "-x", "c",
+                        os.path.join(ROOT, "oracle", "oracle.c"), "-x", "none", *objs, f"-L{dl.PKG}", "-lnic_host",
+                        "-lnicgpu", f"-Wl,-rpath,{dl.PKG}", "-o", exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    run = subprocess.run([exe, "1", "2000"], capture_output=True, text=True, timeout=600)
+    assert run.returncode == 0, run.stdout[-2000:] + run.stderr[-2000:]
+    assert "rx_stage_fuzz: ok" in run.stdout
