@@ -119,6 +119,22 @@ int nicgpu_rx_offload(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const ui
                       uint64_t* out_hits, void* stream);
 
 /* Checksum only (== rx_offload with NICGPU_TUPLE_NONE). */
+/* nicgpu_rx_offload plus L3/L4 checksum verification in the same pass
+ * (out_l34[i] = NICGPU_L34_* flags; may be NULL).  The IPv4 header checksum and
+ * the TCP/UDP checksum over pseudo-header || segment are those of the
+ * reference's PacketGenerator::ipv4_checksum / tcp_checksum / udp_checksum
+ * (src/packet_generator.cpp:200-305): a field verifies when the checksum over
+ * the covered bytes, field included, is 0.  Semantics: oracle/oracle.h
+ * (oracle_l34_verify).  tuple_mode NONE with only out_csum/out_l34 is allowed. */
+#define NICGPU_L34_IPV4 0x01u       /* IPv4 header parsed (Eth + <= 2 tags) */
+#define NICGPU_L34_IPV4_OK 0x02u    /* its header checksum verifies */
+#define NICGPU_L34_L4 0x04u         /* TCP/UDP, unfragmented, datagram within the frame */
+#define NICGPU_L34_L4_OK 0x08u      /* L4 checksum verifies (or UDP carries none) */
+#define NICGPU_L34_UDP_NOCSUM 0x10u /* UDP checksum field 0: not verified */
+int nicgpu_rx_offload_ex(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n,
+                         int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum, uint32_t* out_hash,
+                         uint16_t* out_queue, uint64_t* out_hits, uint8_t* out_l34, void* stream);
+
 int nicgpu_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n,
                           uint16_t* out_csum, void* stream);
 

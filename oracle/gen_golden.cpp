@@ -830,6 +830,88 @@ void gen_qp_batch() {
   gen_qp_batch_case("qp_mix_b", 202, 400, 700, 0);    // ample RX descriptors
   gen_qp_batch_case("qp_tso", 303, 40, 300, 1);       // 9000 B TSO/GSO, odd mss, tiny headers
 }
+
+// ------------------------------------------------------ L3/L4 verification --
+// SURVEY §8 f3.  Frames from build_frame (valid IPv4 header and TCP/UDP
+// checksums), then mutated.  Expected flags use the reference's own
+// compute_checksum (src/checksum.cpp:10-34), which is the same algorithm as
+// PacketGenerator::ipv4_checksum / tcp_checksum / udp_checksum
+// (packet_generator.cpp:200-305, not buildable here: bit_fields): a valid IPv4
+// header has compute_checksum(header) == 0, a valid L4 segment
+// compute_checksum(pseudo-header || segment) == 0.
+std::uint8_t ref_l34(const std::vector<std::uint8_t>& f) {
+  const std::size_t len = f.size();
+  if (len < 14) return 0;
+  std::size_t l3 = 14;
+  unsigned et = (f[12] << 8) | f[13];
+  for (int t = 0; t < 2 && (et == 0x8100 || et == 0x88A8); ++t) {
+    if (len < l3 + 4) return 0;
+    et = (f[l3 + 2] << 8) | f[l3 + 3];
+    l3 += 4;
+  }
+  if (et != 0x0800 || len < l3 + 20 || (f[l3] >> 4) != 4) return 0;
+  const std::size_t ihl = (f[l3] & 15u) * 4u;
+  if (ihl < 20 || l3 + ihl > len) return 0;
+  std::uint8_t fl = ORACLE_L34_IPV4;
+  if (ref_csum(&f[l3], ihl) == 0) fl |= ORACLE_L34_IPV4_OK;
+  const unsigned proto = f[l3 + 9];
+  const unsigned frag = ((f[l3 + 6] << 8) | f[l3 + 7]) & 0x3FFFu;
+  const std::size_t total = (f[l3 + 2] << 8) | f[l3 + 3];
+  if ((proto != 6 && proto != 17) || frag != 0 || total < ihl || l3 + total > len) return fl;
+  const std::size_t seg = total - ihl;
+  if (seg < (proto == 6 ? 20u : 8u)) return fl;
+  fl |= ORACLE_L34_L4;
+  const std::size_t l4 = l3 + ihl;
+  if (proto == 17 && f[l4 + 6] == 0 && f[l4 + 7] == 0) return fl | ORACLE_L34_L4_OK | ORACLE_L34_UDP_NOCSUM;
+  std::vector<std::uint8_t> ps(12 + seg);
+  std::memcpy(ps.data(), &f[l3 + 12], 8);
+  ps[8] = 0;
+  ps[9] = static_cast<std::uint8_t>(proto);
+  ps[10] = static_cast<std::uint8_t>(seg >> 8);
+  ps[11] = static_cast<std::uint8_t>(seg);
+  std::memcpy(ps.data() + 12, &f[l4], seg);
+  if (ref_csum(ps.data(), ps.size()) == 0) fl |= ORACLE_L34_L4_OK;
+  return fl;
+}
+
+void gen_l34() {
+  Rng r{3434};
+  std::vector<std::uint8_t> frames, flags;
+  std::vector<std::uint64_t> desc;
+  const std::size_t sizes[] = {60, 64, 66, 77, 128, 576, 1000, 1514, 1518, 4001, 9000};
+  for (int i = 0; i < 3000; ++i) {
+    FrameSpec s;
+    const std::uint32_t k = r.below(20);
+    s.l3 = k == 0 ? 6 : (k == 1 ? 0 : 4);
+    s.proto = r.below(10) == 0 ? 1 : (r.below(2) ? 6 : 17);
+    s.vlan_tags = r.below(8) == 0 ? 1 + r.below(2) : 0;
+    s.ihl = r.below(6) == 0 ? 6 + r.below(10) : 5;
+    s.frag = r.below(15) == 0;
+    s.total = sizes[r.below(11)] + (r.below(3) == 0 ? r.below(9) : 0);
+    s.balance = r.below(2);
+    auto f = build_frame(r, s);
+    const std::size_t l3 = 14 + 4 * s.vlan_tags;
+    const std::uint32_t m = r.below(16);
+    if (m == 0 && f.size() > 60) f[40 + r.below(static_cast<std::uint32_t>(f.size() - 40))] ^= 1 + r.below(255);  // payload bit error
+    else if (m == 1 && f.size() >= l3 + 20) f[l3 + r.below(20)] ^= 1 + r.below(255);                           // IP header error
+    else if (m == 2 && f.size() >= l3 + 28 && s.proto == 17) { f[l3 + s.ihl * 4 + 6] = 0; f[l3 + s.ihl * 4 + 7] = 0; }  // UDP no checksum
+    else if (m == 3) for (std::uint32_t p = 1 + r.below(30); p--;) f.push_back(r.byte());                       // Ethernet padding / trailer
+    else if (m == 4 && f.size() >= l3 + 4) { f[l3 + 3] = static_cast<std::uint8_t>(f[l3 + 3] + 1 + r.below(4)); }  // total length past the frame
+    else if (m == 5 && f.size() >= l3 + 4) { f[l3 + 2] = 0; f[l3 + 3] = static_cast<std::uint8_t>(r.below(20)); }  // total < IHL
+    else if (m == 6 && f.size() >= l3 + 1) f[l3] = static_cast<std::uint8_t>((f[l3] & 0xF0) | r.below(5));       // IHL < 5
+    else if (m == 7) f.resize(r.below(static_cast<std::uint32_t>(f.size()) + 1));                               // truncation
+    // frames at any byte offset
+    const std::size_t gap = r.below(4) == 0 ? r.below(16) : (16 - frames.size() % 16) % 16;
+    for (std::size_t g = 0; g < gap; ++g) frames.push_back(r.byte());
+    desc.push_back(frames.size() | (static_cast<std::uint64_t>(f.size()) << 40));
+    frames.insert(frames.end(), f.begin(), f.end());
+    flags.push_back(ref_l34(f));
+  }
+  frames.resize(frames.size() + 64, 0);
+  write_bin("l34.frames.bin", frames);
+  write_bin("l34.desc.bin", desc);
+  write_bin("l34.flags.bin", flags);
+}
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -849,6 +931,7 @@ int main(int argc, char** argv) {
   gen_c1();
   gen_tso();
   gen_qp_batch();
+  gen_l34();
   std::printf("golden fixtures written to %s\n", g_out.c_str());
   return 0;
 }

@@ -193,3 +193,41 @@ int oracle_tso_segment_checksums(const uint8_t* pkt, size_t len, uint16_t hdr_le
   free(buf);
   return (int) k;
 }
+
+/* internet_checksum / ipv4_checksum (packet_generator.cpp:200-202, 342-360):
+ * big-endian word sum, odd byte as a high byte, folded, complemented. */
+static uint16_t inet_csum(uint32_t sum, const uint8_t* p, size_t n) {
+  for (size_t i = 0; i < n; i += 2) sum += ((uint32_t) p[i] << 8) | (i + 1 < n ? p[i + 1] : 0u);
+  while (sum >> 16) sum = (sum & 0xFFFFu) + (sum >> 16);
+  return (uint16_t) ~sum;
+}
+
+uint8_t oracle_l34_verify(const uint8_t* f, size_t len) {
+  if (len < 14) return 0;
+  size_t l3 = 14;
+  unsigned et = be16(f + 12);
+  for (int tags = 0; tags < 2 && (et == 0x8100u || et == 0x88A8u); ++tags) {
+    if (len < l3 + 4) return 0;
+    et = be16(f + l3 + 2);
+    l3 += 4;
+  }
+  if (et != 0x0800u || len < l3 + 20 || (f[l3] >> 4) != 4) return 0;
+  const size_t ihl = (size_t) (f[l3] & 15u) * 4;
+  if (ihl < 20 || l3 + ihl > len) return 0;
+  uint8_t flags = ORACLE_L34_IPV4;
+  if (inet_csum(0, f + l3, ihl) == 0) flags |= ORACLE_L34_IPV4_OK;
+  const unsigned proto = f[l3 + 9];
+  const unsigned frag = be16(f + l3 + 6) & 0x3FFFu;
+  const size_t total = be16(f + l3 + 2);
+  if ((proto != 6u && proto != 17u) || frag != 0 || total < ihl || l3 + total > len) return flags;
+  const size_t seg = total - ihl;
+  if (seg < (proto == 6u ? 20u : 8u)) return flags;
+  flags |= ORACLE_L34_L4;
+  const uint8_t* l4 = f + l3 + ihl;
+  if (proto == 17u && be16(l4 + 6) == 0) return flags | ORACLE_L34_L4_OK | ORACLE_L34_UDP_NOCSUM;
+  /* pseudo-header: src_ip, dst_ip, zero, protocol, L4 length (tcp_checksum :208-225) */
+  uint32_t sum = be16(f + l3 + 12) + be16(f + l3 + 14) + be16(f + l3 + 16) + be16(f + l3 + 18) + proto +
+                 (uint32_t) (seg & 0xFFFFu);
+  if (inet_csum(sum, l4, seg) == 0) flags |= ORACLE_L34_L4_OK;
+  return flags;
+}

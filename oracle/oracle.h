@@ -68,6 +68,30 @@ void oracle_rx_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int 
 int oracle_tso_segment_checksums(const uint8_t* pkt, size_t len, uint16_t hdr_len, uint16_t mss,
                                  int segmentation_enabled, uint16_t* out, size_t max_out);
 
+/* L3/L4 checksum verification of one frame.  Flags:
+ *   ORACLE_L34_IPV4     Ethernet (+ <= 2 0x8100/0x88A8 tags), ethertype 0x0800,
+ *                       version 4, IHL >= 5 and the whole IP header in the frame
+ *   ORACLE_L34_IPV4_OK  ... and ipv4_checksum(header) == 0
+ *                       (packet_generator.cpp:200-202, validation_test.cpp:73-76)
+ *   ORACLE_L34_L4       ... and protocol TCP/UDP, not a fragment (MF = 0,
+ *                       offset = 0), IHL*4 <= total_length, the IP datagram
+ *                       within the frame, and the L4 header present (TCP 20 B,
+ *                       UDP 8 B)
+ *   ORACLE_L34_L4_OK    ... and the checksum over pseudo-header (src, dst, 0,
+ *                       proto, L4 length) || L4 segment is 0
+ *                       (tcp_checksum / udp_checksum, packet_generator.cpp:204-305);
+ *                       a UDP checksum field of 0 means "no checksum" (:303-304)
+ *                       and counts as OK
+ *   ORACLE_L34_UDP_NOCSUM  UDP with a zero checksum field.
+ * The L4 segment ends at the IP total length: bytes after it (Ethernet
+ * padding, trailers) are not part of it. */
+#define ORACLE_L34_IPV4 0x01u
+#define ORACLE_L34_IPV4_OK 0x02u
+#define ORACLE_L34_L4 0x04u
+#define ORACLE_L34_L4_OK 0x08u
+#define ORACLE_L34_UDP_NOCSUM 0x10u
+uint8_t oracle_l34_verify(const uint8_t* frame, size_t len);
+
 #ifdef __cplusplus
 }
 #endif

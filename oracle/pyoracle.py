@@ -51,6 +51,8 @@ def lib():
         L.oracle_rx_batch.argtypes = [vp, vp, sz, i32, sz, sz, vp, sz, vp, sz, vp, vp, vp, vp, vp]
         L.oracle_tso_segment_checksums.restype = i32
         L.oracle_tso_segment_checksums.argtypes = [vp, sz, u16, u16, i32, vp, sz]
+        L.oracle_l34_verify.restype = ctypes.c_uint8
+        L.oracle_l34_verify.argtypes = [vp, sz]
         _o = L
     return _o
 
@@ -130,3 +132,15 @@ def tso_segment_checksums(pkt: bytes, hdr_len: int, mss: int, enabled=True):
     out = np.zeros(128, np.uint16)
     r = lib().oracle_tso_segment_checksums(_vp(p), len(pkt), hdr_len, mss, int(enabled), _vp(out), 128)
     return r, out[: max(r, 0)].copy()
+
+
+def l34_batch(frames: np.ndarray, desc: np.ndarray) -> np.ndarray:
+    """oracle_l34_verify for every descriptor."""
+    L = lib()
+    frames = np.ascontiguousarray(frames, np.uint8)
+    base = frames.ctypes.data
+    out = np.empty(desc.size, np.uint8)
+    for i, d in enumerate(desc.tolist()):
+        off, ln = d & ((1 << 40) - 1), d >> 40
+        out[i] = L.oracle_l34_verify(ctypes.c_void_p(base + off), ln)
+    return out

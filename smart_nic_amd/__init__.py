@@ -27,6 +27,12 @@ ERR_NOMEM = -4
 TUPLE_NONE = 0
 TUPLE_AUTO = 1
 TUPLE_RAW = 2
+# L3/L4 verification flags (include/nicgpu.h NICGPU_L34_*)
+L34_IPV4 = 0x01
+L34_IPV4_OK = 0x02
+L34_L4 = 0x04
+L34_L4_OK = 0x08
+L34_UDP_NOCSUM = 0x10
 RAW_MAX_END = 64
 MAX_PACKET = 65535
 DESC_OFFSET_BITS = 40
@@ -51,6 +57,7 @@ ABI_SYMBOLS = (
     "nicgpu_rss_set_table_device",
     "nicgpu_rss_info",
     "nicgpu_rx_offload",
+    "nicgpu_rx_offload_ex",
     "nicgpu_checksum_batch",
     "nicgpu_tso_checksum",
     "nicgpu_segment_gather",
@@ -86,6 +93,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_rss_set_table_device": (i32, [vp, vp, sz, vp]),
         "nicgpu_rss_info": (i32, [vp, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
         "nicgpu_rx_offload": (i32, [vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp]),
+        "nicgpu_rx_offload_ex": (i32, [vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp, vp]),
+        "nicgpu_segment_gather": (i32, [vp, ctypes.c_uint64, vp, sz, vp]),
         "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),
         "nicgpu_tso_checksum": (i32, [vp, vp, vp, vp, vp, sz, vp, vp]),
     }
@@ -199,17 +208,30 @@ class RssContext:
 
 
 def rx_offload(ctx, frames, desc, mode=TUPLE_AUTO, raw_off=0, raw_len=0, csum=None,
-               hash_out=None, queue=None, hits=None, stream=None):
-    """Launch the fused RX checksum + RSS kernel on torch device tensors."""
+               hash_out=None, queue=None, hits=None, stream=None, l34=None):
+    """Launch the fused RX checksum + RSS kernel on torch device tensors.
+
+    l34 (uint8[n], optional): NICGPU_L34_* flags of the L3/L4 checksum
+    verification done in the same pass (nicgpu_rx_offload_ex)."""
     lib = load_library()
     n = desc.numel()
+    if l34 is None:
+        _check(
+            lib.nicgpu_rx_offload(
+                ctx.handle if ctx is not None else None,
+                _ptr(frames), _ptr(desc), n, mode, raw_off, raw_len,
+                _ptr(csum), _ptr(hash_out), _ptr(queue), _ptr(hits), _stream_ptr(stream),
+            ),
+            "nicgpu_rx_offload",
+        )
+        return
     _check(
-        lib.nicgpu_rx_offload(
+        lib.nicgpu_rx_offload_ex(
             ctx.handle if ctx is not None else None,
             _ptr(frames), _ptr(desc), n, mode, raw_off, raw_len,
-            _ptr(csum), _ptr(hash_out), _ptr(queue), _ptr(hits), _stream_ptr(stream),
+            _ptr(csum), _ptr(hash_out), _ptr(queue), _ptr(hits), _ptr(l34), _stream_ptr(stream),
         ),
-        "nicgpu_rx_offload",
+        "nicgpu_rx_offload_ex",
     )
 
 

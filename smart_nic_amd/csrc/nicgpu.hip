@@ -153,6 +153,7 @@ struct RxParams {
   uint32_t* out_hash;
   uint16_t* out_queue;
   unsigned long long* out_hits;
+  uint8_t* out_l34;  // NICGPU_L34_* flags (L3/L4 checksum verification), may be null
 };
 
 // Dynamic LDS layout (sized per launch by rx_lds_bytes):
@@ -211,6 +212,78 @@ __device__ __forceinline__ uint32_t hash_bytes(uint32_t h, const uint32_t* lut, 
     h ^= lut[p * 16 + (b >> 4)] ^ lut[(p + 1) * 16 + (b & 15)];
   }
   return h;
+}
+
+// Sum of the little-endian halfwords at absolute (even-address-low) positions
+// of packet bytes [a, b), from 4-byte words: word k of the packet's 16-B-aligned
+// window comes from the LDS header stage (k < 16) or from global memory.  The
+// same convention as the streamed chunk sums, so sub-range sums subtract
+// exactly from the packet's total.
+__device__ __forceinline__ uint32_t range_sum_le(const uint32_t* stage_w, const uint32_t* __restrict__ glob_w,
+                                                 uint32_t lo, uint32_t a, uint32_t b) {
+  uint32_t s = 0;
+  if (a >= b) return 0;
+  const uint32_t pa = lo + a, pb = lo + b;
+  for (uint32_t k = pa >> 2; 4 * k < pb; ++k) {
+    uint32_t v = k < (uint32_t) (kHdrBytes / 4) ? stage_w[k] : glob_w[k];
+    const uint32_t w0 = 4 * k;
+    const uint32_t first = pa > w0 ? pa - w0 : 0u;      // bytes of this word before the range
+    const uint32_t last = pb < w0 + 4 ? pb - w0 : 4u;   // bytes of this word inside the range end
+    const uint32_t keep = (last == 4u ? 0xFFFFFFFFu : ((1u << (8 * last)) - 1u)) & (0xFFFFFFFFu << (8 * first));
+    v &= keep;
+    s += (v & 0xFFFFu) + (v >> 16);
+  }
+  return s;
+}
+
+// L3/L4 checksum verification of one packet (oracle/oracle.c
+// oracle_l34_verify; reference packet_generator.cpp:200-305).  `sum_le` is the
+// packet's streamed halfword sum; the L4 segment's sum is that minus the bytes
+// before the segment and after the IP datagram, so no byte is read twice
+// except the <= 82 header bytes (from the LDS stage) and any trailer.
+__device__ uint32_t l34_flags(const uint32_t* stage_w, const uint32_t* __restrict__ glob_w, uint32_t lo, uint32_t len,
+                              uint32_t sum_le) {
+  const uint8_t* stage_b = reinterpret_cast<const uint8_t*>(stage_w);
+  const uint8_t* glob_b = reinterpret_cast<const uint8_t*>(glob_w);
+  auto B = [&](uint32_t o) -> uint32_t {
+    const uint32_t a = lo + o;
+    return a < (uint32_t) kHdrBytes ? stage_b[a] : glob_b[a];
+  };
+  if (len < 14u) return 0;
+  uint32_t l3 = 14;
+  uint32_t et = (B(12) << 8) | B(13);
+  for (int t = 0; t < 2 && (et == 0x8100u || et == 0x88A8u); ++t) {
+    if (len < l3 + 4u) return 0;
+    et = (B(l3 + 2) << 8) | B(l3 + 3);
+    l3 += 4;
+  }
+  if (et != 0x0800u || len < l3 + 20u) return 0;
+  const uint32_t v0 = B(l3);
+  if ((v0 >> 4) != 4u) return 0;
+  const uint32_t ihl = (v0 & 15u) * 4u;
+  if (ihl < 20u || l3 + ihl > len) return 0;
+  const uint32_t odd = lo & 1u;  // absolute parity of the packet start (frames are 16-B aligned)
+  uint32_t flags = NICGPU_L34_IPV4;
+  // IPv4 header (starts at an even packet offset): big-endian sum = swap of the
+  // absolute little-endian sum unless the packet starts at an odd address
+  const uint32_t ipx = fold16(range_sum_le(stage_w, glob_w, lo, l3, l3 + ihl));
+  if ((odd ? ipx : bswap16(ipx)) == 0xFFFFu) flags |= NICGPU_L34_IPV4_OK;
+  const uint32_t proto = B(l3 + 9);
+  const uint32_t frag = ((B(l3 + 6) << 8) | B(l3 + 7)) & 0x3FFFu;
+  const uint32_t total = (B(l3 + 2) << 8) | B(l3 + 3);
+  if ((proto != 6u && proto != 17u) || frag != 0u || total < ihl || l3 + total > len) return flags;
+  const uint32_t seg = total - ihl;
+  if (seg < (proto == 6u ? 20u : 8u)) return flags;
+  flags |= NICGPU_L34_L4;
+  const uint32_t l4 = l3 + ihl;
+  if (proto == 17u && B(l4 + 6) == 0u && B(l4 + 7) == 0u) return flags | NICGPU_L34_L4_OK | NICGPU_L34_UDP_NOCSUM;
+  const uint32_t seg_le = sum_le - range_sum_le(stage_w, glob_w, lo, 0, l4) - range_sum_le(stage_w, glob_w, lo, l3 + total, len);
+  const uint32_t sx = fold16(seg_le);
+  const uint32_t seg_be = ((l4 + odd) & 1u) ? sx : bswap16(sx);
+  uint32_t acc = seg_be + proto + seg;  // pseudo-header: src, dst, zero, protocol, L4 length
+  for (uint32_t o = l3 + 12; o < l3 + 20; o += 2) acc += (B(o) << 8) | B(o + 1);
+  if (fold16(acc) == 0xFFFFu) flags |= NICGPU_L34_L4_OK;
+  return flags;
 }
 
 // Tuple extraction + Toeplitz for one packet (oracle/oracle.c oracle_extract_tuple).
@@ -498,6 +571,7 @@ struct RxLdsPtrs {
   uint32_t* hist;
   uint16_t* table_s;
   bool hist_lds, table_lds, want_rss;
+  bool stage;  // first 64 B of every packet staged in LDS (hashing or L3/L4 verify)
 };
 
 // Checksum finish + tuple hash + queue of the tile's packets (one per lane).
@@ -520,6 +594,10 @@ __device__ __forceinline__ void tile_epilogue(const RxParams& P, const RxLdsPtrs
     // packet starts at an even address (RFC 1071 byte-order independence).
     const uint32_t be = (t.off & 1) ? x : bswap16(x);
     if (P.out_csum) P.out_csum[pid] = (uint16_t) (~be & 0xFFFFu);
+    if (P.out_l34)
+      P.out_l34[pid] = (uint8_t) l34_flags(reinterpret_cast<const uint32_t*>(L.hdr + lane * kHdrChunks),
+                                           reinterpret_cast<const uint32_t*>(P.frames + (t.off & ~15ull)),
+                                           (uint32_t) (t.off & 15), t.len, sum);
     if (L.want_rss) {
       const uint32_t h =
           rss_hash_packet(P, L.lut, L.hdr + lane * kHdrChunks, (uint32_t) (t.off & 15), P.frames + t.off, t.len);
@@ -552,11 +630,11 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
   for (;;) {
     plan_batch<U, NT>(B, L.pk, L.marks, b0 + kStep, t.total, lane, t.start, t.nch, ++tag, carry, P.frames);
     __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's wait
-    run = process_batch<U>(A, run, L.S, L.E, L.hdr, L.want_rss);
+    run = process_batch<U>(A, run, L.S, L.E, L.hdr, L.stage);
     if (b0 + kStep >= t.total) break;
     plan_batch<U, NT>(A, L.pk, L.marks, b0 + 2 * kStep, t.total, lane, t.start, t.nch, ++tag, carry, P.frames);
     __builtin_amdgcn_sched_barrier(0);
-    run = process_batch<U>(B, run, L.S, L.E, L.hdr, L.want_rss);
+    run = process_batch<U>(B, run, L.S, L.E, L.hdr, L.stage);
     b0 += 2 * kStep;
     if (b0 >= t.total) break;
   }
@@ -571,10 +649,11 @@ __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
 
   RxLdsPtrs L;
   L.want_rss = P.mode != NICGPU_TUPLE_NONE;
+  L.stage = L.want_rss || P.out_l34 != nullptr;
   L.hist_lds = P.out_hits != nullptr && P.table_n <= (uint32_t) kHistLds;
   L.table_lds = L.want_rss && P.table_n <= (uint32_t) kTableLds;
   uint8_t* base_b = reinterpret_cast<uint8_t*>(lds_dyn);
-  uint8_t* wave_b = base_b + (uint32_t) w * rx_wave_lds(L.want_rss, U);
+  uint8_t* wave_b = base_b + (uint32_t) w * rx_wave_lds(L.stage, U);
   L.S = reinterpret_cast<uint32_t*>(wave_b);
   L.E = L.S + kWave;
   L.pk = reinterpret_cast<uint4*>(wave_b + kScratchOff);
@@ -582,7 +661,7 @@ __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
   L.slotsA = reinterpret_cast<uint32_t*>(wave_b + kScratchOff);
   L.slotsB = L.slotsA + kWave * U;
   L.hdr = reinterpret_cast<uint4*>(wave_b + rx_hdr_off(U));
-  L.lut = reinterpret_cast<uint32_t*>(base_b + (uint32_t) WPB * rx_wave_lds(L.want_rss, U));
+  L.lut = reinterpret_cast<uint32_t*>(base_b + (uint32_t) WPB * rx_wave_lds(L.stage, U));
   L.hist = L.lut + P.lut_words;
   L.table_s = reinterpret_cast<uint16_t*>(L.hist + (L.hist_lds ? P.table_n : 0u));
   // marks never match a live tag (tags start at 1; cleared slots read as 0)
@@ -625,11 +704,11 @@ __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
       for (;;) {
         plan_contig<U, NT>(B, L.slotsB, b0 + kStep, cur.total, lane, cur.start, cur.nch, cur.info, tile16);
         __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's wait
-        run = process_contig<U>(A, L.slotsA, run, L.E, L.hdr, L.want_rss, lane);
+        run = process_contig<U>(A, L.slotsA, run, L.E, L.hdr, L.stage, lane);
         if (b0 + kStep >= cur.total) break;
         plan_contig<U, NT>(A, L.slotsA, b0 + 2 * kStep, cur.total, lane, cur.start, cur.nch, cur.info, tile16);
         __builtin_amdgcn_sched_barrier(0);
-        run = process_contig<U>(B, L.slotsB, run, L.E, L.hdr, L.want_rss, lane);
+        run = process_contig<U>(B, L.slotsB, run, L.E, L.hdr, L.stage, lane);
         b0 += 2 * kStep;
         if (b0 >= cur.total) break;
       }
@@ -756,6 +835,7 @@ __global__ __launch_bounds__(kWave * WPB) void rx_block_kernel(RxParams P) {
 
   RxLdsPtrs L;
   L.want_rss = P.mode != NICGPU_TUPLE_NONE;
+  L.stage = L.want_rss || P.out_l34 != nullptr;
   L.hist_lds = P.out_hits != nullptr && P.table_n <= (uint32_t) kHistLds;
   L.table_lds = L.want_rss && P.table_n <= (uint32_t) kTableLds;
   uint8_t* b = reinterpret_cast<uint8_t*>(lds_dyn);
@@ -763,7 +843,7 @@ __global__ __launch_bounds__(kWave * WPB) void rx_block_kernel(RxParams P) {
   L.E = L.S + kWave;
   uint8_t* p = b + kWave * 8;
   L.hdr = reinterpret_cast<uint4*>(p);
-  p += L.want_rss ? kWave * kHdrChunks * 16 : 0;
+  p += L.stage ? kWave * kHdrChunks * 16 : 0;
   // scratch: block path = 2 slot windows + 2 x (U x WPB) step totals; general path = per-wave pk + marks
   L.slotsA = reinterpret_cast<uint32_t*>(p);
   L.slotsB = L.slotsA + kWin;
@@ -812,11 +892,11 @@ __global__ __launch_bounds__(kWave * WPB) void rx_block_kernel(RxParams P) {
       for (;;) {
         plan_block<U, WPB, NT>(B, L.slotsB, b0 + kWin, t.total, w, lane, t, tile16);
         __builtin_amdgcn_sched_barrier(0);
-        run = process_block<U, WPB>(A, L.slotsA, totA, run, L.S, L.E, L.hdr, L.want_rss, w, lane);
+        run = process_block<U, WPB>(A, L.slotsA, totA, run, L.S, L.E, L.hdr, L.stage, w, lane);
         if (b0 + kWin >= t.total) break;
         plan_block<U, WPB, NT>(A, L.slotsA, b0 + 2 * kWin, t.total, w, lane, t, tile16);
         __builtin_amdgcn_sched_barrier(0);
-        run = process_block<U, WPB>(B, L.slotsB, totB, run, L.S, L.E, L.hdr, L.want_rss, w, lane);
+        run = process_block<U, WPB>(B, L.slotsB, totB, run, L.S, L.E, L.hdr, L.stage, w, lane);
         b0 += 2 * kWin;
         if (b0 >= t.total) break;
       }
@@ -1136,10 +1216,11 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
   if (variant < 0 || variant >= kNumRxVariants) return NICGPU_ERR_INVALID;
   const RxVariant& v = kRxVariants[variant];
   const bool rss = P.mode != NICGPU_TUPLE_NONE;
+  const bool stage = rss || P.out_l34 != nullptr;
   const uint32_t hist_n = (P.out_hits && P.table_n <= (uint32_t) kHistLds) ? P.table_n : 0u;
   const uint32_t table_words = (rss && P.table_n <= (uint32_t) kTableLds) ? (P.table_n + 1u) / 2u : 0u;
-  const uint32_t lds = (v.block ? rx_block_lds_bytes(v.wpb, v.unroll, rss, rss ? P.lut_words : 0u, hist_n)
-                                : rx_lds_bytes(v.wpb, v.unroll, rss, rss ? P.lut_words : 0u, hist_n)) +
+  const uint32_t lds = (v.block ? rx_block_lds_bytes(v.wpb, v.unroll, stage, rss ? P.lut_words : 0u, hist_n)
+                                : rx_lds_bytes(v.wpb, v.unroll, stage, rss ? P.lut_words : 0u, hist_n)) +
                        table_words * 4u;
   int dev = 0;
   (void) hipGetDevice(&dev);
@@ -1313,7 +1394,7 @@ int nicgpu_rss_info(const nicgpu_rss_ctx* ctx, size_t* key_len, size_t* table_n)
 namespace {
 int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n,
                     int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum, uint32_t* out_hash,
-                    uint16_t* out_queue, uint64_t* out_hits, void* stream) {
+                    uint16_t* out_queue, uint64_t* out_hits, uint8_t* out_l34, void* stream) {
   if (tuple_mode != NICGPU_TUPLE_NONE && tuple_mode != NICGPU_TUPLE_AUTO && tuple_mode != NICGPU_TUPLE_RAW)
     return NICGPU_ERR_INVALID;
   if (tuple_mode == NICGPU_TUPLE_RAW && (raw_off > NICGPU_RAW_MAX_END || raw_len > NICGPU_RAW_MAX_END ||
@@ -1324,7 +1405,7 @@ int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frame
   if (n == 0) return NICGPU_OK;
   if (!frames || !desc) return NICGPU_ERR_INVALID;
   if ((reinterpret_cast<uintptr_t>(frames) & 15u) != 0) return NICGPU_ERR_INVALID;
-  if (!out_csum && !out_hash && !out_queue && !out_hits) return NICGPU_OK;
+  if (!out_csum && !out_hash && !out_queue && !out_hits && !out_l34) return NICGPU_OK;
   const DeviceInfo* di = nullptr;
   int st = current_device_info(&di);
   if (st != NICGPU_OK) return st;
@@ -1344,6 +1425,7 @@ int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frame
   P.out_hash = out_hash;
   P.out_queue = out_queue;
   P.out_hits = reinterpret_cast<unsigned long long*>(out_hits);
+  P.out_l34 = out_l34;
   if (ctx) {
     P.lut = ctx->d_lut;
     P.table = ctx->d_table;
@@ -1361,7 +1443,14 @@ int nicgpu_rx_offload(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const ui
                       int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum,
                       uint32_t* out_hash, uint16_t* out_queue, uint64_t* out_hits, void* stream) {
   return rx_offload_impl(0, ctx, frames, desc, n, tuple_mode, raw_off, raw_len, out_csum, out_hash, out_queue,
-                         out_hits, stream);
+                         out_hits, nullptr, stream);
+}
+
+int nicgpu_rx_offload_ex(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n,
+                         int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum, uint32_t* out_hash,
+                         uint16_t* out_queue, uint64_t* out_hits, uint8_t* out_l34, void* stream) {
+  return rx_offload_impl(0, ctx, frames, desc, n, tuple_mode, raw_off, raw_len, out_csum, out_hash, out_queue,
+                         out_hits, out_l34, stream);
 }
 
 int nicgpu_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n, uint16_t* out_csum, void* stream) {
@@ -1526,7 +1615,7 @@ int nicgpu_tune_rx_offload(int variant, const nicgpu_rss_ctx* ctx, const uint8_t
                            size_t n, int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum,
                            uint32_t* out_hash, uint16_t* out_queue, uint64_t* out_hits, void* stream) {
   return rx_offload_impl(variant, ctx, frames, desc, n, tuple_mode, raw_off, raw_len, out_csum, out_hash,
-                         out_queue, out_hits, stream);
+                         out_queue, out_hits, nullptr, stream);
 }
 // blocks_per_cu 0 = occupancy maximum; unroll in {1, 4, 8}
 int nicgpu_tune_stream_read(const uint8_t* buf, size_t bytes, int blocks_per_cu, int unroll, uint32_t* out,

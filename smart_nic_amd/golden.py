@@ -68,3 +68,12 @@ def c1():
 
 def tso():
     return load_bin("tso.frames.bin", np.uint8), load_json("tso.json")
+
+
+def l34():
+    """L3/L4 verification fixture: frames, desc, expected flags."""
+    return (
+        load_bin("l34.frames.bin", np.uint8),
+        load_bin("l34.desc.bin", np.uint64),
+        load_bin("l34.flags.bin", np.uint8),
+    )

@@ -302,3 +302,55 @@ def test_contiguous_unaligned_layouts_vs_oracle(seed):
     np.testing.assert_array_equal(hits, hits_o)
     cs2, *_ = gpu_rx(frames, desc, mode=sna.TUPLE_NONE)
     np.testing.assert_array_equal(cs2, cs_o)
+
+
+# ------------------------------------------- L3/L4 verification (§8 f3) --
+def gpu_l34(frames, desc, key=None, table=(), mode=sna.TUPLE_NONE):
+    n = desc.size
+    ctx = None
+    if mode != sna.TUPLE_NONE:
+        ctx = sna.RssContext(0)
+        ctx.set_key(key)
+        ctx.set_table(table)
+    f = dev(np.concatenate([frames, np.zeros(64, np.uint8)]))
+    d = dev(desc)
+    cs = torch.empty(n, dtype=torch.int16, device="cuda")
+    fl = torch.empty(n, dtype=torch.uint8, device="cuda")
+    h = q = None
+    if mode != sna.TUPLE_NONE:
+        h = torch.empty(n, dtype=torch.int32, device="cuda")
+        q = torch.empty(n, dtype=torch.int16, device="cuda")
+    sna.rx_offload(ctx, f, d, mode, 0, 0, cs, h, q, None, l34=fl)
+    torch.cuda.synchronize()
+    out = host(cs, np.uint16), host(fl, np.uint8), None if h is None else host(h, np.uint32)
+    if ctx is not None:
+        ctx.close()
+    return out
+
+
+@pytest.mark.parametrize("mode", [sna.TUPLE_NONE, sna.TUPLE_AUTO])
+def test_l34_golden(mode):
+    """Flags pinned by the reference's compute_checksum (tests/golden/l34.*):
+    options, VLAN/QinQ, fragments, padding, truncation, bad lengths, UDP
+    without checksum, frames at every byte offset.  Checksum and RSS outputs
+    of the same launch stay exact."""
+    frames, desc, flags = golden.l34()
+    cs, fl, h = gpu_l34(frames, desc, MS_KEY, np.arange(128) % 4, mode)
+    np.testing.assert_array_equal(fl, flags)
+    cs_o, h_o, *_ = po.rx_batch(frames, desc, MS_KEY, np.arange(128) % 4)
+    np.testing.assert_array_equal(cs, cs_o)
+    if h is not None:
+        np.testing.assert_array_equal(h, h_o)
+
+
+@pytest.mark.parametrize("proto", [6, 17])
+def test_l34_generated_batches_vs_oracle(proto):
+    """IMIX batches with valid L3/L4 checksums and 2 % corrupted frames."""
+    rng = np.random.default_rng(40 + proto)
+    n = 60_000
+    frames, desc, corrupted = pktgen.make_batch(pktgen.imix_lengths(n, rng), seed=proto, proto=proto,
+                                                corrupt_frac=0.02)
+    cs, fl, _ = gpu_l34(frames, desc)
+    np.testing.assert_array_equal(fl, po.l34_batch(frames, desc))
+    ok = sna.L34_IPV4 | sna.L34_IPV4_OK | sna.L34_L4 | sna.L34_L4_OK
+    assert ((fl & ok) == ok)[~corrupted].all()
