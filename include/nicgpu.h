@@ -150,6 +150,20 @@ int nicgpu_tso_checksum(const uint8_t* frames, const uint64_t* desc, const uint1
                         const uint16_t* mss, const uint32_t* seg_base, size_t n,
                         uint16_t* out_csum, void* stream);
 
+/* RoCEv2 ICRC over a batch: nic::rocev2::IcrcCalculator
+ * (include/nic/rocev2/packet.h:195-214, src/rocev2/packet.cpp:14-75), one
+ * call per packet today.  Each descriptor's bytes are the span the reference
+ * is handed (BTH through payload; the reference masks no fields).
+ *   NICGPU_ICRC_CALCULATE: out_crc[i] = calculate(span)   (out_ok must be NULL)
+ *   NICGPU_ICRC_VERIFY:    out_ok[i]  = verify(span): span >= 4 B and the
+ *                          CRC-32C of all but its last 4 bytes equals those
+ *                          bytes read big-endian; out_crc[i] (optional) = that
+ *                          CRC, or 0 for spans shorter than 4 B. */
+#define NICGPU_ICRC_CALCULATE 0
+#define NICGPU_ICRC_VERIFY 1
+int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int mode, uint32_t* out_crc,
+                      uint8_t* out_ok, void* stream);
+
 /* One DMA write of the batched QueuePair stage (nic/rx_stage.h):
  *   mem[dst ..] <- prefix bytes (prefix_len 0 or 4; little-endian word, i.e.
  *                  memory order) || mem[src_a, +len_a) || mem[src_b, +len_b).

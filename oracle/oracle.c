@@ -231,3 +231,31 @@ uint8_t oracle_l34_verify(const uint8_t* f, size_t len) {
   if (inet_csum(sum, l4, seg) == 0) flags |= ORACLE_L34_L4_OK;
   return flags;
 }
+
+/* IcrcCalculator::kCrc32cTable / update_crc / calculate / verify
+ * (src/rocev2/packet.cpp:14-75), restated byte at a time. */
+static uint32_t crc32c_table[256];
+static int crc32c_ready = 0;
+
+static void crc32c_init(void) {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int b = 0; b < 8; ++b) c = (c & 1u) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+    crc32c_table[i] = c;
+  }
+  crc32c_ready = 1;
+}
+
+uint32_t oracle_icrc_calculate(const uint8_t* buf, size_t len) {
+  if (!crc32c_ready) crc32c_init();
+  uint32_t crc = 0xFFFFFFFFu;
+  for (size_t i = 0; i < len; ++i) crc = crc32c_table[(uint8_t) (crc ^ buf[i])] ^ (crc >> 8);
+  return crc ^ 0xFFFFFFFFu;
+}
+
+int oracle_icrc_verify(const uint8_t* buf, size_t len) {
+  if (len < 4) return 0;
+  const uint8_t* t = buf + len - 4;
+  const uint32_t stored = ((uint32_t) t[0] << 24) | ((uint32_t) t[1] << 16) | ((uint32_t) t[2] << 8) | t[3];
+  return oracle_icrc_calculate(buf, len - 4) == stored;
+}

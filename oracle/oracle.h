@@ -92,6 +92,17 @@ int oracle_tso_segment_checksums(const uint8_t* pkt, size_t len, uint16_t hdr_le
 #define ORACLE_L34_UDP_NOCSUM 0x10u
 uint8_t oracle_l34_verify(const uint8_t* frame, size_t len);
 
+/* RoCEv2 ICRC as the reference computes it: nic::rocev2::IcrcCalculator
+ * (src/rocev2/packet.cpp:14-56): CRC-32C, reflected polynomial 0x82F63B78,
+ * table-driven byte at a time, initial value 0xFFFFFFFF, final xor
+ * 0xFFFFFFFF, over the whole span (no field masking).  verify (:58-75): span
+ * >= 4 bytes and calculate(span minus its last 4 bytes) equals those 4 bytes
+ * read big-endian.  The reference TU is not buildable here (it includes
+ * bit_fields); parity is pinned by the published CRC-32C vectors
+ * (tests/golden/icrc_kat.json). */
+uint32_t oracle_icrc_calculate(const uint8_t* buf, size_t len);
+int oracle_icrc_verify(const uint8_t* buf, size_t len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -53,6 +53,10 @@ def lib():
         L.oracle_tso_segment_checksums.argtypes = [vp, sz, u16, u16, i32, vp, sz]
         L.oracle_l34_verify.restype = ctypes.c_uint8
         L.oracle_l34_verify.argtypes = [vp, sz]
+        L.oracle_icrc_calculate.restype = u32
+        L.oracle_icrc_calculate.argtypes = [vp, sz]
+        L.oracle_icrc_verify.restype = i32
+        L.oracle_icrc_verify.argtypes = [vp, sz]
         _o = L
     return _o
 
@@ -144,3 +148,22 @@ def l34_batch(frames: np.ndarray, desc: np.ndarray) -> np.ndarray:
         off, ln = d & ((1 << 40) - 1), d >> 40
         out[i] = L.oracle_l34_verify(ctypes.c_void_p(base + off), ln)
     return out
+
+
+def icrc_batch(frames: np.ndarray, desc: np.ndarray, verify=False):
+    """oracle_icrc_calculate (or _verify) for every descriptor.
+    Returns (crc uint32[n], ok uint8[n] or None); in verify mode crc covers all
+    but the last 4 bytes (0 below 4 bytes)."""
+    L = lib()
+    frames = np.ascontiguousarray(frames, np.uint8)
+    base = frames.ctypes.data
+    crc = np.zeros(desc.size, np.uint32)
+    ok = np.zeros(desc.size, np.uint8) if verify else None
+    for i, d in enumerate(desc.tolist()):
+        off, ln = d & ((1 << 40) - 1), d >> 40
+        if verify:
+            ok[i] = L.oracle_icrc_verify(ctypes.c_void_p(base + off), ln)
+            crc[i] = L.oracle_icrc_calculate(ctypes.c_void_p(base + off), ln - 4) if ln >= 4 else 0
+        else:
+            crc[i] = L.oracle_icrc_calculate(ctypes.c_void_p(base + off), ln)
+    return crc, ok

@@ -61,6 +61,7 @@ ABI_SYMBOLS = (
     "nicgpu_checksum_batch",
     "nicgpu_tso_checksum",
     "nicgpu_segment_gather",
+    "nicgpu_icrc_batch",
 )
 
 _lib = None
@@ -95,6 +96,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_rx_offload": (i32, [vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp]),
         "nicgpu_rx_offload_ex": (i32, [vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp, vp]),
         "nicgpu_segment_gather": (i32, [vp, ctypes.c_uint64, vp, sz, vp]),
+        "nicgpu_icrc_batch": (i32, [vp, vp, sz, i32, vp, vp, vp]),
         "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),
         "nicgpu_tso_checksum": (i32, [vp, vp, vp, vp, vp, sz, vp, vp]),
     }
@@ -233,6 +235,17 @@ def rx_offload(ctx, frames, desc, mode=TUPLE_AUTO, raw_off=0, raw_len=0, csum=No
         ),
         "nicgpu_rx_offload_ex",
     )
+
+
+ICRC_CALCULATE = 0
+ICRC_VERIFY = 1
+
+
+def icrc_batch(frames, desc, mode=ICRC_CALCULATE, crc=None, ok=None, stream=None):
+    """RoCEv2 ICRC (CRC-32C) of every descriptor's span (nicgpu_icrc_batch)."""
+    lib = load_library()
+    _check(lib.nicgpu_icrc_batch(_ptr(frames), _ptr(desc), desc.numel(), mode, _ptr(crc), _ptr(ok),
+                                 _stream_ptr(stream)), "nicgpu_icrc_batch")
 
 
 def checksum_batch(frames, desc, csum, stream=None):

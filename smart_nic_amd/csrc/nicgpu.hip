@@ -1119,6 +1119,166 @@ __global__ __launch_bounds__(kBlock) void segment_gather_kernel(GatherParams P) 
   }
 }
 
+// ------------------------------------------------------------ RoCEv2 ICRC --
+// nic::rocev2::IcrcCalculator::calculate / verify (src/rocev2/packet.cpp:14-75)
+// over a batch: CRC-32C (reflected 0x82F63B78, init/xorout 0xFFFFFFFF) of
+// every descriptor's span.  One lane owns one packet at a time and walks it
+// 64 B per step (4 x 16-B loads, slice-by-16 tables in LDS); a finished lane
+// takes the next packet of its wave's range through a ballot (a wave-level
+// work queue), so IMIX lengths do not leave lanes idle.  Every 16-B chunk,
+// whatever part of it belongs to the packet (head, tail, both, none), goes
+// through one branch-free step: with valid bytes [a, b) and running CRC state
+// S, processing them equals a zero-state slice-by-16 of the chunk after
+//   D ^= S at byte a (the standard "xor the state into the next 4 bytes"),
+//   mask D to [a, b), shift it up so the span ends at byte 15
+// (leading zero bytes do not change a zero state), plus S >> 8(b - a) when
+// the span is shorter than 4 bytes.
+struct Crc32cTables {
+  uint32_t t[16][256];
+};
+constexpr Crc32cTables make_crc32c_tables() {
+  Crc32cTables T{};
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int b = 0; b < 8; ++b) c = (c & 1u) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+    T.t[0][i] = c;
+  }
+  for (int k = 1; k < 16; ++k)
+    for (uint32_t i = 0; i < 256; ++i) T.t[k][i] = (T.t[k - 1][i] >> 8) ^ T.t[0][T.t[k - 1][i] & 0xFFu];
+  return T;
+}
+__constant__ Crc32cTables kCrc32c = make_crc32c_tables();
+
+struct IcrcParams {
+  const uint8_t* frames;
+  const uint64_t* desc;
+  uint64_t n;
+  int verify;
+  uint32_t* out_crc;
+  uint8_t* out_ok;
+};
+
+constexpr int kIcrcRing = 128;  // descriptor ring per wave (LDS)
+
+// 128-bit value (x[0] = bytes 0..3) shifted towards higher byte indices by k bytes (0..16).
+__device__ __forceinline__ void shl_bytes(uint32_t x[4], uint32_t k) {
+  const uint32_t q = k >> 2, r = k & 3u;
+  uint32_t y[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int s0 = j - (int) q, s1 = s0 - 1;
+    const uint32_t a = s0 >= 0 ? x[s0 & 3] : 0u;
+    const uint32_t b = s1 >= 0 ? x[s1 & 3] : 0u;
+    y[j] = r ? __builtin_amdgcn_alignbyte(a, b, 4u - r) : a;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) x[j] = y[j];
+}
+
+// One chunk: bytes [a, b) of the 16-B chunk v processed from state S.
+__device__ __forceinline__ uint32_t crc_chunk(const uint32_t* __restrict__ T, u32x4 v, uint32_t a, uint32_t b,
+                                              uint32_t S) {
+  uint32_t x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t s4[4] = {S, 0u, 0u, 0u};
+  shl_bytes(s4, a);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) x[j] = (x[j] ^ s4[j]) & dword_keep((int) a, (int) b, j);
+  shl_bytes(x, 16u - b);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) c ^= T[(15 - i) * 256 + ((x[i >> 2] >> (8 * (i & 3))) & 0xFFu)];
+  const uint32_t h = b - a;
+  return c ^ (h < 4u ? (h ? S >> (8 * h) : S) : 0u);
+}
+
+__global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
+  __shared__ uint32_t T[16 * 256];
+  __shared__ uint64_t ring_all[kWavesPerBlock][kIcrcRing];
+  for (uint32_t i = threadIdx.x; i < 16u * 256u; i += kBlock) T[i] = (&kCrc32c.t[0][0])[i];
+  __syncthreads();
+  const uint32_t lane = lane_id();
+  uint64_t* ring = ring_all[threadIdx.x / kWave];
+  const uint64_t nwaves = (uint64_t) gridDim.x * kWavesPerBlock;
+  const uint64_t wave = (uint64_t) blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+  // contiguous packet range of this wave
+  const uint64_t per = (P.n + nwaves - 1) / nwaves;
+  const uint64_t p0 = wave * per < P.n ? wave * per : P.n;
+  const uint64_t p1 = p0 + per < P.n ? p0 + per : P.n;
+  const u32x4* f16 = reinterpret_cast<const u32x4*>(P.frames);
+
+  uint64_t loaded = p0;
+  auto refill = [&]() __attribute__((always_inline)) {
+    const uint64_t i = loaded + lane;
+    ring[i & (kIcrcRing - 1)] = i < p1 ? P.desc[i] : 0ull;
+    loaded += kWave;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  };
+  refill();
+  refill();
+  uint64_t next = p0 + kWave;
+  uint64_t my = p0 + lane;
+  uint64_t pos = 0, end = 0, off = 0;
+  uint32_t len = 0, S = 0xFFFFFFFFu;
+  auto setup = [&]() __attribute__((always_inline)) {
+    const uint64_t d = ring[my & (kIcrcRing - 1)];
+    off = d & kOffMask;
+    len = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
+    const uint32_t span = P.verify ? (len >= 4u ? len - 4u : 0u) : len;
+    pos = off;
+    end = off + span;
+    S = 0xFFFFFFFFu;
+  };
+  if (my < p1) setup();
+  for (;;) {
+    const bool active = my < p1;
+    if (__ballot(active) == 0ull) break;
+    if (active) {
+      // 4 chunks per step; loads clamped to the span's last chunk
+      const uint64_t c0 = pos >> 4;
+      const uint64_t clast = end > pos ? (end - 1) >> 4 : c0;
+      u32x4 v[4] = {};
+      if (end > pos) {  // an empty span reads nothing (it may sit at the buffer's end)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint64_t c = c0 + u <= clast ? c0 + u : clast;
+          v[u] = f16[c];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t cb = (c0 + u) << 4;  // chunk base address
+        const uint32_t a = pos > cb ? (uint32_t) (pos - cb) : 0u;
+        const uint32_t b = end > cb ? (end - cb >= 16 ? 16u : (uint32_t) (end - cb)) : 0u;
+        if (b > a) S = crc_chunk(T, v[u], a, b, S);
+      }
+      pos = (c0 + 4) << 4;
+    }
+    const bool finished = active && pos >= end;
+    if (finished) {
+      const uint32_t crc = S ^ 0xFFFFFFFFu;
+      if (P.out_crc) P.out_crc[my] = (P.verify && len < 4u) ? 0u : crc;
+      if (P.verify) {
+        uint32_t ok = 0;
+        if (len >= 4u) {
+          const uint8_t* t = P.frames + end;
+          const uint32_t stored = ((uint32_t) t[0] << 24) | ((uint32_t) t[1] << 16) | ((uint32_t) t[2] << 8) | t[3];
+          ok = stored == crc;
+        }
+        P.out_ok[my] = (uint8_t) ok;
+      }
+    }
+    const uint64_t m = __ballot(finished);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
+    if (finished) my = next + rank;
+    next += (uint64_t) __builtin_popcountll(m);
+    // grabbed entries are in the ring (loaded >= next + 64 before this step);
+    // read them before the refill overwrites the oldest 64 slots
+    if (finished && my < p1) setup();
+    if (next + kWave > loaded && loaded < p1) refill();
+  }
+}
+
 struct DeviceInfo {
   bool init = false;
   int status = 0;
@@ -1471,6 +1631,27 @@ int nicgpu_tso_checksum(const uint8_t* frames, const uint64_t* desc, const uint1
   const uint64_t cap = (uint64_t) di->cus * (uint64_t) di->tso_blocks_per_cu * 2;
   const unsigned grid = (unsigned) (want < cap ? want : cap);
   hipLaunchKernelGGL(tso_checksum_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
+  return hip_status(hipGetLastError());
+}
+
+int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int mode, uint32_t* out_crc,
+                      uint8_t* out_ok, void* stream) {
+  if (mode != NICGPU_ICRC_CALCULATE && mode != NICGPU_ICRC_VERIFY) return NICGPU_ERR_INVALID;
+  if (mode == NICGPU_ICRC_CALCULATE && out_ok) return NICGPU_ERR_INVALID;
+  if (mode == NICGPU_ICRC_VERIFY && !out_ok) return NICGPU_ERR_INVALID;
+  if (n == 0) return NICGPU_OK;
+  if (!frames || !desc) return NICGPU_ERR_INVALID;
+  if ((reinterpret_cast<uintptr_t>(frames) & 15u) != 0) return NICGPU_ERR_INVALID;
+  if (!out_crc && !out_ok) return NICGPU_OK;
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  IcrcParams P{frames, desc, n, mode == NICGPU_ICRC_VERIFY, out_crc, out_ok};
+  // enough waves that each owns ~8 packets; at most 8 blocks per CU
+  const uint64_t want = (n + 8 * kBlock - 1) / (8 * kBlock);
+  const uint64_t cap = (uint64_t) di->cus * 8;
+  const unsigned grid = (unsigned) (want < 1 ? 1 : (want < cap ? want : cap));
+  hipLaunchKernelGGL(icrc_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
   return hip_status(hipGetLastError());
 }
 

@@ -43,3 +43,18 @@ def test_gpu_batch_api(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "gpu_batch_test: ok" in r.stdout
+
+
+def test_icrc_host_cpu(tmp_path):
+    exe = _build(tmp_path, "icrc_test")
+    r = subprocess.run([exe, "cpu"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "icrc_test cpu: ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_icrc_batch_gpu(tmp_path):
+    exe = _build(tmp_path, "icrc_test")
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "icrc_test gpu: ok" in r.stdout
