@@ -126,6 +126,11 @@ struct RxBatchResult {
   std::vector<std::uint16_t> rx_queue;
   /// queues[q] = indices into rx_completions dispatched to RSS queue q.
   std::vector<std::vector<std::uint32_t>> queues;
+  /// Wall time of each phase of process_batch (host clock, GPU phases
+  /// include their stream synchronisation).
+  struct Timings {
+    double plan_us{0}, sums_us{0}, resolve_us{0}, gather_us{0}, rss_us{0};
+  } timings;
 };
 
 /// QueuePair::process_once over a batch (src/queue_pair.cpp:67-460).

@@ -14,6 +14,7 @@
 #include "nic/rx_stage.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -403,8 +404,14 @@ BatchedQueuePair::BatchedQueuePair(BatchedQueuePairConfig config) : config_(std:
 RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                               std::span<const RxDescriptor> rx, void* stream) {
   using namespace rx_stage_detail;
+  using clock = std::chrono::steady_clock;
+  auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
   if (mem.base == nullptr && mem.size != 0) throw GpuError("process_batch: null host-memory image", NICGPU_ERR_INVALID);
+  RxBatchResult out;
+  auto t = clock::now();
   const Plan plan = make_plan(config_, mem.size, tx);
+  out.timings.plan_us = us_since(t);
+  t = clock::now();
   const std::size_t np = plan.pieces.size();
 
   // (2) piece sums on the GPU
@@ -420,13 +427,16 @@ RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::
     check(nicgpu_memcpy_async(csum.data(), d_cs.p, np * 2, stream), "nicgpu_memcpy_async");
     check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
   }
+  out.timings.sums_us = us_since(t);
 
   // (3) the reference's control flow
-  RxBatchResult out;
+  t = clock::now();
   std::vector<SegmentWrite> writes;
   std::vector<std::int64_t> write_of_rx;
   QueuePairStats st = stats_;
   resolve(config_, mem.size, plan, csum, tx, rx, st, out, writes, write_of_rx);
+  out.timings.resolve_us = us_since(t);
+  t = clock::now();
 
   // (4) DMA writes of every segment that reached the RX buffer
   if (!writes.empty()) {
@@ -437,6 +447,8 @@ RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::
           "nicgpu_segment_gather");
     check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
   }
+  out.timings.gather_us = us_since(t);
+  t = clock::now();
 
   // (5) RSS over frames delivered with Success
   const std::size_t nrx = out.rx_completions.size();
@@ -475,6 +487,7 @@ RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::
       for (std::size_t i = 0; i < m; ++i) out.queues[q[i]].push_back(which[i]);
     }
   }
+  out.timings.rss_us = us_since(t);
   stats_ = st;
   return out;
 }

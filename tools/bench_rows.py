@@ -1,0 +1,152 @@
+"""Per-row kernel measurements for SURVEY §8 beyond the headline line of
+bench.py: each row's kernel on its BASELINE/SURVEY configuration, inputs
+resident in HBM, HIP events around every launch on the launch stream.
+
+Rows (SURVEY §8 d configs):
+  rx_c2        nicgpu_rx_offload, C2 = 1 M x 1518 B TCP, MS key, table i%4
+  rx_l34_c2    the same launch plus L3/L4 verification (f3, nicgpu_rx_offload_ex)
+  rx_c3        C3 = 4 M IMIX 64/576/1518 (7:4:1), 16 queues (table i%16)
+  icrc_c2      nicgpu_icrc_batch (f4) over the C2 frames
+  icrc_c3      nicgpu_icrc_batch over the C3 frames
+  tso_c5       nicgpu_tso_checksum, C5 = 131072 x 9000 B, H=54, mss=1448 (7 segments)
+
+Algorithmic bytes per launch (SURVEY §8 d): sum(L) + 16 N for the RX rows (frame
+bytes, 8-B descriptor, 8 B of results); ICRC: sum(L) + 8 N + 4 N; TSO:
+sum(L) + 8 N (desc) + 8 N (hdr_len, mss, seg_base) + 2 nseg (checksums).
+Prints one JSON object per row on stdout.
+
+  python tools/bench_rows.py [--rows rx_c2,icrc_c2] [--steps 20] [--warmup 3]
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+MS_KEY = bytes.fromhex("6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c6a42b73bbeac01fa")
+PEAK_GBS = 8000.0
+
+
+def timed(torch, fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    ms = np.array([a.elapsed_time(b) for a, b in ev])
+    return float(np.median(ms)) * 1e3, float(np.mean(ms)) * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", default="rx_c2,rx_l34_c2,rx_c3,icrc_c2,icrc_c3,tso_c5")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    args = ap.parse_args()
+    rows = args.rows.split(",")
+
+    import torch
+
+    import smart_nic_amd as sna
+    from smart_nic_amd import pktgen
+
+    torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    cache = {}
+
+    def batch(name):
+        if name in cache:
+            return cache[name]
+        t0 = time.time()
+        if name == "c2":
+            n = 1 << 20
+            frames, desc, _ = pktgen.make_batch(np.full(n, 1518), seed=42, proto=6, corrupt_frac=0.01)
+        elif name == "c3":
+            n = 4 << 20
+            lens = pktgen.imix_lengths(n, np.random.default_rng(33))
+            frames, desc, _ = pktgen.make_batch(lens, seed=33, proto=17, corrupt_frac=0.01)
+        else:  # c5
+            n = 131072
+            frames, desc, _ = pktgen.make_batch(np.full(n, 9000), seed=55, proto=6, corrupt_frac=0.0)
+        lens = (desc >> np.uint64(40)).astype(np.int64)
+        f = torch.from_numpy(frames).to(dev)
+        d = torch.from_numpy(desc.view(np.int64)).to(dev)
+        cache[name] = (n, int(lens.sum()), f, d)
+        print(f"# batch {name}: {n} frames, {lens.sum() / 1e9:.2f} GB in {time.time() - t0:.1f}s", file=sys.stderr)
+        return cache[name]
+
+    def rss_ctx(nq):
+        ctx = sna.RssContext(dev)
+        ctx.set_key(MS_KEY)
+        ctx.set_table((np.arange(128) % nq).astype(np.uint16))
+        return ctx
+
+    def report(row, workload, n, frame_bytes, alg_bytes, med_us, mean_us, extra=None):
+        rec = {"row": row, "workload": workload, "packets": n, "frame_bytes": frame_bytes,
+               "alg_bytes_per_launch": alg_bytes, "us_median": round(med_us, 2), "us_mean": round(mean_us, 2),
+               "mpkt_s": round(n / med_us, 2), "frame_GBps": round(frame_bytes / med_us / 1e3, 1),
+               "alg_GBps": round(alg_bytes / med_us / 1e3, 1),
+               "roofline_frac": round(alg_bytes / med_us / 1e3 / PEAK_GBS, 4)}
+        if extra:
+            rec.update(extra)
+        print(json.dumps(rec), flush=True)
+
+    for row in rows:
+        if row in ("rx_c2", "rx_l34_c2", "rx_c3"):
+            wl = "c3" if row == "rx_c3" else "c2"
+            n, fb, f, d = batch(wl)
+            ctx = rss_ctx(16 if wl == "c3" else 4)
+            cs = torch.empty(n, dtype=torch.int16, device=dev)
+            hs = torch.empty(n, dtype=torch.int32, device=dev)
+            qs = torch.empty(n, dtype=torch.int16, device=dev)
+            hits = torch.zeros(128, dtype=torch.int64, device=dev)
+            l34 = torch.empty(n, dtype=torch.uint8, device=dev) if row == "rx_l34_c2" else None
+
+            def fn():
+                sna.rx_offload(ctx, f, d, sna.TUPLE_AUTO, 0, 0, cs, hs, qs, hits, l34=l34)
+
+            med, mean = timed(torch, fn, args.steps, args.warmup)
+            alg = fb + 16 * n + (n if l34 is not None else 0)
+            report(row, wl, n, fb, alg, med, mean)
+            ctx.close()
+        elif row in ("icrc_c2", "icrc_c3"):
+            wl = row.split("_")[1]
+            n, fb, f, d = batch(wl)
+            crc = torch.empty(n, dtype=torch.int32, device=dev)
+
+            def fn():
+                sna.icrc_batch(f, d, sna.ICRC_CALCULATE, crc)
+
+            med, mean = timed(torch, fn, args.steps, args.warmup)
+            report(row, wl, n, fb, fb + 12 * n, med, mean)
+        elif row == "tso_c5":
+            n, fb, f, d = batch("c5")
+            H, MSS = 54, 1448
+            nseg = (9000 - H + MSS - 1) // MSS
+            hdr = torch.full((n,), H, dtype=torch.int16, device=dev)
+            mss = torch.full((n,), MSS, dtype=torch.int16, device=dev)
+            base = torch.arange(0, n * nseg, nseg, dtype=torch.int32, device=dev)
+            out = torch.empty(n * nseg, dtype=torch.int16, device=dev)
+
+            def fn():
+                sna.tso_checksum(f, d, hdr, mss, base, out)
+
+            med, mean = timed(torch, fn, args.steps, args.warmup)
+            report(row, "c5", n, fb, fb + 16 * n + 2 * n * nseg, med, mean, {"segments": n * nseg})
+        else:
+            raise SystemExit(f"unknown row {row}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+// bench_rx_stage.cpp — nic::BatchedQueuePair throughput.
+//
+//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps>
+//
+// c3: IMIX 64/576/1518 (7:4:1) frames, each balanced so the whole-frame
+//     checksum verifies; RX descriptors with Layer4 checksum offload, 2 KiB
+//     buffers; RSS over the delivered frames (MS key, table i%16).
+// c5: 9000-B frames with TSO (H = 54, mss = 1448 -> 7 segments), RX verify on:
+//     random payloads fail on the first segment, so the batch exercises the
+//     reference's first-failure abort (queue_pair.cpp:361-364).
+// Host memory image and descriptors are prepared once; each rep runs
+// process_batch on the same batch (the RX buffers are rewritten).  Prints one
+// JSON line: packets/s, frame bytes/s and the per-phase split.
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "nic/rss.h"
+#include "nic/rx_stage.h"
+#include "nicgpu.h"
+
+using namespace nic;
+
+namespace {
+
+std::uint16_t csum(const std::uint8_t* p, std::size_t n) {
+  std::uint64_t s = 0;
+  for (std::size_t i = 0; i + 1 < n; i += 2) s += (std::uint32_t{p[i]} << 8) | p[i + 1];
+  if (n & 1) s += std::uint32_t{p[n - 1]} << 8;
+  while (s >> 16) s = (s & 0xFFFF) + (s >> 16);
+  return static_cast<std::uint16_t>(~s);
+}
+
+void check(int st, const char* what) {
+  if (st != NICGPU_OK) {
+    std::fprintf(stderr, "%s: %s\n", what, nicgpu_strerror(st));
+    std::exit(1);
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const std::string wl = argc > 1 ? argv[1] : "c3";
+  const std::size_t n = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1u << 18);
+  const int reps = argc > 3 ? std::atoi(argv[3]) : 5;
+  std::mt19937_64 rng(7);
+  std::vector<std::size_t> lens(n);
+  for (auto& L : lens) {
+    if (wl == "c5") L = 9000;
+    else {
+      const auto r = rng() % 12;
+      L = r < 7 ? 64 : (r < 11 ? 576 : 1518);
+    }
+  }
+  std::size_t tx_bytes = 0;
+  for (auto L : lens) tx_bytes += (L + 15) & ~std::size_t{15};
+  const std::size_t rx_buf = wl == "c5" ? 1600 : 2048;
+  const std::size_t segs = wl == "c5" ? 7 : 1;
+  const std::size_t nrx = n * segs;
+  const std::size_t mem_size = tx_bytes + nrx * rx_buf;
+  std::vector<std::uint8_t> tx_img(tx_bytes);
+  std::vector<TxDescriptor> tx(n);
+  std::size_t at = 0;
+  for (std::size_t i = 0; i < n; ++i) {
+    std::uint8_t* p = tx_img.data() + at;
+    for (std::size_t b = 0; b < lens[i]; b += 8) {
+      const std::uint64_t r = rng();
+      std::memcpy(p + b, &r, std::min<std::size_t>(8, lens[i] - b));
+    }
+    p[12] = 0x08;
+    p[13] = 0x00;
+    if (wl != "c5") {  // balancing word in the source MAC: whole-frame checksum 0
+      p[10] = p[11] = 0;
+      const std::uint16_t c = csum(p, lens[i]);
+      p[10] = static_cast<std::uint8_t>(c >> 8);
+      p[11] = static_cast<std::uint8_t>(c);
+    }
+    TxDescriptor& t = tx[i];
+    t.buffer_address = at;
+    t.length = static_cast<std::uint32_t>(lens[i]);
+    t.descriptor_index = static_cast<std::uint16_t>(i);
+    t.checksum_offload = true;
+    t.checksum = ChecksumMode::Layer4;
+    if (wl == "c5") {
+      t.tso_enabled = true;
+      t.mss = 1448;
+      t.header_length = 54;
+    }
+    at += (lens[i] + 15) & ~std::size_t{15};
+  }
+  std::vector<RxDescriptor> rx(nrx);
+  for (std::size_t j = 0; j < nrx; ++j) {
+    rx[j].buffer_address = tx_bytes + j * rx_buf;
+    rx[j].buffer_length = static_cast<std::uint32_t>(rx_buf);
+    rx[j].descriptor_index = static_cast<std::uint16_t>(j);
+    rx[j].checksum_offload = true;
+    rx[j].checksum = ChecksumMode::Layer4;
+  }
+  void* mem = nullptr;
+  check(nicgpu_malloc(&mem, mem_size), "nicgpu_malloc");
+  check(nicgpu_memcpy_async(mem, tx_img.data(), tx_bytes, nullptr), "memcpy");
+  check(nicgpu_memset_async(static_cast<std::uint8_t*>(mem) + tx_bytes, 0, mem_size - tx_bytes, nullptr), "memset");
+  check(nicgpu_stream_synchronize(nullptr), "sync");
+
+  const std::vector<std::uint8_t> ms_key = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67,
+                                            0x25, 0x3d, 0x43, 0xa3, 0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb,
+                                            0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3, 0x80, 0x30,
+                                            0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
+  std::vector<std::uint16_t> table(128);
+  for (int i = 0; i < 128; ++i) table[i] = static_cast<std::uint16_t>(i % 16);
+  RssEngine rss{RssConfig{ms_key, table}};
+  BatchedQueuePairConfig cfg;
+  cfg.queue_id = 1;
+  cfg.rss = &rss;
+  BatchedQueuePair qp{cfg};
+  const DeviceHostMemory dm{static_cast<std::byte*>(mem), mem_size};
+
+  std::vector<double> tot;
+  RxBatchResult last;
+  for (int r = 0; r < reps + 1; ++r) {
+    const auto t0 = std::chrono::steady_clock::now();
+    RxBatchResult res = qp.process_batch(dm, tx, rx);
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    if (r > 0) tot.push_back(us);
+    last = std::move(res);
+  }
+  std::sort(tot.begin(), tot.end());
+  const double med = tot[tot.size() / 2];
+  std::size_t ok = 0, frame_bytes = 0;
+  for (const auto& c : last.rx_completions) ok += c.status == 0;
+  for (auto L : lens) frame_bytes += L;
+  const auto& T = last.timings;
+  std::printf(
+      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
+      "\"rx_success\": %zu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
+      "\"phases_us\": {\"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f}}\n",
+      wl.c_str(), n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.plan_us, T.sums_us,
+      T.resolve_us, T.gather_us, T.rss_us);
+  nicgpu_free(mem);
+  return 0;
+}
