@@ -164,6 +164,26 @@ int nicgpu_tso_checksum(const uint8_t* frames, const uint64_t* desc, const uint1
 int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int mode, uint32_t* out_crc,
                       uint8_t* out_ok, void* stream);
 
+/* TSO/GSO segmentation with VLAN insert/strip, materialised:
+ * QueuePair::build_segments (src/queue_pair.cpp:212-278), the TX VLAN insert
+ * (:324-331) and the RX VLAN strip (:389-395) applied to every frame.
+ * flags[i] (NULL = NICGPU_SEG_TSO for every frame): NICGPU_SEG_* bits plus the
+ * VLAN tag in the low 16 bits.  Segmentation happens when NICGPU_SEG_TSO is set,
+ * mss > 0 and L > mss; mss > 9000 or hdr_len > L then produces no segment
+ * (InvalidMss), as do more than 64 segments (TooManySegments); hdr_len >= L
+ * gives one copy of the frame.  Segment k of frame i is written to
+ * out[(seg_base[i] + k) * stride ..] (skipped if it does not fit the slot) with
+ * out_len = its size and out_csum = compute_checksum(segment bytes), the value
+ * the RX verify tests against 0 (:434-447).  seg_base: exclusive prefix sum of
+ * the segment counts under these rules (smart_nic_amd.tso_segment_counts). */
+#define NICGPU_SEG_TSO 0x10000u          /* tso_enabled || gso_enabled */
+#define NICGPU_SEG_VLAN_INSERT 0x20000u  /* TX: prepend 81 00 tag */
+#define NICGPU_SEG_VLAN_STRIP 0x40000u   /* RX: strip 4 bytes when the segment has a VLAN */
+#define NICGPU_SEG_VLAN_PRESENT 0x80000u /* RX descriptor says a VLAN is present */
+int nicgpu_tso_segment(const uint8_t* frames, const uint64_t* desc, const uint16_t* hdr_len, const uint16_t* mss,
+                       const uint32_t* seg_base, const uint32_t* flags, size_t n, uint8_t* out, uint64_t out_size,
+                       uint32_t stride, uint32_t* out_len, uint16_t* out_csum, void* stream);
+
 /* One DMA write of the batched QueuePair stage (nic/rx_stage.h):
  *   mem[dst ..] <- prefix bytes (prefix_len 0 or 4; little-endian word, i.e.
  *                  memory order) || mem[src_a, +len_a) || mem[src_b, +len_b).

@@ -912,6 +912,89 @@ void gen_l34() {
   write_bin("l34.desc.bin", desc);
   write_bin("l34.flags.bin", flags);
 }
+
+// -------------------------------------------- TSO + VLAN materialisation --
+// the segments the reference QueuePair delivers into RX buffers
+// for TSO/GSO frames with TX VLAN insert and RX VLAN strip/present
+// (queue_pair.cpp:212-278, 320-331, 389-395), RX checksum offload off so that
+// every segment is delivered.  Recorded per case: TX status, and for every
+// delivered segment its length, compute_checksum and FNV-1a-64 of its bytes.
+constexpr std::size_t kSlotHash = 9216 + 8;  // bytes of each RX slot hashed
+
+void gen_tso_vlan() {
+  Rng r{4242};
+  std::ostringstream js;
+  js << "{\n \"source\": \"QueuePair::process_once TSO/GSO + VLAN insert/strip (src/queue_pair.cpp:212-278, 320-331, 389-395); segments read back from the RX buffers\",\n \"cases\": [\n";
+  std::vector<std::uint8_t> frames;
+  const int ncase = 160;
+  for (int ci = 0; ci < ncase; ++ci) {
+    const std::size_t lens[] = {0, 3, 60, 64, 200, 1518, 3000, 9000, 9000, 9000};
+    std::size_t L = lens[r.below(10)];
+    std::vector<std::uint8_t> pkt(L);
+    for (auto& b : pkt) b = r.byte();
+    const bool tso = r.below(5) != 0;
+    const bool gso = tso && r.below(3) == 0;
+    const std::uint16_t mss = static_cast<std::uint16_t>(r.below(8) == 0 ? r.below(10) : (r.below(6) == 0 ? 9001 : 100 + r.below(1500)));
+    const std::uint16_t H = static_cast<std::uint16_t>(r.below(6) == 0 ? r.below(5) : (r.below(8) == 0 ? L + r.below(2) : 14 + r.below(60)));
+    const bool ins = r.below(2), strip = r.below(2), present = r.below(3) == 0;
+    const std::uint16_t tag = static_cast<std::uint16_t>(r.u32());
+    std::uint64_t off = frames.size();
+    frames.insert(frames.end(), pkt.begin(), pkt.end());
+    while (frames.size() % 16) frames.push_back(r.byte());
+    frames.insert(frames.end(), 16 * r.below(2), 0xEE);
+
+    const std::size_t slot = 9216 + 64, nrx = 70;
+    HostMemoryConfig mc{.size_bytes = slot * (nrx + 2), .page_size = 4096, .iommu_enabled = false};
+    SimpleHostMemory mem{mc};
+    DMAEngine dma{mem};
+    QueuePairConfig qc{
+        .queue_id = 0,
+        .tx_ring = {.descriptor_size = sizeof(TxDescriptor), .ring_size = 4, .base_address = 0, .queue_id = 0, .host_backed = false},
+        .rx_ring = {.descriptor_size = sizeof(RxDescriptor), .ring_size = nrx + 1, .base_address = 0, .queue_id = 0, .host_backed = false},
+        .tx_completion = {.ring_size = 4, .queue_id = 0},
+        .rx_completion = {.ring_size = nrx + 1, .queue_id = 0},
+    };
+    QueuePair qp{qc, dma};
+    assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(pkt))).ok());
+    TxDescriptor tx{.buffer_address = 0, .length = static_cast<std::uint32_t>(L), .checksum = ChecksumMode::None,
+                    .descriptor_index = 1, .checksum_value = 0, .tso_enabled = tso && !gso, .gso_enabled = gso,
+                    .mss = mss, .header_length = H, .vlan_insert = ins, .vlan_tag = tag};
+    std::vector<std::byte> tb(sizeof(TxDescriptor));
+    std::memcpy(tb.data(), &tx, sizeof(tx));
+    assert(qp.tx_ring().push_descriptor(tb).ok());
+    for (std::size_t i = 0; i < nrx; ++i) {
+      RxDescriptor rx{.buffer_address = slot * (i + 1), .buffer_length = static_cast<std::uint32_t>(slot),
+                      .checksum = ChecksumMode::None, .descriptor_index = static_cast<std::uint16_t>(i),
+                      .checksum_offload = false, .vlan_strip = strip, .vlan_present = present};
+      std::vector<std::byte> rb(sizeof(RxDescriptor));
+      std::memcpy(rb.data(), &rx, sizeof(rx));
+      assert(qp.rx_ring().push_descriptor(rb).ok());
+    }
+    qp.process_once();
+    auto tc = qp.tx_completion().poll_completion();
+    std::size_t k = 0;
+    while (qp.rx_completion().poll_completion()) ++k;
+    // RX memory starts zeroed, so each slot holds its segment followed by
+    // zeros: hash the whole slot (the test zero-pads its own segment the same
+    // way); the checksum of the slot is the segment's (zeros are neutral);
+    // rx_bytes pins the total delivered length.
+    js << "  {\"off\": " << off << ", \"len\": " << L << ", \"hdr\": " << H << ", \"mss\": " << mss << ", \"tso\": "
+       << int(tso) << ", \"insert\": " << int(ins) << ", \"tag\": " << tag << ", \"strip\": " << int(strip)
+       << ", \"present\": " << int(present) << ", \"tx_status\": " << (tc ? tc->status : 99u)
+       << ", \"segments\": " << k << ", \"rx_bytes\": " << qp.stats().rx_bytes << ", \"slot_fnv\": [";
+    std::vector<std::uint16_t> cs;
+    for (std::size_t i = 0; i < k; ++i) {
+      std::vector<std::byte> buf(kSlotHash);
+      assert(mem.read(slot * (i + 1), buf).ok());
+      js << (i ? "," : "") << "\"" << std::hex << fnv1a(buf.data(), buf.size()) << std::dec << "\"";
+      cs.push_back(nic::compute_checksum(buf));
+    }
+    js << "], \"seg_csum\": " << json_arr(cs) << "}" << (ci + 1 < ncase ? "," : "") << "\n";
+  }
+  js << " ]\n}\n";
+  write_bin("tso_vlan.frames.bin", frames);
+  std::ofstream(g_out + "/tso_vlan.json") << js.str();
+}
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -932,6 +1015,7 @@ int main(int argc, char** argv) {
   gen_tso();
   gen_qp_batch();
   gen_l34();
+  gen_tso_vlan();
   std::printf("golden fixtures written to %s\n", g_out.c_str());
   return 0;
 }

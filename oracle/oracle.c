@@ -259,3 +259,48 @@ int oracle_icrc_verify(const uint8_t* buf, size_t len) {
   const uint32_t stored = ((uint32_t) t[0] << 24) | ((uint32_t) t[1] << 16) | ((uint32_t) t[2] << 8) | t[3];
   return oracle_icrc_calculate(buf, len - 4) == stored;
 }
+
+int oracle_tso_segment(const uint8_t* pkt, size_t len, uint16_t hdr_len, uint16_t mss, uint32_t flags,
+                       uint8_t* out, size_t stride, size_t max_seg, uint32_t* lens, uint16_t* csums) {
+  /* build_segments (queue_pair.cpp:212-278) */
+  const int enabled = (flags & ORACLE_SEG_TSO) && mss > 0 && len > mss;
+  size_t h = len, nseg = 1;
+  if (enabled) {
+    if (mss < 1 || mss > 9000) return -1;
+    if (hdr_len > len) return -1;
+    if (hdr_len < len) {
+      h = hdr_len;
+      nseg = (len - h + mss - 1) / mss;
+      if (nseg > 64) return -2;
+    }
+  }
+  if (nseg > max_seg) return -3;
+  const int insert = (flags & ORACLE_SEG_VLAN_INSERT) != 0;
+  const unsigned tag = flags & 0xFFFFu;
+  for (size_t k = 0; k < nseg; ++k) {
+    const size_t p = h + k * mss;
+    const size_t chunk = h < len ? ((len - p < mss) ? len - p : mss) : 0;
+    /* segment = header || chunk; TX VLAN insert prepends 81 00 tag (:324-331) */
+    size_t n = 0;
+    uint8_t* s = (uint8_t*) malloc(h + chunk + 4);
+    if (!s) return -3;
+    if (insert) {
+      s[0] = 0x81; s[1] = 0x00; s[2] = (uint8_t) (tag >> 8); s[3] = (uint8_t) tag;
+      n = 4;
+    }
+    memcpy(s + n, pkt, h);
+    n += h;
+    memcpy(s + n, pkt + p, chunk);
+    n += chunk;
+    /* RX strip of the first 4 bytes when the segment carries a VLAN (:389-395) */
+    const int has_vlan = insert || (flags & ORACLE_SEG_VLAN_PRESENT);
+    size_t from = 0;
+    if ((flags & ORACLE_SEG_VLAN_STRIP) && has_vlan && n >= 4) from = 4;
+    if (n - from > stride) { free(s); return -3; }
+    memcpy(out + k * stride, s + from, n - from);
+    lens[k] = (uint32_t) (n - from);
+    csums[k] = oracle_compute_checksum(s + from, n - from);
+    free(s);
+  }
+  return (int) nseg;
+}

@@ -92,6 +92,20 @@ int oracle_tso_segment_checksums(const uint8_t* pkt, size_t len, uint16_t hdr_le
 #define ORACLE_L34_UDP_NOCSUM 0x10u
 uint8_t oracle_l34_verify(const uint8_t* frame, size_t len);
 
+/* TSO/GSO segmentation with VLAN insert/strip, materialised:
+ * QueuePair::build_segments (src/queue_pair.cpp:212-278), the TX VLAN insert
+ * (:320-331) and the RX VLAN strip (:389-395).  flags: ORACLE_SEG_* | tag.
+ * Writes segment k's delivered bytes at out + k * stride, its length in
+ * lens[k] and compute_checksum in csums[k].  Returns the segment count, -1
+ * for InvalidMss, -2 for TooManySegments, -3 if a segment exceeds stride or
+ * max_seg segments. */
+#define ORACLE_SEG_TSO 0x10000u
+#define ORACLE_SEG_VLAN_INSERT 0x20000u
+#define ORACLE_SEG_VLAN_STRIP 0x40000u
+#define ORACLE_SEG_VLAN_PRESENT 0x80000u
+int oracle_tso_segment(const uint8_t* pkt, size_t len, uint16_t hdr_len, uint16_t mss, uint32_t flags,
+                       uint8_t* out, size_t stride, size_t max_seg, uint32_t* lens, uint16_t* csums);
+
 /* RoCEv2 ICRC as the reference computes it: nic::rocev2::IcrcCalculator
  * (src/rocev2/packet.cpp:14-56): CRC-32C, reflected polynomial 0x82F63B78,
  * table-driven byte at a time, initial value 0xFFFFFFFF, final xor

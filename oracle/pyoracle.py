@@ -53,6 +53,8 @@ def lib():
         L.oracle_tso_segment_checksums.argtypes = [vp, sz, u16, u16, i32, vp, sz]
         L.oracle_l34_verify.restype = ctypes.c_uint8
         L.oracle_l34_verify.argtypes = [vp, sz]
+        L.oracle_tso_segment.restype = i32
+        L.oracle_tso_segment.argtypes = [vp, sz, u16, u16, u32, vp, sz, sz, vp, vp]
         L.oracle_icrc_calculate.restype = u32
         L.oracle_icrc_calculate.argtypes = [vp, sz]
         L.oracle_icrc_verify.restype = i32
@@ -167,3 +169,16 @@ def icrc_batch(frames: np.ndarray, desc: np.ndarray, verify=False):
         else:
             crc[i] = L.oracle_icrc_calculate(ctypes.c_void_p(base + off), ln)
     return crc, ok
+
+
+def tso_segment(pkt: bytes, hdr_len: int, mss: int, flags: int, stride: int = 9224):
+    """oracle_tso_segment: (status_or_count, [segment bytes], [csum])."""
+    L = lib()
+    buf = np.frombuffer(bytes(pkt) + bytes(16), np.uint8)
+    out = np.zeros(64 * stride, np.uint8)
+    lens = np.zeros(64, np.uint32)
+    cs = np.zeros(64, np.uint16)
+    k = L.oracle_tso_segment(_vp(buf), len(pkt), hdr_len, mss, flags, _vp(out), stride, 64, _vp(lens), _vp(cs))
+    if k <= 0:
+        return k, [], []
+    return k, [out[i * stride: i * stride + int(lens[i])].tobytes() for i in range(k)], [int(c) for c in cs[:k]]

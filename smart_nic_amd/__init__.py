@@ -13,6 +13,8 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnicgpu.so")
 HOST_LIB_PATH = os.path.join(_HERE, "libnic_host.so")
@@ -62,6 +64,7 @@ ABI_SYMBOLS = (
     "nicgpu_tso_checksum",
     "nicgpu_segment_gather",
     "nicgpu_icrc_batch",
+    "nicgpu_tso_segment",
 )
 
 _lib = None
@@ -97,6 +100,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_rx_offload_ex": (i32, [vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp, vp]),
         "nicgpu_segment_gather": (i32, [vp, ctypes.c_uint64, vp, sz, vp]),
         "nicgpu_icrc_batch": (i32, [vp, vp, sz, i32, vp, vp, vp]),
+        "nicgpu_tso_segment": (i32, [vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint64, u32, vp, vp, vp]),
         "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),
         "nicgpu_tso_checksum": (i32, [vp, vp, vp, vp, vp, sz, vp, vp]),
     }
@@ -235,6 +239,39 @@ def rx_offload(ctx, frames, desc, mode=TUPLE_AUTO, raw_off=0, raw_len=0, csum=No
         ),
         "nicgpu_rx_offload_ex",
     )
+
+
+SEG_TSO = 0x10000
+SEG_VLAN_INSERT = 0x20000
+SEG_VLAN_STRIP = 0x40000
+SEG_VLAN_PRESENT = 0x80000
+
+
+def tso_segment_counts(lens, hdr_len, mss, flags):
+    """Segments nicgpu_tso_segment writes per frame (queue_pair.cpp:212-278):
+    1 unsegmented, ceil((L - H) / mss) segmented, 0 for InvalidMss /
+    TooManySegments.  Returns (counts int64[n], seg_base uint32[n], total)."""
+    L = np.asarray(lens, np.int64)
+    H = np.broadcast_to(np.asarray(hdr_len, np.int64), L.shape)
+    M = np.broadcast_to(np.asarray(mss, np.int64), L.shape)
+    F = np.broadcast_to(np.asarray(flags, np.int64), L.shape)
+    seg = ((F & SEG_TSO) != 0) & (M > 0) & (L > M)
+    invalid = seg & ((M > 9000) | (H > L))
+    split = seg & ~invalid & (H < L)
+    cnt = np.where(split, (L - H + np.maximum(M, 1) - 1) // np.maximum(M, 1), 1)
+    cnt = np.where(invalid | (cnt > 64), 0, cnt)
+    base = np.zeros(L.shape, np.int64)
+    if L.size > 1:
+        base[1:] = np.cumsum(cnt[:-1])
+    return cnt, base.astype(np.uint32), int(cnt.sum())
+
+
+def tso_segment(frames, desc, hdr_len, mss, seg_base, flags, out, stride, out_len=None, out_csum=None, stream=None):
+    """Materialise TSO/GSO segments with VLAN insert/strip (nicgpu_tso_segment)."""
+    lib = load_library()
+    _check(lib.nicgpu_tso_segment(_ptr(frames), _ptr(desc), _ptr(hdr_len), _ptr(mss), _ptr(seg_base), _ptr(flags),
+                                  desc.numel(), _ptr(out), out.numel() * out.element_size(), stride, _ptr(out_len),
+                                  _ptr(out_csum), _stream_ptr(stream)), "nicgpu_tso_segment")
 
 
 ICRC_CALCULATE = 0

@@ -1070,19 +1070,32 @@ __device__ __forceinline__ uint32_t load_dword_clamped(const uint8_t* mem, uint6
   return v;
 }
 
-// Wave-cooperative copy of [src, src+len) to [dst, dst+len), any alignment.
-__device__ void wave_copy(uint8_t* mem, uint64_t mem_size, uint64_t dst, uint64_t src, uint64_t len, uint32_t lane) {
-  if (len == 0) return;
+// Wave-cooperative copy of smem[src, src+len) to dmem[dst, dst+len), any
+// alignment.  CLAMP: source reads stay inside smem[0, smem_size) (a memory
+// image whose end need not be 16-B padded); otherwise the source is a frame
+// buffer readable in whole 16-B chunks (include/nicgpu.h).  SUM: returns this
+// lane's share of the written bytes' little-endian halfword sum at absolute
+// destination positions (the convention of the RX chunk sums).
+template <bool CLAMP, bool SUM>
+__device__ uint32_t wave_copy(uint8_t* dmem, uint64_t dst, const uint8_t* smem, uint64_t smem_size, uint64_t src,
+                              uint64_t len, uint32_t lane) {
+  uint32_t sum = 0;
+  if (len == 0) return 0;
+  auto byte = [&](uint64_t d, uint64_t s_) __attribute__((always_inline)) {
+    const uint32_t b = smem[s_];
+    dmem[d] = (uint8_t) b;
+    if (SUM) sum += b << (8 * (d & 1));
+  };
   const uint64_t d1 = dst + len;
   const uint64_t A = (dst + 3) & ~3ull;  // first whole dword
   const uint64_t B = d1 & ~3ull;          // end of the last whole dword
   if (A >= B) {                           // no whole dword: bytes only
-    if (lane < len) mem[dst + lane] = mem[src + lane];
-    return;
+    if (lane < len) byte(dst + lane, src + lane);
+    return sum;
   }
   const uint64_t head = A - dst, tail = d1 - B;
-  if (lane < head) mem[dst + lane] = mem[src + lane];
-  if (lane >= 8 && lane - 8 < tail) mem[B + (lane - 8)] = mem[src + (B - dst) + (lane - 8)];
+  if (lane < head) byte(dst + lane, src + lane);
+  if (lane >= 8 && lane - 8 < tail) byte(B + (lane - 8), src + (B - dst) + (lane - 8));
   const uint64_t nw = (B - A) >> 2;
   const uint64_t s0 = src + head;  // source of dword A
   const uint32_t sh = (uint32_t) (s0 & 3);
@@ -1090,15 +1103,21 @@ __device__ void wave_copy(uint8_t* mem, uint64_t mem_size, uint64_t dst, uint64_
   for (uint64_t i = (uint64_t) lane * 4; i < nw; i += 256) {
     uint32_t v[5];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) v[j] = (i + j <= nw) ? load_dword_clamped(mem, mem_size, sa + 4 * (i + j)) : 0u;
+    for (int j = 0; j < 5; ++j) {
+      const uint64_t a = sa + 4 * (i + j);
+      if (CLAMP) v[j] = (i + j <= nw) ? load_dword_clamped(smem, smem_size, a) : 0u;
+      else v[j] = (i + j <= nw && (j < 4 || sh)) ? *reinterpret_cast<const uint32_t*>(smem + a) : 0u;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (i + j < nw) {
         const uint32_t o = sh ? __builtin_amdgcn_alignbyte(v[j + 1], v[j], sh) : v[j];
-        *reinterpret_cast<uint32_t*>(mem + A + 4 * (i + j)) = o;
+        *reinterpret_cast<uint32_t*>(dmem + A + 4 * (i + j)) = o;
+        if (SUM) sum += (o & 0xFFFFu) + (o >> 16);
       }
     }
   }
+  return sum;
 }
 
 __global__ __launch_bounds__(kBlock) void segment_gather_kernel(GatherParams P) {
@@ -1114,8 +1133,96 @@ __global__ __launch_bounds__(kBlock) void segment_gather_kernel(GatherParams P) 
         w.len_a > P.mem_size - w.src_a || w.src_b > P.mem_size || w.len_b > P.mem_size - w.src_b)
       continue;
     if (lane < plen) P.mem[w.dst + lane] = (uint8_t) (w.prefix >> (8 * lane));
-    wave_copy(P.mem, P.mem_size, w.dst + plen, w.src_a, w.len_a, lane);
-    wave_copy(P.mem, P.mem_size, w.dst + plen + w.len_a, w.src_b, w.len_b, lane);
+    wave_copy<true, false>(P.mem, w.dst + plen, P.mem, P.mem_size, w.src_a, w.len_a, lane);
+    wave_copy<true, false>(P.mem, w.dst + plen + w.len_a, P.mem, P.mem_size, w.src_b, w.len_b, lane);
+  }
+}
+
+// ------------------------------------------------- TSO/GSO segmentation --
+// QueuePair::build_segments (src/queue_pair.cpp:212-278) plus the
+// TX VLAN insert (:324-331) and RX VLAN strip (:389-395) that shape each
+// delivered segment, materialised on the GPU.  One wave per frame walks its
+// segments; segment g = seg_base[i] + k is written at out + g * stride and its
+// length and compute_checksum (what handle_rx_segment verifies, :434-447) are
+// reported.  The checksum is summed from the dwords the wave writes, so frame
+// bytes are read once (the header once per segment, from L2) and written once.
+struct TsoSegParams {
+  const uint8_t* frames;
+  const uint64_t* desc;
+  const uint16_t* hdr_len;
+  const uint16_t* mss;
+  const uint32_t* seg_base;
+  const uint32_t* flags;  // per frame: NICGPU_SEG_* | vlan tag (low 16 bits); may be null
+  size_t n;
+  uint8_t* out;
+  uint64_t out_size;
+  uint32_t stride;
+  uint32_t* out_len;
+  uint16_t* out_csum;
+};
+
+__global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
+  const uint32_t lane = lane_id();
+  const uint64_t nwaves = (uint64_t) gridDim.x * kWavesPerBlock;
+  for (uint64_t i = (uint64_t) blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; i < P.n; i += nwaves) {
+    const uint64_t d = P.desc[i];
+    const uint64_t off = d & kOffMask;
+    const uint32_t L = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
+    const uint32_t fl = P.flags ? P.flags[i] : NICGPU_SEG_TSO;
+    const uint32_t tag = fl & 0xFFFFu;
+    const uint32_t mss = P.mss[i];
+    uint32_t H = P.hdr_len[i];
+    // build_segments (:212-278)
+    uint32_t nseg = 1;
+    bool seg = (fl & NICGPU_SEG_TSO) && mss > 0 && L > mss;
+    if (seg) {
+      if (mss > 9000u || H > L) continue;  // InvalidMss: no segment
+      if (H >= L) {
+        seg = false;  // degenerate: one unsegmented copy
+      } else {
+        nseg = (L - H + mss - 1) / mss;
+        if (nseg > 64u) continue;  // TooManySegments
+      }
+    }
+    if (!seg) H = L;
+    const bool insert = fl & NICGPU_SEG_VLAN_INSERT;
+    const bool has_vlan = insert || (fl & NICGPU_SEG_VLAN_PRESENT);
+    for (uint32_t k = 0; k < nseg; ++k) {
+      const uint32_t clen = seg ? min(mss, L - H - k * mss) : 0u;
+      const uint64_t base_len = (uint64_t) H + clen;
+      uint64_t size = base_len + (insert ? 4 : 0);
+      const bool strip = (fl & NICGPU_SEG_VLAN_STRIP) && has_vlan && size >= 4;
+      if (strip) size -= 4;
+      const bool prefix = insert && !strip;
+      const bool strip_base = strip && !insert;
+      const uint64_t g = (uint64_t) P.seg_base[i] + k;
+      const uint64_t dst = g * P.stride;
+      if (dst > P.out_size || size > P.out_size - dst || size > P.stride) continue;  // does not fit its slot
+      uint64_t src_a = off, len_a = H, src_b = off + H + (uint64_t) k * mss, len_b = clen;
+      if (strip_base) {  // the base segment loses its first 4 bytes
+        const uint64_t from_a = len_a < 4 ? len_a : 4;
+        src_a += from_a;
+        len_a -= from_a;
+        src_b += 4 - from_a;
+        len_b -= 4 - from_a;
+      }
+      uint32_t sum = 0;
+      const uint64_t pl = prefix ? 4 : 0;
+      if (lane < pl) {
+        const uint32_t b = lane == 0 ? 0x81u : (lane == 1 ? 0x00u : (lane == 2 ? (tag >> 8) : (tag & 0xFFu)));
+        P.out[dst + lane] = (uint8_t) b;
+        sum += b << (8 * ((dst + lane) & 1));
+      }
+      sum += wave_copy<false, true>(P.out, dst + pl, P.frames, 0, src_a, len_a, lane);
+      sum += wave_copy<false, true>(P.out, dst + pl + len_a, P.frames, 0, src_b, len_b, lane);
+      const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan(sum), 63);
+      if (lane == 0) {
+        const uint32_t x = fold16(tot);
+        const uint32_t be = (dst & 1) ? x : bswap16(x);
+        if (P.out_len) P.out_len[g] = (uint32_t) size;
+        if (P.out_csum) P.out_csum[g] = (uint16_t) (~be & 0xFFFFu);
+      }
+    }
   }
 }
 
@@ -1652,6 +1759,23 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
   const uint64_t cap = (uint64_t) di->cus * 8;
   const unsigned grid = (unsigned) (want < 1 ? 1 : (want < cap ? want : cap));
   hipLaunchKernelGGL(icrc_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
+  return hip_status(hipGetLastError());
+}
+
+int nicgpu_tso_segment(const uint8_t* frames, const uint64_t* desc, const uint16_t* hdr_len, const uint16_t* mss,
+                       const uint32_t* seg_base, const uint32_t* flags, size_t n, uint8_t* out, uint64_t out_size,
+                       uint32_t stride, uint32_t* out_len, uint16_t* out_csum, void* stream) {
+  if (n == 0) return NICGPU_OK;
+  if (!frames || !desc || !hdr_len || !mss || !seg_base || !out || stride == 0) return NICGPU_ERR_INVALID;
+  if ((reinterpret_cast<uintptr_t>(frames) & 15u) != 0) return NICGPU_ERR_INVALID;
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  TsoSegParams P{frames, desc, hdr_len, mss, seg_base, flags, n, out, out_size, stride, out_len, out_csum};
+  const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint64_t cap = (uint64_t) di->cus * 8;
+  const unsigned grid = (unsigned) (want < cap ? want : cap);
+  hipLaunchKernelGGL(tso_segment_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
   return hip_status(hipGetLastError());
 }
 

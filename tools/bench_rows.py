@@ -9,6 +9,8 @@ Rows (SURVEY §8 d configs):
   icrc_c2      nicgpu_icrc_batch (f4) over the C2 frames
   icrc_c3      nicgpu_icrc_batch over the C3 frames
   tso_c5       nicgpu_tso_checksum, C5 = 131072 x 9000 B, H=54, mss=1448 (7 segments)
+  tso_seg_c5   nicgpu_tso_segment (f2): the C5 segments materialised with a VLAN insert,
+               plus their checksums
 
 Algorithmic bytes per launch (SURVEY §8 d): sum(L) + 16 N for the RX rows (frame
 bytes, 8-B descriptor, 8 B of results); ICRC: sum(L) + 8 N + 4 N; TSO:
@@ -49,7 +51,7 @@ def timed(torch, fn, steps, warmup):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--rows", default="rx_c2,rx_l34_c2,rx_c3,icrc_c2,icrc_c3,tso_c5")
+    ap.add_argument("--rows", default="rx_c2,rx_l34_c2,rx_c3,icrc_c2,icrc_c3,tso_c5,tso_seg_c5")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     args = ap.parse_args()
@@ -144,6 +146,27 @@ def main():
 
             med, mean = timed(torch, fn, args.steps, args.warmup)
             report(row, "c5", n, fb, fb + 16 * n + 2 * n * nseg, med, mean, {"segments": n * nseg})
+        elif row == "tso_seg_c5":
+            n, fb, f, d = batch("c5")
+            H, MSS, STRIDE = 54, 1448, 1536
+            fl_np = np.full(n, sna.SEG_TSO | sna.SEG_VLAN_INSERT | 0x0123, np.uint32)
+            cnt, base_np, total = sna.tso_segment_counts(np.full(n, 9000), np.full(n, H), np.full(n, MSS), fl_np)
+            hdr = torch.full((n,), H, dtype=torch.int16, device=dev)
+            mss = torch.full((n,), MSS, dtype=torch.int16, device=dev)
+            base = torch.from_numpy(base_np.view(np.int32)).to(dev)
+            fl = torch.from_numpy(fl_np.view(np.int32)).to(dev)
+            out = torch.empty(total * STRIDE, dtype=torch.uint8, device=dev)
+            ol = torch.empty(total, dtype=torch.int32, device=dev)
+            oc = torch.empty(total, dtype=torch.int16, device=dev)
+
+            def fn():
+                sna.tso_segment(f, d, hdr, mss, base, fl, out, STRIDE, ol, oc)
+
+            med, mean = timed(torch, fn, args.steps, args.warmup)
+            written = int(n * (7 * (H + 4)) + n * (9000 - H))
+            # read frames once + write the segments + 8 B desc, 12 B per-frame params, 6 B per segment out
+            report(row, "c5", n, fb, fb + written + 20 * n + 6 * total, med, mean,
+                   {"segments": total, "bytes_written": written})
         else:
             raise SystemExit(f"unknown row {row}")
 
