@@ -37,6 +37,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <span>
 #include <vector>
 
@@ -137,6 +138,11 @@ struct RxBatchResult {
 class BatchedQueuePair {
 public:
   explicit BatchedQueuePair(BatchedQueuePairConfig config);
+  ~BatchedQueuePair();
+  BatchedQueuePair(const BatchedQueuePair&) = delete;
+  BatchedQueuePair& operator=(const BatchedQueuePair&) = delete;
+  BatchedQueuePair(BatchedQueuePair&&) noexcept;
+  BatchedQueuePair& operator=(BatchedQueuePair&&) noexcept;
 
   /// Process every descriptor of `tx` in order against the RX descriptors `rx`
   /// (the RX ring's contents, rx[0] first).  Synchronises `stream` (a
@@ -149,8 +155,10 @@ public:
   [[nodiscard]] const BatchedQueuePairConfig& config() const noexcept { return config_; }
 
 private:
+  struct Scratch;  // device buffers reused across batches (grown, never shrunk)
   BatchedQueuePairConfig config_;
   QueuePairStats stats_{};
+  std::unique_ptr<Scratch> scratch_;
 };
 
 // Building blocks of process_batch, public so that the host logic can be

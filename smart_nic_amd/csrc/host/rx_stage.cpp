@@ -388,18 +388,34 @@ void check(int st, const char* what) {
   if (st != NICGPU_OK) throw GpuError(std::string(what) + ": " + nicgpu_strerror(st), st);
 }
 
-// Device scratch owned for the duration of one batch.
-struct DevScratch {
+// One growable device buffer.
+struct DevBuf {
   void* p = nullptr;
-  explicit DevScratch(std::size_t n) { check(nicgpu_malloc(&p, n ? n : 16), "nicgpu_malloc"); }
-  ~DevScratch() { nicgpu_free(p); }
-  DevScratch(const DevScratch&) = delete;
-  DevScratch& operator=(const DevScratch&) = delete;
+  std::size_t cap = 0;
+  void* get(std::size_t n) {
+    if (n > cap) {
+      nicgpu_free(p);
+      p = nullptr;
+      cap = 0;
+      check(nicgpu_malloc(&p, n), "nicgpu_malloc");
+      cap = n;
+    }
+    return p;
+  }
+  ~DevBuf() { nicgpu_free(p); }
 };
 
 }  // namespace
 
-BatchedQueuePair::BatchedQueuePair(BatchedQueuePairConfig config) : config_(std::move(config)) {}
+struct BatchedQueuePair::Scratch {
+  DevBuf piece_desc, piece_csum, writes, rss_desc, rss_hash, rss_queue;
+};
+
+BatchedQueuePair::BatchedQueuePair(BatchedQueuePairConfig config)
+    : config_(std::move(config)), scratch_(std::make_unique<Scratch>()) {}
+BatchedQueuePair::~BatchedQueuePair() = default;
+BatchedQueuePair::BatchedQueuePair(BatchedQueuePair&&) noexcept = default;
+BatchedQueuePair& BatchedQueuePair::operator=(BatchedQueuePair&&) noexcept = default;
 
 RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                               std::span<const RxDescriptor> rx, void* stream) {
@@ -419,12 +435,13 @@ RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::
   if (np) {
     std::vector<std::uint64_t> desc(np);
     for (std::size_t i = 0; i < np; ++i) desc[i] = NICGPU_DESC(plan.pieces[i].addr, plan.pieces[i].len);
-    DevScratch d_desc(np * 8), d_cs(np * 2);
-    check(nicgpu_memcpy_async(d_desc.p, desc.data(), np * 8, stream), "nicgpu_memcpy_async");
-    check(nicgpu_checksum_batch(reinterpret_cast<const std::uint8_t*>(mem.base), static_cast<const std::uint64_t*>(d_desc.p),
-                                np, static_cast<std::uint16_t*>(d_cs.p), stream),
+    void* d_desc = scratch_->piece_desc.get(np * 8);
+    void* d_cs = scratch_->piece_csum.get(np * 2);
+    check(nicgpu_memcpy_async(d_desc, desc.data(), np * 8, stream), "nicgpu_memcpy_async");
+    check(nicgpu_checksum_batch(reinterpret_cast<const std::uint8_t*>(mem.base), static_cast<const std::uint64_t*>(d_desc),
+                                np, static_cast<std::uint16_t*>(d_cs), stream),
           "nicgpu_checksum_batch");
-    check(nicgpu_memcpy_async(csum.data(), d_cs.p, np * 2, stream), "nicgpu_memcpy_async");
+    check(nicgpu_memcpy_async(csum.data(), d_cs, np * 2, stream), "nicgpu_memcpy_async");
     check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
   }
   out.timings.sums_us = us_since(t);
@@ -440,10 +457,10 @@ RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::
 
   // (4) DMA writes of every segment that reached the RX buffer
   if (!writes.empty()) {
-    DevScratch d_w(writes.size() * sizeof(SegmentWrite));
-    check(nicgpu_memcpy_async(d_w.p, writes.data(), writes.size() * sizeof(SegmentWrite), stream), "nicgpu_memcpy_async");
+    void* d_w = scratch_->writes.get(writes.size() * sizeof(SegmentWrite));
+    check(nicgpu_memcpy_async(d_w, writes.data(), writes.size() * sizeof(SegmentWrite), stream), "nicgpu_memcpy_async");
     check(nicgpu_segment_gather(reinterpret_cast<std::uint8_t*>(mem.base), mem.size,
-                                static_cast<const nicgpu_segment_write*>(d_w.p), writes.size(), stream),
+                                static_cast<const nicgpu_segment_write*>(d_w), writes.size(), stream),
           "nicgpu_segment_gather");
     check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
   }
@@ -467,15 +484,17 @@ RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::
     }
     if (!which.empty()) {
       const std::size_t m = which.size();
-      DevScratch d_desc(m * 8), d_h(m * 4), d_q(m * 2);
-      check(nicgpu_memcpy_async(d_desc.p, desc.data(), m * 8, stream), "nicgpu_memcpy_async");
+      void* d_desc = scratch_->rss_desc.get(m * 8);
+      void* d_h = scratch_->rss_hash.get(m * 4);
+      void* d_q = scratch_->rss_queue.get(m * 2);
+      check(nicgpu_memcpy_async(d_desc, desc.data(), m * 8, stream), "nicgpu_memcpy_async");
       config_.rss->select_queue_batch(
-          DevicePacketBatch{mem.base, static_cast<const std::uint64_t*>(d_desc.p), m}, config_.tuple,
-          RxBatchOutputs{nullptr, static_cast<std::uint32_t*>(d_h.p), static_cast<std::uint16_t*>(d_q.p)}, stream, true);
+          DevicePacketBatch{mem.base, static_cast<const std::uint64_t*>(d_desc), m}, config_.tuple,
+          RxBatchOutputs{nullptr, static_cast<std::uint32_t*>(d_h), static_cast<std::uint16_t*>(d_q)}, stream, true);
       std::vector<std::uint32_t> h(m);
       std::vector<std::uint16_t> q(m);
-      check(nicgpu_memcpy_async(h.data(), d_h.p, m * 4, stream), "nicgpu_memcpy_async");
-      check(nicgpu_memcpy_async(q.data(), d_q.p, m * 2, stream), "nicgpu_memcpy_async");
+      check(nicgpu_memcpy_async(h.data(), d_h, m * 4, stream), "nicgpu_memcpy_async");
+      check(nicgpu_memcpy_async(q.data(), d_q, m * 2, stream), "nicgpu_memcpy_async");
       check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
       std::uint16_t qmax = 0;
       for (std::size_t i = 0; i < m; ++i) {
