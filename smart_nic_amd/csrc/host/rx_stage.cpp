@@ -144,6 +144,7 @@ struct PacketSums {
 Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx) {
   Plan plan;
   plan.packets.resize(tx.size());
+  plan.pieces.reserve(2 * tx.size());
   for (std::size_t i = 0; i < tx.size(); ++i) {
     const TxDescriptor& t = tx[i];
     PacketPlan& pp = plan.packets[i];
@@ -222,6 +223,10 @@ void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const P
     return e;
   };
 
+  out.tx_completions.reserve(out.tx_completions.size() + tx.size());
+  out.rx_completions.reserve(out.rx_completions.size() + std::min(tx.size(), rx.size()));
+  write_of_rx.reserve(write_of_rx.size() + std::min(tx.size(), rx.size()));
+  writes.reserve(writes.size() + std::min(tx.size(), rx.size()));
   std::size_t rc = 0;  // RX ring consumer position
   for (std::size_t i = 0; i < tx.size(); ++i) {
     const TxDescriptor& t = tx[i];
