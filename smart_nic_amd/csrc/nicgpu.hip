@@ -1035,8 +1035,8 @@ struct RxVariant {
 };
 
 const RxVariant kRxVariants[] = {
-    {rx_block_kernel<2, true, 4>, 2, 4, "blk_u2_nt1_w4", true},
     {rx_offload_kernel<2, true, 4, true>, 2, 4, "u2_nt1_w4_c"},
+    {rx_block_kernel<2, true, 4>, 2, 4, "blk_u2_nt1_w4", true},
     {rx_block_kernel<1, true, 4>, 1, 4, "blk_u1_nt1_w4", true},
     {rx_block_kernel<4, true, 4>, 4, 4, "blk_u4_nt1_w4", true},
     {rx_block_kernel<2, true, 8>, 2, 8, "blk_u2_nt1_w8", true},
