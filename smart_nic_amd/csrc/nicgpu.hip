@@ -175,22 +175,6 @@ __host__ __device__ constexpr uint32_t rx_wave_lds(bool rss, int unroll) {
   return rx_hdr_off(unroll) + (rss ? kWave * kHdrChunks * 16 : 0);
 }
 
-// block path: 2 slot windows + 2 x (U x WPB) step totals; general path: per-wave pk (rewritten every
-// tile, so it may overlay the slots) + per-wave tagged marks, which must never be overlaid (a stale
-// word matching a live tag would map chunks to the wrong packet)
-__host__ __device__ constexpr uint32_t rx_block_scratch_bytes(int unroll, int wpb) {
-  return ((uint32_t) (2 * kWave * wpb * unroll * 4 + 2 * unroll * wpb * 4) > (uint32_t) (wpb * kWave * 16)
-              ? (uint32_t) (2 * kWave * wpb * unroll * 4 + 2 * unroll * wpb * 4)
-              : (uint32_t) (wpb * kWave * 16)) +
-         (uint32_t) (wpb * kWave * unroll * 4);
-}
-
-__host__ __device__ inline uint32_t rx_block_lds_bytes(int wpb, int unroll, bool rss, uint32_t lut_words,
-                                                       uint32_t hist_n) {
-  return (uint32_t) (kWave * 8) + (rss ? (uint32_t) (kWave * kHdrChunks * 16) : 0u) +
-         rx_block_scratch_bytes(unroll, wpb) + lut_words * 4u + hist_n * 4u;
-}
-
 __host__ __device__ inline uint32_t rx_lds_bytes(int wpb, int unroll, bool rss, uint32_t lut_words, uint32_t hist_n) {
   return (uint32_t) wpb * rx_wave_lds(rss, unroll) + lut_words * 4u + hist_n * 4u;
 }
@@ -523,21 +507,21 @@ __device__ __forceinline__ uint32_t process_batch(ChunkBatch<U>& B, uint32_t run
 // wave-uniform.
 // (no padding bytes: struct copies with padding leave scratch allocas behind)
 struct Tile {
-  uint64_t id;
+  uint64_t base;  // packet index of lane 0
   uint64_t off;
   int64_t delta;  // first16 - start: chunk c of this packet is absolute chunk c + delta
   int64_t D;      // common delta of a contiguous tile
   uint32_t len, nch, start, end, info;
   uint32_t total;
   uint32_t contig;  // 0/1
-  uint32_t pad_;
+  uint32_t nvalid;  // lanes holding a packet of this tile (lanes >= nvalid write nothing)
 };
 static_assert(sizeof(Tile) == 64, "Tile must stay padding-free");
 
 template <bool CONTIG>
-__device__ __forceinline__ Tile make_tile(uint64_t id, uint64_t d) {
+__device__ __forceinline__ Tile make_tile(uint64_t base, uint32_t nvalid, uint64_t d) {
   Tile t;
-  t.id = id;
+  t.base = base;
   t.off = d & kOffMask;
   t.len = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
   const uint64_t first16 = t.off >> 4;
@@ -555,7 +539,7 @@ __device__ __forceinline__ Tile make_tile(uint64_t id, uint64_t d) {
   const uint32_t dh = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) ((uint64_t) t.delta >> 32), first_ne);
   t.D = (int64_t) (((uint64_t) dh << 32) | dl);
   t.contig = (CONTIG && __ballot(t.nch != 0u && t.delta != t.D) == 0ull) ? 1u : 0u;
-  t.pad_ = 0;
+  t.nvalid = nvalid;
   return t;
 }
 
@@ -578,7 +562,7 @@ struct RxLdsPtrs {
 __device__ __forceinline__ void tile_epilogue(const RxParams& P, const RxLdsPtrs& L, const Tile& t, uint32_t lane) {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  const uint64_t pid = t.id * kWave + lane;
+  const uint64_t pid = t.base + lane;
   // contiguous tiles record only tail prefixes: a packet starts where the
   // nearest non-empty packet before it ended (0 at the tile start)
   uint32_t base_prefix = 0;
@@ -587,7 +571,7 @@ __device__ __forceinline__ void tile_epilogue(const RxParams& P, const RxLdsPtrs
     const uint32_t prev = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) pidx, 0x138, 0xf, 0xf, false);  // wave_shr:1
     base_prefix = (lane != 0u && prev != 0u) ? L.E[prev - 1u] : 0u;
   }
-  if (pid < P.n) {
+  if (lane < t.nvalid) {
     const uint32_t sum = t.nch ? (L.E[lane] - (t.contig ? base_prefix : L.S[lane])) : 0u;
     const uint32_t x = fold16(sum);
     // LE halfword sums at absolute positions == byte-swapped BE sum when the
@@ -640,7 +624,7 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
   }
 }
 
-template <int U, bool NT, int WPB, bool CONTIG>
+template <int U, bool NT, int WPB, bool CONTIG, bool RANGES>
 __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
   extern __shared__ uint4 lds_dyn[];
   const int w = threadIdx.x / kWave;
@@ -679,17 +663,35 @@ __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
   }
   __syncthreads();
 
-  const uint64_t ntiles = (P.n + kWave - 1) / kWave;
+  // Work split.  RANGES: wave g owns packets [g*n/W, (g+1)*n/W), walked in
+  // tiles of 64 (the last one partial), so every wave streams the same number
+  // of bytes give or take one packet (whole-tile round robin leaves the last
+  // round to a fraction of the waves: 1 M packets = 3.2 tiles per wave).
+  // Otherwise tile k*W + g (round robin).
   const uint64_t nwaves = (uint64_t) gridDim.x * WPB;
-  auto desc_of = [&](uint64_t id) __attribute__((always_inline)) -> uint64_t {
-    return (id < ntiles && id * kWave + lane < P.n) ? P.desc[id * kWave + lane] : 0ull;
+  const uint64_t gw = (uint64_t) blockIdx.x * WPB + w;
+  uint64_t end, step;
+  uint64_t first;
+  if (RANGES) {
+    first = gw * P.n / nwaves;
+    end = (gw + 1) * P.n / nwaves;
+    step = kWave;
+  } else {
+    first = gw * kWave;
+    end = P.n;
+    step = nwaves * kWave;
+  }
+  auto nvalid_of = [&](uint64_t b) __attribute__((always_inline)) -> uint32_t {
+    return b < end ? (uint32_t) (end - b < (uint64_t) kWave ? end - b : (uint64_t) kWave) : 0u;
+  };
+  auto desc_of = [&](uint64_t b) __attribute__((always_inline)) -> uint64_t {
+    return lane < nvalid_of(b) ? P.desc[b + lane] : 0ull;
   };
   // descriptors are prefetched one tile ahead
-  uint64_t id0 = (uint64_t) blockIdx.x * WPB + w;
-  uint64_t d_next = desc_of(id0 + nwaves);
-  Tile cur = make_tile<CONTIG>(id0, desc_of(id0));
+  uint64_t d_next = desc_of(first + step);
+  Tile cur = make_tile<CONTIG>(first, nvalid_of(first), desc_of(first));
 
-  while (cur.id < ntiles) {
+  while (cur.nvalid != 0u) {
     if (cur.contig && cur.total != 0u) {
       // Contiguous tile: chunk c is absolute chunk D + c.  Ping-pong: batch
       // i+1's loads are in flight while batch i is reduced; every plan is
@@ -716,206 +718,9 @@ __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
       run_general_tile<U, NT>(P, L, cur, lane, tag);
     }
     tile_epilogue(P, L, cur, lane);
-    cur = make_tile<CONTIG>(cur.id + nwaves, d_next);
-    d_next = desc_of(cur.id + nwaves);
-  }
-
-  if (L.hist_lds) {
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) {
-      uint32_t v = L.hist[i];
-      if (v) atomicAdd(&P.out_hits[i], (unsigned long long) v);
-    }
-  }
-}
-
-// --------------------------------------------------------------------------
-// Block-cooperative variant.  A block of WPB waves owns a tile of 64 packets
-// (all waves hold the same 64 descriptors).  Contiguous tiles are streamed by
-// the whole block: in a block step of WPB x 64 chunks, wave w reads KiB w, so
-// the waves of a block read adjacent memory (measured read ceiling of this
-// pattern 6.8-7.1 TB/s vs 6.0-6.4 TB/s for one tile per wave,
-// profiles/r01_tune_variants.json) and the grid has 4x fewer, 4x shorter
-// tiles in flight (a shorter tail).  Chunk sums are scanned per wave; the
-// per-wave step totals are exchanged through LDS once per batch (one
-// s_barrier) to form block-wide prefixes.  Packet sums are E - S recorded at
-// the packet's tail and head chunks.  Non-contiguous tiles are split into four
-// 16-packet quarters, one per wave, on the general (marks + prefix-max) path.
-template <int U>
-__device__ __forceinline__ void scatter_slots_win(uint32_t* slots, uint32_t win, uint32_t base, uint32_t lane,
-                                                  uint32_t start, uint32_t nch, uint32_t info) {
-  if (nch == 0u) return;
-  const uint32_t rs = start - base;
-  const uint32_t re = start + nch - 1u - base;
-  const uint32_t lo = info & 15u, hi = (info >> 4) & 31u;
-  const uint32_t common = 1u | (lane << 1);
-#pragma unroll
-  for (uint32_t j = 0; j < (uint32_t) kHdrChunks; ++j) {
-    const uint32_t r = rs + j;
-    if (j < nch && r < win) {
-      uint32_t v = common | (j << 7) | (j == 0 ? (lo << 11) : 0u);
-      v |= (j + 1u == nch) ? ((1u << 15) | (hi << 16)) : (16u << 16);
-      slots[r] = v;
-    }
-  }
-  if (nch > (uint32_t) kHdrChunks && re < win) slots[re] = common | (7u << 7) | (1u << 15) | (hi << 16);
-}
-
-template <int U, int WPB, bool NT>
-__device__ __forceinline__ void plan_block(ContigBatch<U>& B, uint32_t* slots, uint32_t base, uint32_t total,
-                                           uint32_t w, uint32_t lane, const Tile& t, const u32x4* __restrict__ tile16) {
-  constexpr uint32_t kS = (uint32_t) kWave * WPB;
-  if ((lane % WPB) == w) scatter_slots_win<U>(slots, kS * U, base, lane, t.start, t.nch, t.info);
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const uint32_t c = base + (uint32_t) u * kS + w * kWave + lane;
-    const uint32_t ce = c < total ? c : total - 1u;
-    if constexpr (NT) B.v[u] = __builtin_nontemporal_load(tile16 + ce);
-    else B.v[u] = tile16[ce];
-  }
-}
-
-template <int U, int WPB>
-__device__ __forceinline__ uint32_t process_block(ContigBatch<U>& B, uint32_t* slots, uint32_t* tot, uint32_t run,
-                                                  uint32_t* S, uint32_t* E, uint4* hdr, bool stage_hdr, uint32_t w,
-                                                  uint32_t lane) {
-  constexpr uint32_t kS = (uint32_t) kWave * WPB;
-  uint32_t sl[U], incl[U], sv[U];
-  u32x4 vv[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const uint32_t idx = (uint32_t) u * kS + w * kWave + lane;
-    sl[u] = slots[idx];
-    u32x4 v = B.v[u];
-    if (sl[u] != 0u) {
-      slots[idx] = 0u;
-      const int lo = (int) ((sl[u] >> 11) & 15u), hi = (int) ((sl[u] >> 16) & 31u);
-      if (lo != 0 || hi != 16) {
-        v.x &= dword_keep(lo, hi, 0);
-        v.y &= dword_keep(lo, hi, 1);
-        v.z &= dword_keep(lo, hi, 2);
-        v.w &= dword_keep(lo, hi, 3);
-      }
-    }
-    vv[u] = v;
-    sv[u] = add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, 0u))));
-    incl[u] = wave_incl_scan(sv[u]);
-    if (lane == 63u) tot[u * WPB + w] = incl[u];
-  }
-  __syncthreads();  // step totals of every wave (and the next window's slots) are visible
-  uint32_t tw[U * WPB];
-#pragma unroll
-  for (int i = 0; i < U * WPB; ++i) tw[i] = tot[i];
-  uint32_t pre = run;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    uint32_t before = 0;
-#pragma unroll
-    for (int j = 0; j < WPB; ++j) before += (j < (int) w) ? tw[u * WPB + j] : 0u;
-    const uint32_t base_pref = pre + before;
-    if (sl[u] != 0u) {
-      const uint32_t q = (sl[u] >> 1) & 63u, k = (sl[u] >> 7) & 7u;
-      if (k == 0u) S[q] = base_pref + incl[u] - sv[u];
-      if (sl[u] & (1u << 15)) E[q] = base_pref + incl[u];
-      if (stage_hdr && k < (uint32_t) kHdrChunks) hdr[q * kHdrChunks + k] = make_uint4(vv[u].x, vv[u].y, vv[u].z, vv[u].w);
-    }
-#pragma unroll
-    for (int j = 0; j < WPB; ++j) pre += tw[u * WPB + j];
-  }
-  return pre;
-}
-
-template <int U, bool NT, int WPB>
-__global__ __launch_bounds__(kWave * WPB) void rx_block_kernel(RxParams P) {
-  extern __shared__ uint4 lds_dyn[];
-  const uint32_t w = threadIdx.x / kWave;
-  const uint32_t lane = lane_id();
-  constexpr uint32_t kS = (uint32_t) kWave * WPB;
-  constexpr uint32_t kWin = kS * U;
-
-  RxLdsPtrs L;
-  L.want_rss = P.mode != NICGPU_TUPLE_NONE;
-  L.stage = L.want_rss || P.out_l34 != nullptr;
-  L.hist_lds = P.out_hits != nullptr && P.table_n <= (uint32_t) kHistLds;
-  L.table_lds = L.want_rss && P.table_n <= (uint32_t) kTableLds;
-  uint8_t* b = reinterpret_cast<uint8_t*>(lds_dyn);
-  L.S = reinterpret_cast<uint32_t*>(b);
-  L.E = L.S + kWave;
-  uint8_t* p = b + kWave * 8;
-  L.hdr = reinterpret_cast<uint4*>(p);
-  p += L.stage ? kWave * kHdrChunks * 16 : 0;
-  // scratch: block path = 2 slot windows + 2 x (U x WPB) step totals; general path = per-wave pk + marks
-  L.slotsA = reinterpret_cast<uint32_t*>(p);
-  L.slotsB = L.slotsA + kWin;
-  uint32_t* totA = L.slotsB + kWin;
-  uint32_t* totB = totA + U * WPB;
-  L.pk = reinterpret_cast<uint4*>(p + w * kWave * 16);
-  L.marks = reinterpret_cast<uint32_t*>(p + rx_block_scratch_bytes(U, WPB)) - (WPB - w) * kWave * U;
-  p += rx_block_scratch_bytes(U, WPB);
-  // marks never match a live tag (tags start at 1)
-  for (uint32_t i = lane; i < (uint32_t) (kWave * U); i += kWave) L.marks[i] = 0xFFFFFFFFu;
-  L.lut = reinterpret_cast<uint32_t*>(p);
-  L.hist = L.lut + P.lut_words;
-  L.table_s = reinterpret_cast<uint16_t*>(L.hist + (L.hist_lds ? P.table_n : 0u));
-  uint32_t tag = 0;
-
-  if (L.want_rss) {
-    for (uint32_t i = threadIdx.x; i < P.lut_words; i += kWave * WPB) L.lut[i] = P.lut[i];
-  }
-  if (L.hist_lds) {
-    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) L.hist[i] = 0;
-  }
-  if (L.table_lds) {
-    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) L.table_s[i] = P.table[i];
-  }
-
-  const uint64_t ntiles = (P.n + kWave - 1) / kWave;
-  auto desc_of = [&](uint64_t id) __attribute__((always_inline)) -> uint64_t {
-    return (id < ntiles && id * kWave + lane < P.n) ? P.desc[id * kWave + lane] : 0ull;
-  };
-  uint64_t d_cur = desc_of(blockIdx.x);
-  uint64_t d_next = desc_of(blockIdx.x + gridDim.x);
-
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const Tile t = make_tile<true>(tile, d_cur);
-    d_cur = d_next;
-    d_next = desc_of(tile + 2ull * gridDim.x);
-    __syncthreads();  // previous tile's epilogue is done with S/E/hdr/scratch
-    if (t.contig && t.total != 0u) {
-      for (uint32_t i = threadIdx.x; i < 2 * kWin; i += kWave * WPB) L.slotsA[i] = 0u;
-      __syncthreads();
-      const u32x4* tile16 = reinterpret_cast<const u32x4*>(P.frames) + t.D;
-      ContigBatch<U> A, B;
-      uint32_t run = 0, b0 = 0;
-      plan_block<U, WPB, NT>(A, L.slotsA, 0, t.total, w, lane, t, tile16);
-      __syncthreads();  // A's slots from every wave
-      for (;;) {
-        plan_block<U, WPB, NT>(B, L.slotsB, b0 + kWin, t.total, w, lane, t, tile16);
-        __builtin_amdgcn_sched_barrier(0);
-        run = process_block<U, WPB>(A, L.slotsA, totA, run, L.S, L.E, L.hdr, L.stage, w, lane);
-        if (b0 + kWin >= t.total) break;
-        plan_block<U, WPB, NT>(A, L.slotsA, b0 + 2 * kWin, t.total, w, lane, t, tile16);
-        __builtin_amdgcn_sched_barrier(0);
-        run = process_block<U, WPB>(B, L.slotsB, totB, run, L.S, L.E, L.hdr, L.stage, w, lane);
-        b0 += 2 * kWin;
-        if (b0 >= t.total) break;
-      }
-    } else if (t.total != 0u) {
-      // quarter q = w: packets [16w, 16w + 16) on the general path (others read as empty)
-      constexpr uint32_t kQ = (uint32_t) kWave / WPB;
-      const bool mine = (lane / kQ) == w;
-      const Tile m = make_tile<false>(tile, mine ? (t.off | ((uint64_t) t.len << NICGPU_DESC_OFFSET_BITS)) : 0ull);
-      if (m.total != 0u) run_general_tile<U, NT>(P, L, m, lane, tag);
-    }
-    __syncthreads();  // S/E/hdr of all 64 packets complete
-    {
-      constexpr uint32_t kQ = (uint32_t) kWave / WPB;
-      if ((lane / kQ) == w) {
-        Tile e = t;
-        e.contig = 0u;  // both paths record S at the head and E at the tail
-        tile_epilogue(P, L, e, lane);
-      }
-    }
+    const uint64_t nb = cur.base + step;
+    cur = make_tile<CONTIG>(nb, nvalid_of(nb), d_next);
+    d_next = desc_of(nb + step);
   }
 
   if (L.hist_lds) {
@@ -1031,18 +836,16 @@ struct RxVariant {
   int unroll;
   int wpb;
   const char* name;
-  bool block = false;  // rx_block_kernel (block-cooperative) instead of rx_offload_kernel
+  bool ranges = false;  // balanced per-wave packet ranges (grid sized by packets, not tiles)
 };
 
 const RxVariant kRxVariants[] = {
-    {rx_offload_kernel<2, true, 4, true>, 2, 4, "u2_nt1_w4_c"},
-    {rx_block_kernel<2, true, 4>, 2, 4, "blk_u2_nt1_w4", true},
-    {rx_block_kernel<1, true, 4>, 1, 4, "blk_u1_nt1_w4", true},
-    {rx_block_kernel<4, true, 4>, 4, 4, "blk_u4_nt1_w4", true},
-    {rx_block_kernel<2, true, 8>, 2, 8, "blk_u2_nt1_w8", true},
-    {rx_block_kernel<2, false, 4>, 2, 4, "blk_u2_nt0_w4", true},
-    {rx_block_kernel<1, true, 8>, 1, 8, "blk_u1_nt1_w8", true},
-    {rx_offload_kernel<2, true, 4, false>, 2, 4, "u2_nt1_w4"},
+    {rx_offload_kernel<2, true, 4, true, true>, 2, 4, "u2_nt1_w4_c_r", true},
+    {rx_offload_kernel<2, true, 4, true, false>, 2, 4, "u2_nt1_w4_c"},
+    {rx_offload_kernel<3, true, 4, true, true>, 3, 4, "u3_nt1_w4_c_r", true},
+    {rx_offload_kernel<2, true, 8, true, true>, 2, 8, "u2_nt1_w8_c_r", true},
+    {rx_offload_kernel<1, true, 4, true, true>, 1, 4, "u1_nt1_w4_c_r", true},
+    {rx_offload_kernel<2, true, 4, false, true>, 2, 4, "u2_nt1_w4_r", true},
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
 
@@ -1486,13 +1289,14 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
   const bool stage = rss || P.out_l34 != nullptr;
   const uint32_t hist_n = (P.out_hits && P.table_n <= (uint32_t) kHistLds) ? P.table_n : 0u;
   const uint32_t table_words = (rss && P.table_n <= (uint32_t) kTableLds) ? (P.table_n + 1u) / 2u : 0u;
-  const uint32_t lds = (v.block ? rx_block_lds_bytes(v.wpb, v.unroll, stage, rss ? P.lut_words : 0u, hist_n)
-                                : rx_lds_bytes(v.wpb, v.unroll, stage, rss ? P.lut_words : 0u, hist_n)) +
+  const uint32_t lds = rx_lds_bytes(v.wpb, v.unroll, stage, rss ? P.lut_words : 0u, hist_n) +
                        table_words * 4u;
   int dev = 0;
   (void) hipGetDevice(&dev);
   const uint64_t ntiles = (P.n + kWave - 1) / kWave;
-  const uint64_t want = v.block ? ntiles : (ntiles + v.wpb - 1) / (uint64_t) v.wpb;
+  // ranges: at least 16 packets per wave; round robin: one tile per wave
+  const uint64_t want = v.ranges ? (P.n + 16 * (uint64_t) v.wpb - 1) / (16 * (uint64_t) v.wpb)
+                                 : (ntiles + v.wpb - 1) / (uint64_t) v.wpb;
   const uint64_t cap = (uint64_t) di.cus * (uint64_t) rx_blocks_per_cu(dev, variant, lds);
   const unsigned grid = (unsigned) (want < cap ? want : cap);
   hipLaunchKernelGGL(v.kernel, dim3(grid), dim3(kWave * v.wpb), lds, stream, P);
