@@ -610,18 +610,19 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
   uint32_t run = 0, carry = 0;
   ChunkBatch<U> A, B;
   uint32_t b0 = 0;
+  // counted pair loop, single exit at the bottom (see the contiguous path)
+  const uint32_t nbatch = (t.total + kStep - 1) / kStep;
   plan_batch<U, NT>(A, L.pk, L.marks, b0, t.total, lane, t.start, t.nch, ++tag, carry, P.frames);
-  for (;;) {
+  uint32_t bi = 0;
+  for (; bi + 1 < nbatch; bi += 2, b0 += 2 * kStep) {
     plan_batch<U, NT>(B, L.pk, L.marks, b0 + kStep, t.total, lane, t.start, t.nch, ++tag, carry, P.frames);
     __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's wait
     run = process_batch<U>(A, run, L.S, L.E, L.hdr, L.stage);
-    if (b0 + kStep >= t.total) break;
     plan_batch<U, NT>(A, L.pk, L.marks, b0 + 2 * kStep, t.total, lane, t.start, t.nch, ++tag, carry, P.frames);
     __builtin_amdgcn_sched_barrier(0);
     run = process_batch<U>(B, run, L.S, L.E, L.hdr, L.stage);
-    b0 += 2 * kStep;
-    if (b0 >= t.total) break;
   }
+  if (bi < nbatch) run = process_batch<U>(A, run, L.S, L.E, L.hdr, L.stage);
 }
 
 template <int U, bool NT, int WPB, bool CONTIG, bool RANGES>
@@ -700,20 +701,24 @@ __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
       for (uint32_t i = lane; i < (uint32_t) (2 * kWave * U); i += kWave) L.slotsA[i] = 0u;
       __builtin_amdgcn_wave_barrier();
       const u32x4* tile16 = reinterpret_cast<const u32x4*>(P.frames) + cur.D;
+      // A counted loop over pairs of batches with its only exit at the bottom
+      // (a mid-loop break made the wait-count pass drain vmcnt to 0 at the
+      // loop header); an odd last batch is processed after the loop.  A plan
+      // past the end re-reads the last chunk and sets no slot.
       ContigBatch<U> A, B;
       uint32_t run = 0, b0 = 0;
+      const uint32_t nbatch = (cur.total + kStep - 1) / kStep;
       plan_contig<U, NT>(A, L.slotsA, 0, cur.total, lane, cur.start, cur.nch, cur.info, tile16);
-      for (;;) {
+      uint32_t bi = 0;
+      for (; bi + 1 < nbatch; bi += 2, b0 += 2 * kStep) {
         plan_contig<U, NT>(B, L.slotsB, b0 + kStep, cur.total, lane, cur.start, cur.nch, cur.info, tile16);
         __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's wait
         run = process_contig<U>(A, L.slotsA, run, L.E, L.hdr, L.stage, lane);
-        if (b0 + kStep >= cur.total) break;
         plan_contig<U, NT>(A, L.slotsA, b0 + 2 * kStep, cur.total, lane, cur.start, cur.nch, cur.info, tile16);
         __builtin_amdgcn_sched_barrier(0);
         run = process_contig<U>(B, L.slotsB, run, L.E, L.hdr, L.stage, lane);
-        b0 += 2 * kStep;
-        if (b0 >= cur.total) break;
       }
+      if (bi < nbatch) run = process_contig<U>(A, L.slotsA, run, L.E, L.hdr, L.stage, lane);
     } else if (cur.total != 0u) {
       run_general_tile<U, NT>(P, L, cur, lane, tag);
     }
