@@ -845,12 +845,11 @@ struct RxVariant {
 };
 
 const RxVariant kRxVariants[] = {
-    {rx_offload_kernel<2, true, 4, true, true>, 2, 4, "u2_nt1_w4_c_r", true},
     {rx_offload_kernel<2, true, 4, true, false>, 2, 4, "u2_nt1_w4_c"},
-    {rx_offload_kernel<3, true, 4, true, true>, 3, 4, "u3_nt1_w4_c_r", true},
+    {rx_offload_kernel<2, true, 4, true, true>, 2, 4, "u2_nt1_w4_c_r", true},
+    {rx_offload_kernel<2, true, 8, true, false>, 2, 8, "u2_nt1_w8_c"},
     {rx_offload_kernel<2, true, 8, true, true>, 2, 8, "u2_nt1_w8_c_r", true},
-    {rx_offload_kernel<1, true, 4, true, true>, 1, 4, "u1_nt1_w4_c_r", true},
-    {rx_offload_kernel<2, true, 4, false, true>, 2, 4, "u2_nt1_w4_r", true},
+    {rx_offload_kernel<2, true, 4, false, false>, 2, 4, "u2_nt1_w4"},
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
 
