@@ -175,8 +175,13 @@ __host__ __device__ constexpr uint32_t rx_wave_lds(bool rss, int unroll) {
   return rx_hdr_off(unroll) + (rss ? kWave * kHdrChunks * 16 : 0);
 }
 
+// Byte masks of a 16-B chunk keeping bytes [lo, hi): entry lo * 17 + hi (lo 0..15, hi 0..16).
+constexpr uint32_t kMaskEntries = 16 * 17;
+constexpr uint32_t kMaskFull = 16;  // lo = 0, hi = 16
+constexpr uint32_t kMaskTableBytes = kMaskEntries * 16;
+
 __host__ __device__ inline uint32_t rx_lds_bytes(int wpb, int unroll, bool rss, uint32_t lut_words, uint32_t hist_n) {
-  return (uint32_t) wpb * rx_wave_lds(rss, unroll) + lut_words * 4u + hist_n * 4u;
+  return (uint32_t) wpb * rx_wave_lds(rss, unroll) + kMaskTableBytes + lut_words * 4u + hist_n * 4u;
 }
 
 // One byte of packet l at packet offset o: LDS when staged, else global.
@@ -406,6 +411,9 @@ struct ContigBatch {
   u32x4 v[U];
 };
 
+// Slot word of a contiguous window position that needs packet information:
+//   bit 0 valid | q << 1 (6) | k << 7 (3, 7 = tail beyond the header) |
+//   tail << 10 | mask index << 11 (lo * 17 + hi, kMaskFull for a whole chunk)
 template <int U>
 __device__ __forceinline__ void scatter_slots(uint32_t* slots, uint32_t base, uint32_t lane, uint32_t start,
                                               uint32_t nch, uint32_t info) {
@@ -419,31 +427,35 @@ __device__ __forceinline__ void scatter_slots(uint32_t* slots, uint32_t base, ui
   for (uint32_t j = 0; j < (uint32_t) kHdrChunks; ++j) {
     const uint32_t r = rs + j;
     if (j < nch && r < W) {
-      uint32_t v = common | (j << 7) | (j == 0 ? (lo << 11) : 0u);
-      v |= (j + 1u == nch) ? ((1u << 15) | (hi << 16)) : (16u << 16);
-      slots[r] = v;
+      const bool tail = j + 1u == nch;
+      const uint32_t m = (j == 0 ? lo : 0u) * 17u + (tail ? hi : 16u);
+      slots[r] = common | (j << 7) | (tail ? (1u << 10) : 0u) | (m << 11);
     }
   }
-  if (nch > (uint32_t) kHdrChunks && re < W) slots[re] = common | (7u << 7) | (1u << 15) | (hi << 16);
+  if (nch > (uint32_t) kHdrChunks && re < W) slots[re] = common | (7u << 7) | (1u << 10) | (hi << 11);
 }
 
+// The tile's chunks through a buffer resource (base = the tile's first chunk,
+// num_records = its bytes): lane offset lane * 16 is fixed, the batch offset
+// is scalar and the step offset an immediate, so a load costs no VALU, and
+// positions past the tile end read zeros (they carry no slot either).
 template <int U, bool NT>
-__device__ __forceinline__ void plan_contig(ContigBatch<U>& B, uint32_t* slots, uint32_t base, uint32_t total,
-                                            uint32_t lane, uint32_t start, uint32_t nch, uint32_t info,
-                                            const u32x4* __restrict__ tile16) {
+__device__ __forceinline__ void plan_contig(ContigBatch<U>& B, uint32_t* slots, uint32_t base, uint32_t lane,
+                                            uint32_t start, uint32_t nch, uint32_t info,
+                                            __amdgpu_buffer_rsrc_t rsrc) {
   scatter_slots<U>(slots, base, lane, start, nch, info);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const uint32_t c = base + (uint32_t) u * kWave + lane;
-    const uint32_t ce = c < total ? c : total - 1u;
-    if constexpr (NT) B.v[u] = __builtin_nontemporal_load(tile16 + ce);
-    else B.v[u] = tile16[ce];
+    const uint32_t vo = lane * 16u + (uint32_t) u * (kWave * 16u);
+    B.v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int) vo, (int) (base * 16u),
+                                                                            NT ? 2 : 0));
   }
 }
 
 template <int U>
-__device__ __forceinline__ uint32_t process_contig(ContigBatch<U>& B, uint32_t* slots, uint32_t run, uint32_t* E,
-                                                   uint4* hdr, bool stage_hdr, uint32_t lane) {
+__device__ __forceinline__ uint32_t process_contig(ContigBatch<U>& B, uint32_t* slots, const uint4* masks,
+                                                   uint32_t run, uint32_t* E, uint4* hdr, bool stage_hdr,
+                                                   uint32_t lane) {
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -451,12 +463,13 @@ __device__ __forceinline__ uint32_t process_contig(ContigBatch<U>& B, uint32_t* 
     u32x4 v = B.v[u];
     if (sl != 0u) {
       slots[u * kWave + lane] = 0u;
-      const int lo = (int) ((sl >> 11) & 15u), hi = (int) ((sl >> 16) & 31u);
-      if (lo != 0 || hi != 16) {
-        v.x &= dword_keep(lo, hi, 0);
-        v.y &= dword_keep(lo, hi, 1);
-        v.z &= dword_keep(lo, hi, 2);
-        v.w &= dword_keep(lo, hi, 3);
+      const uint32_t mi = sl >> 11;
+      if (mi != kMaskFull) {
+        const uint4 m = masks[mi];
+        v.x &= m.x;
+        v.y &= m.y;
+        v.z &= m.z;
+        v.w &= m.w;
       }
     }
     const uint32_t s = add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, 0u))));
@@ -464,7 +477,7 @@ __device__ __forceinline__ uint32_t process_contig(ContigBatch<U>& B, uint32_t* 
     const uint32_t step_total = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
     if (sl != 0u) {
       const uint32_t q = (sl >> 1) & 63u, k = (sl >> 7) & 7u;
-      if (sl & (1u << 15)) E[q] = run + incl;
+      if (sl & (1u << 10)) E[q] = run + incl;
       if (stage_hdr && k < (uint32_t) kHdrChunks) hdr[q * kHdrChunks + k] = make_uint4(v.x, v.y, v.z, v.w);
     }
     run += step_total;
@@ -554,6 +567,7 @@ struct RxLdsPtrs {
   uint32_t* lut;
   uint32_t* hist;
   uint16_t* table_s;
+  const uint4* masks;  // kMaskEntries byte masks (per block)
   bool hist_lds, table_lds, want_rss;
   bool stage;  // first 64 B of every packet staged in LDS (hashing or L3/L4 verify)
 };
@@ -646,13 +660,19 @@ __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
   L.slotsA = reinterpret_cast<uint32_t*>(wave_b + kScratchOff);
   L.slotsB = L.slotsA + kWave * U;
   L.hdr = reinterpret_cast<uint4*>(wave_b + rx_hdr_off(U));
-  L.lut = reinterpret_cast<uint32_t*>(base_b + (uint32_t) WPB * rx_wave_lds(L.stage, U));
+  uint4* masks_w = reinterpret_cast<uint4*>(base_b + (uint32_t) WPB * rx_wave_lds(L.stage, U));
+  L.masks = masks_w;
+  L.lut = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(masks_w) + kMaskTableBytes);
   L.hist = L.lut + P.lut_words;
   L.table_s = reinterpret_cast<uint16_t*>(L.hist + (L.hist_lds ? P.table_n : 0u));
   // marks never match a live tag (tags start at 1; cleared slots read as 0)
   for (uint32_t i = lane; i < (uint32_t) (kWave * U); i += kWave) L.marks[i] = 0xFFFFFFFFu;
   uint32_t tag = 0;  // batch id of the general path (never reaches 0x3FFFFFF within a launch)
 
+  for (uint32_t i = threadIdx.x; i < kMaskEntries; i += kWave * WPB) {
+    const int lo = (int) (i / 17u), hi = (int) (i % 17u);
+    masks_w[i] = make_uint4(dword_keep(lo, hi, 0), dword_keep(lo, hi, 1), dword_keep(lo, hi, 2), dword_keep(lo, hi, 3));
+  }
   if (L.want_rss) {
     for (uint32_t i = threadIdx.x; i < P.lut_words; i += kWave * WPB) L.lut[i] = P.lut[i];
   }
@@ -696,29 +716,34 @@ __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
     if (cur.contig && cur.total != 0u) {
       // Contiguous tile: chunk c is absolute chunk D + c.  Ping-pong: batch
       // i+1's loads are in flight while batch i is reduced; every plan is
-      // unconditional (a batch past the end re-reads the last chunk) so the
-      // compiler keeps counted vmcnt waits instead of draining at merges.
+      // unconditional (positions past the end read zeros through the buffer
+      // bounds check) so the compiler keeps counted vmcnt waits.
       for (uint32_t i = lane; i < (uint32_t) (2 * kWave * U); i += kWave) L.slotsA[i] = 0u;
       __builtin_amdgcn_wave_barrier();
-      const u32x4* tile16 = reinterpret_cast<const u32x4*>(P.frames) + cur.D;
+      // wave-uniform descriptor inputs (readfirstlane: provably scalar)
+      const uint64_t tb = reinterpret_cast<uint64_t>(P.frames) + (uint64_t) cur.D * 16u;
+      const uint32_t tb_lo = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) tb);
+      const uint32_t tb_hi = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) (tb >> 32));
+      const uint32_t tbytes = (uint32_t) __builtin_amdgcn_readfirstlane((int) (cur.total * 16u));
+      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<void*>(((uint64_t) tb_hi << 32) | tb_lo), (short) 0, (int) tbytes, 0x00020000);
       // A counted loop over pairs of batches with its only exit at the bottom
       // (a mid-loop break made the wait-count pass drain vmcnt to 0 at the
-      // loop header); an odd last batch is processed after the loop.  A plan
-      // past the end re-reads the last chunk and sets no slot.
+      // loop header); an odd last batch is processed after the loop.
       ContigBatch<U> A, B;
       uint32_t run = 0, b0 = 0;
       const uint32_t nbatch = (cur.total + kStep - 1) / kStep;
-      plan_contig<U, NT>(A, L.slotsA, 0, cur.total, lane, cur.start, cur.nch, cur.info, tile16);
+      plan_contig<U, NT>(A, L.slotsA, 0, lane, cur.start, cur.nch, cur.info, rsrc);
       uint32_t bi = 0;
       for (; bi + 1 < nbatch; bi += 2, b0 += 2 * kStep) {
-        plan_contig<U, NT>(B, L.slotsB, b0 + kStep, cur.total, lane, cur.start, cur.nch, cur.info, tile16);
+        plan_contig<U, NT>(B, L.slotsB, b0 + kStep, lane, cur.start, cur.nch, cur.info, rsrc);
         __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's wait
-        run = process_contig<U>(A, L.slotsA, run, L.E, L.hdr, L.stage, lane);
-        plan_contig<U, NT>(A, L.slotsA, b0 + 2 * kStep, cur.total, lane, cur.start, cur.nch, cur.info, tile16);
+        run = process_contig<U>(A, L.slotsA, L.masks, run, L.E, L.hdr, L.stage, lane);
+        plan_contig<U, NT>(A, L.slotsA, b0 + 2 * kStep, lane, cur.start, cur.nch, cur.info, rsrc);
         __builtin_amdgcn_sched_barrier(0);
-        run = process_contig<U>(B, L.slotsB, run, L.E, L.hdr, L.stage, lane);
+        run = process_contig<U>(B, L.slotsB, L.masks, run, L.E, L.hdr, L.stage, lane);
       }
-      if (bi < nbatch) run = process_contig<U>(A, L.slotsA, run, L.E, L.hdr, L.stage, lane);
+      if (bi < nbatch) run = process_contig<U>(A, L.slotsA, L.masks, run, L.E, L.hdr, L.stage, lane);
     } else if (cur.total != 0u) {
       run_general_tile<U, NT>(P, L, cur, lane, tag);
     }

@@ -26,10 +26,10 @@ def main():
     print(name)
     for a, b in sorted(loops):
         ins = [body[x].strip() for x in range(a, b + 1)]
-        loads = sum(1 for x in ins if x.startswith("global_load"))
+        loads = sum(1 for x in ins if x.startswith(("global_load", "buffer_load")))
         waits = [x.split(";")[0].strip() for x in ins if x.startswith("s_waitcnt") and "vmcnt" in x]
         nins = sum(1 for x in ins if x and not x.startswith((";", ".")))
-        print(f"  loop {body[a].split(':')[0]} lines {a}-{b} instr {nins} global_loads {loads} vm_waits {waits}")
+        print(f"  loop {body[a].split(':')[0]} lines {a}-{b} instr {nins} vmem_loads {loads} vm_waits {waits}")
 
 
 if __name__ == "__main__":
