@@ -175,9 +175,11 @@ __host__ __device__ constexpr uint32_t rx_wave_lds(bool rss, int unroll) {
   return rx_hdr_off(unroll) + (rss ? kWave * kHdrChunks * 16 : 0);
 }
 
-// Byte masks of a 16-B chunk keeping bytes [lo, hi): entry lo * 17 + hi (lo 0..15, hi 0..16).
-constexpr uint32_t kMaskEntries = 16 * 17;
-constexpr uint32_t kMaskFull = 16;  // lo = 0, hi = 16
+// Byte masks of a 16-B chunk: entries 0..15 keep bytes >= lo, entries 16..32
+// keep bytes < hi (hi = entry - 16); a chunk's mask is their AND.  Two small
+// tables (528 B) instead of one lo x hi table keep a 4-wave block under 32 KiB
+// of LDS, so 5 blocks fit a CU.
+constexpr uint32_t kMaskEntries = 16 + 17;
 constexpr uint32_t kMaskTableBytes = kMaskEntries * 16;
 
 __host__ __device__ inline uint32_t rx_lds_bytes(int wpb, int unroll, bool rss, uint32_t lut_words, uint32_t hist_n) {
@@ -413,7 +415,7 @@ struct ContigBatch {
 
 // Slot word of a contiguous window position that needs packet information:
 //   bit 0 valid | q << 1 (6) | k << 7 (3, 7 = tail beyond the header) |
-//   tail << 10 | mask index << 11 (lo * 17 + hi, kMaskFull for a whole chunk)
+//   tail << 10 | lo << 11 (4) | hi << 15 (5); lo = 0, hi = 16 is a whole chunk
 template <int U>
 __device__ __forceinline__ void scatter_slots(uint32_t* slots, uint32_t base, uint32_t lane, uint32_t start,
                                               uint32_t nch, uint32_t info) {
@@ -428,11 +430,10 @@ __device__ __forceinline__ void scatter_slots(uint32_t* slots, uint32_t base, ui
     const uint32_t r = rs + j;
     if (j < nch && r < W) {
       const bool tail = j + 1u == nch;
-      const uint32_t m = (j == 0 ? lo : 0u) * 17u + (tail ? hi : 16u);
-      slots[r] = common | (j << 7) | (tail ? (1u << 10) : 0u) | (m << 11);
+      slots[r] = common | (j << 7) | (tail ? (1u << 10) : 0u) | ((j == 0 ? lo : 0u) << 11) | ((tail ? hi : 16u) << 15);
     }
   }
-  if (nch > (uint32_t) kHdrChunks && re < W) slots[re] = common | (7u << 7) | (1u << 10) | (hi << 11);
+  if (nch > (uint32_t) kHdrChunks && re < W) slots[re] = common | (7u << 7) | (1u << 10) | (hi << 15);
 }
 
 // The tile's chunks through a buffer resource (base = the tile's first chunk,
@@ -463,13 +464,13 @@ __device__ __forceinline__ uint32_t process_contig(ContigBatch<U>& B, uint32_t* 
     u32x4 v = B.v[u];
     if (sl != 0u) {
       slots[u * kWave + lane] = 0u;
-      const uint32_t mi = sl >> 11;
-      if (mi != kMaskFull) {
-        const uint4 m = masks[mi];
-        v.x &= m.x;
-        v.y &= m.y;
-        v.z &= m.z;
-        v.w &= m.w;
+      const uint32_t mi = sl >> 11;  // lo | hi << 4
+      if (mi != (16u << 4)) {
+        const uint4 a = masks[mi & 15u], b = masks[16u + (mi >> 4)];
+        v.x &= a.x & b.x;
+        v.y &= a.y & b.y;
+        v.z &= a.z & b.z;
+        v.w &= a.w & b.w;
       }
     }
     const uint32_t s = add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, 0u))));
@@ -639,8 +640,9 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
   if (bi < nbatch) run = process_batch<U>(A, run, L.S, L.E, L.hdr, L.stage);
 }
 
-template <int U, bool NT, int WPB, bool CONTIG, bool RANGES>
-__global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
+template <int U, bool NT, int WPB, bool CONTIG, bool RANGES, int OCC>
+__global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void rx_offload_kernel(
+    RxParams P) {
   extern __shared__ uint4 lds_dyn[];
   const int w = threadIdx.x / kWave;
   const uint32_t lane = lane_id();
@@ -670,7 +672,7 @@ __global__ __launch_bounds__(kWave * WPB) void rx_offload_kernel(RxParams P) {
   uint32_t tag = 0;  // batch id of the general path (never reaches 0x3FFFFFF within a launch)
 
   for (uint32_t i = threadIdx.x; i < kMaskEntries; i += kWave * WPB) {
-    const int lo = (int) (i / 17u), hi = (int) (i % 17u);
+    const int lo = i < 16u ? (int) i : 0, hi = i < 16u ? 16 : (int) i - 16;
     masks_w[i] = make_uint4(dword_keep(lo, hi, 0), dword_keep(lo, hi, 1), dword_keep(lo, hi, 2), dword_keep(lo, hi, 3));
   }
   if (L.want_rss) {
@@ -870,11 +872,11 @@ struct RxVariant {
 };
 
 const RxVariant kRxVariants[] = {
-    {rx_offload_kernel<2, true, 4, true, false>, 2, 4, "u2_nt1_w4_c"},
-    {rx_offload_kernel<2, true, 4, true, true>, 2, 4, "u2_nt1_w4_c_r", true},
-    {rx_offload_kernel<2, true, 8, true, false>, 2, 8, "u2_nt1_w8_c"},
-    {rx_offload_kernel<2, true, 8, true, true>, 2, 8, "u2_nt1_w8_c_r", true},
-    {rx_offload_kernel<2, true, 4, false, false>, 2, 4, "u2_nt1_w4"},
+    {rx_offload_kernel<2, true, 4, true, false, 1>, 2, 4, "u2_nt1_w4_c"},
+    {rx_offload_kernel<2, true, 4, true, false, 5>, 2, 4, "u2_nt1_w4_c_o5"},
+    {rx_offload_kernel<2, true, 8, true, false, 5>, 2, 8, "u2_nt1_w8_c_o5"},
+    {rx_offload_kernel<2, true, 8, true, false, 1>, 2, 8, "u2_nt1_w8_c"},
+    {rx_offload_kernel<2, true, 4, false, false, 1>, 2, 4, "u2_nt1_w4"},
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
 
