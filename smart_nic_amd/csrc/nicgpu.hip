@@ -42,6 +42,7 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kHdrChunks = 4;      // 64 B of each packet staged in LDS
 constexpr int kHdrBytes = kHdrChunks * 16;
+constexpr uint32_t kHdrStride = kHdrChunks + 1;  // LDS uint4 slots per staged packet (see hdr_slot)
 constexpr int kLutPos = 2 * NICGPU_MAX_TUPLE;  // nibble positions
 constexpr int kLutWords = kLutPos * 16;
 constexpr int kHistLds = 1024;     // tables up to this size histogram in LDS
@@ -50,6 +51,8 @@ constexpr uint64_t kOffMask = (1ull << NICGPU_DESC_OFFSET_BITS) - 1;
 
 const uint8_t kDefaultKey[20] = {0x6D, 0x5A, 0x56, 0x6B, 0x65, 0x4E, 0x67, 0x6E, 0x67, 0x55,
                                  0x6A, 0x6B, 0x61, 0x4F, 0x6B, 0x65, 0x6F, 0x49, 0x4D, 0x42};
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------ wave helpers --
 // Inclusive prefix sum over the 64 lanes (Hillis-Steele inside 16-lane rows by
@@ -154,10 +157,25 @@ struct RxParams {
   uint16_t* out_queue;
   unsigned long long* out_hits;
   uint8_t* out_l34;  // NICGPU_L34_* flags (L3/L4 checksum verification), may be null
+  uint32_t dbg;      // tuning builds only (kDbg*): switch parts of the RSS work off to attribute its cost
 };
 
+// Tuning-only knobs (libnicgpu_tune.so; outputs are wrong with any set).
+constexpr uint32_t kDbgNoStage = 1, kDbgNoHash = 2, kDbgNoStore = 4, kDbgNoHist = 8, kDbgNtStore = 16,
+                   kDbgNoHashStore = 32, kDbgNoQueueStore = 64, kDbgNoTable = 128, kDbgSmallOut = 256, kDbgBurstOut = 512,
+                   kDbgStoreSc = 1024 | 2048 | 4096;
+__device__ __forceinline__ bool dbg_on(const RxParams& P, uint32_t bit) {
+#ifdef NICGPU_TUNING
+  return (P.dbg & bit) != 0u;
+#else
+  (void) P;
+  (void) bit;
+  return false;
+#endif
+}
+
 // Dynamic LDS layout (sized per launch by rx_lds_bytes):
-//   per wave: S[64] | E[64] | scratch | hdr[64][kHdrChunks] uint4 (only when hashing)
+//   per wave: S[64] | E[64] | scratch | hdr[64][kHdrStride] uint4 (only when hashing)
 //     scratch = general path: pk[64] uint4 {delta lo, delta hi, end, info} + marks[64 U]
 //               contiguous path: two slot windows of 64 U words (ping-pong)
 //   per block: lut[lut_words] | hist[hist_n]
@@ -172,7 +190,7 @@ __host__ __device__ constexpr uint32_t rx_scratch_bytes(int unroll) {
 __host__ __device__ constexpr uint32_t rx_hdr_off(int unroll) { return kScratchOff + rx_scratch_bytes(unroll); }
 
 __host__ __device__ constexpr uint32_t rx_wave_lds(bool rss, int unroll) {
-  return rx_hdr_off(unroll) + (rss ? kWave * kHdrChunks * 16 : 0);
+  return rx_hdr_off(unroll) + (rss ? kWave * kHdrStride * 16 : 0);
 }
 
 // Byte masks of a 16-B chunk: entries 0..15 keep bytes >= lo, entries 16..32
@@ -186,15 +204,54 @@ __host__ __device__ inline uint32_t rx_lds_bytes(int wpb, int unroll, bool rss, 
   return (uint32_t) wpb * rx_wave_lds(rss, unroll) + kMaskTableBytes + lut_words * 4u + hist_n * 4u;
 }
 
+// Header stage of one wave: chunk k (0..3) of the packet in lane q lives in
+// slot q*5 + k (80-B packet stride, 16 B of padding).  A wave's ds_read_b128
+// of one chunk index is then conflict-free: lanes are served in 16-lane
+// groups ({0-3,12-15,20-27}, ...) and 20*q mod 64 takes 16 distinct values on
+// each group, covering all 64 banks once; dword and byte reads are 4-way
+// instead of 16-way (MI355X_MICROARCH.md §LDS).  With a 64-B stride every
+// dword read of the epilogue was a 16-way conflict (SQ_LDS_BANK_CONFLICT:
+// ~190 cycles per 64-packet tile).  A padded stride keeps every chunk at an
+// immediate offset from the lane's base, unlike an XOR swizzle, which cost
+// hipcc ~100 VGPRs of hoisted addresses.
+__device__ __forceinline__ uint32_t hdr_slot(uint32_t q, uint32_t k) { return q * kHdrStride + k; }
+
+struct HdrView {
+  const uint4* hdr;  // the wave's stage
+  uint32_t q;        // this lane's packet
+  __device__ __forceinline__ uint32_t byte(uint32_t a) const {
+    return reinterpret_cast<const uint8_t*>(hdr + hdr_slot(q, a >> 4))[a & 15u];
+  }
+  __device__ __forceinline__ uint32_t word(uint32_t k) const {
+    return reinterpret_cast<const uint32_t*>(hdr + hdr_slot(q, k >> 2))[k & 3u];
+  }
+  // chunks 0..2 as three ds_read_b128 (hipcc would otherwise split them into
+  // the few dword reads it needs, which are 4-way conflicted even swizzled)
+  __device__ __forceinline__ void chunks3(u32x4& c0, u32x4& c1, u32x4& c2) const {
+    typedef __attribute__((address_space(3))) const uint4* lds_ptr;
+    const uint32_t a0 = (uint32_t) (uintptr_t) (lds_ptr) (hdr + hdr_slot(q, 0));
+    const uint32_t a1 = (uint32_t) (uintptr_t) (lds_ptr) (hdr + hdr_slot(q, 1));
+    const uint32_t a2 = (uint32_t) (uintptr_t) (lds_ptr) (hdr + hdr_slot(q, 2));
+    asm volatile(
+        "ds_read_b128 %0, %3\n\t"
+        "ds_read_b128 %1, %4\n\t"
+        "ds_read_b128 %2, %5\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(c0), "=&v"(c1), "=&v"(c2)
+        : "v"(a0), "v"(a1), "v"(a2)
+        : "memory");
+  }
+};
+
 // One byte of packet l at packet offset o: LDS when staged, else global.
-__device__ __forceinline__ uint32_t pkt_byte(const uint4* hdr_l, uint32_t lo, const uint8_t* __restrict__ pkt,
+__device__ __forceinline__ uint32_t pkt_byte(const HdrView& hv, uint32_t lo, const uint8_t* __restrict__ pkt,
                                              uint32_t o) {
   uint32_t a = lo + o;
-  if (a < (uint32_t) kHdrBytes) return reinterpret_cast<const uint8_t*>(hdr_l)[a];
+  if (a < (uint32_t) kHdrBytes) return hv.byte(a);
   return pkt[o];
 }
 
-__device__ __forceinline__ uint32_t hash_bytes(uint32_t h, const uint32_t* lut, const uint4* hdr_l, uint32_t lo,
+__device__ __forceinline__ uint32_t hash_bytes(uint32_t h, const uint32_t* lut, const HdrView& hdr_l, uint32_t lo,
                                                const uint8_t* __restrict__ pkt, uint32_t src, uint32_t cnt,
                                                uint32_t pos) {
   for (uint32_t i = 0; i < cnt; ++i) {
@@ -210,13 +267,13 @@ __device__ __forceinline__ uint32_t hash_bytes(uint32_t h, const uint32_t* lut, 
 // window comes from the LDS header stage (k < 16) or from global memory.  The
 // same convention as the streamed chunk sums, so sub-range sums subtract
 // exactly from the packet's total.
-__device__ __forceinline__ uint32_t range_sum_le(const uint32_t* stage_w, const uint32_t* __restrict__ glob_w,
+__device__ __forceinline__ uint32_t range_sum_le(const HdrView& stage_w, const uint32_t* __restrict__ glob_w,
                                                  uint32_t lo, uint32_t a, uint32_t b) {
   uint32_t s = 0;
   if (a >= b) return 0;
   const uint32_t pa = lo + a, pb = lo + b;
   for (uint32_t k = pa >> 2; 4 * k < pb; ++k) {
-    uint32_t v = k < (uint32_t) (kHdrBytes / 4) ? stage_w[k] : glob_w[k];
+    uint32_t v = k < (uint32_t) (kHdrBytes / 4) ? stage_w.word(k) : glob_w[k];
     const uint32_t w0 = 4 * k;
     const uint32_t first = pa > w0 ? pa - w0 : 0u;      // bytes of this word before the range
     const uint32_t last = pb < w0 + 4 ? pb - w0 : 4u;   // bytes of this word inside the range end
@@ -232,13 +289,12 @@ __device__ __forceinline__ uint32_t range_sum_le(const uint32_t* stage_w, const 
 // packet's streamed halfword sum; the L4 segment's sum is that minus the bytes
 // before the segment and after the IP datagram, so no byte is read twice
 // except the <= 82 header bytes (from the LDS stage) and any trailer.
-__device__ uint32_t l34_flags(const uint32_t* stage_w, const uint32_t* __restrict__ glob_w, uint32_t lo, uint32_t len,
+__device__ uint32_t l34_flags(const HdrView& stage_w, const uint32_t* __restrict__ glob_w, uint32_t lo, uint32_t len,
                               uint32_t sum_le) {
-  const uint8_t* stage_b = reinterpret_cast<const uint8_t*>(stage_w);
   const uint8_t* glob_b = reinterpret_cast<const uint8_t*>(glob_w);
   auto B = [&](uint32_t o) -> uint32_t {
     const uint32_t a = lo + o;
-    return a < (uint32_t) kHdrBytes ? stage_b[a] : glob_b[a];
+    return a < (uint32_t) kHdrBytes ? stage_w.byte(a) : glob_b[a];
   };
   if (len < 14u) return 0;
   uint32_t l3 = 14;
@@ -278,7 +334,7 @@ __device__ uint32_t l34_flags(const uint32_t* stage_w, const uint32_t* __restric
 }
 
 // Tuple extraction + Toeplitz for one packet (oracle/oracle.c oracle_extract_tuple).
-__device__ __forceinline__ uint32_t rss_hash_packet(const RxParams& P, const uint32_t* lut, const uint4* hdr_l,
+__device__ __forceinline__ uint32_t rss_hash_packet(const RxParams& P, const uint32_t* lut, const HdrView& hdr_l,
                                                     uint32_t lo, const uint8_t* __restrict__ pkt, uint32_t len) {
   uint32_t h = 0;
   if (P.mode == NICGPU_TUPLE_RAW) {
@@ -294,7 +350,8 @@ __device__ __forceinline__ uint32_t rss_hash_packet(const RxParams& P, const uin
     // Fast path: 16-B-aligned frame, Eth (no tag) / IPv4 IHL 5 / TCP|UDP, not a
     // fragment — the first 48 bytes come from LDS in three 16-B reads and the
     // fields are extracted at constant shifts.
-    const uint4 c0 = hdr_l[0], c1 = hdr_l[1], c2 = hdr_l[2];
+    u32x4 c0, c1, c2;
+    hdr_l.chunks3(c0, c1, c2);
     const uint32_t w3 = c0.w;  // bytes 12..15: ethertype | ver/ihl | tos
     const uint32_t w5 = c1.y;  // bytes 20..23: flags/frag | ttl | proto
     const uint32_t proto = w5 >> 24;
@@ -342,7 +399,6 @@ __device__ __forceinline__ uint32_t rss_hash_packet(const RxParams& P, const uin
   return h;
 }
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // A batch of U chunk loads per lane: chunk c = base + 64u + lane.
 template <int U>
@@ -440,7 +496,7 @@ __device__ __forceinline__ void scatter_slots(uint32_t* slots, uint32_t base, ui
 // num_records = its bytes): lane offset lane * 16 is fixed, the batch offset
 // is scalar and the step offset an immediate, so a load costs no VALU, and
 // positions past the tile end read zeros (they carry no slot either).
-template <int U, bool NT>
+template <int U, int CP>
 __device__ __forceinline__ void plan_contig(ContigBatch<U>& B, uint32_t* slots, uint32_t base, uint32_t lane,
                                             uint32_t start, uint32_t nch, uint32_t info,
                                             __amdgpu_buffer_rsrc_t rsrc) {
@@ -449,7 +505,7 @@ __device__ __forceinline__ void plan_contig(ContigBatch<U>& B, uint32_t* slots, 
   for (int u = 0; u < U; ++u) {
     const uint32_t vo = lane * 16u + (uint32_t) u * (kWave * 16u);
     B.v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int) vo, (int) (base * 16u),
-                                                                            NT ? 2 : 0));
+                                                                            CP));
   }
 }
 
@@ -479,7 +535,7 @@ __device__ __forceinline__ uint32_t process_contig(ContigBatch<U>& B, uint32_t* 
     if (sl != 0u) {
       const uint32_t q = (sl >> 1) & 63u, k = (sl >> 7) & 7u;
       if (sl & (1u << 10)) E[q] = run + incl;
-      if (stage_hdr && k < (uint32_t) kHdrChunks) hdr[q * kHdrChunks + k] = make_uint4(v.x, v.y, v.z, v.w);
+      if (stage_hdr && k < (uint32_t) kHdrChunks) hdr[hdr_slot(q, k)] = make_uint4(v.x, v.y, v.z, v.w);
     }
     run += step_total;
   }
@@ -510,7 +566,7 @@ __device__ __forceinline__ uint32_t process_batch(ChunkBatch<U>& B, uint32_t run
       if (m & (1u << 9)) S[q] = run + incl - s;
       if (m & (1u << 10)) E[q] = run + incl;
       const uint32_t slot = m >> 12;
-      if (stage_hdr && slot < (uint32_t) kHdrChunks) hdr[q * kHdrChunks + slot] = make_uint4(v.x, v.y, v.z, v.w);
+      if (stage_hdr && slot < (uint32_t) kHdrChunks) hdr[hdr_slot(q, slot)] = make_uint4(v.x, v.y, v.z, v.w);
     }
     run += step_total;
   }
@@ -573,11 +629,121 @@ struct RxLdsPtrs {
   bool stage;  // first 64 B of every packet staged in LDS (hashing or L3/L4 verify)
 };
 
-// Checksum finish + tuple hash + queue of the tile's packets (one per lane).
-__device__ __forceinline__ void tile_epilogue(const RxParams& P, const RxLdsPtrs& L, const Tile& t, uint32_t lane) {
+// One lane's results of a tile, held in registers so that (DEFER) they are
+// stored only after the next tile's first loads are in flight: on gfx950
+// stores count in vmcnt and complete in order with loads, so stores issued
+// just before a tile's first loads made the first counted wait of every tile
+// also wait for the previous tile's store acknowledgements (tools/tune_rx.py
+// --dbg: without the hash/queue stores C2 ran 16 µs faster, IMIX 29 µs).
+struct TileOut {
+  uint64_t pid;
+  uint32_t cs, h, q, l34;
+  uint32_t valid;  // lane < nvalid
+};
+
+// SST: cache-policy bits of the result stores (0 = plain global stores; 16 =
+// sc1 buffer stores, device scope).
+template <int SST>
+__device__ __forceinline__ void store_out(const RxParams& P, const TileOut& o, bool rss) {
+  if (SST != 0) {
+    if (o.valid) {
+      // per-tile resources: base = this tile's first output, offset = lane
+      const uint32_t l = (uint32_t) (o.pid & 63u);
+      const uint64_t tb = o.pid - l;
+      if (P.out_csum)
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t) o.cs,
+                                              __builtin_amdgcn_make_buffer_rsrc(P.out_csum + tb, (short) 0, 128, 0x00020000),
+                                              (int) (l * 2u), 0, SST);
+      if (P.out_l34) P.out_l34[o.pid] = (uint8_t) o.l34;
+      if (rss) {
+        if (P.out_hash)
+          __builtin_amdgcn_raw_buffer_store_b32(o.h,
+                                                __builtin_amdgcn_make_buffer_rsrc(P.out_hash + tb, (short) 0, 256, 0x00020000),
+                                                (int) (l * 4u), 0, SST);
+        if (P.out_queue)
+          __builtin_amdgcn_raw_buffer_store_b16((uint16_t) o.q,
+                                                __builtin_amdgcn_make_buffer_rsrc(P.out_queue + tb, (short) 0, 128, 0x00020000),
+                                                (int) (l * 2u), 0, SST);
+      }
+    }
+    return;
+  }
+  if (dbg_on(P, kDbgNtStore)) {
+    if (o.valid) {
+      if (P.out_csum) __builtin_nontemporal_store((uint16_t) o.cs, P.out_csum + o.pid);
+      if (rss) {
+        if (P.out_hash) __builtin_nontemporal_store(o.h, P.out_hash + o.pid);
+        if (P.out_queue) __builtin_nontemporal_store((uint16_t) o.q, P.out_queue + o.pid);
+      }
+    }
+    return;
+  }
+  if (dbg_on(P, kDbgStoreSc)) {  // cache-policy experiment on the three output stores
+    if (o.valid) {
+      const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(P.out_csum, (short) 0, 0x7FFFFFFF, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(P.out_hash, (short) 0, 0x7FFFFFFF, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(P.out_queue, (short) 0, 0x7FFFFFFF, 0x00020000);
+      const int off2 = (int) (o.pid * 2), off4 = (int) (o.pid * 4);
+      if (P.dbg & 1024) {
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t) o.cs, rc, off2, 0, 17);
+        __builtin_amdgcn_raw_buffer_store_b32(o.h, rh, off4, 0, 17);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t) o.q, rq, off2, 0, 17);
+      } else if (P.dbg & 2048) {
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t) o.cs, rc, off2, 0, 18);
+        __builtin_amdgcn_raw_buffer_store_b32(o.h, rh, off4, 0, 18);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t) o.q, rq, off2, 0, 18);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t) o.cs, rc, off2, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(o.h, rh, off4, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t) o.q, rq, off2, 0, 16);
+      }
+    }
+    return;
+  }
+  if (dbg_on(P, kDbgBurstOut)) {  // same bytes, written as 4-tile (1 KiB hash) bursts by every 4th tile's wave
+    if (((o.pid >> 6) & 3u) == 3u) {
+      const uint64_t b = (o.pid & ~255ull) + (o.pid & 63u);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (P.out_csum) P.out_csum[b + 64 * j] = (uint16_t) o.cs;
+        if (rss) {
+          if (P.out_hash) P.out_hash[b + 64 * j] = o.h;
+          if (P.out_queue) P.out_queue[b + 64 * j] = (uint16_t) o.q;
+        }
+      }
+    }
+    return;
+  }
+  if (dbg_on(P, kDbgSmallOut)) {  // same stores, into a 64 KiB window (L2-resident): write path vs DRAM
+    const uint64_t w = o.pid & 16383u;
+    if (o.valid) {
+      if (P.out_csum) P.out_csum[w] = (uint16_t) o.cs;
+      if (rss) {
+        if (P.out_hash) P.out_hash[w] = o.h;
+        if (P.out_queue) P.out_queue[w] = (uint16_t) o.q;
+      }
+    }
+    return;
+  }
+  if (o.valid) {
+    if (P.out_csum) P.out_csum[o.pid] = (uint16_t) o.cs;
+    if (P.out_l34) P.out_l34[o.pid] = (uint8_t) o.l34;
+    if (rss && !dbg_on(P, kDbgNoStore)) {
+      if (P.out_hash && !dbg_on(P, kDbgNoHashStore)) P.out_hash[o.pid] = o.h;
+      if (P.out_queue && !dbg_on(P, kDbgNoQueueStore)) P.out_queue[o.pid] = (uint16_t) o.q;
+    }
+  }
+}
+
+// Checksum finish + tuple hash + queue of the tile's packets (one per lane);
+// the hit histogram is updated here (LDS), the outputs are returned.
+__device__ __forceinline__ TileOut tile_epilogue(const RxParams& P, const RxLdsPtrs& L, const Tile& t, uint32_t lane) {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  const uint64_t pid = t.base + lane;
+  TileOut o;
+  o.pid = t.base + lane;
+  o.cs = o.h = o.q = o.l34 = 0;
+  o.valid = lane < t.nvalid ? 1u : 0u;
   // contiguous tiles record only tail prefixes: a packet starts where the
   // nearest non-empty packet before it ended (0 at the tile start)
   uint32_t base_prefix = 0;
@@ -586,24 +752,25 @@ __device__ __forceinline__ void tile_epilogue(const RxParams& P, const RxLdsPtrs
     const uint32_t prev = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) pidx, 0x138, 0xf, 0xf, false);  // wave_shr:1
     base_prefix = (lane != 0u && prev != 0u) ? L.E[prev - 1u] : 0u;
   }
-  if (lane < t.nvalid) {
+  if (o.valid) {
     const uint32_t sum = t.nch ? (L.E[lane] - (t.contig ? base_prefix : L.S[lane])) : 0u;
     const uint32_t x = fold16(sum);
     // LE halfword sums at absolute positions == byte-swapped BE sum when the
     // packet starts at an even address (RFC 1071 byte-order independence).
     const uint32_t be = (t.off & 1) ? x : bswap16(x);
-    if (P.out_csum) P.out_csum[pid] = (uint16_t) (~be & 0xFFFFu);
+    o.cs = ~be & 0xFFFFu;
     if (P.out_l34)
-      P.out_l34[pid] = (uint8_t) l34_flags(reinterpret_cast<const uint32_t*>(L.hdr + lane * kHdrChunks),
-                                           reinterpret_cast<const uint32_t*>(P.frames + (t.off & ~15ull)),
-                                           (uint32_t) (t.off & 15), t.len, sum);
+      o.l34 = l34_flags(HdrView{L.hdr, lane}, reinterpret_cast<const uint32_t*>(P.frames + (t.off & ~15ull)),
+                        (uint32_t) (t.off & 15), t.len, sum);
     if (L.want_rss) {
-      const uint32_t h =
-          rss_hash_packet(P, L.lut, L.hdr + lane * kHdrChunks, (uint32_t) (t.off & 15), P.frames + t.off, t.len);
+      const uint32_t h = dbg_on(P, kDbgNoHash)
+                             ? (uint32_t) o.pid * 2654435761u
+                             : rss_hash_packet(P, L.lut, HdrView{L.hdr, lane}, (uint32_t) (t.off & 15),
+                                               P.frames + t.off, t.len);
       const uint32_t idx = h % P.table_n;
-      if (P.out_hash) P.out_hash[pid] = h;
-      if (P.out_queue) P.out_queue[pid] = L.table_lds ? L.table_s[idx] : P.table[idx];
-      if (P.out_hits) {
+      o.h = h;
+      if (P.out_queue) o.q = dbg_on(P, kDbgNoTable) ? idx : (L.table_lds ? L.table_s[idx] : P.table[idx]);
+      if (P.out_hits && !dbg_on(P, kDbgNoHist)) {
         if (L.hist_lds) atomicAdd(&L.hist[idx], 1u);
         else atomicAdd(&P.out_hits[idx], 1ull);
       }
@@ -611,13 +778,14 @@ __device__ __forceinline__ void tile_epilogue(const RxParams& P, const RxLdsPtrs
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  return o;
 }
 
 // General tiles (packets not contiguous in chunk space): chunk -> packet by
 // marks + DPP prefix-max, ping-pong over the tile.
-template <int U, bool NT>
+template <int U, bool NT, bool DEFER, int SST>
 __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsPtrs& L, const Tile& t, uint32_t lane,
-                                                 uint32_t& tag) {
+                                                 uint32_t& tag, const TileOut& pend) {
   constexpr uint32_t kStep = (uint32_t) kWave * U;
   L.pk[lane] = make_uint4((uint32_t) (uint64_t) t.delta, (uint32_t) ((uint64_t) t.delta >> 32), t.end, t.info);
   __builtin_amdgcn_wave_barrier();
@@ -628,6 +796,10 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
   // counted pair loop, single exit at the bottom (see the contiguous path)
   const uint32_t nbatch = (t.total + kStep - 1) / kStep;
   plan_batch<U, NT>(A, L.pk, L.marks, b0, t.total, lane, t.start, t.nch, ++tag, carry, P.frames);
+  if (DEFER) {
+    __builtin_amdgcn_sched_barrier(0);  // the previous tile's stores after this tile's first loads
+    store_out<SST>(P, pend, L.want_rss);
+  }
   uint32_t bi = 0;
   for (; bi + 1 < nbatch; bi += 2, b0 += 2 * kStep) {
     plan_batch<U, NT>(B, L.pk, L.marks, b0 + kStep, t.total, lane, t.start, t.nch, ++tag, carry, P.frames);
@@ -640,7 +812,9 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
   if (bi < nbatch) run = process_batch<U>(A, run, L.S, L.E, L.hdr, L.stage);
 }
 
-template <int U, bool NT, int WPB, bool CONTIG, bool RANGES, int OCC>
+// CPOL: cache-policy bits of the contiguous path's buffer loads (gfx950: 1 sc0,
+// 2 nt, 16 sc1); -1 = nt when NT.
+template <int U, bool NT, int WPB, bool CONTIG, bool RANGES, int OCC, bool DEFER, int CPOL = -1, int SST = 0>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void rx_offload_kernel(
     RxParams P) {
   extern __shared__ uint4 lds_dyn[];
@@ -650,7 +824,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
 
   RxLdsPtrs L;
   L.want_rss = P.mode != NICGPU_TUPLE_NONE;
-  L.stage = L.want_rss || P.out_l34 != nullptr;
+  L.stage = (L.want_rss || P.out_l34 != nullptr) && !dbg_on(P, kDbgNoStage);
   L.hist_lds = P.out_hits != nullptr && P.table_n <= (uint32_t) kHistLds;
   L.table_lds = L.want_rss && P.table_n <= (uint32_t) kTableLds;
   uint8_t* base_b = reinterpret_cast<uint8_t*>(lds_dyn);
@@ -713,6 +887,10 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   // descriptors are prefetched one tile ahead
   uint64_t d_next = desc_of(first + step);
   Tile cur = make_tile<CONTIG>(first, nvalid_of(first), desc_of(first));
+  TileOut pend;
+  pend.valid = 0;
+  pend.pid = 0;
+  pend.cs = pend.h = pend.q = pend.l34 = 0;
 
   while (cur.nvalid != 0u) {
     if (cur.contig && cur.total != 0u) {
@@ -735,26 +913,35 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
       ContigBatch<U> A, B;
       uint32_t run = 0, b0 = 0;
       const uint32_t nbatch = (cur.total + kStep - 1) / kStep;
-      plan_contig<U, NT>(A, L.slotsA, 0, lane, cur.start, cur.nch, cur.info, rsrc);
+      plan_contig<U, (CPOL >= 0 ? CPOL : (NT ? 2 : 0))>(A, L.slotsA, 0, lane, cur.start, cur.nch, cur.info, rsrc);
+      if (DEFER) {
+        __builtin_amdgcn_sched_barrier(0);  // the previous tile's stores after this tile's first loads
+        store_out<SST>(P, pend, L.want_rss);
+      }
       uint32_t bi = 0;
       for (; bi + 1 < nbatch; bi += 2, b0 += 2 * kStep) {
-        plan_contig<U, NT>(B, L.slotsB, b0 + kStep, lane, cur.start, cur.nch, cur.info, rsrc);
+        plan_contig<U, (CPOL >= 0 ? CPOL : (NT ? 2 : 0))>(B, L.slotsB, b0 + kStep, lane, cur.start, cur.nch, cur.info, rsrc);
         __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's wait
         run = process_contig<U>(A, L.slotsA, L.masks, run, L.E, L.hdr, L.stage, lane);
-        plan_contig<U, NT>(A, L.slotsA, b0 + 2 * kStep, lane, cur.start, cur.nch, cur.info, rsrc);
+        plan_contig<U, (CPOL >= 0 ? CPOL : (NT ? 2 : 0))>(A, L.slotsA, b0 + 2 * kStep, lane, cur.start, cur.nch, cur.info, rsrc);
         __builtin_amdgcn_sched_barrier(0);
         run = process_contig<U>(B, L.slotsB, L.masks, run, L.E, L.hdr, L.stage, lane);
       }
       if (bi < nbatch) run = process_contig<U>(A, L.slotsA, L.masks, run, L.E, L.hdr, L.stage, lane);
     } else if (cur.total != 0u) {
-      run_general_tile<U, NT>(P, L, cur, lane, tag);
+      run_general_tile<U, NT, DEFER, SST>(P, L, cur, lane, tag, pend);
+    } else if (DEFER) {
+      store_out<SST>(P, pend, L.want_rss);
     }
-    tile_epilogue(P, L, cur, lane);
+    const TileOut o = tile_epilogue(P, L, cur, lane);
+    if (DEFER) pend = o;
+    else store_out<SST>(P, o, L.want_rss);
     const uint64_t nb = cur.base + step;
     cur = make_tile<CONTIG>(nb, nvalid_of(nb), d_next);
     d_next = desc_of(nb + step);
   }
 
+  if (DEFER) store_out<SST>(P, pend, L.want_rss);
   if (L.hist_lds) {
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) {
@@ -861,7 +1048,8 @@ __global__ __launch_bounds__(kBlock) void tso_checksum_kernel(TsoParams P) {
 
 // ------------------------------------------------------------ host side --
 // Kernel variants: (loads in flight per lane U, nontemporal loads, waves per
-// block).  Variant 0 is the production choice (tools/tune_rx.py measures the
+// block, contiguous-tile path, ranges, occupancy hint, deferred stores, load
+// cache policy, store cache policy).  Variant 0 is the production choice (tools/tune_rx.py measures the
 // others against it on the GPU; DESIGN.md §4 records the result).
 struct RxVariant {
   void (*kernel)(RxParams);
@@ -872,11 +1060,11 @@ struct RxVariant {
 };
 
 const RxVariant kRxVariants[] = {
-    {rx_offload_kernel<2, true, 4, true, false, 1>, 2, 4, "u2_nt1_w4_c"},
-    {rx_offload_kernel<2, true, 4, true, false, 5>, 2, 4, "u2_nt1_w4_c_o5"},
-    {rx_offload_kernel<2, true, 8, true, false, 5>, 2, 8, "u2_nt1_w8_c_o5"},
-    {rx_offload_kernel<2, true, 8, true, false, 1>, 2, 8, "u2_nt1_w8_c"},
-    {rx_offload_kernel<2, true, 4, false, false, 1>, 2, 4, "u2_nt1_w4"},
+    {rx_offload_kernel<2, true, 4, true, false, 1, true, -1, 16>, 2, 4, "u2_nt1_w4_c_sc1_defer"},
+    {rx_offload_kernel<2, true, 4, true, false, 1, false>, 2, 4, "u2_nt1_w4_c"},
+    {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 16>, 2, 4, "u2_nt1_w4_c_sc1"},
+    {rx_offload_kernel<2, true, 8, true, false, 1, true, -1, 16>, 2, 8, "u2_nt1_w8_c_sc1_defer"},
+    {rx_offload_kernel<2, true, 4, false, false, 1, true, -1, 16>, 2, 4, "u2_nt1_w4_sc1_defer"},
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
 
@@ -1494,6 +1682,9 @@ int nicgpu_rss_info(const nicgpu_rss_ctx* ctx, size_t* key_len, size_t* table_n)
 }  // extern "C"
 
 namespace {
+#ifdef NICGPU_TUNING
+uint32_t g_tune_dbg = 0;  // tools/tune_rx.py --dbg (nicgpu_tune_set_dbg)
+#endif
 int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n,
                     int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum, uint32_t* out_hash,
                     uint16_t* out_queue, uint64_t* out_hits, uint8_t* out_l34, void* stream) {
@@ -1528,6 +1719,9 @@ int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frame
   P.out_queue = out_queue;
   P.out_hits = reinterpret_cast<unsigned long long*>(out_hits);
   P.out_l34 = out_l34;
+#ifdef NICGPU_TUNING
+  P.dbg = g_tune_dbg;
+#endif
   if (ctx) {
     P.lut = ctx->d_lut;
     P.table = ctx->d_table;
@@ -1751,6 +1945,7 @@ int nicgpu_tune_stream_tiles(const uint8_t* buf, size_t bytes, size_t tile_bytes
 }
 int nicgpu_tune_num_variants(void) { return kNumRxVariants; }
 const char* nicgpu_tune_variant_name(int v) { return (v >= 0 && v < kNumRxVariants) ? kRxVariants[v].name : ""; }
+void nicgpu_tune_set_dbg(uint32_t bits) { g_tune_dbg = bits; }
 int nicgpu_tune_rx_offload(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc,
                            size_t n, int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum,
                            uint32_t* out_hash, uint16_t* out_queue, uint64_t* out_hits, void* stream) {

@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--workloads", default="c2,imix,u64")
     ap.add_argument("--variants", default="all")
+    ap.add_argument("--modes", default="auto,none", help="timed tuple modes: auto (checksum+RSS), none (checksum only)")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the read-ceiling sweeps (PMC runs)")
+    ap.add_argument("--dbg", default="", help="comma list of tuning knob masks to time as extra rows "
+                    "(1 no header stage, 2 no hash, 4 no hash/queue/hits stores; outputs wrong)")
     args = ap.parse_args()
 
     import torch
@@ -113,6 +117,9 @@ def main():
         for r in range(args.rounds):
             for v in variants:
                 for mode, bucket in ((sna.TUPLE_AUTO, times), (sna.TUPLE_NONE, times_csum)):
+                    if (mode == sna.TUPLE_AUTO and "auto" not in args.modes) or (
+                            mode == sna.TUPLE_NONE and "none" not in args.modes):
+                        continue
                     run(v, mode)
                     e = [torch.cuda.Event(enable_timing=True) for _ in range(args.iters + 1)]
                     e[0].record()
@@ -122,11 +129,27 @@ def main():
                     torch.cuda.synchronize()
                     bucket[v] += [e[i].elapsed_time(e[i + 1]) * 1e3 for i in range(args.iters)]
         res = {}
+        if args.dbg:
+            tl.nicgpu_tune_set_dbg.argtypes = [u32]
+            for bits in [int(x) for x in args.dbg.split(",")]:
+                tl.nicgpu_tune_set_dbg(bits)
+                ts_dbg = []
+                for r in range(args.rounds):
+                    run(variants[0])
+                    e = [torch.cuda.Event(enable_timing=True) for _ in range(args.iters + 1)]
+                    e[0].record()
+                    for i in range(args.iters):
+                        run(variants[0])
+                        e[i + 1].record()
+                    torch.cuda.synchronize()
+                    ts_dbg += [e[i].elapsed_time(e[i + 1]) * 1e3 for i in range(args.iters)]
+                tl.nicgpu_tune_set_dbg(0)
+                res[f"{names[variants[0]]}_dbg{bits}"] = {"us_median": round(float(np.median(ts_dbg)), 2)}
         for v in variants:
-            med = float(np.median(times[v]))
-            medc = float(np.median(times_csum[v]))
+            med = float(np.median(times[v])) if times[v] else float("nan")
+            medc = float(np.median(times_csum[v])) if times_csum[v] else float("nan")
             res[names[v]] = {
-                "us_median": round(med, 2), "us_min": round(float(np.min(times[v])), 2),
+                "us_median": round(med, 2), "us_min": round(float(np.min(times[v])), 2) if times[v] else None,
                 "alg_gbs": round(alg / med / 1e3, 1), "frac_spec": round(alg / med / 1e3 / 8000, 4),
                 "csum_only_us": round(medc, 2), "csum_only_gbs": round((int(lens.sum()) + 10 * n) / medc / 1e3, 1),
                 "mpkts": round(n / med, 1),
@@ -168,7 +191,7 @@ def main():
         del f, d
 
     # read-only streaming ceiling on the largest buffer
-    if ceiling_buf is not None:
+    if ceiling_buf is not None and not args.no_ceiling:
         nbytes = ceiling_buf.numel() // 16 * 16
         sink = torch.zeros(1, dtype=torch.int32, device="cuda")
         ceil = {}
