@@ -40,9 +40,11 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
-constexpr int kHdrChunks = 4;      // 64 B of each packet staged in LDS
+constexpr int kHdrChunks = 3;      // 48 B of each packet staged in LDS (the IPv4 5-tuple fast path's bytes)
 constexpr int kHdrBytes = kHdrChunks * 16;
-constexpr uint32_t kHdrStride = kHdrChunks + 1;  // LDS uint4 slots per staged packet (see hdr_slot)
+constexpr uint32_t kHdrStride = kHdrChunks;  // LDS uint4 slots per staged packet (see hdr_slot)
+constexpr uint32_t kRingTileBytes = kWave * 8;  // held results of one tile: hash u32[64] | csum u16[64] | queue u16[64]
+constexpr uint32_t kLdsPerCu = 160u * 1024u;  // gfx950  // held results of one tile: hash u32 | csum u16 | queue u16
 constexpr int kLutPos = 2 * NICGPU_MAX_TUPLE;  // nibble positions
 constexpr int kLutWords = kLutPos * 16;
 constexpr int kHistLds = 1024;     // tables up to this size histogram in LDS
@@ -158,6 +160,8 @@ struct RxParams {
   unsigned long long* out_hits;
   uint8_t* out_l34;  // NICGPU_L34_* flags (L3/L4 checksum verification), may be null
   uint32_t dbg;      // tuning builds only (kDbg*): switch parts of the RSS work off to attribute its cost
+  uint32_t hold_r;   // RING kernels: tiles of results each wave holds in LDS before storing them (>= 1)
+  uint32_t ring_off; // RING kernels: LDS byte offset of wave 0's result ring (wave w at + w * hold_r * 512)
 };
 
 // Tuning-only knobs (libnicgpu_tune.so; outputs are wrong with any set).
@@ -204,16 +208,16 @@ __host__ __device__ inline uint32_t rx_lds_bytes(int wpb, int unroll, bool rss, 
   return (uint32_t) wpb * rx_wave_lds(rss, unroll) + kMaskTableBytes + lut_words * 4u + hist_n * 4u;
 }
 
-// Header stage of one wave: chunk k (0..3) of the packet in lane q lives in
-// slot q*5 + k (80-B packet stride, 16 B of padding).  A wave's ds_read_b128
-// of one chunk index is then conflict-free: lanes are served in 16-lane
-// groups ({0-3,12-15,20-27}, ...) and 20*q mod 64 takes 16 distinct values on
-// each group, covering all 64 banks once; dword and byte reads are 4-way
-// instead of 16-way (MI355X_MICROARCH.md §LDS).  With a 64-B stride every
-// dword read of the epilogue was a 16-way conflict (SQ_LDS_BANK_CONFLICT:
-// ~190 cycles per 64-packet tile).  A padded stride keeps every chunk at an
+// Header stage of one wave: chunk k (0..2) of the packet in lane q lives in
+// slot q*3 + k (48-B packet stride).  A wave's ds_read_b128 of one chunk index
+// is conflict-free: lanes are served in 16-lane groups ({0-3,12-15,20-27}, ...)
+// and 12*q mod 64 takes 16 distinct values on each group, covering all 64
+// banks once; dword and byte reads are 4-way.  With a 64-B stride every dword
+// read of the epilogue was a 16-way conflict (SQ_LDS_BANK_CONFLICT: ~190
+// cycles per 64-packet tile).  A dense stride keeps every chunk at an
 // immediate offset from the lane's base, unlike an XOR swizzle, which cost
-// hipcc ~100 VGPRs of hoisted addresses.
+// hipcc ~100 VGPRs of hoisted addresses.  Bytes past the stage are read from
+// global memory (the general parser, L3/L4 verification).
 __device__ __forceinline__ uint32_t hdr_slot(uint32_t q, uint32_t k) { return q * kHdrStride + k; }
 
 struct HdrView {
@@ -644,7 +648,7 @@ struct TileOut {
 // SST: cache-policy bits of the result stores (0 = plain global stores; 16 =
 // sc1 buffer stores, device scope).
 template <int SST>
-__device__ __forceinline__ void store_out(const RxParams& P, const TileOut& o, bool rss) {
+__device__ __forceinline__ void store_out(const RxParams& P, const TileOut& o, bool rss, bool l34 = true) {
   if (SST != 0) {
     if (o.valid) {
       // per-tile resources: base = this tile's first output, offset = lane
@@ -654,7 +658,7 @@ __device__ __forceinline__ void store_out(const RxParams& P, const TileOut& o, b
         __builtin_amdgcn_raw_buffer_store_b16((uint16_t) o.cs,
                                               __builtin_amdgcn_make_buffer_rsrc(P.out_csum + tb, (short) 0, 128, 0x00020000),
                                               (int) (l * 2u), 0, SST);
-      if (P.out_l34) P.out_l34[o.pid] = (uint8_t) o.l34;
+      if (l34 && P.out_l34) P.out_l34[o.pid] = (uint8_t) o.l34;
       if (rss) {
         if (P.out_hash)
           __builtin_amdgcn_raw_buffer_store_b32(o.h,
@@ -727,12 +731,47 @@ __device__ __forceinline__ void store_out(const RxParams& P, const TileOut& o, b
   }
   if (o.valid) {
     if (P.out_csum) P.out_csum[o.pid] = (uint16_t) o.cs;
-    if (P.out_l34) P.out_l34[o.pid] = (uint8_t) o.l34;
+    if (l34 && P.out_l34) P.out_l34[o.pid] = (uint8_t) o.l34;
     if (rss && !dbg_on(P, kDbgNoStore)) {
       if (P.out_hash && !dbg_on(P, kDbgNoHashStore)) P.out_hash[o.pid] = o.h;
       if (P.out_queue && !dbg_on(P, kDbgNoQueueStore)) P.out_queue[o.pid] = (uint16_t) o.q;
     }
   }
+}
+
+// Store the results of the ring's n tiles (bases base0, base0 + step, ...).
+// (Holding 6 B per packet and looking the queue up again here fit 9 tiles
+// instead of 7 on IMIX for no gain there, and cost 64-B batches 10%.)
+template <int SST, typename Lds, typename NValid>
+__device__ __forceinline__ void flush_ring(const RxParams& P, const Lds& L, const uint8_t* ring, uint32_t n,
+                                           uint64_t base0, uint64_t step, uint32_t lane, const NValid& nvalid_of) {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t* slot = ring + i * kRingTileBytes;
+    const uint64_t base = base0 + i * step;
+    TileOut o;
+    o.pid = base + lane;
+    o.h = reinterpret_cast<const uint32_t*>(slot)[lane];
+    o.cs = reinterpret_cast<const uint16_t*>(slot + kWave * 4)[lane];
+    o.q = reinterpret_cast<const uint16_t*>(slot + kWave * 6)[lane];
+    o.l34 = 0;
+    o.valid = lane < nvalid_of(base) ? 1u : 0u;
+    store_out<SST>(P, o, L.want_rss, false);  // out_l34 was stored at the epilogue
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+
+[[maybe_unused]] __device__ __forceinline__ TileOut held_out(uint64_t base, uint32_t nvalid, uint32_t csq, uint32_t h, uint32_t lane) {
+  TileOut o;
+  o.pid = base + lane;
+  o.cs = csq & 0xFFFFu;
+  o.q = csq >> 16;
+  o.h = h;
+  o.l34 = 0;
+  o.valid = lane < nvalid ? 1u : 0u;
+  return o;
 }
 
 // Checksum finish + tuple hash + queue of the tile's packets (one per lane);
@@ -814,7 +853,14 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
 
 // CPOL: cache-policy bits of the contiguous path's buffer loads (gfx950: 1 sc0,
 // 2 nt, 16 sc1); -1 = nt when NT.
-template <int U, bool NT, int WPB, bool CONTIG, bool RANGES, int OCC, bool DEFER, int CPOL = -1, int SST = 0>
+// HOLD > 0: keep up to HOLD tiles' results in registers and store them as one
+// burst when the ring is full and at the end (experiment: do output writes
+// cost less when they are not interleaved with the read stream?).
+// RING: results are held in a per-wave LDS ring of P.hold_r tiles and stored
+// when it is full and at the end, so output writes reach DRAM in bursts
+// instead of interleaved with the read stream.
+template <int U, bool NT, int WPB, bool CONTIG, bool RANGES, int OCC, bool DEFER, int CPOL = -1, int SST = 0,
+          int HOLD = 0, bool RING = false>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void rx_offload_kernel(
     RxParams P) {
   extern __shared__ uint4 lds_dyn[];
@@ -887,6 +933,12 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   // descriptors are prefetched one tile ahead
   uint64_t d_next = desc_of(first + step);
   Tile cur = make_tile<CONTIG>(first, nvalid_of(first), desc_of(first));
+  uint64_t held_b[HOLD > 0 ? HOLD : 1];
+  uint32_t held_v[HOLD > 0 ? HOLD : 1], held_c[HOLD > 0 ? HOLD : 1], held_h[HOLD > 0 ? HOLD : 1];
+  int hold_n = 0;
+  uint8_t* ring = base_b + P.ring_off + (uint32_t) w * P.hold_r * kRingTileBytes;
+  uint32_t ring_n = 0;
+  uint64_t ring_base0 = 0;
   TileOut pend;
   pend.valid = 0;
   pend.pid = 0;
@@ -934,14 +986,54 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
       store_out<SST>(P, pend, L.want_rss);
     }
     const TileOut o = tile_epilogue(P, L, cur, lane);
-    if (DEFER) pend = o;
-    else store_out<SST>(P, o, L.want_rss);
+    if constexpr (RING) {
+      if (P.out_l34 != nullptr) P.out_l34[o.pid] = (uint8_t) o.l34;
+      if (ring_n == P.hold_r) {
+        flush_ring<SST>(P, L, ring, ring_n, ring_base0, step, lane, nvalid_of);
+        ring_n = 0;
+      }
+      if (ring_n == 0) ring_base0 = cur.base;
+      uint8_t* slot = ring + ring_n * kRingTileBytes;
+      reinterpret_cast<uint32_t*>(slot)[lane] = o.h;
+      reinterpret_cast<uint16_t*>(slot + kWave * 4)[lane] = (uint16_t) o.cs;
+      reinterpret_cast<uint16_t*>(slot + kWave * 6)[lane] = (uint16_t) o.q;
+      ++ring_n;
+    } else if constexpr (HOLD > 0) {
+      if (P.out_l34 != nullptr) {
+        store_out<SST>(P, o, L.want_rss);
+      } else {
+        if (hold_n == HOLD) {
+#pragma unroll
+          for (int i = 0; i < HOLD; ++i) store_out<SST>(P, held_out(held_b[i], held_v[i], held_c[i], held_h[i], lane), L.want_rss);
+          hold_n = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < HOLD; ++i)
+          if (i == hold_n) {
+            held_b[i] = cur.base;
+            held_v[i] = cur.nvalid;
+            held_c[i] = o.cs | (o.q << 16);
+            held_h[i] = o.h;
+          }
+        ++hold_n;
+      }
+    } else if (DEFER) {
+      pend = o;
+    } else {
+      store_out<SST>(P, o, L.want_rss);
+    }
     const uint64_t nb = cur.base + step;
     cur = make_tile<CONTIG>(nb, nvalid_of(nb), d_next);
     d_next = desc_of(nb + step);
   }
 
   if (DEFER) store_out<SST>(P, pend, L.want_rss);
+  if constexpr (RING) flush_ring<SST>(P, L, ring, ring_n, ring_base0, step, lane, nvalid_of);
+  if constexpr (HOLD > 0) {
+#pragma unroll
+    for (int i = 0; i < HOLD; ++i)
+      if (i < hold_n) store_out<SST>(P, held_out(held_b[i], held_v[i], held_c[i], held_h[i], lane), L.want_rss);
+  }
   if (L.hist_lds) {
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) {
@@ -1057,14 +1149,22 @@ struct RxVariant {
   int wpb;
   const char* name;
   bool ranges = false;  // balanced per-wave packet ranges (grid sized by packets, not tiles)
+  bool ring = false;    // LDS result ring (P.hold_r, P.ring_off sized at launch)
 };
 
 const RxVariant kRxVariants[] = {
+    // 0 and 2: production; for variant 0 launch_rx picks plain stores (2) when
+    // the ring holds all of a wave's tiles (every write lands after the reads:
+    // C2 -1%) and sc1 stores (0) when the ring is flushed mid-stream (IMIX -3%).
+    // 8-wave blocks (1, 3) measure the same on C2/IMIX/64 B and 12% slower on
+    // 9000 B, whose 2500 tiles underfill 512 slots of 8 waves.
+    {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 16, 0, true>, 2, 4, "u2_nt1_w4_c_sc1_ring", false, true},
+    {rx_offload_kernel<2, true, 8, true, false, 1, false, -1, 16, 0, true>, 2, 8, "u2_nt1_w8_c_sc1_ring", false, true},
+    {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 0, 0, true>, 2, 4, "u2_nt1_w4_c_ring", false, true},
+    {rx_offload_kernel<2, true, 8, true, false, 1, false, -1, 0, 0, true>, 2, 8, "u2_nt1_w8_c_ring", false, true},
     {rx_offload_kernel<2, true, 4, true, false, 1, true, -1, 16>, 2, 4, "u2_nt1_w4_c_sc1_defer"},
     {rx_offload_kernel<2, true, 4, true, false, 1, false>, 2, 4, "u2_nt1_w4_c"},
-    {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 16>, 2, 4, "u2_nt1_w4_c_sc1"},
-    {rx_offload_kernel<2, true, 8, true, false, 1, true, -1, 16>, 2, 8, "u2_nt1_w8_c_sc1_defer"},
-    {rx_offload_kernel<2, true, 4, false, false, 1, true, -1, 16>, 2, 4, "u2_nt1_w4_sc1_defer"},
+    {rx_offload_kernel<2, true, 4, false, false, 1, false, -1, 16, 0, true>, 2, 4, "u2_nt1_w4_sc1_ring", false, true},
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
 
@@ -1501,24 +1601,64 @@ int ensure_table(nicgpu_rss_ctx* ctx, size_t n) {
   return NICGPU_OK;
 }
 
+// LDS result ring of a RING variant at its occupancy: tiles held per wave
+// (as many as the LDS left over allows, at most a wave's share of the batch),
+// and whether that is all of a wave's tiles.
+struct RingPlan {
+  uint32_t hold_r, ring_off, lds;
+  bool holds_all;
+};
+
+RingPlan plan_ring(int dev, int variant, uint32_t lds, uint64_t ntiles, const DeviceInfo& di) {
+  const RxVariant& v = kRxVariants[variant];
+  const int bpc = rx_blocks_per_cu(dev, variant, lds);
+  const uint64_t waves = (uint64_t) di.cus * (uint64_t) bpc * (uint64_t) v.wpb;
+  const uint64_t per_wave = (ntiles + waves - 1) / waves;
+  const uint32_t per_block = kLdsPerCu / (uint32_t) bpc;
+  const uint32_t spare = per_block > lds ? per_block - lds : 0u;
+  uint64_t r = spare / ((uint32_t) v.wpb * kRingTileBytes);
+  if (r > per_wave) r = per_wave;
+  if (r < 1) r = 1;
+  RingPlan rp;
+  rp.hold_r = (uint32_t) r;
+  rp.ring_off = (lds + 15u) & ~15u;
+  rp.lds = rp.ring_off + (uint32_t) v.wpb * rp.hold_r * kRingTileBytes;
+  rp.holds_all = per_wave <= r;
+  return rp;
+}
+
 int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t stream) {
   if (variant < 0 || variant >= kNumRxVariants) return NICGPU_ERR_INVALID;
-  const RxVariant& v = kRxVariants[variant];
   const bool rss = P.mode != NICGPU_TUPLE_NONE;
   const bool stage = rss || P.out_l34 != nullptr;
   const uint32_t hist_n = (P.out_hits && P.table_n <= (uint32_t) kHistLds) ? P.table_n : 0u;
   const uint32_t table_words = (rss && P.table_n <= (uint32_t) kTableLds) ? (P.table_n + 1u) / 2u : 0u;
-  const uint32_t lds = rx_lds_bytes(v.wpb, v.unroll, stage, rss ? P.lut_words : 0u, hist_n) +
-                       table_words * 4u;
+  const uint64_t ntiles = (P.n + kWave - 1) / kWave;
   int dev = 0;
   (void) hipGetDevice(&dev);
-  const uint64_t ntiles = (P.n + kWave - 1) / kWave;
+  auto lds_of = [&](int var) {
+    const RxVariant& vv = kRxVariants[var];
+    return rx_lds_bytes(vv.wpb, vv.unroll, stage, rss ? P.lut_words : 0u, hist_n) + table_words * 4u;
+  };
+  if (variant == 0) variant = plan_ring(dev, 0, lds_of(0), ntiles, di).holds_all ? 2 : 0;
+  const RxVariant& v = kRxVariants[variant];
+  const uint32_t lds = lds_of(variant);
   // ranges: at least 16 packets per wave; round robin: one tile per wave
   const uint64_t want = v.ranges ? (P.n + 16 * (uint64_t) v.wpb - 1) / (16 * (uint64_t) v.wpb)
                                  : (ntiles + v.wpb - 1) / (uint64_t) v.wpb;
-  const uint64_t cap = (uint64_t) di.cus * (uint64_t) rx_blocks_per_cu(dev, variant, lds);
+  int bpc = rx_blocks_per_cu(dev, variant, lds);
+  RxParams Pl = P;
+  uint32_t lds_launch = lds;
+  if (v.ring) {
+    const RingPlan rp = plan_ring(dev, variant, lds, ntiles, di);
+    Pl.hold_r = rp.hold_r;
+    Pl.ring_off = rp.ring_off;
+    lds_launch = rp.lds;
+    bpc = rx_blocks_per_cu(dev, variant, lds_launch);
+  }
+  const uint64_t cap = (uint64_t) di.cus * (uint64_t) bpc;
   const unsigned grid = (unsigned) (want < cap ? want : cap);
-  hipLaunchKernelGGL(v.kernel, dim3(grid), dim3(kWave * v.wpb), lds, stream, P);
+  hipLaunchKernelGGL(v.kernel, dim3(grid), dim3(kWave * v.wpb), lds_launch, stream, Pl);
   return hip_status(hipGetLastError());
 }
 
