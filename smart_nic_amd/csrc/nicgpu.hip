@@ -859,8 +859,11 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
 // RING: results are held in a per-wave LDS ring of P.hold_r tiles and stored
 // when it is full and at the end, so output writes reach DRAM in bursts
 // instead of interleaved with the read stream.
+// GEN = false (tuning only, names "*_xc"): no general path compiled in, so
+// non-contiguous tiles are skipped and their results are wrong; measures what
+// the general path's registers cost the contiguous loop.
 template <int U, bool NT, int WPB, bool CONTIG, bool RANGES, int OCC, bool DEFER, int CPOL = -1, int SST = 0,
-          int HOLD = 0, bool RING = false>
+          int HOLD = 0, bool RING = false, bool GEN = true>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void rx_offload_kernel(
     RxParams P) {
   extern __shared__ uint4 lds_dyn[];
@@ -980,7 +983,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
         run = process_contig<U>(B, L.slotsB, L.masks, run, L.E, L.hdr, L.stage, lane);
       }
       if (bi < nbatch) run = process_contig<U>(A, L.slotsA, L.masks, run, L.E, L.hdr, L.stage, lane);
-    } else if (cur.total != 0u) {
+    } else if (GEN && cur.total != 0u) {
       run_general_tile<U, NT, DEFER, SST>(P, L, cur, lane, tag, pend);
     } else if (DEFER) {
       store_out<SST>(P, pend, L.want_rss);

@@ -245,6 +245,30 @@ def test_full_size_c2_properties():
     np.testing.assert_array_equal(hits2, hits)
 
 
+def test_ring_flushes_small_packets_vs_oracle():
+    """2.5 M x 64 B: more tiles per wave than the LDS result ring holds, so the
+    production kernel flushes the ring mid-stream (sc1 stores) as well as at
+    the end.  Every packet: status and queue properties; a 50 k sample across
+    the batch (every flush round): exact vs the oracle; determinism."""
+    n = 2_500_000
+    frames, desc, corrupted = pktgen.make_batch(np.full(n, 64), seed=11, proto=17, corrupt_frac=0.01)
+    table = np.arange(128) % 4
+    cs, h, q, hits = gpu_rx(frames, desc, MS_KEY, table)
+    np.testing.assert_array_equal(cs != 0, corrupted)
+    np.testing.assert_array_equal(q, table[h % 128])
+    np.testing.assert_array_equal(hits, np.bincount(h % 128, minlength=128).astype(np.uint64))
+    idx = np.sort(np.random.default_rng(1).choice(n, 50_000, replace=False))
+    cs_o, h_o, q_o, _, _ = po.rx_batch(frames, desc[idx], MS_KEY, table)
+    np.testing.assert_array_equal(cs[idx], cs_o)
+    np.testing.assert_array_equal(h[idx], h_o)
+    np.testing.assert_array_equal(q[idx], q_o)
+    cs2, h2, q2, hits2 = gpu_rx(frames, desc, MS_KEY, table)
+    np.testing.assert_array_equal(cs2, cs)
+    np.testing.assert_array_equal(h2, h)
+    np.testing.assert_array_equal(q2, q)
+    np.testing.assert_array_equal(hits2, hits)
+
+
 def test_imix_16q_vs_oracle():
     rng = np.random.default_rng(3)
     n = 200_000
