@@ -100,22 +100,12 @@ __device__ __forceinline__ uint32_t add_halves(uint32_t d, uint32_t acc) {
   return __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, d), (ushort2_t){1, 1}, acc, false);
 }
 
-__device__ __forceinline__ uint32_t chunk_sum(uint4 v) {
-  return add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, 0u))));
-}
 
 __device__ __forceinline__ uint32_t fold16(uint32_t s) {
   uint32_t x = (s & 0xFFFFu) + (s >> 16);
   return (x & 0xFFFFu) + (x >> 16);
 }
 
-// Ones'-complement fold of a 64-bit sum: the value in [1, 0xFFFF] congruent to
-// s mod 0xFFFF, or 0 only for s == 0 (2^32 == 1 mod 0xFFFF).
-__device__ __forceinline__ uint32_t fold64(uint64_t s) {
-  if (s == 0) return 0;
-  uint32_t r = (uint32_t) (s % 0xFFFFull);
-  return r ? r : 0xFFFFu;
-}
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | (x >> 8); }
 
@@ -1065,79 +1055,237 @@ struct TsoParams {
   uint16_t* out;
 };
 
-__device__ __forceinline__ uint32_t range_sum_chunk(uint4 v, uint64_t cbase, uint64_t lo, uint64_t hi) {
-  // sum (LE halfwords) of the bytes of chunk [cbase, cbase+16) that lie in [lo, hi)
-  int a = lo > cbase ? (int) (lo - cbase) : 0;
-  int b = hi < cbase + 16 ? (int) (hi > cbase ? hi - cbase : 0) : 16;
-  if (b <= a) return 0;
-  v.x &= dword_keep(a, b, 0);
-  v.y &= dword_keep(a, b, 1);
-  v.z &= dword_keep(a, b, 2);
-  v.w &= dword_keep(a, b, 3);
-  return chunk_sum(v);
+// Per-frame TSO state (wave-uniform).  Byte positions are relative to the
+// frame's first 16-B chunk a0; the frame is [fo, fo + L), the header
+// [fo, fo + H), segment k's payload [fo + H + k*mss, ... + mss) clipped to L.
+struct TsoFrame {
+  uint64_t f;      // frame index
+  uint64_t a0;     // absolute byte address of the first chunk (16-B aligned)
+  uint32_t fo, L, H, mss, nseg, nsteps, valid, segmented, seg_base;
+  float inv_mss;
+};
+
+// u16 element i of a uniform array through a scalar dword load (a vector
+// u16 load would make hipcc drain vmcnt, i.e. the in-flight batch, at every
+// frame).  An aligned dword never crosses a page, so the <= 2 bytes read past
+// the element cannot fault; they are discarded.
+__device__ __forceinline__ uint32_t scalar_u16(const uint16_t* a, uint64_t i) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(a + i);
+  const uint32_t w = *reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t) 3);
+  return (addr & 2u) ? (w >> 16) : (w & 0xFFFFu);
+}
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  const uint32_t lo = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) x);
+  const uint32_t hi = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) (x >> 32));
+  return ((uint64_t) hi << 32) | lo;
+}
+
+__device__ __forceinline__ TsoFrame tso_frame(const TsoParams& P, uint64_t f) {
+  f = uniform64(f);  // wave-uniform by construction; makes the frame's loads scalar
+  TsoFrame t{};
+  t.f = f;
+  t.valid = f < P.n ? 1u : 0u;
+  if (!t.valid) return t;
+  const uint64_t d = P.desc[f];
+  const uint64_t off = d & kOffMask;
+  t.L = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
+  t.a0 = off & ~15ull;
+  t.fo = (uint32_t) (off & 15u);
+  t.mss = scalar_u16(P.mss, f);
+  t.H = scalar_u16(P.hdr_len, f);
+  t.segmented = (t.mss > 0u && t.L > t.mss && t.H < t.L) ? 1u : 0u;
+  if (!t.segmented) t.H = t.L;  // one "segment" = the whole frame, all of it header
+  t.nseg = t.segmented ? (t.L - t.H + t.mss - 1u) / t.mss : 1u;
+  // TooManySegments: the host drops the frame; nothing is read or written
+  t.nsteps = t.nseg > (uint32_t) kMaxSeg ? 0u : (t.fo + t.L + 1023u) / 1024u;
+  t.inv_mss = t.segmented ? 1.0f / (float) t.mss : 0.0f;
+  t.seg_base = P.seg_base[f];
+  return t;
+}
+
+// One step = 64 chunks (1 KiB) of a frame, chunk c = lane.  Masks the bytes
+// outside the frame, scans the chunk sums across the wave and records the
+// frame prefix sum at every segment boundary x_k = fo + H + k*mss
+// (k = 0..nseg-1; x_0 is the header's end) that falls in this lane's chunk:
+// prefix(x) = run + (scan before this chunk) + (this chunk's bytes below x).
+__device__ __forceinline__ uint32_t tso_step(const TsoFrame& t, u32x4 v, uint32_t step, uint32_t lane, uint32_t run,
+                                             uint32_t* bnd) {
+  const uint32_t cb = step * 1024u + lane * 16u;  // chunk start, frame-relative (a0 = 0)
+  const uint32_t fe = t.fo + t.L;
+  if (cb < t.fo || cb + 16u > fe) {
+    const int lo = cb < t.fo ? (int) (t.fo - cb) : 0;
+    const int hi = cb >= fe ? 0 : (cb + 16u > fe ? (int) (fe - cb) : 16);
+    if (hi <= lo) {
+      v = (u32x4){0u, 0u, 0u, 0u};
+    } else {
+      v.x &= dword_keep(lo, hi, 0);
+      v.y &= dword_keep(lo, hi, 1);
+      v.z &= dword_keep(lo, hi, 2);
+      v.w &= dword_keep(lo, hi, 3);
+    }
+  }
+  const uint32_t s = add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, 0u))));
+  const uint32_t incl = wave_incl_scan(s);
+  const uint32_t before = run + incl - s;
+  if (t.segmented) {
+    // first boundary at or after the chunk start: k = ceil((cb - x_0) / mss)
+    const uint32_t x0 = t.fo + t.H;
+    uint32_t k = 0;
+    if (cb > x0) {
+      const uint32_t rel = cb - x0;
+      k = (uint32_t) ((float) rel * t.inv_mss);
+      if (k * t.mss < rel) ++k;                      // float estimate off by at most one
+      if (k > 0u && (k - 1u) * t.mss >= rel) --k;
+    }
+    for (; k < t.nseg; ++k) {
+      const uint32_t x = x0 + k * t.mss;
+      if (x >= cb + 16u) break;
+      // bytes of this chunk below x (and inside the frame: already masked)
+      const int hi = (int) (x - cb);
+      uint32_t part = 0;
+      if (hi > 0) {
+        part = add_halves(v.x & dword_keep(0, hi, 0), 0u);
+        part = add_halves(v.y & dword_keep(0, hi, 1), part);
+        part = add_halves(v.z & dword_keep(0, hi, 2), part);
+        part = add_halves(v.w & dword_keep(0, hi, 3), part);
+      }
+      bnd[k] = before + part;
+    }
+  }
+  return run + (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
+}
+
+// Segment checksums of a finished frame from its boundary prefixes.
+__device__ __forceinline__ void tso_finish(const TsoParams& P, const TsoFrame& t, uint32_t* bnd, uint32_t total,
+                                           uint32_t lane) {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const uint32_t off_odd = t.fo & 1u;  // frames are 16-B aligned at a0
+  const uint32_t hsum = fold16(t.segmented ? bnd[0] : total);
+  const uint32_t hdr_be = off_odd ? hsum : bswap16(hsum);
+  const uint32_t base = t.seg_base;
+  for (uint32_t k = lane; k < t.nseg; k += kWave) {
+    uint32_t tot;
+    if (t.segmented) {
+      const uint32_t hi = k + 1u < t.nseg ? bnd[k + 1u] : total;
+      const uint32_t px = fold16(hi - bnd[k]);
+      // payload byte at frame offset o sits at segment position o - k*mss
+      const bool swap = ((k * t.mss + t.fo) & 1u) == 0u;
+      tot = fold16(hdr_be + (swap ? bswap16(px) : px));
+    } else {
+      tot = hdr_be;
+    }
+    P.out[base + k] = (uint16_t) (~tot & 0xFFFFu);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+
+// One wave per frame (f = wave, wave + W, ...).  All of a frame's chunks are
+// requested at once — kTsoSteps loads of 16 B per lane cover 9 KiB, a whole
+// MTU-9000 jumbo frame — and reduced in order with counted vmcnt waits; frames
+// beyond that repeat the group.  Straight-line code (unconditional loads
+// through a per-frame buffer resource whose reads past the frame return
+// zeros) keeps the waits counted.  Frame sums are mod 2^32 prefix differences:
+// exact below 64 KiB.
+//
+// Boundaries (mss >= 16: at most one per chunk): before a group's loads, lane
+// k < nseg writes k + 1 into the group's LDS slot of the chunk holding x_k;
+// in each step a chunk lane reads its slot and, only if it holds a boundary,
+// adds the masked bytes below x_k (one LDS mask read) to its exclusive prefix.
+// mss < 16 frames (several boundaries per chunk) take tso_step's search.
+constexpr int kTsoSteps = 9;
+constexpr uint32_t kTsoWindow = (uint32_t) kTsoSteps * kWave;  // chunks per group
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tso_rsrc(const TsoParams& P, const TsoFrame& t) {
+  const uint64_t a = reinterpret_cast<uint64_t>(P.frames) + t.a0;
+  const uint32_t lo = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) a);
+  const uint32_t hi = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) (a >> 32));
+  const uint32_t nb = (uint32_t) __builtin_amdgcn_readfirstlane((int) ((t.fo + t.L + 15u) & ~15u));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t) hi << 32) | lo), (short) 0, (int) nb,
+                                           0x00020000);
+}
+
+// Fast step (mss >= 16 or unsegmented): c = group-relative chunk of this lane.
+__device__ __forceinline__ uint32_t tso_step_slots(const TsoFrame& t, u32x4 v, uint32_t gchunk0, uint32_t c,
+                                                   uint32_t lane, uint32_t run, uint32_t* bnd, uint32_t* slots,
+                                                   const uint4* masks) {
+  const uint32_t chunk = gchunk0 + c;  // frame-relative chunk index
+  const uint32_t clast = (t.fo + t.L + 15u) / 16u - 1u;  // last chunk holding frame bytes (L > 0 here)
+  if (chunk == 0u || chunk == clast) {
+    const uint32_t lo = chunk == 0u ? t.fo : 0u;
+    const uint32_t hi = chunk == clast ? ((t.fo + t.L - 1u) & 15u) + 1u : 16u;
+    const uint4 a = masks[lo], b = masks[16u + hi];
+    v.x &= a.x & b.x;
+    v.y &= a.y & b.y;
+    v.z &= a.z & b.z;
+    v.w &= a.w & b.w;
+  }
+  const uint32_t s = add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, 0u))));
+  const uint32_t incl = wave_incl_scan(s);
+  const uint32_t sl = slots[c];
+  if (sl != 0u) {
+    slots[c] = 0u;
+    const uint32_t k = sl - 1u;
+    const uint32_t hi = (t.fo + t.H + k * t.mss) & 15u;  // bytes of this chunk below x_k
+    const uint4 m = masks[16u + hi];
+    uint32_t part = add_halves(v.x & m.x, 0u);
+    part = add_halves(v.y & m.y, part);
+    part = add_halves(v.z & m.z, part);
+    part = add_halves(v.w & m.w, part);
+    bnd[k] = run + incl - s + part;
+  }
+  (void) lane;
+  return run + (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
 }
 
 __global__ __launch_bounds__(kBlock) void tso_checksum_kernel(TsoParams P) {
-  __shared__ uint32_t seg[kWavesPerBlock][kMaxSeg + 1];
-  const int w = threadIdx.x / kWave;
+  __shared__ uint32_t bnd_s[kWavesPerBlock][kMaxSeg + 1];
+  __shared__ uint32_t slots_s[kWavesPerBlock][kTsoWindow];
+  __shared__ uint4 masks[kMaskEntries];
+  for (uint32_t i = threadIdx.x; i < kMaskEntries; i += kBlock) {
+    const int lo = i < 16u ? (int) i : 0, hi = i < 16u ? 16 : (int) i - 16;
+    masks[i] = make_uint4(dword_keep(lo, hi, 0), dword_keep(lo, hi, 1), dword_keep(lo, hi, 2), dword_keep(lo, hi, 3));
+  }
+  const int w = __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));  // provably wave-uniform: scalar frame state
   const uint32_t lane = lane_id();
+  for (uint32_t i = lane; i < kTsoWindow; i += kWave) slots_s[w][i] = 0u;
+  __syncthreads();
   const uint64_t nwaves = (uint64_t) gridDim.x * kWavesPerBlock;
+  uint32_t* bnd = bnd_s[w];
+  uint32_t* slots = slots_s[w];
   for (uint64_t f = (uint64_t) blockIdx.x * kWavesPerBlock + w; f < P.n; f += nwaves) {
-    const uint64_t d = P.desc[f];
-    const uint64_t off = d & kOffMask;
-    const uint64_t L = d >> NICGPU_DESC_OFFSET_BITS;
-    const uint32_t mss = P.mss[f];
-    uint64_t H = P.hdr_len[f];
-    const bool segmented = mss > 0 && L > mss && H < L;
-    if (!segmented) H = L;  // one "segment" = the whole frame, all of it header
-    const uint32_t nseg = segmented ? (uint32_t) ((L - H + mss - 1) / mss) : 1u;
-    if (nseg > (uint32_t) kMaxSeg) continue;  // TooManySegments: the host drops the frame
-    for (uint32_t i = lane; i <= (uint32_t) kMaxSeg; i += kWave) seg[w][i] = 0;
-    __builtin_amdgcn_wave_barrier();
-
-    const uint64_t a0 = off & ~15ull, a1 = (off + L + 15) & ~15ull;
-    uint64_t hsum64 = 0;
-    for (uint64_t cb = a0 + 16ull * lane; cb < a1; cb += 16ull * kWave) {
-      const uint4 v = *reinterpret_cast<const uint4*>(P.frames + cb);
-      hsum64 += range_sum_chunk(v, cb, off, off + H);
-      if (segmented && cb + 16 > off + H) {
-        // payload bytes of this chunk: segments k0..k1 (k1 <= k0 + 1 when mss >= 16)
-        uint64_t plo = cb > off + H ? cb : off + H;
-        uint64_t phi = cb + 16 < off + L ? cb + 16 : off + L;
-        if (phi > plo) {
-          uint32_t k0 = (uint32_t) ((plo - off - H) / mss);
-          uint32_t k1 = (uint32_t) ((phi - 1 - off - H) / mss);
-          for (uint32_t k = k0; k <= k1; ++k) {
-            uint64_t slo = off + H + (uint64_t) k * mss;
-            uint64_t shi = slo + mss < off + L ? slo + mss : off + L;
-            uint32_t s = range_sum_chunk(v, cb, slo, shi);
-            atomicAdd(&seg[w][k], s);
+    const TsoFrame t = tso_frame(P, f);
+    if (t.nseg > (uint32_t) kMaxSeg) continue;  // TooManySegments: the host drops the frame
+    const __amdgpu_buffer_rsrc_t rs = tso_rsrc(P, t);
+    const bool fast = !t.segmented || t.mss >= 16u;
+    uint32_t run = 0;
+    for (uint32_t g = 0; g < t.nsteps; g += kTsoSteps) {
+      u32x4 v[kTsoSteps];
+#pragma unroll
+      for (int i = 0; i < kTsoSteps; ++i)
+        v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rs, (int) (lane * 16u), (int) ((g + (uint32_t) i) * 1024u), 2));
+      if (fast) {
+        // this group's boundaries into its slot window
+        const uint32_t c0 = g * 64u;
+        if (t.segmented)
+          for (uint32_t k = lane; k < t.nseg; k += kWave) {
+            const uint32_t ck = (t.fo + t.H + k * t.mss) >> 4;
+            if (ck >= c0 && ck < c0 + kTsoWindow) slots[ck - c0] = k + 1u;
           }
-        }
-      }
-    }
-    // wave-reduce the header sum (fold first so the 32-bit adds cannot wrap)
-    uint32_t hsum = fold64(hsum64);
-    for (int o = 32; o >= 1; o >>= 1) hsum += __shfl_xor(hsum, o);
-    hsum = fold16(hsum);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // header BE sum (segment position parity == frame position parity)
-    const uint32_t hdr_be = (off & 1) ? hsum : bswap16(hsum);
-    for (uint32_t k = lane; k < nseg; k += kWave) {
-      uint32_t tot;
-      if (segmented) {
-        uint32_t px = fold16(seg[w][k]);
-        // payload byte at frame offset o sits at segment position o - k*mss
-        const bool swap = (((uint64_t) k * mss + off) & 1ull) == 0;
-        uint32_t pbe = swap ? bswap16(px) : px;
-        tot = fold16(hdr_be + pbe);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+        for (int i = 0; i < kTsoSteps; ++i)
+          run = tso_step_slots(t, v[i], c0, (uint32_t) i * 64u + lane, lane, run, bnd, slots, masks);
       } else {
-        tot = hdr_be;
+#pragma unroll
+        for (int i = 0; i < kTsoSteps; ++i) run = tso_step(t, v[i], g + (uint32_t) i, lane, run, bnd);
       }
-      P.out[P.seg_base[f] + k] = (uint16_t) (~tot & 0xFFFFu);
     }
-    __builtin_amdgcn_wave_barrier();
+    tso_finish(P, t, bnd, run, lane);
   }
 }
 
