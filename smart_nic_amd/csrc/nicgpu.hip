@@ -1434,17 +1434,104 @@ struct TsoSegParams {
   uint16_t* out_csum;
 };
 
+// A frame of up to kSegStage bytes (from its first 16-B chunk) is staged in
+// LDS once — every chunk requested at once, 9 loads of 16 B per lane — and
+// each segment is assembled from the stage: output dwords are written by
+// consecutive lanes (256 B per store instruction), a dword that lies inside
+// one part is two conflict-free LDS reads and a v_alignbyte, and only the few
+// dwords that straddle a part boundary or the segment's ends are built (and,
+// at the ends, stored) byte by byte.  Larger frames copy from global memory.
+constexpr uint32_t kSegStageChunks = (uint32_t) kTsoSteps * kWave;
+constexpr uint32_t kSegStage = kSegStageChunks * 16u;  // 9216 B
+
+__device__ __forceinline__ uint32_t stage_u32(const uint32_t* st, uint32_t s) {
+  const uint32_t lo = st[s >> 2], hi = st[(s >> 2) + 1u];
+  return (s & 3u) ? __builtin_amdgcn_alignbyte(hi, lo, s & 3u) : lo;
+}
+
+// Segment bytes: pl prefix bytes (81 00 tag), then stage[a, +la), then
+// stage[b, ...); written to out[dst, +size) (size = pl + la + lb).  Returns
+// this lane's share of their little-endian halfword sum at absolute positions.
+__device__ __forceinline__ uint32_t seg_copy_stage(uint8_t* out, uint64_t dst, uint32_t size, uint32_t pl,
+                                                   uint32_t tag, const uint8_t* st_b, uint32_t a, uint32_t la,
+                                                   uint32_t b, uint32_t lane) {
+  const uint32_t* st = reinterpret_cast<const uint32_t*>(st_b);
+  const uint64_t d0 = dst & ~3ull;
+  const int lead = (int) (dst - d0);
+  const uint32_t ndw = ((uint32_t) lead + size + 3u) / 4u;
+  const int pa = (int) pl, pb = (int) (pl + la), sz = (int) size;
+  uint32_t sum = 0;
+  for (uint32_t j = lane; j < ndw; j += kWave) {
+    const int r0 = (int) (4u * j) - lead;  // segment position of the dword's first byte
+    const bool full = r0 >= 0 && r0 + 4 <= sz;
+    uint32_t o, keep = 0xFFFFFFFFu;
+    if (full && r0 >= pa && r0 + 4 <= pb) {
+      o = stage_u32(st, a + (uint32_t) (r0 - pa));
+    } else if (full && r0 >= pb) {
+      o = stage_u32(st, b + (uint32_t) (r0 - pb));
+    } else {
+      o = 0;
+      keep = 0;
+      for (int q = 0; q < 4; ++q) {
+        const int r = r0 + q;
+        if (r < 0 || r >= sz) continue;
+        uint32_t val;
+        if (r < pa) val = r == 0 ? 0x81u : (r == 1 ? 0u : (r == 2 ? (tag >> 8) & 0xFFu : tag & 0xFFu));
+        else if (r < pb) val = st_b[a + (uint32_t) (r - pa)];
+        else val = st_b[b + (uint32_t) (r - pb)];
+        o |= val << (8 * q);
+        keep |= 0xFFu << (8 * q);
+      }
+    }
+    uint8_t* p = out + d0 + 4ull * j;
+    if (keep == 0xFFFFFFFFu) {
+      *reinterpret_cast<uint32_t*>(p) = o;
+    } else {
+      for (int q = 0; q < 4; ++q)
+        if ((keep >> (8 * q)) & 0xFFu) p[q] = (uint8_t) (o >> (8 * q));
+      o &= keep;
+    }
+    sum += (o & 0xFFFFu) + (o >> 16);
+  }
+  return sum;
+}
+
 __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
+  __shared__ uint4 stage_s[kWavesPerBlock][kSegStageChunks + 1];  // +1: stage_u32's second dword
+  const int w = __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
   const uint32_t lane = lane_id();
   const uint64_t nwaves = (uint64_t) gridDim.x * kWavesPerBlock;
-  for (uint64_t i = (uint64_t) blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; i < P.n; i += nwaves) {
-    const uint64_t d = P.desc[i];
+  uint4* stage = stage_s[w];
+  // The wave's frames are f0 + t * nwaves.  Their parameters are fetched 64 at
+  // a time, one frame per lane, and broadcast with readlane: a per-frame
+  // global load would make hipcc wait on vmcnt(0) — i.e. for the previous
+  // segments' stores to complete — before every frame and every segment.
+  const uint64_t f0 = (uint64_t) blockIdx.x * kWavesPerBlock + w;
+  for (uint64_t t0 = 0; f0 + t0 * nwaves < P.n; t0 += kWave) {
+    const uint64_t fl_i = f0 + (t0 + lane) * nwaves;
+    const bool have = fl_i < P.n;
+    const uint64_t d_l = have ? P.desc[fl_i] : 0ull;
+    const uint32_t fl_l = have ? (P.flags ? P.flags[fl_i] : (uint32_t) NICGPU_SEG_TSO) : 0u;
+    const uint32_t mh_l = have ? ((uint32_t) P.mss[fl_i] | ((uint32_t) P.hdr_len[fl_i] << 16)) : 0u;
+    const uint32_t sb_l = have ? P.seg_base[fl_i] : 0u;
+    const uint64_t left = (P.n - (f0 + t0 * nwaves) + nwaves - 1) / nwaves;
+    const uint32_t cnt = left < (uint64_t) kWave ? (uint32_t) left : (uint32_t) kWave;
+    uint32_t d_lo = (uint32_t) d_l, d_hi = (uint32_t) (d_l >> 32);
+    uint32_t fl_v = fl_l, mh_v = mh_l, sb_v = sb_l;
+    // consume the loads here, once: otherwise the wait-count pass keeps them
+    // pending around the frame loop and drains vmcnt at every frame
+    asm volatile("" : "+v"(d_lo), "+v"(d_hi), "+v"(fl_v), "+v"(mh_v), "+v"(sb_v));
+  for (uint32_t t = 0; t < cnt; ++t) {
+    const uint64_t d = ((uint64_t) (uint32_t) __builtin_amdgcn_readlane((int) d_hi, (int) t) << 32) |
+                       (uint32_t) __builtin_amdgcn_readlane((int) d_lo, (int) t);
     const uint64_t off = d & kOffMask;
     const uint32_t L = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
-    const uint32_t fl = P.flags ? P.flags[i] : NICGPU_SEG_TSO;
+    const uint32_t fl = (uint32_t) __builtin_amdgcn_readlane((int) fl_v, (int) t);
     const uint32_t tag = fl & 0xFFFFu;
-    const uint32_t mss = P.mss[i];
-    uint32_t H = P.hdr_len[i];
+    const uint32_t mh = (uint32_t) __builtin_amdgcn_readlane((int) mh_v, (int) t);
+    const uint32_t mss = mh & 0xFFFFu;
+    uint32_t H = mh >> 16;
+    const uint32_t seg_base = (uint32_t) __builtin_amdgcn_readlane((int) sb_v, (int) t);
     // build_segments (:212-278)
     uint32_t nseg = 1;
     bool seg = (fl & NICGPU_SEG_TSO) && mss > 0 && L > mss;
@@ -1460,6 +1547,26 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
     if (!seg) H = L;
     const bool insert = fl & NICGPU_SEG_VLAN_INSERT;
     const bool has_vlan = insert || (fl & NICGPU_SEG_VLAN_PRESENT);
+    const uint64_t a0 = off & ~15ull;
+    const uint32_t fo = (uint32_t) (off & 15u);
+    const bool staged = fo + L <= kSegStage;
+    if (staged) {
+      const uint64_t ab = reinterpret_cast<uint64_t>(P.frames) + a0;
+      const uint32_t nb = (fo + L + 15u) & ~15u;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<void*>(uniform64(ab)), (short) 0, __builtin_amdgcn_readfirstlane((int) nb), 0x00020000);
+      u32x4 v[kTsoSteps];
+#pragma unroll
+      for (int c = 0; c < kTsoSteps; ++c)
+        v[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int) (lane * 16u),
+                                                                                (int) ((uint32_t) c * 1024u), 2));
+      __builtin_amdgcn_wave_barrier();  // the previous frame's stage reads are done
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+      for (int c = 0; c < kTsoSteps; ++c) stage[c * kWave + (int) lane] = make_uint4(v[c].x, v[c].y, v[c].z, v[c].w);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
     for (uint32_t k = 0; k < nseg; ++k) {
       const uint32_t clen = seg ? min(mss, L - H - k * mss) : 0u;
       const uint64_t base_len = (uint64_t) H + clen;
@@ -1468,7 +1575,7 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
       if (strip) size -= 4;
       const bool prefix = insert && !strip;
       const bool strip_base = strip && !insert;
-      const uint64_t g = (uint64_t) P.seg_base[i] + k;
+      const uint64_t g = (uint64_t) seg_base + k;
       const uint64_t dst = g * P.stride;
       if (dst > P.out_size || size > P.out_size - dst || size > P.stride) continue;  // does not fit its slot
       uint64_t src_a = off, len_a = H, src_b = off + H + (uint64_t) k * mss, len_b = clen;
@@ -1481,13 +1588,18 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
       }
       uint32_t sum = 0;
       const uint64_t pl = prefix ? 4 : 0;
-      if (lane < pl) {
-        const uint32_t b = lane == 0 ? 0x81u : (lane == 1 ? 0x00u : (lane == 2 ? (tag >> 8) : (tag & 0xFFu)));
-        P.out[dst + lane] = (uint8_t) b;
-        sum += b << (8 * ((dst + lane) & 1));
+      if (staged) {
+        sum = seg_copy_stage(P.out, dst, (uint32_t) size, (uint32_t) pl, tag, reinterpret_cast<const uint8_t*>(stage),
+                             (uint32_t) (src_a - a0), (uint32_t) len_a, (uint32_t) (src_b - a0), lane);
+      } else {
+        if (lane < pl) {
+          const uint32_t b = lane == 0 ? 0x81u : (lane == 1 ? 0x00u : (lane == 2 ? (tag >> 8) : (tag & 0xFFu)));
+          P.out[dst + lane] = (uint8_t) b;
+          sum += b << (8 * ((dst + lane) & 1));
+        }
+        sum += wave_copy<false, true>(P.out, dst + pl, P.frames, 0, src_a, len_a, lane);
+        sum += wave_copy<false, true>(P.out, dst + pl + len_a, P.frames, 0, src_b, len_b, lane);
       }
-      sum += wave_copy<false, true>(P.out, dst + pl, P.frames, 0, src_a, len_a, lane);
-      sum += wave_copy<false, true>(P.out, dst + pl + len_a, P.frames, 0, src_b, len_b, lane);
       const uint32_t tot = (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan(sum), 63);
       if (lane == 0) {
         const uint32_t x = fold16(tot);
@@ -1496,6 +1608,7 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
         if (P.out_csum) P.out_csum[g] = (uint16_t) (~be & 0xFFFFu);
       }
     }
+  }
   }
 }
 
@@ -1664,6 +1777,7 @@ struct DeviceInfo {
   int status = 0;
   int cus = 0;
   int tso_blocks_per_cu = 0;
+  int seg_blocks_per_cu = 0;  // tso_segment_kernel (LDS frame stage)
   // occupancy cache per (variant, dynamic LDS bytes)
   struct Occ { int variant; uint32_t lds; int blocks; };
   std::vector<Occ> occ;
@@ -1686,6 +1800,9 @@ const DeviceInfo& device_info(int dev) {
   int b = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tso_checksum_kernel, kBlock, 0) != hipSuccess || b < 1) b = 1;
   di.tso_blocks_per_cu = b;
+  b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tso_segment_kernel, kBlock, 0) != hipSuccess || b < 1) b = 1;
+  di.seg_blocks_per_cu = b;
   return di;
 }
 
@@ -2093,7 +2210,7 @@ int nicgpu_tso_segment(const uint8_t* frames, const uint64_t* desc, const uint16
   if (st != NICGPU_OK) return st;
   TsoSegParams P{frames, desc, hdr_len, mss, seg_base, flags, n, out, out_size, stride, out_len, out_csum};
   const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-  const uint64_t cap = (uint64_t) di->cus * 8;
+  const uint64_t cap = (uint64_t) di->cus * (uint64_t) di->seg_blocks_per_cu;
   const unsigned grid = (unsigned) (want < cap ? want : cap);
   hipLaunchKernelGGL(tso_segment_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
   return hip_status(hipGetLastError());
