@@ -1444,54 +1444,84 @@ struct TsoSegParams {
 constexpr uint32_t kSegStageChunks = (uint32_t) kTsoSteps * kWave;
 constexpr uint32_t kSegStage = kSegStageChunks * 16u;  // 9216 B
 
-__device__ __forceinline__ uint32_t stage_u32(const uint32_t* st, uint32_t s) {
-  const uint32_t lo = st[s >> 2], hi = st[(s >> 2) + 1u];
-  return (s & 3u) ? __builtin_amdgcn_alignbyte(hi, lo, s & 3u) : lo;
+
+// One dword of a segment at absolute address A (4-aligned), any overlap with
+// the segment: bytes from the prefix / part A / part B, byte stores at the
+// segment's ends.  Returns its halfword sum (absolute positions).
+__device__ __forceinline__ uint32_t seg_dword_bytes(uint8_t* out, uint64_t A, uint64_t dst, int sz, int pa, int pb,
+                                                    uint32_t tag, const uint8_t* st_b, uint32_t a, uint32_t b) {
+  const int r0 = (int) ((int64_t) A - (int64_t) dst);
+  uint32_t o = 0, keep = 0;
+  for (int q = 0; q < 4; ++q) {
+    const int r = r0 + q;
+    if (r < 0 || r >= sz) continue;
+    uint32_t val;
+    if (r < pa) val = r == 0 ? 0x81u : (r == 1 ? 0u : (r == 2 ? (tag >> 8) & 0xFFu : tag & 0xFFu));
+    else if (r < pb) val = st_b[a + (uint32_t) (r - pa)];
+    else val = st_b[b + (uint32_t) (r - pb)];
+    o |= val << (8 * q);
+    keep |= 0xFFu << (8 * q);
+  }
+  uint8_t* p = out + A;
+  if (keep == 0xFFFFFFFFu) {
+    *reinterpret_cast<uint32_t*>(p) = o;
+  } else {
+    for (int q = 0; q < 4; ++q)
+      if ((keep >> (8 * q)) & 0xFFu) p[q] = (uint8_t) (o >> (8 * q));
+  }
+  return (o & 0xFFFFu) + (o >> 16);
 }
 
 // Segment bytes: pl prefix bytes (81 00 tag), then stage[a, +la), then
 // stage[b, ...); written to out[dst, +size) (size = pl + la + lb).  Returns
 // this lane's share of their little-endian halfword sum at absolute positions.
+//  pass 1: every 16-B-aligned destination block that lies inside part A or
+//          part B — five LDS dwords, four v_alignbyte, one 16-B store, and
+//          no branch but the inside test (per-dword branching had made the
+//          kernel SALU-bound);
+//  pass 2: lanes 0..15 take the dwords of the <= 4 blocks pass 1 leaves: the
+//          segment's first and last blocks and the ones holding the part
+//          boundaries pa and pb, byte by byte where a dword straddles.
 __device__ __forceinline__ uint32_t seg_copy_stage(uint8_t* out, uint64_t dst, uint32_t size, uint32_t pl,
                                                    uint32_t tag, const uint8_t* st_b, uint32_t a, uint32_t la,
                                                    uint32_t b, uint32_t lane) {
   const uint32_t* st = reinterpret_cast<const uint32_t*>(st_b);
-  const uint64_t d0 = dst & ~3ull;
-  const int lead = (int) (dst - d0);
-  const uint32_t ndw = ((uint32_t) lead + size + 3u) / 4u;
   const int pa = (int) pl, pb = (int) (pl + la), sz = (int) size;
+  const uint64_t E = dst + size;
+  const uint64_t D16 = (dst + 15) & ~15ull, E16 = E & ~15ull;
+  const uint32_t nblk = E16 > D16 ? (uint32_t) ((E16 - D16) >> 4) : 0u;
+  auto inside16 = [&](int r0) __attribute__((always_inline)) {
+    return (r0 >= pb && r0 + 16 <= sz) || (r0 >= pa && r0 + 16 <= pb);
+  };
   uint32_t sum = 0;
-  for (uint32_t j = lane; j < ndw; j += kWave) {
-    const int r0 = (int) (4u * j) - lead;  // segment position of the dword's first byte
-    const bool full = r0 >= 0 && r0 + 4 <= sz;
-    uint32_t o, keep = 0xFFFFFFFFu;
-    if (full && r0 >= pa && r0 + 4 <= pb) {
-      o = stage_u32(st, a + (uint32_t) (r0 - pa));
-    } else if (full && r0 >= pb) {
-      o = stage_u32(st, b + (uint32_t) (r0 - pb));
-    } else {
-      o = 0;
-      keep = 0;
-      for (int q = 0; q < 4; ++q) {
-        const int r = r0 + q;
-        if (r < 0 || r >= sz) continue;
-        uint32_t val;
-        if (r < pa) val = r == 0 ? 0x81u : (r == 1 ? 0u : (r == 2 ? (tag >> 8) & 0xFFu : tag & 0xFFu));
-        else if (r < pb) val = st_b[a + (uint32_t) (r - pa)];
-        else val = st_b[b + (uint32_t) (r - pb)];
-        o |= val << (8 * q);
-        keep |= 0xFFu << (8 * q);
-      }
+  for (uint32_t j = lane; j < nblk; j += kWave) {
+    const int r0 = (int) (D16 - dst) + 16 * (int) j;
+    const bool inB = r0 >= pb && r0 + 16 <= sz;
+    const bool inA = r0 >= pa && r0 + 16 <= pb;
+    if (inA || inB) {
+      const uint32_t src = inB ? b + (uint32_t) (r0 - pb) : a + (uint32_t) (r0 - pa);
+      const uint32_t k = src >> 2, sh = src & 3u;
+      const uint32_t w0 = st[k], w1 = st[k + 1], w2 = st[k + 2], w3 = st[k + 3], w4 = st[k + 4];
+      u32x4 o;
+      o.x = sh ? __builtin_amdgcn_alignbyte(w1, w0, sh) : w0;
+      o.y = sh ? __builtin_amdgcn_alignbyte(w2, w1, sh) : w1;
+      o.z = sh ? __builtin_amdgcn_alignbyte(w3, w2, sh) : w2;
+      o.w = sh ? __builtin_amdgcn_alignbyte(w4, w3, sh) : w3;
+      *reinterpret_cast<u32x4*>(out + D16 + 16ull * j) = o;
+      sum = add_halves(o.w, add_halves(o.z, add_halves(o.y, add_halves(o.x, sum))));
     }
-    uint8_t* p = out + d0 + 4ull * j;
-    if (keep == 0xFFFFFFFFu) {
-      *reinterpret_cast<uint32_t*>(p) = o;
-    } else {
-      for (int q = 0; q < 4; ++q)
-        if ((keep >> (8 * q)) & 0xFFu) p[q] = (uint8_t) (o >> (8 * q));
-      o &= keep;
-    }
-    sum += (o & 0xFFFFu) + (o >> 16);
+  }
+  if (lane < 16u) {
+    const uint64_t blk[4] = {dst & ~15ull, (dst + (uint64_t) pa) & ~15ull, (dst + (uint64_t) pb) & ~15ull,
+                             (E - 1) & ~15ull};
+    const uint32_t g = lane >> 2;
+    const uint64_t B = blk[g];
+    bool dup = false;
+    for (uint32_t q = 0; q < g; ++q) dup |= blk[q] == B;
+    const bool pass1 = B >= D16 && B < E16 && inside16((int) ((int64_t) B - (int64_t) dst));
+    const uint64_t A = B + 4ull * (lane & 3u);
+    if (size != 0 && !dup && !pass1 && A + 4 > dst && A < E)
+      sum += seg_dword_bytes(out, A, dst, sz, pa, pb, tag, st_b, a, b);
   }
   return sum;
 }
