@@ -1646,16 +1646,18 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
 // nic::rocev2::IcrcCalculator::calculate / verify (src/rocev2/packet.cpp:14-75)
 // over a batch: CRC-32C (reflected 0x82F63B78, init/xorout 0xFFFFFFFF) of
 // every descriptor's span.  One lane owns one packet at a time and walks it
-// 64 B per step (4 x 16-B loads, slice-by-16 tables in LDS); a finished lane
-// takes the next packet of its wave's range through a ballot (a wave-level
-// work queue), so IMIX lengths do not leave lanes idle.  Every 16-B chunk,
-// whatever part of it belongs to the packet (head, tail, both, none), goes
-// through one branch-free step: with valid bytes [a, b) and running CRC state
-// S, processing them equals a zero-state slice-by-16 of the chunk after
+// to the end of a 128-B line per step (up to 8 x 16-B loads, slice-by-16
+// tables in LDS); a finished lane takes the next packet of its wave's range
+// through a ballot (a wave-level work queue), so IMIX lengths do not leave
+// lanes idle.  Every 16-B chunk, whatever part of it belongs to the packet
+// (head, tail, both, none), goes through one branch-free step: with valid
+// bytes [a, b) and running CRC state S, processing them equals a zero-state
+// slice-by-16 of the chunk after
 //   D ^= S at byte a (the standard "xor the state into the next 4 bytes"),
-//   mask D to [a, b), shift it up so the span ends at byte 15
-// (leading zero bytes do not change a zero state), plus S >> 8(b - a) when
-// the span is shorter than 4 bytes.
+//   mask D to [a, b), and look byte i up in the table it would use had the
+//   span been shifted to end at byte 15 (leading zero bytes do not change a
+//   zero state),
+// plus S >> 8(b - a) when the span is shorter than 4 bytes.
 struct Crc32cTables {
   uint32_t t[16][256];
 };
@@ -1683,41 +1685,42 @@ struct IcrcParams {
 
 constexpr int kIcrcRing = 128;  // descriptor ring per wave (LDS)
 
-// 128-bit value (x[0] = bytes 0..3) shifted towards higher byte indices by k bytes (0..16).
-__device__ __forceinline__ void shl_bytes(uint32_t x[4], uint32_t k) {
-  const uint32_t q = k >> 2, r = k & 3u;
-  uint32_t y[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int s0 = j - (int) q, s1 = s0 - 1;
-    const uint32_t a = s0 >= 0 ? x[s0 & 3] : 0u;
-    const uint32_t b = s1 >= 0 ? x[s1 & 3] : 0u;
-    y[j] = r ? __builtin_amdgcn_alignbyte(a, b, 4u - r) : a;
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) x[j] = y[j];
-}
-
-// One chunk: bytes [a, b) of the 16-B chunk v processed from state S.
-__device__ __forceinline__ uint32_t crc_chunk(const uint32_t* __restrict__ T, u32x4 v, uint32_t a, uint32_t b,
-                                              uint32_t S) {
-  uint32_t x[4] = {v.x, v.y, v.z, v.w};
-  uint32_t s4[4] = {S, 0u, 0u, 0u};
-  shl_bytes(s4, a);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) x[j] = (x[j] ^ s4[j]) & dword_keep((int) a, (int) b, j);
-  shl_bytes(x, 16u - b);
+// One chunk: bytes [a, b) of the 16-B chunk v processed from state S,
+// without shifting data: byte i of the chunk goes through
+// slice table b - 1 - i (the table it would use had the span been shifted to
+// end at byte 15).  T holds 15 all-zero tables in front of the 16 slice
+// tables, so bytes at or past b — zeroed by the mask, and T[*][0] = 0 — may
+// index any row: row (b - 1) + (15 - i), with the (15 - i) KiB an immediate
+// LDS offset.  Per byte: one extract, one address add, one LDS read, one
+// xor; the state is xored in at byte a (masked to the span).
+__device__ __forceinline__ uint32_t crc_chunk_ns(const uint32_t* __restrict__ Text, const uint4* masks, u32x4 v,
+                                                 uint32_t a, uint32_t b, uint32_t S) {
+  const uint4 m1 = masks[a], m2 = masks[16u + b];
+  const uint32_t q = a >> 2, sh = 8u * (a & 3u);
+  const uint32_t lo = S << sh, hi = sh ? S >> (32u - sh) : 0u;
+  uint32_t x[4];
+  x[0] = (v.x & m1.x & m2.x) ^ ((q == 0u ? lo : 0u) & m2.x);
+  x[1] = (v.y & m1.y & m2.y) ^ ((q == 1u ? lo : (q == 0u ? hi : 0u)) & m2.y);
+  x[2] = (v.z & m1.z & m2.z) ^ ((q == 2u ? lo : (q == 1u ? hi : 0u)) & m2.z);
+  x[3] = (v.w & m1.w & m2.w) ^ ((q == 3u ? lo : (q == 2u ? hi : 0u)) & m2.w);
+  const uint32_t* Tb = Text + (b - 1u) * 256u;  // b >= 1 whenever a chunk is processed
   uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) c ^= T[(15 - i) * 256 + ((x[i >> 2] >> (8 * (i & 3))) & 0xFFu)];
+  for (int i = 0; i < 16; ++i) c ^= Tb[(15 - i) * 256 + ((x[i >> 2] >> (8 * (i & 3))) & 0xFFu)];
   const uint32_t h = b - a;
   return c ^ (h < 4u ? (h ? S >> (8 * h) : S) : 0u);
 }
 
 __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
-  __shared__ uint32_t T[16 * 256];
+  __shared__ uint32_t Text[31 * 256];  // 15 zero tables, then the 16 slice tables
   __shared__ uint64_t ring_all[kWavesPerBlock][kIcrcRing];
-  for (uint32_t i = threadIdx.x; i < 16u * 256u; i += kBlock) T[i] = (&kCrc32c.t[0][0])[i];
+  __shared__ uint4 masks[kMaskEntries];
+  for (uint32_t i = threadIdx.x; i < 15u * 256u; i += kBlock) Text[i] = 0u;
+  for (uint32_t i = threadIdx.x; i < 16u * 256u; i += kBlock) Text[15u * 256u + i] = (&kCrc32c.t[0][0])[i];
+  for (uint32_t i = threadIdx.x; i < kMaskEntries; i += kBlock) {
+    const int lo = i < 16u ? (int) i : 0, hi = i < 16u ? 16 : (int) i - 16;
+    masks[i] = make_uint4(dword_keep(lo, hi, 0), dword_keep(lo, hi, 1), dword_keep(lo, hi, 2), dword_keep(lo, hi, 3));
+  }
   __syncthreads();
   const uint32_t lane = lane_id();
   uint64_t* ring = ring_all[threadIdx.x / kWave];
@@ -1757,25 +1760,28 @@ __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
     const bool active = my < p1;
     if (__ballot(active) == 0ull) break;
     if (active) {
-      // 4 chunks per step; loads clamped to the span's last chunk
+      // up to the end of the current 128-B line (8 chunks), so a lane reads
+      // every line once (64 B per step fetched most lines twice: 2.2x the
+      // algorithmic bytes); loads clamped to the line and the span's end
       const uint64_t c0 = pos >> 4;
       const uint64_t clast = end > pos ? (end - 1) >> 4 : c0;
-      u32x4 v[4] = {};
+      const uint64_t cl = (c0 | 7u) < clast ? (c0 | 7u) : clast;
+      u32x4 v[8] = {};
       if (end > pos) {  // an empty span reads nothing (it may sit at the buffer's end)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint64_t c = c0 + u <= clast ? c0 + u : clast;
+        for (int u = 0; u < 8; ++u) {
+          const uint64_t c = c0 + u <= cl ? c0 + u : cl;
           v[u] = f16[c];
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const uint64_t cb = (c0 + u) << 4;  // chunk base address
         const uint32_t a = pos > cb ? (uint32_t) (pos - cb) : 0u;
         const uint32_t b = end > cb ? (end - cb >= 16 ? 16u : (uint32_t) (end - cb)) : 0u;
-        if (b > a) S = crc_chunk(T, v[u], a, b, S);
+        if (c0 + u <= cl && b > a) S = crc_chunk_ns(Text, masks, v[u], a, b, S);
       }
-      pos = (c0 + 4) << 4;
+      pos = (cl + 1) << 4;
     }
     const bool finished = active && pos >= end;
     if (finished) {
@@ -1808,6 +1814,7 @@ struct DeviceInfo {
   int cus = 0;
   int tso_blocks_per_cu = 0;
   int seg_blocks_per_cu = 0;  // tso_segment_kernel (LDS frame stage)
+  int icrc_blocks_per_cu = 0;
   // occupancy cache per (variant, dynamic LDS bytes)
   struct Occ { int variant; uint32_t lds; int blocks; };
   std::vector<Occ> occ;
@@ -1833,6 +1840,9 @@ const DeviceInfo& device_info(int dev) {
   b = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tso_segment_kernel, kBlock, 0) != hipSuccess || b < 1) b = 1;
   di.seg_blocks_per_cu = b;
+  b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, icrc_kernel, kBlock, 0) != hipSuccess || b < 1) b = 1;
+  di.icrc_blocks_per_cu = b;
   return di;
 }
 
@@ -2221,9 +2231,10 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
   int st = current_device_info(&di);
   if (st != NICGPU_OK) return st;
   IcrcParams P{frames, desc, n, mode == NICGPU_ICRC_VERIFY, out_crc, out_ok};
-  // enough waves that each owns ~8 packets; at most 8 blocks per CU
-  const uint64_t want = (n + 8 * kBlock - 1) / (8 * kBlock);
-  const uint64_t cap = (uint64_t) di->cus * 8;
+  // every resident wave slot busy (a wave's range is then >= 64 packets, one
+  // work-queue refill); ranges of 8 packets per lane left 3/4 of the slots idle
+  const uint64_t want = (n + kBlock - 1) / kBlock;
+  const uint64_t cap = (uint64_t) di->cus * (uint64_t) di->icrc_blocks_per_cu;
   const unsigned grid = (unsigned) (want < 1 ? 1 : (want < cap ? want : cap));
   hipLaunchKernelGGL(icrc_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
   return hip_status(hipGetLastError());
