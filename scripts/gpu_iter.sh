@@ -9,7 +9,7 @@ rc=$?; tail -4 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error
 timeout -k 10 300 $PT tests/test_gpu_variants.py > gpurun_out/pytest_variants.log 2>&1
 rc=$?; tail -2 gpurun_out/pytest_variants.log; [ $rc -eq 0 ] || exit $rc
 fi
-timeout -k 10 500 python tools/tune_rx.py --rounds ${ROUNDS:-5} --iters 10 --workloads ${WL:-c2,imix,u64,jumbo} --no-ceiling ${DBG:+--dbg $DBG} ${VARIANTS:+--variants $VARIANTS} > gpurun_out/tune.json 2> gpurun_out/tune.err
+timeout -k 10 500 python tools/tune_rx.py --rounds ${ROUNDS:-5} --iters 10 --workloads ${WL:-c2,imix,u64,jumbo} --no-ceiling ${DBG:+--dbg $DBG} ${VARIANTS:+--variants $VARIANTS} ${XPF:+--xpf $XPF} > gpurun_out/tune.json 2> gpurun_out/tune.err
 rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/tune.err; exit $rc; }
 python - <<'EOF'
 import json

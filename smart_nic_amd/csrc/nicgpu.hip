@@ -152,6 +152,7 @@ struct RxParams {
   uint32_t dbg;      // tuning builds only (kDbg*): switch parts of the RSS work off to attribute its cost
   uint32_t hold_r;   // RING kernels: tiles of results each wave holds in LDS before storing them (>= 1)
   uint32_t ring_off; // RING kernels: LDS byte offset of wave 0's result ring (wave w at + w * hold_r * 512)
+  uint32_t xpf_chunks;  // XPF kernels: prefetch the next tile's first batch when it has at most this many chunks
 };
 
 // Tuning-only knobs (libnicgpu_tune.so; outputs are wrong with any set).
@@ -852,8 +853,11 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
 // GEN = false (tuning only, names "*_xc"): no general path compiled in, so
 // non-contiguous tiles are skipped and their results are wrong; measures what
 // the general path's registers cost the contiguous loop.
+// XPF: the next contiguous tile's first batch (slots scattered, loads issued)
+// goes out before this tile's epilogue, so the epilogue overlaps its latency
+// (tiles of at most P.xpf_chunks chunks).
 template <int U, bool NT, int WPB, bool CONTIG, bool RANGES, int OCC, bool DEFER, int CPOL = -1, int SST = 0,
-          int HOLD = 0, bool RING = false, bool GEN = true>
+          int HOLD = 0, bool RING = false, bool GEN = true, bool XPF = false>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void rx_offload_kernel(
     RxParams P) {
   extern __shared__ uint4 lds_dyn[];
@@ -937,28 +941,37 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   pend.pid = 0;
   pend.cs = pend.h = pend.q = pend.l34 = 0;
 
+  // wave-uniform descriptor inputs of a contiguous tile (readfirstlane: provably scalar)
+  auto tile_rsrc = [&](const Tile& t) __attribute__((always_inline)) {
+    const uint64_t tb = reinterpret_cast<uint64_t>(P.frames) + (uint64_t) t.D * 16u;
+    const uint32_t tb_lo = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) tb);
+    const uint32_t tb_hi = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) (tb >> 32));
+    const uint32_t tbytes = (uint32_t) __builtin_amdgcn_readfirstlane((int) (t.total * 16u));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t) tb_hi << 32) | tb_lo), (short) 0,
+                                             (int) tbytes, 0x00020000);
+  };
+  // a contiguous tile's first batch: clear both slot windows, scatter, load
+  ContigBatch<U> A, B;
+  auto tile_first = [&](const Tile& t, __amdgpu_buffer_rsrc_t r) __attribute__((always_inline)) {
+    for (uint32_t i = lane; i < (uint32_t) (2 * kWave * U); i += kWave) L.slotsA[i] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    plan_contig<U, (CPOL >= 0 ? CPOL : (NT ? 2 : 0))>(A, L.slotsA, 0, lane, t.start, t.nch, t.info, r);
+  };
+  bool pre = false;  // (XPF) A already holds cur's first batch
+  __amdgpu_buffer_rsrc_t rsrc_pre = tile_rsrc(cur);
   while (cur.nvalid != 0u) {
     if (cur.contig && cur.total != 0u) {
       // Contiguous tile: chunk c is absolute chunk D + c.  Ping-pong: batch
       // i+1's loads are in flight while batch i is reduced; every plan is
       // unconditional (positions past the end read zeros through the buffer
       // bounds check) so the compiler keeps counted vmcnt waits.
-      for (uint32_t i = lane; i < (uint32_t) (2 * kWave * U); i += kWave) L.slotsA[i] = 0u;
-      __builtin_amdgcn_wave_barrier();
-      // wave-uniform descriptor inputs (readfirstlane: provably scalar)
-      const uint64_t tb = reinterpret_cast<uint64_t>(P.frames) + (uint64_t) cur.D * 16u;
-      const uint32_t tb_lo = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) tb);
-      const uint32_t tb_hi = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) (tb >> 32));
-      const uint32_t tbytes = (uint32_t) __builtin_amdgcn_readfirstlane((int) (cur.total * 16u));
-      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-          reinterpret_cast<void*>(((uint64_t) tb_hi << 32) | tb_lo), (short) 0, (int) tbytes, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rsrc = pre ? rsrc_pre : tile_rsrc(cur);
       // A counted loop over pairs of batches with its only exit at the bottom
       // (a mid-loop break made the wait-count pass drain vmcnt to 0 at the
       // loop header); an odd last batch is processed after the loop.
-      ContigBatch<U> A, B;
       uint32_t run = 0, b0 = 0;
       const uint32_t nbatch = (cur.total + kStep - 1) / kStep;
-      plan_contig<U, (CPOL >= 0 ? CPOL : (NT ? 2 : 0))>(A, L.slotsA, 0, lane, cur.start, cur.nch, cur.info, rsrc);
+      if (!pre) tile_first(cur, rsrc);
       if (DEFER) {
         __builtin_amdgcn_sched_barrier(0);  // the previous tile's stores after this tile's first loads
         store_out<SST>(P, pend, L.want_rss);
@@ -977,6 +990,15 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
       run_general_tile<U, NT, DEFER, SST>(P, L, cur, lane, tag, pend);
     } else if (DEFER) {
       store_out<SST>(P, pend, L.want_rss);
+    }
+    const uint64_t nb = cur.base + step;
+    const Tile nxt = make_tile<CONTIG>(nb, nvalid_of(nb), d_next);
+    pre = false;
+    if (XPF && nxt.contig && nxt.total != 0u && nxt.total <= P.xpf_chunks) {
+      rsrc_pre = tile_rsrc(nxt);
+      tile_first(nxt, rsrc_pre);
+      __builtin_amdgcn_sched_barrier(0);  // the next tile's loads go out before this tile's epilogue
+      pre = true;
     }
     const TileOut o = tile_epilogue(P, L, cur, lane);
     if constexpr (RING) {
@@ -1015,8 +1037,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
     } else {
       store_out<SST>(P, o, L.want_rss);
     }
-    const uint64_t nb = cur.base + step;
-    cur = make_tile<CONTIG>(nb, nvalid_of(nb), d_next);
+    cur = nxt;
     d_next = desc_of(nb + step);
   }
 
@@ -1301,18 +1322,22 @@ struct RxVariant {
   const char* name;
   bool ranges = false;  // balanced per-wave packet ranges (grid sized by packets, not tiles)
   bool ring = false;    // LDS result ring (P.hold_r, P.ring_off sized at launch)
+  bool xpf = false;     // cross-tile prefetch (P.xpf_chunks)
 };
 
 const RxVariant kRxVariants[] = {
     // 0 and 2: production; for variant 0 launch_rx picks plain stores (2) when
     // the ring holds all of a wave's tiles (every write lands after the reads:
     // C2 -1%) and sc1 stores (0) when the ring is flushed mid-stream (IMIX -3%).
+    // Both prefetch the next tile's first batch (XPF: 64 B -1..4%, C2 / IMIX /
+    // 9000 B within noise).
     // 8-wave blocks (1, 3) measure the same on C2/IMIX/64 B and 12% slower on
     // 9000 B, whose 2500 tiles underfill 512 slots of 8 waves.
-    {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 16, 0, true>, 2, 4, "u2_nt1_w4_c_sc1_ring", false, true},
+    {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 16, 0, true, true, true>, 2, 4, "u2_w4_c_sc1_ring_xpf", false, true, true},
     {rx_offload_kernel<2, true, 8, true, false, 1, false, -1, 16, 0, true>, 2, 8, "u2_nt1_w8_c_sc1_ring", false, true},
+    {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 0, 0, true, true, true>, 2, 4, "u2_w4_c_ring_xpf", false, true, true},
+    {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 16, 0, true>, 2, 4, "u2_nt1_w4_c_sc1_ring", false, true},
     {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 0, 0, true>, 2, 4, "u2_nt1_w4_c_ring", false, true},
-    {rx_offload_kernel<2, true, 8, true, false, 1, false, -1, 0, 0, true>, 2, 8, "u2_nt1_w8_c_ring", false, true},
     {rx_offload_kernel<2, true, 4, true, false, 1, true, -1, 16>, 2, 4, "u2_nt1_w4_c_sc1_defer"},
     {rx_offload_kernel<2, true, 4, true, false, 1, false>, 2, 4, "u2_nt1_w4_c"},
     {rx_offload_kernel<2, true, 4, false, false, 1, false, -1, 16, 0, true>, 2, 4, "u2_nt1_w4_sc1_ring", false, true},
@@ -1909,6 +1934,10 @@ int ensure_table(nicgpu_rss_ctx* ctx, size_t n) {
   return NICGPU_OK;
 }
 
+// XPF variants prefetch the next tile's first batch for tiles up to this many
+// 16-B chunks (tools/tune_rx.py sets it through nicgpu_tune_set_xpf).
+uint32_t g_xpf_chunks = 0xFFFFFFFFu;
+
 // LDS result ring of a RING variant at its occupancy: tiles held per wave
 // (as many as the LDS left over allows, at most a wave's share of the batch),
 // and whether that is all of a wave's tiles.
@@ -1956,6 +1985,7 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
                                  : (ntiles + v.wpb - 1) / (uint64_t) v.wpb;
   int bpc = rx_blocks_per_cu(dev, variant, lds);
   RxParams Pl = P;
+  Pl.xpf_chunks = v.xpf ? g_xpf_chunks : 0u;
   uint32_t lds_launch = lds;
   if (v.ring) {
     const RingPlan rp = plan_ring(dev, variant, lds, ntiles, di);
@@ -2395,6 +2425,7 @@ int nicgpu_tune_stream_tiles(const uint8_t* buf, size_t bytes, size_t tile_bytes
 int nicgpu_tune_num_variants(void) { return kNumRxVariants; }
 const char* nicgpu_tune_variant_name(int v) { return (v >= 0 && v < kNumRxVariants) ? kRxVariants[v].name : ""; }
 void nicgpu_tune_set_dbg(uint32_t bits) { g_tune_dbg = bits; }
+void nicgpu_tune_set_xpf(uint32_t max_chunks) { g_xpf_chunks = max_chunks; }
 int nicgpu_tune_rx_offload(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc,
                            size_t n, int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum,
                            uint32_t* out_hash, uint16_t* out_queue, uint64_t* out_hits, void* stream) {

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--variants", default="all")
     ap.add_argument("--modes", default="auto,none", help="timed tuple modes: auto (checksum+RSS), none (checksum only)")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the read-ceiling sweeps (PMC runs)")
+    ap.add_argument("--xpf", type=int, default=-1, help="XPF variants: prefetch tiles of at most this many chunks")
     ap.add_argument("--dbg", default="", help="comma list of tuning knob masks to time as extra rows "
                     "(1 no header stage, 2 no hash, 4 no hash/queue/hits stores; outputs wrong)")
     args = ap.parse_args()
@@ -51,6 +52,9 @@ def main():
     tl.nicgpu_tune_rx_offload.argtypes = [i32, vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp]
     tl.nicgpu_tune_stream_read.restype = i32
     tl.nicgpu_tune_stream_read.argtypes = [vp, sz, i32, i32, vp, vp]
+    if args.xpf >= 0:
+        tl.nicgpu_tune_set_xpf.argtypes = [u32]
+        tl.nicgpu_tune_set_xpf(args.xpf)
     nv = tl.nicgpu_tune_num_variants()
     names = [tl.nicgpu_tune_variant_name(i).decode() for i in range(nv)]
     variants = list(range(nv)) if args.variants == "all" else [int(x) for x in args.variants.split(",")]
