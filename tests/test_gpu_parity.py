@@ -147,6 +147,53 @@ def test_tso_golden():
     np.testing.assert_array_equal(got, exp)
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_tso_checksum_random_vs_oracle(seed):
+    """nicgpu_tso_checksum on random frames: lengths 0..65535 (frames past
+    9 KiB take several load groups), any byte offset, header 0..L, mss 0,
+    1..15 (several boundaries per chunk), 16..9000; every segment checksum of
+    every frame the oracle accepts (oracle_tso_segment_checksums >= 1)."""
+    rng = np.random.default_rng(100 + seed)
+    n = 1500
+    kind = rng.random(n)
+    lens = np.where(kind < 0.15, rng.integers(0, 100, n),
+                    np.where(kind < 0.8, rng.integers(100, 9217, n), rng.integers(9217, 65536, n)))
+    offs = np.zeros(n, np.int64)
+    pos = 0
+    for i in range(n):
+        pos += int(rng.integers(0, 40))
+        offs[i] = pos
+        pos += int(lens[i])
+    frames = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    mk = rng.random(n)
+    mss = np.where(mk < 0.2, 0, np.where(mk < 0.3, rng.integers(1, 16, n),
+                                         np.where(mk < 0.8, rng.integers(16, 1501, n), rng.integers(1501, 9001, n))))
+    hdr = np.minimum(rng.integers(0, 200, n), lens)
+    exp, nseg = [], np.zeros(n, np.int64)
+    for i in range(n):
+        pkt = frames[offs[i]: offs[i] + lens[i]].tobytes()
+        k, cs = po.tso_segment_checksums(pkt, int(hdr[i]), int(mss[i]))
+        exp.append(cs if k >= 1 else None)
+        L, H, M = int(lens[i]), int(hdr[i]), int(mss[i])
+        seg = M > 0 and L > M and H < L
+        nseg[i] = (L - H + M - 1) // M if seg else 1
+    base = np.concatenate([[0], np.cumsum(nseg)[:-1]]).astype(np.uint32)
+    out = torch.full((int(nseg.sum()),), -1, dtype=torch.int16, device="cuda")
+    f = dev(frames)
+    sna.tso_checksum(f, dev(sna.desc_pack(offs, lens)), dev(hdr.astype(np.uint16)), dev(mss.astype(np.uint16)),
+                     dev(base), out)
+    torch.cuda.synchronize()
+    got = host(out, np.uint16)
+    checked = 0
+    for i in range(n):
+        if exp[i] is None:
+            continue
+        g = int(base[i])
+        assert got[g: g + len(exp[i])].tolist() == exp[i].tolist(), (i, int(lens[i]), int(hdr[i]), int(mss[i]))
+        checked += 1
+    assert checked > n // 2
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_random_layouts_vs_oracle(seed):
     """Random lengths 0..9216 (incl. empty), random byte offsets, n not a
@@ -470,6 +517,45 @@ def test_tso_vlan_segments_golden():
         for k in range(want):
             slot = out[(g + k) * stride: (g + k + 1) * stride]
             assert "%x" % tog._fnv(slot.tobytes()) == c["slot_fnv"][k], (i, k)
+
+
+def test_tso_segment_random_vs_oracle():
+    """nicgpu_tso_segment on random frames: lengths 0..20000 (past 9216 B the
+    kernel copies from global memory instead of its LDS stage), any byte
+    offset, header 0..L+8, mss 0..9100 (incl. < 16 and InvalidMss), random
+    VLAN insert / strip / present and tags; every segment's bytes, length and
+    checksum vs the oracle, and slot bytes past a segment stay untouched."""
+    rng = np.random.default_rng(7)
+    n = 600
+    lens = np.where(rng.random(n) < 0.85, rng.integers(0, 9300, n), rng.integers(9300, 20001, n))
+    offs = np.zeros(n, np.int64)
+    pos = 0
+    for i in range(n):
+        pos += int(rng.integers(0, 24))
+        offs[i] = pos
+        pos += int(lens[i])
+    frames = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    mk = rng.random(n)
+    mss = np.where(mk < 0.1, 0, np.where(mk < 0.2, rng.integers(1, 16, n),
+                                         np.where(mk < 0.95, rng.integers(16, 9001, n), rng.integers(9001, 9100, n))))
+    hdr = np.minimum(rng.integers(0, 120, n), lens + 8)
+    fl = (rng.choice([0, sna.SEG_TSO], n, p=[0.2, 0.8])
+          | rng.choice([0, sna.SEG_VLAN_INSERT, sna.SEG_VLAN_STRIP | sna.SEG_VLAN_PRESENT,
+                        sna.SEG_VLAN_INSERT | sna.SEG_VLAN_STRIP, sna.SEG_VLAN_STRIP], n)
+          | rng.integers(0, 65536, n))
+    stride = 20008
+    cnt, base, out, ol, oc = gpu_tso_segment(frames, sna.desc_pack(offs, lens), hdr, mss, fl, stride)
+    for i in range(n):
+        k, segs, cs = po.tso_segment(frames[offs[i]: offs[i] + lens[i]].tobytes(), int(hdr[i]), int(mss[i]),
+                                     int(fl[i]), stride)
+        assert max(k, 0) == cnt[i], (i, k, int(cnt[i]))
+        g = int(base[i])
+        for j in range(max(k, 0)):
+            assert ol[g + j] == len(segs[j])
+            slot = out[(g + j) * stride: (g + j + 1) * stride]
+            assert slot[: len(segs[j])].tobytes() == segs[j], (i, j)
+            assert not slot[len(segs[j]):].any(), (i, j)
+        assert oc[g: g + max(k, 0)].tolist() == cs
 
 
 def test_tso_segment_c5_vs_oracle():
