@@ -16,7 +16,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnicgpu.so")
+# NICGPU_LIB_AB: tools/ab_rows.sh points this at a side build for same-box A/B timing
+LIB_PATH = os.environ.get("NICGPU_LIB_AB") or os.path.join(_HERE, "libnicgpu.so")
 HOST_LIB_PATH = os.path.join(_HERE, "libnic_host.so")
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 
