@@ -1699,6 +1699,32 @@ constexpr Crc32cTables make_crc32c_tables() {
 }
 __constant__ Crc32cTables kCrc32c = make_crc32c_tables();
 
+// kCrcLead.s[n]: the CRC state that n zero bytes take to 0xFFFFFFFF (the
+// zero-byte step is invertible: the top byte of T0[k] is a permutation of k).
+// A packet starting n bytes into its first 16-B chunk starts from s[n] at byte
+// 0 of that chunk with the n leading bytes masked to zero, so the state is
+// always xored in at byte 0 — no per-chunk shift of the state.
+struct CrcLead {
+  uint32_t s[16];
+};
+constexpr CrcLead make_crc_lead() {
+  const Crc32cTables T = make_crc32c_tables();
+  uint32_t top_inv[256] = {};
+  for (uint32_t k = 0; k < 256; ++k) top_inv[T.t[0][k] >> 24] = k;
+  CrcLead R{};
+  uint32_t s = 0xFFFFFFFFu;
+  R.s[0] = s;
+  for (int n = 1; n < 16; ++n) {
+    const uint32_t k = top_inv[s >> 24];
+    s = ((s ^ T.t[0][k]) << 8) | k;
+    R.s[n] = s;
+  }
+  return R;
+}
+constexpr CrcLead kCrcLeadHost = make_crc_lead();
+static_assert(kCrcLeadHost.s[0] == 0xFFFFFFFFu, "lead table");
+__constant__ CrcLead kCrcLead = make_crc_lead();
+
 struct IcrcParams {
   const uint8_t* frames;
   const uint64_t* desc;
@@ -1710,36 +1736,43 @@ struct IcrcParams {
 
 constexpr int kIcrcRing = 128;  // descriptor ring per wave (LDS)
 
-// One chunk: bytes [a, b) of the 16-B chunk v processed from state S,
-// without shifting data: byte i of the chunk goes through
-// slice table b - 1 - i (the table it would use had the span been shifted to
-// end at byte 15).  T holds 15 all-zero tables in front of the 16 slice
-// tables, so bytes at or past b — zeroed by the mask, and T[*][0] = 0 — may
-// index any row: row (b - 1) + (15 - i), with the (15 - i) KiB an immediate
-// LDS offset.  Per byte: one extract, one address add, one LDS read, one
-// xor; the state is xored in at byte a (masked to the span).
-__device__ __forceinline__ uint32_t crc_chunk_ns(const uint32_t* __restrict__ Text, const uint4* masks, u32x4 v,
-                                                 uint32_t a, uint32_t b, uint32_t S) {
-  const uint4 m1 = masks[a], m2 = masks[16u + b];
-  const uint32_t q = a >> 2, sh = 8u * (a & 3u);
-  const uint32_t lo = S << sh, hi = sh ? S >> (32u - sh) : 0u;
+// One chunk: bytes [0, b) of the 16-B chunk v (bytes before the packet's
+// start already masked by m1) processed from state S, without shifting data:
+// byte i of the chunk goes through slice table b - 1 - i (the table it would
+// use had the span been shifted to end at byte 15).  T holds 15 all-zero
+// tables in front of the 16 slice tables, so bytes at or past b — zeroed by
+// the mask m2, and T[*][0] = 0 — may index any row: row (b - 1) + (15 - i),
+// with the (15 - i) KiB an immediate LDS offset.  Per byte: one extract, one
+// address or, one LDS read, one xor; the state is xored in at byte 0
+// (kCrcLead) and its bytes past b carry over shifted.
+template <bool LEAD>
+__device__ __forceinline__ uint32_t crc_chunk_ns(const uint32_t* __restrict__ Text, const uint4& m1, const uint4& m2,
+                                                 u32x4 v, uint32_t b, uint32_t S) {
   uint32_t x[4];
-  x[0] = (v.x & m1.x & m2.x) ^ ((q == 0u ? lo : 0u) & m2.x);
-  x[1] = (v.y & m1.y & m2.y) ^ ((q == 1u ? lo : (q == 0u ? hi : 0u)) & m2.y);
-  x[2] = (v.z & m1.z & m2.z) ^ ((q == 2u ? lo : (q == 1u ? hi : 0u)) & m2.z);
-  x[3] = (v.w & m1.w & m2.w) ^ ((q == 3u ? lo : (q == 2u ? hi : 0u)) & m2.w);
+  if (LEAD) {
+    x[0] = (v.x & m1.x & m2.x) ^ (S & m2.x);
+    x[1] = v.y & m1.y & m2.y;
+    x[2] = v.z & m1.z & m2.z;
+    x[3] = v.w & m1.w & m2.w;
+  } else {
+    x[0] = (v.x ^ S) & m2.x;
+    x[1] = v.y & m2.y;
+    x[2] = v.z & m2.z;
+    x[3] = v.w & m2.w;
+  }
   const uint32_t* Tb = Text + (b - 1u) * 256u;  // b >= 1 whenever a chunk is processed
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < 16; ++i) c ^= Tb[(15 - i) * 256 + ((x[i >> 2] >> (8 * (i & 3))) & 0xFFu)];
-  const uint32_t h = b - a;
-  return c ^ (h < 4u ? (h ? S >> (8 * h) : S) : 0u);
+  return c ^ (b < 4u ? S >> (8u * b) : 0u);
 }
 
 __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
   __shared__ uint32_t Text[31 * 256];  // 15 zero tables, then the 16 slice tables
   __shared__ uint64_t ring_all[kWavesPerBlock][kIcrcRing];
   __shared__ uint4 masks[kMaskEntries];
+  __shared__ uint32_t lead_s[16];
+  if (threadIdx.x < 16u) lead_s[threadIdx.x] = kCrcLead.s[threadIdx.x];
   for (uint32_t i = threadIdx.x; i < 15u * 256u; i += kBlock) Text[i] = 0u;
   for (uint32_t i = threadIdx.x; i < 16u * 256u; i += kBlock) Text[15u * 256u + i] = (&kCrc32c.t[0][0])[i];
   for (uint32_t i = threadIdx.x; i < kMaskEntries; i += kBlock) {
@@ -1769,16 +1802,20 @@ __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
   refill();
   uint64_t next = p0 + kWave;
   uint64_t my = p0 + lane;
-  uint64_t pos = 0, end = 0, off = 0;
-  uint32_t len = 0, S = 0xFFFFFFFFu;
+  // per lane: the packet's first 16-B chunk and 32-bit byte positions
+  // relative to it (frames are < 64 KiB)
+  uint64_t c16 = 0;
+  uint32_t pos = 0, end = 0, len = 0, lb = 0, S = 0xFFFFFFFFu;
   auto setup = [&]() __attribute__((always_inline)) {
     const uint64_t d = ring[my & (kIcrcRing - 1)];
-    off = d & kOffMask;
+    const uint64_t off = d & kOffMask;
     len = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
     const uint32_t span = P.verify ? (len >= 4u ? len - 4u : 0u) : len;
-    pos = off;
-    end = off + span;
-    S = 0xFFFFFFFFu;
+    c16 = off >> 4;
+    lb = (uint32_t) c16 & 7u;  // chunk of the 128-B line the packet starts in
+    pos = (uint32_t) off & 15u;
+    end = pos + span;
+    S = span ? lead_s[pos] : 0xFFFFFFFFu;
   };
   if (my < p1) setup();
   for (;;) {
@@ -1788,25 +1825,29 @@ __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
       // up to the end of the current 128-B line (8 chunks), so a lane reads
       // every line once (64 B per step fetched most lines twice: 2.2x the
       // algorithmic bytes); loads clamped to the line and the span's end
-      const uint64_t c0 = pos >> 4;
-      const uint64_t clast = end > pos ? (end - 1) >> 4 : c0;
-      const uint64_t cl = (c0 | 7u) < clast ? (c0 | 7u) : clast;
+      const uint32_t c0 = pos >> 4;
+      const uint32_t clast = end > pos ? (end - 1u) >> 4 : c0;
+      const uint32_t ce = ((lb + c0) | 7u) - lb;  // last chunk of c0's line
+      const uint32_t cl = ce < clast ? ce : clast;
       u32x4 v[8] = {};
       if (end > pos) {  // an empty span reads nothing (it may sit at the buffer's end)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const uint64_t c = c0 + u <= cl ? c0 + u : cl;
-          v[u] = f16[c];
-        }
+        for (int u = 0; u < 8; ++u) v[u] = f16[c16 + (c0 + (uint32_t) u <= cl ? c0 + (uint32_t) u : cl)];
       }
+      // only the first chunk of a step can start inside it (a packet's first)
+      const uint32_t a = pos & 15u;
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const uint64_t cb = (c0 + u) << 4;  // chunk base address
-        const uint32_t a = pos > cb ? (uint32_t) (pos - cb) : 0u;
-        const uint32_t b = end > cb ? (end - cb >= 16 ? 16u : (uint32_t) (end - cb)) : 0u;
-        if (c0 + u <= cl && b > a) S = crc_chunk_ns(Text, masks, v[u], a, b, S);
+        const uint32_t cb = (c0 + (uint32_t) u) << 4;  // chunk base, packet-relative
+        const uint32_t b = end > cb ? (end - cb >= 16u ? 16u : end - cb) : 0u;
+        const uint4 m2 = masks[16u + b];
+        if (u == 0) {
+          if (b > a) S = crc_chunk_ns<true>(Text, masks[a], m2, v[0], b, S);
+        } else {
+          if (c0 + (uint32_t) u <= cl && b > 0u) S = crc_chunk_ns<false>(Text, m2, m2, v[u], b, S);
+        }
       }
-      pos = (cl + 1) << 4;
+      pos = (cl + 1u) << 4;
     }
     const bool finished = active && pos >= end;
     if (finished) {
@@ -1815,7 +1856,7 @@ __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
       if (P.verify) {
         uint32_t ok = 0;
         if (len >= 4u) {
-          const uint8_t* t = P.frames + end;
+          const uint8_t* t = P.frames + (c16 << 4) + end;
           const uint32_t stored = ((uint32_t) t[0] << 24) | ((uint32_t) t[1] << 16) | ((uint32_t) t[2] << 8) | t[3];
           ok = stored == crc;
         }
