@@ -1736,45 +1736,35 @@ struct IcrcParams {
 
 constexpr int kIcrcRing = 128;  // descriptor ring per wave (LDS)
 
-// One chunk: bytes [0, b) of the 16-B chunk v (bytes before the packet's
-// start already masked by m1) processed from state S, without shifting data:
-// byte i of the chunk goes through slice table b - 1 - i (the table it would
-// use had the span been shifted to end at byte 15).  T holds 15 all-zero
-// tables in front of the 16 slice tables, so bytes at or past b — zeroed by
-// the mask m2, and T[*][0] = 0 — may index any row: row (b - 1) + (15 - i),
-// with the (15 - i) KiB an immediate LDS offset.  Per byte: one extract, one
-// address or, one LDS read, one xor; the state is xored in at byte 0
-// (kCrcLead) and its bytes past b carry over shifted.
-template <bool LEAD>
-__device__ __forceinline__ uint32_t crc_chunk_ns(const uint32_t* __restrict__ Text, const uint4& m1, const uint4& m2,
-                                                 u32x4 v, uint32_t b, uint32_t S) {
-  uint32_t x[4];
-  if (LEAD) {
-    x[0] = (v.x & m1.x & m2.x) ^ (S & m2.x);
-    x[1] = v.y & m1.y & m2.y;
-    x[2] = v.z & m1.z & m2.z;
-    x[3] = v.w & m1.w & m2.w;
-  } else {
-    x[0] = (v.x ^ S) & m2.x;
-    x[1] = v.y & m2.y;
-    x[2] = v.z & m2.z;
-    x[3] = v.w & m2.w;
-  }
-  const uint32_t* Tb = Text + (b - 1u) * 256u;  // b >= 1 whenever a chunk is processed
-  uint32_t c = 0;
+// One chunk: bytes [0, b) of the 16-B chunk v (0 <= b <= 16; bytes before
+// the packet's start already masked) processed from state S, without shifting
+// data: byte i of the chunk goes through slice table b - 1 - i (the table it
+// would use had the span been shifted to end at byte 15).  T holds 16 all-zero
+// tables in front of the 16 slice tables, so a byte at or past b — whatever
+// its value — reads a zero row: row b + (15 - i), with the (15 - i) KiB an
+// immediate LDS offset, and b = 0 is a no-op chunk.  Per byte: one extract,
+// one address or, one LDS read, half an xor3; the state is xored in at byte 0
+// (kCrcLead) and, for b < 4, its bytes past b carry over shifted.
+__device__ __forceinline__ uint32_t crc_chunk_ns(const uint32_t* __restrict__ Text, u32x4 v, uint32_t b,
+                                                 uint32_t S) {
+  const uint32_t x[4] = {v.x ^ S, v.y, v.z, v.w};
+  const uint32_t* Tb = Text + b * 256u;
+  uint32_t t[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) c ^= Tb[(15 - i) * 256 + ((x[i >> 2] >> (8 * (i & 3))) & 0xFFu)];
+  for (int i = 0; i < 16; ++i) t[i] = Tb[(15 - i) * 256 + ((x[i >> 2] >> (8 * (i & 3))) & 0xFFu)];
+  const uint32_t c = (t[0] ^ t[1] ^ t[2]) ^ (t[3] ^ t[4] ^ t[5]) ^ (t[6] ^ t[7] ^ t[8]) ^ (t[9] ^ t[10] ^ t[11]) ^
+                     (t[12] ^ t[13] ^ t[14]) ^ t[15];
   return c ^ (b < 4u ? S >> (8u * b) : 0u);
 }
 
 __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
-  __shared__ uint32_t Text[31 * 256];  // 15 zero tables, then the 16 slice tables
+  __shared__ uint32_t Text[32 * 256];  // 16 zero tables, then the 16 slice tables
   __shared__ uint64_t ring_all[kWavesPerBlock][kIcrcRing];
   __shared__ uint4 masks[kMaskEntries];
   __shared__ uint32_t lead_s[16];
   if (threadIdx.x < 16u) lead_s[threadIdx.x] = kCrcLead.s[threadIdx.x];
-  for (uint32_t i = threadIdx.x; i < 15u * 256u; i += kBlock) Text[i] = 0u;
-  for (uint32_t i = threadIdx.x; i < 16u * 256u; i += kBlock) Text[15u * 256u + i] = (&kCrc32c.t[0][0])[i];
+  for (uint32_t i = threadIdx.x; i < 16u * 256u; i += kBlock) Text[i] = 0u;
+  for (uint32_t i = threadIdx.x; i < 16u * 256u; i += kBlock) Text[16u * 256u + i] = (&kCrc32c.t[0][0])[i];
   for (uint32_t i = threadIdx.x; i < kMaskEntries; i += kBlock) {
     const int lo = i < 16u ? (int) i : 0, hi = i < 16u ? 16 : (int) i - 16;
     masks[i] = make_uint4(dword_keep(lo, hi, 0), dword_keep(lo, hi, 1), dword_keep(lo, hi, 2), dword_keep(lo, hi, 3));
@@ -1815,7 +1805,7 @@ __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
     lb = (uint32_t) c16 & 7u;  // chunk of the 128-B line the packet starts in
     pos = (uint32_t) off & 15u;
     end = pos + span;
-    S = span ? lead_s[pos] : 0xFFFFFFFFu;
+    S = lead_s[pos];  // an empty span runs its pos zero bytes back to 0xFFFFFFFF
   };
   if (my < p1) setup();
   for (;;) {
@@ -1834,18 +1824,25 @@ __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = f16[c16 + (c0 + (uint32_t) u <= cl ? c0 + (uint32_t) u : cl)];
       }
-      // only the first chunk of a step can start inside it (a packet's first)
+      // only the first chunk of a step can start inside it (a packet's first):
+      // its leading bytes are masked; chunks past cl (the line or the span)
+      // get b = 0, a no-op, so every lane runs the same straight-line code
       const uint32_t a = pos & 15u;
+      const uint32_t nc = cl - c0;            // chunks this step, minus one
+      const int32_t er = (int32_t) (end - (c0 << 4));  // span end from c0's base
+      {
+        const uint4 m1 = masks[a];
+        v[0].x &= m1.x;
+        v[0].y &= m1.y;
+        v[0].z &= m1.z;
+        v[0].w &= m1.w;
+      }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const uint32_t cb = (c0 + (uint32_t) u) << 4;  // chunk base, packet-relative
-        const uint32_t b = end > cb ? (end - cb >= 16u ? 16u : end - cb) : 0u;
-        const uint4 m2 = masks[16u + b];
-        if (u == 0) {
-          if (b > a) S = crc_chunk_ns<true>(Text, masks[a], m2, v[0], b, S);
-        } else {
-          if (c0 + (uint32_t) u <= cl && b > 0u) S = crc_chunk_ns<false>(Text, m2, m2, v[u], b, S);
-        }
+        const int32_t r = er - 16 * u;
+        uint32_t b = (uint32_t) (r < 0 ? 0 : (r > 16 ? 16 : r));
+        if ((uint32_t) u > nc) b = 0u;
+        S = crc_chunk_ns(Text, v[u], b, S);
       }
       pos = (cl + 1u) << 4;
     }
