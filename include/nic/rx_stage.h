@@ -149,13 +149,17 @@ public:
   /// hipStream_t; nullptr = default stream) before returning.
   RxBatchResult process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                               std::span<const RxDescriptor> rx, void* stream = nullptr);
+  /// The same into `out`, reusing its storage: a caller that keeps one
+  /// RxBatchResult across batches takes no page faults for the results.
+  void process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+                     RxBatchResult& out, void* stream = nullptr);
 
   [[nodiscard]] const QueuePairStats& stats() const noexcept { return stats_; }
   void reset_stats() noexcept { stats_ = QueuePairStats{}; }
   [[nodiscard]] const BatchedQueuePairConfig& config() const noexcept { return config_; }
 
 private:
-  struct Scratch;  // device buffers reused across batches (grown, never shrunk)
+  struct Scratch;  // device, pinned and host buffers reused across batches (grown, never shrunk)
   BatchedQueuePairConfig config_;
   QueuePairStats stats_{};
   std::unique_ptr<Scratch> scratch_;
@@ -208,6 +212,9 @@ struct SegmentWrite {
 static_assert(sizeof(SegmentWrite) == 40);
 
 Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx);
+/// The same into `plan`, reusing its storage (no page faults once it has grown).
+void make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
+               Plan& plan);
 
 /// Sequential resolution of the batch, given piece_csum[i] =
 /// compute_checksum(bytes of plan.pieces[i]).  Appends completions to `out`,

@@ -80,6 +80,10 @@ int nicgpu_get_device(int* device);
 int nicgpu_set_device(int device);
 int nicgpu_malloc(void** dev_ptr, size_t bytes);
 int nicgpu_free(void* dev_ptr);
+/* Page-locked host memory (hipHostMalloc), for staging descriptor and result
+ * arrays at full PCIe rate. */
+int nicgpu_host_alloc(void** host_ptr, size_t bytes);
+int nicgpu_host_free(void* host_ptr);
 int nicgpu_memset_async(void* dev_ptr, int value, size_t bytes, void* stream);
 /* Copies in any direction (hipMemcpyDefault), enqueued on `stream`. */
 int nicgpu_memcpy_async(void* dst, const void* src, size_t bytes, void* stream);

@@ -49,6 +49,8 @@ ABI_SYMBOLS = (
     "nicgpu_set_device",
     "nicgpu_malloc",
     "nicgpu_free",
+    "nicgpu_host_alloc",
+    "nicgpu_host_free",
     "nicgpu_memset_async",
     "nicgpu_memcpy_async",
     "nicgpu_stream_synchronize",

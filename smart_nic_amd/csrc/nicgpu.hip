@@ -2082,6 +2082,17 @@ int nicgpu_malloc(void** dev_ptr, size_t bytes) {
 
 int nicgpu_free(void* dev_ptr) { return (!dev_ptr || hipFree(dev_ptr) == hipSuccess) ? NICGPU_OK : NICGPU_ERR_HIP; }
 
+int nicgpu_host_alloc(void** host_ptr, size_t bytes) {
+  if (!host_ptr) return NICGPU_ERR_INVALID;
+  *host_ptr = nullptr;
+  if (bytes == 0) return NICGPU_OK;
+  return hipHostMalloc(host_ptr, bytes, hipHostMallocDefault) == hipSuccess ? NICGPU_OK : NICGPU_ERR_NOMEM;
+}
+
+int nicgpu_host_free(void* host_ptr) {
+  return (!host_ptr || hipHostFree(host_ptr) == hipSuccess) ? NICGPU_OK : NICGPU_ERR_HIP;
+}
+
 int nicgpu_memset_async(void* dev_ptr, int value, size_t bytes, void* stream) {
   if (bytes == 0) return NICGPU_OK;
   if (!dev_ptr) return NICGPU_ERR_INVALID;

@@ -125,10 +125,12 @@ int main(int argc, char** argv) {
   RxBatchResult last;
   for (int r = 0; r < reps + 1; ++r) {
     const auto t0 = std::chrono::steady_clock::now();
-    RxBatchResult res = qp.process_batch(dm, tx, rx);
+    qp.process_batch(dm, tx, rx, last);  // one result object reused across batches
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     if (r > 0) tot.push_back(us);
-    last = std::move(res);
+    const auto& P = last.timings;
+    std::fprintf(stderr, "rep %d: %.0f us (plan %.0f sums %.0f resolve %.0f gather %.0f rss %.0f)\n", r, us, P.plan_us,
+                 P.sums_us, P.resolve_us, P.gather_us, P.rss_us);
   }
   std::sort(tot.begin(), tot.end());
   const double med = tot[tot.size() / 2];
