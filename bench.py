@@ -92,6 +92,61 @@ def cpu_baseline(frames, desc, table, gpu_out, n_sample_mt, n_sample_1):
     }
 
 
+def cpu_rows_baseline(pktgen):
+    """The CPU side of the other SURVEY §8 rows, beside the GPU numbers in
+    DESIGN.md §5 (bounded samples, this host): C3 IMIX RX through the compiled
+    reference (16 threads and 1 core), and — the reference TUs for these are
+    not buildable here or have no batch entry point — the oracle restatement
+    on one core for the C5 TSO segment checksums and the C2 ICRC."""
+    import ctypes
+
+    from oracle import pyoracle as po
+
+    vp = ctypes.c_void_p
+    rows = []
+    ref = po.ref_lib()
+    cores = min(16, os.cpu_count() or 1)
+    n3 = 1 << 18
+    lens = pktgen.imix_lengths(n3, np.random.default_rng(33))
+    f3, d3, _ = pktgen.make_batch(lens, seed=33, proto=17, corrupt_frac=0.01)
+    k = np.frombuffer(MS_KEY, np.uint8)
+    t16 = (np.arange(128) % 16).astype(np.uint16)
+    cs = np.zeros(n3, np.uint16)
+    q = np.zeros(n3, np.uint16)
+    if ref is not None:
+        def rx(n, threads):
+            t0 = time.perf_counter()
+            ref.ref_rx_batch(f3.ctypes.data, d3.ctypes.data, n, 1, k.ctypes.data, k.size, t16.ctypes.data, t16.size,
+                             cs.ctypes.data, q.ctypes.data, threads)
+            return time.perf_counter() - t0
+        dtm, dt1 = rx(n3, cores), rx(1 << 16, 1)
+        rows.append({"row": "rx_c3", "value": round(n3 / dtm / 1e6, 4), "unit": "Mpkt/s", "cores": cores,
+                     "kind": "reference", "value_1core": round((1 << 16) / dt1 / 1e6, 4),
+                     "sample": f"{n3} IMIX frames (7:4:1 64/576/1518 B), 16 queues; 1 core over 65536"})
+    L = po.lib()
+    n5 = 4096
+    f5, d5, _ = pktgen.make_batch(np.full(n5, 9000), seed=55, proto=6, corrupt_frac=0.0)
+    h = np.full(n5, 54, np.uint16)
+    m = np.full(n5, 1448, np.uint16)
+    out = np.zeros(n5 * 64, np.uint16)
+    t0 = time.perf_counter()
+    nseg = L.oracle_tso_checksum_batch(vp(f5.ctypes.data), vp(d5.ctypes.data), n5, vp(h.ctypes.data),
+                                       vp(m.ctypes.data), vp(out.ctypes.data))
+    dt = time.perf_counter() - t0
+    rows.append({"row": "tso_c5", "value": round(n5 / dt / 1e6, 4), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+                 "gbs": round(n5 * 9000 / dt / 1e9, 4),
+                 "sample": f"{n5} x 9000 B frames, H 54, mss 1448 ({nseg} segment checksums)"})
+    n2 = 1 << 15
+    f2, d2, _ = pktgen.make_batch(np.full(n2, 1518), seed=42, proto=6, corrupt_frac=0.0)
+    crc = np.zeros(n2, np.uint32)
+    t0 = time.perf_counter()
+    L.oracle_icrc_batch(vp(f2.ctypes.data), vp(d2.ctypes.data), n2, vp(crc.ctypes.data))
+    dt = time.perf_counter() - t0
+    rows.append({"row": "icrc_c2", "value": round(n2 / dt / 1e6, 4), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+                 "gbs": round(n2 * 1518 / dt / 1e9, 4), "sample": f"{n2} x 1518 B spans, CRC-32C"})
+    return rows
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -121,7 +176,7 @@ def main():
     ap.add_argument("--packets", type=int, default=N_PER_GPU, help="packets per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01f_pmc_c2.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01g_pmc_c2.json"))
     args = ap.parse_args()
 
     import torch
@@ -262,6 +317,7 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(frames, desc, table, (g_cs, g_q),
                                            n_sample_mt=min(n, 1 << 18), n_sample_1=min(n, 1 << 16))
+        out["cpu_baseline"]["other_rows"] = cpu_rows_baseline(pktgen)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

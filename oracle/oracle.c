@@ -304,3 +304,23 @@ int oracle_tso_segment(const uint8_t* pkt, size_t len, uint16_t hdr_len, uint16_
   }
   return (int) nseg;
 }
+
+/* ---- batch loops (bench.py CPU baseline) ---- */
+size_t oracle_tso_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n, const uint16_t* hdr_len,
+                                 const uint16_t* mss, uint16_t* out_csum) {
+  size_t w = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t off = desc[i] & ((1ull << 40) - 1);
+    const size_t len = (size_t) (desc[i] >> 40);
+    const int r = oracle_tso_segment_checksums(frames + off, len, hdr_len[i], mss[i], 1, out_csum + w, 64);
+    if (r > 0) w += (size_t) r;
+  }
+  return w;
+}
+
+void oracle_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, uint32_t* out_crc) {
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t off = desc[i] & ((1ull << 40) - 1);
+    out_crc[i] = oracle_icrc_calculate(frames + off, (size_t) (desc[i] >> 40));
+  }
+}

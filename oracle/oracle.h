@@ -117,6 +117,14 @@ int oracle_tso_segment(const uint8_t* pkt, size_t len, uint16_t hdr_len, uint16_
 uint32_t oracle_icrc_calculate(const uint8_t* buf, size_t len);
 int oracle_icrc_verify(const uint8_t* buf, size_t len);
 
+/* Batch loops over the functions above, for bench.py's CPU-baseline leg only
+ * (one core; descriptors as in oracle_rx_batch).  out_csum receives every
+ * frame's segment checksums back to back (at most 64 per frame); returns the
+ * number written. */
+size_t oracle_tso_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n, const uint16_t* hdr_len,
+                                 const uint16_t* mss, uint16_t* out_csum);
+void oracle_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, uint32_t* out_crc);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,10 @@ def lib():
         L.oracle_tso_segment.argtypes = [vp, sz, u16, u16, u32, vp, sz, sz, vp, vp]
         L.oracle_icrc_calculate.restype = u32
         L.oracle_icrc_calculate.argtypes = [vp, sz]
+        L.oracle_tso_checksum_batch.restype = sz
+        L.oracle_tso_checksum_batch.argtypes = [vp, vp, sz, vp, vp, vp]
+        L.oracle_icrc_batch.restype = None
+        L.oracle_icrc_batch.argtypes = [vp, vp, sz, vp]
         L.oracle_icrc_verify.restype = i32
         L.oracle_icrc_verify.argtypes = [vp, sz]
         _o = L
