@@ -113,6 +113,11 @@ struct BatchedQueuePairConfig {
   /// RSS over delivered frames; nullptr = no dispatch.  Not owned.
   RssEngine* rss{nullptr};
   TupleSpec tuple{};
+  /// Threads for the host phases (plan, piece descriptors, resolve): 0 uses
+  /// up to 16 on batches of 32 K descriptors and more (resolve stays
+  /// sequential with an interrupt callback, or when most packets are
+  /// multi-segment); 1 runs them all on the calling thread.
+  unsigned host_threads{0};
 };
 
 struct RxBatchResult {
@@ -216,14 +221,24 @@ Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
 void make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
                Plan& plan);
 
-/// Sequential resolution of the batch, given piece_csum[i] =
-/// compute_checksum(bytes of plan.pieces[i]).  Appends completions to `out`,
-/// updates `stats`, fires interrupts, and lists the DMA writes to perform
-/// (write_of_rx[j] = index into writes of RX completion j, or -1).
+/// The reference's sequential control flow over the batch, given
+/// piece_csum[i] = compute_checksum(bytes of plan.pieces[i]).  Fills
+/// out.tx_completions / out.rx_completions (replacing their contents), sets
+/// out.tx_processed / rx_consumed, adds to `stats`, fires interrupts in
+/// posting order, and lists the DMA writes: writes[j] belongs to RX completion
+/// j (zero-length when nothing reached the buffer) and write_of_rx[j] = j, or
+/// -1 when nothing was written.
+/// Without an interrupt callback it runs on `max_threads` threads (0: as
+/// config.host_threads says; a nonzero value also drops the 32 K minimum, for
+/// tests): every packet's ring position is predicted by a
+/// scan that assumes no RX-side abort before a packet's last segment, chunks
+/// resolve in parallel from their predicted positions, and the batch is
+/// finished sequentially from the first packet whose pops differ.  The result
+/// equals the sequential one.
 void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
              std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
              std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
-             std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx);
+             std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx, unsigned max_threads = 0);
 
 }  // namespace rx_stage_detail
 

@@ -50,9 +50,9 @@ bool dma_ok(std::size_t mem_size, std::uint64_t addr, std::uint64_t len) {
 // Both passes of a count/fill pair see the same partition.
 struct Chunks {
   std::size_t n, k;
-  explicit Chunks(std::size_t n_, std::size_t max_threads = 16) : n(n_) {
+  explicit Chunks(std::size_t n_, std::size_t max_threads = 16, std::size_t grain = 32768) : n(n_) {
     const std::size_t hw = std::max(1u, std::thread::hardware_concurrency());
-    k = std::max<std::size_t>(1, std::min<std::size_t>({hw, max_threads, n / 32768}));
+    k = std::max<std::size_t>(1, std::min<std::size_t>({hw, max_threads, n / grain}));
   }
   std::size_t begin(std::size_t c) const { return n * c / k; }
   template <class F>
@@ -224,7 +224,7 @@ Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
 void make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
                Plan& plan) {
   plan.packets.resize(tx.size());
-  const Chunks ch(tx.size());
+  const Chunks ch(tx.size(), config.host_threads ? config.host_threads : 16);
   std::vector<std::size_t> base(ch.k + 1, 0);
   ch.run([&](std::size_t c, std::size_t b, std::size_t e) {
     std::size_t n = 0;
@@ -244,199 +244,365 @@ void make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
   });
 }
 
+namespace {
+
+void add_stats(QueuePairStats& a, const QueuePairStats& b) {
+  a.tx_packets += b.tx_packets;
+  a.rx_packets += b.rx_packets;
+  a.tx_bytes += b.tx_bytes;
+  a.rx_bytes += b.rx_bytes;
+  a.drops_checksum += b.drops_checksum;
+  a.drops_no_rx_desc += b.drops_no_rx_desc;
+  a.drops_buffer_small += b.drops_buffer_small;
+  a.drops_mtu_exceeded += b.drops_mtu_exceeded;
+  a.drops_invalid_mss += b.drops_invalid_mss;
+  a.drops_too_many_segments += b.drops_too_many_segments;
+  a.tx_tso_segments += b.tx_tso_segments;
+  a.tx_gso_segments += b.tx_gso_segments;
+  a.tx_vlan_insertions += b.tx_vlan_insertions;
+  a.rx_vlan_strips += b.rx_vlan_strips;
+  a.rx_checksum_verified += b.rx_checksum_verified;
+  a.rx_gro_aggregated += b.rx_gro_aggregated;
+}
+
+struct ResolveCtx {
+  const BatchedQueuePairConfig& config;
+  std::size_t mem_size;
+  const Plan& plan;
+  std::span<const std::uint16_t> cs;
+  std::span<const TxDescriptor> tx;
+  std::span<const RxDescriptor> rx;
+};
+
+CompletionEntry make_completion(std::uint16_t qid, std::uint16_t idx, CompletionCode st) {  // :150-158
+  CompletionEntry e{};
+  e.queue_id = qid;
+  e.descriptor_index = idx;
+  e.status = static_cast<std::uint32_t>(st);
+  return e;
+}
+
+CompletionEntry make_tx(std::uint16_t qid, const TxDescriptor& t, CompletionCode st, std::size_t segs, bool tso,
+                        bool gso) {  // :160-177
+  CompletionEntry e = make_completion(qid, t.descriptor_index, st);
+  e.checksum_offloaded = t.checksum_offload;
+  e.tso_performed = tso;
+  e.gso_performed = gso;
+  e.segments_produced = static_cast<std::uint16_t>(std::min<std::size_t>(segs, std::numeric_limits<std::uint16_t>::max()));
+  if (t.vlan_insert) {
+    e.vlan_inserted = true;
+    e.vlan_tag = t.vlan_tag;
+  }
+  return e;
+}
+
+// RX descriptors TX descriptor i pops when the ring has enough of them and no
+// RX-side check aborts it early: 0 when it is dropped before the RX stage
+// (read fault, TX checksum, MTU, invalid mss, too many segments).
+std::size_t rx_need(const ResolveCtx& C, std::size_t i) {
+  const TxDescriptor& t = C.tx[i];
+  const std::uint64_t L = t.length;
+  if (!dma_ok(C.mem_size, t.buffer_address, L)) return 0;
+  if (tx_verify_needed(t)) {
+    const PacketSums ps{&C.plan.packets[i], C.cs, L};
+    if (static_cast<std::uint16_t>(~ps.whole() & 0xFFFFu) != t.checksum_value) return 0;
+  }
+  if (L > C.config.max_mtu) return 0;
+  const SegDecision d = decide_segments(t);
+  if (d.invalid_mss || d.too_many) return 0;
+  return d.nseg;
+}
+
+// QueuePair::process_once (queue_pair.cpp:67-460) for TX descriptor i with
+// the RX ring's consumer at rc: posts its completions through `sink`, adds to
+// `stats`, returns the RX descriptors it popped.  sink.tx(entry, fire) and
+// sink.rx(entry, write or nullptr) see the reference's posting order.
+template <class Sink>
+std::size_t resolve_packet(const ResolveCtx& C, std::size_t i, std::size_t rc, QueuePairStats& stats, Sink& sink) {
+  const std::uint16_t qid = C.config.queue_id;
+  const TxDescriptor& t = C.tx[i];
+  const PacketSums ps{&C.plan.packets[i], C.cs, t.length};
+  const std::uint64_t L = t.length;
+  const std::size_t rc0 = rc;
+  // :75-83 no RX descriptor at all
+  if (rc == C.rx.size()) {
+    sink.tx(make_tx(qid, t, CompletionCode::NoDescriptor, 0, false, false), true);
+    stats.drops_no_rx_desc += 1;
+    return 0;
+  }
+  // :86-92 DMA read
+  if (!dma_ok(C.mem_size, t.buffer_address, L)) {
+    sink.tx(make_tx(qid, t, CompletionCode::Fault, 0, false, false), true);
+    return 0;
+  }
+  // :94-105 TX checksum verify
+  if (tx_verify_needed(t)) {
+    const std::uint16_t computed = static_cast<std::uint16_t>(~ps.whole() & 0xFFFFu);
+    if (computed != t.checksum_value) {
+      sink.tx(make_tx(qid, t, CompletionCode::ChecksumError, 0, false, false), true);
+      stats.drops_checksum += 1;
+      return 0;
+    }
+  }
+  // :195-210 MTU
+  if (L > C.config.max_mtu) {
+    sink.tx(make_tx(qid, t, CompletionCode::MtuExceeded, 0, false, false), true);
+    stats.drops_mtu_exceeded += 1;
+    return 0;
+  }
+  // :212-278 segmentation
+  const SegDecision d = decide_segments(t);
+  if (d.invalid_mss) {
+    sink.tx(make_tx(qid, t, CompletionCode::InvalidMss, 0, false, false), true);
+    stats.drops_invalid_mss += 1;
+    return 0;
+  }
+  if (d.too_many) {
+    sink.tx(make_tx(qid, t, CompletionCode::TooManySegments, 0, false, false), true);
+    stats.drops_too_many_segments += 1;
+    return 0;
+  }
+  const std::uint32_t total = d.nseg;
+  const bool tso = t.tso_enabled && total > 1;
+  const bool gso = t.gso_enabled && total > 1;
+  // :293-303 enough RX descriptors for every segment
+  if (C.rx.size() - rc < total) {
+    sink.tx(make_tx(qid, t, CompletionCode::NoDescriptor, 0, tso, gso), true);
+    stats.drops_no_rx_desc += 1;
+    return 0;
+  }
+  for (std::uint32_t k = 0; k < total; ++k) {
+    RxDescriptor x = C.rx[rc++];
+    if (t.vlan_insert) x.vlan_present = true;  // :320-322
+    // base segment = header || chunk k (or the whole packet)
+    std::uint64_t src_a = t.buffer_address, src_b = 0;
+    std::uint32_t len_a, len_b = 0;
+    if (d.segmented) {
+      len_a = d.H;
+      src_b = t.buffer_address + d.H + static_cast<std::uint64_t>(k) * t.mss;
+      len_b = ps.chunk_len(k);
+    } else {
+      len_a = static_cast<std::uint32_t>(L);
+    }
+    const std::uint64_t base_len = static_cast<std::uint64_t>(len_a) + len_b;
+    // :324-331 VLAN insert, :389-395 strip
+    std::uint64_t size = base_len + (t.vlan_insert ? 4 : 0);
+    const bool has_vlan = t.vlan_insert || x.vlan_present;
+    const bool strip = x.vlan_strip && has_vlan && size >= 4;
+    if (strip) size -= 4;
+    const bool prefix = t.vlan_insert && !strip;
+    const bool strip_base = strip && !t.vlan_insert;  // the base segment loses its first 4 bytes
+    // :397-414 buffer too small
+    if (x.buffer_length < size) {
+      sink.tx(make_tx(qid, t, CompletionCode::Success, total, tso, gso), false);
+      CompletionEntry e = make_completion(qid, x.descriptor_index, CompletionCode::BufferTooSmall);
+      e.vlan_stripped = x.vlan_strip && has_vlan;
+      if (e.vlan_stripped) e.vlan_tag = t.vlan_insert ? t.vlan_tag : x.vlan_tag;
+      sink.rx(e, nullptr);
+      stats.drops_buffer_small += 1;
+      return rc - rc0;
+    }
+    // :416-426 DMA write
+    if (!dma_ok(C.mem_size, x.buffer_address, size)) {
+      sink.tx(make_tx(qid, t, CompletionCode::Fault, total, tso, gso), false);
+      sink.rx(make_completion(qid, x.descriptor_index, CompletionCode::Fault), nullptr);
+      return rc - rc0;
+    }
+    SegmentWrite w{};
+    w.dst = x.buffer_address;
+    if (prefix) {
+      const std::uint32_t tag = t.vlan_tag;
+      w.prefix = 0x81u | (0x00u << 8) | (((tag >> 8) & 0xFFu) << 16) | ((tag & 0xFFu) << 24);
+      w.prefix_len = 4;
+    }
+    if (strip_base) {  // drop the first 4 bytes of header || chunk
+      const std::uint32_t from_a = std::min<std::uint32_t>(4, len_a);
+      src_a += from_a;
+      len_a -= from_a;
+      src_b += 4 - from_a;
+      len_b -= 4 - from_a;
+    }
+    w.src_a = src_a;
+    w.len_a = len_a;
+    w.src_b = src_b;
+    w.len_b = len_b;
+
+    CompletionEntry e = make_completion(qid, x.descriptor_index, CompletionCode::Success);
+    e.gro_aggregated = x.gro_enabled;
+    if (e.gro_aggregated) stats.rx_gro_aggregated += 1;
+    // :434-447 RX checksum verify of the delivered bytes
+    if (x.checksum_offload && x.checksum != ChecksumMode::None) {
+      e.checksum_verified = true;
+      stats.rx_checksum_verified += 1;
+      std::uint32_t first4, rest;
+      ps.segment(k, first4, rest);
+      std::uint32_t sum;
+      if (strip_base) sum = rest;
+      else sum = add1c(first4, rest);
+      if (prefix) sum = add1c(add1c(0x8100u, t.vlan_tag), sum);
+      if ((~sum & 0xFFFFu) != 0) {
+        e.status = static_cast<std::uint32_t>(CompletionCode::ChecksumError);
+        sink.rx(e, &w);
+        sink.tx(make_tx(qid, t, CompletionCode::Success, total, tso, gso), false);
+        stats.drops_checksum += 1;
+        return rc - rc0;
+      }
+    }
+    e.vlan_stripped = x.vlan_strip && has_vlan;
+    if (e.vlan_stripped) {
+      e.vlan_tag = t.vlan_insert ? t.vlan_tag : x.vlan_tag;
+      stats.rx_vlan_strips += 1;
+    }
+    sink.rx(e, &w);
+    stats.rx_packets += 1;
+    stats.rx_bytes += size;
+  }
+  // :280-301 finalize_tx_success
+  sink.tx(make_tx(qid, t, CompletionCode::Success, total, tso, gso), true);
+  stats.tx_packets += total;
+  stats.tx_bytes += L;
+  if (tso) stats.tx_tso_segments += total;
+  if (gso) stats.tx_gso_segments += total;
+  if (t.vlan_insert) stats.tx_vlan_insertions += total;
+  return rc - rc0;
+}
+
+// Appends, firing interrupts in posting order (:371-383).
+struct AppendSink {
+  const BatchedQueuePairConfig& config;
+  RxBatchResult& out;
+  std::vector<SegmentWrite>& writes;
+  std::vector<std::int64_t>& write_of_rx;
+  void tx(const CompletionEntry& e, bool fire) {
+    out.tx_completions.push_back(e);
+    if (fire && config.enable_tx_interrupts && config.on_interrupt) config.on_interrupt(config.queue_id, e);
+  }
+  void rx(const CompletionEntry& e, const SegmentWrite* w) {
+    const std::int64_t j = static_cast<std::int64_t>(out.rx_completions.size());
+    out.rx_completions.push_back(e);
+    writes.push_back(w ? *w : SegmentWrite{});
+    write_of_rx.push_back(w ? j : -1);
+    if (config.enable_rx_interrupts && config.on_interrupt) config.on_interrupt(config.queue_id, e);
+  }
+};
+
+// Writes at known positions (no interrupts: the parallel path runs only
+// without an interrupt callback).
+struct PlaceSink {
+  CompletionEntry* txc;
+  CompletionEntry* rxc;
+  SegmentWrite* w;
+  std::int64_t* wof;
+  std::size_t ti = 0, rj = 0;  // next TX slot, next RX slot
+  void tx(const CompletionEntry& e, bool) { txc[ti] = e; }
+  void rx(const CompletionEntry& e, const SegmentWrite* sw) {
+    rxc[rj] = e;
+    w[rj] = sw ? *sw : SegmentWrite{};
+    wof[rj] = sw ? static_cast<std::int64_t>(rj) : -1;
+    ++rj;
+  }
+};
+
+}  // namespace
+
 void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
              std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
              std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
-             std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx) {
-  const std::uint16_t qid = config.queue_id;
-  auto post_tx = [&](const CompletionEntry& e, bool fire) {
-    out.tx_completions.push_back(e);
-    if (fire && config.enable_tx_interrupts && config.on_interrupt) config.on_interrupt(qid, e);  // :371-376
-  };
-  auto post_rx = [&](const CompletionEntry& e, std::int64_t w) {
-    out.rx_completions.push_back(e);
-    write_of_rx.push_back(w);
-    if (config.enable_rx_interrupts && config.on_interrupt) config.on_interrupt(qid, e);  // :378-383
-  };
-  auto make_completion = [&](std::uint16_t idx, CompletionCode st) {  // :150-158
-    CompletionEntry e{};
-    e.queue_id = qid;
-    e.descriptor_index = idx;
-    e.status = static_cast<std::uint32_t>(st);
-    return e;
-  };
-  auto make_tx = [&](const TxDescriptor& t, CompletionCode st, std::size_t segs, bool tso, bool gso) {  // :160-177
-    CompletionEntry e = make_completion(t.descriptor_index, st);
-    e.checksum_offloaded = t.checksum_offload;
-    e.tso_performed = tso;
-    e.gso_performed = gso;
-    e.segments_produced = static_cast<std::uint16_t>(std::min<std::size_t>(segs, std::numeric_limits<std::uint16_t>::max()));
-    if (t.vlan_insert) {
-      e.vlan_inserted = true;
-      e.vlan_tag = t.vlan_tag;
-    }
-    return e;
-  };
-
-  out.tx_completions.reserve(out.tx_completions.size() + tx.size());
-  out.rx_completions.reserve(out.rx_completions.size() + std::min(tx.size(), rx.size()));
-  write_of_rx.reserve(write_of_rx.size() + std::min(tx.size(), rx.size()));
-  writes.reserve(writes.size() + std::min(tx.size(), rx.size()));
-  std::size_t rc = 0;  // RX ring consumer position
-  for (std::size_t i = 0; i < tx.size(); ++i) {
-    const TxDescriptor& t = tx[i];
-    const PacketPlan& pp = plan.packets[i];
-    const PacketSums ps{&pp, piece_csum, t.length};
-    const std::uint64_t L = t.length;
-    // :75-83 no RX descriptor at all
-    if (rc == rx.size()) {
-      post_tx(make_tx(t, CompletionCode::NoDescriptor, 0, false, false), true);
-      stats.drops_no_rx_desc += 1;
-      continue;
-    }
-    // :86-92 DMA read
-    if (!dma_ok(mem_size, t.buffer_address, L)) {
-      post_tx(make_tx(t, CompletionCode::Fault, 0, false, false), true);
-      continue;
-    }
-    // :94-105 TX checksum verify
-    if (tx_verify_needed(t)) {
-      const std::uint16_t computed = static_cast<std::uint16_t>(~ps.whole() & 0xFFFFu);
-      if (computed != t.checksum_value) {
-        post_tx(make_tx(t, CompletionCode::ChecksumError, 0, false, false), true);
-        stats.drops_checksum += 1;
-        continue;
+             std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx, unsigned max_threads) {
+  const ResolveCtx C{config, mem_size, plan, piece_csum, tx, rx};
+  const std::size_t n = tx.size();
+  const std::size_t want = max_threads ? max_threads : (config.host_threads ? config.host_threads : 16);
+  const Chunks ch(n, config.on_interrupt ? 1 : want, max_threads ? 1 : 32768);
+  std::size_t from = 0, rc = 0;  // first TX descriptor the sequential pass resolves, and its ring position
+  std::size_t nmulti = 0;         // packets of more than one segment (only they can abort early)
+  static thread_local std::vector<std::uint32_t> need_tl;
+  static thread_local std::vector<std::size_t> pos_tl;
+  // the calling thread's buffers, by reference: a worker naming need_tl
+  // would get its own (empty) instance
+  std::vector<std::uint32_t>& need = need_tl;
+  std::vector<std::size_t>& pos = pos_tl;
+  if (ch.k > 1) {
+    // (1) RX descriptors each packet would pop, in parallel; (2) the ring
+    // position of every packet by a scan, assuming no packet aborts before
+    // its last segment; (3) every chunk resolved in parallel from its exact
+    // position into its slots.  A chunk stops at the first packet that pops
+    // a different number of descriptors (an RX-side abort before the last
+    // segment); the batch is then finished sequentially from that packet.
+    // (need, pos: per calling thread, reused, so steady batches take no page faults)
+    need.resize(n);
+    pos.resize(n + 1);
+    std::vector<std::size_t> multi(ch.k, 0);
+    ch.run([&](std::size_t c, std::size_t b, std::size_t e) {
+      std::size_t m = 0;
+      for (std::size_t i = b; i < e; ++i) {
+        need[i] = static_cast<std::uint32_t>(rx_need(C, i));
+        m += need[i] > 1;
       }
-    }
-    // :195-210 MTU
-    if (L > config.max_mtu) {
-      post_tx(make_tx(t, CompletionCode::MtuExceeded, 0, false, false), true);
-      stats.drops_mtu_exceeded += 1;
-      continue;
-    }
-    // :212-278 segmentation
-    const SegDecision d = decide_segments(t);
-    if (d.invalid_mss) {
-      post_tx(make_tx(t, CompletionCode::InvalidMss, 0, false, false), true);
-      stats.drops_invalid_mss += 1;
-      continue;
-    }
-    if (d.too_many) {
-      post_tx(make_tx(t, CompletionCode::TooManySegments, 0, false, false), true);
-      stats.drops_too_many_segments += 1;
-      continue;
-    }
-    const std::uint32_t total = d.nseg;
-    const bool tso = t.tso_enabled && total > 1;
-    const bool gso = t.gso_enabled && total > 1;
-    // :293-303 enough RX descriptors for every segment
-    if (rx.size() - rc < total) {
-      post_tx(make_tx(t, CompletionCode::NoDescriptor, 0, tso, gso), true);
-      stats.drops_no_rx_desc += 1;
-      continue;
-    }
-    bool aborted = false;
-    for (std::uint32_t k = 0; k < total; ++k) {
-      RxDescriptor x = rx[rc++];
-      if (t.vlan_insert) x.vlan_present = true;  // :320-322
-      // base segment = header || chunk k (or the whole packet)
-      std::uint64_t src_a = t.buffer_address, src_b = 0;
-      std::uint32_t len_a, len_b = 0;
-      if (d.segmented) {
-        len_a = d.H;
-        src_b = t.buffer_address + d.H + static_cast<std::uint64_t>(k) * t.mss;
-        len_b = ps.chunk_len(k);
-      } else {
-        len_a = static_cast<std::uint32_t>(L);
-      }
-      const std::uint64_t base_len = static_cast<std::uint64_t>(len_a) + len_b;
-      // :324-331 VLAN insert, :389-395 strip
-      std::uint64_t size = base_len + (t.vlan_insert ? 4 : 0);
-      const bool has_vlan = t.vlan_insert || x.vlan_present;
-      const bool strip = x.vlan_strip && has_vlan && size >= 4;
-      if (strip) size -= 4;
-      const bool prefix = t.vlan_insert && !strip;
-      const bool strip_base = strip && !t.vlan_insert;  // the base segment loses its first 4 bytes
-      // :397-414 buffer too small
-      if (x.buffer_length < size) {
-        post_tx(make_tx(t, CompletionCode::Success, total, tso, gso), false);
-        CompletionEntry e = make_completion(x.descriptor_index, CompletionCode::BufferTooSmall);
-        e.vlan_stripped = x.vlan_strip && has_vlan;
-        if (e.vlan_stripped) e.vlan_tag = t.vlan_insert ? t.vlan_tag : x.vlan_tag;
-        post_rx(e, -1);
-        stats.drops_buffer_small += 1;
-        aborted = true;
-        break;
-      }
-      // :416-426 DMA write
-      if (!dma_ok(mem_size, x.buffer_address, size)) {
-        post_tx(make_tx(t, CompletionCode::Fault, total, tso, gso), false);
-        post_rx(make_completion(x.descriptor_index, CompletionCode::Fault), -1);
-        aborted = true;
-        break;
-      }
-      SegmentWrite w{};
-      w.dst = x.buffer_address;
-      if (prefix) {
-        const std::uint32_t tag = t.vlan_tag;
-        w.prefix = 0x81u | (0x00u << 8) | (((tag >> 8) & 0xFFu) << 16) | ((tag & 0xFFu) << 24);
-        w.prefix_len = 4;
-      }
-      if (strip_base) {  // drop the first 4 bytes of header || chunk
-        const std::uint32_t from_a = std::min<std::uint32_t>(4, len_a);
-        src_a += from_a;
-        len_a -= from_a;
-        src_b += 4 - from_a;
-        len_b -= 4 - from_a;
-      }
-      w.src_a = src_a;
-      w.len_a = len_a;
-      w.src_b = src_b;
-      w.len_b = len_b;
-      writes.push_back(w);
-      const std::int64_t wi = static_cast<std::int64_t>(writes.size()) - 1;
-
-      CompletionEntry e = make_completion(x.descriptor_index, CompletionCode::Success);
-      e.gro_aggregated = x.gro_enabled;
-      if (e.gro_aggregated) stats.rx_gro_aggregated += 1;
-      // :434-447 RX checksum verify of the delivered bytes
-      if (x.checksum_offload && x.checksum != ChecksumMode::None) {
-        e.checksum_verified = true;
-        stats.rx_checksum_verified += 1;
-        std::uint32_t first4, rest;
-        ps.segment(k, first4, rest);
-        std::uint32_t sum;
-        if (strip_base) sum = rest;
-        else sum = add1c(first4, rest);
-        if (prefix) sum = add1c(add1c(0x8100u, t.vlan_tag), sum);
-        if ((~sum & 0xFFFFu) != 0) {
-          e.status = static_cast<std::uint32_t>(CompletionCode::ChecksumError);
-          post_rx(e, wi);
-          post_tx(make_tx(t, CompletionCode::Success, total, tso, gso), false);
-          stats.drops_checksum += 1;
-          aborted = true;
-          break;
-        }
-      }
-      e.vlan_stripped = x.vlan_strip && has_vlan;
-      if (e.vlan_stripped) {
-        e.vlan_tag = t.vlan_insert ? t.vlan_tag : x.vlan_tag;
-        stats.rx_vlan_strips += 1;
-      }
-      post_rx(e, wi);
-      stats.rx_packets += 1;
-      stats.rx_bytes += size;
-    }
-    if (aborted) continue;
-    // :280-301 finalize_tx_success
-    post_tx(make_tx(t, CompletionCode::Success, total, tso, gso), true);
-    stats.tx_packets += total;
-    stats.tx_bytes += L;
-    if (tso) stats.tx_tso_segments += total;
-    if (gso) stats.tx_gso_segments += total;
-    if (t.vlan_insert) stats.tx_vlan_insertions += total;
+      multi[c] = m;
+    });
+    for (auto m : multi) nmulti += m;
   }
-  out.tx_processed = tx.size();
+  // mostly multi-segment batches (TSO) are left to the sequential pass: every
+  // early abort there would end the parallel prefix
+  if (ch.k > 1 && (max_threads || nmulti * 8 <= n)) {
+    std::size_t r = 0;
+    for (std::size_t i = 0; i < n; ++i) {
+      pos[i] = r;
+      if (r != rx.size() && need[i] != 0 && rx.size() - r >= need[i]) r += need[i];
+    }
+    pos[n] = r;
+    out.tx_completions.resize(n);
+    out.rx_completions.resize(r);
+    writes.resize(r);
+    write_of_rx.resize(r);
+    std::vector<std::size_t> stop(ch.k, 0);
+    std::vector<QueuePairStats> cst(ch.k);
+    ch.run([&](std::size_t c, std::size_t b, std::size_t e) {
+      PlaceSink sink{out.tx_completions.data(), out.rx_completions.data(), writes.data(), write_of_rx.data()};
+      QueuePairStats& S = cst[c];
+      std::size_t i = b;
+      for (; i < e; ++i) {
+        sink.ti = i;
+        sink.rj = pos[i];
+        QueuePairStats d{};
+        if (resolve_packet(C, i, pos[i], d, sink) != pos[i + 1] - pos[i]) break;
+        add_stats(S, d);
+      }
+      stop[c] = i;
+    });
+    from = n;
+    for (std::size_t c = 0; c < ch.k; ++c) {
+      add_stats(stats, cst[c]);
+      if (stop[c] != ch.begin(c + 1)) {
+        from = stop[c];
+        break;
+      }
+    }
+    rc = pos[from];
+    if (from == n) {
+      rc = r;
+    } else {
+      out.tx_completions.resize(from);
+      out.rx_completions.resize(rc);
+      writes.resize(rc);
+      write_of_rx.resize(rc);
+    }
+  } else {
+    out.tx_completions.clear();
+    out.rx_completions.clear();
+    writes.clear();
+    write_of_rx.clear();
+  }
+  if (from < n) {
+    out.tx_completions.reserve(n);
+    const std::size_t cap = std::min(n, rx.size());
+    out.rx_completions.reserve(cap);
+    writes.reserve(cap);
+    write_of_rx.reserve(cap);
+    AppendSink sink{config, out, writes, write_of_rx};
+    for (std::size_t i = from; i < n; ++i) rc += resolve_packet(C, i, rc, stats, sink);
+  }
+  out.tx_processed = n;
   out.rx_consumed = rc;
 }
 
@@ -518,9 +684,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
   auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
   if (mem.base == nullptr && mem.size != 0) throw GpuError("process_batch: null host-memory image", NICGPU_ERR_INVALID);
   // reset `out`, keeping its storage
-  out.tx_processed = out.rx_consumed = 0;
-  out.tx_completions.clear();
-  out.rx_completions.clear();
+  out.tx_processed = out.rx_consumed = 0;  // resolve sizes the completion lists
   out.rx_hash.clear();
   out.rx_queue.clear();
   for (auto& q : out.queues) q.clear();
@@ -539,7 +703,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
   std::uint16_t* csum = S.h_csum.get<std::uint16_t>(std::max<std::size_t>(np, 1));
   if (np) {
     std::uint64_t* desc = S.h_desc.get<std::uint64_t>(np);
-    Chunks(np).run([&](std::size_t, std::size_t b, std::size_t e) {
+    Chunks(np, config_.host_threads ? config_.host_threads : 16).run([&](std::size_t, std::size_t b, std::size_t e) {
       for (std::size_t i = b; i < e; ++i) desc[i] = NICGPU_DESC(plan.pieces[i].addr, plan.pieces[i].len);
     });
     void* d_desc = S.piece_desc.get(np * 8);
@@ -557,8 +721,6 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
   t = clock::now();
   std::vector<SegmentWrite>& writes = S.w;
   std::vector<std::int64_t>& write_of_rx = S.write_of_rx;
-  writes.clear();
-  write_of_rx.clear();
   QueuePairStats st = stats_;
   resolve(config_, mem.size, plan, std::span<const std::uint16_t>(csum, np), tx, rx, st, out, writes, write_of_rx);
   out.timings.resolve_us = us_since(t);

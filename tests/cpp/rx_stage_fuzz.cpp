@@ -194,6 +194,29 @@ int run_case(std::uint64_t seed) {
     std::memcpy(ours.data() + d + w.len_a, image.data() + w.src_b, w.len_b);
   }
 
+  // the speculative parallel resolve (no interrupt callback, forced onto 4
+  // threads even for these small batches) must equal the sequential one
+  {
+    BatchedQueuePairConfig pcfg = cfg;
+    pcfg.on_interrupt = nullptr;
+    RxBatchResult pout;
+    QueuePairStats pst{};
+    std::vector<SegmentWrite> pw;
+    std::vector<std::int64_t> pwof;
+    resolve(pcfg, mem_size, plan, cs, tx, rx, pst, pout, pw, pwof, 4);
+    bool pok = pout.tx_completions.size() == out.tx_completions.size() &&
+               pout.rx_completions.size() == out.rx_completions.size() && pw.size() == writes.size() &&
+               pwof == wof && same(pst, st) && pout.rx_consumed == out.rx_consumed;
+    for (std::size_t i = 0; pok && i < out.tx_completions.size(); ++i) pok = same(pout.tx_completions[i], out.tx_completions[i]);
+    for (std::size_t i = 0; pok && i < out.rx_completions.size(); ++i) pok = same(pout.rx_completions[i], out.rx_completions[i]);
+    for (std::size_t i = 0; pok && i < writes.size(); ++i)
+      pok = std::memcmp(&pw[i], &writes[i], sizeof(SegmentWrite)) == 0;
+    if (!pok) {
+      std::fprintf(stderr, "seed %llu: parallel resolve differs from the sequential one\n", (unsigned long long) seed);
+      return 1;
+    }
+  }
+
   bool ok = out.tx_completions.size() == ref_tx.size() && out.rx_completions.size() == ref_rx.size();
   for (std::size_t i = 0; ok && i < ref_tx.size(); ++i) ok = same(out.tx_completions[i], ref_tx[i]);
   for (std::size_t i = 0; ok && i < ref_rx.size(); ++i) ok = same(out.rx_completions[i], ref_rx[i]);

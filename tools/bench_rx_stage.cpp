@@ -1,6 +1,6 @@
 // bench_rx_stage.cpp — nic::BatchedQueuePair throughput.
 //
-//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps>
+//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads]
 //
 // c3: IMIX 64/576/1518 (7:4:1) frames, each balanced so the whole-frame
 //     checksum verifies; RX descriptors with Layer4 checksum offload, 2 KiB
@@ -118,6 +118,7 @@ int main(int argc, char** argv) {
   BatchedQueuePairConfig cfg;
   cfg.queue_id = 1;
   cfg.rss = &rss;
+  if (argc > 4) cfg.host_threads = static_cast<unsigned>(std::atoi(argv[4]));
   BatchedQueuePair qp{cfg};
   const DeviceHostMemory dm{static_cast<std::byte*>(mem), mem_size};
 
@@ -139,10 +140,10 @@ int main(int argc, char** argv) {
   for (auto L : lens) frame_bytes += L;
   const auto& T = last.timings;
   std::printf(
-      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
+      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
       "\"rx_success\": %zu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
       "\"phases_us\": {\"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f}}\n",
-      wl.c_str(), n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.plan_us, T.sums_us,
+      wl.c_str(), cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.plan_us, T.sums_us,
       T.resolve_us, T.gather_us, T.rss_us);
   nicgpu_free(mem);
   return 0;
