@@ -148,7 +148,7 @@ def main():
             report(row, "c5", n, fb, fb + 16 * n + 2 * n * nseg, med, mean, {"segments": n * nseg})
         elif row == "tso_seg_c5":
             n, fb, f, d = batch("c5")
-            H, MSS, STRIDE = 54, 1448, 1536
+            H, MSS, STRIDE = 54, int(os.environ.get("SEG_MSS", 1448)), int(os.environ.get("SEG_STRIDE", 1536))
             fl_np = np.full(n, sna.SEG_TSO | sna.SEG_VLAN_INSERT | 0x0123, np.uint32)
             cnt, base_np, total = sna.tso_segment_counts(np.full(n, 9000), np.full(n, H), np.full(n, MSS), fl_np)
             hdr = torch.full((n,), H, dtype=torch.int16, device=dev)
@@ -163,7 +163,7 @@ def main():
                 sna.tso_segment(f, d, hdr, mss, base, fl, out, STRIDE, ol, oc)
 
             med, mean = timed(torch, fn, args.steps, args.warmup)
-            written = int(n * (7 * (H + 4)) + n * (9000 - H))
+            written = int(total * (H + 4) + n * (9000 - H))
             # read frames once + write the segments + 8 B desc, 12 B per-frame params, 6 B per segment out
             report(row, "c5", n, fb, fb + written + 20 * n + 6 * total, med, mean,
                    {"segments": total, "bytes_written": written})
