@@ -78,6 +78,9 @@ def main():
             n = 4 << 20
             lens = pktgen.imix_lengths(n, np.random.default_rng(33))
             frames, desc, _ = pktgen.make_batch(lens, seed=33, proto=17, corrupt_frac=0.01)
+        elif name == "u64":
+            n = 4 << 20
+            frames, desc, _ = pktgen.make_batch(np.full(n, 64), seed=64, proto=17, corrupt_frac=0.01)
         else:  # c5
             n = 131072
             frames, desc, _ = pktgen.make_batch(np.full(n, 9000), seed=55, proto=6, corrupt_frac=0.0)
@@ -105,8 +108,8 @@ def main():
         print(json.dumps(rec), flush=True)
 
     for row in rows:
-        if row in ("rx_c2", "rx_l34_c2", "rx_c3"):
-            wl = "c3" if row == "rx_c3" else "c2"
+        if row in ("rx_c2", "rx_l34_c2", "rx_c3", "rx_u64"):
+            wl = {"rx_c3": "c3", "rx_u64": "u64"}.get(row, "c2")
             n, fb, f, d = batch(wl)
             ctx = rss_ctx(16 if wl == "c3" else 4)
             cs = torch.empty(n, dtype=torch.int16, device=dev)
