@@ -51,7 +51,7 @@ def timed(torch, fn, steps, warmup):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--rows", default="rx_c2,rx_l34_c2,rx_c3,icrc_c2,icrc_c3,tso_c5,tso_seg_c5")
+    ap.add_argument("--rows", default="rx_c2,rx_l34_c2,rx_c3,rx_u64,icrc_c2,icrc_c3,tso_c5,tso_seg_c5")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     args = ap.parse_args()
