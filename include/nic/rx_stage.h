@@ -116,7 +116,8 @@ struct BatchedQueuePairConfig {
   /// Threads for the host phases (plan, piece descriptors, resolve): 0 uses
   /// up to 16 on batches of 32 K descriptors and more (resolve stays
   /// sequential with an interrupt callback, or when most packets are
-  /// multi-segment); 1 runs them all on the calling thread.
+  /// multi-segment); 1 runs them all on the calling thread.  Workers are
+  /// pinned to the allowed CPUs that follow the calling thread's.
   unsigned host_threads{0};
 };
 

@@ -20,6 +20,9 @@
 #include <string>
 #include <thread>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include "nic/checksum.h"
 #include "nicgpu.h"
 
@@ -45,6 +48,34 @@ bool dma_ok(std::size_t mem_size, std::uint64_t addr, std::uint64_t len) {
   return addr <= mem_size && len <= mem_size - addr;
 }
 
+// Worker placement: chunk c of a pass runs on the c-th allowed CPU after the
+// calling thread's, so a batch's chunks stay on the same few neighbouring
+// cores from pass to pass and batch to batch (their lines then stay in those
+// cores' caches).  Empty when the affinity mask cannot be read.
+std::vector<int> near_cpus(std::size_t k) {
+  std::vector<int> out;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) != 0) return out;
+  const int self = sched_getcpu();
+  if (self < 0) return out;
+  std::vector<int> allowed;
+  for (int c = 0; c < CPU_SETSIZE; ++c)
+    if (CPU_ISSET(c, &set)) allowed.push_back(c);
+  const auto it = std::find(allowed.begin(), allowed.end(), self);
+  const std::size_t at = it == allowed.end() ? 0 : static_cast<std::size_t>(it - allowed.begin());
+  for (std::size_t i = 0; i < k && !allowed.empty(); ++i) out.push_back(allowed[(at + i) % allowed.size()]);
+  return out;
+}
+
+void pin_to(const std::vector<int>& cpus, std::size_t c) {
+  if (c >= cpus.size()) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  CPU_SET(cpus[c], &set);
+  (void) pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+
 // Fixed partition of [0, n) into at most 16 contiguous chunks, run on
 // std::threads when n is large enough to pay for them; f(chunk, begin, end).
 // Both passes of a count/fill pair see the same partition.
@@ -63,7 +94,12 @@ struct Chunks {
     }
     std::vector<std::thread> th;
     th.reserve(k - 1);
-    for (std::size_t c = 1; c < k; ++c) th.emplace_back([&, c] { f(c, begin(c), begin(c + 1)); });
+    const std::vector<int> cpus = near_cpus(k);
+    for (std::size_t c = 1; c < k; ++c)
+      th.emplace_back([&, c] {
+        pin_to(cpus, c);
+        f(c, begin(c), begin(c + 1));
+      });
     f(std::size_t{0}, std::size_t{0}, begin(1));
     for (auto& t : th) t.join();
   }
