@@ -1361,21 +1361,24 @@ struct RxVariant {
 };
 
 const RxVariant kRxVariants[] = {
-    // 0 and 2: production; for variant 0 launch_rx picks plain stores (2) when
+    // 0 and 1: production; for variant 0 launch_rx picks plain stores (1) when
     // the ring holds all of a wave's tiles (every write lands after the reads:
     // C2 -1%) and sc1 stores (0) when the ring is flushed mid-stream (IMIX -3%).
     // Both prefetch the next tile's first batch (XPF: 64 B -1..4%, C2 / IMIX /
     // 9000 B within noise).
-    // 8-wave blocks (1, 3) measure the same on C2/IMIX/64 B and 12% slower on
-    // 9000 B, whose 2500 tiles underfill 512 slots of 8 waves.
     {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 16, 0, true, true, true>, 2, 4, "u2_w4_c_sc1_ring_xpf", false, true, true},
-    {rx_offload_kernel<2, true, 8, true, false, 1, false, -1, 16, 0, true>, 2, 8, "u2_nt1_w8_c_sc1_ring", false, true},
     {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 0, 0, true, true, true>, 2, 4, "u2_w4_c_ring_xpf", false, true, true},
+#ifdef NICGPU_TUNING
+    // candidates and earlier production kernels, timed by tools/tune_rx.py.
+    // 8-wave blocks measure the same on C2/IMIX/64 B and 12% slower on 9000 B,
+    // whose 2500 tiles underfill 512 slots of 8 waves.
+    {rx_offload_kernel<2, true, 8, true, false, 1, false, -1, 16, 0, true>, 2, 8, "u2_nt1_w8_c_sc1_ring", false, true},
     {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 16, 0, true>, 2, 4, "u2_nt1_w4_c_sc1_ring", false, true},
     {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 0, 0, true>, 2, 4, "u2_nt1_w4_c_ring", false, true},
     {rx_offload_kernel<2, true, 4, true, false, 1, true, -1, 16>, 2, 4, "u2_nt1_w4_c_sc1_defer"},
     {rx_offload_kernel<2, true, 4, true, false, 1, false>, 2, 4, "u2_nt1_w4_c"},
     {rx_offload_kernel<2, true, 4, false, false, 1, false, -1, 16, 0, true>, 2, 4, "u2_nt1_w4_sc1_ring", false, true},
+#endif
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
 
@@ -2050,7 +2053,7 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
     const RxVariant& vv = kRxVariants[var];
     return rx_lds_bytes(vv.wpb, vv.unroll, stage, rss ? P.lut_words : 0u, hist_n) + table_words * 4u;
   };
-  if (variant == 0) variant = plan_ring(dev, 0, lds_of(0), ntiles, di).holds_all ? 2 : 0;
+  if (variant == 0) variant = plan_ring(dev, 0, lds_of(0), ntiles, di).holds_all ? 1 : 0;
   const RxVariant& v = kRxVariants[variant];
   const uint32_t lds = lds_of(variant);
   // ranges: at least 16 packets per wave; round robin: one tile per wave
