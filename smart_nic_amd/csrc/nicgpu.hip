@@ -173,7 +173,7 @@ __device__ __forceinline__ bool dbg_on(const RxParams& P, uint32_t bit) {
 //   per wave: S[64] | E[64] | scratch | hdr[64][kHdrStride] uint4 (only when hashing)
 //     scratch = general path: pk[64] uint4 {delta lo, delta hi, end, info} + marks[64 U]
 //               contiguous path: two slot windows of 64 U words (ping-pong)
-//   per block: lut[lut_words] | hist[hist_n]
+//   per block (first): masks | lut[lut_words] | hist[hist_n] | table, then the waves' parts
 constexpr uint32_t kScratchOff = kWave * 4 * 2;
 
 __host__ __device__ constexpr uint32_t rx_scratch_bytes(int unroll) {
@@ -195,8 +195,14 @@ __host__ __device__ constexpr uint32_t rx_wave_lds(bool rss, int unroll) {
 constexpr uint32_t kMaskEntries = 16 + 17;
 constexpr uint32_t kMaskTableBytes = kMaskEntries * 16;
 
-__host__ __device__ inline uint32_t rx_lds_bytes(int wpb, int unroll, bool rss, uint32_t lut_words, uint32_t hist_n) {
-  return (uint32_t) wpb * rx_wave_lds(rss, unroll) + kMaskTableBytes + lut_words * 4u + hist_n * 4u;
+// The block part (masks | lut | hist | table), 16-B rounded; the waves' parts follow it.
+__host__ __device__ inline uint32_t rx_block_bytes(uint32_t lut_words, uint32_t hist_n, uint32_t table_words) {
+  return (kMaskTableBytes + lut_words * 4u + hist_n * 4u + table_words * 4u + 15u) & ~15u;
+}
+
+__host__ __device__ inline uint32_t rx_lds_bytes(int wpb, int unroll, bool rss, uint32_t lut_words, uint32_t hist_n,
+                                                 uint32_t table_words) {
+  return rx_block_bytes(lut_words, hist_n, table_words) + (uint32_t) wpb * rx_wave_lds(rss, unroll);
 }
 
 // Header stage of one wave: chunk k (0..2) of the packet in lane q lives in
@@ -390,12 +396,23 @@ __device__ __forceinline__ uint32_t rss_hash_packet(const RxParams& P, const uin
       const uint32_t t0 = (c1.z >> 16) | (c1.w << 16);   // bytes 26..29
       const uint32_t t1 = (c1.w >> 16) | (c2.x << 16);   // bytes 30..33
       const uint32_t t2 = (c2.x >> 16) | (c2.y << 16);   // bytes 34..37
+      // nibbles pre-scaled to byte offsets four at a time: one extract per
+      // lookup, the table's offset an immediate of the ds_read
+      const uint8_t* lut_b = reinterpret_cast<const uint8_t*>(lut);
+      const uint32_t tw[3] = {t0, t1, t2};
       uint32_t hh = 0;
 #pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        const uint32_t w = i < 4 ? t0 : (i < 8 ? t1 : t2);
-        const uint32_t b = (w >> (8 * (i & 3))) & 0xFFu;
-        hh ^= lut[(2 * i) * 16 + (b >> 4)] ^ lut[(2 * i + 1) * 16 + (b & 15u)];
+      for (int d = 0; d < 3; ++d) {
+        uint32_t hi4 = (tw[d] >> 2) & 0x3C3C3C3Cu;  // 4 x high nibble of each byte
+        uint32_t lo4 = (tw[d] << 2) & 0x3C3C3C3Cu;  // 4 x low nibble
+        asm volatile("" : "+v"(hi4), "+v"(lo4));     // keep them: otherwise folded back into 2 ops per lookup
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int i = 4 * d + k;  // tuple byte
+          const uint32_t ah = (hi4 >> (8 * k)) & 0xFFu, al = (lo4 >> (8 * k)) & 0xFFu;
+          hh ^= *reinterpret_cast<const uint32_t*>(lut_b + (2 * i) * 64 + ah) ^
+                *reinterpret_cast<const uint32_t*>(lut_b + (2 * i + 1) * 64 + al);
+        }
       }
       return hh;
     }
@@ -906,7 +923,12 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   L.hist_lds = P.out_hits != nullptr && P.table_n <= (uint32_t) kHistLds;
   L.table_lds = L.want_rss && P.table_n <= (uint32_t) kTableLds;
   uint8_t* base_b = reinterpret_cast<uint8_t*>(lds_dyn);
-  uint8_t* wave_b = base_b + (uint32_t) w * rx_wave_lds(L.stage, U);
+  // block part first — masks | lut | hist | table — so the LUT sits at a
+  // constant LDS address and the hash's table offsets fold into ds_read
+  // immediates; then the waves' parts
+  const uint32_t block_bytes = rx_block_bytes(L.want_rss ? P.lut_words : 0u, L.hist_lds ? P.table_n : 0u,
+                                              L.table_lds ? (P.table_n + 1u) / 2u : 0u);
+  uint8_t* wave_b = base_b + block_bytes + (uint32_t) w * rx_wave_lds(L.stage, U);
   L.S = reinterpret_cast<uint32_t*>(wave_b);
   L.E = L.S + kWave;
   L.pk = reinterpret_cast<uint4*>(wave_b + kScratchOff);
@@ -914,10 +936,10 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   L.slotsA = reinterpret_cast<uint32_t*>(wave_b + kScratchOff);
   L.slotsB = L.slotsA + kWave * U;
   L.hdr = reinterpret_cast<uint4*>(wave_b + rx_hdr_off(U));
-  uint4* masks_w = reinterpret_cast<uint4*>(base_b + (uint32_t) WPB * rx_wave_lds(L.stage, U));
+  uint4* masks_w = reinterpret_cast<uint4*>(base_b);
   L.masks = masks_w;
-  L.lut = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(masks_w) + kMaskTableBytes);
-  L.hist = L.lut + P.lut_words;
+  L.lut = reinterpret_cast<uint32_t*>(base_b + kMaskTableBytes);
+  L.hist = L.lut + (L.want_rss ? P.lut_words : 0u);
   L.table_s = reinterpret_cast<uint16_t*>(L.hist + (L.hist_lds ? P.table_n : 0u));
   // marks never match a live tag (tags start at 1; cleared slots read as 0)
   for (uint32_t i = lane; i < (uint32_t) (kWave * U); i += kWave) L.marks[i] = 0xFFFFFFFFu;
@@ -2051,7 +2073,7 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
   (void) hipGetDevice(&dev);
   auto lds_of = [&](int var) {
     const RxVariant& vv = kRxVariants[var];
-    return rx_lds_bytes(vv.wpb, vv.unroll, stage, rss ? P.lut_words : 0u, hist_n) + table_words * 4u;
+    return rx_lds_bytes(vv.wpb, vv.unroll, stage, rss ? P.lut_words : 0u, hist_n, table_words);
   };
   if (variant == 0) variant = plan_ring(dev, 0, lds_of(0), ntiles, di).holds_all ? 1 : 0;
   const RxVariant& v = kRxVariants[variant];
