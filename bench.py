@@ -176,7 +176,7 @@ def main():
     ap.add_argument("--packets", type=int, default=N_PER_GPU, help="packets per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01i_pmc_c2.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01j_pmc_c2.json"))
     args = ap.parse_args()
 
     import torch
