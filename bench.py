@@ -176,7 +176,7 @@ def main():
     ap.add_argument("--packets", type=int, default=N_PER_GPU, help="packets per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01j_pmc_c2.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01k_pmc_c2.json"))
     args = ap.parse_args()
 
     import torch
@@ -234,23 +234,36 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    # per-launch HIP events on the launch stream (torch's current stream)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # One HIP event pair on the launch stream (torch's current stream) around
+    # the K launches: average launch duration = region / K, inter-launch gaps
+    # included. Per-launch event pairs inside the timed loop cost ~8 us of wall
+    # time per step on MI355X (tools/launch_gap.py: 259 -> 251 us per C2 step),
+    # so the per-launch spread is taken in a separate, untimed pass below.
+    stream = torch.cuda.current_stream()
+    ev_a, ev_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
+    ev_a.record(stream)
     for i in range(args.steps):
-        ev[i][0].record()
         step()
-        ev[i][1].record()
+    ev_b.record(stream)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     t_wall = time.perf_counter() - t_start
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    kern_avg_s = float(np.mean(kern_ms)) / 1e3
-    kern_med_s = float(np.median(kern_ms)) / 1e3
+    kern_avg_s = ev_a.elapsed_time(ev_b) / 1e3 / args.steps
+
+    # untimed: per-launch event pairs for the median launch duration
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(min(args.steps, 20))]
+    for a, b in ev:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize()
+    kern_med_s = float(np.median([a.elapsed_time(b) for a, b in ev])) / 1e3
 
     t_max = t_wall
     if dist is not None:
@@ -297,6 +310,8 @@ def main():
             "gbs_frames_per_gpu": round(frame_gbs, 2),
             "kernel_us_avg": round(kern_avg_s * 1e6, 2),
             "kernel_us_median": round(kern_med_s * 1e6, 2),
+            "kernel_timing": "kernel_us_avg = one HIP event pair around the K timed launches / K (gaps included); "
+                             "kernel_us_median from per-launch event pairs in a separate untimed pass",
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved_gbs, 1),
