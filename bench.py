@@ -323,13 +323,14 @@ def main():
             },
             "checks": {"status_matches_corruption": status_ok, "queue_is_table_of_hash": queue_ok},
         }
-    # end-to-end (host pinned -> H2D -> kernel -> D2H of results), rank 0 only
-    if rank == 0 and not args.no_e2e:
+    # end-to-end (host pinned -> H2D -> kernel -> D2H of results) and the CPU
+    # baseline: rank 0 at N = 1 only
+    if rank == 0 and world == 1 and not args.no_e2e:
         try:
             out["e2e"] = e2e_rate(torch, sna, ctx, frames, desc, dev)
         except Exception as e:  # report, never hide
             out["e2e"] = {"error": repr(e)}
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(frames, desc, table, (g_cs, g_q),
                                            n_sample_mt=min(n, 1 << 18), n_sample_1=min(n, 1 << 16))
         out["cpu_baseline"]["other_rows"] = cpu_rows_baseline(pktgen)
