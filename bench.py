@@ -176,7 +176,8 @@ def main():
     ap.add_argument("--packets", type=int, default=N_PER_GPU, help="packets per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01k_pmc_c2.json"))
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the same-box read-only streaming ceiling")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01l_pmc_c2.json"))
     args = ap.parse_args()
 
     import torch
@@ -265,6 +266,8 @@ def main():
     torch.cuda.synchronize()
     kern_med_s = float(np.median([a.elapsed_time(b) for a, b in ev])) / 1e3
 
+    ceiling = read_ceiling(torch, f_dev) if (rank == 0 and world == 1 and not args.no_ceiling) else None
+
     t_max = t_wall
     if dist is not None:
         tt = torch.tensor([t_wall], dtype=torch.float64, device=dev)
@@ -320,6 +323,8 @@ def main():
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes,
+                "ceiling_measured": ceiling,
+                "frac_of_ceiling": (round(achieved_gbs / ceiling["gbs"], 4) if ceiling else None),
             },
             "checks": {"status_matches_corruption": status_ok, "queue_is_table_of_hash": queue_ok},
         }
@@ -339,6 +344,43 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def read_ceiling(torch, buf, reps=5):
+    """Same-box read-only streaming ceiling: the best of a few
+    grid shapes of the tuning build's plain 16-B-per-lane streaming read
+    kernel over the resident frame buffer, HIP events per launch, median of
+    `reps`. Reported beside the 8 TB/s spec peak; never used as `peak`."""
+    import ctypes
+
+    path = os.path.join(ROOT, "smart_nic_amd", "libnicgpu_tune.so")
+    if not os.path.exists(path):
+        return None
+    tl = ctypes.CDLL(path)
+    vp, sz, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    tl.nicgpu_tune_stream_read.restype = i32
+    tl.nicgpu_tune_stream_read.argtypes = [vp, sz, i32, i32, vp, vp]
+    stream = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    nbytes = buf.numel() // 16 * 16
+    sink = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    best = None
+    for unroll, bpc in ((1, 8), (2, 4), (4, 2), (4, 4), (8, 2)):
+        ts = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            rc = tl.nicgpu_tune_stream_read(buf.data_ptr(), nbytes, bpc, unroll, sink.data_ptr(), sp)
+            b.record(stream)
+            torch.cuda.synchronize()
+            if rc != 0:
+                return None
+            ts.append(a.elapsed_time(b) * 1e3)
+        gbs = nbytes / float(np.median(ts)) / 1e3
+        if best is None or gbs > best["gbs"]:
+            best = {"gbs": round(gbs, 1), "unroll": unroll, "blocks_per_cu": bpc, "bytes": nbytes,
+                    "kernel": "stream_read_kernel (libnicgpu_tune.so), same buffer, median of %d" % reps}
+    return best
 
 
 def e2e_rate(torch, sna, ctx, frames, desc, dev, chunk_pkts=1 << 16, reps=3):
