@@ -66,3 +66,40 @@ def test_no_gpu_fails_loudly():
     out = (ctypes.c_uint16 * 1)()
     st = lib.nicgpu_checksum_batch(ctypes.addressof(buf) & ~15 or None, desc, 1, out, None)
     assert st in (sna.ERR_NO_DEVICE, sna.ERR_HIP, sna.ERR_INVALID)
+
+
+def test_batch_entry_points_validate_before_device_access():
+    """Every batch entry point of include/nicgpu.h checks its arguments before
+    touching a device (so the results below hold with or without a GPU): an
+    empty batch is a no-op, missing buffers, a misaligned frame base, a bad
+    ICRC mode or a zero slot stride are NICGPU_ERR_INVALID."""
+    lib = sna.load_library()
+    buf = (ctypes.c_uint8 * 64)()
+    base = ctypes.addressof(buf)
+    aligned = (base + 15) & ~15
+    mis = aligned + 1
+    p = aligned  # any non-null pointer for the other arguments
+    OK, INV = sna.OK, sna.ERR_INVALID
+    # nicgpu_tso_checksum(frames, desc, hdr_len, mss, seg_base, n, out, stream)
+    assert lib.nicgpu_tso_checksum(None, None, None, None, None, 0, None, None) == OK
+    assert lib.nicgpu_tso_checksum(None, p, p, p, p, 1, p, None) == INV
+    assert lib.nicgpu_tso_checksum(p, p, p, p, p, 1, None, None) == INV
+    assert lib.nicgpu_tso_checksum(mis, p, p, p, p, 1, p, None) == INV
+    # nicgpu_tso_segment(frames, desc, hdr, mss, seg_base, flags, n, out, out_size, stride, out_len, out_csum, stream)
+    assert lib.nicgpu_tso_segment(None, None, None, None, None, None, 0, None, 0, 0, None, None, None) == OK
+    assert lib.nicgpu_tso_segment(p, p, p, p, p, None, 1, None, 64, 16, None, None, None) == INV
+    assert lib.nicgpu_tso_segment(p, p, p, p, p, None, 1, p, 64, 0, None, None, None) == INV
+    assert lib.nicgpu_tso_segment(mis, p, p, p, p, None, 1, p, 64, 16, None, None, None) == INV
+    # nicgpu_icrc_batch(frames, desc, n, mode, out_crc, out_ok, stream)
+    assert lib.nicgpu_icrc_batch(p, p, 1, 2, p, None, None) == INV            # unknown mode
+    assert lib.nicgpu_icrc_batch(p, p, 1, 0, p, p, None) == INV               # CALCULATE with out_ok
+    assert lib.nicgpu_icrc_batch(p, p, 1, 1, p, None, None) == INV            # VERIFY without out_ok
+    assert lib.nicgpu_icrc_batch(None, None, 0, 0, None, None, None) == OK
+    assert lib.nicgpu_icrc_batch(None, p, 1, 0, p, None, None) == INV
+    assert lib.nicgpu_icrc_batch(mis, p, 1, 0, p, None, None) == INV
+    # nicgpu_segment_gather(mem, mem_size, writes, n, stream)
+    assert lib.nicgpu_segment_gather(None, 0, None, 0, None) == OK
+    assert lib.nicgpu_segment_gather(None, 64, p, 1, None) == INV
+    assert lib.nicgpu_segment_gather(p, 64, None, 1, None) == INV
+    # nicgpu_checksum_batch: the RX pass without RSS
+    assert lib.nicgpu_checksum_batch(None, None, 0, None, None) == OK
