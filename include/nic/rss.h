@@ -64,7 +64,10 @@ public:
   /// called once per packet (hashes += count, queue_hits[idx] += hits for
   /// idx < queue_hits.size()), which requires waiting for the launch: the call
   /// is synchronous on `stream` unless update_stats is false.  Throws
-  /// nic::GpuError.
+  /// nic::GpuError.  Any key length hashes as select_queue does (keys over
+  /// NICGPU_MAX_KEY = 256 B are truncated for the device, which is exact); a
+  /// table over NICGPU_MAX_TABLE = 2^24 entries throws (NICGPU_ERR_INVALID)
+  /// before any device work, where select_queue would accept it.
   void select_queue_batch(const DevicePacketBatch& batch, const TupleSpec& tuple,
                           const RxBatchOutputs& out, void* stream = nullptr,
                           bool update_stats = true) const;

@@ -28,10 +28,24 @@
 // ring consumption, first-failure aborts, statuses, stats — is sequential in
 // the reference and is resolved on the host from those sums, exactly.
 //
+// Buffers that overlap: the reference writes segment after
+// segment, so of two RX buffers that share bytes the later write wins, and a
+// TX buffer that overlaps an earlier RX buffer of the batch is read after that
+// write.  When any RX buffer overlaps another RX buffer or a TX buffer
+// (buffers_disjoint() is false), the batch runs as sub-batches, each ending
+// before the first TX descriptor that reads bytes an earlier descriptor of the
+// sub-batch wrote; within a sub-batch overlapping writes go to successive
+// gather launches in posting order ("layers", schedule_writes()), sources are
+// read from a copy of the image when a write lands on any source, and each
+// layer's delivered frames are hashed before the next layer can overwrite
+// them.  The results are the sequential reference's in every case.
+//
 // Not modelled: address translators / fault injectors of SimpleHostMemory
-// (only the plain bounds check), and aliasing between TX buffers and RX
-// buffers of the same batch (the reference would read bytes written by an
-// earlier segment of the batch; the stage reads every TX buffer first).
+// (only the plain bounds check).
+//
+// Failure: process_batch throws nic::GpuError on a HIP failure.  stats() is
+// then unchanged, but the memory image may hold some of the batch's writes and
+// the RSS engine's stats some of its hashes.
 #pragma once
 
 #include <cstddef>
@@ -164,8 +178,9 @@ public:
   void reset_stats() noexcept { stats_ = QueuePairStats{}; }
   [[nodiscard]] const BatchedQueuePairConfig& config() const noexcept { return config_; }
 
-private:
   struct Scratch;  // device, pinned and host buffers reused across batches (grown, never shrunk)
+
+private:
   BatchedQueuePairConfig config_;
   QueuePairStats stats_{};
   std::unique_ptr<Scratch> scratch_;
@@ -217,6 +232,12 @@ struct SegmentWrite {
 };
 static_assert(sizeof(SegmentWrite) == 40);
 
+/// True when no RX buffer of `rx` (as far as it lies inside the image) shares a
+/// byte with another RX buffer or with a TX buffer of `tx`: then every DMA
+/// write of the batch can run in one parallel gather and read its source in
+/// place.  O(n + m) for buffers laid out in ascending order, a sort otherwise.
+bool buffers_disjoint(std::size_t mem_size, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx);
+
 Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx);
 /// The same into `plan`, reusing its storage (no page faults once it has grown).
 void make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
@@ -240,6 +261,67 @@ void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const P
              std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
              std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
              std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx, unsigned max_threads = 0);
+
+/// The sequential resolve, stopped before the first TX descriptor whose
+/// pieces read bytes that an earlier descriptor of this call writes (that
+/// descriptor must see the written bytes, so its sums are taken again after the
+/// writes).  Same outputs as resolve for the descriptors it covers; returns
+/// their number (at least 1 when tx is not empty).
+std::size_t resolve_prefix(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
+                           std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
+                           std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
+                           std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx);
+
+/// Order of the DMA writes of one resolved sub-batch for parallel gathers.
+/// Writes (RX completions j with write_of_rx[j] >= 0 and at least one byte) are
+/// split into layers: a write goes one layer above every earlier write it
+/// overlaps, so no two writes of a layer overlap and, of two that do, the later
+/// one lands later — the reference's last-write-wins order.
+struct WriteSchedule {
+  std::vector<std::uint32_t> order;        // RX completion indices, layer by layer, ascending within a layer
+  std::vector<std::size_t> layer_begin;    // layer l = order[layer_begin[l], layer_begin[l + 1])
+  bool from_copy{false};                   // a destination overlaps a source: gather from a copy of the image
+};
+void schedule_writes(std::span<const SegmentWrite> writes, std::span<const std::int64_t> write_of_rx,
+                     WriteSchedule& schedule);
+
+/// Device work of run_batch: nicgpu_* launches in BatchedQueuePair; tests run
+/// the same driver with a CPU implementation (tests/cpp/cpu_backend.h).
+class Backend {
+public:
+  virtual ~Backend() = default;
+  /// compute_checksum of every piece over the image as it is now; the span
+  /// stays valid until the next call.
+  virtual std::span<const std::uint16_t> piece_sums(std::span<const Piece> pieces) = 0;
+  /// Keep a copy of the image as it is now (the sources of from_copy gathers).
+  virtual void snapshot() = 0;
+  /// Apply writes whose destinations do not overlap one another; sources are
+  /// read from the image, or from the last snapshot when from_copy.
+  virtual void gather(std::span<const SegmentWrite> writes, bool from_copy) = 0;
+  /// Buffer for n frame descriptors (NICGPU_DESC(address, length)) for rss().
+  virtual std::uint64_t* frame_desc(std::size_t n) = 0;
+  /// config.rss->select_queue_batch over the n frames of frame_desc(n) in the
+  /// image as it is now (stats updated); hash/queue point at n results, valid
+  /// until the next call.
+  virtual void rss(std::size_t n, const std::uint32_t*& hash, const std::uint16_t*& queue) = 0;
+};
+
+/// Host state run_batch reuses across batches.
+struct BatchScratch {
+  Plan plan;
+  std::vector<SegmentWrite> writes, layer;
+  std::vector<std::int64_t> write_of_rx;
+  std::vector<std::uint32_t> which;
+  WriteSchedule schedule;
+  RxBatchResult part;
+};
+
+/// process_batch's driver over any Backend: plan, piece sums, resolve, DMA
+/// writes and RSS, in sub-batches and layers when buffers overlap (see the top
+/// of this header).  Adds to `stats`; replaces out's contents.
+void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
+               std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out, BatchScratch& scratch,
+               Backend& backend);
 
 }  // namespace rx_stage_detail
 

@@ -65,8 +65,14 @@ extern "C" {
 #define NICGPU_TUPLE_RAW 2
 #define NICGPU_RAW_MAX_END 64
 #define NICGPU_MAX_TUPLE 64
-#define NICGPU_MAX_KEY 256    /* key bytes */
-#define NICGPU_MAX_TABLE 65536
+/* Key bytes an RSS context holds.  Longer keys are never needed: tuples are at
+ * most NICGPU_MAX_TUPLE bytes, so key bits past 8 * 64 + 31 are never read and
+ * a longer key hashes exactly like its first NICGPU_MAX_KEY bytes (no wrap
+ * either way, src/rss.cpp:83-89).  nic::RssEngine truncates for the GPU. */
+#define NICGPU_MAX_KEY 256
+/* Indirection-table entries an RSS context holds (tables above 1024 entries are
+ * read from global memory and their hits counted with global atomics). */
+#define NICGPU_MAX_TABLE (1u << 24)
 
 /* Library identity / device probe. */
 int nicgpu_abi_version(void);
@@ -122,7 +128,6 @@ int nicgpu_rx_offload(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const ui
                       uint16_t* out_csum, uint32_t* out_hash, uint16_t* out_queue,
                       uint64_t* out_hits, void* stream);
 
-/* Checksum only (== rx_offload with NICGPU_TUPLE_NONE). */
 /* nicgpu_rx_offload plus L3/L4 checksum verification in the same pass
  * (out_l34[i] = NICGPU_L34_* flags; may be NULL).  The IPv4 header checksum and
  * the TCP/UDP checksum over pseudo-header || segment are those of the
@@ -139,6 +144,7 @@ int nicgpu_rx_offload_ex(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const
                          int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum, uint32_t* out_hash,
                          uint16_t* out_queue, uint64_t* out_hits, uint8_t* out_l34, void* stream);
 
+/* Checksum only (== rx_offload with NICGPU_TUPLE_NONE). */
 int nicgpu_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n,
                           uint16_t* out_csum, void* stream);
 
@@ -205,10 +211,16 @@ typedef struct nicgpu_segment_write {
 } nicgpu_segment_write;
 
 /* Perform n writes (device array) inside the memory image mem[0, mem_size).
- * Destinations must not overlap each other or any source.  Entries reaching
- * outside the image are skipped. */
+ * The writes run in parallel: destinations must not overlap each other or any
+ * source (nic::BatchedQueuePair orders overlapping writes into successive
+ * launches).  Entries reaching outside the image are skipped. */
 int nicgpu_segment_gather(uint8_t* mem, uint64_t mem_size, const nicgpu_segment_write* writes, size_t n,
                           void* stream);
+/* The same with every source read from src[0, mem_size) (a copy of the image
+ * taken earlier, e.g. before a batch whose writes overwrite its own sources);
+ * destinations are in mem and must not overlap each other. */
+int nicgpu_segment_gather_from(uint8_t* mem, const uint8_t* src, uint64_t mem_size,
+                               const nicgpu_segment_write* writes, size_t n, void* stream);
 
 #ifdef __cplusplus
 }

@@ -677,6 +677,36 @@ std::string completion_json(const CompletionEntry& e) {
   return o.str();
 }
 
+// SimpleHostMemory that records every successful write in order: the RX
+// segment DMA writes of QueuePair::handle_rx_segment (:416-426), i.e. each
+// delivered frame's bytes as written, before any later write lands on them.
+class RecordingMemory final : public HostMemory {
+public:
+  explicit RecordingMemory(HostMemoryConfig c) : mem_(c) {}
+  HostMemoryConfig config() const noexcept override { return mem_.config(); }
+  HostMemoryResult translate(HostAddress a, std::size_t n, HostMemoryView& v) override { return mem_.translate(a, n, v); }
+  HostMemoryResult translate_const(HostAddress a, std::size_t n, ConstHostMemoryView& v) const override {
+    return mem_.translate_const(a, n, v);
+  }
+  HostMemoryResult read(HostAddress a, std::span<std::byte> b) const override { return mem_.read(a, b); }
+  HostMemoryResult write(HostAddress a, std::span<const std::byte> d) override {
+    HostMemoryResult r = mem_.write(a, d);
+    if (r.ok() && recording) {
+      const auto* p = reinterpret_cast<const std::uint8_t*>(d.data());
+      writes.emplace_back(p, p + d.size());
+    }
+    return r;
+  }
+  bool recording = false;
+  std::vector<std::vector<std::uint8_t>> writes;
+
+private:
+  SimpleHostMemory mem_;
+};
+
+// flavour 0: mixed sizes; 1: 9000 B TSO/GSO; 2: mixed sizes with overlapping
+// buffers (recycled RX buffers, RX buffers straddling the previous one or
+// lying inside TX buffers), where the reference's in-order writes decide.
 void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t ntx, std::size_t nrx, int flavour) {
   Rng r{seed};
   // TX region, then the RX buffers, then a guard tail; a few descriptors point
@@ -756,6 +786,21 @@ void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t 
     x.gro_enabled = r.below(5) == 0;
     rxs.push_back(x);
   }
+  if (flavour == 2) {
+    for (std::size_t j = 1; j < nrx; ++j) {
+      RxDescriptor& x = rxs[j];
+      const std::uint32_t k = r.below(12);
+      if (k < 3) {  // a recycled buffer
+        const RxDescriptor& y = rxs[r.below(static_cast<std::uint32_t>(j))];
+        x.buffer_address = y.buffer_address;
+        if (r.below(2)) x.buffer_length = y.buffer_length;
+      } else if (k < 5) {  // straddling the previous buffer
+        x.buffer_address = rxs[j - 1].buffer_address + r.below(std::max<std::uint32_t>(1, rxs[j - 1].buffer_length));
+      } else if (k < 7) {  // inside a TX buffer
+        x.buffer_address = tx_addr[r.below(static_cast<std::uint32_t>(ntx))] + r.below(16);
+      }
+    }
+  }
   const std::size_t mem_size = rx_at + 64;
   // DMA faults: a few descriptors addressed past the end of host memory
   // (past the end, or straddling it); RX fault addresses are distinct so no
@@ -766,11 +811,12 @@ void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t 
     if (r.below(80) == 0) rxs[j].buffer_address = mem_size + 1 + j;
 
   HostMemoryConfig mc{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false};
-  SimpleHostMemory mem{mc};
+  RecordingMemory mem{mc};
   std::vector<std::uint8_t> image(mem_size);
   for (std::size_t a = 0; a < tx_end; ++a) image[a] = r.byte();  // RX region starts zeroed
   for (std::size_t i = 0; i < ntx; ++i) std::memcpy(image.data() + tx_addr[i], pkts[i].data(), pkts[i].size());
   assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(image))).ok());
+  mem.recording = true;
   DMAEngine dma{mem};
   QueuePairConfig qc{
       .queue_id = 5,
@@ -801,7 +847,35 @@ void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t 
   while (auto c = qp.tx_completion().poll_completion()) { js << (first ? "" : ",") << "\n  " << completion_json(*c); first = false; }
   js << "],\n \"rx_completions\": [";
   first = true;
-  while (auto c = qp.rx_completion().poll_completion()) { js << (first ? "" : ",") << "\n  " << completion_json(*c); first = false; }
+  std::vector<CompletionEntry> rxc;
+  while (auto c = qp.rx_completion().poll_completion()) {
+    js << (first ? "" : ",") << "\n  " << completion_json(*c);
+    first = false;
+    rxc.push_back(*c);
+  }
+  // RSS of every frame delivered with Success (the reference RssEngine, MS
+  // 40-B key, 128-entry table i % 16, on oracle_extract_tuple AUTO of the
+  // bytes written for it); writes pair with the RX completions that carry one
+  // (Success and ChecksumError: handle_rx_segment writes, then verifies)
+  const std::vector<std::uint8_t>& ms_key = kMsKey;
+  std::vector<std::uint16_t> rss_table(128);
+  for (int i = 0; i < 128; ++i) rss_table[i] = static_cast<std::uint16_t>(i % 16);
+  RssEngine rss_eng{RssConfig{ms_key, rss_table}};
+  std::vector<std::uint32_t> rx_hash(rxc.size(), 0);
+  std::vector<std::uint32_t> rx_queue(rxc.size(), 0xFFFFu);
+  std::size_t wk = 0;
+  for (std::size_t j = 0; j < rxc.size(); ++j) {
+    const auto status = static_cast<CompletionCode>(rxc[j].status);
+    if (status != CompletionCode::Success && status != CompletionCode::ChecksumError) continue;
+    assert(wk < mem.writes.size());
+    const std::vector<std::uint8_t>& bytes = mem.writes[wk++];
+    if (status != CompletionCode::Success) continue;
+    std::uint8_t t[64];
+    const std::size_t tl = oracle_extract_tuple(bytes.data(), bytes.size(), ORACLE_TUPLE_AUTO, 0, 0, t);
+    rx_hash[j] = RssEngine{RssConfig{ms_key, rss_table}}.hash(std::span<const std::uint8_t>(t, tl));
+    rx_queue[j] = *rss_eng.select_queue(std::span<const std::uint8_t>(t, tl));
+  }
+  assert(wk == mem.writes.size());
   const auto& st = qp.stats();
   js << "],\n \"stats\": [" << st.tx_packets << "," << st.rx_packets << "," << st.tx_bytes << "," << st.rx_bytes << ","
      << st.drops_checksum << "," << st.drops_no_rx_desc << "," << st.drops_buffer_small << "," << st.drops_mtu_exceeded
@@ -815,7 +889,15 @@ void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t 
     const std::size_t n = std::min<std::size_t>(rxs[j].buffer_length, mem_size - a);
     js << (j ? "," : "") << "\"" << std::hex << fnv1a(after.data() + a, n) << std::dec << "\"";
   }
-  js << "],\n \"mem_fnv\": \"" << std::hex << fnv1a(after.data(), mem_size) << std::dec << "\"\n}\n";
+  js << "],\n \"mem_fnv\": \"" << std::hex << fnv1a(after.data(), mem_size) << std::dec << "\"";
+  js << ",\n \"rss\": \"RssEngine{MS 40-B key, table i % 16 of 128}::select_queue on oracle_extract_tuple(AUTO) of each Success frame as written\"";
+  js << ",\n \"rx_hash\": [";
+  for (std::size_t j = 0; j < rx_hash.size(); ++j) js << (j ? "," : "") << rx_hash[j];
+  js << "],\n \"rx_queue\": [";
+  for (std::size_t j = 0; j < rx_queue.size(); ++j) js << (j ? "," : "") << rx_queue[j];
+  js << "],\n \"rss_hashes\": " << rss_eng.stats().hashes << ",\n \"rss_queue_hits\": [";
+  for (std::size_t i = 0; i < rss_eng.stats().queue_hits.size(); ++i) js << (i ? "," : "") << rss_eng.stats().queue_hits[i];
+  js << "]\n}\n";
   std::ofstream(g_out + "/" + name + ".json") << js.str();
   write_bin(name + ".mem.bin", image);
   std::vector<std::uint8_t> tb(txs.size() * sizeof(TxDescriptor)), rb(rxs.size() * sizeof(RxDescriptor));
@@ -829,6 +911,7 @@ void gen_qp_batch() {
   gen_qp_batch_case("qp_mix_a", 101, 300, 180, 0);    // RX ring runs dry part-way
   gen_qp_batch_case("qp_mix_b", 202, 400, 700, 0);    // ample RX descriptors
   gen_qp_batch_case("qp_tso", 303, 40, 300, 1);       // 9000 B TSO/GSO, odd mss, tiny headers
+  gen_qp_batch_case("qp_alias", 404, 300, 400, 2);    // overlapping RX/RX and RX/TX buffers
 }
 
 // ------------------------------------------------------ L3/L4 verification --

@@ -66,6 +66,7 @@ ABI_SYMBOLS = (
     "nicgpu_checksum_batch",
     "nicgpu_tso_checksum",
     "nicgpu_segment_gather",
+    "nicgpu_segment_gather_from",
     "nicgpu_icrc_batch",
     "nicgpu_tso_segment",
 )
@@ -102,6 +103,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_rx_offload": (i32, [vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp]),
         "nicgpu_rx_offload_ex": (i32, [vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp, vp]),
         "nicgpu_segment_gather": (i32, [vp, ctypes.c_uint64, vp, sz, vp]),
+        "nicgpu_segment_gather_from": (i32, [vp, vp, ctypes.c_uint64, vp, sz, vp]),
         "nicgpu_icrc_batch": (i32, [vp, vp, sz, i32, vp, vp, vp]),
         "nicgpu_tso_segment": (i32, [vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint64, u32, vp, vp, vp]),
         "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),

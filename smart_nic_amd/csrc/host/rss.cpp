@@ -155,6 +155,17 @@ void RssEngine::select_queue_batch(const DevicePacketBatch& batch, const TupleSp
     }
     return;
   }
+  // The per-packet path takes any key and table (rss.cpp:27-41); an RSS
+  // context holds at most NICGPU_MAX_KEY key bytes and NICGPU_MAX_TABLE
+  // entries.  A longer key is truncated, which hashes identically: tuples are
+  // <= NICGPU_MAX_TUPLE bytes, so no key bit past 8 * 64 + 31 is ever read and
+  // neither key wraps.  A larger table is refused before any device work.
+  static_assert(NICGPU_MAX_KEY * 8 > NICGPU_MAX_TUPLE * 8 + 31, "truncated keys must not wrap");
+  if (config_.table.size() > NICGPU_MAX_TABLE)
+    throw GpuError("select_queue_batch: indirection table of " + std::to_string(config_.table.size()) +
+                       " entries exceeds the GPU limit of NICGPU_MAX_TABLE = " + std::to_string(NICGPU_MAX_TABLE),
+                   NICGPU_ERR_INVALID);
+  const std::size_t key_len = config_.key.size() < NICGPU_MAX_KEY ? config_.key.size() : NICGPU_MAX_KEY;
   int dev = 0;
   int st = nicgpu_get_device(&dev);
   if (st != NICGPU_OK) throw_gpu("nicgpu_get_device", st);
@@ -163,7 +174,7 @@ void RssEngine::select_queue_batch(const DevicePacketBatch& batch, const TupleSp
     g->device = dev;
     st = nicgpu_rss_create(&g->ctx, dev);
     if (st != NICGPU_OK) throw_gpu("nicgpu_rss_create", st);
-    st = nicgpu_rss_set_key(g->ctx, config_.key.data(), config_.key.size(), stream);
+    st = nicgpu_rss_set_key(g->ctx, config_.key.data(), key_len, stream);
     if (st != NICGPU_OK) throw_gpu("nicgpu_rss_set_key", st);
     st = nicgpu_rss_set_table(g->ctx, config_.table.data(), config_.table.size(), stream);
     if (st != NICGPU_OK) throw_gpu("nicgpu_rss_set_table", st);

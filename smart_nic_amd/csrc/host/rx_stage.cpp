@@ -11,12 +11,16 @@
 //    of :416-426) into the RX buffers.
 // 5. GPU: RssEngine::select_queue_batch over the frames delivered with
 //    Success -> per-queue dispatch lists.
+// When buffers overlap (buffers_disjoint() false) run_batch goes through the
+// batch in sub-batches (resolve_prefix) and applies each sub-batch's writes in
+// layers (schedule_writes), so the in-order results of the reference hold.
 #include "nic/rx_stage.h"
 
 #include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <limits>
+#include <map>
 #include <string>
 #include <thread>
 
@@ -642,6 +646,309 @@ void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const P
   out.rx_consumed = rc;
 }
 
+namespace {
+
+struct Span64 {
+  std::uint64_t a, b;  // [a, b)
+};
+
+// Sorted by start (sorting when needed); true when no two spans share a byte.
+bool sort_disjoint(std::vector<Span64>& v, bool sorted) {
+  if (!sorted) std::sort(v.begin(), v.end(), [](const Span64& x, const Span64& y) { return x.a < y.a; });
+  for (std::size_t i = 1; i < v.size(); ++i)
+    if (v[i].a < v[i - 1].b) return false;
+  return true;
+}
+
+// Merged set of byte ranges.
+class IntervalSet {
+public:
+  bool overlaps(std::uint64_t a, std::uint64_t b) const {
+    if (a >= b) return false;
+    auto it = m_.upper_bound(a);
+    if (it != m_.begin() && std::prev(it)->second > a) return true;
+    return it != m_.end() && it->first < b;
+  }
+  void add(std::uint64_t a, std::uint64_t b) {
+    if (a >= b) return;
+    auto it = m_.upper_bound(a);
+    if (it != m_.begin() && std::prev(it)->second >= a) {
+      --it;
+      a = it->first;
+      b = std::max(b, it->second);
+      it = m_.erase(it);
+    }
+    while (it != m_.end() && it->first <= b) {
+      b = std::max(b, it->second);
+      it = m_.erase(it);
+    }
+    m_.emplace(a, b);
+  }
+
+private:
+  std::map<std::uint64_t, std::uint64_t> m_;  // start -> end
+};
+
+inline std::uint64_t write_len(const SegmentWrite& w) {
+  return static_cast<std::uint64_t>(w.prefix_len) + w.len_a + w.len_b;
+}
+
+}  // namespace
+
+bool buffers_disjoint(std::size_t mem_size, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx) {
+  // what an RX descriptor can receive: at most buffer_length bytes inside the
+  // image (:397-426); what a TX descriptor is read from: its whole buffer
+  static thread_local std::vector<Span64> r, t;
+  r.clear();
+  t.clear();
+  bool sorted = true;
+  for (const RxDescriptor& x : rx) {
+    if (x.buffer_address >= mem_size || x.buffer_length == 0) continue;
+    const std::uint64_t b = x.buffer_address + std::min<std::uint64_t>(x.buffer_length, mem_size - x.buffer_address);
+    if (!r.empty() && x.buffer_address < r.back().b) sorted = false;
+    r.push_back({x.buffer_address, b});
+  }
+  if (!sort_disjoint(r, sorted)) return false;
+  if (r.empty()) return true;
+  sorted = true;
+  for (const TxDescriptor& x : tx) {
+    if (x.length == 0 || !dma_ok(mem_size, x.buffer_address, x.length)) continue;
+    if (!t.empty() && x.buffer_address < t.back().a) sorted = false;
+    t.push_back({x.buffer_address, x.buffer_address + x.length});
+  }
+  if (!sorted) std::sort(t.begin(), t.end(), [](const Span64& x, const Span64& y) { return x.a < y.a; });
+  // r: ascending and disjoint, so its ends ascend too; for each TX span (by
+  // start) the first RX span ending after its start is the only candidate
+  std::size_t j = 0;
+  for (const Span64& s : t) {
+    while (j < r.size() && r[j].b <= s.a) ++j;
+    if (j == r.size()) break;
+    if (r[j].a < s.b) return false;
+  }
+  return true;
+}
+
+std::size_t resolve_prefix(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
+                           std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
+                           std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
+                           std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx) {
+  const ResolveCtx C{config, mem_size, plan, piece_csum, tx, rx};
+  out.tx_completions.clear();
+  out.rx_completions.clear();
+  writes.clear();
+  write_of_rx.clear();
+  AppendSink sink{config, out, writes, write_of_rx};
+  IntervalSet written;
+  std::size_t rc = 0, i = 0;
+  for (; i < tx.size(); ++i) {
+    const PacketPlan& pp = plan.packets[i];
+    bool reads_written = false;
+    for (std::uint32_t k = 0; k < pp.npieces && !reads_written; ++k) {
+      const Piece& q = plan.pieces[pp.first_piece + k];
+      reads_written = written.overlaps(q.addr, q.addr + q.len);
+    }
+    if (reads_written) break;
+    const std::size_t w0 = writes.size();
+    rc += resolve_packet(C, i, rc, stats, sink);
+    for (std::size_t j = w0; j < writes.size(); ++j)
+      if (write_of_rx[j] >= 0) written.add(writes[j].dst, writes[j].dst + write_len(writes[j]));
+  }
+  out.tx_processed = i;
+  out.rx_consumed = rc;
+  return i;
+}
+
+void schedule_writes(std::span<const SegmentWrite> writes, std::span<const std::int64_t> write_of_rx,
+                     WriteSchedule& s) {
+  s.order.clear();
+  s.layer_begin.assign(1, 0);
+  s.from_copy = false;
+  // paint[start] = (end, layer of the last write covering [start, end)): that
+  // write's layer is the highest of all the writes covering those bytes
+  std::map<std::uint64_t, std::pair<std::uint64_t, std::uint32_t>> paint;
+  std::vector<std::pair<std::uint32_t, std::uint32_t>> lj;  // (layer, j)
+  std::vector<Span64> dst, src;
+  for (std::size_t j = 0; j < writes.size(); ++j) {
+    if (write_of_rx[j] < 0) continue;
+    const SegmentWrite& w = writes[j];
+    const std::uint64_t n = write_len(w);
+    if (n == 0) continue;
+    const std::uint64_t a = w.dst, b = a + n;
+    auto it = paint.upper_bound(a);
+    if (it != paint.begin() && std::prev(it)->second.first > a) --it;
+    auto e = it;
+    std::uint32_t layer = 0;
+    for (; e != paint.end() && e->first < b; ++e) layer = std::max(layer, e->second.second + 1);
+    if (it != e) {
+      const std::uint64_t ls = it->first, re = std::prev(e)->second.first;
+      const std::uint32_t ll = it->second.second, rl = std::prev(e)->second.second;
+      paint.erase(it, e);
+      if (ls < a) paint.emplace(ls, std::make_pair(a, ll));
+      if (re > b) paint.emplace(b, std::make_pair(re, rl));
+    }
+    paint.emplace(a, std::make_pair(b, layer));
+    lj.emplace_back(layer, static_cast<std::uint32_t>(j));
+    dst.push_back({a, b});
+    if (w.len_a) src.push_back({w.src_a, w.src_a + w.len_a});
+    if (w.len_b) src.push_back({w.src_b, w.src_b + w.len_b});
+  }
+  // layers in order, posting order within each (stable by layer)
+  std::stable_sort(lj.begin(), lj.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+  s.order.reserve(lj.size());
+  for (std::size_t i = 0; i < lj.size(); ++i) {
+    if (i > 0 && lj[i].first != lj[i - 1].first) s.layer_begin.push_back(i);
+    s.order.push_back(lj[i].second);
+  }
+  s.layer_begin.push_back(lj.size());
+  if (lj.empty()) s.layer_begin.assign(1, 0);
+  // does any destination land on any source?
+  std::sort(src.begin(), src.end(), [](const Span64& x, const Span64& y) { return x.a < y.a; });
+  std::vector<Span64> merged;
+  for (const Span64& x : src) {
+    if (!merged.empty() && x.a <= merged.back().b) merged.back().b = std::max(merged.back().b, x.b);
+    else merged.push_back(x);
+  }
+  for (const Span64& d : dst) {
+    auto it = std::upper_bound(merged.begin(), merged.end(), d.a, [](std::uint64_t v, const Span64& x) { return v < x.a; });
+    if ((it != merged.begin() && std::prev(it)->b > d.a) || (it != merged.end() && it->a < d.b)) {
+      s.from_copy = true;
+      break;
+    }
+  }
+}
+
+void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
+               std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out, BatchScratch& S,
+               Backend& dev) {
+  using clock = std::chrono::steady_clock;
+  auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
+  constexpr auto kSuccess = static_cast<std::uint32_t>(CompletionCode::Success);
+  // reset `out`, keeping its storage
+  out.tx_processed = out.rx_consumed = 0;
+  out.tx_completions.clear();
+  out.rx_completions.clear();
+  out.rx_hash.clear();
+  out.rx_queue.clear();
+  for (auto& q : out.queues) q.clear();
+  out.queues.clear();
+  out.timings = RxBatchResult::Timings{};
+
+  const bool disjoint = buffers_disjoint(mem_size, tx, rx);
+  // RSS of the frames part.rx_completions[which[..]] delivered with Success,
+  // from the image as it is now.  The tuple lies in the first 82 bytes, so a
+  // frame longer than NICGPU_MAX_PACKET (max_mtu above 65531) is hashed over
+  // its first NICGPU_MAX_PACKET bytes: the same tuple, hash and queue.
+  auto rss_of = [&](RxBatchResult& part) {
+    const std::size_t m = S.which.size();
+    if (m == 0) return;
+    std::uint64_t* desc = dev.frame_desc(m);
+    for (std::size_t i = 0; i < m; ++i) {
+      const SegmentWrite& w = S.writes[S.which[i]];
+      desc[i] = NICGPU_DESC(w.dst, std::min<std::uint64_t>(write_len(w), NICGPU_MAX_PACKET));
+    }
+    const std::uint32_t* h = nullptr;
+    const std::uint16_t* q = nullptr;
+    dev.rss(m, h, q);
+    for (std::size_t i = 0; i < m; ++i) {
+      part.rx_hash[S.which[i]] = h[i];
+      part.rx_queue[S.which[i]] = q[i];
+    }
+  };
+
+  std::size_t s = 0, r = 0;
+  do {
+    RxBatchResult& part = disjoint ? out : S.part;
+    const auto txs = tx.subspan(s);
+    const auto rxs = rx.subspan(r);
+    auto t = clock::now();
+    make_plan(config, mem_size, txs, S.plan);
+    out.timings.plan_us += us_since(t);
+    t = clock::now();
+    const std::span<const std::uint16_t> cs = dev.piece_sums(S.plan.pieces);
+    out.timings.sums_us += us_since(t);
+    t = clock::now();
+    std::size_t k;
+    if (disjoint) {
+      resolve(config, mem_size, S.plan, cs, txs, rxs, stats, part, S.writes, S.write_of_rx);
+      k = txs.size();
+    } else {
+      k = resolve_prefix(config, mem_size, S.plan, cs, txs, rxs, stats, part, S.writes, S.write_of_rx);
+    }
+    out.timings.resolve_us += us_since(t);
+    const std::size_t nrx = part.rx_completions.size();
+    part.rx_hash.assign(nrx, 0);
+    part.rx_queue.assign(nrx, RxBatchResult::kNoQueue);
+    if (disjoint) {
+      // one parallel gather of every write (zero-length entries write nothing)
+      t = clock::now();
+      if (!S.writes.empty()) dev.gather(S.writes, false);
+      out.timings.gather_us += us_since(t);
+      t = clock::now();
+      if (config.rss != nullptr) {
+        S.which.clear();
+        for (std::size_t j = 0; j < nrx; ++j)
+          if (part.rx_completions[j].status == kSuccess) S.which.push_back(static_cast<std::uint32_t>(j));
+        rss_of(part);
+      }
+      out.timings.rss_us += us_since(t);
+    } else {
+      t = clock::now();
+      schedule_writes(S.writes, S.write_of_rx, S.schedule);
+      const WriteSchedule& ws = S.schedule;
+      if (ws.from_copy) dev.snapshot();
+      out.timings.gather_us += us_since(t);
+      for (std::size_t l = 0; l + 1 < ws.layer_begin.size(); ++l) {
+        t = clock::now();
+        S.layer.clear();
+        for (std::size_t i = ws.layer_begin[l]; i < ws.layer_begin[l + 1]; ++i) S.layer.push_back(S.writes[ws.order[i]]);
+        dev.gather(S.layer, ws.from_copy);
+        out.timings.gather_us += us_since(t);
+        t = clock::now();
+        if (config.rss != nullptr) {
+          S.which.clear();
+          for (std::size_t i = ws.layer_begin[l]; i < ws.layer_begin[l + 1]; ++i)
+            if (part.rx_completions[ws.order[i]].status == kSuccess) S.which.push_back(ws.order[i]);
+          rss_of(part);
+        }
+        out.timings.rss_us += us_since(t);
+      }
+      // Success frames of zero bytes (no layer): hash of an empty tuple
+      if (config.rss != nullptr) {
+        S.which.clear();
+        for (std::size_t j = 0; j < nrx; ++j)
+          if (part.rx_completions[j].status == kSuccess && write_len(S.writes[j]) == 0)
+            S.which.push_back(static_cast<std::uint32_t>(j));
+        rss_of(part);
+      }
+      out.tx_completions.insert(out.tx_completions.end(), part.tx_completions.begin(), part.tx_completions.end());
+      out.rx_completions.insert(out.rx_completions.end(), part.rx_completions.begin(), part.rx_completions.end());
+      out.rx_hash.insert(out.rx_hash.end(), part.rx_hash.begin(), part.rx_hash.end());
+      out.rx_queue.insert(out.rx_queue.end(), part.rx_queue.begin(), part.rx_queue.end());
+    }
+    s += k;
+    r += part.rx_consumed;
+  } while (s < tx.size());
+  out.tx_processed = tx.size();
+  out.rx_consumed = r;
+
+  // per-queue dispatch lists, in posting order
+  if (config.rss != nullptr) {
+    auto t = clock::now();
+    std::vector<std::size_t> cnt;
+    for (std::size_t j = 0; j < out.rx_completions.size(); ++j) {
+      if (out.rx_completions[j].status != kSuccess) continue;
+      const std::uint16_t q = out.rx_queue[j];
+      if (q >= cnt.size()) cnt.resize(static_cast<std::size_t>(q) + 1, 0);
+      cnt[q] += 1;
+    }
+    out.queues.resize(cnt.size());
+    for (std::size_t q = 0; q < cnt.size(); ++q) out.queues[q].reserve(cnt[q]);
+    for (std::size_t j = 0; j < out.rx_completions.size(); ++j)
+      if (out.rx_completions[j].status == kSuccess) out.queues[out.rx_queue[j]].push_back(static_cast<std::uint32_t>(j));
+    out.timings.rss_us += us_since(t);
+  }
+}
+
 }  // namespace rx_stage_detail
 
 namespace {
@@ -690,15 +997,91 @@ struct HostBuf {
 
 // Everything process_batch allocates, kept across batches (grown, never
 // shrunk): the device buffers, pinned staging, and the host-side plan and
-// write list, so a steady stream of batches takes no page faults.
+// write lists, so a steady stream of batches takes no page faults.
 struct BatchedQueuePair::Scratch {
-  DevBuf piece_desc, piece_csum, writes, rss_desc, rss_hash, rss_queue;
+  DevBuf piece_desc, piece_csum, writes, rss_desc, rss_hash, rss_queue, copy;
   HostBuf h_desc, h_csum, h_writes, h_rss_desc, h_hash, h_queue;
-  rx_stage_detail::Plan plan;
-  std::vector<rx_stage_detail::SegmentWrite> w;
-  std::vector<std::int64_t> write_of_rx;
-  std::vector<std::uint32_t> which;
+  rx_stage_detail::BatchScratch host;
 };
+
+namespace {
+
+// The GPU side of run_batch: every operation is a nicgpu_* launch on `stream`
+// over the device-resident image, synchronised before returning.
+class GpuBackend final : public rx_stage_detail::Backend {
+public:
+  GpuBackend(BatchedQueuePair::Scratch& s, const DeviceHostMemory& mem, const BatchedQueuePairConfig& config,
+             void* stream)
+      : S(s), mem_(mem), config_(config), stream_(stream) {}
+
+  std::span<const std::uint16_t> piece_sums(std::span<const rx_stage_detail::Piece> pieces) override {
+    const std::size_t np = pieces.size();
+    std::uint16_t* csum = S.h_csum.get<std::uint16_t>(std::max<std::size_t>(np, 1));
+    if (np == 0) return {};
+    std::uint64_t* desc = S.h_desc.get<std::uint64_t>(np);
+    rx_stage_detail::Chunks(np, config_.host_threads ? config_.host_threads : 16).run([&](std::size_t, std::size_t b, std::size_t e) {
+      for (std::size_t i = b; i < e; ++i) desc[i] = NICGPU_DESC(pieces[i].addr, pieces[i].len);
+    });
+    void* d_desc = S.piece_desc.get(np * 8);
+    void* d_cs = S.piece_csum.get(np * 2);
+    check(nicgpu_memcpy_async(d_desc, desc, np * 8, stream_), "nicgpu_memcpy_async");
+    check(nicgpu_checksum_batch(image(), static_cast<const std::uint64_t*>(d_desc), np, static_cast<std::uint16_t*>(d_cs),
+                                stream_),
+          "nicgpu_checksum_batch");
+    check(nicgpu_memcpy_async(csum, d_cs, np * 2, stream_), "nicgpu_memcpy_async");
+    check(nicgpu_stream_synchronize(stream_), "nicgpu_stream_synchronize");
+    return {csum, np};
+  }
+
+  void snapshot() override {
+    void* c = S.copy.get(std::max<std::size_t>(mem_.size, 1));
+    if (mem_.size) check(nicgpu_memcpy_async(c, mem_.base, mem_.size, stream_), "nicgpu_memcpy_async");
+    have_copy_ = true;
+  }
+
+  void gather(std::span<const rx_stage_detail::SegmentWrite> writes, bool from_copy) override {
+    const std::size_t nw = writes.size();
+    if (nw == 0) return;
+    if (from_copy && !have_copy_) throw GpuError("process_batch: gather from a copy that was never taken", NICGPU_ERR_INVALID);
+    auto* hw = S.h_writes.get<rx_stage_detail::SegmentWrite>(nw);
+    std::memcpy(hw, writes.data(), nw * sizeof(rx_stage_detail::SegmentWrite));
+    void* d_w = S.writes.get(nw * sizeof(rx_stage_detail::SegmentWrite));
+    check(nicgpu_memcpy_async(d_w, hw, nw * sizeof(rx_stage_detail::SegmentWrite), stream_), "nicgpu_memcpy_async");
+    const auto* src = from_copy ? static_cast<const std::uint8_t*>(S.copy.p) : image();
+    check(nicgpu_segment_gather_from(image(), src, mem_.size, static_cast<const nicgpu_segment_write*>(d_w), nw, stream_),
+          "nicgpu_segment_gather_from");
+    check(nicgpu_stream_synchronize(stream_), "nicgpu_stream_synchronize");
+  }
+
+  std::uint64_t* frame_desc(std::size_t n) override { return S.h_rss_desc.get<std::uint64_t>(std::max<std::size_t>(n, 1)); }
+
+  void rss(std::size_t m, const std::uint32_t*& hash, const std::uint16_t*& queue) override {
+    void* d_desc = S.rss_desc.get(m * 8);
+    void* d_h = S.rss_hash.get(m * 4);
+    void* d_q = S.rss_queue.get(m * 2);
+    check(nicgpu_memcpy_async(d_desc, S.h_rss_desc.p, m * 8, stream_), "nicgpu_memcpy_async");
+    config_.rss->select_queue_batch(
+        DevicePacketBatch{mem_.base, static_cast<const std::uint64_t*>(d_desc), m}, config_.tuple,
+        RxBatchOutputs{nullptr, static_cast<std::uint32_t*>(d_h), static_cast<std::uint16_t*>(d_q)}, stream_, true);
+    std::uint32_t* h = S.h_hash.get<std::uint32_t>(m);
+    std::uint16_t* q = S.h_queue.get<std::uint16_t>(m);
+    check(nicgpu_memcpy_async(h, d_h, m * 4, stream_), "nicgpu_memcpy_async");
+    check(nicgpu_memcpy_async(q, d_q, m * 2, stream_), "nicgpu_memcpy_async");
+    check(nicgpu_stream_synchronize(stream_), "nicgpu_stream_synchronize");
+    hash = h;
+    queue = q;
+  }
+
+private:
+  std::uint8_t* image() const { return reinterpret_cast<std::uint8_t*>(mem_.base); }
+  BatchedQueuePair::Scratch& S;
+  const DeviceHostMemory& mem_;
+  const BatchedQueuePairConfig& config_;
+  void* stream_;
+  bool have_copy_ = false;
+};
+
+}  // namespace
 
 BatchedQueuePair::BatchedQueuePair(BatchedQueuePairConfig config)
     : config_(std::move(config)), scratch_(std::make_unique<Scratch>()) {}
@@ -715,157 +1098,11 @@ RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::
 
 void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                      std::span<const RxDescriptor> rx, RxBatchResult& out, void* stream) {
-  using namespace rx_stage_detail;
-  using clock = std::chrono::steady_clock;
-  auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
   if (mem.base == nullptr && mem.size != 0) throw GpuError("process_batch: null host-memory image", NICGPU_ERR_INVALID);
-  // reset `out`, keeping its storage
-  out.tx_processed = out.rx_consumed = 0;  // resolve sizes the completion lists
-  out.rx_hash.clear();
-  out.rx_queue.clear();
-  for (auto& q : out.queues) q.clear();
-  out.queues.clear();
-  out.timings = RxBatchResult::Timings{};
-  Scratch& S = *scratch_;
-
-  auto t = clock::now();
-  make_plan(config_, mem.size, tx, S.plan);
-  const Plan& plan = S.plan;
-  out.timings.plan_us = us_since(t);
-  t = clock::now();
-  const std::size_t np = plan.pieces.size();
-
-  // (2) piece sums on the GPU
-  std::uint16_t* csum = S.h_csum.get<std::uint16_t>(std::max<std::size_t>(np, 1));
-  if (np) {
-    std::uint64_t* desc = S.h_desc.get<std::uint64_t>(np);
-    Chunks(np, config_.host_threads ? config_.host_threads : 16).run([&](std::size_t, std::size_t b, std::size_t e) {
-      for (std::size_t i = b; i < e; ++i) desc[i] = NICGPU_DESC(plan.pieces[i].addr, plan.pieces[i].len);
-    });
-    void* d_desc = S.piece_desc.get(np * 8);
-    void* d_cs = S.piece_csum.get(np * 2);
-    check(nicgpu_memcpy_async(d_desc, desc, np * 8, stream), "nicgpu_memcpy_async");
-    check(nicgpu_checksum_batch(reinterpret_cast<const std::uint8_t*>(mem.base), static_cast<const std::uint64_t*>(d_desc),
-                                np, static_cast<std::uint16_t*>(d_cs), stream),
-          "nicgpu_checksum_batch");
-    check(nicgpu_memcpy_async(csum, d_cs, np * 2, stream), "nicgpu_memcpy_async");
-    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
-  }
-  out.timings.sums_us = us_since(t);
-
-  // (3) the reference's control flow
-  t = clock::now();
-  std::vector<SegmentWrite>& writes = S.w;
-  std::vector<std::int64_t>& write_of_rx = S.write_of_rx;
+  GpuBackend dev{*scratch_, mem, config_, stream};
+  // stats are committed only when the whole batch went through
   QueuePairStats st = stats_;
-  resolve(config_, mem.size, plan, std::span<const std::uint16_t>(csum, np), tx, rx, st, out, writes, write_of_rx);
-  out.timings.resolve_us = us_since(t);
-  t = clock::now();
-
-  // Everything resolve writes (completions, writes, write_of_rx) is read
-  // below on this thread only: a worker thread reading those lines leaves
-  // them shared in another core's cache, and the next batch's resolve then
-  // pays an invalidation per line — measured 24 -> 50-90 ms for 1 M
-  // descriptors on the GPU box's EPYC.  Only make_plan and the piece
-  // descriptors (inputs of this thread) are built in parallel.
-
-  // (4) DMA writes of every segment that reached the RX buffer
-  const std::size_t nw = writes.size();
-  if (nw) {
-    SegmentWrite* hw = S.h_writes.get<SegmentWrite>(nw);
-    std::memcpy(hw, writes.data(), nw * sizeof(SegmentWrite));
-    void* d_w = S.writes.get(nw * sizeof(SegmentWrite));
-    check(nicgpu_memcpy_async(d_w, hw, nw * sizeof(SegmentWrite), stream), "nicgpu_memcpy_async");
-    check(nicgpu_segment_gather(reinterpret_cast<std::uint8_t*>(mem.base), mem.size,
-                                static_cast<const nicgpu_segment_write*>(d_w), nw, stream),
-          "nicgpu_segment_gather");
-    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
-  }
-  out.timings.gather_us = us_since(t);
-  t = clock::now();
-
-  // (5) RSS over frames delivered with Success
-  const std::size_t nrx = out.rx_completions.size();
-  out.rx_hash.assign(nrx, 0);
-  out.rx_queue.assign(nrx, RxBatchResult::kNoQueue);
-  if (config_.rss != nullptr && nrx) {
-    auto delivered = [&](std::size_t j) {
-      return out.rx_completions[j].status == static_cast<std::uint32_t>(CompletionCode::Success) && write_of_rx[j] >= 0;
-    };
-    // compaction: count per chunk, prefix, fill
-    const Chunks ch(nrx, 1);
-    std::vector<std::size_t> base(ch.k + 1, 0);
-    ch.run([&](std::size_t c, std::size_t b, std::size_t e) {
-      std::size_t n = 0;
-      for (std::size_t j = b; j < e; ++j) n += delivered(j);
-      base[c + 1] = n;
-    });
-    for (std::size_t c = 0; c < ch.k; ++c) base[c + 1] += base[c];
-    const std::size_t m = base[ch.k];
-    S.which.resize(m);
-    std::uint32_t* which = S.which.data();
-    std::uint64_t* desc = S.h_rss_desc.get<std::uint64_t>(std::max<std::size_t>(m, 1));
-    bool too_long = false;
-    ch.run([&](std::size_t c, std::size_t b, std::size_t e) {
-      std::size_t at = base[c];
-      bool bad = false;
-      for (std::size_t j = b; j < e; ++j) {
-        if (!delivered(j)) continue;
-        const SegmentWrite& w = writes[static_cast<std::size_t>(write_of_rx[j])];
-        const std::uint64_t len = static_cast<std::uint64_t>(w.prefix_len) + w.len_a + w.len_b;
-        bad |= len > NICGPU_MAX_PACKET;
-        which[at] = static_cast<std::uint32_t>(j);
-        desc[at++] = NICGPU_DESC(w.dst, len);
-      }
-      if (bad) too_long = true;  // benign race: only ever set to true
-    });
-    if (too_long) throw GpuError("process_batch: delivered frame longer than NICGPU_MAX_PACKET", NICGPU_ERR_INVALID);
-    if (m) {
-      void* d_desc = S.rss_desc.get(m * 8);
-      void* d_h = S.rss_hash.get(m * 4);
-      void* d_q = S.rss_queue.get(m * 2);
-      check(nicgpu_memcpy_async(d_desc, desc, m * 8, stream), "nicgpu_memcpy_async");
-      config_.rss->select_queue_batch(
-          DevicePacketBatch{mem.base, static_cast<const std::uint64_t*>(d_desc), m}, config_.tuple,
-          RxBatchOutputs{nullptr, static_cast<std::uint32_t*>(d_h), static_cast<std::uint16_t*>(d_q)}, stream, true);
-      std::uint32_t* h = S.h_hash.get<std::uint32_t>(m);
-      std::uint16_t* q = S.h_queue.get<std::uint16_t>(m);
-      check(nicgpu_memcpy_async(h, d_h, m * 4, stream), "nicgpu_memcpy_async");
-      check(nicgpu_memcpy_async(q, d_q, m * 2, stream), "nicgpu_memcpy_async");
-      check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
-      // scatter, and the per-queue lists (counted per chunk, then filled in order)
-      const Chunks cm(m, 1);
-      std::vector<std::vector<std::size_t>> cnt(cm.k);
-      cm.run([&](std::size_t c, std::size_t b, std::size_t e) {
-        std::vector<std::size_t>& n = cnt[c];
-        for (std::size_t i = b; i < e; ++i) {
-          out.rx_hash[which[i]] = h[i];
-          out.rx_queue[which[i]] = q[i];
-          if (q[i] >= n.size()) n.resize(static_cast<std::size_t>(q[i]) + 1, 0);
-          n[q[i]] += 1;
-        }
-      });
-      std::size_t nq = 0;
-      for (const auto& n : cnt) nq = std::max(nq, n.size());
-      out.queues.resize(nq);
-      // cnt[c][q] becomes chunk c's first slot in queue q
-      for (std::size_t qq = 0; qq < nq; ++qq) {
-        std::size_t at = 0;
-        for (auto& n : cnt) {
-          if (qq >= n.size()) continue;
-          const std::size_t k = n[qq];
-          n[qq] = at;
-          at += k;
-        }
-        out.queues[qq].resize(at);
-      }
-      cm.run([&](std::size_t c, std::size_t b, std::size_t e) {
-        std::vector<std::size_t>& n = cnt[c];
-        for (std::size_t i = b; i < e; ++i) out.queues[q[i]][n[q[i]]++] = which[i];
-      });
-    }
-  }
-  out.timings.rss_us = us_since(t);
+  rx_stage_detail::run_batch(config_, mem.size, tx, rx, st, out, scratch_->host, dev);
   stats_ = st;
 }
 

@@ -1415,6 +1415,7 @@ constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0
 // HBM-bound at 2 x bytes.
 struct GatherParams {
   uint8_t* mem;
+  const uint8_t* src;  // sources: mem itself, or a copy of it
   uint64_t mem_size;
   const nicgpu_segment_write* w;
   size_t n;
@@ -1491,8 +1492,8 @@ __global__ __launch_bounds__(kBlock) void segment_gather_kernel(GatherParams P) 
         w.len_a > P.mem_size - w.src_a || w.src_b > P.mem_size || w.len_b > P.mem_size - w.src_b)
       continue;
     if (lane < plen) P.mem[w.dst + lane] = (uint8_t) (w.prefix >> (8 * lane));
-    wave_copy<true, false>(P.mem, w.dst + plen, P.mem, P.mem_size, w.src_a, w.len_a, lane);
-    wave_copy<true, false>(P.mem, w.dst + plen + w.len_a, P.mem, P.mem_size, w.src_b, w.len_b, lane);
+    wave_copy<true, false>(P.mem, w.dst + plen, P.src, P.mem_size, w.src_a, w.len_a, lane);
+    wave_copy<true, false>(P.mem, w.dst + plen + w.len_a, P.src, P.mem_size, w.src_b, w.len_b, lane);
   }
 }
 
@@ -2398,12 +2399,17 @@ int nicgpu_tso_segment(const uint8_t* frames, const uint64_t* desc, const uint16
 
 int nicgpu_segment_gather(uint8_t* mem, uint64_t mem_size, const nicgpu_segment_write* writes, size_t n,
                           void* stream) {
+  return nicgpu_segment_gather_from(mem, mem, mem_size, writes, n, stream);
+}
+
+int nicgpu_segment_gather_from(uint8_t* mem, const uint8_t* src, uint64_t mem_size,
+                               const nicgpu_segment_write* writes, size_t n, void* stream) {
   if (n == 0) return NICGPU_OK;
-  if (!mem || !writes) return NICGPU_ERR_INVALID;
+  if (!mem || !src || !writes) return NICGPU_ERR_INVALID;
   const DeviceInfo* di = nullptr;
   int st = current_device_info(&di);
   if (st != NICGPU_OK) return st;
-  GatherParams P{mem, mem_size, writes, n};
+  GatherParams P{mem, src, mem_size, writes, n};
   const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
   const uint64_t cap = (uint64_t) di->cus * 8;
   const unsigned grid = (unsigned) (want < cap ? want : cap);

@@ -80,7 +80,7 @@ void test_checksum_batch(std::mt19937_64& rng) {
 }
 
 void test_select_queue_batch(std::mt19937_64& rng, const std::vector<std::uint8_t>& key, std::vector<std::uint16_t> table,
-                             TupleSpec tuple) {
+                             TupleSpec tuple, bool grow_table = true) {
   std::vector<std::uint8_t> frames;
   std::vector<std::uint64_t> desc;
   make_batch(rng, 4000, frames, desc);
@@ -112,6 +112,7 @@ void test_select_queue_batch(std::mt19937_64& rng, const std::vector<std::uint8_
   // a second batch accumulates
   gpu_engine.select_queue_batch(batch, tuple, RxBatchOutputs{nullptr, nullptr, qs.as<std::uint16_t>()});
   assert(gpu_engine.stats().hashes == 2 * n);
+  if (!grow_table) return;
   // set_table invalidates the device table; queue_hits keeps its size
   const std::size_t hits_size = gpu_engine.stats().queue_hits.size();
   assert(hits_size == cpu_engine.config().table.size());
@@ -150,6 +151,19 @@ int main() {
   std::vector<std::uint16_t> big(3000);
   for (std::size_t i = 0; i < big.size(); ++i) big[i] = static_cast<std::uint16_t>(i);
   test_select_queue_batch(rng, ms, big, TupleSpec{TupleMode::Auto, 0, 0});        // table > LDS histogram
+  // keys past NICGPU_MAX_KEY (truncated for the device, exactly) and the
+  // largest tuples; tables past the reference-typical sizes up to the limit
+  std::vector<std::uint8_t> long_key(NICGPU_MAX_KEY + 77);
+  for (auto& b : long_key) b = static_cast<std::uint8_t>(rng());
+  test_select_queue_batch(rng, long_key, t16, TupleSpec{TupleMode::Raw, 0, 64});
+  test_select_queue_batch(rng, std::vector<std::uint8_t>(long_key.begin(), long_key.begin() + NICGPU_MAX_KEY), t16,
+                          TupleSpec{TupleMode::Auto, 0, 0});
+  std::vector<std::uint16_t> t65537(65537);
+  for (std::size_t i = 0; i < t65537.size(); ++i) t65537[i] = static_cast<std::uint16_t>(i * 3);
+  test_select_queue_batch(rng, ms, t65537, TupleSpec{TupleMode::Auto, 0, 0});
+  std::vector<std::uint16_t> tmax(NICGPU_MAX_TABLE);
+  for (std::size_t i = 0; i < tmax.size(); ++i) tmax[i] = static_cast<std::uint16_t>(i ^ (i >> 16));
+  test_select_queue_batch(rng, ms, tmax, TupleSpec{TupleMode::Raw, 0, 64}, false);
   test_errors();
   std::puts("gpu_batch_test: ok");
   return 0;

@@ -7,12 +7,14 @@
 #include <cstdio>
 #include <numeric>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "nic/checksum.h"
 #include "nic/offload.h"
 #include "nic/rss.h"
 #include "nic/tx_rx.h"
+#include "nicgpu.h"
 #include "oracle.h"
 
 using namespace nic;
@@ -160,6 +162,41 @@ void test_rss_random_vs_oracle() {
   }
 }
 
+// The GPU batch path's limits (include/nic/rss.h, select_queue_batch): a
+// table over NICGPU_MAX_TABLE is refused with NICGPU_ERR_INVALID before any
+// device work (so this runs without a GPU), while select_queue takes it, as
+// the reference's does (src/rss.cpp:35-41, 49-61).
+void test_batch_limits() {
+  std::vector<std::uint16_t> table(static_cast<std::size_t>(NICGPU_MAX_TABLE) + 1);
+  for (std::size_t i = 0; i < table.size(); ++i) table[i] = static_cast<std::uint16_t>(i * 7);
+  RssEngine e{RssConfig{{}, table}};
+  bool threw = false;
+  try {
+    e.select_queue_batch(DevicePacketBatch{nullptr, nullptr, 0}, TupleSpec{}, RxBatchOutputs{});
+  } catch (const GpuError& g) {
+    threw = g.status() == NICGPU_ERR_INVALID && std::string(g.what()).find("NICGPU_MAX_TABLE") != std::string::npos;
+  }
+  assert(threw);
+  assert(e.stats().hashes == 0);
+  const std::uint8_t tuple[12] = {192, 168, 1, 100, 192, 168, 1, 1, 0x1F, 0x90, 0, 80};
+  std::uint32_t h = 0, idx = 0;
+  const std::uint16_t q = oracle_select_queue(e.config().key.data(), e.config().key.size(), table.data(), table.size(),
+                                              tuple, sizeof(tuple), &h, &idx);
+  assert(*e.select_queue(tuple) == q && e.stats().hashes == 1);
+  // keys longer than NICGPU_MAX_KEY hash like their first NICGPU_MAX_KEY bytes
+  // for every tuple the GPU path can hand over (<= NICGPU_MAX_TUPLE bytes):
+  // no key bit past 8 * 64 + 31 is read (what select_queue_batch relies on)
+  std::mt19937_64 rng(5);
+  for (int it = 0; it < 50; ++it) {
+    std::vector<std::uint8_t> key(NICGPU_MAX_KEY + 1 + rng() % 300), data(1 + rng() % NICGPU_MAX_TUPLE);
+    for (auto& b : key) b = static_cast<std::uint8_t>(rng());
+    for (auto& b : data) b = static_cast<std::uint8_t>(rng());
+    const std::vector<std::uint8_t> head(key.begin(), key.begin() + NICGPU_MAX_KEY);
+    const RssEngine full{RssConfig{key, {1}}}, cut{RssConfig{head, {1}}};
+    assert(full.hash(data) == cut.hash(data));
+  }
+}
+
 void test_abi_layouts() {
   static_assert(sizeof(TxDescriptor) == 32 && sizeof(RxDescriptor) == 24);
   assert(kMaxTsoSegments == 64 && kMaxMss == 9000 && kJumboMtu == 9000 && kMaxJumboFrame == 9216);
@@ -174,6 +211,7 @@ int main() {
   test_rss_reference_cases();
   test_rss_random_vs_oracle();
   test_abi_layouts();
+  test_batch_limits();
   std::puts("host_api_test: ok");
   return 0;
 }

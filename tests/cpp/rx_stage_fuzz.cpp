@@ -1,11 +1,16 @@
 // rx_stage_fuzz.cpp — randomised batches through the reference QueuePair
 // (src/queue_pair.cpp:67-460, compiled from /root/reference in this
-// container) and through nic::BatchedQueuePair's host logic
-// (rx_stage_detail::make_plan + resolve, piece sums from the oracle), in the
-// same process.  Compared per batch: every TX/RX CompletionEntry in posting
-// order, QueuePairStats, RX descriptors consumed, interrupts delivered (the
-// reference's InterruptDispatcher with a packet threshold of 1) and the whole
-// memory image after the DMA writes.
+// container) and through nic::BatchedQueuePair's driver
+// (rx_stage_detail::run_batch with the CPU backend of cpu_backend.h: piece
+// sums from the oracle), in the same process.  Compared per batch: every
+// TX/RX CompletionEntry in posting order, QueuePairStats, RX descriptors
+// consumed, interrupts delivered (the reference's InterruptDispatcher with a
+// packet threshold of 1), the whole memory image after the DMA writes, and the
+// RSS hash/queue of every frame delivered with Success against the bytes the
+// reference's DMA engine wrote for it (recorded as they are written, so a
+// buffer that a later segment overwrites is hashed as delivered).
+// One batch in three makes RX buffers overlap: recycled buffers, buffers
+// straddling the previous one, and buffers inside the TX region.
 //
 //   rx_stage_fuzz <first_seed> <count>
 #undef NDEBUG
@@ -20,11 +25,14 @@
 #include "nic/queue_pair.h"
 #include "nic/rx_stage.h"
 #include "nic/simple_host_memory.h"
+#include "cpu_backend.h"
 #include "oracle.h"
 
 using namespace nic;
 
 namespace {
+
+std::size_t g_overlapping = 0, g_split = 0, g_snap = 0;  // batches that took each careful step
 
 struct Rng {
   std::uint64_t s;
@@ -47,6 +55,32 @@ bool same(const CompletionEntry& a, const CompletionEntry& b) {
 }
 
 bool same(const QueuePairStats& a, const QueuePairStats& b) { return std::memcmp(&a, &b, sizeof(a)) == 0; }
+
+// SimpleHostMemory that records every successful write (the RX segment DMA
+// writes of QueuePair::handle_rx_segment, :416-426) in order.
+class RecordingMemory final : public HostMemory {
+public:
+  explicit RecordingMemory(HostMemoryConfig c) : mem_(c) {}
+  HostMemoryConfig config() const noexcept override { return mem_.config(); }
+  HostMemoryResult translate(HostAddress a, std::size_t n, HostMemoryView& v) override { return mem_.translate(a, n, v); }
+  HostMemoryResult translate_const(HostAddress a, std::size_t n, ConstHostMemoryView& v) const override {
+    return mem_.translate_const(a, n, v);
+  }
+  HostMemoryResult read(HostAddress a, std::span<std::byte> b) const override { return mem_.read(a, b); }
+  HostMemoryResult write(HostAddress a, std::span<const std::byte> d) override {
+    HostMemoryResult r = mem_.write(a, d);
+    if (r.ok() && recording) {
+      const auto* p = reinterpret_cast<const std::uint8_t*>(d.data());
+      writes.emplace_back(p, p + d.size());
+    }
+    return r;
+  }
+  bool recording = false;
+  std::vector<std::vector<std::uint8_t>> writes;
+
+private:
+  SimpleHostMemory mem_;
+};
 
 // Balance a buffer so that compute_checksum(buf) == 0 by adjusting the 16-bit
 // word at even offset `at` (needs at + 2 <= size).
@@ -115,6 +149,24 @@ int run_case(std::uint64_t seed) {
     x.vlan_tag = static_cast<std::uint16_t>(r.below(65536));
     x.gro_enabled = r.below(4) == 0;
   }
+  // overlapping buffers: the reference writes them in order (last write wins)
+  // and reads a TX buffer after the earlier segments' writes
+  const bool alias = r.below(3) == 0;
+  if (alias && nrx > 1) {
+    for (std::size_t j = 1; j < nrx; ++j) {
+      RxDescriptor& x = rx[j];
+      const std::uint32_t k = r.below(12);
+      if (k < 3) {  // a recycled buffer
+        const RxDescriptor& y = rx[r.below(static_cast<std::uint32_t>(j))];
+        x.buffer_address = y.buffer_address;
+        if (r.below(2)) x.buffer_length = y.buffer_length;
+      } else if (k < 5) {  // straddling the previous buffer
+        x.buffer_address = rx[j - 1].buffer_address + r.below(std::max<std::uint32_t>(1, rx[j - 1].buffer_length));
+      } else if (k < 7 && ntx) {  // inside a TX buffer (read by a later TX descriptor, or an earlier one)
+        x.buffer_address = addr[r.below(static_cast<std::uint32_t>(ntx))] + r.below(16);
+      }
+    }
+  }
   const std::size_t mem_size = at + 32;
   for (std::size_t i = 0; i < ntx; ++i)
     if (r.below(40) == 0) tx[i].buffer_address = r.below(2) ? mem_size + 1 + i : mem_size - tx[i].length / 2;
@@ -125,9 +177,19 @@ int run_case(std::uint64_t seed) {
   const bool tx_irq = r.below(2), rx_irq = r.below(4) != 0;
   const std::uint16_t qid = static_cast<std::uint16_t>(r.below(8));
 
+  // RSS: the 40-B Microsoft key or the reference's 20-B default, 128 entries
+  static const std::vector<std::uint8_t> ms_key = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67,
+                                                   0x25, 0x3d, 0x43, 0xa3, 0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb,
+                                                   0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3, 0x80, 0x30,
+                                                   0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
+  std::vector<std::uint16_t> rss_table(r.below(2) ? 128 : 1 + r.below(200));
+  for (auto& q : rss_table) q = static_cast<std::uint16_t>(r.below(16));
+  const RssConfig rss_cfg{r.below(2) ? ms_key : std::vector<std::uint8_t>{}, rss_table};
+
   // ---- reference
-  SimpleHostMemory mem{HostMemoryConfig{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false}};
+  RecordingMemory mem{HostMemoryConfig{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false}};
   assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(image))).ok());
+  mem.recording = true;
   DMAEngine dma{mem};
   std::size_t ref_irq = 0;
   MsixTable table(8);
@@ -163,7 +225,7 @@ int run_case(std::uint64_t seed) {
   std::vector<std::byte> ref_after(mem_size);
   assert(mem.read(0, ref_after).ok());
 
-  // ---- batched stage (host logic; sums from the oracle)
+  // ---- batched stage: run_batch over the CPU backend
   using namespace rx_stage_detail;
   BatchedQueuePairConfig cfg;
   cfg.queue_id = qid;
@@ -175,28 +237,36 @@ int run_case(std::uint64_t seed) {
     assert(q == qid);
     ++our_irq;
   };
-  const Plan plan = make_plan(cfg, mem_size, tx);
-  std::vector<std::uint16_t> cs(plan.pieces.size());
-  for (std::size_t i = 0; i < cs.size(); ++i) {
-    assert(plan.pieces[i].len <= 65535u);
-    cs[i] = oracle_compute_checksum(image.data() + plan.pieces[i].addr, plan.pieces[i].len);
-  }
+  RssEngine engine{rss_cfg};
+  cfg.rss = &engine;
+  std::vector<std::uint8_t> ours = image;
+  test::CpuBackend dev{ours, &engine, TupleSpec{}};
   RxBatchResult out;
   QueuePairStats st{};
-  std::vector<SegmentWrite> writes;
-  std::vector<std::int64_t> wof;
-  resolve(cfg, mem_size, plan, cs, tx, rx, st, out, writes, wof);
-  std::vector<std::uint8_t> ours = image;
-  for (const auto& w : writes) {
-    std::uint64_t d = w.dst;
-    for (std::uint32_t j = 0; j < w.prefix_len; ++j) ours[d++] = static_cast<std::uint8_t>(w.prefix >> (8 * j));
-    std::memcpy(ours.data() + d, image.data() + w.src_a, w.len_a);
-    std::memcpy(ours.data() + d + w.len_a, image.data() + w.src_b, w.len_b);
-  }
+  BatchScratch scratch;
+  run_batch(cfg, mem_size, tx, rx, st, out, scratch, dev);
+  if (!buffers_disjoint(mem_size, tx, rx)) g_overlapping += 1;
+  if (dev.sum_calls > 1) g_split += 1;
+  if (dev.snapshots) g_snap += 1;
 
   // the speculative parallel resolve (no interrupt callback, forced onto 4
   // threads even for these small batches) must equal the sequential one
   {
+    const Plan plan = make_plan(cfg, mem_size, tx);
+    std::vector<std::uint16_t> cs(plan.pieces.size());
+    for (std::size_t i = 0; i < cs.size(); ++i) {
+      assert(plan.pieces[i].len <= 65535u);
+      cs[i] = oracle_compute_checksum(image.data() + plan.pieces[i].addr, plan.pieces[i].len);
+    }
+    RxBatchResult sout;
+    QueuePairStats sst{};
+    std::vector<SegmentWrite> writes;
+    std::vector<std::int64_t> wof;
+    BatchedQueuePairConfig scfg = cfg;
+    scfg.on_interrupt = nullptr;
+    resolve(scfg, mem_size, plan, cs, tx, rx, sst, sout, writes, wof, 1);
+    const RxBatchResult& out = sout;
+    const QueuePairStats& st = sst;
     BatchedQueuePairConfig pcfg = cfg;
     pcfg.on_interrupt = nullptr;
     RxBatchResult pout;
@@ -217,7 +287,42 @@ int run_case(std::uint64_t seed) {
     }
   }
 
-  bool ok = out.tx_completions.size() == ref_tx.size() && out.rx_completions.size() == ref_rx.size();
+  // RSS of each frame delivered with Success, from the bytes the reference
+  // wrote for it: recorded writes pair with RX completions that carry a write
+  // (Success and ChecksumError: handle_rx_segment writes, then verifies)
+  bool rss_ok = true;
+  {
+    std::size_t k = 0, delivered = 0;
+    RssEngine expect{rss_cfg};
+    for (std::size_t j = 0; j < ref_rx.size() && rss_ok; ++j) {
+      const auto status = static_cast<CompletionCode>(ref_rx[j].status);
+      if (status != CompletionCode::Success && status != CompletionCode::ChecksumError) continue;
+      if (k >= mem.writes.size()) {
+        rss_ok = false;
+        break;
+      }
+      const std::vector<std::uint8_t>& bytes = mem.writes[k++];
+      if (status != CompletionCode::Success) continue;
+      ++delivered;
+      std::uint8_t t[64];
+      const std::size_t tl = oracle_extract_tuple(bytes.data(), bytes.size(), ORACLE_TUPLE_AUTO, 0, 0, t);
+      const std::span<const std::uint8_t> tuple(t, tl);
+      const std::uint32_t h = RssEngine{rss_cfg}.hash(tuple);
+      const std::uint16_t q = *expect.select_queue(tuple);
+      rss_ok = j < out.rx_hash.size() && out.rx_hash[j] == h && out.rx_queue[j] == q;
+    }
+    rss_ok = rss_ok && k == mem.writes.size();
+    rss_ok = rss_ok && engine.stats().hashes == expect.stats().hashes && engine.stats().queue_hits == expect.stats().queue_hits;
+    std::size_t listed = 0;
+    for (std::size_t q = 0; q < out.queues.size() && rss_ok; ++q) {
+      listed += out.queues[q].size();
+      for (std::size_t i = 0; i < out.queues[q].size() && rss_ok; ++i)
+        rss_ok = out.rx_queue[out.queues[q][i]] == q && (i == 0 || out.queues[q][i - 1] < out.queues[q][i]);
+    }
+    rss_ok = rss_ok && listed == delivered;
+  }
+
+  bool ok = rss_ok && out.tx_completions.size() == ref_tx.size() && out.rx_completions.size() == ref_rx.size();
   for (std::size_t i = 0; ok && i < ref_tx.size(); ++i) ok = same(out.tx_completions[i], ref_tx[i]);
   for (std::size_t i = 0; ok && i < ref_rx.size(); ++i) ok = same(out.rx_completions[i], ref_rx[i]);
   ok = ok && same(st, qp.stats());
@@ -225,8 +330,9 @@ int run_case(std::uint64_t seed) {
   ok = ok && our_irq == ref_irq;
   ok = ok && std::memcmp(ours.data(), ref_after.data(), mem_size) == 0;
   if (!ok) {
-    std::fprintf(stderr, "seed %llu: mismatch (tx %zu/%zu rx %zu/%zu irq %zu/%zu)\n", (unsigned long long) seed,
-                 out.tx_completions.size(), ref_tx.size(), out.rx_completions.size(), ref_rx.size(), our_irq, ref_irq);
+    std::fprintf(stderr, "seed %llu: mismatch (alias %d rss %d tx %zu/%zu rx %zu/%zu irq %zu/%zu)\n",
+                 (unsigned long long) seed, int(alias), int(rss_ok), out.tx_completions.size(), ref_tx.size(),
+                 out.rx_completions.size(), ref_rx.size(), our_irq, ref_irq);
     return 1;
   }
   return 0;
@@ -240,6 +346,8 @@ int main(int argc, char** argv) {
   int bad = 0;
   for (std::uint64_t s = first; s < first + count; ++s) bad += run_case(s);
   if (bad) return 1;
-  std::printf("rx_stage_fuzz: ok (%llu batches)\n", (unsigned long long) count);
+  std::printf("rx_stage_fuzz: ok (%llu batches; %zu with overlapping buffers, %zu split into sub-batches, %zu gathered "
+              "from a copy)\n",
+              (unsigned long long) count, g_overlapping, g_split, g_snap);
   return 0;
 }

@@ -101,5 +101,25 @@ def test_batch_entry_points_validate_before_device_access():
     assert lib.nicgpu_segment_gather(None, 0, None, 0, None) == OK
     assert lib.nicgpu_segment_gather(None, 64, p, 1, None) == INV
     assert lib.nicgpu_segment_gather(p, 64, None, 1, None) == INV
-    # nicgpu_checksum_batch: the RX pass without RSS
+    # nicgpu_segment_gather_from(mem, src, mem_size, writes, n, stream)
+    assert lib.nicgpu_segment_gather_from(None, None, 0, None, 0, None) == OK
+    assert lib.nicgpu_segment_gather_from(None, p, 64, p, 1, None) == INV
+    assert lib.nicgpu_segment_gather_from(p, None, 64, p, 1, None) == INV
+    assert lib.nicgpu_segment_gather_from(p, p, 64, None, 1, None) == INV
+    # nicgpu_checksum_batch(frames, desc, n, out, stream): the RX pass without RSS
     assert lib.nicgpu_checksum_batch(None, None, 0, None, None) == OK
+    assert lib.nicgpu_checksum_batch(None, p, 1, p, None) == INV
+    assert lib.nicgpu_checksum_batch(p, None, 1, p, None) == INV
+    assert lib.nicgpu_checksum_batch(mis, p, 1, p, None) == INV
+    # nicgpu_rx_offload_ex(ctx, frames, desc, n, mode, raw_off, raw_len, csum, hash, queue, hits, l34, stream)
+    NONE, AUTO, RAW = sna.TUPLE_NONE, sna.TUPLE_AUTO, sna.TUPLE_RAW
+    assert lib.nicgpu_rx_offload_ex(None, None, None, 0, NONE, 0, 0, None, None, None, None, None, None) == OK
+    assert lib.nicgpu_rx_offload_ex(None, None, p, 1, NONE, 0, 0, p, None, None, None, p, None) == INV
+    assert lib.nicgpu_rx_offload_ex(None, p, None, 1, NONE, 0, 0, p, None, None, None, p, None) == INV
+    assert lib.nicgpu_rx_offload_ex(None, mis, p, 1, NONE, 0, 0, p, None, None, None, p, None) == INV
+    assert lib.nicgpu_rx_offload_ex(None, p, p, 1, NONE, 0, 0, None, p, None, None, None, None) == INV  # hash without RSS
+    assert lib.nicgpu_rx_offload_ex(None, p, p, 1, NONE, 0, 0, None, None, p, None, None, None) == INV  # queue without RSS
+    assert lib.nicgpu_rx_offload_ex(None, p, p, 1, NONE, 0, 0, None, None, None, p, None, None) == INV  # hits without RSS
+    assert lib.nicgpu_rx_offload_ex(None, p, p, 1, 7, 0, 0, p, None, None, None, None, None) == INV     # unknown mode
+    assert lib.nicgpu_rx_offload_ex(None, p, p, 1, RAW, 60, 8, p, None, None, None, None, None) == INV  # window past 64 B
+    assert lib.nicgpu_rx_offload_ex(None, p, p, 1, AUTO, 0, 0, p, p, p, None, None, None) == INV      # RSS without ctx

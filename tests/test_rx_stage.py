@@ -2,9 +2,11 @@
 batches run through the reference QueuePair::process_once
 (tests/golden/qp_*.json; oracle/gen_golden.cpp, src/queue_pair.cpp:67-460).
 
-cpu: the stage's host logic (plan + resolve) with piece checksums from the
-     oracle and the DMA writes applied on a host copy — completions, stats and
-     the RX buffer bytes must equal the reference's.
+cpu: the stage's driver (rx_stage_detail::run_batch) over a CPU backend
+     (tests/cpp/cpu_backend.h: piece checksums from the oracle, DMA writes on a
+     host copy, RSS through the host RssEngine) — completions, stats, the RX
+     buffer bytes and the RSS hash/queue of every delivered frame must equal
+     the reference's.  qp_alias has overlapping RX/RX and RX/TX buffers.
 gpu: the product path end to end (GPU piece sums, GPU gather of the segments,
      GPU RSS of the delivered frames), same comparison plus RSS dispatch.
 """
@@ -19,7 +21,7 @@ from test_host_cpp import _build
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
-CASES = ["qp_mix_a", "qp_mix_b", "qp_tso"]
+CASES = ["qp_mix_a", "qp_mix_b", "qp_tso", "qp_alias"]
 
 
 def _flatten(name, out_dir):
@@ -31,6 +33,9 @@ def _flatten(name, out_dir):
     lines.append(" ".join(str(x) for x in d["stats"]))
     lines.append(" ".join(d["rx_region_fnv"]))
     lines.append(d["mem_fnv"])
+    lines.append(" ".join(str(x) for x in d["rx_hash"]))
+    lines.append(" ".join(str(x) for x in d["rx_queue"]))
+    lines.append(f'{d["rss_hashes"]} {len(d["rss_queue_hits"])} ' + " ".join(str(x) for x in d["rss_queue_hits"]))
     path = os.path.join(out_dir, name + ".expect.txt")
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
