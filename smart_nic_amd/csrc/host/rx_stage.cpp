@@ -696,34 +696,99 @@ inline std::uint64_t write_len(const SegmentWrite& w) {
 }  // namespace
 
 bool buffers_disjoint(std::size_t mem_size, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx) {
-  // what an RX descriptor can receive: at most buffer_length bytes inside the
-  // image (:397-426); what a TX descriptor is read from: its whole buffer
-  static thread_local std::vector<Span64> r, t;
-  r.clear();
-  t.clear();
-  bool sorted = true;
-  for (const RxDescriptor& x : rx) {
-    if (x.buffer_address >= mem_size || x.buffer_length == 0) continue;
-    const std::uint64_t b = x.buffer_address + std::min<std::uint64_t>(x.buffer_length, mem_size - x.buffer_address);
-    if (!r.empty() && x.buffer_address < r.back().b) sorted = false;
-    r.push_back({x.buffer_address, b});
+  // What an RX descriptor can receive: at most buffer_length bytes inside the
+  // image (:397-426); what a TX descriptor is read from: its whole buffer.
+  auto rx_span = [&](const RxDescriptor& x, Span64& sp) {
+    if (x.buffer_address >= mem_size || x.buffer_length == 0) return false;
+    sp = {x.buffer_address, x.buffer_address + std::min<std::uint64_t>(x.buffer_length, mem_size - x.buffer_address)};
+    return true;
+  };
+  auto tx_span = [&](const TxDescriptor& x, Span64& sp) {
+    if (x.length == 0 || !dma_ok(mem_size, x.buffer_address, x.length)) return false;
+    sp = {x.buffer_address, x.buffer_address + x.length};
+    return true;
+  };
+  // RX descriptors whose spans ascend and are disjoint (checked below) are
+  // searched in place: first_after(a) = the first with an end past a, the
+  // only one that can overlap a span starting at a (their ends ascend too).
+  auto next_valid = [&](std::size_t j) {
+    Span64 sp;
+    while (j < rx.size() && !rx_span(rx[j], sp)) ++j;
+    return j;
+  };
+  auto first_after = [&](std::uint64_t a) {
+    std::size_t lo = 0, hi = rx.size();
+    while (lo < hi) {
+      const std::size_t mid = lo + (hi - lo) / 2, m = next_valid(mid);
+      Span64 sp{};
+      if (m == rx.size()) {
+        hi = mid;
+        continue;
+      }
+      (void) rx_span(rx[m], sp);
+      if (sp.b <= a) lo = m + 1;
+      else hi = mid;
+    }
+    return next_valid(lo);
+  };
+  // One parallel pass in the ring layout (no copies, no sort): chunk c checks
+  // its share of the RX descriptors for ascending disjoint spans, and sweeps
+  // its share of the TX spans (ascending within the chunk) against them.
+  const Chunks ch(std::max(rx.size(), tx.size()));
+  struct Part {
+    bool rx_ok = true, tx_asc = true, hit = false, any_rx = false;
+    Span64 rx_first{}, rx_last{};
+  };
+  std::vector<Part> part(ch.k);
+  ch.run([&](std::size_t c, std::size_t, std::size_t) {
+    Part& P = part[c];
+    Span64 sp;
+    for (std::size_t j = rx.size() * c / ch.k, e = rx.size() * (c + 1) / ch.k; j < e; ++j) {
+      if (!rx_span(rx[j], sp)) continue;
+      if (!P.any_rx) P.rx_first = sp;
+      else if (sp.a < P.rx_last.b) P.rx_ok = false;
+      P.any_rx = true;
+      P.rx_last = sp;
+    }
+    std::size_t j = rx.size() + 1;  // not searched yet
+    std::uint64_t last = 0;
+    for (std::size_t i = tx.size() * c / ch.k, e = tx.size() * (c + 1) / ch.k; i < e && !P.hit; ++i) {
+      if (!tx_span(tx[i], sp)) continue;
+      if (j > rx.size()) {
+        j = first_after(sp.a);
+      } else if (sp.a < last) {
+        P.tx_asc = false;
+        return;
+      }
+      last = sp.a;
+      Span64 r{};
+      while (j < rx.size() && (!rx_span(rx[j], r) || r.b <= sp.a)) ++j;
+      if (j < rx.size() && r.a < sp.b) P.hit = true;
+    }
+  });
+  bool rx_ok = true, tx_asc = true, hit = false;
+  const Span64* prev = nullptr;
+  for (const Part& P : part) {
+    rx_ok = rx_ok && P.rx_ok && (!P.any_rx || prev == nullptr || prev->b <= P.rx_first.a);
+    if (P.any_rx) prev = &P.rx_last;
+    tx_asc = tx_asc && P.tx_asc;
+    hit = hit || P.hit;
   }
-  if (!sort_disjoint(r, sorted)) return false;
-  if (r.empty()) return true;
-  sorted = true;
-  for (const TxDescriptor& x : tx) {
-    if (x.length == 0 || !dma_ok(mem_size, x.buffer_address, x.length)) continue;
-    if (!t.empty() && x.buffer_address < t.back().a) sorted = false;
-    t.push_back({x.buffer_address, x.buffer_address + x.length});
-  }
-  if (!sorted) std::sort(t.begin(), t.end(), [](const Span64& x, const Span64& y) { return x.a < y.a; });
-  // r: ascending and disjoint, so its ends ascend too; for each TX span (by
-  // start) the first RX span ending after its start is the only candidate
+  if (rx_ok && tx_asc) return !hit;
+  // general layouts: sort
+  std::vector<Span64> r, t;
+  Span64 sp;
+  for (const RxDescriptor& x : rx)
+    if (rx_span(x, sp)) r.push_back(sp);
+  if (!sort_disjoint(r, false)) return false;
+  for (const TxDescriptor& x : tx)
+    if (tx_span(x, sp)) t.push_back(sp);
+  std::sort(t.begin(), t.end(), [](const Span64& x, const Span64& y) { return x.a < y.a; });
   std::size_t j = 0;
-  for (const Span64& s : t) {
-    while (j < r.size() && r[j].b <= s.a) ++j;
+  for (const Span64& x : t) {
+    while (j < r.size() && r[j].b <= x.a) ++j;
     if (j == r.size()) break;
-    if (r[j].a < s.b) return false;
+    if (r[j].a < x.b) return false;
   }
   return true;
 }

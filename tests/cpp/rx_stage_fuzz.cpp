@@ -14,6 +14,7 @@
 //
 //   rx_stage_fuzz <first_seed> <count>
 #undef NDEBUG
+#include <algorithm>
 #include <cassert>
 #include <cstdio>
 #include <cstdlib>
@@ -89,6 +90,85 @@ void balance(std::vector<std::uint8_t>& b, std::size_t at) {
   const std::uint16_t c = oracle_compute_checksum(b.data(), b.size());  // ~sum
   b[at] = static_cast<std::uint8_t>(c >> 8);
   b[at + 1] = static_cast<std::uint8_t>(c);
+}
+
+// Pairwise definition of rx_stage_detail::buffers_disjoint.
+bool disjoint_brute(std::size_t mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx) {
+  auto rxs = [&](const RxDescriptor& x, std::uint64_t& a, std::uint64_t& b) {
+    if (x.buffer_address >= mem || x.buffer_length == 0) return false;
+    a = x.buffer_address;
+    b = a + std::min<std::uint64_t>(x.buffer_length, mem - a);
+    return true;
+  };
+  for (std::size_t j = 0; j < rx.size(); ++j) {
+    std::uint64_t a, b, c, d;
+    if (!rxs(rx[j], a, b)) continue;
+    for (std::size_t k = j + 1; k < rx.size(); ++k)
+      if (rxs(rx[k], c, d) && c < b && a < d) return false;
+    for (const TxDescriptor& t : tx) {
+      if (t.length == 0 || t.buffer_address > mem || t.length > mem - t.buffer_address) continue;
+      if (t.buffer_address < b && a < t.buffer_address + t.length) return false;
+    }
+  }
+  return true;
+}
+
+// buffers_disjoint on batches large enough to run as parallel chunks (the
+// fuzz batches run as one), against a sort-based check: ring layouts, an
+// overlap at a random place (often a chunk seam), unsorted and invalid entries.
+int check_disjoint_large() {
+  Rng r{99};
+  for (int it = 0; it < 60; ++it) {
+    const std::size_t ntx = 1 + r.below(300000), nrx = 1 + r.below(300000);
+    std::vector<TxDescriptor> tx(ntx);
+    std::vector<RxDescriptor> rx(nrx);
+    std::uint64_t at = 0;
+    for (auto& t : tx) {
+      t.buffer_address = at;
+      t.length = r.below(10) == 0 ? 0 : 1 + r.below(2000);
+      at += t.length + r.below(3);
+    }
+    for (auto& x : rx) {
+      x.buffer_address = at;
+      x.buffer_length = r.below(20) == 0 ? 0 : 1 + r.below(3000);
+      at += x.buffer_length + r.below(3);
+    }
+    const std::size_t mem = at - r.below(2000);
+    const std::uint32_t kind = r.below(6);
+    if (kind == 1) {  // one RX buffer straddles its successor
+      const std::size_t j = r.below(static_cast<std::uint32_t>(nrx));
+      if (j + 1 < nrx) rx[j].buffer_length = static_cast<std::uint32_t>(rx[j + 1].buffer_address - rx[j].buffer_address + 1);
+    } else if (kind == 2) {  // one RX buffer inside the TX region
+      rx[r.below(static_cast<std::uint32_t>(nrx))].buffer_address = r.below(static_cast<std::uint32_t>(std::min<std::uint64_t>(at, 1u << 31)));
+    } else if (kind == 3) {  // TX out of order
+      std::swap(tx[r.below(static_cast<std::uint32_t>(ntx))], tx[r.below(static_cast<std::uint32_t>(ntx))]);
+    } else if (kind == 4) {  // RX out of order (still disjoint)
+      std::swap(rx[r.below(static_cast<std::uint32_t>(nrx))], rx[r.below(static_cast<std::uint32_t>(nrx))]);
+    } else if (kind == 5) {  // invalid RX entries sprinkled in
+      for (int k = 0; k < 50; ++k) rx[r.below(static_cast<std::uint32_t>(nrx))].buffer_address = mem + r.below(100);
+    }
+    // sort-based reference
+    std::vector<std::pair<std::uint64_t, std::uint64_t>> rs, ts;
+    for (const auto& x : rx)
+      if (x.buffer_address < mem && x.buffer_length)
+        rs.emplace_back(x.buffer_address, x.buffer_address + std::min<std::uint64_t>(x.buffer_length, mem - x.buffer_address));
+    for (const auto& t : tx)
+      if (t.length && t.buffer_address <= mem && t.length <= mem - t.buffer_address)
+        ts.emplace_back(t.buffer_address, t.buffer_address + t.length);
+    std::sort(rs.begin(), rs.end());
+    bool expect = true;
+    for (std::size_t i = 1; i < rs.size(); ++i) expect = expect && rs[i].first >= rs[i - 1].second;
+    for (const auto& [a, b] : ts) {
+      auto it = std::upper_bound(rs.begin(), rs.end(), std::pair<std::uint64_t, std::uint64_t>(a, ~std::uint64_t{0}));
+      if (it != rs.begin() && std::prev(it)->second > a) expect = false;
+      if (it != rs.end() && it->first < b) expect = false;
+    }
+    if (rx_stage_detail::buffers_disjoint(mem, tx, rx) != expect) {
+      std::fprintf(stderr, "buffers_disjoint: large case %d (kind %u) differs\n", it, kind);
+      return 1;
+    }
+  }
+  return 0;
 }
 
 int run_case(std::uint64_t seed) {
@@ -245,6 +325,10 @@ int run_case(std::uint64_t seed) {
   QueuePairStats st{};
   BatchScratch scratch;
   run_batch(cfg, mem_size, tx, rx, st, out, scratch, dev);
+  if (buffers_disjoint(mem_size, tx, rx) != disjoint_brute(mem_size, tx, rx)) {
+    std::fprintf(stderr, "seed %llu: buffers_disjoint differs from the pairwise check\n", (unsigned long long) seed);
+    return 1;
+  }
   if (!buffers_disjoint(mem_size, tx, rx)) g_overlapping += 1;
   if (dev.sum_calls > 1) g_split += 1;
   if (dev.snapshots) g_snap += 1;
@@ -343,7 +427,7 @@ int run_case(std::uint64_t seed) {
 int main(int argc, char** argv) {
   const std::uint64_t first = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
   const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 200;
-  int bad = 0;
+  int bad = check_disjoint_large();
   for (std::uint64_t s = first; s < first + count; ++s) bad += run_case(s);
   if (bad) return 1;
   std::printf("rx_stage_fuzz: ok (%llu batches; %zu with overlapping buffers, %zu split into sub-batches, %zu gathered "
