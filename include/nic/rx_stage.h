@@ -150,6 +150,7 @@ struct RxBatchResult {
   /// Wall time of each phase of process_batch (host clock, GPU phases
   /// include their stream synchronisation).
   struct Timings {
+    double check_us{0};  // buffers_disjoint (overlapping buffers?)
     double plan_us{0}, sums_us{0}, resolve_us{0}, gather_us{0}, rss_us{0};
   } timings;
 };

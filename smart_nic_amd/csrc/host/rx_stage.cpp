@@ -898,7 +898,9 @@ void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
   out.queues.clear();
   out.timings = RxBatchResult::Timings{};
 
+  auto t0 = clock::now();
   const bool disjoint = buffers_disjoint(mem_size, tx, rx);
+  out.timings.check_us = us_since(t0);
   // RSS of the frames part.rx_completions[which[..]] delivered with Success,
   // from the image as it is now.  The tuple lies in the first 82 bytes, so a
   // frame longer than NICGPU_MAX_PACKET (max_mtu above 65531) is hashed over

@@ -130,8 +130,8 @@ int main(int argc, char** argv) {
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     if (r > 0) tot.push_back(us);
     const auto& P = last.timings;
-    std::fprintf(stderr, "rep %d: %.0f us (plan %.0f sums %.0f resolve %.0f gather %.0f rss %.0f)\n", r, us, P.plan_us,
-                 P.sums_us, P.resolve_us, P.gather_us, P.rss_us);
+    std::fprintf(stderr, "rep %d: %.0f us (check %.0f plan %.0f sums %.0f resolve %.0f gather %.0f rss %.0f)\n", r, us,
+                 P.check_us, P.plan_us, P.sums_us, P.resolve_us, P.gather_us, P.rss_us);
   }
   std::sort(tot.begin(), tot.end());
   const double med = tot[tot.size() / 2];
@@ -142,8 +142,8 @@ int main(int argc, char** argv) {
   std::printf(
       "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
       "\"rx_success\": %zu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
-      "\"phases_us\": {\"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f}}\n",
-      wl.c_str(), cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.plan_us, T.sums_us,
+      "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f}}\n",
+      wl.c_str(), cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
       T.resolve_us, T.gather_us, T.rss_us);
   nicgpu_free(mem);
   return 0;
