@@ -153,12 +153,16 @@ struct RxParams {
   uint32_t hold_r;   // RING kernels: tiles of results each wave holds in LDS before storing them (>= 1)
   uint32_t ring_off; // RING kernels: LDS byte offset of wave 0's result ring (wave w at + w * hold_r * 512)
   uint32_t xpf_chunks;  // XPF kernels: prefetch the next tile's first batch when it has at most this many chunks
+  unsigned long long* stamps;  // tuning builds only: per wave {start, end, XCC_ID, HW_ID} (s_memrealtime, 100 MHz)
 };
+
+// s_waitcnt immediate for vmcnt(0) alone (gfx9 encoding: expcnt 7, lgkmcnt 15).
+constexpr int kVmcnt0 = 0x0F70;
 
 // Tuning-only knobs (libnicgpu_tune.so; outputs are wrong with any set).
 constexpr uint32_t kDbgNoStage = 1, kDbgNoHash = 2, kDbgNoStore = 4, kDbgNoHist = 8, kDbgNtStore = 16,
                    kDbgNoHashStore = 32, kDbgNoQueueStore = 64, kDbgNoTable = 128, kDbgSmallOut = 256, kDbgBurstOut = 512,
-                   kDbgStoreSc = 1024 | 2048 | 4096;
+                   kDbgStoreSc = 1024 | 2048 | 4096, kDbgRotate = 8192;
 __device__ __forceinline__ bool dbg_on(const RxParams& P, uint32_t bit) {
 #ifdef NICGPU_TUNING
   return (P.dbg & bit) != 0u;
@@ -851,7 +855,20 @@ __device__ __forceinline__ TileOut tile_epilogue(const RxParams& P, const RxLdsP
                                                P.frames + t.off, t.len);
       const uint32_t idx = h % P.table_n;
       o.h = h;
-      if (P.out_queue) o.q = dbg_on(P, kDbgNoTable) ? idx : (L.table_lds ? L.table_s[idx] : P.table[idx]);
+      if (P.out_queue) {
+        if (dbg_on(P, kDbgNoTable)) {
+          o.q = idx;
+        } else if (L.table_lds) {
+          o.q = L.table_s[idx];
+        } else {
+          o.q = P.table[idx];
+          // wait for this load here, on this path only: left to the merged
+          // path after the branch, the wait lands at the ring write as a
+          // vmcnt(0) on the LDS-table path too, i.e. it drains the next
+          // tile's prefetched first batch at every tile end
+          __builtin_amdgcn_s_waitcnt(kVmcnt0);
+        }
+      }
       if (P.out_hits && !dbg_on(P, kDbgNoHist)) {
         if (L.hist_lds) atomicAdd(&L.hist[idx], 1u);
         else atomicAdd(&P.out_hits[idx], 1ull);
@@ -959,6 +976,9 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
     for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) L.table_s[i] = P.table[i];
   }
   __syncthreads();
+#ifdef NICGPU_TUNING
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // Work split.  RANGES: wave g owns packets [g*n/W, (g+1)*n/W), walked in
   // tiles of 64 (the last one partial), so every wave streams the same number
@@ -966,7 +986,10 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   // round to a fraction of the waves: 1 M packets = 3.2 tiles per wave).
   // Otherwise tile k*W + g (round robin).
   const uint64_t nwaves = (uint64_t) gridDim.x * WPB;
-  const uint64_t gw = (uint64_t) blockIdx.x * WPB + w;
+  const uint64_t gw_hw = (uint64_t) blockIdx.x * WPB + w;
+  // tuning: kDbgRotate hands block b the tiles of block b + 1 (does a slow
+  // XCD follow its hardware or its data?  Its hardware: profiles/r02_wave_stamps_c2.jsonl)
+  const uint64_t gw = dbg_on(P, kDbgRotate) ? (gw_hw + WPB) % nwaves : gw_hw;
   uint64_t end, step;
   uint64_t first;
   if (RANGES) {
@@ -1112,6 +1135,15 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
       if (v) atomicAdd(&P.out_hits[i], (unsigned long long) v);
     }
   }
+#ifdef NICGPU_TUNING
+  if (P.stamps != nullptr && lane == 0) {  // vector stores from lane 0
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    P.stamps[4 * gw_hw + 0] = t_start;
+    P.stamps[4 * gw_hw + 1] = t_end;
+    P.stamps[4 * gw_hw + 2] = (unsigned) __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID[3:0]
+    P.stamps[4 * gw_hw + 3] = (unsigned) __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+  }
+#endif
 }
 
 // ------------------------------------------------------------- TSO / GSO --
@@ -2272,6 +2304,7 @@ int nicgpu_rss_info(const nicgpu_rss_ctx* ctx, size_t* key_len, size_t* table_n)
 namespace {
 #ifdef NICGPU_TUNING
 uint32_t g_tune_dbg = 0;  // tools/tune_rx.py --dbg (nicgpu_tune_set_dbg)
+unsigned long long* g_tune_stamps = nullptr;  // tools/wave_stamps.py (nicgpu_tune_set_stamps)
 #endif
 int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n,
                     int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum, uint32_t* out_hash,
@@ -2309,6 +2342,7 @@ int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frame
   P.out_l34 = out_l34;
 #ifdef NICGPU_TUNING
   P.dbg = g_tune_dbg;
+  P.stamps = g_tune_stamps;
 #endif
   if (ctx) {
     P.lut = ctx->d_lut;
@@ -2540,6 +2574,9 @@ int nicgpu_tune_stream_tiles(const uint8_t* buf, size_t bytes, size_t tile_bytes
 int nicgpu_tune_num_variants(void) { return kNumRxVariants; }
 const char* nicgpu_tune_variant_name(int v) { return (v >= 0 && v < kNumRxVariants) ? kRxVariants[v].name : ""; }
 void nicgpu_tune_set_dbg(uint32_t bits) { g_tune_dbg = bits; }
+// per-wave {start, end, XCC_ID, HW_ID} of every RX launch into buf (4 u64 per
+// wave of the grid; NULL switches it off)
+void nicgpu_tune_set_stamps(unsigned long long* buf) { g_tune_stamps = buf; }
 void nicgpu_tune_set_xpf(uint32_t max_chunks) { g_xpf_chunks = max_chunks; }
 int nicgpu_tune_rx_offload(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc,
                            size_t n, int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum,
