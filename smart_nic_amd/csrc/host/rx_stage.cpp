@@ -29,28 +29,16 @@
 
 #include "nic/checksum.h"
 #include "nicgpu.h"
+#include "../qp_logic.h"
 
 namespace nic {
 namespace rx_stage_detail {
 namespace {
 
-constexpr std::uint32_t kRun = 65534;  // even, so every run starts at an even offset
+using nicqp::dma_ok;
 
-inline std::uint32_t add1c(std::uint32_t a, std::uint32_t b) {
-  const std::uint32_t x = a + b;
-  return (x & 0xFFFFu) + (x >> 16);
-}
-inline std::uint32_t swap16(std::uint32_t x) { return ((x & 0xFFu) << 8) | (x >> 8); }
-// Folded sum of a piece from its checksum (compute_checksum = ~fold(sum)).
-inline std::uint32_t piece_sum(std::span<const std::uint16_t> cs, std::uint32_t i) {
-  return static_cast<std::uint32_t>(~cs[i]) & 0xFFFFu;
-}
-inline std::uint32_t at_offset(std::uint32_t s, std::uint64_t off) { return (off & 1) ? swap16(s) : s; }
-
-bool dma_ok(std::size_t mem_size, std::uint64_t addr, std::uint64_t len) {
-  // SimpleHostMemory::translate_view bounds rule (simple_host_memory.cpp:85-93)
-  return addr <= mem_size && len <= mem_size - addr;
-}
+// The shared per-packet logic (qp_logic.h) over this library's types.
+using Ctx = nicqp::Ctx<TxDescriptor, RxDescriptor, PacketPlan>;
 
 // Worker placement: chunk c of a pass runs on the c-th allowed CPU after the
 // calling thread's, so a batch's chunks stay on the same few neighbouring
@@ -109,147 +97,19 @@ struct Chunks {
   }
 };
 
-struct SegDecision {
-  bool segmented = false;  // build_segments produced chunks
-  bool invalid_mss = false;
-  bool too_many = false;
-  std::uint32_t nseg = 1;
-  std::uint32_t H = 0;
-};
-
-// build_segments (queue_pair.cpp:212-278) without the copies.
-SegDecision decide_segments(const TxDescriptor& t) {
-  SegDecision d;
-  const std::uint64_t L = t.length;
-  const bool enabled = (t.tso_enabled || t.gso_enabled) && t.mss > 0 && L > t.mss;
-  if (!enabled) return d;
-  if (t.mss < kMinMss || t.mss > kMaxMss) {
-    d.invalid_mss = true;
-    return d;
-  }
-  if (t.header_length > L) {
-    d.invalid_mss = true;
-    return d;
-  }
-  d.H = t.header_length;
-  if (d.H >= L) return d;  // degenerate: one unsegmented copy (:250-252)
-  const std::uint64_t n = (L - d.H + t.mss - 1) / t.mss;
-  if (n > kMaxTsoSegments) {
-    d.too_many = true;
-    return d;
-  }
-  d.segmented = true;
-  d.nseg = static_cast<std::uint32_t>(n);
-  return d;
-}
-
-inline bool tx_verify_needed(const TxDescriptor& t) { return !t.checksum_offload && t.checksum != ChecksumMode::None; }
-
-// Sums a resolve step needs, for one TX packet.
-struct PacketSums {
-  const PacketPlan* p;
-  std::span<const std::uint16_t> cs;
-  std::uint64_t L;
-
-  std::uint32_t s(std::uint32_t k) const { return piece_sum(cs, p->first_piece + k); }
-
-  std::uint32_t chunk_len(std::uint32_t k) const {
-    const std::uint64_t o = static_cast<std::uint64_t>(p->hdr_len) + static_cast<std::uint64_t>(k) * p->mss;
-    return static_cast<std::uint32_t>(std::min<std::uint64_t>(p->mss, L - o));
-  }
-  // whole packet, as compute_checksum(packet) sums it
-  std::uint32_t whole() const {
-    std::uint32_t acc = 0;
-    if (p->kind == PacketPlan::kPlain) {
-      for (std::uint32_t i = 0; i < p->npieces; ++i) acc = add1c(acc, s(i));  // all runs start at even offsets
-      return acc;
-    }
-    const std::uint32_t H = p->hdr_len;
-    if (H >= 4) {
-      acc = add1c(s(0), s(1));
-      for (std::uint32_t k = 0; k < p->nseg; ++k)
-        acc = add1c(acc, at_offset(s(2 + k), H + static_cast<std::uint64_t>(k) * p->mss));
-    } else {
-      acc = s(0);
-      for (std::uint32_t k = 0; k < p->nseg; ++k) {
-        const std::uint64_t o = H + static_cast<std::uint64_t>(k) * p->mss;
-        const std::uint32_t n0 = std::min<std::uint32_t>(4 - H, chunk_len(k));
-        acc = add1c(acc, at_offset(s(1 + 2 * k), o));
-        acc = add1c(acc, at_offset(s(2 + 2 * k), o + n0));
-      }
-    }
-    return acc;
-  }
-  // segment k: sum of its first 4 bytes and of the rest (rest placed at offset 4)
-  void segment(std::uint32_t k, std::uint32_t& first4, std::uint32_t& rest) const {
-    if (p->kind == PacketPlan::kPlain) {
-      first4 = s(0);
-      rest = 0;
-      for (std::uint32_t i = 1; i < p->npieces; ++i) rest = add1c(rest, s(i));
-      return;
-    }
-    const std::uint32_t H = p->hdr_len;
-    if (H >= 4) {
-      first4 = s(0);
-      rest = add1c(s(1), at_offset(s(2 + k), H - 4));
-    } else {
-      first4 = add1c(s(0), at_offset(s(1 + 2 * k), H));
-      rest = s(2 + 2 * k);
-    }
-  }
-};
-
 }  // namespace
 
 namespace {
 
-// One TX descriptor's plan; writes its pieces to `out` unless it is null.
-// Returns the number of pieces.
+// One TX descriptor's plan (nicqp::plan_packet); writes its pieces to `out`
+// unless it is null.  Returns the number of pieces.
 std::uint32_t plan_packet(const BatchedQueuePairConfig& config, std::size_t mem_size, const TxDescriptor& t,
                           PacketPlan& pp, Piece* out) {
-  std::uint32_t np = 0;
-  auto put = [&](std::uint64_t addr, std::uint64_t len) {
-    if (out) out[np] = Piece{addr, static_cast<std::uint32_t>(len)};
-    ++np;
-  };
-  pp = PacketPlan{};
-  const std::uint64_t L = t.length;
-  if (!dma_ok(mem_size, t.buffer_address, L)) return 0;  // read fault: no bytes
-  const bool verify = tx_verify_needed(t);
-  const bool mtu_drop = L > config.max_mtu;
-  const SegDecision d = decide_segments(t);
-  const bool dropped = mtu_drop || d.invalid_mss || d.too_many;
-  if (dropped && !verify) return 0;
-  const std::uint64_t a = t.buffer_address;
-  if (!d.segmented || dropped) {
-    pp.kind = PacketPlan::kPlain;
-    put(a, std::min<std::uint64_t>(4, L));
-    for (std::uint64_t o = 4; o < L; o += kRun) put(a + o, std::min<std::uint64_t>(kRun, L - o));
-  } else {
-    pp.kind = PacketPlan::kSegmented;
-    pp.nseg = d.nseg;
-    pp.hdr_len = d.H;
-    pp.mss = t.mss;
-    if (d.H >= 4) {
-      put(a, 4);
-      put(a + 4, d.H - 4);
-      for (std::uint32_t k = 0; k < d.nseg; ++k) {
-        const std::uint64_t o = d.H + static_cast<std::uint64_t>(k) * t.mss;
-        put(a + o, std::min<std::uint64_t>(t.mss, L - o));
-      }
-    } else {
-      put(a, d.H);
-      for (std::uint32_t k = 0; k < d.nseg; ++k) {
-        const std::uint64_t o = d.H + static_cast<std::uint64_t>(k) * t.mss;
-        const std::uint64_t len = std::min<std::uint64_t>(t.mss, L - o);
-        const std::uint64_t n0 = std::min<std::uint64_t>(4 - d.H, len);
-        put(a + o, n0);
-        put(a + o + n0, len - n0);
-      }
-    }
-  }
-  pp.npieces = np;
-  return np;
+  std::uint32_t k = 0;
+  return nicqp::plan_packet(config.max_mtu, mem_size, t, pp, [&](std::uint64_t addr, std::uint64_t len) {
+    if (out) out[k] = Piece{addr, static_cast<std::uint32_t>(len)};
+    ++k;
+  });
 }
 
 }  // namespace
@@ -305,206 +165,16 @@ void add_stats(QueuePairStats& a, const QueuePairStats& b) {
   a.rx_gro_aggregated += b.rx_gro_aggregated;
 }
 
-struct ResolveCtx {
-  const BatchedQueuePairConfig& config;
-  std::size_t mem_size;
-  const Plan& plan;
-  std::span<const std::uint16_t> cs;
-  std::span<const TxDescriptor> tx;
-  std::span<const RxDescriptor> rx;
-};
-
-CompletionEntry make_completion(std::uint16_t qid, std::uint16_t idx, CompletionCode st) {  // :150-158
-  CompletionEntry e{};
-  e.queue_id = qid;
-  e.descriptor_index = idx;
-  e.status = static_cast<std::uint32_t>(st);
-  return e;
+Ctx make_ctx(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
+             std::span<const std::uint16_t> cs, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx) {
+  return Ctx{config.queue_id, config.max_mtu, mem_size, plan.packets.data(), cs.data(), tx.data(), rx.data(), rx.size()};
 }
 
-CompletionEntry make_tx(std::uint16_t qid, const TxDescriptor& t, CompletionCode st, std::size_t segs, bool tso,
-                        bool gso) {  // :160-177
-  CompletionEntry e = make_completion(qid, t.descriptor_index, st);
-  e.checksum_offloaded = t.checksum_offload;
-  e.tso_performed = tso;
-  e.gso_performed = gso;
-  e.segments_produced = static_cast<std::uint16_t>(std::min<std::size_t>(segs, std::numeric_limits<std::uint16_t>::max()));
-  if (t.vlan_insert) {
-    e.vlan_inserted = true;
-    e.vlan_tag = t.vlan_tag;
-  }
-  return e;
-}
+std::size_t rx_need(const Ctx& C, std::size_t i) { return nicqp::rx_need(C, i); }
 
-// RX descriptors TX descriptor i pops when the ring has enough of them and no
-// RX-side check aborts it early: 0 when it is dropped before the RX stage
-// (read fault, TX checksum, MTU, invalid mss, too many segments).
-std::size_t rx_need(const ResolveCtx& C, std::size_t i) {
-  const TxDescriptor& t = C.tx[i];
-  const std::uint64_t L = t.length;
-  if (!dma_ok(C.mem_size, t.buffer_address, L)) return 0;
-  if (tx_verify_needed(t)) {
-    const PacketSums ps{&C.plan.packets[i], C.cs, L};
-    if (static_cast<std::uint16_t>(~ps.whole() & 0xFFFFu) != t.checksum_value) return 0;
-  }
-  if (L > C.config.max_mtu) return 0;
-  const SegDecision d = decide_segments(t);
-  if (d.invalid_mss || d.too_many) return 0;
-  return d.nseg;
-}
-
-// QueuePair::process_once (queue_pair.cpp:67-460) for TX descriptor i with
-// the RX ring's consumer at rc: posts its completions through `sink`, adds to
-// `stats`, returns the RX descriptors it popped.  sink.tx(entry, fire) and
-// sink.rx(entry, write or nullptr) see the reference's posting order.
 template <class Sink>
-std::size_t resolve_packet(const ResolveCtx& C, std::size_t i, std::size_t rc, QueuePairStats& stats, Sink& sink) {
-  const std::uint16_t qid = C.config.queue_id;
-  const TxDescriptor& t = C.tx[i];
-  const PacketSums ps{&C.plan.packets[i], C.cs, t.length};
-  const std::uint64_t L = t.length;
-  const std::size_t rc0 = rc;
-  // :75-83 no RX descriptor at all
-  if (rc == C.rx.size()) {
-    sink.tx(make_tx(qid, t, CompletionCode::NoDescriptor, 0, false, false), true);
-    stats.drops_no_rx_desc += 1;
-    return 0;
-  }
-  // :86-92 DMA read
-  if (!dma_ok(C.mem_size, t.buffer_address, L)) {
-    sink.tx(make_tx(qid, t, CompletionCode::Fault, 0, false, false), true);
-    return 0;
-  }
-  // :94-105 TX checksum verify
-  if (tx_verify_needed(t)) {
-    const std::uint16_t computed = static_cast<std::uint16_t>(~ps.whole() & 0xFFFFu);
-    if (computed != t.checksum_value) {
-      sink.tx(make_tx(qid, t, CompletionCode::ChecksumError, 0, false, false), true);
-      stats.drops_checksum += 1;
-      return 0;
-    }
-  }
-  // :195-210 MTU
-  if (L > C.config.max_mtu) {
-    sink.tx(make_tx(qid, t, CompletionCode::MtuExceeded, 0, false, false), true);
-    stats.drops_mtu_exceeded += 1;
-    return 0;
-  }
-  // :212-278 segmentation
-  const SegDecision d = decide_segments(t);
-  if (d.invalid_mss) {
-    sink.tx(make_tx(qid, t, CompletionCode::InvalidMss, 0, false, false), true);
-    stats.drops_invalid_mss += 1;
-    return 0;
-  }
-  if (d.too_many) {
-    sink.tx(make_tx(qid, t, CompletionCode::TooManySegments, 0, false, false), true);
-    stats.drops_too_many_segments += 1;
-    return 0;
-  }
-  const std::uint32_t total = d.nseg;
-  const bool tso = t.tso_enabled && total > 1;
-  const bool gso = t.gso_enabled && total > 1;
-  // :293-303 enough RX descriptors for every segment
-  if (C.rx.size() - rc < total) {
-    sink.tx(make_tx(qid, t, CompletionCode::NoDescriptor, 0, tso, gso), true);
-    stats.drops_no_rx_desc += 1;
-    return 0;
-  }
-  for (std::uint32_t k = 0; k < total; ++k) {
-    RxDescriptor x = C.rx[rc++];
-    if (t.vlan_insert) x.vlan_present = true;  // :320-322
-    // base segment = header || chunk k (or the whole packet)
-    std::uint64_t src_a = t.buffer_address, src_b = 0;
-    std::uint32_t len_a, len_b = 0;
-    if (d.segmented) {
-      len_a = d.H;
-      src_b = t.buffer_address + d.H + static_cast<std::uint64_t>(k) * t.mss;
-      len_b = ps.chunk_len(k);
-    } else {
-      len_a = static_cast<std::uint32_t>(L);
-    }
-    const std::uint64_t base_len = static_cast<std::uint64_t>(len_a) + len_b;
-    // :324-331 VLAN insert, :389-395 strip
-    std::uint64_t size = base_len + (t.vlan_insert ? 4 : 0);
-    const bool has_vlan = t.vlan_insert || x.vlan_present;
-    const bool strip = x.vlan_strip && has_vlan && size >= 4;
-    if (strip) size -= 4;
-    const bool prefix = t.vlan_insert && !strip;
-    const bool strip_base = strip && !t.vlan_insert;  // the base segment loses its first 4 bytes
-    // :397-414 buffer too small
-    if (x.buffer_length < size) {
-      sink.tx(make_tx(qid, t, CompletionCode::Success, total, tso, gso), false);
-      CompletionEntry e = make_completion(qid, x.descriptor_index, CompletionCode::BufferTooSmall);
-      e.vlan_stripped = x.vlan_strip && has_vlan;
-      if (e.vlan_stripped) e.vlan_tag = t.vlan_insert ? t.vlan_tag : x.vlan_tag;
-      sink.rx(e, nullptr);
-      stats.drops_buffer_small += 1;
-      return rc - rc0;
-    }
-    // :416-426 DMA write
-    if (!dma_ok(C.mem_size, x.buffer_address, size)) {
-      sink.tx(make_tx(qid, t, CompletionCode::Fault, total, tso, gso), false);
-      sink.rx(make_completion(qid, x.descriptor_index, CompletionCode::Fault), nullptr);
-      return rc - rc0;
-    }
-    SegmentWrite w{};
-    w.dst = x.buffer_address;
-    if (prefix) {
-      const std::uint32_t tag = t.vlan_tag;
-      w.prefix = 0x81u | (0x00u << 8) | (((tag >> 8) & 0xFFu) << 16) | ((tag & 0xFFu) << 24);
-      w.prefix_len = 4;
-    }
-    if (strip_base) {  // drop the first 4 bytes of header || chunk
-      const std::uint32_t from_a = std::min<std::uint32_t>(4, len_a);
-      src_a += from_a;
-      len_a -= from_a;
-      src_b += 4 - from_a;
-      len_b -= 4 - from_a;
-    }
-    w.src_a = src_a;
-    w.len_a = len_a;
-    w.src_b = src_b;
-    w.len_b = len_b;
-
-    CompletionEntry e = make_completion(qid, x.descriptor_index, CompletionCode::Success);
-    e.gro_aggregated = x.gro_enabled;
-    if (e.gro_aggregated) stats.rx_gro_aggregated += 1;
-    // :434-447 RX checksum verify of the delivered bytes
-    if (x.checksum_offload && x.checksum != ChecksumMode::None) {
-      e.checksum_verified = true;
-      stats.rx_checksum_verified += 1;
-      std::uint32_t first4, rest;
-      ps.segment(k, first4, rest);
-      std::uint32_t sum;
-      if (strip_base) sum = rest;
-      else sum = add1c(first4, rest);
-      if (prefix) sum = add1c(add1c(0x8100u, t.vlan_tag), sum);
-      if ((~sum & 0xFFFFu) != 0) {
-        e.status = static_cast<std::uint32_t>(CompletionCode::ChecksumError);
-        sink.rx(e, &w);
-        sink.tx(make_tx(qid, t, CompletionCode::Success, total, tso, gso), false);
-        stats.drops_checksum += 1;
-        return rc - rc0;
-      }
-    }
-    e.vlan_stripped = x.vlan_strip && has_vlan;
-    if (e.vlan_stripped) {
-      e.vlan_tag = t.vlan_insert ? t.vlan_tag : x.vlan_tag;
-      stats.rx_vlan_strips += 1;
-    }
-    sink.rx(e, &w);
-    stats.rx_packets += 1;
-    stats.rx_bytes += size;
-  }
-  // :280-301 finalize_tx_success
-  sink.tx(make_tx(qid, t, CompletionCode::Success, total, tso, gso), true);
-  stats.tx_packets += total;
-  stats.tx_bytes += L;
-  if (tso) stats.tx_tso_segments += total;
-  if (gso) stats.tx_gso_segments += total;
-  if (t.vlan_insert) stats.tx_vlan_insertions += total;
-  return rc - rc0;
+std::size_t resolve_packet(const Ctx& C, std::size_t i, std::size_t rc, QueuePairStats& stats, Sink& sink) {
+  return nicqp::resolve_packet<CompletionEntry, SegmentWrite>(C, i, rc, stats, sink);
 }
 
 // Appends, firing interrupts in posting order (:371-383).
@@ -549,7 +219,7 @@ void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const P
              std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
              std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
              std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx, unsigned max_threads) {
-  const ResolveCtx C{config, mem_size, plan, piece_csum, tx, rx};
+  const Ctx C = make_ctx(config, mem_size, plan, piece_csum, tx, rx);
   const std::size_t n = tx.size();
   const std::size_t want = max_threads ? max_threads : (config.host_threads ? config.host_threads : 16);
   const Chunks ch(n, config.on_interrupt ? 1 : want, max_threads ? 1 : 32768);
@@ -797,7 +467,7 @@ std::size_t resolve_prefix(const BatchedQueuePairConfig& config, std::size_t mem
                            std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
                            std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
                            std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx) {
-  const ResolveCtx C{config, mem_size, plan, piece_csum, tx, rx};
+  const Ctx C = make_ctx(config, mem_size, plan, piece_csum, tx, rx);
   out.tx_completions.clear();
   out.rx_completions.clear();
   writes.clear();
