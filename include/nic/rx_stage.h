@@ -133,6 +133,11 @@ struct BatchedQueuePairConfig {
   /// multi-segment); 1 runs them all on the calling thread.  Workers are
   /// pinned to the allowed CPUs that follow the calling thread's.
   unsigned host_threads{0};
+  /// Resolve on the device (nicgpu_qp_*, the decisions of qp_logic.h) when
+  /// the batch's buffers do not overlap and no interrupt callback is set: the
+  /// host then only moves descriptors and completions.  false: every batch is
+  /// resolved on the host (the path the fuzz compares with the reference).
+  bool device_resolve{true};
 };
 
 struct RxBatchResult {
@@ -152,6 +157,9 @@ struct RxBatchResult {
   struct Timings {
     double check_us{0};  // buffers_disjoint (overlapping buffers?)
     double plan_us{0}, sums_us{0}, resolve_us{0}, gather_us{0}, rss_us{0};
+    double copy_us{0};   // device resolve: descriptors up, completions down
+    bool device{false};     // resolved on the device
+    bool host_tail{false};  // ... and the rest on the host (positions not settled in 8 relaxation steps)
   } timings;
 };
 
@@ -182,6 +190,8 @@ public:
   struct Scratch;  // device, pinned and host buffers reused across batches (grown, never shrunk)
 
 private:
+  void process_on_device(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+                         QueuePairStats& stats, RxBatchResult& out, void* stream);
   BatchedQueuePairConfig config_;
   QueuePairStats stats_{};
   std::unique_ptr<Scratch> scratch_;
@@ -273,6 +283,19 @@ std::size_t resolve_prefix(const BatchedQueuePairConfig& config, std::size_t mem
                            std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
                            std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx);
 
+/// The device resolve's algorithm (nicgpu_qp_resolve) on the host, for the
+/// tests: ring positions by relaxation — every packet resolved at the
+/// exclusive scan of the previous step's pops (clamped to the ring's end),
+/// starting from rx_need — for at most max_steps steps, then the packets
+/// before the first one whose position is not yet exact resolved at their
+/// positions.  Returns that count; rx_used is its ring position and steps the
+/// steps taken.  Outputs as resolve's for those packets.
+std::size_t resolve_relaxed(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
+                            std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
+                            std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
+                            std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx, int max_steps,
+                            std::size_t& rx_used, int& steps);
+
 /// Order of the DMA writes of one resolved sub-batch for parallel gathers.
 /// Writes (RX completions j with write_of_rx[j] >= 0 and at least one byte) are
 /// split into layers: a write goes one layer above every earlier write it
@@ -320,9 +343,14 @@ struct BatchScratch {
 /// process_batch's driver over any Backend: plan, piece sums, resolve, DMA
 /// writes and RSS, in sub-batches and layers when buffers overlap (see the top
 /// of this header).  Adds to `stats`; replaces out's contents.
+/// Per-queue dispatch lists (out.queues) of the Success completions, from out.rx_queue.
+void build_queue_lists(RxBatchResult& out);
+
+/// disjoint: buffers_disjoint(mem_size, tx, rx) when the caller knows it (-1:
+/// computed here).
 void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
                std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out, BatchScratch& scratch,
-               Backend& backend);
+               Backend& backend, int disjoint = -1);
 
 }  // namespace rx_stage_detail
 

@@ -222,6 +222,118 @@ int nicgpu_segment_gather(uint8_t* mem, uint64_t mem_size, const nicgpu_segment_
 int nicgpu_segment_gather_from(uint8_t* mem, const uint8_t* src, uint64_t mem_size,
                                const nicgpu_segment_write* writes, size_t n, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Batched QueuePair on the device: the per-packet decisions of
+ * QueuePair::process_once (src/queue_pair.cpp:67-460) for a whole batch, run
+ * by nic::BatchedQueuePair (include/nic/rx_stage.h) when the batch's buffers
+ * do not overlap and no interrupt callback is set.  The decision logic is
+ * smart_nic_amd/csrc/qp_logic.h, the same source the host resolve uses.
+ *
+ * C mirrors of the reference PODs, same layouts (include/nic/tx_rx.h:37-62,
+ * include/nic/completion_queue.h:13-26, include/nic/queue_pair.h:36-53). */
+typedef struct nicgpu_tx_descriptor {
+  uint64_t buffer_address;
+  uint32_t length;
+  uint8_t checksum; /* ChecksumMode: 0 None, 1 Layer3, 2 Layer4 */
+  uint8_t pad0;
+  uint16_t descriptor_index;
+  uint16_t checksum_value;
+  uint8_t checksum_offload;
+  uint8_t tso_enabled;
+  uint8_t gso_enabled;
+  uint8_t pad1;
+  uint16_t mss;
+  uint16_t header_length;
+  uint8_t vlan_insert;
+  uint8_t pad2;
+  uint16_t vlan_tag;
+  uint16_t pad3;
+} nicgpu_tx_descriptor; /* 32 B */
+
+typedef struct nicgpu_rx_descriptor {
+  uint64_t buffer_address;
+  uint32_t buffer_length;
+  uint8_t checksum;
+  uint8_t pad0;
+  uint16_t descriptor_index;
+  uint8_t checksum_offload;
+  uint8_t vlan_strip;
+  uint8_t vlan_present;
+  uint8_t pad1;
+  uint16_t vlan_tag;
+  uint8_t gro_enabled;
+  uint8_t pad2;
+} nicgpu_rx_descriptor; /* 24 B */
+
+typedef struct nicgpu_completion {
+  uint16_t queue_id;
+  uint16_t descriptor_index;
+  uint32_t status; /* CompletionCode */
+  uint8_t checksum_offloaded;
+  uint8_t checksum_verified;
+  uint8_t tso_performed;
+  uint8_t gso_performed;
+  uint8_t vlan_inserted;
+  uint8_t vlan_stripped;
+  uint8_t gro_aggregated;
+  uint8_t pad0;
+  uint16_t segments_produced;
+  uint16_t vlan_tag;
+} nicgpu_completion; /* 20 B */
+
+typedef struct nicgpu_qp_stats {
+  uint64_t tx_packets, rx_packets, tx_bytes, rx_bytes, drops_checksum, drops_no_rx_desc, drops_buffer_small,
+      drops_mtu_exceeded, drops_invalid_mss, drops_too_many_segments, tx_tso_segments, tx_gso_segments,
+      tx_vlan_insertions, rx_vlan_strips, rx_checksum_verified, rx_gro_aggregated;
+} nicgpu_qp_stats;
+
+/* Device buffers of a QueuePair context (valid until the next
+ * nicgpu_qp_reserve / nicgpu_qp_plan that grows them). */
+typedef struct nicgpu_qp_view {
+  nicgpu_tx_descriptor* tx;     /* [ntx]  the caller uploads the TX descriptors here */
+  nicgpu_rx_descriptor* rx;     /* [nrx]  and the RX descriptors (the ring, rx[0] first) */
+  uint32_t* piece_base;         /* [ntx + 1] first piece of each TX descriptor */
+  uint16_t* piece_csum;         /* [npieces] compute_checksum of each piece */
+  nicgpu_completion* txc;       /* [ntx]  TX completions, in posting order */
+  nicgpu_completion* rxc;       /* [nrx]  RX completions, in posting order */
+  nicgpu_segment_write* writes; /* [nrx]  DMA write of RX completion j (all lengths 0: none) */
+  uint64_t* rss_desc;           /* [nrx]  frames delivered with Success (NICGPU_DESC) */
+  uint32_t* rss_hash;           /* [nrx]  their hashes / queues, as RSS leaves them */
+  uint16_t* rss_queue;
+  uint32_t* rx_hash;            /* [nrx]  per RX completion: hash (0 unless Success) */
+  uint16_t* rx_queue;           /* [nrx]  per RX completion: queue (0xFFFF unless Success) */
+} nicgpu_qp_view;
+
+typedef struct nicgpu_qp nicgpu_qp;
+int nicgpu_qp_create(nicgpu_qp** out, int device);
+int nicgpu_qp_destroy(nicgpu_qp* q);
+/* Capacity for ntx TX and nrx RX descriptors; fills *view. */
+int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view);
+/* The plan (qp_logic.h plan_packet) of view.tx[0, ntx) and the checksum of
+ * every piece over the image mem[0, mem_size): *npieces on return.
+ * Synchronises `stream`; refreshes *view (the piece buffers may grow). */
+int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
+                   uint64_t* npieces, nicgpu_qp_view* view, void* stream);
+/* The reference's control flow over view.tx[0, ntx) against view.rx[0, nrx)
+ * from the piece sums: TX descriptors [0, *done) are resolved, with
+ * completions in view.txc[0, *done) and view.rxc[0, *rx_used), their writes in
+ * view.writes and their statistics in *stats.  Ring positions are found by
+ * relaxation: each packet is resolved at the exclusive scan of the previous
+ * step's pops (first guess: what it needs), which is exact for at least one
+ * more packet per step and, when a packet's pops do not depend on where in the
+ * ring it lands (a ring that runs short, failed segment checksums on uniform
+ * RX descriptors), for all of them after two.  After 8 steps *done stops at
+ * the first packet not yet exact and the caller resolves the rest in order
+ * (piece checksums from view.piece_base[*done]).  Synchronises `stream`. */
+int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu, uint16_t queue_id,
+                      uint64_t* done, uint64_t* rx_used, nicgpu_qp_stats* stats, void* stream);
+/* The frames of view.rxc[0, nrx) delivered with Success, as RSS descriptors
+ * (view.rss_desc[0, *m), lengths clipped to NICGPU_MAX_PACKET); view.rx_hash /
+ * rx_queue reset to 0 / 0xFFFF.  Synchronises `stream`. */
+int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, uint64_t* m, void* stream);
+/* view.rx_hash / rx_queue of those frames from view.rss_hash / rss_queue. */
+int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t m, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,6 +67,13 @@ ABI_SYMBOLS = (
     "nicgpu_tso_checksum",
     "nicgpu_segment_gather",
     "nicgpu_segment_gather_from",
+    "nicgpu_qp_create",
+    "nicgpu_qp_destroy",
+    "nicgpu_qp_reserve",
+    "nicgpu_qp_plan",
+    "nicgpu_qp_resolve",
+    "nicgpu_qp_rss_list",
+    "nicgpu_qp_rss_scatter",
     "nicgpu_icrc_batch",
     "nicgpu_tso_segment",
 )

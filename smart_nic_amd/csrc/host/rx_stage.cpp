@@ -317,6 +317,74 @@ void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const P
 }
 
 namespace {
+struct NullSink {
+  void tx(const CompletionEntry&, bool) {}
+  void rx(const CompletionEntry&, const SegmentWrite*) {}
+};
+struct PlaceAt {  // writes at known positions (resolve_relaxed)
+  CompletionEntry* txc;
+  CompletionEntry* rxc;
+  SegmentWrite* w;
+  std::int64_t* wof;
+  std::size_t ti, rj;
+  void tx(const CompletionEntry& e, bool) { txc[ti] = e; }
+  void rx(const CompletionEntry& e, const SegmentWrite* sw) {
+    rxc[rj] = e;
+    w[rj] = sw ? *sw : SegmentWrite{};
+    wof[rj] = sw ? static_cast<std::int64_t>(rj) : -1;
+    ++rj;
+  }
+};
+}  // namespace
+
+std::size_t resolve_relaxed(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
+                            std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
+                            std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
+                            std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx, int max_steps,
+                            std::size_t& rx_used, int& steps) {
+  const Ctx C = make_ctx(config, mem_size, plan, piece_csum, tx, rx);
+  const std::size_t n = tx.size(), m = rx.size();
+  std::vector<std::uint32_t> pops(n), pos(n + 1, 0);
+  for (std::size_t i = 0; i < n; ++i) pops[i] = static_cast<std::uint32_t>(rx_need(C, i));
+  std::size_t lim = n;
+  steps = 0;
+  for (int it = 0; it < max_steps; ++it) {
+    ++steps;
+    std::uint32_t r = 0;
+    for (std::size_t i = 0; i < n; ++i) {
+      pos[i] = r;
+      r += pops[i];
+    }
+    pos[n] = r;
+    std::size_t first = n;
+    for (std::size_t i = 0; i < n; ++i) {  // one kernel launch: every packet against the same pos
+      QueuePairStats d{};
+      NullSink sink;
+      const std::size_t rc = pos[i] < m ? pos[i] : m;
+      const auto popped = static_cast<std::uint32_t>(resolve_packet(C, i, rc, d, sink));
+      if (popped != pops[i]) {
+        first = std::min(first, i);
+        pops[i] = popped;
+      }
+    }
+    lim = first;
+    if (first == n) break;
+  }
+  rx_used = pos[lim];
+  out.tx_completions.assign(lim, CompletionEntry{});
+  out.rx_completions.assign(rx_used, CompletionEntry{});
+  writes.assign(rx_used, SegmentWrite{});
+  write_of_rx.assign(rx_used, -1);
+  for (std::size_t i = 0; i < lim; ++i) {
+    PlaceAt sink{out.tx_completions.data(), out.rx_completions.data(), writes.data(), write_of_rx.data(), i, pos[i]};
+    resolve_packet(C, i, pos[i], stats, sink);
+  }
+  out.tx_processed = lim;
+  out.rx_consumed = rx_used;
+  return lim;
+}
+
+namespace {
 
 struct Span64 {
   std::uint64_t a, b;  // [a, b)
@@ -554,7 +622,7 @@ void schedule_writes(std::span<const SegmentWrite> writes, std::span<const std::
 
 void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
                std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out, BatchScratch& S,
-               Backend& dev) {
+               Backend& dev, int disjoint_hint) {
   using clock = std::chrono::steady_clock;
   auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
   constexpr auto kSuccess = static_cast<std::uint32_t>(CompletionCode::Success);
@@ -569,7 +637,7 @@ void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
   out.timings = RxBatchResult::Timings{};
 
   auto t0 = clock::now();
-  const bool disjoint = buffers_disjoint(mem_size, tx, rx);
+  const bool disjoint = disjoint_hint >= 0 ? disjoint_hint != 0 : buffers_disjoint(mem_size, tx, rx);
   out.timings.check_us = us_since(t0);
   // RSS of the frames part.rx_completions[which[..]] delivered with Success,
   // from the image as it is now.  The tuple lies in the first 82 bytes, so a
@@ -668,22 +736,27 @@ void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
   out.tx_processed = tx.size();
   out.rx_consumed = r;
 
-  // per-queue dispatch lists, in posting order
   if (config.rss != nullptr) {
     auto t = clock::now();
-    std::vector<std::size_t> cnt;
-    for (std::size_t j = 0; j < out.rx_completions.size(); ++j) {
-      if (out.rx_completions[j].status != kSuccess) continue;
-      const std::uint16_t q = out.rx_queue[j];
-      if (q >= cnt.size()) cnt.resize(static_cast<std::size_t>(q) + 1, 0);
-      cnt[q] += 1;
-    }
-    out.queues.resize(cnt.size());
-    for (std::size_t q = 0; q < cnt.size(); ++q) out.queues[q].reserve(cnt[q]);
-    for (std::size_t j = 0; j < out.rx_completions.size(); ++j)
-      if (out.rx_completions[j].status == kSuccess) out.queues[out.rx_queue[j]].push_back(static_cast<std::uint32_t>(j));
+    build_queue_lists(out);
     out.timings.rss_us += us_since(t);
   }
+}
+
+void build_queue_lists(RxBatchResult& out) {
+  // per-queue dispatch lists of the Success frames, in posting order
+  constexpr auto kSuccess = static_cast<std::uint32_t>(CompletionCode::Success);
+  std::vector<std::size_t> cnt;
+  for (std::size_t j = 0; j < out.rx_completions.size(); ++j) {
+    if (out.rx_completions[j].status != kSuccess) continue;
+    const std::uint16_t q = out.rx_queue[j];
+    if (q >= cnt.size()) cnt.resize(static_cast<std::size_t>(q) + 1, 0);
+    cnt[q] += 1;
+  }
+  out.queues.resize(cnt.size());
+  for (std::size_t q = 0; q < cnt.size(); ++q) out.queues[q].reserve(cnt[q]);
+  for (std::size_t j = 0; j < out.rx_completions.size(); ++j)
+    if (out.rx_completions[j].status == kSuccess) out.queues[out.rx_queue[j]].push_back(static_cast<std::uint32_t>(j));
 }
 
 }  // namespace rx_stage_detail
@@ -739,7 +812,43 @@ struct BatchedQueuePair::Scratch {
   DevBuf piece_desc, piece_csum, writes, rss_desc, rss_hash, rss_queue, copy;
   HostBuf h_desc, h_csum, h_writes, h_rss_desc, h_hash, h_queue;
   rx_stage_detail::BatchScratch host;
+  nicgpu_qp* qp = nullptr;  // device resolve context (created on first use, on the current device)
+  int qp_device = -1;
+  std::vector<std::uint16_t> tail_cs;
+  ~Scratch() {
+    if (qp) (void) nicgpu_qp_destroy(qp);
+  }
 };
+
+// The device mirrors (nicgpu.h) of the PODs the device resolve moves.
+static_assert(sizeof(nicgpu_tx_descriptor) == sizeof(TxDescriptor) && sizeof(nicgpu_rx_descriptor) == sizeof(RxDescriptor));
+static_assert(offsetof(nicgpu_tx_descriptor, length) == offsetof(TxDescriptor, length) &&
+              offsetof(nicgpu_tx_descriptor, checksum) == offsetof(TxDescriptor, checksum) &&
+              offsetof(nicgpu_tx_descriptor, descriptor_index) == offsetof(TxDescriptor, descriptor_index) &&
+              offsetof(nicgpu_tx_descriptor, checksum_value) == offsetof(TxDescriptor, checksum_value) &&
+              offsetof(nicgpu_tx_descriptor, checksum_offload) == offsetof(TxDescriptor, checksum_offload) &&
+              offsetof(nicgpu_tx_descriptor, tso_enabled) == offsetof(TxDescriptor, tso_enabled) &&
+              offsetof(nicgpu_tx_descriptor, gso_enabled) == offsetof(TxDescriptor, gso_enabled) &&
+              offsetof(nicgpu_tx_descriptor, mss) == offsetof(TxDescriptor, mss) &&
+              offsetof(nicgpu_tx_descriptor, header_length) == offsetof(TxDescriptor, header_length) &&
+              offsetof(nicgpu_tx_descriptor, vlan_insert) == offsetof(TxDescriptor, vlan_insert) &&
+              offsetof(nicgpu_tx_descriptor, vlan_tag) == offsetof(TxDescriptor, vlan_tag));
+static_assert(offsetof(nicgpu_rx_descriptor, buffer_length) == offsetof(RxDescriptor, buffer_length) &&
+              offsetof(nicgpu_rx_descriptor, checksum) == offsetof(RxDescriptor, checksum) &&
+              offsetof(nicgpu_rx_descriptor, descriptor_index) == offsetof(RxDescriptor, descriptor_index) &&
+              offsetof(nicgpu_rx_descriptor, checksum_offload) == offsetof(RxDescriptor, checksum_offload) &&
+              offsetof(nicgpu_rx_descriptor, vlan_strip) == offsetof(RxDescriptor, vlan_strip) &&
+              offsetof(nicgpu_rx_descriptor, vlan_present) == offsetof(RxDescriptor, vlan_present) &&
+              offsetof(nicgpu_rx_descriptor, vlan_tag) == offsetof(RxDescriptor, vlan_tag) &&
+              offsetof(nicgpu_rx_descriptor, gro_enabled) == offsetof(RxDescriptor, gro_enabled));
+static_assert(sizeof(nicgpu_completion) == sizeof(CompletionEntry) &&
+              offsetof(nicgpu_completion, status) == offsetof(CompletionEntry, status) &&
+              offsetof(nicgpu_completion, checksum_offloaded) == offsetof(CompletionEntry, checksum_offloaded) &&
+              offsetof(nicgpu_completion, gro_aggregated) == offsetof(CompletionEntry, gro_aggregated) &&
+              offsetof(nicgpu_completion, segments_produced) == offsetof(CompletionEntry, segments_produced) &&
+              offsetof(nicgpu_completion, vlan_tag) == offsetof(CompletionEntry, vlan_tag));
+static_assert(sizeof(nicgpu_qp_stats) == sizeof(QueuePairStats));
+static_assert(sizeof(nicgpu_segment_write) == sizeof(rx_stage_detail::SegmentWrite));
 
 namespace {
 
@@ -835,12 +944,141 @@ RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::
 
 void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                      std::span<const RxDescriptor> rx, RxBatchResult& out, void* stream) {
+  using clock = std::chrono::steady_clock;
   if (mem.base == nullptr && mem.size != 0) throw GpuError("process_batch: null host-memory image", NICGPU_ERR_INVALID);
-  GpuBackend dev{*scratch_, mem, config_, stream};
+  const auto t0 = clock::now();
+  const bool disjoint = rx_stage_detail::buffers_disjoint(mem.size, tx, rx);
+  const double check_us = std::chrono::duration<double, std::micro>(clock::now() - t0).count();
   // stats are committed only when the whole batch went through
   QueuePairStats st = stats_;
-  rx_stage_detail::run_batch(config_, mem.size, tx, rx, st, out, scratch_->host, dev);
+  if (disjoint && config_.device_resolve && !config_.on_interrupt) {
+    process_on_device(mem, tx, rx, st, out, stream);
+  } else {
+    GpuBackend dev{*scratch_, mem, config_, stream};
+    rx_stage_detail::run_batch(config_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint ? 1 : 0);
+  }
+  out.timings.check_us = check_us;
   stats_ = st;
+}
+
+// Disjoint buffers, no interrupt callback: plan, piece sums and the
+// reference's control flow on the device (nicgpu_qp_*), the part after a
+// descriptor whose RX side ends it early (or where the ring runs short)
+// resolved here in order, then the DMA writes and RSS of the whole batch on
+// the device; the host moves descriptors up and completions down.
+void BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
+                                         std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out,
+                                         void* stream) {
+  using namespace rx_stage_detail;
+  using clock = std::chrono::steady_clock;
+  auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
+  Scratch& S = *scratch_;
+  out.tx_processed = out.rx_consumed = 0;
+  for (auto& q : out.queues) q.clear();
+  out.queues.clear();
+  out.timings = RxBatchResult::Timings{};
+  out.timings.device = true;
+  int dev = 0;
+  check(nicgpu_get_device(&dev), "nicgpu_get_device");
+  if (S.qp == nullptr || S.qp_device != dev) {
+    if (S.qp) (void) nicgpu_qp_destroy(S.qp);
+    S.qp = nullptr;
+    check(nicgpu_qp_create(&S.qp, dev), "nicgpu_qp_create");
+    S.qp_device = dev;
+  }
+  const std::size_t ntx = tx.size(), nrx = rx.size();
+  nicgpu_qp_view v{};
+  auto t = clock::now();
+  check(nicgpu_qp_reserve(S.qp, ntx, nrx, &v), "nicgpu_qp_reserve");
+  check(nicgpu_memcpy_async(v.tx, tx.data(), ntx * sizeof(TxDescriptor), stream), "nicgpu_memcpy_async");
+  check(nicgpu_memcpy_async(v.rx, rx.data(), nrx * sizeof(RxDescriptor), stream), "nicgpu_memcpy_async");
+  out.timings.copy_us += us_since(t);
+  t = clock::now();
+  std::uint64_t np = 0;
+  check(nicgpu_qp_plan(S.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &np, &v,
+                       stream),
+        "nicgpu_qp_plan");
+  out.timings.sums_us += us_since(t);
+  t = clock::now();
+  std::uint64_t done = 0, used = 0;
+  nicgpu_qp_stats ds{};
+  check(nicgpu_qp_resolve(S.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, &done, &used, &ds, stream),
+        "nicgpu_qp_resolve");
+  const QueuePairStats d{ds.tx_packets,         ds.rx_packets,         ds.tx_bytes,
+                         ds.rx_bytes,           ds.drops_checksum,     ds.drops_no_rx_desc,
+                         ds.drops_buffer_small, ds.drops_mtu_exceeded, ds.drops_invalid_mss,
+                         ds.drops_too_many_segments, ds.tx_tso_segments, ds.tx_gso_segments,
+                         ds.tx_vlan_insertions, ds.rx_vlan_strips,     ds.rx_checksum_verified,
+                         ds.rx_gro_aggregated};
+  add_stats(st, d);
+  std::size_t nrx_total = used;
+  out.rx_consumed = used;
+  out.tx_completions.resize(ntx);
+  if (done < ntx) {
+    out.timings.host_tail = true;
+    // the rest, in order, from ring position `used` (the host resolve; its
+    // plan of tx[done..] lists the same pieces as the device's from piece_base[done])
+    const auto tail_tx = tx.subspan(done);
+    const auto tail_rx = rx.subspan(used);
+    make_plan(config_, mem.size, tail_tx, S.host.plan);
+    std::uint32_t pb = 0;
+    check(nicgpu_memcpy_async(&pb, v.piece_base + done, sizeof(pb), stream), "nicgpu_memcpy_async");
+    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+    if (np - pb != S.host.plan.pieces.size()) throw GpuError("process_batch: device and host plans differ", NICGPU_ERR_INVALID);
+    S.tail_cs.resize(np - pb);
+    check(nicgpu_memcpy_async(S.tail_cs.data(), v.piece_csum + pb, S.tail_cs.size() * 2, stream), "nicgpu_memcpy_async");
+    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+    RxBatchResult& part = S.host.part;
+    resolve(config_, mem.size, S.host.plan, S.tail_cs, tail_tx, tail_rx, st, part, S.host.writes, S.host.write_of_rx);
+    const std::size_t tr = part.rx_completions.size();
+    check(nicgpu_memcpy_async(v.txc + done, part.tx_completions.data(), part.tx_completions.size() * sizeof(CompletionEntry),
+                              stream),
+          "nicgpu_memcpy_async");
+    check(nicgpu_memcpy_async(v.rxc + used, part.rx_completions.data(), tr * sizeof(CompletionEntry), stream),
+          "nicgpu_memcpy_async");
+    check(nicgpu_memcpy_async(v.writes + used, S.host.writes.data(), tr * sizeof(SegmentWrite), stream),
+          "nicgpu_memcpy_async");
+    nrx_total += tr;
+    out.rx_consumed += part.rx_consumed;
+  }
+  out.tx_processed = ntx;
+  out.timings.resolve_us += us_since(t);
+  // DMA writes: zero-length entries (completions without a write) write nothing
+  t = clock::now();
+  if (nrx_total)
+    check(nicgpu_segment_gather(reinterpret_cast<std::uint8_t*>(mem.base), mem.size, v.writes, nrx_total, stream),
+          "nicgpu_segment_gather");
+  check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+  out.timings.gather_us += us_since(t);
+  t = clock::now();
+  out.rx_completions.resize(nrx_total);
+  out.rx_hash.resize(nrx_total);
+  out.rx_queue.resize(nrx_total);
+  if (config_.rss != nullptr) {
+    std::uint64_t m = 0;
+    check(nicgpu_qp_rss_list(S.qp, nrx_total, &m, stream), "nicgpu_qp_rss_list");
+    if (m)
+      config_.rss->select_queue_batch(DevicePacketBatch{mem.base, v.rss_desc, m}, config_.tuple,
+                                      RxBatchOutputs{nullptr, v.rss_hash, v.rss_queue}, stream, true);
+    check(nicgpu_qp_rss_scatter(S.qp, m, stream), "nicgpu_qp_rss_scatter");
+    check(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, stream), "nicgpu_memcpy_async");
+    check(nicgpu_memcpy_async(out.rx_queue.data(), v.rx_queue, nrx_total * 2, stream), "nicgpu_memcpy_async");
+  } else {
+    std::fill(out.rx_hash.begin(), out.rx_hash.end(), 0u);
+    std::fill(out.rx_queue.begin(), out.rx_queue.end(), RxBatchResult::kNoQueue);
+  }
+  out.timings.rss_us += us_since(t);
+  t = clock::now();
+  check(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), stream), "nicgpu_memcpy_async");
+  check(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry), stream),
+        "nicgpu_memcpy_async");
+  check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+  out.timings.copy_us += us_since(t);
+  if (config_.rss != nullptr) {
+    t = clock::now();
+    build_queue_lists(out);
+    out.timings.rss_us += us_since(t);
+  }
 }
 
 }  // namespace nic

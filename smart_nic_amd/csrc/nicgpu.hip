@@ -27,6 +27,7 @@
 //  * No MFMA: this is byte-integer work bounded by HBM read bandwidth.
 
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <cstdint>
 #include <cstring>
@@ -34,6 +35,7 @@
 #include <vector>
 
 #include "nicgpu.h"
+#include "qp_logic.h"
 
 namespace {
 
@@ -2448,6 +2450,416 @@ int nicgpu_segment_gather_from(uint8_t* mem, const uint8_t* src, uint64_t mem_si
   const uint64_t cap = (uint64_t) di->cus * 8;
   const unsigned grid = (unsigned) (want < cap ? want : cap);
   hipLaunchKernelGGL(segment_gather_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
+  return hip_status(hipGetLastError());
+}
+
+}  // extern "C"
+
+// ---------------------------------------------- batched QueuePair (f1) --
+// The per-packet decisions of QueuePair::process_once over a whole batch on
+// the device: one thread per TX descriptor, decisions from qp_logic.h (the
+// source the host resolve uses, fuzzed against the compiled reference).
+//   plan     count pieces per descriptor, exclusive scan, fill the piece
+//            descriptors; the RX kernel sums every piece (one pass over the
+//            TX bytes)
+//   resolve  RX descriptors each packet pops if nothing ends it early
+//            (rx_need), exclusive scan = every packet's ring position, while
+//            the ring lasts; a dry pass finds the first packet whose RX side
+//            ends it early (its pops differ); the full pass posts the
+//            completions, DMA writes and per-block statistics of every packet
+//            before that.  The caller resolves the rest on the host, in order.
+//   rss      Success frames compacted into RSS descriptors; the hashes and
+//            queues scattered back per completion.
+namespace {
+
+struct QpPlan {
+  uint32_t kind, nseg, first_piece, npieces, hdr_len, mss;
+};
+using QpCtx = nicqp::Ctx<nicgpu_tx_descriptor, nicgpu_rx_descriptor, QpPlan>;
+constexpr unsigned kQpBlock = 256;
+constexpr unsigned kQpStats = 16;
+constexpr int kQpRelaxSteps = 8;  // position relaxations before the host takes the rest
+
+struct QpNullSink {
+  __device__ void tx(const nicgpu_completion&, bool) {}
+  __device__ void rx(const nicgpu_completion&, const nicgpu_segment_write*) {}
+};
+
+struct QpDevSink {
+  nicgpu_completion* txc;
+  nicgpu_completion* rxc;
+  nicgpu_segment_write* w;
+  uint64_t ti, rj;
+  __device__ void tx(const nicgpu_completion& e, bool) { txc[ti] = e; }
+  __device__ void rx(const nicgpu_completion& e, const nicgpu_segment_write* sw) {
+    rxc[rj] = e;
+    if (sw) {
+      w[rj] = *sw;
+    } else {
+      nicgpu_segment_write z{};
+      w[rj] = z;
+    }
+    ++rj;
+  }
+};
+
+__global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
+                                                            uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
+                                                            uint32_t* counts) {
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i <= n; i += (uint64_t) gridDim.x * kQpBlock) {
+    if (i == n) {
+      counts[n] = 0;
+      continue;
+    }
+    QpPlan pp;
+    counts[i] = nicqp::plan_packet(max_mtu, mem_size, tx[i], pp, [](uint64_t, uint64_t) {});
+    plans[i] = pp;
+  }
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_fill_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
+                                                           uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
+                                                           const uint32_t* __restrict__ base, uint64_t* desc) {
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
+    uint32_t at = base[i];
+    plans[i].first_piece = at;
+    QpPlan pp;
+    nicqp::plan_packet(max_mtu, mem_size, tx[i], pp, [&](uint64_t a, uint64_t len) { desc[at++] = NICGPU_DESC(a, len); });
+  }
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_need_kernel(QpCtx C, uint64_t n, uint32_t* need) {
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i <= n; i += (uint64_t) gridDim.x * kQpBlock)
+    need[i] = i < n ? nicqp::rx_need(C, i) : 0u;
+}
+
+// One relaxation step of the ring positions: every packet resolved (without
+// outputs) at pos[i] = the exclusive scan of pops; pops[i] becomes what it
+// actually popped there (the ring checks of :75-83 and :293-303 included),
+// and scal[0] the first packet whose pops changed.  The sequential positions
+// are the fixed point, and each step makes at least one more packet exact:
+// pos[0] = 0 always is, so after k steps packets [0, k) are.
+__global__ __launch_bounds__(kQpBlock) void qp_relax_kernel(QpCtx C, uint32_t* pops, const uint32_t* __restrict__ pos,
+                                                            uint64_t n, unsigned long long* scal) {
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
+    nicgpu_qp_stats st{};
+    QpNullSink sink;
+    // a guess past the ring's end is clamped to it (the sequential positions
+    // never pass it; resolve_packet must not index past rx[nrx - 1])
+    const uint64_t rc = pos[i] < C.nrx ? (uint64_t) pos[i] : C.nrx;
+    const uint32_t popped = (uint32_t) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(C, i, rc, st, sink);
+    if (popped != pops[i]) {
+      atomicMin(&scal[0], (unsigned long long) i);
+      pops[i] = popped;
+    }
+  }
+}
+
+// packets [0, lim) at their (exact) positions: completions, writes, per-block stats
+__global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32_t* __restrict__ pos, uint64_t lim,
+                                                           nicgpu_completion* txc, nicgpu_completion* rxc,
+                                                           nicgpu_segment_write* writes, uint64_t* partials) {
+  __shared__ uint64_t red[kQpStats][kQpBlock / kWave];
+  nicgpu_qp_stats st{};
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < lim; i += (uint64_t) gridDim.x * kQpBlock) {
+    if (pos[i] > C.nrx) continue;  // exact positions never pass the ring's end (defensive)
+    QpDevSink sink{txc, rxc, writes, i, pos[i]};
+    (void) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(C, i, pos[i], st, sink);
+  }
+  uint64_t v[kQpStats];
+  static_assert(sizeof(nicgpu_qp_stats) == kQpStats * 8, "16 counters");
+  __builtin_memcpy(v, &st, sizeof(v));
+  const uint32_t lane = lane_id(), w = threadIdx.x / kWave;
+#pragma unroll
+  for (int k = 0; k < (int) kQpStats; ++k) {
+    unsigned long long x = v[k];
+    for (int off = kWave / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    if (lane == 0) red[k][w] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < kQpStats) {
+    uint64_t x = 0;
+    for (unsigned j = 0; j < kQpBlock / kWave; ++j) x += red[threadIdx.x][j];
+    partials[(uint64_t) blockIdx.x * kQpStats + threadIdx.x] = x;
+  }
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_flag_kernel(const nicgpu_completion* __restrict__ rxc, uint64_t nrx,
+                                                           uint32_t* flags, uint32_t* rx_hash, uint16_t* rx_queue) {
+  for (uint64_t j = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; j <= nrx; j += (uint64_t) gridDim.x * kQpBlock) {
+    flags[j] = j < nrx && rxc[j].status == nicqp::kSuccess ? 1u : 0u;
+    if (j < nrx) {
+      rx_hash[j] = 0;
+      rx_queue[j] = 0xFFFFu;
+    }
+  }
+}
+
+// The tuple lies in a frame's first 82 bytes, so a frame longer than
+// NICGPU_MAX_PACKET (max_mtu above 65531) is hashed over its first
+// NICGPU_MAX_PACKET bytes: the same tuple, hash and queue.
+__global__ __launch_bounds__(kQpBlock) void qp_rss_fill_kernel(const uint32_t* __restrict__ flags,
+                                                               const uint32_t* __restrict__ at,
+                                                               const nicgpu_segment_write* __restrict__ writes,
+                                                               uint64_t nrx, uint64_t* desc, uint32_t* which) {
+  for (uint64_t j = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; j < nrx; j += (uint64_t) gridDim.x * kQpBlock) {
+    if (!flags[j]) continue;
+    const nicgpu_segment_write w = writes[j];
+    uint64_t len = (uint64_t) w.prefix_len + w.len_a + w.len_b;
+    if (len > NICGPU_MAX_PACKET) len = NICGPU_MAX_PACKET;
+    desc[at[j]] = NICGPU_DESC(w.dst, len);
+    which[at[j]] = (uint32_t) j;
+  }
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_scatter_kernel(const uint32_t* __restrict__ which,
+                                                              const uint32_t* __restrict__ h,
+                                                              const uint16_t* __restrict__ q, uint64_t m,
+                                                              uint32_t* rx_hash, uint16_t* rx_queue) {
+  for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < m; k += (uint64_t) gridDim.x * kQpBlock) {
+    rx_hash[which[k]] = h[k];
+    rx_queue[which[k]] = q[k];
+  }
+}
+
+template <class T>
+int qp_grow(T*& p, size_t& cap, size_t want) {
+  if (want <= cap) return NICGPU_OK;
+  if (p) (void) hipFree(p);
+  p = nullptr;
+  cap = 0;
+  size_t n = want + want / 4 + 64;
+  if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) return NICGPU_ERR_NOMEM;
+  cap = n;
+  return NICGPU_OK;
+}
+
+}  // namespace
+
+struct nicgpu_qp {
+  int device = 0;
+  size_t cap_tx = 0, cap_rx = 0, cap_pieces = 0, cap_tmp = 0, cap_part = 0;
+  size_t c_tx = 0, c_rx = 0, c_plans = 0, c_counts = 0, c_base = 0, c_need = 0, c_pos = 0, c_txc = 0;
+  size_t c_rxc = 0, c_w = 0, c_flags = 0, c_at = 0, c_desc = 0, c_which = 0, c_h = 0, c_q = 0, c_rh = 0, c_rq = 0;
+  size_t c_pdesc = 0, c_pcs = 0, c_part = 0, c_tmp = 0;
+  nicgpu_tx_descriptor* tx = nullptr;
+  nicgpu_rx_descriptor* rx = nullptr;
+  QpPlan* plans = nullptr;
+  uint32_t *counts = nullptr, *base = nullptr, *need = nullptr, *pos = nullptr;
+  uint64_t* piece_desc = nullptr;
+  uint16_t* piece_csum = nullptr;
+  nicgpu_completion *txc = nullptr, *rxc = nullptr;
+  nicgpu_segment_write* writes = nullptr;
+  uint32_t *flags = nullptr, *at = nullptr, *which = nullptr, *rss_hash = nullptr, *rx_hash = nullptr;
+  uint64_t* rss_desc = nullptr;
+  uint16_t *rss_queue = nullptr, *rx_queue = nullptr;
+  uint64_t* partials = nullptr;
+  unsigned long long* scal = nullptr;
+  uint8_t* tmp = nullptr;
+  uint64_t host_scal[4] = {0, 0, 0, 0};
+  unsigned grid = 1;
+};
+
+namespace {
+
+void qp_fill_view(const nicgpu_qp* q, nicgpu_qp_view* v) {
+  if (!v) return;
+  v->tx = q->tx;
+  v->rx = q->rx;
+  v->piece_base = q->base;
+  v->piece_csum = q->piece_csum;
+  v->txc = q->txc;
+  v->rxc = q->rxc;
+  v->writes = q->writes;
+  v->rss_desc = q->rss_desc;
+  v->rss_hash = q->rss_hash;
+  v->rss_queue = q->rss_queue;
+  v->rx_hash = q->rx_hash;
+  v->rx_queue = q->rx_queue;
+}
+
+unsigned qp_grid(const nicgpu_qp* q, uint64_t n) {
+  const uint64_t want = (n + kQpBlock) / kQpBlock;
+  return (unsigned) (want < q->grid ? (want ? want : 1) : q->grid);
+}
+
+// hipcub exclusive sum of in[0, n) into out[0, n) (n includes the trailing 0)
+int qp_scan(nicgpu_qp* q, const uint32_t* in, uint32_t* out, size_t n, hipStream_t s) {
+  size_t tb = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int) n, s) != hipSuccess) return NICGPU_ERR_HIP;
+  int st = qp_grow(q->tmp, q->c_tmp, tb);
+  if (st != NICGPU_OK) return st;
+  return hip_status(hipcub::DeviceScan::ExclusiveSum(q->tmp, tb, in, out, (int) n, s));
+}
+
+}  // namespace
+
+extern "C" {
+
+int nicgpu_qp_create(nicgpu_qp** out, int device) {
+  if (!out) return NICGPU_ERR_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return NICGPU_ERR_NO_DEVICE;
+  DeviceGuard g(device);
+  const DeviceInfo& di = device_info(device);
+  if (di.status != NICGPU_OK) return di.status;
+  auto* q = new nicgpu_qp();
+  q->device = device;
+  q->grid = (unsigned) di.cus * 8u;
+  if (hipMalloc(&q->scal, 4 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&q->partials, (size_t) q->grid * kQpStats * sizeof(uint64_t)) != hipSuccess) {
+    nicgpu_qp_destroy(q);
+    return NICGPU_ERR_NOMEM;
+  }
+  *out = q;
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_destroy(nicgpu_qp* q) {
+  if (!q) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  void* bufs[] = {q->tx, q->rx, q->plans, q->counts, q->base, q->need, q->pos, q->piece_desc, q->piece_csum,
+                  q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
+                  q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp};
+  for (void* b : bufs)
+    if (b) (void) hipFree(b);
+  delete q;
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view) {
+  if (!q) return NICGPU_ERR_INVALID;
+  if (ntx > 0xFFFFFFFFull / 64u || nrx > 0xFFFFFFFEull) return NICGPU_ERR_INVALID;  // 32-bit ring positions
+  DeviceGuard g(q->device);
+  int st = NICGPU_OK;
+  const size_t t1 = ntx + 1, r1 = nrx + 1;
+  if (st == NICGPU_OK) st = qp_grow(q->tx, q->c_tx, ntx ? ntx : 1);
+  if (st == NICGPU_OK) st = qp_grow(q->rx, q->c_rx, nrx ? nrx : 1);
+  if (st == NICGPU_OK) st = qp_grow(q->plans, q->c_plans, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->counts, q->c_counts, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->base, q->c_base, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->need, q->c_need, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->pos, q->c_pos, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->txc, q->c_txc, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->rxc, q->c_rxc, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->writes, q->c_w, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->flags, q->c_flags, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->at, q->c_at, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->rss_desc, q->c_desc, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->which, q->c_which, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->rss_hash, q->c_h, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->rss_queue, q->c_q, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->rx_hash, q->c_rh, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->rx_queue, q->c_rq, r1);
+  q->cap_tx = ntx;
+  q->cap_rx = nrx;
+  qp_fill_view(q, view);
+  return st;
+}
+
+int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
+                   uint64_t* npieces, nicgpu_qp_view* view, void* stream) {
+  if (!q || !npieces || ntx > q->cap_tx) return NICGPU_ERR_INVALID;
+  if (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0)) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  *npieces = 0;
+  const unsigned grid = qp_grid(q, ntx + 1);
+  hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
+                     q->plans, q->counts);
+  int st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&q->host_scal[0], q->base + ntx, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  if (st != NICGPU_OK) return st;
+  const uint64_t np = (uint32_t) q->host_scal[0];
+  st = qp_grow(q->piece_desc, q->c_pdesc, np ? np : 1);
+  if (st == NICGPU_OK) st = qp_grow(q->piece_csum, q->c_pcs, np ? np : 1);
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
+                     q->plans, q->base, q->piece_desc);
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK && np) st = nicgpu_checksum_batch(mem, q->piece_desc, np, q->piece_csum, stream);
+  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  *npieces = np;
+  qp_fill_view(q, view);
+  return st;
+}
+
+int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu, uint16_t queue_id,
+                      uint64_t* done, uint64_t* rx_used, nicgpu_qp_stats* stats, void* stream) {
+  if (!q || !done || !rx_used || !stats || ntx > q->cap_tx || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  QpCtx C{queue_id, max_mtu, mem_size, q->plans, q->piece_csum, q->tx, q->rx, (uint64_t) nrx};
+  const unsigned grid = qp_grid(q, ntx + 1);
+  // first guess: every packet pops what it needs (rx_need), then relax
+  hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, (uint64_t) ntx, q->need);
+  int st = hip_status(hipGetLastError());
+  uint64_t lim = 0;
+  unsigned long long first = 0;
+  for (int it = 0; st == NICGPU_OK; ++it) {
+    st = qp_scan(q, q->need, q->pos, ntx + 1, s);
+    const unsigned long long init = (unsigned long long) ntx;
+    if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->scal, &init, sizeof(init), hipMemcpyHostToDevice, s));
+    if (st != NICGPU_OK) break;
+    hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, (uint64_t) ntx, q->scal);
+    st = hip_status(hipGetLastError());
+    if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&first, q->scal, sizeof(first), hipMemcpyDeviceToHost, s));
+    if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+    if (st != NICGPU_OK) break;
+    // pos is exact up to and including `first` (pops before it agreed)
+    lim = first < ntx ? (uint64_t) first : (uint64_t) ntx;
+    if (first >= ntx || it + 1 == kQpRelaxSteps) break;
+  }
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, lim, q->txc, q->rxc, q->writes,
+                     q->partials);
+  st = hip_status(hipGetLastError());
+  std::vector<uint64_t> part((size_t) grid * kQpStats);
+  uint32_t used = 0;
+  if (st == NICGPU_OK)
+    st = hip_status(hipMemcpyAsync(part.data(), q->partials, part.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&used, q->pos + lim, sizeof(used), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  if (st != NICGPU_OK) return st;
+  uint64_t sum[kQpStats] = {};
+  for (unsigned b = 0; b < grid; ++b)
+    for (unsigned k = 0; k < kQpStats; ++k) sum[k] += part[(size_t) b * kQpStats + k];
+  std::memcpy(stats, sum, sizeof(sum));
+  *done = lim;
+  *rx_used = used;
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, uint64_t* m, void* stream) {
+  if (!q || !m || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const unsigned grid = qp_grid(q, nrx + 1);
+  hipLaunchKernelGGL(qp_flag_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->rxc, (uint64_t) nrx, q->flags, q->rx_hash,
+                     q->rx_queue);
+  int st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = qp_scan(q, q->flags, q->at, nrx + 1, s);
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_rss_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->flags, q->at, q->writes, (uint64_t) nrx,
+                     q->rss_desc, q->which);
+  uint32_t cnt = 0;
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&cnt, q->at + nrx, sizeof(cnt), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  *m = cnt;
+  return st;
+}
+
+int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t m, void* stream) {
+  if (!q || m > q->cap_rx) return NICGPU_ERR_INVALID;
+  if (m == 0) return NICGPU_OK;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(qp_scatter_kernel, dim3(qp_grid(q, m)), dim3(kQpBlock), 0, s, q->which, q->rss_hash, q->rss_queue,
+                     (uint64_t) m, q->rx_hash, q->rx_queue);
   return hip_status(hipGetLastError());
 }
 

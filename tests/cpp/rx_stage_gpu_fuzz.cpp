@@ -1,0 +1,211 @@
+// rx_stage_gpu_fuzz.cpp — nic::BatchedQueuePair's device resolve (nicgpu_qp_*,
+// the path process_batch takes for batches whose buffers do not overlap)
+// against its host resolve (rx_stage_detail::run_batch over the CPU backend of
+// cpu_backend.h), which rx_stage_fuzz.cpp checks against the compiled
+// reference QueuePair.  Random batches of every descriptor kind (TSO/GSO, VLAN,
+// bad checksums, MTU, invalid mss, faults, RX rings that run short, buffers
+// too small, failing segment checksums), small and large (several grid
+// blocks, host tails).  Compared: every completion, the statistics, RX
+// descriptors consumed, the memory image, RSS hash / queue per completion, the
+// dispatch lists and the RSS engine's stats.  GPU only.
+//
+//   rx_stage_gpu_fuzz <first_seed> <count>
+#undef NDEBUG
+#include <cassert>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "cpu_backend.h"
+#include "nic/rss.h"
+#include "nic/rx_stage.h"
+#include "nicgpu.h"
+#include "oracle.h"
+
+using namespace nic;
+
+namespace {
+
+struct Rng {
+  std::uint64_t s;
+  std::uint64_t next() {
+    std::uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  std::uint32_t below(std::uint32_t n) { return n ? static_cast<std::uint32_t>((next() >> 32) % n) : 0; }
+  std::uint8_t byte() { return static_cast<std::uint8_t>(next() >> 56); }
+};
+
+bool same(const CompletionEntry& a, const CompletionEntry& b) {
+  return a.queue_id == b.queue_id && a.descriptor_index == b.descriptor_index && a.status == b.status &&
+         a.checksum_offloaded == b.checksum_offloaded && a.checksum_verified == b.checksum_verified &&
+         a.tso_performed == b.tso_performed && a.gso_performed == b.gso_performed && a.vlan_inserted == b.vlan_inserted &&
+         a.vlan_stripped == b.vlan_stripped && a.gro_aggregated == b.gro_aggregated &&
+         a.segments_produced == b.segments_produced && a.vlan_tag == b.vlan_tag;
+}
+
+void balance(std::vector<std::uint8_t>& b, std::size_t at) {
+  b[at] = b[at + 1] = 0;
+  const std::uint16_t c = oracle_compute_checksum(b.data(), b.size());
+  b[at] = static_cast<std::uint8_t>(c >> 8);
+  b[at + 1] = static_cast<std::uint8_t>(c);
+}
+
+const std::vector<std::uint8_t> kMsKey = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67,
+                                          0x25, 0x3d, 0x43, 0xa3, 0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb,
+                                          0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3, 0x80, 0x30,
+                                          0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
+
+std::size_t g_tail = 0, g_device = 0, g_short = 0;  // host tails, device batches, batches with NoDescriptor
+
+int run_case(std::uint64_t seed) {
+  Rng r{seed * 104729 + 3};
+  const bool large = r.below(8) == 0;
+  const std::size_t ntx = large ? 20000 + r.below(60000) : 1 + r.below(300);
+  const std::size_t nrx = r.below(4) == 0 ? r.below(static_cast<std::uint32_t>(ntx + 1)) : ntx * (1 + r.below(3));
+  const std::size_t mtus[] = {9000, 1500, 3000, 65535};
+  const std::size_t max_mtu = mtus[r.below(4)];
+  const bool tso_heavy = r.below(4) == 0;
+  std::vector<TxDescriptor> tx(ntx);
+  std::vector<std::uint8_t> image;
+  std::size_t at = 0;
+  std::vector<std::pair<std::size_t, std::vector<std::uint8_t>>> pkts;
+  for (std::size_t i = 0; i < ntx; ++i) {
+    const std::uint32_t pick = r.below(16);
+    std::size_t L = pick < 4 ? r.below(70) : (pick < 10 ? 60 + r.below(1500) : (pick < 15 ? 9000 : 9000 + r.below(70000)));
+    if (large && L > 9000) L = 1518;
+    std::vector<std::uint8_t> p(L);
+    const bool zero = r.below(40) == 0;
+    for (auto& b : p) b = zero ? 0 : r.byte();
+    if (L >= 16 && r.below(4) != 0) balance(p, 10);
+    at += r.below(3) == 0 ? r.below(9) : 0;
+    TxDescriptor& t = tx[i];
+    t.buffer_address = at;
+    t.length = static_cast<std::uint32_t>(L);
+    t.descriptor_index = static_cast<std::uint16_t>(r.below(65536));
+    t.checksum = static_cast<ChecksumMode>(r.below(3));
+    t.checksum_offload = r.below(2);
+    const std::uint16_t good = oracle_compute_checksum(p.data(), L);
+    t.checksum_value = r.below(6) == 0 ? static_cast<std::uint16_t>(r.below(65536)) : good;
+    if (r.below(tso_heavy ? 2 : 4) == 0) {
+      t.tso_enabled = r.below(2);
+      t.gso_enabled = !t.tso_enabled || r.below(3) == 0;
+      const std::uint32_t mp = r.below(10);
+      t.mss = static_cast<std::uint16_t>(mp == 0 ? 0 : (mp == 1 ? 9001 + r.below(3) : (mp < 3 ? 1 + r.below(9) : 50 + r.below(2000))));
+      const std::uint32_t hp = r.below(8);
+      t.header_length = static_cast<std::uint16_t>(hp == 0 ? r.below(4) : (hp == 1 ? L + r.below(2) : (hp == 2 ? r.below(12) : 14 + r.below(60))));
+    }
+    if (r.below(5) == 0) {
+      t.vlan_insert = true;
+      t.vlan_tag = static_cast<std::uint16_t>(r.below(65536));
+    }
+    pkts.emplace_back(at, std::move(p));
+    at += L;
+  }
+  at = (at + 15) & ~std::size_t{15};
+  std::vector<RxDescriptor> rx(nrx);
+  for (std::size_t j = 0; j < nrx; ++j) {
+    RxDescriptor& x = rx[j];
+    const std::uint32_t bp = r.below(10);
+    x.buffer_length = bp == 0 ? r.below(200) : (bp < 5 ? 2000 : 9300);
+    x.buffer_address = at + r.below(5);
+    at = x.buffer_address + x.buffer_length + r.below(4);
+    x.descriptor_index = static_cast<std::uint16_t>(r.below(65536));
+    x.checksum = static_cast<ChecksumMode>(r.below(3));
+    x.checksum_offload = r.below(3) != 0;
+    x.vlan_strip = r.below(3) == 0;
+    x.vlan_present = r.below(3) == 0;
+    x.vlan_tag = static_cast<std::uint16_t>(r.below(65536));
+    x.gro_enabled = r.below(4) == 0;
+  }
+  const std::size_t mem_size = at + 32;
+  for (std::size_t i = 0; i < ntx; ++i)
+    if (r.below(60) == 0) tx[i].buffer_address = r.below(2) ? mem_size + 1 + i : mem_size - tx[i].length / 2;
+  for (std::size_t j = 0; j < nrx; ++j)
+    if (r.below(70) == 0) rx[j].buffer_address = mem_size + 1 + j;
+  image.assign(mem_size, 0);
+  for (auto& [a, p] : pkts) std::memcpy(image.data() + a, p.data(), p.size());
+  std::vector<std::uint16_t> table(r.below(2) ? 128 : 1 + r.below(300));
+  for (auto& q : table) q = static_cast<std::uint16_t>(r.below(16));
+  const RssConfig rss_cfg{r.below(2) ? kMsKey : std::vector<std::uint8_t>{}, table};
+  const std::uint16_t qid = static_cast<std::uint16_t>(r.below(8));
+
+  BatchedQueuePairConfig cfg;
+  cfg.queue_id = qid;
+  cfg.max_mtu = max_mtu;
+  if (!rx_stage_detail::buffers_disjoint(mem_size, tx, rx)) return 0;  // the host path's business (rx_stage_fuzz)
+
+  // host resolve
+  RssEngine host_rss{rss_cfg};
+  cfg.rss = &host_rss;
+  std::vector<std::uint8_t> host_img = image;
+  test::CpuBackend cpu{host_img, &host_rss, TupleSpec{}};
+  RxBatchResult ho;
+  QueuePairStats hs{};
+  rx_stage_detail::BatchScratch scratch;
+  rx_stage_detail::run_batch(cfg, mem_size, tx, rx, hs, ho, scratch, cpu);
+
+  // device resolve
+  RssEngine dev_rss{rss_cfg};
+  cfg.rss = &dev_rss;
+  void* d = nullptr;
+  assert(nicgpu_malloc(&d, mem_size + 64) == NICGPU_OK);
+  assert(nicgpu_memcpy_async(d, image.data(), mem_size, nullptr) == NICGPU_OK);
+  BatchedQueuePair qp{cfg};
+  RxBatchResult go;
+  qp.process_batch(DeviceHostMemory{static_cast<std::byte*>(d), mem_size}, tx, rx, go);
+  std::vector<std::uint8_t> dev_img(mem_size);
+  assert(nicgpu_memcpy_async(dev_img.data(), d, mem_size, nullptr) == NICGPU_OK);
+  assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+  nicgpu_free(d);
+  if (!go.timings.device) {
+    std::fprintf(stderr, "seed %llu: disjoint batch not resolved on the device\n", (unsigned long long) seed);
+    return 1;
+  }
+  g_device += 1;
+  bool ok = go.tx_completions.size() == ho.tx_completions.size() && go.rx_completions.size() == ho.rx_completions.size();
+  for (std::size_t i = 0; ok && i < ho.tx_completions.size(); ++i) ok = same(go.tx_completions[i], ho.tx_completions[i]);
+  for (std::size_t i = 0; ok && i < ho.rx_completions.size(); ++i) ok = same(go.rx_completions[i], ho.rx_completions[i]);
+  const bool comp_ok = ok;
+  ok = ok && std::memcmp(&hs, &qp.stats(), sizeof(hs)) == 0;
+  const bool stats_ok = ok;
+  ok = ok && go.rx_consumed == ho.rx_consumed && go.tx_processed == ho.tx_processed;
+  ok = ok && host_img == dev_img;
+  const bool mem_ok = ok;
+  ok = ok && go.rx_hash == ho.rx_hash && go.rx_queue == ho.rx_queue && go.queues == ho.queues;
+  ok = ok && dev_rss.stats().hashes == host_rss.stats().hashes && dev_rss.stats().queue_hits == host_rss.stats().queue_hits;
+  if (!ok) {
+    std::fprintf(stderr,
+                 "seed %llu: device resolve differs (ntx %zu nrx %zu: completions %d stats %d memory %d; tx %zu/%zu rx "
+                 "%zu/%zu consumed %zu/%zu)\n",
+                 (unsigned long long) seed, ntx, nrx, int(comp_ok), int(stats_ok), int(mem_ok), go.tx_completions.size(),
+                 ho.tx_completions.size(), go.rx_completions.size(), ho.rx_completions.size(), go.rx_consumed,
+                 ho.rx_consumed);
+    return 1;
+  }
+  if (go.timings.host_tail) g_tail += 1;
+  for (const auto& c : ho.tx_completions)
+    if (c.status == static_cast<std::uint32_t>(CompletionCode::NoDescriptor)) {
+      g_short += 1;
+      break;
+    }
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  assert(gpu_device_count() >= 1);
+  const std::uint64_t first = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
+  const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 300;
+  int bad = 0;
+  for (std::uint64_t s = first; s < first + count; ++s) bad += run_case(s);
+  if (bad) return 1;
+  std::printf("rx_stage_gpu_fuzz: ok (%llu batches, %zu resolved on the device, %zu of them with a host tail, %zu "
+              "running out of RX descriptors)\n",
+              (unsigned long long) count, g_device, g_tail, g_short);
+  return 0;
+}

@@ -7,8 +7,10 @@ cpu: the stage's driver (rx_stage_detail::run_batch) over a CPU backend
      host copy, RSS through the host RssEngine) — completions, stats, the RX
      buffer bytes and the RSS hash/queue of every delivered frame must equal
      the reference's.  qp_alias has overlapping RX/RX and RX/TX buffers.
-gpu: the product path end to end (GPU piece sums, GPU gather of the segments,
-     GPU RSS of the delivered frames), same comparison plus RSS dispatch.
+gpu: the product path end to end, both resolvers: the device resolve
+     (nicgpu_qp_*, taken for disjoint buffers) and the host resolve with GPU
+     piece sums, gather and RSS; same comparison plus RSS dispatch.  A GPU
+     fuzz compares the two resolvers on random batches.
 """
 
 import json
@@ -73,6 +75,19 @@ def test_rx_stage_gpu(tmp_path):
     exe = _build(tmp_path, "rx_stage_test")
     for n in CASES:
         _run(exe, "gpu", n, tmp_path)
+
+
+@pytest.mark.gpu
+def test_rx_stage_device_resolve_vs_host_resolve(tmp_path):
+    """Random batches with disjoint buffers: the device resolve (nicgpu_qp_*,
+    process_batch's path for them) against the host resolve over the CPU
+    backend (the path rx_stage_fuzz pins to the reference QueuePair) —
+    completions, stats, memory image, RSS dispatch."""
+    exe = _build(tmp_path, "rx_stage_gpu_fuzz")
+    r = subprocess.run([exe, "1", "300"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "rx_stage_gpu_fuzz: ok" in r.stdout
+    print(r.stdout.strip())
 
 
 @pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="needs /root/reference (build container)")

@@ -1,6 +1,8 @@
 // bench_rx_stage.cpp — nic::BatchedQueuePair throughput.
 //
-//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads]
+//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host]
+//   (device: BatchedQueuePair's device resolve, the default for disjoint
+//   buffers; host: the host resolve, BatchedQueuePairConfig::device_resolve off)
 //
 // c3: IMIX 64/576/1518 (7:4:1) frames, each balanced so the whole-frame
 //     checksum verifies; RX descriptors with Layer4 checksum offload, 2 KiB
@@ -119,6 +121,7 @@ int main(int argc, char** argv) {
   cfg.queue_id = 1;
   cfg.rss = &rss;
   if (argc > 4) cfg.host_threads = static_cast<unsigned>(std::atoi(argv[4]));
+  if (argc > 5) cfg.device_resolve = std::string(argv[5]) != "host";
   BatchedQueuePair qp{cfg};
   const DeviceHostMemory dm{static_cast<std::byte*>(mem), mem_size};
 
@@ -130,8 +133,9 @@ int main(int argc, char** argv) {
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     if (r > 0) tot.push_back(us);
     const auto& P = last.timings;
-    std::fprintf(stderr, "rep %d: %.0f us (check %.0f plan %.0f sums %.0f resolve %.0f gather %.0f rss %.0f)\n", r, us,
-                 P.check_us, P.plan_us, P.sums_us, P.resolve_us, P.gather_us, P.rss_us);
+    std::fprintf(stderr, "rep %d: %.0f us (%s: check %.0f plan %.0f sums %.0f resolve %.0f gather %.0f rss %.0f copy %.0f)\n", r,
+                 us, P.device ? "device" : "host", P.check_us, P.plan_us, P.sums_us, P.resolve_us, P.gather_us, P.rss_us,
+                 P.copy_us);
   }
   std::sort(tot.begin(), tot.end());
   const double med = tot[tot.size() / 2];
@@ -140,11 +144,11 @@ int main(int argc, char** argv) {
   for (auto L : lens) frame_bytes += L;
   const auto& T = last.timings;
   std::printf(
-      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
+      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
       "\"rx_success\": %zu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
-      "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f}}\n",
-      wl.c_str(), cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
-      T.resolve_us, T.gather_us, T.rss_us);
+      "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f}}\n",
+      wl.c_str(), T.device ? "device" : "host", cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
+      T.resolve_us, T.gather_us, T.rss_us, T.copy_us);
   nicgpu_free(mem);
   return 0;
 }
