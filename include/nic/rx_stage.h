@@ -190,8 +190,9 @@ public:
   struct Scratch;  // device, pinned and host buffers reused across batches (grown, never shrunk)
 
 private:
-  void process_on_device(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
-                         QueuePairStats& stats, RxBatchResult& out, void* stream);
+  // false (nothing written) when disjoint() says the buffers overlap
+  bool process_on_device(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+                         QueuePairStats& stats, RxBatchResult& out, void* stream, const std::function<bool()>& disjoint);
   BatchedQueuePairConfig config_;
   QueuePairStats stats_{};
   std::unique_ptr<Scratch> scratch_;

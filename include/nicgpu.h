@@ -302,6 +302,9 @@ typedef struct nicgpu_qp_view {
   uint16_t* rss_queue;
   uint32_t* rx_hash;            /* [nrx]  per RX completion: hash (0 unless Success) */
   uint16_t* rx_queue;           /* [nrx]  per RX completion: queue (0xFFFF unless Success) */
+  uint32_t* queue_which;        /* [nrx]  Success completions grouped by queue (nicgpu_qp_group) */
+  uint32_t* queue_start;        /* [65536] queue q = queue_which[queue_start[q], queue_end[q]) */
+  uint32_t* queue_end;
 } nicgpu_qp_view;
 
 typedef struct nicgpu_qp nicgpu_qp;
@@ -333,6 +336,12 @@ int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, u
 int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, uint64_t* m, void* stream);
 /* view.rx_hash / rx_queue of those frames from view.rss_hash / rss_queue. */
 int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t m, void* stream);
+/* The RSS dispatch lists: the m frames of nicgpu_qp_rss_list grouped by queue
+ * (a stable sort, so each queue lists its completions in posting order) into
+ * view.queue_which, with each queue's range in view.queue_start / queue_end
+ * for queues [0, *nq) (*nq = largest queue + 1; 0 when m is 0).
+ * Synchronises `stream`. */
+int nicgpu_qp_group(nicgpu_qp* q, size_t m, uint64_t* nq, void* stream);
 
 #ifdef __cplusplus
 }

@@ -74,6 +74,7 @@ ABI_SYMBOLS = (
     "nicgpu_qp_resolve",
     "nicgpu_qp_rss_list",
     "nicgpu_qp_rss_scatter",
+    "nicgpu_qp_group",
     "nicgpu_icrc_batch",
     "nicgpu_tso_segment",
 )

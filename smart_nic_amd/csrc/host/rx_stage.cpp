@@ -946,14 +946,36 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
                                      std::span<const RxDescriptor> rx, RxBatchResult& out, void* stream) {
   using clock = std::chrono::steady_clock;
   if (mem.base == nullptr && mem.size != 0) throw GpuError("process_batch: null host-memory image", NICGPU_ERR_INVALID);
-  const auto t0 = clock::now();
-  const bool disjoint = rx_stage_detail::buffers_disjoint(mem.size, tx, rx);
-  const double check_us = std::chrono::duration<double, std::micro>(clock::now() - t0).count();
+  // the overlap check runs beside the device resolve's side-effect-free
+  // first steps (descriptor upload, plan, sums, positions), which are dropped
+  // if the buffers do overlap
+  bool disjoint = false;
+  double check_us = 0;
+  auto check_overlap = [&] {
+    const auto t0 = clock::now();
+    disjoint = rx_stage_detail::buffers_disjoint(mem.size, tx, rx);
+    check_us = std::chrono::duration<double, std::micro>(clock::now() - t0).count();
+  };
   // stats are committed only when the whole batch went through
   QueuePairStats st = stats_;
-  if (disjoint && config_.device_resolve && !config_.on_interrupt) {
-    process_on_device(mem, tx, rx, st, out, stream);
+  bool on_device = false;
+  if (config_.device_resolve && !config_.on_interrupt) {
+    struct Joiner {
+      std::thread th;
+      ~Joiner() {
+        if (th.joinable()) th.join();
+      }
+    } j{std::thread(check_overlap)};
+    auto wait = [&] {
+      if (j.th.joinable()) j.th.join();
+      return disjoint;
+    };
+    on_device = process_on_device(mem, tx, rx, st, out, stream, wait);
+    wait();
   } else {
+    check_overlap();
+  }
+  if (!on_device) {
     GpuBackend dev{*scratch_, mem, config_, stream};
     rx_stage_detail::run_batch(config_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint ? 1 : 0);
   }
@@ -966,9 +988,9 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
 // descriptor whose RX side ends it early (or where the ring runs short)
 // resolved here in order, then the DMA writes and RSS of the whole batch on
 // the device; the host moves descriptors up and completions down.
-void BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
+bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                          std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out,
-                                         void* stream) {
+                                         void* stream, const std::function<bool()>& disjoint) {
   using namespace rx_stage_detail;
   using clock = std::chrono::steady_clock;
   auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
@@ -1004,6 +1026,9 @@ void BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   nicgpu_qp_stats ds{};
   check(nicgpu_qp_resolve(S.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, &done, &used, &ds, stream),
         "nicgpu_qp_resolve");
+  out.timings.resolve_us += us_since(t);
+  if (!disjoint()) return false;  // nothing written yet: the host path takes the batch
+  t = clock::now();
   const QueuePairStats d{ds.tx_packets,         ds.rx_packets,         ds.tx_bytes,
                          ds.rx_bytes,           ds.drops_checksum,     ds.drops_no_rx_desc,
                          ds.drops_buffer_small, ds.drops_mtu_exceeded, ds.drops_invalid_mss,
@@ -1063,6 +1088,18 @@ void BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
     check(nicgpu_qp_rss_scatter(S.qp, m, stream), "nicgpu_qp_rss_scatter");
     check(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, stream), "nicgpu_memcpy_async");
     check(nicgpu_memcpy_async(out.rx_queue.data(), v.rx_queue, nrx_total * 2, stream), "nicgpu_memcpy_async");
+    // dispatch lists grouped on the device (stable sort by queue)
+    std::uint64_t nq = 0;
+    check(nicgpu_qp_group(S.qp, m, &nq, stream), "nicgpu_qp_group");
+    std::uint32_t* which = S.h_hash.get<std::uint32_t>(std::max<std::uint64_t>(m, 1) + 2 * nq);
+    std::uint32_t* qs = which + m;
+    std::uint32_t* qe = qs + nq;
+    check(nicgpu_memcpy_async(which, v.queue_which, m * 4, stream), "nicgpu_memcpy_async");
+    check(nicgpu_memcpy_async(qs, v.queue_start, nq * 4, stream), "nicgpu_memcpy_async");
+    check(nicgpu_memcpy_async(qe, v.queue_end, nq * 4, stream), "nicgpu_memcpy_async");
+    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+    out.queues.resize(nq);
+    for (std::uint64_t q = 0; q < nq; ++q) out.queues[q].assign(which + qs[q], which + qe[q]);
   } else {
     std::fill(out.rx_hash.begin(), out.rx_hash.end(), 0u);
     std::fill(out.rx_queue.begin(), out.rx_queue.end(), RxBatchResult::kNoQueue);
@@ -1074,11 +1111,7 @@ void BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
         "nicgpu_memcpy_async");
   check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
   out.timings.copy_us += us_since(t);
-  if (config_.rss != nullptr) {
-    t = clock::now();
-    build_queue_lists(out);
-    out.timings.rss_us += us_since(t);
-  }
+  return true;
 }
 
 }  // namespace nic

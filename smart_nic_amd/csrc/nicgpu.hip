@@ -2622,6 +2622,16 @@ __global__ __launch_bounds__(kQpBlock) void qp_scatter_kernel(const uint32_t* __
   }
 }
 
+// queue range boundaries of the sorted keys
+__global__ __launch_bounds__(kQpBlock) void qp_bounds_kernel(const uint16_t* __restrict__ key, uint64_t m,
+                                                             uint32_t* start, uint32_t* end) {
+  for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < m; k += (uint64_t) gridDim.x * kQpBlock) {
+    const uint16_t q = key[k];
+    if (k == 0 || key[k - 1] != q) start[q] = (uint32_t) k;
+    if (k + 1 == m || key[k + 1] != q) end[q] = (uint32_t) (k + 1);
+  }
+}
+
 template <class T>
 int qp_grow(T*& p, size_t& cap, size_t want) {
   if (want <= cap) return NICGPU_OK;
@@ -2654,6 +2664,9 @@ struct nicgpu_qp {
   uint64_t* rss_desc = nullptr;
   uint16_t *rss_queue = nullptr, *rx_queue = nullptr;
   uint64_t* partials = nullptr;
+  uint16_t* sorted_key = nullptr;
+  uint32_t *queue_which = nullptr, *queue_start = nullptr, *queue_end = nullptr;
+  size_t c_sk = 0, c_qw = 0;
   unsigned long long* scal = nullptr;
   uint8_t* tmp = nullptr;
   uint64_t host_scal[4] = {0, 0, 0, 0};
@@ -2676,6 +2689,9 @@ void qp_fill_view(const nicgpu_qp* q, nicgpu_qp_view* v) {
   v->rss_queue = q->rss_queue;
   v->rx_hash = q->rx_hash;
   v->rx_queue = q->rx_queue;
+  v->queue_which = q->queue_which;
+  v->queue_start = q->queue_start;
+  v->queue_end = q->queue_end;
 }
 
 unsigned qp_grid(const nicgpu_qp* q, uint64_t n) {
@@ -2708,7 +2724,9 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
   q->device = device;
   q->grid = (unsigned) di.cus * 8u;
   if (hipMalloc(&q->scal, 4 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc(&q->partials, (size_t) q->grid * kQpStats * sizeof(uint64_t)) != hipSuccess) {
+      hipMalloc(&q->partials, (size_t) q->grid * kQpStats * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&q->queue_start, 65536 * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&q->queue_end, 65536 * sizeof(uint32_t)) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
   }
@@ -2721,7 +2739,8 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
   DeviceGuard g(q->device);
   void* bufs[] = {q->tx, q->rx, q->plans, q->counts, q->base, q->need, q->pos, q->piece_desc, q->piece_csum,
                   q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
-                  q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp};
+                  q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sorted_key, q->queue_which,
+                  q->queue_start, q->queue_end};
   for (void* b : bufs)
     if (b) (void) hipFree(b);
   delete q;
@@ -2752,6 +2771,8 @@ int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view
   if (st == NICGPU_OK) st = qp_grow(q->rss_queue, q->c_q, r1);
   if (st == NICGPU_OK) st = qp_grow(q->rx_hash, q->c_rh, r1);
   if (st == NICGPU_OK) st = qp_grow(q->rx_queue, q->c_rq, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->sorted_key, q->c_sk, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->queue_which, q->c_qw, r1);
   q->cap_tx = ntx;
   q->cap_rx = nrx;
   qp_fill_view(q, view);
@@ -2850,6 +2871,36 @@ int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, uint64_t* m, void* stream) {
   if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&cnt, q->at + nrx, sizeof(cnt), hipMemcpyDeviceToHost, s));
   if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
   *m = cnt;
+  return st;
+}
+
+int nicgpu_qp_group(nicgpu_qp* q, size_t m, uint64_t* nq, void* stream) {
+  if (!q || !nq || m > q->cap_rx) return NICGPU_ERR_INVALID;
+  *nq = 0;
+  if (m == 0) return NICGPU_OK;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  size_t tb = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, q->rss_queue, q->sorted_key, q->which, q->queue_which, (int) m, 0,
+                                         16, s) != hipSuccess)
+    return NICGPU_ERR_HIP;
+  int st = qp_grow(q->tmp, q->c_tmp, tb);
+  if (st != NICGPU_OK) return st;
+  st = hip_status(hipcub::DeviceRadixSort::SortPairs(q->tmp, tb, q->rss_queue, q->sorted_key, q->which, q->queue_which,
+                                                     (int) m, 0, 16, s));
+  uint16_t last = 0;
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&last, q->sorted_key + m - 1, sizeof(last), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  if (st != NICGPU_OK) return st;
+  const uint64_t n = (uint64_t) last + 1;
+  st = hip_status(hipMemsetAsync(q->queue_start, 0, n * sizeof(uint32_t), s));
+  if (st == NICGPU_OK) st = hip_status(hipMemsetAsync(q->queue_end, 0, n * sizeof(uint32_t), s));
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_bounds_kernel, dim3(qp_grid(q, m)), dim3(kQpBlock), 0, s, q->sorted_key, (uint64_t) m,
+                     q->queue_start, q->queue_end);
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  *nq = n;
   return st;
 }
 
