@@ -177,7 +177,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the same-box read-only streaming ceiling")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02a_pmc_c2.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02d_pmc_c2.json"))
     args = ap.parse_args()
 
     import torch
