@@ -95,9 +95,11 @@ def cpu_baseline(frames, desc, table, gpu_out, n_sample_mt, n_sample_1):
 def cpu_rows_baseline(pktgen):
     """The CPU side of the other SURVEY §8 rows, beside the GPU numbers in
     DESIGN.md §5 (bounded samples, this host): C3 IMIX RX through the compiled
-    reference (16 threads and 1 core), and — the reference TUs for these are
-    not buildable here or have no batch entry point — the oracle restatement
-    on one core for the C5 TSO segment checksums and the C2 ICRC."""
+    reference (16 threads and 1 core), the reference QueuePair over a C3-style
+    batch for row f1 (1 core; the reference is single-threaded), and — the
+    reference TUs for these are not buildable here or have no batch entry
+    point — the oracle restatement on one core for the C5 TSO segment
+    checksums and the C2 ICRC."""
     import ctypes
 
     from oracle import pyoracle as po
@@ -136,6 +138,17 @@ def cpu_rows_baseline(pktgen):
     rows.append({"row": "tso_c5", "value": round(n5 / dt / 1e6, 4), "unit": "Mpkt/s", "cores": 1, "kind": "port",
                  "gbs": round(n5 * 9000 / dt / 1e9, 4),
                  "sample": f"{n5} x 9000 B frames, H 54, mss 1448 ({nseg} segment checksums)"})
+    # row f1: the reference's own QueuePair::process_once over a C3-style
+    # batch (oracle/_ref/ref_qp_bench, compiled from the reference sources in
+    # the build container; the GPU side is tools/bench_rx_stage.cpp)
+    qp_bench = os.path.join(ROOT, "oracle", "_ref", "ref_qp_bench")
+    if os.path.exists(qp_bench):
+        import json as _json
+        import subprocess
+
+        r = subprocess.run([qp_bench, str(1 << 18), "3"], capture_output=True, text=True, timeout=120)
+        if r.returncode == 0 and r.stdout.strip():
+            rows.append(_json.loads(r.stdout.strip().splitlines()[-1]))
     n2 = 1 << 15
     f2, d2, _ = pktgen.make_batch(np.full(n2, 1518), seed=42, proto=6, corrupt_frac=0.0)
     crc = np.zeros(n2, np.uint32)

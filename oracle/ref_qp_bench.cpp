@@ -1,0 +1,124 @@
+// ref_qp_bench.cpp — CPU baseline of SURVEY §8 row f1 (TEST/MEASUREMENT
+// INFRASTRUCTURE ONLY): the reference's own QueuePair::process_once
+// (src/queue_pair.cpp:67-460, compiled from /root/reference by
+// `make -C oracle ref`; no reference source is copied) over the C3-style batch
+// that tools/bench_rx_stage.cpp gives nic::BatchedQueuePair: IMIX 64/576/1518
+// (7:4:1) frames, each balanced so the whole-frame checksum verifies, TX
+// checksum offload, RX descriptors with Layer4 checksum offload and 2 KiB
+// buffers.  One thread (the reference is single-threaded).  Prints one JSON
+// line: descriptors per second through push + process_once + poll.
+//
+//   ref_qp_bench [tx_descriptors] [reps]
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "nic/dma_engine.h"
+#include "nic/queue_pair.h"
+#include "nic/simple_host_memory.h"
+
+using namespace nic;
+
+namespace {
+
+std::uint16_t csum(const std::uint8_t* p, std::size_t n) {
+  std::uint64_t s = 0;
+  for (std::size_t i = 0; i + 1 < n; i += 2) s += (std::uint32_t{p[i]} << 8) | p[i + 1];
+  if (n & 1) s += std::uint32_t{p[n - 1]} << 8;
+  while (s >> 16) s = (s & 0xFFFF) + (s >> 16);
+  return static_cast<std::uint16_t>(~s);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const std::size_t n = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : (1u << 18);
+  const int reps = argc > 2 ? std::atoi(argv[2]) : 3;
+  std::mt19937_64 rng(7);
+  std::vector<std::size_t> lens(n);
+  for (auto& L : lens) {
+    const auto r = rng() % 12;
+    L = r < 7 ? 64 : (r < 11 ? 576 : 1518);
+  }
+  std::size_t tx_bytes = 0;
+  for (auto L : lens) tx_bytes += (L + 15) & ~std::size_t{15};
+  const std::size_t rx_buf = 2048;
+  const std::size_t mem_size = tx_bytes + n * rx_buf;
+  std::vector<std::uint8_t> img(tx_bytes);
+  std::vector<TxDescriptor> tx(n);
+  std::size_t at = 0, frame_bytes = 0;
+  for (std::size_t i = 0; i < n; ++i) {
+    std::uint8_t* p = img.data() + at;
+    for (std::size_t b = 0; b < lens[i]; b += 8) {
+      const std::uint64_t r = rng();
+      std::memcpy(p + b, &r, std::min<std::size_t>(8, lens[i] - b));
+    }
+    p[12] = 0x08;
+    p[13] = 0x00;
+    p[10] = p[11] = 0;
+    const std::uint16_t c = csum(p, lens[i]);
+    p[10] = static_cast<std::uint8_t>(c >> 8);
+    p[11] = static_cast<std::uint8_t>(c);
+    TxDescriptor& t = tx[i];
+    t.buffer_address = at;
+    t.length = static_cast<std::uint32_t>(lens[i]);
+    t.descriptor_index = static_cast<std::uint16_t>(i);
+    t.checksum_offload = true;
+    t.checksum = ChecksumMode::Layer4;
+    at += (lens[i] + 15) & ~std::size_t{15};
+    frame_bytes += lens[i];
+  }
+  std::vector<RxDescriptor> rx(n);
+  for (std::size_t j = 0; j < n; ++j) {
+    rx[j].buffer_address = tx_bytes + j * rx_buf;
+    rx[j].buffer_length = static_cast<std::uint32_t>(rx_buf);
+    rx[j].descriptor_index = static_cast<std::uint16_t>(j);
+    rx[j].checksum_offload = true;
+    rx[j].checksum = ChecksumMode::Layer4;
+  }
+  SimpleHostMemory mem{HostMemoryConfig{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false}};
+  if (!mem.write(0, std::as_bytes(std::span<const std::uint8_t>(img))).ok()) return 1;
+  DMAEngine dma{mem};
+  std::vector<double> secs;
+  std::size_t ok = 0;
+  for (int r = 0; r < reps; ++r) {
+    QueuePairConfig qc{
+        .queue_id = 1,
+        .tx_ring = {.descriptor_size = sizeof(TxDescriptor), .ring_size = n + 1, .base_address = 0, .queue_id = 1, .host_backed = false},
+        .rx_ring = {.descriptor_size = sizeof(RxDescriptor), .ring_size = n + 1, .base_address = 0, .queue_id = 1, .host_backed = false},
+        .tx_completion = {.ring_size = n + 1, .queue_id = 1},
+        .rx_completion = {.ring_size = n + 1, .queue_id = 1},
+    };
+    QueuePair qp{qc, dma};
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::byte> b(sizeof(TxDescriptor));
+    for (const auto& t : tx) {
+      std::memcpy(b.data(), &t, sizeof(t));
+      if (!qp.tx_ring().push_descriptor(b).ok()) return 2;
+    }
+    std::vector<std::byte> br(sizeof(RxDescriptor));
+    for (const auto& x : rx) {
+      std::memcpy(br.data(), &x, sizeof(x));
+      if (!qp.rx_ring().push_descriptor(br).ok()) return 3;
+    }
+    while (qp.process_once()) {
+    }
+    ok = 0;
+    while (auto c = qp.rx_completion().poll_completion()) ok += c->status == static_cast<std::uint32_t>(CompletionCode::Success);
+    while (auto c = qp.tx_completion().poll_completion()) {
+    }
+    secs.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+  }
+  std::sort(secs.begin(), secs.end());
+  const double med = secs[secs.size() / 2];
+  std::printf("{\"row\": \"f1_c3\", \"value\": %.4f, \"unit\": \"Mpkt/s\", \"cores\": 1, \"kind\": \"reference\", "
+              "\"gbs\": %.4f, \"rx_success\": %zu, \"sample\": \"%zu IMIX TX descriptors (7:4:1 64/576/1518 B) "
+              "through the reference QueuePair::process_once (push, process, poll), 2 KiB RX buffers, Layer4 RX "
+              "verify; median of %d\"}\n",
+              n / med / 1e6, frame_bytes / med / 1e9, ok, n, reps);
+  return 0;
+}
