@@ -112,6 +112,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_rx_offload_ex": (i32, [vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp, vp]),
         "nicgpu_segment_gather": (i32, [vp, ctypes.c_uint64, vp, sz, vp]),
         "nicgpu_segment_gather_from": (i32, [vp, vp, ctypes.c_uint64, vp, sz, vp]),
+        "nicgpu_qp_create": (i32, [vp, i32]),
+        "nicgpu_qp_destroy": (i32, [vp]),
+        "nicgpu_qp_reserve": (i32, [vp, sz, sz, vp]),
+        "nicgpu_qp_plan": (i32, [vp, vp, ctypes.c_uint64, sz, ctypes.c_uint64, vp, vp, vp]),
+        "nicgpu_qp_resolve": (i32, [vp, ctypes.c_uint64, sz, sz, ctypes.c_uint64, ctypes.c_uint16, vp, vp, vp, vp]),
+        "nicgpu_qp_rss_list": (i32, [vp, sz, vp, vp]),
+        "nicgpu_qp_rss_scatter": (i32, [vp, sz, vp]),
+        "nicgpu_qp_group": (i32, [vp, sz, vp, vp]),
         "nicgpu_icrc_batch": (i32, [vp, vp, sz, i32, vp, vp, vp]),
         "nicgpu_tso_segment": (i32, [vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint64, u32, vp, vp, vp]),
         "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),

@@ -111,6 +111,15 @@ def test_batch_entry_points_validate_before_device_access():
     assert lib.nicgpu_checksum_batch(None, p, 1, p, None) == INV
     assert lib.nicgpu_checksum_batch(p, None, 1, p, None) == INV
     assert lib.nicgpu_checksum_batch(mis, p, 1, p, None) == INV
+    # the device QueuePair context (nicgpu_qp_*): no context, no outputs -> INVALID
+    assert lib.nicgpu_qp_create(None, 0) == INV
+    assert lib.nicgpu_qp_destroy(None) == INV
+    assert lib.nicgpu_qp_reserve(None, 1, 1, p) == INV
+    assert lib.nicgpu_qp_plan(None, p, 64, 1, 9000, p, p, None) == INV
+    assert lib.nicgpu_qp_resolve(None, 64, 1, 1, 9000, 0, p, p, p, None) == INV
+    assert lib.nicgpu_qp_rss_list(None, 1, p, None) == INV
+    assert lib.nicgpu_qp_rss_scatter(None, 1, None) == INV
+    assert lib.nicgpu_qp_group(None, 1, p, None) == INV
     # nicgpu_rx_offload_ex(ctx, frames, desc, n, mode, raw_off, raw_len, csum, hash, queue, hits, l34, stream)
     NONE, AUTO, RAW = sna.TUPLE_NONE, sna.TUPLE_AUTO, sna.TUPLE_RAW
     assert lib.nicgpu_rx_offload_ex(None, None, None, 0, NONE, 0, 0, None, None, None, None, None, None) == OK
