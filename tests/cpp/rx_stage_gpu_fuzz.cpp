@@ -195,10 +195,103 @@ int run_case(std::uint64_t seed) {
   return 0;
 }
 
+// Full-size f1 workloads (tools/bench_rx_stage.cpp's): C3 = 1 M IMIX frames
+// (balanced so every RX verify passes), C5 = 131072 x 9000 B TSO (H 54, mss
+// 1448; random payloads, so every packet ends at its first segment's
+// checksum).  Device resolve against host resolve, everything compared.
+int run_full(const char* wl) {
+  const bool c5 = std::strcmp(wl, "c5") == 0;
+  const std::size_t n = c5 ? 131072 : (1u << 20);
+  Rng r{c5 ? 55u : 33u};
+  std::vector<std::size_t> lens(n);
+  for (auto& L : lens) {
+    const std::uint32_t k = r.below(12);
+    L = c5 ? 9000 : (k < 7 ? 64 : (k < 11 ? 576 : 1518));
+  }
+  std::size_t tx_bytes = 0;
+  for (auto L : lens) tx_bytes += (L + 15) & ~std::size_t{15};
+  const std::size_t rx_buf = c5 ? 1600 : 2048, segs = c5 ? 7 : 1, nrx = n * segs;
+  const std::size_t mem_size = tx_bytes + nrx * rx_buf;
+  std::vector<std::uint8_t> image(mem_size, 0);
+  std::vector<TxDescriptor> tx(n);
+  std::size_t at = 0;
+  for (std::size_t i = 0; i < n; ++i) {
+    std::uint8_t* p = image.data() + at;
+    for (std::size_t b = 0; b < lens[i]; ++b) p[b] = r.byte();
+    p[12] = 0x08;
+    p[13] = 0x00;
+    if (!c5) {
+      p[10] = p[11] = 0;
+      const std::uint16_t c = oracle_compute_checksum(p, lens[i]);
+      p[10] = static_cast<std::uint8_t>(c >> 8);
+      p[11] = static_cast<std::uint8_t>(c);
+    }
+    TxDescriptor& t = tx[i];
+    t.buffer_address = at;
+    t.length = static_cast<std::uint32_t>(lens[i]);
+    t.descriptor_index = static_cast<std::uint16_t>(i);
+    t.checksum_offload = true;
+    t.checksum = ChecksumMode::Layer4;
+    if (c5) {
+      t.tso_enabled = true;
+      t.mss = 1448;
+      t.header_length = 54;
+    }
+    at += (lens[i] + 15) & ~std::size_t{15};
+  }
+  std::vector<RxDescriptor> rx(nrx);
+  for (std::size_t j = 0; j < nrx; ++j) {
+    rx[j].buffer_address = tx_bytes + j * rx_buf;
+    rx[j].buffer_length = static_cast<std::uint32_t>(rx_buf);
+    rx[j].descriptor_index = static_cast<std::uint16_t>(j);
+    rx[j].checksum_offload = true;
+    rx[j].checksum = ChecksumMode::Layer4;
+  }
+  std::vector<std::uint16_t> table(128);
+  for (int i = 0; i < 128; ++i) table[i] = static_cast<std::uint16_t>(i % 16);
+  const RssConfig rss_cfg{kMsKey, table};
+  BatchedQueuePairConfig cfg;
+  cfg.queue_id = 1;
+  RssEngine host_rss{rss_cfg};
+  cfg.rss = &host_rss;
+  std::vector<std::uint8_t> host_img = image;
+  test::CpuBackend cpu{host_img, &host_rss, TupleSpec{}};
+  RxBatchResult ho;
+  QueuePairStats hs{};
+  rx_stage_detail::BatchScratch scratch;
+  rx_stage_detail::run_batch(cfg, mem_size, tx, rx, hs, ho, scratch, cpu);
+  RssEngine dev_rss{rss_cfg};
+  cfg.rss = &dev_rss;
+  void* d = nullptr;
+  assert(nicgpu_malloc(&d, mem_size + 64) == NICGPU_OK);
+  assert(nicgpu_memcpy_async(d, image.data(), mem_size, nullptr) == NICGPU_OK);
+  BatchedQueuePair qp{cfg};
+  RxBatchResult go;
+  qp.process_batch(DeviceHostMemory{static_cast<std::byte*>(d), mem_size}, tx, rx, go);
+  std::vector<std::uint8_t> dev_img(mem_size);
+  assert(nicgpu_memcpy_async(dev_img.data(), d, mem_size, nullptr) == NICGPU_OK);
+  assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+  nicgpu_free(d);
+  bool ok = go.timings.device && !go.timings.host_tail && go.tx_completions.size() == ho.tx_completions.size() &&
+            go.rx_completions.size() == ho.rx_completions.size();
+  for (std::size_t i = 0; ok && i < ho.tx_completions.size(); ++i) ok = same(go.tx_completions[i], ho.tx_completions[i]);
+  for (std::size_t i = 0; ok && i < ho.rx_completions.size(); ++i) ok = same(go.rx_completions[i], ho.rx_completions[i]);
+  ok = ok && std::memcmp(&hs, &qp.stats(), sizeof(hs)) == 0 && go.rx_consumed == ho.rx_consumed;
+  ok = ok && host_img == dev_img && go.rx_hash == ho.rx_hash && go.rx_queue == ho.rx_queue && go.queues == ho.queues;
+  ok = ok && dev_rss.stats().hashes == host_rss.stats().hashes && dev_rss.stats().queue_hits == host_rss.stats().queue_hits;
+  std::size_t succ = 0;
+  for (const auto& c : go.rx_completions) succ += c.status == 0;
+  std::printf("rx_stage_gpu_fuzz full %s: %s (%zu TX, %zu RX completions, %zu Success, device %d, host tail %d)\n", wl,
+              ok ? "ok" : "MISMATCH", go.tx_completions.size(), go.rx_completions.size(), succ, int(go.timings.device),
+              int(go.timings.host_tail));
+  return ok ? 0 : 1;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   assert(gpu_device_count() >= 1);
+  if (argc > 1 && std::strcmp(argv[1], "full") == 0) return run_full(argc > 2 ? argv[2] : "c3");
   const std::uint64_t first = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
   const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 300;
   int bad = 0;

@@ -117,3 +117,22 @@ def test_full_size_c5_tso_linearity():
         k, exp = po.tso_segment_checksums(frames[offs[i]: offs[i] + L].tobytes(), H, M)
         assert k == nseg
         assert seg[i].astype(np.uint16).tolist() == list(exp), int(i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wl", ["c3", "c5"])
+def test_f1_full_size_device_vs_host(tmp_path, wl):
+    """Row f1 at the bench sizes (tools/bench_rx_stage.cpp): 1 M IMIX TX
+    descriptors (C3) and 131072 x 9000 B TSO frames (C5, every packet ending at
+    its first segment's checksum: positions settle by relaxation without a host
+    tail).  The device resolve must equal the host resolve in every
+    completion, stat, memory byte and RSS dispatch list."""
+    import subprocess
+
+    from test_host_cpp import _build
+
+    exe = _build(tmp_path, "rx_stage_gpu_fuzz")
+    r = subprocess.run([exe, "full", wl], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert f"full {wl}: ok" in r.stdout
+    print(r.stdout.strip())
