@@ -2924,7 +2924,8 @@ int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t m, void* stream) {
 namespace {
 template <int U>
 __global__ __launch_bounds__(256) void stream_read_kernel(const u32x4* __restrict__ p, uint64_t n16,
-                                                          uint32_t* __restrict__ out) {
+                                                          uint32_t* __restrict__ out, unsigned long long* stamps) {
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   uint32_t acc = 0;
   const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
   uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
@@ -2940,6 +2941,13 @@ __global__ __launch_bounds__(256) void stream_read_kernel(const u32x4* __restric
     acc = add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, acc))));
   }
   if (acc == 0x12345678u) out[0] = acc;  // keep the loads live
+  if (stamps != nullptr && (threadIdx.x & 63) == 0) {  // per wave, as the RX kernel's (tools/wave_stamps.py)
+    const uint64_t w = ((uint64_t) blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    stamps[4 * w + 0] = t_start;
+    stamps[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
+    stamps[4 * w + 2] = (unsigned) __builtin_amdgcn_s_getreg((3 << 11) | 20);
+    stamps[4 * w + 3] = (unsigned) __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  }
 }
 
 // lane l of a wave reads the 32-B pair (2l, 2l+1) of each 2-KiB step
@@ -3059,9 +3067,9 @@ int nicgpu_tune_stream_read(const uint8_t* buf, size_t bytes, int blocks_per_cu,
   hipStream_t s = static_cast<hipStream_t>(stream);
   const u32x4* p = reinterpret_cast<const u32x4*>(buf);
   if (unroll == 2) hipLaunchKernelGGL(stream_read_pairs_kernel, dim3(grid), dim3(256), 0, s, p, n16, out);
-  else if (unroll == 8) hipLaunchKernelGGL(stream_read_kernel<8>, dim3(grid), dim3(256), 0, s, p, n16, out);
-  else if (unroll == 4) hipLaunchKernelGGL(stream_read_kernel<4>, dim3(grid), dim3(256), 0, s, p, n16, out);
-  else hipLaunchKernelGGL(stream_read_kernel<1>, dim3(grid), dim3(256), 0, s, p, n16, out);
+  else if (unroll == 8) hipLaunchKernelGGL(stream_read_kernel<8>, dim3(grid), dim3(256), 0, s, p, n16, out, g_tune_stamps);
+  else if (unroll == 4) hipLaunchKernelGGL(stream_read_kernel<4>, dim3(grid), dim3(256), 0, s, p, n16, out, g_tune_stamps);
+  else hipLaunchKernelGGL(stream_read_kernel<1>, dim3(grid), dim3(256), 0, s, p, n16, out, g_tune_stamps);
   return hip_status(hipGetLastError());
 }
 }  // extern "C"

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--workloads", default="c2,imix")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--launches", type=int, default=5)
+    ap.add_argument("--stream", action="store_true", help="stamp the read-ceiling kernel instead of the RX kernel")
     ap.add_argument("--dbg", type=int, default=0, help="nicgpu_tune_set_dbg bits for the stamped launches (8192: rotate)")
     args = ap.parse_args()
 
@@ -46,6 +47,8 @@ def main():
     tl.nicgpu_tune_rx_offload.restype = i32
     tl.nicgpu_tune_rx_offload.argtypes = [i32, vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp]
     tl.nicgpu_tune_set_stamps.argtypes = [vp]
+    tl.nicgpu_tune_stream_read.restype = i32
+    tl.nicgpu_tune_stream_read.argtypes = [vp, sz, i32, i32, vp, vp]
     tl.nicgpu_tune_set_dbg.argtypes = [u32]
     tl.nicgpu_tune_set_dbg(args.dbg)
     tl.nicgpu_tune_variant_name.restype = ctypes.c_char_p
@@ -82,7 +85,12 @@ def main():
         qs = torch.empty(n, dtype=torch.int16, device="cuda")
         hits = torch.zeros(128, dtype=torch.int64, device="cuda")
 
+        sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+
         def run():
+            if args.stream:  # the same-box read ceiling's kernel (unroll 4, 2 blocks per CU) over the frames
+                assert tl.nicgpu_tune_stream_read(f.data_ptr(), f.numel() // 16 * 16, 2, 4, sink.data_ptr(), sp) == 0
+                return
             assert tl.nicgpu_tune_rx_offload(args.variant, h, f.data_ptr(), d.data_ptr(), n, sna.TUPLE_AUTO, 0, 0,
                                              cs.data_ptr(), hs.data_ptr(), qs.data_ptr(), hits.data_ptr(), sp) == 0
 
@@ -118,7 +126,7 @@ def main():
                 "tail_last10pct_us": round(span - q(end, 0.9), 1), "per_xcd": per_xcd,
             })
         best = int(np.argmin(spans))
-        out = {"workload": w, "dbg": args.dbg, "variant": tl.nicgpu_tune_variant_name(args.variant).decode(), "packets": int(n),
+        out = {"workload": w, "kernel": "stream_read<4>" if args.stream else "rx", "dbg": args.dbg, "variant": tl.nicgpu_tune_variant_name(args.variant).decode(), "packets": int(n),
                "bytes": int(lens.sum()), "spans_us": [round(x, 1) for x in spans], "best": rows[best]}
         print(json.dumps(out), flush=True)
         del f, d
