@@ -111,7 +111,10 @@ struct QueuePairStats {
 
 namespace nic {
 
-/// Device-resident image of the host memory the DMA engine addresses.
+/// Device-resident image of the host memory the DMA engine addresses.  The
+/// kernels read it in 16-B chunks: `base` must be 16-B aligned and the
+/// allocation must cover `size` rounded up to a multiple of 16 (nicgpu.h,
+/// "Batch layout in HBM").
 struct DeviceHostMemory {
   std::byte* base{nullptr};  // device pointer; host address a <-> base[a]
   std::size_t size{0};
@@ -155,7 +158,7 @@ struct RxBatchResult {
   /// Wall time of each phase of process_batch (host clock, GPU phases
   /// include their stream synchronisation).
   struct Timings {
-    double check_us{0};  // buffers_disjoint (overlapping buffers?)
+    double check_us{0};  // overlapping buffers? (nicgpu_qp_check on the device path, else buffers_disjoint)
     double plan_us{0}, sums_us{0}, resolve_us{0}, gather_us{0}, rss_us{0};
     double copy_us{0};   // device resolve: descriptors up, completions down
     bool device{false};     // resolved on the device
@@ -192,7 +195,7 @@ public:
 private:
   // false (nothing written) when disjoint() says the buffers overlap
   bool process_on_device(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
-                         QueuePairStats& stats, RxBatchResult& out, void* stream, const std::function<bool()>& disjoint);
+                         QueuePairStats& stats, RxBatchResult& out, void* stream, int& disjoint, double& check_us);
   BatchedQueuePairConfig config_;
   QueuePairStats stats_{};
   std::unique_ptr<Scratch> scratch_;

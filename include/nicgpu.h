@@ -310,8 +310,17 @@ typedef struct nicgpu_qp_view {
 typedef struct nicgpu_qp nicgpu_qp;
 int nicgpu_qp_create(nicgpu_qp** out, int device);
 int nicgpu_qp_destroy(nicgpu_qp* q);
-/* Capacity for ntx TX and nrx RX descriptors; fills *view. */
+/* Capacity for ntx TX and nrx RX descriptors (ntx <= 2^32 / 64, so that piece
+ * indices fit 32 bits; nrx < 2^31 - 1); fills *view. */
 int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view);
+/* Whether the buffers of view.tx[0, ntx) and view.rx[0, nrx) are disjoint, as
+ * nic::rx_stage_detail::buffers_disjoint defines it (RX spans: at most
+ * buffer_length bytes inside the image; TX spans: the whole buffer; an
+ * overlap among RX spans or between an RX and a TX span is one).  *verdict =
+ * 1 disjoint, 0 not, -1 undecided: the RX spans, in ring order, are not
+ * ascending and apart (the caller then sorts on the host).  Synchronises
+ * `stream`. */
+int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int* verdict, void* stream);
 /* The plan (qp_logic.h plan_packet) of view.tx[0, ntx) and the checksum of
  * every piece over the image mem[0, mem_size): *npieces on return.
  * Synchronises `stream`; refreshes *view (the piece buffers may grow). */

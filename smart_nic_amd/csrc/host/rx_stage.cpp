@@ -946,38 +946,21 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
                                      std::span<const RxDescriptor> rx, RxBatchResult& out, void* stream) {
   using clock = std::chrono::steady_clock;
   if (mem.base == nullptr && mem.size != 0) throw GpuError("process_batch: null host-memory image", NICGPU_ERR_INVALID);
-  // the overlap check runs beside the device resolve's side-effect-free
-  // first steps (descriptor upload, plan, sums, positions), which are dropped
-  // if the buffers do overlap
-  bool disjoint = false;
-  double check_us = 0;
-  auto check_overlap = [&] {
-    const auto t0 = clock::now();
-    disjoint = rx_stage_detail::buffers_disjoint(mem.size, tx, rx);
-    check_us = std::chrono::duration<double, std::micro>(clock::now() - t0).count();
-  };
   // stats are committed only when the whole batch went through
   QueuePairStats st = stats_;
+  int disjoint = -1;  // unknown; the device path checks on the device
+  double check_us = 0;
   bool on_device = false;
-  if (config_.device_resolve && !config_.on_interrupt) {
-    struct Joiner {
-      std::thread th;
-      ~Joiner() {
-        if (th.joinable()) th.join();
-      }
-    } j{std::thread(check_overlap)};
-    auto wait = [&] {
-      if (j.th.joinable()) j.th.join();
-      return disjoint;
-    };
-    on_device = process_on_device(mem, tx, rx, st, out, stream, wait);
-    wait();
-  } else {
-    check_overlap();
-  }
+  if (config_.device_resolve && !config_.on_interrupt)
+    on_device = process_on_device(mem, tx, rx, st, out, stream, disjoint, check_us);
   if (!on_device) {
+    if (disjoint < 0) {
+      const auto t0 = clock::now();
+      disjoint = rx_stage_detail::buffers_disjoint(mem.size, tx, rx) ? 1 : 0;
+      check_us += std::chrono::duration<double, std::micro>(clock::now() - t0).count();
+    }
     GpuBackend dev{*scratch_, mem, config_, stream};
-    rx_stage_detail::run_batch(config_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint ? 1 : 0);
+    rx_stage_detail::run_batch(config_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint);
   }
   out.timings.check_us = check_us;
   stats_ = st;
@@ -990,7 +973,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
 // the device; the host moves descriptors up and completions down.
 bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                          std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out,
-                                         void* stream, const std::function<bool()>& disjoint) {
+                                         void* stream, int& disjoint, double& check_us) {
   using namespace rx_stage_detail;
   using clock = std::chrono::steady_clock;
   auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
@@ -1015,6 +998,15 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   check(nicgpu_memcpy_async(v.tx, tx.data(), ntx * sizeof(TxDescriptor), stream), "nicgpu_memcpy_async");
   check(nicgpu_memcpy_async(v.rx, rx.data(), nrx * sizeof(RxDescriptor), stream), "nicgpu_memcpy_async");
   out.timings.copy_us += us_since(t);
+  // overlapping buffers go to the host path before anything is written; a
+  // ring whose RX buffers are not in ascending address order is sorted there
+  t = clock::now();
+  int verdict = -1;
+  check(nicgpu_qp_check(S.qp, mem.size, ntx, nrx, &verdict, stream), "nicgpu_qp_check");
+  if (verdict < 0) verdict = buffers_disjoint(mem.size, tx, rx) ? 1 : 0;
+  disjoint = verdict;
+  check_us += us_since(t);
+  if (!disjoint) return false;
   t = clock::now();
   std::uint64_t np = 0;
   check(nicgpu_qp_plan(S.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &np, &v,
@@ -1027,7 +1019,6 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   check(nicgpu_qp_resolve(S.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, &done, &used, &ds, stream),
         "nicgpu_qp_resolve");
   out.timings.resolve_us += us_since(t);
-  if (!disjoint()) return false;  // nothing written yet: the host path takes the batch
   t = clock::now();
   const QueuePairStats d{ds.tx_packets,         ds.rx_packets,         ds.tx_bytes,
                          ds.rx_bytes,           ds.drops_checksum,     ds.drops_no_rx_desc,

@@ -2632,6 +2632,44 @@ __global__ __launch_bounds__(kQpBlock) void qp_bounds_kernel(const uint16_t* __r
   }
 }
 
+// Overlap check (nicgpu_qp_check), the spans of rx_stage.cpp buffers_disjoint:
+// what an RX descriptor can receive (at most buffer_length bytes inside the
+// image, queue_pair.cpp:397-426) and what a TX descriptor is read from.
+struct QpRxEnd {  // end of RX descriptor j's span; 0 when it receives nothing
+  uint64_t mem_size;
+  __host__ __device__ uint64_t operator()(const nicgpu_rx_descriptor& x) const {
+    if (x.buffer_address >= mem_size || x.buffer_length == 0) return 0;
+    const uint64_t room = mem_size - x.buffer_address;
+    return x.buffer_address + (x.buffer_length < room ? (uint64_t) x.buffer_length : room);
+  }
+};
+
+// end_max = inclusive running max of the RX span ends.  RX spans ascend and are
+// disjoint iff every span starts at or after the running max before it
+// (flag[0] stays 0); a TX span [a, b) then meets an RX span iff the first RX
+// descriptor whose running max passes a (its own end, so it has a span) starts
+// before b (flag[1]).  TX order does not matter.
+__global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t ntx,
+                                                            const nicgpu_rx_descriptor* __restrict__ rx, uint64_t nrx,
+                                                            uint64_t mem_size, const uint64_t* __restrict__ end_max,
+                                                            unsigned long long* flag) {
+  const uint64_t n = ntx > nrx ? ntx : nrx;
+  for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < n; k += (uint64_t) gridDim.x * kQpBlock) {
+    if (k < nrx && k > 0 && QpRxEnd{mem_size}(rx[k]) != 0 && rx[k].buffer_address < end_max[k - 1]) flag[0] = 1;
+    if (k < ntx) {
+      const uint64_t a = tx[k].buffer_address, len = tx[k].length;
+      if (len == 0 || !nicqp::dma_ok(mem_size, a, len)) continue;
+      uint64_t lo = 0, hi = nrx;
+      while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (end_max[mid] <= a) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < nrx && rx[lo].buffer_address < a + len) flag[1] = 1;
+    }
+  }
+}
+
 template <class T>
 int qp_grow(T*& p, size_t& cap, size_t want) {
   if (want <= cap) return NICGPU_OK;
@@ -2666,7 +2704,8 @@ struct nicgpu_qp {
   uint64_t* partials = nullptr;
   uint16_t* sorted_key = nullptr;
   uint32_t *queue_which = nullptr, *queue_start = nullptr, *queue_end = nullptr;
-  size_t c_sk = 0, c_qw = 0;
+  size_t c_sk = 0, c_qw = 0, c_em = 0;
+  uint64_t* end_max = nullptr;  // [nrx] nicgpu_qp_check's running max of RX span ends
   unsigned long long* scal = nullptr;
   uint8_t* tmp = nullptr;
   uint64_t host_scal[4] = {0, 0, 0, 0};
@@ -2740,7 +2779,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
   void* bufs[] = {q->tx, q->rx, q->plans, q->counts, q->base, q->need, q->pos, q->piece_desc, q->piece_csum,
                   q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
                   q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sorted_key, q->queue_which,
-                  q->queue_start, q->queue_end};
+                  q->queue_start, q->queue_end, q->end_max};
   for (void* b : bufs)
     if (b) (void) hipFree(b);
   delete q;
@@ -2749,7 +2788,8 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
 
 int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view) {
   if (!q) return NICGPU_ERR_INVALID;
-  if (ntx > 0xFFFFFFFFull / 64u || nrx > 0xFFFFFFFEull) return NICGPU_ERR_INVALID;  // 32-bit ring positions
+  // 32-bit ring positions; hipcub scans and sorts take int counts
+  if (ntx > 0xFFFFFFFFull / 64u || nrx > 0x7FFFFFFEull) return NICGPU_ERR_INVALID;
   DeviceGuard g(q->device);
   int st = NICGPU_OK;
   const size_t t1 = ntx + 1, r1 = nrx + 1;
@@ -2773,6 +2813,7 @@ int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view
   if (st == NICGPU_OK) st = qp_grow(q->rx_queue, q->c_rq, r1);
   if (st == NICGPU_OK) st = qp_grow(q->sorted_key, q->c_sk, r1);
   if (st == NICGPU_OK) st = qp_grow(q->queue_which, q->c_qw, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->end_max, q->c_em, r1);
   q->cap_tx = ntx;
   q->cap_rx = nrx;
   qp_fill_view(q, view);
@@ -2806,6 +2847,36 @@ int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t n
   *npieces = np;
   qp_fill_view(q, view);
   return st;
+}
+
+int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int* verdict, void* stream) {
+  if (!q || !verdict || ntx > q->cap_tx || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  *verdict = -1;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int st = hip_status(hipMemsetAsync(q->scal, 0, 2 * sizeof(unsigned long long), s));
+  if (st == NICGPU_OK && nrx) {
+    hipcub::TransformInputIterator<uint64_t, QpRxEnd, const nicgpu_rx_descriptor*> ends(q->rx, QpRxEnd{mem_size});
+    size_t tb = 0;
+    if (hipcub::DeviceScan::InclusiveScan(nullptr, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s) != hipSuccess)
+      return NICGPU_ERR_HIP;
+    st = qp_grow(q->tmp, q->c_tmp, tb);
+    if (st == NICGPU_OK)
+      st = hip_status(hipcub::DeviceScan::InclusiveScan(q->tmp, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s));
+  }
+  if (st != NICGPU_OK) return st;
+  const uint64_t n = ntx > nrx ? ntx : nrx;
+  if (n) {
+    hipLaunchKernelGGL(qp_check_kernel, dim3(qp_grid(q, n)), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, q->rx,
+                       (uint64_t) nrx, mem_size, q->end_max, q->scal);
+    st = hip_status(hipGetLastError());
+  }
+  unsigned long long f[2] = {0, 0};
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(f, q->scal, sizeof(f), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  if (st != NICGPU_OK) return st;
+  *verdict = f[0] ? -1 : (f[1] ? 0 : 1);
+  return NICGPU_OK;
 }
 
 int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu, uint16_t queue_id,

@@ -9,7 +9,14 @@
 // descriptors consumed, the memory image, RSS hash / queue per completion, the
 // dispatch lists and the RSS engine's stats.  GPU only.
 //
+// `check` mode: nicgpu_qp_check (the device path's overlap check) against
+// rx_stage_detail::buffers_disjoint on random layouts — ascending rings with
+// and without TX/RX and RX/RX overlaps (touching ends included), shuffled
+// rings, invalid and clipped descriptors.
+//
 //   rx_stage_gpu_fuzz <first_seed> <count>
+//   rx_stage_gpu_fuzz full c3|c5
+//   rx_stage_gpu_fuzz check [count]
 #undef NDEBUG
 #include <cassert>
 #include <cstdio>
@@ -287,10 +294,95 @@ int run_full(const char* wl) {
   return ok ? 0 : 1;
 }
 
+// Device overlap check vs host buffers_disjoint (see the header comment).
+int run_check(std::uint64_t count) {
+  nicgpu_qp* q = nullptr;
+  assert(nicgpu_qp_create(&q, 0) == NICGPU_OK);
+  std::size_t decided = 0, overlaps = 0, undecided = 0, bad = 0;
+  for (std::uint64_t seed = 1; seed <= count; ++seed) {
+    Rng r{seed * 7919 + 11};
+    const int kind = static_cast<int>(r.below(5));
+    const bool big = r.below(10) == 0;
+    const std::size_t nrx = big ? 50000 + r.below(200000) : r.below(400);
+    const std::size_t ntx = big ? 50000 + r.below(200000) : r.below(400);
+    std::vector<RxDescriptor> rx(nrx);
+    std::vector<TxDescriptor> tx(ntx);
+    // RX ring ascending from address 0 with random gaps (0 = touching)
+    std::uint64_t at = 0;
+    for (auto& d : rx) {
+      at += r.below(3) == 0 ? 0 : r.below(64);
+      d.buffer_address = at;
+      d.buffer_length = 1 + r.below(2048);
+      at += d.buffer_length;
+    }
+    const std::uint64_t rx_end = at;
+    for (auto& t : tx) {  // TX buffers after the ring, touching it or not
+      at += r.below(2) ? 0 : r.below(32);
+      t.buffer_address = at;
+      t.length = 1 + r.below(1600);
+      at += t.length;
+    }
+    std::uint64_t mem_size = at + r.below(64);
+    if (kind == 1 && ntx && nrx) {  // some TX buffers overlap an RX buffer (or just touch one)
+      for (int k = 0, m = 1 + static_cast<int>(r.below(3)); k < m; ++k) {
+        const RxDescriptor& d = rx[r.below(static_cast<std::uint32_t>(nrx))];
+        TxDescriptor& t = tx[r.below(static_cast<std::uint32_t>(ntx))];
+        switch (r.below(3)) {
+          case 0: t.buffer_address = d.buffer_address + r.below(d.buffer_length); break;
+          case 1: t.buffer_address = d.buffer_address + d.buffer_length; break;  // touches: no overlap
+          default: t.buffer_address = d.buffer_address > t.length ? d.buffer_address - t.length : 0; break;
+        }
+      }
+    } else if (kind == 2 && nrx > 1) {  // two neighbouring RX buffers overlap
+      const std::size_t j = 1 + r.below(static_cast<std::uint32_t>(nrx - 1));
+      rx[j].buffer_address = rx[j - 1].buffer_address + r.below(rx[j - 1].buffer_length);
+    } else if (kind == 3 && nrx > 1) {  // shuffled ring
+      for (std::size_t j = nrx - 1; j > 0; --j) std::swap(rx[j], rx[r.below(static_cast<std::uint32_t>(j + 1))]);
+    } else if (kind == 4) {  // invalid / clipped descriptors, a smaller image
+      mem_size = rx_end ? rx_end - r.below(static_cast<std::uint32_t>(std::min<std::uint64_t>(rx_end, 4096))) : 0;
+      for (auto& d : rx)
+        if (r.below(8) == 0) d.buffer_length = 0;
+      for (auto& t : tx) {
+        if (r.below(4) == 0) t.buffer_address = r.below(static_cast<std::uint32_t>(mem_size + 1));
+        if (r.below(8) == 0) t.length = 0;
+      }
+    }
+    nicgpu_qp_view v{};
+    assert(nicgpu_qp_reserve(q, ntx, nrx, &v) == NICGPU_OK);
+    if (ntx) assert(nicgpu_memcpy_async(v.tx, tx.data(), ntx * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
+    if (nrx) assert(nicgpu_memcpy_async(v.rx, rx.data(), nrx * sizeof(RxDescriptor), nullptr) == NICGPU_OK);
+    int verdict = 9;
+    assert(nicgpu_qp_check(q, mem_size, ntx, nrx, &verdict, nullptr) == NICGPU_OK);
+    const bool host = rx_stage_detail::buffers_disjoint(mem_size, tx, rx);
+    if (verdict < 0) {
+      ++undecided;
+      if (kind == 0 || kind == 1) {  // an ascending ring apart is always decided
+        std::printf("check seed %llu kind %d: undecided on an ascending ring\n", (unsigned long long) seed, kind);
+        ++bad;
+      }
+    } else {
+      ++decided;
+      overlaps += verdict == 0;
+      if ((verdict == 1) != host) {
+        std::printf("check seed %llu kind %d (ntx %zu nrx %zu): device %d host %d\n", (unsigned long long) seed, kind, ntx,
+                    nrx, verdict, int(host));
+        ++bad;
+      }
+    }
+  }
+  nicgpu_qp_destroy(q);
+  if (bad) return 1;
+  std::printf("rx_stage_gpu_fuzz check: ok (%llu layouts: %zu decided on the device, %zu of them overlapping; %zu "
+              "left to the host sort)\n",
+              (unsigned long long) count, decided, overlaps, undecided);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   assert(gpu_device_count() >= 1);
+  if (argc > 1 && std::strcmp(argv[1], "check") == 0) return run_check(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 400);
   if (argc > 1 && std::strcmp(argv[1], "full") == 0) return run_full(argc > 2 ? argv[2] : "c3");
   const std::uint64_t first = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
   const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 300;

@@ -90,6 +90,20 @@ def test_rx_stage_device_resolve_vs_host_resolve(tmp_path):
     print(r.stdout.strip())
 
 
+@pytest.mark.gpu
+def test_rx_stage_device_overlap_check(tmp_path):
+    """nicgpu_qp_check, the device path's overlap check, against the host's
+    buffers_disjoint on 600 random layouts (ascending rings with and without
+    TX/RX and RX/RX overlaps or touching ends, shuffled rings, invalid and
+    clipped descriptors): equal whenever the device decides, and it decides
+    every ascending ring."""
+    exe = _build(tmp_path, "rx_stage_gpu_fuzz")
+    r = subprocess.run([exe, "check", "600"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "rx_stage_gpu_fuzz check: ok" in r.stdout
+    print(r.stdout.strip())
+
+
 @pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="needs /root/reference (build container)")
 def test_rx_stage_fuzz_vs_reference_queue_pair():
     """2000 random batches: the reference QueuePair (compiled in place from

@@ -105,7 +105,7 @@ int main(int argc, char** argv) {
     rx[j].checksum = ChecksumMode::Layer4;
   }
   void* mem = nullptr;
-  check(nicgpu_malloc(&mem, mem_size), "nicgpu_malloc");
+  check(nicgpu_malloc(&mem, (mem_size + 15) / 16 * 16), "nicgpu_malloc");
   check(nicgpu_memcpy_async(mem, tx_img.data(), tx_bytes, nullptr), "memcpy");
   check(nicgpu_memset_async(static_cast<std::uint8_t*>(mem) + tx_bytes, 0, mem_size - tx_bytes, nullptr), "memset");
   check(nicgpu_stream_synchronize(nullptr), "sync");
