@@ -94,6 +94,15 @@ int nicgpu_memset_async(void* dev_ptr, int value, size_t bytes, void* stream);
 /* Copies in any direction (hipMemcpyDefault), enqueued on `stream`. */
 int nicgpu_memcpy_async(void* dst, const void* src, size_t bytes, void* stream);
 int nicgpu_stream_synchronize(void* stream);
+/* A non-blocking stream on the current device (hipStreamNonBlocking: no
+ * implicit ordering with the null stream), and completion events for ordering
+ * one stream after another (copies beside compute). */
+int nicgpu_stream_create(void** stream);
+int nicgpu_stream_destroy(void* stream);
+int nicgpu_event_create(void** event);
+int nicgpu_event_destroy(void* event);
+int nicgpu_event_record(void* event, void* stream);
+int nicgpu_stream_wait_event(void* stream, void* event);
 
 /* RSS context: the uploaded Toeplitz key (as a nibble lookup table of 32-bit
  * key windows, built on the device) and indirection table, on one device.

@@ -54,6 +54,12 @@ ABI_SYMBOLS = (
     "nicgpu_memset_async",
     "nicgpu_memcpy_async",
     "nicgpu_stream_synchronize",
+    "nicgpu_stream_create",
+    "nicgpu_stream_destroy",
+    "nicgpu_event_create",
+    "nicgpu_event_destroy",
+    "nicgpu_event_record",
+    "nicgpu_stream_wait_event",
     "nicgpu_rss_create",
     "nicgpu_rss_destroy",
     "nicgpu_rss_set_key",
@@ -125,6 +131,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_icrc_batch": (i32, [vp, vp, sz, i32, vp, vp, vp]),
         "nicgpu_tso_segment": (i32, [vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint64, u32, vp, vp, vp]),
         "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),
+        "nicgpu_stream_create": (i32, [ctypes.POINTER(vp)]),
+        "nicgpu_stream_destroy": (i32, [vp]),
+        "nicgpu_event_create": (i32, [ctypes.POINTER(vp)]),
+        "nicgpu_event_destroy": (i32, [vp]),
+        "nicgpu_event_record": (i32, [vp, vp]),
+        "nicgpu_stream_wait_event": (i32, [vp, vp]),
         "nicgpu_tso_checksum": (i32, [vp, vp, vp, vp, vp, sz, vp, vp]),
     }
     for name, (res, args) in sig.items():

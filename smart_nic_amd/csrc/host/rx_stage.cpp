@@ -814,11 +814,59 @@ struct BatchedQueuePair::Scratch {
   rx_stage_detail::BatchScratch host;
   nicgpu_qp* qp = nullptr;  // device resolve context (created on first use, on the current device)
   int qp_device = -1;
+  // side stream of the device resolve (copies beside the main stream's
+  // kernels) and its two ordering events; same device as qp
+  void* side = nullptr;
+  void* ev_tx = nullptr;    // TX descriptors uploaded
+  void* ev_rx = nullptr;    // RX descriptors uploaded
+  void* ev_done = nullptr;  // completions final
   std::vector<std::uint16_t> tail_cs;
-  ~Scratch() {
+  void release() {
     if (qp) (void) nicgpu_qp_destroy(qp);
+    if (ev_tx) (void) nicgpu_event_destroy(ev_tx);
+    if (ev_rx) (void) nicgpu_event_destroy(ev_rx);
+    if (ev_done) (void) nicgpu_event_destroy(ev_done);
+    if (side) (void) nicgpu_stream_destroy(side);
+    qp = nullptr;
+    side = ev_tx = ev_rx = ev_done = nullptr;
   }
+  ~Scratch() { release(); }
 };
+
+namespace {
+
+// A pageable host<->device copy keeps the thread that issues it busy until the
+// copy is staged, so copies meant to run beside the main stream's work are
+// issued from a helper thread; errors come back to the caller at finish().
+class SideJob {
+public:
+  template <class F>
+  void start(F f) {
+    th_ = std::thread([this, f] { f(*this); });
+  }
+  // records the first failure
+  bool ok(int st, const char* what) {
+    if (st != NICGPU_OK && status_ == NICGPU_OK) {
+      status_ = st;
+      what_ = what;
+    }
+    return status_ == NICGPU_OK;
+  }
+  void finish() {
+    if (th_.joinable()) th_.join();
+    check(status_, what_);
+  }
+  ~SideJob() {
+    if (th_.joinable()) th_.join();
+  }
+
+private:
+  std::thread th_;
+  int status_ = NICGPU_OK;
+  const char* what_ = "";
+};
+
+}  // namespace
 
 // The device mirrors (nicgpu.h) of the PODs the device resolve moves.
 static_assert(sizeof(nicgpu_tx_descriptor) == sizeof(TxDescriptor) && sizeof(nicgpu_rx_descriptor) == sizeof(RxDescriptor));
@@ -986,17 +1034,40 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   int dev = 0;
   check(nicgpu_get_device(&dev), "nicgpu_get_device");
   if (S.qp == nullptr || S.qp_device != dev) {
-    if (S.qp) (void) nicgpu_qp_destroy(S.qp);
-    S.qp = nullptr;
+    S.release();
     check(nicgpu_qp_create(&S.qp, dev), "nicgpu_qp_create");
     S.qp_device = dev;
+    check(nicgpu_stream_create(&S.side), "nicgpu_stream_create");
+    check(nicgpu_event_create(&S.ev_tx), "nicgpu_event_create");
+    check(nicgpu_event_create(&S.ev_rx), "nicgpu_event_create");
+    check(nicgpu_event_create(&S.ev_done), "nicgpu_event_create");
   }
   const std::size_t ntx = tx.size(), nrx = rx.size();
   nicgpu_qp_view v{};
   auto t = clock::now();
   check(nicgpu_qp_reserve(S.qp, ntx, nrx, &v), "nicgpu_qp_reserve");
+  // TX descriptors first, alone on the link; then the RX descriptors go up on
+  // the side stream while the plan and piece sums (TX descriptors only) run on
+  // the main one.  (Descriptor arrays in page-locked memory upload without
+  // staging and without holding the issuing thread.)
   check(nicgpu_memcpy_async(v.tx, tx.data(), ntx * sizeof(TxDescriptor), stream), "nicgpu_memcpy_async");
-  check(nicgpu_memcpy_async(v.rx, rx.data(), nrx * sizeof(RxDescriptor), stream), "nicgpu_memcpy_async");
+  check(nicgpu_event_record(S.ev_tx, stream), "nicgpu_event_record");
+  SideJob up;
+  up.start([&](SideJob& j) {
+    j.ok(nicgpu_stream_wait_event(S.side, S.ev_tx), "nicgpu_stream_wait_event") &&
+        j.ok(nicgpu_memcpy_async(v.rx, rx.data(), nrx * sizeof(RxDescriptor), S.side), "nicgpu_memcpy_async") &&
+        j.ok(nicgpu_event_record(S.ev_rx, S.side), "nicgpu_event_record");
+  });
+  out.timings.copy_us += us_since(t);
+  t = clock::now();
+  std::uint64_t np = 0;
+  check(nicgpu_qp_plan(S.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &np, &v,
+                       stream),
+        "nicgpu_qp_plan");
+  out.timings.sums_us += us_since(t);
+  t = clock::now();
+  up.finish();
+  check(nicgpu_stream_wait_event(stream, S.ev_rx), "nicgpu_stream_wait_event");
   out.timings.copy_us += us_since(t);
   // overlapping buffers go to the host path before anything is written; a
   // ring whose RX buffers are not in ascending address order is sorted there
@@ -1007,12 +1078,6 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   disjoint = verdict;
   check_us += us_since(t);
   if (!disjoint) return false;
-  t = clock::now();
-  std::uint64_t np = 0;
-  check(nicgpu_qp_plan(S.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &np, &v,
-                       stream),
-        "nicgpu_qp_plan");
-  out.timings.sums_us += us_since(t);
   t = clock::now();
   std::uint64_t done = 0, used = 0;
   nicgpu_qp_stats ds{};
@@ -1059,6 +1124,21 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   }
   out.tx_processed = ntx;
   out.timings.resolve_us += us_since(t);
+  // the completions are final: they go down on the side stream while the
+  // writes and RSS run on the main one
+  t = clock::now();
+  out.rx_completions.resize(nrx_total);
+  SideJob down;
+  check(nicgpu_event_record(S.ev_done, stream), "nicgpu_event_record");
+  down.start([&](SideJob& j) {
+    j.ok(nicgpu_stream_wait_event(S.side, S.ev_done), "nicgpu_stream_wait_event") &&
+        j.ok(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), S.side),
+             "nicgpu_memcpy_async") &&
+        j.ok(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry), S.side),
+             "nicgpu_memcpy_async") &&
+        j.ok(nicgpu_stream_synchronize(S.side), "nicgpu_stream_synchronize");
+  });
+  out.timings.copy_us += us_since(t);
   // DMA writes: zero-length entries (completions without a write) write nothing
   t = clock::now();
   if (nrx_total)
@@ -1067,7 +1147,6 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
   out.timings.gather_us += us_since(t);
   t = clock::now();
-  out.rx_completions.resize(nrx_total);
   out.rx_hash.resize(nrx_total);
   out.rx_queue.resize(nrx_total);
   if (config_.rss != nullptr) {
@@ -1077,11 +1156,12 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
       config_.rss->select_queue_batch(DevicePacketBatch{mem.base, v.rss_desc, m}, config_.tuple,
                                       RxBatchOutputs{nullptr, v.rss_hash, v.rss_queue}, stream, true);
     check(nicgpu_qp_rss_scatter(S.qp, m, stream), "nicgpu_qp_rss_scatter");
-    check(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, stream), "nicgpu_memcpy_async");
-    check(nicgpu_memcpy_async(out.rx_queue.data(), v.rx_queue, nrx_total * 2, stream), "nicgpu_memcpy_async");
-    // dispatch lists grouped on the device (stable sort by queue)
+    // dispatch lists grouped on the device (stable sort by queue), enqueued
+    // before the downloads (a pageable download holds this thread until done)
     std::uint64_t nq = 0;
     check(nicgpu_qp_group(S.qp, m, &nq, stream), "nicgpu_qp_group");
+    check(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, stream), "nicgpu_memcpy_async");
+    check(nicgpu_memcpy_async(out.rx_queue.data(), v.rx_queue, nrx_total * 2, stream), "nicgpu_memcpy_async");
     std::uint32_t* which = S.h_hash.get<std::uint32_t>(std::max<std::uint64_t>(m, 1) + 2 * nq);
     std::uint32_t* qs = which + m;
     std::uint32_t* qe = qs + nq;
@@ -1097,10 +1177,7 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   }
   out.timings.rss_us += us_since(t);
   t = clock::now();
-  check(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), stream), "nicgpu_memcpy_async");
-  check(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry), stream),
-        "nicgpu_memcpy_async");
-  check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+  down.finish();
   out.timings.copy_us += us_since(t);
   return true;
 }

@@ -1443,8 +1443,8 @@ constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0
 // src/queue_pair.cpp:416-426): dst <- prefix (0/4 B, the inserted VLAN tag)
 // || [src_a, +len_a) || [src_b, +len_b), all inside one memory image.  One
 // wave per write.  Whole destination dwords are assembled from two aligned
-// source dwords with v_alignbyte (4 dwords = 16 B per lane per step, lanes
-// contiguous); the partial dwords at the ends of each part are written with
+// source dwords with v_alignbyte (16 B per lane per step, lanes contiguous,
+// wave_copy16); the partial dwords at the ends of each part are written with
 // byte stores, so writes that share a dword never race.  Pure byte movement:
 // HBM-bound at 2 x bytes.
 struct GatherParams {
@@ -1469,7 +1469,7 @@ __device__ __forceinline__ uint32_t load_dword_clamped(const uint8_t* mem, uint6
 // buffer readable in whole 16-B chunks (include/nicgpu.h).  SUM: returns this
 // lane's share of the written bytes' little-endian halfword sum at absolute
 // destination positions (the convention of the RX chunk sums).
-template <bool CLAMP, bool SUM>
+template <bool CLAMP, bool SUM, int DW = 4>  // DW: whole dwords per lane per step
 __device__ uint32_t wave_copy(uint8_t* dmem, uint64_t dst, const uint8_t* smem, uint64_t smem_size, uint64_t src,
                               uint64_t len, uint32_t lane) {
   uint32_t sum = 0;
@@ -1493,16 +1493,16 @@ __device__ uint32_t wave_copy(uint8_t* dmem, uint64_t dst, const uint8_t* smem, 
   const uint64_t s0 = src + head;  // source of dword A
   const uint32_t sh = (uint32_t) (s0 & 3);
   const uint64_t sa = s0 & ~3ull;
-  for (uint64_t i = (uint64_t) lane * 4; i < nw; i += 256) {
-    uint32_t v[5];
+  for (uint64_t i = (uint64_t) lane * DW; i < nw; i += (uint64_t) kWave * DW) {
+    uint32_t v[DW + 1];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
+    for (int j = 0; j < DW + 1; ++j) {
       const uint64_t a = sa + 4 * (i + j);
       if (CLAMP) v[j] = (i + j <= nw) ? load_dword_clamped(smem, smem_size, a) : 0u;
-      else v[j] = (i + j <= nw && (j < 4 || sh)) ? *reinterpret_cast<const uint32_t*>(smem + a) : 0u;
+      else v[j] = (i + j <= nw && (j < DW || sh)) ? *reinterpret_cast<const uint32_t*>(smem + a) : 0u;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < DW; ++j) {
       if (i + j < nw) {
         const uint32_t o = sh ? __builtin_amdgcn_alignbyte(v[j + 1], v[j], sh) : v[j];
         *reinterpret_cast<uint32_t*>(dmem + A + 4 * (i + j)) = o;
@@ -1513,12 +1513,70 @@ __device__ uint32_t wave_copy(uint8_t* dmem, uint64_t dst, const uint8_t* smem, 
   return sum;
 }
 
+// wave_copy for the gather: each lane moves 16 B per step with one dwordx4
+// load and store (4-B aligned: the sources and destinations of segment writes
+// have any byte alignment; whole dwords are assembled as in wave_copy), the
+// fifth source dword of the byte shift from the next lane.  Sources are
+// clamped to the image, whose end need not be 16-B padded.
+__device__ void wave_copy16(uint8_t* dmem, uint64_t dst, const uint8_t* smem, uint64_t smem_size, uint64_t src,
+                            uint64_t len, uint32_t lane) {
+  if (len == 0) return;
+  const uint64_t d1 = dst + len;
+  const uint64_t A = (dst + 3) & ~3ull;
+  const uint64_t B = d1 & ~3ull;
+  if (A >= B) {
+    if (lane < len) dmem[dst + lane] = smem[src + lane];
+    return;
+  }
+  const uint64_t head = A - dst, tail = d1 - B;
+  if (lane < head) dmem[dst + lane] = smem[src + lane];
+  if (lane >= 8 && lane - 8 < tail) dmem[B + (lane - 8)] = smem[src + (B - dst) + (lane - 8)];
+  const uint64_t nw = (B - A) >> 2;
+  const uint64_t s0 = src + head;
+  const uint32_t sh = (uint32_t) (s0 & 3);
+  const uint64_t sa = s0 & ~3ull;
+  const uint64_t steps = (nw + 255) / 256;  // wave-uniform trip count (the shuffle needs every lane)
+  for (uint64_t k = 0; k < steps; ++k) {
+    const uint64_t i = k * 256 + (uint64_t) lane * 4;
+    const uint64_t a = sa + 4 * i;
+    uint32_t v[5] = {0, 0, 0, 0, 0};
+    if (i < nw) {
+      if (a + 16 <= smem_size) {
+        __builtin_memcpy(v, smem + a, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = load_dword_clamped(smem, smem_size, a + 4 * j);
+      }
+    }
+    const uint32_t up = (uint32_t) __builtin_amdgcn_ds_bpermute((int) (((lane + 1) & 63) << 2), (int) v[0]);
+    if (i < nw && sh) v[4] = (lane < 63 && i + 4 < nw) ? up : (i + 4 <= nw ? load_dword_clamped(smem, smem_size, a + 16) : 0u);
+    if (i < nw) {
+      uint32_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = sh ? __builtin_amdgcn_alignbyte(v[j + 1], v[j], sh) : v[j];
+      uint8_t* d = dmem + A + 4 * i;
+      if (i + 4 <= nw) {
+        __builtin_memcpy(d, o, 16);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (i + j < nw) reinterpret_cast<uint32_t*>(d)[j] = o[j];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void segment_gather_kernel(GatherParams P) {
   const uint32_t lane = lane_id();
   const uint64_t wave = (uint64_t) blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
   const uint64_t nwaves = (uint64_t) gridDim.x * kWavesPerBlock;
+  // the next write's entry is loaded while this one copies (one memory
+  // latency per write instead of two)
+  nicgpu_segment_write next{};
+  if (wave < P.n) next = P.w[wave];
   for (uint64_t e = wave; e < P.n; e += nwaves) {
-    const nicgpu_segment_write w = P.w[e];
+    const nicgpu_segment_write w = next;
+    if (e + nwaves < P.n) next = P.w[e + nwaves];
     const uint64_t plen = w.prefix_len == 4 ? 4 : 0;
     const uint64_t total = plen + w.len_a + w.len_b;
     // entries outside the image are skipped (the host validated them)
@@ -1526,8 +1584,8 @@ __global__ __launch_bounds__(kBlock) void segment_gather_kernel(GatherParams P) 
         w.len_a > P.mem_size - w.src_a || w.src_b > P.mem_size || w.len_b > P.mem_size - w.src_b)
       continue;
     if (lane < plen) P.mem[w.dst + lane] = (uint8_t) (w.prefix >> (8 * lane));
-    wave_copy<true, false>(P.mem, w.dst + plen, P.src, P.mem_size, w.src_a, w.len_a, lane);
-    wave_copy<true, false>(P.mem, w.dst + plen + w.len_a, P.src, P.mem_size, w.src_b, w.len_b, lane);
+    wave_copy16(P.mem, w.dst + plen, P.src, P.mem_size, w.src_a, w.len_a, lane);
+    wave_copy16(P.mem, w.dst + plen + w.len_a, P.src, P.mem_size, w.src_b, w.len_b, lane);
   }
 }
 
@@ -2202,6 +2260,44 @@ int nicgpu_memcpy_async(void* dst, const void* src, size_t bytes, void* stream) 
 
 int nicgpu_stream_synchronize(void* stream) {
   return hip_status(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+}
+
+int nicgpu_stream_create(void** stream) {
+  if (!stream) return NICGPU_ERR_INVALID;
+  *stream = nullptr;
+  hipStream_t s = nullptr;
+  const int st = hip_status(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  if (st == NICGPU_OK) *stream = s;
+  return st;
+}
+
+int nicgpu_stream_destroy(void* stream) {
+  if (!stream) return NICGPU_ERR_INVALID;
+  return hip_status(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+}
+
+int nicgpu_event_create(void** event) {
+  if (!event) return NICGPU_ERR_INVALID;
+  *event = nullptr;
+  hipEvent_t e = nullptr;
+  const int st = hip_status(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (st == NICGPU_OK) *event = e;
+  return st;
+}
+
+int nicgpu_event_destroy(void* event) {
+  if (!event) return NICGPU_ERR_INVALID;
+  return hip_status(hipEventDestroy(static_cast<hipEvent_t>(event)));
+}
+
+int nicgpu_event_record(void* event, void* stream) {
+  if (!event) return NICGPU_ERR_INVALID;
+  return hip_status(hipEventRecord(static_cast<hipEvent_t>(event), static_cast<hipStream_t>(stream)));
+}
+
+int nicgpu_stream_wait_event(void* stream, void* event) {
+  if (!event) return NICGPU_ERR_INVALID;
+  return hip_status(hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(event), 0));
 }
 
 int nicgpu_rss_create(nicgpu_rss_ctx** out, int device) {

@@ -116,6 +116,13 @@ def test_batch_entry_points_validate_before_device_access():
     assert lib.nicgpu_qp_destroy(None) == INV
     assert lib.nicgpu_qp_reserve(None, 1, 1, p) == INV
     assert lib.nicgpu_qp_plan(None, p, 64, 1, 9000, p, p, None) == INV
+    # streams and events: null handles -> INVALID (no device touched)
+    assert lib.nicgpu_stream_create(None) == INV
+    assert lib.nicgpu_stream_destroy(None) == INV
+    assert lib.nicgpu_event_create(None) == INV
+    assert lib.nicgpu_event_destroy(None) == INV
+    assert lib.nicgpu_event_record(None, None) == INV
+    assert lib.nicgpu_stream_wait_event(None, None) == INV
     assert lib.nicgpu_qp_check(None, 64, 1, 1, p, None) == INV
     assert lib.nicgpu_qp_resolve(None, 64, 1, 1, 9000, 0, p, p, p, None) == INV
     assert lib.nicgpu_qp_rss_list(None, 1, p, None) == INV

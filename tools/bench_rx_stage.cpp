@@ -1,8 +1,10 @@
 // bench_rx_stage.cpp — nic::BatchedQueuePair throughput.
 //
-//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host]
+//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host] [pageable|pinned]
 //   (device: BatchedQueuePair's device resolve, the default for disjoint
-//   buffers; host: the host resolve, BatchedQueuePairConfig::device_resolve off)
+//   buffers; host: the host resolve, BatchedQueuePairConfig::device_resolve off;
+//   pinned: the descriptor arrays in page-locked memory, as a descriptor ring
+//   the device DMAs from would be, so they go up without staging)
 //
 // c3: IMIX 64/576/1518 (7:4:1) frames, each balanced so the whole-frame
 //     checksum verifies; RX descriptors with Layer4 checksum offload, 2 KiB
@@ -19,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <span>
 #include <string>
 #include <vector>
 
@@ -122,33 +125,47 @@ int main(int argc, char** argv) {
   cfg.rss = &rss;
   if (argc > 4) cfg.host_threads = static_cast<unsigned>(std::atoi(argv[4]));
   if (argc > 5) cfg.device_resolve = std::string(argv[5]) != "host";
+  const bool pinned = argc > 6 && std::string(argv[6]) == "pinned";
   BatchedQueuePair qp{cfg};
   const DeviceHostMemory dm{static_cast<std::byte*>(mem), mem_size};
+  std::span<const TxDescriptor> txs{tx};
+  std::span<const RxDescriptor> rxs{rx};
+  void *ptx = nullptr, *prx = nullptr;
+  if (pinned) {
+    check(nicgpu_host_alloc(&ptx, n * sizeof(TxDescriptor)), "nicgpu_host_alloc");
+    check(nicgpu_host_alloc(&prx, nrx * sizeof(RxDescriptor)), "nicgpu_host_alloc");
+    std::memcpy(ptx, tx.data(), n * sizeof(TxDescriptor));
+    std::memcpy(prx, rx.data(), nrx * sizeof(RxDescriptor));
+    txs = {static_cast<const TxDescriptor*>(ptx), n};
+    rxs = {static_cast<const RxDescriptor*>(prx), nrx};
+  }
 
-  std::vector<double> tot;
+  std::vector<std::pair<double, RxBatchResult::Timings>> tot;
   RxBatchResult last;
   for (int r = 0; r < reps + 1; ++r) {
     const auto t0 = std::chrono::steady_clock::now();
-    qp.process_batch(dm, tx, rx, last);  // one result object reused across batches
+    qp.process_batch(dm, txs, rxs, last);  // one result object reused across batches
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-    if (r > 0) tot.push_back(us);
+    if (r > 0) tot.emplace_back(us, last.timings);
     const auto& P = last.timings;
     std::fprintf(stderr, "rep %d: %.0f us (%s: check %.0f plan %.0f sums %.0f resolve %.0f gather %.0f rss %.0f copy %.0f)\n", r,
                  us, P.device ? "device" : "host", P.check_us, P.plan_us, P.sums_us, P.resolve_us, P.gather_us, P.rss_us,
                  P.copy_us);
   }
-  std::sort(tot.begin(), tot.end());
-  const double med = tot[tot.size() / 2];
+  std::sort(tot.begin(), tot.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  const double med = tot[tot.size() / 2].first;
   std::size_t ok = 0, frame_bytes = 0;
   for (const auto& c : last.rx_completions) ok += c.status == 0;
   for (auto L : lens) frame_bytes += L;
-  const auto& T = last.timings;
+  const auto& T = tot[tot.size() / 2].second;  // the median batch's phases
   std::printf(
-      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
+      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
       "\"rx_success\": %zu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
       "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f}}\n",
-      wl.c_str(), T.device ? "device" : "host", cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
+      wl.c_str(), T.device ? "device" : "host", pinned ? "pinned" : "pageable", cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
       T.resolve_us, T.gather_us, T.rss_us, T.copy_us);
   nicgpu_free(mem);
+  if (ptx) nicgpu_host_free(ptx);
+  if (prx) nicgpu_host_free(prx);
   return 0;
 }
