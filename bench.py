@@ -190,6 +190,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the same-box read-only streaming ceiling")
+    ap.add_argument("--dist", action="store_true",
+                    help="take the multi-rank path (RCCL init, key/table broadcast, barriers, max-reduce) even at "
+                         "world size 1, to exercise it on a one-GPU box")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02d_pmc_c2.json"))
     args = ap.parse_args()
 
@@ -202,7 +205,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
