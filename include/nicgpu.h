@@ -331,8 +331,10 @@ int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view
  * `stream`. */
 int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int* verdict, void* stream);
 /* The plan (qp_logic.h plan_packet) of view.tx[0, ntx) and the checksum of
- * every piece over the image mem[0, mem_size): *npieces on return.
- * Synchronises `stream`; refreshes *view (the piece buffers may grow). */
+ * every piece over the image mem[0, mem_size): *npieces on return.  Waits for
+ * `stream` once (the piece count sizes the piece buffers); the piece
+ * descriptors and checksums are then enqueued on it.  Refreshes *view (the
+ * piece buffers may grow). */
 int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
                    uint64_t* npieces, nicgpu_qp_view* view, void* stream);
 /* The reference's control flow over view.tx[0, ntx) against view.rx[0, nrx)
@@ -357,8 +359,8 @@ int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t m, void* stream);
 /* The RSS dispatch lists: the m frames of nicgpu_qp_rss_list grouped by queue
  * (a stable sort, so each queue lists its completions in posting order) into
  * view.queue_which, with each queue's range in view.queue_start / queue_end
- * for queues [0, *nq) (*nq = largest queue + 1; 0 when m is 0).
- * Synchronises `stream`. */
+ * for queues [0, *nq) (*nq = largest queue + 1; 0 when m is 0).  Waits for
+ * `stream` once (for *nq); the lists are then enqueued on it. */
 int nicgpu_qp_group(nicgpu_qp* q, size_t m, uint64_t* nq, void* stream);
 
 #ifdef __cplusplus

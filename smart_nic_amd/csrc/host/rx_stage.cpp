@@ -18,9 +18,12 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 
@@ -808,6 +811,92 @@ struct HostBuf {
 // Everything process_batch allocates, kept across batches (grown, never
 // shrunk): the device buffers, pinned staging, and the host-side plan and
 // write lists, so a steady stream of batches takes no page faults.
+namespace {
+
+// The stage's helper thread, started on first use and reused across batches
+// (a thread per job costs tens of µs, a tenth of a small batch).  One job at
+// a time: start() follows the previous job's wait().
+class SideWorker {
+public:
+  ~SideWorker() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+  void start(std::function<void()> f) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+    job_ = std::move(f);
+    done_ = false;
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [this] { return done_; });
+  }
+
+private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [this] { return stop_ || job_ != nullptr; });
+      if (!job_) return;  // stopping, nothing queued
+      std::function<void()> f = std::move(job_);
+      job_ = nullptr;
+      lk.unlock();
+      f();
+      lk.lock();
+      done_ = true;
+      cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::thread th_;
+  std::function<void()> job_;
+  bool done_ = true, stop_ = false;
+};
+
+// A pageable host<->device copy keeps the thread that issues it busy until the
+// copy is staged, so copies meant to run beside the main stream's work are
+// issued from the helper thread; errors come back to the caller at finish().
+class SideJob {
+public:
+  explicit SideJob(SideWorker& w) : w_(w) {}
+  template <class F>
+  void start(F f) {
+    w_.start([this, f] { f(*this); });
+    running_ = true;
+  }
+  // records the first failure
+  bool ok(int st, const char* what) {
+    if (st != NICGPU_OK && status_ == NICGPU_OK) {
+      status_ = st;
+      what_ = what;
+    }
+    return status_ == NICGPU_OK;
+  }
+  void finish() {
+    if (running_) w_.wait();
+    running_ = false;
+    check(status_, what_);
+  }
+  ~SideJob() {
+    if (running_) w_.wait();
+  }
+
+private:
+  SideWorker& w_;
+  bool running_ = false;
+  int status_ = NICGPU_OK;
+  const char* what_ = "";
+};
+
+}  // namespace
+
 struct BatchedQueuePair::Scratch {
   DevBuf piece_desc, piece_csum, writes, rss_desc, rss_hash, rss_queue, copy;
   HostBuf h_desc, h_csum, h_writes, h_rss_desc, h_hash, h_queue;
@@ -821,6 +910,7 @@ struct BatchedQueuePair::Scratch {
   void* ev_rx = nullptr;    // RX descriptors uploaded
   void* ev_done = nullptr;  // completions final
   std::vector<std::uint16_t> tail_cs;
+  SideWorker worker;  // issues the side stream's copies
   void release() {
     if (qp) (void) nicgpu_qp_destroy(qp);
     if (ev_tx) (void) nicgpu_event_destroy(ev_tx);
@@ -832,41 +922,6 @@ struct BatchedQueuePair::Scratch {
   }
   ~Scratch() { release(); }
 };
-
-namespace {
-
-// A pageable host<->device copy keeps the thread that issues it busy until the
-// copy is staged, so copies meant to run beside the main stream's work are
-// issued from a helper thread; errors come back to the caller at finish().
-class SideJob {
-public:
-  template <class F>
-  void start(F f) {
-    th_ = std::thread([this, f] { f(*this); });
-  }
-  // records the first failure
-  bool ok(int st, const char* what) {
-    if (st != NICGPU_OK && status_ == NICGPU_OK) {
-      status_ = st;
-      what_ = what;
-    }
-    return status_ == NICGPU_OK;
-  }
-  void finish() {
-    if (th_.joinable()) th_.join();
-    check(status_, what_);
-  }
-  ~SideJob() {
-    if (th_.joinable()) th_.join();
-  }
-
-private:
-  std::thread th_;
-  int status_ = NICGPU_OK;
-  const char* what_ = "";
-};
-
-}  // namespace
 
 // The device mirrors (nicgpu.h) of the PODs the device resolve moves.
 static_assert(sizeof(nicgpu_tx_descriptor) == sizeof(TxDescriptor) && sizeof(nicgpu_rx_descriptor) == sizeof(RxDescriptor));
@@ -1052,7 +1107,7 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   // staging and without holding the issuing thread.)
   check(nicgpu_memcpy_async(v.tx, tx.data(), ntx * sizeof(TxDescriptor), stream), "nicgpu_memcpy_async");
   check(nicgpu_event_record(S.ev_tx, stream), "nicgpu_event_record");
-  SideJob up;
+  SideJob up{S.worker};
   up.start([&](SideJob& j) {
     j.ok(nicgpu_stream_wait_event(S.side, S.ev_tx), "nicgpu_stream_wait_event") &&
         j.ok(nicgpu_memcpy_async(v.rx, rx.data(), nrx * sizeof(RxDescriptor), S.side), "nicgpu_memcpy_async") &&
@@ -1128,7 +1183,7 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   // writes and RSS run on the main one
   t = clock::now();
   out.rx_completions.resize(nrx_total);
-  SideJob down;
+  SideJob down{S.worker};
   check(nicgpu_event_record(S.ev_done, stream), "nicgpu_event_record");
   down.start([&](SideJob& j) {
     j.ok(nicgpu_stream_wait_event(S.side, S.ev_done), "nicgpu_stream_wait_event") &&
@@ -1144,8 +1199,7 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   if (nrx_total)
     check(nicgpu_segment_gather(reinterpret_cast<std::uint8_t*>(mem.base), mem.size, v.writes, nrx_total, stream),
           "nicgpu_segment_gather");
-  check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
-  out.timings.gather_us += us_since(t);
+  out.timings.gather_us += us_since(t);  // enqueued: the RSS steps wait for it in stream order
   t = clock::now();
   out.rx_hash.resize(nrx_total);
   out.rx_queue.resize(nrx_total);
@@ -1174,6 +1228,7 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   } else {
     std::fill(out.rx_hash.begin(), out.rx_hash.end(), 0u);
     std::fill(out.rx_queue.begin(), out.rx_queue.end(), RxBatchResult::kNoQueue);
+    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");  // the image holds the writes on return
   }
   out.timings.rss_us += us_since(t);
   t = clock::now();

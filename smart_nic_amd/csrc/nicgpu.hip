@@ -2939,7 +2939,6 @@ int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t n
                      q->plans, q->base, q->piece_desc);
   st = hip_status(hipGetLastError());
   if (st == NICGPU_OK && np) st = nicgpu_checksum_batch(mem, q->piece_desc, np, q->piece_csum, stream);
-  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
   *npieces = np;
   qp_fill_view(q, view);
   return st;
@@ -3066,7 +3065,6 @@ int nicgpu_qp_group(nicgpu_qp* q, size_t m, uint64_t* nq, void* stream) {
   hipLaunchKernelGGL(qp_bounds_kernel, dim3(qp_grid(q, m)), dim3(kQpBlock), 0, s, q->sorted_key, (uint64_t) m,
                      q->queue_start, q->queue_end);
   st = hip_status(hipGetLastError());
-  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
   *nq = n;
   return st;
 }
