@@ -46,7 +46,7 @@ constexpr int kHdrChunks = 3;      // 48 B of each packet staged in LDS (the IPv
 constexpr int kHdrBytes = kHdrChunks * 16;
 constexpr uint32_t kHdrStride = kHdrChunks;  // LDS uint4 slots per staged packet (see hdr_slot)
 constexpr uint32_t kRingTileBytes = kWave * 8;  // held results of one tile: hash u32[64] | csum u16[64] | queue u16[64]
-constexpr uint32_t kLdsPerCu = 160u * 1024u;  // gfx950  // held results of one tile: hash u32 | csum u16 | queue u16
+constexpr uint32_t kLdsPerCu = 160u * 1024u;  // gfx950
 constexpr int kLutPos = 2 * NICGPU_MAX_TUPLE;  // nibble positions
 constexpr int kLutWords = kLutPos * 16;
 constexpr int kHistLds = 1024;     // tables up to this size histogram in LDS
@@ -1429,6 +1429,9 @@ const RxVariant kRxVariants[] = {
     // 8-wave blocks measure the same on C2/IMIX/64 B and 12% slower on 9000 B,
     // whose 2500 tiles underfill 512 slots of 8 waves.
     {rx_offload_kernel<2, true, 8, true, false, 1, false, -1, 16, 0, true>, 2, 8, "u2_nt1_w8_c_sc1_ring", false, true},
+    // deeper per-wave batches for lower occupancies (nicgpu_tune_set_bpc)
+    {rx_offload_kernel<4, true, 4, true, false, 1, false, -1, 16, 0, true, true, true>, 4, 4, "u4_w4_c_sc1_ring_xpf", false, true, true},
+    {rx_offload_kernel<4, true, 4, true, false, 1, false, -1, 0, 0, true, true, true>, 4, 4, "u4_w4_c_ring_xpf", false, true, true},
     {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 16, 0, true>, 2, 4, "u2_nt1_w4_c_sc1_ring", false, true},
     {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 0, 0, true>, 2, 4, "u2_nt1_w4_c_ring", false, true},
     {rx_offload_kernel<2, true, 4, true, false, 1, true, -1, 16>, 2, 4, "u2_nt1_w4_c_sc1_defer"},
@@ -2062,16 +2065,27 @@ const DeviceInfo& device_info(int dev) {
   return di;
 }
 
+#ifdef NICGPU_TUNING
+// tuning: at most this many RX blocks per CU (0 = occupancy maximum); the LDS
+// request is padded so the hardware cannot place more (nicgpu_tune_set_bpc)
+uint32_t g_bpc_cap = 0;
+#endif
+
 int rx_blocks_per_cu(int dev, int variant, uint32_t lds) {
   std::lock_guard<std::mutex> lk(g_mu);
   DeviceInfo& di = g_dev[dev & 63];
+#ifdef NICGPU_TUNING
+  auto capped = [](int b) { return g_bpc_cap && b > (int) g_bpc_cap ? (int) g_bpc_cap : b; };
+#else
+  auto capped = [](int b) { return b; };
+#endif
   for (const auto& o : di.occ)
-    if (o.variant == variant && o.lds == lds) return o.blocks;
+    if (o.variant == variant && o.lds == lds) return capped(o.blocks);
   int b = 0;
   const RxVariant& v = kRxVariants[variant];
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, v.kernel, kWave * v.wpb, lds) != hipSuccess || b < 1) b = 1;
   di.occ.push_back({variant, lds, b});
-  return b;
+  return capped(b);
 }
 
 int current_device_info(const DeviceInfo** out) {
@@ -2185,6 +2199,12 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
     lds_launch = rp.lds;
     bpc = rx_blocks_per_cu(dev, variant, lds_launch);
   }
+#ifdef NICGPU_TUNING
+  if (g_bpc_cap) {  // pad the LDS request so no more than the cap fit on a CU
+    const uint32_t floor_lds = kLdsPerCu / (g_bpc_cap + 1u) + 16u;
+    if (lds_launch < floor_lds) lds_launch = floor_lds;
+  }
+#endif
   const uint64_t cap = (uint64_t) di.cus * (uint64_t) bpc;
   const unsigned grid = (unsigned) (want < cap ? want : cap);
   hipLaunchKernelGGL(v.kernel, dim3(grid), dim3(kWave * v.wpb), lds_launch, stream, Pl);
@@ -3214,6 +3234,7 @@ void nicgpu_tune_set_dbg(uint32_t bits) { g_tune_dbg = bits; }
 // wave of the grid; NULL switches it off)
 void nicgpu_tune_set_stamps(unsigned long long* buf) { g_tune_stamps = buf; }
 void nicgpu_tune_set_xpf(uint32_t max_chunks) { g_xpf_chunks = max_chunks; }
+void nicgpu_tune_set_bpc(uint32_t cap) { g_bpc_cap = cap; }
 int nicgpu_tune_rx_offload(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc,
                            size_t n, int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum,
                            uint32_t* out_hash, uint16_t* out_queue, uint64_t* out_hits, void* stream) {

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--modes", default="auto,none", help="timed tuple modes: auto (checksum+RSS), none (checksum only)")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the read-ceiling sweeps (PMC runs)")
     ap.add_argument("--xpf", type=int, default=-1, help="XPF variants: prefetch tiles of at most this many chunks")
+    ap.add_argument("--bpcs", default="0", help="comma list of RX blocks-per-CU caps to A/B per variant "
+                    "(nicgpu_tune_set_bpc; 0 = occupancy maximum)")
     ap.add_argument("--dbg", default="", help="comma list of tuning knob masks to time as extra rows "
                     "(1 no header stage, 2 no hash, 4 no hash/queue/hits stores; outputs wrong)")
     args = ap.parse_args()
@@ -56,8 +58,14 @@ def main():
         tl.nicgpu_tune_set_xpf.argtypes = [u32]
         tl.nicgpu_tune_set_xpf(args.xpf)
     nv = tl.nicgpu_tune_num_variants()
-    names = [tl.nicgpu_tune_variant_name(i).decode() for i in range(nv)]
-    variants = list(range(nv)) if args.variants == "all" else [int(x) for x in args.variants.split(",")]
+    base_names = [tl.nicgpu_tune_variant_name(i).decode() for i in range(nv)]
+    base_variants = list(range(nv)) if args.variants == "all" else [int(x) for x in args.variants.split(",")]
+    bpcs = [int(x) for x in args.bpcs.split(",")]
+    tl.nicgpu_tune_set_bpc.argtypes = [u32]
+    # (variant, blocks-per-CU cap) combinations, named variant[_bpcN]
+    combos = [(v, b) for v in base_variants for b in bpcs]
+    variants = list(range(len(combos)))
+    names = [base_names[v] + (f"_bpc{b}" if b else "") for v, b in combos]
 
     torch.cuda.set_device(0)
     stream = torch.cuda.current_stream()
@@ -102,14 +110,18 @@ def main():
         hits = torch.zeros(128, dtype=torch.int64, device="cuda")
         alg = int(lens.sum()) + 16 * n
 
-        def run(v, mode=sna.TUPLE_AUTO):
+        def run(c, mode=sna.TUPLE_AUTO):
+            v, b = combos[c]
+            tl.nicgpu_tune_set_bpc(b)
             st = tl.nicgpu_tune_rx_offload(v, h, f.data_ptr(), d.data_ptr(), n, mode, 0, 0, cs.data_ptr(),
                                            hs.data_ptr() if mode else None, qs.data_ptr() if mode else None,
                                            hits.data_ptr() if mode else None, sp)
             assert st == 0, st
 
-        # correctness vs variant 0
-        run(0)
+        # correctness vs variant 0 at full occupancy
+        tl.nicgpu_tune_set_bpc(0)
+        assert tl.nicgpu_tune_rx_offload(0, h, f.data_ptr(), d.data_ptr(), n, sna.TUPLE_AUTO, 0, 0, cs.data_ptr(),
+                                         hs.data_ptr(), qs.data_ptr(), hits.data_ptr(), sp) == 0
         torch.cuda.synchronize()
         ref = (cs.clone(), hs.clone(), qs.clone())
         for v in variants:
