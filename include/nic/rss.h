@@ -11,7 +11,9 @@
 //
 // Added: select_queue_batch(), the same classification for every packet of a
 // device-resident batch in one GPU launch (fused with the RX checksum), with
-// the stats updated exactly as the equivalent sequence of select_queue calls.
+// the stats updated exactly as the equivalent sequence of select_queue calls;
+// select_queue_batch_enqueue() / account_batch(), the same split into an
+// enqueue-only launch and a later stats update, for pipelines.
 #pragma once
 
 #include <cstddef>
@@ -72,6 +74,19 @@ public:
                           const RxBatchOutputs& out, void* stream = nullptr,
                           bool update_stats = true) const;
 
+  /// Pipelined form (new): select_queue_batch over the first min(batch.count,
+  /// *count_dev) packets, the count read on the device (a uint64 an earlier
+  /// launch of `stream` wrote), enqueued without waiting.  Per-table-index hits
+  /// are added into `hits_dev` (table size u64, caller-owned); the stats change
+  /// only when the caller hands the downloaded count and hits to
+  /// account_batch().  Throws nic::GpuError.
+  void select_queue_batch_enqueue(const DevicePacketBatch& batch, const std::uint64_t* count_dev,
+                                  const TupleSpec& tuple, const RxBatchOutputs& out,
+                                  std::uint64_t* hits_dev, void* stream = nullptr) const;
+  /// The stats of `count` select_queue calls whose table-index hits are
+  /// `hits` (hashes += count, queue_hits[i] += hits[i] for i < queue_hits.size()).
+  void account_batch(std::uint64_t count, std::span<const std::uint64_t> hits) const;
+
 private:
   RssConfig config_;
   mutable RssStats stats_;
@@ -81,6 +96,7 @@ private:
   [[nodiscard]] std::uint32_t toeplitz_hash(std::span<const std::uint8_t> key,
                                             std::span<const std::uint8_t> data) const;
   void ensure_defaults();
+  void ensure_gpu(void* stream) const;  // device key LUT + table on the current device
 };
 
 }  // namespace nic

@@ -137,6 +137,15 @@ int nicgpu_rx_offload(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const ui
                       uint16_t* out_csum, uint32_t* out_hash, uint16_t* out_queue,
                       uint64_t* out_hits, void* stream);
 
+/* nicgpu_rx_offload over the first min(n_max, *n_dev) packets, the count read
+ * on the device when the launch runs (n_dev: a device uint64 another kernel of
+ * the same stream wrote), so a pipeline need not wait for it.  The launch is
+ * sized for n_max; outputs past the count are left alone. */
+int nicgpu_rx_offload_count(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n_max,
+                            const uint64_t* n_dev, int tuple_mode, uint32_t raw_off, uint32_t raw_len,
+                            uint16_t* out_csum, uint32_t* out_hash, uint16_t* out_queue, uint64_t* out_hits,
+                            void* stream);
+
 /* nicgpu_rx_offload plus L3/L4 checksum verification in the same pass
  * (out_l34[i] = NICGPU_L34_* flags; may be NULL).  The IPv4 header checksum and
  * the TCP/UDP checksum over pseudo-header || segment are those of the
@@ -314,6 +323,7 @@ typedef struct nicgpu_qp_view {
   uint32_t* queue_which;        /* [nrx]  Success completions grouped by queue (nicgpu_qp_group) */
   uint32_t* queue_start;        /* [65536] queue q = queue_which[queue_start[q], queue_end[q]) */
   uint32_t* queue_end;
+  uint64_t* rss_count;          /* [1]    frames listed by nicgpu_qp_rss_list (device scalar) */
 } nicgpu_qp_view;
 
 typedef struct nicgpu_qp nicgpu_qp;
@@ -351,17 +361,22 @@ int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t n
 int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu, uint16_t queue_id,
                       uint64_t* done, uint64_t* rx_used, nicgpu_qp_stats* stats, void* stream);
 /* The frames of view.rxc[0, nrx) delivered with Success, as RSS descriptors
- * (view.rss_desc[0, *m), lengths clipped to NICGPU_MAX_PACKET); view.rx_hash /
- * rx_queue reset to 0 / 0xFFFF.  Synchronises `stream`. */
-int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, uint64_t* m, void* stream);
-/* view.rx_hash / rx_queue of those frames from view.rss_hash / rss_queue. */
-int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t m, void* stream);
-/* The RSS dispatch lists: the m frames of nicgpu_qp_rss_list grouped by queue
- * (a stable sort, so each queue lists its completions in posting order) into
- * view.queue_which, with each queue's range in view.queue_start / queue_end
- * for queues [0, *nq) (*nq = largest queue + 1; 0 when m is 0).  Waits for
- * `stream` once (for *nq); the lists are then enqueued on it. */
-int nicgpu_qp_group(nicgpu_qp* q, size_t m, uint64_t* nq, void* stream);
+ * (view.rss_desc[0, m), lengths clipped to NICGPU_MAX_PACKET), m written to
+ * the device scalar view.rss_count; view.rx_hash / rx_queue reset to 0 /
+ * 0xFFFF.  Enqueued only (no wait): the steps below and
+ * nicgpu_rx_offload_count read m on the device. */
+int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, void* stream);
+/* view.rx_hash / rx_queue of those m frames from view.rss_hash / rss_queue
+ * (nrx: the bound the list was made over).  Enqueued only. */
+int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t nrx, void* stream);
+/* The RSS dispatch lists: the m listed frames grouped by queue (a stable sort,
+ * so each queue lists its completions in posting order) into
+ * view.queue_which[0, m), with each queue's range in view.queue_start /
+ * queue_end for queues [0, nq) (nq <= 65536, at least the largest queue the
+ * indirection table holds + 1; empty queues get start = end = 0).  The sort
+ * runs over the nrx bound with the unlisted entries keyed past every queue.
+ * Enqueued only. */
+int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream);
 
 #ifdef __cplusplus
 }

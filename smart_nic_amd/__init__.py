@@ -80,6 +80,7 @@ ABI_SYMBOLS = (
     "nicgpu_qp_check",
     "nicgpu_qp_resolve",
     "nicgpu_qp_rss_list",
+    "nicgpu_rx_offload_count",
     "nicgpu_qp_rss_scatter",
     "nicgpu_qp_group",
     "nicgpu_icrc_batch",
@@ -116,6 +117,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_rss_set_table_device": (i32, [vp, vp, sz, vp]),
         "nicgpu_rss_info": (i32, [vp, ctypes.POINTER(sz), ctypes.POINTER(sz)]),
         "nicgpu_rx_offload": (i32, [vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp]),
+        "nicgpu_rx_offload_count": (i32, [vp, vp, vp, sz, vp, i32, u32, u32, vp, vp, vp, vp, vp]),
         "nicgpu_rx_offload_ex": (i32, [vp, vp, vp, sz, i32, u32, u32, vp, vp, vp, vp, vp, vp]),
         "nicgpu_segment_gather": (i32, [vp, ctypes.c_uint64, vp, sz, vp]),
         "nicgpu_segment_gather_from": (i32, [vp, vp, ctypes.c_uint64, vp, sz, vp]),
@@ -125,9 +127,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_qp_plan": (i32, [vp, vp, ctypes.c_uint64, sz, ctypes.c_uint64, vp, vp, vp]),
         "nicgpu_qp_check": (i32, [vp, ctypes.c_uint64, sz, sz, vp, vp]),
         "nicgpu_qp_resolve": (i32, [vp, ctypes.c_uint64, sz, sz, ctypes.c_uint64, ctypes.c_uint16, vp, vp, vp, vp]),
-        "nicgpu_qp_rss_list": (i32, [vp, sz, vp, vp]),
+        "nicgpu_qp_rss_list": (i32, [vp, sz, vp]),
         "nicgpu_qp_rss_scatter": (i32, [vp, sz, vp]),
-        "nicgpu_qp_group": (i32, [vp, sz, vp, vp]),
+        "nicgpu_qp_group": (i32, [vp, sz, sz, vp]),
         "nicgpu_icrc_batch": (i32, [vp, vp, sz, i32, vp, vp, vp]),
         "nicgpu_tso_segment": (i32, [vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint64, u32, vp, vp, vp]),
         "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),

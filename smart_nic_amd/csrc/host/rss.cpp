@@ -165,21 +165,8 @@ void RssEngine::select_queue_batch(const DevicePacketBatch& batch, const TupleSp
     throw GpuError("select_queue_batch: indirection table of " + std::to_string(config_.table.size()) +
                        " entries exceeds the GPU limit of NICGPU_MAX_TABLE = " + std::to_string(NICGPU_MAX_TABLE),
                    NICGPU_ERR_INVALID);
-  const std::size_t key_len = config_.key.size() < NICGPU_MAX_KEY ? config_.key.size() : NICGPU_MAX_KEY;
-  int dev = 0;
-  int st = nicgpu_get_device(&dev);
-  if (st != NICGPU_OK) throw_gpu("nicgpu_get_device", st);
-  if (!gpu_ || gpu_->device != dev) {
-    auto g = std::make_shared<detail::RssGpuState>();
-    g->device = dev;
-    st = nicgpu_rss_create(&g->ctx, dev);
-    if (st != NICGPU_OK) throw_gpu("nicgpu_rss_create", st);
-    st = nicgpu_rss_set_key(g->ctx, config_.key.data(), key_len, stream);
-    if (st != NICGPU_OK) throw_gpu("nicgpu_rss_set_key", st);
-    st = nicgpu_rss_set_table(g->ctx, config_.table.data(), config_.table.size(), stream);
-    if (st != NICGPU_OK) throw_gpu("nicgpu_rss_set_table", st);
-    gpu_ = std::move(g);
-  }
+  ensure_gpu(stream);
+  int st = NICGPU_OK;
   std::uint64_t* hits = nullptr;
   const std::size_t tn = config_.table.size();
   if (update_stats) {
@@ -206,10 +193,50 @@ void RssEngine::select_queue_batch(const DevicePacketBatch& batch, const TupleSp
     st = nicgpu_memcpy_async(h.data(), hits, tn * sizeof(std::uint64_t), stream);
     if (st == NICGPU_OK) st = nicgpu_stream_synchronize(stream);
     if (st != NICGPU_OK) throw_gpu("stats readback", st);
-    // identical to `count` sequential select_queue calls (rss.cpp:45, 56-58)
-    stats_.hashes += batch.count;
-    for (std::size_t i = 0; i < tn && i < stats_.queue_hits.size(); ++i) stats_.queue_hits[i] += h[i];
+    account_batch(batch.count, h);
   }
+}
+
+void RssEngine::ensure_gpu(void* stream) const {
+  const std::size_t key_len = config_.key.size() < NICGPU_MAX_KEY ? config_.key.size() : NICGPU_MAX_KEY;
+  int dev = 0;
+  int st = nicgpu_get_device(&dev);
+  if (st != NICGPU_OK) throw_gpu("nicgpu_get_device", st);
+  if (!gpu_ || gpu_->device != dev) {
+    auto g = std::make_shared<detail::RssGpuState>();
+    g->device = dev;
+    st = nicgpu_rss_create(&g->ctx, dev);
+    if (st != NICGPU_OK) throw_gpu("nicgpu_rss_create", st);
+    st = nicgpu_rss_set_key(g->ctx, config_.key.data(), key_len, stream);
+    if (st != NICGPU_OK) throw_gpu("nicgpu_rss_set_key", st);
+    st = nicgpu_rss_set_table(g->ctx, config_.table.data(), config_.table.size(), stream);
+    if (st != NICGPU_OK) throw_gpu("nicgpu_rss_set_table", st);
+    gpu_ = std::move(g);
+  }
+}
+
+void RssEngine::select_queue_batch_enqueue(const DevicePacketBatch& batch, const std::uint64_t* count_dev,
+                                           const TupleSpec& tuple, const RxBatchOutputs& out,
+                                           std::uint64_t* hits_dev, void* stream) const {
+  if (config_.table.size() > NICGPU_MAX_TABLE)
+    throw GpuError("select_queue_batch_enqueue: indirection table of " + std::to_string(config_.table.size()) +
+                       " entries exceeds the GPU limit of NICGPU_MAX_TABLE = " + std::to_string(NICGPU_MAX_TABLE),
+                   NICGPU_ERR_INVALID);
+  if (count_dev == nullptr) throw GpuError("select_queue_batch_enqueue: null device count", NICGPU_ERR_INVALID);
+  if (tuple.mode == TupleMode::None)
+    throw GpuError("select_queue_batch_enqueue: TupleMode::None cannot produce hashes", NICGPU_ERR_INVALID);
+  if (batch.count == 0) return;
+  ensure_gpu(stream);
+  const int st = nicgpu_rx_offload_count(gpu_->ctx, reinterpret_cast<const std::uint8_t*>(batch.frames), batch.desc,
+                                         batch.count, count_dev, static_cast<int>(tuple.mode), tuple.raw_offset,
+                                         tuple.raw_length, out.checksum, out.hash, out.queue, hits_dev, stream);
+  if (st != NICGPU_OK) throw_gpu("nicgpu_rx_offload_count", st);
+}
+
+void RssEngine::account_batch(std::uint64_t count, std::span<const std::uint64_t> hits) const {
+  // identical to `count` sequential select_queue calls (rss.cpp:45, 56-58)
+  stats_.hashes += count;
+  for (std::size_t i = 0; i < hits.size() && i < stats_.queue_hits.size(); ++i) stats_.queue_hits[i] += hits[i];
 }
 
 }  // namespace nic

@@ -21,6 +21,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <functional>
+#include <future>
 #include <limits>
 #include <map>
 #include <mutex>
@@ -899,7 +900,8 @@ private:
 
 struct BatchedQueuePair::Scratch {
   DevBuf piece_desc, piece_csum, writes, rss_desc, rss_hash, rss_queue, copy;
-  HostBuf h_desc, h_csum, h_writes, h_rss_desc, h_hash, h_queue;
+  HostBuf h_desc, h_csum, h_writes, h_rss_desc, h_hash, h_queue, h_meta;
+  DevBuf hits;  // device resolve: per-table-index RSS hits of the batch
   rx_stage_detail::BatchScratch host;
   nicgpu_qp* qp = nullptr;  // device resolve context (created on first use, on the current device)
   int qp_device = -1;
@@ -908,17 +910,19 @@ struct BatchedQueuePair::Scratch {
   void* side = nullptr;
   void* ev_tx = nullptr;    // TX descriptors uploaded
   void* ev_rx = nullptr;    // RX descriptors uploaded
-  void* ev_done = nullptr;  // completions final
+  void* ev_resolved = nullptr;  // completions final
+  void* ev_done = nullptr;      // DMA writes and RSS done
   std::vector<std::uint16_t> tail_cs;
   SideWorker worker;  // issues the side stream's copies
   void release() {
     if (qp) (void) nicgpu_qp_destroy(qp);
     if (ev_tx) (void) nicgpu_event_destroy(ev_tx);
     if (ev_rx) (void) nicgpu_event_destroy(ev_rx);
+    if (ev_resolved) (void) nicgpu_event_destroy(ev_resolved);
     if (ev_done) (void) nicgpu_event_destroy(ev_done);
     if (side) (void) nicgpu_stream_destroy(side);
     qp = nullptr;
-    side = ev_tx = ev_rx = ev_done = nullptr;
+    side = ev_tx = ev_rx = ev_resolved = ev_done = nullptr;
   }
   ~Scratch() { release(); }
 };
@@ -1095,6 +1099,7 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
     check(nicgpu_stream_create(&S.side), "nicgpu_stream_create");
     check(nicgpu_event_create(&S.ev_tx), "nicgpu_event_create");
     check(nicgpu_event_create(&S.ev_rx), "nicgpu_event_create");
+    check(nicgpu_event_create(&S.ev_resolved), "nicgpu_event_create");
     check(nicgpu_event_create(&S.ev_done), "nicgpu_event_create");
   }
   const std::size_t ntx = tx.size(), nrx = rx.size();
@@ -1179,60 +1184,98 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   }
   out.tx_processed = ntx;
   out.timings.resolve_us += us_since(t);
-  // the completions are final: they go down on the side stream while the
-  // writes and RSS run on the main one
+  // Everything from here is enqueued without waiting.  The completions are
+  // final: they go down on the side stream at once, while this thread
+  // enqueues the DMA writes and the RSS list, launch, scatter and dispatch
+  // lists (their sizes read on the device); the RSS results follow them down.
   t = clock::now();
+  const bool rss = config_.rss != nullptr && nrx_total != 0;
+  std::size_t tn = 0, nq = 0;
+  if (rss) {
+    const auto& table = config_.rss->config().table;
+    tn = table.size();
+    for (const std::uint16_t q : table) nq = std::max<std::size_t>(nq, std::size_t{q} + 1);
+  }
   out.rx_completions.resize(nrx_total);
+  out.rx_hash.resize(nrx_total);
+  out.rx_queue.resize(nrx_total);
+  // pinned landing space: [count][hits tn] u64, then [start nq][end nq][which nrx] u32
+  auto* meta = S.h_meta.get<std::uint64_t>(1 + tn);
+  auto* qs = S.h_hash.get<std::uint32_t>(2 * nq + nrx_total + 1);
+  auto* qe = qs + nq;
+  auto* which = qe + nq;
+  meta[0] = 0;
+  auto* hits = rss ? static_cast<std::uint64_t*>(S.hits.get(std::max<std::size_t>(tn, 1) * sizeof(std::uint64_t)))
+                   : nullptr;
+  std::promise<void> rss_recorded;  // ev_done is recorded (the side job must not wait on it before)
+  std::future<void> rss_ready = rss_recorded.get_future();
   SideJob down{S.worker};
-  check(nicgpu_event_record(S.ev_done, stream), "nicgpu_event_record");
+  check(nicgpu_event_record(S.ev_resolved, stream), "nicgpu_event_record");
   down.start([&](SideJob& j) {
-    j.ok(nicgpu_stream_wait_event(S.side, S.ev_done), "nicgpu_stream_wait_event") &&
-        j.ok(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), S.side),
-             "nicgpu_memcpy_async") &&
-        j.ok(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry), S.side),
-             "nicgpu_memcpy_async") &&
-        j.ok(nicgpu_stream_synchronize(S.side), "nicgpu_stream_synchronize");
+    bool ok = j.ok(nicgpu_stream_wait_event(S.side, S.ev_resolved), "nicgpu_stream_wait_event") &&
+              j.ok(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), S.side),
+                   "nicgpu_memcpy_async") &&
+              j.ok(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry), S.side),
+                   "nicgpu_memcpy_async");
+    rss_ready.wait();
+    ok = ok && j.ok(nicgpu_stream_wait_event(S.side, S.ev_done), "nicgpu_stream_wait_event");
+    if (ok && rss)
+      ok = j.ok(nicgpu_memcpy_async(meta, v.rss_count, sizeof(std::uint64_t), S.side), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(meta + 1, hits, tn * sizeof(std::uint64_t), S.side), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(qs, v.queue_start, nq * 4, S.side), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(qe, v.queue_end, nq * 4, S.side), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, S.side), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(out.rx_queue.data(), v.rx_queue, nrx_total * 2, S.side), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_stream_synchronize(S.side), "nicgpu_stream_synchronize") &&
+           j.ok(nicgpu_memcpy_async(which, v.queue_which, meta[0] * 4, S.side), "nicgpu_memcpy_async");
+    ok = ok && j.ok(nicgpu_stream_synchronize(S.side), "nicgpu_stream_synchronize");
   });
+  // the side job must not be left waiting on the promise if this thread throws
+  struct Release {
+    std::promise<void>& p;
+    bool done = false;
+    void operator()() {
+      if (!done) p.set_value();
+      done = true;
+    }
+    ~Release() { (*this)(); }
+  } release{rss_recorded};
   out.timings.copy_us += us_since(t);
-  // DMA writes: zero-length entries (completions without a write) write nothing
   t = clock::now();
   if (nrx_total)
     check(nicgpu_segment_gather(reinterpret_cast<std::uint8_t*>(mem.base), mem.size, v.writes, nrx_total, stream),
           "nicgpu_segment_gather");
-  out.timings.gather_us += us_since(t);  // enqueued: the RSS steps wait for it in stream order
+  out.timings.gather_us += us_since(t);
   t = clock::now();
-  out.rx_hash.resize(nrx_total);
-  out.rx_queue.resize(nrx_total);
-  if (config_.rss != nullptr) {
-    std::uint64_t m = 0;
-    check(nicgpu_qp_rss_list(S.qp, nrx_total, &m, stream), "nicgpu_qp_rss_list");
-    if (m)
-      config_.rss->select_queue_batch(DevicePacketBatch{mem.base, v.rss_desc, m}, config_.tuple,
-                                      RxBatchOutputs{nullptr, v.rss_hash, v.rss_queue}, stream, true);
-    check(nicgpu_qp_rss_scatter(S.qp, m, stream), "nicgpu_qp_rss_scatter");
-    // dispatch lists grouped on the device (stable sort by queue), enqueued
-    // before the downloads (a pageable download holds this thread until done)
-    std::uint64_t nq = 0;
-    check(nicgpu_qp_group(S.qp, m, &nq, stream), "nicgpu_qp_group");
-    check(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, stream), "nicgpu_memcpy_async");
-    check(nicgpu_memcpy_async(out.rx_queue.data(), v.rx_queue, nrx_total * 2, stream), "nicgpu_memcpy_async");
-    std::uint32_t* which = S.h_hash.get<std::uint32_t>(std::max<std::uint64_t>(m, 1) + 2 * nq);
-    std::uint32_t* qs = which + m;
-    std::uint32_t* qe = qs + nq;
-    check(nicgpu_memcpy_async(which, v.queue_which, m * 4, stream), "nicgpu_memcpy_async");
-    check(nicgpu_memcpy_async(qs, v.queue_start, nq * 4, stream), "nicgpu_memcpy_async");
-    check(nicgpu_memcpy_async(qe, v.queue_end, nq * 4, stream), "nicgpu_memcpy_async");
-    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
-    out.queues.resize(nq);
-    for (std::uint64_t q = 0; q < nq; ++q) out.queues[q].assign(which + qs[q], which + qe[q]);
-  } else {
-    std::fill(out.rx_hash.begin(), out.rx_hash.end(), 0u);
-    std::fill(out.rx_queue.begin(), out.rx_queue.end(), RxBatchResult::kNoQueue);
-    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");  // the image holds the writes on return
+  if (rss) {
+    check(nicgpu_qp_rss_list(S.qp, nrx_total, stream), "nicgpu_qp_rss_list");
+    check(nicgpu_memset_async(hits, 0, tn * sizeof(std::uint64_t), stream), "nicgpu_memset_async");
+    config_.rss->select_queue_batch_enqueue(DevicePacketBatch{mem.base, v.rss_desc, nrx_total}, v.rss_count,
+                                            config_.tuple, RxBatchOutputs{nullptr, v.rss_hash, v.rss_queue}, hits,
+                                            stream);
+    check(nicgpu_qp_rss_scatter(S.qp, nrx_total, stream), "nicgpu_qp_rss_scatter");
+    check(nicgpu_qp_group(S.qp, nrx_total, nq, stream), "nicgpu_qp_group");
   }
+  check(nicgpu_event_record(S.ev_done, stream), "nicgpu_event_record");
+  release();
   out.timings.rss_us += us_since(t);
   t = clock::now();
+  if (!rss) {
+    std::fill(out.rx_hash.begin(), out.rx_hash.end(), 0u);
+    std::fill(out.rx_queue.begin(), out.rx_queue.end(), RxBatchResult::kNoQueue);
+  }
+  // the side stream waited for everything this stream did, so the image holds
+  // the writes once the job is done
   down.finish();
+  if (rss) {
+    const std::uint64_t m = meta[0];
+    config_.rss->account_batch(m, std::span<const std::uint64_t>(meta + 1, tn));
+    std::size_t used_q = 0;  // largest queue with frames + 1
+    for (std::size_t q = 0; q < nq; ++q)
+      if (qe[q] > qs[q]) used_q = q + 1;
+    out.queues.resize(used_q);
+    for (std::size_t q = 0; q < used_q; ++q) out.queues[q].assign(which + qs[q], which + qe[q]);
+  }
   out.timings.copy_us += us_since(t);
   return true;
 }

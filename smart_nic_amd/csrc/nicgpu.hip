@@ -156,6 +156,7 @@ struct RxParams {
   uint32_t ring_off; // RING kernels: LDS byte offset of wave 0's result ring (wave w at + w * hold_r * 512)
   uint32_t xpf_chunks;  // XPF kernels: prefetch the next tile's first batch when it has at most this many chunks
   unsigned long long* stamps;  // tuning builds only: per wave {start, end, XCC_ID, HW_ID} (s_memrealtime, 100 MHz)
+  const unsigned long long* n_dev;  // batch size read on the device (min(n, *n_dev)); null: n
 };
 
 // s_waitcnt immediate for vmcnt(0) alone (gfx9 encoding: expcnt 7, lgkmcnt 15).
@@ -989,18 +990,21 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   // Otherwise tile k*W + g (round robin).
   const uint64_t nwaves = (uint64_t) gridDim.x * WPB;
   const uint64_t gw_hw = (uint64_t) blockIdx.x * WPB + w;
+  // packets in this launch: n, or a count another kernel left on the device
+  // (the grid is sized for n; waves past the count have no tile)
+  const uint64_t n_all = P.n_dev ? (*P.n_dev < P.n ? (uint64_t) *P.n_dev : P.n) : P.n;
   // tuning: kDbgRotate hands block b the tiles of block b + 1 (does a slow
   // XCD follow its hardware or its data?  Its hardware: profiles/r02_wave_stamps_c2.jsonl)
   const uint64_t gw = dbg_on(P, kDbgRotate) ? (gw_hw + WPB) % nwaves : gw_hw;
   uint64_t end, step;
   uint64_t first;
   if (RANGES) {
-    first = gw * P.n / nwaves;
-    end = (gw + 1) * P.n / nwaves;
+    first = gw * n_all / nwaves;
+    end = (gw + 1) * n_all / nwaves;
     step = kWave;
   } else {
     first = gw * kWave;
-    end = P.n;
+    end = n_all;
     step = nwaves * kWave;
   }
   auto nvalid_of = [&](uint64_t b) __attribute__((always_inline)) -> uint32_t {
@@ -2426,7 +2430,8 @@ unsigned long long* g_tune_stamps = nullptr;  // tools/wave_stamps.py (nicgpu_tu
 #endif
 int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n,
                     int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum, uint32_t* out_hash,
-                    uint16_t* out_queue, uint64_t* out_hits, uint8_t* out_l34, void* stream) {
+                    uint16_t* out_queue, uint64_t* out_hits, uint8_t* out_l34, void* stream,
+                    const uint64_t* n_dev = nullptr) {
   if (tuple_mode != NICGPU_TUPLE_NONE && tuple_mode != NICGPU_TUPLE_AUTO && tuple_mode != NICGPU_TUPLE_RAW)
     return NICGPU_ERR_INVALID;
   if (tuple_mode == NICGPU_TUPLE_RAW && (raw_off > NICGPU_RAW_MAX_END || raw_len > NICGPU_RAW_MAX_END ||
@@ -2458,6 +2463,7 @@ int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frame
   P.out_queue = out_queue;
   P.out_hits = reinterpret_cast<unsigned long long*>(out_hits);
   P.out_l34 = out_l34;
+  P.n_dev = reinterpret_cast<const unsigned long long*>(n_dev);
 #ifdef NICGPU_TUNING
   P.dbg = g_tune_dbg;
   P.stamps = g_tune_stamps;
@@ -2487,6 +2493,15 @@ int nicgpu_rx_offload_ex(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const
                          uint16_t* out_queue, uint64_t* out_hits, uint8_t* out_l34, void* stream) {
   return rx_offload_impl(0, ctx, frames, desc, n, tuple_mode, raw_off, raw_len, out_csum, out_hash, out_queue,
                          out_hits, out_l34, stream);
+}
+
+int nicgpu_rx_offload_count(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n_max,
+                            const uint64_t* n_dev, int tuple_mode, uint32_t raw_off, uint32_t raw_len,
+                            uint16_t* out_csum, uint32_t* out_hash, uint16_t* out_queue, uint64_t* out_hits,
+                            void* stream) {
+  if (!n_dev) return NICGPU_ERR_INVALID;
+  return rx_offload_impl(0, ctx, frames, desc, n_max, tuple_mode, raw_off, raw_len, out_csum, out_hash, out_queue,
+                         out_hits, nullptr, stream, n_dev);
 }
 
 int nicgpu_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n, uint16_t* out_csum, void* stream) {
@@ -2717,8 +2732,13 @@ __global__ __launch_bounds__(kQpBlock) void qp_flag_kernel(const nicgpu_completi
 __global__ __launch_bounds__(kQpBlock) void qp_rss_fill_kernel(const uint32_t* __restrict__ flags,
                                                                const uint32_t* __restrict__ at,
                                                                const nicgpu_segment_write* __restrict__ writes,
-                                                               uint64_t nrx, uint64_t* desc, uint32_t* which) {
-  for (uint64_t j = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; j < nrx; j += (uint64_t) gridDim.x * kQpBlock) {
+                                                               uint64_t nrx, uint64_t* desc, uint32_t* which,
+                                                               unsigned long long* count) {
+  for (uint64_t j = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; j <= nrx; j += (uint64_t) gridDim.x * kQpBlock) {
+    if (j == nrx) {
+      *count = at[nrx];  // the later steps read the count here, in stream order
+      continue;
+    }
     if (!flags[j]) continue;
     const nicgpu_segment_write w = writes[j];
     uint64_t len = (uint64_t) w.prefix_len + w.len_a + w.len_b;
@@ -2730,19 +2750,34 @@ __global__ __launch_bounds__(kQpBlock) void qp_rss_fill_kernel(const uint32_t* _
 
 __global__ __launch_bounds__(kQpBlock) void qp_scatter_kernel(const uint32_t* __restrict__ which,
                                                               const uint32_t* __restrict__ h,
-                                                              const uint16_t* __restrict__ q, uint64_t m,
+                                                              const uint16_t* __restrict__ q,
+                                                              const unsigned long long* __restrict__ count,
                                                               uint32_t* rx_hash, uint16_t* rx_queue) {
+  const uint64_t m = *count;
   for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < m; k += (uint64_t) gridDim.x * kQpBlock) {
     rx_hash[which[k]] = h[k];
     rx_queue[which[k]] = q[k];
   }
 }
 
-// queue range boundaries of the sorted keys
-__global__ __launch_bounds__(kQpBlock) void qp_bounds_kernel(const uint16_t* __restrict__ key, uint64_t m,
-                                                             uint32_t* start, uint32_t* end) {
+// sort keys of the first nrx RSS entries: the queue of the first *count, a
+// key past every queue (0x10000) for the rest, so the sort leaves them last
+__global__ __launch_bounds__(kQpBlock) void qp_keys_kernel(const uint16_t* __restrict__ q,
+                                                           const unsigned long long* __restrict__ count, uint64_t nrx,
+                                                           uint32_t* key) {
+  const uint64_t m = *count;
+  for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < nrx; k += (uint64_t) gridDim.x * kQpBlock)
+    key[k] = k < m ? (uint32_t) q[k] : 0x10000u;
+}
+
+// queue range boundaries of the first *count sorted keys, for queues below nq
+__global__ __launch_bounds__(kQpBlock) void qp_bounds_kernel(const uint32_t* __restrict__ key,
+                                                             const unsigned long long* __restrict__ count,
+                                                             uint64_t nq, uint32_t* start, uint32_t* end) {
+  const uint64_t m = *count;
   for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < m; k += (uint64_t) gridDim.x * kQpBlock) {
-    const uint16_t q = key[k];
+    const uint32_t q = key[k];
+    if (q >= nq) continue;
     if (k == 0 || key[k - 1] != q) start[q] = (uint32_t) k;
     if (k + 1 == m || key[k + 1] != q) end[q] = (uint32_t) (k + 1);
   }
@@ -2818,9 +2853,9 @@ struct nicgpu_qp {
   uint64_t* rss_desc = nullptr;
   uint16_t *rss_queue = nullptr, *rx_queue = nullptr;
   uint64_t* partials = nullptr;
-  uint16_t* sorted_key = nullptr;
+  uint32_t *sort_key = nullptr, *sorted_key = nullptr;
   uint32_t *queue_which = nullptr, *queue_start = nullptr, *queue_end = nullptr;
-  size_t c_sk = 0, c_qw = 0, c_em = 0;
+  size_t c_sk = 0, c_qw = 0, c_em = 0, c_key = 0;
   uint64_t* end_max = nullptr;  // [nrx] nicgpu_qp_check's running max of RX span ends
   unsigned long long* scal = nullptr;
   uint8_t* tmp = nullptr;
@@ -2847,6 +2882,7 @@ void qp_fill_view(const nicgpu_qp* q, nicgpu_qp_view* v) {
   v->queue_which = q->queue_which;
   v->queue_start = q->queue_start;
   v->queue_end = q->queue_end;
+  v->rss_count = reinterpret_cast<uint64_t*>(q->scal + 3);
 }
 
 unsigned qp_grid(const nicgpu_qp* q, uint64_t n) {
@@ -2894,7 +2930,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
   DeviceGuard g(q->device);
   void* bufs[] = {q->tx, q->rx, q->plans, q->counts, q->base, q->need, q->pos, q->piece_desc, q->piece_csum,
                   q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
-                  q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sorted_key, q->queue_which,
+                  q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sort_key, q->sorted_key, q->queue_which,
                   q->queue_start, q->queue_end, q->end_max};
   for (void* b : bufs)
     if (b) (void) hipFree(b);
@@ -2927,6 +2963,7 @@ int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view
   if (st == NICGPU_OK) st = qp_grow(q->rss_queue, q->c_q, r1);
   if (st == NICGPU_OK) st = qp_grow(q->rx_hash, q->c_rh, r1);
   if (st == NICGPU_OK) st = qp_grow(q->rx_queue, q->c_rq, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->sort_key, q->c_key, r1);
   if (st == NICGPU_OK) st = qp_grow(q->sorted_key, q->c_sk, r1);
   if (st == NICGPU_OK) st = qp_grow(q->queue_which, q->c_qw, r1);
   if (st == NICGPU_OK) st = qp_grow(q->end_max, q->c_em, r1);
@@ -3040,8 +3077,8 @@ int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, u
   return NICGPU_OK;
 }
 
-int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, uint64_t* m, void* stream) {
-  if (!q || !m || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, void* stream) {
+  if (!q || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned grid = qp_grid(q, nrx + 1);
@@ -3051,51 +3088,46 @@ int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, uint64_t* m, void* stream) {
   if (st == NICGPU_OK) st = qp_scan(q, q->flags, q->at, nrx + 1, s);
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_rss_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->flags, q->at, q->writes, (uint64_t) nrx,
-                     q->rss_desc, q->which);
-  uint32_t cnt = 0;
-  st = hip_status(hipGetLastError());
-  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&cnt, q->at + nrx, sizeof(cnt), hipMemcpyDeviceToHost, s));
-  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
-  *m = cnt;
-  return st;
+                     q->rss_desc, q->which, q->scal + 3);
+  return hip_status(hipGetLastError());
 }
 
-int nicgpu_qp_group(nicgpu_qp* q, size_t m, uint64_t* nq, void* stream) {
-  if (!q || !nq || m > q->cap_rx) return NICGPU_ERR_INVALID;
-  *nq = 0;
-  if (m == 0) return NICGPU_OK;
+int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream) {
+  if (!q || nrx > q->cap_rx || nq > 65536) return NICGPU_ERR_INVALID;
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  int st = NICGPU_OK;
+  if (nq) {
+    st = hip_status(hipMemsetAsync(q->queue_start, 0, nq * sizeof(uint32_t), s));
+    if (st == NICGPU_OK) st = hip_status(hipMemsetAsync(q->queue_end, 0, nq * sizeof(uint32_t), s));
+  }
+  if (st != NICGPU_OK || nrx == 0) return st;
+  hipLaunchKernelGGL(qp_keys_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->rss_queue, q->scal + 3,
+                     (uint64_t) nrx, q->sort_key);
+  st = hip_status(hipGetLastError());
+  if (st != NICGPU_OK) return st;
+  // stable: each queue keeps its completions in posting order
   size_t tb = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, q->rss_queue, q->sorted_key, q->which, q->queue_which, (int) m, 0,
-                                         16, s) != hipSuccess)
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, q->sort_key, q->sorted_key, q->which, q->queue_which, (int) nrx,
+                                         0, 17, s) != hipSuccess)
     return NICGPU_ERR_HIP;
-  int st = qp_grow(q->tmp, q->c_tmp, tb);
-  if (st != NICGPU_OK) return st;
-  st = hip_status(hipcub::DeviceRadixSort::SortPairs(q->tmp, tb, q->rss_queue, q->sorted_key, q->which, q->queue_which,
-                                                     (int) m, 0, 16, s));
-  uint16_t last = 0;
-  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&last, q->sorted_key + m - 1, sizeof(last), hipMemcpyDeviceToHost, s));
-  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
-  if (st != NICGPU_OK) return st;
-  const uint64_t n = (uint64_t) last + 1;
-  st = hip_status(hipMemsetAsync(q->queue_start, 0, n * sizeof(uint32_t), s));
-  if (st == NICGPU_OK) st = hip_status(hipMemsetAsync(q->queue_end, 0, n * sizeof(uint32_t), s));
-  if (st != NICGPU_OK) return st;
-  hipLaunchKernelGGL(qp_bounds_kernel, dim3(qp_grid(q, m)), dim3(kQpBlock), 0, s, q->sorted_key, (uint64_t) m,
-                     q->queue_start, q->queue_end);
-  st = hip_status(hipGetLastError());
-  *nq = n;
-  return st;
+  st = qp_grow(q->tmp, q->c_tmp, tb);
+  if (st == NICGPU_OK)
+    st = hip_status(hipcub::DeviceRadixSort::SortPairs(q->tmp, tb, q->sort_key, q->sorted_key, q->which,
+                                                       q->queue_which, (int) nrx, 0, 17, s));
+  if (st != NICGPU_OK || nq == 0) return st;
+  hipLaunchKernelGGL(qp_bounds_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->sorted_key, q->scal + 3,
+                     (uint64_t) nq, q->queue_start, q->queue_end);
+  return hip_status(hipGetLastError());
 }
 
-int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t m, void* stream) {
-  if (!q || m > q->cap_rx) return NICGPU_ERR_INVALID;
-  if (m == 0) return NICGPU_OK;
+int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t nrx, void* stream) {
+  if (!q || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  if (nrx == 0) return NICGPU_OK;
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(qp_scatter_kernel, dim3(qp_grid(q, m)), dim3(kQpBlock), 0, s, q->which, q->rss_hash, q->rss_queue,
-                     (uint64_t) m, q->rx_hash, q->rx_queue);
+  hipLaunchKernelGGL(qp_scatter_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->which, q->rss_hash,
+                     q->rss_queue, q->scal + 3, q->rx_hash, q->rx_queue);
   return hip_status(hipGetLastError());
 }
 

@@ -125,11 +125,15 @@ def test_batch_entry_points_validate_before_device_access():
     assert lib.nicgpu_stream_wait_event(None, None) == INV
     assert lib.nicgpu_qp_check(None, 64, 1, 1, p, None) == INV
     assert lib.nicgpu_qp_resolve(None, 64, 1, 1, 9000, 0, p, p, p, None) == INV
-    assert lib.nicgpu_qp_rss_list(None, 1, p, None) == INV
+    assert lib.nicgpu_qp_rss_list(None, 1, None) == INV
     assert lib.nicgpu_qp_rss_scatter(None, 1, None) == INV
-    assert lib.nicgpu_qp_group(None, 1, p, None) == INV
+    assert lib.nicgpu_qp_group(None, 1, 4, None) == INV
     # nicgpu_rx_offload_ex(ctx, frames, desc, n, mode, raw_off, raw_len, csum, hash, queue, hits, l34, stream)
     NONE, AUTO, RAW = sna.TUPLE_NONE, sna.TUPLE_AUTO, sna.TUPLE_RAW
+    # nicgpu_rx_offload_count: a device count is required; then the same checks as nicgpu_rx_offload
+    assert lib.nicgpu_rx_offload_count(None, p, p, 1, None, NONE, 0, 0, p, None, None, None, None) == INV
+    assert lib.nicgpu_rx_offload_count(None, mis, p, 1, p, NONE, 0, 0, p, None, None, None, None) == INV
+    assert lib.nicgpu_rx_offload_count(None, p, p, 1, p, AUTO, 0, 0, p, p, p, None, None) == INV  # RSS without ctx
     assert lib.nicgpu_rx_offload_ex(None, None, None, 0, NONE, 0, 0, None, None, None, None, None, None) == OK
     assert lib.nicgpu_rx_offload_ex(None, None, p, 1, NONE, 0, 0, p, None, None, None, p, None) == INV
     assert lib.nicgpu_rx_offload_ex(None, p, None, 1, NONE, 0, 0, p, None, None, None, p, None) == INV
