@@ -186,16 +186,42 @@ public:
   void process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                      RxBatchResult& out, void* stream = nullptr);
 
+  /// Pipelined form of process_batch for a stream of batches: submit() returns
+  /// once the batch's work is enqueued on `stream` (the descriptors are no
+  /// longer read after it returns), and collect() waits for the oldest
+  /// submitted batch and swaps its results into `out` (false: none pending).
+  /// At most two batches are pending, so batch k's completions come down while
+  /// batch k+1's descriptors go up.  The results, the memory image and the
+  /// statistics equal those of process_batch called in submission order; a
+  /// batch's QueuePair and RSS statistics are added when it is collected.
+  /// Batches that cannot run on the device (overlapping buffers, an interrupt
+  /// callback, device_resolve off) are processed during submit().  Throws
+  /// std::logic_error on a third submit() or a process_batch() while batches
+  /// are pending.
+  void submit(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+              void* stream = nullptr);
+  bool collect(RxBatchResult& out);
+  [[nodiscard]] std::size_t pending() const noexcept;
+
   [[nodiscard]] const QueuePairStats& stats() const noexcept { return stats_; }
   void reset_stats() noexcept { stats_ = QueuePairStats{}; }
   [[nodiscard]] const BatchedQueuePairConfig& config() const noexcept { return config_; }
 
   struct Scratch;  // device, pinned and host buffers reused across batches (grown, never shrunk)
+  struct Slot;     // one batch in flight on the device: its context, events and landing buffers
 
 private:
-  // false (nothing written) when disjoint() says the buffers overlap
-  bool process_on_device(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
-                         QueuePairStats& stats, RxBatchResult& out, void* stream, int& disjoint, double& check_us);
+  // Device resolve of one batch in three steps: front() uploads, plans, checks
+  // and resolves (false, nothing written, when the buffers overlap); back()
+  // enqueues the DMA writes and RSS and starts the downloads into `out`;
+  // finish() waits for them and completes `out`.
+  bool front(Slot& sl, const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+             QueuePairStats& stats, RxBatchResult& out, void* stream, int& disjoint, double& check_us);
+  void back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult& out, void* stream);
+  void finish(Slot& sl, RxBatchResult& out);
+  // the host path (buffers_disjoint unless `disjoint` is known, then run_batch)
+  void on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+               QueuePairStats& stats, RxBatchResult& out, void* stream, int disjoint, double& check_us);
   BatchedQueuePairConfig config_;
   QueuePairStats stats_{};
   std::unique_ptr<Scratch> scratch_;

@@ -25,6 +25,8 @@
 #include <limits>
 #include <map>
 #include <mutex>
+#include <optional>
+#include <stdexcept>
 #include <string>
 #include <thread>
 
@@ -898,31 +900,84 @@ private:
 
 }  // namespace
 
-struct BatchedQueuePair::Scratch {
-  DevBuf piece_desc, piece_csum, writes, rss_desc, rss_hash, rss_queue, copy;
-  HostBuf h_desc, h_csum, h_writes, h_rss_desc, h_hash, h_queue, h_meta;
-  DevBuf hits;  // device resolve: per-table-index RSS hits of the batch
-  rx_stage_detail::BatchScratch host;
-  nicgpu_qp* qp = nullptr;  // device resolve context (created on first use, on the current device)
-  int qp_device = -1;
-  // side stream of the device resolve (copies beside the main stream's
-  // kernels) and its two ordering events; same device as qp
-  void* side = nullptr;
-  void* ev_tx = nullptr;    // TX descriptors uploaded
-  void* ev_rx = nullptr;    // RX descriptors uploaded
+// One batch in flight on the device.  process_batch uses slot 0; submit()
+// alternates between the two, so batch k's buffers stay untouched while its
+// results come down and batch k+1 is planned and resolved in the other.
+struct BatchedQueuePair::Slot {
+  nicgpu_qp* qp = nullptr;   // device resolve context (same device as the Scratch streams)
+  void* ev_tx = nullptr;     // TX descriptors uploaded
+  void* ev_rx = nullptr;     // RX descriptors uploaded
   void* ev_resolved = nullptr;  // completions final
   void* ev_done = nullptr;      // DMA writes and RSS done
-  std::vector<std::uint16_t> tail_cs;
-  SideWorker worker;  // issues the side stream's copies
+  DevBuf hits;               // per-table-index RSS hits of the batch
+  HostBuf h_meta, h_lists;   // pinned landing space of the downloads
+  SideWorker worker;         // issues the downloads
+  // the batch, between front() and finish()
+  nicgpu_qp_view v{};
+  std::size_t ntx = 0, nrx_total = 0, tn = 0, nq = 0;
+  bool rss = false;
+  std::uint64_t* meta = nullptr;  // [count][hits tn]
+  std::uint32_t *qs = nullptr, *qe = nullptr, *which = nullptr;
+  std::optional<SideJob> down;
+  std::promise<void> rss_recorded;  // ev_done is recorded (the download job waits for it)
+  bool rss_released = false;
+  // submit(): where the batch's results land until collect(), and its stats
+  RxBatchResult result;
+  QueuePairStats stats{};
+  bool on_device = false;
+
+  void release_rss() {
+    if (!rss_released) rss_recorded.set_value();
+    rss_released = true;
+  }
+  void wait() {  // the batch's downloads, if any are running (errors dropped)
+    if (down) {
+      release_rss();
+      down.reset();
+    }
+  }
   void release() {
+    wait();
     if (qp) (void) nicgpu_qp_destroy(qp);
-    if (ev_tx) (void) nicgpu_event_destroy(ev_tx);
-    if (ev_rx) (void) nicgpu_event_destroy(ev_rx);
-    if (ev_resolved) (void) nicgpu_event_destroy(ev_resolved);
-    if (ev_done) (void) nicgpu_event_destroy(ev_done);
-    if (side) (void) nicgpu_stream_destroy(side);
+    for (void* e : {ev_tx, ev_rx, ev_resolved, ev_done})
+      if (e) (void) nicgpu_event_destroy(e);
     qp = nullptr;
-    side = ev_tx = ev_rx = ev_resolved = ev_done = nullptr;
+    ev_tx = ev_rx = ev_resolved = ev_done = nullptr;
+  }
+  void create(int dev) {
+    check(nicgpu_qp_create(&qp, dev), "nicgpu_qp_create");
+    for (void** e : {&ev_tx, &ev_rx, &ev_resolved, &ev_done}) check(nicgpu_event_create(e), "nicgpu_event_create");
+  }
+  ~Slot() { release(); }
+};
+
+struct BatchedQueuePair::Scratch {
+  DevBuf piece_desc, piece_csum, writes, rss_desc, rss_hash, rss_queue, copy;
+  HostBuf h_desc, h_csum, h_writes, h_rss_desc, h_hash, h_queue;
+  rx_stage_detail::BatchScratch host;
+  std::vector<std::uint16_t> tail_cs;
+  // device resolve: side streams for uploads beside the plan and downloads
+  // beside the next steps, created with the slots on the current device
+  int device = -1;
+  void* side_up = nullptr;
+  void* side_down = nullptr;
+  SideWorker up_worker;  // issues the RX descriptor uploads
+  Slot slot[2];
+  unsigned head = 0, pending = 0;  // submit(): oldest pending slot, batches pending
+  void release() {
+    for (Slot& sl : slot) sl.release();
+    if (side_up) (void) nicgpu_stream_destroy(side_up);
+    if (side_down) (void) nicgpu_stream_destroy(side_down);
+    side_up = side_down = nullptr;
+    device = -1;
+  }
+  void ensure(int dev) {
+    if (device == dev) return;
+    release();
+    check(nicgpu_stream_create(&side_up), "nicgpu_stream_create");
+    check(nicgpu_stream_create(&side_down), "nicgpu_stream_create");
+    for (Slot& sl : slot) sl.create(dev);
+    device = dev;
   }
   ~Scratch() { release(); }
 };
@@ -1051,36 +1106,88 @@ RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::
 
 void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                      std::span<const RxDescriptor> rx, RxBatchResult& out, void* stream) {
-  using clock = std::chrono::steady_clock;
   if (mem.base == nullptr && mem.size != 0) throw GpuError("process_batch: null host-memory image", NICGPU_ERR_INVALID);
+  if (scratch_->pending) throw std::logic_error("process_batch: collect() the submitted batches first");
   // stats are committed only when the whole batch went through
   QueuePairStats st = stats_;
   int disjoint = -1;  // unknown; the device path checks on the device
   double check_us = 0;
   bool on_device = false;
-  if (config_.device_resolve && !config_.on_interrupt)
-    on_device = process_on_device(mem, tx, rx, st, out, stream, disjoint, check_us);
-  if (!on_device) {
-    if (disjoint < 0) {
-      const auto t0 = clock::now();
-      disjoint = rx_stage_detail::buffers_disjoint(mem.size, tx, rx) ? 1 : 0;
-      check_us += std::chrono::duration<double, std::micro>(clock::now() - t0).count();
+  if (config_.device_resolve && !config_.on_interrupt) {
+    int dev = 0;
+    check(nicgpu_get_device(&dev), "nicgpu_get_device");
+    scratch_->ensure(dev);
+    Slot& sl = scratch_->slot[0];
+    on_device = front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);
+    if (on_device) {
+      back(sl, mem, out, stream);
+      finish(sl, out);
     }
-    GpuBackend dev{*scratch_, mem, config_, stream};
-    rx_stage_detail::run_batch(config_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint);
   }
+  if (!on_device) on_host(mem, tx, rx, st, out, stream, disjoint, check_us);
   out.timings.check_us = check_us;
   stats_ = st;
 }
 
+void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
+                               std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out, void* stream,
+                               int disjoint, double& check_us) {
+  using clock = std::chrono::steady_clock;
+  if (disjoint < 0) {
+    const auto t0 = clock::now();
+    disjoint = rx_stage_detail::buffers_disjoint(mem.size, tx, rx) ? 1 : 0;
+    check_us += std::chrono::duration<double, std::micro>(clock::now() - t0).count();
+  }
+  GpuBackend dev{*scratch_, mem, config_, stream};
+  rx_stage_detail::run_batch(config_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint);
+}
+
+void BatchedQueuePair::submit(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
+                              std::span<const RxDescriptor> rx, void* stream) {
+  if (mem.base == nullptr && mem.size != 0) throw GpuError("submit: null host-memory image", NICGPU_ERR_INVALID);
+  Scratch& S = *scratch_;
+  if (S.pending == 2) throw std::logic_error("submit: two batches pending; collect() one first");
+  int dev = 0;
+  check(nicgpu_get_device(&dev), "nicgpu_get_device");
+  if (S.pending == 0) S.ensure(dev);
+  else if (S.device != dev) throw std::logic_error("submit: batches pending on another device");
+  Slot& sl = S.slot[(S.head + S.pending) % 2];
+  sl.stats = QueuePairStats{};
+  sl.on_device = false;
+  int disjoint = -1;
+  double check_us = 0;
+  if (config_.device_resolve && !config_.on_interrupt) {
+    sl.on_device = front(sl, mem, tx, rx, sl.stats, sl.result, stream, disjoint, check_us);
+    if (sl.on_device) back(sl, mem, sl.result, stream);
+  }
+  if (!sl.on_device) on_host(mem, tx, rx, sl.stats, sl.result, stream, disjoint, check_us);
+  sl.result.timings.check_us = check_us;
+  ++S.pending;
+}
+
+bool BatchedQueuePair::collect(RxBatchResult& out) {
+  Scratch& S = *scratch_;
+  if (S.pending == 0) return false;
+  Slot& sl = S.slot[S.head];
+  // the slot is free again whatever finish() does
+  S.head = (S.head + 1) % 2;
+  --S.pending;
+  if (sl.on_device) finish(sl, sl.result);
+  rx_stage_detail::add_stats(stats_, sl.stats);
+  std::swap(out, sl.result);
+  return true;
+}
+
+std::size_t BatchedQueuePair::pending() const noexcept { return scratch_->pending; }
+
 // Disjoint buffers, no interrupt callback: plan, piece sums and the
 // reference's control flow on the device (nicgpu_qp_*), the part after a
 // descriptor whose RX side ends it early (or where the ring runs short)
-// resolved here in order, then the DMA writes and RSS of the whole batch on
-// the device; the host moves descriptors up and completions down.
-bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
-                                         std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out,
-                                         void* stream, int& disjoint, double& check_us) {
+// resolved here in order.  The host moves descriptors up; back() and finish()
+// do the rest.
+bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
+                             std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out, void* stream,
+                             int& disjoint, double& check_us) {
   using namespace rx_stage_detail;
   using clock = std::chrono::steady_clock;
   auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
@@ -1090,50 +1197,40 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   out.queues.clear();
   out.timings = RxBatchResult::Timings{};
   out.timings.device = true;
-  int dev = 0;
-  check(nicgpu_get_device(&dev), "nicgpu_get_device");
-  if (S.qp == nullptr || S.qp_device != dev) {
-    S.release();
-    check(nicgpu_qp_create(&S.qp, dev), "nicgpu_qp_create");
-    S.qp_device = dev;
-    check(nicgpu_stream_create(&S.side), "nicgpu_stream_create");
-    check(nicgpu_event_create(&S.ev_tx), "nicgpu_event_create");
-    check(nicgpu_event_create(&S.ev_rx), "nicgpu_event_create");
-    check(nicgpu_event_create(&S.ev_resolved), "nicgpu_event_create");
-    check(nicgpu_event_create(&S.ev_done), "nicgpu_event_create");
-  }
   const std::size_t ntx = tx.size(), nrx = rx.size();
-  nicgpu_qp_view v{};
+  nicgpu_qp_view& v = sl.v;
   auto t = clock::now();
-  check(nicgpu_qp_reserve(S.qp, ntx, nrx, &v), "nicgpu_qp_reserve");
-  // TX descriptors first, alone on the link; then the RX descriptors go up on
-  // the side stream while the plan and piece sums (TX descriptors only) run on
-  // the main one.  (Descriptor arrays in page-locked memory upload without
-  // staging and without holding the issuing thread.)
-  check(nicgpu_memcpy_async(v.tx, tx.data(), ntx * sizeof(TxDescriptor), stream), "nicgpu_memcpy_async");
-  check(nicgpu_event_record(S.ev_tx, stream), "nicgpu_event_record");
-  SideJob up{S.worker};
+  check(nicgpu_qp_reserve(sl.qp, ntx, nrx, &v), "nicgpu_qp_reserve");
+  // Both uploads go on the upload stream, so they need not wait behind the
+  // previous batch's DMA writes and RSS on the caller's stream (submit()).
+  // TX descriptors first, alone on the link; then the RX descriptors go up
+  // while the plan and piece sums (TX descriptors only) run on the caller's
+  // stream.  (Descriptor arrays in page-locked memory upload without staging
+  // and without holding the issuing thread.)
+  check(nicgpu_memcpy_async(v.tx, tx.data(), ntx * sizeof(TxDescriptor), S.side_up), "nicgpu_memcpy_async");
+  check(nicgpu_event_record(sl.ev_tx, S.side_up), "nicgpu_event_record");
+  SideJob up{S.up_worker};
   up.start([&](SideJob& j) {
-    j.ok(nicgpu_stream_wait_event(S.side, S.ev_tx), "nicgpu_stream_wait_event") &&
-        j.ok(nicgpu_memcpy_async(v.rx, rx.data(), nrx * sizeof(RxDescriptor), S.side), "nicgpu_memcpy_async") &&
-        j.ok(nicgpu_event_record(S.ev_rx, S.side), "nicgpu_event_record");
+    j.ok(nicgpu_memcpy_async(v.rx, rx.data(), nrx * sizeof(RxDescriptor), S.side_up), "nicgpu_memcpy_async") &&
+        j.ok(nicgpu_event_record(sl.ev_rx, S.side_up), "nicgpu_event_record");
   });
+  check(nicgpu_stream_wait_event(stream, sl.ev_tx), "nicgpu_stream_wait_event");
   out.timings.copy_us += us_since(t);
   t = clock::now();
   std::uint64_t np = 0;
-  check(nicgpu_qp_plan(S.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &np, &v,
+  check(nicgpu_qp_plan(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &np, &v,
                        stream),
         "nicgpu_qp_plan");
   out.timings.sums_us += us_since(t);
   t = clock::now();
   up.finish();
-  check(nicgpu_stream_wait_event(stream, S.ev_rx), "nicgpu_stream_wait_event");
+  check(nicgpu_stream_wait_event(stream, sl.ev_rx), "nicgpu_stream_wait_event");
   out.timings.copy_us += us_since(t);
   // overlapping buffers go to the host path before anything is written; a
   // ring whose RX buffers are not in ascending address order is sorted there
   t = clock::now();
   int verdict = -1;
-  check(nicgpu_qp_check(S.qp, mem.size, ntx, nrx, &verdict, stream), "nicgpu_qp_check");
+  check(nicgpu_qp_check(sl.qp, mem.size, ntx, nrx, &verdict, stream), "nicgpu_qp_check");
   if (verdict < 0) verdict = buffers_disjoint(mem.size, tx, rx) ? 1 : 0;
   disjoint = verdict;
   check_us += us_since(t);
@@ -1141,7 +1238,7 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   t = clock::now();
   std::uint64_t done = 0, used = 0;
   nicgpu_qp_stats ds{};
-  check(nicgpu_qp_resolve(S.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, &done, &used, &ds, stream),
+  check(nicgpu_qp_resolve(sl.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, &done, &used, &ds, stream),
         "nicgpu_qp_resolve");
   out.timings.resolve_us += us_since(t);
   t = clock::now();
@@ -1184,100 +1281,117 @@ bool BatchedQueuePair::process_on_device(const DeviceHostMemory& mem, std::span<
   }
   out.tx_processed = ntx;
   out.timings.resolve_us += us_since(t);
-  // Everything from here is enqueued without waiting.  The completions are
-  // final: they go down on the side stream at once, while this thread
-  // enqueues the DMA writes and the RSS list, launch, scatter and dispatch
-  // lists (their sizes read on the device); the RSS results follow them down.
-  t = clock::now();
-  const bool rss = config_.rss != nullptr && nrx_total != 0;
-  std::size_t tn = 0, nq = 0;
-  if (rss) {
+  sl.ntx = ntx;
+  sl.nrx_total = nrx_total;
+  return true;
+}
+
+// Everything here is enqueued without waiting.  The completions are final:
+// they go down on the side stream at once, while this thread enqueues the DMA
+// writes and the RSS list, launch, scatter and dispatch lists (their sizes
+// read on the device); the RSS results follow them down.
+void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult& out, void* stream) {
+  using clock = std::chrono::steady_clock;
+  auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
+  Scratch& S = *scratch_;
+  const nicgpu_qp_view& v = sl.v;
+  const std::size_t ntx = sl.ntx, nrx_total = sl.nrx_total;
+  auto t = clock::now();
+  sl.rss = config_.rss != nullptr && nrx_total != 0;
+  sl.tn = sl.nq = 0;
+  if (sl.rss) {
     const auto& table = config_.rss->config().table;
-    tn = table.size();
-    for (const std::uint16_t q : table) nq = std::max<std::size_t>(nq, std::size_t{q} + 1);
+    sl.tn = table.size();
+    for (const std::uint16_t q : table) sl.nq = std::max<std::size_t>(sl.nq, std::size_t{q} + 1);
   }
+  const std::size_t tn = sl.tn, nq = sl.nq;
+  const bool rss = sl.rss;
   out.rx_completions.resize(nrx_total);
   out.rx_hash.resize(nrx_total);
   out.rx_queue.resize(nrx_total);
   // pinned landing space: [count][hits tn] u64, then [start nq][end nq][which nrx] u32
-  auto* meta = S.h_meta.get<std::uint64_t>(1 + tn);
-  auto* qs = S.h_hash.get<std::uint32_t>(2 * nq + nrx_total + 1);
-  auto* qe = qs + nq;
-  auto* which = qe + nq;
-  meta[0] = 0;
-  auto* hits = rss ? static_cast<std::uint64_t*>(S.hits.get(std::max<std::size_t>(tn, 1) * sizeof(std::uint64_t)))
-                   : nullptr;
-  std::promise<void> rss_recorded;  // ev_done is recorded (the side job must not wait on it before)
-  std::future<void> rss_ready = rss_recorded.get_future();
-  SideJob down{S.worker};
-  check(nicgpu_event_record(S.ev_resolved, stream), "nicgpu_event_record");
-  down.start([&](SideJob& j) {
-    bool ok = j.ok(nicgpu_stream_wait_event(S.side, S.ev_resolved), "nicgpu_stream_wait_event") &&
-              j.ok(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), S.side),
+  sl.meta = sl.h_meta.get<std::uint64_t>(1 + tn);
+  sl.qs = sl.h_lists.get<std::uint32_t>(2 * nq + nrx_total + 1);
+  sl.qe = sl.qs + nq;
+  sl.which = sl.qe + nq;
+  sl.meta[0] = 0;
+  std::uint64_t* hits =
+      rss ? static_cast<std::uint64_t*>(sl.hits.get(std::max<std::size_t>(tn, 1) * sizeof(std::uint64_t))) : nullptr;
+  sl.rss_recorded = std::promise<void>();
+  sl.rss_released = false;
+  std::shared_future<void> rss_ready = sl.rss_recorded.get_future().share();
+  check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");
+  sl.down.emplace(sl.worker);
+  sl.down->start([&sl, &S, &out, &v, ntx, nrx_total, tn, nq, rss, hits, rss_ready](SideJob& j) {
+    bool ok = j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_resolved), "nicgpu_stream_wait_event") &&
+              j.ok(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), S.side_down),
                    "nicgpu_memcpy_async") &&
-              j.ok(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry), S.side),
+              j.ok(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry),
+                                       S.side_down),
                    "nicgpu_memcpy_async");
     rss_ready.wait();
-    ok = ok && j.ok(nicgpu_stream_wait_event(S.side, S.ev_done), "nicgpu_stream_wait_event");
+    ok = ok && j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_done), "nicgpu_stream_wait_event");
     if (ok && rss)
-      ok = j.ok(nicgpu_memcpy_async(meta, v.rss_count, sizeof(std::uint64_t), S.side), "nicgpu_memcpy_async") &&
-           j.ok(nicgpu_memcpy_async(meta + 1, hits, tn * sizeof(std::uint64_t), S.side), "nicgpu_memcpy_async") &&
-           j.ok(nicgpu_memcpy_async(qs, v.queue_start, nq * 4, S.side), "nicgpu_memcpy_async") &&
-           j.ok(nicgpu_memcpy_async(qe, v.queue_end, nq * 4, S.side), "nicgpu_memcpy_async") &&
-           j.ok(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, S.side), "nicgpu_memcpy_async") &&
-           j.ok(nicgpu_memcpy_async(out.rx_queue.data(), v.rx_queue, nrx_total * 2, S.side), "nicgpu_memcpy_async") &&
-           j.ok(nicgpu_stream_synchronize(S.side), "nicgpu_stream_synchronize") &&
-           j.ok(nicgpu_memcpy_async(which, v.queue_which, meta[0] * 4, S.side), "nicgpu_memcpy_async");
-    ok = ok && j.ok(nicgpu_stream_synchronize(S.side), "nicgpu_stream_synchronize");
+      ok = j.ok(nicgpu_memcpy_async(sl.meta, v.rss_count, sizeof(std::uint64_t), S.side_down), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(sl.meta + 1, hits, tn * sizeof(std::uint64_t), S.side_down), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(sl.qs, v.queue_start, nq * 4, S.side_down), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(sl.qe, v.queue_end, nq * 4, S.side_down), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, S.side_down), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(out.rx_queue.data(), v.rx_queue, nrx_total * 2, S.side_down), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_stream_synchronize(S.side_down), "nicgpu_stream_synchronize") &&
+           j.ok(nicgpu_memcpy_async(sl.which, v.queue_which, sl.meta[0] * 4, S.side_down), "nicgpu_memcpy_async");
+    ok = ok && j.ok(nicgpu_stream_synchronize(S.side_down), "nicgpu_stream_synchronize");
   });
-  // the side job must not be left waiting on the promise if this thread throws
-  struct Release {
-    std::promise<void>& p;
-    bool done = false;
-    void operator()() {
-      if (!done) p.set_value();
-      done = true;
+  try {
+    out.timings.copy_us += us_since(t);
+    t = clock::now();
+    if (nrx_total)
+      check(nicgpu_segment_gather(reinterpret_cast<std::uint8_t*>(mem.base), mem.size, v.writes, nrx_total, stream),
+            "nicgpu_segment_gather");
+    out.timings.gather_us += us_since(t);
+    t = clock::now();
+    if (rss) {
+      check(nicgpu_qp_rss_list(sl.qp, nrx_total, stream), "nicgpu_qp_rss_list");
+      check(nicgpu_memset_async(hits, 0, tn * sizeof(std::uint64_t), stream), "nicgpu_memset_async");
+      config_.rss->select_queue_batch_enqueue(DevicePacketBatch{mem.base, v.rss_desc, nrx_total}, v.rss_count,
+                                              config_.tuple, RxBatchOutputs{nullptr, v.rss_hash, v.rss_queue}, hits,
+                                              stream);
+      check(nicgpu_qp_rss_scatter(sl.qp, nrx_total, stream), "nicgpu_qp_rss_scatter");
+      check(nicgpu_qp_group(sl.qp, nrx_total, nq, stream), "nicgpu_qp_group");
     }
-    ~Release() { (*this)(); }
-  } release{rss_recorded};
-  out.timings.copy_us += us_since(t);
-  t = clock::now();
-  if (nrx_total)
-    check(nicgpu_segment_gather(reinterpret_cast<std::uint8_t*>(mem.base), mem.size, v.writes, nrx_total, stream),
-          "nicgpu_segment_gather");
-  out.timings.gather_us += us_since(t);
-  t = clock::now();
-  if (rss) {
-    check(nicgpu_qp_rss_list(S.qp, nrx_total, stream), "nicgpu_qp_rss_list");
-    check(nicgpu_memset_async(hits, 0, tn * sizeof(std::uint64_t), stream), "nicgpu_memset_async");
-    config_.rss->select_queue_batch_enqueue(DevicePacketBatch{mem.base, v.rss_desc, nrx_total}, v.rss_count,
-                                            config_.tuple, RxBatchOutputs{nullptr, v.rss_hash, v.rss_queue}, hits,
-                                            stream);
-    check(nicgpu_qp_rss_scatter(S.qp, nrx_total, stream), "nicgpu_qp_rss_scatter");
-    check(nicgpu_qp_group(S.qp, nrx_total, nq, stream), "nicgpu_qp_group");
+    check(nicgpu_event_record(sl.ev_done, stream), "nicgpu_event_record");
+  } catch (...) {
+    sl.wait();  // the downloads must not outlive this batch's buffers
+    throw;
   }
-  check(nicgpu_event_record(S.ev_done, stream), "nicgpu_event_record");
-  release();
+  sl.release_rss();
   out.timings.rss_us += us_since(t);
-  t = clock::now();
   if (!rss) {
     std::fill(out.rx_hash.begin(), out.rx_hash.end(), 0u);
     std::fill(out.rx_queue.begin(), out.rx_queue.end(), RxBatchResult::kNoQueue);
   }
-  // the side stream waited for everything this stream did, so the image holds
-  // the writes once the job is done
-  down.finish();
-  if (rss) {
-    const std::uint64_t m = meta[0];
-    config_.rss->account_batch(m, std::span<const std::uint64_t>(meta + 1, tn));
+}
+
+// The downloads waited for everything the batch did on the caller's stream,
+// so the image holds its writes once they are done.
+void BatchedQueuePair::finish(Slot& sl, RxBatchResult& out) {
+  using clock = std::chrono::steady_clock;
+  const auto t = clock::now();
+  struct Reset {  // the slot's job is over whatever finish() throws
+    Slot& sl;
+    ~Reset() { sl.down.reset(); }
+  } reset{sl};
+  sl.down->finish();
+  if (sl.rss) {
+    const std::uint64_t m = sl.meta[0];
+    config_.rss->account_batch(m, std::span<const std::uint64_t>(sl.meta + 1, sl.tn));
     std::size_t used_q = 0;  // largest queue with frames + 1
-    for (std::size_t q = 0; q < nq; ++q)
-      if (qe[q] > qs[q]) used_q = q + 1;
+    for (std::size_t q = 0; q < sl.nq; ++q)
+      if (sl.qe[q] > sl.qs[q]) used_q = q + 1;
     out.queues.resize(used_q);
-    for (std::size_t q = 0; q < used_q; ++q) out.queues[q].assign(which + qs[q], which + qe[q]);
+    for (std::size_t q = 0; q < used_q; ++q) out.queues[q].assign(sl.which + sl.qs[q], sl.which + sl.qe[q]);
   }
-  out.timings.copy_us += us_since(t);
-  return true;
+  out.timings.copy_us += std::chrono::duration<double, std::micro>(clock::now() - t).count();
 }
 
 }  // namespace nic

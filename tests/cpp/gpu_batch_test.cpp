@@ -5,6 +5,8 @@
 // nic::compute_checksum_batch        vs nic::compute_checksum per frame
 // nic::RssEngine::select_queue_batch vs nic::RssEngine::select_queue per tuple,
 //                                       including RssStats after the batch.
+// nic::RssEngine::select_queue_batch_enqueue (device count) + account_batch
+//                                    vs select_queue_batch over that count.
 #undef NDEBUG
 #include <cassert>
 #include <cstdio>
@@ -124,6 +126,48 @@ void test_select_queue_batch(std::mt19937_64& rng, const std::vector<std::uint8_
   assert(gpu_engine.stats().queue_hits.size() == hits_size);
 }
 
+// select_queue_batch_enqueue over a device count + account_batch equals
+// select_queue_batch over the first `count` packets (outputs past the count
+// untouched, stats identical).
+void test_enqueue_count(std::mt19937_64& rng, const std::vector<std::uint8_t>& key, const std::vector<std::uint16_t>& table) {
+  std::vector<std::uint8_t> frames;
+  std::vector<std::uint64_t> desc;
+  make_batch(rng, 3000, frames, desc);
+  const std::size_t n = desc.size();
+  for (const std::size_t count : {std::size_t{0}, std::size_t{1}, std::size_t{63}, std::size_t{1777}, n}) {
+    DevBuf f(frames.size()), d(n * 8), hs(n * 4), qs(n * 2), hs2(n * 4), qs2(n * 2), cnt(8), hits(table.size() * 8);
+    to_dev(f, frames);
+    to_dev(d, desc);
+    to_dev(cnt, std::vector<std::uint64_t>{count});
+    const std::vector<std::uint32_t> fill_h(n, 0xA5A5A5A5u);
+    const std::vector<std::uint16_t> fill_q(n, 0x5A5Au);
+    to_dev(hs, fill_h);
+    to_dev(qs, fill_q);
+    to_dev(hits, std::vector<std::uint64_t>(table.size(), 0));
+    RssEngine a{RssConfig{key, table}}, b{RssConfig{key, table}};
+    a.select_queue_batch_enqueue(DevicePacketBatch{f.as<std::byte>(), d.as<std::uint64_t>(), n}, cnt.as<std::uint64_t>(),
+                                 TupleSpec{TupleMode::Auto, 0, 0},
+                                 RxBatchOutputs{nullptr, hs.as<std::uint32_t>(), qs.as<std::uint16_t>()},
+                                 hits.as<std::uint64_t>());
+    const auto h_hits = from_dev<std::uint64_t>(hits, table.size());
+    a.account_batch(count, h_hits);
+    if (count)
+      b.select_queue_batch(DevicePacketBatch{f.as<std::byte>(), d.as<std::uint64_t>(), count},
+                           TupleSpec{TupleMode::Auto, 0, 0},
+                           RxBatchOutputs{nullptr, hs2.as<std::uint32_t>(), qs2.as<std::uint16_t>()});
+    const auto h = from_dev<std::uint32_t>(hs, n), h2 = from_dev<std::uint32_t>(hs2, n);
+    const auto q = from_dev<std::uint16_t>(qs, n), q2 = from_dev<std::uint16_t>(qs2, n);
+    for (std::size_t i = 0; i < n; ++i) {
+      if (i < count) {
+        assert(h[i] == h2[i] && q[i] == q2[i]);
+      } else {
+        assert(h[i] == 0xA5A5A5A5u && q[i] == 0x5A5Au);
+      }
+    }
+    assert(a.stats().hashes == b.stats().hashes && a.stats().queue_hits == b.stats().queue_hits);
+  }
+}
+
 void test_errors() {
   bool threw = false;
   try {
@@ -146,6 +190,7 @@ int main() {
   std::vector<std::uint16_t> t16(128);
   for (int i = 0; i < 128; ++i) t16[i] = static_cast<std::uint16_t>(i % 16);
   test_select_queue_batch(rng, ms, t16, TupleSpec{TupleMode::Auto, 0, 0});
+  test_enqueue_count(rng, ms, t16);
   test_select_queue_batch(rng, {}, {}, TupleSpec{TupleMode::Auto, 0, 0});         // reference defaults
   test_select_queue_batch(rng, {}, {0, 1, 2, 3, 4, 5, 6}, TupleSpec{TupleMode::Raw, 26, 36});  // key wrap
   std::vector<std::uint16_t> big(3000);

@@ -17,6 +17,7 @@
 //   rx_stage_gpu_fuzz <first_seed> <count>
 //   rx_stage_gpu_fuzz full c3|c5
 //   rx_stage_gpu_fuzz check [count]
+//   rx_stage_gpu_fuzz pipeline [count]   (submit/collect vs process_batch in order)
 #undef NDEBUG
 #include <cassert>
 #include <cstdio>
@@ -294,6 +295,132 @@ int run_full(const char* wl) {
   return ok ? 0 : 1;
 }
 
+// submit()/collect() against process_batch in submission order: sequences
+// of batches over one memory image, where later batches read bytes earlier
+// ones wrote (TX buffers inside the RX ring), some batches overlap their own
+// buffers (host path) and the RX windows wrap the ring.  Results, statistics,
+// the image and the RSS engine's stats must all be equal.
+std::size_t g_pipe_batches = 0, g_pipe_host = 0;
+
+int run_pipeline(std::uint64_t seed) {
+  Rng r{seed * 7727 + 5};
+  const std::size_t tx_region = 1u << 20, ring = 512, buf = 2048;
+  const std::size_t mem_size = tx_region + ring * buf;
+  std::vector<std::uint8_t> image(mem_size, 0);
+  for (std::size_t i = 0; i < tx_region; ++i) image[i] = r.byte();
+  // balanced frames at 2 KiB strides so some TX verifies pass
+  for (std::size_t a = 0; a + 2048 <= tx_region; a += 2048) {
+    std::vector<std::uint8_t> f(image.begin() + a, image.begin() + a + 1518);
+    balance(f, 10);
+    std::memcpy(image.data() + a, f.data(), f.size());
+  }
+  std::vector<std::uint16_t> table(128);
+  for (auto& q : table) q = static_cast<std::uint16_t>(r.below(16));
+  const RssConfig rss_cfg{kMsKey, table};
+  const int nb = 5 + static_cast<int>(r.below(4));
+  std::vector<std::vector<TxDescriptor>> txs(nb);
+  std::vector<std::vector<RxDescriptor>> rxs(nb);
+  std::size_t ring_at = 0;
+  for (int b = 0; b < nb; ++b) {
+    const std::size_t ntx = 1 + r.below(b % 3 == 0 ? 3000 : 300);
+    const std::size_t nrx = std::min<std::size_t>(ring / 2, ntx * (1 + r.below(2)) + r.below(5));
+    // one batch in four may also read its own RX window (overlap: the host path)
+    const bool own = r.below(4) == 0;
+    for (std::size_t i = 0; i < ntx; ++i) {
+      TxDescriptor t{};
+      if (r.below(6) == 0) {  // a frame an earlier batch delivered into the ring
+        const std::size_t slot = own ? r.below(ring) : (ring_at + nrx + r.below(static_cast<std::uint32_t>(ring - nrx))) % ring;
+        t.buffer_address = tx_region + slot * buf;
+        t.length = 64 + r.below(1400);
+      } else {
+        t.buffer_address = r.below(static_cast<std::uint32_t>(tx_region / 2048)) * 2048;
+        t.length = r.below(4) ? 1518 : 1 + r.below(2000);
+      }
+      t.descriptor_index = static_cast<std::uint16_t>(i);
+      t.checksum = static_cast<ChecksumMode>(r.below(3));
+      t.checksum_offload = r.below(4) != 0;
+      if (r.below(8) == 0) {
+        t.tso_enabled = true;
+        t.mss = static_cast<std::uint16_t>(200 + r.below(1200));
+        t.header_length = 54;
+      }
+      if (r.below(8) == 0) {
+        t.vlan_insert = true;
+        t.vlan_tag = static_cast<std::uint16_t>(r.below(65536));
+      }
+      txs[b].push_back(t);
+    }
+    for (std::size_t j = 0; j < nrx; ++j) {
+      RxDescriptor x{};
+      x.buffer_address = tx_region + ((ring_at + j) % ring) * buf;
+      x.buffer_length = static_cast<std::uint32_t>(r.below(10) ? buf : r.below(300));
+      x.descriptor_index = static_cast<std::uint16_t>(j);
+      x.checksum = static_cast<ChecksumMode>(r.below(3));
+      x.checksum_offload = r.below(3) != 0;
+      x.vlan_strip = r.below(4) == 0;
+      rxs[b].push_back(x);
+    }
+    ring_at = (ring_at + nrx) % ring;
+  }
+  BatchedQueuePairConfig cfg;
+  cfg.queue_id = 3;
+  void *d_seq = nullptr, *d_pipe = nullptr;
+  assert(nicgpu_malloc(&d_seq, mem_size + 64) == NICGPU_OK);
+  assert(nicgpu_malloc(&d_pipe, mem_size + 64) == NICGPU_OK);
+  assert(nicgpu_memcpy_async(d_seq, image.data(), mem_size, nullptr) == NICGPU_OK);
+  assert(nicgpu_memcpy_async(d_pipe, image.data(), mem_size, nullptr) == NICGPU_OK);
+  assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+  const DeviceHostMemory m_seq{static_cast<std::byte*>(d_seq), mem_size}, m_pipe{static_cast<std::byte*>(d_pipe), mem_size};
+
+  RssEngine rss_seq{rss_cfg}, rss_pipe{rss_cfg};
+  cfg.rss = &rss_seq;
+  BatchedQueuePair seq{cfg};
+  cfg.rss = &rss_pipe;
+  BatchedQueuePair pipe{cfg};
+  std::vector<RxBatchResult> want(nb), got;
+  for (int b = 0; b < nb; ++b) seq.process_batch(m_seq, txs[b], rxs[b], want[b]);
+  RxBatchResult out;
+  for (int b = 0; b < nb; ++b) {
+    if (pipe.pending() == 2 || (pipe.pending() == 1 && r.below(3) == 0)) {
+      assert(pipe.collect(out));
+      got.push_back(std::move(out));
+      out = RxBatchResult{};
+    }
+    pipe.submit(m_pipe, txs[b], rxs[b]);
+  }
+  while (pipe.collect(out)) {
+    got.push_back(std::move(out));
+    out = RxBatchResult{};
+  }
+  bool ok = static_cast<int>(got.size()) == nb;
+  for (int b = 0; ok && b < nb; ++b) {
+    const RxBatchResult &w = want[b], &g = got[b];
+    ok = w.tx_completions.size() == g.tx_completions.size() && w.rx_completions.size() == g.rx_completions.size() &&
+         w.rx_consumed == g.rx_consumed && w.tx_processed == g.tx_processed && w.rx_hash == g.rx_hash &&
+         w.rx_queue == g.rx_queue && w.queues == g.queues && w.timings.device == g.timings.device;
+    for (std::size_t i = 0; ok && i < w.tx_completions.size(); ++i) ok = same(w.tx_completions[i], g.tx_completions[i]);
+    for (std::size_t i = 0; ok && i < w.rx_completions.size(); ++i) ok = same(w.rx_completions[i], g.rx_completions[i]);
+    if (!ok) std::fprintf(stderr, "pipeline seed %llu: batch %d differs\n", (unsigned long long) seed, b);
+    g_pipe_host += !w.timings.device;
+  }
+  g_pipe_batches += nb;
+  ok = ok && std::memcmp(&seq.stats(), &pipe.stats(), sizeof(QueuePairStats)) == 0;
+  ok = ok && rss_seq.stats().hashes == rss_pipe.stats().hashes && rss_seq.stats().queue_hits == rss_pipe.stats().queue_hits;
+  std::vector<std::uint8_t> a(mem_size), b(mem_size);
+  assert(nicgpu_memcpy_async(a.data(), d_seq, mem_size, nullptr) == NICGPU_OK);
+  assert(nicgpu_memcpy_async(b.data(), d_pipe, mem_size, nullptr) == NICGPU_OK);
+  assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+  ok = ok && a == b;
+  nicgpu_free(d_seq);
+  nicgpu_free(d_pipe);
+  if (!ok) {
+    std::fprintf(stderr, "pipeline seed %llu: pipelined run differs from process_batch in order\n",
+                 (unsigned long long) seed);
+    return 1;
+  }
+  return 0;
+}
+
 // Device overlap check vs host buffers_disjoint (see the header comment).
 int run_check(std::uint64_t count) {
   nicgpu_qp* q = nullptr;
@@ -383,6 +510,15 @@ int run_check(std::uint64_t count) {
 int main(int argc, char** argv) {
   assert(gpu_device_count() >= 1);
   if (argc > 1 && std::strcmp(argv[1], "check") == 0) return run_check(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 400);
+  if (argc > 1 && std::strcmp(argv[1], "pipeline") == 0) {
+    const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 40;
+    int bad = 0;
+    for (std::uint64_t s = 1; s <= count; ++s) bad += run_pipeline(s);
+    if (bad) return 1;
+    std::printf("rx_stage_gpu_fuzz pipeline: ok (%llu sequences, %zu batches, %zu of them on the host path)\n",
+                (unsigned long long) count, g_pipe_batches, g_pipe_host);
+    return 0;
+  }
   if (argc > 1 && std::strcmp(argv[1], "full") == 0) return run_full(argc > 2 ? argv[2] : "c3");
   const std::uint64_t first = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
   const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 300;

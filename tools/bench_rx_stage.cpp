@@ -1,10 +1,12 @@
 // bench_rx_stage.cpp — nic::BatchedQueuePair throughput.
 //
-//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host] [pageable|pinned]
+//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host] [pageable|pinned] [sync|pipelined]
 //   (device: BatchedQueuePair's device resolve, the default for disjoint
 //   buffers; host: the host resolve, BatchedQueuePairConfig::device_resolve off;
 //   pinned: the descriptor arrays in page-locked memory, as a descriptor ring
-//   the device DMAs from would be, so they go up without staging)
+//   the device DMAs from would be, so they go up without staging; pipelined:
+//   submit()/collect() with two batches in flight, reported per batch over
+//   the whole run, against process_batch one batch at a time)
 //
 // c3: IMIX 64/576/1518 (7:4:1) frames, each balanced so the whole-frame
 //     checksum verifies; RX descriptors with Layer4 checksum offload, 2 KiB
@@ -142,7 +144,30 @@ int main(int argc, char** argv) {
 
   std::vector<std::pair<double, RxBatchResult::Timings>> tot;
   RxBatchResult last;
-  for (int r = 0; r < reps + 1; ++r) {
+  const bool pipelined = argc > 7 && std::string(argv[7]) == "pipelined";
+  if (pipelined) {
+    // warm-up (both slots grow their buffers), then `reps` batches with two in
+    // flight: per-batch time = the whole run / reps (the first upload and the
+    // last download included)
+    // (six batches: the three result sets in rotation, the caller's and the
+    // two slots', each take their first-touch page faults here)
+    for (int w = 0; w < 6; ++w) {
+      if (qp.pending() == 2) qp.collect(last);
+      qp.submit(dm, txs, rxs);
+    }
+    while (qp.collect(last)) {
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < reps; ++r) {
+      if (qp.pending() == 2) qp.collect(last);
+      qp.submit(dm, txs, rxs);
+    }
+    while (qp.collect(last)) {
+    }
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / reps;
+    for (int r = 0; r < reps; ++r) tot.emplace_back(us, last.timings);
+  }
+  for (int r = 0; r < (pipelined ? 0 : reps + 1); ++r) {
     const auto t0 = std::chrono::steady_clock::now();
     qp.process_batch(dm, txs, rxs, last);  // one result object reused across batches
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
@@ -159,10 +184,10 @@ int main(int argc, char** argv) {
   for (auto L : lens) frame_bytes += L;
   const auto& T = tot[tot.size() / 2].second;  // the median batch's phases
   std::printf(
-      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
+      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"mode\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
       "\"rx_success\": %zu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
       "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f}}\n",
-      wl.c_str(), T.device ? "device" : "host", pinned ? "pinned" : "pageable", cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
+      wl.c_str(), T.device ? "device" : "host", pinned ? "pinned" : "pageable", pipelined ? "pipelined" : "sync", cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
       T.resolve_us, T.gather_us, T.rss_us, T.copy_us);
   nicgpu_free(mem);
   if (ptx) nicgpu_host_free(ptx);
