@@ -26,7 +26,10 @@
 // materialises the written segments into the RX buffers, and one RX offload
 // launch over the delivered frames (RSS).  The control flow between them —
 // ring consumption, first-failure aborts, statuses, stats — is sequential in
-// the reference and is resolved on the host from those sums, exactly.
+// the reference.  It is resolved exactly from those sums: on the device when
+// the batch's buffers are disjoint and no interrupt callback is set (ring
+// positions by relaxation, nicgpu_qp_*; the host finishes in order after the
+// first packet whose position did not settle), otherwise on the host.
 //
 // Buffers that overlap: the reference writes segment after
 // segment, so of two RX buffers that share bytes the later write wins, and a
@@ -43,9 +46,9 @@
 // Not modelled: address translators / fault injectors of SimpleHostMemory
 // (only the plain bounds check).
 //
-// Failure: process_batch throws nic::GpuError on a HIP failure.  stats() is
-// then unchanged, but the memory image may hold some of the batch's writes and
-// the RSS engine's stats some of its hashes.
+// Failure: process_batch (or submit / collect) throws nic::GpuError on a HIP
+// failure.  stats() is then unchanged, but the memory image may hold some of
+// the batch's writes and the RSS engine's stats some of its hashes.
 #pragma once
 
 #include <cstddef>
