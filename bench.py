@@ -96,10 +96,11 @@ def cpu_rows_baseline(pktgen):
     """The CPU side of the other SURVEY §8 rows, beside the GPU numbers in
     DESIGN.md §5 (bounded samples, this host): C3 IMIX RX through the compiled
     reference (16 threads and 1 core), the reference QueuePair over a C3-style
-    batch for row f1 (1 core; the reference is single-threaded), and — the
+    batch for row f1 and over C5 TSO frames with every segment materialised
+    for row f2 (1 core; the reference is single-threaded), and — the
     reference TUs for these are not buildable here or have no batch entry
     point — the oracle restatement on one core for the C5 TSO segment
-    checksums and the C2 ICRC."""
+    checksums, the L3/L4 verification (row f3) and the C2 ICRC."""
     import ctypes
 
     from oracle import pyoracle as po
@@ -146,9 +147,23 @@ def cpu_rows_baseline(pktgen):
         import json as _json
         import subprocess
 
-        r = subprocess.run([qp_bench, str(1 << 18), "3"], capture_output=True, text=True, timeout=120)
-        if r.returncode == 0 and r.stdout.strip():
-            rows.append(_json.loads(r.stdout.strip().splitlines()[-1]))
+        # row f1 (C3 descriptors), then row f2's materialised segmentation:
+        # the same QueuePair building and writing every TSO segment of C5
+        for args in ([str(1 << 18), "3", "c3"], [str(1 << 14), "3", "c5seg"]):
+            r = subprocess.run([qp_bench, *args], capture_output=True, text=True, timeout=120)
+            if r.returncode == 0 and r.stdout.strip():
+                rows.append(_json.loads(r.stdout.strip().splitlines()[-1]))
+    # row f3: the L3/L4 verification of the restatement (the reference has no
+    # RX-side L3/L4 verify; PacketGenerator's checksums are its definition)
+    n34 = 1 << 15
+    f34, d34, _ = pktgen.make_batch(np.full(n34, 1518), seed=42, proto=6, corrupt_frac=0.0)
+    fl = np.zeros(n34, np.uint8)
+    t0 = time.perf_counter()
+    L.oracle_l34_batch(vp(f34.ctypes.data), vp(d34.ctypes.data), n34, vp(fl.ctypes.data))
+    dt = time.perf_counter() - t0
+    rows.append({"row": "l34_c2", "value": round(n34 / dt / 1e6, 4), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+                 "gbs": round(n34 * 1518 / dt / 1e9, 4),
+                 "sample": f"{n34} x 1518 B TCP frames, IPv4 header + TCP pseudo-header checksum verification"})
     n2 = 1 << 15
     f2, d2, _ = pktgen.make_batch(np.full(n2, 1518), seed=42, proto=6, corrupt_frac=0.0)
     crc = np.zeros(n2, np.uint32)

@@ -318,6 +318,13 @@ size_t oracle_tso_checksum_batch(const uint8_t* frames, const uint64_t* desc, si
   return w;
 }
 
+void oracle_l34_batch(const uint8_t* frames, const uint64_t* desc, size_t n, uint8_t* out_flags) {
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t off = desc[i] & ((1ull << 40) - 1);
+    out_flags[i] = oracle_l34_verify(frames + off, (size_t) (desc[i] >> 40));
+  }
+}
+
 void oracle_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, uint32_t* out_crc) {
   for (size_t i = 0; i < n; ++i) {
     const uint64_t off = desc[i] & ((1ull << 40) - 1);

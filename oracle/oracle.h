@@ -123,6 +123,8 @@ int oracle_icrc_verify(const uint8_t* buf, size_t len);
  * number written. */
 size_t oracle_tso_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n, const uint16_t* hdr_len,
                                  const uint16_t* mss, uint16_t* out_csum);
+/* oracle_l34_verify over a packed batch (the CPU leg of bench.py's f3 row). */
+void oracle_l34_batch(const uint8_t* frames, const uint64_t* desc, size_t n, uint8_t* out_flags);
 void oracle_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, uint32_t* out_crc);
 
 #ifdef __cplusplus

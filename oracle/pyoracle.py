@@ -59,6 +59,8 @@ def lib():
         L.oracle_icrc_calculate.argtypes = [vp, sz]
         L.oracle_tso_checksum_batch.restype = sz
         L.oracle_tso_checksum_batch.argtypes = [vp, vp, sz, vp, vp, vp]
+        L.oracle_l34_batch.restype = None
+        L.oracle_l34_batch.argtypes = [vp, vp, sz, vp]
         L.oracle_icrc_batch.restype = None
         L.oracle_icrc_batch.argtypes = [vp, vp, sz, vp]
         L.oracle_icrc_verify.restype = i32
