@@ -147,9 +147,10 @@ def cpu_rows_baseline(pktgen):
         import json as _json
         import subprocess
 
-        # row f1 (C3 descriptors), then row f2's materialised segmentation:
-        # the same QueuePair building and writing every TSO segment of C5
-        for args in ([str(1 << 18), "3", "c3"], [str(1 << 14), "3", "c5seg"]):
+        # row f1 (C3 descriptors, C5 TSO with RX verify), then row f2's
+        # materialised segmentation: the same QueuePair building and writing
+        # every TSO segment of C5
+        for args in ([str(1 << 18), "3", "c3"], [str(1 << 15), "3", "c5"], [str(1 << 14), "3", "c5seg"]):
             r = subprocess.run([qp_bench, *args], capture_output=True, text=True, timeout=120)
             if r.returncode == 0 and r.stdout.strip():
                 rows.append(_json.loads(r.stdout.strip().splitlines()[-1]))

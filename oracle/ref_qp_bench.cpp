@@ -9,11 +9,13 @@
 //   c5seg  9000 B frames with TSO (H 54, mss 1448 -> 7 segments), RX verify
 //          off, 1600 B RX buffers: every segment built and DMA-written, the
 //          reference's build_segments + handle_rx_segment (row f2,
-//          materialised segmentation).
+//          materialised segmentation);
+//   c5     the same frames with Layer4 RX verify on: random payloads fail the
+//          first segment's checksum and end the packet there (row f1's C5).
 // One thread (the reference is single-threaded).  Prints one JSON line:
 // descriptors per second through push + process_once + poll.
 //
-//   ref_qp_bench [tx_descriptors] [reps] [c3|c5seg]
+//   ref_qp_bench [tx_descriptors] [reps] [c3|c5seg|c5]
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -43,7 +45,8 @@ std::uint16_t csum(const std::uint8_t* p, std::size_t n) {
 int main(int argc, char** argv) {
   const std::size_t n = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : (1u << 18);
   const int reps = argc > 2 ? std::atoi(argv[2]) : 3;
-  const bool seg = argc > 3 && std::strcmp(argv[3], "c5seg") == 0;
+  const bool c5v = argc > 3 && std::strcmp(argv[3], "c5") == 0;  // TSO, RX verify on
+  const bool seg = c5v || (argc > 3 && std::strcmp(argv[3], "c5seg") == 0);
   std::mt19937_64 rng(7);
   std::vector<std::size_t> lens(n);
   for (auto& L : lens) {
@@ -89,8 +92,8 @@ int main(int argc, char** argv) {
     rx[j].buffer_address = tx_bytes + j * rx_buf;
     rx[j].buffer_length = static_cast<std::uint32_t>(rx_buf);
     rx[j].descriptor_index = static_cast<std::uint16_t>(j);
-    rx[j].checksum_offload = !seg;
-    rx[j].checksum = seg ? ChecksumMode::None : ChecksumMode::Layer4;
+    rx[j].checksum_offload = !seg || c5v;
+    rx[j].checksum = seg && !c5v ? ChecksumMode::None : ChecksumMode::Layer4;
   }
   SimpleHostMemory mem{HostMemoryConfig{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false}};
   if (!mem.write(0, std::as_bytes(std::span<const std::uint8_t>(img))).ok()) return 1;
@@ -127,7 +130,13 @@ int main(int argc, char** argv) {
   }
   std::sort(secs.begin(), secs.end());
   const double med = secs[secs.size() / 2];
-  if (seg)
+  if (c5v)
+    std::printf("{\"row\": \"f1_c5\", \"value\": %.4f, \"unit\": \"Mpkt/s\", \"cores\": 1, \"kind\": \"reference\", "
+                "\"gbs\": %.4f, \"rx_success\": %zu, \"sample\": \"%zu x 9000 B TSO frames (H 54, mss 1448) through the "
+                "reference QueuePair::process_once with Layer4 RX verify: each ends at its first segment's checksum; median "
+                "of %d\"}\n",
+                n / med / 1e6, frame_bytes / med / 1e9, ok, n, reps);
+  else if (seg)
     std::printf("{\"row\": \"tso_seg_c5\", \"value\": %.4f, \"unit\": \"Mpkt/s\", \"cores\": 1, \"kind\": \"reference\", "
                 "\"gbs\": %.4f, \"rx_success\": %zu, \"sample\": \"%zu x 9000 B TSO frames (H 54, mss 1448, 7 segments each) "
                 "through the reference QueuePair::process_once (push, process, poll): every segment built and written "

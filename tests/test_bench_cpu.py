@@ -18,14 +18,14 @@ QP_BENCH = os.path.join(ROOT, "oracle", "_ref", "ref_qp_bench")
 
 
 @pytest.mark.skipif(not os.path.exists(QP_BENCH), reason="oracle/_ref/ref_qp_bench not built (needs /root/reference)")
-@pytest.mark.parametrize("mode,row,success_per_tx", [("c3", "f1_c3", 1), ("c5seg", "tso_seg_c5", 7)])
+@pytest.mark.parametrize("mode,row,success_per_tx", [("c3", "f1_c3", 1), ("c5seg", "tso_seg_c5", 7), ("c5", "f1_c5", 0)])
 def test_ref_qp_bench_rows(mode, row, success_per_tx):
     r = subprocess.run([QP_BENCH, "256", "1", mode], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["row"] == row and d["kind"] == "reference" and d["cores"] == 1 and d["value"] > 0
     # C3 frames are balanced so every RX verify passes; C5 with RX verify off
-    # delivers all 7 segments of every frame
+    # delivers all 7 segments of every frame; with it on, random segments fail
     assert d["rx_success"] == 256 * success_per_tx
 
 
