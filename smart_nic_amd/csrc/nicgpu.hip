@@ -165,7 +165,7 @@ constexpr int kVmcnt0 = 0x0F70;
 // Tuning-only knobs (libnicgpu_tune.so; outputs are wrong with any set).
 constexpr uint32_t kDbgNoStage = 1, kDbgNoHash = 2, kDbgNoStore = 4, kDbgNoHist = 8, kDbgNtStore = 16,
                    kDbgNoHashStore = 32, kDbgNoQueueStore = 64, kDbgNoTable = 128, kDbgSmallOut = 256, kDbgBurstOut = 512,
-                   kDbgStoreSc = 1024 | 2048 | 4096, kDbgRotate = 8192;
+                   kDbgStoreSc = 1024 | 2048 | 4096, kDbgRotate = 8192, kDbgNoFlush = 16384;
 __device__ __forceinline__ bool dbg_on(const RxParams& P, uint32_t bit) {
 #ifdef NICGPU_TUNING
   return (P.dbg & bit) != 0u;
@@ -1134,7 +1134,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
     for (int i = 0; i < HOLD; ++i)
       if (i < hold_n) store_out<SST>(P, held_out(held_b[i], held_v[i], held_c[i], held_h[i], lane), L.want_rss);
   }
-  if (L.hist_lds) {
+  if (L.hist_lds && !dbg_on(P, kDbgNoFlush)) {
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) {
       uint32_t v = L.hist[i];
