@@ -189,17 +189,20 @@ public:
   void process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                      RxBatchResult& out, void* stream = nullptr);
 
-  /// Pipelined form of process_batch for a stream of batches: submit() returns
-  /// once the batch's work is enqueued on `stream` (the descriptors are no
-  /// longer read after it returns), and collect() waits for the oldest
-  /// submitted batch and swaps its results into `out` (false: none pending).
-  /// At most two batches are pending, so batch k's completions come down while
-  /// batch k+1's descriptors go up.  The results, the memory image and the
-  /// statistics equal those of process_batch called in submission order; a
-  /// batch's QueuePair and RSS statistics are added when it is collected.
-  /// Batches that cannot run on the device (overlapping buffers, an interrupt
-  /// callback, device_resolve off) are processed during submit().  Throws
-  /// std::logic_error on a third submit() or a process_batch() while batches
+  /// Pipelined form of process_batch for a stream of batches: submit() puts
+  /// the batch's descriptors on their way to the device and hands the rest
+  /// (plan, resolve, DMA writes, RSS, downloads) to the stage's job thread,
+  /// which works on `stream` in submission order; collect() waits for the
+  /// oldest submitted batch and swaps its results into `out` (false: none
+  /// pending).  At most three batches are pending, so batch k's completions
+  /// come down while batch k+1 is resolved and batch k+2's descriptors go up.
+  /// The descriptor arrays (and `mem`) must stay valid and unchanged until the
+  /// batch is collected.  The results, the memory image and the statistics
+  /// equal those of process_batch called in submission order; a batch's
+  /// QueuePair and RSS statistics are added when it is collected, and a
+  /// batch's error is thrown by its collect().  With an interrupt callback the
+  /// batch is processed during submit(), on the caller's thread.  Throws
+  /// std::logic_error on a fourth submit() or a process_batch() while batches
   /// are pending.
   void submit(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
               void* stream = nullptr);
@@ -214,10 +217,12 @@ public:
   struct Slot;     // one batch in flight on the device: its context, events and landing buffers
 
 private:
-  // Device resolve of one batch in three steps: front() uploads, plans, checks
-  // and resolves (false, nothing written, when the buffers overlap); back()
+  // Device resolve of one batch in four steps: upload() sends the descriptors
+  // up, front() plans, checks and resolves (false, nothing written, when the
+  // buffers overlap); back()
   // enqueues the DMA writes and RSS and starts the downloads into `out`;
   // finish() waits for them and completes `out`.
+  void upload(Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx, bool rx_beside);
   bool front(Slot& sl, const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
              QueuePairStats& stats, RxBatchResult& out, void* stream, int& disjoint, double& check_us);
   void back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult& out, void* stream);

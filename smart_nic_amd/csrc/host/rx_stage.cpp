@@ -20,6 +20,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <future>
 #include <limits>
@@ -900,9 +901,59 @@ private:
 
 }  // namespace
 
+namespace {
+
+// In-order job runner: submit()'s batches are planned, resolved and enqueued
+// on the device by this thread while the caller uploads the next batch.
+class JobQueue {
+public:
+  ~JobQueue() { stop(); }
+  void push(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_all();
+  }
+  // runs what is queued, then ends the thread (a later push starts another)
+  void stop() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = false;
+  }
+
+private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;
+      std::function<void()> f = std::move(q_.front());
+      q_.pop_front();
+      lk.unlock();
+      f();  // jobs catch their own exceptions
+      lk.lock();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::thread th_;
+  std::deque<std::function<void()>> q_;
+  bool stop_ = false;
+};
+
+}  // namespace
+
 // One batch in flight on the device.  process_batch uses slot 0; submit()
-// alternates between the two, so batch k's buffers stay untouched while its
-// results come down and batch k+1 is planned and resolved in the other.
+// cycles through all of them, so batch k's buffers stay untouched while its
+// results come down, batch k+1 is planned and resolved and batch k+2's
+// descriptors go up.
 struct BatchedQueuePair::Slot {
   nicgpu_qp* qp = nullptr;   // device resolve context (same device as the Scratch streams)
   void* ev_tx = nullptr;     // TX descriptors uploaded
@@ -921,10 +972,19 @@ struct BatchedQueuePair::Slot {
   std::optional<SideJob> down;
   std::promise<void> rss_recorded;  // ev_done is recorded (the download job waits for it)
   bool rss_released = false;
-  // submit(): where the batch's results land until collect(), and its stats
+  double upload_us = 0;  // time upload() held its thread
+  std::optional<SideJob> up;  // process_batch: the RX upload beside the plan
+  // submit(): the batch, where its results land until collect(), its stats,
+  // and the job that plans, resolves and enqueues it
+  DeviceHostMemory mem{};
+  std::span<const TxDescriptor> tx;
+  std::span<const RxDescriptor> rx;
+  void* stream = nullptr;
   RxBatchResult result;
   QueuePairStats stats{};
   bool on_device = false;
+  std::promise<void> job_done;
+  std::future<void> job;
 
   void release_rss() {
     if (!rss_released) rss_recorded.set_value();
@@ -938,6 +998,7 @@ struct BatchedQueuePair::Slot {
   }
   void release() {
     wait();
+    up.reset();
     if (qp) (void) nicgpu_qp_destroy(qp);
     for (void* e : {ev_tx, ev_rx, ev_resolved, ev_done})
       if (e) (void) nicgpu_event_destroy(e);
@@ -961,9 +1022,11 @@ struct BatchedQueuePair::Scratch {
   int device = -1;
   void* side_up = nullptr;
   void* side_down = nullptr;
-  SideWorker up_worker;  // issues the RX descriptor uploads
-  Slot slot[2];
+  SideWorker up_worker;  // process_batch: issues the RX descriptor uploads
+  static constexpr unsigned kSlots = 3;
+  Slot slot[kSlots];
   unsigned head = 0, pending = 0;  // submit(): oldest pending slot, batches pending
+  JobQueue jobs;                   // submit(): plans, resolves and enqueues the batches in order
   void release() {
     for (Slot& sl : slot) sl.release();
     if (side_up) (void) nicgpu_stream_destroy(side_up);
@@ -979,7 +1042,10 @@ struct BatchedQueuePair::Scratch {
     for (Slot& sl : slot) sl.create(dev);
     device = dev;
   }
-  ~Scratch() { release(); }
+  ~Scratch() {
+    jobs.stop();  // no job may still use a slot
+    release();
+  }
 };
 
 // The device mirrors (nicgpu.h) of the PODs the device resolve moves.
@@ -1094,8 +1160,25 @@ private:
 BatchedQueuePair::BatchedQueuePair(BatchedQueuePairConfig config)
     : config_(std::move(config)), scratch_(std::make_unique<Scratch>()) {}
 BatchedQueuePair::~BatchedQueuePair() = default;
-BatchedQueuePair::BatchedQueuePair(BatchedQueuePair&&) noexcept = default;
-BatchedQueuePair& BatchedQueuePair::operator=(BatchedQueuePair&&) noexcept = default;
+// The job thread's queued batches call back into the object that submitted
+// them, so a move first lets them finish (their downloads and collect() need
+// only the heap-held Scratch).
+BatchedQueuePair::BatchedQueuePair(BatchedQueuePair&& o) noexcept {
+  if (o.scratch_) o.scratch_->jobs.stop();
+  config_ = std::move(o.config_);
+  stats_ = o.stats_;
+  scratch_ = std::move(o.scratch_);
+}
+BatchedQueuePair& BatchedQueuePair::operator=(BatchedQueuePair&& o) noexcept {
+  if (this != &o) {
+    if (scratch_) scratch_->jobs.stop();
+    if (o.scratch_) o.scratch_->jobs.stop();
+    config_ = std::move(o.config_);
+    stats_ = o.stats_;
+    scratch_ = std::move(o.scratch_);
+  }
+  return *this;
+}
 
 RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                               std::span<const RxDescriptor> rx, void* stream) {
@@ -1118,6 +1201,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
     check(nicgpu_get_device(&dev), "nicgpu_get_device");
     scratch_->ensure(dev);
     Slot& sl = scratch_->slot[0];
+    upload(sl, tx, rx, true);
     on_device = front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);
     if (on_device) {
       back(sl, mem, out, stream);
@@ -1146,32 +1230,53 @@ void BatchedQueuePair::submit(const DeviceHostMemory& mem, std::span<const TxDes
                               std::span<const RxDescriptor> rx, void* stream) {
   if (mem.base == nullptr && mem.size != 0) throw GpuError("submit: null host-memory image", NICGPU_ERR_INVALID);
   Scratch& S = *scratch_;
-  if (S.pending == 2) throw std::logic_error("submit: two batches pending; collect() one first");
+  if (S.pending == Scratch::kSlots) throw std::logic_error("submit: three batches pending; collect() one first");
   int dev = 0;
   check(nicgpu_get_device(&dev), "nicgpu_get_device");
   if (S.pending == 0) S.ensure(dev);
   else if (S.device != dev) throw std::logic_error("submit: batches pending on another device");
-  Slot& sl = S.slot[(S.head + S.pending) % 2];
+  Slot& sl = S.slot[(S.head + S.pending) % Scratch::kSlots];
   sl.stats = QueuePairStats{};
   sl.on_device = false;
-  int disjoint = -1;
-  double check_us = 0;
-  if (config_.device_resolve && !config_.on_interrupt) {
-    sl.on_device = front(sl, mem, tx, rx, sl.stats, sl.result, stream, disjoint, check_us);
-    if (sl.on_device) back(sl, mem, sl.result, stream);
-  }
-  if (!sl.on_device) on_host(mem, tx, rx, sl.stats, sl.result, stream, disjoint, check_us);
-  sl.result.timings.check_us = check_us;
+  sl.mem = mem;
+  sl.tx = tx;
+  sl.rx = rx;
+  sl.stream = stream;
+  const bool device = config_.device_resolve && !config_.on_interrupt;
+  // the descriptors go up now, on this thread, beside the earlier batches'
+  // device work; the rest runs in submission order on the job thread
+  if (device) upload(sl, tx, rx, false);
+  sl.job_done = std::promise<void>();
+  sl.job = sl.job_done.get_future();
+  auto run = [this, &sl, device] {
+    try {
+      int disjoint = -1;
+      double check_us = 0;
+      if (device) {
+        sl.on_device = front(sl, sl.mem, sl.tx, sl.rx, sl.stats, sl.result, sl.stream, disjoint, check_us);
+        if (sl.on_device) back(sl, sl.mem, sl.result, sl.stream);
+      }
+      if (!sl.on_device) on_host(sl.mem, sl.tx, sl.rx, sl.stats, sl.result, sl.stream, disjoint, check_us);
+      sl.result.timings.check_us = check_us;
+      sl.job_done.set_value();
+    } catch (...) {
+      sl.job_done.set_exception(std::current_exception());
+    }
+  };
   ++S.pending;
+  // an interrupt callback keeps firing on the caller's thread
+  if (config_.on_interrupt) run();
+  else S.jobs.push(run);
 }
 
 bool BatchedQueuePair::collect(RxBatchResult& out) {
   Scratch& S = *scratch_;
   if (S.pending == 0) return false;
   Slot& sl = S.slot[S.head];
-  // the slot is free again whatever finish() does
-  S.head = (S.head + 1) % 2;
+  // the slot is free again whatever the batch throws
+  S.head = (S.head + 1) % Scratch::kSlots;
   --S.pending;
+  sl.job.get();  // the job's exception, if any
   if (sl.on_device) finish(sl, sl.result);
   rx_stage_detail::add_stats(stats_, sl.stats);
   std::swap(out, sl.result);
@@ -1179,6 +1284,35 @@ bool BatchedQueuePair::collect(RxBatchResult& out) {
 }
 
 std::size_t BatchedQueuePair::pending() const noexcept { return scratch_->pending; }
+
+// The descriptors up on the upload stream, so they need not wait behind
+// earlier batches' DMA writes and RSS on the caller's stream: TX first, alone
+// on the link, then RX — issued from the helper thread when `rx_beside`, so
+// the plan and piece sums (TX descriptors only) run while it goes up.
+// (Descriptor arrays in page-locked memory upload without staging and without
+// holding the issuing thread.)
+void BatchedQueuePair::upload(Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+                              bool rx_beside) {
+  using clock = std::chrono::steady_clock;
+  const auto t = clock::now();
+  Scratch& S = *scratch_;
+  const std::size_t ntx = tx.size(), nrx = rx.size();
+  nicgpu_qp_view& v = sl.v;
+  check(nicgpu_qp_reserve(sl.qp, ntx, nrx, &v), "nicgpu_qp_reserve");
+  check(nicgpu_memcpy_async(v.tx, tx.data(), ntx * sizeof(TxDescriptor), S.side_up), "nicgpu_memcpy_async");
+  check(nicgpu_event_record(sl.ev_tx, S.side_up), "nicgpu_event_record");
+  if (rx_beside) {
+    sl.up.emplace(S.up_worker);
+    sl.up->start([&sl, &S, &v, rx](SideJob& j) {
+      j.ok(nicgpu_memcpy_async(v.rx, rx.data(), rx.size() * sizeof(RxDescriptor), S.side_up), "nicgpu_memcpy_async") &&
+          j.ok(nicgpu_event_record(sl.ev_rx, S.side_up), "nicgpu_event_record");
+    });
+  } else {
+    check(nicgpu_memcpy_async(v.rx, rx.data(), nrx * sizeof(RxDescriptor), S.side_up), "nicgpu_memcpy_async");
+    check(nicgpu_event_record(sl.ev_rx, S.side_up), "nicgpu_event_record");
+  }
+  sl.upload_us = std::chrono::duration<double, std::micro>(clock::now() - t).count();
+}
 
 // Disjoint buffers, no interrupt callback: plan, piece sums and the
 // reference's control flow on the device (nicgpu_qp_*), the part after a
@@ -1199,31 +1333,19 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   out.timings.device = true;
   const std::size_t ntx = tx.size(), nrx = rx.size();
   nicgpu_qp_view& v = sl.v;
+  out.timings.copy_us += sl.upload_us;
   auto t = clock::now();
-  check(nicgpu_qp_reserve(sl.qp, ntx, nrx, &v), "nicgpu_qp_reserve");
-  // Both uploads go on the upload stream, so they need not wait behind the
-  // previous batch's DMA writes and RSS on the caller's stream (submit()).
-  // TX descriptors first, alone on the link; then the RX descriptors go up
-  // while the plan and piece sums (TX descriptors only) run on the caller's
-  // stream.  (Descriptor arrays in page-locked memory upload without staging
-  // and without holding the issuing thread.)
-  check(nicgpu_memcpy_async(v.tx, tx.data(), ntx * sizeof(TxDescriptor), S.side_up), "nicgpu_memcpy_async");
-  check(nicgpu_event_record(sl.ev_tx, S.side_up), "nicgpu_event_record");
-  SideJob up{S.up_worker};
-  up.start([&](SideJob& j) {
-    j.ok(nicgpu_memcpy_async(v.rx, rx.data(), nrx * sizeof(RxDescriptor), S.side_up), "nicgpu_memcpy_async") &&
-        j.ok(nicgpu_event_record(sl.ev_rx, S.side_up), "nicgpu_event_record");
-  });
   check(nicgpu_stream_wait_event(stream, sl.ev_tx), "nicgpu_stream_wait_event");
-  out.timings.copy_us += us_since(t);
-  t = clock::now();
   std::uint64_t np = 0;
   check(nicgpu_qp_plan(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &np, &v,
                        stream),
         "nicgpu_qp_plan");
   out.timings.sums_us += us_since(t);
   t = clock::now();
-  up.finish();
+  if (sl.up) {
+    sl.up->finish();
+    sl.up.reset();
+  }
   check(nicgpu_stream_wait_event(stream, sl.ev_rx), "nicgpu_stream_wait_event");
   out.timings.copy_us += us_since(t);
   // overlapping buffers go to the host path before anything is written; a

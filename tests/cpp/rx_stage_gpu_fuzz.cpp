@@ -381,7 +381,7 @@ int run_pipeline(std::uint64_t seed) {
   for (int b = 0; b < nb; ++b) seq.process_batch(m_seq, txs[b], rxs[b], want[b]);
   RxBatchResult out;
   for (int b = 0; b < nb; ++b) {
-    if (pipe.pending() == 2 || (pipe.pending() == 1 && r.below(3) == 0)) {
+    while (pipe.pending() == 3 || (pipe.pending() > 0 && r.below(3) == 0)) {
       assert(pipe.collect(out));
       got.push_back(std::move(out));
       out = RxBatchResult{};

@@ -5,7 +5,7 @@
 //   buffers; host: the host resolve, BatchedQueuePairConfig::device_resolve off;
 //   pinned: the descriptor arrays in page-locked memory, as a descriptor ring
 //   the device DMAs from would be, so they go up without staging; pipelined:
-//   submit()/collect() with two batches in flight, reported per batch over
+//   submit()/collect() with three batches in flight, reported per batch over
 //   the whole run, against process_batch one batch at a time)
 //
 // c3: IMIX 64/576/1518 (7:4:1) frames, each balanced so the whole-frame
@@ -146,20 +146,20 @@ int main(int argc, char** argv) {
   RxBatchResult last;
   const bool pipelined = argc > 7 && std::string(argv[7]) == "pipelined";
   if (pipelined) {
-    // warm-up (both slots grow their buffers), then `reps` batches with two in
+    // warm-up (every slot grows its buffers), then `reps` batches with three in
     // flight: per-batch time = the whole run / reps (the first upload and the
     // last download included)
-    // (six batches: the three result sets in rotation, the caller's and the
-    // two slots', each take their first-touch page faults here)
-    for (int w = 0; w < 6; ++w) {
-      if (qp.pending() == 2) qp.collect(last);
+    // (eight batches: the four result sets in rotation, the caller's and the
+    // three slots', each take their first-touch page faults here)
+    for (int w = 0; w < 8; ++w) {
+      if (qp.pending() == 3) qp.collect(last);
       qp.submit(dm, txs, rxs);
     }
     while (qp.collect(last)) {
     }
     const auto t0 = std::chrono::steady_clock::now();
     for (int r = 0; r < reps; ++r) {
-      if (qp.pending() == 2) qp.collect(last);
+      if (qp.pending() == 3) qp.collect(last);
       qp.submit(dm, txs, rxs);
     }
     while (qp.collect(last)) {
