@@ -1248,8 +1248,9 @@ void BatchedQueuePair::submit(const DeviceHostMemory& mem, std::span<const TxDes
   if (device) upload(sl, tx, rx, false);
   sl.job_done = std::promise<void>();
   sl.job = sl.job_done.get_future();
-  auto run = [this, &sl, device] {
+  auto run = [this, &sl, device, dev] {
     try {
+      check(nicgpu_set_device(dev), "nicgpu_set_device");  // the HIP device is per thread
       int disjoint = -1;
       double check_us = 0;
       if (device) {
@@ -1304,7 +1305,9 @@ void BatchedQueuePair::upload(Slot& sl, std::span<const TxDescriptor> tx, std::s
   if (rx_beside) {
     sl.up.emplace(S.up_worker);
     sl.up->start([&sl, &S, &v, rx](SideJob& j) {
-      j.ok(nicgpu_memcpy_async(v.rx, rx.data(), rx.size() * sizeof(RxDescriptor), S.side_up), "nicgpu_memcpy_async") &&
+      j.ok(nicgpu_set_device(S.device), "nicgpu_set_device") &&
+          j.ok(nicgpu_memcpy_async(v.rx, rx.data(), rx.size() * sizeof(RxDescriptor), S.side_up),
+               "nicgpu_memcpy_async") &&
           j.ok(nicgpu_event_record(sl.ev_rx, S.side_up), "nicgpu_event_record");
     });
   } else {
@@ -1445,7 +1448,8 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");
   sl.down.emplace(sl.worker);
   sl.down->start([&sl, &S, &out, &v, ntx, nrx_total, tn, nq, rss, hits, rss_ready](SideJob& j) {
-    bool ok = j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_resolved), "nicgpu_stream_wait_event") &&
+    bool ok = j.ok(nicgpu_set_device(S.device), "nicgpu_set_device") &&
+              j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_resolved), "nicgpu_stream_wait_event") &&
               j.ok(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), S.side_down),
                    "nicgpu_memcpy_async") &&
               j.ok(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry),
