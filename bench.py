@@ -176,6 +176,41 @@ def cpu_rows_baseline(pktgen):
     return rows
 
 
+def gpu_rows():
+    """Every other SURVEY §8 row measured live on this box, after the timed
+    region (child processes, one at a time): the RX kernel on C3 IMIX and
+    64 B, L3/L4 verification, ICRC, TSO checksums and segmentation
+    (tools/bench_rows.py: HIP events per launch, medians, algorithmic bytes
+    and roofline fraction per row), and the batched QueuePair stage of row f1
+    on C3 and C5, one batch at a time and pipelined
+    (tools/bin/bench_rx_stage, built by __graft_entry__.build()).  Errors are
+    reported, never hidden."""
+    import subprocess
+
+    rows, errors = [], []
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_rows.py"), "--steps", "10", "--warmup", "2",
+                            "--rows", "rx_c3,rx_u64,rx_l34_c2,icrc_c2,icrc_c3,tso_c5,tso_seg_c5"],
+                           capture_output=True, text=True, timeout=300)
+        rows += [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+        if r.returncode != 0:
+            errors.append(f"bench_rows.py rc={r.returncode}: {r.stderr[-400:]}")
+    except Exception as e:  # report, never hide
+        errors.append(f"bench_rows.py: {e!r}")
+    stage = os.path.join(ROOT, "tools", "bin", "bench_rx_stage")
+    for args in (["c3", "1048576", "6", "0", "device", "pinned", "sync"],
+                 ["c3", "1048576", "12", "0", "device", "pinned", "pipelined"],
+                 ["c5", "131072", "6", "0", "device", "pinned", "sync"]):
+        try:
+            r = subprocess.run([stage, *args], capture_output=True, text=True, timeout=180)
+            rows += [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+            if r.returncode != 0:
+                errors.append(f"bench_rx_stage {' '.join(args)} rc={r.returncode}: {r.stderr[-400:]}")
+        except Exception as e:
+            errors.append(f"bench_rx_stage {' '.join(args)}: {e!r}")
+    return rows, errors
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -206,6 +241,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the same-box read-only streaming ceiling")
+    ap.add_argument("--no-rows", action="store_true",
+                    help="skip the other SURVEY §8 rows (tools/bench_rows.py and the f1 stage, ~2 min) at N = 1")
     ap.add_argument("--dist", action="store_true",
                     help="take the multi-rank path (RCCL init, key/table broadcast, barriers, max-reduce) even at "
                          "world size 1, to exercise it on a one-GPU box")
@@ -367,6 +404,10 @@ def main():
             out["e2e"] = e2e_rate(torch, sna, ctx, frames, desc, dev)
         except Exception as e:  # report, never hide
             out["e2e"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and not args.no_rows:
+        out["gpu_rows"], errors = gpu_rows()
+        if errors:
+            out["gpu_rows_errors"] = errors
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(frames, desc, table, (g_cs, g_q),
                                            n_sample_mt=min(n, 1 << 18), n_sample_1=min(n, 1 << 16))
