@@ -374,8 +374,8 @@ int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t nrx, void* stream);
  * view.queue_which[0, m), with each queue's range in view.queue_start /
  * queue_end for queues [0, nq) (nq <= 65536, at least the largest queue the
  * indirection table holds + 1; empty queues get start = end = 0).  The sort
- * runs over the nrx bound with the unlisted entries keyed past every queue.
- * Enqueued only. */
+ * runs over the nrx bound with the unlisted entries keyed nq, past every
+ * queue, on the low bits that hold 0..nq only.  Enqueued only. */
 int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream);
 
 #ifdef __cplusplus

@@ -2761,13 +2761,13 @@ __global__ __launch_bounds__(kQpBlock) void qp_scatter_kernel(const uint32_t* __
 }
 
 // sort keys of the first nrx RSS entries: the queue of the first *count, a
-// key past every queue (0x10000) for the rest, so the sort leaves them last
+// key past every queue (nq) for the rest, so the sort leaves them last
 __global__ __launch_bounds__(kQpBlock) void qp_keys_kernel(const uint16_t* __restrict__ q,
                                                            const unsigned long long* __restrict__ count, uint64_t nrx,
-                                                           uint32_t* key) {
+                                                           uint32_t nq, uint32_t* key) {
   const uint64_t m = *count;
   for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < nrx; k += (uint64_t) gridDim.x * kQpBlock)
-    key[k] = k < m ? (uint32_t) q[k] : 0x10000u;
+    key[k] = k < m ? (uint32_t) q[k] : nq;
 }
 
 // queue range boundaries of the first *count sorted keys, for queues below nq
@@ -3103,18 +3103,21 @@ int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream) {
   }
   if (st != NICGPU_OK || nrx == 0) return st;
   hipLaunchKernelGGL(qp_keys_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->rss_queue, q->scal + 3,
-                     (uint64_t) nrx, q->sort_key);
+                     (uint64_t) nrx, (uint32_t) nq, q->sort_key);
   st = hip_status(hipGetLastError());
   if (st != NICGPU_OK) return st;
-  // stable: each queue keeps its completions in posting order
+  // stable: each queue keeps its completions in posting order.  Keys run
+  // 0..nq, so only their low bits are sorted (16 queues: 5 bits, one pass).
+  int end_bit = 1;
+  while ((1ull << end_bit) <= (unsigned long long) nq) ++end_bit;
   size_t tb = 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, q->sort_key, q->sorted_key, q->which, q->queue_which, (int) nrx,
-                                         0, 17, s) != hipSuccess)
+                                         0, end_bit, s) != hipSuccess)
     return NICGPU_ERR_HIP;
   st = qp_grow(q->tmp, q->c_tmp, tb);
   if (st == NICGPU_OK)
     st = hip_status(hipcub::DeviceRadixSort::SortPairs(q->tmp, tb, q->sort_key, q->sorted_key, q->which,
-                                                       q->queue_which, (int) nrx, 0, 17, s));
+                                                       q->queue_which, (int) nrx, 0, end_bit, s));
   if (st != NICGPU_OK || nq == 0) return st;
   hipLaunchKernelGGL(qp_bounds_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->sorted_key, q->scal + 3,
                      (uint64_t) nq, q->queue_start, q->queue_end);
