@@ -56,6 +56,7 @@
 #include <functional>
 #include <memory>
 #include <span>
+#include <utility>
 #include <vector>
 
 #include "nic/gpu_batch.h"
@@ -121,6 +122,18 @@ namespace nic {
 struct DeviceHostMemory {
   std::byte* base{nullptr};  // device pointer; host address a <-> base[a]
   std::size_t size{0};
+};
+
+/// Descriptor arrays already in device memory — e.g. host-backed rings, whose
+/// descriptors live in the image itself (mem.base + the ring's address).  The
+/// stage copies them in stream order (no PCIe upload) and fetches host copies
+/// only when a host step needs them (a ring whose RX buffers are not in
+/// address order, a host tail, overlapping buffers).
+struct DeviceDescriptors {
+  const TxDescriptor* tx{nullptr};
+  std::size_t ntx{0};
+  const RxDescriptor* rx{nullptr};
+  std::size_t nrx{0};
 };
 
 struct BatchedQueuePairConfig {
@@ -207,6 +220,11 @@ public:
   void submit(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
               void* stream = nullptr);
   bool collect(RxBatchResult& out);
+  /// Both forms with descriptors already in device memory (DeviceDescriptors;
+  /// they must stay valid until the batch is done or collected).
+  void process_batch(const DeviceHostMemory& mem, const DeviceDescriptors& d, RxBatchResult& out,
+                     void* stream = nullptr);
+  void submit(const DeviceHostMemory& mem, const DeviceDescriptors& d, void* stream = nullptr);
   [[nodiscard]] std::size_t pending() const noexcept;
 
   [[nodiscard]] const QueuePairStats& stats() const noexcept { return stats_; }
@@ -227,6 +245,10 @@ private:
              QueuePairStats& stats, RxBatchResult& out, void* stream, int& disjoint, double& check_us);
   void back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult& out, void* stream);
   void finish(Slot& sl, RxBatchResult& out);
+  void enqueue(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+               const DeviceDescriptors* d, void* stream);
+  std::pair<std::span<const TxDescriptor>, std::span<const RxDescriptor>> host_spans(
+      Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx, void* stream);
   // the host path (buffers_disjoint unless `disjoint` is known, then run_batch)
   void on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                QueuePairStats& stats, RxBatchResult& out, void* stream, int disjoint, double& check_us);

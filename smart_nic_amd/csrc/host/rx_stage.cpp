@@ -974,6 +974,14 @@ struct BatchedQueuePair::Slot {
   bool rss_released = false;
   double upload_us = 0;  // time upload() held its thread
   std::optional<SideJob> up;  // process_batch: the RX upload beside the plan
+  // descriptors already in device memory (DeviceDescriptors): no upload; host
+  // copies fetched only when a host step needs them
+  const TxDescriptor* tx_dev = nullptr;
+  const RxDescriptor* rx_dev = nullptr;
+  std::size_t ntx_dev = 0, nrx_dev = 0;
+  std::vector<TxDescriptor> htx;
+  std::vector<RxDescriptor> hrx;
+  bool fetched = false;
   // submit(): the batch, where its results land until collect(), its stats,
   // and the job that plans, resolves and enqueues it
   DeviceHostMemory mem{};
@@ -1201,6 +1209,8 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
     check(nicgpu_get_device(&dev), "nicgpu_get_device");
     scratch_->ensure(dev);
     Slot& sl = scratch_->slot[0];
+    sl.tx_dev = nullptr;
+    sl.rx_dev = nullptr;
     upload(sl, tx, rx, true);
     on_device = front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);
     if (on_device) {
@@ -1226,8 +1236,71 @@ void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDe
   rx_stage_detail::run_batch(config_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint);
 }
 
+void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDescriptors& d, RxBatchResult& out,
+                                     void* stream) {
+  if (mem.base == nullptr && mem.size != 0) throw GpuError("process_batch: null host-memory image", NICGPU_ERR_INVALID);
+  if ((d.ntx && !d.tx) || (d.nrx && !d.rx)) throw GpuError("process_batch: null device descriptors", NICGPU_ERR_INVALID);
+  if (scratch_->pending) throw std::logic_error("process_batch: collect() the submitted batches first");
+  int dev = 0;
+  check(nicgpu_get_device(&dev), "nicgpu_get_device");
+  scratch_->ensure(dev);
+  Slot& sl = scratch_->slot[0];
+  sl.tx_dev = d.tx;
+  sl.rx_dev = d.rx;
+  sl.ntx_dev = d.ntx;
+  sl.nrx_dev = d.nrx;
+  sl.fetched = false;
+  QueuePairStats st = stats_;
+  int disjoint = -1;
+  double check_us = 0;
+  bool on_device = false;
+  if (config_.device_resolve && !config_.on_interrupt) {
+    on_device = front(sl, mem, {}, {}, st, out, stream, disjoint, check_us);
+    if (on_device) {
+      back(sl, mem, out, stream);
+      finish(sl, out);
+    }
+  }
+  if (!on_device) {
+    const auto [htx, hrx] = host_spans(sl, {}, {}, stream);
+    on_host(mem, htx, hrx, st, out, stream, disjoint, check_us);
+  }
+  out.timings.check_us = check_us;
+  stats_ = st;
+}
+
+// The batch's descriptors on the host: the caller's spans, or (device
+// descriptors) copies fetched once, in stream order.
+std::pair<std::span<const TxDescriptor>, std::span<const RxDescriptor>> BatchedQueuePair::host_spans(
+    Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx, void* stream) {
+  if (!sl.tx_dev && !sl.rx_dev) return {tx, rx};
+  if (!sl.fetched) {
+    sl.htx.resize(sl.ntx_dev);
+    sl.hrx.resize(sl.nrx_dev);
+    if (sl.ntx_dev)
+      check(nicgpu_memcpy_async(sl.htx.data(), sl.tx_dev, sl.ntx_dev * sizeof(TxDescriptor), stream),
+            "nicgpu_memcpy_async");
+    if (sl.nrx_dev)
+      check(nicgpu_memcpy_async(sl.hrx.data(), sl.rx_dev, sl.nrx_dev * sizeof(RxDescriptor), stream),
+            "nicgpu_memcpy_async");
+    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+    sl.fetched = true;
+  }
+  return {sl.htx, sl.hrx};
+}
+
 void BatchedQueuePair::submit(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                               std::span<const RxDescriptor> rx, void* stream) {
+  enqueue(mem, tx, rx, nullptr, stream);
+}
+
+void BatchedQueuePair::submit(const DeviceHostMemory& mem, const DeviceDescriptors& d, void* stream) {
+  if ((d.ntx && !d.tx) || (d.nrx && !d.rx)) throw GpuError("submit: null device descriptors", NICGPU_ERR_INVALID);
+  enqueue(mem, {}, {}, &d, stream);
+}
+
+void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
+                               std::span<const RxDescriptor> rx, const DeviceDescriptors* d, void* stream) {
   if (mem.base == nullptr && mem.size != 0) throw GpuError("submit: null host-memory image", NICGPU_ERR_INVALID);
   Scratch& S = *scratch_;
   if (S.pending == Scratch::kSlots) throw std::logic_error("submit: three batches pending; collect() one first");
@@ -1242,10 +1315,16 @@ void BatchedQueuePair::submit(const DeviceHostMemory& mem, std::span<const TxDes
   sl.tx = tx;
   sl.rx = rx;
   sl.stream = stream;
+  sl.tx_dev = d ? d->tx : nullptr;
+  sl.rx_dev = d ? d->rx : nullptr;
+  sl.ntx_dev = d ? d->ntx : 0;
+  sl.nrx_dev = d ? d->nrx : 0;
+  sl.fetched = false;
   const bool device = config_.device_resolve && !config_.on_interrupt;
-  // the descriptors go up now, on this thread, beside the earlier batches'
-  // device work; the rest runs in submission order on the job thread
-  if (device) upload(sl, tx, rx, false);
+  // host descriptors go up now, on this thread, beside the earlier batches'
+  // device work (device descriptors are copied in the job, in stream order);
+  // the rest runs in submission order on the job thread
+  if (device && !d) upload(sl, tx, rx, false);
   sl.job_done = std::promise<void>();
   sl.job = sl.job_done.get_future();
   auto run = [this, &sl, device, dev] {
@@ -1257,7 +1336,10 @@ void BatchedQueuePair::submit(const DeviceHostMemory& mem, std::span<const TxDes
         sl.on_device = front(sl, sl.mem, sl.tx, sl.rx, sl.stats, sl.result, sl.stream, disjoint, check_us);
         if (sl.on_device) back(sl, sl.mem, sl.result, sl.stream);
       }
-      if (!sl.on_device) on_host(sl.mem, sl.tx, sl.rx, sl.stats, sl.result, sl.stream, disjoint, check_us);
+      if (!sl.on_device) {
+        const auto [htx, hrx] = host_spans(sl, sl.tx, sl.rx, sl.stream);
+        on_host(sl.mem, htx, hrx, sl.stats, sl.result, sl.stream, disjoint, check_us);
+      }
       sl.result.timings.check_us = check_us;
       sl.job_done.set_value();
     } catch (...) {
@@ -1334,11 +1416,18 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   out.queues.clear();
   out.timings = RxBatchResult::Timings{};
   out.timings.device = true;
-  const std::size_t ntx = tx.size(), nrx = rx.size();
+  const bool dev_desc = sl.tx_dev || sl.rx_dev;
+  const std::size_t ntx = dev_desc ? sl.ntx_dev : tx.size(), nrx = dev_desc ? sl.nrx_dev : rx.size();
   nicgpu_qp_view& v = sl.v;
-  out.timings.copy_us += sl.upload_us;
   auto t = clock::now();
-  check(nicgpu_stream_wait_event(stream, sl.ev_tx), "nicgpu_stream_wait_event");
+  if (dev_desc) {  // device descriptors: copied in stream order (they may sit in the image)
+    check(nicgpu_qp_reserve(sl.qp, ntx, nrx, &v), "nicgpu_qp_reserve");
+    if (ntx) check(nicgpu_memcpy_async(v.tx, sl.tx_dev, ntx * sizeof(TxDescriptor), stream), "nicgpu_memcpy_async");
+    if (nrx) check(nicgpu_memcpy_async(v.rx, sl.rx_dev, nrx * sizeof(RxDescriptor), stream), "nicgpu_memcpy_async");
+  } else {
+    out.timings.copy_us += sl.upload_us;
+    check(nicgpu_stream_wait_event(stream, sl.ev_tx), "nicgpu_stream_wait_event");
+  }
   std::uint64_t np = 0;
   check(nicgpu_qp_plan(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &np, &v,
                        stream),
@@ -1349,14 +1438,17 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     sl.up->finish();
     sl.up.reset();
   }
-  check(nicgpu_stream_wait_event(stream, sl.ev_rx), "nicgpu_stream_wait_event");
+  if (!dev_desc) check(nicgpu_stream_wait_event(stream, sl.ev_rx), "nicgpu_stream_wait_event");
   out.timings.copy_us += us_since(t);
   // overlapping buffers go to the host path before anything is written; a
   // ring whose RX buffers are not in ascending address order is sorted there
   t = clock::now();
   int verdict = -1;
   check(nicgpu_qp_check(sl.qp, mem.size, ntx, nrx, &verdict, stream), "nicgpu_qp_check");
-  if (verdict < 0) verdict = buffers_disjoint(mem.size, tx, rx) ? 1 : 0;
+  if (verdict < 0) {
+    const auto [htx, hrx] = host_spans(sl, tx, rx, stream);
+    verdict = buffers_disjoint(mem.size, htx, hrx) ? 1 : 0;
+  }
   disjoint = verdict;
   check_us += us_since(t);
   if (!disjoint) return false;
@@ -1381,8 +1473,9 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     out.timings.host_tail = true;
     // the rest, in order, from ring position `used` (the host resolve; its
     // plan of tx[done..] lists the same pieces as the device's from piece_base[done])
-    const auto tail_tx = tx.subspan(done);
-    const auto tail_rx = rx.subspan(used);
+    const auto [htx, hrx] = host_spans(sl, tx, rx, stream);
+    const auto tail_tx = htx.subspan(done);
+    const auto tail_rx = hrx.subspan(used);
     make_plan(config_, mem.size, tail_tx, S.host.plan);
     std::uint32_t pb = 0;
     check(nicgpu_memcpy_async(&pb, v.piece_base + done, sizeof(pb), stream), "nicgpu_memcpy_async");

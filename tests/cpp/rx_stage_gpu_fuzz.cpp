@@ -7,7 +7,9 @@
 // too small, failing segment checksums), small and large (several grid
 // blocks, host tails).  Compared: every completion, the statistics, RX
 // descriptors consumed, the memory image, RSS hash / queue per completion, the
-// dispatch lists and the RSS engine's stats.  GPU only.
+// dispatch lists and the RSS engine's stats.  Odd seeds (here and in
+// `pipeline`) hand the descriptors over in device memory (DeviceDescriptors).
+// GPU only.
 //
 // `check` mode: nicgpu_qp_check (the device path's overlap check) against
 // rx_stage_detail::buffers_disjoint on random layouts — ascending rings with
@@ -15,7 +17,7 @@
 // rings, invalid and clipped descriptors.
 //
 //   rx_stage_gpu_fuzz <first_seed> <count>
-//   rx_stage_gpu_fuzz full c3|c5
+//   rx_stage_gpu_fuzz full c3|c5 [dev]
 //   rx_stage_gpu_fuzz check [count]
 //   rx_stage_gpu_fuzz pipeline [count]   (submit/collect vs process_batch in order)
 #undef NDEBUG
@@ -67,7 +69,7 @@ const std::vector<std::uint8_t> kMsKey = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x
                                           0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3, 0x80, 0x30,
                                           0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
 
-std::size_t g_tail = 0, g_device = 0, g_short = 0;  // host tails, device batches, batches with NoDescriptor
+std::size_t g_tail = 0, g_device = 0, g_short = 0, g_devdesc = 0;  // host tails, device batches, NoDescriptor, device descriptors
 
 int run_case(std::uint64_t seed) {
   Rng r{seed * 104729 + 3};
@@ -159,12 +161,27 @@ int run_case(std::uint64_t seed) {
   // device resolve
   RssEngine dev_rss{rss_cfg};
   cfg.rss = &dev_rss;
+  // odd seeds hand the descriptors over in device memory (DeviceDescriptors),
+  // placed in the same allocation past the image
+  const bool dev_desc = seed & 1;
+  const std::size_t desc_at = (mem_size + 64 + 255) & ~std::size_t{255};
+  const std::size_t rx_at = desc_at + ((ntx * sizeof(TxDescriptor) + 255) & ~std::size_t{255});
   void* d = nullptr;
-  assert(nicgpu_malloc(&d, mem_size + 64) == NICGPU_OK);
+  assert(nicgpu_malloc(&d, rx_at + nrx * sizeof(RxDescriptor) + 64) == NICGPU_OK);
   assert(nicgpu_memcpy_async(d, image.data(), mem_size, nullptr) == NICGPU_OK);
+  std::byte* base = static_cast<std::byte*>(d);
+  if (ntx) assert(nicgpu_memcpy_async(base + desc_at, tx.data(), ntx * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
+  if (nrx) assert(nicgpu_memcpy_async(base + rx_at, rx.data(), nrx * sizeof(RxDescriptor), nullptr) == NICGPU_OK);
   BatchedQueuePair qp{cfg};
   RxBatchResult go;
-  qp.process_batch(DeviceHostMemory{static_cast<std::byte*>(d), mem_size}, tx, rx, go);
+  if (dev_desc) {
+    const DeviceDescriptors dd{reinterpret_cast<const TxDescriptor*>(base + desc_at), ntx,
+                               reinterpret_cast<const RxDescriptor*>(base + rx_at), nrx};
+    qp.process_batch(DeviceHostMemory{base, mem_size}, dd, go);
+    g_devdesc += 1;
+  } else {
+    qp.process_batch(DeviceHostMemory{base, mem_size}, tx, rx, go);
+  }
   std::vector<std::uint8_t> dev_img(mem_size);
   assert(nicgpu_memcpy_async(dev_img.data(), d, mem_size, nullptr) == NICGPU_OK);
   assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
@@ -206,8 +223,9 @@ int run_case(std::uint64_t seed) {
 // Full-size f1 workloads (tools/bench_rx_stage.cpp's): C3 = 1 M IMIX frames
 // (balanced so every RX verify passes), C5 = 131072 x 9000 B TSO (H 54, mss
 // 1448; random payloads, so every packet ends at its first segment's
-// checksum).  Device resolve against host resolve, everything compared.
-int run_full(const char* wl) {
+// checksum).  Device resolve against host resolve, everything compared;
+// `dev` hands the descriptors over in device memory.
+int run_full(const char* wl, bool dev_desc) {
   const bool c5 = std::strcmp(wl, "c5") == 0;
   const std::size_t n = c5 ? 131072 : (1u << 20);
   Rng r{c5 ? 55u : 33u};
@@ -270,12 +288,25 @@ int run_full(const char* wl) {
   rx_stage_detail::run_batch(cfg, mem_size, tx, rx, hs, ho, scratch, cpu);
   RssEngine dev_rss{rss_cfg};
   cfg.rss = &dev_rss;
+  const std::size_t ntx = tx.size();
+  const std::size_t desc_at = (mem_size + 64 + 255) & ~std::size_t{255};
+  const std::size_t rx_at = desc_at + ((ntx * sizeof(TxDescriptor) + 255) & ~std::size_t{255});
   void* d = nullptr;
-  assert(nicgpu_malloc(&d, mem_size + 64) == NICGPU_OK);
+  assert(nicgpu_malloc(&d, rx_at + nrx * sizeof(RxDescriptor) + 64) == NICGPU_OK);
   assert(nicgpu_memcpy_async(d, image.data(), mem_size, nullptr) == NICGPU_OK);
+  std::byte* base = static_cast<std::byte*>(d);
+  if (ntx) assert(nicgpu_memcpy_async(base + desc_at, tx.data(), ntx * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
+  if (nrx) assert(nicgpu_memcpy_async(base + rx_at, rx.data(), nrx * sizeof(RxDescriptor), nullptr) == NICGPU_OK);
   BatchedQueuePair qp{cfg};
   RxBatchResult go;
-  qp.process_batch(DeviceHostMemory{static_cast<std::byte*>(d), mem_size}, tx, rx, go);
+  if (dev_desc) {
+    const DeviceDescriptors dd{reinterpret_cast<const TxDescriptor*>(base + desc_at), ntx,
+                               reinterpret_cast<const RxDescriptor*>(base + rx_at), nrx};
+    qp.process_batch(DeviceHostMemory{base, mem_size}, dd, go);
+    g_devdesc += 1;
+  } else {
+    qp.process_batch(DeviceHostMemory{base, mem_size}, tx, rx, go);
+  }
   std::vector<std::uint8_t> dev_img(mem_size);
   assert(nicgpu_memcpy_async(dev_img.data(), d, mem_size, nullptr) == NICGPU_OK);
   assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
@@ -289,9 +320,10 @@ int run_full(const char* wl) {
   ok = ok && dev_rss.stats().hashes == host_rss.stats().hashes && dev_rss.stats().queue_hits == host_rss.stats().queue_hits;
   std::size_t succ = 0;
   for (const auto& c : go.rx_completions) succ += c.status == 0;
-  std::printf("rx_stage_gpu_fuzz full %s: %s (%zu TX, %zu RX completions, %zu Success, device %d, host tail %d)\n", wl,
-              ok ? "ok" : "MISMATCH", go.tx_completions.size(), go.rx_completions.size(), succ, int(go.timings.device),
-              int(go.timings.host_tail));
+  std::printf("rx_stage_gpu_fuzz full %s: %s (%zu TX, %zu RX completions, %zu Success, device %d, host tail %d, device "
+              "descriptors %d)\n",
+              wl, ok ? "ok" : "MISMATCH", go.tx_completions.size(), go.rx_completions.size(), succ,
+              int(go.timings.device), int(go.timings.host_tail), int(dev_desc));
   return ok ? 0 : 1;
 }
 
@@ -300,7 +332,7 @@ int run_full(const char* wl) {
 // ones wrote (TX buffers inside the RX ring), some batches overlap their own
 // buffers (host path) and the RX windows wrap the ring.  Results, statistics,
 // the image and the RSS engine's stats must all be equal.
-std::size_t g_pipe_batches = 0, g_pipe_host = 0;
+std::size_t g_pipe_batches = 0, g_pipe_host = 0, g_pipe_devdesc = 0;
 
 int run_pipeline(std::uint64_t seed) {
   Rng r{seed * 7727 + 5};
@@ -379,6 +411,28 @@ int run_pipeline(std::uint64_t seed) {
   BatchedQueuePair pipe{cfg};
   std::vector<RxBatchResult> want(nb), got;
   for (int b = 0; b < nb; ++b) seq.process_batch(m_seq, txs[b], rxs[b], want[b]);
+  // odd seeds: the pipelined side gets its descriptors in device memory, and
+  // runs a batch through process_batch now and then when nothing is pending
+  const bool dev_desc = seed & 1;
+  std::vector<DeviceDescriptors> dd(nb);
+  void* d_desc = nullptr;
+  if (dev_desc) {
+    std::size_t bytes = 0;
+    for (int b = 0; b < nb; ++b) bytes += txs[b].size() * sizeof(TxDescriptor) + rxs[b].size() * sizeof(RxDescriptor);
+    assert(nicgpu_malloc(&d_desc, bytes + 64) == NICGPU_OK);
+    std::byte* p = static_cast<std::byte*>(d_desc);
+    for (int b = 0; b < nb; ++b) {
+      assert(nicgpu_memcpy_async(p, txs[b].data(), txs[b].size() * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
+      dd[b].tx = reinterpret_cast<const TxDescriptor*>(p);
+      dd[b].ntx = txs[b].size();
+      p += txs[b].size() * sizeof(TxDescriptor);
+      assert(nicgpu_memcpy_async(p, rxs[b].data(), rxs[b].size() * sizeof(RxDescriptor), nullptr) == NICGPU_OK);
+      dd[b].rx = reinterpret_cast<const RxDescriptor*>(p);
+      dd[b].nrx = rxs[b].size();
+      p += rxs[b].size() * sizeof(RxDescriptor);
+    }
+    assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+  }
   RxBatchResult out;
   for (int b = 0; b < nb; ++b) {
     while (pipe.pending() == 3 || (pipe.pending() > 0 && r.below(3) == 0)) {
@@ -386,7 +440,15 @@ int run_pipeline(std::uint64_t seed) {
       got.push_back(std::move(out));
       out = RxBatchResult{};
     }
-    pipe.submit(m_pipe, txs[b], rxs[b]);
+    if (!dev_desc) {
+      pipe.submit(m_pipe, txs[b], rxs[b]);
+    } else if (pipe.pending() == 0 && r.below(3) == 0) {
+      pipe.process_batch(m_pipe, dd[b], out);
+      got.push_back(std::move(out));
+      out = RxBatchResult{};
+    } else {
+      pipe.submit(m_pipe, dd[b]);
+    }
   }
   while (pipe.collect(out)) {
     got.push_back(std::move(out));
@@ -404,6 +466,7 @@ int run_pipeline(std::uint64_t seed) {
     g_pipe_host += !w.timings.device;
   }
   g_pipe_batches += nb;
+  if (dev_desc) g_pipe_devdesc += nb;
   ok = ok && std::memcmp(&seq.stats(), &pipe.stats(), sizeof(QueuePairStats)) == 0;
   ok = ok && rss_seq.stats().hashes == rss_pipe.stats().hashes && rss_seq.stats().queue_hits == rss_pipe.stats().queue_hits;
   std::vector<std::uint8_t> a(mem_size), b(mem_size);
@@ -413,6 +476,7 @@ int run_pipeline(std::uint64_t seed) {
   ok = ok && a == b;
   nicgpu_free(d_seq);
   nicgpu_free(d_pipe);
+  if (d_desc) nicgpu_free(d_desc);
   if (!ok) {
     std::fprintf(stderr, "pipeline seed %llu: pipelined run differs from process_batch in order\n",
                  (unsigned long long) seed);
@@ -515,18 +579,19 @@ int main(int argc, char** argv) {
     int bad = 0;
     for (std::uint64_t s = 1; s <= count; ++s) bad += run_pipeline(s);
     if (bad) return 1;
-    std::printf("rx_stage_gpu_fuzz pipeline: ok (%llu sequences, %zu batches, %zu of them on the host path)\n",
-                (unsigned long long) count, g_pipe_batches, g_pipe_host);
+    std::printf("rx_stage_gpu_fuzz pipeline: ok (%llu sequences, %zu batches, %zu of them on the host path, %zu "
+                "with device descriptors)\n",
+                (unsigned long long) count, g_pipe_batches, g_pipe_host, g_pipe_devdesc);
     return 0;
   }
-  if (argc > 1 && std::strcmp(argv[1], "full") == 0) return run_full(argc > 2 ? argv[2] : "c3");
+  if (argc > 1 && std::strcmp(argv[1], "full") == 0) return run_full(argc > 2 ? argv[2] : "c3", argc > 3 && std::strcmp(argv[3], "dev") == 0);
   const std::uint64_t first = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
   const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 300;
   int bad = 0;
   for (std::uint64_t s = first; s < first + count; ++s) bad += run_case(s);
   if (bad) return 1;
   std::printf("rx_stage_gpu_fuzz: ok (%llu batches, %zu resolved on the device, %zu of them with a host tail, %zu "
-              "running out of RX descriptors)\n",
-              (unsigned long long) count, g_device, g_tail, g_short);
+              "running out of RX descriptors, %zu with device descriptors)\n",
+              (unsigned long long) count, g_device, g_tail, g_short, g_devdesc);
   return 0;
 }

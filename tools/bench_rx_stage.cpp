@@ -1,10 +1,12 @@
 // bench_rx_stage.cpp — nic::BatchedQueuePair throughput.
 //
-//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host] [pageable|pinned] [sync|pipelined]
+//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host] [pageable|pinned|device] [sync|pipelined]
 //   (device: BatchedQueuePair's device resolve, the default for disjoint
 //   buffers; host: the host resolve, BatchedQueuePairConfig::device_resolve off;
 //   pinned: the descriptor arrays in page-locked memory, as a descriptor ring
-//   the device DMAs from would be, so they go up without staging; pipelined:
+//   the device DMAs from would be, so they go up without staging; device: the
+//   descriptor arrays already in device memory (DeviceDescriptors, as a
+//   host-backed ring in the image would be), no upload at all; pipelined:
 //   submit()/collect() with three batches in flight, reported per batch over
 //   the whole run, against process_batch one batch at a time)
 //
@@ -127,7 +129,8 @@ int main(int argc, char** argv) {
   cfg.rss = &rss;
   if (argc > 4) cfg.host_threads = static_cast<unsigned>(std::atoi(argv[4]));
   if (argc > 5) cfg.device_resolve = std::string(argv[5]) != "host";
-  const bool pinned = argc > 6 && std::string(argv[6]) == "pinned";
+  const std::string desc_kind = argc > 6 ? argv[6] : "pageable";
+  const bool pinned = desc_kind == "pinned", dev_desc = desc_kind == "device";
   BatchedQueuePair qp{cfg};
   const DeviceHostMemory dm{static_cast<std::byte*>(mem), mem_size};
   std::span<const TxDescriptor> txs{tx};
@@ -141,6 +144,20 @@ int main(int argc, char** argv) {
     txs = {static_cast<const TxDescriptor*>(ptx), n};
     rxs = {static_cast<const RxDescriptor*>(prx), nrx};
   }
+  void *dtx = nullptr, *drx = nullptr;
+  DeviceDescriptors dd;
+  if (dev_desc) {
+    check(nicgpu_malloc(&dtx, n * sizeof(TxDescriptor)), "nicgpu_malloc");
+    check(nicgpu_malloc(&drx, nrx * sizeof(RxDescriptor)), "nicgpu_malloc");
+    check(nicgpu_memcpy_async(dtx, tx.data(), n * sizeof(TxDescriptor), nullptr), "memcpy");
+    check(nicgpu_memcpy_async(drx, rx.data(), nrx * sizeof(RxDescriptor), nullptr), "memcpy");
+    check(nicgpu_stream_synchronize(nullptr), "sync");
+    dd = {static_cast<const TxDescriptor*>(dtx), n, static_cast<const RxDescriptor*>(drx), nrx};
+  }
+  auto submit = [&] {
+    if (dev_desc) qp.submit(dm, dd);
+    else qp.submit(dm, txs, rxs);
+  };
 
   std::vector<std::pair<double, RxBatchResult::Timings>> tot;
   RxBatchResult last;
@@ -153,14 +170,14 @@ int main(int argc, char** argv) {
     // three slots', each take their first-touch page faults here)
     for (int w = 0; w < 8; ++w) {
       if (qp.pending() == 3) qp.collect(last);
-      qp.submit(dm, txs, rxs);
+      submit();
     }
     while (qp.collect(last)) {
     }
     const auto t0 = std::chrono::steady_clock::now();
     for (int r = 0; r < reps; ++r) {
       if (qp.pending() == 3) qp.collect(last);
-      qp.submit(dm, txs, rxs);
+      submit();
     }
     while (qp.collect(last)) {
     }
@@ -169,7 +186,9 @@ int main(int argc, char** argv) {
   }
   for (int r = 0; r < (pipelined ? 0 : reps + 1); ++r) {
     const auto t0 = std::chrono::steady_clock::now();
-    qp.process_batch(dm, txs, rxs, last);  // one result object reused across batches
+    // one result object reused across batches
+    if (dev_desc) qp.process_batch(dm, dd, last);
+    else qp.process_batch(dm, txs, rxs, last);
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     if (r > 0) tot.emplace_back(us, last.timings);
     const auto& P = last.timings;
@@ -187,10 +206,12 @@ int main(int argc, char** argv) {
       "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"mode\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
       "\"rx_success\": %zu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
       "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f}}\n",
-      wl.c_str(), T.device ? "device" : "host", pinned ? "pinned" : "pageable", pipelined ? "pipelined" : "sync", cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
+      wl.c_str(), T.device ? "device" : "host", desc_kind.c_str(), pipelined ? "pipelined" : "sync", cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
       T.resolve_us, T.gather_us, T.rss_us, T.copy_us);
   nicgpu_free(mem);
   if (ptx) nicgpu_host_free(ptx);
   if (prx) nicgpu_host_free(prx);
+  if (dtx) nicgpu_free(dtx);
+  if (drx) nicgpu_free(drx);
   return 0;
 }
