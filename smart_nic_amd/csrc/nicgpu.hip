@@ -1441,6 +1441,10 @@ const RxVariant kRxVariants[] = {
     {rx_offload_kernel<2, true, 4, true, false, 1, true, -1, 16>, 2, 4, "u2_nt1_w4_c_sc1_defer"},
     {rx_offload_kernel<2, true, 4, true, false, 1, false>, 2, 4, "u2_nt1_w4_c"},
     {rx_offload_kernel<2, true, 4, false, false, 1, false, -1, 16, 0, true>, 2, 4, "u2_nt1_w4_sc1_ring", false, true},
+    // bigger blocks: fewer blocks add their histogram bins into the same
+    // counters at the end (1024 -> 512 / 256 same-address atomics)
+    {rx_offload_kernel<2, true, 8, true, false, 1, false, -1, 16, 0, true, true, true>, 2, 8, "u2_w8_c_sc1_ring_xpf", false, true, true},
+    {rx_offload_kernel<2, true, 16, true, false, 1, false, -1, 16, 0, true, true, true>, 2, 16, "u2_w16_c_sc1_ring_xpf", false, true, true},
 #endif
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
