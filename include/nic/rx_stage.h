@@ -157,6 +157,10 @@ struct BatchedQueuePairConfig {
   /// host then only moves descriptors and completions.  false: every batch is
   /// resolved on the host (the path the fuzz compares with the reference).
   bool device_resolve{true};
+  /// Leave the results of device-resolved batches in device memory
+  /// (RxBatchResult::dev) instead of copying them to the host vectors: for
+  /// consumers that read completions, hashes and dispatch lists on the GPU.
+  bool results_on_device{false};
 };
 
 struct RxBatchResult {
@@ -173,6 +177,24 @@ struct RxBatchResult {
   std::vector<std::vector<std::uint32_t>> queues;
   /// Wall time of each phase of process_batch (host clock, GPU phases
   /// include their stream synchronisation).
+  /// With BatchedQueuePairConfig::results_on_device, for a batch resolved on
+  /// the device (timings.device): the results in device memory, in the
+  /// stage's buffers, and the vectors above (queues included) left empty.
+  /// Valid until the stage's next process_batch() or submit(); ready when
+  /// process_batch() / collect() returns.  Host-resolved batches fill the
+  /// vectors as usual and leave this empty.
+  struct DeviceResults {
+    const CompletionEntry* tx_completions{nullptr};  // [ntx], posting order
+    const CompletionEntry* rx_completions{nullptr};  // [nrx], posting order
+    std::size_t ntx{0}, nrx{0};
+    const std::uint32_t* rx_hash{nullptr};   // [nrx]; null without an RssEngine
+    const std::uint16_t* rx_queue{nullptr};  // [nrx]; null without an RssEngine
+    /// RX completion indices grouped by queue: queue q's are
+    /// queue_which[queue_start[q] .. queue_end[q]) (host vectors, one entry per
+    /// queue up to the largest with frames).
+    const std::uint32_t* queue_which{nullptr};
+    std::vector<std::uint32_t> queue_start, queue_end;
+  } dev;
   struct Timings {
     double check_us{0};  // overlapping buffers? (nicgpu_qp_check on the device path, else buffers_disjoint)
     double plan_us{0}, sums_us{0}, resolve_us{0}, gather_us{0}, rss_us{0};

@@ -4,7 +4,7 @@ set -e
 REV=${REV:-HEAD}
 tmp=$(mktemp -d)
 git show "$REV:smart_nic_amd/csrc/nicgpu.hip" > "$tmp/nicgpu.hip"
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Iinclude -shared \
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Iinclude -Ismart_nic_amd/csrc -shared \
   -o smart_nic_amd/libnicgpu_ab.so "$tmp/nicgpu.hip"
 rm -rf "$tmp"
 echo "built smart_nic_amd/libnicgpu_ab.so from $REV"

@@ -1227,6 +1227,7 @@ void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDe
                                std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out, void* stream,
                                int disjoint, double& check_us) {
   using clock = std::chrono::steady_clock;
+  out.dev = RxBatchResult::DeviceResults{};
   if (disjoint < 0) {
     const auto t0 = clock::now();
     disjoint = rx_stage_detail::buffers_disjoint(mem.size, tx, rx) ? 1 : 0;
@@ -1416,6 +1417,7 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   out.queues.clear();
   out.timings = RxBatchResult::Timings{};
   out.timings.device = true;
+  out.dev = RxBatchResult::DeviceResults{};
   const bool dev_desc = sl.tx_dev || sl.rx_dev;
   const std::size_t ntx = dev_desc ? sl.ntx_dev : tx.size(), nrx = dev_desc ? sl.nrx_dev : rx.size();
   nicgpu_qp_view& v = sl.v;
@@ -1468,7 +1470,8 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   add_stats(st, d);
   std::size_t nrx_total = used;
   out.rx_consumed = used;
-  out.tx_completions.resize(ntx);
+  if (config_.results_on_device) out.tx_completions.clear();
+  else out.tx_completions.resize(ntx);
   if (done < ntx) {
     out.timings.host_tail = true;
     // the rest, in order, from ring position `used` (the host resolve; its
@@ -1524,9 +1527,24 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   }
   const std::size_t tn = sl.tn, nq = sl.nq;
   const bool rss = sl.rss;
-  out.rx_completions.resize(nrx_total);
-  out.rx_hash.resize(nrx_total);
-  out.rx_queue.resize(nrx_total);
+  const bool keep = config_.results_on_device;  // results stay in the slot's device buffers
+  if (keep) {
+    out.rx_completions.clear();
+    out.rx_hash.clear();
+    out.rx_queue.clear();
+    RxBatchResult::DeviceResults& d = out.dev;
+    d.tx_completions = reinterpret_cast<const CompletionEntry*>(v.txc);
+    d.rx_completions = reinterpret_cast<const CompletionEntry*>(v.rxc);
+    d.ntx = ntx;
+    d.nrx = nrx_total;
+    d.rx_hash = rss ? v.rx_hash : nullptr;
+    d.rx_queue = rss ? v.rx_queue : nullptr;
+    d.queue_which = rss ? v.queue_which : nullptr;
+  } else {
+    out.rx_completions.resize(nrx_total);
+    out.rx_hash.resize(nrx_total);
+    out.rx_queue.resize(nrx_total);
+  }
   // pinned landing space: [count][hits tn] u64, then [start nq][end nq][which nrx] u32
   sl.meta = sl.h_meta.get<std::uint64_t>(1 + tn);
   sl.qs = sl.h_lists.get<std::uint32_t>(2 * nq + nrx_total + 1);
@@ -1540,25 +1558,27 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   std::shared_future<void> rss_ready = sl.rss_recorded.get_future().share();
   check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");
   sl.down.emplace(sl.worker);
-  sl.down->start([&sl, &S, &out, &v, ntx, nrx_total, tn, nq, rss, hits, rss_ready](SideJob& j) {
+  sl.down->start([&sl, &S, &out, &v, ntx, nrx_total, tn, nq, rss, keep, hits, rss_ready](SideJob& j) {
     bool ok = j.ok(nicgpu_set_device(S.device), "nicgpu_set_device") &&
-              j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_resolved), "nicgpu_stream_wait_event") &&
-              j.ok(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), S.side_down),
-                   "nicgpu_memcpy_async") &&
-              j.ok(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry),
-                                       S.side_down),
-                   "nicgpu_memcpy_async");
+              j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_resolved), "nicgpu_stream_wait_event");
+    if (ok && !keep)
+      ok = j.ok(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), S.side_down),
+                "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry), S.side_down),
+                "nicgpu_memcpy_async");
     rss_ready.wait();
     ok = ok && j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_done), "nicgpu_stream_wait_event");
     if (ok && rss)
       ok = j.ok(nicgpu_memcpy_async(sl.meta, v.rss_count, sizeof(std::uint64_t), S.side_down), "nicgpu_memcpy_async") &&
            j.ok(nicgpu_memcpy_async(sl.meta + 1, hits, tn * sizeof(std::uint64_t), S.side_down), "nicgpu_memcpy_async") &&
            j.ok(nicgpu_memcpy_async(sl.qs, v.queue_start, nq * 4, S.side_down), "nicgpu_memcpy_async") &&
-           j.ok(nicgpu_memcpy_async(sl.qe, v.queue_end, nq * 4, S.side_down), "nicgpu_memcpy_async") &&
-           j.ok(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, S.side_down), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(sl.qe, v.queue_end, nq * 4, S.side_down), "nicgpu_memcpy_async");
+    if (ok && rss && !keep)
+      ok = j.ok(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, S.side_down), "nicgpu_memcpy_async") &&
            j.ok(nicgpu_memcpy_async(out.rx_queue.data(), v.rx_queue, nrx_total * 2, S.side_down), "nicgpu_memcpy_async") &&
            j.ok(nicgpu_stream_synchronize(S.side_down), "nicgpu_stream_synchronize") &&
            j.ok(nicgpu_memcpy_async(sl.which, v.queue_which, sl.meta[0] * 4, S.side_down), "nicgpu_memcpy_async");
+    // (with the results kept on the device this is where the batch is known done)
     ok = ok && j.ok(nicgpu_stream_synchronize(S.side_down), "nicgpu_stream_synchronize");
   });
   try {
@@ -1585,7 +1605,7 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   }
   sl.release_rss();
   out.timings.rss_us += us_since(t);
-  if (!rss) {
+  if (!rss && !keep) {
     std::fill(out.rx_hash.begin(), out.rx_hash.end(), 0u);
     std::fill(out.rx_queue.begin(), out.rx_queue.end(), RxBatchResult::kNoQueue);
   }
@@ -1607,8 +1627,13 @@ void BatchedQueuePair::finish(Slot& sl, RxBatchResult& out) {
     std::size_t used_q = 0;  // largest queue with frames + 1
     for (std::size_t q = 0; q < sl.nq; ++q)
       if (sl.qe[q] > sl.qs[q]) used_q = q + 1;
-    out.queues.resize(used_q);
-    for (std::size_t q = 0; q < used_q; ++q) out.queues[q].assign(sl.which + sl.qs[q], sl.which + sl.qe[q]);
+    if (config_.results_on_device) {
+      out.dev.queue_start.assign(sl.qs, sl.qs + used_q);
+      out.dev.queue_end.assign(sl.qe, sl.qe + used_q);
+    } else {
+      out.queues.resize(used_q);
+      for (std::size_t q = 0; q < used_q; ++q) out.queues[q].assign(sl.which + sl.qs[q], sl.which + sl.qe[q]);
+    }
   }
   out.timings.copy_us += std::chrono::duration<double, std::micro>(clock::now() - t).count();
 }

@@ -8,7 +8,9 @@
 // blocks, host tails).  Compared: every completion, the statistics, RX
 // descriptors consumed, the memory image, RSS hash / queue per completion, the
 // dispatch lists and the RSS engine's stats.  Odd seeds (here and in
-// `pipeline`) hand the descriptors over in device memory (DeviceDescriptors).
+// `pipeline`) hand the descriptors over in device memory (DeviceDescriptors);
+// seeds with bit 1 set leave the results there (results_on_device) and
+// compare them after copying them down.
 // GPU only.
 //
 // `check` mode: nicgpu_qp_check (the device path's overlap check) against
@@ -17,7 +19,7 @@
 // rings, invalid and clipped descriptors.
 //
 //   rx_stage_gpu_fuzz <first_seed> <count>
-//   rx_stage_gpu_fuzz full c3|c5 [dev]
+//   rx_stage_gpu_fuzz full c3|c5 [dev] [keep]
 //   rx_stage_gpu_fuzz check [count]
 //   rx_stage_gpu_fuzz pipeline [count]   (submit/collect vs process_batch in order)
 #undef NDEBUG
@@ -70,6 +72,43 @@ const std::vector<std::uint8_t> kMsKey = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x
                                           0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
 
 std::size_t g_tail = 0, g_device = 0, g_short = 0, g_devdesc = 0;  // host tails, device batches, NoDescriptor, device descriptors
+
+// BatchedQueuePairConfig::results_on_device: copy RxBatchResult::dev into the
+// host vectors, as the host-result form fills them, so the comparisons apply.
+// Called before the stage's next process_batch / submit (the view's lifetime).
+std::size_t g_keep = 0;
+bool materialize(RxBatchResult& o) {
+  if (!o.timings.device) return o.dev.tx_completions == nullptr && o.dev.ntx == 0;
+  if (!o.tx_completions.empty() || !o.rx_completions.empty() || !o.queues.empty()) return false;
+  const auto& d = o.dev;
+  if (d.ntx && !d.tx_completions) return false;
+  if (d.nrx && !d.rx_completions) return false;
+  o.tx_completions.resize(d.ntx);
+  o.rx_completions.resize(d.nrx);
+  o.rx_hash.assign(d.nrx, 0u);
+  o.rx_queue.assign(d.nrx, RxBatchResult::kNoQueue);
+  if (d.ntx)
+    assert(nicgpu_memcpy_async(o.tx_completions.data(), d.tx_completions, d.ntx * sizeof(CompletionEntry), nullptr) ==
+           NICGPU_OK);
+  if (d.nrx)
+    assert(nicgpu_memcpy_async(o.rx_completions.data(), d.rx_completions, d.nrx * sizeof(CompletionEntry), nullptr) ==
+           NICGPU_OK);
+  if (d.rx_hash && d.nrx) {
+    assert(nicgpu_memcpy_async(o.rx_hash.data(), d.rx_hash, d.nrx * 4, nullptr) == NICGPU_OK);
+    assert(nicgpu_memcpy_async(o.rx_queue.data(), d.rx_queue, d.nrx * 2, nullptr) == NICGPU_OK);
+  }
+  assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+  if (d.queue_start.size() != d.queue_end.size() || (!d.queue_start.empty() && !d.queue_which)) return false;
+  for (std::size_t q = 0; q < d.queue_start.size(); ++q) {
+    std::vector<std::uint32_t> w(d.queue_end[q] - d.queue_start[q]);
+    if (!w.empty())
+      assert(nicgpu_memcpy_async(w.data(), d.queue_which + d.queue_start[q], w.size() * 4, nullptr) == NICGPU_OK);
+    assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+    o.queues.push_back(std::move(w));
+  }
+  ++g_keep;
+  return true;
+}
 
 int run_case(std::uint64_t seed) {
   Rng r{seed * 104729 + 3};
@@ -164,6 +203,7 @@ int run_case(std::uint64_t seed) {
   // odd seeds hand the descriptors over in device memory (DeviceDescriptors),
   // placed in the same allocation past the image
   const bool dev_desc = seed & 1;
+  const bool keep = (seed >> 1) & 1;  // results_on_device
   const std::size_t desc_at = (mem_size + 64 + 255) & ~std::size_t{255};
   const std::size_t rx_at = desc_at + ((ntx * sizeof(TxDescriptor) + 255) & ~std::size_t{255});
   void* d = nullptr;
@@ -172,6 +212,7 @@ int run_case(std::uint64_t seed) {
   std::byte* base = static_cast<std::byte*>(d);
   if (ntx) assert(nicgpu_memcpy_async(base + desc_at, tx.data(), ntx * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
   if (nrx) assert(nicgpu_memcpy_async(base + rx_at, rx.data(), nrx * sizeof(RxDescriptor), nullptr) == NICGPU_OK);
+  cfg.results_on_device = keep;
   BatchedQueuePair qp{cfg};
   RxBatchResult go;
   if (dev_desc) {
@@ -181,6 +222,10 @@ int run_case(std::uint64_t seed) {
     g_devdesc += 1;
   } else {
     qp.process_batch(DeviceHostMemory{base, mem_size}, tx, rx, go);
+  }
+  if (keep && !materialize(go)) {
+    std::fprintf(stderr, "results on the device: the view is not as documented\n");
+    return 1;
   }
   std::vector<std::uint8_t> dev_img(mem_size);
   assert(nicgpu_memcpy_async(dev_img.data(), d, mem_size, nullptr) == NICGPU_OK);
@@ -224,8 +269,9 @@ int run_case(std::uint64_t seed) {
 // (balanced so every RX verify passes), C5 = 131072 x 9000 B TSO (H 54, mss
 // 1448; random payloads, so every packet ends at its first segment's
 // checksum).  Device resolve against host resolve, everything compared;
-// `dev` hands the descriptors over in device memory.
-int run_full(const char* wl, bool dev_desc) {
+// `dev` hands the descriptors over in device memory, `keep` leaves the results
+// there (results_on_device).
+int run_full(const char* wl, bool dev_desc, bool keep) {
   const bool c5 = std::strcmp(wl, "c5") == 0;
   const std::size_t n = c5 ? 131072 : (1u << 20);
   Rng r{c5 ? 55u : 33u};
@@ -297,6 +343,7 @@ int run_full(const char* wl, bool dev_desc) {
   std::byte* base = static_cast<std::byte*>(d);
   if (ntx) assert(nicgpu_memcpy_async(base + desc_at, tx.data(), ntx * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
   if (nrx) assert(nicgpu_memcpy_async(base + rx_at, rx.data(), nrx * sizeof(RxDescriptor), nullptr) == NICGPU_OK);
+  cfg.results_on_device = keep;
   BatchedQueuePair qp{cfg};
   RxBatchResult go;
   if (dev_desc) {
@@ -306,6 +353,10 @@ int run_full(const char* wl, bool dev_desc) {
     g_devdesc += 1;
   } else {
     qp.process_batch(DeviceHostMemory{base, mem_size}, tx, rx, go);
+  }
+  if (keep && !materialize(go)) {
+    std::fprintf(stderr, "results on the device: the view is not as documented\n");
+    return 1;
   }
   std::vector<std::uint8_t> dev_img(mem_size);
   assert(nicgpu_memcpy_async(dev_img.data(), d, mem_size, nullptr) == NICGPU_OK);
@@ -408,7 +459,10 @@ int run_pipeline(std::uint64_t seed) {
   cfg.rss = &rss_seq;
   BatchedQueuePair seq{cfg};
   cfg.rss = &rss_pipe;
+  const bool keep = (seed >> 1) & 1;  // results_on_device on the pipelined side
+  cfg.results_on_device = keep;
   BatchedQueuePair pipe{cfg};
+  bool view_ok = true;
   std::vector<RxBatchResult> want(nb), got;
   for (int b = 0; b < nb; ++b) seq.process_batch(m_seq, txs[b], rxs[b], want[b]);
   // odd seeds: the pipelined side gets its descriptors in device memory, and
@@ -437,6 +491,7 @@ int run_pipeline(std::uint64_t seed) {
   for (int b = 0; b < nb; ++b) {
     while (pipe.pending() == 3 || (pipe.pending() > 0 && r.below(3) == 0)) {
       assert(pipe.collect(out));
+      if (keep) view_ok &= materialize(out);
       got.push_back(std::move(out));
       out = RxBatchResult{};
     }
@@ -444,6 +499,7 @@ int run_pipeline(std::uint64_t seed) {
       pipe.submit(m_pipe, txs[b], rxs[b]);
     } else if (pipe.pending() == 0 && r.below(3) == 0) {
       pipe.process_batch(m_pipe, dd[b], out);
+      if (keep) view_ok &= materialize(out);
       got.push_back(std::move(out));
       out = RxBatchResult{};
     } else {
@@ -451,10 +507,11 @@ int run_pipeline(std::uint64_t seed) {
     }
   }
   while (pipe.collect(out)) {
+    if (keep) view_ok &= materialize(out);
     got.push_back(std::move(out));
     out = RxBatchResult{};
   }
-  bool ok = static_cast<int>(got.size()) == nb;
+  bool ok = view_ok && static_cast<int>(got.size()) == nb;
   for (int b = 0; ok && b < nb; ++b) {
     const RxBatchResult &w = want[b], &g = got[b];
     ok = w.tx_completions.size() == g.tx_completions.size() && w.rx_completions.size() == g.rx_completions.size() &&
@@ -580,18 +637,25 @@ int main(int argc, char** argv) {
     for (std::uint64_t s = 1; s <= count; ++s) bad += run_pipeline(s);
     if (bad) return 1;
     std::printf("rx_stage_gpu_fuzz pipeline: ok (%llu sequences, %zu batches, %zu of them on the host path, %zu "
-                "with device descriptors)\n",
-                (unsigned long long) count, g_pipe_batches, g_pipe_host, g_pipe_devdesc);
+                "with device descriptors, %zu results left on the device)\n",
+                (unsigned long long) count, g_pipe_batches, g_pipe_host, g_pipe_devdesc, g_keep);
     return 0;
   }
-  if (argc > 1 && std::strcmp(argv[1], "full") == 0) return run_full(argc > 2 ? argv[2] : "c3", argc > 3 && std::strcmp(argv[3], "dev") == 0);
+  if (argc > 1 && std::strcmp(argv[1], "full") == 0) {
+    bool dev = false, keep = false;
+    for (int a = 3; a < argc; ++a) {
+      dev |= std::strcmp(argv[a], "dev") == 0;
+      keep |= std::strcmp(argv[a], "keep") == 0;
+    }
+    return run_full(argc > 2 ? argv[2] : "c3", dev, keep);
+  }
   const std::uint64_t first = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1;
   const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 300;
   int bad = 0;
   for (std::uint64_t s = first; s < first + count; ++s) bad += run_case(s);
   if (bad) return 1;
   std::printf("rx_stage_gpu_fuzz: ok (%llu batches, %zu resolved on the device, %zu of them with a host tail, %zu "
-              "running out of RX descriptors, %zu with device descriptors)\n",
-              (unsigned long long) count, g_device, g_tail, g_short, g_devdesc);
+              "running out of RX descriptors, %zu with device descriptors, %zu with results left on the device)\n",
+              (unsigned long long) count, g_device, g_tail, g_short, g_devdesc, g_keep);
   return 0;
 }

@@ -120,20 +120,21 @@ def test_full_size_c5_tso_linearity():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wl,desc", [("c3", "host"), ("c5", "host"), ("c3", "dev")])
+@pytest.mark.parametrize("wl,desc", [("c3", "host"), ("c5", "host"), ("c3", "dev"), ("c5", "dev keep")])
 def test_f1_full_size_device_vs_host(tmp_path, wl, desc):
     """Row f1 at the bench sizes (tools/bench_rx_stage.cpp): 1 M IMIX TX
     descriptors (C3) and 131072 x 9000 B TSO frames (C5, every packet ending at
     its first segment's checksum: positions settle by relaxation without a host
     tail).  The device resolve must equal the host resolve in every
     completion, stat, memory byte and RSS dispatch list.  `dev`: the
-    descriptors handed over in device memory (DeviceDescriptors)."""
+    descriptors handed over in device memory (DeviceDescriptors); `keep`: the
+    results left there (results_on_device) and copied down to compare."""
     import subprocess
 
     from test_host_cpp import _build
 
     exe = _build(tmp_path, "rx_stage_gpu_fuzz")
-    r = subprocess.run([exe, "full", wl] + (["dev"] if desc == "dev" else []), capture_output=True, text=True, timeout=300)
+    r = subprocess.run([exe, "full", wl] + [a for a in desc.split() if a != "host"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert f"full {wl}: ok" in r.stdout
     print(r.stdout.strip())

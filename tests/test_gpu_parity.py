@@ -558,6 +558,49 @@ def test_tso_segment_random_vs_oracle():
         assert oc[g: g + max(k, 0)].tolist() == cs
 
 
+def test_tso_segment_several_frames_per_wave():
+    """16384 frames, so each of the kernel's waves (at most 4096) walks about
+    four and the next frame's loads overlap this frame's segments: staged frames
+    (0..1500 B) mixed with unstaged ones (9300..9800 B, TSO mss 1448), invalid
+    mss, too many segments, frames that do not fit their slot, VLAN variants;
+    every segment vs the oracle and slot tails untouched."""
+    rng = np.random.default_rng(16)
+    n = 16384
+    big = rng.random(n) < 0.1
+    lens = np.where(big, rng.integers(9300, 9801, n), rng.integers(0, 1501, n))
+    offs = np.zeros(n, np.int64)
+    pos = 0
+    for i in range(n):
+        pos += int(rng.integers(0, 20))
+        offs[i] = pos
+        pos += int(lens[i])
+    frames = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    mk = rng.random(n)
+    mss = np.where(big, 1448, np.where(mk < 0.05, rng.integers(1, 16, n),
+                                       np.where(mk < 0.1, rng.integers(9001, 9100, n), rng.integers(100, 1449, n))))
+    hdr = np.where(big, 54, np.minimum(rng.integers(0, 120, n), lens + 8))
+    fl = (np.where(big | (rng.random(n) < 0.8), sna.SEG_TSO, 0)
+          | rng.choice([0, sna.SEG_VLAN_INSERT, sna.SEG_VLAN_STRIP | sna.SEG_VLAN_PRESENT,
+                        sna.SEG_VLAN_INSERT | sna.SEG_VLAN_STRIP], n)
+          | rng.integers(0, 65536, n))
+    stride = 1600
+    cnt, base, out, ol, oc = gpu_tso_segment(frames, sna.desc_pack(offs, lens), hdr, mss, fl, stride)
+    segs_seen = 0
+    for i in range(n):
+        k, segs, cs = po.tso_segment(frames[offs[i]: offs[i] + lens[i]].tobytes(), int(hdr[i]), int(mss[i]),
+                                     int(fl[i]), stride)
+        assert max(k, 0) == cnt[i], (i, k, int(cnt[i]))
+        g = int(base[i])
+        for j in range(max(k, 0)):
+            assert ol[g + j] == len(segs[j])
+            slot = out[(g + j) * stride: (g + j + 1) * stride]
+            assert slot[: len(segs[j])].tobytes() == segs[j], (i, j)
+            assert not slot[len(segs[j]):].any(), (i, j)
+        assert oc[g: g + max(k, 0)].tolist() == cs
+        segs_seen += max(k, 0)
+    assert segs_seen > n
+
+
 def test_tso_segment_c5_vs_oracle():
     """C5 shape (9000 B, H = 54, mss = 1448 and 1447, VLAN variants) at 4096
     frames, unaligned frame offsets; every segment vs the oracle."""

@@ -1,6 +1,6 @@
 // bench_rx_stage.cpp — nic::BatchedQueuePair throughput.
 //
-//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host] [pageable|pinned|device] [sync|pipelined]
+//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host] [pageable|pinned|device] [sync|pipelined] [host|device]
 //   (device: BatchedQueuePair's device resolve, the default for disjoint
 //   buffers; host: the host resolve, BatchedQueuePairConfig::device_resolve off;
 //   pinned: the descriptor arrays in page-locked memory, as a descriptor ring
@@ -8,7 +8,9 @@
 //   descriptor arrays already in device memory (DeviceDescriptors, as a
 //   host-backed ring in the image would be), no upload at all; pipelined:
 //   submit()/collect() with three batches in flight, reported per batch over
-//   the whole run, against process_batch one batch at a time)
+//   the whole run, against process_batch one batch at a time; the last
+//   argument: results copied to the host vectors, or left in device memory
+//   (BatchedQueuePairConfig::results_on_device))
 //
 // c3: IMIX 64/576/1518 (7:4:1) frames, each balanced so the whole-frame
 //     checksum verifies; RX descriptors with Layer4 checksum offload, 2 KiB
@@ -129,6 +131,7 @@ int main(int argc, char** argv) {
   cfg.rss = &rss;
   if (argc > 4) cfg.host_threads = static_cast<unsigned>(std::atoi(argv[4]));
   if (argc > 5) cfg.device_resolve = std::string(argv[5]) != "host";
+  cfg.results_on_device = argc > 8 && std::string(argv[8]) == "device";
   const std::string desc_kind = argc > 6 ? argv[6] : "pageable";
   const bool pinned = desc_kind == "pinned", dev_desc = desc_kind == "device";
   BatchedQueuePair qp{cfg};
@@ -199,14 +202,21 @@ int main(int argc, char** argv) {
   std::sort(tot.begin(), tot.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
   const double med = tot[tot.size() / 2].first;
   std::size_t ok = 0, frame_bytes = 0;
+  if (last.timings.device && cfg.results_on_device) {  // the last batch's completions, copied down to count
+    last.rx_completions.resize(last.dev.nrx);
+    check(nicgpu_memcpy_async(last.rx_completions.data(), last.dev.rx_completions,
+                              last.dev.nrx * sizeof(CompletionEntry), nullptr),
+          "memcpy");
+    check(nicgpu_stream_synchronize(nullptr), "sync");
+  }
   for (const auto& c : last.rx_completions) ok += c.status == 0;
   for (auto L : lens) frame_bytes += L;
   const auto& T = tot[tot.size() / 2].second;  // the median batch's phases
   std::printf(
-      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"mode\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
+      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"mode\": \"%s\", \"results\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
       "\"rx_success\": %zu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
       "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f}}\n",
-      wl.c_str(), T.device ? "device" : "host", desc_kind.c_str(), pipelined ? "pipelined" : "sync", cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
+      wl.c_str(), T.device ? "device" : "host", desc_kind.c_str(), pipelined ? "pipelined" : "sync", cfg.results_on_device ? "device" : "host", cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
       T.resolve_us, T.gather_us, T.rss_us, T.copy_us);
   nicgpu_free(mem);
   if (ptx) nicgpu_host_free(ptx);
