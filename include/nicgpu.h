@@ -130,7 +130,8 @@ int nicgpu_rss_info(const nicgpu_rss_ctx* ctx, size_t* key_len, size_t* table_n)
  *   out_hash[i]  = toeplitz(key, tuple(frame i))             (u32)
  *   out_queue[i] = table[out_hash[i] % table_n]              (u16)
  *   out_hits[j] += #packets with out_hash % table_n == j     (u64[table_n], accumulated)
- * With tuple_mode NONE only out_csum is produced (ctx may be NULL).
+ * With tuple_mode NONE only out_csum is produced (ctx may be NULL).  With
+ * out_csum NULL (and no L3/L4 flags) only each packet's headers are read.
  * RX status per queue_pair.cpp:437-438 is (out_csum[i] == 0). */
 int nicgpu_rx_offload(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc,
                       size_t n, int tuple_mode, uint32_t raw_off, uint32_t raw_len,

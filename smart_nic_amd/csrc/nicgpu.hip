@@ -1152,6 +1152,91 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
 #endif
 }
 
+// ------------------------------------------------------- RSS, headers only --
+// nicgpu_rx_offload with neither checksums nor L3/L4 flags requested (the
+// batched stage's dispatch, RssEngine::select_queue_batch): the hash and the
+// queue depend on a packet's headers only, so a batch need not stream its
+// frames.  One lane per packet loads the packet's first kHdrChunks chunks (the
+// ones inside it) into the same per-wave header stage rx_offload_kernel fills
+// and runs the same rss_hash_packet — bytes past the stage come from global
+// memory there as well — then the table lookup and the LDS histogram.  About
+// 48 B read per packet instead of the whole frame.
+__host__ __device__ inline uint32_t rss_only_block_bytes(uint32_t lut_words, uint32_t hist_n, uint32_t table_words) {
+  return (lut_words * 4u + hist_n * 4u + table_words * 4u + 15u) & ~15u;
+}
+constexpr uint32_t kRssOnlyWaveBytes = (uint32_t) kWave * kHdrStride * 16u;
+
+__global__ __launch_bounds__(kBlock) void rss_only_kernel(RxParams P) {
+  extern __shared__ uint4 lds_dyn[];
+  const uint32_t w = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
+  const uint32_t lane = lane_id();
+  const bool hist_lds = P.out_hits != nullptr && P.table_n <= (uint32_t) kHistLds;
+  const bool table_lds = P.table_n <= (uint32_t) kTableLds;
+  uint8_t* base_b = reinterpret_cast<uint8_t*>(lds_dyn);
+  uint32_t* lut = reinterpret_cast<uint32_t*>(base_b);
+  uint32_t* hist = lut + P.lut_words;
+  uint16_t* table_s = reinterpret_cast<uint16_t*>(hist + (hist_lds ? P.table_n : 0u));
+  const uint32_t block_bytes =
+      rss_only_block_bytes(P.lut_words, hist_lds ? P.table_n : 0u, table_lds ? (P.table_n + 1u) / 2u : 0u);
+  uint4* hdr = reinterpret_cast<uint4*>(base_b + block_bytes + w * kRssOnlyWaveBytes);
+  for (uint32_t i = threadIdx.x; i < P.lut_words; i += kBlock) lut[i] = P.lut[i];
+  if (hist_lds)
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kBlock) hist[i] = 0;
+  if (table_lds)
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kBlock) table_s[i] = P.table[i];
+  __syncthreads();
+  const uint64_t n_all = P.n_dev ? (*P.n_dev < P.n ? (uint64_t) *P.n_dev : P.n) : P.n;
+  const uint64_t stride = (uint64_t) gridDim.x * kWavesPerBlock * kWave;
+  auto desc_of = [&](uint64_t b) __attribute__((always_inline)) { return b + lane < n_all ? P.desc[b + lane] : 0ull; };
+  // the header chunks inside the packet (none for an empty or absent one)
+  auto load_hdr = [&](uint64_t d, u32x4* c) __attribute__((always_inline)) {
+    const uint64_t off = d & kOffMask;
+    const uint32_t len = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
+    const uint32_t nch = len ? (uint32_t) (((off + len - 1) >> 4) - (off >> 4) + 1) : 0u;
+    const u32x4* src = reinterpret_cast<const u32x4*>(P.frames + (off & ~15ull));
+#pragma unroll
+    for (int k = 0; k < kHdrChunks; ++k) c[k] = (uint32_t) k < nch ? src[k] : (u32x4){0u, 0u, 0u, 0u};
+  };
+  // software pipeline: tile b + stride's descriptors and headers are in flight
+  // while tile b hashes, and tile b + 2 stride's descriptors behind them
+  uint64_t b = ((uint64_t) blockIdx.x * kWavesPerBlock + w) * kWave;
+  uint64_t d = desc_of(b), dn = desc_of(b + stride);
+  u32x4 c[kHdrChunks];
+  load_hdr(d, c);
+  for (; b < n_all; b += stride) {
+    __builtin_amdgcn_wave_barrier();  // the previous tile's stage reads are done
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+    for (int k = 0; k < kHdrChunks; ++k) hdr[hdr_slot(lane, (uint32_t) k)] = make_uint4(c[k].x, c[k].y, c[k].z, c[k].w);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const uint64_t dc = d;
+    d = dn;
+    dn = desc_of(b + 2 * stride);
+    load_hdr(d, c);
+    const uint64_t i = b + lane;
+    if (i < n_all) {
+      const uint64_t off = dc & kOffMask;
+      const uint32_t len = (uint32_t) (dc >> NICGPU_DESC_OFFSET_BITS);
+      const uint32_t h = rss_hash_packet(P, lut, HdrView{hdr, lane}, (uint32_t) (off & 15u), P.frames + off, len);
+      const uint32_t idx = h % P.table_n;
+      if (P.out_hash) P.out_hash[i] = h;
+      if (P.out_queue) P.out_queue[i] = table_lds ? table_s[idx] : P.table[idx];
+      if (P.out_hits) {
+        if (hist_lds) atomicAdd(&hist[idx], 1u);
+        else atomicAdd(&P.out_hits[idx], 1ull);
+      }
+    }
+  }
+  if (hist_lds) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kBlock) {
+      const uint32_t v = hist[i];
+      if (v) atomicAdd(&P.out_hits[i], (unsigned long long) v);
+    }
+  }
+}
+
 // ------------------------------------------------------------- TSO / GSO --
 // One wave per frame.  Each lane streams 16-B chunks of the payload region;
 // a chunk overlaps at most two segments (mss >= 16 in the fast path), so the
@@ -2177,6 +2262,33 @@ RingPlan plan_ring(int dev, int variant, uint32_t lds, uint64_t ntiles, const De
   return rp;
 }
 
+int rss_only_blocks_per_cu(int dev, uint32_t lds) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceInfo& di = g_dev[dev & 63];
+  constexpr int kRssOnlyVariant = -1;  // occupancy cache key
+  for (const auto& o : di.occ)
+    if (o.variant == kRssOnlyVariant && o.lds == lds) return o.blocks;
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rss_only_kernel, kBlock, lds) != hipSuccess || b < 1) b = 1;
+  di.occ.push_back({kRssOnlyVariant, lds, b});
+  return b;
+}
+
+int launch_rss_only(const RxParams& P, const DeviceInfo& di, hipStream_t stream) {
+  const uint32_t hist_n = (P.out_hits && P.table_n <= (uint32_t) kHistLds) ? P.table_n : 0u;
+  const uint32_t table_words = P.table_n <= (uint32_t) kTableLds ? (P.table_n + 1u) / 2u : 0u;
+  const uint32_t lds = rss_only_block_bytes(P.lut_words, hist_n, table_words) + kWavesPerBlock * kRssOnlyWaveBytes;
+  // as many blocks as fit a CU (registers and LDS), one grid-stride pass each
+  int dev = 0;
+  (void) hipGetDevice(&dev);
+  const uint32_t bpc = (uint32_t) rss_only_blocks_per_cu(dev, lds);
+  const uint64_t want = (P.n + kBlock - 1) / kBlock;
+  const uint64_t cap = (uint64_t) di.cus * bpc;
+  const unsigned grid = (unsigned) (want < cap ? want : cap);
+  hipLaunchKernelGGL(rss_only_kernel, dim3(grid), dim3(kBlock), lds, stream, P);
+  return hip_status(hipGetLastError());
+}
+
 int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t stream) {
   if (variant < 0 || variant >= kNumRxVariants) return NICGPU_ERR_INVALID;
   const bool rss = P.mode != NICGPU_TUPLE_NONE;
@@ -2479,6 +2591,9 @@ int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frame
     uint32_t max_tuple = tuple_mode == NICGPU_TUPLE_RAW ? raw_len : 36u;
     P.lut_words = 2u * max_tuple * 16u;
   }
+  // hash and queue only: the headers suffice (rss_only_kernel)
+  if (variant == 0 && !out_csum && !out_l34 && tuple_mode != NICGPU_TUPLE_NONE)
+    return launch_rss_only(P, *di, static_cast<hipStream_t>(stream));
   return launch_rx(P, *di, variant, static_cast<hipStream_t>(stream));
 }
 }  // namespace

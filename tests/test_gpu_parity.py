@@ -67,6 +67,16 @@ def gpu_rx(frames, desc, key=b"", table=(), mode=sna.TUPLE_AUTO, raw_off=0, raw_
     sna.rx_offload(ctx, f, d, mode, raw_off, raw_len, cs, h, q, hits)
     torch.cuda.synchronize()
     out = host(cs, np.uint16), host(h, np.uint32), host(q, np.uint16), host(hits, np.uint64)
+    # the same batch without checksums takes the header-only kernel
+    # (rss_only_kernel): hash, queue and hits must not change
+    h2 = torch.empty(n, dtype=torch.int32, device="cuda")
+    q2 = torch.empty(n, dtype=torch.int16, device="cuda")
+    hits2 = torch.zeros(tn, dtype=torch.int64, device="cuda")
+    sna.rx_offload(ctx, f, d, mode, raw_off, raw_len, None, h2, q2, hits2)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host(h2, np.uint32), out[1], err_msg="header-only RSS: hash")
+    np.testing.assert_array_equal(host(q2, np.uint16), out[2], err_msg="header-only RSS: queue")
+    np.testing.assert_array_equal(host(hits2, np.uint64), out[3], err_msg="header-only RSS: hits")
     ctx.close()
     return out
 
@@ -257,6 +267,76 @@ def test_set_key_device_matches_host():
     meta = golden.c1()[2]
     np.testing.assert_array_equal(host(h, np.uint32), meta["hash"])
     np.testing.assert_array_equal(host(q, np.uint16), meta["queue"])
+
+
+@pytest.mark.parametrize("tn", [16, 128, 4000])
+def test_rss_only_imix_vs_oracle(tn):
+    """Header-only RSS (no checksum requested) over 200 K IMIX frames at random
+    byte offsets with VLAN-tagged, IPv6, fragmented and short frames mixed in;
+    tables that fit LDS and one that does not (hits through global atomics);
+    hash, queue and hits vs the oracle, and the device-count launch
+    (nicgpu_rx_offload_count) over a prefix."""
+    rng = np.random.default_rng(tn)
+    n = 200_000
+    lens = pktgen.imix_lengths(n, rng)
+    frames, desc, _ = pktgen.make_batch(lens, seed=tn, proto=6, corrupt_frac=0.0)
+    # odd byte offsets for one packet in four: move its bytes 1..15 B later
+    offs = (desc & np.uint64((1 << 40) - 1)).astype(np.int64)
+    ln = (desc >> np.uint64(40)).astype(np.int64)
+    shift = np.where(rng.random(n) < 0.25, rng.integers(1, 16, n), 0)
+    blob = np.zeros(len(frames) + 16 * n + 64, np.uint8)
+    new_offs = np.zeros(n, np.int64)
+    pos = 0
+    for i in range(n):
+        pos += int(shift[i])
+        new_offs[i] = pos
+        blob[pos: pos + ln[i]] = frames[offs[i]: offs[i] + ln[i]]
+        pos += int(ln[i]) + (-(pos + int(ln[i])) % 16)
+    # short and odd frames: truncate some, tag some with 802.1Q, make some IPv6 / fragments
+    for i in rng.choice(n, 3000, replace=False):
+        k = rng.integers(0, 4)
+        o = new_offs[i]
+        if k == 0:
+            ln[i] = int(rng.integers(0, 40))
+        elif k == 1 and ln[i] >= 64:
+            blob[o + 12: o + 14] = (0x81, 0x00)
+        elif k == 2 and ln[i] >= 64:
+            blob[o + 12: o + 14] = (0x86, 0xDD)
+            blob[o + 14] = 0x60
+        elif ln[i] >= 64:
+            blob[o + 20] |= 0x20  # more fragments
+    desc2 = sna.desc_pack(new_offs, ln)
+    key = bytes(MS_KEY)
+    table = rng.integers(0, 16, tn).astype(np.uint16)
+    _, h_o, q_o, _, hits_o = po.rx_batch(blob, desc2, key, table)
+    ctx = sna.RssContext(0)
+    ctx.set_key(key)
+    ctx.set_table(table)
+    f, d = dev(blob), dev(desc2)
+    h = torch.empty(n, dtype=torch.int32, device="cuda")
+    q = torch.empty(n, dtype=torch.int16, device="cuda")
+    hits = torch.zeros(tn, dtype=torch.int64, device="cuda")
+    sna.rx_offload(ctx, f, d, sna.TUPLE_AUTO, 0, 0, None, h, q, hits)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host(h, np.uint32), h_o)
+    np.testing.assert_array_equal(host(q, np.uint16), q_o)
+    np.testing.assert_array_equal(host(hits, np.uint64), hits_o)
+    # device-count launch over the first m packets: the rest untouched
+    m = 123_457
+    lib = sna.load_library()
+    n_dev = torch.tensor([m], dtype=torch.int64, device="cuda")
+    h.fill_(-1)
+    q.fill_(-1)
+    hits.zero_()
+    assert lib.nicgpu_rx_offload_count(ctx.handle, f.data_ptr(), d.data_ptr(), n, n_dev.data_ptr(), sna.TUPLE_AUTO,
+                                       0, 0, None, h.data_ptr(), q.data_ptr(), hits.data_ptr(), None) == sna.OK
+    torch.cuda.synchronize()
+    hh, qq = host(h, np.uint32), host(q, np.uint16)
+    np.testing.assert_array_equal(hh[:m], h_o[:m])
+    np.testing.assert_array_equal(qq[:m], q_o[:m])
+    assert (hh[m:] == 0xFFFFFFFF).all() and (qq[m:] == 0xFFFF).all()
+    np.testing.assert_array_equal(host(hits, np.uint64), np.bincount(h_o[:m] % tn, minlength=tn).astype(np.uint64))
+    ctx.close()
 
 
 def test_invalid_arguments():

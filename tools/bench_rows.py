@@ -10,6 +10,7 @@ Rows (SURVEY §8 d configs):
   rx_c3        C3 = 4 M IMIX 64/576/1518 (7:4:1), 16 queues (table i%16)
   icrc_c2      nicgpu_icrc_batch (f4) over the C2 frames
   icrc_c3      nicgpu_icrc_batch over the C3 frames
+  rss_c2/rss_c3  hash + queue + hits only (no checksum): the header-only kernel
   tso_c5       nicgpu_tso_checksum, C5 = 131072 x 9000 B, H=54, mss=1448 (7 segments)
   tso_seg_c5   nicgpu_tso_segment (f2): the C5 segments materialised with a VLAN insert,
                plus their checksums
@@ -139,6 +140,24 @@ def main():
             region, med = timed(torch, fn, args.steps, args.warmup)
             alg = fb + 16 * n + (n if l34 is not None else 0)
             report(row, wl, n, fb, alg, region, med)
+            ctx.close()
+        elif row in ("rss_c2", "rss_c3"):
+            # hash + queue + hits without checksums: the header-only kernel
+            wl = row.split("_")[1]
+            n, fb, f, d = batch(wl)
+            ctx = rss_ctx(16 if wl == "c3" else 4)
+            hs = torch.empty(n, dtype=torch.int32, device=dev)
+            qs = torch.empty(n, dtype=torch.int16, device=dev)
+            hits = torch.zeros(128, dtype=torch.int64, device=dev)
+
+            def fn():
+                sna.rx_offload(ctx, f, d, sna.TUPLE_AUTO, 0, 0, None, hs, qs, hits)
+
+            region, med = timed(torch, fn, args.steps, args.warmup)
+            lens = (d.cpu().numpy().view(np.uint64) >> np.uint64(40)).astype(np.int64)
+            hdr = int(np.minimum(lens, 48).sum())
+            # descriptors + the staged header bytes + hash/queue out
+            report(row, wl, n, fb, 16 * n + hdr + 6 * n, region, med, {"header_bytes": hdr})
             ctx.close()
         elif row in ("icrc_c2", "icrc_c3"):
             wl = row.split("_")[1]
