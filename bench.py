@@ -181,8 +181,9 @@ def gpu_rows():
     region (child processes, one at a time): the RX kernel on C3 IMIX and
     64 B, L3/L4 verification, ICRC, TSO checksums and segmentation
     (tools/bench_rows.py: HIP events per launch, medians, algorithmic bytes
-    and roofline fraction per row), and the batched QueuePair stage of row f1
-    on C3 and C5, one batch at a time and pipelined
+    and roofline fraction per row), RSS without checksums, and the batched
+    QueuePair stage of row f1 on C3 and C5, one batch at a time and pipelined,
+    with host and with device-resident descriptors and results
     (tools/bin/bench_rx_stage, built by __graft_entry__.build()).  Errors are
     reported, never hidden."""
     import subprocess
@@ -190,7 +191,7 @@ def gpu_rows():
     rows, errors = [], []
     try:
         r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_rows.py"), "--steps", "10", "--warmup", "2",
-                            "--rows", "rx_c3,rx_u64,rx_l34_c2,icrc_c2,icrc_c3,tso_c5,tso_seg_c5"],
+                            "--rows", "rx_c3,rx_u64,rx_l34_c2,rss_c2,rss_c3,icrc_c2,icrc_c3,tso_c5,tso_seg_c5"],
                            capture_output=True, text=True, timeout=300)
         rows += [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
         if r.returncode != 0:
@@ -200,7 +201,10 @@ def gpu_rows():
     stage = os.path.join(ROOT, "tools", "bin", "bench_rx_stage")
     for args in (["c3", "1048576", "6", "0", "device", "pinned", "sync"],
                  ["c3", "1048576", "12", "0", "device", "pinned", "pipelined"],
-                 ["c5", "131072", "6", "0", "device", "pinned", "sync"]):
+                 ["c5", "131072", "6", "0", "device", "pinned", "sync"],
+                 # descriptor rings and results kept in HBM (DeviceDescriptors, results_on_device)
+                 ["c3", "1048576", "6", "0", "device", "device", "sync", "device"],
+                 ["c3", "1048576", "12", "0", "device", "device", "pipelined", "device"]):
         try:
             r = subprocess.run([stage, *args], capture_output=True, text=True, timeout=180)
             rows += [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
