@@ -558,11 +558,18 @@ def test_icrc_random_batches_vs_oracle(seed):
 
 
 # --------------------------------------- TSO/GSO + VLAN materialisation (§8 f2) --
-def gpu_tso_segment(frames, desc, hdr, mss, flags, stride):
+def gpu_tso_segment(frames, desc, hdr, mss, flags, stride, fill_seed=None):
+    """fill_seed: the output starts as seeded random bytes instead of zeros (the
+    kernel rewrites slot bytes past a segment's end up to its 128-B line with
+    their own values; those bytes must come back unchanged)."""
     lens = (desc >> np.uint64(40)).astype(np.int64)
     cnt, base, total = sna.tso_segment_counts(lens, hdr, mss, flags)
     f = dev(np.concatenate([frames, np.zeros(64, np.uint8)]))
-    out = torch.zeros(max(total, 1) * stride, dtype=torch.uint8, device="cuda")
+    nbytes = max(total, 1) * stride
+    if fill_seed is None:
+        out = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+    else:
+        out = dev(np.random.default_rng(fill_seed).integers(0, 256, nbytes, dtype=np.uint8))
     ol = torch.zeros(max(total, 1), dtype=torch.int32, device="cuda")
     oc = torch.zeros(max(total, 1), dtype=torch.int16, device="cuda")
     sna.tso_segment(f, dev(desc), dev(np.asarray(hdr, np.uint16)), dev(np.asarray(mss, np.uint16)), dev(base),
@@ -624,7 +631,8 @@ def test_tso_segment_random_vs_oracle():
                         sna.SEG_VLAN_INSERT | sna.SEG_VLAN_STRIP, sna.SEG_VLAN_STRIP], n)
           | rng.integers(0, 65536, n))
     stride = 20008
-    cnt, base, out, ol, oc = gpu_tso_segment(frames, sna.desc_pack(offs, lens), hdr, mss, fl, stride)
+    cnt, base, out, ol, oc = gpu_tso_segment(frames, sna.desc_pack(offs, lens), hdr, mss, fl, stride, fill_seed=3)
+    fill = np.random.default_rng(3).integers(0, 256, out.size, dtype=np.uint8)
     for i in range(n):
         k, segs, cs = po.tso_segment(frames[offs[i]: offs[i] + lens[i]].tobytes(), int(hdr[i]), int(mss[i]),
                                      int(fl[i]), stride)
@@ -634,16 +642,18 @@ def test_tso_segment_random_vs_oracle():
             assert ol[g + j] == len(segs[j])
             slot = out[(g + j) * stride: (g + j + 1) * stride]
             assert slot[: len(segs[j])].tobytes() == segs[j], (i, j)
-            assert not slot[len(segs[j]):].any(), (i, j)
+            assert np.array_equal(slot[len(segs[j]):], fill[(g + j) * stride + len(segs[j]): (g + j + 1) * stride]), (i, j)
         assert oc[g: g + max(k, 0)].tolist() == cs
 
 
-def test_tso_segment_several_frames_per_wave():
+@pytest.mark.parametrize("stride,fill_seed", [(1600, None), (1531, 5)])
+def test_tso_segment_several_frames_per_wave(stride, fill_seed):
     """16384 frames, so each of the kernel's waves (at most 4096) walks about
     four and the next frame's loads overlap this frame's segments: staged frames
     (0..1500 B) mixed with unstaged ones (9300..9800 B, TSO mss 1448), invalid
     mss, too many segments, frames that do not fit their slot, VLAN variants;
-    every segment vs the oracle and slot tails untouched."""
+    every segment vs the oracle and slot tails untouched (zeros, or random
+    bytes with a stride that is not a multiple of 16)."""
     rng = np.random.default_rng(16)
     n = 16384
     big = rng.random(n) < 0.1
@@ -663,8 +673,9 @@ def test_tso_segment_several_frames_per_wave():
           | rng.choice([0, sna.SEG_VLAN_INSERT, sna.SEG_VLAN_STRIP | sna.SEG_VLAN_PRESENT,
                         sna.SEG_VLAN_INSERT | sna.SEG_VLAN_STRIP], n)
           | rng.integers(0, 65536, n))
-    stride = 1600
-    cnt, base, out, ol, oc = gpu_tso_segment(frames, sna.desc_pack(offs, lens), hdr, mss, fl, stride)
+    cnt, base, out, ol, oc = gpu_tso_segment(frames, sna.desc_pack(offs, lens), hdr, mss, fl, stride, fill_seed)
+    fill = (np.zeros(out.size, np.uint8) if fill_seed is None
+            else np.random.default_rng(fill_seed).integers(0, 256, out.size, dtype=np.uint8))
     segs_seen = 0
     for i in range(n):
         k, segs, cs = po.tso_segment(frames[offs[i]: offs[i] + lens[i]].tobytes(), int(hdr[i]), int(mss[i]),
@@ -675,7 +686,7 @@ def test_tso_segment_several_frames_per_wave():
             assert ol[g + j] == len(segs[j])
             slot = out[(g + j) * stride: (g + j + 1) * stride]
             assert slot[: len(segs[j])].tobytes() == segs[j], (i, j)
-            assert not slot[len(segs[j]):].any(), (i, j)
+            assert np.array_equal(slot[len(segs[j]):], fill[(g + j) * stride + len(segs[j]): (g + j + 1) * stride]), (i, j)
         assert oc[g: g + max(k, 0)].tolist() == cs
         segs_seen += max(k, 0)
     assert segs_seen > n
@@ -695,7 +706,8 @@ def test_tso_segment_c5_vs_oracle():
                                     sna.SEG_VLAN_INSERT | sna.SEG_VLAN_STRIP], n) | rng.integers(0, 65536, n))
     desc = sna.desc_pack(offs, lens)
     stride = 1536
-    cnt, base, out, ol, oc = gpu_tso_segment(frames, desc, hdr, mss, fl, stride)
+    cnt, base, out, ol, oc = gpu_tso_segment(frames, desc, hdr, mss, fl, stride, fill_seed=9)
+    fill = np.random.default_rng(9).integers(0, 256, out.size, dtype=np.uint8)
     for i in range(0, n, 7):
         k, segs, cs = po.tso_segment(frames[offs[i]: offs[i] + 9000].tobytes(), int(hdr[i]), int(mss[i]), int(fl[i]),
                                      stride)
@@ -704,4 +716,6 @@ def test_tso_segment_c5_vs_oracle():
         for j in range(k):
             assert ol[g + j] == len(segs[j])
             assert out[(g + j) * stride: (g + j) * stride + len(segs[j])].tobytes() == segs[j]
+            lo, hi = (g + j) * stride + len(segs[j]), (g + j + 1) * stride
+            assert np.array_equal(out[lo:hi], fill[lo:hi])
         assert oc[g:g + k].tolist() == cs
