@@ -1,0 +1,74 @@
+"""Summarise scripts/gpu_rows_prof.sh: for every §8 row, the row's dominant
+kernel (largest total time in its rocprofv3 kernel-trace stats), its average
+launch duration there, the HIP-event timing bench_rows.py printed in the same
+run, and its HBM traffic per launch from the FETCH_SIZE / WRITE_SIZE passes
+(gfx950 correction as tools/pmc_summary.py: read bytes = 2 x FETCH_SIZE x 1024,
+written = WRITE_SIZE x 1024) against the row's algorithmic bytes.
+
+  python tools/rows_prof_summary.py gpurun_out/rows_prof TAG > profiles/TAG_rows_prof.json
+"""
+
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+
+def top_kernel(stats_csv):
+    rows = list(csv.DictReader(open(stats_csv)))
+    rows.sort(key=lambda r: float(r["TotalDurationNs"]), reverse=True)
+    r = rows[0]
+    return r["Name"], int(r["Calls"]), float(r["AverageNs"]) / 1e3, [
+        {"kernel": x["Name"][:120], "calls": int(x["Calls"]), "avg_us": round(float(x["AverageNs"]) / 1e3, 2)}
+        for x in rows[:6]]
+
+
+def per_dispatch_median(counter_csv, counter, kernel):
+    vals = {}
+    for r in csv.DictReader(open(counter_csv)):
+        if r["Counter_Name"] != counter or r["Kernel_Name"] != kernel:
+            continue
+        vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return statistics.median(vals.values()) if vals else None
+
+
+def main():
+    root, tag = sys.argv[1], sys.argv[2]
+    out = {"what": "every §8 row's dominant kernel under rocprofv3 (scripts/gpu_rows_prof.sh): kernel-trace "
+                   "average beside bench_rows.py's HIP-event timing of the same run, and HBM traffic per launch "
+                   "(2 x FETCH_SIZE + WRITE_SIZE, KiB -> B; separate --pmc passes) over the algorithmic bytes",
+           "rows": []}
+    for d in sorted(glob.glob(os.path.join(root, "kt_*"))):
+        row = os.path.basename(d)[3:]
+        stats = os.path.join(d, f"{tag}_kernel_stats.csv")
+        if not os.path.exists(stats):
+            continue
+        kernel, calls, avg_us, top = top_kernel(stats)
+        rec = {"row": row, "kernel": kernel[:160], "calls": calls, "rocprof_avg_us": round(avg_us, 2), "top": top}
+        bj = os.path.join(root, f"{row}.json")
+        if os.path.exists(bj):
+            lines = [json.loads(l) for l in open(bj) if l.startswith("{")]
+            if lines and "alg_bytes_per_launch" in lines[0]:
+                b = lines[0]
+                rec.update({"hip_event_region_us": b.get("us_region_avg"), "hip_event_median_us": b.get("us_median"),
+                            "alg_bytes_per_launch": b["alg_bytes_per_launch"]})
+        f = os.path.join(root, f"FETCH_SIZE_{row}", f"{tag}_counter_collection.csv")
+        w = os.path.join(root, f"WRITE_SIZE_{row}", f"{tag}_counter_collection.csv")
+        if os.path.exists(f) and os.path.exists(w):
+            fk = per_dispatch_median(f, "FETCH_SIZE", kernel)
+            wk = per_dispatch_median(w, "WRITE_SIZE", kernel)
+            if fk is not None and wk is not None:
+                traffic = int(2 * fk * 1024 + wk * 1024)
+                rec.update({"fetch_size_kb": fk, "write_size_kb": wk, "hbm_bytes_per_launch": traffic})
+                if rec.get("alg_bytes_per_launch"):
+                    rec["traffic_over_alg"] = round(traffic / rec["alg_bytes_per_launch"], 4)
+                    rec["alg_GBps_rocprof"] = round(rec["alg_bytes_per_launch"] / (avg_us * 1e3), 1)
+                    rec["frac_of_8TBps_rocprof"] = round(rec["alg_bytes_per_launch"] / (avg_us * 1e3) / 8000.0, 4)
+        out["rows"].append(rec)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
