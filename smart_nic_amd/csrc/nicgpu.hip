@@ -2889,6 +2889,62 @@ __global__ __launch_bounds__(kQpBlock) void qp_keys_kernel(const uint16_t* __res
     key[k] = k < m ? (uint32_t) q[k] : nq;
 }
 
+// Dispatch lists for tables of fewer than 64 queues: a stable counting sort
+// of the keys (queue of each delivered frame, nq for entries past *count) in
+// 64-entry tiles, one wave per tile.  qp_gcount_kernel writes each tile's
+// per-key counts in key-major order (cnt[key * T + tile], plus a trailing 0);
+// their exclusive scan is every (key, tile)'s first output slot, and
+// qp_gscatter_kernel adds each entry's rank among the tile's entries of its
+// key (ballot + mbcnt) — the order radix sort keeps, in 4 launches instead of
+// rocprim's ~20 merge-sort passes (128 of ~1020 us of kernels per 1 M batch).
+__global__ __launch_bounds__(kQpBlock) void qp_gcount_kernel(const uint16_t* __restrict__ q,
+                                                             const unsigned long long* __restrict__ count,
+                                                             uint64_t nrx, uint32_t nq, uint64_t T, uint32_t* cnt) {
+  const uint64_t m = *count;
+  const uint32_t lane = lane_id();
+  const uint64_t waves = (uint64_t) gridDim.x * (kQpBlock / kWave);
+  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(uint64_t) (nq + 1) * T] = 0u;
+  for (uint64_t t = (uint64_t) blockIdx.x * (kQpBlock / kWave) + threadIdx.x / kWave; t < T; t += waves) {
+    const uint64_t k = t * kWave + lane;
+    const uint32_t key = k < nrx ? (k < m && q[k] < nq ? (uint32_t) q[k] : nq) : nq + 1u;
+    uint32_t mine = 0;
+    for (uint32_t b = 0; b <= nq; ++b) {
+      const uint32_t c = (uint32_t) __builtin_popcountll(__ballot(key == b));
+      if (lane == b) mine = c;
+    }
+    if (lane <= nq) cnt[(uint64_t) lane * T + t] = mine;
+  }
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_gscatter_kernel(const uint16_t* __restrict__ q,
+                                                               const unsigned long long* __restrict__ count,
+                                                               uint64_t nrx, uint32_t nq, uint64_t T,
+                                                               const uint32_t* __restrict__ off,
+                                                               const uint32_t* __restrict__ which, uint32_t* out,
+                                                               uint32_t* start, uint32_t* end) {
+  const uint64_t m = *count;
+  const uint32_t lane = lane_id();
+  const uint64_t waves = (uint64_t) gridDim.x * (kQpBlock / kWave);
+  const uint64_t gt = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x;
+  if (gt < nq) {  // queue gt's range; an empty queue keeps start = end = 0
+    const uint32_t a = off[gt * T], b = off[(gt + 1) * T];
+    if (b > a) {
+      start[gt] = a;
+      end[gt] = b;
+    }
+  }
+  for (uint64_t t = (uint64_t) blockIdx.x * (kQpBlock / kWave) + threadIdx.x / kWave; t < T; t += waves) {
+    const uint64_t k = t * kWave + lane;
+    const uint32_t key = k < nrx ? (k < m && q[k] < nq ? (uint32_t) q[k] : nq) : nq + 1u;
+    uint32_t rank = 0;
+    for (uint32_t b = 0; b <= nq; ++b) {
+      const uint64_t v = __ballot(key == b);
+      if (key == b) rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (v >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) v, 0u));
+    }
+    if (k < nrx) out[off[(uint64_t) key * T + t] + rank] = which[k];
+  }
+}
+
 // queue range boundaries of the first *count sorted keys, for queues below nq
 __global__ __launch_bounds__(kQpBlock) void qp_bounds_kernel(const uint32_t* __restrict__ key,
                                                              const unsigned long long* __restrict__ count,
@@ -3221,6 +3277,23 @@ int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream) {
     if (st == NICGPU_OK) st = hip_status(hipMemsetAsync(q->queue_end, 0, nq * sizeof(uint32_t), s));
   }
   if (st != NICGPU_OK || nrx == 0) return st;
+  if (nq < kWave) {  // counting sort: counts in sort_key, their scan in sorted_key (both hold nrx + 64)
+    const uint64_t T = (nrx + kWave - 1) / kWave;
+    const uint64_t nc = (uint64_t) (nq + 1) * T + 1;
+    st = qp_grow(q->sort_key, q->c_key, nc);
+    if (st == NICGPU_OK) st = qp_grow(q->sorted_key, q->c_sk, nc);
+    if (st != NICGPU_OK) return st;
+    const unsigned grid = qp_grid(q, nrx > nq ? nrx : nq);
+    hipLaunchKernelGGL(qp_gcount_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->rss_queue, q->scal + 3, (uint64_t) nrx,
+                       (uint32_t) nq, T, q->sort_key);
+    st = hip_status(hipGetLastError());
+    if (st == NICGPU_OK) st = qp_scan(q, q->sort_key, q->sorted_key, nc, s);
+    if (st != NICGPU_OK) return st;
+    hipLaunchKernelGGL(qp_gscatter_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->rss_queue, q->scal + 3,
+                       (uint64_t) nrx, (uint32_t) nq, T, q->sorted_key, q->which, q->queue_which, q->queue_start,
+                       q->queue_end);
+    return hip_status(hipGetLastError());
+  }
   hipLaunchKernelGGL(qp_keys_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->rss_queue, q->scal + 3,
                      (uint64_t) nrx, (uint32_t) nq, q->sort_key);
   st = hip_status(hipGetLastError());

@@ -178,7 +178,10 @@ int run_case(std::uint64_t seed) {
   image.assign(mem_size, 0);
   for (auto& [a, p] : pkts) std::memcpy(image.data() + a, p.data(), p.size());
   std::vector<std::uint16_t> table(r.below(2) ? 128 : 1 + r.below(300));
-  for (auto& q : table) q = static_cast<std::uint16_t>(r.below(16));
+  // mostly < 64 queues (the dispatch lists' counting sort), one batch in four
+  // up to 300 (the radix-sort path)
+  const std::uint64_t queues = r.below(4) == 0 ? 300 : 1 + r.below(63);
+  for (auto& q : table) q = static_cast<std::uint16_t>(r.below(queues));
   const RssConfig rss_cfg{r.below(2) ? kMsKey : std::vector<std::uint8_t>{}, table};
   const std::uint16_t qid = static_cast<std::uint16_t>(r.below(8));
 
