@@ -2778,7 +2778,9 @@ __global__ __launch_bounds__(kQpBlock) void qp_fill_kernel(const nicgpu_tx_descr
   }
 }
 
-__global__ __launch_bounds__(kQpBlock) void qp_need_kernel(QpCtx C, uint64_t n, uint32_t* need) {
+__global__ __launch_bounds__(kQpBlock) void qp_need_kernel(QpCtx C, uint64_t n, uint32_t* need,
+                                                           unsigned long long* scal) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) scal[0] = n;  // the first relaxation step's "nothing changed"
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i <= n; i += (uint64_t) gridDim.x * kQpBlock)
     need[i] = i < n ? nicqp::rx_need(C, i) : 0u;
 }
@@ -2926,12 +2928,10 @@ __global__ __launch_bounds__(kQpBlock) void qp_gscatter_kernel(const uint16_t* _
   const uint32_t lane = lane_id();
   const uint64_t waves = (uint64_t) gridDim.x * (kQpBlock / kWave);
   const uint64_t gt = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x;
-  if (gt < nq) {  // queue gt's range; an empty queue keeps start = end = 0
+  if (gt < nq) {  // queue gt's range; an empty queue gets start = end = 0
     const uint32_t a = off[gt * T], b = off[(gt + 1) * T];
-    if (b > a) {
-      start[gt] = a;
-      end[gt] = b;
-    }
+    start[gt] = b > a ? a : 0u;
+    end[gt] = b > a ? b : 0u;
   }
   for (uint64_t t = (uint64_t) blockIdx.x * (kQpBlock / kWave) + threadIdx.x / kWave; t < T; t += waves) {
     const uint64_t k = t * kWave + lane;
@@ -3214,14 +3214,15 @@ int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, u
   QpCtx C{queue_id, max_mtu, mem_size, q->plans, q->piece_csum, q->tx, q->rx, (uint64_t) nrx};
   const unsigned grid = qp_grid(q, ntx + 1);
   // first guess: every packet pops what it needs (rx_need), then relax
-  hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, (uint64_t) ntx, q->need);
+  hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, (uint64_t) ntx, q->need, q->scal);
   int st = hip_status(hipGetLastError());
   uint64_t lim = 0;
   unsigned long long first = 0;
   for (int it = 0; st == NICGPU_OK; ++it) {
     st = qp_scan(q, q->need, q->pos, ntx + 1, s);
-    const unsigned long long init = (unsigned long long) ntx;
-    if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->scal, &init, sizeof(init), hipMemcpyHostToDevice, s));
+    const unsigned long long init = (unsigned long long) ntx;  // step 0's was set by qp_need_kernel
+    if (st == NICGPU_OK && it > 0)
+      st = hip_status(hipMemcpyAsync(q->scal, &init, sizeof(init), hipMemcpyHostToDevice, s));
     if (st != NICGPU_OK) break;
     hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, (uint64_t) ntx, q->scal);
     st = hip_status(hipGetLastError());
@@ -3272,7 +3273,7 @@ int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream) {
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   int st = NICGPU_OK;
-  if (nq) {
+  if (nq && (nq >= kWave || nrx == 0)) {  // the counting sort writes every queue's bounds itself
     st = hip_status(hipMemsetAsync(q->queue_start, 0, nq * sizeof(uint32_t), s));
     if (st == NICGPU_OK) st = hip_status(hipMemsetAsync(q->queue_end, 0, nq * sizeof(uint32_t), s));
   }
