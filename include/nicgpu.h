@@ -348,6 +348,13 @@ int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int
  * piece buffers may grow). */
 int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
                    uint64_t* npieces, nicgpu_qp_view* view, void* stream);
+/* nicgpu_qp_plan with the plan (which reads only view.tx) on plan_stream,
+ * waited for once, and the piece checksums (which read the image) enqueued on
+ * sums_stream behind it.  A batched stage plans batch k+1 on a side stream
+ * while batch k's DMA writes, which may write bytes batch k+1 sends, still run
+ * on the main one. */
+int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
+                      uint64_t* npieces, nicgpu_qp_view* view, void* plan_stream, void* sums_stream);
 /* The reference's control flow over view.tx[0, ntx) against view.rx[0, nrx)
  * from the piece sums: TX descriptors [0, *done) are resolved, with
  * completions in view.txc[0, *done) and view.rxc[0, *rx_used), their writes in

@@ -1,6 +1,6 @@
-# Same-box A/B of the f1 stage: smart_nic_amd/ab/libnicgpu.so (A, built from
-# HEAD's nicgpu.hip by scripts/ab_build.sh and moved there) against the working
-# tree's libnicgpu.so (B), alternating processes; the RX-stage GPU tests first.
+# Same-box A/B of the f1 stage: smart_nic_amd/ab/{libnicgpu,libnic_host}.so (A,
+# built from HEAD in a git worktree) against the working tree's libraries (B),
+# alternating processes (LD_LIBRARY_PATH beats the driver's RUNPATH); the RX-stage GPU tests first.
 set -o pipefail
 mkdir -p gpurun_out
 PT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"

@@ -77,6 +77,7 @@ ABI_SYMBOLS = (
     "nicgpu_qp_destroy",
     "nicgpu_qp_reserve",
     "nicgpu_qp_plan",
+    "nicgpu_qp_plan_on",
     "nicgpu_qp_check",
     "nicgpu_qp_resolve",
     "nicgpu_qp_rss_list",
@@ -125,6 +126,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_qp_destroy": (i32, [vp]),
         "nicgpu_qp_reserve": (i32, [vp, sz, sz, vp]),
         "nicgpu_qp_plan": (i32, [vp, vp, ctypes.c_uint64, sz, ctypes.c_uint64, vp, vp, vp]),
+        "nicgpu_qp_plan_on": (i32, [vp, vp, ctypes.c_uint64, sz, ctypes.c_uint64, vp, vp, vp, vp]),
         "nicgpu_qp_check": (i32, [vp, ctypes.c_uint64, sz, sz, vp, vp]),
         "nicgpu_qp_resolve": (i32, [vp, ctypes.c_uint64, sz, sz, ctypes.c_uint64, ctypes.c_uint16, vp, vp, vp, vp]),
         "nicgpu_qp_rss_list": (i32, [vp, sz, vp]),

@@ -960,6 +960,7 @@ struct BatchedQueuePair::Slot {
   void* ev_rx = nullptr;     // RX descriptors uploaded
   void* ev_resolved = nullptr;  // completions final
   void* ev_done = nullptr;      // DMA writes and RSS done
+  void* ev_submit = nullptr;    // the caller's stream when device descriptors were handed over
   DevBuf hits;               // per-table-index RSS hits of the batch
   HostBuf h_meta, h_lists;   // pinned landing space of the downloads
   SideWorker worker;         // issues the downloads
@@ -1008,14 +1009,15 @@ struct BatchedQueuePair::Slot {
     wait();
     up.reset();
     if (qp) (void) nicgpu_qp_destroy(qp);
-    for (void* e : {ev_tx, ev_rx, ev_resolved, ev_done})
+    for (void* e : {ev_tx, ev_rx, ev_resolved, ev_done, ev_submit})
       if (e) (void) nicgpu_event_destroy(e);
     qp = nullptr;
-    ev_tx = ev_rx = ev_resolved = ev_done = nullptr;
+    ev_tx = ev_rx = ev_resolved = ev_done = ev_submit = nullptr;
   }
   void create(int dev) {
     check(nicgpu_qp_create(&qp, dev), "nicgpu_qp_create");
-    for (void** e : {&ev_tx, &ev_rx, &ev_resolved, &ev_done}) check(nicgpu_event_create(e), "nicgpu_event_create");
+    for (void** e : {&ev_tx, &ev_rx, &ev_resolved, &ev_done, &ev_submit})
+      check(nicgpu_event_create(e), "nicgpu_event_create");
   }
   ~Slot() { release(); }
 };
@@ -1030,6 +1032,7 @@ struct BatchedQueuePair::Scratch {
   int device = -1;
   void* side_up = nullptr;
   void* side_down = nullptr;
+  void* side_plan = nullptr;  // plan and overlap check of a batch beside the earlier batch's writes
   SideWorker up_worker;  // process_batch: issues the RX descriptor uploads
   static constexpr unsigned kSlots = 3;
   Slot slot[kSlots];
@@ -1039,7 +1042,8 @@ struct BatchedQueuePair::Scratch {
     for (Slot& sl : slot) sl.release();
     if (side_up) (void) nicgpu_stream_destroy(side_up);
     if (side_down) (void) nicgpu_stream_destroy(side_down);
-    side_up = side_down = nullptr;
+    if (side_plan) (void) nicgpu_stream_destroy(side_plan);
+    side_up = side_down = side_plan = nullptr;
     device = -1;
   }
   void ensure(int dev) {
@@ -1047,6 +1051,7 @@ struct BatchedQueuePair::Scratch {
     release();
     check(nicgpu_stream_create(&side_up), "nicgpu_stream_create");
     check(nicgpu_stream_create(&side_down), "nicgpu_stream_create");
+    check(nicgpu_stream_create(&side_plan), "nicgpu_stream_create");
     for (Slot& sl : slot) sl.create(dev);
     device = dev;
   }
@@ -1251,6 +1256,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDe
   sl.ntx_dev = d.ntx;
   sl.nrx_dev = d.nrx;
   sl.fetched = false;
+  check(nicgpu_event_record(sl.ev_submit, stream), "nicgpu_event_record");  // a producer's writes before this call
   QueuePairStats st = stats_;
   int disjoint = -1;
   double check_us = 0;
@@ -1326,6 +1332,7 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
   // device work (device descriptors are copied in the job, in stream order);
   // the rest runs in submission order on the job thread
   if (device && !d) upload(sl, tx, rx, false);
+  if (device && d) check(nicgpu_event_record(sl.ev_submit, stream), "nicgpu_event_record");
   sl.job_done = std::promise<void>();
   sl.job = sl.job_done.get_future();
   auto run = [this, &sl, device, dev] {
@@ -1422,31 +1429,49 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   const std::size_t ntx = dev_desc ? sl.ntx_dev : tx.size(), nrx = dev_desc ? sl.nrx_dev : rx.size();
   nicgpu_qp_view& v = sl.v;
   auto t = clock::now();
-  if (dev_desc) {  // device descriptors: copied in stream order (they may sit in the image)
+  // The plan and the overlap check read descriptors only, so they run on the
+  // side stream `ps` — beside the earlier batches' DMA writes and RSS still on
+  // `stream` — unless the descriptors are device arrays inside the image
+  // (those writes may change them: copied in stream order).  The piece sums
+  // read the image and stay on `stream`.
+  auto inside = [&](const void* p, std::size_t bytes) {
+    const auto a = reinterpret_cast<std::uintptr_t>(p), b = reinterpret_cast<std::uintptr_t>(mem.base);
+    return bytes && a < b + mem.size && b < a + bytes;
+  };
+  const bool side = !dev_desc || (!inside(sl.tx_dev, ntx * sizeof(TxDescriptor)) &&
+                                  !inside(sl.rx_dev, nrx * sizeof(RxDescriptor)));
+  void* ps = side ? S.side_plan : stream;
+  if (dev_desc) {
     check(nicgpu_qp_reserve(sl.qp, ntx, nrx, &v), "nicgpu_qp_reserve");
-    if (ntx) check(nicgpu_memcpy_async(v.tx, sl.tx_dev, ntx * sizeof(TxDescriptor), stream), "nicgpu_memcpy_async");
-    if (nrx) check(nicgpu_memcpy_async(v.rx, sl.rx_dev, nrx * sizeof(RxDescriptor), stream), "nicgpu_memcpy_async");
+    // after whatever the caller enqueued on `stream` before handing them over
+    if (side) check(nicgpu_stream_wait_event(ps, sl.ev_submit), "nicgpu_stream_wait_event");
+    if (ntx) check(nicgpu_memcpy_async(v.tx, sl.tx_dev, ntx * sizeof(TxDescriptor), ps), "nicgpu_memcpy_async");
+    if (nrx) check(nicgpu_memcpy_async(v.rx, sl.rx_dev, nrx * sizeof(RxDescriptor), ps), "nicgpu_memcpy_async");
   } else {
     out.timings.copy_us += sl.upload_us;
-    check(nicgpu_stream_wait_event(stream, sl.ev_tx), "nicgpu_stream_wait_event");
+    check(nicgpu_stream_wait_event(ps, sl.ev_tx), "nicgpu_stream_wait_event");
   }
   std::uint64_t np = 0;
-  check(nicgpu_qp_plan(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &np, &v,
-                       stream),
-        "nicgpu_qp_plan");
+  check(nicgpu_qp_plan_on(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &np,
+                          &v, ps, stream),
+        "nicgpu_qp_plan_on");
   out.timings.sums_us += us_since(t);
   t = clock::now();
   if (sl.up) {
     sl.up->finish();
     sl.up.reset();
   }
-  if (!dev_desc) check(nicgpu_stream_wait_event(stream, sl.ev_rx), "nicgpu_stream_wait_event");
+  if (!dev_desc) {
+    check(nicgpu_stream_wait_event(ps, sl.ev_rx), "nicgpu_stream_wait_event");
+    if (side) check(nicgpu_stream_wait_event(stream, sl.ev_rx), "nicgpu_stream_wait_event");
+  }
   out.timings.copy_us += us_since(t);
   // overlapping buffers go to the host path before anything is written; a
-  // ring whose RX buffers are not in ascending address order is sorted there
+  // ring whose RX buffers are not in ascending address order is sorted there.
+  // The check synchronises `ps`: the descriptors are then in place for `stream`.
   t = clock::now();
   int verdict = -1;
-  check(nicgpu_qp_check(sl.qp, mem.size, ntx, nrx, &verdict, stream), "nicgpu_qp_check");
+  check(nicgpu_qp_check(sl.qp, mem.size, ntx, nrx, &verdict, ps), "nicgpu_qp_check");
   if (verdict < 0) {
     const auto [htx, hrx] = host_spans(sl, tx, rx, stream);
     verdict = buffers_disjoint(mem.size, htx, hrx) ? 1 : 0;

@@ -3036,6 +3036,7 @@ struct nicgpu_qp {
   uint8_t* tmp = nullptr;
   uint64_t host_scal[4] = {0, 0, 0, 0};
   unsigned grid = 1;
+  hipEvent_t planned = nullptr;  // nicgpu_qp_plan_on: the piece descriptors are written
 };
 
 namespace {
@@ -3096,6 +3097,10 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
   }
+  if (hipEventCreateWithFlags(&q->planned, hipEventDisableTiming) != hipSuccess) {
+    nicgpu_qp_destroy(q);
+    return NICGPU_ERR_HIP;
+  }
   *out = q;
   return NICGPU_OK;
 }
@@ -3109,6 +3114,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
                   q->queue_start, q->queue_end, q->end_max};
   for (void* b : bufs)
     if (b) (void) hipFree(b);
+  if (q->planned) (void) hipEventDestroy(q->planned);
   delete q;
   return NICGPU_OK;
 }
@@ -3150,10 +3156,15 @@ int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view
 
 int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
                    uint64_t* npieces, nicgpu_qp_view* view, void* stream) {
+  return nicgpu_qp_plan_on(q, mem, mem_size, ntx, max_mtu, npieces, view, stream, stream);
+}
+
+int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
+                      uint64_t* npieces, nicgpu_qp_view* view, void* plan_stream, void* sums_stream) {
   if (!q || !npieces || ntx > q->cap_tx) return NICGPU_ERR_INVALID;
   if (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0)) return NICGPU_ERR_INVALID;
   DeviceGuard g(q->device);
-  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipStream_t s = static_cast<hipStream_t>(plan_stream);
   *npieces = 0;
   const unsigned grid = qp_grid(q, ntx + 1);
   hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
@@ -3170,7 +3181,11 @@ int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t n
   hipLaunchKernelGGL(qp_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
                      q->plans, q->base, q->piece_desc);
   st = hip_status(hipGetLastError());
-  if (st == NICGPU_OK && np) st = nicgpu_checksum_batch(mem, q->piece_desc, np, q->piece_csum, stream);
+  if (st == NICGPU_OK && sums_stream != plan_stream) {  // the sums read the pieces the fill wrote
+    st = hip_status(hipEventRecord(q->planned, s));
+    if (st == NICGPU_OK) st = hip_status(hipStreamWaitEvent(static_cast<hipStream_t>(sums_stream), q->planned, 0));
+  }
+  if (st == NICGPU_OK && np) st = nicgpu_checksum_batch(mem, q->piece_desc, np, q->piece_csum, sums_stream);
   *npieces = np;
   qp_fill_view(q, view);
   return st;

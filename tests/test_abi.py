@@ -116,6 +116,7 @@ def test_batch_entry_points_validate_before_device_access():
     assert lib.nicgpu_qp_destroy(None) == INV
     assert lib.nicgpu_qp_reserve(None, 1, 1, p) == INV
     assert lib.nicgpu_qp_plan(None, p, 64, 1, 9000, p, p, None) == INV
+    assert lib.nicgpu_qp_plan_on(None, p, 64, 1, 9000, p, p, None, None) == INV
     # streams and events: null handles -> INVALID (no device touched)
     assert lib.nicgpu_stream_create(None) == INV
     assert lib.nicgpu_stream_destroy(None) == INV
