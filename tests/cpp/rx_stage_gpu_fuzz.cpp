@@ -473,23 +473,44 @@ int run_pipeline(std::uint64_t seed) {
   const bool dev_desc = seed & 1;
   std::vector<DeviceDescriptors> dd(nb);
   void* d_desc = nullptr;
+  // The descriptors are written to dd[] by a device-to-device copy enqueued on
+  // the caller's stream just before each hand-over (a device-side producer),
+  // from a staged copy; dd[] starts zeroed, so a stage that read them before
+  // that copy landed would see empty rings.
+  void* d_src = nullptr;
+  std::size_t desc_bytes = 0;
   if (dev_desc) {
     std::size_t bytes = 0;
     for (int b = 0; b < nb; ++b) bytes += txs[b].size() * sizeof(TxDescriptor) + rxs[b].size() * sizeof(RxDescriptor);
+    desc_bytes = bytes;
     assert(nicgpu_malloc(&d_desc, bytes + 64) == NICGPU_OK);
-    std::byte* p = static_cast<std::byte*>(d_desc);
+    assert(nicgpu_malloc(&d_src, bytes + 64) == NICGPU_OK);
+    std::byte* p = static_cast<std::byte*>(d_src);
     for (int b = 0; b < nb; ++b) {
       assert(nicgpu_memcpy_async(p, txs[b].data(), txs[b].size() * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
-      dd[b].tx = reinterpret_cast<const TxDescriptor*>(p);
+      dd[b].tx = reinterpret_cast<const TxDescriptor*>(static_cast<std::byte*>(d_desc) + (p - static_cast<std::byte*>(d_src)));
       dd[b].ntx = txs[b].size();
       p += txs[b].size() * sizeof(TxDescriptor);
       assert(nicgpu_memcpy_async(p, rxs[b].data(), rxs[b].size() * sizeof(RxDescriptor), nullptr) == NICGPU_OK);
-      dd[b].rx = reinterpret_cast<const RxDescriptor*>(p);
+      dd[b].rx = reinterpret_cast<const RxDescriptor*>(static_cast<std::byte*>(d_desc) + (p - static_cast<std::byte*>(d_src)));
       dd[b].nrx = rxs[b].size();
       p += rxs[b].size() * sizeof(RxDescriptor);
     }
+    assert(nicgpu_memset_async(d_desc, 0, bytes + 64, nullptr) == NICGPU_OK);
     assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
   }
+  // a slow producer: ~0.1 ms of other work on the stream ahead of the copy
+  constexpr std::size_t kBusy = std::size_t{512} << 20;
+  void* d_busy = nullptr;
+  if (dev_desc) assert(nicgpu_malloc(&d_busy, kBusy) == NICGPU_OK);
+  auto produce = [&](int b) {  // the producer: batch b's descriptors into dd[b], on the caller's stream
+    assert(nicgpu_memset_async(d_busy, b & 0xFF, kBusy, nullptr) == NICGPU_OK);
+    const std::size_t at = reinterpret_cast<const std::byte*>(dd[b].tx) - static_cast<std::byte*>(d_desc);
+    const std::size_t len = dd[b].ntx * sizeof(TxDescriptor) + dd[b].nrx * sizeof(RxDescriptor);
+    if (len) assert(nicgpu_memcpy_async(static_cast<std::byte*>(d_desc) + at, static_cast<std::byte*>(d_src) + at, len,
+                                        nullptr) == NICGPU_OK);
+  };
+  (void) desc_bytes;
   RxBatchResult out;
   for (int b = 0; b < nb; ++b) {
     while (pipe.pending() == 3 || (pipe.pending() > 0 && r.below(3) == 0)) {
@@ -501,11 +522,13 @@ int run_pipeline(std::uint64_t seed) {
     if (!dev_desc) {
       pipe.submit(m_pipe, txs[b], rxs[b]);
     } else if (pipe.pending() == 0 && r.below(3) == 0) {
+      produce(b);
       pipe.process_batch(m_pipe, dd[b], out);
       if (keep) view_ok &= materialize(out);
       got.push_back(std::move(out));
       out = RxBatchResult{};
     } else {
+      produce(b);
       pipe.submit(m_pipe, dd[b]);
     }
   }
@@ -537,6 +560,8 @@ int run_pipeline(std::uint64_t seed) {
   nicgpu_free(d_seq);
   nicgpu_free(d_pipe);
   if (d_desc) nicgpu_free(d_desc);
+  if (d_src) nicgpu_free(d_src);
+  if (d_busy) nicgpu_free(d_busy);
   if (!ok) {
     std::fprintf(stderr, "pipeline seed %llu: pipelined run differs from process_batch in order\n",
                  (unsigned long long) seed);
