@@ -13,7 +13,9 @@ g++ -std=c++20 -O2 -Iinclude tools/bench_rx_stage.cpp -Lsmart_nic_amd -lnic_host
 for i in 1 2 3; do
   for side in A B; do
     if [ $side = A ]; then export LD_LIBRARY_PATH=$PWD/smart_nic_amd/ab; else unset LD_LIBRARY_PATH; fi
-    for mode in "1024 12 0 device pinned pipelined" "65536 9 0 device pinned sync" "1048576 12 0 device device pipelined device" "1048576 9 0 device device sync device"; do
+    if [ "${MODESET:-}" = pinned1m ]; then set -- "1048576 12 0 device pinned pipelined" "1048576 9 0 device pinned sync"
+    else set -- "1024 12 0 device pinned pipelined" "65536 9 0 device pinned sync" "1048576 12 0 device device pipelined device" "1048576 9 0 device device sync device"; fi
+    for mode in "$@"; do
       timeout -k 10 120 ./gpurun_out/bench_rx_stage c3 $mode 2>> gpurun_out/f1_ab.err | sed "s/^{/{\"side\": \"$side\", /" >> gpurun_out/f1_ab.jsonl || exit 1
     done
   done
