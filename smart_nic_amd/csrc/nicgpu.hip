@@ -2807,16 +2807,25 @@ __global__ __launch_bounds__(kQpBlock) void qp_relax_kernel(QpCtx C, uint32_t* p
   }
 }
 
-// packets [0, lim) at their (exact) positions: completions, writes, per-block stats
+// packets [0, lim) at their (exact) positions: completions, writes, per-block
+// stats.  With `guess` (the pops the positions were scanned from) the pass is
+// speculative: first[0] becomes the first packet that popped otherwise, and
+// only [0, first] is exact — all of it when nothing differed.
 __global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32_t* __restrict__ pos, uint64_t lim,
                                                            nicgpu_completion* txc, nicgpu_completion* rxc,
-                                                           nicgpu_segment_write* writes, uint64_t* partials) {
+                                                           nicgpu_segment_write* writes, uint64_t* partials,
+                                                           const uint32_t* __restrict__ guess,
+                                                           unsigned long long* first) {
   __shared__ uint64_t red[kQpStats][kQpBlock / kWave];
   nicgpu_qp_stats st{};
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < lim; i += (uint64_t) gridDim.x * kQpBlock) {
-    if (pos[i] > C.nrx) continue;  // exact positions never pass the ring's end (defensive)
+    if (pos[i] > C.nrx) {  // exact positions never pass the ring's end: a guess past it is wrong
+      if (guess) atomicMin(first, (unsigned long long) i);
+      continue;
+    }
     QpDevSink sink{txc, rxc, writes, i, pos[i]};
-    (void) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(C, i, pos[i], st, sink);
+    const uint32_t popped = (uint32_t) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(C, i, pos[i], st, sink);
+    if (guess && popped != guess[i]) atomicMin(first, (unsigned long long) i);
   }
   uint64_t v[kQpStats];
   static_assert(sizeof(nicgpu_qp_stats) == kQpStats * 8, "16 counters");
@@ -3228,37 +3237,48 @@ int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, u
   hipStream_t s = static_cast<hipStream_t>(stream);
   QpCtx C{queue_id, max_mtu, mem_size, q->plans, q->piece_csum, q->tx, q->rx, (uint64_t) nrx};
   const unsigned grid = qp_grid(q, ntx + 1);
-  // first guess: every packet pops what it needs (rx_need), then relax
+  // first guess: every packet pops what it needs (rx_need).  The final pass
+  // runs on it speculatively and reports the first packet that popped
+  // otherwise; a batch that settles at once (uniform RX descriptors, no early
+  // ends) is then resolved in one host round trip, without a relaxation step.
   hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, (uint64_t) ntx, q->need, q->scal);
   int st = hip_status(hipGetLastError());
-  uint64_t lim = 0;
-  unsigned long long first = 0;
-  for (int it = 0; st == NICGPU_OK; ++it) {
-    st = qp_scan(q, q->need, q->pos, ntx + 1, s);
-    const unsigned long long init = (unsigned long long) ntx;  // step 0's was set by qp_need_kernel
-    if (st == NICGPU_OK && it > 0)
-      st = hip_status(hipMemcpyAsync(q->scal, &init, sizeof(init), hipMemcpyHostToDevice, s));
-    if (st != NICGPU_OK) break;
-    hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, (uint64_t) ntx, q->scal);
-    st = hip_status(hipGetLastError());
-    if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&first, q->scal, sizeof(first), hipMemcpyDeviceToHost, s));
-    if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
-    if (st != NICGPU_OK) break;
-    // pos is exact up to and including `first` (pops before it agreed)
-    lim = first < ntx ? (uint64_t) first : (uint64_t) ntx;
-    if (first >= ntx || it + 1 == kQpRelaxSteps) break;
-  }
-  if (st != NICGPU_OK) return st;
-  hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, lim, q->txc, q->rxc, q->writes,
-                     q->partials);
-  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
   std::vector<uint64_t> part((size_t) grid * kQpStats);
   uint32_t used = 0;
-  if (st == NICGPU_OK)
-    st = hip_status(hipMemcpyAsync(part.data(), q->partials, part.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&used, q->pos + lim, sizeof(used), hipMemcpyDeviceToHost, s));
-  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  unsigned long long first = 0;
+  auto full = [&](uint64_t lim_, const uint32_t* guess) {
+    hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, lim_, q->txc, q->rxc, q->writes,
+                       q->partials, guess, q->scal);
+    int e = hip_status(hipGetLastError());
+    if (e == NICGPU_OK)
+      e = hip_status(hipMemcpyAsync(part.data(), q->partials, part.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    if (e == NICGPU_OK) e = hip_status(hipMemcpyAsync(&used, q->pos + lim_, sizeof(used), hipMemcpyDeviceToHost, s));
+    if (guess && e == NICGPU_OK) e = hip_status(hipMemcpyAsync(&first, q->scal, sizeof(first), hipMemcpyDeviceToHost, s));
+    if (e == NICGPU_OK) e = hip_status(hipStreamSynchronize(s));
+    return e;
+  };
+  if (st == NICGPU_OK) st = full((uint64_t) ntx, q->need);  // scal[0] = ntx from qp_need_kernel
   if (st != NICGPU_OK) return st;
+  uint64_t lim = (uint64_t) ntx;
+  if (first < ntx) {  // relax from the same guess (the speculative pass left `need` as it was)
+    for (int it = 0; st == NICGPU_OK; ++it) {
+      if (it > 0) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
+      const unsigned long long init = (unsigned long long) ntx;
+      if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->scal, &init, sizeof(init), hipMemcpyHostToDevice, s));
+      if (st != NICGPU_OK) break;
+      hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, (uint64_t) ntx, q->scal);
+      st = hip_status(hipGetLastError());
+      if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&first, q->scal, sizeof(first), hipMemcpyDeviceToHost, s));
+      if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+      if (st != NICGPU_OK) break;
+      // pos is exact up to and including `first` (pops before it agreed)
+      lim = first < ntx ? (uint64_t) first : (uint64_t) ntx;
+      if (first >= ntx || it + 1 == kQpRelaxSteps) break;
+    }
+    if (st == NICGPU_OK) st = full(lim, nullptr);
+    if (st != NICGPU_OK) return st;
+  }
   uint64_t sum[kQpStats] = {};
   for (unsigned b = 0; b < grid; ++b)
     for (unsigned k = 0; k < kQpStats; ++k) sum[k] += part[(size_t) b * kQpStats + k];
