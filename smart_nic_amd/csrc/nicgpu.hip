@@ -2779,8 +2779,8 @@ __global__ __launch_bounds__(kQpBlock) void qp_fill_kernel(const nicgpu_tx_descr
 }
 
 __global__ __launch_bounds__(kQpBlock) void qp_need_kernel(QpCtx C, uint64_t n, uint32_t* need,
-                                                           unsigned long long* scal) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) scal[0] = n;  // the first relaxation step's "nothing changed"
+                                                           unsigned long long* first) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *first = n;  // the speculative final pass's "nothing differed"
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i <= n; i += (uint64_t) gridDim.x * kQpBlock)
     need[i] = i < n ? nicqp::rx_need(C, i) : 0u;
 }
@@ -2814,9 +2814,13 @@ __global__ __launch_bounds__(kQpBlock) void qp_relax_kernel(QpCtx C, uint32_t* p
 __global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32_t* __restrict__ pos, uint64_t lim,
                                                            nicgpu_completion* txc, nicgpu_completion* rxc,
                                                            nicgpu_segment_write* writes, uint64_t* partials,
-                                                           const uint32_t* __restrict__ guess,
-                                                           unsigned long long* first) {
+                                                           const uint32_t* __restrict__ guess) {
   __shared__ uint64_t red[kQpStats][kQpBlock / kWave];
+  // after the per-block stats: [0] the RX descriptors used (pos[lim]), [1] the
+  // first mismatch (seeded with n by qp_need_kernel) — one download for all
+  uint64_t* tail = partials + (uint64_t) gridDim.x * kQpStats;
+  unsigned long long* first = reinterpret_cast<unsigned long long*>(tail + 1);
+  if (blockIdx.x == 0 && threadIdx.x == 0) tail[0] = pos[lim];
   nicgpu_qp_stats st{};
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < lim; i += (uint64_t) gridDim.x * kQpBlock) {
     if (pos[i] > C.nrx) {  // exact positions never pass the ring's end: a guess past it is wrong
@@ -3100,7 +3104,7 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
   q->device = device;
   q->grid = (unsigned) di.cus * 8u;
   if (hipMalloc(&q->scal, 4 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc(&q->partials, (size_t) q->grid * kQpStats * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&q->partials, ((size_t) q->grid * kQpStats + 2) * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&q->queue_start, 65536 * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&q->queue_end, 65536 * sizeof(uint32_t)) != hipSuccess) {
     nicgpu_qp_destroy(q);
@@ -3241,24 +3245,26 @@ int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, u
   // runs on it speculatively and reports the first packet that popped
   // otherwise; a batch that settles at once (uniform RX descriptors, no early
   // ends) is then resolved in one host round trip, without a relaxation step.
-  hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, (uint64_t) ntx, q->need, q->scal);
+  hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, (uint64_t) ntx, q->need,
+                     reinterpret_cast<unsigned long long*>(q->partials + (size_t) grid * kQpStats + 1));
   int st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
-  std::vector<uint64_t> part((size_t) grid * kQpStats);
-  uint32_t used = 0;
+  // per-block stats, then the RX descriptors used and the first mismatch
+  std::vector<uint64_t> part((size_t) grid * kQpStats + 2);
+  uint64_t used = 0;
   unsigned long long first = 0;
   auto full = [&](uint64_t lim_, const uint32_t* guess) {
     hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, lim_, q->txc, q->rxc, q->writes,
-                       q->partials, guess, q->scal);
+                       q->partials, guess);
     int e = hip_status(hipGetLastError());
     if (e == NICGPU_OK)
       e = hip_status(hipMemcpyAsync(part.data(), q->partials, part.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    if (e == NICGPU_OK) e = hip_status(hipMemcpyAsync(&used, q->pos + lim_, sizeof(used), hipMemcpyDeviceToHost, s));
-    if (guess && e == NICGPU_OK) e = hip_status(hipMemcpyAsync(&first, q->scal, sizeof(first), hipMemcpyDeviceToHost, s));
     if (e == NICGPU_OK) e = hip_status(hipStreamSynchronize(s));
+    used = part[(size_t) grid * kQpStats];
+    if (guess) first = (unsigned long long) part[(size_t) grid * kQpStats + 1];
     return e;
   };
-  if (st == NICGPU_OK) st = full((uint64_t) ntx, q->need);  // scal[0] = ntx from qp_need_kernel
+  if (st == NICGPU_OK) st = full((uint64_t) ntx, q->need);
   if (st != NICGPU_OK) return st;
   uint64_t lim = (uint64_t) ntx;
   if (first < ntx) {  // relax from the same guess (the speculative pass left `need` as it was)
