@@ -3048,6 +3048,11 @@ struct nicgpu_qp {
   unsigned long long* scal = nullptr;
   uint8_t* tmp = nullptr;
   uint64_t host_scal[4] = {0, 0, 0, 0};
+  // page-locked landing space of the small downloads (a pageable one is staged
+  // and waited for on the host): [grid * kQpStats + 2] the resolve's stats,
+  // RX count and first mismatch, then misc(): piece count, check flags, relax verdict
+  uint64_t* hp = nullptr;
+  uint64_t* misc() const { return hp + (size_t) grid * kQpStats + 2; }
   unsigned grid = 1;
   hipEvent_t planned = nullptr;  // nicgpu_qp_plan_on: the piece descriptors are written
 };
@@ -3110,6 +3115,11 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
   }
+  if (hipHostMalloc(reinterpret_cast<void**>(&q->hp), ((size_t) q->grid * kQpStats + 2 + 8) * sizeof(uint64_t)) !=
+      hipSuccess) {
+    nicgpu_qp_destroy(q);
+    return NICGPU_ERR_NOMEM;
+  }
   if (hipEventCreateWithFlags(&q->planned, hipEventDisableTiming) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_HIP;
@@ -3127,6 +3137,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
                   q->queue_start, q->queue_end, q->end_max};
   for (void* b : bufs)
     if (b) (void) hipFree(b);
+  if (q->hp) (void) hipHostFree(q->hp);
   if (q->planned) (void) hipEventDestroy(q->planned);
   delete q;
   return NICGPU_OK;
@@ -3184,10 +3195,11 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
                      q->plans, q->counts);
   int st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
-  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&q->host_scal[0], q->base + ntx, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  uint32_t* np_h = reinterpret_cast<uint32_t*>(q->misc());
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(np_h, q->base + ntx, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
   if (st != NICGPU_OK) return st;
-  const uint64_t np = (uint32_t) q->host_scal[0];
+  const uint64_t np = *np_h;
   st = qp_grow(q->piece_desc, q->c_pdesc, np ? np : 1);
   if (st == NICGPU_OK) st = qp_grow(q->piece_csum, q->c_pcs, np ? np : 1);
   if (st != NICGPU_OK) return st;
@@ -3226,8 +3238,8 @@ int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int
                        (uint64_t) nrx, mem_size, q->end_max, q->scal);
     st = hip_status(hipGetLastError());
   }
-  unsigned long long f[2] = {0, 0};
-  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(f, q->scal, sizeof(f), hipMemcpyDeviceToHost, s));
+  uint64_t* f = q->misc() + 1;
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(f, q->scal, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
   if (st != NICGPU_OK) return st;
   *verdict = f[0] ? -1 : (f[1] ? 0 : 1);
@@ -3250,7 +3262,8 @@ int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, u
   int st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
   // per-block stats, then the RX descriptors used and the first mismatch
-  std::vector<uint64_t> part((size_t) grid * kQpStats + 2);
+  const uint64_t* part = q->hp;  // grid * kQpStats + 2 (page-locked)
+  const size_t npart = (size_t) grid * kQpStats + 2;
   uint64_t used = 0;
   unsigned long long first = 0;
   auto full = [&](uint64_t lim_, const uint32_t* guess) {
@@ -3258,7 +3271,7 @@ int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, u
                        q->partials, guess);
     int e = hip_status(hipGetLastError());
     if (e == NICGPU_OK)
-      e = hip_status(hipMemcpyAsync(part.data(), q->partials, part.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+      e = hip_status(hipMemcpyAsync(q->hp, q->partials, npart * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     if (e == NICGPU_OK) e = hip_status(hipStreamSynchronize(s));
     used = part[(size_t) grid * kQpStats];
     if (guess) first = (unsigned long long) part[(size_t) grid * kQpStats + 1];
@@ -3270,14 +3283,15 @@ int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, u
   if (first < ntx) {  // relax from the same guess (the speculative pass left `need` as it was)
     for (int it = 0; st == NICGPU_OK; ++it) {
       if (it > 0) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
-      const unsigned long long init = (unsigned long long) ntx;
-      if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->scal, &init, sizeof(init), hipMemcpyHostToDevice, s));
+      q->misc()[4] = (uint64_t) ntx;  // page-locked source; the step below waits for the stream
+      if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->scal, q->misc() + 4, sizeof(uint64_t), hipMemcpyHostToDevice, s));
       if (st != NICGPU_OK) break;
       hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, (uint64_t) ntx, q->scal);
       st = hip_status(hipGetLastError());
-      if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(&first, q->scal, sizeof(first), hipMemcpyDeviceToHost, s));
+      if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->misc() + 3, q->scal, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
       if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
       if (st != NICGPU_OK) break;
+      first = (unsigned long long) q->misc()[3];
       // pos is exact up to and including `first` (pops before it agreed)
       lim = first < ntx ? (uint64_t) first : (uint64_t) ntx;
       if (first >= ntx || it + 1 == kQpRelaxSteps) break;
