@@ -1513,6 +1513,12 @@ const RxVariant kRxVariants[] = {
     // 9000 B within noise).
     {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 16, 0, true, true, true>, 2, 4, "u2_w4_c_sc1_ring_xpf", false, true, true},
     {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 0, 0, true, true, true>, 2, 4, "u2_w4_c_ring_xpf", false, true, true},
+    // 2: production for batches of at least kRxW8Tiles tiles.  8-wave blocks:
+    // half the blocks add their histogram bins into the same counters at the
+    // end (1024 -> 512 same-address atomics per bin).  IMIX (4 M packets) -2%,
+    // 4 M x 64 B -3%; C2 +0.6% and 9000 B +15% (2500 tiles underfill 512
+    // slots of 8 waves) keep 4-wave blocks (profiles/r02y_tune_variants.json).
+    {rx_offload_kernel<2, true, 8, true, false, 1, false, -1, 16, 0, true, true, true>, 2, 8, "u2_w8_c_sc1_ring_xpf", false, true, true},
 #ifdef NICGPU_TUNING
     // candidates and earlier production kernels, timed by tools/tune_rx.py.
     // 8-wave blocks measure the same on C2/IMIX/64 B and 12% slower on 9000 B,
@@ -1526,13 +1532,13 @@ const RxVariant kRxVariants[] = {
     {rx_offload_kernel<2, true, 4, true, false, 1, true, -1, 16>, 2, 4, "u2_nt1_w4_c_sc1_defer"},
     {rx_offload_kernel<2, true, 4, true, false, 1, false>, 2, 4, "u2_nt1_w4_c"},
     {rx_offload_kernel<2, true, 4, false, false, 1, false, -1, 16, 0, true>, 2, 4, "u2_nt1_w4_sc1_ring", false, true},
-    // bigger blocks: fewer blocks add their histogram bins into the same
-    // counters at the end (1024 -> 512 / 256 same-address atomics)
-    {rx_offload_kernel<2, true, 8, true, false, 1, false, -1, 16, 0, true, true, true>, 2, 8, "u2_w8_c_sc1_ring_xpf", false, true, true},
+    // bigger blocks still: 256 same-address atomics per bin
     {rx_offload_kernel<2, true, 16, true, false, 1, false, -1, 16, 0, true, true, true>, 2, 16, "u2_w16_c_sc1_ring_xpf", false, true, true},
 #endif
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
+constexpr int kRxW8 = 2;
+constexpr uint64_t kRxW8Tiles = 32768;  // 2 M packets: IMIX and 64-B batches of C3's size, not C2 (16 K tiles)
 
 // ------------------------------------------------------ segment gather --
 // The DMA writes of the batched QueuePair stage (QueuePair::handle_rx_segment,
@@ -2302,7 +2308,12 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
     const RxVariant& vv = kRxVariants[var];
     return rx_lds_bytes(vv.wpb, vv.unroll, stage, rss ? P.lut_words : 0u, hist_n, table_words);
   };
-  if (variant == 0) variant = plan_ring(dev, 0, lds_of(0), ntiles, di).holds_all ? 1 : 0;
+  if (variant == 0) {
+    // many tiles with a hit histogram: 8-wave blocks (what they save is half
+    // the end-of-block histogram flushes; the ring flushes mid-stream: sc1)
+    if (ntiles >= kRxW8Tiles && hist_n) variant = kRxW8;
+    else variant = plan_ring(dev, 0, lds_of(0), ntiles, di).holds_all ? 1 : 0;
+  }
   const RxVariant& v = kRxVariants[variant];
   const uint32_t lds = lds_of(variant);
   // ranges: at least 16 packets per wave; round robin: one tile per wave
