@@ -1165,8 +1165,11 @@ __host__ __device__ inline uint32_t rss_only_block_bytes(uint32_t lut_words, uin
   return (lut_words * 4u + hist_n * 4u + table_words * 4u + 15u) & ~15u;
 }
 constexpr uint32_t kRssOnlyWaveBytes = (uint32_t) kWave * kHdrStride * 16u;
+constexpr int kRssWpb = 8;  // waves per block (half the end-of-block histogram flushes of 4)
 
-__global__ __launch_bounds__(kBlock) void rss_only_kernel(RxParams P) {
+template <int WPB>  // waves per block
+__global__ __launch_bounds__(kWave * WPB) void rss_only_kernel(RxParams P) {
+  constexpr uint32_t kThreads = kWave * WPB;
   extern __shared__ uint4 lds_dyn[];
   const uint32_t w = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
   const uint32_t lane = lane_id();
@@ -1179,14 +1182,14 @@ __global__ __launch_bounds__(kBlock) void rss_only_kernel(RxParams P) {
   const uint32_t block_bytes =
       rss_only_block_bytes(P.lut_words, hist_lds ? P.table_n : 0u, table_lds ? (P.table_n + 1u) / 2u : 0u);
   uint4* hdr = reinterpret_cast<uint4*>(base_b + block_bytes + w * kRssOnlyWaveBytes);
-  for (uint32_t i = threadIdx.x; i < P.lut_words; i += kBlock) lut[i] = P.lut[i];
+  for (uint32_t i = threadIdx.x; i < P.lut_words; i += kThreads) lut[i] = P.lut[i];
   if (hist_lds)
-    for (uint32_t i = threadIdx.x; i < P.table_n; i += kBlock) hist[i] = 0;
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kThreads) hist[i] = 0;
   if (table_lds)
-    for (uint32_t i = threadIdx.x; i < P.table_n; i += kBlock) table_s[i] = P.table[i];
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kThreads) table_s[i] = P.table[i];
   __syncthreads();
   const uint64_t n_all = P.n_dev ? (*P.n_dev < P.n ? (uint64_t) *P.n_dev : P.n) : P.n;
-  const uint64_t stride = (uint64_t) gridDim.x * kWavesPerBlock * kWave;
+  const uint64_t stride = (uint64_t) gridDim.x * WPB * kWave;
   auto desc_of = [&](uint64_t b) __attribute__((always_inline)) { return b + lane < n_all ? P.desc[b + lane] : 0ull; };
   // the header chunks inside the packet (none for an empty or absent one)
   auto load_hdr = [&](uint64_t d, u32x4* c) __attribute__((always_inline)) {
@@ -1199,7 +1202,7 @@ __global__ __launch_bounds__(kBlock) void rss_only_kernel(RxParams P) {
   };
   // software pipeline: tile b + stride's descriptors and headers are in flight
   // while tile b hashes, and tile b + 2 stride's descriptors behind them
-  uint64_t b = ((uint64_t) blockIdx.x * kWavesPerBlock + w) * kWave;
+  uint64_t b = ((uint64_t) blockIdx.x * WPB + w) * kWave;
   uint64_t d = desc_of(b), dn = desc_of(b + stride);
   u32x4 c[kHdrChunks];
   load_hdr(d, c);
@@ -1230,7 +1233,7 @@ __global__ __launch_bounds__(kBlock) void rss_only_kernel(RxParams P) {
   }
   if (hist_lds) {
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < P.table_n; i += kBlock) {
+    for (uint32_t i = threadIdx.x; i < P.table_n; i += kThreads) {
       const uint32_t v = hist[i];
       if (v) atomicAdd(&P.out_hits[i], (unsigned long long) v);
     }
@@ -2275,7 +2278,9 @@ int rss_only_blocks_per_cu(int dev, uint32_t lds) {
   for (const auto& o : di.occ)
     if (o.variant == kRssOnlyVariant && o.lds == lds) return o.blocks;
   int b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rss_only_kernel, kBlock, lds) != hipSuccess || b < 1) b = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rss_only_kernel<kRssWpb>, kWave * kRssWpb, lds) != hipSuccess ||
+      b < 1)
+    b = 1;
   di.occ.push_back({kRssOnlyVariant, lds, b});
   return b;
 }
@@ -2283,15 +2288,16 @@ int rss_only_blocks_per_cu(int dev, uint32_t lds) {
 int launch_rss_only(const RxParams& P, const DeviceInfo& di, hipStream_t stream) {
   const uint32_t hist_n = (P.out_hits && P.table_n <= (uint32_t) kHistLds) ? P.table_n : 0u;
   const uint32_t table_words = P.table_n <= (uint32_t) kTableLds ? (P.table_n + 1u) / 2u : 0u;
-  const uint32_t lds = rss_only_block_bytes(P.lut_words, hist_n, table_words) + kWavesPerBlock * kRssOnlyWaveBytes;
+  const uint32_t lds = rss_only_block_bytes(P.lut_words, hist_n, table_words) + kRssWpb * kRssOnlyWaveBytes;
   // as many blocks as fit a CU (registers and LDS), one grid-stride pass each
   int dev = 0;
   (void) hipGetDevice(&dev);
   const uint32_t bpc = (uint32_t) rss_only_blocks_per_cu(dev, lds);
-  const uint64_t want = (P.n + kBlock - 1) / kBlock;
+  constexpr uint32_t kThreads = kWave * kRssWpb;
+  const uint64_t want = (P.n + kThreads - 1) / kThreads;
   const uint64_t cap = (uint64_t) di.cus * bpc;
   const unsigned grid = (unsigned) (want < cap ? want : cap);
-  hipLaunchKernelGGL(rss_only_kernel, dim3(grid), dim3(kBlock), lds, stream, P);
+  hipLaunchKernelGGL(rss_only_kernel<kRssWpb>, dim3(grid), dim3(kThreads), lds, stream, P);
   return hip_status(hipGetLastError());
 }
 
