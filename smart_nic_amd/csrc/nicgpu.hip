@@ -1165,7 +1165,7 @@ __host__ __device__ inline uint32_t rss_only_block_bytes(uint32_t lut_words, uin
   return (lut_words * 4u + hist_n * 4u + table_words * 4u + 15u) & ~15u;
 }
 constexpr uint32_t kRssOnlyWaveBytes = (uint32_t) kWave * kHdrStride * 16u;
-constexpr int kRssWpb = 8;  // waves per block (half the end-of-block histogram flushes of 4)
+constexpr int kRssWpb = 16;  // waves per block: more header gathers in flight per CU, 1/4 of the flushes of 4
 
 template <int WPB>  // waves per block
 __global__ __launch_bounds__(kWave * WPB) void rss_only_kernel(RxParams P) {
