@@ -40,20 +40,30 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(frames, desc, table, gpu_out, n_sample_mt, n_sample_1):
+def usable_cores():
+    """CPUs this process may run on (the box's affinity mask), and the host's count."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    return usable, os.cpu_count() or usable
+
+
+def cpu_baseline(frames, desc, table, gpu_out, n_sample_1, label):
     """Reference C++ path (oracle/_ref/libref.so: the reference's own
     src/checksum.cpp + src/rss.cpp, compiled in the build container) or, if it
-    is absent, the oracle restatement, timed on this host's cores.  Also checks
-    the GPU outputs bit-exactly on the sample."""
-    import ctypes
-
+    is absent, the oracle restatement, timed on this host's cores: one core
+    over a bounded sample, and every usable core (one RssEngine per thread,
+    rss.h:43 is not thread-safe) over the whole batch.  Also checks the GPU
+    outputs bit-exactly on both."""
     from oracle import pyoracle as po
 
     ref = po.ref_lib()
     kind = "reference" if ref is not None else "port"
-    cores = min(16, os.cpu_count() or 1)
+    usable, host_cpus = usable_cores()
     k = np.frombuffer(MS_KEY, np.uint8)
     t = np.ascontiguousarray(table.astype(np.uint16))
+    n_all = desc.size
 
     def run(n, threads):
         cs = np.zeros(n, np.uint16)
@@ -70,26 +80,39 @@ def cpu_baseline(frames, desc, table, gpu_out, n_sample_mt, n_sample_1):
         return time.perf_counter() - t0, cs, q
 
     dt1, cs1, q1 = run(n_sample_1, 1)
-    if ref is not None:
-        dtm, csm, qm = run(n_sample_mt, cores)
-    else:
-        dtm, csm, qm, cores = dt1, cs1, q1, 1
-        n_sample_mt = n_sample_1
     g_cs, g_q = gpu_out
-    ok = bool(np.array_equal(csm, g_cs[:n_sample_mt]) and np.array_equal(qm, g_q[:n_sample_mt])
-              and np.array_equal(cs1, g_cs[:n_sample_1]) and np.array_equal(q1, g_q[:n_sample_1]))
-    return {
-        "value": round(n_sample_mt / dtm / 1e6, 4),
+    ok = bool(np.array_equal(cs1, g_cs[:n_sample_1]) and np.array_equal(q1, g_q[:n_sample_1]))
+    legs = {}
+    if ref is not None:
+        for threads in sorted({min(16, usable), usable}):
+            dt, cs, q = run(n_all, threads)
+            ok = ok and bool(np.array_equal(cs, g_cs) and np.array_equal(q, g_q))
+            legs[threads] = dt
+        cores = usable
+        dtm, n_mt = legs[usable], n_all
+    else:
+        cores, dtm, n_mt = 1, dt1, n_sample_1
+    out = {
+        "value": round(n_mt / dtm / 1e6, 4),
         "unit": "Mpkt/s",
         "cores": cores,
         "kind": kind,
-        "sample": f"first {n_sample_mt} of the C2 batch (1518 B TCP) on {cores} threads, one RssEngine per thread; "
-                  f"1 core: {round(n_sample_1 / dt1 / 1e6, 4)} Mpkt/s over {n_sample_1} packets",
+        "sample": f"{label}: all {n_mt} packets on {cores} threads (every usable core, one RssEngine per thread); "
+                  f"1 core: first {n_sample_1} packets",
         "value_1core": round(n_sample_1 / dt1 / 1e6, 4),
-        "gbs": round(n_sample_mt * PKT_LEN / dtm / 1e9, 4),
+        "gbs": round(float(frames_bytes(desc[:n_mt])) / dtm / 1e9, 4),
         "gpu_matches_cpu_on_sample": ok,
         "cpu_model": _cpu_model(),
+        "usable_cores": usable,
+        "host_cpus": host_cpus,
     }
+    if 16 in legs and usable != 16:
+        out["value_16threads"] = round(n_all / legs[16] / 1e6, 4)
+    return out
+
+
+def frames_bytes(desc):
+    return int((desc >> np.uint64(40)).astype(np.int64).sum())
 
 
 def cpu_rows_baseline(pktgen):
@@ -108,8 +131,8 @@ def cpu_rows_baseline(pktgen):
     vp = ctypes.c_void_p
     rows = []
     ref = po.ref_lib()
-    cores = min(16, os.cpu_count() or 1)
-    n3 = 1 << 18
+    cores = usable_cores()[0]
+    n3 = 1 << 20
     lens = pktgen.imix_lengths(n3, np.random.default_rng(33))
     f3, d3, _ = pktgen.make_batch(lens, seed=33, proto=17, corrupt_frac=0.01)
     k = np.frombuffer(MS_KEY, np.uint8)
@@ -125,7 +148,8 @@ def cpu_rows_baseline(pktgen):
         dtm, dt1 = rx(n3, cores), rx(1 << 16, 1)
         rows.append({"row": "rx_c3", "value": round(n3 / dtm / 1e6, 4), "unit": "Mpkt/s", "cores": cores,
                      "kind": "reference", "value_1core": round((1 << 16) / dt1 / 1e6, 4),
-                     "sample": f"{n3} IMIX frames (7:4:1 64/576/1518 B), 16 queues; 1 core over 65536"})
+                     "sample": f"{n3} IMIX frames (7:4:1 64/576/1518 B), 16 queues, every usable core; "
+                               f"1 core over 65536"})
     L = po.lib()
     n5 = 4096
     f5, d5, _ = pktgen.make_batch(np.full(n5, 9000), seed=55, proto=6, corrupt_frac=0.0)
@@ -228,12 +252,36 @@ def _cpu_model():
 
 def load_traffic(path):
     """HBM bytes per launch from a committed rocprofv3 PMC summary (see
-    profiles/README.md), or None."""
+    profiles/README.md) and where it came from: the profile names the kernel
+    source it measured (sha256 of smart_nic_amd/csrc/nicgpu.hip); a profile
+    of another source is reported as stale, never silently."""
+    import hashlib
+
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            prof = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, {"profile": os.path.relpath(path, ROOT), "error": "unreadable"}
+    src = os.path.join(ROOT, "smart_nic_amd", "csrc", "nicgpu.hip")
+    try:
+        with open(src, "rb") as f:
+            cur = hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        cur = None
+    rec = prof.get("kernel_source_sha256")
+    info = {"profile": os.path.relpath(path, ROOT), "measured_in_this_run": False,
+            "profile_kernel_source": rec, "current_kernel_source": cur,
+            "stale": (rec is None or rec != cur)}
+    if info["stale"]:
+        log(f"warning: {info['profile']} was measured on kernel source {rec}, this tree is {cur}: traffic may be stale")
+    return prof.get("hbm_bytes_per_launch"), info
+
+
+WORKLOAD_TEXT = {
+    "c2": "C2: 1M x 1518 B TCP per GPU, checksum verify + RSS (MS 40-B key, 128-entry table i%4, IPv4 4-tuple)",
+    "c3": "C3: IMIX 64/576/1518 B at 7:4:1, 4M packets per GPU (job batch byte-sharded), checksum verify + RSS "
+          "(MS 40-B key, 128-entry table i%16, IPv4 4-tuple)",
+}
 
 
 def main():
@@ -241,7 +289,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--packets", type=int, default=N_PER_GPU, help="packets per GPU")
+    ap.add_argument("--workload", choices=("c2", "c3"), default="c2",
+                    help="c2 (BASELINE configs[1], the metric's config) or c3 (IMIX, byte-balanced shards)")
+    ap.add_argument("--packets", type=int, default=None, help="packets per GPU (default: the workload's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the same-box read-only streaming ceiling")
@@ -256,26 +306,20 @@ def main():
     import torch
 
     import smart_nic_amd as sna
+    from smart_nic_amd import dist as sdist
     from smart_nic_amd import pktgen
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1 or args.dist:
-        import torch.distributed as dist
+    ranks = sdist.init_ranks(force=args.dist, backend="nccl")
+    rank, world, dev = ranks.rank, ranks.world, ranks.device
+    shard = sdist.plan_shard(args.workload, ranks, args.packets)
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
-
-    n = args.packets
+    n = shard.lengths.size
     t0 = time.time()
-    frames, desc, corrupted = pktgen.make_batch(np.full(n, PKT_LEN), seed=42 + rank, proto=6, corrupt_frac=0.01)
-    log(f"[rank {rank}] generated {n} x {PKT_LEN} B in {time.time() - t0:.1f}s")
-    table = (np.arange(128) % 4).astype(np.uint16)
+    frames, desc, corrupted = pktgen.make_batch(shard.lengths, seed=shard.seed, proto=shard.proto, corrupt_frac=0.01)
+    bytes_local = int(shard.lengths.sum())
+    log(f"[rank {rank}] {args.workload}: packets [{shard.lo}, {shard.hi}) of {shard.job_packets}, "
+        f"{bytes_local / 1e9:.2f} GB in {time.time() - t0:.1f}s")
+    table = (np.arange(128) % shard.queues).astype(np.uint16)
 
     f_dev = torch.from_numpy(frames).to(dev)
     d_dev = torch.from_numpy(desc.view(np.int64)).to(dev)
@@ -285,18 +329,8 @@ def main():
     hits = torch.zeros(128, dtype=torch.int64, device=dev)
 
     # RSS key + table: rank 0's copy, RCCL-broadcast over xGMI to every rank.
-    key_dev = torch.tensor(list(MS_KEY), dtype=torch.uint8, device=dev)
-    tab_dev = torch.from_numpy(table.astype(np.int32)).to(dev)
-    if dist is not None:
-        from smart_nic_amd import dist as sdist
-
-        if rank != 0:
-            key_dev.zero_()
-            tab_dev.zero_()
-        key_dev, tab_dev = sdist.broadcast_rss_config(key_dev, tab_dev, dist)
-    else:
-        tab_dev = tab_dev.to(torch.int16)
-    ctx = sna.RssContext(dev)
+    key_dev, tab_dev = sdist.setup_rss(ranks, MS_KEY, table)
+    ctx = sna.RssContext(dev.index)
     ctx.set_key_device(key_dev)
     ctx.set_table_device(tab_dev)
     torch.cuda.synchronize()
@@ -315,8 +349,7 @@ def main():
     # so the per-launch spread is taken in a separate, untimed pass below.
     stream = torch.cuda.current_stream()
     ev_a, ev_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if dist is not None:
-        dist.barrier()
+    sdist.barrier(ranks)
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     ev_a.record(stream)
@@ -324,8 +357,7 @@ def main():
         step()
     ev_b.record(stream)
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    sdist.barrier(ranks)
     t_wall = time.perf_counter() - t_start
     kern_avg_s = ev_a.elapsed_time(ev_b) / 1e3 / args.steps
 
@@ -341,11 +373,15 @@ def main():
 
     ceiling = read_ceiling(torch, f_dev) if (rank == 0 and world == 1 and not args.no_ceiling) else None
 
-    t_max = t_wall
-    if dist is not None:
-        tt = torch.tensor([t_wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
+    t_max = sdist.max_over_ranks(t_wall, ranks.dist, dev)
+
+    # one more launch with the histogram zeroed: the job-wide RssStats of one
+    # batch (all-reduce of the per-table-index hits), checked against the
+    # per-rank histograms and against this rank's hashes
+    hits.zero_()
+    step()
+    torch.cuda.synchronize()
+    job_hits, per_rank_hits, hits_sum_ok = sdist.job_queue_hits(ranks, hits)
 
     # correctness of this run (cheap properties on every rank)
     g_cs = cs.cpu().numpy().view(np.uint16)
@@ -353,16 +389,21 @@ def main():
     g_q = qs.cpu().numpy().view(np.uint16)
     status_ok = bool(np.array_equal(g_cs != 0, corrupted))
     queue_ok = bool(np.array_equal(g_q, table[g_h % 128]))
+    local_hits_ok = bool(np.array_equal(per_rank_hits[rank], np.bincount(g_h % 128, minlength=128).astype(np.uint64)))
+    checks = {"status_matches_corruption": status_ok, "queue_is_table_of_hash": queue_ok,
+              "queue_hits_is_bincount_of_table_index": local_hits_ok}
+    checks_all = sdist.sum_over_ranks(int(all(checks.values())), ranks.dist, dev)
+    job_hits_ok = bool(hits_sum_ok and int(job_hits.sum()) == shard.job_packets)
 
-    total_pkts = n * world * args.steps
+    total_pkts = shard.job_packets * args.steps
     value = total_pkts / t_max / 1e6
-    alg_bytes = n * (PKT_LEN + DESC_BYTES + RESULT_BYTES)
+    alg_bytes = bytes_local + n * (DESC_BYTES + RESULT_BYTES)
     achieved_gbs = alg_bytes / kern_avg_s / 1e9
-    frame_gbs = n * PKT_LEN / kern_avg_s / 1e9
+    frame_gbs = bytes_local / kern_avg_s / 1e9
 
     out = None
     if rank == 0:
-        traffic = load_traffic(args.traffic_json)
+        traffic, traffic_src = load_traffic(args.traffic_json) if args.workload == "c2" else (None, None)
         out = {
             "metric": "Mpkt/s + GB/s device-resident RX checksum+RSS, 1518B batch; % HBM roofline",
             "value": round(value, 3),
@@ -375,14 +416,19 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (seeded Eth/IPv4/TCP frames, valid IPv4+TCP checksums, whole-frame balancing word, 1% corrupted)",
+            "data": "synthetic (seeded Eth/IPv4/" + ("TCP" if shard.proto == 6 else "UDP") +
+                    " frames, valid IPv4+L4 checksums, whole-frame balancing word, 1% corrupted)",
             "config": {
-                "workload": "C2: 1M x 1518 B TCP per GPU, checksum verify + RSS (MS 40-B key, 128-entry table i%4, IPv4 4-tuple)",
+                "workload": WORKLOAD_TEXT[args.workload],
                 "packets_per_gpu": n,
-                "packet_bytes": PKT_LEN,
-                "parallelism": f"replicas x{world} (packet shards, key/table RCCL broadcast)",
+                "job_packets": shard.job_packets,
+                "job_bytes": shard.job_bytes,
+                "packet_bytes": PKT_LEN if args.workload == "c2" else "imix",
+                "parallelism": f"replicas x{world} (contiguous packet shards"
+                               + (", byte-balanced" if args.workload == "c3" else "")
+                               + ", key/table RCCL broadcast, no data-path collective)",
             },
-            "gbs_frames": round(frame_gbs * world, 2),
+            "gbs_frames": round(shard.job_bytes / kern_avg_s / 1e9, 2) if world > 1 else round(frame_gbs, 2),
             "gbs_frames_per_gpu": round(frame_gbs, 2),
             "kernel_us_avg": round(kern_avg_s * 1e6, 2),
             "kernel_us_median": round(kern_med_s * 1e6, 2),
@@ -395,15 +441,18 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "alg_bytes_per_launch": alg_bytes,
                 "ceiling_measured": ceiling,
                 "frac_of_ceiling": (round(achieved_gbs / ceiling["gbs"], 4) if ceiling else None),
             },
-            "checks": {"status_matches_corruption": status_ok, "queue_is_table_of_hash": queue_ok},
+            "checks": dict(checks, all_ranks_ok=checks_all == world, job_queue_hits_ok=job_hits_ok),
+            "rss_stats_job": {"hashes": int(job_hits.sum()), "queue_hits_nonzero": int((job_hits > 0).sum()),
+                              "queue_hits_per_rank_sum": [int(h.sum()) for h in per_rank_hits]},
         }
     # end-to-end (host pinned -> H2D -> kernel -> D2H of results) and the CPU
     # baseline: rank 0 at N = 1 only
-    if rank == 0 and world == 1 and not args.no_e2e:
+    if rank == 0 and world == 1 and not args.no_e2e and args.workload == "c2":
         try:
             out["e2e"] = e2e_rate(torch, sna, ctx, frames, desc, dev)
         except Exception as e:  # report, never hide
@@ -413,14 +462,12 @@ def main():
         if errors:
             out["gpu_rows_errors"] = errors
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(frames, desc, table, (g_cs, g_q),
-                                           n_sample_mt=min(n, 1 << 18), n_sample_1=min(n, 1 << 16))
+        out["cpu_baseline"] = cpu_baseline(frames, desc, table, (g_cs, g_q), n_sample_1=min(n, 1 << 16),
+                                           label=args.workload.upper())
         out["cpu_baseline"]["other_rows"] = cpu_rows_baseline(pktgen)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    sdist.finish(ranks)
 
 
 def read_ceiling(torch, buf, reps=5):

@@ -128,7 +128,12 @@ struct DeviceHostMemory {
 /// descriptors live in the image itself (mem.base + the ring's address).  The
 /// stage copies them in stream order (no PCIe upload) and fetches host copies
 /// only when a host step needs them (a ring whose RX buffers are not in
-/// address order, a host tail, overlapping buffers).
+/// address order, a host tail, overlapping buffers).  The descriptors are read
+/// once, at the start of the batch; the reference DMA-reads each slot when it
+/// pops it (descriptor_ring.cpp:97-106), so an RX buffer of the batch that
+/// overlaps the descriptor arrays (inside the image) would change a later
+/// descriptor there.  That case is not modelled: process_batch / submit throw
+/// GpuError (NICGPU_ERR_INVALID) for it before anything is written.
 struct DeviceDescriptors {
   const TxDescriptor* tx{nullptr};
   std::size_t ntx{0};
@@ -269,6 +274,7 @@ private:
   void finish(Slot& sl, RxBatchResult& out);
   void enqueue(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                const DeviceDescriptors* d, void* stream);
+  void check_rings_unwritten(Slot& sl, const DeviceHostMemory& mem, void* stream);
   std::pair<std::span<const TxDescriptor>, std::span<const RxDescriptor>> host_spans(
       Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx, void* stream);
   // the host path (buffers_disjoint unless `disjoint` is known, then run_batch)

@@ -45,6 +45,7 @@ extern "C" {
 #define NICGPU_ERR_HIP (-2)        /* a HIP runtime call failed */
 #define NICGPU_ERR_NO_DEVICE (-3)  /* no gfx950 device visible */
 #define NICGPU_ERR_NOMEM (-4)
+#define NICGPU_ERR_RANGE (-5)    /* a batch too large for 32-bit piece indices: split it */
 
 #define NICGPU_DESC_OFFSET_BITS 40
 /* Longest packet the kernels accept: 64 KiB - 1 (the TSO super-frame limit of
@@ -330,8 +331,11 @@ typedef struct nicgpu_qp_view {
 typedef struct nicgpu_qp nicgpu_qp;
 int nicgpu_qp_create(nicgpu_qp** out, int device);
 int nicgpu_qp_destroy(nicgpu_qp* q);
-/* Capacity for ntx TX and nrx RX descriptors (ntx <= 2^32 / 64, so that piece
- * indices fit 32 bits; nrx < 2^31 - 1); fills *view. */
+/* Capacity for ntx TX and nrx RX descriptors (ntx <= 2^32 / 256 and
+ * nrx < 2^31 - 1); fills *view.  Piece indices are 32-bit: a batch plans at
+ * most 256 pieces per TX descriptor unless one of them is a huge plain packet
+ * that is verified and then dropped (one piece per 64 KiB); nicgpu_qp_plan
+ * then returns NICGPU_ERR_RANGE before anything is sized from the count. */
 int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view);
 /* Whether the buffers of view.tx[0, ntx) and view.rx[0, nrx) are disjoint, as
  * nic::rx_stage_detail::buffers_disjoint defines it (RX spans: at most
@@ -342,7 +346,9 @@ int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view
  * `stream`. */
 int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int* verdict, void* stream);
 /* The plan (qp_logic.h plan_packet) of view.tx[0, ntx) and the checksum of
- * every piece over the image mem[0, mem_size): *npieces on return.  Waits for
+ * every piece over the image mem[0, mem_size): *npieces on return
+ * (NICGPU_ERR_RANGE, nothing enqueued after the count, when a descriptor plans
+ * more than 256 pieces: the total may then not fit 32 bits).  Waits for
  * `stream` once (the piece count sizes the piece buffers); the piece
  * descriptors and checksums are then enqueued on it.  Refreshes *view (the
  * piece buffers may grow). */

@@ -139,6 +139,9 @@ void make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
     base[c + 1] = n;
   });
   for (std::size_t c = 0; c < ch.k; ++c) base[c + 1] += base[c];
+  // PacketPlan::first_piece is 32-bit (the device plan's layout)
+  if (base[ch.k] > 0xFFFFFFFFull)
+    throw GpuError("process_batch: more than 2^32 checksum pieces in one batch; split it", NICGPU_ERR_RANGE);
   plan.pieces.resize(base[ch.k]);
   ch.run([&](std::size_t c, std::size_t b, std::size_t e) {
     std::size_t at = base[c];
@@ -1269,11 +1272,42 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDe
     }
   }
   if (!on_device) {
+    check_rings_unwritten(sl, mem, stream);
     const auto [htx, hrx] = host_spans(sl, {}, {}, stream);
     on_host(mem, htx, hrx, st, out, stream, disjoint, check_us);
   }
   out.timings.check_us = check_us;
   stats_ = st;
+}
+
+// Device descriptor arrays inside the image: no RX buffer of the batch may
+// overlap them (an RX write there would change a descriptor the reference pops
+// later, descriptor_ring.cpp:97-106; the stage reads them once).  Throws
+// before anything is written.
+void BatchedQueuePair::check_rings_unwritten(Slot& sl, const DeviceHostMemory& mem, void* stream) {
+  if (!sl.tx_dev && !sl.rx_dev) return;
+  const auto b = reinterpret_cast<std::uintptr_t>(mem.base);
+  struct Span { std::uint64_t lo, hi; };
+  Span rings[2];
+  int nr = 0;
+  auto add = [&](const void* p, std::size_t bytes) {
+    const auto a = reinterpret_cast<std::uintptr_t>(p);
+    if (!bytes || a >= b + mem.size || a + bytes <= b) return;
+    const std::uint64_t lo = a > b ? a - b : 0, hi = std::min<std::uint64_t>(a + bytes - b, mem.size);
+    rings[nr++] = Span{lo, hi};
+  };
+  add(sl.tx_dev, sl.ntx_dev * sizeof(TxDescriptor));
+  add(sl.rx_dev, sl.nrx_dev * sizeof(RxDescriptor));
+  if (nr == 0) return;
+  const auto hrx = host_spans(sl, {}, {}, stream).second;
+  for (const RxDescriptor& d : hrx) {
+    if (d.buffer_length == 0 || d.buffer_address >= mem.size) continue;
+    const std::uint64_t lo = d.buffer_address, hi = std::min<std::uint64_t>(lo + d.buffer_length, mem.size);
+    for (int k = 0; k < nr; ++k)
+      if (lo < rings[k].hi && rings[k].lo < hi)
+        throw GpuError("process_batch: an RX buffer overlaps the descriptor arrays inside the image (not modelled)",
+                       NICGPU_ERR_INVALID);
+  }
 }
 
 // The batch's descriptors on the host: the caller's spans, or (device
@@ -1345,6 +1379,7 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
         if (sl.on_device) back(sl, sl.mem, sl.result, sl.stream);
       }
       if (!sl.on_device) {
+        check_rings_unwritten(sl, sl.mem, sl.stream);
         const auto [htx, hrx] = host_spans(sl, sl.tx, sl.rx, sl.stream);
         on_host(sl.mem, htx, hrx, sl.stats, sl.result, sl.stream, disjoint, check_us);
       }
@@ -1440,6 +1475,7 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   };
   const bool side = !dev_desc || (!inside(sl.tx_dev, ntx * sizeof(TxDescriptor)) &&
                                   !inside(sl.rx_dev, nrx * sizeof(RxDescriptor)));
+  if (!side) check_rings_unwritten(sl, mem, stream);
   void* ps = side ? S.side_plan : stream;
   if (dev_desc) {
     check(nicgpu_qp_reserve(sl.qp, ntx, nrx, &v), "nicgpu_qp_reserve");
@@ -1452,15 +1488,18 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     check(nicgpu_stream_wait_event(ps, sl.ev_tx), "nicgpu_stream_wait_event");
   }
   std::uint64_t np = 0;
-  check(nicgpu_qp_plan_on(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &np,
-                          &v, ps, stream),
-        "nicgpu_qp_plan_on");
+  const int pst = nicgpu_qp_plan_on(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx,
+                                    config_.max_mtu, &np, &v, ps, stream);
   out.timings.sums_us += us_since(t);
   t = clock::now();
   if (sl.up) {
     sl.up->finish();
     sl.up.reset();
   }
+  // a descriptor planning more pieces than 32-bit piece indices allow: the
+  // host path (which refuses the batch if its total does not fit either)
+  if (pst == NICGPU_ERR_RANGE) return false;
+  check(pst, "nicgpu_qp_plan_on");
   if (!dev_desc) {
     check(nicgpu_stream_wait_event(ps, sl.ev_rx), "nicgpu_stream_wait_event");
     if (side) check(nicgpu_stream_wait_event(stream, sl.ev_rx), "nicgpu_stream_wait_event");

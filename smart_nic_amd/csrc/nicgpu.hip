@@ -1994,44 +1994,112 @@ struct IcrcParams {
 
 constexpr int kIcrcRing = 128;  // descriptor ring per wave (LDS)
 
-// One chunk: bytes [0, b) of the 16-B chunk v (0 <= b <= 16; bytes before
-// the packet's start already masked) processed from state S, without shifting
-// data: byte i of the chunk goes through slice table b - 1 - i (the table it
-// would use had the span been shifted to end at byte 15).  T holds 16 all-zero
-// tables in front of the 16 slice tables, so a byte at or past b — whatever
-// its value — reads a zero row: row b + (15 - i), with the (15 - i) KiB an
-// immediate LDS offset, and b = 0 is a no-op chunk.  Per byte: one extract,
-// one address or, one LDS read, half an xor3; the state is xored in at byte 0
-// (kCrcLead) and, for b < 4, its bytes past b carry over shifted.
-__device__ __forceinline__ uint32_t crc_chunk_ns(const uint32_t* __restrict__ Text, u32x4 v, uint32_t b,
-                                                 uint32_t S) {
-  const uint32_t x[4] = {v.x ^ S, v.y, v.z, v.w};
-  const uint32_t* Tb = Text + b * 256u;
-  uint32_t t[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) t[i] = Tb[(15 - i) * 256 + ((x[i >> 2] >> (8 * (i & 3))) & 0xFFu)];
-  const uint32_t c = (t[0] ^ t[1] ^ t[2]) ^ (t[3] ^ t[4] ^ t[5]) ^ (t[6] ^ t[7] ^ t[8]) ^ (t[9] ^ t[10] ^ t[11]) ^
-                     (t[12] ^ t[13] ^ t[14]) ^ t[15];
-  return c ^ (b < 4u ? S >> (8u * b) : 0u);
+constexpr int kIcrcWpb = 16;  // waves per block: one 1024-thread block per CU shares the table image
+constexpr int kIcrcThreads = kWave * kIcrcWpb;
+constexpr uint32_t kNibPairBytes = 4096u;            // two nibble positions: 16 rows of 256 B
+constexpr uint32_t kNibBytes = 16u * kNibPairBytes;  // the 32 nibble positions of a 16-B chunk: 64 KiB
+constexpr uint32_t kUnshiftWords = 16u * 8u * 16u;   // G_k, k = 0..15: 8 nibbles x 16 values
+
+// G_k = x^(-8k) mod P in the reflected register: undoes k trailing zero bytes
+// (the zero-byte step S -> (S >> 8) ^ T0[S & 0xFF] is linear and invertible:
+// the top byte of T0[k] is a permutation of k).  Gt[k][j][v] = G_k(v << 4j).
+struct CrcUnshift {
+  uint32_t g[16][8][16];
+};
+constexpr CrcUnshift make_crc_unshift() {
+  const Crc32cTables T = make_crc32c_tables();
+  uint32_t top_inv[256] = {};
+  for (uint32_t k = 0; k < 256; ++k) top_inv[T.t[0][k] >> 24] = k;
+  CrcUnshift G{};
+  for (int j = 0; j < 8; ++j)
+    for (uint32_t v = 0; v < 16; ++v) {
+      uint32_t s = v << (4 * j);
+      for (int k = 0; k < 16; ++k) {
+        G.g[k][j][v] = s;
+        const uint32_t b = top_inv[s >> 24];
+        s = ((s ^ T.t[0][b]) << 8) | b;
+      }
+    }
+  return G;
+}
+__constant__ CrcUnshift kCrcUnshift = make_crc_unshift();
+
+// One 16-B chunk through the CRC register from state S: the chunk x (bytes
+// outside the packet already zeroed) with S xored into its first 4 bytes, then
+// slice-by-16 by NIBBLES from a zero state: nibble h of byte i contributes
+// T_{15-i}[v << 4h].  Every nibble table is stored 32 times, copy c in LDS bank
+// c only, and lane l reads copy l % 32, so the 32 lanes of a ds_read_b32 lane
+// group hit 32 distinct banks: the 32 lookups per chunk never conflict (byte
+// tables put 3-4 lanes of a group on one bank).  Row v of a table is 256 B
+// apart, so a lookup address is {copy byte, nibble byte, 0, 0} — one
+// v_perm_b32 from the chunk's nibble bytes (x & 0x0F0F0F0F and
+// (x >> 4) & 0x0F0F0F0F) and the lane's copy byte — plus an immediate (two
+// positions share a 4-KiB block: the second at +128 B).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  // hipcc folds table words in one v_xor_b32 (and one lgkmcnt wait) at a
+  // time; v_bitop3_b32 0x96 is a ^ b ^ c
+  uint32_t d;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
 }
 
-__global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
-  __shared__ uint32_t Text[32 * 256];  // 16 zero tables, then the 16 slice tables
-  __shared__ uint64_t ring_all[kWavesPerBlock][kIcrcRing];
+// The 8 table words of dword W (0..3) of a chunk.
+template <int W>
+__device__ __forceinline__ void crc_dword_words(const uint8_t* __restrict__ Tn, uint32_t x, uint32_t cb, uint32_t* t) {
+  const uint32_t y = x & 0x0F0F0F0Fu, z = (x >> 4) & 0x0F0F0F0Fu;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t sel = 0x0C0C0004u | ((uint32_t) k << 8);
+    const uint32_t off = (uint32_t) (4 * W + k) * kNibPairBytes;
+    t[2 * k] = *reinterpret_cast<const uint32_t*>(Tn + __builtin_amdgcn_perm(cb, y, sel) + off);
+    t[2 * k + 1] = *reinterpret_cast<const uint32_t*>(Tn + __builtin_amdgcn_perm(cb, z, sel) + off + 128u);
+  }
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t crc_dword_nib(const uint8_t* __restrict__ Tn, uint32_t x, uint32_t cb) {
+  uint32_t t[8];
+  crc_dword_words<W>(Tn, x, cb, t);
+  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+}
+
+// Dwords 1..3 of a chunk: 24 lookups, independent of the CRC state.
+__device__ __forceinline__ uint32_t crc_chunk_part(const uint8_t* __restrict__ Tn, uint32_t x1, uint32_t x2,
+                                                   uint32_t x3, uint32_t cb) {
+  uint32_t t[24];
+  crc_dword_words<1>(Tn, x1, cb, t);
+  crc_dword_words<2>(Tn, x2, cb, t + 8);
+  crc_dword_words<3>(Tn, x3, cb, t + 16);
+  const uint32_t a = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), xor3(t[6], t[7], t[8]));
+  const uint32_t b = xor3(xor3(t[9], t[10], t[11]), xor3(t[12], t[13], t[14]), xor3(t[15], t[16], t[17]));
+  const uint32_t c = xor3(xor3(t[18], t[19], t[20]), t[21], xor3(t[22], t[23], 0u));
+  return xor3(a, b, c);
+}
+
+__global__ __launch_bounds__(kIcrcThreads) void icrc_kernel(IcrcParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t Tn[kNibBytes];
+  __shared__ uint32_t Gt[kUnshiftWords];
+  __shared__ uint64_t ring_all[kIcrcWpb][kIcrcRing];
   __shared__ uint4 masks[kMaskEntries];
   __shared__ uint32_t lead_s[16];
   if (threadIdx.x < 16u) lead_s[threadIdx.x] = kCrcLead.s[threadIdx.x];
-  for (uint32_t i = threadIdx.x; i < 16u * 256u; i += kBlock) Text[i] = 0u;
-  for (uint32_t i = threadIdx.x; i < 16u * 256u; i += kBlock) Text[16u * 256u + i] = (&kCrc32c.t[0][0])[i];
-  for (uint32_t i = threadIdx.x; i < kMaskEntries; i += kBlock) {
+  for (uint32_t q = threadIdx.x; q < kNibBytes / 16u; q += kIcrcThreads) {
+    const uint32_t o = q * 16u;
+    const uint32_t pair = o >> 12, v = (o >> 8) & 15u, half = (o >> 7) & 1u;  // byte `pair`, nibble `half`
+    const uint32_t val = kCrc32c.t[15u - pair][half ? v << 4 : v];
+    reinterpret_cast<uint4*>(Tn)[q] = make_uint4(val, val, val, val);
+  }
+  for (uint32_t i = threadIdx.x; i < kUnshiftWords; i += kIcrcThreads) Gt[i] = (&kCrcUnshift.g[0][0][0])[i];
+  for (uint32_t i = threadIdx.x; i < kMaskEntries; i += kIcrcThreads) {
     const int lo = i < 16u ? (int) i : 0, hi = i < 16u ? 16 : (int) i - 16;
     masks[i] = make_uint4(dword_keep(lo, hi, 0), dword_keep(lo, hi, 1), dword_keep(lo, hi, 2), dword_keep(lo, hi, 3));
   }
   __syncthreads();
   const uint32_t lane = lane_id();
+  const uint32_t cb = (lane & 31u) << 2;  // this lane's copy: bank lane % 32
   uint64_t* ring = ring_all[threadIdx.x / kWave];
-  const uint64_t nwaves = (uint64_t) gridDim.x * kWavesPerBlock;
-  const uint64_t wave = (uint64_t) blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+  const uint64_t nwaves = (uint64_t) gridDim.x * kIcrcWpb;
+  const uint64_t wave = (uint64_t) blockIdx.x * kIcrcWpb + threadIdx.x / kWave;
   // contiguous packet range of this wave
   const uint64_t per = (P.n + nwaves - 1) / nwaves;
   const uint64_t p0 = wave * per < P.n ? wave * per : P.n;
@@ -2053,7 +2121,7 @@ __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
   // per lane: the packet's first 16-B chunk and 32-bit byte positions
   // relative to it (frames are < 64 KiB)
   uint64_t c16 = 0;
-  uint32_t pos = 0, end = 0, len = 0, lb = 0, S = 0xFFFFFFFFu;
+  uint32_t pos = 0, end = 0, len = 0, lb = 0, kz = 0, S = 0xFFFFFFFFu;
   auto setup = [&]() __attribute__((always_inline)) {
     const uint64_t d = ring[my & (kIcrcRing - 1)];
     const uint64_t off = d & kOffMask;
@@ -2063,7 +2131,11 @@ __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
     lb = (uint32_t) c16 & 7u;  // chunk of the 128-B line the packet starts in
     pos = (uint32_t) off & 15u;
     end = pos + span;
-    S = lead_s[pos];  // an empty span runs its pos zero bytes back to 0xFFFFFFFF
+    // the state that pos zero bytes take to 0xFFFFFFFF, entered at byte 0 of
+    // the first chunk with the pos leading bytes zeroed; an empty span
+    // processes no chunk.  kz: zero bytes after the span in its last chunk.
+    S = span ? lead_s[pos] : 0xFFFFFFFFu;
+    kz = span ? (16u - (end & 15u)) & 15u : 0u;
   };
   if (my < p1) setup();
   for (;;) {
@@ -2071,42 +2143,52 @@ __global__ __launch_bounds__(kBlock) void icrc_kernel(IcrcParams P) {
     if (__ballot(active) == 0ull) break;
     if (active) {
       // up to the end of the current 128-B line (8 chunks), so a lane reads
-      // every line once (64 B per step fetched most lines twice: 2.2x the
-      // algorithmic bytes); loads clamped to the line and the span's end
+      // every line once; loads clamped to the line and the span's end
       const uint32_t c0 = pos >> 4;
       const uint32_t clast = end > pos ? (end - 1u) >> 4 : c0;
       const uint32_t ce = ((lb + c0) | 7u) - lb;  // last chunk of c0's line
       const uint32_t cl = ce < clast ? ce : clast;
-      u32x4 v[8] = {};
-      if (end > pos) {  // an empty span reads nothing (it may sit at the buffer's end)
+      const uint32_t nproc = end > pos ? cl - c0 + 1u : 0u;  // chunks this step
+      u32x4 v[8];  // unread chunks are never processed (u >= nproc)
+      if (nproc) {  // an empty span reads nothing (it may sit at the buffer's end)
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = f16[c16 + (c0 + (uint32_t) u <= cl ? c0 + (uint32_t) u : cl)];
       }
-      // only the first chunk of a step can start inside it (a packet's first):
-      // its leading bytes are masked; chunks past cl (the line or the span)
-      // get b = 0, a no-op, so every lane runs the same straight-line code
-      const uint32_t a = pos & 15u;
-      const uint32_t nc = cl - c0;            // chunks this step, minus one
+      // every chunk processed whole: bytes before the packet (its first
+      // chunk) and past the span (its last) zeroed, so the last chunk adds
+      // trailing zero bytes that G_k takes back at the end
       const int32_t er = (int32_t) (end - (c0 << 4));  // span end from c0's base
-      {
-        const uint4 m1 = masks[a];
-        v[0].x &= m1.x;
-        v[0].y &= m1.y;
-        v[0].z &= m1.z;
-        v[0].w &= m1.w;
-      }
+      const uint4 m0 = masks[pos & 15u];
+      uint32_t part[8];
+      uint32_t x0[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int32_t r = er - 16 * u;
-        uint32_t b = (uint32_t) (r < 0 ? 0 : (r > 16 ? 16 : r));
-        if ((uint32_t) u > nc) b = 0u;
-        S = crc_chunk_ns(Text, v[u], b, S);
+        const uint4 mt = masks[16 + (r < 0 ? 0 : (r > 16 ? 16 : r))];
+        uint4 m = mt;
+        if (u == 0) {
+          m.x &= m0.x;
+          m.y &= m0.y;
+          m.z &= m0.z;
+          m.w &= m0.w;
+        }
+        x0[u] = v[u].x & m.x;
+        part[u] = crc_chunk_part(Tn, v[u].y & m.y, v[u].z & m.z, v[u].w & m.w, cb);
       }
-      pos = (cl + 1u) << 4;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t Sn = part[u] ^ crc_dword_nib<0>(Tn, x0[u] ^ S, cb);
+        S = (uint32_t) u < nproc ? Sn : S;
+      }
+      pos = nproc ? (cl + 1u) << 4 : end;
     }
     const bool finished = active && pos >= end;
     if (finished) {
-      const uint32_t crc = S ^ 0xFFFFFFFFu;
+      // undo the k trailing zero bytes of the last chunk
+      uint32_t g = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g ^= Gt[kz * 128u + (uint32_t) j * 16u + ((S >> (4 * j)) & 15u)];
+      const uint32_t crc = g ^ 0xFFFFFFFFu;
       if (P.out_crc) P.out_crc[my] = (P.verify && len < 4u) ? 0u : crc;
       if (P.verify) {
         uint32_t ok = 0;
@@ -2162,7 +2244,7 @@ const DeviceInfo& device_info(int dev) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tso_segment_kernel, kBlock, 0) != hipSuccess || b < 1) b = 1;
   di.seg_blocks_per_cu = b;
   b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, icrc_kernel, kBlock, 0) != hipSuccess || b < 1) b = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, icrc_kernel, kIcrcThreads, 0) != hipSuccess || b < 1) b = 1;
   di.icrc_blocks_per_cu = b;
   return di;
 }
@@ -2361,6 +2443,7 @@ const char* nicgpu_strerror(int status) {
     case NICGPU_ERR_HIP: return "HIP runtime error";
     case NICGPU_ERR_NO_DEVICE: return "no gfx950 device";
     case NICGPU_ERR_NOMEM: return "out of device memory";
+    case NICGPU_ERR_RANGE: return "batch too large for 32-bit piece indices";
     default: return "unknown status";
   }
 }
@@ -2676,10 +2759,10 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
   IcrcParams P{frames, desc, n, mode == NICGPU_ICRC_VERIFY, out_crc, out_ok};
   // every resident wave slot busy (a wave's range is then >= 64 packets, one
   // work-queue refill); ranges of 8 packets per lane left 3/4 of the slots idle
-  const uint64_t want = (n + kBlock - 1) / kBlock;
+  const uint64_t want = (n + kIcrcThreads - 1) / kIcrcThreads;
   const uint64_t cap = (uint64_t) di->cus * (uint64_t) di->icrc_blocks_per_cu;
   const unsigned grid = (unsigned) (want < 1 ? 1 : (want < cap ? want : cap));
-  hipLaunchKernelGGL(icrc_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
+  hipLaunchKernelGGL(icrc_kernel, dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
   return hip_status(hipGetLastError());
 }
 
@@ -2770,16 +2853,18 @@ struct QpDevSink {
   }
 };
 
+// counts[n] must be 0 on entry: a descriptor that plans more than
+// kQpMaxPieces pieces counts 0 and sets it to 1, so the 32-bit scan of the
+// counts (n <= 2^32 / kQpMaxPieces) cannot wrap and the caller sees the flag.
+constexpr uint32_t kQpMaxPieces = 256;
 __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
                                                             uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
                                                             uint32_t* counts) {
-  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i <= n; i += (uint64_t) gridDim.x * kQpBlock) {
-    if (i == n) {
-      counts[n] = 0;
-      continue;
-    }
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
     QpPlan pp;
-    counts[i] = nicqp::plan_packet(max_mtu, mem_size, tx[i], pp, [](uint64_t, uint64_t) {});
+    const uint32_t c = nicqp::plan_packet(max_mtu, mem_size, tx[i], pp, [](uint64_t, uint64_t) {});
+    counts[i] = c <= kQpMaxPieces ? c : 0u;
+    if (c > kQpMaxPieces) counts[n] = 1u;
     plans[i] = pp;
   }
 }
@@ -3163,7 +3248,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
 int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view) {
   if (!q) return NICGPU_ERR_INVALID;
   // 32-bit ring positions; hipcub scans and sorts take int counts
-  if (ntx > 0xFFFFFFFFull / 64u || nrx > 0x7FFFFFFEull) return NICGPU_ERR_INVALID;
+  if (ntx > 0xFFFFFFFFull / kQpMaxPieces || nrx > 0x7FFFFFFEull) return NICGPU_ERR_INVALID;
   DeviceGuard g(q->device);
   int st = NICGPU_OK;
   const size_t t1 = ntx + 1, r1 = nrx + 1;
@@ -3208,14 +3293,19 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
   hipStream_t s = static_cast<hipStream_t>(plan_stream);
   *npieces = 0;
   const unsigned grid = qp_grid(q, ntx + 1);
-  hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->counts);
-  int st = hip_status(hipGetLastError());
-  if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
+  int st = hip_status(hipMemsetAsync(q->counts + ntx, 0, sizeof(uint32_t), s));
+  if (st == NICGPU_OK)
+    hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
+                       q->plans, q->counts);
+  if (st == NICGPU_OK) st = hip_status(hipGetLastError());
   uint32_t* np_h = reinterpret_cast<uint32_t*>(q->misc());
+  // the overflow flag first: the scan below adds it in as the last count
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(np_h + 1, q->counts + ntx, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
   if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(np_h, q->base + ntx, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
   if (st != NICGPU_OK) return st;
+  if (np_h[1] != 0u) return NICGPU_ERR_RANGE;
   const uint64_t np = *np_h;
   st = qp_grow(q->piece_desc, q->c_pdesc, np ? np : 1);
   if (st == NICGPU_OK) st = qp_grow(q->piece_csum, q->c_pcs, np ? np : 1);

@@ -21,6 +21,7 @@
 //   rx_stage_gpu_fuzz <first_seed> <count>
 //   rx_stage_gpu_fuzz full c3|c5 [dev] [keep]
 //   rx_stage_gpu_fuzz check [count]
+//   rx_stage_gpu_fuzz edges             (piece-count limit, descriptor rings inside the image)
 //   rx_stage_gpu_fuzz pipeline [count]   (submit/collect vs process_batch in order)
 #undef NDEBUG
 #include <cassert>
@@ -654,11 +655,116 @@ int run_check(std::uint64_t count) {
   return 0;
 }
 
+// Edge cases of the device path's limits:
+//  - a TX descriptor whose plan has more pieces than 32-bit piece indices
+//    allow per descriptor (a 17 MB plain packet, TX-verified, then dropped for
+//    its MTU: one piece per 64 KiB) makes nicgpu_qp_plan return
+//    NICGPU_ERR_RANGE; the batch must then go to the host path and still equal
+//    the host resolve;
+//  - device descriptor arrays inside the image that an RX buffer of the same
+//    batch overlaps: not modelled, process_batch must throw before writing.
+int run_edges() {
+  const std::size_t big = 17u << 20;  // > 256 * 65534 B
+  const std::size_t mem_size = big + (1u << 20);
+  std::vector<std::uint8_t> image(mem_size);
+  Rng r{777};
+  for (auto& b : image) b = r.byte();
+  std::vector<TxDescriptor> tx(8);
+  for (std::size_t i = 0; i < tx.size(); ++i) {
+    TxDescriptor& t = tx[i];
+    t.buffer_address = i == 3 ? 0 : big + i * 2048;
+    t.length = i == 3 ? static_cast<std::uint32_t>(big) : 1518;
+    t.descriptor_index = static_cast<std::uint16_t>(i);
+    t.checksum = ChecksumMode::Layer4;
+    t.checksum_offload = i == 3 ? false : true;  // descriptor 3: TX verify of 17 MB
+    t.checksum_value = oracle_compute_checksum(image.data() + t.buffer_address, t.length);
+  }
+  std::vector<RxDescriptor> rx(8);
+  for (std::size_t j = 0; j < rx.size(); ++j) {
+    rx[j].buffer_address = big + 512 * 1024 + j * 2048;
+    rx[j].buffer_length = 2048;
+    rx[j].checksum = ChecksumMode::None;
+  }
+  BatchedQueuePairConfig cfg;
+  cfg.max_mtu = 9000;
+  std::vector<std::uint8_t> host_img = image;
+  test::CpuBackend cpu{host_img, nullptr, TupleSpec{}};
+  RxBatchResult ho;
+  QueuePairStats hs{};
+  rx_stage_detail::BatchScratch scratch;
+  rx_stage_detail::run_batch(cfg, mem_size, tx, rx, hs, ho, scratch, cpu);
+  void* d = nullptr;
+  assert(nicgpu_malloc(&d, mem_size + 64) == NICGPU_OK);
+  assert(nicgpu_memcpy_async(d, image.data(), mem_size, nullptr) == NICGPU_OK);
+  BatchedQueuePair qp{cfg};
+  RxBatchResult go;
+  qp.process_batch(DeviceHostMemory{static_cast<std::byte*>(d), mem_size}, tx, rx, go);
+  std::vector<std::uint8_t> dev_img(mem_size);
+  assert(nicgpu_memcpy_async(dev_img.data(), d, mem_size, nullptr) == NICGPU_OK);
+  assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+  bool ok = !go.timings.device && go.tx_completions.size() == ho.tx_completions.size() &&
+            go.rx_completions.size() == ho.rx_completions.size() && host_img == dev_img;
+  for (std::size_t i = 0; ok && i < ho.tx_completions.size(); ++i) ok = same(go.tx_completions[i], ho.tx_completions[i]);
+  for (std::size_t i = 0; ok && i < ho.rx_completions.size(); ++i) ok = same(go.rx_completions[i], ho.rx_completions[i]);
+  ok = ok && std::memcmp(&hs, &qp.stats(), sizeof(hs)) == 0;
+  ok = ok && ho.tx_completions[3].status == static_cast<std::uint32_t>(CompletionCode::MtuExceeded);
+  if (!ok) std::fprintf(stderr, "edges: the over-range batch differs from the host resolve\n");
+  // the piece-count limit itself, straight through the C-ABI
+  {
+    nicgpu_qp* q = nullptr;
+    assert(nicgpu_qp_create(&q, 0) == NICGPU_OK);
+    nicgpu_qp_view v{};
+    assert(nicgpu_qp_reserve(q, tx.size(), rx.size(), &v) == NICGPU_OK);
+    assert(nicgpu_memcpy_async(v.tx, tx.data(), tx.size() * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
+    std::uint64_t np = 0;
+    const int st = nicgpu_qp_plan(q, static_cast<const std::uint8_t*>(d), mem_size, tx.size(), 9000, &np, &v, nullptr);
+    if (st != NICGPU_ERR_RANGE) {
+      std::fprintf(stderr, "edges: nicgpu_qp_plan returned %d, want NICGPU_ERR_RANGE\n", st);
+      ok = false;
+    }
+    tx[3].length = 1518;  // the same batch without the huge packet plans normally
+    assert(nicgpu_memcpy_async(v.tx, tx.data(), tx.size() * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
+    ok = ok && nicgpu_qp_plan(q, static_cast<const std::uint8_t*>(d), mem_size, tx.size(), 9000, &np, &v, nullptr) ==
+                   NICGPU_OK && np == 2 * tx.size();
+    nicgpu_qp_destroy(q);
+  }
+  // descriptor arrays inside the image, overwritten by an RX buffer
+  {
+    std::byte* base = static_cast<std::byte*>(d);
+    const std::size_t ring_at = big + 256 * 1024;  // TX descriptors here, RX ring after them
+    assert(nicgpu_memcpy_async(base + ring_at, tx.data(), tx.size() * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
+    assert(nicgpu_memcpy_async(base + ring_at + 4096, rx.data(), rx.size() * sizeof(RxDescriptor), nullptr) ==
+           NICGPU_OK);
+    std::vector<RxDescriptor> rx2 = rx;
+    const DeviceDescriptors dd{reinterpret_cast<const TxDescriptor*>(base + ring_at), tx.size(),
+                               reinterpret_cast<const RxDescriptor*>(base + ring_at + 4096), rx.size()};
+    BatchedQueuePair qp2{cfg};
+    RxBatchResult o2;
+    qp2.process_batch(DeviceHostMemory{base, mem_size}, dd, o2);  // rings apart from every RX buffer: fine
+    rx2[5].buffer_address = ring_at + 64;  // now RX descriptor 5 writes over the TX descriptor ring
+    assert(nicgpu_memcpy_async(base + ring_at + 4096, rx2.data(), rx2.size() * sizeof(RxDescriptor), nullptr) ==
+           NICGPU_OK);
+    assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+    bool threw = false;
+    try {
+      qp2.process_batch(DeviceHostMemory{base, mem_size}, dd, o2);
+    } catch (const GpuError& e) {
+      threw = e.status() == NICGPU_ERR_INVALID;
+    }
+    if (!threw) std::fprintf(stderr, "edges: an RX buffer over the descriptor ring was not refused\n");
+    ok = ok && threw;
+  }
+  nicgpu_free(d);
+  if (ok) std::printf("rx_stage_gpu_fuzz edges: ok (over-range plan took the host path; ring overwrite refused)\n");
+  return ok ? 0 : 1;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   assert(gpu_device_count() >= 1);
   if (argc > 1 && std::strcmp(argv[1], "check") == 0) return run_check(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 400);
+  if (argc > 1 && std::strcmp(argv[1], "edges") == 0) return run_edges();
   if (argc > 1 && std::strcmp(argv[1], "pipeline") == 0) {
     const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 40;
     int bad = 0;

@@ -118,6 +118,19 @@ def test_rx_stage_device_overlap_check(tmp_path):
     print(r.stdout.strip())
 
 
+@pytest.mark.gpu
+def test_rx_stage_device_limits(tmp_path):
+    """The device path's limits: a descriptor planning more pieces than 32-bit
+    piece indices allow makes nicgpu_qp_plan return NICGPU_ERR_RANGE and the
+    batch takes the host path (equal to the host resolve); descriptor arrays
+    inside the image that an RX buffer of the batch overlaps are refused."""
+    exe = _build(tmp_path, "rx_stage_gpu_fuzz")
+    r = subprocess.run([exe, "edges"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "rx_stage_gpu_fuzz edges: ok" in r.stdout
+    print(r.stdout.strip())
+
+
 @pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="needs /root/reference (build container)")
 def test_rx_stage_fuzz_vs_reference_queue_pair():
     """2000 random batches: the reference QueuePair (compiled in place from
