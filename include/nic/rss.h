@@ -25,6 +25,8 @@
 
 #include "nic/gpu_batch.h"
 
+struct nicgpu_rss_ctx;  // nicgpu.h
+
 namespace nic {
 
 struct RssConfig {
@@ -86,6 +88,11 @@ public:
   /// The stats of `count` select_queue calls whose table-index hits are
   /// `hits` (hashes += count, queue_hits[i] += hits[i] for i < queue_hits.size()).
   void account_batch(std::uint64_t count, std::span<const std::uint64_t> hits) const;
+
+  /// The device key LUT + table on the current HIP device (created on first
+  /// use; valid while the engine lives with this key and table), for fused
+  /// launches such as nicgpu_qp_deliver.  Throws nic::GpuError.
+  [[nodiscard]] const nicgpu_rss_ctx* device_context(void* stream = nullptr) const;
 
 private:
   RssConfig config_;

@@ -391,6 +391,17 @@ int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t nrx, void* stream);
  * runs over the nrx bound with the unlisted entries keyed nq, past every
  * queue, on the low bits that hold 0..nq only.  Enqueued only. */
 int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream);
+/* The DMA writes view.writes[0, nrx) (as nicgpu_segment_gather) and, unless
+ * tuple_mode is NICGPU_TUPLE_NONE, the RSS of every RX completion whose status
+ * is Success, hashed from the bytes its write delivers (as nicgpu_rx_offload
+ * over those frames with ctx and the tuple mode): view.rx_hash / rx_queue per
+ * completion (0 / 0xFFFF for the others), the table-index hits added into
+ * hits_dev (ctx's table size, u64), the Success count in *view.rss_count.  One
+ * launch, the headers taken from the bytes the writes move (no read-back);
+ * nicgpu_qp_group then lists the completions per queue.  Replaces
+ * nicgpu_segment_gather + nicgpu_qp_rss_list + an RSS launch + nicgpu_qp_rss_scatter. */
+int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx, const nicgpu_rss_ctx* ctx,
+                      int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint64_t* hits_dev, void* stream);
 
 #ifdef __cplusplus
 }

@@ -233,6 +233,15 @@ void RssEngine::select_queue_batch_enqueue(const DevicePacketBatch& batch, const
   if (st != NICGPU_OK) throw_gpu("nicgpu_rx_offload_count", st);
 }
 
+const nicgpu_rss_ctx* RssEngine::device_context(void* stream) const {
+  if (config_.table.size() > NICGPU_MAX_TABLE)
+    throw GpuError("device_context: indirection table of " + std::to_string(config_.table.size()) +
+                       " entries exceeds the GPU limit of NICGPU_MAX_TABLE = " + std::to_string(NICGPU_MAX_TABLE),
+                   NICGPU_ERR_INVALID);
+  ensure_gpu(stream);
+  return gpu_->ctx;
+}
+
 void RssEngine::account_batch(std::uint64_t count, std::span<const std::uint64_t> hits) const {
   // identical to `count` sequential select_queue calls (rss.cpp:45, 56-58)
   stats_.hashes += count;

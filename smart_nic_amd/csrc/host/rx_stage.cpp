@@ -1648,20 +1648,22 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   try {
     out.timings.copy_us += us_since(t);
     t = clock::now();
-    if (nrx_total)
-      check(nicgpu_segment_gather(reinterpret_cast<std::uint8_t*>(mem.base), mem.size, v.writes, nrx_total, stream),
-            "nicgpu_segment_gather");
+    // the DMA writes and the RSS of the frames they deliver, one launch
+    // (the headers hashed from the bytes the writes move)
+    const nicgpu_rss_ctx* rctx = nullptr;
+    if (rss) {
+      if (config_.tuple.mode == TupleMode::None)
+        throw GpuError("process_batch: TupleMode::None cannot produce hashes", NICGPU_ERR_INVALID);
+      rctx = config_.rss->device_context(stream);
+      check(nicgpu_memset_async(hits, 0, tn * sizeof(std::uint64_t), stream), "nicgpu_memset_async");
+    }
+    check(nicgpu_qp_deliver(sl.qp, reinterpret_cast<std::uint8_t*>(mem.base), mem.size, nrx_total, rctx,
+                            rss ? static_cast<int>(config_.tuple.mode) : NICGPU_TUPLE_NONE, config_.tuple.raw_offset,
+                            config_.tuple.raw_length, rss ? hits : nullptr, stream),
+          "nicgpu_qp_deliver");
     out.timings.gather_us += us_since(t);
     t = clock::now();
-    if (rss) {
-      check(nicgpu_qp_rss_list(sl.qp, nrx_total, stream), "nicgpu_qp_rss_list");
-      check(nicgpu_memset_async(hits, 0, tn * sizeof(std::uint64_t), stream), "nicgpu_memset_async");
-      config_.rss->select_queue_batch_enqueue(DevicePacketBatch{mem.base, v.rss_desc, nrx_total}, v.rss_count,
-                                              config_.tuple, RxBatchOutputs{nullptr, v.rss_hash, v.rss_queue}, hits,
-                                              stream);
-      check(nicgpu_qp_rss_scatter(sl.qp, nrx_total, stream), "nicgpu_qp_rss_scatter");
-      check(nicgpu_qp_group(sl.qp, nrx_total, nq, stream), "nicgpu_qp_group");
-    }
+    if (rss) check(nicgpu_qp_group(sl.qp, nrx_total, nq, stream), "nicgpu_qp_group");
     check(nicgpu_event_record(sl.ev_done, stream), "nicgpu_event_record");
   } catch (...) {
     sl.wait();  // the downloads must not outlive this batch's buffers

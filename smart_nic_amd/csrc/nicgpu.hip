@@ -1694,6 +1694,270 @@ __global__ __launch_bounds__(kBlock) void segment_gather_kernel(GatherParams P) 
   }
 }
 
+// --------------------------------------------- fused delivery (row f1) --
+// The batched QueuePair stage's DMA writes and the RSS of the frames they
+// deliver in one launch (nicgpu_qp_deliver).  A wave takes a tile of 64 RX
+// completions and walks their bytes as ONE stream of destination 16-B chunks,
+// as the RX kernel walks packets: every write splits into up to three items
+// (VLAN prefix, part A, part B — queue_pair.cpp:352-359, 392-395, 416-426
+// already resolved into the write), every item into the destination chunks it
+// touches, and lane l of a step takes stream entry base + l.  So one wave
+// instruction moves up to 1 KiB whatever the frame sizes (the one-wave-per-
+// write gather left 60 of 64 lanes idle on 64-B frames and kept one write's
+// load latency per wave in flight).  A chunk's source is five dwords from the
+// item's source at the chunk's byte shift; whole chunks are one 16-B store,
+// item edges dword or byte stores, so no byte outside a segment is written.
+//
+// RSS: for a completion with status Success, the lanes whose chunk lies in its
+// frame's first three destination chunks also OR their bytes into the wave's
+// header stage (the RX kernel's 48-B-per-packet layout), and after the tile
+// the owning lane hashes the frame from the stage exactly as rss_only_kernel
+// (rss_hash_packet; bytes past the stage, rare, from the frame just written).
+// The hash and queue land per completion (0 / 0xFFFF for the others), the
+// table-index hits in a block histogram, the Success count in *count — what
+// qp_flag/qp_rss_fill, the RSS launch and qp_scatter produced in four launches
+// with the headers read back from HBM.
+struct DeliverParams {
+  uint8_t* mem;
+  uint64_t mem_size;
+  const nicgpu_segment_write* w;
+  const nicgpu_completion* rxc;  // statuses (RSS of Success completions)
+  uint64_t n;
+  RxParams rss;                  // mode NICGPU_TUPLE_NONE: no RSS
+  uint32_t* rx_hash;
+  uint16_t* rx_queue;
+  unsigned long long* hits;
+  unsigned long long* count;
+};
+
+constexpr int kDlvWpb = 8;  // waves per block
+constexpr uint32_t kDlvRec = 24;  // item record: dst u64 | src (or prefix word) u64 | len u32 | first entry u32
+constexpr uint32_t kDlvWaveBytes = 256u + 64u * 8u + 192u * kDlvRec + 64u * kHdrStride * 16u;  // marks|wdst|items|stage
+
+// block part: RSS LUT | histogram | table (as rss_only_kernel), then 16 B for the Success count
+__host__ __device__ inline uint32_t dlv_block_bytes(bool rss, uint32_t lut_words, uint32_t hist_n,
+                                                    uint32_t table_words) {
+  return (rss ? rss_only_block_bytes(lut_words, hist_n, table_words) : 0u) + 16u;
+}
+
+__device__ __forceinline__ uint32_t dlv_chunks(uint64_t d, uint64_t n) {
+  return n ? (uint32_t) (((d + n - 1) >> 4) - (d >> 4) + 1) : 0u;
+}
+
+// Stores the bytes [lo, hi) (absolute) of the 16-B destination chunk at D
+// from o; whole chunk: one 16-B store, else whole dwords and bytes.
+__device__ __forceinline__ void dlv_store(uint8_t* mem, uint64_t D, uint64_t lo, uint64_t hi, const uint32_t* o) {
+  if (lo == D && hi == D + 16) {
+    u32x4 v = {o[0], o[1], o[2], o[3]};
+    *reinterpret_cast<u32x4*>(mem + D) = v;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t a = D + 4u * i;
+    if (a >= lo && a + 4 <= hi) {
+      *reinterpret_cast<uint32_t*>(mem + a) = o[i];
+    } else if (a + 4 > lo && a < hi) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (a + b >= lo && a + b < hi) mem[a + b] = (uint8_t) (o[i] >> (8 * b));
+    }
+  }
+}
+
+template <bool RSS>
+__global__ __launch_bounds__(kWave * kDlvWpb) void deliver_kernel(DeliverParams P) {
+  constexpr uint32_t kThreads = kWave * kDlvWpb;
+  extern __shared__ uint4 lds_dyn[];
+  const uint32_t w = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
+  const uint32_t lane = lane_id();
+  const RxParams& R = P.rss;
+  const bool hist_lds = RSS && R.table_n <= (uint32_t) kHistLds;
+  const bool table_lds = RSS && R.table_n <= (uint32_t) kTableLds;
+  uint8_t* base_b = reinterpret_cast<uint8_t*>(lds_dyn);
+  uint32_t* lut = reinterpret_cast<uint32_t*>(base_b);
+  uint32_t* hist = lut + (RSS ? R.lut_words : 0u);
+  uint16_t* table_s = reinterpret_cast<uint16_t*>(hist + (hist_lds ? R.table_n : 0u));
+  const uint32_t block_bytes = dlv_block_bytes(RSS, R.lut_words, hist_lds ? R.table_n : 0u,
+                                               table_lds ? (R.table_n + 1u) / 2u : 0u);
+  uint32_t* cnt_s = reinterpret_cast<uint32_t*>(base_b + block_bytes - 16u);
+  uint8_t* wave_b = base_b + block_bytes + w * kDlvWaveBytes;
+  uint32_t* marks = reinterpret_cast<uint32_t*>(wave_b);
+  uint64_t* wdst = reinterpret_cast<uint64_t*>(wave_b + 256u);
+  uint8_t* items = wave_b + 256u + 512u;
+  uint4* stage = reinterpret_cast<uint4*>(items + 192u * kDlvRec);
+  if (RSS) {
+    for (uint32_t i = threadIdx.x; i < R.lut_words; i += kThreads) lut[i] = R.lut[i];
+    if (hist_lds)
+      for (uint32_t i = threadIdx.x; i < R.table_n; i += kThreads) hist[i] = 0;
+    if (table_lds)
+      for (uint32_t i = threadIdx.x; i < R.table_n; i += kThreads) table_s[i] = R.table[i];
+    if (threadIdx.x == 0) *cnt_s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t) kHdrChunks; ++k) stage[hdr_slot(lane, k)] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+  const uint64_t ntiles = (P.n + kWave - 1) / kWave;
+  const uint64_t nwaves = (uint64_t) gridDim.x * kDlvWpb;
+  uint32_t my_count = 0;
+  for (uint64_t tile = (uint64_t) blockIdx.x * kDlvWpb + w; tile < ntiles; tile += nwaves) {
+    // ---- this lane's write: its items and their stream entries
+    const uint64_t j = tile * kWave + lane;
+    nicgpu_segment_write wr{};
+    bool flag = false;
+    if (j < P.n) {
+      wr = P.w[j];
+      if (RSS) flag = P.rxc[j].status == nicqp::kSuccess;
+    }
+    const uint64_t plen = wr.prefix_len == 4 ? 4 : 0;
+    const uint64_t total = plen + wr.len_a + wr.len_b;
+    // entries outside the image are skipped (the host validated them)
+    const bool ok = j < P.n && !(wr.prefix_len > 4 || wr.dst > P.mem_size || total > P.mem_size - wr.dst ||
+                                 wr.src_a > P.mem_size || wr.len_a > P.mem_size - wr.src_a ||
+                                 wr.src_b > P.mem_size || wr.len_b > P.mem_size - wr.src_b);
+    const uint64_t d1 = wr.dst + plen, d2 = d1 + wr.len_a;
+    const uint32_t c0 = ok ? dlv_chunks(wr.dst, plen) : 0u;
+    const uint32_t c1 = ok ? dlv_chunks(d1, wr.len_a) : 0u;
+    const uint32_t c2 = ok ? dlv_chunks(d2, wr.len_b) : 0u;
+    const uint32_t cw = c0 + c1 + c2;
+    const uint32_t incl = wave_incl_scan(cw);
+    const uint32_t F = incl - cw;
+    const uint32_t total_e = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
+    auto put = [&](uint32_t k, uint64_t d, uint64_t src, uint32_t len, uint32_t first) __attribute__((always_inline)) {
+      uint8_t* r = items + (lane * 3u + k) * kDlvRec;
+      *reinterpret_cast<uint64_t*>(r) = d;
+      *reinterpret_cast<uint64_t*>(r + 8) = src;
+      *reinterpret_cast<uint32_t*>(r + 16) = len;
+      *reinterpret_cast<uint32_t*>(r + 20) = first;
+    };
+    put(0, wr.dst, wr.prefix, c0 ? 4u : 0u, F);
+    put(1, d1, wr.src_a, c1 ? wr.len_a : 0u, F + c0);
+    put(2, d2, wr.src_b, c2 ? wr.len_b : 0u, F + c0 + c1);
+    wdst[lane] = (wr.dst >> 4) | (flag && ok ? 1ull << 63 : 0ull);
+    // ---- the stream: 64 entries per step
+    uint32_t carry = 0;  // item (id + 1) of the entry before this step
+    for (uint32_t W = 0; W < total_e; W += kWave) {
+      marks[lane] = 0u;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (c0 && F >= W && F - W < kWave) marks[F - W] = lane * 3u + 1u;
+      if (c1 && F + c0 >= W && F + c0 - W < kWave) marks[F + c0 - W] = lane * 3u + 2u;
+      if (c2 && F + c0 + c1 >= W && F + c0 + c1 - W < kWave) marks[F + c0 + c1 - W] = lane * 3u + 3u;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      uint32_t it = wave_incl_max(marks[lane]);
+      it = it > carry ? it : carry;
+      carry = (uint32_t) __builtin_amdgcn_readlane((int) it, 63);
+      const uint32_t pos = W + lane;
+      if (pos < total_e) {
+        const uint32_t id = it - 1u, q = id / 3u, k = id - 3u * q;
+        const uint8_t* r = items + id * kDlvRec;
+        const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
+        const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
+        const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
+        const uint32_t first = *reinterpret_cast<const uint32_t*>(r + 20);
+        const uint64_t D = ((d >> 4) + (pos - first)) << 4;
+        const uint64_t lo = D > d ? D : d, hi = D + 16 < d + len ? D + 16 : d + len;
+        uint32_t o[4];
+        if (k == 0) {  // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): 4 bytes at d
+          const uint32_t sh = (uint32_t) (d - D);  // may be "negative": the prefix started in the chunk before
+          const uint64_t pw = src & 0xFFFFFFFFull;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const int64_t rel = (int64_t) (D + 4u * i + b) - (int64_t) d;
+              if (rel >= 0 && rel < 4) v |= (uint32_t) ((pw >> (8 * rel)) & 0xFFu) << (8 * b);
+            }
+            o[i] = v;
+          }
+          (void) sh;
+        } else {
+          // source of destination byte D: before the item's source by up to
+          // 15 bytes on its first chunk, so possibly below address 0 (signed)
+          const int64_t a = (int64_t) D + ((int64_t) src - (int64_t) d);
+          const int64_t a4 = a & ~(int64_t) 3;
+          const uint32_t sh = (uint32_t) (a & 3);
+          uint32_t v[5];
+          if (a4 >= 0 && (uint64_t) a4 + 20 <= P.mem_size) {
+            __builtin_memcpy(v, P.mem + a4, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
+            v[4] = *reinterpret_cast<const uint32_t*>(P.mem + a4 + 16);
+          } else {  // bytes outside the image read as 0 (never stored: outside [lo, hi))
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+              uint32_t x = 0;
+#pragma unroll
+              for (int b = 0; b < 4; ++b) {
+                const int64_t e = a4 + 4 * i + b;
+                if (e >= 0 && (uint64_t) e < P.mem_size) x |= (uint32_t) P.mem[e] << (8 * b);
+              }
+              v[i] = x;
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = sh ? __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh) : v[i];
+        }
+        dlv_store(P.mem, D, lo, hi, o);
+        if (RSS) {
+          const uint64_t wd = wdst[q];
+          const uint64_t kc = (D >> 4) - (wd & ~(1ull << 63));
+          if ((wd >> 63) && kc < (uint64_t) kHdrChunks) {
+            uint32_t* st = reinterpret_cast<uint32_t*>(stage + hdr_slot(q, (uint32_t) kc));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uint64_t a = D + 4u * i;
+              const int b0 = lo > a ? (int) (lo - a) : 0, b1 = hi < a + 4 ? (int) (hi - a) : 4;
+              if (b1 > b0) atomicOr(st + i, o[i] & dword_keep(b0, b1, 0));
+            }
+          }
+        }
+      }
+    }
+    if (RSS) {
+      // the frames' bytes are in the stage; bytes past it come from the frame
+      // this wave just wrote (its stores retired first)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (j < P.n) {
+        if (flag && ok) {
+          uint64_t len = total;
+          if (len > NICGPU_MAX_PACKET) len = NICGPU_MAX_PACKET;  // the tuple lies in the first 82 B
+          const uint32_t h = rss_hash_packet(R, lut, HdrView{stage, lane}, (uint32_t) (wr.dst & 15u), P.mem + wr.dst,
+                                             (uint32_t) len);
+          const uint32_t idx = h % R.table_n;
+          P.rx_hash[j] = h;
+          P.rx_queue[j] = table_lds ? table_s[idx] : R.table[idx];
+          if (hist_lds) atomicAdd(&hist[idx], 1u);
+          else atomicAdd(&P.hits[idx], 1ull);
+          ++my_count;
+        } else {
+          P.rx_hash[j] = 0u;
+          P.rx_queue[j] = 0xFFFFu;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+      for (uint32_t k = 0; k < (uint32_t) kHdrChunks; ++k) stage[hdr_slot(lane, k)] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  if (RSS) {
+    const uint32_t c = (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan(my_count), 63);
+    if (lane == 0 && c) atomicAdd(cnt_s, c);
+    __syncthreads();
+    if (threadIdx.x == 0 && *cnt_s) atomicAdd(P.count, (unsigned long long) *cnt_s);
+    if (hist_lds)
+      for (uint32_t i = threadIdx.x; i < R.table_n; i += kThreads) {
+        const uint32_t v = hist[i];
+        if (v) atomicAdd(&P.hits[i], (unsigned long long) v);
+      }
+  }
+}
+
 // ------------------------------------------------- TSO/GSO segmentation --
 // QueuePair::build_segments (src/queue_pair.cpp:212-278) plus the
 // TX VLAN insert (:324-331) and RX VLAN strip (:389-395) that shape each
@@ -1929,18 +2193,13 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
 // nic::rocev2::IcrcCalculator::calculate / verify (src/rocev2/packet.cpp:14-75)
 // over a batch: CRC-32C (reflected 0x82F63B78, init/xorout 0xFFFFFFFF) of
 // every descriptor's span.  One lane owns one packet at a time and walks it
-// to the end of a 128-B line per step (up to 8 x 16-B loads, slice-by-16
-// tables in LDS); a finished lane takes the next packet of its wave's range
-// through a ballot (a wave-level work queue), so IMIX lengths do not leave
-// lanes idle.  Every 16-B chunk, whatever part of it belongs to the packet
-// (head, tail, both, none), goes through one branch-free step: with valid
-// bytes [a, b) and running CRC state S, processing them equals a zero-state
-// slice-by-16 of the chunk after
-//   D ^= S at byte a (the standard "xor the state into the next 4 bytes"),
-//   mask D to [a, b), and look byte i up in the table it would use had the
-//   span been shifted to end at byte 15 (leading zero bytes do not change a
-//   zero state),
-// plus S >> 8(b - a) when the span is shorter than 4 bytes.
+// to the end of a 128-B line per step (up to 8 x 16-B loads); a finished lane
+// takes the next packet of its wave's range through a ballot (a wave-level
+// work queue), so IMIX lengths do not leave lanes idle.  Every 16-B chunk goes
+// through the CRC register whole: bytes before the packet (its first chunk)
+// and past the span (its last) are zeroed, the state enters at byte 0 of the
+// first chunk (kCrcLead), and the k zero bytes the last chunk appends are
+// taken back once per packet by G_k = x^(-8k) (kCrcUnshift).
 struct Crc32cTables {
   uint32_t t[16][256];
 };
@@ -2173,11 +2432,18 @@ __global__ __launch_bounds__(kIcrcThreads) void icrc_kernel(IcrcParams P) {
           m.w &= m0.w;
         }
         x0[u] = v[u].x & m.x;
+#ifndef NICGPU_ICRC_MEMONLY
         part[u] = crc_chunk_part(Tn, v[u].y & m.y, v[u].z & m.z, v[u].w & m.w, cb);
+#endif
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
+#ifdef NICGPU_ICRC_MEMONLY  // timing only: the loads and masks without the table work
+        const uint32_t Sn = (x0[u] ^ S) + v[u].y + v[u].z + v[u].w;
+        (void) part;
+#else
         const uint32_t Sn = part[u] ^ crc_dword_nib<0>(Tn, x0[u] ^ S, cb);
+#endif
         S = (uint32_t) u < nproc ? Sn : S;
       }
       pos = nproc ? (cl + 1u) << 4 : end;
@@ -2364,6 +2630,20 @@ int rss_only_blocks_per_cu(int dev, uint32_t lds) {
       b < 1)
     b = 1;
   di.occ.push_back({kRssOnlyVariant, lds, b});
+  return b;
+}
+
+template <bool RSS>
+int dlv_blocks_per_cu(int dev, uint32_t lds) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  DeviceInfo& di = g_dev[dev & 63];
+  constexpr int kKey = RSS ? -2 : -3;  // occupancy cache key
+  for (const auto& o : di.occ)
+    if (o.variant == kKey && o.lds == lds) return o.blocks;
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, deliver_kernel<RSS>, kWave * kDlvWpb, lds) != hipSuccess || b < 1)
+    b = 1;
+  di.occ.push_back({kKey, lds, b});
   return b;
 }
 
@@ -3001,7 +3281,7 @@ __global__ __launch_bounds__(kQpBlock) void qp_scatter_kernel(const uint32_t* __
 __global__ __launch_bounds__(kQpBlock) void qp_keys_kernel(const uint16_t* __restrict__ q,
                                                            const unsigned long long* __restrict__ count, uint64_t nrx,
                                                            uint32_t nq, uint32_t* key) {
-  const uint64_t m = *count;
+  const uint64_t m = count ? *count : nrx;
   for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < nrx; k += (uint64_t) gridDim.x * kQpBlock)
     key[k] = k < m ? (uint32_t) q[k] : nq;
 }
@@ -3017,7 +3297,7 @@ __global__ __launch_bounds__(kQpBlock) void qp_keys_kernel(const uint16_t* __res
 __global__ __launch_bounds__(kQpBlock) void qp_gcount_kernel(const uint16_t* __restrict__ q,
                                                              const unsigned long long* __restrict__ count,
                                                              uint64_t nrx, uint32_t nq, uint64_t T, uint32_t* cnt) {
-  const uint64_t m = *count;
+  const uint64_t m = count ? *count : nrx;
   const uint32_t lane = lane_id();
   const uint64_t waves = (uint64_t) gridDim.x * (kQpBlock / kWave);
   if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(uint64_t) (nq + 1) * T] = 0u;
@@ -3039,7 +3319,7 @@ __global__ __launch_bounds__(kQpBlock) void qp_gscatter_kernel(const uint16_t* _
                                                                const uint32_t* __restrict__ off,
                                                                const uint32_t* __restrict__ which, uint32_t* out,
                                                                uint32_t* start, uint32_t* end) {
-  const uint64_t m = *count;
+  const uint64_t m = count ? *count : nrx;
   const uint32_t lane = lane_id();
   const uint64_t waves = (uint64_t) gridDim.x * (kQpBlock / kWave);
   const uint64_t gt = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x;
@@ -3056,15 +3336,20 @@ __global__ __launch_bounds__(kQpBlock) void qp_gscatter_kernel(const uint16_t* _
       const uint64_t v = __ballot(key == b);
       if (key == b) rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (v >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) v, 0u));
     }
-    if (k < nrx) out[off[(uint64_t) key * T + t] + rank] = which[k];
+    if (k < nrx) out[off[(uint64_t) key * T + t] + rank] = which ? which[k] : (uint32_t) k;
   }
 }
 
-// queue range boundaries of the first *count sorted keys, for queues below nq
+__global__ __launch_bounds__(kQpBlock) void qp_iota_kernel(uint32_t* v, uint64_t n) {
+  for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < n; k += (uint64_t) gridDim.x * kQpBlock)
+    v[k] = (uint32_t) k;
+}
+
+// queue range boundaries of the first *count (null: nrx) sorted keys, for queues below nq
 __global__ __launch_bounds__(kQpBlock) void qp_bounds_kernel(const uint32_t* __restrict__ key,
-                                                             const unsigned long long* __restrict__ count,
+                                                             const unsigned long long* __restrict__ count, uint64_t nrx,
                                                              uint64_t nq, uint32_t* start, uint32_t* end) {
-  const uint64_t m = *count;
+  const uint64_t m = count ? *count : nrx;
   for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < m; k += (uint64_t) gridDim.x * kQpBlock) {
     const uint32_t q = key[k];
     if (q >= nq) continue;
@@ -3157,6 +3442,7 @@ struct nicgpu_qp {
   uint64_t* misc() const { return hp + (size_t) grid * kQpStats + 2; }
   unsigned grid = 1;
   hipEvent_t planned = nullptr;  // nicgpu_qp_plan_on: the piece descriptors are written
+  bool delivered = false;  // the RSS results are per completion (nicgpu_qp_deliver), not compacted
 };
 
 namespace {
@@ -3417,6 +3703,7 @@ int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, u
 
 int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, void* stream) {
   if (!q || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  q->delivered = false;
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned grid = qp_grid(q, nrx + 1);
@@ -3440,6 +3727,12 @@ int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream) {
     if (st == NICGPU_OK) st = hip_status(hipMemsetAsync(q->queue_end, 0, nq * sizeof(uint32_t), s));
   }
   if (st != NICGPU_OK || nrx == 0) return st;
+  // after nicgpu_qp_deliver: the queue of every completion (0xFFFF unless
+  // Success), in posting order, and the completion's own index as its entry;
+  // after nicgpu_qp_rss_list + scatter: the compacted Success frames
+  const uint16_t* keyq = q->delivered ? q->rx_queue : q->rss_queue;
+  const unsigned long long* cnt = q->delivered ? nullptr : reinterpret_cast<const unsigned long long*>(q->scal + 3);
+  const uint32_t* which = q->delivered ? nullptr : q->which;
   if (nq < kWave) {  // counting sort: counts in sort_key, their scan in sorted_key (both hold nrx + 64)
     const uint64_t T = (nrx + kWave - 1) / kWave;
     const uint64_t nc = (uint64_t) (nq + 1) * T + 1;
@@ -3447,19 +3740,22 @@ int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream) {
     if (st == NICGPU_OK) st = qp_grow(q->sorted_key, q->c_sk, nc);
     if (st != NICGPU_OK) return st;
     const unsigned grid = qp_grid(q, nrx > nq ? nrx : nq);
-    hipLaunchKernelGGL(qp_gcount_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->rss_queue, q->scal + 3, (uint64_t) nrx,
+    hipLaunchKernelGGL(qp_gcount_kernel, dim3(grid), dim3(kQpBlock), 0, s, keyq, cnt, (uint64_t) nrx,
                        (uint32_t) nq, T, q->sort_key);
     st = hip_status(hipGetLastError());
     if (st == NICGPU_OK) st = qp_scan(q, q->sort_key, q->sorted_key, nc, s);
     if (st != NICGPU_OK) return st;
-    hipLaunchKernelGGL(qp_gscatter_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->rss_queue, q->scal + 3,
-                       (uint64_t) nrx, (uint32_t) nq, T, q->sorted_key, q->which, q->queue_which, q->queue_start,
+    hipLaunchKernelGGL(qp_gscatter_kernel, dim3(grid), dim3(kQpBlock), 0, s, keyq, cnt,
+                       (uint64_t) nrx, (uint32_t) nq, T, q->sorted_key, which, q->queue_which, q->queue_start,
                        q->queue_end);
     return hip_status(hipGetLastError());
   }
-  hipLaunchKernelGGL(qp_keys_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->rss_queue, q->scal + 3,
+  hipLaunchKernelGGL(qp_keys_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, keyq, cnt,
                      (uint64_t) nrx, (uint32_t) nq, q->sort_key);
   st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK && q->delivered)  // the sort's values: each completion's index
+    hipLaunchKernelGGL(qp_iota_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->which, (uint64_t) nrx);
+  if (st == NICGPU_OK) st = hip_status(hipGetLastError());
   if (st != NICGPU_OK) return st;
   // stable: each queue keeps its completions in posting order.  Keys run
   // 0..nq, so only their low bits are sorted (16 queues: 5 bits, one pass).
@@ -3474,8 +3770,8 @@ int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream) {
     st = hip_status(hipcub::DeviceRadixSort::SortPairs(q->tmp, tb, q->sort_key, q->sorted_key, q->which,
                                                        q->queue_which, (int) nrx, 0, end_bit, s));
   if (st != NICGPU_OK || nq == 0) return st;
-  hipLaunchKernelGGL(qp_bounds_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->sorted_key, q->scal + 3,
-                     (uint64_t) nq, q->queue_start, q->queue_end);
+  hipLaunchKernelGGL(qp_bounds_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->sorted_key, cnt,
+                     (uint64_t) nrx, (uint64_t) nq, q->queue_start, q->queue_end);
   return hip_status(hipGetLastError());
 }
 
@@ -3486,6 +3782,61 @@ int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t nrx, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(qp_scatter_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->which, q->rss_hash,
                      q->rss_queue, q->scal + 3, q->rx_hash, q->rx_queue);
+  return hip_status(hipGetLastError());
+}
+
+
+int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx, const nicgpu_rss_ctx* ctx,
+                      int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint64_t* hits_dev, void* stream) {
+  if (!q || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  if (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0)) return NICGPU_ERR_INVALID;
+  if (tuple_mode != NICGPU_TUPLE_NONE && tuple_mode != NICGPU_TUPLE_AUTO && tuple_mode != NICGPU_TUPLE_RAW)
+    return NICGPU_ERR_INVALID;
+  if (tuple_mode == NICGPU_TUPLE_RAW && (raw_off > NICGPU_RAW_MAX_END || raw_len > NICGPU_RAW_MAX_END ||
+                                         raw_off + raw_len > NICGPU_RAW_MAX_END))
+    return NICGPU_ERR_INVALID;
+  const bool rss = tuple_mode != NICGPU_TUPLE_NONE;
+  if (rss && (!ctx || ctx->table_n == 0 || !hits_dev || ctx->device != q->device)) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  q->delivered = rss;
+  int st = NICGPU_OK;
+  if (rss) st = hip_status(hipMemsetAsync(q->scal + 3, 0, sizeof(uint64_t), s));
+  if (st != NICGPU_OK || nrx == 0) return st;
+  const DeviceInfo* di = nullptr;
+  st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  DeliverParams P{};
+  P.mem = mem;
+  P.mem_size = mem_size;
+  P.w = q->writes;
+  P.rxc = q->rxc;
+  P.n = nrx;
+  P.rss.mode = tuple_mode;
+  P.rss.raw_off = raw_off;
+  P.rss.raw_len = raw_len;
+  if (rss) {
+    P.rss.lut = ctx->d_lut;
+    P.rss.table = ctx->d_table;
+    P.rss.table_n = (uint32_t) ctx->table_n;
+    P.rss.lut_words = 2u * (tuple_mode == NICGPU_TUPLE_RAW ? raw_len : 36u) * 16u;
+    P.rx_hash = q->rx_hash;
+    P.rx_queue = q->rx_queue;
+    P.hits = reinterpret_cast<unsigned long long*>(hits_dev);
+    P.count = reinterpret_cast<unsigned long long*>(q->scal + 3);
+  }
+  const uint32_t hist_n = (rss && P.rss.table_n <= (uint32_t) kHistLds) ? P.rss.table_n : 0u;
+  const uint32_t table_words = (rss && P.rss.table_n <= (uint32_t) kTableLds) ? (P.rss.table_n + 1u) / 2u : 0u;
+  const uint32_t lds = dlv_block_bytes(rss, P.rss.lut_words, hist_n, table_words) + kDlvWpb * kDlvWaveBytes;
+  int dev = 0;
+  (void) hipGetDevice(&dev);
+  const int bpc = rss ? dlv_blocks_per_cu<true>(dev, lds) : dlv_blocks_per_cu<false>(dev, lds);
+  const uint64_t ntiles = (nrx + kWave - 1) / kWave;
+  const uint64_t want = (ntiles + kDlvWpb - 1) / kDlvWpb;
+  const uint64_t cap = (uint64_t) di->cus * (uint64_t) bpc;
+  const unsigned grid = (unsigned) (want < cap ? want : cap);
+  if (rss) hipLaunchKernelGGL(deliver_kernel<true>, dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+  else hipLaunchKernelGGL(deliver_kernel<false>, dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
   return hip_status(hipGetLastError());
 }
 
