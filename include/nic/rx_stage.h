@@ -158,9 +158,13 @@ struct BatchedQueuePairConfig {
   /// pinned to the allowed CPUs that follow the calling thread's.
   unsigned host_threads{0};
   /// Resolve on the device (nicgpu_qp_*, the decisions of qp_logic.h) when
-  /// the batch's buffers do not overlap and no interrupt callback is set: the
-  /// host then only moves descriptors and completions.  false: every batch is
-  /// resolved on the host (the path the fuzz compares with the reference).
+  /// the batch's buffers do not overlap: the host then only moves descriptors
+  /// and completions.  false: every batch is resolved on the host (the path
+  /// the fuzz compares with the reference).  Interrupt callbacks do not change
+  /// the path: every path resolves without firing them, and
+  /// rx_stage_detail::replay_interrupts fires them from the batch's
+  /// completions, in posting order, on the thread that completes the batch
+  /// (process_batch, or collect for submitted batches).
   bool device_resolve{true};
   /// Leave the results of device-resolved batches in device memory
   /// (RxBatchResult::dev) instead of copying them to the host vectors: for
@@ -240,8 +244,8 @@ public:
   /// batch is collected.  The results, the memory image and the statistics
   /// equal those of process_batch called in submission order; a batch's
   /// QueuePair and RSS statistics are added when it is collected, and a
-  /// batch's error is thrown by its collect().  With an interrupt callback the
-  /// batch is processed during submit(), on the caller's thread.  Throws
+  /// batch's error is thrown by its collect(), which also fires the batch's
+  /// interrupt callbacks (on the caller's thread, in posting order).  Throws
   /// std::logic_error on a fourth submit() or a process_batch() while batches
   /// are pending.
   void submit(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
@@ -275,12 +279,14 @@ private:
   void enqueue(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                const DeviceDescriptors* d, void* stream);
   void check_rings_unwritten(Slot& sl, const DeviceHostMemory& mem, void* stream);
+  void fire_interrupts(const RxBatchResult& r);  // config_.on_interrupt over r's completions
   std::pair<std::span<const TxDescriptor>, std::span<const RxDescriptor>> host_spans(
       Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx, void* stream);
   // the host path (buffers_disjoint unless `disjoint` is known, then run_batch)
   void on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                QueuePairStats& stats, RxBatchResult& out, void* stream, int disjoint, double& check_us);
   BatchedQueuePairConfig config_;
+  BatchedQueuePairConfig quiet_;  // config_ without the interrupt callback (every resolve; replayed after)
   QueuePairStats stats_{};
   std::unique_ptr<Scratch> scratch_;
 };
@@ -383,6 +389,22 @@ std::size_t resolve_relaxed(const BatchedQueuePairConfig& config, std::size_t me
                             std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
                             std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx, int max_steps,
                             std::size_t& rx_used, int& steps);
+
+/// The interrupt callbacks of a batch (QueuePair::process_once with an
+/// InterruptDispatcher, queue_pair.cpp:371-383), fired from its completions in
+/// posting order — what resolve's own firing delivers, so every path can
+/// resolve without a callback (on the device, in parallel) and fire after.
+/// Per TX descriptor, in order: its RX completions (each an RX interrupt when
+/// enable_rx_interrupts), then its TX completion's interrupt when
+/// enable_tx_interrupts and the reference fires one: a drop before any RX
+/// descriptor is popped (no RX completion), or every segment delivered with
+/// Success.  The TX completions that fire none (BufferTooSmall, a DMA write
+/// fault or a failed RX verify of a segment: queue_pair.cpp:398-399, 442-443)
+/// are the ones whose packet ends at a non-Success RX completion, so the RX
+/// completions a packet posted are its Success ones up to the first that is
+/// not, at most segments_produced of them.
+void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> tx_completions,
+                       std::span<const CompletionEntry> rx_completions);
 
 /// Order of the DMA writes of one resolved sub-batch for parallel gathers.
 /// Writes (RX completions j with write_of_rx[j] >= 0 and at least one byte) are

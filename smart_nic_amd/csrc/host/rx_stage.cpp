@@ -121,6 +121,34 @@ std::uint32_t plan_packet(const BatchedQueuePairConfig& config, std::size_t mem_
 
 }  // namespace
 
+void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> txc,
+                       std::span<const CompletionEntry> rxc) {
+  if (!config.on_interrupt || (!config.enable_tx_interrupts && !config.enable_rx_interrupts)) return;
+  constexpr auto kOk = static_cast<std::uint32_t>(CompletionCode::Success);
+  constexpr auto kFault = static_cast<std::uint32_t>(CompletionCode::Fault);
+  const std::uint16_t q = config.queue_id;
+  std::size_t j = 0;
+  for (const CompletionEntry& t : txc) {
+    // the packets that popped RX descriptors: Success (all delivered, or an
+    // RX-side abort), and a DMA write fault after some segment (segments_produced > 0)
+    const bool popped = t.status == kOk || (t.status == kFault && t.segments_produced > 0);
+    bool fires = !popped;
+    if (popped) {
+      fires = true;
+      for (std::uint32_t k = 0; k < t.segments_produced && j < rxc.size(); ++k) {
+        const CompletionEntry& e = rxc[j++];
+        if (config.enable_rx_interrupts) config.on_interrupt(q, e);
+        if (e.status != kOk) {  // the packet ends here and its TX completion fires none
+          fires = false;
+          break;
+        }
+      }
+      if (t.status != kOk) fires = false;
+    }
+    if (fires && config.enable_tx_interrupts) config.on_interrupt(q, t);
+  }
+}
+
 // Count pass, prefix over the chunks, fill pass (each chunk in its own thread).
 Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx) {
   Plan plan;
@@ -1030,6 +1058,7 @@ struct BatchedQueuePair::Scratch {
   HostBuf h_desc, h_csum, h_writes, h_rss_desc, h_hash, h_queue;
   rx_stage_detail::BatchScratch host;
   std::vector<std::uint16_t> tail_cs;
+  std::vector<CompletionEntry> irq_tx, irq_rx;  // completions fetched for the interrupt callbacks
   // device resolve: side streams for uploads beside the plan and downloads
   // beside the next steps, created with the slots on the current device
   int device = -1;
@@ -1174,7 +1203,9 @@ private:
 }  // namespace
 
 BatchedQueuePair::BatchedQueuePair(BatchedQueuePairConfig config)
-    : config_(std::move(config)), scratch_(std::make_unique<Scratch>()) {}
+    : config_(std::move(config)), quiet_(config_), scratch_(std::make_unique<Scratch>()) {
+  quiet_.on_interrupt = nullptr;
+}
 BatchedQueuePair::~BatchedQueuePair() = default;
 // The job thread's queued batches call back into the object that submitted
 // them, so a move first lets them finish (their downloads and collect() need
@@ -1182,6 +1213,7 @@ BatchedQueuePair::~BatchedQueuePair() = default;
 BatchedQueuePair::BatchedQueuePair(BatchedQueuePair&& o) noexcept {
   if (o.scratch_) o.scratch_->jobs.stop();
   config_ = std::move(o.config_);
+  quiet_ = std::move(o.quiet_);
   stats_ = o.stats_;
   scratch_ = std::move(o.scratch_);
 }
@@ -1190,6 +1222,7 @@ BatchedQueuePair& BatchedQueuePair::operator=(BatchedQueuePair&& o) noexcept {
     if (scratch_) scratch_->jobs.stop();
     if (o.scratch_) o.scratch_->jobs.stop();
     config_ = std::move(o.config_);
+    quiet_ = std::move(o.quiet_);
     stats_ = o.stats_;
     scratch_ = std::move(o.scratch_);
   }
@@ -1212,7 +1245,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
   int disjoint = -1;  // unknown; the device path checks on the device
   double check_us = 0;
   bool on_device = false;
-  if (config_.device_resolve && !config_.on_interrupt) {
+  if (config_.device_resolve) {
     int dev = 0;
     check(nicgpu_get_device(&dev), "nicgpu_get_device");
     scratch_->ensure(dev);
@@ -1229,6 +1262,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
   if (!on_device) on_host(mem, tx, rx, st, out, stream, disjoint, check_us);
   out.timings.check_us = check_us;
   stats_ = st;
+  if (config_.on_interrupt) fire_interrupts(out);
 }
 
 void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
@@ -1242,7 +1276,7 @@ void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDe
     check_us += std::chrono::duration<double, std::micro>(clock::now() - t0).count();
   }
   GpuBackend dev{*scratch_, mem, config_, stream};
-  rx_stage_detail::run_batch(config_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint);
+  rx_stage_detail::run_batch(quiet_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint);
 }
 
 void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDescriptors& d, RxBatchResult& out,
@@ -1264,7 +1298,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDe
   int disjoint = -1;
   double check_us = 0;
   bool on_device = false;
-  if (config_.device_resolve && !config_.on_interrupt) {
+  if (config_.device_resolve) {
     on_device = front(sl, mem, {}, {}, st, out, stream, disjoint, check_us);
     if (on_device) {
       back(sl, mem, out, stream);
@@ -1278,6 +1312,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDe
   }
   out.timings.check_us = check_us;
   stats_ = st;
+  if (config_.on_interrupt) fire_interrupts(out);
 }
 
 // Device descriptor arrays inside the image: no RX buffer of the batch may
@@ -1361,7 +1396,7 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
   sl.ntx_dev = d ? d->ntx : 0;
   sl.nrx_dev = d ? d->nrx : 0;
   sl.fetched = false;
-  const bool device = config_.device_resolve && !config_.on_interrupt;
+  const bool device = config_.device_resolve;
   // host descriptors go up now, on this thread, beside the earlier batches'
   // device work (device descriptors are copied in the job, in stream order);
   // the rest runs in submission order on the job thread
@@ -1390,9 +1425,7 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
     }
   };
   ++S.pending;
-  // an interrupt callback keeps firing on the caller's thread
-  if (config_.on_interrupt) run();
-  else S.jobs.push(run);
+  S.jobs.push(run);  // interrupt callbacks fire in collect(), on the caller's thread
 }
 
 bool BatchedQueuePair::collect(RxBatchResult& out) {
@@ -1406,7 +1439,27 @@ bool BatchedQueuePair::collect(RxBatchResult& out) {
   if (sl.on_device) finish(sl, sl.result);
   rx_stage_detail::add_stats(stats_, sl.stats);
   std::swap(out, sl.result);
+  if (config_.on_interrupt) fire_interrupts(out);
   return true;
+}
+
+// Completions still on the device (results_on_device) are fetched first.
+void BatchedQueuePair::fire_interrupts(const RxBatchResult& r) {
+  if (!r.timings.device || !config_.results_on_device) {
+    rx_stage_detail::replay_interrupts(config_, r.tx_completions, r.rx_completions);
+    return;
+  }
+  Scratch& S = *scratch_;
+  S.irq_tx.resize(r.dev.ntx);
+  S.irq_rx.resize(r.dev.nrx);
+  if (r.dev.ntx)
+    check(nicgpu_memcpy_async(S.irq_tx.data(), r.dev.tx_completions, r.dev.ntx * sizeof(CompletionEntry), nullptr),
+          "nicgpu_memcpy_async");
+  if (r.dev.nrx)
+    check(nicgpu_memcpy_async(S.irq_rx.data(), r.dev.rx_completions, r.dev.nrx * sizeof(CompletionEntry), nullptr),
+          "nicgpu_memcpy_async");
+  check(nicgpu_stream_synchronize(nullptr), "nicgpu_stream_synchronize");
+  rx_stage_detail::replay_interrupts(config_, S.irq_tx, S.irq_rx);
 }
 
 std::size_t BatchedQueuePair::pending() const noexcept { return scratch_->pending; }
@@ -1552,7 +1605,7 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     check(nicgpu_memcpy_async(S.tail_cs.data(), v.piece_csum + pb, S.tail_cs.size() * 2, stream), "nicgpu_memcpy_async");
     check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
     RxBatchResult& part = S.host.part;
-    resolve(config_, mem.size, S.host.plan, S.tail_cs, tail_tx, tail_rx, st, part, S.host.writes, S.host.write_of_rx);
+    resolve(quiet_, mem.size, S.host.plan, S.tail_cs, tail_tx, tail_rx, st, part, S.host.writes, S.host.write_of_rx);
     const std::size_t tr = part.rx_completions.size();
     check(nicgpu_memcpy_async(v.txc + done, part.tx_completions.data(), part.tx_completions.size() * sizeof(CompletionEntry),
                               stream),

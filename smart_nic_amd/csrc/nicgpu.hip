@@ -1731,8 +1731,10 @@ struct DeliverParams {
 };
 
 constexpr int kDlvWpb = 8;  // waves per block
+constexpr int kDlvU = 4;    // 64-entry sub-steps per step (loads in flight per lane)
 constexpr uint32_t kDlvRec = 24;  // item record: dst u64 | src (or prefix word) u64 | len u32 | first entry u32
-constexpr uint32_t kDlvWaveBytes = 256u + 64u * 8u + 192u * kDlvRec + 64u * kHdrStride * 16u;  // marks|wdst|items|stage
+constexpr uint32_t kDlvMarks = 4u * kWave * kDlvU;  // bytes
+constexpr uint32_t kDlvWaveBytes = kDlvMarks + 64u * 8u + 192u * kDlvRec + 64u * kHdrStride * 16u;  // marks|wdst|items|stage
 
 // block part: RSS LUT | histogram | table (as rss_only_kernel), then 16 B for the Success count
 __host__ __device__ inline uint32_t dlv_block_bytes(bool rss, uint32_t lut_words, uint32_t hist_n,
@@ -1766,7 +1768,7 @@ __device__ __forceinline__ void dlv_store(uint8_t* mem, uint64_t D, uint64_t lo,
 }
 
 template <bool RSS>
-__global__ __launch_bounds__(kWave * kDlvWpb) void deliver_kernel(DeliverParams P) {
+__global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu(4, 8))) void deliver_kernel(DeliverParams P) {
   constexpr uint32_t kThreads = kWave * kDlvWpb;
   extern __shared__ uint4 lds_dyn[];
   const uint32_t w = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
@@ -1783,8 +1785,8 @@ __global__ __launch_bounds__(kWave * kDlvWpb) void deliver_kernel(DeliverParams 
   uint32_t* cnt_s = reinterpret_cast<uint32_t*>(base_b + block_bytes - 16u);
   uint8_t* wave_b = base_b + block_bytes + w * kDlvWaveBytes;
   uint32_t* marks = reinterpret_cast<uint32_t*>(wave_b);
-  uint64_t* wdst = reinterpret_cast<uint64_t*>(wave_b + 256u);
-  uint8_t* items = wave_b + 256u + 512u;
+  uint64_t* wdst = reinterpret_cast<uint64_t*>(wave_b + kDlvMarks);
+  uint8_t* items = wave_b + kDlvMarks + 512u;
   uint4* stage = reinterpret_cast<uint4*>(items + 192u * kDlvRec);
   if (RSS) {
     for (uint32_t i = threadIdx.x; i < R.lut_words; i += kThreads) lut[i] = R.lut[i];
@@ -1834,72 +1836,100 @@ __global__ __launch_bounds__(kWave * kDlvWpb) void deliver_kernel(DeliverParams 
     put(1, d1, wr.src_a, c1 ? wr.len_a : 0u, F + c0);
     put(2, d2, wr.src_b, c2 ? wr.len_b : 0u, F + c0 + c1);
     wdst[lane] = (wr.dst >> 4) | (flag && ok ? 1ull << 63 : 0ull);
-    // ---- the stream: 64 entries per step
+    // ---- the stream: kDlvU x 64 entries per step, every load of the step
+    // issued before its first store (one memory latency per step)
     uint32_t carry = 0;  // item (id + 1) of the entry before this step
-    for (uint32_t W = 0; W < total_e; W += kWave) {
-      marks[lane] = 0u;
+    for (uint32_t W = 0; W < total_e; W += kWave * kDlvU) {
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) marks[u * kWave + lane] = 0u;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      if (c0 && F >= W && F - W < kWave) marks[F - W] = lane * 3u + 1u;
-      if (c1 && F + c0 >= W && F + c0 - W < kWave) marks[F + c0 - W] = lane * 3u + 2u;
-      if (c2 && F + c0 + c1 >= W && F + c0 + c1 - W < kWave) marks[F + c0 + c1 - W] = lane * 3u + 3u;
+      constexpr uint32_t kSpan = kWave * kDlvU;
+      if (c0 && F >= W && F - W < kSpan) marks[F - W] = lane * 3u + 1u;
+      if (c1 && F + c0 >= W && F + c0 - W < kSpan) marks[F + c0 - W] = lane * 3u + 2u;
+      if (c2 && F + c0 + c1 >= W && F + c0 + c1 - W < kSpan) marks[F + c0 + c1 - W] = lane * 3u + 3u;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      uint32_t it = wave_incl_max(marks[lane]);
-      it = it > carry ? it : carry;
-      carry = (uint32_t) __builtin_amdgcn_readlane((int) it, 63);
-      const uint32_t pos = W + lane;
-      if (pos < total_e) {
-        const uint32_t id = it - 1u, q = id / 3u, k = id - 3u * q;
-        const uint8_t* r = items + id * kDlvRec;
-        const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
-        const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
-        const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
-        const uint32_t first = *reinterpret_cast<const uint32_t*>(r + 20);
-        const uint64_t D = ((d >> 4) + (pos - first)) << 4;
-        const uint64_t lo = D > d ? D : d, hi = D + 16 < d + len ? D + 16 : d + len;
+      uint32_t itv[kDlvU];
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) {
+        uint32_t it = wave_incl_max(marks[u * kWave + lane]);
+        it = it > carry ? it : carry;
+        carry = (uint32_t) __builtin_amdgcn_readlane((int) it, 63);
+        itv[u] = it;
+      }
+      // phase A: every entry's chunk, item and source window; loads issued
+      uint64_t Dv[kDlvU], lov[kDlvU], hiv[kDlvU], dv[kDlvU], pwv[kDlvU];
+      uint32_t vv[kDlvU][5], shv[kDlvU], idv[kDlvU];
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) {
+        const uint32_t pos = W + (uint32_t) u * kWave + lane;
+        idv[u] = pos < total_e ? itv[u] - 1u : 0xFFFFFFFFu;
+        Dv[u] = lov[u] = hiv[u] = dv[u] = pwv[u] = 0;
+        shv[u] = 0;
+        if (pos < total_e) {
+          const uint32_t id = itv[u] - 1u, q = id / 3u, k = id - 3u * q;
+          const uint8_t* r = items + id * kDlvRec;
+          const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
+          const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
+          const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
+          const uint32_t first = *reinterpret_cast<const uint32_t*>(r + 20);
+          const uint64_t D = ((d >> 4) + (pos - first)) << 4;
+          Dv[u] = D;
+          dv[u] = d;
+          lov[u] = D > d ? D : d;
+          hiv[u] = D + 16 < d + len ? D + 16 : d + len;
+          if (k == 0) {
+            pwv[u] = src & 0xFFFFFFFFull;  // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): 4 bytes at d
+          } else {
+            // source of destination byte D: before the item's source by up to
+            // 15 bytes on its first chunk, so possibly below address 0 (signed)
+            const int64_t a = (int64_t) D + ((int64_t) src - (int64_t) d);
+            const int64_t a4 = a & ~(int64_t) 3;
+            shv[u] = (uint32_t) (a & 3) | 4u;  // bit 2: a source window (not the prefix)
+            if (a4 >= 0 && (uint64_t) a4 + 20 <= P.mem_size) {
+              __builtin_memcpy(vv[u], P.mem + a4, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
+              vv[u][4] = *reinterpret_cast<const uint32_t*>(P.mem + a4 + 16);
+            } else {  // bytes outside the image read as 0 (never stored: outside [lo, hi))
+#pragma unroll
+              for (int i = 0; i < 5; ++i) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                  const int64_t e = a4 + 4 * i + bb;
+                  if (e >= 0 && (uint64_t) e < P.mem_size) x |= (uint32_t) P.mem[e] << (8 * bb);
+                }
+                vv[u][i] = x;
+              }
+            }
+          }
+        }
+      }
+      // phase B: align, store, and the header stage of Success frames
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) {
+        if (idv[u] == 0xFFFFFFFFu) continue;
+        const uint64_t D = Dv[u], lo = lov[u], hi = hiv[u];
         uint32_t o[4];
-        if (k == 0) {  // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): 4 bytes at d
-          const uint32_t sh = (uint32_t) (d - D);  // may be "negative": the prefix started in the chunk before
-          const uint64_t pw = src & 0xFFFFFFFFull;
+        if (shv[u] & 4u) {
+          const uint32_t sh = shv[u] & 3u;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = sh ? __builtin_amdgcn_alignbyte(vv[u][i + 1], vv[u][i], sh) : vv[u][i];
+        } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             uint32_t v = 0;
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-              const int64_t rel = (int64_t) (D + 4u * i + b) - (int64_t) d;
-              if (rel >= 0 && rel < 4) v |= (uint32_t) ((pw >> (8 * rel)) & 0xFFu) << (8 * b);
+            for (int bb = 0; bb < 4; ++bb) {
+              const int64_t rel = (int64_t) (D + 4u * i + bb) - (int64_t) dv[u];
+              if (rel >= 0 && rel < 4) v |= (uint32_t) ((pwv[u] >> (8 * rel)) & 0xFFu) << (8 * bb);
             }
             o[i] = v;
           }
-          (void) sh;
-        } else {
-          // source of destination byte D: before the item's source by up to
-          // 15 bytes on its first chunk, so possibly below address 0 (signed)
-          const int64_t a = (int64_t) D + ((int64_t) src - (int64_t) d);
-          const int64_t a4 = a & ~(int64_t) 3;
-          const uint32_t sh = (uint32_t) (a & 3);
-          uint32_t v[5];
-          if (a4 >= 0 && (uint64_t) a4 + 20 <= P.mem_size) {
-            __builtin_memcpy(v, P.mem + a4, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
-            v[4] = *reinterpret_cast<const uint32_t*>(P.mem + a4 + 16);
-          } else {  // bytes outside the image read as 0 (never stored: outside [lo, hi))
-#pragma unroll
-            for (int i = 0; i < 5; ++i) {
-              uint32_t x = 0;
-#pragma unroll
-              for (int b = 0; b < 4; ++b) {
-                const int64_t e = a4 + 4 * i + b;
-                if (e >= 0 && (uint64_t) e < P.mem_size) x |= (uint32_t) P.mem[e] << (8 * b);
-              }
-              v[i] = x;
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) o[i] = sh ? __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh) : v[i];
         }
         dlv_store(P.mem, D, lo, hi, o);
         if (RSS) {
+          const uint32_t q = idv[u] / 3u;
           const uint64_t wd = wdst[q];
           const uint64_t kc = (D >> 4) - (wd & ~(1ull << 63));
           if ((wd >> 63) && kc < (uint64_t) kHdrChunks) {

@@ -314,9 +314,11 @@ int run_case(std::uint64_t seed) {
   cfg.enable_tx_interrupts = tx_irq;
   cfg.enable_rx_interrupts = rx_irq;
   std::size_t our_irq = 0;
-  cfg.on_interrupt = [&](std::uint16_t q, const CompletionEntry&) {
+  std::vector<CompletionEntry> fired;  // what resolve's own firing delivered, in order
+  cfg.on_interrupt = [&](std::uint16_t q, const CompletionEntry& e) {
     assert(q == qid);
     ++our_irq;
+    fired.push_back(e);
   };
   RssEngine engine{rss_cfg};
   cfg.rss = &engine;
@@ -432,7 +434,23 @@ int run_case(std::uint64_t seed) {
     rss_ok = rss_ok && listed == delivered;
   }
 
-  bool ok = rss_ok && out.tx_completions.size() == ref_tx.size() && out.rx_completions.size() == ref_rx.size();
+  // the replay from the completions (what the device path and the pipelined
+  // stage fire) delivers the same callbacks in the same order
+  bool irq_ok = true;
+  {
+    std::vector<CompletionEntry> replayed;
+    BatchedQueuePairConfig rcfg = cfg;
+    rcfg.on_interrupt = [&](std::uint16_t q, const CompletionEntry& e) {
+      irq_ok = irq_ok && q == qid;
+      replayed.push_back(e);
+    };
+    replay_interrupts(rcfg, out.tx_completions, out.rx_completions);
+    irq_ok = irq_ok && replayed.size() == fired.size();
+    for (std::size_t i = 0; irq_ok && i < fired.size(); ++i) irq_ok = same(replayed[i], fired[i]);
+    if (!irq_ok) std::fprintf(stderr, "seed %llu: replayed interrupts differ (%zu / %zu)\n", (unsigned long long) seed,
+                              replayed.size(), fired.size());
+  }
+  bool ok = irq_ok && rss_ok && out.tx_completions.size() == ref_tx.size() && out.rx_completions.size() == ref_rx.size();
   for (std::size_t i = 0; ok && i < ref_tx.size(); ++i) ok = same(out.tx_completions[i], ref_tx[i]);
   for (std::size_t i = 0; ok && i < ref_rx.size(); ++i) ok = same(out.rx_completions[i], ref_rx[i]);
   ok = ok && same(st, qp.stats());

@@ -73,6 +73,7 @@ const std::vector<std::uint8_t> kMsKey = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x
                                           0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
 
 std::size_t g_tail = 0, g_device = 0, g_short = 0, g_devdesc = 0;  // host tails, device batches, NoDescriptor, device descriptors
+std::size_t g_irq = 0;  // interrupt callbacks compared
 
 // BatchedQueuePairConfig::results_on_device: copy RxBatchResult::dev into the
 // host vectors, as the host-result form fills them, so the comparisons apply.
@@ -190,6 +191,14 @@ int run_case(std::uint64_t seed) {
   cfg.queue_id = qid;
   cfg.max_mtu = max_mtu;
   if (!rx_stage_detail::buffers_disjoint(mem_size, tx, rx)) return 0;  // the host path's business (rx_stage_fuzz)
+  // interrupt callbacks on most seeds: the host resolve fires them as it
+  // posts; the device path replays them from the completions afterwards
+  const bool irq = (seed % 4) != 3;
+  cfg.enable_tx_interrupts = r.below(2);
+  cfg.enable_rx_interrupts = r.below(4) != 0;
+  std::vector<CompletionEntry> fired_host, fired_dev;
+  if (irq)
+    cfg.on_interrupt = [&fired_host](std::uint16_t, const CompletionEntry& e) { fired_host.push_back(e); };
 
   // host resolve
   RssEngine host_rss{rss_cfg};
@@ -217,6 +226,7 @@ int run_case(std::uint64_t seed) {
   if (ntx) assert(nicgpu_memcpy_async(base + desc_at, tx.data(), ntx * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
   if (nrx) assert(nicgpu_memcpy_async(base + rx_at, rx.data(), nrx * sizeof(RxDescriptor), nullptr) == NICGPU_OK);
   cfg.results_on_device = keep;
+  if (irq) cfg.on_interrupt = [&fired_dev](std::uint16_t, const CompletionEntry& e) { fired_dev.push_back(e); };
   BatchedQueuePair qp{cfg};
   RxBatchResult go;
   if (dev_desc) {
@@ -227,6 +237,14 @@ int run_case(std::uint64_t seed) {
   } else {
     qp.process_batch(DeviceHostMemory{base, mem_size}, tx, rx, go);
   }
+  bool irq_ok = fired_dev.size() == fired_host.size();
+  for (std::size_t i = 0; irq_ok && i < fired_host.size(); ++i) irq_ok = same(fired_dev[i], fired_host[i]);
+  if (!irq_ok) {
+    std::fprintf(stderr, "seed %llu: interrupt callbacks differ (%zu device, %zu host)\n", (unsigned long long) seed,
+                 fired_dev.size(), fired_host.size());
+    return 1;
+  }
+  g_irq += irq ? fired_dev.size() : 0;
   if (keep && !materialize(go)) {
     std::fprintf(stderr, "results on the device: the view is not as documented\n");
     return 1;
@@ -328,6 +346,12 @@ int run_full(const char* wl, bool dev_desc, bool keep) {
   const RssConfig rss_cfg{kMsKey, table};
   BatchedQueuePairConfig cfg;
   cfg.queue_id = 1;
+  // RX and TX interrupt callbacks on: fired by the host resolve as it posts,
+  // replayed by the device path from the completions
+  cfg.enable_tx_interrupts = true;
+  const bool irq = true;
+  std::vector<CompletionEntry> fired_host, fired_dev;
+  cfg.on_interrupt = [&fired_host](std::uint16_t, const CompletionEntry& e) { fired_host.push_back(e); };
   RssEngine host_rss{rss_cfg};
   cfg.rss = &host_rss;
   std::vector<std::uint8_t> host_img = image;
@@ -348,6 +372,7 @@ int run_full(const char* wl, bool dev_desc, bool keep) {
   if (ntx) assert(nicgpu_memcpy_async(base + desc_at, tx.data(), ntx * sizeof(TxDescriptor), nullptr) == NICGPU_OK);
   if (nrx) assert(nicgpu_memcpy_async(base + rx_at, rx.data(), nrx * sizeof(RxDescriptor), nullptr) == NICGPU_OK);
   cfg.results_on_device = keep;
+  if (irq) cfg.on_interrupt = [&fired_dev](std::uint16_t, const CompletionEntry& e) { fired_dev.push_back(e); };
   BatchedQueuePair qp{cfg};
   RxBatchResult go;
   if (dev_desc) {
@@ -358,6 +383,10 @@ int run_full(const char* wl, bool dev_desc, bool keep) {
   } else {
     qp.process_batch(DeviceHostMemory{base, mem_size}, tx, rx, go);
   }
+  bool irq_ok = fired_dev.size() == fired_host.size() && !fired_host.empty();
+  for (std::size_t i = 0; irq_ok && i < fired_host.size(); ++i) irq_ok = same(fired_dev[i], fired_host[i]);
+  if (!irq_ok) std::fprintf(stderr, "full %s: interrupt callbacks differ (%zu device, %zu host)\n", wl,
+                            fired_dev.size(), fired_host.size());
   if (keep && !materialize(go)) {
     std::fprintf(stderr, "results on the device: the view is not as documented\n");
     return 1;
@@ -373,12 +402,13 @@ int run_full(const char* wl, bool dev_desc, bool keep) {
   ok = ok && std::memcmp(&hs, &qp.stats(), sizeof(hs)) == 0 && go.rx_consumed == ho.rx_consumed;
   ok = ok && host_img == dev_img && go.rx_hash == ho.rx_hash && go.rx_queue == ho.rx_queue && go.queues == ho.queues;
   ok = ok && dev_rss.stats().hashes == host_rss.stats().hashes && dev_rss.stats().queue_hits == host_rss.stats().queue_hits;
+  ok = ok && irq_ok;
   std::size_t succ = 0;
   for (const auto& c : go.rx_completions) succ += c.status == 0;
   std::printf("rx_stage_gpu_fuzz full %s: %s (%zu TX, %zu RX completions, %zu Success, device %d, host tail %d, device "
-              "descriptors %d)\n",
+              "descriptors %d, %zu interrupt callbacks)\n",
               wl, ok ? "ok" : "MISMATCH", go.tx_completions.size(), go.rx_completions.size(), succ,
-              int(go.timings.device), int(go.timings.host_tail), int(dev_desc));
+              int(go.timings.device), int(go.timings.host_tail), int(dev_desc), fired_dev.size());
   return ok ? 0 : 1;
 }
 
@@ -461,8 +491,12 @@ int run_pipeline(std::uint64_t seed) {
 
   RssEngine rss_seq{rss_cfg}, rss_pipe{rss_cfg};
   cfg.rss = &rss_seq;
+  cfg.enable_tx_interrupts = r.below(2);
+  std::vector<CompletionEntry> irq_seq, irq_pipe;
+  cfg.on_interrupt = [&irq_seq](std::uint16_t, const CompletionEntry& e) { irq_seq.push_back(e); };
   BatchedQueuePair seq{cfg};
   cfg.rss = &rss_pipe;
+  cfg.on_interrupt = [&irq_pipe](std::uint16_t, const CompletionEntry& e) { irq_pipe.push_back(e); };
   const bool keep = (seed >> 1) & 1;  // results_on_device on the pipelined side
   cfg.results_on_device = keep;
   BatchedQueuePair pipe{cfg};
@@ -552,6 +586,10 @@ int run_pipeline(std::uint64_t seed) {
   g_pipe_batches += nb;
   if (dev_desc) g_pipe_devdesc += nb;
   ok = ok && std::memcmp(&seq.stats(), &pipe.stats(), sizeof(QueuePairStats)) == 0;
+  bool irq_ok = irq_seq.size() == irq_pipe.size();
+  for (std::size_t i = 0; irq_ok && i < irq_seq.size(); ++i) irq_ok = same(irq_seq[i], irq_pipe[i]);
+  if (!irq_ok) std::fprintf(stderr, "pipeline seed %llu: interrupt callbacks differ\n", (unsigned long long) seed);
+  ok = ok && irq_ok;
   ok = ok && rss_seq.stats().hashes == rss_pipe.stats().hashes && rss_seq.stats().queue_hits == rss_pipe.stats().queue_hits;
   std::vector<std::uint8_t> a(mem_size), b(mem_size);
   assert(nicgpu_memcpy_async(a.data(), d_seq, mem_size, nullptr) == NICGPU_OK);
@@ -789,7 +827,8 @@ int main(int argc, char** argv) {
   for (std::uint64_t s = first; s < first + count; ++s) bad += run_case(s);
   if (bad) return 1;
   std::printf("rx_stage_gpu_fuzz: ok (%llu batches, %zu resolved on the device, %zu of them with a host tail, %zu "
-              "running out of RX descriptors, %zu with device descriptors, %zu with results left on the device)\n",
-              (unsigned long long) count, g_device, g_tail, g_short, g_devdesc, g_keep);
+              "running out of RX descriptors, %zu with device descriptors, %zu with results left on the device, "
+              "%zu interrupt callbacks equal)\n",
+              (unsigned long long) count, g_device, g_tail, g_short, g_devdesc, g_keep, g_irq);
   return 0;
 }

@@ -1,6 +1,6 @@
 // bench_rx_stage.cpp — nic::BatchedQueuePair throughput.
 //
-//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host] [pageable|pinned|device] [sync|pipelined] [host|device]
+//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host] [pageable|pinned|device] [sync|pipelined] [host|device] [irq]
 //   (device: BatchedQueuePair's device resolve, the default for disjoint
 //   buffers; host: the host resolve, BatchedQueuePairConfig::device_resolve off;
 //   pinned: the descriptor arrays in page-locked memory, as a descriptor ring
@@ -10,7 +10,9 @@
 //   submit()/collect() with three batches in flight, reported per batch over
 //   the whole run, against process_batch one batch at a time; the last
 //   argument: results copied to the host vectors, or left in device memory
-//   (BatchedQueuePairConfig::results_on_device))
+//   (BatchedQueuePairConfig::results_on_device)); irq: RX and TX interrupt
+//   callbacks on (a counting callback, as an InterruptDispatcher delivers
+//   them: queue_pair.cpp:371-383), replayed from the completions
 //
 // c3: IMIX 64/576/1518 (7:4:1) frames, each balanced so the whole-frame
 //     checksum verifies; RX descriptors with Layer4 checksum offload, 2 KiB
@@ -132,6 +134,15 @@ int main(int argc, char** argv) {
   if (argc > 4) cfg.host_threads = static_cast<unsigned>(std::atoi(argv[4]));
   if (argc > 5) cfg.device_resolve = std::string(argv[5]) != "host";
   cfg.results_on_device = argc > 8 && std::string(argv[8]) == "device";
+  const bool irq = argc > 9 && std::string(argv[9]) == "irq";
+  std::uint64_t irq_count = 0, irq_sum = 0;
+  if (irq) {
+    cfg.enable_tx_interrupts = true;
+    cfg.on_interrupt = [&irq_count, &irq_sum](std::uint16_t, const CompletionEntry& e) {
+      ++irq_count;
+      irq_sum += e.descriptor_index;
+    };
+  }
   const std::string desc_kind = argc > 6 ? argv[6] : "pageable";
   const bool pinned = desc_kind == "pinned", dev_desc = desc_kind == "device";
   BatchedQueuePair qp{cfg};
@@ -214,9 +225,10 @@ int main(int argc, char** argv) {
   const auto& T = tot[tot.size() / 2].second;  // the median batch's phases
   std::printf(
       "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"mode\": \"%s\", \"results\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
-      "\"rx_success\": %zu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
+      "\"rx_success\": %zu, \"interrupts\": %s, \"irq_callbacks\": %llu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
       "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f}}\n",
-      wl.c_str(), T.device ? "device" : "host", desc_kind.c_str(), pipelined ? "pipelined" : "sync", cfg.results_on_device ? "device" : "host", cfg.host_threads, n, last.rx_completions.size(), ok, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
+      wl.c_str(), T.device ? "device" : "host", desc_kind.c_str(), pipelined ? "pipelined" : "sync", cfg.results_on_device ? "device" : "host", cfg.host_threads, n, last.rx_completions.size(), ok,
+      irq ? "true" : "false", (unsigned long long) irq_count, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
       T.resolve_us, T.gather_us, T.rss_us, T.copy_us);
   nicgpu_free(mem);
   if (ptx) nicgpu_host_free(ptx);
