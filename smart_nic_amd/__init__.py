@@ -84,6 +84,7 @@ ABI_SYMBOLS = (
     "nicgpu_rx_offload_count",
     "nicgpu_qp_rss_scatter",
     "nicgpu_qp_group",
+    "nicgpu_qp_deliver",
     "nicgpu_icrc_batch",
     "nicgpu_tso_segment",
 )
@@ -132,6 +133,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_qp_rss_list": (i32, [vp, sz, vp]),
         "nicgpu_qp_rss_scatter": (i32, [vp, sz, vp]),
         "nicgpu_qp_group": (i32, [vp, sz, sz, vp]),
+        "nicgpu_qp_deliver": (i32, [vp, vp, ctypes.c_uint64, sz, vp, i32, u32, u32, vp, vp]),
         "nicgpu_icrc_batch": (i32, [vp, vp, sz, i32, vp, vp, vp]),
         "nicgpu_tso_segment": (i32, [vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint64, u32, vp, vp, vp]),
         "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),

@@ -49,7 +49,7 @@ constexpr uint32_t kRingTileBytes = kWave * 8;  // held results of one tile: has
 constexpr uint32_t kLdsPerCu = 160u * 1024u;  // gfx950
 constexpr int kLutPos = 2 * NICGPU_MAX_TUPLE;  // nibble positions
 constexpr int kLutWords = kLutPos * 16;
-constexpr int kHistLds = 1024;     // tables up to this size histogram in LDS
+constexpr int kHistLds = 1024;     // tables up to this size histogram in LDS (kHistLdsMax)
 constexpr int kTableLds = 2048;    // tables up to this size are read from LDS
 constexpr uint64_t kOffMask = (1ull << NICGPU_DESC_OFFSET_BITS) - 1;
 
@@ -83,6 +83,51 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// End-of-block flush of a block's LDS hit histogram (RssStats.queue_hits per
+// table index, rss.cpp:54-58) into `out`.  Every block adding its bins to the
+// same table_n addresses queued 1024-deep same-address atomic chains exactly
+// when the blocks finish together (4 M x 64 B: 7.7 of 88 us).  With replicas
+// (a context's kHistRep copies of the histogram, each on lines of its own)
+// block b adds into replica b % kHistRep; after every flushing wave's
+// vmcnt(0) and a barrier, one lane takes a ticket on a done counter (the
+// guide's atomic hand-off: no L2 write-back fence), and the block that takes
+// the last ticket moves the replicas into `out` with returning exchanges
+// (atomics are performed past the XCD L2s, so no stale copy is read) and
+// resets the ticket for the next launch.  hist[0] carries the verdict.
+// Replicas are built only with -DNICGPU_HIST_REP: the r03 A/B (3 rounds,
+// production vs replicas vs direct flush) measured them neutral on C2, C3 and
+// 4 M x 64 B, and one context's ticket is shared by every stream using it.
+constexpr uint32_t kHistRep = 16;
+constexpr int kHistLdsMax = 1024;  // = kHistLds (tables histogrammed in LDS)
+static_assert(kHistLdsMax == kHistLds, "replica stride");
+__device__ __forceinline__ void flush_hist(uint32_t* hist, uint32_t table_n, unsigned long long* out,
+                                           unsigned long long* rep, unsigned int* done, uint32_t nthreads) {
+  __syncthreads();
+  if (rep == nullptr) {
+    for (uint32_t i = threadIdx.x; i < table_n; i += nthreads) {
+      const uint32_t v = hist[i];
+      if (v) atomicAdd(&out[i], (unsigned long long) v);
+    }
+    return;
+  }
+  unsigned long long* mine = rep + (size_t) (blockIdx.x % kHistRep) * kHistLdsMax;
+  for (uint32_t i = threadIdx.x; i < table_n; i += nthreads) {
+    const uint32_t v = hist[i];
+    if (v) atomicAdd(&mine[i], (unsigned long long) v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's adds are performed
+  __syncthreads();
+  if (threadIdx.x == 0) hist[0] = atomicAdd(done, 1u) == gridDim.x - 1u ? 1u : 0u;
+  __syncthreads();
+  if (hist[0] == 0u) return;
+  for (uint32_t i = threadIdx.x; i < table_n; i += nthreads) {
+    unsigned long long sum = 0;
+    for (uint32_t r = 0; r < kHistRep; ++r) sum += atomicExch(rep + (size_t) r * kHistLdsMax + i, 0ull);
+    if (sum) atomicAdd(&out[i], sum);
+  }
+  if (threadIdx.x == 0) atomicExch(done, 0u);
+}
 
 // Keep bytes [lo, hi) of a 16-B chunk (lo in 0..15, hi in 1..16).
 __device__ __forceinline__ uint32_t dword_keep(int lo, int hi, int i) {
@@ -157,6 +202,8 @@ struct RxParams {
   uint32_t xpf_chunks;  // XPF kernels: prefetch the next tile's first batch when it has at most this many chunks
   unsigned long long* stamps;  // tuning builds only: per wave {start, end, XCC_ID, HW_ID} (s_memrealtime, 100 MHz)
   const unsigned long long* n_dev;  // batch size read on the device (min(n, *n_dev)); null: n
+  unsigned long long* hits_rep;  // per-context histogram replicas (flush_hist), or null
+  unsigned int* hits_done;       // their done ticket
 };
 
 // s_waitcnt immediate for vmcnt(0) alone (gfx9 encoding: expcnt 7, lgkmcnt 15).
@@ -1134,13 +1181,8 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
     for (int i = 0; i < HOLD; ++i)
       if (i < hold_n) store_out<SST>(P, held_out(held_b[i], held_v[i], held_c[i], held_h[i], lane), L.want_rss);
   }
-  if (L.hist_lds && !dbg_on(P, kDbgNoFlush)) {
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) {
-      uint32_t v = L.hist[i];
-      if (v) atomicAdd(&P.out_hits[i], (unsigned long long) v);
-    }
-  }
+  if (L.hist_lds && !dbg_on(P, kDbgNoFlush))
+    flush_hist(L.hist, P.table_n, P.out_hits, P.hits_rep, P.hits_done, kWave * WPB);
 #ifdef NICGPU_TUNING
   if (P.stamps != nullptr && lane == 0) {  // vector stores from lane 0
     const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
@@ -1231,13 +1273,7 @@ __global__ __launch_bounds__(kWave * WPB) void rss_only_kernel(RxParams P) {
       }
     }
   }
-  if (hist_lds) {
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < P.table_n; i += kThreads) {
-      const uint32_t v = hist[i];
-      if (v) atomicAdd(&P.out_hits[i], (unsigned long long) v);
-    }
-  }
+  if (hist_lds) flush_hist(hist, P.table_n, P.out_hits, P.hits_rep, P.hits_done, kThreads);
 }
 
 // ------------------------------------------------------------- TSO / GSO --
@@ -1514,14 +1550,17 @@ const RxVariant kRxVariants[] = {
     // C2 -1%) and sc1 stores (0) when the ring is flushed mid-stream (IMIX -3%).
     // Both prefetch the next tile's first batch (XPF: 64 B -1..4%, C2 / IMIX /
     // 9000 B within noise).
-    {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 16, 0, true, true, true>, 2, 4, "u2_w4_c_sc1_ring_xpf", false, true, true},
-    {rx_offload_kernel<2, true, 4, true, false, 1, false, -1, 0, 0, true, true, true>, 2, 4, "u2_w4_c_ring_xpf", false, true, true},
+    // OCC 4: at most 128 VGPRs, the 4 waves per SIMD the LDS allows anyway
+    // (left free, hipcc took variant 1 to 129 VGPRs with the histogram
+    // replicas' flush: 3 waves per SIMD)
+    {rx_offload_kernel<2, true, 4, true, false, 4, false, -1, 16, 0, true, true, true>, 2, 4, "u2_w4_c_sc1_ring_xpf", false, true, true},
+    {rx_offload_kernel<2, true, 4, true, false, 4, false, -1, 0, 0, true, true, true>, 2, 4, "u2_w4_c_ring_xpf", false, true, true},
     // 2: production for batches of at least kRxW8Tiles tiles.  8-wave blocks:
     // half the blocks add their histogram bins into the same counters at the
     // end (1024 -> 512 same-address atomics per bin).  IMIX (4 M packets) -2%,
     // 4 M x 64 B -3%; C2 +0.6% and 9000 B +15% (2500 tiles underfill 512
     // slots of 8 waves) keep 4-wave blocks (profiles/r02y_tune_variants.json).
-    {rx_offload_kernel<2, true, 8, true, false, 1, false, -1, 16, 0, true, true, true>, 2, 8, "u2_w8_c_sc1_ring_xpf", false, true, true},
+    {rx_offload_kernel<2, true, 8, true, false, 4, false, -1, 16, 0, true, true, true>, 2, 8, "u2_w8_c_sc1_ring_xpf", false, true, true},
 #ifdef NICGPU_TUNING
     // candidates and earlier production kernels, timed by tools/tune_rx.py.
     // 8-wave blocks measure the same on C2/IMIX/64 B and 12% slower on 9000 B,
@@ -1980,11 +2019,7 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
     if (lane == 0 && c) atomicAdd(cnt_s, c);
     __syncthreads();
     if (threadIdx.x == 0 && *cnt_s) atomicAdd(P.count, (unsigned long long) *cnt_s);
-    if (hist_lds)
-      for (uint32_t i = threadIdx.x; i < R.table_n; i += kThreads) {
-        const uint32_t v = hist[i];
-        if (v) atomicAdd(&P.hits[i], (unsigned long long) v);
-      }
+    if (hist_lds) flush_hist(hist, R.table_n, P.hits, R.hits_rep, R.hits_done, kThreads);
   }
 }
 
@@ -2581,6 +2616,8 @@ int current_device_info(const DeviceInfo** out) {
 
 struct nicgpu_rss_ctx {
   int device = 0;
+  unsigned long long* d_rep = nullptr;  // kHistRep x kHistLds hit-histogram replicas (flush_hist), zeroed
+  unsigned int* d_done = nullptr;       // their done ticket
   uint8_t* d_key = nullptr;      // NICGPU_MAX_KEY bytes
   uint32_t* d_lut = nullptr;     // kLutWords
   uint16_t* d_table = nullptr;   // capacity table_cap
@@ -2860,9 +2897,16 @@ int nicgpu_rss_create(nicgpu_rss_ctx** out, int device) {
   if (di.status != NICGPU_OK) return di.status;
   auto* ctx = new nicgpu_rss_ctx();
   ctx->device = device;
-  if (hipMalloc(&ctx->d_key, NICGPU_MAX_KEY) != hipSuccess || hipMalloc(&ctx->d_lut, kLutWords * sizeof(uint32_t)) != hipSuccess) {
+  const size_t rep_bytes = (size_t) kHistRep * kHistLdsMax * sizeof(unsigned long long);
+  if (hipMalloc(&ctx->d_key, NICGPU_MAX_KEY) != hipSuccess || hipMalloc(&ctx->d_lut, kLutWords * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&ctx->d_rep, rep_bytes + 256) != hipSuccess) {
     nicgpu_rss_destroy(ctx);
     return NICGPU_ERR_NOMEM;
+  }
+  ctx->d_done = reinterpret_cast<unsigned int*>(reinterpret_cast<uint8_t*>(ctx->d_rep) + rep_bytes);
+  if (hipMemset(ctx->d_rep, 0, rep_bytes + 256) != hipSuccess) {
+    nicgpu_rss_destroy(ctx);
+    return NICGPU_ERR_HIP;
   }
   // reference defaults (src/rss.cpp:96-108): 20-B key, 128 zeros
   int st = nicgpu_rss_set_key(ctx, nullptr, 0, nullptr);
@@ -2882,6 +2926,7 @@ int nicgpu_rss_destroy(nicgpu_rss_ctx* ctx) {
   if (ctx->d_key) (void) hipFree(ctx->d_key);
   if (ctx->d_lut) (void) hipFree(ctx->d_lut);
   if (ctx->d_table) (void) hipFree(ctx->d_table);
+  if (ctx->d_rep) (void) hipFree(ctx->d_rep);
   delete ctx;
   return NICGPU_OK;
 }
@@ -2998,6 +3043,12 @@ int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frame
     P.lut = ctx->d_lut;
     P.table = ctx->d_table;
     P.table_n = (uint32_t) ctx->table_n;
+#ifdef NICGPU_HIST_REP  // off: measured neutral (r03 A/B), and a ctx shared by two streams would race on d_done
+    if (out_hits && P.table_n <= (uint32_t) kHistLds) {
+      P.hits_rep = ctx->d_rep;
+      P.hits_done = ctx->d_done;
+    }
+#endif
     uint32_t max_tuple = tuple_mode == NICGPU_TUPLE_RAW ? raw_len : 36u;
     P.lut_words = 2u * max_tuple * 16u;
   }
@@ -3854,6 +3905,12 @@ int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx,
     P.rx_queue = q->rx_queue;
     P.hits = reinterpret_cast<unsigned long long*>(hits_dev);
     P.count = reinterpret_cast<unsigned long long*>(q->scal + 3);
+#ifdef NICGPU_HIST_REP
+    if (P.rss.table_n <= (uint32_t) kHistLds) {
+      P.rss.hits_rep = ctx->d_rep;
+      P.rss.hits_done = ctx->d_done;
+    }
+#endif
   }
   const uint32_t hist_n = (rss && P.rss.table_n <= (uint32_t) kHistLds) ? P.rss.table_n : 0u;
   const uint32_t table_words = (rss && P.rss.table_n <= (uint32_t) kTableLds) ? (P.rss.table_n + 1u) / 2u : 0u;
@@ -4027,6 +4084,61 @@ int nicgpu_tune_stream_read(const uint8_t* buf, size_t bytes, int blocks_per_cu,
   else if (unroll == 8) hipLaunchKernelGGL(stream_read_kernel<8>, dim3(grid), dim3(256), 0, s, p, n16, out, g_tune_stamps);
   else if (unroll == 4) hipLaunchKernelGGL(stream_read_kernel<4>, dim3(grid), dim3(256), 0, s, p, n16, out, g_tune_stamps);
   else hipLaunchKernelGGL(stream_read_kernel<1>, dim3(grid), dim3(256), 0, s, p, n16, out, g_tune_stamps);
+  return hip_status(hipGetLastError());
+}
+// FETCH_SIZE calibration (MI355X_MICROARCH.md: the x2 correction holds for
+// 16-B/lane coalesced streaming reads only; "calibrate on a known byte count
+// in your own access pattern").  Each kernel reads a known set of whole
+// 128-B lines or line prefixes of `buf` in one access shape of this build:
+//   shape 0  coalesced 16 B per lane over the whole buffer (the RX stream)
+//   shape 1  lane-owned line walk: lane l reads its own 128-B lines, 16 B per
+//            load (ICRC: 64 different lines per wave instruction)
+//   shape 2  per-packet header gather: 48 B (3 x 16 B) at the start of every
+//            1536-B slot (rss_only_kernel's shape on C2 frames)
+//   shape 3  the same with 64 B (4 x 16 B) per slot
+//   shape 4  the same with 128 B (8 x 16 B, one whole line) per slot
+// tools/calib_fetch.py runs them under rocprofv3 --pmc FETCH_SIZE and divides
+// the bytes each shape must bring from HBM by what FETCH_SIZE reports.
+__global__ __launch_bounds__(256) void calib_kernel(int shape, const u32x4* __restrict__ p, uint64_t n16,
+                                                   uint32_t* __restrict__ out) {
+  const uint64_t tid = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  const uint64_t nthr = (uint64_t) gridDim.x * 256;
+  uint32_t acc = 0;
+  if (shape == 0) {
+    for (uint64_t i = tid; i < n16; i += nthr) {
+      const u32x4 v = __builtin_nontemporal_load(p + i);
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  } else if (shape == 1) {
+    const uint64_t nlines = n16 / 8;
+    for (uint64_t l = tid; l < nlines; l += nthr) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const u32x4 v = p[l * 8 + k];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+      }
+    }
+  } else {
+    const int nk = shape == 2 ? 3 : (shape == 3 ? 4 : 8);
+    const uint64_t nslot = n16 / 96;  // 1536-B slots
+    for (uint64_t q = tid; q < nslot; q += nthr) {
+      for (int k = 0; k < nk; ++k) {
+        const u32x4 v = p[q * 96 + k];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+      }
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;  // keeps the loads
+}
+
+int nicgpu_tune_calib(int shape, const uint8_t* buf, size_t bytes, uint32_t* out, void* stream) {
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  if (shape < 0 || shape > 4) return NICGPU_ERR_INVALID;
+  const unsigned grid = (unsigned) (di->cus * 8);
+  hipLaunchKernelGGL(calib_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), shape,
+                     reinterpret_cast<const u32x4*>(buf), (uint64_t) (bytes / 16), out);
   return hip_status(hipGetLastError());
 }
 }  // extern "C"
