@@ -1,0 +1,140 @@
+// rx_queue_manager.h — nic::BatchedQueueManager: the reference's QueueManager
+// (include/nic/queue_manager.h, src/queue_manager.cpp) over batches of the
+// batched QueuePair stage (rx_stage.h).
+//
+// QueueManager::process_once (queue_manager.cpp:54-78) serves one TX
+// descriptor of the queue pair at the scheduler's index — weighted round robin
+// with credits: a queue keeps the turn for `weight` descriptors (0 counts as 1,
+// :14-16) — and skips a queue whose process_once returns false (its TX ring is
+// empty), counting scheduler_advances / scheduler_skips.  Draining it until it
+// returns false over one batch per queue pair is what process_batch does:
+//
+//   * the schedule (which queue serves each descriptor, the advances, the
+//     skips — including the final call that finds every ring empty, and the
+//     index/credit carried to the next batch) is computed on the host from
+//     the batch sizes alone: process_once returns true for every descriptor of
+//     a batch (the stage's rings are not host-backed, so no pop or decode
+//     fails);
+//   * when no queue's RX buffer overlaps a byte another queue reads or writes,
+//     each queue pair's results are independent of the order the scheduler
+//     interleaves them in, so every queue's batch goes to its own
+//     BatchedQueuePair on the device, all in flight at once (submit/collect);
+//   * otherwise the interleaving decides the bytes (a queue writes into
+//     another's TX buffer before or after it is read): the schedule is replayed
+//     run by run, each run of one queue's consecutive descriptors a host-path
+//     batch of that queue, in the reference's order;
+//   * interrupt callbacks fire in the order the reference's single
+//     InterruptDispatcher would see them: run by run, each run's descriptors
+//     replayed from its queue's completions (rx_stage_detail::replay_interrupts).
+//
+// Statistics: queue_stats(i) is queue pair i's QueuePairStats, stats() their
+// aggregate plus the scheduler counters exactly as aggregate_stats
+// (:119-139), stats_summary() the same text as :102-117.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <optional>
+#include <span>
+#include <string>
+#include <vector>
+
+#include "nic/rx_stage.h"
+
+#if __has_include("nic/queue_manager.h")
+#include "nic/queue_manager.h"  // reference build: its QueueManagerStats
+#else
+namespace nic {
+// Same members and order as include/nic/queue_manager.h:18-34.
+struct QueueManagerStats {
+  std::uint64_t total_tx_packets{0};
+  std::uint64_t total_rx_packets{0};
+  std::uint64_t total_tx_bytes{0};
+  std::uint64_t total_rx_bytes{0};
+  std::uint64_t total_drops_checksum{0};
+  std::uint64_t total_drops_no_rx_desc{0};
+  std::uint64_t total_drops_buffer_small{0};
+  std::uint64_t total_tx_tso_segments{0};
+  std::uint64_t total_tx_gso_segments{0};
+  std::uint64_t total_tx_vlan_insertions{0};
+  std::uint64_t total_rx_vlan_strips{0};
+  std::uint64_t total_rx_checksum_verified{0};
+  std::uint64_t total_rx_gro_aggregated{0};
+  std::uint64_t scheduler_advances{0};
+  std::uint64_t scheduler_skips{0};
+};
+}  // namespace nic
+#endif
+
+namespace nic {
+
+/// QueueManagerConfig (queue_manager.h:14-16) for batched queue pairs.
+struct BatchedQueueManagerConfig {
+  std::vector<BatchedQueuePairConfig> queue_configs;
+};
+
+/// One queue pair's share of a batch: the TX descriptors to send and the
+/// contents of its RX ring (rx[0] first; what a batch leaves unconsumed is the
+/// caller's to pass again, first, with the next one).
+struct QueueBatch {
+  std::span<const TxDescriptor> tx;
+  std::span<const RxDescriptor> rx;
+};
+
+/// How one drain served the queues: runs of consecutive descriptors of one
+/// queue, in order, and the scheduler counters it added.
+struct QueueSchedule {
+  struct Run {
+    std::uint32_t queue;
+    std::uint32_t count;
+  };
+  std::vector<Run> runs;
+  std::uint64_t advances{0}, skips{0};
+};
+
+namespace qm_detail {
+/// The scheduler of queue_manager.cpp:54-78 drained over `pending[q]`
+/// descriptors per queue from (index, credit); both are advanced to where the
+/// reference leaves them.  weights: already 0 -> 1.
+QueueSchedule schedule(std::span<const std::uint8_t> weights, std::span<const std::size_t> pending, std::size_t& index,
+                       std::size_t& credit);
+/// No queue's RX buffer overlaps a byte another queue's TX or RX buffer
+/// covers (clipped to the image, as the stage's own check).
+bool queues_disjoint(std::size_t mem_size, std::span<const QueueBatch> batches);
+}  // namespace qm_detail
+
+class BatchedQueueManager {
+public:
+  explicit BatchedQueueManager(BatchedQueueManagerConfig config);
+  ~BatchedQueueManager();
+  BatchedQueueManager(const BatchedQueueManager&) = delete;
+  BatchedQueueManager& operator=(const BatchedQueueManager&) = delete;
+
+  [[nodiscard]] std::size_t queue_count() const noexcept { return qps_.size(); }
+  /// The queue pair's stage (its config has no interrupt callback: the
+  /// manager fires them, in the scheduler's order); nullptr past the end.
+  [[nodiscard]] BatchedQueuePair* queue(std::size_t index) noexcept;
+  [[nodiscard]] std::optional<QueuePairStats> queue_stats(std::size_t index) const noexcept;
+
+  /// QueueManager::process_once until it returns false, over batches[q] for
+  /// queue pair q (batches.size() == queue_count()); results into out[q]
+  /// (resized).  Synchronises `stream`.  Returns the schedule it served.
+  QueueSchedule process_batch(const DeviceHostMemory& mem, std::span<const QueueBatch> batches,
+                              std::vector<RxBatchResult>& out, void* stream = nullptr);
+
+  /// Scheduler index/credit/counters and every queue pair's statistics
+  /// (QueueManager::reset, :80-93; the rings are the caller's).
+  void reset();
+  [[nodiscard]] QueueManagerStats stats() const;
+  [[nodiscard]] std::string stats_summary() const;
+
+private:
+  struct Queue;
+  std::vector<std::unique_ptr<Queue>> qps_;
+  std::vector<std::uint8_t> weights_;
+  std::size_t index_{0}, credit_{0};
+  std::uint64_t advances_{0}, skips_{0};
+};
+
+}  // namespace nic

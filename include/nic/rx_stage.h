@@ -143,6 +143,7 @@ struct DeviceDescriptors {
 
 struct BatchedQueuePairConfig {
   std::uint16_t queue_id{0};
+  std::uint8_t weight{1};           // QueuePairConfig::weight (queue_pair.h:31): BatchedQueueManager's share (0 -> 1)
   std::size_t max_mtu{kJumboMtu};   // QueuePairConfig::max_mtu (queue_pair.h:32)
   bool enable_tx_interrupts{false};  // QueuePairConfig defaults (queue_pair.h:33-34)
   bool enable_rx_interrupts{true};
@@ -267,14 +268,17 @@ public:
 
 private:
   // Device resolve of one batch in four steps: upload() sends the descriptors
-  // up, front() plans, checks and resolves (false, nothing written, when the
-  // buffers overlap); back()
-  // enqueues the DMA writes and RSS and starts the downloads into `out`;
+  // up; front() plans and checks (false, nothing written, when the buffers
+  // overlap), starts the resolve, enqueues the DMA writes and RSS of the
+  // completions it settles and then waits for it; back() enqueues the rest of
+  // the writes and starts the downloads (dispatch lists included) into `out`;
   // finish() waits for them and completes `out`.
   void upload(Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx, bool rx_beside);
   bool front(Slot& sl, const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
              QueuePairStats& stats, RxBatchResult& out, void* stream, int& disjoint, double& check_us);
   void back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult& out, void* stream);
+  void deliver(Slot& sl, const DeviceHostMemory& mem, std::size_t a, std::size_t b, unsigned flags,
+               const nicgpu_rss_ctx* rctx, std::uint64_t* hits, void* stream);
   void finish(Slot& sl, RxBatchResult& out);
   void enqueue(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                const DeviceDescriptors* d, void* stream);
@@ -405,6 +409,14 @@ std::size_t resolve_relaxed(const BatchedQueuePairConfig& config, std::size_t me
 /// not, at most segments_produced of them.
 void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> tx_completions,
                        std::span<const CompletionEntry> rx_completions);
+/// The same over TX completions [at.tx, at.tx + n) only, from RX completion
+/// at.rx; `at` is advanced past them (a caller interleaving several queue
+/// pairs' completions in the order a scheduler served them).
+struct InterruptCursor {
+  std::size_t tx{0}, rx{0};
+};
+void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> tx_completions,
+                       std::span<const CompletionEntry> rx_completions, InterruptCursor& at, std::size_t n);
 
 /// Order of the DMA writes of one resolved sub-batch for parallel gathers.
 /// Writes (RX completions j with write_of_rx[j] >= 0 and at least one byte) are

@@ -345,6 +345,14 @@ int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view
  * ascending and apart (the caller then sorts on the host).  Synchronises
  * `stream`. */
 int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int* verdict, void* stream);
+/* The kernels of the next plan/check/resolve read the caller's device arrays
+ * tx[0, ntx) and rx[0, nrx) in place of view.tx / view.rx (no copy; view is
+ * refreshed to point at them).  They must stay valid and unchanged until the
+ * batch is resolved, and lie outside the memory image the batch writes (a
+ * write there would change a descriptor the reference pops later).  A later
+ * nicgpu_qp_reserve returns the context to its own arrays. */
+int nicgpu_qp_bind(nicgpu_qp* q, const nicgpu_tx_descriptor* tx, size_t ntx, const nicgpu_rx_descriptor* rx,
+                   size_t nrx, nicgpu_qp_view* view);
 /* The plan (qp_logic.h plan_packet) of view.tx[0, ntx) and the checksum of
  * every piece over the image mem[0, mem_size): *npieces on return
  * (NICGPU_ERR_RANGE, nothing enqueued after the count, when a descriptor plans
@@ -374,6 +382,20 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
  * (piece checksums from view.piece_base[*done]).  Synchronises `stream`. */
 int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu, uint16_t queue_id,
                       uint64_t* done, uint64_t* rx_used, nicgpu_qp_stats* stats, void* stream);
+/* nicgpu_qp_resolve in two halves.  _start enqueues the speculative pass
+ * (every packet at the scan of what it needs) on `stream` and returns without
+ * waiting; its settled prefix — the RX completions of the packets before the
+ * first one that popped otherwise, all of them when none did — is a device
+ * scalar that nicgpu_qp_deliver_range(NICGPU_DELIVER_SETTLED) reads, so the DMA
+ * writes can be enqueued before the host has seen the resolve.  _finish waits
+ * for the pass only (not for work enqueued after it), relaxes on `stream` when
+ * the guess was wrong (those steps then wait behind that work), and returns
+ * what nicgpu_qp_resolve does plus *rx_settled (<= *rx_used; may be null).
+ * One resolve may be pending per nicgpu_qp. */
+int nicgpu_qp_resolve_start(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu,
+                            uint16_t queue_id, void* stream);
+int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, uint64_t* rx_settled,
+                             nicgpu_qp_stats* stats);
 /* The frames of view.rxc[0, nrx) delivered with Success, as RSS descriptors
  * (view.rss_desc[0, m), lengths clipped to NICGPU_MAX_PACKET), m written to
  * the device scalar view.rss_count; view.rx_hash / rx_queue reset to 0 /
@@ -402,6 +424,16 @@ int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream);
  * nicgpu_segment_gather + nicgpu_qp_rss_list + an RSS launch + nicgpu_qp_rss_scatter. */
 int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx, const nicgpu_rss_ctx* ctx,
                       int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint64_t* hits_dev, void* stream);
+#define NICGPU_DELIVER_SETTLED 1u /* end at the settled prefix of the pending nicgpu_qp_resolve_start */
+#define NICGPU_DELIVER_APPEND 2u  /* add to *view.rss_count instead of resetting it (a later range) */
+/* nicgpu_qp_deliver over completions [rx_begin, rx_end) (bounded on the device
+ * with NICGPU_DELIVER_SETTLED).  Ranges of one batch may be delivered in any
+ * order when the batch's buffers are disjoint (nicgpu_qp_check verdict 1): the
+ * settled prefix first, the rest after nicgpu_qp_resolve_finish with APPEND;
+ * hits_dev accumulates over the ranges, nicgpu_qp_group runs after the last. */
+int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t rx_begin, size_t rx_end,
+                            unsigned flags, const nicgpu_rss_ctx* ctx, int tuple_mode, uint32_t raw_off,
+                            uint32_t raw_len, uint64_t* hits_dev, void* stream);
 
 #ifdef __cplusplus
 }

@@ -25,6 +25,9 @@
 
 #include "nic/checksum.h"
 #include "nic/dma_engine.h"
+#include "nic/interrupt_dispatcher.h"
+#include "nic/msix.h"
+#include "nic/queue_manager.h"
 #include "nic/queue_pair.h"
 #include "nic/rss.h"
 #include "nic/simple_host_memory.h"
@@ -914,6 +917,220 @@ void gen_qp_batch() {
   gen_qp_batch_case("qp_alias", 404, 300, 400, 2);    // overlapping RX/RX and RX/TX buffers
 }
 
+// ------------------------------------------------------------ QueueManager --
+// SURVEY §8 f1, the caller of the batched QueuePair: QueueManager::process_once
+// (src/queue_manager.cpp:54-78) drained — weighted round robin with credits,
+// skips of queues whose TX ring is empty — over several queue pairs sharing
+// one host memory and one InterruptDispatcher, in two rounds (the scheduler's
+// index/credit and the RX descriptors a round left carry into the next).
+// Recorded per round and queue: the TX/RX completions in posting order and the
+// RX descriptors consumed; per round: the MSI-X vectors fired in order (queue
+// q -> vector q, packet threshold 1, so one per InterruptDispatcher::
+// on_completion) and the scheduler's advances/skips; at the end: every
+// QueuePairStats, QueueManagerStats (aggregate_stats, :119-139) and an FNV of
+// the memory.  flavour 1: some RX buffers of queue q lie in queue q+1's TX
+// buffers, so the order the scheduler serves the queues decides the bytes.
+struct QmRound {
+  std::vector<std::vector<TxDescriptor>> tx;  // [queue]
+  std::vector<std::vector<RxDescriptor>> rx;
+};
+
+void gen_qm_case(const std::string& name, std::uint64_t seed, const std::vector<std::uint8_t>& weights,
+                 const std::vector<std::vector<std::size_t>>& ntx, const std::vector<std::vector<std::size_t>>& nrx,
+                 int flavour) {
+  Rng r{seed};
+  const std::size_t Q = weights.size(), R = ntx.size();
+  std::vector<QmRound> rounds(R);
+  std::vector<std::uint8_t> image;
+  std::vector<std::vector<std::uint64_t>> tx_addr(Q);  // every TX buffer of a queue (for flavour 1)
+  // per round and queue: a TX region then an RX region, appended to the image
+  for (std::size_t k = 0; k < R; ++k) {
+    rounds[k].tx.resize(Q);
+    rounds[k].rx.resize(Q);
+    for (std::size_t q = 0; q < Q; ++q) {
+      for (std::size_t i = 0; i < ntx[k][q]; ++i) {
+        const std::uint32_t pick = r.below(16);
+        std::size_t L = pick < 5 ? 64 : pick < 8 ? 576 : pick < 11 ? 1518 : pick < 12 ? r.below(60)
+                        : pick < 13 ? 9000 : pick < 14 ? 9001 + r.below(100) : 64 + r.below(3000);
+        FrameSpec fs;
+        fs.total = L;
+        fs.proto = r.below(2) ? 6 : 17;
+        fs.balance = r.below(4) != 0;
+        std::vector<std::uint8_t> f = L >= 14 ? build_frame(r, fs) : std::vector<std::uint8_t>(L);
+        if (L < 14) for (auto& b : f) b = r.byte();
+        image.resize(image.size() + r.below(8));
+        TxDescriptor t{};
+        t.buffer_address = image.size();
+        t.length = static_cast<std::uint32_t>(L);
+        t.descriptor_index = static_cast<std::uint16_t>(100 * q + i);
+        const std::uint32_t cm = r.below(5);
+        t.checksum = cm < 2 ? ChecksumMode::None : (cm < 4 ? ChecksumMode::Layer4 : ChecksumMode::Layer3);
+        t.checksum_offload = r.below(3) != 0;
+        const std::uint16_t good = ref_csum(f.data(), L);
+        t.checksum_value = r.below(6) == 0 ? static_cast<std::uint16_t>(good ^ (1u + r.below(0xFFFE))) : good;
+        if (L > 1518 && r.below(2) == 0) {
+          (r.below(2) ? t.tso_enabled : t.gso_enabled) = true;
+          t.mss = r.below(8) == 0 ? static_cast<std::uint16_t>(1 + r.below(30)) : static_cast<std::uint16_t>(1448);
+          t.header_length = 54;
+        }
+        if (r.below(6) == 0) { t.vlan_insert = true; t.vlan_tag = static_cast<std::uint16_t>(r.u32()); }
+        image.insert(image.end(), f.begin(), f.end());
+        tx_addr[q].push_back(t.buffer_address);
+        rounds[k].tx[q].push_back(t);
+      }
+      image.resize((image.size() + 63) & ~std::size_t{63});
+      for (std::size_t j = 0; j < nrx[k][q]; ++j) {
+        RxDescriptor x{};
+        const std::uint32_t bp = r.below(10);
+        const std::uint32_t blen = bp == 0 ? r.below(1600) : (bp == 1 ? 64 : (bp < 7 ? 1600 : 9216 + 8));
+        image.resize(image.size() + r.below(4));
+        x.buffer_address = image.size();
+        x.buffer_length = blen;
+        image.resize(image.size() + blen);
+        x.descriptor_index = static_cast<std::uint16_t>(1000 + 100 * q + j);
+        x.checksum_offload = r.below(4) != 0;
+        const std::uint32_t cm = r.below(5);
+        x.checksum = cm == 0 ? ChecksumMode::None : (cm < 3 ? ChecksumMode::Layer4 : ChecksumMode::Layer3);
+        x.vlan_strip = r.below(3) == 0;
+        x.vlan_present = r.below(4) == 0;
+        x.vlan_tag = static_cast<std::uint16_t>(r.u32());
+        x.gro_enabled = r.below(5) == 0;
+        rounds[k].rx[q].push_back(x);
+      }
+    }
+  }
+  if (flavour == 1)  // RX buffers of queue q inside queue q+1's TX buffers (any round)
+    for (std::size_t k = 0; k < R; ++k)
+      for (std::size_t q = 0; q < Q; ++q)
+        for (RxDescriptor& x : rounds[k].rx[q]) {
+          const auto& ta = tx_addr[(q + 1) % Q];
+          if (!ta.empty() && r.below(3) == 0) x.buffer_address = ta[r.below(static_cast<std::uint32_t>(ta.size()))] + r.below(8);
+        }
+  image.resize(image.size() + 64);
+  const std::size_t mem_size = image.size();
+  HostMemoryConfig mc{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false};
+  SimpleHostMemory mem{mc};
+  assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(image))).ok());
+  DMAEngine dma{mem};
+  std::vector<std::uint16_t> fired;
+  MsixMapping mapping{Q, 0};
+  for (std::size_t q = 0; q < Q; ++q) mapping.set_queue_vector(q, static_cast<std::uint16_t>(q));
+  InterruptDispatcher irq{MsixTable{Q}, mapping, CoalesceConfig{1, 0},
+                          [&](std::uint16_t v, std::uint32_t) { fired.push_back(v); }};
+  std::size_t tot_tx = 0, tot_rx = 0;
+  for (std::size_t k = 0; k < R; ++k)
+    for (std::size_t q = 0; q < Q; ++q) { tot_tx += ntx[k][q]; tot_rx += nrx[k][q]; }
+  QueueManagerConfig qmc;
+  for (std::size_t q = 0; q < Q; ++q) {
+    const auto id = static_cast<std::uint16_t>(q);
+    QueuePairConfig c{
+        .queue_id = id,
+        .tx_ring = {.descriptor_size = sizeof(TxDescriptor), .ring_size = tot_tx + 1, .base_address = 0, .queue_id = id, .host_backed = false},
+        .rx_ring = {.descriptor_size = sizeof(RxDescriptor), .ring_size = tot_rx + 1, .base_address = 0, .queue_id = id, .host_backed = false},
+        .tx_completion = {.ring_size = tot_tx + 1, .queue_id = id},
+        .rx_completion = {.ring_size = 70 * tot_tx + 1, .queue_id = id},
+    };
+    c.interrupt_dispatcher = &irq;
+    c.weight = weights[q];
+    c.max_mtu = 9000;
+    c.enable_tx_interrupts = q % 2 == 0;
+    c.enable_rx_interrupts = q % 3 != 2;
+    qmc.queue_configs.push_back(c);
+  }
+  QueueManager qm{qmc, dma};
+  std::ostringstream js;
+  js << "{\n \"source\": \"QueueManager::process_once drained per round (src/queue_manager.cpp:54-78), stats :119-139\",\n"
+     << " \"queues\": " << Q << ", \"weights\": " << json_arr(weights) << ", \"max_mtu\": 9000, \"mem_size\": " << mem_size
+     << ",\n \"enable_tx_interrupts\": [";
+  for (std::size_t q = 0; q < Q; ++q) js << (q ? "," : "") << int(q % 2 == 0);
+  js << "], \"enable_rx_interrupts\": [";
+  for (std::size_t q = 0; q < Q; ++q) js << (q ? "," : "") << int(q % 3 != 2);
+  js << "],\n \"rounds\": [";
+  std::vector<TxDescriptor> all_tx;
+  std::vector<RxDescriptor> all_rx;
+  std::uint64_t adv0 = 0, skip0 = 0;
+  for (std::size_t k = 0; k < R; ++k) {
+    for (std::size_t q = 0; q < Q; ++q) {
+      QueuePair& qp = *qm.queue(q);
+      for (const TxDescriptor& t : rounds[k].tx[q]) {
+        std::vector<std::byte> b(sizeof(TxDescriptor));
+        std::memcpy(b.data(), &t, sizeof(t));
+        assert(qp.tx_ring().push_descriptor(b).ok());
+        all_tx.push_back(t);
+      }
+      for (const RxDescriptor& x : rounds[k].rx[q]) {
+        std::vector<std::byte> b(sizeof(RxDescriptor));
+        std::memcpy(b.data(), &x, sizeof(x));
+        assert(qp.rx_ring().push_descriptor(b).ok());
+        all_rx.push_back(x);
+      }
+    }
+    std::vector<std::size_t> avail0(Q);
+    for (std::size_t q = 0; q < Q; ++q) avail0[q] = qm.queue(q)->rx_ring().available();
+    fired.clear();
+    while (qm.process_once()) {
+    }
+    const QueueManagerStats ms = qm.stats();
+    js << (k ? "," : "") << "\n  {\"ntx\": " << json_arr(ntx[k]) << ", \"nrx\": " << json_arr(nrx[k])
+       << ", \"advances\": " << ms.scheduler_advances - adv0 << ", \"skips\": " << ms.scheduler_skips - skip0
+       << ", \"rx_consumed\": [";
+    adv0 = ms.scheduler_advances;
+    skip0 = ms.scheduler_skips;
+    for (std::size_t q = 0; q < Q; ++q) js << (q ? "," : "") << avail0[q] - qm.queue(q)->rx_ring().available();
+    js << "],\n   \"irq_vectors\": " << json_arr(fired) << ",\n   \"tx_completions\": [";
+    for (std::size_t q = 0; q < Q; ++q) {
+      js << (q ? "," : "") << "[";
+      bool first = true;
+      while (auto c = qm.queue(q)->tx_completion().poll_completion()) { js << (first ? "" : ",") << completion_json(*c); first = false; }
+      js << "]";
+    }
+    js << "],\n   \"rx_completions\": [";
+    for (std::size_t q = 0; q < Q; ++q) {
+      js << (q ? "," : "") << "[";
+      bool first = true;
+      while (auto c = qm.queue(q)->rx_completion().poll_completion()) { js << (first ? "" : ",") << completion_json(*c); first = false; }
+      js << "]";
+    }
+    js << "]}";
+  }
+  js << "],\n \"stats\": [";
+  for (std::size_t q = 0; q < Q; ++q) {
+    const QueuePairStats st = *qm.queue_stats(q);
+    js << (q ? "," : "") << "\n  [" << st.tx_packets << "," << st.rx_packets << "," << st.tx_bytes << "," << st.rx_bytes
+       << "," << st.drops_checksum << "," << st.drops_no_rx_desc << "," << st.drops_buffer_small << ","
+       << st.drops_mtu_exceeded << "," << st.drops_invalid_mss << "," << st.drops_too_many_segments << ","
+       << st.tx_tso_segments << "," << st.tx_gso_segments << "," << st.tx_vlan_insertions << "," << st.rx_vlan_strips
+       << "," << st.rx_checksum_verified << "," << st.rx_gro_aggregated << "]";
+  }
+  const QueueManagerStats ms = qm.stats();
+  js << "],\n \"qm_stats\": [" << ms.total_tx_packets << "," << ms.total_rx_packets << "," << ms.total_tx_bytes << ","
+     << ms.total_rx_bytes << "," << ms.total_drops_checksum << "," << ms.total_drops_no_rx_desc << ","
+     << ms.total_drops_buffer_small << "," << ms.total_tx_tso_segments << "," << ms.total_tx_gso_segments << ","
+     << ms.total_tx_vlan_insertions << "," << ms.total_rx_vlan_strips << "," << ms.total_rx_checksum_verified << ","
+     << ms.total_rx_gro_aggregated << "," << ms.scheduler_advances << "," << ms.scheduler_skips << "],\n"
+     << " \"stats_summary\": \"" << qm.stats_summary() << "\",\n";
+  std::vector<std::byte> after(mem_size);
+  assert(mem.read(0, after).ok());
+  js << " \"mem_fnv\": \"" << std::hex << fnv1a(after.data(), mem_size) << std::dec << "\"\n}\n";
+  std::ofstream(g_out + "/" + name + ".json") << js.str();
+  write_bin(name + ".mem.bin", image);
+  std::vector<std::uint8_t> tb(all_tx.size() * sizeof(TxDescriptor)), rb(all_rx.size() * sizeof(RxDescriptor));
+  std::memcpy(tb.data(), all_tx.data(), tb.size());
+  std::memcpy(rb.data(), all_rx.data(), rb.size());
+  write_bin(name + ".tx.bin", tb);
+  write_bin(name + ".rx.bin", rb);
+}
+
+void gen_qm() {
+  // 4 queues, weights 1/3/2/1: queue 3 has nothing to send in round 0, queue 1
+  // runs its RX ring dry; round 1 carries the leftovers and the scheduler state
+  gen_qm_case("qm_mix", 505, {1, 3, 2, 1}, {{40, 90, 25, 0}, {10, 0, 30, 20}}, {{60, 50, 80, 10}, {30, 20, 10, 40}}, 0);
+  // weight 0 (served as 1, queue_manager.cpp:14-16), single-descriptor queues
+  gen_qm_case("qm_weights", 606, {0, 5, 1}, {{1, 33, 7}, {12, 1, 0}}, {{5, 70, 20}, {30, 3, 2}}, 0);
+  // cross-queue aliasing: the served order decides what is read and written
+  gen_qm_case("qm_alias", 707, {2, 1, 3}, {{30, 25, 20}, {15, 15, 15}}, {{40, 40, 40}, {20, 20, 20}}, 1);
+}
+
 // ------------------------------------------------------ L3/L4 verification --
 // SURVEY §8 f3.  Frames from build_frame (valid IPv4 header and TCP/UDP
 // checksums), then mutated.  Expected flags use the reference's own
@@ -1091,6 +1308,11 @@ int main(int argc, char** argv) {
     if (e.hash(std::span<const std::uint8_t>(t)) != 0x51ccc178u) { std::fprintf(stderr, "MS vector mismatch\n"); return 1; }
     if (e.hash(std::span<const std::uint8_t>(t.data(), 8)) != 0x323e8fc2u) { std::fprintf(stderr, "MS vector mismatch\n"); return 1; }
   }
+  if (argc > 2 && std::string(argv[2]) == "qm") {  // only the QueueManager fixtures
+    gen_qm();
+    std::printf("qm fixtures written to %s\n", g_out.c_str());
+    return 0;
+  }
   gen_checksum();
   gen_rss();
   gen_rx_mix();
@@ -1099,6 +1321,7 @@ int main(int argc, char** argv) {
   gen_qp_batch();
   gen_l34();
   gen_tso_vlan();
+  gen_qm();
   std::printf("golden fixtures written to %s\n", g_out.c_str());
   return 0;
 }

@@ -1,31 +1,25 @@
-# Same-box A/B of the f1 stage: smart_nic_amd/ab/{libnicgpu,libnic_host}.so (A,
-# built from HEAD in a git worktree) against the working tree's libraries (B),
-# alternating processes (LD_LIBRARY_PATH beats the driver's RUNPATH); the RX-stage GPU tests first.
+#!/bin/bash
+# Row f1 A/B: the f1 GPU tests on the production build, then the pipelined C3 stage bench and
+# the deliver_kernel's average duration (kernel trace) per deliver-kernel variant
+# (smart_nic_amd/ab/<variant>/libnicgpu.so, picked up through LD_LIBRARY_PATH).
 set -o pipefail
-mkdir -p gpurun_out
-PT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
-timeout -k 10 900 $PT tests/test_rx_stage.py tests/test_gpu_fullsize.py -k "rx_stage or f1_full" -m gpu \
-  > gpurun_out/pytest_f1.log 2>&1
-rc=$?; grep -E "passed|failed" gpurun_out/pytest_f1.log | tail -3; [ $rc -eq 0 ] || exit $rc
-g++ -std=c++20 -O2 -Iinclude tools/bench_rx_stage.cpp -Lsmart_nic_amd -lnic_host -lnicgpu \
-    -Wl,-rpath,"$PWD/smart_nic_amd" -o gpurun_out/bench_rx_stage || exit 1
-: > gpurun_out/f1_ab.jsonl
-for i in 1 2 3; do
-  for side in A B; do
-    if [ $side = A ]; then export LD_LIBRARY_PATH=$PWD/smart_nic_amd/ab; else unset LD_LIBRARY_PATH; fi
-    if [ "${MODESET:-}" = pinned1m ]; then set -- "1048576 12 0 device pinned pipelined" "1048576 9 0 device pinned sync"
-    else set -- "1024 12 0 device pinned pipelined" "65536 9 0 device pinned sync" "1048576 12 0 device device pipelined device" "1048576 9 0 device device sync device"; fi
-    for mode in "$@"; do
-      timeout -k 10 120 ./gpurun_out/bench_rx_stage c3 $mode 2>> gpurun_out/f1_ab.err | sed "s/^{/{\"side\": \"$side\", /" >> gpurun_out/f1_ab.jsonl || exit 1
-    done
-  done
-done
-python - <<'PY'
-import json, collections
-d = collections.defaultdict(list)
-for l in open("gpurun_out/f1_ab.jsonl"):
-    r = json.loads(l)
-    d[(r["tx_descriptors"], r["descriptors"], r["mode"], r["side"])].append(r["us_median"])
-for k, v in sorted(d.items()):
-    print(k, v)
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out/f1ab
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v -k "rx_stage or f1_full or queue_manager" --timeout 300 --timeout-method thread > gpurun_out/f1ab/test.log 2>&1; rc=$?
+grep -E "passed|failed" gpurun_out/f1ab/test.log | tail -3; [ $rc -eq 0 ] || exit $rc
+ARGS="c3 1048576 12 0 device device pipelined device"
+cd /tmp && export TMPDIR=/tmp
+for v in prod ${VARIANTS:-u2 u8 w4 w16u2}; do
+  if [ $v = prod ]; then LP=""; else LP=$R/smart_nic_amd/ab/$v; fi
+  LD_LIBRARY_PATH=$LP timeout -k 10 120 $R/tools/bin/bench_rx_stage $ARGS > $R/gpurun_out/f1ab/$v.json 2>&1 || { echo "$v bench failed"; tail -3 $R/gpurun_out/f1ab/$v.json; exit 1; }
+  LD_LIBRARY_PATH=$LP timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/f1ab/tr_$v -o f1 --output-format csv -- $R/tools/bin/bench_rx_stage c3 1048576 6 0 device device pipelined device > $R/gpurun_out/f1ab/tr_$v.log 2>&1 || { echo "$v trace failed"; exit 1; }
+  python3 - $v <<'PY'
+import csv, glob, json, os, sys
+v = sys.argv[1]
+R = os.environ["GRAFT_REPO_ROOT"] + "/gpurun_out/f1ab"
+j = [l for l in open(f"{R}/{v}.json") if l.startswith("{")][-1]
+st = glob.glob(f"{R}/tr_{v}/**/*kernel_stats.csv", recursive=True)[0]
+d = [r for r in csv.DictReader(open(st)) if "deliver_kernel" in r["Name"]]
+print(v, "pipelined_us", json.loads(j)["us_median"], "deliver_avg_us", [round(float(r["AverageNs"]) / 1e3, 1) for r in d])
 PY
+done

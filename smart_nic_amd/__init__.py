@@ -76,15 +76,19 @@ ABI_SYMBOLS = (
     "nicgpu_qp_create",
     "nicgpu_qp_destroy",
     "nicgpu_qp_reserve",
+    "nicgpu_qp_bind",
     "nicgpu_qp_plan",
     "nicgpu_qp_plan_on",
     "nicgpu_qp_check",
     "nicgpu_qp_resolve",
+    "nicgpu_qp_resolve_start",
+    "nicgpu_qp_resolve_finish",
     "nicgpu_qp_rss_list",
     "nicgpu_rx_offload_count",
     "nicgpu_qp_rss_scatter",
     "nicgpu_qp_group",
     "nicgpu_qp_deliver",
+    "nicgpu_qp_deliver_range",
     "nicgpu_icrc_batch",
     "nicgpu_tso_segment",
 )
@@ -126,14 +130,18 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_qp_create": (i32, [vp, i32]),
         "nicgpu_qp_destroy": (i32, [vp]),
         "nicgpu_qp_reserve": (i32, [vp, sz, sz, vp]),
+        "nicgpu_qp_bind": (i32, [vp, vp, sz, vp, sz, vp]),
         "nicgpu_qp_plan": (i32, [vp, vp, ctypes.c_uint64, sz, ctypes.c_uint64, vp, vp, vp]),
         "nicgpu_qp_plan_on": (i32, [vp, vp, ctypes.c_uint64, sz, ctypes.c_uint64, vp, vp, vp, vp]),
         "nicgpu_qp_check": (i32, [vp, ctypes.c_uint64, sz, sz, vp, vp]),
         "nicgpu_qp_resolve": (i32, [vp, ctypes.c_uint64, sz, sz, ctypes.c_uint64, ctypes.c_uint16, vp, vp, vp, vp]),
+        "nicgpu_qp_resolve_start": (i32, [vp, ctypes.c_uint64, sz, sz, ctypes.c_uint64, ctypes.c_uint16, vp]),
+        "nicgpu_qp_resolve_finish": (i32, [vp, vp, vp, vp, vp]),
         "nicgpu_qp_rss_list": (i32, [vp, sz, vp]),
         "nicgpu_qp_rss_scatter": (i32, [vp, sz, vp]),
         "nicgpu_qp_group": (i32, [vp, sz, sz, vp]),
         "nicgpu_qp_deliver": (i32, [vp, vp, ctypes.c_uint64, sz, vp, i32, u32, u32, vp, vp]),
+        "nicgpu_qp_deliver_range": (i32, [vp, vp, ctypes.c_uint64, sz, sz, u32, vp, i32, u32, u32, vp, vp]),
         "nicgpu_icrc_batch": (i32, [vp, vp, sz, i32, vp, vp, vp]),
         "nicgpu_tso_segment": (i32, [vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint64, u32, vp, vp, vp]),
         "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),

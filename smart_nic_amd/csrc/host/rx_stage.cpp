@@ -124,11 +124,20 @@ std::uint32_t plan_packet(const BatchedQueuePairConfig& config, std::size_t mem_
 void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> txc,
                        std::span<const CompletionEntry> rxc) {
   if (!config.on_interrupt || (!config.enable_tx_interrupts && !config.enable_rx_interrupts)) return;
+  InterruptCursor at;
+  replay_interrupts(config, txc, rxc, at, txc.size());
+}
+
+void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> txc,
+                       std::span<const CompletionEntry> rxc, InterruptCursor& at, std::size_t n) {
   constexpr auto kOk = static_cast<std::uint32_t>(CompletionCode::Success);
   constexpr auto kFault = static_cast<std::uint32_t>(CompletionCode::Fault);
+  const bool any = config.on_interrupt && (config.enable_tx_interrupts || config.enable_rx_interrupts);
   const std::uint16_t q = config.queue_id;
-  std::size_t j = 0;
-  for (const CompletionEntry& t : txc) {
+  std::size_t j = at.rx;
+  const std::size_t end = std::min(txc.size(), at.tx + n);
+  for (std::size_t i = at.tx; i < end; ++i) {
+    const CompletionEntry& t = txc[i];
     // the packets that popped RX descriptors: Success (all delivered, or an
     // RX-side abort), and a DMA write fault after some segment (segments_produced > 0)
     const bool popped = t.status == kOk || (t.status == kFault && t.segments_produced > 0);
@@ -137,7 +146,7 @@ void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const Com
       fires = true;
       for (std::uint32_t k = 0; k < t.segments_produced && j < rxc.size(); ++k) {
         const CompletionEntry& e = rxc[j++];
-        if (config.enable_rx_interrupts) config.on_interrupt(q, e);
+        if (any && config.enable_rx_interrupts) config.on_interrupt(q, e);
         if (e.status != kOk) {  // the packet ends here and its TX completion fires none
           fires = false;
           break;
@@ -145,8 +154,10 @@ void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const Com
       }
       if (t.status != kOk) fires = false;
     }
-    if (fires && config.enable_tx_interrupts) config.on_interrupt(q, t);
+    if (any && fires && config.enable_tx_interrupts) config.on_interrupt(q, t);
   }
+  at.tx = end;
+  at.rx = j;
 }
 
 // Count pass, prefix over the chunks, fill pass (each chunk in its own thread).
@@ -998,6 +1009,8 @@ struct BatchedQueuePair::Slot {
   // the batch, between front() and finish()
   nicgpu_qp_view v{};
   std::size_t ntx = 0, nrx_total = 0, tn = 0, nq = 0;
+  std::size_t settled = 0;  // completions [0, settled) delivered with the resolve
+  bool relaxed = false;     // completions rewritten after the resolve's event
   bool rss = false;
   std::uint64_t* meta = nullptr;  // [count][hits tn]
   std::uint32_t *qs = nullptr, *qe = nullptr, *which = nullptr;
@@ -1532,10 +1545,18 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   void* ps = side ? S.side_plan : stream;
   if (dev_desc) {
     check(nicgpu_qp_reserve(sl.qp, ntx, nrx, &v), "nicgpu_qp_reserve");
-    // after whatever the caller enqueued on `stream` before handing them over
-    if (side) check(nicgpu_stream_wait_event(ps, sl.ev_submit), "nicgpu_stream_wait_event");
-    if (ntx) check(nicgpu_memcpy_async(v.tx, sl.tx_dev, ntx * sizeof(TxDescriptor), ps), "nicgpu_memcpy_async");
-    if (nrx) check(nicgpu_memcpy_async(v.rx, sl.rx_dev, nrx * sizeof(RxDescriptor), ps), "nicgpu_memcpy_async");
+    if (side) {
+      // read in place (outside the image, so no write of the batch changes
+      // them), after whatever the caller enqueued on `stream` before handing
+      // them over — no copy to compete with the earlier batch's DMA writes
+      check(nicgpu_stream_wait_event(ps, sl.ev_submit), "nicgpu_stream_wait_event");
+      check(nicgpu_qp_bind(sl.qp, reinterpret_cast<const nicgpu_tx_descriptor*>(sl.tx_dev), ntx,
+                           reinterpret_cast<const nicgpu_rx_descriptor*>(sl.rx_dev), nrx, &v),
+            "nicgpu_qp_bind");
+    } else {  // inside the image: copied in stream order, before this batch writes
+      if (ntx) check(nicgpu_memcpy_async(v.tx, sl.tx_dev, ntx * sizeof(TxDescriptor), ps), "nicgpu_memcpy_async");
+      if (nrx) check(nicgpu_memcpy_async(v.rx, sl.rx_dev, nrx * sizeof(RxDescriptor), ps), "nicgpu_memcpy_async");
+    }
   } else {
     out.timings.copy_us += sl.upload_us;
     check(nicgpu_stream_wait_event(ps, sl.ev_tx), "nicgpu_stream_wait_event");
@@ -1558,6 +1579,14 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     if (side) check(nicgpu_stream_wait_event(stream, sl.ev_rx), "nicgpu_stream_wait_event");
   }
   out.timings.copy_us += us_since(t);
+  // the speculative resolve goes in behind the piece sums before the overlap
+  // check's verdict (it writes only the context's completions and writes),
+  // so the stream does not wait for this thread's round trip on the check
+  t = clock::now();
+  check(nicgpu_qp_resolve_start(sl.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, stream),
+        "nicgpu_qp_resolve_start");
+  check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");  // final unless relaxed / tail below
+  out.timings.resolve_us += us_since(t);
   // overlapping buffers go to the host path before anything is written; a
   // ring whose RX buffers are not in ascending address order is sorted there.
   // The check synchronises `ps`: the descriptors are then in place for `stream`.
@@ -1572,10 +1601,32 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   check_us += us_since(t);
   if (!disjoint) return false;
   t = clock::now();
-  std::uint64_t done = 0, used = 0;
+  // the DMA writes and RSS of the completions the resolve settles (bounded on
+  // the device) go in at once: the host waits for the resolve while they are
+  // already queued, so the stream does not idle on this thread's round trip
+  sl.tn = sl.nq = 0;
+  const nicgpu_rss_ctx* rctx = nullptr;
+  std::uint64_t* hits = nullptr;
+  if (config_.rss != nullptr) {
+    if (config_.tuple.mode == TupleMode::None)
+      throw GpuError("process_batch: TupleMode::None cannot produce hashes", NICGPU_ERR_INVALID);
+    const auto& table = config_.rss->config().table;
+    sl.tn = table.size();
+    for (const std::uint16_t q : table) sl.nq = std::max<std::size_t>(sl.nq, std::size_t{q} + 1);
+    rctx = config_.rss->device_context(stream);
+    hits = static_cast<std::uint64_t*>(sl.hits.get(std::max<std::size_t>(sl.tn, 1) * sizeof(std::uint64_t)));
+    check(nicgpu_memset_async(hits, 0, sl.tn * sizeof(std::uint64_t), stream), "nicgpu_memset_async");
+  }
+  out.timings.resolve_us += us_since(t);
+  t = clock::now();
+  deliver(sl, mem, 0, nrx, NICGPU_DELIVER_SETTLED, rctx, hits, stream);
+  out.timings.gather_us += us_since(t);
+  t = clock::now();
+  std::uint64_t done = 0, used = 0, settled = 0;
   nicgpu_qp_stats ds{};
-  check(nicgpu_qp_resolve(sl.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, &done, &used, &ds, stream),
-        "nicgpu_qp_resolve");
+  check(nicgpu_qp_resolve_finish(sl.qp, &done, &used, &settled, &ds), "nicgpu_qp_resolve_finish");
+  sl.settled = settled;
+  sl.relaxed = done < ntx || settled < used;  // completions rewritten after ev_resolved
   out.timings.resolve_us += us_since(t);
   t = clock::now();
   const QueuePairStats d{ds.tx_packets,         ds.rx_packets,         ds.tx_bytes,
@@ -1628,6 +1679,16 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
 // they go down on the side stream at once, while this thread enqueues the DMA
 // writes and the RSS list, launch, scatter and dispatch lists (their sizes
 // read on the device); the RSS results follow them down.
+// The DMA writes and RSS of completions [a, b) (NICGPU_DELIVER_SETTLED: b
+// lowered on the device to the pending resolve's settled prefix).
+void BatchedQueuePair::deliver(Slot& sl, const DeviceHostMemory& mem, std::size_t a, std::size_t b, unsigned flags,
+                               const nicgpu_rss_ctx* rctx, std::uint64_t* hits, void* stream) {
+  check(nicgpu_qp_deliver_range(sl.qp, reinterpret_cast<std::uint8_t*>(mem.base), mem.size, a, b, flags, rctx,
+                                rctx ? static_cast<int>(config_.tuple.mode) : NICGPU_TUPLE_NONE, config_.tuple.raw_offset,
+                                config_.tuple.raw_length, rctx ? hits : nullptr, stream),
+        "nicgpu_qp_deliver_range");
+}
+
 void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult& out, void* stream) {
   using clock = std::chrono::steady_clock;
   auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
@@ -1636,12 +1697,7 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   const std::size_t ntx = sl.ntx, nrx_total = sl.nrx_total;
   auto t = clock::now();
   sl.rss = config_.rss != nullptr && nrx_total != 0;
-  sl.tn = sl.nq = 0;
-  if (sl.rss) {
-    const auto& table = config_.rss->config().table;
-    sl.tn = table.size();
-    for (const std::uint16_t q : table) sl.nq = std::max<std::size_t>(sl.nq, std::size_t{q} + 1);
-  }
+  if (!sl.rss) sl.tn = sl.nq = 0;
   const std::size_t tn = sl.tn, nq = sl.nq;
   const bool rss = sl.rss;
   const bool keep = config_.results_on_device;  // results stay in the slot's device buffers
@@ -1668,13 +1724,15 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   sl.qe = sl.qs + nq;
   sl.which = sl.qe + nq;
   sl.meta[0] = 0;
-  std::uint64_t* hits =
-      rss ? static_cast<std::uint64_t*>(sl.hits.get(std::max<std::size_t>(tn, 1) * sizeof(std::uint64_t))) : nullptr;
+  std::uint64_t* hits = config_.rss ? static_cast<std::uint64_t*>(sl.hits.get(std::max<std::size_t>(sl.tn, 1) * 8)) : nullptr;
   sl.rss_recorded = std::promise<void>();
   sl.rss_released = false;
   std::shared_future<void> rss_ready = sl.rss_recorded.get_future().share();
-  check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");
+  if (sl.relaxed) check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");
   sl.down.emplace(sl.worker);
+  // the dispatch lists are made here too, on the download stream: they read
+  // this slot's buffers only, so the next batch's piece sums need not queue
+  // behind them on `stream`
   sl.down->start([&sl, &S, &out, &v, ntx, nrx_total, tn, nq, rss, keep, hits, rss_ready](SideJob& j) {
     bool ok = j.ok(nicgpu_set_device(S.device), "nicgpu_set_device") &&
               j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_resolved), "nicgpu_stream_wait_event");
@@ -1685,6 +1743,7 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
                 "nicgpu_memcpy_async");
     rss_ready.wait();
     ok = ok && j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_done), "nicgpu_stream_wait_event");
+    if (ok && rss) ok = j.ok(nicgpu_qp_group(sl.qp, nrx_total, nq, S.side_down), "nicgpu_qp_group");
     if (ok && rss)
       ok = j.ok(nicgpu_memcpy_async(sl.meta, v.rss_count, sizeof(std::uint64_t), S.side_down), "nicgpu_memcpy_async") &&
            j.ok(nicgpu_memcpy_async(sl.meta + 1, hits, tn * sizeof(std::uint64_t), S.side_down), "nicgpu_memcpy_async") &&
@@ -1701,22 +1760,13 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   try {
     out.timings.copy_us += us_since(t);
     t = clock::now();
-    // the DMA writes and the RSS of the frames they deliver, one launch
-    // (the headers hashed from the bytes the writes move)
-    const nicgpu_rss_ctx* rctx = nullptr;
-    if (rss) {
-      if (config_.tuple.mode == TupleMode::None)
-        throw GpuError("process_batch: TupleMode::None cannot produce hashes", NICGPU_ERR_INVALID);
-      rctx = config_.rss->device_context(stream);
-      check(nicgpu_memset_async(hits, 0, tn * sizeof(std::uint64_t), stream), "nicgpu_memset_async");
-    }
-    check(nicgpu_qp_deliver(sl.qp, reinterpret_cast<std::uint8_t*>(mem.base), mem.size, nrx_total, rctx,
-                            rss ? static_cast<int>(config_.tuple.mode) : NICGPU_TUPLE_NONE, config_.tuple.raw_offset,
-                            config_.tuple.raw_length, rss ? hits : nullptr, stream),
-          "nicgpu_qp_deliver");
+    // the rest of the DMA writes and RSS (the settled prefix went in with the
+    // resolve), one launch: the headers hashed from the bytes the writes move
+    if (sl.settled < nrx_total)
+      deliver(sl, mem, sl.settled, nrx_total, NICGPU_DELIVER_APPEND,
+              config_.rss ? config_.rss->device_context(stream) : nullptr, hits, stream);
     out.timings.gather_us += us_since(t);
     t = clock::now();
-    if (rss) check(nicgpu_qp_group(sl.qp, nrx_total, nq, stream), "nicgpu_qp_group");
     check(nicgpu_event_record(sl.ev_done, stream), "nicgpu_event_record");
   } catch (...) {
     sl.wait();  // the downloads must not outlive this batch's buffers

@@ -30,6 +30,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -1761,7 +1762,8 @@ struct DeliverParams {
   uint64_t mem_size;
   const nicgpu_segment_write* w;
   const nicgpu_completion* rxc;  // statuses (RSS of Success completions)
-  uint64_t n;
+  uint64_t j0, n;                // completions [j0, n) ...
+  const unsigned long long* n_dev;  // ... with n lowered to *n_dev (a speculative resolve's settled prefix)
   RxParams rss;                  // mode NICGPU_TUPLE_NONE: no RSS
   uint32_t* rx_hash;
   uint16_t* rx_queue;
@@ -1769,8 +1771,18 @@ struct DeliverParams {
   unsigned long long* count;
 };
 
-constexpr int kDlvWpb = 8;  // waves per block
-constexpr int kDlvU = 4;    // 64-entry sub-steps per step (loads in flight per lane)
+#ifndef NICGPU_DLV_WPB
+#define NICGPU_DLV_WPB 8
+#endif
+#ifndef NICGPU_DLV_U
+#define NICGPU_DLV_U 4
+#endif
+#ifndef NICGPU_DLV_RESERVE
+#define NICGPU_DLV_RESERVE 0
+#endif
+constexpr int kDlvReserveCus = NICGPU_DLV_RESERVE;  // default of NICGPU_DLV_RESERVE_CUS (tuning)
+constexpr int kDlvWpb = NICGPU_DLV_WPB;  // waves per block
+constexpr int kDlvU = NICGPU_DLV_U;      // 64-entry sub-steps per step (loads in flight per lane)
 constexpr uint32_t kDlvRec = 24;  // item record: dst u64 | src (or prefix word) u64 | len u32 | first entry u32
 constexpr uint32_t kDlvMarks = 4u * kWave * kDlvU;  // bytes
 constexpr uint32_t kDlvWaveBytes = kDlvMarks + 64u * 8u + 192u * kDlvRec + 64u * kHdrStride * 16u;  // marks|wdst|items|stage
@@ -1838,22 +1850,27 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
     for (uint32_t k = 0; k < (uint32_t) kHdrChunks; ++k) stage[hdr_slot(lane, k)] = make_uint4(0u, 0u, 0u, 0u);
   }
   __syncthreads();
-  const uint64_t ntiles = (P.n + kWave - 1) / kWave;
+  uint64_t n = P.n;
+  if (P.n_dev) {
+    const uint64_t m = *P.n_dev;
+    n = m < n ? m : n;
+  }
+  const uint64_t ntiles = n > P.j0 ? (n - P.j0 + kWave - 1) / kWave : 0;
   const uint64_t nwaves = (uint64_t) gridDim.x * kDlvWpb;
   uint32_t my_count = 0;
   for (uint64_t tile = (uint64_t) blockIdx.x * kDlvWpb + w; tile < ntiles; tile += nwaves) {
     // ---- this lane's write: its items and their stream entries
-    const uint64_t j = tile * kWave + lane;
+    const uint64_t j = P.j0 + tile * kWave + lane;
     nicgpu_segment_write wr{};
     bool flag = false;
-    if (j < P.n) {
+    if (j < n) {
       wr = P.w[j];
       if (RSS) flag = P.rxc[j].status == nicqp::kSuccess;
     }
     const uint64_t plen = wr.prefix_len == 4 ? 4 : 0;
     const uint64_t total = plen + wr.len_a + wr.len_b;
     // entries outside the image are skipped (the host validated them)
-    const bool ok = j < P.n && !(wr.prefix_len > 4 || wr.dst > P.mem_size || total > P.mem_size - wr.dst ||
+    const bool ok = j < n && !(wr.prefix_len > 4 || wr.dst > P.mem_size || total > P.mem_size - wr.dst ||
                                  wr.src_a > P.mem_size || wr.len_a > P.mem_size - wr.src_a ||
                                  wr.src_b > P.mem_size || wr.len_b > P.mem_size - wr.src_b);
     const uint64_t d1 = wr.dst + plen, d2 = d1 + wr.len_a;
@@ -1928,7 +1945,9 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
             shv[u] = (uint32_t) (a & 3) | 4u;  // bit 2: a source window (not the prefix)
             if (a4 >= 0 && (uint64_t) a4 + 20 <= P.mem_size) {
               __builtin_memcpy(vv[u], P.mem + a4, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
-              vv[u][4] = *reinterpret_cast<const uint32_t*>(P.mem + a4 + 16);
+              // the fifth dword only for a shifted window (equal alignment of
+              // source and destination, the common case, needs four)
+              vv[u][4] = (a & 3) ? *reinterpret_cast<const uint32_t*>(P.mem + a4 + 16) : 0u;
             } else {  // bytes outside the image read as 0 (never stored: outside [lo, hi))
 #pragma unroll
               for (int i = 0; i < 5; ++i) {
@@ -1989,7 +2008,7 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      if (j < P.n) {
+      if (j < n) {
         if (flag && ok) {
           uint64_t len = total;
           if (len > NICGPU_MAX_PACKET) len = NICGPU_MAX_PACKET;  // the tuple lies in the first 82 B
@@ -3189,6 +3208,9 @@ struct QpPlan {
 using QpCtx = nicqp::Ctx<nicgpu_tx_descriptor, nicgpu_rx_descriptor, QpPlan>;
 constexpr unsigned kQpBlock = 256;
 constexpr unsigned kQpStats = 16;
+// after the per-block stats: RX used, first mismatch, settled prefix, then the
+// batch's 16 stats totals — the one download a resolve needs
+constexpr unsigned kQpTail = 3 + 16;
 constexpr int kQpRelaxSteps = 8;  // position relaxations before the host takes the rest
 
 struct QpNullSink {
@@ -3309,6 +3331,34 @@ __global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32
     uint64_t x = 0;
     for (unsigned j = 0; j < kQpBlock / kWave; ++j) x += red[threadIdx.x][j];
     partials[(uint64_t) blockIdx.x * kQpStats + threadIdx.x] = x;
+  }
+}
+
+// After a final pass: the per-block stats summed into tail[3..19), and after
+// the speculative one tail[2] = the RX completions it made final — those of
+// the packets before the first mismatch, [0, pos[first]), or all `used` when
+// nothing differed.  nicgpu_qp_deliver_range(NICGPU_DELIVER_SETTLED) reads it
+// on the device, so the DMA writes start before the host has seen the resolve.
+constexpr unsigned kQpReduceThreads = 1024;
+__global__ __launch_bounds__(kQpReduceThreads) void qp_reduce_kernel(const uint64_t* __restrict__ partials,
+                                                                     unsigned nblocks, const uint32_t* __restrict__ pos,
+                                                                     uint64_t ntx, bool settle) {
+  __shared__ uint64_t red[kQpReduceThreads];
+  uint64_t* tail = const_cast<uint64_t*>(partials) + (size_t) nblocks * kQpStats;
+  const unsigned k = threadIdx.x % kQpStats, r = threadIdx.x / kQpStats;
+  constexpr unsigned kRows = kQpReduceThreads / kQpStats;
+  uint64_t x = 0;
+  for (unsigned b = r; b < nblocks; b += kRows) x += partials[(size_t) b * kQpStats + k];
+  red[threadIdx.x] = x;
+  __syncthreads();
+  for (unsigned h = kRows / 2; h > 0; h >>= 1) {
+    if (r < h) red[threadIdx.x] += red[threadIdx.x + h * kQpStats];
+    __syncthreads();
+  }
+  if (threadIdx.x < kQpStats) tail[3 + threadIdx.x] = red[threadIdx.x];
+  if (settle && threadIdx.x == 0) {
+    const uint64_t first = tail[1];
+    tail[2] = first < ntx ? (uint64_t) pos[first] : tail[0];
   }
 }
 
@@ -3497,8 +3547,14 @@ struct nicgpu_qp {
   size_t c_tx = 0, c_rx = 0, c_plans = 0, c_counts = 0, c_base = 0, c_need = 0, c_pos = 0, c_txc = 0;
   size_t c_rxc = 0, c_w = 0, c_flags = 0, c_at = 0, c_desc = 0, c_which = 0, c_h = 0, c_q = 0, c_rh = 0, c_rq = 0;
   size_t c_pdesc = 0, c_pcs = 0, c_part = 0, c_tmp = 0;
+  // the descriptors the kernels read: the context's own copies (tx_own /
+  // rx_own, sized by nicgpu_qp_reserve) or the caller's (nicgpu_qp_bind)
   nicgpu_tx_descriptor* tx = nullptr;
   nicgpu_rx_descriptor* rx = nullptr;
+  nicgpu_tx_descriptor* tx_own = nullptr;
+  nicgpu_rx_descriptor* rx_own = nullptr;
+  uint8_t* tmp_chk = nullptr;  // nicgpu_qp_check's scan storage (it may run beside a resolve)
+  size_t c_tmp_chk = 0;
   QpPlan* plans = nullptr;
   uint32_t *counts = nullptr, *base = nullptr, *need = nullptr, *pos = nullptr;
   uint64_t* piece_desc = nullptr;
@@ -3517,12 +3573,22 @@ struct nicgpu_qp {
   uint8_t* tmp = nullptr;
   uint64_t host_scal[4] = {0, 0, 0, 0};
   // page-locked landing space of the small downloads (a pageable one is staged
-  // and waited for on the host): [grid * kQpStats + 2] the resolve's stats,
-  // RX count and first mismatch, then misc(): piece count, check flags, relax verdict
+  // and waited for on the host): [kQpTail] the resolve's RX count, first
+  // mismatch, settled prefix and stats totals, then misc(): piece count, check
+  // flags, relax verdict
   uint64_t* hp = nullptr;
-  uint64_t* misc() const { return hp + (size_t) grid * kQpStats + 2; }
+  uint64_t* misc() const { return hp + kQpTail; }
   unsigned grid = 1;
-  hipEvent_t planned = nullptr;  // nicgpu_qp_plan_on: the piece descriptors are written
+  hipEvent_t planned = nullptr;   // nicgpu_qp_plan_on: the piece descriptors are written
+  hipEvent_t resolved = nullptr;  // nicgpu_qp_resolve_start: its partials are on the host
+  // the resolve between nicgpu_qp_resolve_start and _finish
+  struct Pending {
+    bool on = false;
+    uint64_t mem_size = 0, ntx = 0, nrx = 0, max_mtu = 0;
+    uint16_t queue_id = 0;
+    hipStream_t s = nullptr;
+    unsigned grid = 1;
+  } res;
   bool delivered = false;  // the RSS results are per completion (nicgpu_qp_deliver), not compacted
 };
 
@@ -3578,18 +3644,19 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
   q->device = device;
   q->grid = (unsigned) di.cus * 8u;
   if (hipMalloc(&q->scal, 4 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc(&q->partials, ((size_t) q->grid * kQpStats + 2) * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&q->partials, ((size_t) q->grid * kQpStats + kQpTail) * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&q->queue_start, 65536 * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&q->queue_end, 65536 * sizeof(uint32_t)) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
   }
-  if (hipHostMalloc(reinterpret_cast<void**>(&q->hp), ((size_t) q->grid * kQpStats + 2 + 8) * sizeof(uint64_t)) !=
+  if (hipHostMalloc(reinterpret_cast<void**>(&q->hp), (kQpTail + 16) * sizeof(uint64_t)) !=
       hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
   }
-  if (hipEventCreateWithFlags(&q->planned, hipEventDisableTiming) != hipSuccess) {
+  if (hipEventCreateWithFlags(&q->planned, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&q->resolved, hipEventDisableTiming) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_HIP;
   }
@@ -3600,7 +3667,7 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
 int nicgpu_qp_destroy(nicgpu_qp* q) {
   if (!q) return NICGPU_ERR_INVALID;
   DeviceGuard g(q->device);
-  void* bufs[] = {q->tx, q->rx, q->plans, q->counts, q->base, q->need, q->pos, q->piece_desc, q->piece_csum,
+  void* bufs[] = {q->tx_own, q->rx_own, q->tmp_chk, q->plans, q->counts, q->base, q->need, q->pos, q->piece_desc, q->piece_csum,
                   q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
                   q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sort_key, q->sorted_key, q->queue_which,
                   q->queue_start, q->queue_end, q->end_max};
@@ -3608,6 +3675,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
     if (b) (void) hipFree(b);
   if (q->hp) (void) hipHostFree(q->hp);
   if (q->planned) (void) hipEventDestroy(q->planned);
+  if (q->resolved) (void) hipEventDestroy(q->resolved);
   delete q;
   return NICGPU_OK;
 }
@@ -3619,8 +3687,10 @@ int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view
   DeviceGuard g(q->device);
   int st = NICGPU_OK;
   const size_t t1 = ntx + 1, r1 = nrx + 1;
-  if (st == NICGPU_OK) st = qp_grow(q->tx, q->c_tx, ntx ? ntx : 1);
-  if (st == NICGPU_OK) st = qp_grow(q->rx, q->c_rx, nrx ? nrx : 1);
+  if (st == NICGPU_OK) st = qp_grow(q->tx_own, q->c_tx, ntx ? ntx : 1);
+  if (st == NICGPU_OK) st = qp_grow(q->rx_own, q->c_rx, nrx ? nrx : 1);
+  q->tx = q->tx_own;
+  q->rx = q->rx_own;
   if (st == NICGPU_OK) st = qp_grow(q->plans, q->c_plans, t1);
   if (st == NICGPU_OK) st = qp_grow(q->counts, q->c_counts, t1);
   if (st == NICGPU_OK) st = qp_grow(q->base, q->c_base, t1);
@@ -3645,6 +3715,15 @@ int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view
   q->cap_rx = nrx;
   qp_fill_view(q, view);
   return st;
+}
+
+int nicgpu_qp_bind(nicgpu_qp* q, const nicgpu_tx_descriptor* tx, size_t ntx, const nicgpu_rx_descriptor* rx,
+                   size_t nrx, nicgpu_qp_view* view) {
+  if (!q || ntx > q->cap_tx || nrx > q->cap_rx || (ntx && !tx) || (nrx && !rx)) return NICGPU_ERR_INVALID;
+  q->tx = ntx ? const_cast<nicgpu_tx_descriptor*>(tx) : q->tx_own;
+  q->rx = nrx ? const_cast<nicgpu_rx_descriptor*>(rx) : q->rx_own;
+  qp_fill_view(q, view);
+  return NICGPU_OK;
 }
 
 int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
@@ -3701,9 +3780,9 @@ int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int
     size_t tb = 0;
     if (hipcub::DeviceScan::InclusiveScan(nullptr, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s) != hipSuccess)
       return NICGPU_ERR_HIP;
-    st = qp_grow(q->tmp, q->c_tmp, tb);
+    st = qp_grow(q->tmp_chk, q->c_tmp_chk, tb);
     if (st == NICGPU_OK)
-      st = hip_status(hipcub::DeviceScan::InclusiveScan(q->tmp, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s));
+      st = hip_status(hipcub::DeviceScan::InclusiveScan(q->tmp_chk, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s));
   }
   if (st != NICGPU_OK) return st;
   const uint64_t n = ntx > nrx ? ntx : nrx;
@@ -3720,66 +3799,102 @@ int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int
   return NICGPU_OK;
 }
 
-int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu, uint16_t queue_id,
-                      uint64_t* done, uint64_t* rx_used, nicgpu_qp_stats* stats, void* stream) {
-  if (!q || !done || !rx_used || !stats || ntx > q->cap_tx || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+int nicgpu_qp_resolve_start(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu,
+                            uint16_t queue_id, void* stream) {
+  if (!q || ntx > q->cap_tx || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  q->res = nicgpu_qp::Pending{};
   QpCtx C{queue_id, max_mtu, mem_size, q->plans, q->piece_csum, q->tx, q->rx, (uint64_t) nrx};
   const unsigned grid = qp_grid(q, ntx + 1);
+  uint64_t* tail = q->partials + (size_t) grid * kQpStats;
   // first guess: every packet pops what it needs (rx_need).  The final pass
   // runs on it speculatively and reports the first packet that popped
   // otherwise; a batch that settles at once (uniform RX descriptors, no early
-  // ends) is then resolved in one host round trip, without a relaxation step.
+  // ends) needs no relaxation step and no host round trip before its DMA writes.
   hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, (uint64_t) ntx, q->need,
-                     reinterpret_cast<unsigned long long*>(q->partials + (size_t) grid * kQpStats + 1));
+                     reinterpret_cast<unsigned long long*>(tail + 1));
   int st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
-  // per-block stats, then the RX descriptors used and the first mismatch
-  const uint64_t* part = q->hp;  // grid * kQpStats + 2 (page-locked)
-  const size_t npart = (size_t) grid * kQpStats + 2;
-  uint64_t used = 0;
-  unsigned long long first = 0;
-  auto full = [&](uint64_t lim_, const uint32_t* guess) {
-    hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, lim_, q->txc, q->rxc, q->writes,
-                       q->partials, guess);
-    int e = hip_status(hipGetLastError());
-    if (e == NICGPU_OK)
-      e = hip_status(hipMemcpyAsync(q->hp, q->partials, npart * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    if (e == NICGPU_OK) e = hip_status(hipStreamSynchronize(s));
-    used = part[(size_t) grid * kQpStats];
-    if (guess) first = (unsigned long long) part[(size_t) grid * kQpStats + 1];
-    return e;
-  };
-  if (st == NICGPU_OK) st = full((uint64_t) ntx, q->need);
   if (st != NICGPU_OK) return st;
-  uint64_t lim = (uint64_t) ntx;
+  hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, (uint64_t) ntx, q->txc, q->rxc,
+                     q->writes, q->partials, q->need);
+  st = hip_status(hipGetLastError());
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_reduce_kernel, dim3(1), dim3(kQpReduceThreads), 0, s, q->partials, grid, q->pos,
+                     (uint64_t) ntx, true);
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->hp, tail, kQpTail * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipEventRecord(q->resolved, s));
+  if (st != NICGPU_OK) return st;
+  q->res = nicgpu_qp::Pending{true, mem_size, (uint64_t) ntx, (uint64_t) nrx, max_mtu, queue_id, s, grid};
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, uint64_t* rx_settled,
+                             nicgpu_qp_stats* stats) {
+  if (!q || !done || !rx_used || !stats || !q->res.on) return NICGPU_ERR_INVALID;
+  const nicgpu_qp::Pending R = q->res;
+  q->res.on = false;
+  DeviceGuard g(q->device);
+  hipStream_t s = R.s;
+  const uint64_t ntx = R.ntx;
+  QpCtx C{R.queue_id, R.max_mtu, R.mem_size, q->plans, q->piece_csum, q->tx, q->rx, R.nrx};
+  const unsigned grid = R.grid;
+  const uint64_t* part = q->hp;  // the tail, kQpTail words (page-locked)
+  uint64_t* tail = q->partials + (size_t) grid * kQpStats;
+  int st = hip_status(hipEventSynchronize(q->resolved));
+  if (st != NICGPU_OK) return st;
+  uint64_t used = part[0];
+  const unsigned long long first0 = (unsigned long long) part[1];
+  const uint64_t settled = part[2];
+  unsigned long long first = first0;
+  uint64_t lim = ntx;
   if (first < ntx) {  // relax from the same guess (the speculative pass left `need` as it was)
+    // everything from here waits on the stream, behind whatever was enqueued
+    // after the start (a settled-prefix delivery reads none of what follows)
     for (int it = 0; st == NICGPU_OK; ++it) {
       if (it > 0) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
-      q->misc()[4] = (uint64_t) ntx;  // page-locked source; the step below waits for the stream
+      q->misc()[4] = ntx;  // page-locked source; the step below waits for the stream
       if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->scal, q->misc() + 4, sizeof(uint64_t), hipMemcpyHostToDevice, s));
       if (st != NICGPU_OK) break;
-      hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, (uint64_t) ntx, q->scal);
+      hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, ntx, q->scal);
       st = hip_status(hipGetLastError());
       if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->misc() + 3, q->scal, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
       if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
       if (st != NICGPU_OK) break;
       first = (unsigned long long) q->misc()[3];
       // pos is exact up to and including `first` (pops before it agreed)
-      lim = first < ntx ? (uint64_t) first : (uint64_t) ntx;
+      lim = first < ntx ? (uint64_t) first : ntx;
       if (first >= ntx || it + 1 == kQpRelaxSteps) break;
     }
-    if (st == NICGPU_OK) st = full(lim, nullptr);
+    if (st == NICGPU_OK) {
+      hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, lim, q->txc, q->rxc, q->writes,
+                         q->partials, static_cast<const uint32_t*>(nullptr));
+      st = hip_status(hipGetLastError());
+    }
+    if (st == NICGPU_OK) {
+      hipLaunchKernelGGL(qp_reduce_kernel, dim3(1), dim3(kQpReduceThreads), 0, s, q->partials, grid, q->pos, ntx, false);
+      st = hip_status(hipGetLastError());
+    }
+    if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->hp, tail, kQpTail * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
     if (st != NICGPU_OK) return st;
+    used = part[0];
   }
-  uint64_t sum[kQpStats] = {};
-  for (unsigned b = 0; b < grid; ++b)
-    for (unsigned k = 0; k < kQpStats; ++k) sum[k] += part[(size_t) b * kQpStats + k];
-  std::memcpy(stats, sum, sizeof(sum));
+  std::memcpy(stats, part + 3, kQpStats * sizeof(uint64_t));
   *done = lim;
   *rx_used = used;
+  if (rx_settled) *rx_settled = settled < used ? settled : used;
   return NICGPU_OK;
+}
+
+int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu, uint16_t queue_id,
+                      uint64_t* done, uint64_t* rx_used, nicgpu_qp_stats* stats, void* stream) {
+  if (!q || !done || !rx_used || !stats) return NICGPU_ERR_INVALID;
+  const int st = nicgpu_qp_resolve_start(q, mem_size, ntx, nrx, max_mtu, queue_id, stream);
+  if (st != NICGPU_OK) return st;
+  return nicgpu_qp_resolve_finish(q, done, rx_used, nullptr, stats);
 }
 
 int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, void* stream) {
@@ -3869,7 +3984,16 @@ int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t nrx, void* stream) {
 
 int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx, const nicgpu_rss_ctx* ctx,
                       int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint64_t* hits_dev, void* stream) {
-  if (!q || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  return nicgpu_qp_deliver_range(q, mem, mem_size, 0, nrx, 0u, ctx, tuple_mode, raw_off, raw_len, hits_dev, stream);
+}
+
+int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t rx_begin, size_t rx_end,
+                            unsigned flags, const nicgpu_rss_ctx* ctx, int tuple_mode, uint32_t raw_off,
+                            uint32_t raw_len, uint64_t* hits_dev, void* stream) {
+  if (!q || rx_end > q->cap_rx || rx_begin > rx_end) return NICGPU_ERR_INVALID;
+  if (flags & ~(unsigned) (NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_APPEND)) return NICGPU_ERR_INVALID;
+  // the settled prefix of the resolve started last (its grid places the tail)
+  if ((flags & NICGPU_DELIVER_SETTLED) && !q->res.on) return NICGPU_ERR_INVALID;
   if (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0)) return NICGPU_ERR_INVALID;
   if (tuple_mode != NICGPU_TUPLE_NONE && tuple_mode != NICGPU_TUPLE_AUTO && tuple_mode != NICGPU_TUPLE_RAW)
     return NICGPU_ERR_INVALID;
@@ -3882,8 +4006,8 @@ int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx,
   hipStream_t s = static_cast<hipStream_t>(stream);
   q->delivered = rss;
   int st = NICGPU_OK;
-  if (rss) st = hip_status(hipMemsetAsync(q->scal + 3, 0, sizeof(uint64_t), s));
-  if (st != NICGPU_OK || nrx == 0) return st;
+  if (rss && !(flags & NICGPU_DELIVER_APPEND)) st = hip_status(hipMemsetAsync(q->scal + 3, 0, sizeof(uint64_t), s));
+  if (st != NICGPU_OK || rx_end == rx_begin) return st;
   const DeviceInfo* di = nullptr;
   st = current_device_info(&di);
   if (st != NICGPU_OK) return st;
@@ -3892,7 +4016,10 @@ int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx,
   P.mem_size = mem_size;
   P.w = q->writes;
   P.rxc = q->rxc;
-  P.n = nrx;
+  P.j0 = rx_begin;
+  P.n = rx_end;
+  if (flags & NICGPU_DELIVER_SETTLED)
+    P.n_dev = reinterpret_cast<const unsigned long long*>(q->partials + (size_t) q->res.grid * kQpStats + 2);
   P.rss.mode = tuple_mode;
   P.rss.raw_off = raw_off;
   P.rss.raw_len = raw_len;
@@ -3918,9 +4045,16 @@ int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx,
   int dev = 0;
   (void) hipGetDevice(&dev);
   const int bpc = rss ? dlv_blocks_per_cu<true>(dev, lds) : dlv_blocks_per_cu<false>(dev, lds);
-  const uint64_t ntiles = (nrx + kWave - 1) / kWave;
+  const uint64_t ntiles = (rx_end - rx_begin + kWave - 1) / kWave;
   const uint64_t want = (ntiles + kDlvWpb - 1) / kDlvWpb;
-  const uint64_t cap = (uint64_t) di->cus * (uint64_t) bpc;
+  // CUs left without a delivery block, so the next batch's plan and check
+  // (small launches on a side stream) find wave slots while this one runs
+  static const int reserve = [] {
+    const char* e = std::getenv("NICGPU_DLV_RESERVE_CUS");
+    return e ? std::atoi(e) : kDlvReserveCus;
+  }();
+  const uint64_t cus = (uint64_t) (di->cus > reserve + 8 ? di->cus - reserve : di->cus);
+  const uint64_t cap = cus * (uint64_t) bpc;
   const unsigned grid = (unsigned) (want < cap ? want : cap);
   if (rss) hipLaunchKernelGGL(deliver_kernel<true>, dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
   else hipLaunchKernelGGL(deliver_kernel<false>, dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
