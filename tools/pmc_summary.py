@@ -52,6 +52,12 @@ def main():
         "algorithmic_bytes_per_launch": alg,
         "ratio_traffic_over_algorithmic": round(hbm / alg, 4),
     }
+    # sha256[:16] of the kernel source the GPU run used (scripts/gpu_round.sh writes it)
+    try:
+        with open(f"{sys.argv[1]}/kernel_source.sha") as f:
+            out["kernel_source_sha256"] = f.read().split()[0][:16]
+    except OSError:
+        pass
     print(json.dumps(out, indent=1))
 
 
