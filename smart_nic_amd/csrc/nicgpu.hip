@@ -29,7 +29,6 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
-#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -206,16 +205,7 @@ struct RxParams {
   const unsigned long long* n_dev;  // batch size read on the device (min(n, *n_dev)); null: n
   unsigned long long* hits_rep;  // per-context histogram replicas (flush_hist), or null
   unsigned int* hits_done;       // their done ticket
-  uint32_t dyn_slot;             // DYN kernels: this launch's slot of g_dyn_pool
 };
-
-// DYN kernels deal tiles from counters (rx_offload_kernel): one slot per
-// launch, taken round robin by the host, so a slot is reused 64 launches
-// later; 8 group counters and a done counter, each on its own 128-B line.
-// The last block of a launch puts the slot back to zero.
-constexpr uint32_t kDynSlots = 64, kDynStride = 32, kDynGroups = 8;
-constexpr uint32_t kDynSlotWords = (kDynGroups + 1u) * kDynStride;
-__device__ unsigned int g_dyn_pool[kDynSlots * kDynSlotWords];
 
 // s_waitcnt immediate for vmcnt(0) alone (gfx9 encoding: expcnt 7, lgkmcnt 15).
 constexpr int kVmcnt0 = 0x0F70;
@@ -850,14 +840,14 @@ __device__ __forceinline__ void store_out(const RxParams& P, const TileOut& o, b
 // Store the results of the ring's n tiles (bases base0, base0 + step, ...).
 // (Holding 6 B per packet and looking the queue up again here fit 9 tiles
 // instead of 7 on IMIX for no gain there, and cost 64-B batches 10%.)
-template <int SST, typename Lds, typename NValid, typename BaseOf>
+template <int SST, typename Lds, typename NValid>
 __device__ __forceinline__ void flush_ring(const RxParams& P, const Lds& L, const uint8_t* ring, uint32_t n,
-                                           const BaseOf& base_of, uint32_t lane, const NValid& nvalid_of) {
+                                           uint64_t base0, uint64_t step, uint32_t lane, const NValid& nvalid_of) {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   for (uint32_t i = 0; i < n; ++i) {
     const uint8_t* slot = ring + i * kRingTileBytes;
-    const uint64_t base = base_of(i);
+    const uint64_t base = base0 + i * step;
     TileOut o;
     o.pid = base + lane;
     o.h = reinterpret_cast<const uint32_t*>(slot)[lane];
@@ -986,17 +976,8 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
 // XPF: the next contiguous tile's first batch (slots scattered, loads issued)
 // goes out before this tile's epilogue, so the epilogue overlaps its latency
 // (tiles of at most P.xpf_chunks chunks).
-// DYN: tiles are dealt, not fixed.  The tiles are split into 8 contiguous
-// group ranges, group g for the blocks with blockIdx % 8 == g (one XCD under
-// round-robin placement: speed only, never correctness).  A wave's first two
-// tiles are fixed (its index in the group, then that plus the group's wave
-// count); the rest come from the group's counter, one returning atomic per
-// tile issued a whole tile before its value is needed; a wave whose group is
-// exhausted takes tiles from the next groups' counters, so the waves of a
-// fast XCD finish the ranges of a slow one.  RING only (ring slots record
-// their tile bases: at most 64 slots).
 template <int U, bool NT, int WPB, bool CONTIG, bool RANGES, int OCC, bool DEFER, int CPOL = -1, int SST = 0,
-          int HOLD = 0, bool RING = false, bool GEN = true, bool XPF = false, bool DYN = false>
+          int HOLD = 0, bool RING = false, bool GEN = true, bool XPF = false>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void rx_offload_kernel(
     RxParams P) {
   extern __shared__ uint4 lds_dyn[];
@@ -1065,59 +1046,10 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   const uint64_t gw = dbg_on(P, kDbgRotate) ? (gw_hw + WPB) % nwaves : gw_hw;
   uint64_t end, step;
   uint64_t first;
-  static_assert(!DYN || (RING && !RANGES && HOLD == 0 && !DEFER), "DYN: ring kernels only");
-  // DYN state (see above): END = no tile
-  constexpr uint64_t kEnd = ~0ull;
-  unsigned int* dcnt = DYN ? g_dyn_pool + (size_t) P.dyn_slot * kDynSlotWords : nullptr;
-  const uint64_t dT = DYN ? (n_all + kWave - 1) / kWave : 0;
-  const uint32_t dgrp = DYN ? blockIdx.x % kDynGroups : 0u;
-  uint32_t probe = 0;
-  uint32_t tk = 0;  // lane 0: the pending ticket
-  auto dnw = [&](uint32_t g) __attribute__((always_inline)) -> uint64_t {  // waves of group g
-    return (uint64_t) ((gridDim.x + kDynGroups - 1u - g) / kDynGroups) * WPB;
-  };
-  auto dissue = [&]() __attribute__((always_inline)) {
-    if (lane == 0u) {
-      // the offset through a VGPR the compiler cannot prove uniform: a
-      // uniform address makes the atomic optimizer wait (vmcnt(0)) for the
-      // result right after the atomic, which is the latency this hides
-      uint32_t off = ((dgrp + probe) % kDynGroups) * kDynStride;
-      asm volatile("" : "+v"(off));
-      tk = __hip_atomic_fetch_add(dcnt + off, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  };
-  // the base of the tile the pending ticket names (a new ticket issued), or
-  // kEnd when every group is exhausted; an exhausted group's ticket moves the
-  // probe on (one synchronous round trip per group, at the end only)
-  auto dnext = [&]() __attribute__((always_inline)) -> uint64_t {
-    while (probe < kDynGroups) {
-      const uint32_t t = (uint32_t) __builtin_amdgcn_readfirstlane((int) tk);
-      const uint32_t g = (dgrp + probe) % kDynGroups;
-      const uint64_t lo = (uint64_t) g * dT / kDynGroups, hi = (uint64_t) (g + 1u) * dT / kDynGroups;
-      const uint64_t idx = lo + 2u * dnw(g) + t;
-      if (idx < hi) {
-        dissue();
-        return idx * kWave;
-      }
-      ++probe;
-      if (probe < kDynGroups) dissue();
-    }
-    return kEnd;
-  };
-  uint64_t dyn_b1 = 0;
   if (RANGES) {
     first = gw * n_all / nwaves;
     end = (gw + 1) * n_all / nwaves;
     step = kWave;
-  } else if (DYN) {
-    end = n_all;
-    step = 0;
-    const uint64_t lo = (uint64_t) dgrp * dT / kDynGroups, hi = (uint64_t) (dgrp + 1u) * dT / kDynGroups;
-    const uint64_t wig = (uint64_t) (blockIdx.x / kDynGroups) * WPB + (uint32_t) w;  // wave in group
-    const uint64_t s0 = lo + wig, s1 = lo + dnw(dgrp) + wig;
-    dissue();
-    first = s0 < hi ? s0 * kWave : dnext();
-    dyn_b1 = s1 < hi ? s1 * kWave : dnext();
   } else {
     first = gw * kWave;
     end = n_all;
@@ -1130,8 +1062,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
     return lane < nvalid_of(b) ? P.desc[b + lane] : 0ull;
   };
   // descriptors are prefetched one tile ahead
-  uint64_t nxt_base = DYN ? dyn_b1 : first + step;
-  uint64_t d_next = desc_of(nxt_base);
+  uint64_t d_next = desc_of(first + step);
   Tile cur = make_tile<CONTIG>(first, nvalid_of(first), desc_of(first));
   uint64_t held_b[HOLD > 0 ? HOLD : 1];
   uint32_t held_v[HOLD > 0 ? HOLD : 1], held_c[HOLD > 0 ? HOLD : 1], held_h[HOLD > 0 ? HOLD : 1];
@@ -1139,15 +1070,6 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   uint8_t* ring = base_b + P.ring_off + (uint32_t) w * P.hold_r * kRingTileBytes;
   uint32_t ring_n = 0;
   uint64_t ring_base0 = 0;
-  uint64_t slot_b = 0;  // DYN: lane i holds the base of ring slot i
-  auto ring_base_of = [&](uint32_t i) __attribute__((always_inline)) -> uint64_t {
-    if (DYN) {
-      const uint32_t lo = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) slot_b, (int) i);
-      const uint32_t hi = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) (slot_b >> 32), (int) i);
-      return ((uint64_t) hi << 32) | lo;
-    }
-    return ring_base0 + i * step;
-  };
   TileOut pend;
   pend.valid = 0;
   pend.pid = 0;
@@ -1203,11 +1125,8 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
     } else if (DEFER) {
       store_out<SST>(P, pend, L.want_rss);
     }
-    const uint64_t nb = nxt_base;
+    const uint64_t nb = cur.base + step;
     const Tile nxt = make_tile<CONTIG>(nb, nvalid_of(nb), d_next);
-    // DYN: the tile after nxt, here where this tile's loads are all consumed
-    // (its wait for the ticket drains nothing the next tile prefetched)
-    const uint64_t nb2 = DYN ? (nb == kEnd ? kEnd : dnext()) : nb + step;
     pre = false;
     if (XPF && nxt.contig && nxt.total != 0u && nxt.total <= P.xpf_chunks) {
       rsrc_pre = tile_rsrc(nxt);
@@ -1219,11 +1138,10 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
     if constexpr (RING) {
       if (P.out_l34 != nullptr) P.out_l34[o.pid] = (uint8_t) o.l34;
       if (ring_n == P.hold_r) {
-        flush_ring<SST>(P, L, ring, ring_n, ring_base_of, lane, nvalid_of);
+        flush_ring<SST>(P, L, ring, ring_n, ring_base0, step, lane, nvalid_of);
         ring_n = 0;
       }
       if (ring_n == 0) ring_base0 = cur.base;
-      if (DYN && lane == ring_n) slot_b = cur.base;
       uint8_t* slot = ring + ring_n * kRingTileBytes;
       reinterpret_cast<uint32_t*>(slot)[lane] = o.h;
       reinterpret_cast<uint16_t*>(slot + kWave * 4)[lane] = (uint16_t) o.cs;
@@ -1254,22 +1172,11 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
       store_out<SST>(P, o, L.want_rss);
     }
     cur = nxt;
-    nxt_base = nb2;
-    d_next = desc_of(nxt_base);
+    d_next = desc_of(nb + step);
   }
 
   if (DEFER) store_out<SST>(P, pend, L.want_rss);
-  if constexpr (RING) flush_ring<SST>(P, L, ring, ring_n, ring_base_of, lane, nvalid_of);
-  if constexpr (DYN) {
-    // the last block to finish puts the slot back to zero for its next launch
-    __syncthreads();
-    if (threadIdx.x == 0u &&
-        __hip_atomic_fetch_add(dcnt + kDynGroups * kDynStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-            gridDim.x - 1u) {
-      for (uint32_t g = 0; g <= kDynGroups; ++g)
-        __hip_atomic_exchange(dcnt + g * kDynStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if constexpr (RING) flush_ring<SST>(P, L, ring, ring_n, ring_base0, step, lane, nvalid_of);
   if constexpr (HOLD > 0) {
 #pragma unroll
     for (int i = 0; i < HOLD; ++i)
@@ -1636,7 +1543,6 @@ struct RxVariant {
   bool ranges = false;  // balanced per-wave packet ranges (grid sized by packets, not tiles)
   bool ring = false;    // LDS result ring (P.hold_r, P.ring_off sized at launch)
   bool xpf = false;     // cross-tile prefetch (P.xpf_chunks)
-  bool dyn = false;     // tiles dealt by counters (P.dyn_slot; ring of at most 64 slots)
 };
 
 const RxVariant kRxVariants[] = {
@@ -1656,9 +1562,6 @@ const RxVariant kRxVariants[] = {
     // 4 M x 64 B -3%; C2 +0.6% and 9000 B +15% (2500 tiles underfill 512
     // slots of 8 waves) keep 4-wave blocks (profiles/r02y_tune_variants.json).
     {rx_offload_kernel<2, true, 8, true, false, 4, false, -1, 16, 0, true, true, true>, 2, 8, "u2_w8_c_sc1_ring_xpf", false, true, true},
-    // 3 and 4: variants 0 and 1 with tiles dealt by per-group counters (DYN)
-    {rx_offload_kernel<2, true, 4, true, false, 4, false, -1, 16, 0, true, true, true, true>, 2, 4, "u2_w4_c_sc1_ring_xpf_dyn", false, true, true, true},
-    {rx_offload_kernel<2, true, 4, true, false, 4, false, -1, 0, 0, true, true, true, true>, 2, 4, "u2_w4_c_ring_xpf_dyn", false, true, true, true},
 #ifdef NICGPU_TUNING
     // candidates and earlier production kernels, timed by tools/tune_rx.py.
     // 8-wave blocks measure the same on C2/IMIX/64 B and 12% slower on 9000 B,
@@ -1678,7 +1581,6 @@ const RxVariant kRxVariants[] = {
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
 constexpr int kRxW8 = 2;
-constexpr int kRxDyn = 3;  // variants 0 / 1 dealt by counters: 3 / 4
 constexpr uint64_t kRxW8Tiles = 32768;  // 2 M packets: IMIX and 64-B batches of C3's size, not C2 (16 K tiles)
 
 // ------------------------------------------------------ segment gather --
@@ -2377,11 +2279,7 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
 // every descriptor's span.  One lane owns one packet at a time and walks it
 // to the end of a 128-B line per step (up to 8 x 16-B loads); a finished lane
 // takes the next packet of its wave's range through a ballot (a wave-level
-// work queue), so IMIX lengths do not leave lanes idle.  Every 16-B chunk goes
-// through the CRC register whole: bytes before the packet (its first chunk)
-// and past the span (its last) are zeroed, the state enters at byte 0 of the
-// first chunk (kCrcLead), and the k zero bytes the last chunk appends are
-// taken back once per packet by G_k = x^(-8k) (kCrcUnshift).
+// work queue), so IMIX lengths do not leave lanes idle.
 struct Crc32cTables {
   uint32_t t[16][256];
 };
@@ -2437,226 +2335,11 @@ constexpr int kIcrcRing = 128;  // descriptor ring per wave (LDS)
 
 constexpr int kIcrcWpb = 16;  // waves per block: one 1024-thread block per CU shares the table image
 constexpr int kIcrcThreads = kWave * kIcrcWpb;
-constexpr uint32_t kNibPairBytes = 4096u;            // two nibble positions: 16 rows of 256 B
-constexpr uint32_t kNibBytes = 16u * kNibPairBytes;  // the 32 nibble positions of a 16-B chunk: 64 KiB
-constexpr uint32_t kUnshiftWords = 16u * 8u * 16u;   // G_k, k = 0..15: 8 nibbles x 16 values
-
-// G_k = x^(-8k) mod P in the reflected register: undoes k trailing zero bytes
-// (the zero-byte step S -> (S >> 8) ^ T0[S & 0xFF] is linear and invertible:
-// the top byte of T0[k] is a permutation of k).  Gt[k][j][v] = G_k(v << 4j).
-struct CrcUnshift {
-  uint32_t g[16][8][16];
-};
-constexpr CrcUnshift make_crc_unshift() {
-  const Crc32cTables T = make_crc32c_tables();
-  uint32_t top_inv[256] = {};
-  for (uint32_t k = 0; k < 256; ++k) top_inv[T.t[0][k] >> 24] = k;
-  CrcUnshift G{};
-  for (int j = 0; j < 8; ++j)
-    for (uint32_t v = 0; v < 16; ++v) {
-      uint32_t s = v << (4 * j);
-      for (int k = 0; k < 16; ++k) {
-        G.g[k][j][v] = s;
-        const uint32_t b = top_inv[s >> 24];
-        s = ((s ^ T.t[0][b]) << 8) | b;
-      }
-    }
-  return G;
-}
-__constant__ CrcUnshift kCrcUnshift = make_crc_unshift();
-
-// One 16-B chunk through the CRC register from state S: the chunk x (bytes
-// outside the packet already zeroed) with S xored into its first 4 bytes, then
-// slice-by-16 by NIBBLES from a zero state: nibble h of byte i contributes
-// T_{15-i}[v << 4h].  Every nibble table is stored 32 times, copy c in LDS bank
-// c only, and lane l reads copy l % 32, so the 32 lanes of a ds_read_b32 lane
-// group hit 32 distinct banks: the 32 lookups per chunk never conflict (byte
-// tables put 3-4 lanes of a group on one bank).  Row v of a table is 256 B
-// apart, so a lookup address is {copy byte, nibble byte, 0, 0} — one
-// v_perm_b32 from the chunk's nibble bytes (x & 0x0F0F0F0F and
-// (x >> 4) & 0x0F0F0F0F) and the lane's copy byte — plus an immediate (two
-// positions share a 4-KiB block: the second at +128 B).
+// a ^ b ^ c in one VALU op (hipcc folds table words one v_xor_b32 at a time)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  // hipcc folds table words in one v_xor_b32 (and one lgkmcnt wait) at a
-  // time; v_bitop3_b32 0x96 is a ^ b ^ c
   uint32_t d;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
   return d;
-}
-
-// The 8 table words of dword W (0..3) of a chunk.
-template <int W>
-__device__ __forceinline__ void crc_dword_words(const uint8_t* __restrict__ Tn, uint32_t x, uint32_t cb, uint32_t* t) {
-  const uint32_t y = x & 0x0F0F0F0Fu, z = (x >> 4) & 0x0F0F0F0Fu;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t sel = 0x0C0C0004u | ((uint32_t) k << 8);
-    const uint32_t off = (uint32_t) (4 * W + k) * kNibPairBytes;
-    t[2 * k] = *reinterpret_cast<const uint32_t*>(Tn + __builtin_amdgcn_perm(cb, y, sel) + off);
-    t[2 * k + 1] = *reinterpret_cast<const uint32_t*>(Tn + __builtin_amdgcn_perm(cb, z, sel) + off + 128u);
-  }
-}
-
-template <int W>
-__device__ __forceinline__ uint32_t crc_dword_nib(const uint8_t* __restrict__ Tn, uint32_t x, uint32_t cb) {
-  uint32_t t[8];
-  crc_dword_words<W>(Tn, x, cb, t);
-  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
-}
-
-// Dwords 1..3 of a chunk: 24 lookups, independent of the CRC state.
-__device__ __forceinline__ uint32_t crc_chunk_part(const uint8_t* __restrict__ Tn, uint32_t x1, uint32_t x2,
-                                                   uint32_t x3, uint32_t cb) {
-  uint32_t t[24];
-  crc_dword_words<1>(Tn, x1, cb, t);
-  crc_dword_words<2>(Tn, x2, cb, t + 8);
-  crc_dword_words<3>(Tn, x3, cb, t + 16);
-  const uint32_t a = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), xor3(t[6], t[7], t[8]));
-  const uint32_t b = xor3(xor3(t[9], t[10], t[11]), xor3(t[12], t[13], t[14]), xor3(t[15], t[16], t[17]));
-  const uint32_t c = xor3(xor3(t[18], t[19], t[20]), t[21], xor3(t[22], t[23], 0u));
-  return xor3(a, b, c);
-}
-
-__global__ __launch_bounds__(kIcrcThreads) void icrc_kernel(IcrcParams P) {
-  __shared__ __attribute__((aligned(16))) uint8_t Tn[kNibBytes];
-  __shared__ uint32_t Gt[kUnshiftWords];
-  __shared__ uint64_t ring_all[kIcrcWpb][kIcrcRing];
-  __shared__ uint4 masks[kMaskEntries];
-  __shared__ uint32_t lead_s[16];
-  if (threadIdx.x < 16u) lead_s[threadIdx.x] = kCrcLead.s[threadIdx.x];
-  for (uint32_t q = threadIdx.x; q < kNibBytes / 16u; q += kIcrcThreads) {
-    const uint32_t o = q * 16u;
-    const uint32_t pair = o >> 12, v = (o >> 8) & 15u, half = (o >> 7) & 1u;  // byte `pair`, nibble `half`
-    const uint32_t val = kCrc32c.t[15u - pair][half ? v << 4 : v];
-    reinterpret_cast<uint4*>(Tn)[q] = make_uint4(val, val, val, val);
-  }
-  for (uint32_t i = threadIdx.x; i < kUnshiftWords; i += kIcrcThreads) Gt[i] = (&kCrcUnshift.g[0][0][0])[i];
-  for (uint32_t i = threadIdx.x; i < kMaskEntries; i += kIcrcThreads) {
-    const int lo = i < 16u ? (int) i : 0, hi = i < 16u ? 16 : (int) i - 16;
-    masks[i] = make_uint4(dword_keep(lo, hi, 0), dword_keep(lo, hi, 1), dword_keep(lo, hi, 2), dword_keep(lo, hi, 3));
-  }
-  __syncthreads();
-  const uint32_t lane = lane_id();
-  const uint32_t cb = (lane & 31u) << 2;  // this lane's copy: bank lane % 32
-  uint64_t* ring = ring_all[threadIdx.x / kWave];
-  const uint64_t nwaves = (uint64_t) gridDim.x * kIcrcWpb;
-  const uint64_t wave = (uint64_t) blockIdx.x * kIcrcWpb + threadIdx.x / kWave;
-  // contiguous packet range of this wave
-  const uint64_t per = (P.n + nwaves - 1) / nwaves;
-  const uint64_t p0 = wave * per < P.n ? wave * per : P.n;
-  const uint64_t p1 = p0 + per < P.n ? p0 + per : P.n;
-  const u32x4* f16 = reinterpret_cast<const u32x4*>(P.frames);
-
-  uint64_t loaded = p0;
-  auto refill = [&]() __attribute__((always_inline)) {
-    const uint64_t i = loaded + lane;
-    ring[i & (kIcrcRing - 1)] = i < p1 ? P.desc[i] : 0ull;
-    loaded += kWave;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  };
-  refill();
-  refill();
-  uint64_t next = p0 + kWave;
-  uint64_t my = p0 + lane;
-  // per lane: the packet's first 16-B chunk and 32-bit byte positions
-  // relative to it (frames are < 64 KiB)
-  uint64_t c16 = 0;
-  uint32_t pos = 0, end = 0, len = 0, lb = 0, kz = 0, S = 0xFFFFFFFFu;
-  auto setup = [&]() __attribute__((always_inline)) {
-    const uint64_t d = ring[my & (kIcrcRing - 1)];
-    const uint64_t off = d & kOffMask;
-    len = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
-    const uint32_t span = P.verify ? (len >= 4u ? len - 4u : 0u) : len;
-    c16 = off >> 4;
-    lb = (uint32_t) c16 & 7u;  // chunk of the 128-B line the packet starts in
-    pos = (uint32_t) off & 15u;
-    end = pos + span;
-    // the state that pos zero bytes take to 0xFFFFFFFF, entered at byte 0 of
-    // the first chunk with the pos leading bytes zeroed; an empty span
-    // processes no chunk.  kz: zero bytes after the span in its last chunk.
-    S = span ? lead_s[pos] : 0xFFFFFFFFu;
-    kz = span ? (16u - (end & 15u)) & 15u : 0u;
-  };
-  if (my < p1) setup();
-  for (;;) {
-    const bool active = my < p1;
-    if (__ballot(active) == 0ull) break;
-    if (active) {
-      // up to the end of the current 128-B line (8 chunks), so a lane reads
-      // every line once; loads clamped to the line and the span's end
-      const uint32_t c0 = pos >> 4;
-      const uint32_t clast = end > pos ? (end - 1u) >> 4 : c0;
-      const uint32_t ce = ((lb + c0) | 7u) - lb;  // last chunk of c0's line
-      const uint32_t cl = ce < clast ? ce : clast;
-      const uint32_t nproc = end > pos ? cl - c0 + 1u : 0u;  // chunks this step
-      u32x4 v[8];  // unread chunks are never processed (u >= nproc)
-      if (nproc) {  // an empty span reads nothing (it may sit at the buffer's end)
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = f16[c16 + (c0 + (uint32_t) u <= cl ? c0 + (uint32_t) u : cl)];
-      }
-      // every chunk processed whole: bytes before the packet (its first
-      // chunk) and past the span (its last) zeroed, so the last chunk adds
-      // trailing zero bytes that G_k takes back at the end
-      const int32_t er = (int32_t) (end - (c0 << 4));  // span end from c0's base
-      const uint4 m0 = masks[pos & 15u];
-      uint32_t part[8];
-      uint32_t x0[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int32_t r = er - 16 * u;
-        const uint4 mt = masks[16 + (r < 0 ? 0 : (r > 16 ? 16 : r))];
-        uint4 m = mt;
-        if (u == 0) {
-          m.x &= m0.x;
-          m.y &= m0.y;
-          m.z &= m0.z;
-          m.w &= m0.w;
-        }
-        x0[u] = v[u].x & m.x;
-#ifndef NICGPU_ICRC_MEMONLY
-        part[u] = crc_chunk_part(Tn, v[u].y & m.y, v[u].z & m.z, v[u].w & m.w, cb);
-#endif
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-#ifdef NICGPU_ICRC_MEMONLY  // timing only: the loads and masks without the table work
-        const uint32_t Sn = (x0[u] ^ S) + v[u].y + v[u].z + v[u].w;
-        (void) part;
-#else
-        const uint32_t Sn = part[u] ^ crc_dword_nib<0>(Tn, x0[u] ^ S, cb);
-#endif
-        S = (uint32_t) u < nproc ? Sn : S;
-      }
-      pos = nproc ? (cl + 1u) << 4 : end;
-    }
-    const bool finished = active && pos >= end;
-    if (finished) {
-      // undo the k trailing zero bytes of the last chunk
-      uint32_t g = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g ^= Gt[kz * 128u + (uint32_t) j * 16u + ((S >> (4 * j)) & 15u)];
-      const uint32_t crc = g ^ 0xFFFFFFFFu;
-      if (P.out_crc) P.out_crc[my] = (P.verify && len < 4u) ? 0u : crc;
-      if (P.verify) {
-        uint32_t ok = 0;
-        if (len >= 4u) {
-          const uint8_t* t = P.frames + (c16 << 4) + end;
-          const uint32_t stored = ((uint32_t) t[0] << 24) | ((uint32_t) t[1] << 16) | ((uint32_t) t[2] << 8) | t[3];
-          ok = stored == crc;
-        }
-        P.out_ok[my] = (uint8_t) ok;
-      }
-    }
-    const uint64_t m = __ballot(finished);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
-    if (finished) my = next + rank;
-    next += (uint64_t) __builtin_popcountll(m);
-    // grabbed entries are in the ring (loaded >= next + 64 before this step);
-    // read them before the refill overwrites the oldest 64 slots
-    if (finished && my < p1) setup();
-    if (next + kWave > loaded && loaded < p1) refill();
-  }
 }
 
 // Byte tables, slice-by-4: one lookup per byte instead of the nibble tables'
@@ -2686,9 +2369,11 @@ __device__ __forceinline__ uint32_t b4_dword(const uint8_t* __restrict__ Tb, uin
   return xor3(t0, t1, t2) ^ t3;
 }
 
-// MODE 0: load a window, then process it; 2: the next window of the same
-// packet is loaded before this one is processed (prefetch); 1: timing only,
-// loads and masks without the table work (results wrong).
+// MODE 0: production; 1: timing only, the loads and masks without the table
+// work (results wrong).  Measured (profiles/r03_icrc_variants.jsonl): the
+// timing-only kernel takes 92% of the production time, so the lane-per-packet
+// line walk, not the table work, bounds this kernel; 4-chunk windows and a
+// prefetch of the packet's next window were slower.
 template <int CH, int MODE>  // CH: chunks per step, to the end of the packet's aligned CH x 16-B window
 __global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t Tb[kB4Bytes];
@@ -2751,8 +2436,6 @@ __global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
     cur = 0;
     S = span ? lead_s[pos] : 0xFFFFFFFFu;
   };
-  u32x4 vn[MODE == 2 ? CH : 1];
-  bool have = false;  // MODE 2: vn holds the window at cur
   if (my < p1) setup();
   for (;;) {
     const bool active = my < p1;
@@ -2766,24 +2449,8 @@ __global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
       const uint32_t cl = ce < clast ? ce : clast;
       const uint32_t lim = ((cl + 1u) << 4 < end4 ? (cl + 1u) << 4 : end4) - cur;  // dwords [0, lim) of the step
       u32x4 v[CH];
-      if (MODE == 2 && have) {
 #pragma unroll
-        for (int u = 0; u < CH; ++u) v[u] = vn[MODE == 2 ? u : 0];
-      } else {
-#pragma unroll
-        for (int u = 0; u < CH; ++u) v[u] = f16[c16 + (c0 + (uint32_t) u <= cl ? c0 + (uint32_t) u : cl)];
-      }
-      if (MODE == 2) {
-        // the packet's next window, in flight while this one is processed
-        const uint32_t n0 = cl + 1u;
-        have = n0 <= clast;
-        if (have) {
-          const uint32_t ne = ((lb + n0) | (uint32_t) (CH - 1)) - lb;
-          const uint32_t nl = ne < clast ? ne : clast;
-#pragma unroll
-          for (int u = 0; u < CH; ++u) vn[MODE == 2 ? u : 0] = f16[c16 + (n0 + (uint32_t) u <= nl ? n0 + (uint32_t) u : nl)];
-        }
-      }
+      for (int u = 0; u < CH; ++u) v[u] = f16[c16 + (c0 + (uint32_t) u <= cl ? c0 + (uint32_t) u : cl)];
       __builtin_amdgcn_sched_barrier(0);  // every load of the step in flight before the chain starts
       const uint4 m0 = lead_m[c0 == 0u ? pos : 0u];
       v[0][0] &= m0.x;
@@ -2840,7 +2507,6 @@ struct DeviceInfo {
   int tso_blocks_per_cu = 0;
   int seg_blocks_per_cu = 0;  // tso_segment_kernel (LDS frame stage)
   int icrc_blocks_per_cu = 0;
-  int icrc_b4_blocks_per_cu = 0;
   // occupancy cache per (variant, dynamic LDS bytes)
   struct Occ { int variant; uint32_t lds; int blocks; };
   std::vector<Occ> occ;
@@ -2867,11 +2533,8 @@ const DeviceInfo& device_info(int dev) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, tso_segment_kernel, kBlock, 0) != hipSuccess || b < 1) b = 1;
   di.seg_blocks_per_cu = b;
   b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, icrc_kernel, kIcrcThreads, 0) != hipSuccess || b < 1) b = 1;
-  di.icrc_blocks_per_cu = b;
-  b = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, icrc_b4_kernel<8, 0>, kIcrcThreads, 0) != hipSuccess || b < 1) b = 1;
-  di.icrc_b4_blocks_per_cu = b;
+  di.icrc_blocks_per_cu = b;
   return di;
 }
 
@@ -2972,7 +2635,6 @@ RingPlan plan_ring(int dev, int variant, uint32_t lds, uint64_t ntiles, const De
   const uint32_t spare = per_block > lds ? per_block - lds : 0u;
   uint64_t r = spare / ((uint32_t) v.wpb * kRingTileBytes);
   if (r > per_wave) r = per_wave;
-  if (v.dyn && r > 64) r = 64;  // slot bases in one VGPR lane each
   if (r < 1) r = 1;
   RingPlan rp;
   rp.hold_r = (uint32_t) r;
@@ -3042,13 +2704,8 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
   if (variant == 0) {
     // many tiles with a hit histogram: 8-wave blocks (what they save is half
     // the end-of-block histogram flushes; the ring flushes mid-stream: sc1)
-    // NICGPU_RX_DYN=1: variants 0 / 1 with tiles dealt by counters (A/B)
-    static const bool dyn = [] {
-      const char* e = std::getenv("NICGPU_RX_DYN");
-      return e && e[0] == '1';
-    }();
     if (ntiles >= kRxW8Tiles && hist_n) variant = kRxW8;
-    else variant = (plan_ring(dev, 0, lds_of(0), ntiles, di).holds_all ? 1 : 0) + (dyn ? kRxDyn : 0);
+    else variant = plan_ring(dev, 0, lds_of(0), ntiles, di).holds_all ? 1 : 0;
   }
   const RxVariant& v = kRxVariants[variant];
   const uint32_t lds = lds_of(variant);
@@ -3058,10 +2715,6 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
   int bpc = rx_blocks_per_cu(dev, variant, lds);
   RxParams Pl = P;
   Pl.xpf_chunks = v.xpf ? g_xpf_chunks : 0u;
-  if (v.dyn) {
-    static std::atomic<uint32_t> next_slot{0};
-    Pl.dyn_slot = next_slot.fetch_add(1u, std::memory_order_relaxed) % kDynSlots;
-  }
   uint32_t lds_launch = lds;
   if (v.ring) {
     const RingPlan rp = plan_ring(dev, variant, lds, ntiles, di);
@@ -3425,30 +3078,16 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
   IcrcParams P{frames, desc, n, mode == NICGPU_ICRC_VERIFY, out_crc, out_ok};
   // every resident wave slot busy (a wave's range is then >= 64 packets, one
   // work-queue refill); ranges of 8 packets per lane left 3/4 of the slots idle
-  // NICGPU_ICRC=nib: the nibble-table kernel (A/B); default: byte tables
-  // NICGPU_ICRC=b4w4: byte tables, 4-chunk steps
-  static const int var = [] {
+  // NICGPU_ICRC=b4mem: timing only, the loads without the table work (results wrong)
+  static const bool memonly = [] {
     const char* e = std::getenv("NICGPU_ICRC");
-    if (!e) return 0;
-    const char* names[] = {"b4", "nib", "b4w4", "b4mem", "b4pf", "b4w4pf"};
-    for (int i = 0; i < 6; ++i)
-      if (std::strcmp(e, names[i]) == 0) return i;
-    return 0;
+    return e && std::strcmp(e, "b4mem") == 0;
   }();
-  const bool nib = var == 1;
   const uint64_t want = (n + kIcrcThreads - 1) / kIcrcThreads;
-  const uint64_t cap = (uint64_t) di->cus * (uint64_t) (nib ? di->icrc_blocks_per_cu : di->icrc_b4_blocks_per_cu);
+  const uint64_t cap = (uint64_t) di->cus * (uint64_t) di->icrc_blocks_per_cu;
   const unsigned grid = (unsigned) (want < 1 ? 1 : (want < cap ? want : cap));
-  if (nib)
-    hipLaunchKernelGGL(icrc_kernel, dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
-  else if (var == 2)
-    hipLaunchKernelGGL((icrc_b4_kernel<4, 0>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
-  else if (var == 3)
+  if (memonly)
     hipLaunchKernelGGL((icrc_b4_kernel<8, 1>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
-  else if (var == 4)
-    hipLaunchKernelGGL((icrc_b4_kernel<8, 2>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
-  else if (var == 5)
-    hipLaunchKernelGGL((icrc_b4_kernel<4, 2>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
   else
     hipLaunchKernelGGL((icrc_b4_kernel<8, 0>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
   return hip_status(hipGetLastError());
