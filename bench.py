@@ -277,6 +277,27 @@ def load_traffic(path):
     return prof.get("hbm_bytes_per_launch"), info
 
 
+def load_rows_traffic(path):
+    """Per-row HBM traffic from a committed rows profile (tools/rows_prof_summary.py:
+    FETCH_SIZE calibrated per access shape), with the kernel source it measured;
+    a profile of another source is reported as stale, never silently."""
+    import hashlib
+
+    try:
+        with open(path) as f:
+            prof = json.load(f)
+    except (OSError, ValueError):
+        return {"profile": os.path.relpath(path, ROOT), "error": "unreadable"}
+    with open(os.path.join(ROOT, "smart_nic_amd", "csrc", "nicgpu.hip"), "rb") as f:
+        cur = hashlib.sha256(f.read()).hexdigest()[:16]
+    rec = prof.get("kernel_source_sha256")
+    keep = ("rocprof_avg_us", "access_shape", "fetch_factor", "hbm_bytes_per_launch", "traffic_over_alg",
+            "fetch_bytes_per_packet", "fetch_over_same_shape_min", "frac_of_8TBps_rocprof")
+    rows = {r["row"]: {k: r[k] for k in keep if k in r} for r in prof.get("rows", [])}
+    return {"profile": os.path.relpath(path, ROOT), "measured_in_this_run": False, "profile_kernel_source": rec,
+            "current_kernel_source": cur, "stale": rec is None or rec != cur, "rows": rows}
+
+
 WORKLOAD_TEXT = {
     "c2": "C2: 1M x 1518 B TCP per GPU, checksum verify + RSS (MS 40-B key, 128-entry table i%4, IPv4 4-tuple)",
     "c3": "C3: IMIX 64/576/1518 B at 7:4:1, 4M packets per GPU (job batch byte-sharded), checksum verify + RSS "
@@ -300,7 +321,8 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="take the multi-rank path (RCCL init, key/table broadcast, barriers, max-reduce) even at "
                          "world size 1, to exercise it on a one-GPU box")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02zz_pmc_c2.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03a_pmc_c2.json"))
+    ap.add_argument("--rows-prof-json", default=os.path.join(ROOT, "profiles", "r03_rows_prof.json"))
     args = ap.parse_args()
 
     import torch
@@ -461,6 +483,7 @@ def main():
         out["gpu_rows"], errors = gpu_rows()
         if errors:
             out["gpu_rows_errors"] = errors
+        out["gpu_rows_traffic"] = load_rows_traffic(args.rows_prof_json)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(frames, desc, table, (g_cs, g_q), n_sample_1=min(n, 1 << 16),
                                            label=args.workload.upper())

@@ -8,6 +8,7 @@ R=$GRAFT_REPO_ROOT
 TAG=${TAG:-r02r}
 O=$R/gpurun_out/rows_prof
 mkdir -p $O
+sha256sum $R/smart_nic_amd/csrc/nicgpu.hip > $O/kernel_source.sha
 g++ -std=c++20 -O2 -I$R/include $R/tools/bench_rx_stage.cpp -L$R/smart_nic_amd -lnic_host -lnicgpu \
     -Wl,-rpath,"$R/smart_nic_amd" -o $O/bench_rx_stage || exit 1
 cd /tmp && export TMPDIR=/tmp
@@ -19,5 +20,8 @@ for row in ${ROWS:-rx_c2 rx_c3 rx_u64 rx_l34_c2 rss_c2 rss_c3 icrc_c2 icrc_c3 ts
   echo "row $row done"
 done
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_f1 -o $TAG -- $O/bench_rx_stage c3 1048576 12 0 device device pipelined device > $O/f1.json 2> $O/kt_f1.err || { echo "kt f1 failed"; tail -5 $O/kt_f1.err; exit 1; }
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d $O/${c}_f1 -o $TAG -- $O/bench_rx_stage c3 1048576 4 0 device device pipelined device > /dev/null 2> $O/${c}_f1.err || { echo "pmc $c f1 failed"; tail -5 $O/${c}_f1.err; exit 1; }
+done
 cat $O/f1.json
 echo done

@@ -1784,7 +1784,7 @@ constexpr int kDlvReserveCus = NICGPU_DLV_RESERVE;  // default of NICGPU_DLV_RES
 constexpr int kDlvWpb = NICGPU_DLV_WPB;  // waves per block
 constexpr int kDlvU = NICGPU_DLV_U;      // 64-entry sub-steps per step (loads in flight per lane)
 constexpr uint32_t kDlvRec = 24;  // item record: dst u64 | src (or prefix word) u64 | len u32 | first entry u32
-constexpr uint32_t kDlvMarks = 4u * kWave * kDlvU;  // bytes
+constexpr uint32_t kDlvMarks = (kWave * kDlvU + 15u) & ~15u;  // bytes: one u8 mark per stream entry (item id + 1 <= 192)
 constexpr uint32_t kDlvWaveBytes = kDlvMarks + 64u * 8u + 192u * kDlvRec + 64u * kHdrStride * 16u;  // marks|wdst|items|stage
 
 // block part: RSS LUT | histogram | table (as rss_only_kernel), then 16 B for the Success count
@@ -1835,7 +1835,7 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
                                                table_lds ? (R.table_n + 1u) / 2u : 0u);
   uint32_t* cnt_s = reinterpret_cast<uint32_t*>(base_b + block_bytes - 16u);
   uint8_t* wave_b = base_b + block_bytes + w * kDlvWaveBytes;
-  uint32_t* marks = reinterpret_cast<uint32_t*>(wave_b);
+  uint8_t* marks = wave_b;
   uint64_t* wdst = reinterpret_cast<uint64_t*>(wave_b + kDlvMarks);
   uint8_t* items = wave_b + kDlvMarks + 512u;
   uint4* stage = reinterpret_cast<uint4*>(items + 192u * kDlvRec);
@@ -1901,9 +1901,9 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       constexpr uint32_t kSpan = kWave * kDlvU;
-      if (c0 && F >= W && F - W < kSpan) marks[F - W] = lane * 3u + 1u;
-      if (c1 && F + c0 >= W && F + c0 - W < kSpan) marks[F + c0 - W] = lane * 3u + 2u;
-      if (c2 && F + c0 + c1 >= W && F + c0 + c1 - W < kSpan) marks[F + c0 + c1 - W] = lane * 3u + 3u;
+      if (c0 && F >= W && F - W < kSpan) marks[F - W] = (uint8_t) (lane * 3u + 1u);
+      if (c1 && F + c0 >= W && F + c0 - W < kSpan) marks[F + c0 - W] = (uint8_t) (lane * 3u + 2u);
+      if (c2 && F + c0 + c1 >= W && F + c0 + c1 - W < kSpan) marks[F + c0 + c1 - W] = (uint8_t) (lane * 3u + 3u);
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       uint32_t itv[kDlvU];
@@ -1914,15 +1914,21 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
         carry = (uint32_t) __builtin_amdgcn_readlane((int) it, 63);
         itv[u] = it;
       }
-      // phase A: every entry's chunk, item and source window; loads issued
-      uint64_t Dv[kDlvU], lov[kDlvU], hiv[kDlvU], dv[kDlvU], pwv[kDlvU];
-      uint32_t vv[kDlvU][5], shv[kDlvU], idv[kDlvU];
+      // phase A: every entry's chunk, item and source window; loads issued.
+      // Per entry: the destination chunk, one packed word (bytes [lo, hi) of
+      // the chunk, source shift, owning write) and five source dwords — a
+      // prefix item's 4 bytes are placed into them here — so that kDlvU
+      // entries' loads fit in flight per lane.
+      uint64_t Dc[kDlvU];  // destination chunk index; ~0: no entry
+      uint32_t pk[kDlvU];  // lo - D (bits 0-4) | hi - D (8-12) | shift (16-17) | write q (20-25)
+      uint32_t vv[kDlvU][5];
 #pragma unroll
       for (int u = 0; u < kDlvU; ++u) {
         const uint32_t pos = W + (uint32_t) u * kWave + lane;
-        idv[u] = pos < total_e ? itv[u] - 1u : 0xFFFFFFFFu;
-        Dv[u] = lov[u] = hiv[u] = dv[u] = pwv[u] = 0;
-        shv[u] = 0;
+        Dc[u] = ~0ull;
+        pk[u] = 0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) vv[u][i] = 0;
         if (pos < total_e) {
           const uint32_t id = itv[u] - 1u, q = id / 3u, k = id - 3u * q;
           const uint8_t* r = items + id * kDlvRec;
@@ -1931,18 +1937,28 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
           const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
           const uint32_t first = *reinterpret_cast<const uint32_t*>(r + 20);
           const uint64_t D = ((d >> 4) + (pos - first)) << 4;
-          Dv[u] = D;
-          dv[u] = d;
-          lov[u] = D > d ? D : d;
-          hiv[u] = D + 16 < d + len ? D + 16 : d + len;
+          const uint64_t lo = D > d ? D : d;
+          const uint64_t hi = D + 16 < d + len ? D + 16 : d + len;
+          Dc[u] = D >> 4;
+          pk[u] = (uint32_t) (lo - D) | ((uint32_t) (hi - D) << 8) | (q << 20);
           if (k == 0) {
-            pwv[u] = src & 0xFFFFFFFFull;  // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): 4 bytes at d
+            // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): its 4 bytes at d
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              uint32_t v = 0;
+#pragma unroll
+              for (int bb = 0; bb < 4; ++bb) {
+                const int64_t rel = (int64_t) (D + 4u * i + bb) - (int64_t) d;
+                if (rel >= 0 && rel < 4) v |= (uint32_t) ((src >> (8 * rel)) & 0xFFu) << (8 * bb);
+              }
+              vv[u][i] = v;
+            }
           } else {
             // source of destination byte D: before the item's source by up to
             // 15 bytes on its first chunk, so possibly below address 0 (signed)
             const int64_t a = (int64_t) D + ((int64_t) src - (int64_t) d);
             const int64_t a4 = a & ~(int64_t) 3;
-            shv[u] = (uint32_t) (a & 3) | 4u;  // bit 2: a source window (not the prefix)
+            pk[u] |= (uint32_t) (a & 3) << 16;
             if (a4 >= 0 && (uint64_t) a4 + 20 <= P.mem_size) {
               __builtin_memcpy(vv[u], P.mem + a4, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
               // the fifth dword only for a shifted window (equal alignment of
@@ -1966,30 +1982,17 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
       // phase B: align, store, and the header stage of Success frames
 #pragma unroll
       for (int u = 0; u < kDlvU; ++u) {
-        if (idv[u] == 0xFFFFFFFFu) continue;
-        const uint64_t D = Dv[u], lo = lov[u], hi = hiv[u];
+        if (Dc[u] == ~0ull) continue;
+        const uint64_t D = Dc[u] << 4, lo = D + (pk[u] & 31u), hi = D + ((pk[u] >> 8) & 31u);
+        const uint32_t sh = (pk[u] >> 16) & 3u;
         uint32_t o[4];
-        if (shv[u] & 4u) {
-          const uint32_t sh = shv[u] & 3u;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) o[i] = sh ? __builtin_amdgcn_alignbyte(vv[u][i + 1], vv[u][i], sh) : vv[u][i];
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb) {
-              const int64_t rel = (int64_t) (D + 4u * i + bb) - (int64_t) dv[u];
-              if (rel >= 0 && rel < 4) v |= (uint32_t) ((pwv[u] >> (8 * rel)) & 0xFFu) << (8 * bb);
-            }
-            o[i] = v;
-          }
-        }
+        for (int i = 0; i < 4; ++i) o[i] = sh ? __builtin_amdgcn_alignbyte(vv[u][i + 1], vv[u][i], sh) : vv[u][i];
         dlv_store(P.mem, D, lo, hi, o);
         if (RSS) {
-          const uint32_t q = idv[u] / 3u;
+          const uint32_t q = pk[u] >> 20;
           const uint64_t wd = wdst[q];
-          const uint64_t kc = (D >> 4) - (wd & ~(1ull << 63));
+          const uint64_t kc = Dc[u] - (wd & ~(1ull << 63));
           if ((wd >> 63) && kc < (uint64_t) kHdrChunks) {
             uint32_t* st = reinterpret_cast<uint32_t*>(stage + hdr_slot(q, (uint32_t) kc));
 #pragma unroll
@@ -2440,17 +2443,57 @@ __global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
   for (;;) {
     const bool active = my < p1;
     if (__ballot(active) == 0ull) break;
-    if (active && cur < end4) {
-      // up to the end of the current CH-chunk window; every chunk of the
-      // step is processed (predicated on the dword being below lim), so all
-      // CH loads issue before the first is used
-      const uint32_t c0 = cur >> 4, clast = (end4 - 1u) >> 4;
-      const uint32_t ce = ((lb + c0) | (uint32_t) (CH - 1)) - lb;
-      const uint32_t cl = ce < clast ? ce : clast;
-      const uint32_t lim = ((cl + 1u) << 4 < end4 ? (cl + 1u) << 4 : end4) - cur;  // dwords [0, lim) of the step
-      u32x4 v[CH];
+    const bool work = active && cur < end4;
+    // up to the end of the current CH-chunk window; every chunk of the step
+    // is processed (predicated on the dword being below lim), so all CH loads
+    // issue before the first is used
+    const uint32_t c0 = cur >> 4, clast = work ? (end4 - 1u) >> 4 : c0;
+    const uint32_t ce = ((lb + c0) | (uint32_t) (CH - 1)) - lb;
+    const uint32_t cl = ce < clast ? ce : clast;
+    const uint32_t lim = ((cl + 1u) << 4 < end4 ? (cl + 1u) << 4 : end4) - cur;  // dwords [0, lim) of the step
+    u32x4 v[CH];
+    if constexpr (MODE == 2) {
+      // Coalesced loads: lane m loads chunk m % 2 of the 32-B window of lane
+      // 32u + m / 2 (every 16 lanes read 8 whole windows: 256 contiguous
+      // bytes where the packets are back to back), then each lane takes its
+      // window's two chunks back with ds_bpermute.  Lanes without a window
+      // publish none, and a window's second chunk is read only inside it.
+      static_assert(CH == 2, "pairs");
+      // the aligned pair holding chunk c0, as an absolute chunk index (c0 is
+      // the pair's second chunk when c16 + c0 is odd: the first is then not
+      // the packet's and is not read); bit k: chunk k of the pair is read
+      const bool odd = ((lb + c0) & 1u) != 0u;
+      const uint64_t P0 = c16 + c0 - (odd ? 1u : 0u);
+      const uint64_t need = (odd ? 0u : 1u) | ((odd || cl > c0) ? 2u : 0u);
+      const uint64_t pub = work ? ((P0 << 2) | need) : 0ull;
+      u32x4 R[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int src = (int) ((32u * (uint32_t) u + (lane >> 1)) << 2);
+        const uint64_t pw = ((uint64_t) (uint32_t) __builtin_amdgcn_ds_bpermute(src, (int) (uint32_t) (pub >> 32)) << 32) |
+                            (uint32_t) __builtin_amdgcn_ds_bpermute(src, (int) (uint32_t) pub);
+        const uint32_t k = lane & 1u;
+        R[u] = u32x4{0u, 0u, 0u, 0u};
+        if ((pw >> k) & 1u) R[u] = f16[(pw >> 2) + k];
+      }
+      u32x4 T[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int src = (int) ((2u * (lane & 31u) + (uint32_t) k) << 2);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t a = (uint32_t) __builtin_amdgcn_ds_bpermute(src, (int) R[0][d]);
+          const uint32_t b = (uint32_t) __builtin_amdgcn_ds_bpermute(src, (int) R[1][d]);
+          T[k][d] = lane < 32u ? a : b;
+        }
+      }
+      v[0] = odd ? T[1] : T[0];
+      v[1] = T[1];
+    } else if (work) {
 #pragma unroll
       for (int u = 0; u < CH; ++u) v[u] = f16[c16 + (c0 + (uint32_t) u <= cl ? c0 + (uint32_t) u : cl)];
+    }
+    if (work) {
       __builtin_amdgcn_sched_barrier(0);  // every load of the step in flight before the chain starts
       const uint4 m0 = lead_m[c0 == 0u ? pos : 0u];
       v[0][0] &= m0.x;
@@ -3078,16 +3121,19 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
   IcrcParams P{frames, desc, n, mode == NICGPU_ICRC_VERIFY, out_crc, out_ok};
   // every resident wave slot busy (a wave's range is then >= 64 packets, one
   // work-queue refill); ranges of 8 packets per lane left 3/4 of the slots idle
-  // NICGPU_ICRC=b4mem: timing only, the loads without the table work (results wrong)
-  static const bool memonly = [] {
+  // NICGPU_ICRC=b4mem: timing only, the loads without the table work
+  // (results wrong); b4tp: 32-B windows loaded coalesced and transposed
+  static const int var = [] {
     const char* e = std::getenv("NICGPU_ICRC");
-    return e && std::strcmp(e, "b4mem") == 0;
+    return !e ? 0 : std::strcmp(e, "b4mem") == 0 ? 1 : std::strcmp(e, "b4tp") == 0 ? 2 : 0;
   }();
   const uint64_t want = (n + kIcrcThreads - 1) / kIcrcThreads;
   const uint64_t cap = (uint64_t) di->cus * (uint64_t) di->icrc_blocks_per_cu;
   const unsigned grid = (unsigned) (want < 1 ? 1 : (want < cap ? want : cap));
-  if (memonly)
+  if (var == 1)
     hipLaunchKernelGGL((icrc_b4_kernel<8, 1>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
+  else if (var == 2)
+    hipLaunchKernelGGL((icrc_b4_kernel<2, 2>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
   else
     hipLaunchKernelGGL((icrc_b4_kernel<8, 0>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
   return hip_status(hipGetLastError());
