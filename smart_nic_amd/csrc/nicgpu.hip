@@ -2375,8 +2375,9 @@ __device__ __forceinline__ uint32_t b4_dword(const uint8_t* __restrict__ Tb, uin
 // MODE 0: production; 1: timing only, the loads and masks without the table
 // work (results wrong).  Measured (profiles/r03_icrc_variants.jsonl): the
 // timing-only kernel takes 92% of the production time, so the lane-per-packet
-// line walk, not the table work, bounds this kernel; 4-chunk windows and a
-// prefetch of the packet's next window were slower.
+// line walk, not the table work, bounds this kernel; 4-chunk windows, a
+// prefetch of the packet's next window, and 32-B windows loaded coalesced and
+// transposed back with ds_bpermute were all slower.
 template <int CH, int MODE>  // CH: chunks per step, to the end of the packet's aligned CH x 16-B window
 __global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t Tb[kB4Bytes];
@@ -2443,57 +2444,17 @@ __global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
   for (;;) {
     const bool active = my < p1;
     if (__ballot(active) == 0ull) break;
-    const bool work = active && cur < end4;
-    // up to the end of the current CH-chunk window; every chunk of the step
-    // is processed (predicated on the dword being below lim), so all CH loads
-    // issue before the first is used
-    const uint32_t c0 = cur >> 4, clast = work ? (end4 - 1u) >> 4 : c0;
-    const uint32_t ce = ((lb + c0) | (uint32_t) (CH - 1)) - lb;
-    const uint32_t cl = ce < clast ? ce : clast;
-    const uint32_t lim = ((cl + 1u) << 4 < end4 ? (cl + 1u) << 4 : end4) - cur;  // dwords [0, lim) of the step
-    u32x4 v[CH];
-    if constexpr (MODE == 2) {
-      // Coalesced loads: lane m loads chunk m % 2 of the 32-B window of lane
-      // 32u + m / 2 (every 16 lanes read 8 whole windows: 256 contiguous
-      // bytes where the packets are back to back), then each lane takes its
-      // window's two chunks back with ds_bpermute.  Lanes without a window
-      // publish none, and a window's second chunk is read only inside it.
-      static_assert(CH == 2, "pairs");
-      // the aligned pair holding chunk c0, as an absolute chunk index (c0 is
-      // the pair's second chunk when c16 + c0 is odd: the first is then not
-      // the packet's and is not read); bit k: chunk k of the pair is read
-      const bool odd = ((lb + c0) & 1u) != 0u;
-      const uint64_t P0 = c16 + c0 - (odd ? 1u : 0u);
-      const uint64_t need = (odd ? 0u : 1u) | ((odd || cl > c0) ? 2u : 0u);
-      const uint64_t pub = work ? ((P0 << 2) | need) : 0ull;
-      u32x4 R[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int src = (int) ((32u * (uint32_t) u + (lane >> 1)) << 2);
-        const uint64_t pw = ((uint64_t) (uint32_t) __builtin_amdgcn_ds_bpermute(src, (int) (uint32_t) (pub >> 32)) << 32) |
-                            (uint32_t) __builtin_amdgcn_ds_bpermute(src, (int) (uint32_t) pub);
-        const uint32_t k = lane & 1u;
-        R[u] = u32x4{0u, 0u, 0u, 0u};
-        if ((pw >> k) & 1u) R[u] = f16[(pw >> 2) + k];
-      }
-      u32x4 T[2];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int src = (int) ((2u * (lane & 31u) + (uint32_t) k) << 2);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const uint32_t a = (uint32_t) __builtin_amdgcn_ds_bpermute(src, (int) R[0][d]);
-          const uint32_t b = (uint32_t) __builtin_amdgcn_ds_bpermute(src, (int) R[1][d]);
-          T[k][d] = lane < 32u ? a : b;
-        }
-      }
-      v[0] = odd ? T[1] : T[0];
-      v[1] = T[1];
-    } else if (work) {
+    if (active && cur < end4) {
+      // up to the end of the current CH-chunk window; every chunk of the
+      // step is processed (predicated on the dword being below lim), so all
+      // CH loads issue before the first is used
+      const uint32_t c0 = cur >> 4, clast = (end4 - 1u) >> 4;
+      const uint32_t ce = ((lb + c0) | (uint32_t) (CH - 1)) - lb;
+      const uint32_t cl = ce < clast ? ce : clast;
+      const uint32_t lim = ((cl + 1u) << 4 < end4 ? (cl + 1u) << 4 : end4) - cur;  // dwords [0, lim) of the step
+      u32x4 v[CH];
 #pragma unroll
       for (int u = 0; u < CH; ++u) v[u] = f16[c16 + (c0 + (uint32_t) u <= cl ? c0 + (uint32_t) u : cl)];
-    }
-    if (work) {
       __builtin_amdgcn_sched_barrier(0);  // every load of the step in flight before the chain starts
       const uint4 m0 = lead_m[c0 == 0u ? pos : 0u];
       v[0][0] &= m0.x;
@@ -3121,19 +3082,16 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
   IcrcParams P{frames, desc, n, mode == NICGPU_ICRC_VERIFY, out_crc, out_ok};
   // every resident wave slot busy (a wave's range is then >= 64 packets, one
   // work-queue refill); ranges of 8 packets per lane left 3/4 of the slots idle
-  // NICGPU_ICRC=b4mem: timing only, the loads without the table work
-  // (results wrong); b4tp: 32-B windows loaded coalesced and transposed
+  // NICGPU_ICRC=b4mem: timing only, the loads without the table work (results wrong)
   static const int var = [] {
     const char* e = std::getenv("NICGPU_ICRC");
-    return !e ? 0 : std::strcmp(e, "b4mem") == 0 ? 1 : std::strcmp(e, "b4tp") == 0 ? 2 : 0;
+    return e && std::strcmp(e, "b4mem") == 0 ? 1 : 0;
   }();
   const uint64_t want = (n + kIcrcThreads - 1) / kIcrcThreads;
   const uint64_t cap = (uint64_t) di->cus * (uint64_t) di->icrc_blocks_per_cu;
   const unsigned grid = (unsigned) (want < 1 ? 1 : (want < cap ? want : cap));
   if (var == 1)
     hipLaunchKernelGGL((icrc_b4_kernel<8, 1>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
-  else if (var == 2)
-    hipLaunchKernelGGL((icrc_b4_kernel<2, 2>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
   else
     hipLaunchKernelGGL((icrc_b4_kernel<8, 0>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
   return hip_status(hipGetLastError());
