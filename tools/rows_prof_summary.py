@@ -67,7 +67,14 @@ def main():
         bj = os.path.join(root, f"{row}.json")
         if os.path.exists(bj):
             lines = [json.loads(l) for l in open(bj) if l.startswith("{")]
-            if lines and "alg_bytes_per_launch" in lines[0]:
+            if row == "f1" and lines and "frame_GBps" in lines[-1]:
+                # the delivery reads and writes every delivered frame once:
+                # 2 x the batch's frame bytes (frame_GBps x batch time)
+                b = lines[-1]
+                rec.update({"stage_batch_us_median": b["us_median"],
+                            "alg_bytes_per_launch": int(2 * b["frame_GBps"] * b["us_median"] * 1e3),
+                            "alg_bytes_note": "2 x the frames delivered (read + written); write records, statuses and hashes not counted"})
+            elif lines and "alg_bytes_per_launch" in lines[0]:
                 b = lines[0]
                 rec.update({"hip_event_region_us": b.get("us_region_avg"), "hip_event_median_us": b.get("us_median"),
                             "alg_bytes_per_launch": b["alg_bytes_per_launch"]})
