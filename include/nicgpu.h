@@ -369,25 +369,6 @@ int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t n
  * on the main one. */
 int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
                       uint64_t* npieces, nicgpu_qp_view* view, void* plan_stream, void* sums_stream);
-/* nicgpu_qp_plan_on without its wait: the count, scan, piece descriptors and
- * piece checksums are all enqueued, the descriptors written only within the
- * piece buffers' current capacity and the checksums taken over the pieces
- * that fit (their number read on the device), and the piece count and the
- * range flag come down to page-locked memory on plan_stream.  *pending = 1;
- * once plan_stream has been waited for (nicgpu_qp_check waits for its
- * stream), nicgpu_qp_plan_finish reports the outcome.  With no piece buffers
- * yet this is nicgpu_qp_plan_on (*pending = 0, *npieces set).  Saves the
- * plan's host round trip when consecutive batches fit the same buffers. */
-#define NICGPU_PLAN_REDO 1
-int nicgpu_qp_plan_async(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
-                         uint64_t* npieces, nicgpu_qp_view* view, void* plan_stream, void* sums_stream,
-                         int* pending);
-/* After nicgpu_qp_plan_async (*pending = 1) and a wait for its plan_stream:
- * NICGPU_OK with *npieces; NICGPU_ERR_RANGE as nicgpu_qp_plan_on; or
- * NICGPU_PLAN_REDO (*npieces set) when the pieces outgrew the buffers: wait
- * for every stream that read them, then plan again with nicgpu_qp_plan_on
- * (and redo whatever read the sums). */
-int nicgpu_qp_plan_finish(nicgpu_qp* q, uint64_t* npieces);
 /* The reference's control flow over view.tx[0, ntx) against view.rx[0, nrx)
  * from the piece sums: TX descriptors [0, *done) are resolved, with
  * completions in view.txc[0, *done) and view.rxc[0, *rx_used), their writes in

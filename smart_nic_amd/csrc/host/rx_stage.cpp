@@ -19,7 +19,6 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
-#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -1563,18 +1562,8 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     check(nicgpu_stream_wait_event(ps, sl.ev_tx), "nicgpu_stream_wait_event");
   }
   std::uint64_t np = 0;
-  // the plan without its host round trip when the piece buffers from earlier
-  // batches are large enough (checked after the overlap check, which waits
-  // for `ps`; a batch that outgrows them is planned and resolved again)
-  int plan_pending = 0;
-  static const bool sync_plan = [] {  // NICGPU_F1_SYNC_PLAN=1: the round-2 plan with its wait (A/B)
-    const char* e = std::getenv("NICGPU_F1_SYNC_PLAN");
-    return e && e[0] == '1';
-  }();
-  const int pst = sync_plan ? nicgpu_qp_plan_on(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx,
-                                                config_.max_mtu, &np, &v, ps, stream)
-                            : nicgpu_qp_plan_async(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size,
-                                                   ntx, config_.max_mtu, &np, &v, ps, stream, &plan_pending);
+  const int pst = nicgpu_qp_plan_on(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx,
+                                    config_.max_mtu, &np, &v, ps, stream);
   out.timings.sums_us += us_since(t);
   t = clock::now();
   if (sl.up) {
@@ -1594,11 +1583,9 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   // check's verdict (it writes only the context's completions and writes),
   // so the stream does not wait for this thread's round trip on the check
   t = clock::now();
-  if (!plan_pending) {
-    check(nicgpu_qp_resolve_start(sl.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, stream),
-          "nicgpu_qp_resolve_start");
-    check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");  // final unless relaxed / tail below
-  }
+  check(nicgpu_qp_resolve_start(sl.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, stream),
+        "nicgpu_qp_resolve_start");
+  check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");  // final unless relaxed / tail below
   out.timings.resolve_us += us_since(t);
   // overlapping buffers go to the host path before anything is written; a
   // ring whose RX buffers are not in ascending address order is sorted there.
@@ -1606,27 +1593,6 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   t = clock::now();
   int verdict = -1;
   check(nicgpu_qp_check(sl.qp, mem.size, ntx, nrx, &verdict, ps), "nicgpu_qp_check");
-  if (plan_pending) {
-    // the asynchronous plan's count is on the host now (the check waited for
-    // `ps`); the resolve reads the piece sums, so it goes in only after the
-    // plan is known to fit the piece buffers
-    const int fst = nicgpu_qp_plan_finish(sl.qp, &np);
-    if (fst == NICGPU_ERR_RANGE) return false;  // as the synchronous plan: the host path
-    if (fst == NICGPU_PLAN_REDO) {
-      // the pieces outgrew the buffers (nothing was read or written past
-      // them): wait for the sums, then plan again, growing the buffers
-      check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
-      const int rst = nicgpu_qp_plan_on(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx,
-                                        config_.max_mtu, &np, &v, ps, stream);
-      if (rst == NICGPU_ERR_RANGE) return false;
-      check(rst, "nicgpu_qp_plan_on");
-    } else {
-      check(fst, "nicgpu_qp_plan_finish");
-    }
-    check(nicgpu_qp_resolve_start(sl.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, stream),
-          "nicgpu_qp_resolve_start");
-    check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");
-  }
   if (verdict < 0) {
     const auto [htx, hrx] = host_spans(sl, tx, rx, stream);
     verdict = buffers_disjoint(mem.size, htx, hrx) ? 1 : 0;

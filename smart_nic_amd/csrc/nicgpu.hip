@@ -3203,22 +3203,14 @@ __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_desc
   }
 }
 
-// cap: the piece buffers' capacity (pieces at or past it are not written: an
-// asynchronous plan learns the total only afterwards); np_out (may be null):
-// min(total, cap), the piece count the sums then read on the device
 __global__ __launch_bounds__(kQpBlock) void qp_fill_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
                                                            uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
-                                                           const uint32_t* __restrict__ base, uint64_t* desc,
-                                                           uint64_t cap, unsigned long long* np_out) {
-  if (np_out && blockIdx.x == 0 && threadIdx.x == 0) *np_out = base[n] < cap ? base[n] : cap;
+                                                           const uint32_t* __restrict__ base, uint64_t* desc) {
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
     uint32_t at = base[i];
     plans[i].first_piece = at;
     QpPlan pp;
-    nicqp::plan_packet(max_mtu, mem_size, tx[i], pp, [&](uint64_t a, uint64_t len) {
-      if (at < cap) desc[at] = NICGPU_DESC(a, len);
-      ++at;
-    });
+    nicqp::plan_packet(max_mtu, mem_size, tx[i], pp, [&](uint64_t a, uint64_t len) { desc[at++] = NICGPU_DESC(a, len); });
   }
 }
 
@@ -3539,7 +3531,6 @@ struct nicgpu_qp {
   uint64_t* misc() const { return hp + kQpTail; }
   unsigned grid = 1;
   hipEvent_t planned = nullptr;   // nicgpu_qp_plan_on: the piece descriptors are written
-  size_t plan_cap = 0;            // nicgpu_qp_plan_async: the piece capacity the asynchronous plan wrote within
   hipEvent_t resolved = nullptr;  // nicgpu_qp_resolve_start: its partials are on the host
   // the resolve between nicgpu_qp_resolve_start and _finish
   struct Pending {
@@ -3603,7 +3594,7 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
   auto* q = new nicgpu_qp();
   q->device = device;
   q->grid = (unsigned) di.cus * 8u;
-  if (hipMalloc(&q->scal, 8 * sizeof(unsigned long long)) != hipSuccess ||
+  if (hipMalloc(&q->scal, 4 * sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&q->partials, ((size_t) q->grid * kQpStats + kQpTail) * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&q->queue_start, 65536 * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&q->queue_end, 65536 * sizeof(uint32_t)) != hipSuccess) {
@@ -3717,7 +3708,7 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
   if (st == NICGPU_OK) st = qp_grow(q->piece_csum, q->c_pcs, np ? np : 1);
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->base, q->piece_desc, ~0ull, nullptr);
+                     q->plans, q->base, q->piece_desc);
   st = hip_status(hipGetLastError());
   if (st == NICGPU_OK && sums_stream != plan_stream) {  // the sums read the pieces the fill wrote
     st = hip_status(hipEventRecord(q->planned, s));
@@ -3727,54 +3718,6 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
   *npieces = np;
   qp_fill_view(q, view);
   return st;
-}
-
-int nicgpu_qp_plan_async(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
-                         uint64_t* npieces, nicgpu_qp_view* view, void* plan_stream, void* sums_stream,
-                         int* pending) {
-  if (!q || !pending || !npieces || ntx > q->cap_tx) return NICGPU_ERR_INVALID;
-  if (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0)) return NICGPU_ERR_INVALID;
-  *pending = 0;
-  const size_t cap = q->c_pdesc < q->c_pcs ? q->c_pdesc : q->c_pcs;
-  *npieces = 0;
-  if (cap == 0)  // no piece buffers yet: the synchronous plan sizes them
-    return nicgpu_qp_plan_on(q, mem, mem_size, ntx, max_mtu, npieces, view, plan_stream, sums_stream);
-  DeviceGuard g(q->device);
-  hipStream_t s = static_cast<hipStream_t>(plan_stream);
-  const unsigned grid = qp_grid(q, ntx + 1);
-  unsigned long long* np_dev = q->scal + 4;
-  uint32_t* np_h = reinterpret_cast<uint32_t*>(q->misc());
-  int st = hip_status(hipMemsetAsync(q->counts + ntx, 0, sizeof(uint32_t), s));
-  if (st == NICGPU_OK)
-    hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                       q->plans, q->counts);
-  if (st == NICGPU_OK) st = hip_status(hipGetLastError());
-  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(np_h + 1, q->counts + ntx, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
-  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(np_h, q->base + ntx, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  if (st != NICGPU_OK) return st;
-  hipLaunchKernelGGL(qp_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->base, q->piece_desc, (uint64_t) cap, np_dev);
-  st = hip_status(hipGetLastError());
-  if (st == NICGPU_OK && sums_stream != plan_stream) {
-    st = hip_status(hipEventRecord(q->planned, s));
-    if (st == NICGPU_OK) st = hip_status(hipStreamWaitEvent(static_cast<hipStream_t>(sums_stream), q->planned, 0));
-  }
-  if (st == NICGPU_OK)
-    st = nicgpu_rx_offload_count(nullptr, mem, q->piece_desc, cap, reinterpret_cast<const uint64_t*>(np_dev),
-                                 NICGPU_TUPLE_NONE, 0, 0, q->piece_csum, nullptr, nullptr, nullptr, sums_stream);
-  q->plan_cap = cap;
-  *pending = 1;
-  qp_fill_view(q, view);
-  return st;
-}
-
-int nicgpu_qp_plan_finish(nicgpu_qp* q, uint64_t* npieces) {
-  if (!q || !npieces) return NICGPU_ERR_INVALID;
-  const uint32_t* np_h = reinterpret_cast<const uint32_t*>(q->misc());
-  if (np_h[1] != 0u) return NICGPU_ERR_RANGE;
-  *npieces = np_h[0];
-  return np_h[0] <= q->plan_cap ? NICGPU_OK : NICGPU_PLAN_REDO;
 }
 
 int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int* verdict, void* stream) {

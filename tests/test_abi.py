@@ -117,8 +117,6 @@ def test_batch_entry_points_validate_before_device_access():
     assert lib.nicgpu_qp_reserve(None, 1, 1, p) == INV
     assert lib.nicgpu_qp_plan(None, p, 64, 1, 9000, p, p, None) == INV
     assert lib.nicgpu_qp_plan_on(None, p, 64, 1, 9000, p, p, None, None) == INV
-    assert lib.nicgpu_qp_plan_async(None, p, 64, 1, 9000, p, p, None, None, p) == INV
-    assert lib.nicgpu_qp_plan_finish(None, p) == INV
     # streams and events: null handles -> INVALID (no device touched)
     assert lib.nicgpu_stream_create(None) == INV
     assert lib.nicgpu_stream_destroy(None) == INV
