@@ -3196,7 +3196,7 @@ __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_desc
                                                             uint32_t* counts) {
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
     QpPlan pp;
-    const uint32_t c = nicqp::plan_packet(max_mtu, mem_size, tx[i], pp, [](uint64_t, uint64_t) {});
+    const uint32_t c = nicqp::plan_packet(max_mtu, mem_size, nicqp::desc_load(tx + i), pp, [](uint64_t, uint64_t) {});
     counts[i] = c <= kQpMaxPieces ? c : 0u;
     if (c > kQpMaxPieces) counts[n] = 1u;
     plans[i] = pp;
@@ -3210,7 +3210,8 @@ __global__ __launch_bounds__(kQpBlock) void qp_fill_kernel(const nicgpu_tx_descr
     uint32_t at = base[i];
     plans[i].first_piece = at;
     QpPlan pp;
-    nicqp::plan_packet(max_mtu, mem_size, tx[i], pp, [&](uint64_t a, uint64_t len) { desc[at++] = NICGPU_DESC(a, len); });
+    nicqp::plan_packet(max_mtu, mem_size, nicqp::desc_load(tx + i), pp,
+                       [&](uint64_t a, uint64_t len) { desc[at++] = NICGPU_DESC(a, len); });
   }
 }
 

@@ -24,6 +24,37 @@
 
 namespace nicqp {
 
+// A descriptor read whole: on the device, 16- or 8-B loads into registers
+// (field-by-field reads of the 32-B TX / 24-B RX PODs cost seven memory
+// instructions per descriptor); on the host, a plain copy.
+template <class T>
+NICQP_HD T desc_load(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  T v;
+  if constexpr (sizeof(T) % 16 == 0) {
+    if ((reinterpret_cast<uintptr_t>(p) & 15u) == 0) {
+      typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+      u4 w[sizeof(T) / 16];
+#pragma unroll
+      for (unsigned k = 0; k < sizeof(T) / 16; ++k) w[k] = reinterpret_cast<const u4*>(p)[k];
+      __builtin_memcpy(&v, w, sizeof(T));
+      return v;
+    }
+  }
+  if constexpr (sizeof(T) % 8 == 0) {
+    if ((reinterpret_cast<uintptr_t>(p) & 7u) == 0) {
+      typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+      u2 w[sizeof(T) / 8];
+#pragma unroll
+      for (unsigned k = 0; k < sizeof(T) / 8; ++k) w[k] = reinterpret_cast<const u2*>(p)[k];
+      __builtin_memcpy(&v, w, sizeof(T));
+      return v;
+    }
+  }
+#endif
+  return *p;
+}
+
 constexpr uint32_t kRun = 65534;  // even, so every run of a plain packet starts at an even offset
 constexpr uint64_t kMinMss = 1, kMaxMss = 9000, kMaxTsoSegments = 64;  // include/nic/offload.h:21-23
 // CompletionCode (include/nic/tx_rx.h:26-35)
@@ -256,7 +287,7 @@ NICQP_HD Comp make_tx(uint16_t qid, const Tx& t, uint32_t st, uint64_t segs, boo
 // (read fault, TX checksum, MTU, invalid mss, too many segments).
 template <class Tx, class Rx, class Plan>
 NICQP_HD uint32_t rx_need(const Ctx<Tx, Rx, Plan>& C, uint64_t i) {
-  const Tx& t = C.tx[i];
+  const Tx t = desc_load(C.tx + i);
   const uint64_t L = t.length;
   if (!dma_ok(C.mem_size, t.buffer_address, L)) return 0;
   if (tx_verify_needed(t)) {
@@ -276,7 +307,7 @@ NICQP_HD uint32_t rx_need(const Ctx<Tx, Rx, Plan>& C, uint64_t i) {
 template <class Comp, class Write, class Tx, class Rx, class Plan, class Stats, class Sink>
 NICQP_HD uint64_t resolve_packet(const Ctx<Tx, Rx, Plan>& C, uint64_t i, uint64_t rc, Stats& stats, Sink& sink) {
   const uint16_t qid = C.queue_id;
-  const Tx& t = C.tx[i];
+  const Tx t = desc_load(C.tx + i);
   const PacketSums<Plan> ps{&C.plans[i], C.cs, (uint64_t) t.length};
   const uint64_t L = t.length;
   const uint64_t rc0 = rc;
@@ -328,7 +359,7 @@ NICQP_HD uint64_t resolve_packet(const Ctx<Tx, Rx, Plan>& C, uint64_t i, uint64_
     return 0;
   }
   for (uint32_t k = 0; k < total; ++k) {
-    const auto& xr = C.rx[rc++];
+    const auto xr = desc_load(C.rx + rc++);
     const bool x_present = xr.vlan_present || t.vlan_insert;  // :320-322
     // base segment = header || chunk k (or the whole packet)
     uint64_t src_a = t.buffer_address, src_b = 0;
