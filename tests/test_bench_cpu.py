@@ -44,3 +44,53 @@ def test_l34_batch_matches_per_frame():
     for i, d in enumerate(desc.tolist()):
         off, n = d & ((1 << 40) - 1), d >> 40
         assert out[i] == L.oracle_l34_verify(vp(frames.ctypes.data + off), n)
+
+
+def test_committed_traffic_profiles_name_their_kernel_source():
+    """bench.py's roofline traffic and gpu_rows_traffic come from committed
+    rocprofv3 summaries that name the kernel source they measured; the
+    defaults must be those of this tree (else the bench line marks them
+    stale)."""
+    import bench
+
+    traffic, info = bench.load_traffic(os.path.join(ROOT, "profiles", "r03zz_pmc_c2.json"))
+    assert traffic and traffic > 1_600_000_000 and info["profile_kernel_source"]
+    rows = bench.load_rows_traffic(os.path.join(ROOT, "profiles", "r03_rows_prof.json"))
+    assert rows.get("error") is None and rows["profile_kernel_source"]
+    for r in ("rx_c2", "rx_c3", "rx_u64", "icrc_c2", "tso_c5", "tso_seg_c5", "f1"):
+        assert r in rows["rows"], r
+        assert abs(rows["rows"][r].get("fetch_factor", 0) - 2.0) < 0.01  # calibrated streams / line walks
+        assert 0.95 < rows["rows"][r]["traffic_over_alg"] < 1.3
+    assert 0 < rows["rows"]["rss_c2"]["fetch_over_same_shape_min"] < 2
+
+
+def test_rows_summary_applies_per_shape_calibration(tmp_path):
+    """tools/rows_prof_summary.py on a synthetic rocprofv3 tree: a stream row
+    doubles FETCH_SIZE, a header-gather row reports FETCH per packet over the
+    calibration kernel's per-slot FETCH."""
+    import csv
+
+    root = tmp_path / "rows"
+    for row, fetch_kb, write_kb in (("rx_c2", 1000.0, 10.0), ("rss_c2", 300.0, 5.0)):
+        kt = root / f"kt_{row}"
+        kt.mkdir(parents=True)
+        with open(kt / "T_kernel_stats.csv", "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs", "StdDev"])
+            w.writerow([f"k_{row}", 2, 2000, 1000, 100, 1000, 1000, 0])
+        (root / f"{row}.json").write_text(json.dumps({"row": row, "packets": 1024, "alg_bytes_per_launch": 2048000,
+                                                      "us_region_avg": 1.0, "us_median": 1.0}) + "\n")
+        for c, v in (("FETCH_SIZE", fetch_kb), ("WRITE_SIZE", write_kb)):
+            d = root / f"{c}_{row}"
+            d.mkdir()
+            with open(d / "T_counter_collection.csv", "w", newline="") as f:
+                w = csv.writer(f)
+                w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+                w.writerow([1, f"k_{row}", c, v])
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rows_prof_summary.py"), str(root), "T"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    out = {x["row"]: x for x in json.loads(r.stdout)["rows"]}
+    assert out["rx_c2"]["hbm_bytes_per_launch"] == int(2 * 1000.0 * 1024 + 10.0 * 1024)
+    calib = json.load(open(os.path.join(ROOT, "profiles", "r03_calib_fetch.json")))["shapes"]["hdr48"]
+    assert abs(out["rss_c2"]["fetch_over_same_shape_min"] - 300.0 * 1024 / 1024 / calib["fetch_bytes_per_slot"]) < 1e-3
