@@ -2336,7 +2336,12 @@ struct IcrcParams {
 
 constexpr int kIcrcRing = 128;  // descriptor ring per wave (LDS)
 
-constexpr int kIcrcWpb = 16;  // waves per block: one 1024-thread block per CU shares the table image
+// waves per block: one block per CU shares the table image.  8 waves, not 16:
+// each lane walks its own packet's lines, so a CU's waves keep waves x 64
+// lines in flight; same-box sweep (profiles/r03_icrc_wpb_sweep.txt, median us
+// C2 / C3): 4 waves 566 / 727, 6: 435 / 545, 8: 379 / 460, 10: 459 / 444,
+// 12: 469 / 434, 16: 452 / 491.
+constexpr int kIcrcWpb = 8;
 constexpr int kIcrcThreads = kWave * kIcrcWpb;
 // a ^ b ^ c in one VALU op (hipcc folds table words one v_xor_b32 at a time)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -2353,8 +2358,8 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // ds_read_b32 banks by (a / 4) mod 32, so the two halves of a row are two
 // tables on the same 32 banks).  A lookup address is one v_perm_b32:
 // {copy byte, byte j of the state, table pair, 0}.  128 KiB of LDS: one
-// 1024-thread block per CU.  Each lane walks its packet dword by dword
-// (a serial chain per lane; 16 waves per CU cover its latency); the packet's
+// block (8 waves) per CU.  Each lane walks its packet dword by dword
+// (a serial chain per lane; 8 waves per CU cover its latency); the packet's
 // 1..3 leading bytes in its first dword are masked and the state enters
 // through kCrcLead, and its 0..3 bytes past the last whole dword take byte
 // steps on T0 at the end, so no trailing-zero unshift is needed.
