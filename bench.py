@@ -49,18 +49,56 @@ def usable_cores():
     return usable, os.cpu_count() or usable
 
 
+def cgroup_cpu_limit():
+    """The CPU quota of this process's cgroup in CPUs (cgroup v2 cpu.max or v1
+    cfs_quota/period), or None when unlimited or unreadable."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            lines = f.read().splitlines()
+    except OSError:
+        lines = []
+    cands = []
+    for line in lines:
+        parts = line.split(":", 2)
+        if len(parts) == 3 and (parts[0] == "0" or "cpu" in parts[1].split(",")):
+            rel = parts[2].lstrip("/")
+            cands += [os.path.join("/sys/fs/cgroup", rel), os.path.join("/sys/fs/cgroup/cpu", rel)]
+    cands += ["/sys/fs/cgroup", "/sys/fs/cgroup/cpu"]
+    for d in cands:
+        try:
+            with open(os.path.join(d, "cpu.max")) as f:
+                q, p = f.read().split()[:2]
+            if q != "max":
+                return float(q) / float(p)
+            return None
+        except (OSError, ValueError):
+            pass
+        try:
+            with open(os.path.join(d, "cpu.cfs_quota_us")) as f:
+                q = int(f.read())
+            with open(os.path.join(d, "cpu.cfs_period_us")) as f:
+                p = int(f.read())
+            return q / p if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    return None
+
+
 def cpu_baseline(frames, desc, table, gpu_out, n_sample_1, label):
     """Reference C++ path (oracle/_ref/libref.so: the reference's own
     src/checksum.cpp + src/rss.cpp, compiled in the build container) or, if it
     is absent, the oracle restatement, timed on this host's cores: one core
-    over a bounded sample, and every usable core (one RssEngine per thread,
-    rss.h:43 is not thread-safe) over the whole batch.  Also checks the GPU
-    outputs bit-exactly on both."""
+    over a bounded sample, then a thread sweep (1, 8, 16, 32, 64, 128 and every
+    usable core; one RssEngine per thread, rss.h:43 is not thread-safe) over
+    the whole batch.  `value` is the best leg and `cores` the threads that
+    produced it; the cgroup quota and the sweep are reported beside it.  Also
+    checks the GPU outputs bit-exactly on every leg."""
     from oracle import pyoracle as po
 
     ref = po.ref_lib()
     kind = "reference" if ref is not None else "port"
     usable, host_cpus = usable_cores()
+    quota = cgroup_cpu_limit()
     k = np.frombuffer(MS_KEY, np.uint8)
     t = np.ascontiguousarray(table.astype(np.uint16))
     n_all = desc.size
@@ -82,32 +120,36 @@ def cpu_baseline(frames, desc, table, gpu_out, n_sample_1, label):
     dt1, cs1, q1 = run(n_sample_1, 1)
     g_cs, g_q = gpu_out
     ok = bool(np.array_equal(cs1, g_cs[:n_sample_1]) and np.array_equal(q1, g_q[:n_sample_1]))
-    legs = {}
+    sweep = {}
     if ref is not None:
-        for threads in sorted({min(16, usable), usable}):
-            dt, cs, q = run(n_all, threads)
-            ok = ok and bool(np.array_equal(cs, g_cs) and np.array_equal(q, g_q))
-            legs[threads] = dt
-        cores = usable
-        dtm, n_mt = legs[usable], n_all
+        for threads in sorted({t for t in (1, 8, 16, 32, 64, 128) if t <= usable} | {usable}):
+            dt, cs, q = run(n_all, threads) if threads > 1 else (dt1 * n_all / n_sample_1, None, None)
+            if cs is not None:
+                ok = ok and bool(np.array_equal(cs, g_cs) and np.array_equal(q, g_q))
+            sweep[threads] = n_all / dt / 1e6
+        cores = max(sweep, key=sweep.get)
+        best = sweep[cores]
+        n_mt = n_all if cores > 1 else n_sample_1
     else:
-        cores, dtm, n_mt = 1, dt1, n_sample_1
+        cores, n_mt = 1, n_sample_1
+        best = n_sample_1 / dt1 / 1e6
     out = {
-        "value": round(n_mt / dtm / 1e6, 4),
+        "value": round(best, 4),
         "unit": "Mpkt/s",
         "cores": cores,
         "kind": kind,
-        "sample": f"{label}: all {n_mt} packets on {cores} threads (every usable core, one RssEngine per thread); "
-                  f"1 core: first {n_sample_1} packets",
+        "sample": f"{label}: best leg of a thread sweep, {n_mt} packets on {cores} threads (one RssEngine per "
+                  f"thread); 1-thread leg over the first {n_sample_1} packets",
         "value_1core": round(n_sample_1 / dt1 / 1e6, 4),
-        "gbs": round(float(frames_bytes(desc[:n_mt])) / dtm / 1e9, 4),
+        "gbs": round(best * 1e6 * float(frames_bytes(desc[:n_mt])) / n_mt / 1e9, 4),
         "gpu_matches_cpu_on_sample": ok,
         "cpu_model": _cpu_model(),
         "usable_cores": usable,
         "host_cpus": host_cpus,
+        "cgroup_cpu_quota": (round(quota, 2) if quota is not None else None),
+        "effective_cores": (min(usable, int(quota + 0.999)) if quota is not None else usable),
+        "thread_sweep_mpkts": {str(t): round(v, 4) for t, v in sweep.items()},
     }
-    if 16 in legs and usable != 16:
-        out["value_16threads"] = round(n_all / legs[16] / 1e6, 4)
     return out
 
 
@@ -145,10 +187,13 @@ def cpu_rows_baseline(pktgen):
             ref.ref_rx_batch(f3.ctypes.data, d3.ctypes.data, n, 1, k.ctypes.data, k.size, t16.ctypes.data, t16.size,
                              cs.ctypes.data, q.ctypes.data, threads)
             return time.perf_counter() - t0
-        dtm, dt1 = rx(n3, cores), rx(1 << 16, 1)
-        rows.append({"row": "rx_c3", "value": round(n3 / dtm / 1e6, 4), "unit": "Mpkt/s", "cores": cores,
+        sweep = {t: n3 / rx(n3, t) / 1e6 for t in sorted({min(16, cores), min(64, cores), cores})}
+        best_t = max(sweep, key=sweep.get)
+        dt1 = rx(1 << 16, 1)
+        rows.append({"row": "rx_c3", "value": round(sweep[best_t], 4), "unit": "Mpkt/s", "cores": best_t,
                      "kind": "reference", "value_1core": round((1 << 16) / dt1 / 1e6, 4),
-                     "sample": f"{n3} IMIX frames (7:4:1 64/576/1518 B), 16 queues, every usable core; "
+                     "thread_sweep_mpkts": {str(t): round(v, 4) for t, v in sweep.items()},
+                     "sample": f"{n3} IMIX frames (7:4:1 64/576/1518 B), 16 queues, best of a thread sweep; "
                                f"1 core over 65536"})
     L = po.lib()
     n5 = 4096
@@ -288,8 +333,11 @@ def load_rows_traffic(path):
             prof = json.load(f)
     except (OSError, ValueError):
         return {"profile": os.path.relpath(path, ROOT), "error": "unreadable"}
-    with open(os.path.join(ROOT, "smart_nic_amd", "csrc", "nicgpu.hip"), "rb") as f:
-        cur = hashlib.sha256(f.read()).hexdigest()[:16]
+    try:
+        with open(os.path.join(ROOT, "smart_nic_amd", "csrc", "nicgpu.hip"), "rb") as f:
+            cur = hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        cur = None
     rec = prof.get("kernel_source_sha256")
     keep = ("rocprof_avg_us", "access_shape", "fetch_factor", "hbm_bytes_per_launch", "traffic_over_alg",
             "fetch_bytes_per_packet", "fetch_over_same_shape_min", "frac_of_8TBps_rocprof")
@@ -297,6 +345,11 @@ def load_rows_traffic(path):
     return {"profile": os.path.relpath(path, ROOT), "measured_in_this_run": False, "profile_kernel_source": rec,
             "current_kernel_source": cur, "stale": rec is None or rec != cur, "rows": rows}
 
+
+METRIC_TEXT = {
+    "c2": "Mpkt/s + GB/s device-resident RX checksum+RSS, 1518B batch; % HBM roofline",
+    "c3": "Mpkt/s + GB/s device-resident RX checksum+RSS, IMIX batch; % HBM roofline",
+}
 
 WORKLOAD_TEXT = {
     "c2": "C2: 1M x 1518 B TCP per GPU, checksum verify + RSS (MS 40-B key, 128-entry table i%4, IPv4 4-tuple)",
@@ -427,7 +480,7 @@ def main():
     if rank == 0:
         traffic, traffic_src = load_traffic(args.traffic_json) if args.workload == "c2" else (None, None)
         out = {
-            "metric": "Mpkt/s + GB/s device-resident RX checksum+RSS, 1518B batch; % HBM roofline",
+            "metric": METRIC_TEXT[args.workload],
             "value": round(value, 3),
             "unit": "Mpkt/s",
             "n_gpus": world,

@@ -120,6 +120,10 @@ public:
   /// QueueManager::process_once until it returns false, over batches[q] for
   /// queue pair q (batches.size() == queue_count()); results into out[q]
   /// (resized).  Synchronises `stream`.  Returns the schedule it served.
+  /// If a queue pair's batch throws, the statistics of the queue pairs whose
+  /// batches completed are kept (their writes are in memory), the scheduler
+  /// state (index, credit, advances, skips) is not advanced, and the
+  /// exception propagates.
   QueueSchedule process_batch(const DeviceHostMemory& mem, std::span<const QueueBatch> batches,
                               std::vector<RxBatchResult>& out, void* stream = nullptr);
 

@@ -165,7 +165,9 @@ struct BatchedQueuePairConfig {
   /// the path: every path resolves without firing them, and
   /// rx_stage_detail::replay_interrupts fires them from the batch's
   /// completions, in posting order, on the thread that completes the batch
-  /// (process_batch, or collect for submitted batches).
+  /// (process_batch, or collect for submitted batches).  Batches of more than
+  /// NICGPU_QP_MAX_TX (2^32 / 256, about 16.7 M) TX descriptors, or more than
+  /// NICGPU_QP_MAX_RX RX descriptors, take the host path (32-bit piece indices).
   bool device_resolve{true};
   /// Leave the results of device-resolved batches in device memory
   /// (RxBatchResult::dev) instead of copying them to the host vectors: for

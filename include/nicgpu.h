@@ -329,6 +329,11 @@ typedef struct nicgpu_qp_view {
 } nicgpu_qp_view;
 
 typedef struct nicgpu_qp nicgpu_qp;
+/* Largest batch nicgpu_qp_reserve accepts: piece indices are 32-bit and a TX
+ * descriptor plans at most 256 pieces.  nic::BatchedQueuePair sends larger
+ * batches to its host path (include/nic/rx_stage.h). */
+#define NICGPU_QP_MAX_TX (0xFFFFFFFFull / 256u)
+#define NICGPU_QP_MAX_RX 0x7FFFFFFEull
 int nicgpu_qp_create(nicgpu_qp** out, int device);
 int nicgpu_qp_destroy(nicgpu_qp* q);
 /* Capacity for ntx TX and nrx RX descriptors (ntx <= 2^32 / 256 and

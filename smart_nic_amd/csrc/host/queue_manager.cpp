@@ -235,7 +235,14 @@ QueueSchedule BatchedQueueManager::process_batch(const DeviceHostMemory& mem, st
           if (!err) err = std::current_exception();
         }
       }
-      if (err) std::rethrow_exception(err);
+      if (err) {
+        // the stages whose batches went through advanced their own statistics
+        // (a stage commits a batch's stats only when it completes): carry them
+        // over before rethrowing; the scheduler state stays where it was, as
+        // no schedule was completed
+        for (std::size_t q = 0; q < Q; ++q) add_delta(qps_[q]->stats, qps_[q]->stage.stats(), before[q]);
+        std::rethrow_exception(err);
+      }
     } else {
       for (std::size_t q = 0; q < Q; ++q)
         if (n[q]) qps_[q]->stage.process_batch(mem, batches[q].tx, batches[q].rx, out[q], stream);

@@ -1249,6 +1249,13 @@ BatchedQueuePair& BatchedQueuePair::operator=(BatchedQueuePair&& o) noexcept {
   return *this;
 }
 
+// Batches past the device context's 32-bit piece indices (nicgpu.h
+// NICGPU_QP_MAX_TX) take the host path, as a descriptor planning too many
+// pieces does (front(): NICGPU_ERR_RANGE).
+static bool device_fits(std::size_t ntx, std::size_t nrx) noexcept {
+  return ntx <= NICGPU_QP_MAX_TX && nrx <= NICGPU_QP_MAX_RX;
+}
+
 RxBatchResult BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                               std::span<const RxDescriptor> rx, void* stream) {
   RxBatchResult out;
@@ -1265,7 +1272,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
   int disjoint = -1;  // unknown; the device path checks on the device
   double check_us = 0;
   bool on_device = false;
-  if (config_.device_resolve) {
+  if (config_.device_resolve && device_fits(tx.size(), rx.size())) {
     int dev = 0;
     check(nicgpu_get_device(&dev), "nicgpu_get_device");
     scratch_->ensure(dev);
@@ -1318,7 +1325,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDe
   int disjoint = -1;
   double check_us = 0;
   bool on_device = false;
-  if (config_.device_resolve) {
+  if (config_.device_resolve && device_fits(d.ntx, d.nrx)) {
     on_device = front(sl, mem, {}, {}, st, out, stream, disjoint, check_us);
     if (on_device) {
       back(sl, mem, out, stream);
@@ -1416,7 +1423,7 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
   sl.ntx_dev = d ? d->ntx : 0;
   sl.nrx_dev = d ? d->nrx : 0;
   sl.fetched = false;
-  const bool device = config_.device_resolve;
+  const bool device = config_.device_resolve && (d ? device_fits(d->ntx, d->nrx) : device_fits(tx.size(), rx.size()));
   // host descriptors go up now, on this thread, beside the earlier batches'
   // device work (device descriptors are copied in the job, in stream order);
   // the rest runs in submission order on the job thread
@@ -1588,7 +1595,11 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   out.timings.copy_us += us_since(t);
   // the speculative resolve goes in behind the piece sums before the overlap
   // check's verdict (it writes only the context's completions and writes),
-  // so the stream does not wait for this thread's round trip on the check
+  // so the stream does not wait for this thread's round trip on the check.
+  // For an overlapping or unsorted batch that pass (need/scan/full/reduce and
+  // its small download) is wasted GPU time: the host path then redoes the
+  // batch, and the context's resolve state stays set until the next start.
+  // Results are unaffected; disjoint rings are the common case.
   t = clock::now();
   check(nicgpu_qp_resolve_start(sl.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, stream),
         "nicgpu_qp_resolve_start");

@@ -3640,7 +3640,8 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
 int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view) {
   if (!q) return NICGPU_ERR_INVALID;
   // 32-bit ring positions; hipcub scans and sorts take int counts
-  if (ntx > 0xFFFFFFFFull / kQpMaxPieces || nrx > 0x7FFFFFFEull) return NICGPU_ERR_INVALID;
+  static_assert(NICGPU_QP_MAX_TX == 0xFFFFFFFFull / kQpMaxPieces, "include/nicgpu.h limit");
+  if (ntx > NICGPU_QP_MAX_TX || nrx > NICGPU_QP_MAX_RX) return NICGPU_ERR_INVALID;
   DeviceGuard g(q->device);
   int st = NICGPU_OK;
   const size_t t1 = ntx + 1, r1 = nrx + 1;

@@ -792,8 +792,62 @@ int run_edges() {
     if (!threw) std::fprintf(stderr, "edges: an RX buffer over the descriptor ring was not refused\n");
     ok = ok && threw;
   }
+  // a batch of more TX descriptors than the device context's 32-bit piece
+  // indices allow (NICGPU_QP_MAX_TX): refused by nicgpu_qp_reserve, so the
+  // stage takes the host path (equal to the host resolve) instead of throwing
+  {
+    const std::size_t ntx = NICGPU_QP_MAX_TX + 1;
+    {
+      nicgpu_qp* q = nullptr;
+      assert(nicgpu_qp_create(&q, 0) == NICGPU_OK);
+      nicgpu_qp_view v{};
+      if (nicgpu_qp_reserve(q, ntx, 4, &v) != NICGPU_ERR_INVALID) {
+        std::fprintf(stderr, "edges: nicgpu_qp_reserve accepted %zu TX descriptors\n", ntx);
+        ok = false;
+      }
+      nicgpu_qp_destroy(q);
+    }
+    std::vector<TxDescriptor> btx(ntx);
+    for (std::size_t i = 0; i < ntx; ++i) {  // every descriptor sends the same 64-B frame
+      TxDescriptor& t = btx[i];
+      t.buffer_address = big;
+      t.length = 64;
+      t.descriptor_index = static_cast<std::uint16_t>(i);
+    }
+    std::vector<RxDescriptor> brx(4);
+    for (std::size_t j = 0; j < brx.size(); ++j) {
+      brx[j].buffer_address = big + 512 * 1024 + j * 2048;
+      brx[j].buffer_length = 2048;
+    }
+    std::vector<std::uint8_t> himg = image;
+    test::CpuBackend hcpu{himg, nullptr, TupleSpec{}};
+    RxBatchResult bh;
+    QueuePairStats bhs{};
+    rx_stage_detail::BatchScratch bscratch;
+    rx_stage_detail::run_batch(cfg, mem_size, btx, brx, bhs, bh, bscratch, hcpu);
+    assert(nicgpu_memcpy_async(d, image.data(), mem_size, nullptr) == NICGPU_OK);
+    BatchedQueuePair bqp{cfg};
+    RxBatchResult bg;
+    bool threw = false;
+    try {
+      bqp.process_batch(DeviceHostMemory{static_cast<std::byte*>(d), mem_size}, btx, brx, bg);
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "edges: a batch of %zu TX descriptors threw: %s\n", ntx, e.what());
+      threw = true;
+    }
+    bool same_all = !threw && !bg.timings.device && bg.tx_completions.size() == ntx &&
+                    bg.rx_completions.size() == bh.rx_completions.size() &&
+                    std::memcmp(&bhs, &bqp.stats(), sizeof(bhs)) == 0;
+    for (std::size_t i = 0; same_all && i < ntx; ++i) same_all = same(bg.tx_completions[i], bh.tx_completions[i]);
+    for (std::size_t i = 0; same_all && i < bh.rx_completions.size(); ++i)
+      same_all = same(bg.rx_completions[i], bh.rx_completions[i]);
+    if (!same_all) std::fprintf(stderr, "edges: the over-count batch differs from the host resolve\n");
+    ok = ok && same_all;
+  }
   nicgpu_free(d);
-  if (ok) std::printf("rx_stage_gpu_fuzz edges: ok (over-range plan took the host path; ring overwrite refused)\n");
+  if (ok)
+    std::printf("rx_stage_gpu_fuzz edges: ok (over-range plan and over-count batch took the host path; ring "
+                "overwrite refused)\n");
   return ok ? 0 : 1;
 }
 

@@ -1,8 +1,9 @@
 """Multi-process (world_size 2, gloo on CPU) coverage of the N>1 path: key and
 table broadcast from rank 0, byte-balanced contiguous sharding, per-rank
 processing (oracle stands in for the kernel here — no GPU on CPU runners),
-hit-histogram sum and max-over-ranks timing.  The union of the shards must
-equal the single-process result exactly."""
+hit-histogram sum and max-over-ranks timing.  Every rank processes its slice
+of one job batch; the concatenated results must equal one single-process run
+over the whole batch exactly."""
 
 import os
 import socket
@@ -16,6 +17,7 @@ import torch.multiprocessing as mp
 from smart_nic_amd import dist as sdist
 from smart_nic_amd import pktgen
 
+JOB_SEED = 2024
 MS_KEY = bytes.fromhex("6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c6a42b73bbeac01fa")
 
 
@@ -44,7 +46,12 @@ def _worker(rank, world, port, q):
         key_t, tab_t = sdist.setup_rss(ranks, MS_KEY if rank == 0 else bytes(40), table)
         shard = sdist.plan_shard("c3", ranks, packets_per_gpu=1500)
         c2 = sdist.plan_shard("c2", ranks, packets_per_gpu=64)
-        frames, desc, _ = pktgen.make_batch(shard.lengths, seed=shard.seed, proto=shard.proto)
+        # the job batch, made once from one seed (as a NIC's ring would hold
+        # it), and this rank's contiguous slice of it by the shard bounds
+        job = pktgen.imix_lengths(3000, np.random.default_rng(sdist.WORKLOADS["c3"]["seed"]))
+        assert np.array_equal(shard.lengths, job[shard.lo:shard.hi])
+        frames, desc_all, _ = pktgen.make_batch(job, seed=JOB_SEED, proto=shard.proto)
+        desc = np.ascontiguousarray(desc_all[shard.lo:shard.hi])
         cs, h, qq, _, hits = po.rx_batch(frames, desc, bytes(key_t.numpy()), tab_t.numpy().view(np.uint16))
         hits_t = torch.from_numpy(hits.astype(np.int64))
         job, per, ok = sdist.job_queue_hits(ranks, hits_t)
@@ -74,20 +81,19 @@ def test_two_rank_sharding_matches_single_process():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # the job batch: 3000 IMIX lengths from the workload seed; each rank's
-    # frames come from its own seed over its own lengths
+    # ONE single-process run over the whole job batch; each rank's results
+    # must be exactly its slice of it, and the slices must tile the batch
     job = pktgen.imix_lengths(3000, np.random.default_rng(sdist.WORKLOADS["c3"]["seed"]))
     table = (np.arange(128) % 16).astype(np.uint16)
+    frames, desc, _ = pktgen.make_batch(job, seed=JOB_SEED, proto=17)
+    cs, h, qq, _, want_hits = po.rx_batch(frames, desc, MS_KEY, table)
     assert res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == 3000
-    want_hits = np.zeros(128, np.uint64)
     for r in res:
         lo, hi = r[1], r[2]
-        frames, desc, _ = pktgen.make_batch(job[lo:hi], seed=r[14], proto=17)
-        cs, h, qq, _, hits = po.rx_batch(frames, desc, MS_KEY, table)
-        np.testing.assert_array_equal(r[3], cs)
-        np.testing.assert_array_equal(r[4], h)
-        np.testing.assert_array_equal(r[5], qq)
-        want_hits += hits
+        np.testing.assert_array_equal(r[3], cs[lo:hi])
+        np.testing.assert_array_equal(r[4], h[lo:hi])
+        np.testing.assert_array_equal(r[5], qq[lo:hi])
+    assert np.array_equal(np.concatenate([r[4] for r in res]), h)
     for r in res:
         np.testing.assert_array_equal(r[6], want_hits)  # summed histogram on every rank
         assert r[11]  # all-reduce == sum of the all-gathered per-rank histograms
