@@ -298,21 +298,18 @@ def _cpu_model():
 def load_traffic(path):
     """HBM bytes per launch from a committed rocprofv3 PMC summary (see
     profiles/README.md) and where it came from: the profile names the kernel
-    source it measured (sha256 of smart_nic_amd/csrc/nicgpu.hip); a profile
+    source it measured (tools/kernel_sha.py "rx": the RX kernel's sources); a profile
     of another source is reported as stale, never silently."""
-    import hashlib
 
     try:
         with open(path) as f:
             prof = json.load(f)
     except (OSError, ValueError):
         return None, {"profile": os.path.relpath(path, ROOT), "error": "unreadable"}
-    src = os.path.join(ROOT, "smart_nic_amd", "csrc", "nicgpu.hip")
-    try:
-        with open(src, "rb") as f:
-            cur = hashlib.sha256(f.read()).hexdigest()[:16]
-    except OSError:
-        cur = None
+    from tools.kernel_sha import kernel_source_sha
+
+    cur = kernel_source_sha("rx")
+    cur = cur[:16] if cur else None
     rec = prof.get("kernel_source_sha256")
     info = {"profile": os.path.relpath(path, ROOT), "measured_in_this_run": False,
             "profile_kernel_source": rec, "current_kernel_source": cur,
@@ -326,18 +323,16 @@ def load_rows_traffic(path):
     """Per-row HBM traffic from a committed rows profile (tools/rows_prof_summary.py:
     FETCH_SIZE calibrated per access shape), with the kernel source it measured;
     a profile of another source is reported as stale, never silently."""
-    import hashlib
 
     try:
         with open(path) as f:
             prof = json.load(f)
     except (OSError, ValueError):
         return {"profile": os.path.relpath(path, ROOT), "error": "unreadable"}
-    try:
-        with open(os.path.join(ROOT, "smart_nic_amd", "csrc", "nicgpu.hip"), "rb") as f:
-            cur = hashlib.sha256(f.read()).hexdigest()[:16]
-    except OSError:
-        cur = None
+    from tools.kernel_sha import kernel_source_sha
+
+    cur = kernel_source_sha("all")
+    cur = cur[:16] if cur else None
     rec = prof.get("kernel_source_sha256")
     keep = ("rocprof_avg_us", "access_shape", "fetch_factor", "hbm_bytes_per_launch", "traffic_over_alg",
             "fetch_bytes_per_packet", "fetch_over_same_shape_min", "frac_of_8TBps_rocprof")

@@ -6,7 +6,7 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 TAG=${TAG:-r01}
 mkdir -p gpurun_out/prof
-sha256sum smart_nic_amd/csrc/nicgpu.hip > gpurun_out/prof/kernel_source.sha
+python tools/kernel_sha.py rx > gpurun_out/prof/kernel_source.sha
 PT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
 timeout -k 10 600 $PT tests -m gpu --ignore=tests/test_gpu_variants.py > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -6 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc

@@ -8,7 +8,7 @@ R=$GRAFT_REPO_ROOT
 TAG=${TAG:-r02r}
 O=$R/gpurun_out/rows_prof
 mkdir -p $O
-sha256sum $R/smart_nic_amd/csrc/nicgpu.hip > $O/kernel_source.sha
+python $R/tools/kernel_sha.py all > $O/kernel_source.sha
 g++ -std=c++20 -O2 -I$R/include $R/tools/bench_rx_stage.cpp -L$R/smart_nic_amd -lnic_host -lnicgpu \
     -Wl,-rpath,"$R/smart_nic_amd" -o $O/bench_rx_stage || exit 1
 cd /tmp && export TMPDIR=/tmp

@@ -1,0 +1,1332 @@
+// f1.hip — row f1: the batched QueuePair RX stage on the device.
+// The DMA writes of resolved completions (segment_gather_kernel), the fused
+// delivery + RSS of the delivered frames (deliver_kernel), and the per-packet
+// decisions of QueuePair::process_once over a whole batch (nicgpu_qp_*;
+// src/queue_pair.cpp:67-460 through qp_logic.h).  DESIGN.md §4.6.
+
+#include "common.h"
+#include "host.h"
+#include "qp_logic.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <cstdlib>
+#include <mutex>
+#include <vector>
+
+using namespace nicgpu_detail;
+
+namespace {
+
+// ------------------------------------------------------ segment gather --
+// The DMA writes of the batched QueuePair stage (QueuePair::handle_rx_segment,
+// src/queue_pair.cpp:416-426): dst <- prefix (0/4 B, the inserted VLAN tag)
+// || [src_a, +len_a) || [src_b, +len_b), all inside one memory image.  One
+// wave per write.  Whole destination dwords are assembled from two aligned
+// source dwords with v_alignbyte (16 B per lane per step, lanes contiguous,
+// wave_copy16); the partial dwords at the ends of each part are written with
+// byte stores, so writes that share a dword never race.  Pure byte movement:
+// HBM-bound at 2 x bytes.
+struct GatherParams {
+  uint8_t* mem;
+  const uint8_t* src;  // sources: mem itself, or a copy of it
+  uint64_t mem_size;
+  const nicgpu_segment_write* w;
+  size_t n;
+};
+
+// wave_copy for the gather: each lane moves 16 B per step with one dwordx4
+// load and store (4-B aligned: the sources and destinations of segment writes
+// have any byte alignment; whole dwords are assembled as in wave_copy), the
+// fifth source dword of the byte shift from the next lane.  Sources are
+// clamped to the image, whose end need not be 16-B padded.
+__device__ void wave_copy16(uint8_t* dmem, uint64_t dst, const uint8_t* smem, uint64_t smem_size, uint64_t src,
+                            uint64_t len, uint32_t lane) {
+  if (len == 0) return;
+  const uint64_t d1 = dst + len;
+  const uint64_t A = (dst + 3) & ~3ull;
+  const uint64_t B = d1 & ~3ull;
+  if (A >= B) {
+    if (lane < len) dmem[dst + lane] = smem[src + lane];
+    return;
+  }
+  const uint64_t head = A - dst, tail = d1 - B;
+  if (lane < head) dmem[dst + lane] = smem[src + lane];
+  if (lane >= 8 && lane - 8 < tail) dmem[B + (lane - 8)] = smem[src + (B - dst) + (lane - 8)];
+  const uint64_t nw = (B - A) >> 2;
+  const uint64_t s0 = src + head;
+  const uint32_t sh = (uint32_t) (s0 & 3);
+  const uint64_t sa = s0 & ~3ull;
+  const uint64_t steps = (nw + 255) / 256;  // wave-uniform trip count (the shuffle needs every lane)
+  for (uint64_t k = 0; k < steps; ++k) {
+    const uint64_t i = k * 256 + (uint64_t) lane * 4;
+    const uint64_t a = sa + 4 * i;
+    uint32_t v[5] = {0, 0, 0, 0, 0};
+    if (i < nw) {
+      if (a + 16 <= smem_size) {
+        __builtin_memcpy(v, smem + a, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = load_dword_clamped(smem, smem_size, a + 4 * j);
+      }
+    }
+    const uint32_t up = (uint32_t) __builtin_amdgcn_ds_bpermute((int) (((lane + 1) & 63) << 2), (int) v[0]);
+    if (i < nw && sh) v[4] = (lane < 63 && i + 4 < nw) ? up : (i + 4 <= nw ? load_dword_clamped(smem, smem_size, a + 16) : 0u);
+    if (i < nw) {
+      uint32_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = sh ? __builtin_amdgcn_alignbyte(v[j + 1], v[j], sh) : v[j];
+      uint8_t* d = dmem + A + 4 * i;
+      if (i + 4 <= nw) {
+        __builtin_memcpy(d, o, 16);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (i + j < nw) reinterpret_cast<uint32_t*>(d)[j] = o[j];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void segment_gather_kernel(GatherParams P) {
+  const uint32_t lane = lane_id();
+  const uint64_t wave = (uint64_t) blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+  const uint64_t nwaves = (uint64_t) gridDim.x * kWavesPerBlock;
+  // the next write's entry is loaded while this one copies (one memory
+  // latency per write instead of two)
+  nicgpu_segment_write next{};
+  if (wave < P.n) next = P.w[wave];
+  for (uint64_t e = wave; e < P.n; e += nwaves) {
+    const nicgpu_segment_write w = next;
+    if (e + nwaves < P.n) next = P.w[e + nwaves];
+    const uint64_t plen = w.prefix_len == 4 ? 4 : 0;
+    const uint64_t total = plen + w.len_a + w.len_b;
+    // entries outside the image are skipped (the host validated them)
+    if (w.prefix_len > 4 || w.dst > P.mem_size || total > P.mem_size - w.dst || w.src_a > P.mem_size ||
+        w.len_a > P.mem_size - w.src_a || w.src_b > P.mem_size || w.len_b > P.mem_size - w.src_b)
+      continue;
+    if (lane < plen) P.mem[w.dst + lane] = (uint8_t) (w.prefix >> (8 * lane));
+    wave_copy16(P.mem, w.dst + plen, P.src, P.mem_size, w.src_a, w.len_a, lane);
+    wave_copy16(P.mem, w.dst + plen + w.len_a, P.src, P.mem_size, w.src_b, w.len_b, lane);
+  }
+}
+
+// --------------------------------------------- fused delivery (row f1) --
+// The batched QueuePair stage's DMA writes and the RSS of the frames they
+// deliver in one launch (nicgpu_qp_deliver).  A wave takes a tile of 64 RX
+// completions and walks their bytes as ONE stream of destination 16-B chunks,
+// as the RX kernel walks packets: every write splits into up to three items
+// (VLAN prefix, part A, part B — queue_pair.cpp:352-359, 392-395, 416-426
+// already resolved into the write), every item into the destination chunks it
+// touches, and lane l of a step takes stream entry base + l.  So one wave
+// instruction moves up to 1 KiB whatever the frame sizes (the one-wave-per-
+// write gather left 60 of 64 lanes idle on 64-B frames and kept one write's
+// load latency per wave in flight).  A chunk's source is five dwords from the
+// item's source at the chunk's byte shift; whole chunks are one 16-B store,
+// item edges dword or byte stores, so no byte outside a segment is written.
+//
+// RSS: for a completion with status Success, the lanes whose chunk lies in its
+// frame's first three destination chunks also OR their bytes into the wave's
+// header stage (the RX kernel's 48-B-per-packet layout), and after the tile
+// the owning lane hashes the frame from the stage exactly as rss_only_kernel
+// (rss_hash_packet; bytes past the stage, rare, from the frame just written).
+// The hash and queue land per completion (0 / 0xFFFF for the others), the
+// table-index hits in a block histogram, the Success count in *count — what
+// qp_flag/qp_rss_fill, the RSS launch and qp_scatter produced in four launches
+// with the headers read back from HBM.
+struct DeliverParams {
+  uint8_t* mem;
+  uint64_t mem_size;
+  const nicgpu_segment_write* w;
+  const nicgpu_completion* rxc;  // statuses (RSS of Success completions)
+  uint64_t j0, n;                // completions [j0, n) ...
+  const unsigned long long* n_dev;  // ... with n lowered to *n_dev (a speculative resolve's settled prefix)
+  RxParams rss;                  // mode NICGPU_TUPLE_NONE: no RSS
+  uint32_t* rx_hash;
+  uint16_t* rx_queue;
+  unsigned long long* hits;
+  unsigned long long* count;
+};
+
+#ifndef NICGPU_DLV_WPB
+#define NICGPU_DLV_WPB 8
+#endif
+#ifndef NICGPU_DLV_U
+#define NICGPU_DLV_U 4
+#endif
+#ifndef NICGPU_DLV_RESERVE
+#define NICGPU_DLV_RESERVE 0
+#endif
+constexpr int kDlvReserveCus = NICGPU_DLV_RESERVE;  // default of NICGPU_DLV_RESERVE_CUS (tuning)
+constexpr int kDlvWpb = NICGPU_DLV_WPB;  // waves per block
+constexpr int kDlvU = NICGPU_DLV_U;      // 64-entry sub-steps per step (loads in flight per lane)
+constexpr uint32_t kDlvRec = 24;  // item record: dst u64 | src (or prefix word) u64 | len u32 | first entry u32
+constexpr uint32_t kDlvMarks = (kWave * kDlvU + 15u) & ~15u;  // bytes: one u8 mark per stream entry (item id + 1 <= 192)
+constexpr uint32_t kDlvWaveBytes = kDlvMarks + 64u * 8u + 192u * kDlvRec + 64u * kHdrStride * 16u;  // marks|wdst|items|stage
+
+// block part: RSS LUT | histogram | table (as rss_only_kernel), then 16 B for the Success count
+__host__ __device__ inline uint32_t dlv_block_bytes(bool rss, uint32_t lut_words, uint32_t hist_n,
+                                                    uint32_t table_words) {
+  return (rss ? rss_only_block_bytes(lut_words, hist_n, table_words) : 0u) + 16u;
+}
+
+__device__ __forceinline__ uint32_t dlv_chunks(uint64_t d, uint64_t n) {
+  return n ? (uint32_t) (((d + n - 1) >> 4) - (d >> 4) + 1) : 0u;
+}
+
+// Stores the bytes [lo, hi) (absolute) of the 16-B destination chunk at D
+// from o; whole chunk: one 16-B store, else whole dwords and bytes.
+__device__ __forceinline__ void dlv_store(uint8_t* mem, uint64_t D, uint64_t lo, uint64_t hi, const uint32_t* o) {
+  if (lo == D && hi == D + 16) {
+    u32x4 v = {o[0], o[1], o[2], o[3]};
+    *reinterpret_cast<u32x4*>(mem + D) = v;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t a = D + 4u * i;
+    if (a >= lo && a + 4 <= hi) {
+      *reinterpret_cast<uint32_t*>(mem + a) = o[i];
+    } else if (a + 4 > lo && a < hi) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (a + b >= lo && a + b < hi) mem[a + b] = (uint8_t) (o[i] >> (8 * b));
+    }
+  }
+}
+
+template <bool RSS>
+__global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu(4, 8))) void deliver_kernel(DeliverParams P) {
+  constexpr uint32_t kThreads = kWave * kDlvWpb;
+  extern __shared__ uint4 lds_dyn[];
+  const uint32_t w = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
+  const uint32_t lane = lane_id();
+  const RxParams& R = P.rss;
+  const bool hist_lds = RSS && R.table_n <= (uint32_t) kHistLds;
+  const bool table_lds = RSS && R.table_n <= (uint32_t) kTableLds;
+  uint8_t* base_b = reinterpret_cast<uint8_t*>(lds_dyn);
+  uint32_t* lut = reinterpret_cast<uint32_t*>(base_b);
+  uint32_t* hist = lut + (RSS ? R.lut_words : 0u);
+  uint16_t* table_s = reinterpret_cast<uint16_t*>(hist + (hist_lds ? R.table_n : 0u));
+  const uint32_t block_bytes = dlv_block_bytes(RSS, R.lut_words, hist_lds ? R.table_n : 0u,
+                                               table_lds ? (R.table_n + 1u) / 2u : 0u);
+  uint32_t* cnt_s = reinterpret_cast<uint32_t*>(base_b + block_bytes - 16u);
+  uint8_t* wave_b = base_b + block_bytes + w * kDlvWaveBytes;
+  uint8_t* marks = wave_b;
+  uint64_t* wdst = reinterpret_cast<uint64_t*>(wave_b + kDlvMarks);
+  uint8_t* items = wave_b + kDlvMarks + 512u;
+  uint4* stage = reinterpret_cast<uint4*>(items + 192u * kDlvRec);
+  if (RSS) {
+    for (uint32_t i = threadIdx.x; i < R.lut_words; i += kThreads) lut[i] = R.lut[i];
+    if (hist_lds)
+      for (uint32_t i = threadIdx.x; i < R.table_n; i += kThreads) hist[i] = 0;
+    if (table_lds)
+      for (uint32_t i = threadIdx.x; i < R.table_n; i += kThreads) table_s[i] = R.table[i];
+    if (threadIdx.x == 0) *cnt_s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t) kHdrChunks; ++k) stage[hdr_slot(lane, k)] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+  uint64_t n = P.n;
+  if (P.n_dev) {
+    const uint64_t m = *P.n_dev;
+    n = m < n ? m : n;
+  }
+  const uint64_t ntiles = n > P.j0 ? (n - P.j0 + kWave - 1) / kWave : 0;
+  const uint64_t nwaves = (uint64_t) gridDim.x * kDlvWpb;
+  uint32_t my_count = 0;
+  for (uint64_t tile = (uint64_t) blockIdx.x * kDlvWpb + w; tile < ntiles; tile += nwaves) {
+    // ---- this lane's write: its items and their stream entries
+    const uint64_t j = P.j0 + tile * kWave + lane;
+    nicgpu_segment_write wr{};
+    bool flag = false;
+    if (j < n) {
+      wr = P.w[j];
+      if (RSS) flag = P.rxc[j].status == nicqp::kSuccess;
+    }
+    const uint64_t plen = wr.prefix_len == 4 ? 4 : 0;
+    const uint64_t total = plen + wr.len_a + wr.len_b;
+    // entries outside the image are skipped (the host validated them)
+    const bool ok = j < n && !(wr.prefix_len > 4 || wr.dst > P.mem_size || total > P.mem_size - wr.dst ||
+                                 wr.src_a > P.mem_size || wr.len_a > P.mem_size - wr.src_a ||
+                                 wr.src_b > P.mem_size || wr.len_b > P.mem_size - wr.src_b);
+    const uint64_t d1 = wr.dst + plen, d2 = d1 + wr.len_a;
+    const uint32_t c0 = ok ? dlv_chunks(wr.dst, plen) : 0u;
+    const uint32_t c1 = ok ? dlv_chunks(d1, wr.len_a) : 0u;
+    const uint32_t c2 = ok ? dlv_chunks(d2, wr.len_b) : 0u;
+    const uint32_t cw = c0 + c1 + c2;
+    const uint32_t incl = wave_incl_scan(cw);
+    const uint32_t F = incl - cw;
+    const uint32_t total_e = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
+    auto put = [&](uint32_t k, uint64_t d, uint64_t src, uint32_t len, uint32_t first) __attribute__((always_inline)) {
+      uint8_t* r = items + (lane * 3u + k) * kDlvRec;
+      *reinterpret_cast<uint64_t*>(r) = d;
+      *reinterpret_cast<uint64_t*>(r + 8) = src;
+      *reinterpret_cast<uint32_t*>(r + 16) = len;
+      *reinterpret_cast<uint32_t*>(r + 20) = first;
+    };
+    put(0, wr.dst, wr.prefix, c0 ? 4u : 0u, F);
+    put(1, d1, wr.src_a, c1 ? wr.len_a : 0u, F + c0);
+    put(2, d2, wr.src_b, c2 ? wr.len_b : 0u, F + c0 + c1);
+    wdst[lane] = (wr.dst >> 4) | (flag && ok ? 1ull << 63 : 0ull);
+    // ---- the stream: kDlvU x 64 entries per step, every load of the step
+    // issued before its first store (one memory latency per step)
+    uint32_t carry = 0;  // item (id + 1) of the entry before this step
+    for (uint32_t W = 0; W < total_e; W += kWave * kDlvU) {
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) marks[u * kWave + lane] = 0u;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      constexpr uint32_t kSpan = kWave * kDlvU;
+      if (c0 && F >= W && F - W < kSpan) marks[F - W] = (uint8_t) (lane * 3u + 1u);
+      if (c1 && F + c0 >= W && F + c0 - W < kSpan) marks[F + c0 - W] = (uint8_t) (lane * 3u + 2u);
+      if (c2 && F + c0 + c1 >= W && F + c0 + c1 - W < kSpan) marks[F + c0 + c1 - W] = (uint8_t) (lane * 3u + 3u);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      uint32_t itv[kDlvU];
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) {
+        uint32_t it = wave_incl_max(marks[u * kWave + lane]);
+        it = it > carry ? it : carry;
+        carry = (uint32_t) __builtin_amdgcn_readlane((int) it, 63);
+        itv[u] = it;
+      }
+      // phase A: every entry's chunk, item and source window; loads issued.
+      // Per entry: the destination chunk, one packed word (bytes [lo, hi) of
+      // the chunk, source shift, owning write) and five source dwords — a
+      // prefix item's 4 bytes are placed into them here — so that kDlvU
+      // entries' loads fit in flight per lane.
+      uint64_t Dc[kDlvU];  // destination chunk index; ~0: no entry
+      uint32_t pk[kDlvU];  // lo - D (bits 0-4) | hi - D (8-12) | shift (16-17) | write q (20-25)
+      uint32_t vv[kDlvU][5];
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) {
+        const uint32_t pos = W + (uint32_t) u * kWave + lane;
+        Dc[u] = ~0ull;
+        pk[u] = 0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) vv[u][i] = 0;
+        if (pos < total_e) {
+          const uint32_t id = itv[u] - 1u, q = id / 3u, k = id - 3u * q;
+          const uint8_t* r = items + id * kDlvRec;
+          const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
+          const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
+          const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
+          const uint32_t first = *reinterpret_cast<const uint32_t*>(r + 20);
+          const uint64_t D = ((d >> 4) + (pos - first)) << 4;
+          const uint64_t lo = D > d ? D : d;
+          const uint64_t hi = D + 16 < d + len ? D + 16 : d + len;
+          Dc[u] = D >> 4;
+          pk[u] = (uint32_t) (lo - D) | ((uint32_t) (hi - D) << 8) | (q << 20);
+          if (k == 0) {
+            // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): its 4 bytes at d
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              uint32_t v = 0;
+#pragma unroll
+              for (int bb = 0; bb < 4; ++bb) {
+                const int64_t rel = (int64_t) (D + 4u * i + bb) - (int64_t) d;
+                if (rel >= 0 && rel < 4) v |= (uint32_t) ((src >> (8 * rel)) & 0xFFu) << (8 * bb);
+              }
+              vv[u][i] = v;
+            }
+          } else {
+            // source of destination byte D: before the item's source by up to
+            // 15 bytes on its first chunk, so possibly below address 0 (signed)
+            const int64_t a = (int64_t) D + ((int64_t) src - (int64_t) d);
+            const int64_t a4 = a & ~(int64_t) 3;
+            pk[u] |= (uint32_t) (a & 3) << 16;
+            if (a4 >= 0 && (uint64_t) a4 + 20 <= P.mem_size) {
+              __builtin_memcpy(vv[u], P.mem + a4, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
+              // the fifth dword only for a shifted window (equal alignment of
+              // source and destination, the common case, needs four)
+              vv[u][4] = (a & 3) ? *reinterpret_cast<const uint32_t*>(P.mem + a4 + 16) : 0u;
+            } else {  // bytes outside the image read as 0 (never stored: outside [lo, hi))
+#pragma unroll
+              for (int i = 0; i < 5; ++i) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                  const int64_t e = a4 + 4 * i + bb;
+                  if (e >= 0 && (uint64_t) e < P.mem_size) x |= (uint32_t) P.mem[e] << (8 * bb);
+                }
+                vv[u][i] = x;
+              }
+            }
+          }
+        }
+      }
+      // phase B: align, store, and the header stage of Success frames
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) {
+        if (Dc[u] == ~0ull) continue;
+        const uint64_t D = Dc[u] << 4, lo = D + (pk[u] & 31u), hi = D + ((pk[u] >> 8) & 31u);
+        const uint32_t sh = (pk[u] >> 16) & 3u;
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = sh ? __builtin_amdgcn_alignbyte(vv[u][i + 1], vv[u][i], sh) : vv[u][i];
+        dlv_store(P.mem, D, lo, hi, o);
+        if (RSS) {
+          const uint32_t q = pk[u] >> 20;
+          const uint64_t wd = wdst[q];
+          const uint64_t kc = Dc[u] - (wd & ~(1ull << 63));
+          if ((wd >> 63) && kc < (uint64_t) kHdrChunks) {
+            uint32_t* st = reinterpret_cast<uint32_t*>(stage + hdr_slot(q, (uint32_t) kc));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uint64_t a = D + 4u * i;
+              const int b0 = lo > a ? (int) (lo - a) : 0, b1 = hi < a + 4 ? (int) (hi - a) : 4;
+              if (b1 > b0) atomicOr(st + i, o[i] & dword_keep(b0, b1, 0));
+            }
+          }
+        }
+      }
+    }
+    if (RSS) {
+      // the frames' bytes are in the stage; bytes past it come from the frame
+      // this wave just wrote (its stores retired first)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (j < n) {
+        if (flag && ok) {
+          uint64_t len = total;
+          if (len > NICGPU_MAX_PACKET) len = NICGPU_MAX_PACKET;  // the tuple lies in the first 82 B
+          const uint32_t h = rss_hash_packet(R, lut, HdrView{stage, lane}, (uint32_t) (wr.dst & 15u), P.mem + wr.dst,
+                                             (uint32_t) len);
+          const uint32_t idx = h % R.table_n;
+          P.rx_hash[j] = h;
+          P.rx_queue[j] = table_lds ? table_s[idx] : R.table[idx];
+          if (hist_lds) atomicAdd(&hist[idx], 1u);
+          else atomicAdd(&P.hits[idx], 1ull);
+          ++my_count;
+        } else {
+          P.rx_hash[j] = 0u;
+          P.rx_queue[j] = 0xFFFFu;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+      for (uint32_t k = 0; k < (uint32_t) kHdrChunks; ++k) stage[hdr_slot(lane, k)] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  if (RSS) {
+    const uint32_t c = (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan(my_count), 63);
+    if (lane == 0 && c) atomicAdd(cnt_s, c);
+    __syncthreads();
+    if (threadIdx.x == 0 && *cnt_s) atomicAdd(P.count, (unsigned long long) *cnt_s);
+    if (hist_lds) flush_hist(hist, R.table_n, P.hits, R.hits_rep, R.hits_done, kThreads);
+  }
+}
+
+template <bool RSS>
+int dlv_blocks_per_cu(uint32_t lds) {
+  return blocks_per_cu(reinterpret_cast<const void*>(deliver_kernel<RSS>), kWave * kDlvWpb, lds);
+}
+
+}  // namespace
+
+extern "C" {
+
+int nicgpu_segment_gather(uint8_t* mem, uint64_t mem_size, const nicgpu_segment_write* writes, size_t n,
+                          void* stream) {
+  return nicgpu_segment_gather_from(mem, mem, mem_size, writes, n, stream);
+}
+
+int nicgpu_segment_gather_from(uint8_t* mem, const uint8_t* src, uint64_t mem_size,
+                               const nicgpu_segment_write* writes, size_t n, void* stream) {
+  if (n == 0) return NICGPU_OK;
+  if (!mem || !src || !writes) return NICGPU_ERR_INVALID;
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  GatherParams P{mem, src, mem_size, writes, n};
+  const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint64_t cap = (uint64_t) di->cus * 8;
+  const unsigned grid = (unsigned) (want < cap ? want : cap);
+  hipLaunchKernelGGL(segment_gather_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
+  return hip_status(hipGetLastError());
+}
+
+}  // extern "C"
+
+// ---------------------------------------------- batched QueuePair (f1) --
+// The per-packet decisions of QueuePair::process_once over a whole batch on
+// the device: one thread per TX descriptor, decisions from qp_logic.h (the
+// source the host resolve uses, fuzzed against the compiled reference).
+//   plan     count pieces per descriptor, exclusive scan, fill the piece
+//            descriptors; the RX kernel sums every piece (one pass over the
+//            TX bytes)
+//   resolve  RX descriptors each packet pops if nothing ends it early
+//            (rx_need), exclusive scan = every packet's ring position, while
+//            the ring lasts; a dry pass finds the first packet whose RX side
+//            ends it early (its pops differ); the full pass posts the
+//            completions, DMA writes and per-block statistics of every packet
+//            before that.  The caller resolves the rest on the host, in order.
+//   rss      Success frames compacted into RSS descriptors; the hashes and
+//            queues scattered back per completion.
+namespace {
+
+struct QpPlan {
+  uint32_t kind, nseg, first_piece, npieces, hdr_len, mss;
+};
+using QpCtx = nicqp::Ctx<nicgpu_tx_descriptor, nicgpu_rx_descriptor, QpPlan>;
+constexpr unsigned kQpBlock = 256;
+constexpr unsigned kQpStats = 16;
+// after the per-block stats: RX used, first mismatch, settled prefix, then the
+// batch's 16 stats totals — the one download a resolve needs
+constexpr unsigned kQpTail = 3 + 16;
+constexpr int kQpRelaxSteps = 8;  // position relaxations before the host takes the rest
+
+struct QpNullSink {
+  __device__ void tx(const nicgpu_completion&, bool) {}
+  __device__ void rx(const nicgpu_completion&, const nicgpu_segment_write*) {}
+};
+
+struct QpDevSink {
+  nicgpu_completion* txc;
+  nicgpu_completion* rxc;
+  nicgpu_segment_write* w;
+  uint64_t ti, rj;
+  __device__ void tx(const nicgpu_completion& e, bool) { txc[ti] = e; }
+  __device__ void rx(const nicgpu_completion& e, const nicgpu_segment_write* sw) {
+    rxc[rj] = e;
+    if (sw) {
+      w[rj] = *sw;
+    } else {
+      nicgpu_segment_write z{};
+      w[rj] = z;
+    }
+    ++rj;
+  }
+};
+
+// counts[n] must be 0 on entry: a descriptor that plans more than
+// kQpMaxPieces pieces counts 0 and sets it to 1, so the 32-bit scan of the
+// counts (n <= 2^32 / kQpMaxPieces) cannot wrap and the caller sees the flag.
+constexpr uint32_t kQpMaxPieces = 256;
+__global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
+                                                            uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
+                                                            uint32_t* counts) {
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
+    QpPlan pp;
+    const uint32_t c = nicqp::plan_packet(max_mtu, mem_size, nicqp::desc_load(tx + i), pp, [](uint64_t, uint64_t) {});
+    counts[i] = c <= kQpMaxPieces ? c : 0u;
+    if (c > kQpMaxPieces) counts[n] = 1u;
+    plans[i] = pp;
+  }
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_fill_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
+                                                           uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
+                                                           const uint32_t* __restrict__ base, uint64_t* desc) {
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
+    uint32_t at = base[i];
+    plans[i].first_piece = at;
+    QpPlan pp;
+    nicqp::plan_packet(max_mtu, mem_size, nicqp::desc_load(tx + i), pp,
+                       [&](uint64_t a, uint64_t len) { desc[at++] = NICGPU_DESC(a, len); });
+  }
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_need_kernel(QpCtx C, uint64_t n, uint32_t* need,
+                                                           unsigned long long* first) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *first = n;  // the speculative final pass's "nothing differed"
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i <= n; i += (uint64_t) gridDim.x * kQpBlock)
+    need[i] = i < n ? nicqp::rx_need(C, i) : 0u;
+}
+
+// One relaxation step of the ring positions: every packet resolved (without
+// outputs) at pos[i] = the exclusive scan of pops; pops[i] becomes what it
+// actually popped there (the ring checks of :75-83 and :293-303 included),
+// and scal[0] the first packet whose pops changed.  The sequential positions
+// are the fixed point, and each step makes at least one more packet exact:
+// pos[0] = 0 always is, so after k steps packets [0, k) are.
+__global__ __launch_bounds__(kQpBlock) void qp_relax_kernel(QpCtx C, uint32_t* pops, const uint32_t* __restrict__ pos,
+                                                            uint64_t n, unsigned long long* scal) {
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
+    nicgpu_qp_stats st{};
+    QpNullSink sink;
+    // a guess past the ring's end is clamped to it (the sequential positions
+    // never pass it; resolve_packet must not index past rx[nrx - 1])
+    const uint64_t rc = pos[i] < C.nrx ? (uint64_t) pos[i] : C.nrx;
+    const uint32_t popped = (uint32_t) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(C, i, rc, st, sink);
+    if (popped != pops[i]) {
+      atomicMin(&scal[0], (unsigned long long) i);
+      pops[i] = popped;
+    }
+  }
+}
+
+// packets [0, lim) at their (exact) positions: completions, writes, per-block
+// stats.  With `guess` (the pops the positions were scanned from) the pass is
+// speculative: first[0] becomes the first packet that popped otherwise, and
+// only [0, first] is exact — all of it when nothing differed.
+__global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32_t* __restrict__ pos, uint64_t lim,
+                                                           nicgpu_completion* txc, nicgpu_completion* rxc,
+                                                           nicgpu_segment_write* writes, uint64_t* partials,
+                                                           const uint32_t* __restrict__ guess) {
+  __shared__ uint64_t red[kQpStats][kQpBlock / kWave];
+  // after the per-block stats: [0] the RX descriptors used (pos[lim]), [1] the
+  // first mismatch (seeded with n by qp_need_kernel) — one download for all
+  uint64_t* tail = partials + (uint64_t) gridDim.x * kQpStats;
+  unsigned long long* first = reinterpret_cast<unsigned long long*>(tail + 1);
+  if (blockIdx.x == 0 && threadIdx.x == 0) tail[0] = pos[lim];
+  nicgpu_qp_stats st{};
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < lim; i += (uint64_t) gridDim.x * kQpBlock) {
+    if (pos[i] > C.nrx) {  // exact positions never pass the ring's end: a guess past it is wrong
+      if (guess) atomicMin(first, (unsigned long long) i);
+      continue;
+    }
+    QpDevSink sink{txc, rxc, writes, i, pos[i]};
+    const uint32_t popped = (uint32_t) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(C, i, pos[i], st, sink);
+    if (guess && popped != guess[i]) atomicMin(first, (unsigned long long) i);
+  }
+  uint64_t v[kQpStats];
+  static_assert(sizeof(nicgpu_qp_stats) == kQpStats * 8, "16 counters");
+  __builtin_memcpy(v, &st, sizeof(v));
+  const uint32_t lane = lane_id(), w = threadIdx.x / kWave;
+#pragma unroll
+  for (int k = 0; k < (int) kQpStats; ++k) {
+    unsigned long long x = v[k];
+    for (int off = kWave / 2; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    if (lane == 0) red[k][w] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < kQpStats) {
+    uint64_t x = 0;
+    for (unsigned j = 0; j < kQpBlock / kWave; ++j) x += red[threadIdx.x][j];
+    partials[(uint64_t) blockIdx.x * kQpStats + threadIdx.x] = x;
+  }
+}
+
+// After a final pass: the per-block stats summed into tail[3..19), and after
+// the speculative one tail[2] = the RX completions it made final — those of
+// the packets before the first mismatch, [0, pos[first]), or all `used` when
+// nothing differed.  nicgpu_qp_deliver_range(NICGPU_DELIVER_SETTLED) reads it
+// on the device, so the DMA writes start before the host has seen the resolve.
+constexpr unsigned kQpReduceThreads = 1024;
+__global__ __launch_bounds__(kQpReduceThreads) void qp_reduce_kernel(const uint64_t* __restrict__ partials,
+                                                                     unsigned nblocks, const uint32_t* __restrict__ pos,
+                                                                     uint64_t ntx, bool settle) {
+  __shared__ uint64_t red[kQpReduceThreads];
+  uint64_t* tail = const_cast<uint64_t*>(partials) + (size_t) nblocks * kQpStats;
+  const unsigned k = threadIdx.x % kQpStats, r = threadIdx.x / kQpStats;
+  constexpr unsigned kRows = kQpReduceThreads / kQpStats;
+  uint64_t x = 0;
+  for (unsigned b = r; b < nblocks; b += kRows) x += partials[(size_t) b * kQpStats + k];
+  red[threadIdx.x] = x;
+  __syncthreads();
+  for (unsigned h = kRows / 2; h > 0; h >>= 1) {
+    if (r < h) red[threadIdx.x] += red[threadIdx.x + h * kQpStats];
+    __syncthreads();
+  }
+  if (threadIdx.x < kQpStats) tail[3 + threadIdx.x] = red[threadIdx.x];
+  if (settle && threadIdx.x == 0) {
+    const uint64_t first = tail[1];
+    tail[2] = first < ntx ? (uint64_t) pos[first] : tail[0];
+  }
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_flag_kernel(const nicgpu_completion* __restrict__ rxc, uint64_t nrx,
+                                                           uint32_t* flags, uint32_t* rx_hash, uint16_t* rx_queue) {
+  for (uint64_t j = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; j <= nrx; j += (uint64_t) gridDim.x * kQpBlock) {
+    flags[j] = j < nrx && rxc[j].status == nicqp::kSuccess ? 1u : 0u;
+    if (j < nrx) {
+      rx_hash[j] = 0;
+      rx_queue[j] = 0xFFFFu;
+    }
+  }
+}
+
+// The tuple lies in a frame's first 82 bytes, so a frame longer than
+// NICGPU_MAX_PACKET (max_mtu above 65531) is hashed over its first
+// NICGPU_MAX_PACKET bytes: the same tuple, hash and queue.
+__global__ __launch_bounds__(kQpBlock) void qp_rss_fill_kernel(const uint32_t* __restrict__ flags,
+                                                               const uint32_t* __restrict__ at,
+                                                               const nicgpu_segment_write* __restrict__ writes,
+                                                               uint64_t nrx, uint64_t* desc, uint32_t* which,
+                                                               unsigned long long* count) {
+  for (uint64_t j = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; j <= nrx; j += (uint64_t) gridDim.x * kQpBlock) {
+    if (j == nrx) {
+      *count = at[nrx];  // the later steps read the count here, in stream order
+      continue;
+    }
+    if (!flags[j]) continue;
+    const nicgpu_segment_write w = writes[j];
+    uint64_t len = (uint64_t) w.prefix_len + w.len_a + w.len_b;
+    if (len > NICGPU_MAX_PACKET) len = NICGPU_MAX_PACKET;
+    desc[at[j]] = NICGPU_DESC(w.dst, len);
+    which[at[j]] = (uint32_t) j;
+  }
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_scatter_kernel(const uint32_t* __restrict__ which,
+                                                              const uint32_t* __restrict__ h,
+                                                              const uint16_t* __restrict__ q,
+                                                              const unsigned long long* __restrict__ count,
+                                                              uint32_t* rx_hash, uint16_t* rx_queue) {
+  const uint64_t m = *count;
+  for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < m; k += (uint64_t) gridDim.x * kQpBlock) {
+    rx_hash[which[k]] = h[k];
+    rx_queue[which[k]] = q[k];
+  }
+}
+
+// sort keys of the first nrx RSS entries: the queue of the first *count, a
+// key past every queue (nq) for the rest, so the sort leaves them last
+__global__ __launch_bounds__(kQpBlock) void qp_keys_kernel(const uint16_t* __restrict__ q,
+                                                           const unsigned long long* __restrict__ count, uint64_t nrx,
+                                                           uint32_t nq, uint32_t* key) {
+  const uint64_t m = count ? *count : nrx;
+  for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < nrx; k += (uint64_t) gridDim.x * kQpBlock)
+    key[k] = k < m ? (uint32_t) q[k] : nq;
+}
+
+// Dispatch lists for tables of fewer than 64 queues: a stable counting sort
+// of the keys (queue of each delivered frame, nq for entries past *count) in
+// 64-entry tiles, one wave per tile.  qp_gcount_kernel writes each tile's
+// per-key counts in key-major order (cnt[key * T + tile], plus a trailing 0);
+// their exclusive scan is every (key, tile)'s first output slot, and
+// qp_gscatter_kernel adds each entry's rank among the tile's entries of its
+// key (ballot + mbcnt) — the order radix sort keeps, in 4 launches instead of
+// rocprim's ~20 merge-sort passes (128 of ~1020 us of kernels per 1 M batch).
+__global__ __launch_bounds__(kQpBlock) void qp_gcount_kernel(const uint16_t* __restrict__ q,
+                                                             const unsigned long long* __restrict__ count,
+                                                             uint64_t nrx, uint32_t nq, uint64_t T, uint32_t* cnt) {
+  const uint64_t m = count ? *count : nrx;
+  const uint32_t lane = lane_id();
+  const uint64_t waves = (uint64_t) gridDim.x * (kQpBlock / kWave);
+  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(uint64_t) (nq + 1) * T] = 0u;
+  for (uint64_t t = (uint64_t) blockIdx.x * (kQpBlock / kWave) + threadIdx.x / kWave; t < T; t += waves) {
+    const uint64_t k = t * kWave + lane;
+    const uint32_t key = k < nrx ? (k < m && q[k] < nq ? (uint32_t) q[k] : nq) : nq + 1u;
+    uint32_t mine = 0;
+    for (uint32_t b = 0; b <= nq; ++b) {
+      const uint32_t c = (uint32_t) __builtin_popcountll(__ballot(key == b));
+      if (lane == b) mine = c;
+    }
+    if (lane <= nq) cnt[(uint64_t) lane * T + t] = mine;
+  }
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_gscatter_kernel(const uint16_t* __restrict__ q,
+                                                               const unsigned long long* __restrict__ count,
+                                                               uint64_t nrx, uint32_t nq, uint64_t T,
+                                                               const uint32_t* __restrict__ off,
+                                                               const uint32_t* __restrict__ which, uint32_t* out,
+                                                               uint32_t* start, uint32_t* end) {
+  const uint64_t m = count ? *count : nrx;
+  const uint32_t lane = lane_id();
+  const uint64_t waves = (uint64_t) gridDim.x * (kQpBlock / kWave);
+  const uint64_t gt = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x;
+  if (gt < nq) {  // queue gt's range; an empty queue gets start = end = 0
+    const uint32_t a = off[gt * T], b = off[(gt + 1) * T];
+    start[gt] = b > a ? a : 0u;
+    end[gt] = b > a ? b : 0u;
+  }
+  for (uint64_t t = (uint64_t) blockIdx.x * (kQpBlock / kWave) + threadIdx.x / kWave; t < T; t += waves) {
+    const uint64_t k = t * kWave + lane;
+    const uint32_t key = k < nrx ? (k < m && q[k] < nq ? (uint32_t) q[k] : nq) : nq + 1u;
+    uint32_t rank = 0;
+    for (uint32_t b = 0; b <= nq; ++b) {
+      const uint64_t v = __ballot(key == b);
+      if (key == b) rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (v >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) v, 0u));
+    }
+    if (k < nrx) out[off[(uint64_t) key * T + t] + rank] = which ? which[k] : (uint32_t) k;
+  }
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_iota_kernel(uint32_t* v, uint64_t n) {
+  for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < n; k += (uint64_t) gridDim.x * kQpBlock)
+    v[k] = (uint32_t) k;
+}
+
+// queue range boundaries of the first *count (null: nrx) sorted keys, for queues below nq
+__global__ __launch_bounds__(kQpBlock) void qp_bounds_kernel(const uint32_t* __restrict__ key,
+                                                             const unsigned long long* __restrict__ count, uint64_t nrx,
+                                                             uint64_t nq, uint32_t* start, uint32_t* end) {
+  const uint64_t m = count ? *count : nrx;
+  for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < m; k += (uint64_t) gridDim.x * kQpBlock) {
+    const uint32_t q = key[k];
+    if (q >= nq) continue;
+    if (k == 0 || key[k - 1] != q) start[q] = (uint32_t) k;
+    if (k + 1 == m || key[k + 1] != q) end[q] = (uint32_t) (k + 1);
+  }
+}
+
+// Overlap check (nicgpu_qp_check), the spans of rx_stage.cpp buffers_disjoint:
+// what an RX descriptor can receive (at most buffer_length bytes inside the
+// image, queue_pair.cpp:397-426) and what a TX descriptor is read from.
+struct QpRxEnd {  // end of RX descriptor j's span; 0 when it receives nothing
+  uint64_t mem_size;
+  __host__ __device__ uint64_t operator()(const nicgpu_rx_descriptor& x) const {
+    if (x.buffer_address >= mem_size || x.buffer_length == 0) return 0;
+    const uint64_t room = mem_size - x.buffer_address;
+    return x.buffer_address + (x.buffer_length < room ? (uint64_t) x.buffer_length : room);
+  }
+};
+
+// end_max = inclusive running max of the RX span ends.  RX spans ascend and are
+// disjoint iff every span starts at or after the running max before it
+// (flag[0] stays 0); a TX span [a, b) then meets an RX span iff the first RX
+// descriptor whose running max passes a (its own end, so it has a span) starts
+// before b (flag[1]).  TX order does not matter.
+__global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t ntx,
+                                                            const nicgpu_rx_descriptor* __restrict__ rx, uint64_t nrx,
+                                                            uint64_t mem_size, const uint64_t* __restrict__ end_max,
+                                                            unsigned long long* flag) {
+  const uint64_t n = ntx > nrx ? ntx : nrx;
+  for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < n; k += (uint64_t) gridDim.x * kQpBlock) {
+    if (k < nrx && k > 0 && QpRxEnd{mem_size}(rx[k]) != 0 && rx[k].buffer_address < end_max[k - 1]) flag[0] = 1;
+    if (k < ntx) {
+      const uint64_t a = tx[k].buffer_address, len = tx[k].length;
+      if (len == 0 || !nicqp::dma_ok(mem_size, a, len)) continue;
+      uint64_t lo = 0, hi = nrx;
+      while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (end_max[mid] <= a) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < nrx && rx[lo].buffer_address < a + len) flag[1] = 1;
+    }
+  }
+}
+
+template <class T>
+int qp_grow(T*& p, size_t& cap, size_t want) {
+  if (want <= cap) return NICGPU_OK;
+  if (p) (void) hipFree(p);
+  p = nullptr;
+  cap = 0;
+  size_t n = want + want / 4 + 64;
+  if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) return NICGPU_ERR_NOMEM;
+  cap = n;
+  return NICGPU_OK;
+}
+
+}  // namespace
+
+struct nicgpu_qp {
+  int device = 0;
+  size_t cap_tx = 0, cap_rx = 0, cap_pieces = 0, cap_tmp = 0, cap_part = 0;
+  size_t c_tx = 0, c_rx = 0, c_plans = 0, c_counts = 0, c_base = 0, c_need = 0, c_pos = 0, c_txc = 0;
+  size_t c_rxc = 0, c_w = 0, c_flags = 0, c_at = 0, c_desc = 0, c_which = 0, c_h = 0, c_q = 0, c_rh = 0, c_rq = 0;
+  size_t c_pdesc = 0, c_pcs = 0, c_part = 0, c_tmp = 0;
+  // the descriptors the kernels read: the context's own copies (tx_own /
+  // rx_own, sized by nicgpu_qp_reserve) or the caller's (nicgpu_qp_bind)
+  nicgpu_tx_descriptor* tx = nullptr;
+  nicgpu_rx_descriptor* rx = nullptr;
+  nicgpu_tx_descriptor* tx_own = nullptr;
+  nicgpu_rx_descriptor* rx_own = nullptr;
+  uint8_t* tmp_chk = nullptr;  // nicgpu_qp_check's scan storage (it may run beside a resolve)
+  size_t c_tmp_chk = 0;
+  QpPlan* plans = nullptr;
+  uint32_t *counts = nullptr, *base = nullptr, *need = nullptr, *pos = nullptr;
+  uint64_t* piece_desc = nullptr;
+  uint16_t* piece_csum = nullptr;
+  nicgpu_completion *txc = nullptr, *rxc = nullptr;
+  nicgpu_segment_write* writes = nullptr;
+  uint32_t *flags = nullptr, *at = nullptr, *which = nullptr, *rss_hash = nullptr, *rx_hash = nullptr;
+  uint64_t* rss_desc = nullptr;
+  uint16_t *rss_queue = nullptr, *rx_queue = nullptr;
+  uint64_t* partials = nullptr;
+  uint32_t *sort_key = nullptr, *sorted_key = nullptr;
+  uint32_t *queue_which = nullptr, *queue_start = nullptr, *queue_end = nullptr;
+  size_t c_sk = 0, c_qw = 0, c_em = 0, c_key = 0;
+  uint64_t* end_max = nullptr;  // [nrx] nicgpu_qp_check's running max of RX span ends
+  unsigned long long* scal = nullptr;
+  uint8_t* tmp = nullptr;
+  uint64_t host_scal[4] = {0, 0, 0, 0};
+  // page-locked landing space of the small downloads (a pageable one is staged
+  // and waited for on the host): [kQpTail] the resolve's RX count, first
+  // mismatch, settled prefix and stats totals, then misc(): piece count, check
+  // flags, relax verdict
+  uint64_t* hp = nullptr;
+  uint64_t* misc() const { return hp + kQpTail; }
+  unsigned grid = 1;
+  hipEvent_t planned = nullptr;   // nicgpu_qp_plan_on: the piece descriptors are written
+  hipEvent_t resolved = nullptr;  // nicgpu_qp_resolve_start: its partials are on the host
+  // the resolve between nicgpu_qp_resolve_start and _finish
+  struct Pending {
+    bool on = false;
+    uint64_t mem_size = 0, ntx = 0, nrx = 0, max_mtu = 0;
+    uint16_t queue_id = 0;
+    hipStream_t s = nullptr;
+    unsigned grid = 1;
+  } res;
+  bool delivered = false;  // the RSS results are per completion (nicgpu_qp_deliver), not compacted
+};
+
+namespace {
+
+void qp_fill_view(const nicgpu_qp* q, nicgpu_qp_view* v) {
+  if (!v) return;
+  v->tx = q->tx;
+  v->rx = q->rx;
+  v->piece_base = q->base;
+  v->piece_csum = q->piece_csum;
+  v->txc = q->txc;
+  v->rxc = q->rxc;
+  v->writes = q->writes;
+  v->rss_desc = q->rss_desc;
+  v->rss_hash = q->rss_hash;
+  v->rss_queue = q->rss_queue;
+  v->rx_hash = q->rx_hash;
+  v->rx_queue = q->rx_queue;
+  v->queue_which = q->queue_which;
+  v->queue_start = q->queue_start;
+  v->queue_end = q->queue_end;
+  v->rss_count = reinterpret_cast<uint64_t*>(q->scal + 3);
+}
+
+unsigned qp_grid(const nicgpu_qp* q, uint64_t n) {
+  const uint64_t want = (n + kQpBlock) / kQpBlock;
+  return (unsigned) (want < q->grid ? (want ? want : 1) : q->grid);
+}
+
+// hipcub exclusive sum of in[0, n) into out[0, n) (n includes the trailing 0)
+int qp_scan(nicgpu_qp* q, const uint32_t* in, uint32_t* out, size_t n, hipStream_t s) {
+  size_t tb = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int) n, s) != hipSuccess) return NICGPU_ERR_HIP;
+  int st = qp_grow(q->tmp, q->c_tmp, tb);
+  if (st != NICGPU_OK) return st;
+  return hip_status(hipcub::DeviceScan::ExclusiveSum(q->tmp, tb, in, out, (int) n, s));
+}
+
+}  // namespace
+
+extern "C" {
+
+int nicgpu_qp_create(nicgpu_qp** out, int device) {
+  if (!out) return NICGPU_ERR_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return NICGPU_ERR_NO_DEVICE;
+  DeviceGuard g(device);
+  const DeviceInfo& di = device_info(device);
+  if (di.status != NICGPU_OK) return di.status;
+  auto* q = new nicgpu_qp();
+  q->device = device;
+  q->grid = (unsigned) di.cus * 8u;
+  if (hipMalloc(&q->scal, 4 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&q->partials, ((size_t) q->grid * kQpStats + kQpTail) * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&q->queue_start, 65536 * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&q->queue_end, 65536 * sizeof(uint32_t)) != hipSuccess) {
+    nicgpu_qp_destroy(q);
+    return NICGPU_ERR_NOMEM;
+  }
+  if (hipHostMalloc(reinterpret_cast<void**>(&q->hp), (kQpTail + 16) * sizeof(uint64_t)) !=
+      hipSuccess) {
+    nicgpu_qp_destroy(q);
+    return NICGPU_ERR_NOMEM;
+  }
+  if (hipEventCreateWithFlags(&q->planned, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&q->resolved, hipEventDisableTiming) != hipSuccess) {
+    nicgpu_qp_destroy(q);
+    return NICGPU_ERR_HIP;
+  }
+  *out = q;
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_destroy(nicgpu_qp* q) {
+  if (!q) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  void* bufs[] = {q->tx_own, q->rx_own, q->tmp_chk, q->plans, q->counts, q->base, q->need, q->pos, q->piece_desc, q->piece_csum,
+                  q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
+                  q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sort_key, q->sorted_key, q->queue_which,
+                  q->queue_start, q->queue_end, q->end_max};
+  for (void* b : bufs)
+    if (b) (void) hipFree(b);
+  if (q->hp) (void) hipHostFree(q->hp);
+  if (q->planned) (void) hipEventDestroy(q->planned);
+  if (q->resolved) (void) hipEventDestroy(q->resolved);
+  delete q;
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view) {
+  if (!q) return NICGPU_ERR_INVALID;
+  // 32-bit ring positions; hipcub scans and sorts take int counts
+  static_assert(NICGPU_QP_MAX_TX == 0xFFFFFFFFull / kQpMaxPieces, "include/nicgpu.h limit");
+  if (ntx > NICGPU_QP_MAX_TX || nrx > NICGPU_QP_MAX_RX) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  int st = NICGPU_OK;
+  const size_t t1 = ntx + 1, r1 = nrx + 1;
+  if (st == NICGPU_OK) st = qp_grow(q->tx_own, q->c_tx, ntx ? ntx : 1);
+  if (st == NICGPU_OK) st = qp_grow(q->rx_own, q->c_rx, nrx ? nrx : 1);
+  q->tx = q->tx_own;
+  q->rx = q->rx_own;
+  if (st == NICGPU_OK) st = qp_grow(q->plans, q->c_plans, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->counts, q->c_counts, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->base, q->c_base, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->need, q->c_need, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->pos, q->c_pos, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->txc, q->c_txc, t1);
+  if (st == NICGPU_OK) st = qp_grow(q->rxc, q->c_rxc, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->writes, q->c_w, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->flags, q->c_flags, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->at, q->c_at, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->rss_desc, q->c_desc, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->which, q->c_which, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->rss_hash, q->c_h, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->rss_queue, q->c_q, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->rx_hash, q->c_rh, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->rx_queue, q->c_rq, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->sort_key, q->c_key, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->sorted_key, q->c_sk, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->queue_which, q->c_qw, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->end_max, q->c_em, r1);
+  q->cap_tx = ntx;
+  q->cap_rx = nrx;
+  qp_fill_view(q, view);
+  return st;
+}
+
+int nicgpu_qp_bind(nicgpu_qp* q, const nicgpu_tx_descriptor* tx, size_t ntx, const nicgpu_rx_descriptor* rx,
+                   size_t nrx, nicgpu_qp_view* view) {
+  if (!q || ntx > q->cap_tx || nrx > q->cap_rx || (ntx && !tx) || (nrx && !rx)) return NICGPU_ERR_INVALID;
+  q->tx = ntx ? const_cast<nicgpu_tx_descriptor*>(tx) : q->tx_own;
+  q->rx = nrx ? const_cast<nicgpu_rx_descriptor*>(rx) : q->rx_own;
+  qp_fill_view(q, view);
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
+                   uint64_t* npieces, nicgpu_qp_view* view, void* stream) {
+  return nicgpu_qp_plan_on(q, mem, mem_size, ntx, max_mtu, npieces, view, stream, stream);
+}
+
+int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
+                      uint64_t* npieces, nicgpu_qp_view* view, void* plan_stream, void* sums_stream) {
+  if (!q || !npieces || ntx > q->cap_tx) return NICGPU_ERR_INVALID;
+  if (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0)) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(plan_stream);
+  *npieces = 0;
+  const unsigned grid = qp_grid(q, ntx + 1);
+  int st = hip_status(hipMemsetAsync(q->counts + ntx, 0, sizeof(uint32_t), s));
+  if (st == NICGPU_OK)
+    hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
+                       q->plans, q->counts);
+  if (st == NICGPU_OK) st = hip_status(hipGetLastError());
+  uint32_t* np_h = reinterpret_cast<uint32_t*>(q->misc());
+  // the overflow flag first: the scan below adds it in as the last count
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(np_h + 1, q->counts + ntx, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(np_h, q->base + ntx, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  if (st != NICGPU_OK) return st;
+  if (np_h[1] != 0u) return NICGPU_ERR_RANGE;
+  const uint64_t np = *np_h;
+  st = qp_grow(q->piece_desc, q->c_pdesc, np ? np : 1);
+  if (st == NICGPU_OK) st = qp_grow(q->piece_csum, q->c_pcs, np ? np : 1);
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
+                     q->plans, q->base, q->piece_desc);
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK && sums_stream != plan_stream) {  // the sums read the pieces the fill wrote
+    st = hip_status(hipEventRecord(q->planned, s));
+    if (st == NICGPU_OK) st = hip_status(hipStreamWaitEvent(static_cast<hipStream_t>(sums_stream), q->planned, 0));
+  }
+  if (st == NICGPU_OK && np) st = nicgpu_checksum_batch(mem, q->piece_desc, np, q->piece_csum, sums_stream);
+  *npieces = np;
+  qp_fill_view(q, view);
+  return st;
+}
+
+int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int* verdict, void* stream) {
+  if (!q || !verdict || ntx > q->cap_tx || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  *verdict = -1;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int st = hip_status(hipMemsetAsync(q->scal, 0, 2 * sizeof(unsigned long long), s));
+  if (st == NICGPU_OK && nrx) {
+    hipcub::TransformInputIterator<uint64_t, QpRxEnd, const nicgpu_rx_descriptor*> ends(q->rx, QpRxEnd{mem_size});
+    size_t tb = 0;
+    if (hipcub::DeviceScan::InclusiveScan(nullptr, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s) != hipSuccess)
+      return NICGPU_ERR_HIP;
+    st = qp_grow(q->tmp_chk, q->c_tmp_chk, tb);
+    if (st == NICGPU_OK)
+      st = hip_status(hipcub::DeviceScan::InclusiveScan(q->tmp_chk, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s));
+  }
+  if (st != NICGPU_OK) return st;
+  const uint64_t n = ntx > nrx ? ntx : nrx;
+  if (n) {
+    hipLaunchKernelGGL(qp_check_kernel, dim3(qp_grid(q, n)), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, q->rx,
+                       (uint64_t) nrx, mem_size, q->end_max, q->scal);
+    st = hip_status(hipGetLastError());
+  }
+  uint64_t* f = q->misc() + 1;
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(f, q->scal, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  if (st != NICGPU_OK) return st;
+  *verdict = f[0] ? -1 : (f[1] ? 0 : 1);
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_resolve_start(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu,
+                            uint16_t queue_id, void* stream) {
+  if (!q || ntx > q->cap_tx || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  q->res = nicgpu_qp::Pending{};
+  QpCtx C{queue_id, max_mtu, mem_size, q->plans, q->piece_csum, q->tx, q->rx, (uint64_t) nrx};
+  const unsigned grid = qp_grid(q, ntx + 1);
+  uint64_t* tail = q->partials + (size_t) grid * kQpStats;
+  // first guess: every packet pops what it needs (rx_need).  The final pass
+  // runs on it speculatively and reports the first packet that popped
+  // otherwise; a batch that settles at once (uniform RX descriptors, no early
+  // ends) needs no relaxation step and no host round trip before its DMA writes.
+  hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, (uint64_t) ntx, q->need,
+                     reinterpret_cast<unsigned long long*>(tail + 1));
+  int st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, (uint64_t) ntx, q->txc, q->rxc,
+                     q->writes, q->partials, q->need);
+  st = hip_status(hipGetLastError());
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_reduce_kernel, dim3(1), dim3(kQpReduceThreads), 0, s, q->partials, grid, q->pos,
+                     (uint64_t) ntx, true);
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->hp, tail, kQpTail * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipEventRecord(q->resolved, s));
+  if (st != NICGPU_OK) return st;
+  q->res = nicgpu_qp::Pending{true, mem_size, (uint64_t) ntx, (uint64_t) nrx, max_mtu, queue_id, s, grid};
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, uint64_t* rx_settled,
+                             nicgpu_qp_stats* stats) {
+  if (!q || !done || !rx_used || !stats || !q->res.on) return NICGPU_ERR_INVALID;
+  const nicgpu_qp::Pending R = q->res;
+  q->res.on = false;
+  DeviceGuard g(q->device);
+  hipStream_t s = R.s;
+  const uint64_t ntx = R.ntx;
+  QpCtx C{R.queue_id, R.max_mtu, R.mem_size, q->plans, q->piece_csum, q->tx, q->rx, R.nrx};
+  const unsigned grid = R.grid;
+  const uint64_t* part = q->hp;  // the tail, kQpTail words (page-locked)
+  uint64_t* tail = q->partials + (size_t) grid * kQpStats;
+  int st = hip_status(hipEventSynchronize(q->resolved));
+  if (st != NICGPU_OK) return st;
+  uint64_t used = part[0];
+  const unsigned long long first0 = (unsigned long long) part[1];
+  const uint64_t settled = part[2];
+  unsigned long long first = first0;
+  uint64_t lim = ntx;
+  if (first < ntx) {  // relax from the same guess (the speculative pass left `need` as it was)
+    // everything from here waits on the stream, behind whatever was enqueued
+    // after the start (a settled-prefix delivery reads none of what follows)
+    for (int it = 0; st == NICGPU_OK; ++it) {
+      if (it > 0) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
+      q->misc()[4] = ntx;  // page-locked source; the step below waits for the stream
+      if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->scal, q->misc() + 4, sizeof(uint64_t), hipMemcpyHostToDevice, s));
+      if (st != NICGPU_OK) break;
+      hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, ntx, q->scal);
+      st = hip_status(hipGetLastError());
+      if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->misc() + 3, q->scal, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+      if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+      if (st != NICGPU_OK) break;
+      first = (unsigned long long) q->misc()[3];
+      // pos is exact up to and including `first` (pops before it agreed)
+      lim = first < ntx ? (uint64_t) first : ntx;
+      if (first >= ntx || it + 1 == kQpRelaxSteps) break;
+    }
+    if (st == NICGPU_OK) {
+      hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, lim, q->txc, q->rxc, q->writes,
+                         q->partials, static_cast<const uint32_t*>(nullptr));
+      st = hip_status(hipGetLastError());
+    }
+    if (st == NICGPU_OK) {
+      hipLaunchKernelGGL(qp_reduce_kernel, dim3(1), dim3(kQpReduceThreads), 0, s, q->partials, grid, q->pos, ntx, false);
+      st = hip_status(hipGetLastError());
+    }
+    if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->hp, tail, kQpTail * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+    if (st != NICGPU_OK) return st;
+    used = part[0];
+  }
+  std::memcpy(stats, part + 3, kQpStats * sizeof(uint64_t));
+  *done = lim;
+  *rx_used = used;
+  if (rx_settled) *rx_settled = settled < used ? settled : used;
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu, uint16_t queue_id,
+                      uint64_t* done, uint64_t* rx_used, nicgpu_qp_stats* stats, void* stream) {
+  if (!q || !done || !rx_used || !stats) return NICGPU_ERR_INVALID;
+  const int st = nicgpu_qp_resolve_start(q, mem_size, ntx, nrx, max_mtu, queue_id, stream);
+  if (st != NICGPU_OK) return st;
+  return nicgpu_qp_resolve_finish(q, done, rx_used, nullptr, stats);
+}
+
+int nicgpu_qp_rss_list(nicgpu_qp* q, size_t nrx, void* stream) {
+  if (!q || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  q->delivered = false;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const unsigned grid = qp_grid(q, nrx + 1);
+  hipLaunchKernelGGL(qp_flag_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->rxc, (uint64_t) nrx, q->flags, q->rx_hash,
+                     q->rx_queue);
+  int st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = qp_scan(q, q->flags, q->at, nrx + 1, s);
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_rss_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->flags, q->at, q->writes, (uint64_t) nrx,
+                     q->rss_desc, q->which, q->scal + 3);
+  return hip_status(hipGetLastError());
+}
+
+int nicgpu_qp_group(nicgpu_qp* q, size_t nrx, size_t nq, void* stream) {
+  if (!q || nrx > q->cap_rx || nq > 65536) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int st = NICGPU_OK;
+  if (nq && (nq >= kWave || nrx == 0)) {  // the counting sort writes every queue's bounds itself
+    st = hip_status(hipMemsetAsync(q->queue_start, 0, nq * sizeof(uint32_t), s));
+    if (st == NICGPU_OK) st = hip_status(hipMemsetAsync(q->queue_end, 0, nq * sizeof(uint32_t), s));
+  }
+  if (st != NICGPU_OK || nrx == 0) return st;
+  // after nicgpu_qp_deliver: the queue of every completion (0xFFFF unless
+  // Success), in posting order, and the completion's own index as its entry;
+  // after nicgpu_qp_rss_list + scatter: the compacted Success frames
+  const uint16_t* keyq = q->delivered ? q->rx_queue : q->rss_queue;
+  const unsigned long long* cnt = q->delivered ? nullptr : reinterpret_cast<const unsigned long long*>(q->scal + 3);
+  const uint32_t* which = q->delivered ? nullptr : q->which;
+  if (nq < kWave) {  // counting sort: counts in sort_key, their scan in sorted_key (both hold nrx + 64)
+    const uint64_t T = (nrx + kWave - 1) / kWave;
+    const uint64_t nc = (uint64_t) (nq + 1) * T + 1;
+    st = qp_grow(q->sort_key, q->c_key, nc);
+    if (st == NICGPU_OK) st = qp_grow(q->sorted_key, q->c_sk, nc);
+    if (st != NICGPU_OK) return st;
+    const unsigned grid = qp_grid(q, nrx > nq ? nrx : nq);
+    hipLaunchKernelGGL(qp_gcount_kernel, dim3(grid), dim3(kQpBlock), 0, s, keyq, cnt, (uint64_t) nrx,
+                       (uint32_t) nq, T, q->sort_key);
+    st = hip_status(hipGetLastError());
+    if (st == NICGPU_OK) st = qp_scan(q, q->sort_key, q->sorted_key, nc, s);
+    if (st != NICGPU_OK) return st;
+    hipLaunchKernelGGL(qp_gscatter_kernel, dim3(grid), dim3(kQpBlock), 0, s, keyq, cnt,
+                       (uint64_t) nrx, (uint32_t) nq, T, q->sorted_key, which, q->queue_which, q->queue_start,
+                       q->queue_end);
+    return hip_status(hipGetLastError());
+  }
+  hipLaunchKernelGGL(qp_keys_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, keyq, cnt,
+                     (uint64_t) nrx, (uint32_t) nq, q->sort_key);
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK && q->delivered)  // the sort's values: each completion's index
+    hipLaunchKernelGGL(qp_iota_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->which, (uint64_t) nrx);
+  if (st == NICGPU_OK) st = hip_status(hipGetLastError());
+  if (st != NICGPU_OK) return st;
+  // stable: each queue keeps its completions in posting order.  Keys run
+  // 0..nq, so only their low bits are sorted (16 queues: 5 bits, one pass).
+  int end_bit = 1;
+  while ((1ull << end_bit) <= (unsigned long long) nq) ++end_bit;
+  size_t tb = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, q->sort_key, q->sorted_key, q->which, q->queue_which, (int) nrx,
+                                         0, end_bit, s) != hipSuccess)
+    return NICGPU_ERR_HIP;
+  st = qp_grow(q->tmp, q->c_tmp, tb);
+  if (st == NICGPU_OK)
+    st = hip_status(hipcub::DeviceRadixSort::SortPairs(q->tmp, tb, q->sort_key, q->sorted_key, q->which,
+                                                       q->queue_which, (int) nrx, 0, end_bit, s));
+  if (st != NICGPU_OK || nq == 0) return st;
+  hipLaunchKernelGGL(qp_bounds_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->sorted_key, cnt,
+                     (uint64_t) nrx, (uint64_t) nq, q->queue_start, q->queue_end);
+  return hip_status(hipGetLastError());
+}
+
+int nicgpu_qp_rss_scatter(nicgpu_qp* q, size_t nrx, void* stream) {
+  if (!q || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  if (nrx == 0) return NICGPU_OK;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(qp_scatter_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, q->which, q->rss_hash,
+                     q->rss_queue, q->scal + 3, q->rx_hash, q->rx_queue);
+  return hip_status(hipGetLastError());
+}
+
+
+int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx, const nicgpu_rss_ctx* ctx,
+                      int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint64_t* hits_dev, void* stream) {
+  return nicgpu_qp_deliver_range(q, mem, mem_size, 0, nrx, 0u, ctx, tuple_mode, raw_off, raw_len, hits_dev, stream);
+}
+
+int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t rx_begin, size_t rx_end,
+                            unsigned flags, const nicgpu_rss_ctx* ctx, int tuple_mode, uint32_t raw_off,
+                            uint32_t raw_len, uint64_t* hits_dev, void* stream) {
+  if (!q || rx_end > q->cap_rx || rx_begin > rx_end) return NICGPU_ERR_INVALID;
+  if (flags & ~(unsigned) (NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_APPEND)) return NICGPU_ERR_INVALID;
+  // the settled prefix of the resolve started last (its grid places the tail)
+  if ((flags & NICGPU_DELIVER_SETTLED) && !q->res.on) return NICGPU_ERR_INVALID;
+  if (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0)) return NICGPU_ERR_INVALID;
+  if (tuple_mode != NICGPU_TUPLE_NONE && tuple_mode != NICGPU_TUPLE_AUTO && tuple_mode != NICGPU_TUPLE_RAW)
+    return NICGPU_ERR_INVALID;
+  if (tuple_mode == NICGPU_TUPLE_RAW && (raw_off > NICGPU_RAW_MAX_END || raw_len > NICGPU_RAW_MAX_END ||
+                                         raw_off + raw_len > NICGPU_RAW_MAX_END))
+    return NICGPU_ERR_INVALID;
+  const bool rss = tuple_mode != NICGPU_TUPLE_NONE;
+  if (rss && (!ctx || ctx->table_n == 0 || !hits_dev || ctx->device != q->device)) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  q->delivered = rss;
+  int st = NICGPU_OK;
+  if (rss && !(flags & NICGPU_DELIVER_APPEND)) st = hip_status(hipMemsetAsync(q->scal + 3, 0, sizeof(uint64_t), s));
+  if (st != NICGPU_OK || rx_end == rx_begin) return st;
+  const DeviceInfo* di = nullptr;
+  st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  DeliverParams P{};
+  P.mem = mem;
+  P.mem_size = mem_size;
+  P.w = q->writes;
+  P.rxc = q->rxc;
+  P.j0 = rx_begin;
+  P.n = rx_end;
+  if (flags & NICGPU_DELIVER_SETTLED)
+    P.n_dev = reinterpret_cast<const unsigned long long*>(q->partials + (size_t) q->res.grid * kQpStats + 2);
+  P.rss.mode = tuple_mode;
+  P.rss.raw_off = raw_off;
+  P.rss.raw_len = raw_len;
+  if (rss) {
+    P.rss.lut = ctx->d_lut;
+    P.rss.table = ctx->d_table;
+    P.rss.table_n = (uint32_t) ctx->table_n;
+    P.rss.lut_words = 2u * (tuple_mode == NICGPU_TUPLE_RAW ? raw_len : 36u) * 16u;
+    P.rx_hash = q->rx_hash;
+    P.rx_queue = q->rx_queue;
+    P.hits = reinterpret_cast<unsigned long long*>(hits_dev);
+    P.count = reinterpret_cast<unsigned long long*>(q->scal + 3);
+#ifdef NICGPU_HIST_REP
+    if (P.rss.table_n <= (uint32_t) kHistLds) {
+      P.rss.hits_rep = ctx->d_rep;
+      P.rss.hits_done = ctx->d_done;
+    }
+#endif
+  }
+  const uint32_t hist_n = (rss && P.rss.table_n <= (uint32_t) kHistLds) ? P.rss.table_n : 0u;
+  const uint32_t table_words = (rss && P.rss.table_n <= (uint32_t) kTableLds) ? (P.rss.table_n + 1u) / 2u : 0u;
+  const uint32_t lds = dlv_block_bytes(rss, P.rss.lut_words, hist_n, table_words) + kDlvWpb * kDlvWaveBytes;
+  const int bpc = rss ? dlv_blocks_per_cu<true>(lds) : dlv_blocks_per_cu<false>(lds);
+  const uint64_t ntiles = (rx_end - rx_begin + kWave - 1) / kWave;
+  const uint64_t want = (ntiles + kDlvWpb - 1) / kDlvWpb;
+  // CUs left without a delivery block, so the next batch's plan and check
+  // (small launches on a side stream) find wave slots while this one runs
+  static const int reserve = [] {
+    const char* e = std::getenv("NICGPU_DLV_RESERVE_CUS");
+    return e ? std::atoi(e) : kDlvReserveCus;
+  }();
+  const uint64_t cus = (uint64_t) (di->cus > reserve + 8 ? di->cus - reserve : di->cus);
+  const uint64_t cap = cus * (uint64_t) bpc;
+  const unsigned grid = (unsigned) (want < cap ? want : cap);
+  if (rss) hipLaunchKernelGGL(deliver_kernel<true>, dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+  else hipLaunchKernelGGL(deliver_kernel<false>, dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+  return hip_status(hipGetLastError());
+}
+
+}  // extern "C"

@@ -1,7 +1,7 @@
 // qp_logic.h — the per-packet decisions of QueuePair::process_once
 // (src/queue_pair.cpp:67-460) for the batched RX stage, in one
 // source for both resolvers: the host one (host/rx_stage.cpp, fuzzed against
-// the compiled reference QueuePair) and the device one (nicgpu.hip).
+// the compiled reference QueuePair) and the device one (f1.hip).
 //
 // Plain templates over the descriptor, completion, write and stats types: the
 // nic:: types on the host, their nicgpu_* C mirrors on the device (same field

@@ -1,0 +1,204 @@
+// tune.hip — tuning-only entry points, built into libnicgpu_tune.so and never
+// into the product library: read-only streaming kernels that measure a box's
+// HBM read ceiling with the RX kernel's access width, and the FETCH_SIZE
+// calibration kernels (tools/calib_fetch.py).
+
+#include "common.h"
+#include "host.h"
+
+using namespace nicgpu_detail;
+
+namespace {
+template <int U>
+__global__ __launch_bounds__(256) void stream_read_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                          uint32_t* __restrict__ out, unsigned long long* stamps) {
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  uint32_t acc = 0;
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+  uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = add_halves(v[u].w, add_halves(v[u].z, add_halves(v[u].y, add_halves(v[u].x, acc))));
+  }
+  for (; i < n16; i += stride) {
+    u32x4 v = p[i];
+    acc = add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, acc))));
+  }
+  if (acc == 0x12345678u) out[0] = acc;  // keep the loads live
+  if (stamps != nullptr && (threadIdx.x & 63) == 0) {  // per wave, as the RX kernel's (tools/wave_stamps.py)
+    const uint64_t w = ((uint64_t) blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    stamps[4 * w + 0] = t_start;
+    stamps[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
+    stamps[4 * w + 2] = (unsigned) __builtin_amdgcn_s_getreg((3 << 11) | 20);
+    stamps[4 * w + 3] = (unsigned) __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  }
+}
+
+// lane l of a wave reads the 32-B pair (2l, 2l+1) of each 2-KiB step
+__global__ __launch_bounds__(256) void stream_read_pairs_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                                uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wid = ((uint64_t) blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nw = ((uint64_t) gridDim.x * blockDim.x) >> 6;
+  for (uint64_t step = wid; step * 128 + 127 < n16; step += nw) {
+    const u32x4* q = p + step * 128 + 2 * lane;
+    u32x4 a = __builtin_nontemporal_load(q);
+    u32x4 b = __builtin_nontemporal_load(q + 1);
+    acc = add_halves(a.w, add_halves(a.z, add_halves(a.y, add_halves(a.x, acc))));
+    acc = add_halves(b.w, add_halves(b.z, add_halves(b.y, add_halves(b.x, acc))));
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// tile-per-wave streaming (the RX kernel's access pattern without its compute):
+// wave w streams region [t*R, (t+1)*R) for tiles t = w, w + nwaves, ...; each
+// step every lane loads 16 B (1 KiB per wave), U steps in flight.
+template <int U>
+__global__ __launch_bounds__(256) void stream_read_tiles_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                                uint64_t tile16, uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wid = ((uint64_t) blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nw = ((uint64_t) gridDim.x * blockDim.x) >> 6;
+  const uint64_t ntiles = n16 / tile16;
+  for (uint64_t t = wid; t < ntiles; t += nw) {
+    const u32x4* q = p + t * tile16 + lane;
+    for (uint64_t st = 0; st + 64 * U <= tile16; st += 64 * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(q + st + 64 * u);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc = add_halves(v[u].w, add_halves(v[u].z, add_halves(v[u].y, add_halves(v[u].x, acc))));
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// block-cooperative tiles: the block's waves stream ONE tile together, wave w
+// reading KiB w of every (waves x 1 KiB) block step.
+template <int U>
+__global__ __launch_bounds__(256) void stream_read_btiles_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                                 uint64_t tile16, uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t ntiles = n16 / tile16;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const u32x4* q = p + t * tile16 + w * 64 + lane;
+    for (uint64_t st = 0; st + 256 * U <= tile16; st += 256 * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(q + st + 256 * u);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc = add_halves(v[u].w, add_halves(v[u].z, add_halves(v[u].y, add_halves(v[u].x, acc))));
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+}  // namespace
+
+extern "C" {
+int nicgpu_tune_stream_btiles(const uint8_t* buf, size_t bytes, size_t tile_bytes, int blocks_per_cu, int unroll,
+                              uint32_t* out, void* stream) {
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  const unsigned grid = (unsigned) (di->cus * (blocks_per_cu > 0 ? blocks_per_cu : 4));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const u32x4* p = reinterpret_cast<const u32x4*>(buf);
+  const uint64_t t16 = tile_bytes / 16;
+  if (unroll == 4) hipLaunchKernelGGL(stream_read_btiles_kernel<4>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  else if (unroll == 2) hipLaunchKernelGGL(stream_read_btiles_kernel<2>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  else hipLaunchKernelGGL(stream_read_btiles_kernel<1>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  return hip_status(hipGetLastError());
+}
+int nicgpu_tune_stream_tiles(const uint8_t* buf, size_t bytes, size_t tile_bytes, int blocks_per_cu, int unroll,
+                             uint32_t* out, void* stream) {
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  const unsigned grid = (unsigned) (di->cus * (blocks_per_cu > 0 ? blocks_per_cu : 4));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const u32x4* p = reinterpret_cast<const u32x4*>(buf);
+  const uint64_t t16 = tile_bytes / 16;
+  if (unroll == 4) hipLaunchKernelGGL(stream_read_tiles_kernel<4>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  else if (unroll == 2) hipLaunchKernelGGL(stream_read_tiles_kernel<2>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  else hipLaunchKernelGGL(stream_read_tiles_kernel<1>, dim3(grid), dim3(256), 0, s, p, bytes / 16, t16, out);
+  return hip_status(hipGetLastError());
+}
+// blocks_per_cu 0 = occupancy maximum; unroll in {1, 4, 8}
+int nicgpu_tune_stream_read(const uint8_t* buf, size_t bytes, int blocks_per_cu, int unroll, uint32_t* out,
+                            void* stream) {
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  const uint64_t n16 = bytes / 16;
+  const int bpc = blocks_per_cu > 0 ? blocks_per_cu : 8;
+  const unsigned grid = (unsigned) (di->cus * bpc);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const u32x4* p = reinterpret_cast<const u32x4*>(buf);
+  if (unroll == 2) hipLaunchKernelGGL(stream_read_pairs_kernel, dim3(grid), dim3(256), 0, s, p, n16, out);
+  else if (unroll == 8) hipLaunchKernelGGL(stream_read_kernel<8>, dim3(grid), dim3(256), 0, s, p, n16, out, g_tune_stamps);
+  else if (unroll == 4) hipLaunchKernelGGL(stream_read_kernel<4>, dim3(grid), dim3(256), 0, s, p, n16, out, g_tune_stamps);
+  else hipLaunchKernelGGL(stream_read_kernel<1>, dim3(grid), dim3(256), 0, s, p, n16, out, g_tune_stamps);
+  return hip_status(hipGetLastError());
+}
+// FETCH_SIZE calibration (MI355X_MICROARCH.md: the x2 correction holds for
+// 16-B/lane coalesced streaming reads only; "calibrate on a known byte count
+// in your own access pattern").  Each kernel reads a known set of whole
+// 128-B lines or line prefixes of `buf` in one access shape of this build:
+//   shape 0  coalesced 16 B per lane over the whole buffer (the RX stream)
+//   shape 1  lane-owned line walk: lane l reads its own 128-B lines, 16 B per
+//            load (ICRC: 64 different lines per wave instruction)
+//   shape 2  per-packet header gather: 48 B (3 x 16 B) at the start of every
+//            1536-B slot (rss_only_kernel's shape on C2 frames)
+//   shape 3  the same with 64 B (4 x 16 B) per slot
+//   shape 4  the same with 128 B (8 x 16 B, one whole line) per slot
+// tools/calib_fetch.py runs them under rocprofv3 --pmc FETCH_SIZE and divides
+// the bytes each shape must bring from HBM by what FETCH_SIZE reports.
+__global__ __launch_bounds__(256) void calib_kernel(int shape, const u32x4* __restrict__ p, uint64_t n16,
+                                                   uint32_t* __restrict__ out) {
+  const uint64_t tid = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  const uint64_t nthr = (uint64_t) gridDim.x * 256;
+  uint32_t acc = 0;
+  if (shape == 0) {
+    for (uint64_t i = tid; i < n16; i += nthr) {
+      const u32x4 v = __builtin_nontemporal_load(p + i);
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  } else if (shape == 1) {
+    const uint64_t nlines = n16 / 8;
+    for (uint64_t l = tid; l < nlines; l += nthr) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const u32x4 v = p[l * 8 + k];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+      }
+    }
+  } else {
+    const int nk = shape == 2 ? 3 : (shape == 3 ? 4 : 8);
+    const uint64_t nslot = n16 / 96;  // 1536-B slots
+    for (uint64_t q = tid; q < nslot; q += nthr) {
+      for (int k = 0; k < nk; ++k) {
+        const u32x4 v = p[q * 96 + k];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+      }
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;  // keeps the loads
+}
+
+int nicgpu_tune_calib(int shape, const uint8_t* buf, size_t bytes, uint32_t* out, void* stream) {
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  if (shape < 0 || shape > 4) return NICGPU_ERR_INVALID;
+  const unsigned grid = (unsigned) (di->cus * 8);
+  hipLaunchKernelGGL(calib_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), shape,
+                     reinterpret_cast<const u32x4*>(buf), (uint64_t) (bytes / 16), out);
+  return hip_status(hipGetLastError());
+}
+}  // extern "C"

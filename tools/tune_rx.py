@@ -36,8 +36,6 @@ def main():
     ap.add_argument("--xpf", type=int, default=-1, help="XPF variants: prefetch tiles of at most this many chunks")
     ap.add_argument("--bpcs", default="0", help="comma list of RX blocks-per-CU caps to A/B per variant "
                     "(nicgpu_tune_set_bpc; 0 = occupancy maximum)")
-    ap.add_argument("--dbg", default="", help="comma list of tuning knob masks to time as extra rows "
-                    "(1 no header stage, 2 no hash, 4 no hash/queue/hits stores; outputs wrong)")
     args = ap.parse_args()
 
     import torch
@@ -145,22 +143,6 @@ def main():
                     torch.cuda.synchronize()
                     bucket[v] += [e[i].elapsed_time(e[i + 1]) * 1e3 for i in range(args.iters)]
         res = {}
-        if args.dbg:
-            tl.nicgpu_tune_set_dbg.argtypes = [u32]
-            for bits in [int(x) for x in args.dbg.split(",")]:
-                tl.nicgpu_tune_set_dbg(bits)
-                ts_dbg = []
-                for r in range(args.rounds):
-                    run(variants[0])
-                    e = [torch.cuda.Event(enable_timing=True) for _ in range(args.iters + 1)]
-                    e[0].record()
-                    for i in range(args.iters):
-                        run(variants[0])
-                        e[i + 1].record()
-                    torch.cuda.synchronize()
-                    ts_dbg += [e[i].elapsed_time(e[i + 1]) * 1e3 for i in range(args.iters)]
-                tl.nicgpu_tune_set_dbg(0)
-                res[f"{names[variants[0]]}_dbg{bits}"] = {"us_median": round(float(np.median(ts_dbg)), 2)}
         for v in variants:
             med = float(np.median(times[v])) if times[v] else float("nan")
             medc = float(np.median(times_csum[v])) if times_csum[v] else float("nan")

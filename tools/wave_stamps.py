@@ -35,7 +35,6 @@ def main():
     ap.add_argument("--launches", type=int, default=5)
     ap.add_argument("--stream", action="store_true", help="stamp the read-ceiling kernel instead of the RX kernel")
     ap.add_argument("--bpc", type=int, default=0, help="RX blocks-per-CU cap (nicgpu_tune_set_bpc; 0 = occupancy maximum)")
-    ap.add_argument("--dbg", type=int, default=0, help="nicgpu_tune_set_dbg bits for the stamped launches (8192: rotate)")
     args = ap.parse_args()
 
     import torch
@@ -50,8 +49,6 @@ def main():
     tl.nicgpu_tune_set_stamps.argtypes = [vp]
     tl.nicgpu_tune_stream_read.restype = i32
     tl.nicgpu_tune_stream_read.argtypes = [vp, sz, i32, i32, vp, vp]
-    tl.nicgpu_tune_set_dbg.argtypes = [u32]
-    tl.nicgpu_tune_set_dbg(args.dbg)
     tl.nicgpu_tune_set_bpc.argtypes = [u32]
     tl.nicgpu_tune_set_bpc(args.bpc)
     tl.nicgpu_tune_variant_name.restype = ctypes.c_char_p
@@ -129,7 +126,7 @@ def main():
                 "tail_last10pct_us": round(span - q(end, 0.9), 1), "per_xcd": per_xcd,
             })
         best = int(np.argmin(spans))
-        out = {"workload": w, "kernel": "stream_read<4>" if args.stream else "rx", "dbg": args.dbg, "bpc": args.bpc, "variant": tl.nicgpu_tune_variant_name(args.variant).decode(), "packets": int(n),
+        out = {"workload": w, "kernel": "stream_read<4>" if args.stream else "rx", "bpc": args.bpc, "variant": tl.nicgpu_tune_variant_name(args.variant).decode(), "packets": int(n),
                "bytes": int(lens.sum()), "spans_us": [round(x, 1) for x in spans], "best": rows[best]}
         print(json.dumps(out), flush=True)
         del f, d
