@@ -146,7 +146,12 @@ struct DeliverParams {
   uint16_t* rx_queue;
   unsigned long long* hits;
   unsigned long long* count;
+  uint64_t alt_dst;  // tuning (kDlvPackedDst): destination = src_a + alt_dst
 };
+
+// Tuning-only modes of deliver_kernel (libnicgpu_tune.so, tools/f1_deliver_bench.py;
+// results are wrong with any set): attribute the delivery's time.
+constexpr int kDlvNoStore = 1, kDlvNoLoad = 2, kDlvNoHash = 4, kDlvPackedDst = 8, kDlvNoDrain = 16;
 
 #ifndef NICGPU_DLV_WPB
 #define NICGPU_DLV_WPB 8
@@ -195,7 +200,7 @@ __device__ __forceinline__ void dlv_store(uint8_t* mem, uint64_t D, uint64_t lo,
   }
 }
 
-template <bool RSS>
+template <bool RSS, int MODE = 0>
 __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu(4, 8))) void deliver_kernel(DeliverParams P) {
   constexpr uint32_t kThreads = kWave * kDlvWpb;
   extern __shared__ uint4 lds_dyn[];
@@ -243,6 +248,7 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
     if (j < n) {
       wr = P.w[j];
       if (RSS) flag = P.rxc[j].status == nicqp::kSuccess;
+      if constexpr ((MODE & kDlvPackedDst) != 0) wr.dst = wr.src_a + P.alt_dst;
     }
     const uint64_t plen = wr.prefix_len == 4 ? 4 : 0;
     const uint64_t total = plen + wr.len_a + wr.len_b;
@@ -336,7 +342,10 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
             const int64_t a = (int64_t) D + ((int64_t) src - (int64_t) d);
             const int64_t a4 = a & ~(int64_t) 3;
             pk[u] |= (uint32_t) (a & 3) << 16;
-            if (a4 >= 0 && (uint64_t) a4 + 20 <= P.mem_size) {
+            if constexpr ((MODE & kDlvNoLoad) != 0) {
+#pragma unroll
+              for (int i = 0; i < 5; ++i) vv[u][i] = (uint32_t) a4 * 0x9E3779B1u + i;
+            } else if (a4 >= 0 && (uint64_t) a4 + 20 <= P.mem_size) {
               __builtin_memcpy(vv[u], P.mem + a4, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
               // the fifth dword only for a shifted window (equal alignment of
               // source and destination, the common case, needs four)
@@ -365,8 +374,12 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
         uint32_t o[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = sh ? __builtin_amdgcn_alignbyte(vv[u][i + 1], vv[u][i], sh) : vv[u][i];
-        dlv_store(P.mem, D, lo, hi, o);
-        if (RSS) {
+        if constexpr ((MODE & kDlvNoStore) != 0) {
+          if ((o[0] ^ o[1] ^ o[2] ^ o[3]) == 0x12345678u && lo == D + 3) P.mem[D] = 0;  // keeps the loads
+        } else {
+          dlv_store(P.mem, D, lo, hi, o);
+        }
+        if (RSS && (MODE & kDlvNoHash) == 0) {
           const uint32_t q = pk[u] >> 20;
           const uint64_t wd = wdst[q];
           const uint64_t kc = Dc[u] - (wd & ~(1ull << 63));
@@ -382,10 +395,10 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
         }
       }
     }
-    if (RSS) {
+    if (RSS && (MODE & kDlvNoHash) == 0) {
       // the frames' bytes are in the stage; bytes past it come from the frame
       // this wave just wrote (its stores retired first)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr ((MODE & kDlvNoDrain) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       if (j < n) {
@@ -425,6 +438,28 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
 template <bool RSS>
 int dlv_blocks_per_cu(uint32_t lds) {
   return blocks_per_cu(reinterpret_cast<const void*>(deliver_kernel<RSS>), kWave * kDlvWpb, lds);
+}
+
+template <int MODE>
+int launch_deliver(const DeliverParams& P, bool rss, int cus_total, hipStream_t s) {
+  const uint32_t hist_n = (rss && P.rss.table_n <= (uint32_t) kHistLds) ? P.rss.table_n : 0u;
+  const uint32_t table_words = (rss && P.rss.table_n <= (uint32_t) kTableLds) ? (P.rss.table_n + 1u) / 2u : 0u;
+  const uint32_t lds = dlv_block_bytes(rss, P.rss.lut_words, hist_n, table_words) + kDlvWpb * kDlvWaveBytes;
+  const int bpc = rss ? dlv_blocks_per_cu<true>(lds) : dlv_blocks_per_cu<false>(lds);
+  const uint64_t ntiles = (P.n - P.j0 + kWave - 1) / kWave;
+  const uint64_t want = (ntiles + kDlvWpb - 1) / kDlvWpb;
+  // CUs left without a delivery block, so the next batch's plan and check
+  // (small launches on a side stream) find wave slots while this one runs
+  static const int reserve = [] {
+    const char* e = std::getenv("NICGPU_DLV_RESERVE_CUS");
+    return e ? std::atoi(e) : kDlvReserveCus;
+  }();
+  const uint64_t cus = (uint64_t) (cus_total > reserve + 8 ? cus_total - reserve : cus_total);
+  const uint64_t cap = cus * (uint64_t) bpc;
+  const unsigned grid = (unsigned) (want < cap ? want : cap);
+  if (rss) hipLaunchKernelGGL((deliver_kernel<true, MODE>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+  else hipLaunchKernelGGL((deliver_kernel<false, MODE>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+  return hip_status(hipGetLastError());
 }
 
 }  // namespace
@@ -1309,24 +1344,53 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
     }
 #endif
   }
-  const uint32_t hist_n = (rss && P.rss.table_n <= (uint32_t) kHistLds) ? P.rss.table_n : 0u;
-  const uint32_t table_words = (rss && P.rss.table_n <= (uint32_t) kTableLds) ? (P.rss.table_n + 1u) / 2u : 0u;
-  const uint32_t lds = dlv_block_bytes(rss, P.rss.lut_words, hist_n, table_words) + kDlvWpb * kDlvWaveBytes;
-  const int bpc = rss ? dlv_blocks_per_cu<true>(lds) : dlv_blocks_per_cu<false>(lds);
-  const uint64_t ntiles = (rx_end - rx_begin + kWave - 1) / kWave;
-  const uint64_t want = (ntiles + kDlvWpb - 1) / kDlvWpb;
-  // CUs left without a delivery block, so the next batch's plan and check
-  // (small launches on a side stream) find wave slots while this one runs
-  static const int reserve = [] {
-    const char* e = std::getenv("NICGPU_DLV_RESERVE_CUS");
-    return e ? std::atoi(e) : kDlvReserveCus;
-  }();
-  const uint64_t cus = (uint64_t) (di->cus > reserve + 8 ? di->cus - reserve : di->cus);
-  const uint64_t cap = cus * (uint64_t) bpc;
-  const unsigned grid = (unsigned) (want < cap ? want : cap);
-  if (rss) hipLaunchKernelGGL(deliver_kernel<true>, dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
-  else hipLaunchKernelGGL(deliver_kernel<false>, dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
-  return hip_status(hipGetLastError());
+  return launch_deliver<0>(P, rss, di->cus, s);
 }
 
 }  // extern "C"
+
+#ifdef NICGPU_TUNING
+// tools/f1_deliver_bench.py: one delivery launch over a caller-built write
+// list in a timing-only mode (kDlv*; 0 = production), RSS when ctx is given.
+extern "C" int nicgpu_tune_deliver(int mode, uint8_t* mem, uint64_t mem_size, const nicgpu_segment_write* w,
+                                   const nicgpu_completion* rxc, size_t n, const nicgpu_rss_ctx* ctx,
+                                   uint32_t* rx_hash, uint16_t* rx_queue, uint64_t* hits, uint64_t* count,
+                                   uint64_t alt_dst, void* stream) {
+  if (n == 0) return NICGPU_OK;
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  DeliverParams P{};
+  P.mem = mem;
+  P.mem_size = mem_size;
+  P.w = w;
+  P.rxc = rxc;
+  P.j0 = 0;
+  P.n = n;
+  P.alt_dst = alt_dst;
+  const bool rss = ctx != nullptr;
+  P.rss.mode = rss ? NICGPU_TUPLE_AUTO : NICGPU_TUPLE_NONE;
+  if (rss) {
+    P.rss.lut = ctx->d_lut;
+    P.rss.table = ctx->d_table;
+    P.rss.table_n = (uint32_t) ctx->table_n;
+    P.rss.lut_words = 2u * 36u * 16u;
+    P.rx_hash = rx_hash;
+    P.rx_queue = rx_queue;
+    P.hits = reinterpret_cast<unsigned long long*>(hits);
+    P.count = reinterpret_cast<unsigned long long*>(count);
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (mode) {
+    case 0: return launch_deliver<0>(P, rss, di->cus, s);
+    case kDlvNoStore: return launch_deliver<kDlvNoStore>(P, rss, di->cus, s);
+    case kDlvNoLoad: return launch_deliver<kDlvNoLoad>(P, rss, di->cus, s);
+    case kDlvNoHash: return launch_deliver<kDlvNoHash>(P, rss, di->cus, s);
+    case kDlvPackedDst: return launch_deliver<kDlvPackedDst>(P, rss, di->cus, s);
+    case kDlvNoDrain: return launch_deliver<kDlvNoDrain>(P, rss, di->cus, s);
+    case kDlvNoLoad | kDlvNoHash: return launch_deliver<kDlvNoLoad | kDlvNoHash>(P, rss, di->cus, s);
+    case kDlvNoStore | kDlvNoHash: return launch_deliver<kDlvNoStore | kDlvNoHash>(P, rss, di->cus, s);
+    default: return NICGPU_ERR_INVALID;
+  }
+}
+#endif  // NICGPU_TUNING
