@@ -229,17 +229,19 @@ struct HdrView {
   }
 };
 
-// One byte of packet l at packet offset o: LDS when staged, else global.
-__device__ __forceinline__ uint32_t pkt_byte(const HdrView& hv, uint32_t lo, const uint8_t* __restrict__ pkt,
-                                             uint32_t o) {
+// One byte of packet l at packet offset o: LDS when staged, else pkt[o] —
+// a pointer to the packet, or (deliver_kernel) an accessor of the packet's
+// source parts.
+template <class Pkt>
+__device__ __forceinline__ uint32_t pkt_byte(const HdrView& hv, uint32_t lo, const Pkt& pkt, uint32_t o) {
   uint32_t a = lo + o;
   if (a < (uint32_t) kHdrBytes) return hv.byte(a);
   return pkt[o];
 }
 
+template <class Pkt>
 __device__ __forceinline__ uint32_t hash_bytes(uint32_t h, const uint32_t* lut, const HdrView& hdr_l, uint32_t lo,
-                                               const uint8_t* __restrict__ pkt, uint32_t src, uint32_t cnt,
-                                               uint32_t pos) {
+                                               const Pkt& pkt, uint32_t src, uint32_t cnt, uint32_t pos) {
   for (uint32_t i = 0; i < cnt; ++i) {
     uint32_t b = pkt_byte(hdr_l, lo, pkt, src + i);
     uint32_t p = 2 * (pos + i);
@@ -355,8 +357,9 @@ __device__ __forceinline__ uint32_t range_sum_le(const HdrView& stage_w, const u
 }
 
 // Tuple extraction + Toeplitz for one packet (oracle/oracle.c oracle_extract_tuple).
+template <class Pkt>
 __device__ __forceinline__ uint32_t rss_hash_packet(const RxParams& P, const uint32_t* lut, const HdrView& hdr_l,
-                                                    uint32_t lo, const uint8_t* __restrict__ pkt, uint32_t len) {
+                                                    uint32_t lo, const Pkt& pkt, uint32_t len) {
   uint32_t h = 0;
   if (P.mode == NICGPU_TUPLE_RAW) {
     uint32_t cnt = 0;

@@ -151,22 +151,24 @@ struct DeliverParams {
 
 // Tuning-only modes of deliver_kernel (libnicgpu_tune.so, tools/f1_deliver_bench.py;
 // results are wrong with any set): attribute the delivery's time.
-constexpr int kDlvNoStore = 1, kDlvNoLoad = 2, kDlvNoHash = 4, kDlvPackedDst = 8, kDlvNoDrain = 16;
+constexpr int kDlvNoStore = 1, kDlvNoLoad = 2, kDlvNoHash = 4, kDlvPackedDst = 8, kDlvNoDrain = 16, kDlvV1 = 32;
 
 #ifndef NICGPU_DLV_WPB
 #define NICGPU_DLV_WPB 8
 #endif
 #ifndef NICGPU_DLV_U
-#define NICGPU_DLV_U 4
+#define NICGPU_DLV_U 2
 #endif
 #ifndef NICGPU_DLV_RESERVE
 #define NICGPU_DLV_RESERVE 0
 #endif
 constexpr int kDlvReserveCus = NICGPU_DLV_RESERVE;  // default of NICGPU_DLV_RESERVE_CUS (tuning)
 constexpr int kDlvWpb = NICGPU_DLV_WPB;  // waves per block
-constexpr int kDlvU = NICGPU_DLV_U;      // 64-entry sub-steps per step (loads in flight per lane)
+constexpr int kDlvU = NICGPU_DLV_U;      // 64-entry sub-steps per step (two steps in flight: loads and stores)
+static_assert(kDlvU <= 4, "marks area");
 constexpr uint32_t kDlvRec = 24;  // item record: dst u64 | src (or prefix word) u64 | len u32 | first entry u32
-constexpr uint32_t kDlvMarks = (kWave * kDlvU + 15u) & ~15u;  // bytes: one u8 mark per stream entry (item id + 1 <= 192)
+constexpr int kDlvU1 = 4;  // round 3's kernel (deliver_v1_kernel, tuning builds): sub-steps per step
+constexpr uint32_t kDlvMarks = (uint32_t) kWave * 4u;  // bytes: one u8 mark per stream entry (item id + 1 <= 192), U <= 4
 constexpr uint32_t kDlvWaveBytes = kDlvMarks + 64u * 8u + 192u * kDlvRec + 64u * kHdrStride * 16u;  // marks|wdst|items|stage
 
 // block part: RSS LUT | histogram | table (as rss_only_kernel), then 16 B for the Success count
@@ -200,8 +202,343 @@ __device__ __forceinline__ void dlv_store(uint8_t* mem, uint64_t D, uint64_t lo,
   }
 }
 
+// The source parts of a delivered frame, as rss_hash_packet reads bytes past
+// the LDS header stage: frame byte o is the VLAN prefix word's byte o (o <
+// plen), else part A's, else part B's.  Sources are TX buffers, which the
+// device path's overlap check keeps apart from every RX buffer of the batch,
+// so they hold the frame's bytes while this wave's stores are in flight.
+struct FrameParts {
+  const uint8_t* mem;
+  uint64_t src_a, src_b;
+  uint32_t prefix, plen, len_a;
+  __device__ __forceinline__ uint32_t operator[](uint32_t o) const {
+    if (o < plen) return (prefix >> (8 * o)) & 0xFFu;
+    o -= plen;
+    return o < len_a ? (uint32_t) mem[src_a + o] : (uint32_t) mem[src_b + (o - len_a)];
+  }
+};
+
+// One step of the stream held between its loads and its stores: kDlvU x 64
+// entries, per entry the destination chunk (chunk index < 2^32: images below
+// 64 GiB, checked at launch), one packed word and five source dwords.  Every
+// load is unconditional: dummy entries (past the stream's end, VLAN prefix
+// items) read the image start, and a window leaving the image is read from
+// inside it and rebuilt in the store phase (images of at least 64 B; smaller
+// ones are written byte by byte).
+struct DlvStep {
+  uint32_t dc[kDlvU];     // destination chunk; ~0: no entry
+  uint32_t pk[kDlvU];     // lo - D (0-4) | hi - D (8-12) | shift (16-17) | write q (20-25) | item k (26-27) | window dword shift + 4 (28-31)
+  uint32_t vv[kDlvU][5];  // source dwords of the 4-aligned window (clamped into the image)
+};
+
+// Software-pipelined delivery: step s+1's loads are issued before step s's
+// stores, so every wave has loads in flight while its stores drain (round 3's
+// kernel issued each step's loads after the previous step's stores, and on
+// gfx950 a load's vmcnt wait also covers every store issued before it: its
+// time was the loads' plus the stores', 85 + 145 us of a 236-us C3 batch,
+// tools/f1_deliver_bench.py).  The loads are unconditional (DlvStep) so hipcc
+// keeps counted vmcnt waits.
+// RSS hashes from the LDS header stage at the tile end without draining the
+// stores: bytes past the stage come from the sources (FrameParts).
 template <bool RSS, int MODE = 0>
 __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu(4, 8))) void deliver_kernel(DeliverParams P) {
+  constexpr uint32_t kThreads = kWave * kDlvWpb;
+  constexpr uint32_t kSpan = kWave * kDlvU;
+  extern __shared__ uint4 lds_dyn[];
+  const uint32_t w = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
+  const uint32_t lane = lane_id();
+  const RxParams& R = P.rss;
+  const bool hist_lds = RSS && R.table_n <= (uint32_t) kHistLds;
+  const bool table_lds = RSS && R.table_n <= (uint32_t) kTableLds;
+  uint8_t* base_b = reinterpret_cast<uint8_t*>(lds_dyn);
+  uint32_t* lut = reinterpret_cast<uint32_t*>(base_b);
+  uint32_t* hist = lut + (RSS ? R.lut_words : 0u);
+  uint16_t* table_s = reinterpret_cast<uint16_t*>(hist + (hist_lds ? R.table_n : 0u));
+  const uint32_t block_bytes = dlv_block_bytes(RSS, R.lut_words, hist_lds ? R.table_n : 0u,
+                                               table_lds ? (R.table_n + 1u) / 2u : 0u);
+  uint32_t* cnt_s = reinterpret_cast<uint32_t*>(base_b + block_bytes - 16u);
+  uint8_t* wave_b = base_b + block_bytes + w * kDlvWaveBytes;
+  uint8_t* marks = wave_b;
+  uint64_t* wdst = reinterpret_cast<uint64_t*>(wave_b + kDlvMarks);
+  uint8_t* items = wave_b + kDlvMarks + 512u;
+  uint4* stage = reinterpret_cast<uint4*>(items + 192u * kDlvRec);
+  if (RSS) {
+    for (uint32_t i = threadIdx.x; i < R.lut_words; i += kThreads) lut[i] = R.lut[i];
+    if (hist_lds)
+      for (uint32_t i = threadIdx.x; i < R.table_n; i += kThreads) hist[i] = 0;
+    if (table_lds)
+      for (uint32_t i = threadIdx.x; i < R.table_n; i += kThreads) table_s[i] = R.table[i];
+    if (threadIdx.x == 0) *cnt_s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t) kHdrChunks; ++k) stage[hdr_slot(lane, k)] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  __syncthreads();
+  uint64_t n = P.n;
+  if (P.n_dev) {
+    const uint64_t m = *P.n_dev;
+    n = m < n ? m : n;
+  }
+  const uint64_t ntiles = n > P.j0 ? (n - P.j0 + kWave - 1) / kWave : 0;
+  const uint64_t nwaves = (uint64_t) gridDim.x * kDlvWpb;
+  const uint64_t msize = P.mem_size;
+  uint32_t my_count = 0;
+  // images below 64 B take the byte-wise path (no 20-B windows to clamp into)
+  const bool tiny = msize < 64;
+  for (uint64_t tile = (uint64_t) blockIdx.x * kDlvWpb + w; tile < ntiles; tile += nwaves) {
+    // ---- this lane's write: its items and their stream entries
+    const uint64_t j = P.j0 + tile * kWave + lane;
+    uint32_t F, c0, c1, c2, total_e;
+    bool flag;
+    {
+      nicgpu_segment_write wr{};
+      flag = false;
+      if (j < n) {
+        wr = P.w[j];
+        if (RSS) flag = P.rxc[j].status == nicqp::kSuccess;
+        if constexpr ((MODE & kDlvPackedDst) != 0) wr.dst = wr.src_a + P.alt_dst;
+      }
+      const uint64_t plen = wr.prefix_len == 4 ? 4 : 0;
+      const uint64_t total = plen + wr.len_a + wr.len_b;
+      // entries outside the image are skipped (the host validated them); the
+      // chunk indices are 32-bit (images below 64 GiB, nicgpu_qp_deliver_range)
+      const bool ok = j < n && !(wr.prefix_len > 4 || wr.dst > msize || total > msize - wr.dst ||
+                                   wr.src_a > msize || wr.len_a > msize - wr.src_a ||
+                                   wr.src_b > msize || wr.len_b > msize - wr.src_b);
+      flag = flag && ok;
+      const uint64_t d1 = wr.dst + plen, d2 = d1 + wr.len_a;
+      c0 = ok ? dlv_chunks(wr.dst, plen) : 0u;
+      c1 = ok ? dlv_chunks(d1, wr.len_a) : 0u;
+      c2 = ok ? dlv_chunks(d2, wr.len_b) : 0u;
+      const uint32_t cw = c0 + c1 + c2;
+      const uint32_t incl = wave_incl_scan(cw);
+      F = incl - cw;
+      total_e = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
+      // item records: k 0 = VLAN prefix (src = the prefix word), 1 = part A, 2 = part B
+      auto put = [&](uint32_t k, uint64_t d, uint64_t src, uint32_t len, uint32_t first) __attribute__((always_inline)) {
+        uint8_t* r = items + (lane * 3u + k) * kDlvRec;
+        *reinterpret_cast<uint64_t*>(r) = d;
+        *reinterpret_cast<uint64_t*>(r + 8) = src;
+        *reinterpret_cast<uint32_t*>(r + 16) = len;
+        *reinterpret_cast<uint32_t*>(r + 20) = first;
+      };
+      // (lengths kept for the hash even for items without chunks: ok frames only)
+      put(0, wr.dst, wr.prefix, ok ? (uint32_t) plen : 0u, F);
+      put(1, d1, wr.src_a, ok ? wr.len_a : 0u, F + c0);
+      put(2, d2, wr.src_b, ok ? wr.len_b : 0u, F + c0 + c1);
+      wdst[lane] = (wr.dst >> 4) | (flag ? 1ull << 63 : 0ull);
+    }
+    if (tiny) {
+      // byte by byte, one lane per write (images below 64 B only)
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      for (uint32_t k = 0; k < 3u; ++k) {
+        const uint8_t* r = items + (lane * 3u + k) * kDlvRec;
+        const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
+        const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
+        const uint32_t len = (c0 + c1 + c2) ? *reinterpret_cast<const uint32_t*>(r + 16) : 0u;
+        for (uint32_t i = 0; i < len; ++i) {
+          const uint32_t b = k == 0u ? (uint32_t) (src >> (8 * i)) & 0xFFu : (uint32_t) P.mem[src + i];
+          P.mem[d + i] = (uint8_t) b;
+          const uint64_t kc = ((d + i) >> 4) - (wdst[lane] & ~(1ull << 63));
+          if (RSS && flag && kc < (uint64_t) kHdrChunks)
+            reinterpret_cast<uint8_t*>(stage + hdr_slot(lane, (uint32_t) kc))[(d + i) & 15u] = (uint8_t) b;
+        }
+      }
+      total_e = 0;
+    }
+    uint32_t carry = 0;  // item (id + 1) of the entry before the step being planned
+    // ---- load phase of the step at stream position W: entries, windows, loads
+    auto plan = [&](DlvStep& S, uint32_t W) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) marks[u * kWave + lane] = 0u;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (c0 && F >= W && F - W < kSpan) marks[F - W] = (uint8_t) (lane * 3u + 1u);
+      if (c1 && F + c0 >= W && F + c0 - W < kSpan) marks[F + c0 - W] = (uint8_t) (lane * 3u + 2u);
+      if (c2 && F + c0 + c1 >= W && F + c0 + c1 - W < kSpan) marks[F + c0 + c1 - W] = (uint8_t) (lane * 3u + 3u);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) {
+        uint32_t it = wave_incl_max(marks[u * kWave + lane]);
+        it = it > carry ? it : carry;
+        carry = (uint32_t) __builtin_amdgcn_readlane((int) it, 63);
+        const uint32_t pos = W + (uint32_t) u * kWave + lane;
+        const bool valid = pos < total_e;
+        const uint32_t id = valid ? it - 1u : 0u, q = id / 3u, k = id - 3u * q;
+        const uint8_t* r = items + id * kDlvRec;
+        const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
+        const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
+        const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
+        const uint32_t first = *reinterpret_cast<const uint32_t*>(r + 20);
+        const uint64_t D = ((d >> 4) + (pos - first)) << 4;
+        const uint64_t lo = D > d ? D : d;
+        const uint64_t hi = D + 16 < d + len ? D + 16 : d + len;
+        // source of destination byte D: before the item's source by up to
+        // 15 bytes on its first chunk, so possibly below address 0 (signed);
+        // a window leaving the image is read from inside it (`sd` dwords
+        // away, -4..5) and rebuilt in the store phase
+        const int64_t a = (int64_t) D + ((int64_t) src - (int64_t) d);
+        const int64_t a4 = a & ~(int64_t) 3;
+        const int64_t top = (int64_t) ((msize - 20) & ~3ull);
+        const int64_t la = k == 0u ? 0 : (a4 < 0 ? 0 : (a4 > top ? top : a4));
+        const int32_t sd = (int32_t) ((a4 - la) >> 2);  // window dword i = loaded dword i + sd
+        S.dc[u] = valid ? (uint32_t) (D >> 4) : 0xFFFFFFFFu;
+        S.pk[u] = (uint32_t) (lo - D) | ((uint32_t) (hi - D) << 8) | ((uint32_t) (a & 3) << 16) |
+                  ((uint32_t) (k == 0u ? 0 : sd + 4) << 28) | (q << 20) | (k << 26);
+        const uint8_t* lp = P.mem + la;
+        if constexpr ((MODE & kDlvNoLoad) != 0) {
+#pragma unroll
+          for (int i = 0; i < 5; ++i) S.vv[u][i] = (uint32_t) la * 0x9E3779B1u + i;
+        } else {
+          __builtin_memcpy(S.vv[u], lp, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
+          S.vv[u][4] = *reinterpret_cast<const uint32_t*>(lp + 16);
+        }
+      }
+    };
+    // ---- store phase: the entries' bytes (prefix and clamped windows
+    // rebuilt here), stores, and the header stage of Success frames
+    auto store = [&](const DlvStep& S) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) {
+        if (S.dc[u] == 0xFFFFFFFFu) continue;
+        const uint32_t pk = S.pk[u];
+        const uint64_t D = (uint64_t) S.dc[u] << 4, lo = D + (pk & 31u), hi = D + ((pk >> 8) & 31u);
+        const uint32_t q = (pk >> 20) & 63u, k = (pk >> 26) & 3u;
+        const int32_t sd = (int32_t) (pk >> 28) - 4;
+        uint32_t v[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) v[i] = S.vv[u][i];
+        if (sd < 0) {  // rare: a window starting before the image, read from its start
+#pragma unroll
+          for (int i = 0; i < 5; ++i) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int m = 0; m < 5; ++m)
+              if (i + sd == m) x = S.vv[u][m];
+            v[i] = x;
+          }
+        } else if (sd > 0) {  // rare: a window past the image end: bytes inside it, byte by byte
+          const int64_t a4 = (int64_t) ((msize - 20) & ~3ull) + 4 * sd;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb) {
+              const uint64_t e = (uint64_t) (a4 + 4 * i + bb);
+              if (e < msize) x |= (uint32_t) P.mem[e] << (8 * bb);
+            }
+            v[i] = x;
+          }
+        }
+        if (k == 0u) {  // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): its 4 bytes at d
+          const uint8_t* r = items + (3u * q) * kDlvRec;
+          const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
+          const uint32_t pw = *reinterpret_cast<const uint32_t*>(r + 8);
+          const int32_t rel = (int32_t) (d - D);  // prefix byte b sits at chunk byte rel + b
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb) {
+              const int32_t pb = 4 * i + bb - rel;
+              if (pb >= 0 && pb < 4) x |= ((pw >> (8 * pb)) & 0xFFu) << (8 * bb);
+            }
+            v[i] = x;
+          }
+        }
+        const uint32_t sh = k == 0u ? 0u : (pk >> 16) & 3u;
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = sh ? __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh) : v[i];
+        if constexpr ((MODE & kDlvNoStore) != 0) {
+          if ((o[0] ^ o[1] ^ o[2] ^ o[3]) == 0x12345678u && lo == D + 3) P.mem[D] = 0;  // keeps the loads
+        } else {
+          dlv_store(P.mem, D, lo, hi, o);
+        }
+        if (RSS && (MODE & kDlvNoHash) == 0) {
+          const uint64_t wd = wdst[q];
+          const uint64_t kc = (uint64_t) S.dc[u] - (wd & ~(1ull << 63));
+          if ((wd >> 63) && kc < (uint64_t) kHdrChunks) {
+            uint32_t* st = reinterpret_cast<uint32_t*>(stage + hdr_slot(q, (uint32_t) kc));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uint64_t ad = D + 4u * i;
+              const int b0 = lo > ad ? (int) (lo - ad) : 0, b1 = hi < ad + 4 ? (int) (hi - ad) : 4;
+              if (b1 > b0) atomicOr(st + i, o[i] & dword_keep(b0, b1, 0));
+            }
+          }
+        }
+      }
+    };
+    // ---- the stream, ping-pong over pairs of steps (a counted loop with its
+    // only exit at the bottom, as the RX kernel's: hipcc then keeps counted
+    // vmcnt waits); the plan past the last step loads dummies only
+    const uint32_t nsteps = (total_e + kSpan - 1) / kSpan;
+    DlvStep A, B;
+    if (nsteps) plan(A, 0);
+    uint32_t s = 0;
+    for (; s + 1 < nsteps; s += 2) {
+      plan(B, (s + 1) * kSpan);
+      __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's stores
+      store(A);
+      plan(A, (s + 2) * kSpan);
+      __builtin_amdgcn_sched_barrier(0);
+      store(B);
+    }
+    if (s < nsteps) store(A);
+    if (RSS && (MODE & kDlvNoHash) == 0) {
+      // the frames' header bytes are in the stage (LDS, in order within the
+      // wave); bytes past it come from the sources — no wait for the stores
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (j < n) {
+        if (flag) {
+          const uint8_t* r = items + (lane * 3u) * kDlvRec;
+          const uint64_t dst = *reinterpret_cast<const uint64_t*>(r);
+          const uint32_t pw = *reinterpret_cast<const uint32_t*>(r + 8);
+          const uint32_t plen = *reinterpret_cast<const uint32_t*>(r + 16);
+          const uint64_t src_a = *reinterpret_cast<const uint64_t*>(r + kDlvRec + 8);
+          const uint32_t len_a = *reinterpret_cast<const uint32_t*>(r + kDlvRec + 16);
+          const uint64_t src_b = *reinterpret_cast<const uint64_t*>(r + 2 * kDlvRec + 8);
+          const uint32_t len_b = *reinterpret_cast<const uint32_t*>(r + 2 * kDlvRec + 16);
+          uint64_t len = (uint64_t) plen + len_a + len_b;
+          if (len > NICGPU_MAX_PACKET) len = NICGPU_MAX_PACKET;  // the tuple lies in the first 82 B
+          const FrameParts fp{P.mem, src_a, src_b, pw, plen, len_a};
+          const uint32_t h = rss_hash_packet(R, lut, HdrView{stage, lane}, (uint32_t) (dst & 15u), fp, (uint32_t) len);
+          const uint32_t idx = h % R.table_n;
+          P.rx_hash[j] = h;
+          P.rx_queue[j] = table_lds ? table_s[idx] : R.table[idx];
+          if (hist_lds) atomicAdd(&hist[idx], 1u);
+          else atomicAdd(&P.hits[idx], 1ull);
+          ++my_count;
+        } else {
+          P.rx_hash[j] = 0u;
+          P.rx_queue[j] = 0xFFFFu;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+      for (uint32_t k = 0; k < (uint32_t) kHdrChunks; ++k) stage[hdr_slot(lane, k)] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  if (RSS) {
+    const uint32_t c = (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan(my_count), 63);
+    if (lane == 0 && c) atomicAdd(cnt_s, c);
+    __syncthreads();
+    if (threadIdx.x == 0 && *cnt_s) atomicAdd(P.count, (unsigned long long) *cnt_s);
+    if (hist_lds) flush_hist(hist, R.table_n, P.hits, R.hits_rep, R.hits_done, kThreads);
+  }
+}
+
+#ifdef NICGPU_TUNING
+// round 3's delivery (each step's loads after the previous step's stores,
+// a vmcnt(0) drain before the hash), for the A/B of tools/f1_deliver_bench.py
+template <bool RSS, int MODE = 0>
+__global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu(4, 8))) void deliver_v1_kernel(DeliverParams P) {
   constexpr uint32_t kThreads = kWave * kDlvWpb;
   extern __shared__ uint4 lds_dyn[];
   const uint32_t w = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
@@ -275,23 +612,23 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
     put(1, d1, wr.src_a, c1 ? wr.len_a : 0u, F + c0);
     put(2, d2, wr.src_b, c2 ? wr.len_b : 0u, F + c0 + c1);
     wdst[lane] = (wr.dst >> 4) | (flag && ok ? 1ull << 63 : 0ull);
-    // ---- the stream: kDlvU x 64 entries per step, every load of the step
+    // ---- the stream: kDlvU1 x 64 entries per step, every load of the step
     // issued before its first store (one memory latency per step)
     uint32_t carry = 0;  // item (id + 1) of the entry before this step
-    for (uint32_t W = 0; W < total_e; W += kWave * kDlvU) {
+    for (uint32_t W = 0; W < total_e; W += kWave * kDlvU1) {
 #pragma unroll
-      for (int u = 0; u < kDlvU; ++u) marks[u * kWave + lane] = 0u;
+      for (int u = 0; u < kDlvU1; ++u) marks[u * kWave + lane] = 0u;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      constexpr uint32_t kSpan = kWave * kDlvU;
+      constexpr uint32_t kSpan = kWave * kDlvU1;
       if (c0 && F >= W && F - W < kSpan) marks[F - W] = (uint8_t) (lane * 3u + 1u);
       if (c1 && F + c0 >= W && F + c0 - W < kSpan) marks[F + c0 - W] = (uint8_t) (lane * 3u + 2u);
       if (c2 && F + c0 + c1 >= W && F + c0 + c1 - W < kSpan) marks[F + c0 + c1 - W] = (uint8_t) (lane * 3u + 3u);
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      uint32_t itv[kDlvU];
+      uint32_t itv[kDlvU1];
 #pragma unroll
-      for (int u = 0; u < kDlvU; ++u) {
+      for (int u = 0; u < kDlvU1; ++u) {
         uint32_t it = wave_incl_max(marks[u * kWave + lane]);
         it = it > carry ? it : carry;
         carry = (uint32_t) __builtin_amdgcn_readlane((int) it, 63);
@@ -300,13 +637,13 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
       // phase A: every entry's chunk, item and source window; loads issued.
       // Per entry: the destination chunk, one packed word (bytes [lo, hi) of
       // the chunk, source shift, owning write) and five source dwords — a
-      // prefix item's 4 bytes are placed into them here — so that kDlvU
+      // prefix item's 4 bytes are placed into them here — so that kDlvU1
       // entries' loads fit in flight per lane.
-      uint64_t Dc[kDlvU];  // destination chunk index; ~0: no entry
-      uint32_t pk[kDlvU];  // lo - D (bits 0-4) | hi - D (8-12) | shift (16-17) | write q (20-25)
-      uint32_t vv[kDlvU][5];
+      uint64_t Dc[kDlvU1];  // destination chunk index; ~0: no entry
+      uint32_t pk[kDlvU1];  // lo - D (bits 0-4) | hi - D (8-12) | shift (16-17) | write q (20-25)
+      uint32_t vv[kDlvU1][5];
 #pragma unroll
-      for (int u = 0; u < kDlvU; ++u) {
+      for (int u = 0; u < kDlvU1; ++u) {
         const uint32_t pos = W + (uint32_t) u * kWave + lane;
         Dc[u] = ~0ull;
         pk[u] = 0;
@@ -367,7 +704,7 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
       }
       // phase B: align, store, and the header stage of Success frames
 #pragma unroll
-      for (int u = 0; u < kDlvU; ++u) {
+      for (int u = 0; u < kDlvU1; ++u) {
         if (Dc[u] == ~0ull) continue;
         const uint64_t D = Dc[u] << 4, lo = D + (pk[u] & 31u), hi = D + ((pk[u] >> 8) & 31u);
         const uint32_t sh = (pk[u] >> 16) & 3u;
@@ -434,6 +771,7 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
     if (hist_lds) flush_hist(hist, R.table_n, P.hits, R.hits_rep, R.hits_done, kThreads);
   }
 }
+#endif  // NICGPU_TUNING
 
 template <bool RSS>
 int dlv_blocks_per_cu(uint32_t lds) {
@@ -457,6 +795,13 @@ int launch_deliver(const DeliverParams& P, bool rss, int cus_total, hipStream_t 
   const uint64_t cus = (uint64_t) (cus_total > reserve + 8 ? cus_total - reserve : cus_total);
   const uint64_t cap = cus * (uint64_t) bpc;
   const unsigned grid = (unsigned) (want < cap ? want : cap);
+#ifdef NICGPU_TUNING
+  if constexpr ((MODE & kDlvV1) != 0) {
+    if (rss) hipLaunchKernelGGL((deliver_v1_kernel<true, MODE & ~kDlvV1>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+    else hipLaunchKernelGGL((deliver_v1_kernel<false, MODE & ~kDlvV1>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+    return hip_status(hipGetLastError());
+  }
+#endif
   if (rss) hipLaunchKernelGGL((deliver_kernel<true, MODE>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
   else hipLaunchKernelGGL((deliver_kernel<false, MODE>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
   return hip_status(hipGetLastError());
@@ -1387,9 +1732,11 @@ extern "C" int nicgpu_tune_deliver(int mode, uint8_t* mem, uint64_t mem_size, co
     case kDlvNoLoad: return launch_deliver<kDlvNoLoad>(P, rss, di->cus, s);
     case kDlvNoHash: return launch_deliver<kDlvNoHash>(P, rss, di->cus, s);
     case kDlvPackedDst: return launch_deliver<kDlvPackedDst>(P, rss, di->cus, s);
-    case kDlvNoDrain: return launch_deliver<kDlvNoDrain>(P, rss, di->cus, s);
     case kDlvNoLoad | kDlvNoHash: return launch_deliver<kDlvNoLoad | kDlvNoHash>(P, rss, di->cus, s);
     case kDlvNoStore | kDlvNoHash: return launch_deliver<kDlvNoStore | kDlvNoHash>(P, rss, di->cus, s);
+    case kDlvV1: return launch_deliver<kDlvV1>(P, rss, di->cus, s);
+    case kDlvV1 | kDlvNoStore | kDlvNoHash: return launch_deliver<kDlvV1 | kDlvNoStore | kDlvNoHash>(P, rss, di->cus, s);
+    case kDlvV1 | kDlvNoLoad | kDlvNoHash: return launch_deliver<kDlvV1 | kDlvNoLoad | kDlvNoHash>(P, rss, di->cus, s);
     default: return NICGPU_ERR_INVALID;
   }
 }

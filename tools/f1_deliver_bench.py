@@ -11,8 +11,8 @@ one process, rounds interleaved:
   no_rss           the same writes without RSS (deliver_kernel<false>)
   mode N           tuning modes of deliver_kernel (f1.hip kDlv*; outputs wrong):
                    1 no stores, 2 no loads, 4 no hash, 8 packed destinations
-                   (the frames written contiguously, as the source), 16 no drain
-                   before the hash
+                   (the frames written contiguously, as the source); 32 round 3's
+                   kernel (deliver_v1_kernel), 32|1|4 and 32|2|4 its loads / stores alone
   gather           nicgpu_segment_gather (one wave per write) over the same list
   copy_packed      torch copy of the TX bytes to a packed destination (a plain
                    device copy of the same bytes: the copy ceiling)
@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--slot", type=int, default=2048)
-    ap.add_argument("--modes", default="0,1,2,4,8,16,6,5")
+    ap.add_argument("--modes", default="0,1,2,4,8,6,5,32,37,38")
     args = ap.parse_args()
 
     import torch
