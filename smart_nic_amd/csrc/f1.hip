@@ -156,19 +156,15 @@ constexpr int kDlvNoStore = 1, kDlvNoLoad = 2, kDlvNoHash = 4, kDlvPackedDst = 8
 #ifndef NICGPU_DLV_WPB
 #define NICGPU_DLV_WPB 8
 #endif
-#ifndef NICGPU_DLV_U
-#define NICGPU_DLV_U 2
-#endif
 #ifndef NICGPU_DLV_RESERVE
 #define NICGPU_DLV_RESERVE 0
 #endif
 constexpr int kDlvReserveCus = NICGPU_DLV_RESERVE;  // default of NICGPU_DLV_RESERVE_CUS (tuning)
 constexpr int kDlvWpb = NICGPU_DLV_WPB;  // waves per block
-constexpr int kDlvU = NICGPU_DLV_U;      // 64-entry sub-steps per step (two steps in flight: loads and stores)
-static_assert(kDlvU <= 4, "marks area");
+// round 3's kernel (deliver_v1_kernel, tuning builds only): sub-steps per step, records, per-wave LDS
+constexpr int kDlvU1 = 4;
 constexpr uint32_t kDlvRec = 24;  // item record: dst u64 | src (or prefix word) u64 | len u32 | first entry u32
-constexpr int kDlvU1 = 4;  // round 3's kernel (deliver_v1_kernel, tuning builds): sub-steps per step
-constexpr uint32_t kDlvMarks = (uint32_t) kWave * 4u;  // bytes: one u8 mark per stream entry (item id + 1 <= 192), U <= 4
+constexpr uint32_t kDlvMarks = (uint32_t) kWave * kDlvU1;  // bytes: one u8 mark per stream entry (item id + 1 <= 192)
 constexpr uint32_t kDlvWaveBytes = kDlvMarks + 64u * 8u + 192u * kDlvRec + 64u * kHdrStride * 16u;  // marks|wdst|items|stage
 
 // block part: RSS LUT | histogram | table (as rss_only_kernel), then 16 B for the Success count
@@ -218,35 +214,77 @@ struct FrameParts {
   }
 };
 
-// One step of the stream held between its loads and its stores: kDlvU x 64
-// entries, per entry the destination chunk (chunk index < 2^32: images below
-// 64 GiB, checked at launch), one packed word and five source dwords.  Every
-// load is unconditional: dummy entries (past the stream's end, VLAN prefix
-// items) read the image start, and a window leaving the image is read from
+// Stores bytes [x, y) (0 <= x < y <= 16, not the whole chunk) of the 16-B
+// destination chunk at D from o, in at most seven store instructions per
+// wave whatever the lanes' ranges (byte, short, three dwords, short, byte at
+// per-lane addresses): a partial chunk then costs a wave seven exec-masked
+// stores, not the 20 of a per-byte walk (round 3: more than half of the
+// delivery's store instructions, SQ_INSTS_VMEM_WR).
+__device__ __forceinline__ uint32_t chunk_word_at(const uint32_t* o, uint32_t p) {  // chunk bytes p..p+3 (p < 16)
+  const uint32_t i = p >> 2;
+  const uint32_t lo = i == 0u ? o[0] : i == 1u ? o[1] : i == 2u ? o[2] : o[3];
+  const uint32_t hi = i == 0u ? o[1] : i == 1u ? o[2] : i == 2u ? o[3] : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, p & 3u);
+}
+__device__ __forceinline__ void dlv_store_partial(uint8_t* mem, uint64_t D, uint32_t x, uint32_t y, const uint32_t* o) {
+  uint32_t p = x;
+  if ((p & 1u) && p < y) {
+    mem[D + p] = (uint8_t) chunk_word_at(o, p);
+    ++p;
+  }
+  if ((p & 2u) && p + 2u <= y) {
+    *reinterpret_cast<uint16_t*>(mem + D + p) = (uint16_t) chunk_word_at(o, p);
+    p += 2u;
+  }
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+    if (p + 4u <= y) {
+      *reinterpret_cast<uint32_t*>(mem + D + p) = chunk_word_at(o, p);
+      p += 4u;
+    }
+  if (p + 2u <= y) {
+    *reinterpret_cast<uint16_t*>(mem + D + p) = (uint16_t) chunk_word_at(o, p);
+    p += 2u;
+  }
+  if (p < y) mem[D + p] = (uint8_t) chunk_word_at(o, p);
+}
+
+// ---- delivery by 8-lane groups --------------------------------------------
+// Round 3's stream mapped every 16-B chunk to its write through LDS marks, a
+// DPP prefix-max and item lookups: ~375 wave-instructions per KiB moved, 60 M
+// VALU per C3 batch (SQ_INSTS_VALU), 87 us of a 234-us launch with neither
+// loads nor stores (tools/f1_deliver_bench.py mode 7).  Here a wave's 64 lanes
+// are 8 groups of 8; a group copies ONE 128-B destination line of one frame
+// per step (lane i its chunk i), so a line's bytes leave in one store
+// instruction and the per-chunk work is an address and a window.  Groups take
+// the tile's writes from a wave-level queue (ballot + popcount) as they finish
+// one.  A write's lines run over its items (VLAN prefix, part A, part B) in
+// order.  Steps are pipelined kDlvDepth deep: step s + kDlvDepth - 1 is planned
+// and its loads issued before step s's stores.
+constexpr int kDlvDepth = 4;          // steps in flight per wave
+constexpr uint32_t kDlvItemRec = 24;  // item: dst u64 | src (prefix word) u64 | len u32 | first line u32
+// per wave: items[64][3] | wmeta[64] {lines u32, first line of A u16, of B u16} | wdst[64] u64 | order[64] u8 | stage
+constexpr uint32_t kDlvWaveBytes3 = 64u * 3u * kDlvItemRec + 64u * 8u + 64u * 8u + 64u + 64u * kHdrStride * 16u;
+
+// One step held between its loads and its stores: one destination chunk per
+// lane.  Every load is unconditional: lanes without a chunk and VLAN prefix
+// items read the image start, and a window leaving the image is read from
 // inside it and rebuilt in the store phase (images of at least 64 B; smaller
 // ones are written byte by byte).
 struct DlvStep {
-  uint32_t dc[kDlvU];     // destination chunk; ~0: no entry
-  uint32_t pk[kDlvU];     // lo - D (0-4) | hi - D (8-12) | shift (16-17) | write q (20-25) | item k (26-27) | window dword shift + 4 (28-31)
-  uint32_t vv[kDlvU][5];  // source dwords of the 4-aligned window (clamped into the image)
+  uint64_t D;     // destination chunk address
+  uint32_t pk;    // lo - D (0-4) | hi - D (5-9) | shift (10-11) | write w (12-17) | header chunk kc (18-19, 3 none) |
+                  // prefix item (20) | window dword shift + 4 (21-24) | valid (25)
+  uint32_t vv[5]; // source dwords of the 4-aligned window
 };
 
-// Software-pipelined delivery: step s+1's loads are issued before step s's
-// stores, so every wave has loads in flight while its stores drain (round 3's
-// kernel issued each step's loads after the previous step's stores, and on
-// gfx950 a load's vmcnt wait also covers every store issued before it: its
-// time was the loads' plus the stores', 85 + 145 us of a 236-us C3 batch,
-// tools/f1_deliver_bench.py).  The loads are unconditional (DlvStep) so hipcc
-// keeps counted vmcnt waits.
-// RSS hashes from the LDS header stage at the tile end without draining the
-// stores: bytes past the stage come from the sources (FrameParts).
 template <bool RSS, int MODE = 0>
 __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu(4, 8))) void deliver_kernel(DeliverParams P) {
   constexpr uint32_t kThreads = kWave * kDlvWpb;
-  constexpr uint32_t kSpan = kWave * kDlvU;
   extern __shared__ uint4 lds_dyn[];
   const uint32_t w = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
   const uint32_t lane = lane_id();
+  const uint32_t grp = lane >> 3, gi = lane & 7u;
   const RxParams& R = P.rss;
   const bool hist_lds = RSS && R.table_n <= (uint32_t) kHistLds;
   const bool table_lds = RSS && R.table_n <= (uint32_t) kTableLds;
@@ -257,11 +295,12 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
   const uint32_t block_bytes = dlv_block_bytes(RSS, R.lut_words, hist_lds ? R.table_n : 0u,
                                                table_lds ? (R.table_n + 1u) / 2u : 0u);
   uint32_t* cnt_s = reinterpret_cast<uint32_t*>(base_b + block_bytes - 16u);
-  uint8_t* wave_b = base_b + block_bytes + w * kDlvWaveBytes;
-  uint8_t* marks = wave_b;
-  uint64_t* wdst = reinterpret_cast<uint64_t*>(wave_b + kDlvMarks);
-  uint8_t* items = wave_b + kDlvMarks + 512u;
-  uint4* stage = reinterpret_cast<uint4*>(items + 192u * kDlvRec);
+  uint8_t* wave_b = base_b + block_bytes + w * kDlvWaveBytes3;
+  uint8_t* items = wave_b;
+  uint2* wmeta = reinterpret_cast<uint2*>(items + 64u * 3u * kDlvItemRec);
+  uint64_t* wdst = reinterpret_cast<uint64_t*>(wmeta + 64);
+  uint8_t* order = reinterpret_cast<uint8_t*>(wdst + 64);
+  uint4* stage = reinterpret_cast<uint4*>(order + 64);
   if (RSS) {
     for (uint32_t i = threadIdx.x; i < R.lut_words; i += kThreads) lut[i] = R.lut[i];
     if (hist_lds)
@@ -281,14 +320,15 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
   const uint64_t ntiles = n > P.j0 ? (n - P.j0 + kWave - 1) / kWave : 0;
   const uint64_t nwaves = (uint64_t) gridDim.x * kDlvWpb;
   const uint64_t msize = P.mem_size;
+  const int64_t top = (int64_t) ((msize - 20) & ~3ull);  // last 4-aligned 20-B window inside the image
   uint32_t my_count = 0;
   // images below 64 B take the byte-wise path (no 20-B windows to clamp into)
   const bool tiny = msize < 64;
   for (uint64_t tile = (uint64_t) blockIdx.x * kDlvWpb + w; tile < ntiles; tile += nwaves) {
-    // ---- this lane's write: its items and their stream entries
+    // ---- this lane's write: items, lines, queue order
     const uint64_t j = P.j0 + tile * kWave + lane;
-    uint32_t F, c0, c1, c2, total_e;
     bool flag;
+    uint32_t nq;  // writes with lines, in the queue
     {
       nicgpu_segment_write wr{};
       flag = false;
@@ -299,43 +339,45 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
       }
       const uint64_t plen = wr.prefix_len == 4 ? 4 : 0;
       const uint64_t total = plen + wr.len_a + wr.len_b;
-      // entries outside the image are skipped (the host validated them); the
-      // chunk indices are 32-bit (images below 64 GiB, nicgpu_qp_deliver_range)
+      // entries outside the image are skipped (the host validated them)
       const bool ok = j < n && !(wr.prefix_len > 4 || wr.dst > msize || total > msize - wr.dst ||
                                    wr.src_a > msize || wr.len_a > msize - wr.src_a ||
                                    wr.src_b > msize || wr.len_b > msize - wr.src_b);
       flag = flag && ok;
       const uint64_t d1 = wr.dst + plen, d2 = d1 + wr.len_a;
-      c0 = ok ? dlv_chunks(wr.dst, plen) : 0u;
-      c1 = ok ? dlv_chunks(d1, wr.len_a) : 0u;
-      c2 = ok ? dlv_chunks(d2, wr.len_b) : 0u;
-      const uint32_t cw = c0 + c1 + c2;
-      const uint32_t incl = wave_incl_scan(cw);
-      F = incl - cw;
-      total_e = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
-      // item records: k 0 = VLAN prefix (src = the prefix word), 1 = part A, 2 = part B
+      auto lines = [](uint64_t d, uint64_t len) -> uint32_t {
+        return len ? (uint32_t) (((d + len - 1) >> 7) - (d >> 7) + 1) : 0u;
+      };
+      const uint32_t n0 = ok ? lines(wr.dst, plen) : 0u;
+      const uint32_t n1 = ok ? lines(d1, wr.len_a) : 0u;
+      const uint32_t n2 = ok ? lines(d2, wr.len_b) : 0u;
       auto put = [&](uint32_t k, uint64_t d, uint64_t src, uint32_t len, uint32_t first) __attribute__((always_inline)) {
-        uint8_t* r = items + (lane * 3u + k) * kDlvRec;
+        uint8_t* r = items + (lane * 3u + k) * kDlvItemRec;
         *reinterpret_cast<uint64_t*>(r) = d;
         *reinterpret_cast<uint64_t*>(r + 8) = src;
         *reinterpret_cast<uint32_t*>(r + 16) = len;
         *reinterpret_cast<uint32_t*>(r + 20) = first;
       };
-      // (lengths kept for the hash even for items without chunks: ok frames only)
-      put(0, wr.dst, wr.prefix, ok ? (uint32_t) plen : 0u, F);
-      put(1, d1, wr.src_a, ok ? wr.len_a : 0u, F + c0);
-      put(2, d2, wr.src_b, ok ? wr.len_b : 0u, F + c0 + c1);
+      put(0, wr.dst, wr.prefix, ok ? (uint32_t) plen : 0u, 0u);
+      put(1, d1, wr.src_a, ok ? wr.len_a : 0u, n0);
+      put(2, d2, wr.src_b, ok ? wr.len_b : 0u, n0 + n1);
+      const uint32_t nl = n0 + n1 + n2;
+      wmeta[lane] = make_uint2(nl, (n0 & 0xFFFFu) | ((n0 + n1) << 16));
       wdst[lane] = (wr.dst >> 4) | (flag ? 1ull << 63 : 0ull);
+      const uint64_t has = __ballot(nl != 0u);
+      if (nl) order[__builtin_amdgcn_mbcnt_hi((uint32_t) (has >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) has, 0u))] = (uint8_t) lane;
+      nq = (uint32_t) __builtin_popcountll(has);
+      if (tiny) nq = 0;
     }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     if (tiny) {
       // byte by byte, one lane per write (images below 64 B only)
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       for (uint32_t k = 0; k < 3u; ++k) {
-        const uint8_t* r = items + (lane * 3u + k) * kDlvRec;
+        const uint8_t* r = items + (lane * 3u + k) * kDlvItemRec;
         const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
         const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
-        const uint32_t len = (c0 + c1 + c2) ? *reinterpret_cast<const uint32_t*>(r + 16) : 0u;
+        const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
         for (uint32_t i = 0; i < len; ++i) {
           const uint32_t b = k == 0u ? (uint32_t) (src >> (8 * i)) & 0xFFu : (uint32_t) P.mem[src + i];
           P.mem[d + i] = (uint8_t) b;
@@ -344,149 +386,181 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
             reinterpret_cast<uint8_t*>(stage + hdr_slot(lane, (uint32_t) kc))[(d + i) & 15u] = (uint8_t) b;
         }
       }
-      total_e = 0;
     }
-    uint32_t carry = 0;  // item (id + 1) of the entry before the step being planned
-    // ---- load phase of the step at stream position W: entries, windows, loads
-    auto plan = [&](DlvStep& S, uint32_t W) __attribute__((always_inline)) {
-#pragma unroll
-      for (int u = 0; u < kDlvU; ++u) marks[u * kWave + lane] = 0u;
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      if (c0 && F >= W && F - W < kSpan) marks[F - W] = (uint8_t) (lane * 3u + 1u);
-      if (c1 && F + c0 >= W && F + c0 - W < kSpan) marks[F + c0 - W] = (uint8_t) (lane * 3u + 2u);
-      if (c2 && F + c0 + c1 >= W && F + c0 + c1 - W < kSpan) marks[F + c0 + c1 - W] = (uint8_t) (lane * 3u + 3u);
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#pragma unroll
-      for (int u = 0; u < kDlvU; ++u) {
-        uint32_t it = wave_incl_max(marks[u * kWave + lane]);
-        it = it > carry ? it : carry;
-        carry = (uint32_t) __builtin_amdgcn_readlane((int) it, 63);
-        const uint32_t pos = W + (uint32_t) u * kWave + lane;
-        const bool valid = pos < total_e;
-        const uint32_t id = valid ? it - 1u : 0u, q = id / 3u, k = id - 3u * q;
-        const uint8_t* r = items + id * kDlvRec;
-        const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
-        const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
-        const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
-        const uint32_t first = *reinterpret_cast<const uint32_t*>(r + 20);
-        const uint64_t D = ((d >> 4) + (pos - first)) << 4;
-        const uint64_t lo = D > d ? D : d;
-        const uint64_t hi = D + 16 < d + len ? D + 16 : d + len;
-        // source of destination byte D: before the item's source by up to
-        // 15 bytes on its first chunk, so possibly below address 0 (signed);
-        // a window leaving the image is read from inside it (`sd` dwords
-        // away, -4..5) and rebuilt in the store phase
-        const int64_t a = (int64_t) D + ((int64_t) src - (int64_t) d);
-        const int64_t a4 = a & ~(int64_t) 3;
-        const int64_t top = (int64_t) ((msize - 20) & ~3ull);
-        const int64_t la = k == 0u ? 0 : (a4 < 0 ? 0 : (a4 > top ? top : a4));
-        const int32_t sd = (int32_t) ((a4 - la) >> 2);  // window dword i = loaded dword i + sd
-        S.dc[u] = valid ? (uint32_t) (D >> 4) : 0xFFFFFFFFu;
-        S.pk[u] = (uint32_t) (lo - D) | ((uint32_t) (hi - D) << 8) | ((uint32_t) (a & 3) << 16) |
-                  ((uint32_t) (k == 0u ? 0 : sd + 4) << 28) | (q << 20) | (k << 26);
-        const uint8_t* lp = P.mem + la;
-        if constexpr ((MODE & kDlvNoLoad) != 0) {
-#pragma unroll
-          for (int i = 0; i < 5; ++i) S.vv[u][i] = (uint32_t) la * 0x9E3779B1u + i;
-        } else {
-          __builtin_memcpy(S.vv[u], lp, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
-          S.vv[u][4] = *reinterpret_cast<const uint32_t*>(lp + 16);
-        }
+    // ---- the groups' queue: group state (write gw, its line t of nl; the
+    // first lines of its items A and B), refilled from order[] as groups finish
+    uint32_t next = 8u < nq ? 8u : nq;  // wave-uniform: queue position
+    uint32_t gw = 64u, t = 0, nl = 0, f1 = 0, f2 = 0;
+    auto take = [&](uint32_t qpos) __attribute__((always_inline)) {
+      gw = qpos < nq ? (uint32_t) order[qpos] : 64u;
+      t = 0;
+      if (gw < 64u) {
+        const uint2 m = wmeta[gw];
+        nl = m.x;
+        f1 = m.y & 0xFFFFu;
+        f2 = m.y >> 16;
       }
     };
-    // ---- store phase: the entries' bytes (prefix and clamped windows
-    // rebuilt here), stores, and the header stage of Success frames
+    take(grp);
+    // ---- load phase of one step: this lane's chunk of its group's line
+    auto plan = [&](DlvStep& S) __attribute__((always_inline)) {
+      const bool active = gw < 64u;
+      const uint32_t k = t >= f2 ? 2u : (t >= f1 ? 1u : 0u);
+      const uint32_t wi = active ? gw : 0u;
+      const uint8_t* r = items + (wi * 3u + k) * kDlvItemRec;
+      const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
+      const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
+      const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
+      const uint32_t first = *reinterpret_cast<const uint32_t*>(r + 20);
+      const uint64_t D = ((((d >> 7) + (t - first)) << 3) + gi) << 4;
+      const uint64_t lo = D > d ? D : d;
+      const uint64_t hi = D + 16 < d + len ? D + 16 : d + len;
+      const bool valid = active && lo < hi;
+      const uint64_t kc64 = (D >> 4) - (wdst[wi] & ~(1ull << 63));
+      const uint32_t kc = (RSS && (wdst[wi] >> 63) && kc64 < (uint64_t) kHdrChunks) ? (uint32_t) kc64 : 3u;
+      // source of destination byte D: before the item's source by up to 15
+      // bytes on its first chunk, so possibly below address 0 (signed); a
+      // window leaving the image is read from inside it (sd dwords away)
+      const int64_t a = (int64_t) D + ((int64_t) src - (int64_t) d);
+      const int64_t a4 = a & ~(int64_t) 3;
+      const int64_t la = (!valid || k == 0u) ? 0 : (a4 < 0 ? 0 : (a4 > top ? top : a4));
+      const int32_t sd = (!valid || k == 0u) ? 0 : (int32_t) ((a4 - la) >> 2);
+      S.D = D;
+      S.pk = (valid ? (uint32_t) (lo - D) | ((uint32_t) (hi - D) << 5) : 0u) | ((uint32_t) (a & 3) << 10) |
+             (wi << 12) | (kc << 18) | ((uint32_t) (k == 0u) << 20) | ((uint32_t) (sd + 4) << 21) |
+             ((uint32_t) valid << 25);
+      const uint8_t* lp = P.mem + la;
+      if constexpr ((MODE & kDlvNoLoad) != 0) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) S.vv[i] = (uint32_t) la * 0x9E3779B1u + i;
+      } else {
+        __builtin_memcpy(S.vv, lp, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
+        S.vv[4] = *reinterpret_cast<const uint32_t*>(lp + 16);
+      }
+      // advance the group; groups past their write's last line take the next
+      // write of the queue, in group order
+      ++t;
+      const bool done = active && t >= nl;
+      const uint64_t fin = __ballot(done && gi == 0u);
+      if (fin) {
+        const uint32_t rank = (uint32_t) __builtin_popcountll(fin & ((1ull << (8u * grp)) - 1ull));
+        if (done) take(next + rank);
+        next += (uint32_t) __builtin_popcountll(fin);
+      }
+    };
+    // ---- store phase: bytes (prefix items and clamped windows rebuilt),
+    // stores, and the header stage of Success frames
     auto store = [&](const DlvStep& S) __attribute__((always_inline)) {
+      const uint32_t pk = S.pk;
+      if (!((pk >> 25) & 1u)) return;
+      const uint64_t D = S.D;
+      const uint32_t x = pk & 31u, y = (pk >> 5) & 31u, wi = (pk >> 12) & 63u, kc = (pk >> 18) & 3u;
+      const int32_t sd = (int32_t) ((pk >> 21) & 15u) - 4;
+      // the chunk's bytes o -> memory and the header stage
+      auto put_chunk = [&](const uint32_t* o) __attribute__((always_inline)) {
+        if constexpr ((MODE & kDlvNoStore) != 0) {
+          if ((o[0] ^ o[1] ^ o[2] ^ o[3]) == 0x12345678u && x == 3u) P.mem[D] = 0;  // keeps the loads
+        } else if (x == 0u && y == 16u) {
+          u32x4 q = {o[0], o[1], o[2], o[3]};
+          *reinterpret_cast<u32x4*>(P.mem + D) = q;
+        } else {
+          dlv_store_partial(P.mem, D, x, y, o);
+        }
+        if (RSS && (MODE & kDlvNoHash) == 0 && kc < 3u) {
+          uint32_t* st = reinterpret_cast<uint32_t*>(stage + hdr_slot(wi, kc));
 #pragma unroll
-      for (int u = 0; u < kDlvU; ++u) {
-        if (S.dc[u] == 0xFFFFFFFFu) continue;
-        const uint32_t pk = S.pk[u];
-        const uint64_t D = (uint64_t) S.dc[u] << 4, lo = D + (pk & 31u), hi = D + ((pk >> 8) & 31u);
-        const uint32_t q = (pk >> 20) & 63u, k = (pk >> 26) & 3u;
-        const int32_t sd = (int32_t) (pk >> 28) - 4;
-        uint32_t v[5];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) v[i] = S.vv[u][i];
-        if (sd < 0) {  // rare: a window starting before the image, read from its start
-#pragma unroll
-          for (int i = 0; i < 5; ++i) {
-            uint32_t x = 0;
-#pragma unroll
-            for (int m = 0; m < 5; ++m)
-              if (i + sd == m) x = S.vv[u][m];
-            v[i] = x;
-          }
-        } else if (sd > 0) {  // rare: a window past the image end: bytes inside it, byte by byte
-          const int64_t a4 = (int64_t) ((msize - 20) & ~3ull) + 4 * sd;
-#pragma unroll
-          for (int i = 0; i < 5; ++i) {
-            uint32_t x = 0;
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb) {
-              const uint64_t e = (uint64_t) (a4 + 4 * i + bb);
-              if (e < msize) x |= (uint32_t) P.mem[e] << (8 * bb);
-            }
-            v[i] = x;
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t keep = dword_keep((int) x, (int) y, i);
+            if (keep) atomicOr(st + i, o[i] & keep);
           }
         }
-        if (k == 0u) {  // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): its 4 bytes at d
-          const uint8_t* r = items + (3u * q) * kDlvRec;
+      };
+      if (sd != 0 || ((pk >> 20) & 1u)) {
+        // rare: a VLAN prefix item, or a window leaving the image.  Handled
+        // whole in this branch, so its loads are waited for here and the
+        // common path keeps its counted waits.
+        uint32_t v[5];
+        uint32_t sh = (pk >> 10) & 3u;
+        if ((pk >> 20) & 1u) {  // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): its 4 bytes at the item's d
+          const uint8_t* r = items + (wi * 3u) * kDlvItemRec;
           const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
           const uint32_t pw = *reinterpret_cast<const uint32_t*>(r + 8);
           const int32_t rel = (int32_t) (d - D);  // prefix byte b sits at chunk byte rel + b
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            uint32_t x = 0;
+            uint32_t z = 0;
 #pragma unroll
             for (int bb = 0; bb < 4; ++bb) {
               const int32_t pb = 4 * i + bb - rel;
-              if (pb >= 0 && pb < 4) x |= ((pw >> (8 * pb)) & 0xFFu) << (8 * bb);
+              if (pb >= 0 && pb < 4) z |= ((pw >> (8 * pb)) & 0xFFu) << (8 * bb);
             }
-            v[i] = x;
+            v[i] = z;
+          }
+          v[4] = 0;
+          sh = 0;
+        } else if (sd < 0) {  // a window starting before the image, read from its start
+#pragma unroll
+          for (int i = 0; i < 5; ++i) {
+            uint32_t z = 0;
+#pragma unroll
+            for (int m = 0; m < 5; ++m)
+              if (i + sd == m) z = S.vv[m];
+            v[i] = z;
+          }
+        } else {  // a window past the image end: the bytes inside it, byte by byte
+          const int64_t a4 = top + 4 * sd;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) {
+            uint32_t z = 0;
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb) {
+              const uint64_t e = (uint64_t) (a4 + 4 * i + bb);
+              if (e < msize) z |= (uint32_t) P.mem[e] << (8 * bb);
+            }
+            v[i] = z;
           }
         }
-        const uint32_t sh = k == 0u ? 0u : (pk >> 16) & 3u;
         uint32_t o[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = sh ? __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh) : v[i];
-        if constexpr ((MODE & kDlvNoStore) != 0) {
-          if ((o[0] ^ o[1] ^ o[2] ^ o[3]) == 0x12345678u && lo == D + 3) P.mem[D] = 0;  // keeps the loads
-        } else {
-          dlv_store(P.mem, D, lo, hi, o);
-        }
-        if (RSS && (MODE & kDlvNoHash) == 0) {
-          const uint64_t wd = wdst[q];
-          const uint64_t kc = (uint64_t) S.dc[u] - (wd & ~(1ull << 63));
-          if ((wd >> 63) && kc < (uint64_t) kHdrChunks) {
-            uint32_t* st = reinterpret_cast<uint32_t*>(stage + hdr_slot(q, (uint32_t) kc));
+        for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
+        put_chunk(o);
+      } else {
+        const uint32_t sh = (pk >> 10) & 3u;
+        uint32_t o[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const uint64_t ad = D + 4u * i;
-              const int b0 = lo > ad ? (int) (lo - ad) : 0, b1 = hi < ad + 4 ? (int) (hi - ad) : 4;
-              if (b1 > b0) atomicOr(st + i, o[i] & dword_keep(b0, b1, 0));
-            }
-          }
-        }
+        for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_alignbyte(S.vv[i + 1], S.vv[i], sh);
+        put_chunk(o);
       }
     };
-    // ---- the stream, ping-pong over pairs of steps (a counted loop with its
-    // only exit at the bottom, as the RX kernel's: hipcc then keeps counted
-    // vmcnt waits); the plan past the last step loads dummies only
-    const uint32_t nsteps = (total_e + kSpan - 1) / kSpan;
-    DlvStep A, B;
-    if (nsteps) plan(A, 0);
-    uint32_t s = 0;
-    for (; s + 1 < nsteps; s += 2) {
-      plan(B, (s + 1) * kSpan);
-      __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's stores
-      store(A);
-      plan(A, (s + 2) * kSpan);
-      __builtin_amdgcn_sched_barrier(0);
-      store(B);
+    // ---- the pipeline: kDlvDepth steps in flight; a loop with its only exit
+    // at the bottom (hipcc then keeps counted vmcnt waits); steps planned past
+    // the last line are empty
+    if (nq) {
+      DlvStep S0, S1, S2, S3;
+      static_assert(kDlvDepth == 4, "four step buffers");
+      plan(S0);
+      plan(S1);
+      plan(S2);
+      bool more;
+      do {
+        plan(S3);
+        __builtin_amdgcn_sched_barrier(0);
+        store(S0);
+        plan(S0);
+        __builtin_amdgcn_sched_barrier(0);
+        store(S1);
+        plan(S1);
+        __builtin_amdgcn_sched_barrier(0);
+        store(S2);
+        plan(S2);
+        __builtin_amdgcn_sched_barrier(0);
+        store(S3);
+        more = __ballot(gw < 64u) != 0ull;  // a group still has lines: S0..S2 and later steps
+      } while (more);
+      store(S0);
+      store(S1);
+      store(S2);
     }
-    if (s < nsteps) store(A);
     if (RSS && (MODE & kDlvNoHash) == 0) {
       // the frames' header bytes are in the stage (LDS, in order within the
       // wave); bytes past it come from the sources — no wait for the stores
@@ -494,14 +568,14 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       if (j < n) {
         if (flag) {
-          const uint8_t* r = items + (lane * 3u) * kDlvRec;
+          const uint8_t* r = items + (lane * 3u) * kDlvItemRec;
           const uint64_t dst = *reinterpret_cast<const uint64_t*>(r);
           const uint32_t pw = *reinterpret_cast<const uint32_t*>(r + 8);
           const uint32_t plen = *reinterpret_cast<const uint32_t*>(r + 16);
-          const uint64_t src_a = *reinterpret_cast<const uint64_t*>(r + kDlvRec + 8);
-          const uint32_t len_a = *reinterpret_cast<const uint32_t*>(r + kDlvRec + 16);
-          const uint64_t src_b = *reinterpret_cast<const uint64_t*>(r + 2 * kDlvRec + 8);
-          const uint32_t len_b = *reinterpret_cast<const uint32_t*>(r + 2 * kDlvRec + 16);
+          const uint64_t src_a = *reinterpret_cast<const uint64_t*>(r + kDlvItemRec + 8);
+          const uint32_t len_a = *reinterpret_cast<const uint32_t*>(r + kDlvItemRec + 16);
+          const uint64_t src_b = *reinterpret_cast<const uint64_t*>(r + 2 * kDlvItemRec + 8);
+          const uint32_t len_b = *reinterpret_cast<const uint32_t*>(r + 2 * kDlvItemRec + 16);
           uint64_t len = (uint64_t) plen + len_a + len_b;
           if (len > NICGPU_MAX_PACKET) len = NICGPU_MAX_PACKET;  // the tuple lies in the first 82 B
           const FrameParts fp{P.mem, src_a, src_b, pw, plen, len_a};
@@ -782,7 +856,8 @@ template <int MODE>
 int launch_deliver(const DeliverParams& P, bool rss, int cus_total, hipStream_t s) {
   const uint32_t hist_n = (rss && P.rss.table_n <= (uint32_t) kHistLds) ? P.rss.table_n : 0u;
   const uint32_t table_words = (rss && P.rss.table_n <= (uint32_t) kTableLds) ? (P.rss.table_n + 1u) / 2u : 0u;
-  const uint32_t lds = dlv_block_bytes(rss, P.rss.lut_words, hist_n, table_words) + kDlvWpb * kDlvWaveBytes;
+  const uint32_t wave_bytes = (MODE & kDlvV1) ? kDlvWaveBytes : kDlvWaveBytes3;
+  const uint32_t lds = dlv_block_bytes(rss, P.rss.lut_words, hist_n, table_words) + kDlvWpb * wave_bytes;
   const int bpc = rss ? dlv_blocks_per_cu<true>(lds) : dlv_blocks_per_cu<false>(lds);
   const uint64_t ntiles = (P.n - P.j0 + kWave - 1) / kWave;
   const uint64_t want = (ntiles + kDlvWpb - 1) / kDlvWpb;
@@ -1734,7 +1809,10 @@ extern "C" int nicgpu_tune_deliver(int mode, uint8_t* mem, uint64_t mem_size, co
     case kDlvPackedDst: return launch_deliver<kDlvPackedDst>(P, rss, di->cus, s);
     case kDlvNoLoad | kDlvNoHash: return launch_deliver<kDlvNoLoad | kDlvNoHash>(P, rss, di->cus, s);
     case kDlvNoStore | kDlvNoHash: return launch_deliver<kDlvNoStore | kDlvNoHash>(P, rss, di->cus, s);
+    case kDlvNoStore | kDlvNoLoad | kDlvNoHash: return launch_deliver<kDlvNoStore | kDlvNoLoad | kDlvNoHash>(P, rss, di->cus, s);
     case kDlvV1: return launch_deliver<kDlvV1>(P, rss, di->cus, s);
+    case kDlvV1 | kDlvNoStore | kDlvNoLoad | kDlvNoHash:
+      return launch_deliver<kDlvV1 | kDlvNoStore | kDlvNoLoad | kDlvNoHash>(P, rss, di->cus, s);
     case kDlvV1 | kDlvNoStore | kDlvNoHash: return launch_deliver<kDlvV1 | kDlvNoStore | kDlvNoHash>(P, rss, di->cus, s);
     case kDlvV1 | kDlvNoLoad | kDlvNoHash: return launch_deliver<kDlvV1 | kDlvNoLoad | kDlvNoHash>(P, rss, di->cus, s);
     default: return NICGPU_ERR_INVALID;

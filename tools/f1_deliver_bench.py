@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--slot", type=int, default=2048)
-    ap.add_argument("--modes", default="0,1,2,4,8,6,5,32,37,38")
+    ap.add_argument("--modes", default="0,1,2,4,8,6,5,7,32")
     args = ap.parse_args()
 
     import torch
