@@ -249,42 +249,49 @@ __device__ __forceinline__ void dlv_store_partial(uint8_t* mem, uint64_t D, uint
   if (p < y) mem[D + p] = (uint8_t) chunk_word_at(o, p);
 }
 
-// ---- delivery by 8-lane groups --------------------------------------------
-// Round 3's stream mapped every 16-B chunk to its write through LDS marks, a
-// DPP prefix-max and item lookups: ~375 wave-instructions per KiB moved, 60 M
-// VALU per C3 batch (SQ_INSTS_VALU), 87 us of a 234-us launch with neither
-// loads nor stores (tools/f1_deliver_bench.py mode 7).  Here a wave's 64 lanes
-// are 8 groups of 8; a group copies ONE 128-B destination line of one frame
-// per step (lane i its chunk i), so a line's bytes leave in one store
-// instruction and the per-chunk work is an address and a window.  Groups take
-// the tile's writes from a wave-level queue (ballot + popcount) as they finish
-// one.  A write's lines run over its items (VLAN prefix, part A, part B) in
-// order.  Steps are pipelined kDlvDepth deep: step s + kDlvDepth - 1 is planned
-// and its loads issued before step s's stores.
-constexpr int kDlvDepth = 4;          // steps in flight per wave
-constexpr uint32_t kDlvItemRec = 24;  // item: dst u64 | src (prefix word) u64 | len u32 | first line u32
-// per wave: items[64][3] | wmeta[64] {lines u32, first line of A u16, of B u16} | wdst[64] u64 | order[64] u8 | stage
-constexpr uint32_t kDlvWaveBytes3 = 64u * 3u * kDlvItemRec + 64u * 8u + 64u * 8u + 64u + 64u * kHdrStride * 16u;
+// ---- the delivery's steps -------------------------------------------------
+// Attribution of round 3's kernel (tools/f1_deliver_bench.py, C3 1 M):
+// 234 us, of which 87 us with neither loads nor stores (the stream mapping's
+// instructions: SQ_INSTS_VALU 60 M), loads alone +22 us, stores alone +80 us
+// (842 K store instructions for 369 K 64-entry sub-steps: a per-dword and
+// per-byte walk of every partial chunk, executed by the whole wave whenever one
+// lane had one), and the two never overlapped.  So the hot path here is lean:
+// a chunk that is whole, from a 4-aligned source inside the image (every chunk
+// but the edges of a frame for any sane buffer alignment) is one 16-B load and
+// one 16-B store with no other work; the others (partial chunks, unaligned or
+// out-of-image sources, VLAN prefix items) take a slow path that the wave runs
+// only when one of its lanes needs it, and partial chunks whose 16-B source
+// window could be loaded do so without another load.  Offsets are 32-bit for
+// images below 4 GiB (template WIDE otherwise).  Steps are pipelined: step
+// s+1's loads are issued before step s's stores.
+#ifndef NICGPU_DLV_U
+#define NICGPU_DLV_U 2
+#endif
+constexpr int kDlvU = NICGPU_DLV_U;  // 64-entry sub-steps per step (two steps in flight)
+static_assert(kDlvU <= kDlvU1, "marks area");
 
-// One step held between its loads and its stores: one destination chunk per
-// lane.  Every load is unconditional: lanes without a chunk and VLAN prefix
-// items read the image start, and a window leaving the image is read from
-// inside it and rebuilt in the store phase (images of at least 64 B; smaller
-// ones are written byte by byte).
+template <bool WIDE>
+struct DlvOff { typedef uint32_t T; };
+template <>
+struct DlvOff<true> { typedef uint64_t T; };
+
+// One step held between its loads and its stores.
+template <bool WIDE>
 struct DlvStep {
-  uint64_t D;     // destination chunk address
-  uint32_t pk;    // lo - D (0-4) | hi - D (5-9) | shift (10-11) | write w (12-17) | header chunk kc (18-19, 3 none) |
-                  // prefix item (20) | window dword shift + 4 (21-24) | valid (25)
-  uint32_t vv[5]; // source dwords of the 4-aligned window
+  typename DlvOff<WIDE>::T D[kDlvU];  // destination chunk address
+  uint32_t pk[kDlvU];  // lo - D (0-4) | hi - D (5-9) | write q (10-15) | item k (16-17) | header chunk kc (18-19, 3 none) |
+                       // loaded (20: 4-aligned 16-B window at a, inside the image) | valid (21)
+  u32x4 v[kDlvU];      // the source window at a (loaded lanes)
 };
 
-template <bool RSS, int MODE = 0>
-__global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu(4, 8))) void deliver_kernel(DeliverParams P) {
+template <bool RSS, int MODE, bool WIDE>
+__device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
+  typedef typename DlvOff<WIDE>::T Off;
   constexpr uint32_t kThreads = kWave * kDlvWpb;
+  constexpr uint32_t kSpan = kWave * kDlvU;
   extern __shared__ uint4 lds_dyn[];
   const uint32_t w = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
   const uint32_t lane = lane_id();
-  const uint32_t grp = lane >> 3, gi = lane & 7u;
   const RxParams& R = P.rss;
   const bool hist_lds = RSS && R.table_n <= (uint32_t) kHistLds;
   const bool table_lds = RSS && R.table_n <= (uint32_t) kTableLds;
@@ -295,12 +302,11 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
   const uint32_t block_bytes = dlv_block_bytes(RSS, R.lut_words, hist_lds ? R.table_n : 0u,
                                                table_lds ? (R.table_n + 1u) / 2u : 0u);
   uint32_t* cnt_s = reinterpret_cast<uint32_t*>(base_b + block_bytes - 16u);
-  uint8_t* wave_b = base_b + block_bytes + w * kDlvWaveBytes3;
-  uint8_t* items = wave_b;
-  uint2* wmeta = reinterpret_cast<uint2*>(items + 64u * 3u * kDlvItemRec);
-  uint64_t* wdst = reinterpret_cast<uint64_t*>(wmeta + 64);
-  uint8_t* order = reinterpret_cast<uint8_t*>(wdst + 64);
-  uint4* stage = reinterpret_cast<uint4*>(order + 64);
+  uint8_t* wave_b = base_b + block_bytes + w * kDlvWaveBytes;
+  uint8_t* marks = wave_b;
+  uint64_t* wdst = reinterpret_cast<uint64_t*>(wave_b + kDlvMarks);
+  uint8_t* items = wave_b + kDlvMarks + 512u;
+  uint4* stage = reinterpret_cast<uint4*>(items + 192u * kDlvRec);
   if (RSS) {
     for (uint32_t i = threadIdx.x; i < R.lut_words; i += kThreads) lut[i] = R.lut[i];
     if (hist_lds)
@@ -320,15 +326,12 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
   const uint64_t ntiles = n > P.j0 ? (n - P.j0 + kWave - 1) / kWave : 0;
   const uint64_t nwaves = (uint64_t) gridDim.x * kDlvWpb;
   const uint64_t msize = P.mem_size;
-  const int64_t top = (int64_t) ((msize - 20) & ~3ull);  // last 4-aligned 20-B window inside the image
   uint32_t my_count = 0;
-  // images below 64 B take the byte-wise path (no 20-B windows to clamp into)
-  const bool tiny = msize < 64;
   for (uint64_t tile = (uint64_t) blockIdx.x * kDlvWpb + w; tile < ntiles; tile += nwaves) {
-    // ---- this lane's write: items, lines, queue order
+    // ---- this lane's write: its items and their stream entries
     const uint64_t j = P.j0 + tile * kWave + lane;
+    uint32_t F, c0, c1, c2, total_e;
     bool flag;
-    uint32_t nq;  // writes with lines, in the queue
     {
       nicgpu_segment_write wr{};
       flag = false;
@@ -345,221 +348,172 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
                                    wr.src_b > msize || wr.len_b > msize - wr.src_b);
       flag = flag && ok;
       const uint64_t d1 = wr.dst + plen, d2 = d1 + wr.len_a;
-      auto lines = [](uint64_t d, uint64_t len) -> uint32_t {
-        return len ? (uint32_t) (((d + len - 1) >> 7) - (d >> 7) + 1) : 0u;
-      };
-      const uint32_t n0 = ok ? lines(wr.dst, plen) : 0u;
-      const uint32_t n1 = ok ? lines(d1, wr.len_a) : 0u;
-      const uint32_t n2 = ok ? lines(d2, wr.len_b) : 0u;
+      c0 = ok ? dlv_chunks(wr.dst, plen) : 0u;
+      c1 = ok ? dlv_chunks(d1, wr.len_a) : 0u;
+      c2 = ok ? dlv_chunks(d2, wr.len_b) : 0u;
+      const uint32_t cw = c0 + c1 + c2;
+      const uint32_t incl = wave_incl_scan(cw);
+      F = incl - cw;
+      total_e = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
+      // item records: k 0 = VLAN prefix (src = the prefix word), 1 = part A, 2 = part B
       auto put = [&](uint32_t k, uint64_t d, uint64_t src, uint32_t len, uint32_t first) __attribute__((always_inline)) {
-        uint8_t* r = items + (lane * 3u + k) * kDlvItemRec;
+        uint8_t* r = items + (lane * 3u + k) * kDlvRec;
         *reinterpret_cast<uint64_t*>(r) = d;
         *reinterpret_cast<uint64_t*>(r + 8) = src;
         *reinterpret_cast<uint32_t*>(r + 16) = len;
         *reinterpret_cast<uint32_t*>(r + 20) = first;
       };
-      put(0, wr.dst, wr.prefix, ok ? (uint32_t) plen : 0u, 0u);
-      put(1, d1, wr.src_a, ok ? wr.len_a : 0u, n0);
-      put(2, d2, wr.src_b, ok ? wr.len_b : 0u, n0 + n1);
-      const uint32_t nl = n0 + n1 + n2;
-      wmeta[lane] = make_uint2(nl, (n0 & 0xFFFFu) | ((n0 + n1) << 16));
+      // (lengths kept for the hash even for items without chunks: ok frames only)
+      put(0, wr.dst, wr.prefix, ok ? (uint32_t) plen : 0u, F);
+      put(1, d1, wr.src_a, ok ? wr.len_a : 0u, F + c0);
+      put(2, d2, wr.src_b, ok ? wr.len_b : 0u, F + c0 + c1);
       wdst[lane] = (wr.dst >> 4) | (flag ? 1ull << 63 : 0ull);
-      const uint64_t has = __ballot(nl != 0u);
-      if (nl) order[__builtin_amdgcn_mbcnt_hi((uint32_t) (has >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) has, 0u))] = (uint8_t) lane;
-      nq = (uint32_t) __builtin_popcountll(has);
-      if (tiny) nq = 0;
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    if (tiny) {
-      // byte by byte, one lane per write (images below 64 B only)
-      for (uint32_t k = 0; k < 3u; ++k) {
-        const uint8_t* r = items + (lane * 3u + k) * kDlvItemRec;
-        const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
-        const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
+    uint32_t carry = 0;  // item (id + 1) of the entry before the step being planned
+    // ---- load phase of the step at stream position W
+    auto plan = [&](DlvStep<WIDE>& S, uint32_t W) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) marks[u * kWave + lane] = 0u;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (c0 && F >= W && F - W < kSpan) marks[F - W] = (uint8_t) (lane * 3u + 1u);
+      if (c1 && F + c0 >= W && F + c0 - W < kSpan) marks[F + c0 - W] = (uint8_t) (lane * 3u + 2u);
+      if (c2 && F + c0 + c1 >= W && F + c0 + c1 - W < kSpan) marks[F + c0 + c1 - W] = (uint8_t) (lane * 3u + 3u);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) {
+        uint32_t it = wave_incl_max(marks[u * kWave + lane]);
+        it = it > carry ? it : carry;
+        carry = (uint32_t) __builtin_amdgcn_readlane((int) it, 63);
+        const uint32_t pos = W + (uint32_t) u * kWave + lane;
+        const bool valid = pos < total_e;
+        const uint32_t id = valid ? it - 1u : 0u, q = id / 3u, k = id - 3u * q;
+        const uint8_t* r = items + id * kDlvRec;
+        const Off d = *reinterpret_cast<const Off*>(r);
+        const Off src = *reinterpret_cast<const Off*>(r + 8);
         const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
-        for (uint32_t i = 0; i < len; ++i) {
-          const uint32_t b = k == 0u ? (uint32_t) (src >> (8 * i)) & 0xFFu : (uint32_t) P.mem[src + i];
-          P.mem[d + i] = (uint8_t) b;
-          const uint64_t kc = ((d + i) >> 4) - (wdst[lane] & ~(1ull << 63));
-          if (RSS && flag && kc < (uint64_t) kHdrChunks)
-            reinterpret_cast<uint8_t*>(stage + hdr_slot(lane, (uint32_t) kc))[(d + i) & 15u] = (uint8_t) b;
-        }
-      }
-    }
-    // ---- the groups' queue: group state (write gw, its line t of nl; the
-    // first lines of its items A and B), refilled from order[] as groups finish
-    uint32_t next = 8u < nq ? 8u : nq;  // wave-uniform: queue position
-    uint32_t gw = 64u, t = 0, nl = 0, f1 = 0, f2 = 0;
-    auto take = [&](uint32_t qpos) __attribute__((always_inline)) {
-      gw = qpos < nq ? (uint32_t) order[qpos] : 64u;
-      t = 0;
-      if (gw < 64u) {
-        const uint2 m = wmeta[gw];
-        nl = m.x;
-        f1 = m.y & 0xFFFFu;
-        f2 = m.y >> 16;
-      }
-    };
-    take(grp);
-    // ---- load phase of one step: this lane's chunk of its group's line
-    auto plan = [&](DlvStep& S) __attribute__((always_inline)) {
-      const bool active = gw < 64u;
-      const uint32_t k = t >= f2 ? 2u : (t >= f1 ? 1u : 0u);
-      const uint32_t wi = active ? gw : 0u;
-      const uint8_t* r = items + (wi * 3u + k) * kDlvItemRec;
-      const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
-      const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
-      const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
-      const uint32_t first = *reinterpret_cast<const uint32_t*>(r + 20);
-      const uint64_t D = ((((d >> 7) + (t - first)) << 3) + gi) << 4;
-      const uint64_t lo = D > d ? D : d;
-      const uint64_t hi = D + 16 < d + len ? D + 16 : d + len;
-      const bool valid = active && lo < hi;
-      const uint64_t kc64 = (D >> 4) - (wdst[wi] & ~(1ull << 63));
-      const uint32_t kc = (RSS && (wdst[wi] >> 63) && kc64 < (uint64_t) kHdrChunks) ? (uint32_t) kc64 : 3u;
-      // source of destination byte D: before the item's source by up to 15
-      // bytes on its first chunk, so possibly below address 0 (signed); a
-      // window leaving the image is read from inside it (sd dwords away)
-      const int64_t a = (int64_t) D + ((int64_t) src - (int64_t) d);
-      const int64_t a4 = a & ~(int64_t) 3;
-      const int64_t la = (!valid || k == 0u) ? 0 : (a4 < 0 ? 0 : (a4 > top ? top : a4));
-      const int32_t sd = (!valid || k == 0u) ? 0 : (int32_t) ((a4 - la) >> 2);
-      S.D = D;
-      S.pk = (valid ? (uint32_t) (lo - D) | ((uint32_t) (hi - D) << 5) : 0u) | ((uint32_t) (a & 3) << 10) |
-             (wi << 12) | (kc << 18) | ((uint32_t) (k == 0u) << 20) | ((uint32_t) (sd + 4) << 21) |
-             ((uint32_t) valid << 25);
-      const uint8_t* lp = P.mem + la;
-      if constexpr ((MODE & kDlvNoLoad) != 0) {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) S.vv[i] = (uint32_t) la * 0x9E3779B1u + i;
-      } else {
-        __builtin_memcpy(S.vv, lp, 16);  // dword-aligned dwordx4 (gfx950 unaligned access mode)
-        S.vv[4] = *reinterpret_cast<const uint32_t*>(lp + 16);
-      }
-      // advance the group; groups past their write's last line take the next
-      // write of the queue, in group order
-      ++t;
-      const bool done = active && t >= nl;
-      const uint64_t fin = __ballot(done && gi == 0u);
-      if (fin) {
-        const uint32_t rank = (uint32_t) __builtin_popcountll(fin & ((1ull << (8u * grp)) - 1ull));
-        if (done) take(next + rank);
-        next += (uint32_t) __builtin_popcountll(fin);
-      }
-    };
-    // ---- store phase: bytes (prefix items and clamped windows rebuilt),
-    // stores, and the header stage of Success frames
-    auto store = [&](const DlvStep& S) __attribute__((always_inline)) {
-      const uint32_t pk = S.pk;
-      if (!((pk >> 25) & 1u)) return;
-      const uint64_t D = S.D;
-      const uint32_t x = pk & 31u, y = (pk >> 5) & 31u, wi = (pk >> 12) & 63u, kc = (pk >> 18) & 3u;
-      const int32_t sd = (int32_t) ((pk >> 21) & 15u) - 4;
-      // the chunk's bytes o -> memory and the header stage
-      auto put_chunk = [&](const uint32_t* o) __attribute__((always_inline)) {
-        if constexpr ((MODE & kDlvNoStore) != 0) {
-          if ((o[0] ^ o[1] ^ o[2] ^ o[3]) == 0x12345678u && x == 3u) P.mem[D] = 0;  // keeps the loads
-        } else if (x == 0u && y == 16u) {
-          u32x4 q = {o[0], o[1], o[2], o[3]};
-          *reinterpret_cast<u32x4*>(P.mem + D) = q;
+        const uint32_t first = *reinterpret_cast<const uint32_t*>(r + 20);
+        const Off D = ((d >> 4) + (Off) (pos - first)) << 4;
+        const Off lo = D > d ? D : d;
+        const Off hi = D + 16 < d + len ? D + 16 : d + len;
+        // source of destination byte D (the item's source less up to 15 bytes
+        // on its first chunk: below address 0 wraps, failing `in`)
+        const Off a = D + (src - d);
+        const bool in = a <= (Off) msize - 16u && (a & 3u) == 0u && k != 0u;
+        const uint64_t wd = wdst[q];
+        const uint64_t kc64 = (uint64_t) (D >> 4) - (wd & ~(1ull << 63));
+        const uint32_t kc = (RSS && (MODE & kDlvNoHash) == 0 && (wd >> 63) && kc64 < (uint64_t) kHdrChunks)
+                                ? (uint32_t) kc64 : 3u;
+        S.D[u] = D;
+        S.pk[u] = (uint32_t) (lo - D) | ((uint32_t) (hi - D) << 5) | (q << 10) | (k << 16) | (kc << 18) |
+                  ((uint32_t) (valid && in) << 20) | ((uint32_t) valid << 21);
+        if constexpr ((MODE & kDlvNoLoad) != 0) {
+          S.v[u] = (u32x4){(uint32_t) a, 1u, 2u, 3u};
         } else {
-          dlv_store_partial(P.mem, D, x, y, o);
+          S.v[u] = *reinterpret_cast<const u32x4*>(P.mem + ((valid && in) ? a : (Off) 0));
         }
-        if (RSS && (MODE & kDlvNoHash) == 0 && kc < 3u) {
-          uint32_t* st = reinterpret_cast<uint32_t*>(stage + hdr_slot(wi, kc));
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t keep = dword_keep((int) x, (int) y, i);
-            if (keep) atomicOr(st + i, o[i] & keep);
-          }
-        }
-      };
-      if (sd != 0 || ((pk >> 20) & 1u)) {
-        // rare: a VLAN prefix item, or a window leaving the image.  Handled
-        // whole in this branch, so its loads are waited for here and the
-        // common path keeps its counted waits.
-        uint32_t v[5];
-        uint32_t sh = (pk >> 10) & 3u;
-        if ((pk >> 20) & 1u) {  // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): its 4 bytes at the item's d
-          const uint8_t* r = items + (wi * 3u) * kDlvItemRec;
-          const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
-          const uint32_t pw = *reinterpret_cast<const uint32_t*>(r + 8);
-          const int32_t rel = (int32_t) (d - D);  // prefix byte b sits at chunk byte rel + b
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            uint32_t z = 0;
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb) {
-              const int32_t pb = 4 * i + bb - rel;
-              if (pb >= 0 && pb < 4) z |= ((pw >> (8 * pb)) & 0xFFu) << (8 * bb);
-            }
-            v[i] = z;
-          }
-          v[4] = 0;
-          sh = 0;
-        } else if (sd < 0) {  // a window starting before the image, read from its start
-#pragma unroll
-          for (int i = 0; i < 5; ++i) {
-            uint32_t z = 0;
-#pragma unroll
-            for (int m = 0; m < 5; ++m)
-              if (i + sd == m) z = S.vv[m];
-            v[i] = z;
-          }
-        } else {  // a window past the image end: the bytes inside it, byte by byte
-          const int64_t a4 = top + 4 * sd;
-#pragma unroll
-          for (int i = 0; i < 5; ++i) {
-            uint32_t z = 0;
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb) {
-              const uint64_t e = (uint64_t) (a4 + 4 * i + bb);
-              if (e < msize) z |= (uint32_t) P.mem[e] << (8 * bb);
-            }
-            v[i] = z;
-          }
-        }
-        uint32_t o[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
-        put_chunk(o);
-      } else {
-        const uint32_t sh = (pk >> 10) & 3u;
-        uint32_t o[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_alignbyte(S.vv[i + 1], S.vv[i], sh);
-        put_chunk(o);
       }
     };
-    // ---- the pipeline: kDlvDepth steps in flight; a loop with its only exit
-    // at the bottom (hipcc then keeps counted vmcnt waits); steps planned past
-    // the last line are empty
-    if (nq) {
-      DlvStep S0, S1, S2, S3;
-      static_assert(kDlvDepth == 4, "four step buffers");
-      plan(S0);
-      plan(S1);
-      plan(S2);
-      bool more;
-      do {
-        plan(S3);
+    // ---- store phase
+    auto store = [&](const DlvStep<WIDE>& S) __attribute__((always_inline)) {
+      bool slow = false;
+#pragma unroll
+      for (int u = 0; u < kDlvU; ++u) {
+        const uint32_t pk = S.pk[u];
+        const uint32_t x = pk & 31u, y = (pk >> 5) & 31u;
+        const bool hot = ((pk >> 20) & 1u) && x == 0u && y == 16u;  // whole chunk, loaded window
+        if (hot) {
+          if constexpr ((MODE & kDlvNoStore) != 0) {
+            if ((S.v[u].x ^ S.v[u].w) == 0x12345678u) P.mem[S.D[u]] = 0;  // keeps the loads
+          } else {
+            *reinterpret_cast<u32x4*>(P.mem + S.D[u]) = S.v[u];
+          }
+          const uint32_t kc = (pk >> 18) & 3u;
+          if (kc < 3u) stage[hdr_slot((pk >> 10) & 63u, kc)] = make_uint4(S.v[u].x, S.v[u].y, S.v[u].z, S.v[u].w);
+        }
+        slow = slow || (((pk >> 21) & 1u) && !hot);
+      }
+      if (slow) {
+        // partial chunks, unaligned or out-of-image sources, VLAN prefixes;
+        // the loads here are waited for inside this branch only
+#pragma unroll
+        for (int u = 0; u < kDlvU; ++u) {
+          const uint32_t pk = S.pk[u];
+          const uint32_t x = pk & 31u, y = (pk >> 5) & 31u;
+          const bool loaded = (pk >> 20) & 1u;
+          if (!((pk >> 21) & 1u) || (loaded && x == 0u && y == 16u)) continue;
+          const Off D = S.D[u];
+          const uint32_t q = (pk >> 10) & 63u, k = (pk >> 16) & 3u, kc = (pk >> 18) & 3u;
+          uint32_t o[4] = {S.v[u].x, S.v[u].y, S.v[u].z, S.v[u].w};
+          if (!loaded) {
+            const uint8_t* r = items + (q * 3u + k) * kDlvRec;
+            const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
+            const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
+            if (k == 0u) {
+              // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): its 4 bytes at d
+              const int32_t rel = (int32_t) (d - (uint64_t) D);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                uint32_t z = 0;
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                  const int32_t pb = 4 * i + bb - rel;
+                  if (pb >= 0 && pb < 4) z |= (uint32_t) ((src >> (8 * pb)) & 0xFFu) << (8 * bb);
+                }
+                o[i] = z;
+              }
+            } else {
+              // the chunk's bytes [x, y) from the source, byte by byte (rare:
+              // unaligned sources and windows leaving the image)
+              const uint64_t s0 = (uint64_t) D + (src - d);
+              o[0] = o[1] = o[2] = o[3] = 0u;
+#pragma unroll 1
+              for (uint32_t b = x; b < y; ++b) {
+                const uint32_t z = (uint32_t) P.mem[s0 + b] << (8u * (b & 3u));
+                o[0] |= (b >> 2) == 0u ? z : 0u;
+                o[1] |= (b >> 2) == 1u ? z : 0u;
+                o[2] |= (b >> 2) == 2u ? z : 0u;
+                o[3] |= (b >> 2) == 3u ? z : 0u;
+              }
+            }
+          }
+          if constexpr ((MODE & kDlvNoStore) == 0) {
+            if (x == 0u && y == 16u) {
+              u32x4 vq = {o[0], o[1], o[2], o[3]};
+              *reinterpret_cast<u32x4*>(P.mem + D) = vq;
+            } else {
+              dlv_store_partial(P.mem, (uint64_t) D, x, y, o);
+            }
+          }
+          if (kc < 3u) {
+            uint32_t* st = reinterpret_cast<uint32_t*>(stage + hdr_slot(q, kc));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uint32_t keep = dword_keep((int) x, (int) y, i);
+              if (keep) atomicOr(st + i, o[i] & keep);
+            }
+          }
+        }
+      }
+    };
+    // ---- the stream, ping-pong over pairs of steps (a counted loop with its
+    // only exit at the bottom, as the RX kernel's: hipcc then keeps counted
+    // vmcnt waits); the plan past the last step is empty
+    const uint32_t nsteps = (total_e + kSpan - 1) / kSpan;
+    if (nsteps) {
+      DlvStep<WIDE> A, B;
+      plan(A, 0);
+      uint32_t s = 0;
+      for (; s + 1 < nsteps; s += 2) {
+        plan(B, (s + 1) * kSpan);
+        __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's stores
+        store(A);
+        plan(A, (s + 2) * kSpan);
         __builtin_amdgcn_sched_barrier(0);
-        store(S0);
-        plan(S0);
-        __builtin_amdgcn_sched_barrier(0);
-        store(S1);
-        plan(S1);
-        __builtin_amdgcn_sched_barrier(0);
-        store(S2);
-        plan(S2);
-        __builtin_amdgcn_sched_barrier(0);
-        store(S3);
-        more = __ballot(gw < 64u) != 0ull;  // a group still has lines: S0..S2 and later steps
-      } while (more);
-      store(S0);
-      store(S1);
-      store(S2);
+        store(B);
+      }
+      if (s < nsteps) store(A);
     }
     if (RSS && (MODE & kDlvNoHash) == 0) {
       // the frames' header bytes are in the stage (LDS, in order within the
@@ -568,14 +522,14 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       if (j < n) {
         if (flag) {
-          const uint8_t* r = items + (lane * 3u) * kDlvItemRec;
+          const uint8_t* r = items + (lane * 3u) * kDlvRec;
           const uint64_t dst = *reinterpret_cast<const uint64_t*>(r);
           const uint32_t pw = *reinterpret_cast<const uint32_t*>(r + 8);
           const uint32_t plen = *reinterpret_cast<const uint32_t*>(r + 16);
-          const uint64_t src_a = *reinterpret_cast<const uint64_t*>(r + kDlvItemRec + 8);
-          const uint32_t len_a = *reinterpret_cast<const uint32_t*>(r + kDlvItemRec + 16);
-          const uint64_t src_b = *reinterpret_cast<const uint64_t*>(r + 2 * kDlvItemRec + 8);
-          const uint32_t len_b = *reinterpret_cast<const uint32_t*>(r + 2 * kDlvItemRec + 16);
+          const uint64_t src_a = *reinterpret_cast<const uint64_t*>(r + kDlvRec + 8);
+          const uint32_t len_a = *reinterpret_cast<const uint32_t*>(r + kDlvRec + 16);
+          const uint64_t src_b = *reinterpret_cast<const uint64_t*>(r + 2 * kDlvRec + 8);
+          const uint32_t len_b = *reinterpret_cast<const uint32_t*>(r + 2 * kDlvRec + 16);
           uint64_t len = (uint64_t) plen + len_a + len_b;
           if (len > NICGPU_MAX_PACKET) len = NICGPU_MAX_PACKET;  // the tuple lies in the first 82 B
           const FrameParts fp{P.mem, src_a, src_b, pw, plen, len_a};
@@ -606,6 +560,11 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
     if (threadIdx.x == 0 && *cnt_s) atomicAdd(P.count, (unsigned long long) *cnt_s);
     if (hist_lds) flush_hist(hist, R.table_n, P.hits, R.hits_rep, R.hits_done, kThreads);
   }
+}
+
+template <bool RSS, int MODE = 0, bool WIDE = false>
+__global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu(4, 8))) void deliver_kernel(DeliverParams P) {
+  deliver_tiles<RSS, MODE, WIDE>(P);
 }
 
 #ifdef NICGPU_TUNING
@@ -856,7 +815,7 @@ template <int MODE>
 int launch_deliver(const DeliverParams& P, bool rss, int cus_total, hipStream_t s) {
   const uint32_t hist_n = (rss && P.rss.table_n <= (uint32_t) kHistLds) ? P.rss.table_n : 0u;
   const uint32_t table_words = (rss && P.rss.table_n <= (uint32_t) kTableLds) ? (P.rss.table_n + 1u) / 2u : 0u;
-  const uint32_t wave_bytes = (MODE & kDlvV1) ? kDlvWaveBytes : kDlvWaveBytes3;
+  const uint32_t wave_bytes = kDlvWaveBytes;
   const uint32_t lds = dlv_block_bytes(rss, P.rss.lut_words, hist_n, table_words) + kDlvWpb * wave_bytes;
   const int bpc = rss ? dlv_blocks_per_cu<true>(lds) : dlv_blocks_per_cu<false>(lds);
   const uint64_t ntiles = (P.n - P.j0 + kWave - 1) / kWave;
@@ -877,8 +836,12 @@ int launch_deliver(const DeliverParams& P, bool rss, int cus_total, hipStream_t 
     return hip_status(hipGetLastError());
   }
 #endif
-  if (rss) hipLaunchKernelGGL((deliver_kernel<true, MODE>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
-  else hipLaunchKernelGGL((deliver_kernel<false, MODE>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+  // 32-bit offsets for images below 4 GiB
+  const bool wide = P.mem_size > 0xFFFFFFF0ull;
+  if (rss && !wide) hipLaunchKernelGGL((deliver_kernel<true, MODE, false>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+  else if (rss) hipLaunchKernelGGL((deliver_kernel<true, MODE, true>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+  else if (!wide) hipLaunchKernelGGL((deliver_kernel<false, MODE, false>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+  else hipLaunchKernelGGL((deliver_kernel<false, MODE, true>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
   return hip_status(hipGetLastError());
 }
 
