@@ -326,6 +326,9 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   const uint64_t ntiles = n > P.j0 ? (n - P.j0 + kWave - 1) / kWave : 0;
   const uint64_t nwaves = (uint64_t) gridDim.x * kDlvWpb;
   const uint64_t msize = P.mem_size;
+  // where lanes without a whole aligned window load from: the image start, or
+  // the write records for an image below 16 B (always >= 40 readable bytes)
+  const uint8_t* dummy = msize >= 16u ? P.mem : reinterpret_cast<const uint8_t*>(P.w);
   uint32_t my_count = 0;
   for (uint64_t tile = (uint64_t) blockIdx.x * kDlvWpb + w; tile < ntiles; tile += nwaves) {
     // ---- this lane's write: its items and their stream entries
@@ -400,18 +403,21 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
         // source of destination byte D (the item's source less up to 15 bytes
         // on its first chunk: below address 0 wraps, failing `in`)
         const Off a = D + (src - d);
-        const bool in = a <= (Off) msize - 16u && (a & 3u) == 0u && k != 0u;
+        const bool in = msize >= 16u && a <= (Off) msize - 16u && (a & 3u) == 0u && k != 0u;
         const uint64_t wd = wdst[q];
         const uint64_t kc64 = (uint64_t) (D >> 4) - (wd & ~(1ull << 63));
         const uint32_t kc = (RSS && (MODE & kDlvNoHash) == 0 && (wd >> 63) && kc64 < (uint64_t) kHdrChunks)
                                 ? (uint32_t) kc64 : 3u;
         S.D[u] = D;
-        S.pk[u] = (uint32_t) (lo - D) | ((uint32_t) (hi - D) << 5) | (q << 10) | (k << 16) | (kc << 18) |
-                  ((uint32_t) (valid && in) << 20) | ((uint32_t) valid << 21);
+        // (lanes without an entry: lo / hi belong to another item, so the
+        // fields are left 0 — they could otherwise spill into the flags)
+        S.pk[u] = valid ? (uint32_t) (lo - D) | ((uint32_t) (hi - D) << 5) | (q << 10) | (k << 16) | (kc << 18) |
+                              ((uint32_t) in << 20) | (1u << 21)
+                        : 0u;
         if constexpr ((MODE & kDlvNoLoad) != 0) {
           S.v[u] = (u32x4){(uint32_t) a, 1u, 2u, 3u};
         } else {
-          S.v[u] = *reinterpret_cast<const u32x4*>(P.mem + ((valid && in) ? a : (Off) 0));
+          S.v[u] = *reinterpret_cast<const u32x4*>(((valid && in) ? P.mem + a : dummy));
         }
       }
     };
