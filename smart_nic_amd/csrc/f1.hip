@@ -275,18 +275,38 @@ struct DlvOff { typedef uint32_t T; };
 template <>
 struct DlvOff<true> { typedef uint64_t T; };
 
+// An item (a write's VLAN prefix, part A or part B) as the steps read it, one
+// LDS record per item, so an entry's addresses are a few adds: destination
+// chunk D = (dbase + pos) << 4, source a = D + sdelta, bytes [max(d, D),
+// min(dend, D + 16)) of the chunk; its frame's header chunk kc = pos - kcb.
+template <bool WIDE>
+struct DlvItem {
+  typedef typename DlvOff<WIDE>::T Off;
+  Off dbase;   // (d >> 4) - first entry (wrapping)
+  Off sdelta;  // src - d (wrapping); the prefix word for a VLAN prefix item
+  Off d, dend;
+  uint32_t kcb;   // first entry - (d's chunk - the frame's first chunk)
+  uint32_t meta;  // write q (0-5) | item k (6-7) | Success frame (8)
+};
+
 // One step held between its loads and its stores.
 template <bool WIDE>
 struct DlvStep {
   typename DlvOff<WIDE>::T D[kDlvU];  // destination chunk address
-  uint32_t pk[kDlvU];  // lo - D (0-4) | hi - D (5-9) | write q (10-15) | item k (16-17) | header chunk kc (18-19, 3 none) |
+  uint32_t pk[kDlvU];  // lo - D (0-4) | hi - D (5-9) | item id (10-17) | header chunk kc (18-19, 3 none) |
                        // loaded (20: 4-aligned 16-B window at a, inside the image) | valid (21)
   u32x4 v[kDlvU];      // the source window at a (loaded lanes)
 };
 
+template <bool WIDE>
+__host__ __device__ constexpr uint32_t dlv_wave_bytes() {  // marks | items | stage
+  return kDlvMarks + 192u * (uint32_t) sizeof(DlvItem<WIDE>) + 64u * kHdrStride * 16u;
+}
+
 template <bool RSS, int MODE, bool WIDE>
 __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   typedef typename DlvOff<WIDE>::T Off;
+  typedef DlvItem<WIDE> Item;
   constexpr uint32_t kThreads = kWave * kDlvWpb;
   constexpr uint32_t kSpan = kWave * kDlvU;
   extern __shared__ uint4 lds_dyn[];
@@ -302,11 +322,10 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   const uint32_t block_bytes = dlv_block_bytes(RSS, R.lut_words, hist_lds ? R.table_n : 0u,
                                                table_lds ? (R.table_n + 1u) / 2u : 0u);
   uint32_t* cnt_s = reinterpret_cast<uint32_t*>(base_b + block_bytes - 16u);
-  uint8_t* wave_b = base_b + block_bytes + w * kDlvWaveBytes;
+  uint8_t* wave_b = base_b + block_bytes + w * dlv_wave_bytes<WIDE>();
   uint8_t* marks = wave_b;
-  uint64_t* wdst = reinterpret_cast<uint64_t*>(wave_b + kDlvMarks);
-  uint8_t* items = wave_b + kDlvMarks + 512u;
-  uint4* stage = reinterpret_cast<uint4*>(items + 192u * kDlvRec);
+  Item* items = reinterpret_cast<Item*>(wave_b + kDlvMarks);
+  uint4* stage = reinterpret_cast<uint4*>(items + 192);
   if (RSS) {
     for (uint32_t i = threadIdx.x; i < R.lut_words; i += kThreads) lut[i] = R.lut[i];
     if (hist_lds)
@@ -358,19 +377,21 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
       const uint32_t incl = wave_incl_scan(cw);
       F = incl - cw;
       total_e = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
-      // item records: k 0 = VLAN prefix (src = the prefix word), 1 = part A, 2 = part B
-      auto put = [&](uint32_t k, uint64_t d, uint64_t src, uint32_t len, uint32_t first) __attribute__((always_inline)) {
-        uint8_t* r = items + (lane * 3u + k) * kDlvRec;
-        *reinterpret_cast<uint64_t*>(r) = d;
-        *reinterpret_cast<uint64_t*>(r + 8) = src;
-        *reinterpret_cast<uint32_t*>(r + 16) = len;
-        *reinterpret_cast<uint32_t*>(r + 20) = first;
-      };
+      const uint64_t fc = wr.dst >> 4;  // the frame's first chunk
       // (lengths kept for the hash even for items without chunks: ok frames only)
-      put(0, wr.dst, wr.prefix, ok ? (uint32_t) plen : 0u, F);
-      put(1, d1, wr.src_a, ok ? wr.len_a : 0u, F + c0);
-      put(2, d2, wr.src_b, ok ? wr.len_b : 0u, F + c0 + c1);
-      wdst[lane] = (wr.dst >> 4) | (flag ? 1ull << 63 : 0ull);
+      auto put = [&](uint32_t k, uint64_t d, uint64_t src_or_word, uint64_t len, uint32_t first) __attribute__((always_inline)) {
+        Item it;
+        it.dbase = (Off) ((d >> 4) - first);
+        it.sdelta = k == 0u ? (Off) src_or_word : (Off) (src_or_word - d);
+        it.d = (Off) d;
+        it.dend = (Off) (d + (ok ? len : 0u));
+        it.kcb = first - (uint32_t) ((d >> 4) - fc);
+        it.meta = lane | (k << 6) | (flag ? 1u << 8 : 0u);
+        items[lane * 3u + k] = it;
+      };
+      put(0, wr.dst, wr.prefix, plen, F);
+      put(1, d1, wr.src_a, wr.len_a, F + c0);
+      put(2, d2, wr.src_b, wr.len_b, F + c0 + c1);
     }
     uint32_t carry = 0;  // item (id + 1) of the entry before the step being planned
     // ---- load phase of the step at stream position W
@@ -391,29 +412,21 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
         carry = (uint32_t) __builtin_amdgcn_readlane((int) it, 63);
         const uint32_t pos = W + (uint32_t) u * kWave + lane;
         const bool valid = pos < total_e;
-        const uint32_t id = valid ? it - 1u : 0u, q = id / 3u, k = id - 3u * q;
-        const uint8_t* r = items + id * kDlvRec;
-        const Off d = *reinterpret_cast<const Off*>(r);
-        const Off src = *reinterpret_cast<const Off*>(r + 8);
-        const uint32_t len = *reinterpret_cast<const uint32_t*>(r + 16);
-        const uint32_t first = *reinterpret_cast<const uint32_t*>(r + 20);
-        const Off D = ((d >> 4) + (Off) (pos - first)) << 4;
-        const Off lo = D > d ? D : d;
-        const Off hi = D + 16 < d + len ? D + 16 : d + len;
-        // source of destination byte D (the item's source less up to 15 bytes
-        // on its first chunk: below address 0 wraps, failing `in`)
-        const Off a = D + (src - d);
+        const uint32_t id = valid ? it - 1u : 0u;
+        const Item I = items[id];
+        const Off D = (I.dbase + (Off) pos) << 4;
+        const Off a = D + I.sdelta;
+        const uint32_t x = I.d > D ? (uint32_t) (I.d - D) : 0u;
+        const uint32_t y = I.dend - D < 16u ? (uint32_t) (I.dend - D) : 16u;
+        const uint32_t k = (I.meta >> 6) & 3u;
+        // a chunk whose 4-aligned source window lies in the image (the item's
+        // source less up to 15 bytes on its first chunk: below 0 wraps, out)
         const bool in = msize >= 16u && a <= (Off) msize - 16u && (a & 3u) == 0u && k != 0u;
-        const uint64_t wd = wdst[q];
-        const uint64_t kc64 = (uint64_t) (D >> 4) - (wd & ~(1ull << 63));
-        const uint32_t kc = (RSS && (MODE & kDlvNoHash) == 0 && (wd >> 63) && kc64 < (uint64_t) kHdrChunks)
-                                ? (uint32_t) kc64 : 3u;
+        const uint32_t kc32 = pos - I.kcb;
+        const uint32_t kc = (RSS && (MODE & kDlvNoHash) == 0 && (I.meta & 256u) && kc32 < (uint32_t) kHdrChunks) ? kc32 : 3u;
         S.D[u] = D;
-        // (lanes without an entry: lo / hi belong to another item, so the
-        // fields are left 0 — they could otherwise spill into the flags)
-        S.pk[u] = valid ? (uint32_t) (lo - D) | ((uint32_t) (hi - D) << 5) | (q << 10) | (k << 16) | (kc << 18) |
-                              ((uint32_t) in << 20) | (1u << 21)
-                        : 0u;
+        // (lanes without an entry leave the word 0: x / y belong to another item)
+        S.pk[u] = valid ? x | (y << 5) | (id << 10) | (kc << 18) | ((uint32_t) in << 20) | (1u << 21) : 0u;
         if constexpr ((MODE & kDlvNoLoad) != 0) {
           S.v[u] = (u32x4){(uint32_t) a, 1u, 2u, 3u};
         } else {
@@ -427,8 +440,7 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
 #pragma unroll
       for (int u = 0; u < kDlvU; ++u) {
         const uint32_t pk = S.pk[u];
-        const uint32_t x = pk & 31u, y = (pk >> 5) & 31u;
-        const bool hot = ((pk >> 20) & 1u) && x == 0u && y == 16u;  // whole chunk, loaded window
+        const bool hot = (pk & ((1u << 20) | 1023u)) == ((1u << 20) | (16u << 5));  // loaded, bytes [0, 16)
         if (hot) {
           if constexpr ((MODE & kDlvNoStore) != 0) {
             if ((S.v[u].x ^ S.v[u].w) == 0x12345678u) P.mem[S.D[u]] = 0;  // keeps the loads
@@ -436,7 +448,8 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
             *reinterpret_cast<u32x4*>(P.mem + S.D[u]) = S.v[u];
           }
           const uint32_t kc = (pk >> 18) & 3u;
-          if (kc < 3u) stage[hdr_slot((pk >> 10) & 63u, kc)] = make_uint4(S.v[u].x, S.v[u].y, S.v[u].z, S.v[u].w);
+          if (kc < 3u)
+            stage[hdr_slot(items[(pk >> 10) & 255u].meta & 63u, kc)] = make_uint4(S.v[u].x, S.v[u].y, S.v[u].z, S.v[u].w);
         }
         slow = slow || (((pk >> 21) & 1u) && !hot);
       }
@@ -450,33 +463,32 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
           const bool loaded = (pk >> 20) & 1u;
           if (!((pk >> 21) & 1u) || (loaded && x == 0u && y == 16u)) continue;
           const Off D = S.D[u];
-          const uint32_t q = (pk >> 10) & 63u, k = (pk >> 16) & 3u, kc = (pk >> 18) & 3u;
+          const Item I = items[(pk >> 10) & 255u];
+          const uint32_t q = I.meta & 63u, k = (I.meta >> 6) & 3u, kc = (pk >> 18) & 3u;
           uint32_t o[4] = {S.v[u].x, S.v[u].y, S.v[u].z, S.v[u].w};
           if (!loaded) {
-            const uint8_t* r = items + (q * 3u + k) * kDlvRec;
-            const uint64_t d = *reinterpret_cast<const uint64_t*>(r);
-            const uint64_t src = *reinterpret_cast<const uint64_t*>(r + 8);
             if (k == 0u) {
               // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): its 4 bytes at d
-              const int32_t rel = (int32_t) (d - (uint64_t) D);
+              const uint32_t pw = (uint32_t) I.sdelta;
+              const int32_t rel = (int32_t) (I.d - D);
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
                 uint32_t z = 0;
 #pragma unroll
                 for (int bb = 0; bb < 4; ++bb) {
                   const int32_t pb = 4 * i + bb - rel;
-                  if (pb >= 0 && pb < 4) z |= (uint32_t) ((src >> (8 * pb)) & 0xFFu) << (8 * bb);
+                  if (pb >= 0 && pb < 4) z |= ((pw >> (8 * pb)) & 0xFFu) << (8 * bb);
                 }
                 o[i] = z;
               }
             } else {
               // the chunk's bytes [x, y) from the source, byte by byte (rare:
               // unaligned sources and windows leaving the image)
-              const uint64_t s0 = (uint64_t) D + (src - d);
+              const Off s0 = D + I.sdelta;
               o[0] = o[1] = o[2] = o[3] = 0u;
 #pragma unroll 1
               for (uint32_t b = x; b < y; ++b) {
-                const uint32_t z = (uint32_t) P.mem[s0 + b] << (8u * (b & 3u));
+                const uint32_t z = (uint32_t) P.mem[(Off) (s0 + b)] << (8u * (b & 3u));
                 o[0] |= (b >> 2) == 0u ? z : 0u;
                 o[1] |= (b >> 2) == 1u ? z : 0u;
                 o[2] |= (b >> 2) == 2u ? z : 0u;
@@ -503,23 +515,30 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
         }
       }
     };
-    // ---- the stream, ping-pong over pairs of steps (a counted loop with its
-    // only exit at the bottom, as the RX kernel's: hipcc then keeps counted
-    // vmcnt waits); the plan past the last step is empty
+    // ---- the stream: three step buffers in rotation, so a buffer is loaded
+    // again only after another step's stores have issued (a buffer reloaded
+    // right after its stores makes hipcc wait for them: gfx950 counts stores
+    // in vmcnt, in order with the loads); a counted loop with its only exit at
+    // the bottom keeps counted waits; plans past the last step are empty
     const uint32_t nsteps = (total_e + kSpan - 1) / kSpan;
     if (nsteps) {
-      DlvStep<WIDE> A, B;
+      DlvStep<WIDE> A, B, C;
       plan(A, 0);
+      plan(B, kSpan);
       uint32_t s = 0;
-      for (; s + 1 < nsteps; s += 2) {
-        plan(B, (s + 1) * kSpan);
-        __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's stores
+      for (; s + 3 <= nsteps; s += 3) {
+        plan(C, (s + 2) * kSpan);
+        __builtin_amdgcn_sched_barrier(0);
         store(A);
-        plan(A, (s + 2) * kSpan);
+        plan(A, (s + 3) * kSpan);
         __builtin_amdgcn_sched_barrier(0);
         store(B);
+        plan(B, (s + 4) * kSpan);
+        __builtin_amdgcn_sched_barrier(0);
+        store(C);
       }
       if (s < nsteps) store(A);
+      if (s + 1 < nsteps) store(B);
     }
     if (RSS && (MODE & kDlvNoHash) == 0) {
       // the frames' header bytes are in the stage (LDS, in order within the
@@ -528,18 +547,14 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       if (j < n) {
         if (flag) {
-          const uint8_t* r = items + (lane * 3u) * kDlvRec;
-          const uint64_t dst = *reinterpret_cast<const uint64_t*>(r);
-          const uint32_t pw = *reinterpret_cast<const uint32_t*>(r + 8);
-          const uint32_t plen = *reinterpret_cast<const uint32_t*>(r + 16);
-          const uint64_t src_a = *reinterpret_cast<const uint64_t*>(r + kDlvRec + 8);
-          const uint32_t len_a = *reinterpret_cast<const uint32_t*>(r + kDlvRec + 16);
-          const uint64_t src_b = *reinterpret_cast<const uint64_t*>(r + 2 * kDlvRec + 8);
-          const uint32_t len_b = *reinterpret_cast<const uint32_t*>(r + 2 * kDlvRec + 16);
+          const Item I0 = items[lane * 3u], I1 = items[lane * 3u + 1u], I2 = items[lane * 3u + 2u];
+          const uint32_t plen = (uint32_t) (I0.dend - I0.d);
+          const uint32_t len_a = (uint32_t) (I1.dend - I1.d), len_b = (uint32_t) (I2.dend - I2.d);
           uint64_t len = (uint64_t) plen + len_a + len_b;
           if (len > NICGPU_MAX_PACKET) len = NICGPU_MAX_PACKET;  // the tuple lies in the first 82 B
-          const FrameParts fp{P.mem, src_a, src_b, pw, plen, len_a};
-          const uint32_t h = rss_hash_packet(R, lut, HdrView{stage, lane}, (uint32_t) (dst & 15u), fp, (uint32_t) len);
+          const FrameParts fp{P.mem, (uint64_t) (Off) (I1.d + I1.sdelta), (uint64_t) (Off) (I2.d + I2.sdelta),
+                              (uint32_t) I0.sdelta, plen, len_a};
+          const uint32_t h = rss_hash_packet(R, lut, HdrView{stage, lane}, (uint32_t) (I0.d & 15u), fp, (uint32_t) len);
           const uint32_t idx = h % R.table_n;
           P.rx_hash[j] = h;
           P.rx_queue[j] = table_lds ? table_s[idx] : R.table[idx];
@@ -821,7 +836,8 @@ template <int MODE>
 int launch_deliver(const DeliverParams& P, bool rss, int cus_total, hipStream_t s) {
   const uint32_t hist_n = (rss && P.rss.table_n <= (uint32_t) kHistLds) ? P.rss.table_n : 0u;
   const uint32_t table_words = (rss && P.rss.table_n <= (uint32_t) kTableLds) ? (P.rss.table_n + 1u) / 2u : 0u;
-  const uint32_t wave_bytes = kDlvWaveBytes;
+  const bool wide = P.mem_size > 0xFFFFFFF0ull;  // 32-bit offsets for images below 4 GiB
+  const uint32_t wave_bytes = (MODE & kDlvV1) ? kDlvWaveBytes : (wide ? dlv_wave_bytes<true>() : dlv_wave_bytes<false>());
   const uint32_t lds = dlv_block_bytes(rss, P.rss.lut_words, hist_n, table_words) + kDlvWpb * wave_bytes;
   const int bpc = rss ? dlv_blocks_per_cu<true>(lds) : dlv_blocks_per_cu<false>(lds);
   const uint64_t ntiles = (P.n - P.j0 + kWave - 1) / kWave;
@@ -842,8 +858,6 @@ int launch_deliver(const DeliverParams& P, bool rss, int cus_total, hipStream_t 
     return hip_status(hipGetLastError());
   }
 #endif
-  // 32-bit offsets for images below 4 GiB
-  const bool wide = P.mem_size > 0xFFFFFFF0ull;
   if (rss && !wide) hipLaunchKernelGGL((deliver_kernel<true, MODE, false>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
   else if (rss) hipLaunchKernelGGL((deliver_kernel<true, MODE, true>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
   else if (!wide) hipLaunchKernelGGL((deliver_kernel<false, MODE, false>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);

@@ -202,3 +202,41 @@ int nicgpu_tune_calib(int shape, const uint8_t* buf, size_t bytes, uint32_t* out
   return hip_status(hipGetLastError());
 }
 }  // extern "C"
+
+// Write-pattern ceiling for the f1 delivery (tools/f1_deliver_bench.py
+// --patterns): frames of `flen` bytes at `slot`-byte strides (slot = flen
+// rounded to 16 = packed), one 16-B store per lane per chunk, consecutive
+// lanes on consecutive chunks (a frame's chunks, then the next frame's), no
+// loads: what HBM and the caches take for the delivery's store shape.
+namespace {
+template <bool NT>
+__global__ __launch_bounds__(256) void store_pattern_kernel(uint8_t* __restrict__ mem, uint64_t nframes, uint32_t flen,
+                                                            uint32_t slot) {
+  const uint32_t nch = (flen + 15u) / 16u;
+  const uint64_t total = nframes * nch;
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+  const u32x4 v = {threadIdx.x, blockIdx.x, 0x5A5A5A5Au, flen};
+  for (uint64_t c = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; c < total; c += stride) {
+    const uint64_t f = c / nch, k = c - f * nch;
+    u32x4* p = reinterpret_cast<u32x4*>(mem + f * slot + k * 16u);
+    if (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+  }
+}
+}  // namespace
+
+extern "C" int nicgpu_tune_store_pattern(uint8_t* mem, uint64_t nframes, uint32_t flen, uint32_t slot, int blocks_per_cu,
+                                         int nt, void* stream) {
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  if (slot < ((flen + 15u) & ~15u) || (slot & 15u)) return NICGPU_ERR_INVALID;
+  const unsigned grid = (unsigned) (di->cus * (blocks_per_cu > 0 ? blocks_per_cu : 8));
+  if (nt)
+    hipLaunchKernelGGL(store_pattern_kernel<true>, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), mem, nframes,
+                       flen, slot);
+  else
+    hipLaunchKernelGGL(store_pattern_kernel<false>, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), mem, nframes,
+                       flen, slot);
+  return hip_status(hipGetLastError());
+}

@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--slot", type=int, default=2048)
     ap.add_argument("--modes", default="0,1,2,4,8,6,5,7,32")
+    ap.add_argument("--patterns", action="store_true",
+                    help="also time bare 16-B store kernels writing 64/576/1518-B frames at 2-KiB strides and packed "
+                         "(nicgpu_tune_store_pattern): the store shape's ceiling")
     args = ap.parse_args()
 
     import torch
@@ -110,6 +113,16 @@ def main():
     for m in [int(x) for x in args.modes.split(",") if x]:
         if m:
             cases[f"mode{m}"] = deliver(m)
+    if args.patterns:
+        tl.nicgpu_tune_store_pattern.restype = i32
+        tl.nicgpu_tune_store_pattern.argtypes = [vp, u64, ctypes.c_uint32, ctypes.c_uint32, i32, i32, vp]
+        rx_base = mem.data_ptr() + tx_bytes
+        for flen in (64, 576, 1518):
+            nf = int((lens == flen).sum())
+            for slot, nt in ((args.slot, 0), (args.slot, 1), ((flen + 15) // 16 * 16, 0)):
+                def pat(nf=nf, flen=flen, slot=slot, nt=nt):
+                    assert tl.nicgpu_tune_store_pattern(rx_base, nf, flen, slot, 8, nt, sp) == 0
+                cases[f"store_{flen}B_slot{slot}" + ("_nt" if nt else "")] = pat
     times = {k: [] for k in cases}
     for _ in range(args.rounds):
         for name, fn in cases.items():
@@ -135,7 +148,11 @@ def main():
     for name, ts in times.items():
         med = float(np.median(ts))
         out["us_median"][name] = round(med, 1)
-        out["tbps_rw"][name] = round(moved / med / 1e6, 3)
+        if name.startswith("store_"):
+            flen = int(name.split("_")[1][:-1])
+            out["tbps_rw"][name] = round(int((lens == flen).sum()) * ((flen + 15) // 16 * 16) / med / 1e6, 3)
+        else:
+            out["tbps_rw"][name] = round(moved / med / 1e6, 3)
     print(json.dumps(out), flush=True)
 
 
