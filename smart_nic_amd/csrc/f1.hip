@@ -276,25 +276,24 @@ template <>
 struct DlvOff<true> { typedef uint64_t T; };
 
 // An item (a write's VLAN prefix, part A or part B) as the steps read it, one
-// LDS record per item, so an entry's addresses are a few adds: destination
-// chunk D = (dbase + pos) << 4, source a = D + sdelta, bytes [max(d, D),
-// min(dend, D + 16)) of the chunk; its frame's header chunk kc = pos - kcb.
+// LDS record per item, so that a chunk of the hot path costs a few adds:
+// destination chunk D = (dbase + pos) << 4, source a = D + sdelta, and it is
+// hot (whole, from a 4-aligned window inside the image) iff pos - h0 < hn.
 template <bool WIDE>
 struct DlvItem {
   typedef typename DlvOff<WIDE>::T Off;
   Off dbase;   // (d >> 4) - first entry (wrapping)
-  Off sdelta;  // src - d (wrapping); the prefix word for a VLAN prefix item
+  Off sdelta;  // src - d (wrapping); 1 for a VLAN prefix item (its windows are never loaded)
   Off d, dend;
-  uint32_t kcb;   // first entry - (d's chunk - the frame's first chunk)
-  uint32_t meta;  // write q (0-5) | item k (6-7) | Success frame (8)
+  uint32_t h0;    // first hot entry; the prefix word for a VLAN prefix item
+  uint32_t meta;  // hot entries (0-19) | item k (20-21) | write q (22-27)
 };
 
 // One step held between its loads and its stores.
 template <bool WIDE>
 struct DlvStep {
   typename DlvOff<WIDE>::T D[kDlvU];  // destination chunk address
-  uint32_t pk[kDlvU];  // lo - D (0-4) | hi - D (5-9) | item id (10-17) | header chunk kc (18-19, 3 none) |
-                       // loaded (20: 4-aligned 16-B window at a, inside the image) | valid (21)
+  uint32_t pk[kDlvU];  // item id (0-7) | hot (8) | valid (9) | loaded (10: the 4-aligned window at a, in the image)
   u32x4 v[kDlvU];      // the source window at a (loaded lanes)
 };
 
@@ -309,6 +308,7 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   typedef DlvItem<WIDE> Item;
   constexpr uint32_t kThreads = kWave * kDlvWpb;
   constexpr uint32_t kSpan = kWave * kDlvU;
+  constexpr bool kHash = RSS && (MODE & kDlvNoHash) == 0;
   extern __shared__ uint4 lds_dyn[];
   const uint32_t w = (uint32_t) __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
   const uint32_t lane = lane_id();
@@ -333,8 +333,6 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
     if (table_lds)
       for (uint32_t i = threadIdx.x; i < R.table_n; i += kThreads) table_s[i] = R.table[i];
     if (threadIdx.x == 0) *cnt_s = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < (uint32_t) kHdrChunks; ++k) stage[hdr_slot(lane, k)] = make_uint4(0u, 0u, 0u, 0u);
   }
   __syncthreads();
   uint64_t n = P.n;
@@ -345,15 +343,17 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   const uint64_t ntiles = n > P.j0 ? (n - P.j0 + kWave - 1) / kWave : 0;
   const uint64_t nwaves = (uint64_t) gridDim.x * kDlvWpb;
   const uint64_t msize = P.mem_size;
-  // where lanes without a whole aligned window load from: the image start, or
-  // the write records for an image below 16 B (always >= 40 readable bytes)
+  // where lanes without a hot chunk load from: the image start, or the write
+  // records for an image below 16 B (always >= 40 readable bytes)
   const uint8_t* dummy = msize >= 16u ? P.mem : reinterpret_cast<const uint8_t*>(P.w);
   uint32_t my_count = 0;
   for (uint64_t tile = (uint64_t) blockIdx.x * kDlvWpb + w; tile < ntiles; tile += nwaves) {
     // ---- this lane's write: its items and their stream entries
     const uint64_t j = P.j0 + tile * kWave + lane;
     uint32_t F, c0, c1, c2, total_e;
-    bool flag;
+    bool flag, hdr_src;
+    uint32_t hlo;       // the staged header's byte offset (HdrView lo)
+    u32x4 hdr[kHdrChunks];  // the frame's first bytes, from its source (hdr_src frames)
     {
       nicgpu_segment_write wr{};
       flag = false;
@@ -369,6 +369,20 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
                                    wr.src_a > msize || wr.len_a > msize - wr.src_a ||
                                    wr.src_b > msize || wr.len_b > msize - wr.src_b);
       flag = flag && ok;
+      // RSS: a frame whose first 48 bytes are all part A's (no VLAN prefix)
+      // stages them from the source now, in flight during the stream; the
+      // others are staged byte by byte at the tile end
+      hdr_src = kHash && flag && plen == 0 && (wr.len_a >= (uint32_t) kHdrBytes || wr.len_b == 0);
+      hlo = (uint32_t) ((hdr_src ? wr.src_a : wr.dst) & 15u);
+      {
+        const uint64_t hb = wr.src_a & ~15ull;
+        const uint64_t hend = wr.src_a + (wr.len_a < (uint32_t) kHdrBytes ? wr.len_a : (uint32_t) kHdrBytes);
+#pragma unroll
+        for (int k = 0; k < kHdrChunks; ++k) {
+          const bool need = hdr_src && hb + 16u * k < hend;
+          hdr[k] = *reinterpret_cast<const u32x4*>(need ? P.mem + hb + 16u * k : dummy);
+        }
+      }
       const uint64_t d1 = wr.dst + plen, d2 = d1 + wr.len_a;
       c0 = ok ? dlv_chunks(wr.dst, plen) : 0u;
       c1 = ok ? dlv_chunks(d1, wr.len_a) : 0u;
@@ -377,21 +391,30 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
       const uint32_t incl = wave_incl_scan(cw);
       F = incl - cw;
       total_e = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
-      const uint64_t fc = wr.dst >> 4;  // the frame's first chunk
       // (lengths kept for the hash even for items without chunks: ok frames only)
-      auto put = [&](uint32_t k, uint64_t d, uint64_t src_or_word, uint64_t len, uint32_t first) __attribute__((always_inline)) {
+      auto put = [&](uint32_t k, uint64_t d, uint64_t src_or_word, uint64_t len, uint32_t first, uint32_t nch)
+                     __attribute__((always_inline)) {
         Item it;
         it.dbase = (Off) ((d >> 4) - first);
-        it.sdelta = k == 0u ? (Off) src_or_word : (Off) (src_or_word - d);
+        it.sdelta = k == 0u ? (Off) 1 : (Off) (src_or_word - d);
         it.d = (Off) d;
         it.dend = (Off) (d + (ok ? len : 0u));
-        it.kcb = first - (uint32_t) ((d >> 4) - fc);
-        it.meta = lane | (k << 6) | (flag ? 1u << 8 : 0u);
+        // hot entries: the item's whole chunks (d and d + len cut the first
+        // and last), when the source is 4-aligned to the destination and every
+        // hot window lies in the image (it does: whole chunks read their own
+        // 16 bytes, inside the source)
+        const uint64_t e = d + len;
+        const uint32_t whole_lo = (d & 15u) ? 1u : 0u;
+        const uint32_t whole_hi = (e & 15u) ? 1u : 0u;
+        const bool aligned = k != 0u && ((src_or_word - d) & 3u) == 0u && nch > whole_lo + whole_hi;
+        const uint32_t hn = aligned ? nch - whole_lo - whole_hi : 0u;
+        it.h0 = k == 0u ? (uint32_t) src_or_word : first + whole_lo;
+        it.meta = hn | (k << 20) | (lane << 22);
         items[lane * 3u + k] = it;
       };
-      put(0, wr.dst, wr.prefix, plen, F);
-      put(1, d1, wr.src_a, wr.len_a, F + c0);
-      put(2, d2, wr.src_b, wr.len_b, F + c0 + c1);
+      put(0, wr.dst, wr.prefix, plen, F, c0);
+      put(1, d1, wr.src_a, wr.len_a, F + c0, c1);
+      put(2, d2, wr.src_b, wr.len_b, F + c0 + c1, c2);
     }
     uint32_t carry = 0;  // item (id + 1) of the entry before the step being planned
     // ---- load phase of the step at stream position W
@@ -415,22 +438,18 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
         const uint32_t id = valid ? it - 1u : 0u;
         const Item I = items[id];
         const Off D = (I.dbase + (Off) pos) << 4;
+        const bool hot = valid && pos - I.h0 < (I.meta & 0xFFFFFu);
+        // partial chunks load their window too when it is 4-aligned and in the
+        // image (below 0 wraps, out), so the store phase never loads but for
+        // unaligned sources (every load here is unconditional)
         const Off a = D + I.sdelta;
-        const uint32_t x = I.d > D ? (uint32_t) (I.d - D) : 0u;
-        const uint32_t y = I.dend - D < 16u ? (uint32_t) (I.dend - D) : 16u;
-        const uint32_t k = (I.meta >> 6) & 3u;
-        // a chunk whose 4-aligned source window lies in the image (the item's
-        // source less up to 15 bytes on its first chunk: below 0 wraps, out)
-        const bool in = msize >= 16u && a <= (Off) msize - 16u && (a & 3u) == 0u && k != 0u;
-        const uint32_t kc32 = pos - I.kcb;
-        const uint32_t kc = (RSS && (MODE & kDlvNoHash) == 0 && (I.meta & 256u) && kc32 < (uint32_t) kHdrChunks) ? kc32 : 3u;
+        const bool loaded = hot || (valid && (a & 3u) == 0u && msize >= 16u && a <= (Off) msize - 16u);
         S.D[u] = D;
-        // (lanes without an entry leave the word 0: x / y belong to another item)
-        S.pk[u] = valid ? x | (y << 5) | (id << 10) | (kc << 18) | ((uint32_t) in << 20) | (1u << 21) : 0u;
+        S.pk[u] = id | ((uint32_t) hot << 8) | ((uint32_t) valid << 9) | ((uint32_t) loaded << 10);
         if constexpr ((MODE & kDlvNoLoad) != 0) {
-          S.v[u] = (u32x4){(uint32_t) a, 1u, 2u, 3u};
+          S.v[u] = (u32x4){(uint32_t) D, 1u, 2u, 3u};
         } else {
-          S.v[u] = *reinterpret_cast<const u32x4*>(((valid && in) ? P.mem + a : dummy));
+          S.v[u] = *reinterpret_cast<const u32x4*>(loaded ? P.mem + a : dummy);
         }
       }
     };
@@ -440,60 +459,53 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
 #pragma unroll
       for (int u = 0; u < kDlvU; ++u) {
         const uint32_t pk = S.pk[u];
-        const bool hot = (pk & ((1u << 20) | 1023u)) == ((1u << 20) | (16u << 5));  // loaded, bytes [0, 16)
-        if (hot) {
+        if (pk & 256u) {
           if constexpr ((MODE & kDlvNoStore) != 0) {
             if ((S.v[u].x ^ S.v[u].w) == 0x12345678u) P.mem[S.D[u]] = 0;  // keeps the loads
           } else {
             *reinterpret_cast<u32x4*>(P.mem + S.D[u]) = S.v[u];
           }
-          const uint32_t kc = (pk >> 18) & 3u;
-          if (kc < 3u)
-            stage[hdr_slot(items[(pk >> 10) & 255u].meta & 63u, kc)] = make_uint4(S.v[u].x, S.v[u].y, S.v[u].z, S.v[u].w);
         }
-        slow = slow || (((pk >> 21) & 1u) && !hot);
+        slow = slow || (pk & 768u) == 512u;
       }
       if (slow) {
-        // partial chunks, unaligned or out-of-image sources, VLAN prefixes;
-        // the loads here are waited for inside this branch only
+        // partial chunks, unaligned or out-of-image sources, VLAN prefixes:
+        // bytes [x, y) of the chunk, read here (waited for in this branch only)
 #pragma unroll
         for (int u = 0; u < kDlvU; ++u) {
           const uint32_t pk = S.pk[u];
-          const uint32_t x = pk & 31u, y = (pk >> 5) & 31u;
-          const bool loaded = (pk >> 20) & 1u;
-          if (!((pk >> 21) & 1u) || (loaded && x == 0u && y == 16u)) continue;
+          if ((pk & 768u) != 512u) continue;
           const Off D = S.D[u];
-          const Item I = items[(pk >> 10) & 255u];
-          const uint32_t q = I.meta & 63u, k = (I.meta >> 6) & 3u, kc = (pk >> 18) & 3u;
+          const Item I = items[pk & 255u];
+          const uint32_t k = (I.meta >> 20) & 3u;
+          const uint32_t x = I.d > D ? (uint32_t) (I.d - D) : 0u;
+          const uint32_t y = I.dend - D < 16u ? (uint32_t) (I.dend - D) : 16u;
           uint32_t o[4] = {S.v[u].x, S.v[u].y, S.v[u].z, S.v[u].w};
-          if (!loaded) {
-            if (k == 0u) {
-              // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): its 4 bytes at d
-              const uint32_t pw = (uint32_t) I.sdelta;
-              const int32_t rel = (int32_t) (I.d - D);
+          if (k == 0u) {
+            // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): its 4 bytes at d
+            const uint32_t pw = I.h0;
+            const int32_t rel = (int32_t) (I.d - D);
 #pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                uint32_t z = 0;
+            for (int i = 0; i < 4; ++i) {
+              uint32_t z = 0;
 #pragma unroll
-                for (int bb = 0; bb < 4; ++bb) {
-                  const int32_t pb = 4 * i + bb - rel;
-                  if (pb >= 0 && pb < 4) z |= ((pw >> (8 * pb)) & 0xFFu) << (8 * bb);
-                }
-                o[i] = z;
+              for (int bb = 0; bb < 4; ++bb) {
+                const int32_t pb = 4 * i + bb - rel;
+                if (pb >= 0 && pb < 4) z |= ((pw >> (8 * pb)) & 0xFFu) << (8 * bb);
               }
-            } else {
-              // the chunk's bytes [x, y) from the source, byte by byte (rare:
-              // unaligned sources and windows leaving the image)
-              const Off s0 = D + I.sdelta;
-              o[0] = o[1] = o[2] = o[3] = 0u;
+              o[i] = z;
+            }
+          } else if (!((pk >> 10) & 1u)) {
+            // byte by byte (rare: unaligned sources, windows leaving the image)
+            const Off s0 = D + I.sdelta;
+            o[0] = o[1] = o[2] = o[3] = 0u;
 #pragma unroll 1
-              for (uint32_t b = x; b < y; ++b) {
-                const uint32_t z = (uint32_t) P.mem[(Off) (s0 + b)] << (8u * (b & 3u));
-                o[0] |= (b >> 2) == 0u ? z : 0u;
-                o[1] |= (b >> 2) == 1u ? z : 0u;
-                o[2] |= (b >> 2) == 2u ? z : 0u;
-                o[3] |= (b >> 2) == 3u ? z : 0u;
-              }
+            for (uint32_t b = x; b < y; ++b) {
+              const uint32_t z = (uint32_t) P.mem[(Off) (s0 + b)] << (8u * (b & 3u));
+              o[0] |= (b >> 2) == 0u ? z : 0u;
+              o[1] |= (b >> 2) == 1u ? z : 0u;
+              o[2] |= (b >> 2) == 2u ? z : 0u;
+              o[3] |= (b >> 2) == 3u ? z : 0u;
             }
           }
           if constexpr ((MODE & kDlvNoStore) == 0) {
@@ -502,14 +514,6 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
               *reinterpret_cast<u32x4*>(P.mem + D) = vq;
             } else {
               dlv_store_partial(P.mem, (uint64_t) D, x, y, o);
-            }
-          }
-          if (kc < 3u) {
-            uint32_t* st = reinterpret_cast<uint32_t*>(stage + hdr_slot(q, kc));
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const uint32_t keep = dword_keep((int) x, (int) y, i);
-              if (keep) atomicOr(st + i, o[i] & keep);
             }
           }
         }
@@ -521,6 +525,15 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
     // in vmcnt, in order with the loads); a counted loop with its only exit at
     // the bottom keeps counted waits; plans past the last step are empty
     const uint32_t nsteps = (total_e + kSpan - 1) / kSpan;
+    bool staged = false;
+    auto stage_hdr = [&]() __attribute__((always_inline)) {
+      // the header loads were issued before every step's: done by now
+      if (kHash && !staged) {
+#pragma unroll
+        for (int k = 0; k < kHdrChunks; ++k) stage[hdr_slot(lane, (uint32_t) k)] = make_uint4(hdr[k].x, hdr[k].y, hdr[k].z, hdr[k].w);
+        staged = true;
+      }
+    };
     if (nsteps) {
       DlvStep<WIDE> A, B, C;
       plan(A, 0);
@@ -530,6 +543,7 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
         plan(C, (s + 2) * kSpan);
         __builtin_amdgcn_sched_barrier(0);
         store(A);
+        stage_hdr();
         plan(A, (s + 3) * kSpan);
         __builtin_amdgcn_sched_barrier(0);
         store(B);
@@ -540,9 +554,8 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
       if (s < nsteps) store(A);
       if (s + 1 < nsteps) store(B);
     }
-    if (RSS && (MODE & kDlvNoHash) == 0) {
-      // the frames' header bytes are in the stage (LDS, in order within the
-      // wave); bytes past it come from the sources — no wait for the stores
+    if (kHash) {
+      stage_hdr();
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       if (j < n) {
@@ -553,8 +566,14 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
           uint64_t len = (uint64_t) plen + len_a + len_b;
           if (len > NICGPU_MAX_PACKET) len = NICGPU_MAX_PACKET;  // the tuple lies in the first 82 B
           const FrameParts fp{P.mem, (uint64_t) (Off) (I1.d + I1.sdelta), (uint64_t) (Off) (I2.d + I2.sdelta),
-                              (uint32_t) I0.sdelta, plen, len_a};
-          const uint32_t h = rss_hash_packet(R, lut, HdrView{stage, lane}, (uint32_t) (I0.d & 15u), fp, (uint32_t) len);
+                              I0.h0, plen, len_a};
+          if (!hdr_src) {
+            // a VLAN prefix or a part A shorter than the header: staged byte by byte
+            uint8_t* sb = reinterpret_cast<uint8_t*>(stage + hdr_slot(lane, 0));
+            const uint32_t nb = len < (uint64_t) kHdrBytes - hlo ? (uint32_t) len : (uint32_t) kHdrBytes - hlo;
+            for (uint32_t o = 0; o < nb; ++o) sb[hdr_slot(0, (hlo + o) >> 4) * 16u + ((hlo + o) & 15u)] = (uint8_t) fp[o];
+          }
+          const uint32_t h = rss_hash_packet(R, lut, HdrView{stage, lane}, hlo, fp, (uint32_t) len);
           const uint32_t idx = h % R.table_n;
           P.rx_hash[j] = h;
           P.rx_queue[j] = table_lds ? table_s[idx] : R.table[idx];
@@ -568,11 +587,7 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#pragma unroll
-      for (uint32_t k = 0; k < (uint32_t) kHdrChunks; ++k) stage[hdr_slot(lane, k)] = make_uint4(0u, 0u, 0u, 0u);
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   }
   if (RSS) {
     const uint32_t c = (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan(my_count), 63);
