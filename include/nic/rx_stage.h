@@ -314,10 +314,13 @@ struct Piece {
 //               [4, L) in runs of <= 65534 bytes
 //   kSegmented  H >= 4: [0, 4), [4, H), then chunk k = [H + k*mss, +len_k);
 //               H < 4:  [0, H), then per chunk [.., +min(4 - H, len_k)) and its rest
+//   kPlainSplit (split plans, the device stage's) the whole packet in runs of
+//               <= 65534 bytes: one piece below 64 KiB, the first piece's sum
+//               taken split as its first min(4, L) bytes and the rest
 // Segment sums are composed from pieces (first 4 bytes | the rest, so that a
 // VLAN strip of a segment's first 4 bytes, queue_pair.cpp:392-395, is exact).
 struct PacketPlan {
-  enum Kind : std::uint8_t { kNoBytes, kPlain, kSegmented };
+  enum Kind : std::uint8_t { kNoBytes, kPlain, kSegmented, kPlainSplit };
   Kind kind{kNoBytes};
   std::uint32_t nseg{0};  // segments build_segments produces (kSegmented)
   std::uint32_t first_piece{0};
@@ -326,9 +329,14 @@ struct PacketPlan {
   std::uint32_t mss{0};      // (kSegmented)
 };
 
+/// Piece sums of a plan: piece_csum[i] = compute_checksum(bytes of pieces[i]);
+/// for a split plan (split4) 2 x pieces.size() entries instead — those of every
+/// piece's bytes past its first 4, then those of its first min(4, len) bytes
+/// (nicgpu_checksum_batch_split's two outputs).
 struct Plan {
   std::vector<PacketPlan> packets;
   std::vector<Piece> pieces;
+  bool split4{false};
 };
 
 /// One DMA write: dst <- prefix (0 or 4 bytes) || [src_a, +len_a) || [src_b, +len_b).
@@ -349,13 +357,16 @@ static_assert(sizeof(SegmentWrite) == 40);
 /// place.  O(n + m) for buffers laid out in ascending order, a sort otherwise.
 bool buffers_disjoint(std::size_t mem_size, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx);
 
-Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx);
+/// split4: kPlainSplit plans for plain packets (Plan::split4), as the device plans them.
+Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
+               bool split4 = false);
 /// The same into `plan`, reusing its storage (no page faults once it has grown).
 void make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
-               Plan& plan);
+               Plan& plan, bool split4 = false);
 
-/// The reference's sequential control flow over the batch, given
-/// piece_csum[i] = compute_checksum(bytes of plan.pieces[i]).  Fills
+/// The reference's sequential control flow over the batch, given the plan's
+/// piece sums (Plan: piece_csum[i] = compute_checksum(bytes of plan.pieces[i]),
+/// split in two halves for a split plan).  Fills
 /// out.tx_completions / out.rx_completions (replacing their contents), sets
 /// out.tx_processed / rx_consumed, adds to `stats`, fires interrupts in
 /// posting order, and lists the DMA writes: writes[j] belongs to RX completion

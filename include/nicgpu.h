@@ -168,6 +168,14 @@ int nicgpu_rx_offload_ex(const nicgpu_rss_ctx* ctx, const uint8_t* frames, const
 int nicgpu_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n,
                           uint16_t* out_csum, void* stream);
 
+/* Split sums (the batched QueuePair stage's piece pass, one piece per plain
+ * packet): out_head4[i] = compute_checksum(first min(4, len_i) bytes of frame
+ * i), out_rest[i] = compute_checksum(its bytes past the first 4) — the two
+ * sums queue_pair.cpp:392-395 / :434-447 take of a segment with and without
+ * its VLAN tag, from one pass over the frame. */
+int nicgpu_checksum_batch_split(const uint8_t* frames, const uint64_t* desc, size_t n, uint16_t* out_rest,
+                                uint16_t* out_head4, void* stream);
+
 /* Per-segment checksums of TSO/GSO segmentation without materialising the
  * segments: for frame i (desc[i]) with header length hdr_len[i] and mss[i],
  * segment k = frame[0:H] || frame[H + k*mss : min(L, H + (k+1)*mss)], and
@@ -313,7 +321,8 @@ typedef struct nicgpu_qp_view {
   nicgpu_tx_descriptor* tx;     /* [ntx]  the caller uploads the TX descriptors here */
   nicgpu_rx_descriptor* rx;     /* [nrx]  and the RX descriptors (the ring, rx[0] first) */
   uint32_t* piece_base;         /* [ntx + 1] first piece of each TX descriptor */
-  uint16_t* piece_csum;         /* [npieces] compute_checksum of each piece */
+  uint16_t* piece_csum;         /* [2 npieces] split sums of each piece (nicgpu_checksum_batch_split):
+                                   [0, npieces) past its first 4 bytes, then [npieces, 2 npieces) its first 4 */
   nicgpu_completion* txc;       /* [ntx]  TX completions, in posting order */
   nicgpu_completion* rxc;       /* [nrx]  RX completions, in posting order */
   nicgpu_segment_write* writes; /* [nrx]  DMA write of RX completion j (all lengths 0: none) */

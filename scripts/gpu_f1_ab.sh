@@ -1,25 +1,17 @@
-#!/bin/bash
-# Row f1 A/B: the f1 GPU tests on the production build, then the pipelined C3 stage bench and
-# the deliver_kernel's average duration (kernel trace) per deliver-kernel variant
-# (smart_nic_amd/ab/<variant>/libnicgpu.so, picked up through LD_LIBRARY_PATH).
+# f1 delivery A/B: the f1 GPU tests on the production build, then the
+# delivery attribution on libnicgpu_tune.so and on each extra tuning library
+# named in AB_LIBS (built in-tree beforehand), then the stage's C3 1 M batch.
 set -o pipefail
-R=$GRAFT_REPO_ROOT
-mkdir -p $R/gpurun_out/f1ab
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -v -k "rx_stage or f1_full or queue_manager" --timeout 300 --timeout-method thread > gpurun_out/f1ab/test.log 2>&1; rc=$?
-grep -E "passed|failed" gpurun_out/f1ab/test.log | tail -3; [ $rc -eq 0 ] || exit $rc
-ARGS="c3 1048576 12 0 device device pipelined device"
-cd /tmp && export TMPDIR=/tmp
-for v in prod ${VARIANTS:-u2 u8 w4 w16u2}; do
-  if [ $v = prod ]; then LP=""; else LP=$R/smart_nic_amd/ab/$v; fi
-  LD_LIBRARY_PATH=$LP timeout -k 10 120 $R/tools/bin/bench_rx_stage $ARGS > $R/gpurun_out/f1ab/$v.json 2>&1 || { echo "$v bench failed"; tail -3 $R/gpurun_out/f1ab/$v.json; exit 1; }
-  LD_LIBRARY_PATH=$LP timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/f1ab/tr_$v -o f1 --output-format csv -- $R/tools/bin/bench_rx_stage c3 1048576 6 0 device device pipelined device > $R/gpurun_out/f1ab/tr_$v.log 2>&1 || { echo "$v trace failed"; exit 1; }
-  python3 - $v <<'PY'
-import csv, glob, json, os, sys
-v = sys.argv[1]
-R = os.environ["GRAFT_REPO_ROOT"] + "/gpurun_out/f1ab"
-j = [l for l in open(f"{R}/{v}.json") if l.startswith("{")][-1]
-st = glob.glob(f"{R}/tr_{v}/**/*kernel_stats.csv", recursive=True)[0]
-d = [r for r in csv.DictReader(open(st)) if "deliver_kernel" in r["Name"]]
-print(v, "pipelined_us", json.loads(j)["us_median"], "deliver_avg_us", [round(float(r["AverageNs"]) / 1e3, 1) for r in d])
-PY
+mkdir -p gpurun_out
+PT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
+timeout -k 10 120 $PT -m gpu tests/test_gpu_unaligned.py > gpurun_out/f1_unaligned.log 2>&1 || { tail -20 gpurun_out/f1_unaligned.log; exit 1; }
+timeout -k 10 500 $PT -m gpu tests/test_rx_stage.py tests/test_queue_manager.py tests/test_gpu_fullsize.py ${EXTRA_TESTS} > gpurun_out/f1_pytest.log 2>&1
+rc=$?; tail -4 gpurun_out/f1_pytest.log; [ $rc -eq 0 ] || exit $rc
+for lib in smart_nic_amd/libnicgpu_tune.so ${AB_LIBS}; do
+  timeout -k 10 300 python tools/f1_deliver_bench.py --lib $lib ${ATTR_ARGS} >> gpurun_out/f1attr.json 2> gpurun_out/f1attr.err || { tail gpurun_out/f1attr.err; exit 1; }
+done
+cat gpurun_out/f1attr.json
+for mode in pipelined sync; do
+  timeout -k 10 200 tools/bin/bench_rx_stage c3 1048576 12 0 device device $mode device > gpurun_out/f1_c3_$mode.json 2> gpurun_out/f1_c3.err || { tail gpurun_out/f1_c3.err; exit 1; }
+  cat gpurun_out/f1_c3_$mode.json
 done

@@ -70,6 +70,7 @@ ABI_SYMBOLS = (
     "nicgpu_rx_offload",
     "nicgpu_rx_offload_ex",
     "nicgpu_checksum_batch",
+    "nicgpu_checksum_batch_split",
     "nicgpu_tso_checksum",
     "nicgpu_segment_gather",
     "nicgpu_segment_gather_from",
@@ -145,6 +146,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_icrc_batch": (i32, [vp, vp, sz, i32, vp, vp, vp]),
         "nicgpu_tso_segment": (i32, [vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint64, u32, vp, vp, vp]),
         "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),
+        "nicgpu_checksum_batch_split": (i32, [vp, vp, sz, vp, vp, vp]),
         "nicgpu_stream_create": (i32, [ctypes.POINTER(vp)]),
         "nicgpu_stream_destroy": (i32, [vp]),
         "nicgpu_event_create": (i32, [ctypes.POINTER(vp)]),

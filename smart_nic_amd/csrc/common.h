@@ -142,6 +142,7 @@ struct RxParams {
   uint16_t* out_queue;
   unsigned long long* out_hits;
   uint8_t* out_l34;  // NICGPU_L34_* flags (L3/L4 checksum verification), may be null
+  uint16_t* out_cs4;  // split sums (no RSS): checksum of each packet's first min(4, len) bytes, out_csum then of the rest
   uint32_t hold_r;   // RING kernels: tiles of results each wave holds in LDS before storing them (>= 1)
   uint32_t ring_off; // RING kernels: LDS byte offset of wave 0's result ring (wave w at + w * hold_r * 512)
   uint32_t xpf_chunks;  // XPF kernels: prefetch the next tile's first batch when it has at most this many chunks

@@ -151,7 +151,10 @@ struct DeliverParams {
 
 // Tuning-only modes of deliver_kernel (libnicgpu_tune.so, tools/f1_deliver_bench.py;
 // results are wrong with any set): attribute the delivery's time.
-constexpr int kDlvNoStore = 1, kDlvNoLoad = 2, kDlvNoHash = 4, kDlvPackedDst = 8, kDlvNoDrain = 16, kDlvV1 = 32;
+constexpr int kDlvNoStore = 1, kDlvNoLoad = 2, kDlvNoHash = 4, kDlvPackedDst = 8, kDlvV1 = 32;
+#ifdef NICGPU_TUNING
+constexpr int kDlvNoDrain = 16;  // deliver_v1_kernel only
+#endif
 
 #ifndef NICGPU_DLV_WPB
 #define NICGPU_DLV_WPB 8
@@ -177,6 +180,7 @@ __device__ __forceinline__ uint32_t dlv_chunks(uint64_t d, uint64_t n) {
   return n ? (uint32_t) (((d + n - 1) >> 4) - (d >> 4) + 1) : 0u;
 }
 
+#ifdef NICGPU_TUNING
 // Stores the bytes [lo, hi) (absolute) of the 16-B destination chunk at D
 // from o; whole chunk: one 16-B store, else whole dwords and bytes.
 __device__ __forceinline__ void dlv_store(uint8_t* mem, uint64_t D, uint64_t lo, uint64_t hi, const uint32_t* o) {
@@ -197,6 +201,8 @@ __device__ __forceinline__ void dlv_store(uint8_t* mem, uint64_t D, uint64_t lo,
     }
   }
 }
+
+#endif
 
 // The source parts of a delivered frame, as rss_hash_packet reads bytes past
 // the LDS header stage: frame byte o is the VLAN prefix word's byte o (o <
@@ -252,22 +258,27 @@ __device__ __forceinline__ void dlv_store_partial(uint8_t* mem, uint64_t D, uint
 // ---- the delivery's steps -------------------------------------------------
 // Attribution of round 3's kernel (tools/f1_deliver_bench.py, C3 1 M):
 // 234 us, of which 87 us with neither loads nor stores (the stream mapping's
-// instructions: SQ_INSTS_VALU 60 M), loads alone +22 us, stores alone +80 us
-// (842 K store instructions for 369 K 64-entry sub-steps: a per-dword and
-// per-byte walk of every partial chunk, executed by the whole wave whenever one
-// lane had one), and the two never overlapped.  So the hot path here is lean:
-// a chunk that is whole, from a 4-aligned source inside the image (every chunk
-// but the edges of a frame for any sane buffer alignment) is one 16-B load and
-// one 16-B store with no other work; the others (partial chunks, unaligned or
-// out-of-image sources, VLAN prefix items) take a slow path that the wave runs
-// only when one of its lanes needs it, and partial chunks whose 16-B source
-// window could be loaded do so without another load.  Offsets are 32-bit for
-// images below 4 GiB (template WIDE otherwise).  Steps are pipelined: step
-// s+1's loads are issued before step s's stores.
+// instructions: SQ_INSTS_VALU 60 M), loads alone +22 us, stores alone +80 us,
+// and the two never overlapped.  Round 4's counters (profiles/r04b_f1_stall.txt)
+// then showed what bounds a lean stream: the texture addresser, 85 % busy at
+// 721 K store instructions where a copy of the same bytes needs 364 K — a
+// partial chunk (every 1518-B frame ends 14 B into one) cost four exec-masked
+// stores, each as dear to the addresser as a whole 16-B one.  So every chunk
+// of an item of 16 B or more is ONE 16-B load and ONE 16-B store: the window
+// [W, W + 16) with W = the chunk's start clamped into [d, e - 16] — an edge
+// chunk's window reaches into its neighbour, whose bytes it rewrites with
+// their own values (both lie in the item), so no byte outside the item is
+// written and the result is the same in any order.  Edge windows are byte
+// aligned: gfx950 global accesses in the HSA unaligned mode (the mode hipcc
+// compiles memcpy of byte pointers for; tests/test_gpu_unaligned.py).  Only
+// VLAN prefixes and items under 16 B take a slow path, which the wave runs
+// only when one of its lanes has one.  Offsets are 32-bit for images below
+// 4 GiB (template WIDE otherwise).  Steps are pipelined: step s+1's loads are
+// issued before step s's stores.
 #ifndef NICGPU_DLV_U
 #define NICGPU_DLV_U 2
 #endif
-constexpr int kDlvU = NICGPU_DLV_U;  // 64-entry sub-steps per step (two steps in flight)
+constexpr int kDlvU = NICGPU_DLV_U;  // 64-entry sub-steps per step
 static_assert(kDlvU <= kDlvU1, "marks area");
 
 template <bool WIDE>
@@ -275,37 +286,40 @@ struct DlvOff { typedef uint32_t T; };
 template <>
 struct DlvOff<true> { typedef uint64_t T; };
 
-// An item (a write's VLAN prefix, part A or part B) as the steps read it, one
-// LDS record per item, so that a chunk of the hot path costs a few adds:
-// destination chunk D = (dbase + pos) << 4, source a = D + sdelta, and it is
-// hot (whole, from a 4-aligned window inside the image) iff pos - h0 < hn.
+// An item (a write's VLAN prefix, part A or part B) as the steps read it: the
+// window fields in one 16-B (narrow) LDS record, so that a chunk costs a few
+// adds — chunk D = (dbase + pos) << 4, window W = min(max(D, lo), hi), source
+// W + sdelta — and a meta word beside it.  The item's bytes are [lo, hi + 16).
 template <bool WIDE>
-struct DlvItem {
+struct DlvWin {
   typedef typename DlvOff<WIDE>::T Off;
   Off dbase;   // (d >> 4) - first entry (wrapping)
-  Off sdelta;  // src - d (wrapping); 1 for a VLAN prefix item (its windows are never loaded)
-  Off d, dend;
-  uint32_t h0;    // first hot entry; the prefix word for a VLAN prefix item
-  uint32_t meta;  // hot entries (0-19) | item k (20-21) | write q (22-27)
+  Off sdelta;  // src - d (wrapping); the prefix word for a VLAN prefix item
+  Off lo, hi;  // d, e - 16 (wrapping)
 };
+// meta: window item (bit 0: 16 B or more, not a prefix) | item k (1-2) | write q (3-8)
+constexpr uint32_t kDlvWinItem = 1u;
 
 // One step held between its loads and its stores.
 template <bool WIDE>
 struct DlvStep {
-  typename DlvOff<WIDE>::T D[kDlvU];  // destination chunk address
-  uint32_t pk[kDlvU];  // item id (0-7) | hot (8) | valid (9) | loaded (10: the 4-aligned window at a, in the image)
-  u32x4 v[kDlvU];      // the source window at a (loaded lanes)
+  typename DlvOff<WIDE>::T D[kDlvU];  // the window W (window items), else the chunk D
+  uint32_t pk[kDlvU];  // item id (0-7) | window (8) | valid (9)
+  u32x4 v[kDlvU];      // the source window (window items)
 };
 
+// marks | windows | metas; the RSS header stage takes the windows' place at
+// the tile end, once every lane holds its own three (it is no larger)
 template <bool WIDE>
-__host__ __device__ constexpr uint32_t dlv_wave_bytes() {  // marks | items | stage
-  return kDlvMarks + 192u * (uint32_t) sizeof(DlvItem<WIDE>) + 64u * kHdrStride * 16u;
+__host__ __device__ constexpr uint32_t dlv_wave_bytes() {
+  static_assert(192u * sizeof(DlvWin<WIDE>) >= 64u * kHdrStride * 16u, "stage fits the windows");
+  return kDlvMarks + 192u * (uint32_t) sizeof(DlvWin<WIDE>) + 192u * 4u;
 }
 
 template <bool RSS, int MODE, bool WIDE>
 __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   typedef typename DlvOff<WIDE>::T Off;
-  typedef DlvItem<WIDE> Item;
+  typedef DlvWin<WIDE> Win;
   constexpr uint32_t kThreads = kWave * kDlvWpb;
   constexpr uint32_t kSpan = kWave * kDlvU;
   constexpr bool kHash = RSS && (MODE & kDlvNoHash) == 0;
@@ -324,8 +338,9 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   uint32_t* cnt_s = reinterpret_cast<uint32_t*>(base_b + block_bytes - 16u);
   uint8_t* wave_b = base_b + block_bytes + w * dlv_wave_bytes<WIDE>();
   uint8_t* marks = wave_b;
-  Item* items = reinterpret_cast<Item*>(wave_b + kDlvMarks);
-  uint4* stage = reinterpret_cast<uint4*>(items + 192);
+  Win* wins = reinterpret_cast<Win*>(wave_b + kDlvMarks);
+  uint32_t* metas = reinterpret_cast<uint32_t*>(wins + 192);
+  uint4* stage = reinterpret_cast<uint4*>(wins);  // at the tile end
   if (RSS) {
     for (uint32_t i = threadIdx.x; i < R.lut_words; i += kThreads) lut[i] = R.lut[i];
     if (hist_lds)
@@ -343,7 +358,7 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   const uint64_t ntiles = n > P.j0 ? (n - P.j0 + kWave - 1) / kWave : 0;
   const uint64_t nwaves = (uint64_t) gridDim.x * kDlvWpb;
   const uint64_t msize = P.mem_size;
-  // where lanes without a hot chunk load from: the image start, or the write
+  // where lanes without a window load from: the image start, or the write
   // records for an image below 16 B (always >= 40 readable bytes)
   const uint8_t* dummy = msize >= 16u ? P.mem : reinterpret_cast<const uint8_t*>(P.w);
   uint32_t my_count = 0;
@@ -351,9 +366,7 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
     // ---- this lane's write: its items and their stream entries
     const uint64_t j = P.j0 + tile * kWave + lane;
     uint32_t F, c0, c1, c2, total_e;
-    bool flag, hdr_src;
-    uint32_t hlo;       // the staged header's byte offset (HdrView lo)
-    u32x4 hdr[kHdrChunks];  // the frame's first bytes, from its source (hdr_src frames)
+    bool flag;
     {
       nicgpu_segment_write wr{};
       flag = false;
@@ -369,20 +382,6 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
                                    wr.src_a > msize || wr.len_a > msize - wr.src_a ||
                                    wr.src_b > msize || wr.len_b > msize - wr.src_b);
       flag = flag && ok;
-      // RSS: a frame whose first 48 bytes are all part A's (no VLAN prefix)
-      // stages them from the source now, in flight during the stream; the
-      // others are staged byte by byte at the tile end
-      hdr_src = kHash && flag && plen == 0 && (wr.len_a >= (uint32_t) kHdrBytes || wr.len_b == 0);
-      hlo = (uint32_t) ((hdr_src ? wr.src_a : wr.dst) & 15u);
-      {
-        const uint64_t hb = wr.src_a & ~15ull;
-        const uint64_t hend = wr.src_a + (wr.len_a < (uint32_t) kHdrBytes ? wr.len_a : (uint32_t) kHdrBytes);
-#pragma unroll
-        for (int k = 0; k < kHdrChunks; ++k) {
-          const bool need = hdr_src && hb + 16u * k < hend;
-          hdr[k] = *reinterpret_cast<const u32x4*>(need ? P.mem + hb + 16u * k : dummy);
-        }
-      }
       const uint64_t d1 = wr.dst + plen, d2 = d1 + wr.len_a;
       c0 = ok ? dlv_chunks(wr.dst, plen) : 0u;
       c1 = ok ? dlv_chunks(d1, wr.len_a) : 0u;
@@ -392,29 +391,20 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
       F = incl - cw;
       total_e = (uint32_t) __builtin_amdgcn_readlane((int) incl, 63);
       // (lengths kept for the hash even for items without chunks: ok frames only)
-      auto put = [&](uint32_t k, uint64_t d, uint64_t src_or_word, uint64_t len, uint32_t first, uint32_t nch)
+      auto put = [&](uint32_t k, uint64_t d, uint64_t src_or_word, uint64_t len, uint32_t first)
                      __attribute__((always_inline)) {
-        Item it;
+        if (!ok) len = 0;
+        Win it;
         it.dbase = (Off) ((d >> 4) - first);
-        it.sdelta = k == 0u ? (Off) 1 : (Off) (src_or_word - d);
-        it.d = (Off) d;
-        it.dend = (Off) (d + (ok ? len : 0u));
-        // hot entries: the item's whole chunks (d and d + len cut the first
-        // and last), when the source is 4-aligned to the destination and every
-        // hot window lies in the image (it does: whole chunks read their own
-        // 16 bytes, inside the source)
-        const uint64_t e = d + len;
-        const uint32_t whole_lo = (d & 15u) ? 1u : 0u;
-        const uint32_t whole_hi = (e & 15u) ? 1u : 0u;
-        const bool aligned = k != 0u && ((src_or_word - d) & 3u) == 0u && nch > whole_lo + whole_hi;
-        const uint32_t hn = aligned ? nch - whole_lo - whole_hi : 0u;
-        it.h0 = k == 0u ? (uint32_t) src_or_word : first + whole_lo;
-        it.meta = hn | (k << 20) | (lane << 22);
-        items[lane * 3u + k] = it;
+        it.sdelta = k == 0u ? (Off) src_or_word : (Off) (src_or_word - d);
+        it.lo = (Off) d;
+        it.hi = (Off) (d + len - 16u);
+        wins[lane * 3u + k] = it;
+        metas[lane * 3u + k] = (k != 0u && len >= 16u ? kDlvWinItem : 0u) | (k << 1) | (lane << 3);
       };
-      put(0, wr.dst, wr.prefix, plen, F, c0);
-      put(1, d1, wr.src_a, wr.len_a, F + c0, c1);
-      put(2, d2, wr.src_b, wr.len_b, F + c0 + c1, c2);
+      put(0, wr.dst, wr.prefix, plen, F);
+      put(1, d1, wr.src_a, wr.len_a, F + c0);
+      put(2, d2, wr.src_b, wr.len_b, F + c0 + c1);
     }
     uint32_t carry = 0;  // item (id + 1) of the entry before the step being planned
     // ---- load phase of the step at stream position W
@@ -436,20 +426,19 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
         const uint32_t pos = W + (uint32_t) u * kWave + lane;
         const bool valid = pos < total_e;
         const uint32_t id = valid ? it - 1u : 0u;
-        const Item I = items[id];
+        const Win I = wins[id];
+        const bool win = valid && (metas[id] & kDlvWinItem);
         const Off D = (I.dbase + (Off) pos) << 4;
-        const bool hot = valid && pos - I.h0 < (I.meta & 0xFFFFFu);
-        // partial chunks load their window too when it is 4-aligned and in the
-        // image (below 0 wraps, out), so the store phase never loads but for
-        // unaligned sources (every load here is unconditional)
-        const Off a = D + I.sdelta;
-        const bool loaded = hot || (valid && (a & 3u) == 0u && msize >= 16u && a <= (Off) msize - 16u);
-        S.D[u] = D;
-        S.pk[u] = id | ((uint32_t) hot << 8) | ((uint32_t) valid << 9) | ((uint32_t) loaded << 10);
+        const Off Wn = D < I.lo ? I.lo : (D > I.hi ? I.hi : D);
+        S.D[u] = win ? Wn : D;
+        S.pk[u] = id | ((uint32_t) win << 8) | ((uint32_t) valid << 9);
         if constexpr ((MODE & kDlvNoLoad) != 0) {
           S.v[u] = (u32x4){(uint32_t) D, 1u, 2u, 3u};
         } else {
-          S.v[u] = *reinterpret_cast<const u32x4*>(loaded ? P.mem + a : dummy);
+          const uint8_t* src = win ? P.mem + (Off) (Wn + I.sdelta) : dummy;
+          u32x4 v;
+          __builtin_memcpy(&v, src, 16);  // byte-aligned dwordx4 for edge windows
+          S.v[u] = v;
         }
       }
     };
@@ -463,28 +452,29 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
           if constexpr ((MODE & kDlvNoStore) != 0) {
             if ((S.v[u].x ^ S.v[u].w) == 0x12345678u) P.mem[S.D[u]] = 0;  // keeps the loads
           } else {
-            *reinterpret_cast<u32x4*>(P.mem + S.D[u]) = S.v[u];
+            __builtin_memcpy(P.mem + S.D[u], &S.v[u], 16);
           }
         }
         slow = slow || (pk & 768u) == 512u;
       }
       if (slow) {
-        // partial chunks, unaligned or out-of-image sources, VLAN prefixes:
-        // bytes [x, y) of the chunk, read here (waited for in this branch only)
+        // VLAN prefixes and items under 16 B: bytes [x, y) of chunk D, read
+        // here byte by byte (waited for in this branch only)
 #pragma unroll
         for (int u = 0; u < kDlvU; ++u) {
           const uint32_t pk = S.pk[u];
           if ((pk & 768u) != 512u) continue;
           const Off D = S.D[u];
-          const Item I = items[pk & 255u];
-          const uint32_t k = (I.meta >> 20) & 3u;
-          const uint32_t x = I.d > D ? (uint32_t) (I.d - D) : 0u;
-          const uint32_t y = I.dend - D < 16u ? (uint32_t) (I.dend - D) : 16u;
-          uint32_t o[4] = {S.v[u].x, S.v[u].y, S.v[u].z, S.v[u].w};
+          const Win I = wins[pk & 255u];
+          const uint32_t k = (metas[pk & 255u] >> 1) & 3u;
+          const Off dend = I.hi + (Off) 16u;
+          const uint32_t x = I.lo > D ? (uint32_t) (I.lo - D) : 0u;
+          const uint32_t y = dend - D < 16u ? (uint32_t) (dend - D) : 16u;
+          uint32_t o[4] = {0u, 0u, 0u, 0u};
           if (k == 0u) {
             // VLAN prefix 81 00 tag (queue_pair.cpp:352-359): its 4 bytes at d
-            const uint32_t pw = I.h0;
-            const int32_t rel = (int32_t) (I.d - D);
+            const uint32_t pw = (uint32_t) I.sdelta;
+            const int32_t rel = (int32_t) (I.lo - D);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               uint32_t z = 0;
@@ -495,10 +485,8 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
               }
               o[i] = z;
             }
-          } else if (!((pk >> 10) & 1u)) {
-            // byte by byte (rare: unaligned sources, windows leaving the image)
+          } else {
             const Off s0 = D + I.sdelta;
-            o[0] = o[1] = o[2] = o[3] = 0u;
 #pragma unroll 1
             for (uint32_t b = x; b < y; ++b) {
               const uint32_t z = (uint32_t) P.mem[(Off) (s0 + b)] << (8u * (b & 3u));
@@ -508,14 +496,7 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
               o[3] |= (b >> 2) == 3u ? z : 0u;
             }
           }
-          if constexpr ((MODE & kDlvNoStore) == 0) {
-            if (x == 0u && y == 16u) {
-              u32x4 vq = {o[0], o[1], o[2], o[3]};
-              *reinterpret_cast<u32x4*>(P.mem + D) = vq;
-            } else {
-              dlv_store_partial(P.mem, (uint64_t) D, x, y, o);
-            }
-          }
+          if constexpr ((MODE & kDlvNoStore) == 0) dlv_store_partial(P.mem, (uint64_t) D, x, y, o);
         }
       }
     };
@@ -525,15 +506,6 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
     // in vmcnt, in order with the loads); a counted loop with its only exit at
     // the bottom keeps counted waits; plans past the last step are empty
     const uint32_t nsteps = (total_e + kSpan - 1) / kSpan;
-    bool staged = false;
-    auto stage_hdr = [&]() __attribute__((always_inline)) {
-      // the header loads were issued before every step's: done by now
-      if (kHash && !staged) {
-#pragma unroll
-        for (int k = 0; k < kHdrChunks; ++k) stage[hdr_slot(lane, (uint32_t) k)] = make_uint4(hdr[k].x, hdr[k].y, hdr[k].z, hdr[k].w);
-        staged = true;
-      }
-    };
     if (nsteps) {
       DlvStep<WIDE> A, B, C;
       plan(A, 0);
@@ -543,7 +515,6 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
         plan(C, (s + 2) * kSpan);
         __builtin_amdgcn_sched_barrier(0);
         store(A);
-        stage_hdr();
         plan(A, (s + 3) * kSpan);
         __builtin_amdgcn_sched_barrier(0);
         store(B);
@@ -555,20 +526,29 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
       if (s + 1 < nsteps) store(B);
     }
     if (kHash) {
-      stage_hdr();
+      // every lane reads its items before the stage overwrites them
+      const Win I0 = wins[lane * 3u], I1 = wins[lane * 3u + 1u], I2 = wins[lane * 3u + 2u];
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       if (j < n) {
         if (flag) {
-          const Item I0 = items[lane * 3u], I1 = items[lane * 3u + 1u], I2 = items[lane * 3u + 2u];
-          const uint32_t plen = (uint32_t) (I0.dend - I0.d);
-          const uint32_t len_a = (uint32_t) (I1.dend - I1.d), len_b = (uint32_t) (I2.dend - I2.d);
+          const uint32_t plen = (uint32_t) (I0.hi + 16u - I0.lo);
+          const uint32_t len_a = (uint32_t) (I1.hi + 16u - I1.lo), len_b = (uint32_t) (I2.hi + 16u - I2.lo);
           uint64_t len = (uint64_t) plen + len_a + len_b;
           if (len > NICGPU_MAX_PACKET) len = NICGPU_MAX_PACKET;  // the tuple lies in the first 82 B
-          const FrameParts fp{P.mem, (uint64_t) (Off) (I1.d + I1.sdelta), (uint64_t) (Off) (I2.d + I2.sdelta),
-                              I0.h0, plen, len_a};
-          if (!hdr_src) {
-            // a VLAN prefix or a part A shorter than the header: staged byte by byte
+          const uint64_t src_a = (uint64_t) (Off) (I1.lo + I1.sdelta);
+          const FrameParts fp{P.mem, src_a, (uint64_t) (Off) (I2.lo + I2.sdelta), (uint32_t) I0.sdelta, plen, len_a};
+          // a frame whose first 48 bytes are all part A's (no VLAN prefix)
+          // stages them from its source, three 16-B loads; the others byte by byte
+          const bool hdr_src = plen == 0u && (len_a >= (uint32_t) kHdrBytes || len_b == 0u);
+          const uint32_t hlo = (uint32_t) ((hdr_src ? src_a : (uint64_t) I0.lo) & 15u);
+          if (hdr_src) {
+            const uint64_t hb = src_a & ~15ull;
+            const uint64_t hend = src_a + (len_a < (uint32_t) kHdrBytes ? len_a : (uint32_t) kHdrBytes);
+#pragma unroll
+            for (int k = 0; k < kHdrChunks; ++k)
+              if (hb + 16u * k < hend) stage[hdr_slot(lane, (uint32_t) k)] = *reinterpret_cast<const uint4*>(P.mem + hb + 16u * k);
+          } else {
             uint8_t* sb = reinterpret_cast<uint8_t*>(stage + hdr_slot(lane, 0));
             const uint32_t nb = len < (uint64_t) kHdrBytes - hlo ? (uint32_t) len : (uint32_t) kHdrBytes - hlo;
             for (uint32_t o = 0; o < nb; ++o) sb[hdr_slot(0, (hlo + o) >> 4) * 16u + ((hlo + o) & 15u)] = (uint8_t) fp[o];
@@ -598,8 +578,13 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   }
 }
 
+#ifndef NICGPU_DLV_OCC
+#define NICGPU_DLV_OCC 4
+#endif
+// waves per SIMD the delivery is compiled for (tuning: 6, 80 VGPRs, which
+// its LDS allows, spills the RSS variant and measured slower)
 template <bool RSS, int MODE = 0, bool WIDE = false>
-__global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu(4, 8))) void deliver_kernel(DeliverParams P) {
+__global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu(NICGPU_DLV_OCC, 8))) void deliver_kernel(DeliverParams P) {
   deliver_tiles<RSS, MODE, WIDE>(P);
 }
 
@@ -966,7 +951,8 @@ __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_desc
                                                             uint32_t* counts) {
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
     QpPlan pp;
-    const uint32_t c = nicqp::plan_packet(max_mtu, mem_size, nicqp::desc_load(tx + i), pp, [](uint64_t, uint64_t) {});
+    const uint32_t c =
+        nicqp::plan_packet(max_mtu, mem_size, nicqp::desc_load(tx + i), pp, [](uint64_t, uint64_t) {}, /*split4=*/true);
     counts[i] = c <= kQpMaxPieces ? c : 0u;
     if (c > kQpMaxPieces) counts[n] = 1u;
     plans[i] = pp;
@@ -980,8 +966,9 @@ __global__ __launch_bounds__(kQpBlock) void qp_fill_kernel(const nicgpu_tx_descr
     uint32_t at = base[i];
     plans[i].first_piece = at;
     QpPlan pp;
-    nicqp::plan_packet(max_mtu, mem_size, nicqp::desc_load(tx + i), pp,
-                       [&](uint64_t a, uint64_t len) { desc[at++] = NICGPU_DESC(a, len); });
+    nicqp::plan_packet(
+        max_mtu, mem_size, nicqp::desc_load(tx + i), pp, [&](uint64_t a, uint64_t len) { desc[at++] = NICGPU_DESC(a, len); },
+        /*split4=*/true);
   }
 }
 
@@ -1280,7 +1267,8 @@ struct nicgpu_qp {
   QpPlan* plans = nullptr;
   uint32_t *counts = nullptr, *base = nullptr, *need = nullptr, *pos = nullptr;
   uint64_t* piece_desc = nullptr;
-  uint16_t* piece_csum = nullptr;
+  uint16_t* piece_csum = nullptr;  // [2 np]: split sums (rests, then first-4 parts)
+  uint64_t np = 0;                 // pieces of the last plan
   nicgpu_completion *txc = nullptr, *rxc = nullptr;
   nicgpu_segment_write* writes = nullptr;
   uint32_t *flags = nullptr, *at = nullptr, *which = nullptr, *rss_hash = nullptr, *rx_hash = nullptr;
@@ -1477,7 +1465,7 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
   if (np_h[1] != 0u) return NICGPU_ERR_RANGE;
   const uint64_t np = *np_h;
   st = qp_grow(q->piece_desc, q->c_pdesc, np ? np : 1);
-  if (st == NICGPU_OK) st = qp_grow(q->piece_csum, q->c_pcs, np ? np : 1);
+  if (st == NICGPU_OK) st = qp_grow(q->piece_csum, q->c_pcs, np ? 2 * np : 1);
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
                      q->plans, q->base, q->piece_desc);
@@ -1486,7 +1474,9 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
     st = hip_status(hipEventRecord(q->planned, s));
     if (st == NICGPU_OK) st = hip_status(hipStreamWaitEvent(static_cast<hipStream_t>(sums_stream), q->planned, 0));
   }
-  if (st == NICGPU_OK && np) st = nicgpu_checksum_batch(mem, q->piece_desc, np, q->piece_csum, sums_stream);
+  if (st == NICGPU_OK && np)
+    st = nicgpu_checksum_batch_split(mem, q->piece_desc, np, q->piece_csum, q->piece_csum + np, sums_stream);
+  q->np = np;
   *npieces = np;
   qp_fill_view(q, view);
   return st;
@@ -1528,7 +1518,7 @@ int nicgpu_qp_resolve_start(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t 
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   q->res = nicgpu_qp::Pending{};
-  QpCtx C{queue_id, max_mtu, mem_size, q->plans, q->piece_csum, q->tx, q->rx, (uint64_t) nrx};
+  QpCtx C{queue_id, max_mtu, mem_size, q->plans, q->piece_csum, q->piece_csum + q->np, q->tx, q->rx, (uint64_t) nrx};
   const unsigned grid = qp_grid(q, ntx + 1);
   uint64_t* tail = q->partials + (size_t) grid * kQpStats;
   // first guess: every packet pops what it needs (rx_need).  The final pass
@@ -1562,7 +1552,7 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
   DeviceGuard g(q->device);
   hipStream_t s = R.s;
   const uint64_t ntx = R.ntx;
-  QpCtx C{R.queue_id, R.max_mtu, R.mem_size, q->plans, q->piece_csum, q->tx, q->rx, R.nrx};
+  QpCtx C{R.queue_id, R.max_mtu, R.mem_size, q->plans, q->piece_csum, q->piece_csum + q->np, q->tx, q->rx, R.nrx};
   const unsigned grid = R.grid;
   const uint64_t* part = q->hp;  // the tail, kQpTail words (page-locked)
   uint64_t* tail = q->partials + (size_t) grid * kQpStats;

@@ -111,12 +111,15 @@ namespace {
 // One TX descriptor's plan (nicqp::plan_packet); writes its pieces to `out`
 // unless it is null.  Returns the number of pieces.
 std::uint32_t plan_packet(const BatchedQueuePairConfig& config, std::size_t mem_size, const TxDescriptor& t,
-                          PacketPlan& pp, Piece* out) {
+                          PacketPlan& pp, Piece* out, bool split4) {
   std::uint32_t k = 0;
-  return nicqp::plan_packet(config.max_mtu, mem_size, t, pp, [&](std::uint64_t addr, std::uint64_t len) {
-    if (out) out[k] = Piece{addr, static_cast<std::uint32_t>(len)};
-    ++k;
-  });
+  return nicqp::plan_packet(
+      config.max_mtu, mem_size, t, pp,
+      [&](std::uint64_t addr, std::uint64_t len) {
+        if (out) out[k] = Piece{addr, static_cast<std::uint32_t>(len)};
+        ++k;
+      },
+      split4);
 }
 
 }  // namespace
@@ -168,20 +171,22 @@ void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const Com
 }
 
 // Count pass, prefix over the chunks, fill pass (each chunk in its own thread).
-Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx) {
+Plan make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
+               bool split4) {
   Plan plan;
-  make_plan(config, mem_size, tx, plan);
+  make_plan(config, mem_size, tx, plan, split4);
   return plan;
 }
 
 void make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
-               Plan& plan) {
+               Plan& plan, bool split4) {
+  plan.split4 = split4;
   plan.packets.resize(tx.size());
   const Chunks ch(tx.size(), config.host_threads ? config.host_threads : 16);
   std::vector<std::size_t> base(ch.k + 1, 0);
   ch.run([&](std::size_t c, std::size_t b, std::size_t e) {
     std::size_t n = 0;
-    for (std::size_t i = b; i < e; ++i) n += plan_packet(config, mem_size, tx[i], plan.packets[i], nullptr);
+    for (std::size_t i = b; i < e; ++i) n += plan_packet(config, mem_size, tx[i], plan.packets[i], nullptr, split4);
     base[c + 1] = n;
   });
   for (std::size_t c = 0; c < ch.k; ++c) base[c + 1] += base[c];
@@ -193,7 +198,7 @@ void make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
     std::size_t at = base[c];
     for (std::size_t i = b; i < e; ++i) {
       PacketPlan& pp = plan.packets[i];
-      const std::uint32_t np = plan_packet(config, mem_size, tx[i], pp, plan.pieces.data() + at);
+      const std::uint32_t np = plan_packet(config, mem_size, tx[i], pp, plan.pieces.data() + at, split4);
       pp.first_piece = static_cast<std::uint32_t>(at);
       at += np;
     }
@@ -223,7 +228,10 @@ void add_stats(QueuePairStats& a, const QueuePairStats& b) {
 
 Ctx make_ctx(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
              std::span<const std::uint16_t> cs, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx) {
-  return Ctx{config.queue_id, config.max_mtu, mem_size, plan.packets.data(), cs.data(), tx.data(), rx.data(), rx.size()};
+  const std::size_t np = plan.pieces.size();
+  if (cs.size() < (plan.split4 ? 2 * np : np)) throw std::invalid_argument("resolve: fewer piece sums than the plan's pieces");
+  return Ctx{config.queue_id, config.max_mtu, mem_size,  plan.packets.data(), cs.data(),
+             plan.split4 ? cs.data() + np : nullptr,   tx.data(), rx.data(), rx.size()};
 }
 
 std::size_t rx_need(const Ctx& C, std::size_t i) { return nicqp::rx_need(C, i); }
@@ -1665,13 +1673,16 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     const auto [htx, hrx] = host_spans(sl, tx, rx, stream);
     const auto tail_tx = htx.subspan(done);
     const auto tail_rx = hrx.subspan(used);
-    make_plan(config_, mem.size, tail_tx, S.host.plan);
+    make_plan(config_, mem.size, tail_tx, S.host.plan, /*split4=*/true);
     std::uint32_t pb = 0;
     check(nicgpu_memcpy_async(&pb, v.piece_base + done, sizeof(pb), stream), "nicgpu_memcpy_async");
     check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
     if (np - pb != S.host.plan.pieces.size()) throw GpuError("process_batch: device and host plans differ", NICGPU_ERR_INVALID);
-    S.tail_cs.resize(np - pb);
-    check(nicgpu_memcpy_async(S.tail_cs.data(), v.piece_csum + pb, S.tail_cs.size() * 2, stream), "nicgpu_memcpy_async");
+    // the device's split sums of those pieces: rests, then first-4 parts
+    const std::size_t m = np - pb;
+    S.tail_cs.resize(2 * m);
+    check(nicgpu_memcpy_async(S.tail_cs.data(), v.piece_csum + pb, m * 2, stream), "nicgpu_memcpy_async");
+    check(nicgpu_memcpy_async(S.tail_cs.data() + m, v.piece_csum + np + pb, m * 2, stream), "nicgpu_memcpy_async");
     check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
     RxBatchResult& part = S.host.part;
     resolve(quiet_, mem.size, S.host.plan, S.tail_cs, tail_tx, tail_rx, st, part, S.host.writes, S.host.write_of_rx);

@@ -69,7 +69,7 @@ enum : uint32_t {
   kTooManySegments = 7,
 };
 // PacketPlan::Kind (include/nic/rx_stage.h)
-enum : uint32_t { kNoBytes = 0, kPlain = 1, kSegmented = 2 };
+enum : uint32_t { kNoBytes = 0, kPlain = 1, kSegmented = 2, kPlainSplit = 3 };
 
 NICQP_HD uint32_t add1c(uint32_t a, uint32_t b) {
   const uint32_t x = a + b;
@@ -126,10 +126,14 @@ NICQP_HD bool tx_verify_needed(const Tx& t) {
 // (:105-116) and the RX verifies (:434-447) need; put(addr, len) receives
 // them in order.  Returns the number of pieces (0: no decision reads bytes).
 //   kPlain      [0, min(4, L)) then [4, L) in runs of <= kRun bytes
+//   kPlainSplit (split4) [0, L) in runs of <= kRun bytes: one piece per
+//               packet below 64 KiB, the first one's sum split into its first
+//               min(4, len) bytes and the rest (PacketSums::cs4)
 //   kSegmented  H >= 4: [0, 4), [4, H), then chunk k = [H + k*mss, +len_k)
 //               H < 4:  [0, H), then per chunk [.., +min(4 - H, len_k)) and its rest
 template <class Tx, class Plan, class Put>
-NICQP_HD uint32_t plan_packet(uint64_t max_mtu, uint64_t mem_size, const Tx& t, Plan& pp, Put&& put) {
+NICQP_HD uint32_t plan_packet(uint64_t max_mtu, uint64_t mem_size, const Tx& t, Plan& pp, Put&& put,
+                              bool split4 = false) {
   uint32_t np = 0;
   pp.kind = static_cast<decltype(pp.kind)>(kNoBytes);
   pp.nseg = 0;
@@ -144,7 +148,15 @@ NICQP_HD uint32_t plan_packet(uint64_t max_mtu, uint64_t mem_size, const Tx& t, 
   const bool dropped = mtu_drop || d.invalid_mss || d.too_many;
   if (dropped && !verify) return 0;
   const uint64_t a = t.buffer_address;
-  if (!d.segmented || dropped) {
+  if ((!d.segmented || dropped) && split4) {
+    pp.kind = static_cast<decltype(pp.kind)>(kPlainSplit);
+    put(a, min64(kRun, L));
+    ++np;
+    for (uint64_t o = kRun; o < L; o += kRun) {
+      put(a + o, min64(kRun, L - o));
+      ++np;
+    }
+  } else if (!d.segmented || dropped) {
     pp.kind = static_cast<decltype(pp.kind)>(kPlain);
     put(a, min64(4, L));
     ++np;
@@ -184,14 +196,21 @@ NICQP_HD uint32_t plan_packet(uint64_t max_mtu, uint64_t mem_size, const Tx& t, 
 }
 
 // Sums a resolve step needs, for one TX packet.  cs = compute_checksum of
-// each piece, i.e. ~fold(sum).
+// each piece, i.e. ~fold(sum); with cs4 (split sums, the device's piece pass)
+// cs covers each piece's bytes past its first 4 and cs4 its first min(4, len):
+// both exact, so a piece's sum is add1c of the two and a kPlainSplit packet's
+// first4 / rest need no 4-byte piece of their own.
 template <class Plan>
 struct PacketSums {
   const Plan* p;
   const uint16_t* cs;
+  const uint16_t* cs4;  // null: cs covers whole pieces
   uint64_t L;
 
-  NICQP_HD uint32_t s(uint32_t k) const { return (uint32_t) (uint16_t) ~cs[p->first_piece + k]; }
+  NICQP_HD uint32_t r(uint32_t k) const { return (uint32_t) (uint16_t) ~cs[p->first_piece + k]; }
+  NICQP_HD uint32_t h(uint32_t k) const { return (uint32_t) (uint16_t) ~cs4[p->first_piece + k]; }
+  // whole piece k (the rest starts 4 bytes in: same byte parity)
+  NICQP_HD uint32_t s(uint32_t k) const { return cs4 ? add1c(h(k), r(k)) : r(k); }
   NICQP_HD uint32_t chunk_len(uint32_t k) const {
     const uint64_t o = (uint64_t) p->hdr_len + (uint64_t) k * p->mss;
     return (uint32_t) min64(p->mss, L - o);
@@ -199,7 +218,7 @@ struct PacketSums {
   // whole packet, as compute_checksum(packet) sums it
   NICQP_HD uint32_t whole() const {
     uint32_t acc = 0;
-    if ((uint32_t) p->kind == kPlain) {
+    if ((uint32_t) p->kind == kPlain || (uint32_t) p->kind == kPlainSplit) {
       for (uint32_t i = 0; i < p->npieces; ++i) acc = add1c(acc, s(i));  // all runs start at even offsets
       return acc;
     }
@@ -220,6 +239,12 @@ struct PacketSums {
   }
   // segment k: sum of its first 4 bytes and of the rest (rest placed at offset 4)
   NICQP_HD void segment(uint32_t k, uint32_t& first4, uint32_t& rest) const {
+    if ((uint32_t) p->kind == kPlainSplit) {
+      first4 = h(0);
+      rest = r(0);
+      for (uint32_t i = 1; i < p->npieces; ++i) rest = add1c(rest, s(i));
+      return;
+    }
     if ((uint32_t) p->kind == kPlain) {
       first4 = s(0);
       rest = 0;
@@ -243,8 +268,9 @@ struct Ctx {
   uint16_t queue_id;
   uint64_t max_mtu;
   uint64_t mem_size;
-  const Plan* plans;   // plans[i] for tx[i]
-  const uint16_t* cs;  // piece checksums
+  const Plan* plans;    // plans[i] for tx[i]
+  const uint16_t* cs;   // piece checksums
+  const uint16_t* cs4;  // their first-4-byte parts (split sums), or null
   const Tx* tx;
   const Rx* rx;
   uint64_t nrx;
@@ -291,7 +317,7 @@ NICQP_HD uint32_t rx_need(const Ctx<Tx, Rx, Plan>& C, uint64_t i) {
   const uint64_t L = t.length;
   if (!dma_ok(C.mem_size, t.buffer_address, L)) return 0;
   if (tx_verify_needed(t)) {
-    const PacketSums<Plan> ps{&C.plans[i], C.cs, L};
+    const PacketSums<Plan> ps{&C.plans[i], C.cs, C.cs4, L};
     if ((uint16_t) (~ps.whole() & 0xFFFFu) != t.checksum_value) return 0;
   }
   if (L > C.max_mtu) return 0;
@@ -308,7 +334,7 @@ template <class Comp, class Write, class Tx, class Rx, class Plan, class Stats, 
 NICQP_HD uint64_t resolve_packet(const Ctx<Tx, Rx, Plan>& C, uint64_t i, uint64_t rc, Stats& stats, Sink& sink) {
   const uint16_t qid = C.queue_id;
   const Tx t = desc_load(C.tx + i);
-  const PacketSums<Plan> ps{&C.plans[i], C.cs, (uint64_t) t.length};
+  const PacketSums<Plan> ps{&C.plans[i], C.cs, C.cs4, (uint64_t) t.length};
   const uint64_t L = t.length;
   const uint64_t rc0 = rc;
   // :75-83 no RX descriptor at all

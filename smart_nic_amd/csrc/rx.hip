@@ -284,6 +284,10 @@ __device__ __forceinline__ void store_out(const RxParams& P, const TileOut& o, b
         __builtin_amdgcn_raw_buffer_store_b16((uint16_t) o.cs,
                                               __builtin_amdgcn_make_buffer_rsrc(P.out_csum + tb, (short) 0, 128, 0x00020000),
                                               (int) (l * 2u), 0, SST);
+      if (P.out_cs4)  // (split sums: no RSS, the queue slot holds the first-4 sum)
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t) o.q,
+                                              __builtin_amdgcn_make_buffer_rsrc(P.out_cs4 + tb, (short) 0, 128, 0x00020000),
+                                              (int) (l * 2u), 0, SST);
       if (l34 && P.out_l34) P.out_l34[o.pid] = (uint8_t) o.l34;
       if (rss) {
         if (P.out_hash)
@@ -300,6 +304,7 @@ __device__ __forceinline__ void store_out(const RxParams& P, const TileOut& o, b
   }
   if (o.valid) {
     if (P.out_csum) P.out_csum[o.pid] = (uint16_t) o.cs;
+    if (P.out_cs4) P.out_cs4[o.pid] = (uint16_t) o.q;
     if (l34 && P.out_l34) P.out_l34[o.pid] = (uint8_t) o.l34;
     if (rss) {
       if (P.out_hash) P.out_hash[o.pid] = o.h;
@@ -351,11 +356,28 @@ __device__ __forceinline__ TileOut tile_epilogue(const RxParams& P, const RxLdsP
   }
   if (o.valid) {
     const uint32_t sum = t.nch ? (L.E[lane] - (t.contig ? base_prefix : L.S[lane])) : 0u;
-    const uint32_t x = fold16(sum);
     // LE halfword sums at absolute positions == byte-swapped BE sum when the
     // packet starts at an even address (RFC 1071 byte-order independence).
-    const uint32_t be = (t.off & 1) ? x : bswap16(x);
-    o.cs = ~be & 0xFFFFu;
+    auto finish = [&](uint32_t s) __attribute__((always_inline)) {
+      const uint32_t x = fold16(s);
+      return ~((t.off & 1) ? x : bswap16(x)) & 0xFFFFu;
+    };
+    if (P.out_cs4) {
+      // split sums: the first min(4, len) bytes from the stage, at their
+      // absolute halfword positions; the rest is the exact difference (sum
+      // is the integer sum of the packet's halfwords), so both equal the
+      // sums of two separate pieces [0, 4) and [4, len)
+      const uint32_t lo = (uint32_t) (t.off & 15);
+      const HdrView hv{L.hdr, lane};
+      uint32_t head = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < 4u; ++i)
+        if (i < t.len) head += hv.byte(lo + i) << (8u * ((lo + i) & 1u));
+      o.cs = finish(sum - head);
+      o.q = finish(head);
+    } else {
+      o.cs = finish(sum);
+    }
     if (P.out_l34)
       o.l34 = l34_flags(HdrView{L.hdr, lane}, reinterpret_cast<const uint32_t*>(P.frames + (t.off & ~15ull)),
                         (uint32_t) (t.off & 15), t.len, sum);
@@ -433,7 +455,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
 
   RxLdsPtrs L;
   L.want_rss = P.mode != NICGPU_TUPLE_NONE;
-  L.stage = L.want_rss || P.out_l34 != nullptr;
+  L.stage = L.want_rss || P.out_l34 != nullptr || P.out_cs4 != nullptr;
   L.hist_lds = P.out_hits != nullptr && P.table_n <= (uint32_t) kHistLds;
   L.table_lds = L.want_rss && P.table_n <= (uint32_t) kTableLds;
   uint8_t* base_b = reinterpret_cast<uint8_t*>(lds_dyn);
@@ -776,7 +798,7 @@ int launch_rss_only(const RxParams& P, const DeviceInfo& di, hipStream_t stream)
 int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t stream) {
   if (variant < 0 || variant >= kNumRxVariants) return NICGPU_ERR_INVALID;
   const bool rss = P.mode != NICGPU_TUPLE_NONE;
-  const bool stage = rss || P.out_l34 != nullptr;
+  const bool stage = rss || P.out_l34 != nullptr || P.out_cs4 != nullptr;
   const uint32_t hist_n = (P.out_hits && P.table_n <= (uint32_t) kHistLds) ? P.table_n : 0u;
   const uint32_t table_words = (rss && P.table_n <= (uint32_t) kTableLds) ? (P.table_n + 1u) / 2u : 0u;
   const uint64_t ntiles = (P.n + kWave - 1) / kWave;
@@ -822,7 +844,7 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
 int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frames, const uint64_t* desc, size_t n,
                     int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint16_t* out_csum, uint32_t* out_hash,
                     uint16_t* out_queue, uint64_t* out_hits, uint8_t* out_l34, void* stream,
-                    const uint64_t* n_dev = nullptr) {
+                    const uint64_t* n_dev = nullptr, uint16_t* out_cs4 = nullptr) {
   if (tuple_mode != NICGPU_TUPLE_NONE && tuple_mode != NICGPU_TUPLE_AUTO && tuple_mode != NICGPU_TUPLE_RAW)
     return NICGPU_ERR_INVALID;
   if (tuple_mode == NICGPU_TUPLE_RAW && (raw_off > NICGPU_RAW_MAX_END || raw_len > NICGPU_RAW_MAX_END ||
@@ -830,6 +852,7 @@ int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frame
     return NICGPU_ERR_INVALID;
   if (tuple_mode != NICGPU_TUPLE_NONE && (!ctx || ctx->table_n == 0)) return NICGPU_ERR_INVALID;
   if (tuple_mode == NICGPU_TUPLE_NONE && (out_hash || out_queue || out_hits)) return NICGPU_ERR_INVALID;
+  if (out_cs4 && (!out_csum || tuple_mode != NICGPU_TUPLE_NONE)) return NICGPU_ERR_INVALID;
   if (n == 0) return NICGPU_OK;
   if (!frames || !desc) return NICGPU_ERR_INVALID;
   if ((reinterpret_cast<uintptr_t>(frames) & 15u) != 0) return NICGPU_ERR_INVALID;
@@ -854,6 +877,7 @@ int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frame
   P.out_queue = out_queue;
   P.out_hits = reinterpret_cast<unsigned long long*>(out_hits);
   P.out_l34 = out_l34;
+  P.out_cs4 = out_cs4;
   P.n_dev = reinterpret_cast<const unsigned long long*>(n_dev);
 #ifdef NICGPU_TUNING
   P.stamps = g_tune_stamps;
@@ -906,6 +930,13 @@ int nicgpu_rx_offload_count(const nicgpu_rss_ctx* ctx, const uint8_t* frames, co
 int nicgpu_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n, uint16_t* out_csum, void* stream) {
   return nicgpu_rx_offload(nullptr, frames, desc, n, NICGPU_TUPLE_NONE, 0, 0, out_csum, nullptr, nullptr, nullptr,
                            stream);
+}
+
+int nicgpu_checksum_batch_split(const uint8_t* frames, const uint64_t* desc, size_t n, uint16_t* out_rest,
+                                uint16_t* out_head4, void* stream) {
+  if (n && (!out_rest || !out_head4)) return NICGPU_ERR_INVALID;
+  return rx_offload_impl(0, nullptr, frames, desc, n, NICGPU_TUPLE_NONE, 0, 0, out_rest, nullptr, nullptr, nullptr,
+                         nullptr, stream, nullptr, out_head4);
 }
 
 }  // extern "C"

@@ -240,3 +240,25 @@ extern "C" int nicgpu_tune_store_pattern(uint8_t* mem, uint64_t nframes, uint32_
                        flen, slot);
   return hip_status(hipGetLastError());
 }
+
+// ---- unaligned 16-B global accesses (tests/test_gpu_unaligned.py) --------
+// deliver_kernel's edge windows load and store 16 B at any byte alignment
+// (one dwordx4 each, the HSA unaligned access mode).  Lane i copies the 16 B
+// at src + 17 i + soff to dst + 19 i + doff: every byte alignment of both.
+__global__ __launch_bounds__(256) void unaligned_copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                             uint32_t n, uint32_t soff, uint32_t doff) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  u32x4 v;
+  __builtin_memcpy(&v, src + 17u * i + soff, 16);
+  __builtin_memcpy(dst + 19u * i + doff, &v, 16);
+}
+
+extern "C" int nicgpu_tune_unaligned_copy(const uint8_t* src, uint8_t* dst, uint32_t n, uint32_t soff, uint32_t doff,
+                                          void* stream) {
+  if (!src || !dst) return NICGPU_ERR_INVALID;
+  if (n == 0) return NICGPU_OK;
+  hipLaunchKernelGGL(unaligned_copy_kernel, dim3((n + 255u) / 256u), dim3(256), 0, static_cast<hipStream_t>(stream), src,
+                     dst, n, soff, doff);
+  return hip_status(hipGetLastError());
+}

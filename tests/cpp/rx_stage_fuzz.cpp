@@ -35,6 +35,7 @@ namespace {
 
 std::size_t g_overlapping = 0, g_split = 0, g_snap = 0;  // batches that took each careful step
 int g_steps_max = 0;                                        // most relaxation steps a batch needed
+std::size_t g_split_pieces_saved = 0;                       // pieces the split plans did without
 
 struct Rng {
   std::uint64_t s;
@@ -397,6 +398,35 @@ int run_case(std::uint64_t seed) {
       }
       if (max_steps > 2) g_steps_max = std::max(g_steps_max, steps);
     }
+    // the device's split plans (one piece per plain packet, its sum taken as
+    // its first 4 bytes | the rest, nicgpu_checksum_batch_split) resolve to
+    // the same result
+    {
+      const Plan sp = make_plan(cfg, mem_size, tx, /*split4=*/true);
+      const std::size_t m = sp.pieces.size();
+      std::vector<std::uint16_t> scs(2 * m);
+      for (std::size_t i = 0; i < m; ++i) {
+        const Piece& pc = sp.pieces[i];
+        const std::uint32_t h = pc.len < 4u ? pc.len : 4u;
+        scs[i] = oracle_compute_checksum(image.data() + pc.addr + h, pc.len - h);
+        scs[m + i] = oracle_compute_checksum(image.data() + pc.addr, h);
+      }
+      RxBatchResult xout;
+      QueuePairStats xst{};
+      std::vector<SegmentWrite> xw;
+      std::vector<std::int64_t> xwof;
+      resolve(scfg, mem_size, sp, scs, tx, rx, xst, xout, xw, xwof, 1);
+      bool xok = m <= plan.pieces.size() && xout.tx_completions.size() == out.tx_completions.size() &&
+                 xout.rx_completions.size() == out.rx_completions.size() && xwof == wof && same(xst, st);
+      for (std::size_t i = 0; xok && i < out.tx_completions.size(); ++i) xok = same(xout.tx_completions[i], out.tx_completions[i]);
+      for (std::size_t i = 0; xok && i < out.rx_completions.size(); ++i) xok = same(xout.rx_completions[i], out.rx_completions[i]);
+      for (std::size_t i = 0; xok && i < writes.size(); ++i) xok = std::memcmp(&xw[i], &writes[i], sizeof(SegmentWrite)) == 0;
+      if (!xok) {
+        std::fprintf(stderr, "seed %llu: resolve over split piece sums differs\n", (unsigned long long) seed);
+        return 1;
+      }
+      g_split_pieces_saved += plan.pieces.size() - m;
+    }
   }
 
   // RSS of each frame delivered with Success, from the bytes the reference
@@ -475,7 +505,7 @@ int main(int argc, char** argv) {
   for (std::uint64_t s = first; s < first + count; ++s) bad += run_case(s);
   if (bad) return 1;
   std::printf("rx_stage_fuzz: ok (%llu batches; %zu with overlapping buffers, %zu split into sub-batches, %zu gathered "
-              "from a copy; relaxation settled every batch in <= %d steps)\n",
-              (unsigned long long) count, g_overlapping, g_split, g_snap, g_steps_max);
+              "from a copy; relaxation settled every batch in <= %d steps; split plans equal, %zu pieces fewer)\n",
+              (unsigned long long) count, g_overlapping, g_split, g_snap, g_steps_max, g_split_pieces_saved);
   return 0;
 }

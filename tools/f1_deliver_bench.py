@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--slot", type=int, default=2048)
     ap.add_argument("--modes", default="0,1,2,4,8,6,5,7,32")
+    ap.add_argument("--lib", default=os.path.join(ROOT, "smart_nic_amd", "libnicgpu_tune.so"),
+                    help="tuning library to time (an A/B build of libnicgpu_tune.so)")
     ap.add_argument("--patterns", action="store_true",
                     help="also time bare 16-B store kernels writing 64/576/1518-B frames at 2-KiB strides and packed "
                          "(nicgpu_tune_store_pattern): the store shape's ceiling")
@@ -56,7 +58,7 @@ def main():
     from smart_nic_amd import pktgen
 
     assert WRITE_DT.itemsize == 40 and COMPL_DT.itemsize == 20
-    tl = ctypes.CDLL(os.path.join(ROOT, "smart_nic_amd", "libnicgpu_tune.so"))
+    tl = ctypes.CDLL(args.lib)
     vp, sz, i32, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
     tl.nicgpu_tune_deliver.restype = i32
     tl.nicgpu_tune_deliver.argtypes = [i32, vp, u64, vp, vp, sz, vp, vp, vp, vp, vp, u64, vp]
@@ -143,7 +145,7 @@ def main():
     got = mem[tx_bytes: tx_bytes + k * args.slot].view(k, args.slot).cpu().numpy()
     ok = all(np.array_equal(got[i, : lens[i]], frames[int(off[i]): int(off[i]) + lens[i]]) for i in range(k))
     moved = 2 * int(lens.sum())
-    out = {"n": n, "slot": args.slot, "frame_bytes": int(lens.sum()), "moved_bytes": moved, "delivered_ok": bool(ok),
+    out = {"lib": os.path.basename(args.lib), "n": n, "slot": args.slot, "frame_bytes": int(lens.sum()), "moved_bytes": moved, "delivered_ok": bool(ok),
            "success_count": int(cnt.item()), "us_median": {}, "tbps_rw": {}}
     for name, ts in times.items():
         med = float(np.median(ts))
