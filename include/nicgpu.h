@@ -440,6 +440,7 @@ int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx,
                       int tuple_mode, uint32_t raw_off, uint32_t raw_len, uint64_t* hits_dev, void* stream);
 #define NICGPU_DELIVER_SETTLED 1u /* end at the settled prefix of the pending nicgpu_qp_resolve_start */
 #define NICGPU_DELIVER_APPEND 2u  /* add to *view.rss_count instead of resetting it (a later range) */
+#define NICGPU_DELIVER_RESET_HITS 4u /* set hits_dev to this range's hits instead of adding (no memset first) */
 /* nicgpu_qp_deliver over completions [rx_begin, rx_end) (bounded on the device
  * with NICGPU_DELIVER_SETTLED).  Ranges of one batch may be delivered in any
  * order when the batch's buffers are disjoint (nicgpu_qp_check verdict 1): the

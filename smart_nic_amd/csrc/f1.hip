@@ -146,6 +146,13 @@ struct DeliverParams {
   uint16_t* rx_queue;
   unsigned long long* hits;
   unsigned long long* count;
+  // the context's accumulator ([0] count, [1 + i] hits of table entry i; zero
+  // between launches) and its done ticket: blocks add into it and the last
+  // block moves it into count / hits, so neither needs a memset before the
+  // launch; null (tuning): blocks add into count / hits directly
+  unsigned long long* acc;
+  unsigned int* done;
+  uint32_t add_count, add_hits;  // the last block adds (1) or stores (0)
   uint64_t alt_dst;  // tuning (kDlvPackedDst): destination = src_a + alt_dst
 };
 
@@ -278,6 +285,15 @@ __device__ __forceinline__ void dlv_store_partial(uint8_t* mem, uint64_t D, uint
 #ifndef NICGPU_DLV_U
 #define NICGPU_DLV_U 2
 #endif
+#ifndef NICGPU_DLV_BUF
+#define NICGPU_DLV_BUF 1
+#endif
+#ifndef NICGPU_DLV_LCP
+#define NICGPU_DLV_LCP 0  // cache policy of the buffer loads (2: nt)
+#endif
+#ifndef NICGPU_DLV_SCP
+#define NICGPU_DLV_SCP 0  // and of the buffer stores
+#endif
 constexpr int kDlvU = NICGPU_DLV_U;  // 64-entry sub-steps per step
 static_assert(kDlvU <= kDlvU1, "marks area");
 
@@ -361,6 +377,15 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   // where lanes without a window load from: the image start, or the write
   // records for an image below 16 B (always >= 40 readable bytes)
   const uint8_t* dummy = msize >= 16u ? P.mem : reinterpret_cast<const uint8_t*>(P.w);
+  // images below 4 GiB: the hot path's loads and stores are buffer accesses
+  // (scalar base, 32-bit offsets) — with 64-bit per-lane addresses the
+  // texture addresser took ~5x the cycles per instruction of a buffer copy
+  // and bounded the kernel (profiles/r04b_f1_stall.txt); lanes without a
+  // window use offset msize, out of range: no memory access, loads read 0,
+  // stores are dropped
+  constexpr bool kBuf = !WIDE && NICGPU_DLV_BUF != 0;
+  const __amdgpu_buffer_rsrc_t mrs =
+      __builtin_amdgcn_make_buffer_rsrc(P.mem, (short) 0, (int) (uint32_t) (WIDE ? 0u : msize), 0x00020000);
   uint32_t my_count = 0;
   for (uint64_t tile = (uint64_t) blockIdx.x * kDlvWpb + w; tile < ntiles; tile += nwaves) {
     // ---- this lane's write: its items and their stream entries
@@ -434,6 +459,9 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
         S.pk[u] = id | ((uint32_t) win << 8) | ((uint32_t) valid << 9);
         if constexpr ((MODE & kDlvNoLoad) != 0) {
           S.v[u] = (u32x4){(uint32_t) D, 1u, 2u, 3u};
+        } else if constexpr (kBuf) {
+          const uint32_t off = win ? (uint32_t) (Wn + I.sdelta) : (uint32_t) msize;
+          S.v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(mrs, (int) off, 0, NICGPU_DLV_LCP));
         } else {
           const uint8_t* src = win ? P.mem + (Off) (Wn + I.sdelta) : dummy;
           u32x4 v;
@@ -448,12 +476,13 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
 #pragma unroll
       for (int u = 0; u < kDlvU; ++u) {
         const uint32_t pk = S.pk[u];
-        if (pk & 256u) {
-          if constexpr ((MODE & kDlvNoStore) != 0) {
-            if ((S.v[u].x ^ S.v[u].w) == 0x12345678u) P.mem[S.D[u]] = 0;  // keeps the loads
-          } else {
-            __builtin_memcpy(P.mem + S.D[u], &S.v[u], 16);
-          }
+        if constexpr ((MODE & kDlvNoStore) != 0) {
+          if ((pk & 256u) && (S.v[u].x ^ S.v[u].w) == 0x12345678u) P.mem[S.D[u]] = 0;  // keeps the loads
+        } else if constexpr (kBuf) {
+          const uint32_t off = (pk & 256u) ? (uint32_t) S.D[u] : (uint32_t) msize;
+          __builtin_amdgcn_raw_buffer_store_b128(S.v[u], mrs, (int) off, 0, NICGPU_DLV_SCP);
+        } else if (pk & 256u) {
+          __builtin_memcpy(P.mem + S.D[u], &S.v[u], 16);
         }
         slow = slow || (pk & 768u) == 512u;
       }
@@ -558,7 +587,7 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
           P.rx_hash[j] = h;
           P.rx_queue[j] = table_lds ? table_s[idx] : R.table[idx];
           if (hist_lds) atomicAdd(&hist[idx], 1u);
-          else atomicAdd(&P.hits[idx], 1ull);
+          else atomicAdd(P.acc ? &P.acc[1 + idx] : &P.hits[idx], 1ull);
           ++my_count;
         } else {
           P.rx_hash[j] = 0u;
@@ -573,8 +602,32 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
     const uint32_t c = (uint32_t) __builtin_amdgcn_readlane((int) wave_incl_scan(my_count), 63);
     if (lane == 0 && c) atomicAdd(cnt_s, c);
     __syncthreads();
-    if (threadIdx.x == 0 && *cnt_s) atomicAdd(P.count, (unsigned long long) *cnt_s);
-    if (hist_lds) flush_hist(hist, R.table_n, P.hits, R.hits_rep, R.hits_done, kThreads);
+    if (P.acc == nullptr) {
+      if (threadIdx.x == 0 && *cnt_s) atomicAdd(P.count, (unsigned long long) *cnt_s);
+      if (hist_lds) flush_hist(hist, R.table_n, P.hits, R.hits_rep, R.hits_done, kThreads);
+      return;
+    }
+    if (threadIdx.x == 0 && *cnt_s) atomicAdd(&P.acc[0], (unsigned long long) *cnt_s);
+    if (hist_lds)
+      for (uint32_t i = threadIdx.x; i < R.table_n; i += kThreads)
+        if (hist[i]) atomicAdd(&P.acc[1 + i], (unsigned long long) hist[i]);
+    // the last block to finish (flush_hist's ticket hand-off) moves the
+    // accumulator out and leaves it zero for the next launch
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's adds are performed
+    __syncthreads();
+    if (threadIdx.x == 0) *cnt_s = atomicAdd(P.done, 1u) == gridDim.x - 1u ? 1u : 0u;
+    __syncthreads();
+    if (*cnt_s == 0u) return;
+    for (uint32_t i = threadIdx.x; i <= R.table_n; i += kThreads) {
+      const unsigned long long v = atomicExch(&P.acc[i], 0ull);
+      unsigned long long* dst = i == 0u ? P.count : &P.hits[i - 1u];
+      if (i == 0u ? P.add_count : P.add_hits) {
+        if (v) atomicAdd(dst, v);
+      } else {
+        *dst = v;
+      }
+    }
+    if (threadIdx.x == 0) atomicExch(P.done, 0u);
   }
 }
 
@@ -1280,6 +1333,9 @@ struct nicgpu_qp {
   size_t c_sk = 0, c_qw = 0, c_em = 0, c_key = 0;
   uint64_t* end_max = nullptr;  // [nrx] nicgpu_qp_check's running max of RX span ends
   unsigned long long* scal = nullptr;
+  unsigned long long* dlv_acc = nullptr;  // the delivery's accumulator (DeliverParams::acc), zero between launches
+  size_t c_dlv_acc = 0;
+  unsigned int* dlv_done = nullptr;       // its done ticket
   uint8_t* tmp = nullptr;
   uint64_t host_scal[4] = {0, 0, 0, 0};
   // page-locked landing space of the small downloads (a pageable one is staged
@@ -1356,7 +1412,9 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
   if (hipMalloc(&q->scal, 4 * sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&q->partials, ((size_t) q->grid * kQpStats + kQpTail) * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&q->queue_start, 65536 * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc(&q->queue_end, 65536 * sizeof(uint32_t)) != hipSuccess) {
+      hipMalloc(&q->queue_end, 65536 * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&q->dlv_done, sizeof(unsigned int)) != hipSuccess ||
+      hipMemset(q->dlv_done, 0, sizeof(unsigned int)) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
   }
@@ -1380,7 +1438,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
   void* bufs[] = {q->tx_own, q->rx_own, q->tmp_chk, q->plans, q->counts, q->base, q->need, q->pos, q->piece_desc, q->piece_csum,
                   q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
                   q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sort_key, q->sorted_key, q->queue_which,
-                  q->queue_start, q->queue_end, q->end_max};
+                  q->queue_start, q->queue_end, q->end_max, q->dlv_acc, q->dlv_done};
   for (void* b : bufs)
     if (b) (void) hipFree(b);
   if (q->hp) (void) hipHostFree(q->hp);
@@ -1704,7 +1762,8 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
                             unsigned flags, const nicgpu_rss_ctx* ctx, int tuple_mode, uint32_t raw_off,
                             uint32_t raw_len, uint64_t* hits_dev, void* stream) {
   if (!q || rx_end > q->cap_rx || rx_begin > rx_end) return NICGPU_ERR_INVALID;
-  if (flags & ~(unsigned) (NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_APPEND)) return NICGPU_ERR_INVALID;
+  if (flags & ~(unsigned) (NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_APPEND | NICGPU_DELIVER_RESET_HITS))
+    return NICGPU_ERR_INVALID;
   // the settled prefix of the resolve started last (its grid places the tail)
   if ((flags & NICGPU_DELIVER_SETTLED) && !q->res.on) return NICGPU_ERR_INVALID;
   if (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0)) return NICGPU_ERR_INVALID;
@@ -1719,8 +1778,21 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
   hipStream_t s = static_cast<hipStream_t>(stream);
   q->delivered = rss;
   int st = NICGPU_OK;
-  if (rss && !(flags & NICGPU_DELIVER_APPEND)) st = hip_status(hipMemsetAsync(q->scal + 3, 0, sizeof(uint64_t), s));
-  if (st != NICGPU_OK || rx_end == rx_begin) return st;
+  const bool add_count = (flags & NICGPU_DELIVER_APPEND) != 0, add_hits = (flags & NICGPU_DELIVER_RESET_HITS) == 0;
+  if (rx_end == rx_begin) {  // no launch: the resets by hand
+    if (rss && !add_count) st = hip_status(hipMemsetAsync(q->scal + 3, 0, sizeof(uint64_t), s));
+    if (rss && !add_hits && st == NICGPU_OK) st = hip_status(hipMemsetAsync(hits_dev, 0, ctx->table_n * sizeof(uint64_t), s));
+    return st;
+  }
+  if (rss && ctx->table_n + 1 > q->c_dlv_acc) {  // once per table size: a zero accumulator
+    if (q->dlv_acc) (void) hipFree(q->dlv_acc);
+    q->dlv_acc = nullptr;
+    q->c_dlv_acc = 0;
+    if (hipMalloc(&q->dlv_acc, (ctx->table_n + 1) * sizeof(unsigned long long)) != hipSuccess) return NICGPU_ERR_NOMEM;
+    q->c_dlv_acc = ctx->table_n + 1;
+    st = hip_status(hipMemsetAsync(q->dlv_acc, 0, q->c_dlv_acc * sizeof(unsigned long long), s));
+    if (st != NICGPU_OK) return st;
+  }
   const DeviceInfo* di = nullptr;
   st = current_device_info(&di);
   if (st != NICGPU_OK) return st;
@@ -1745,6 +1817,10 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
     P.rx_queue = q->rx_queue;
     P.hits = reinterpret_cast<unsigned long long*>(hits_dev);
     P.count = reinterpret_cast<unsigned long long*>(q->scal + 3);
+    P.acc = q->dlv_acc;
+    P.done = q->dlv_done;
+    P.add_count = add_count ? 1u : 0u;
+    P.add_hits = add_hits ? 1u : 0u;
 #ifdef NICGPU_HIST_REP
     if (P.rss.table_n <= (uint32_t) kHistLds) {
       P.rss.hits_rep = ctx->d_rep;

@@ -1641,11 +1641,10 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     for (const std::uint16_t q : table) sl.nq = std::max<std::size_t>(sl.nq, std::size_t{q} + 1);
     rctx = config_.rss->device_context(stream);
     hits = static_cast<std::uint64_t*>(sl.hits.get(std::max<std::size_t>(sl.tn, 1) * sizeof(std::uint64_t)));
-    check(nicgpu_memset_async(hits, 0, sl.tn * sizeof(std::uint64_t), stream), "nicgpu_memset_async");
   }
   out.timings.resolve_us += us_since(t);
   t = clock::now();
-  deliver(sl, mem, 0, nrx, NICGPU_DELIVER_SETTLED, rctx, hits, stream);
+  deliver(sl, mem, 0, nrx, NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_RESET_HITS, rctx, hits, stream);  // hits set, not added
   out.timings.gather_us += us_since(t);
   t = clock::now();
   std::uint64_t done = 0, used = 0, settled = 0;
