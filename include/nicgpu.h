@@ -46,6 +46,7 @@ extern "C" {
 #define NICGPU_ERR_NO_DEVICE (-3)  /* no gfx950 device visible */
 #define NICGPU_ERR_NOMEM (-4)
 #define NICGPU_ERR_RANGE (-5)    /* a batch too large for 32-bit piece indices: split it */
+#define NICGPU_ERR_AGAIN (-6)    /* an asynchronous plan outgrew its buffers: redo the batch (the next plan fits) */
 
 #define NICGPU_DESC_OFFSET_BITS 40
 /* Longest packet the kernels accept: 64 KiB - 1 (the TSO super-frame limit of
@@ -321,8 +322,7 @@ typedef struct nicgpu_qp_view {
   nicgpu_tx_descriptor* tx;     /* [ntx]  the caller uploads the TX descriptors here */
   nicgpu_rx_descriptor* rx;     /* [nrx]  and the RX descriptors (the ring, rx[0] first) */
   uint32_t* piece_base;         /* [ntx + 1] first piece of each TX descriptor */
-  uint16_t* piece_csum;         /* [2 npieces] split sums of each piece (nicgpu_checksum_batch_split):
-                                   [0, npieces) past its first 4 bytes, then [npieces, 2 npieces) its first 4 */
+  uint16_t* piece_csum;         /* [npieces] split sums (nicgpu_checksum_batch_split): each piece past its first 4 bytes */
   nicgpu_completion* txc;       /* [ntx]  TX completions, in posting order */
   nicgpu_completion* rxc;       /* [nrx]  RX completions, in posting order */
   nicgpu_segment_write* writes; /* [nrx]  DMA write of RX completion j (all lengths 0: none) */
@@ -335,6 +335,7 @@ typedef struct nicgpu_qp_view {
   uint32_t* queue_start;        /* [65536] queue q = queue_which[queue_start[q], queue_end[q]) */
   uint32_t* queue_end;
   uint64_t* rss_count;          /* [1]    frames listed by nicgpu_qp_rss_list (device scalar) */
+  uint16_t* piece_cs4;          /* [npieces] and of each piece's first min(4, len) bytes */
 } nicgpu_qp_view;
 
 typedef struct nicgpu_qp nicgpu_qp;
@@ -383,6 +384,18 @@ int nicgpu_qp_plan(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t n
  * on the main one. */
 int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
                       uint64_t* npieces, nicgpu_qp_view* view, void* plan_stream, void* sums_stream);
+/* nicgpu_qp_plan_on without its wait: nothing is read back.  The piece
+ * buffers hold at least ntx + ntx / 4 + 64 pieces (and what the last resolve
+ * reported); the fill and the sums use the piece count the scan leaves on the
+ * device, bounded by that capacity.  When the plan does not fit, the next
+ * nicgpu_qp_resolve_start settles nothing and nicgpu_qp_resolve_finish returns
+ * NICGPU_ERR_AGAIN: the caller redoes the batch (the next plan is sized from
+ * this one's count); NICGPU_ERR_RANGE likewise when a descriptor plans more
+ * than 256 pieces (as nicgpu_qp_plan).  Refreshes *view. */
+int nicgpu_qp_plan_async(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
+                         nicgpu_qp_view* view, void* plan_stream, void* sums_stream);
+/* The piece count of the plan the last nicgpu_qp_resolve_finish resolved. */
+int nicgpu_qp_piece_count(const nicgpu_qp* q, uint64_t* npieces);
 /* The reference's control flow over view.tx[0, ntx) against view.rx[0, nrx)
  * from the piece sums: TX descriptors [0, *done) are resolved, with
  * completions in view.txc[0, *done) and view.rxc[0, *rx_used), their writes in
@@ -396,7 +409,8 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
  * (piece checksums from view.piece_base[*done]).  Synchronises `stream`. */
 int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu, uint16_t queue_id,
                       uint64_t* done, uint64_t* rx_used, nicgpu_qp_stats* stats, void* stream);
-/* nicgpu_qp_resolve in two halves.  _start enqueues the speculative pass
+/* nicgpu_qp_resolve in two halves (NICGPU_ERR_AGAIN / _RANGE from _finish:
+ * see nicgpu_qp_plan_async).  _start enqueues the speculative pass
  * (every packet at the scan of what it needs) on `stream` and returns without
  * waiting; its settled prefix — the RX completions of the packets before the
  * first one that popped otherwise, all of them when none did — is a device

@@ -80,6 +80,8 @@ ABI_SYMBOLS = (
     "nicgpu_qp_bind",
     "nicgpu_qp_plan",
     "nicgpu_qp_plan_on",
+    "nicgpu_qp_plan_async",
+    "nicgpu_qp_piece_count",
     "nicgpu_qp_check",
     "nicgpu_qp_resolve",
     "nicgpu_qp_resolve_start",
@@ -134,6 +136,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_qp_bind": (i32, [vp, vp, sz, vp, sz, vp]),
         "nicgpu_qp_plan": (i32, [vp, vp, ctypes.c_uint64, sz, ctypes.c_uint64, vp, vp, vp]),
         "nicgpu_qp_plan_on": (i32, [vp, vp, ctypes.c_uint64, sz, ctypes.c_uint64, vp, vp, vp, vp]),
+        "nicgpu_qp_plan_async": (i32, [vp, vp, ctypes.c_uint64, sz, ctypes.c_uint64, vp, vp, vp]),
+        "nicgpu_qp_piece_count": (i32, [vp, vp]),
         "nicgpu_qp_check": (i32, [vp, ctypes.c_uint64, sz, sz, vp, vp]),
         "nicgpu_qp_resolve": (i32, [vp, ctypes.c_uint64, sz, sz, ctypes.c_uint64, ctypes.c_uint16, vp, vp, vp, vp]),
         "nicgpu_qp_resolve_start": (i32, [vp, ctypes.c_uint64, sz, sz, ctypes.c_uint64, ctypes.c_uint16, vp]),

@@ -10,6 +10,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -289,10 +290,10 @@ __device__ __forceinline__ void dlv_store_partial(uint8_t* mem, uint64_t D, uint
 #define NICGPU_DLV_BUF 1
 #endif
 #ifndef NICGPU_DLV_LCP
-#define NICGPU_DLV_LCP 0  // cache policy of the buffer loads (2: nt)
+#define NICGPU_DLV_LCP 2  // cache policy of the buffer loads (2: nt)
 #endif
 #ifndef NICGPU_DLV_SCP
-#define NICGPU_DLV_SCP 0  // and of the buffer stores
+#define NICGPU_DLV_SCP 2  // and of the buffer stores (nt: 218 -> 188 us, r04c A/B)
 #endif
 constexpr int kDlvU = NICGPU_DLV_U;  // 64-entry sub-steps per step
 static_assert(kDlvU <= kDlvU1, "marks area");
@@ -969,7 +970,7 @@ constexpr unsigned kQpBlock = 256;
 constexpr unsigned kQpStats = 16;
 // after the per-block stats: RX used, first mismatch, settled prefix, then the
 // batch's 16 stats totals — the one download a resolve needs
-constexpr unsigned kQpTail = 3 + 16;
+constexpr unsigned kQpTail = 3 + 16 + 2;  // ... then [19] the plan overflowed (1 buffers, 2 pieces per descriptor), [20] its piece count
 constexpr int kQpRelaxSteps = 8;  // position relaxations before the host takes the rest
 
 struct QpNullSink {
@@ -995,41 +996,65 @@ struct QpDevSink {
   }
 };
 
-// counts[n] must be 0 on entry: a descriptor that plans more than
-// kQpMaxPieces pieces counts 0 and sets it to 1, so the 32-bit scan of the
-// counts (n <= 2^32 / kQpMaxPieces) cannot wrap and the caller sees the flag.
+// A descriptor that plans more than kQpMaxPieces pieces counts 0 and sets
+// *ovf to this call's generation (flags compared with the generation need no
+// reset before the launch), so the 32-bit scan of the counts (n <= 2^32 /
+// kQpMaxPieces) cannot wrap and the caller sees the flag.
 constexpr uint32_t kQpMaxPieces = 256;
 __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
                                                             uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
-                                                            uint32_t* counts) {
+                                                            uint32_t* counts, unsigned long long* ovf,
+                                                            unsigned long long gen) {
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
     QpPlan pp;
     const uint32_t c =
         nicqp::plan_packet(max_mtu, mem_size, nicqp::desc_load(tx + i), pp, [](uint64_t, uint64_t) {}, /*split4=*/true);
     counts[i] = c <= kQpMaxPieces ? c : 0u;
-    if (c > kQpMaxPieces) counts[n] = 1u;
+    if (c > kQpMaxPieces) *ovf = gen;
     plans[i] = pp;
   }
 }
 
+// Piece descriptors below `cap` only; the first thread leaves the piece count
+// in g[5], the count the sums run over, min(count, cap), in g[4], and the
+// generation in g[3] when the plan does not fit (nicgpu_qp_plan_async).
 __global__ __launch_bounds__(kQpBlock) void qp_fill_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
                                                            uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
-                                                           const uint32_t* __restrict__ base, uint64_t* desc) {
+                                                           const uint32_t* __restrict__ base, uint64_t* desc,
+                                                           uint64_t cap, unsigned long long* g, unsigned long long gen) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint64_t np = base[n];
+    g[5] = np;
+    g[4] = np < cap ? np : cap;
+    if (np > cap) g[3] = gen;
+  }
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
-    uint32_t at = base[i];
-    plans[i].first_piece = at;
+    uint64_t at = base[i];
+    plans[i].first_piece = (uint32_t) at;
     QpPlan pp;
     nicqp::plan_packet(
-        max_mtu, mem_size, nicqp::desc_load(tx + i), pp, [&](uint64_t a, uint64_t len) { desc[at++] = NICGPU_DESC(a, len); },
+        max_mtu, mem_size, nicqp::desc_load(tx + i), pp,
+        [&](uint64_t a, uint64_t len) {
+          if (at < cap) desc[at] = NICGPU_DESC(a, len);
+          ++at;
+        },
         /*split4=*/true);
   }
 }
 
+// The plan this resolve reads did not fit its buffers (or a descriptor planned
+// more than 256 pieces): no kernel of the resolve reads a piece sum then.
+__device__ __forceinline__ bool qp_plan_bad(const unsigned long long* g, unsigned long long gen) {
+  return g[0] == gen || g[3] == gen;
+}
+
 __global__ __launch_bounds__(kQpBlock) void qp_need_kernel(QpCtx C, uint64_t n, uint32_t* need,
-                                                           unsigned long long* first) {
+                                                           unsigned long long* first, const unsigned long long* g,
+                                                           unsigned long long gen) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *first = n;  // the speculative final pass's "nothing differed"
+  const bool bad = qp_plan_bad(g, gen);
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i <= n; i += (uint64_t) gridDim.x * kQpBlock)
-    need[i] = i < n ? nicqp::rx_need(C, i) : 0u;
+    need[i] = i < n && !bad ? nicqp::rx_need(C, i) : 0u;
 }
 
 // One relaxation step of the ring positions: every packet resolved (without
@@ -1061,7 +1086,8 @@ __global__ __launch_bounds__(kQpBlock) void qp_relax_kernel(QpCtx C, uint32_t* p
 __global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32_t* __restrict__ pos, uint64_t lim,
                                                            nicgpu_completion* txc, nicgpu_completion* rxc,
                                                            nicgpu_segment_write* writes, uint64_t* partials,
-                                                           const uint32_t* __restrict__ guess) {
+                                                           const uint32_t* __restrict__ guess, const unsigned long long* g,
+                                                           unsigned long long gen) {
   __shared__ uint64_t red[kQpStats][kQpBlock / kWave];
   // after the per-block stats: [0] the RX descriptors used (pos[lim]), [1] the
   // first mismatch (seeded with n by qp_need_kernel) — one download for all
@@ -1069,6 +1095,7 @@ __global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32
   unsigned long long* first = reinterpret_cast<unsigned long long*>(tail + 1);
   if (blockIdx.x == 0 && threadIdx.x == 0) tail[0] = pos[lim];
   nicgpu_qp_stats st{};
+  if (qp_plan_bad(g, gen)) lim = 0;
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < lim; i += (uint64_t) gridDim.x * kQpBlock) {
     if (pos[i] > C.nrx) {  // exact positions never pass the ring's end: a guess past it is wrong
       if (guess) atomicMin(first, (unsigned long long) i);
@@ -1104,7 +1131,8 @@ __global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32
 constexpr unsigned kQpReduceThreads = 1024;
 __global__ __launch_bounds__(kQpReduceThreads) void qp_reduce_kernel(const uint64_t* __restrict__ partials,
                                                                      unsigned nblocks, const uint32_t* __restrict__ pos,
-                                                                     uint64_t ntx, bool settle) {
+                                                                     uint64_t ntx, bool settle, const unsigned long long* g,
+                                                                     unsigned long long gen) {
   __shared__ uint64_t red[kQpReduceThreads];
   uint64_t* tail = const_cast<uint64_t*>(partials) + (size_t) nblocks * kQpStats;
   const unsigned k = threadIdx.x % kQpStats, r = threadIdx.x / kQpStats;
@@ -1118,9 +1146,14 @@ __global__ __launch_bounds__(kQpReduceThreads) void qp_reduce_kernel(const uint6
     __syncthreads();
   }
   if (threadIdx.x < kQpStats) tail[3 + threadIdx.x] = red[threadIdx.x];
-  if (settle && threadIdx.x == 0) {
-    const uint64_t first = tail[1];
-    tail[2] = first < ntx ? (uint64_t) pos[first] : tail[0];
+  if (threadIdx.x == 0) {
+    const bool bad = qp_plan_bad(g, gen);
+    if (settle) {
+      const uint64_t first = tail[1];
+      tail[2] = bad ? 0u : (first < ntx ? (uint64_t) pos[first] : tail[0]);
+    }
+    tail[19] = g[0] == gen ? 2u : (g[3] == gen ? 1u : 0u);
+    tail[20] = g[5];
   }
 }
 
@@ -1271,10 +1304,10 @@ struct QpRxEnd {  // end of RX descriptor j's span; 0 when it receives nothing
 __global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t ntx,
                                                             const nicgpu_rx_descriptor* __restrict__ rx, uint64_t nrx,
                                                             uint64_t mem_size, const uint64_t* __restrict__ end_max,
-                                                            unsigned long long* flag) {
+                                                            unsigned long long* flag, unsigned long long gen) {
   const uint64_t n = ntx > nrx ? ntx : nrx;
   for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < n; k += (uint64_t) gridDim.x * kQpBlock) {
-    if (k < nrx && k > 0 && QpRxEnd{mem_size}(rx[k]) != 0 && rx[k].buffer_address < end_max[k - 1]) flag[0] = 1;
+    if (k < nrx && k > 0 && QpRxEnd{mem_size}(rx[k]) != 0 && rx[k].buffer_address < end_max[k - 1]) flag[0] = gen;
     if (k < ntx) {
       const uint64_t a = tx[k].buffer_address, len = tx[k].length;
       if (len == 0 || !nicqp::dma_ok(mem_size, a, len)) continue;
@@ -1284,7 +1317,7 @@ __global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_desc
         if (end_max[mid] <= a) lo = mid + 1;
         else hi = mid;
       }
-      if (lo < nrx && rx[lo].buffer_address < a + len) flag[1] = 1;
+      if (lo < nrx && rx[lo].buffer_address < a + len) flag[1] = gen;
     }
   }
 }
@@ -1320,8 +1353,12 @@ struct nicgpu_qp {
   QpPlan* plans = nullptr;
   uint32_t *counts = nullptr, *base = nullptr, *need = nullptr, *pos = nullptr;
   uint64_t* piece_desc = nullptr;
-  uint16_t* piece_csum = nullptr;  // [2 np]: split sums (rests, then first-4 parts)
-  uint64_t np = 0;                 // pieces of the last plan
+  uint16_t* piece_csum = nullptr;  // split sums: each piece past its first 4 bytes ...
+  uint16_t* piece_cs4 = nullptr;   // ... and its first min(4, len)
+  size_t c_pcs4 = 0;
+  uint64_t np = 0;                 // pieces of the last plan (nicgpu_qp_plan_on) or resolved plan
+  uint64_t want_pieces = 0;        // piece capacity an overflowing async plan asked for
+  unsigned long long plan_gen = 0; // generation of the last plan: its overflow flags in gflags
   nicgpu_completion *txc = nullptr, *rxc = nullptr;
   nicgpu_segment_write* writes = nullptr;
   uint32_t *flags = nullptr, *at = nullptr, *which = nullptr, *rss_hash = nullptr, *rx_hash = nullptr;
@@ -1336,6 +1373,11 @@ struct nicgpu_qp {
   unsigned long long* dlv_acc = nullptr;  // the delivery's accumulator (DeliverParams::acc), zero between launches
   size_t c_dlv_acc = 0;
   unsigned int* dlv_done = nullptr;       // its done ticket
+  // zeroed once; flags are set to a call's generation: [0] a descriptor plans
+  // > 256 pieces, [1..2] the check's, [3] the plan does not fit; then the
+  // device piece counts [4] min(count, capacity), [5] count
+  unsigned long long* gflags = nullptr;
+  unsigned long long gen = 0;             // generation of the last plan / check call
   uint8_t* tmp = nullptr;
   uint64_t host_scal[4] = {0, 0, 0, 0};
   // page-locked landing space of the small downloads (a pageable one is staged
@@ -1366,6 +1408,7 @@ void qp_fill_view(const nicgpu_qp* q, nicgpu_qp_view* v) {
   v->rx = q->rx;
   v->piece_base = q->base;
   v->piece_csum = q->piece_csum;
+  v->piece_cs4 = q->piece_cs4;
   v->txc = q->txc;
   v->rxc = q->rxc;
   v->writes = q->writes;
@@ -1414,7 +1457,9 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
       hipMalloc(&q->queue_start, 65536 * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&q->queue_end, 65536 * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&q->dlv_done, sizeof(unsigned int)) != hipSuccess ||
-      hipMemset(q->dlv_done, 0, sizeof(unsigned int)) != hipSuccess) {
+      hipMemset(q->dlv_done, 0, sizeof(unsigned int)) != hipSuccess ||
+      hipMalloc(&q->gflags, 6 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(q->gflags, 0, 6 * sizeof(unsigned long long)) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
   }
@@ -1438,7 +1483,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
   void* bufs[] = {q->tx_own, q->rx_own, q->tmp_chk, q->plans, q->counts, q->base, q->need, q->pos, q->piece_desc, q->piece_csum,
                   q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
                   q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sort_key, q->sorted_key, q->queue_which,
-                  q->queue_start, q->queue_end, q->end_max, q->dlv_acc, q->dlv_done};
+                  q->queue_start, q->queue_end, q->end_max, q->dlv_acc, q->dlv_done, q->gflags, q->piece_cs4};
   for (void* b : bufs)
     if (b) (void) hipFree(b);
   if (q->hp) (void) hipHostFree(q->hp);
@@ -1508,36 +1553,80 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
   hipStream_t s = static_cast<hipStream_t>(plan_stream);
   *npieces = 0;
   const unsigned grid = qp_grid(q, ntx + 1);
-  int st = hip_status(hipMemsetAsync(q->counts + ntx, 0, sizeof(uint32_t), s));
-  if (st == NICGPU_OK)
-    hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                       q->plans, q->counts);
-  if (st == NICGPU_OK) st = hip_status(hipGetLastError());
+  const unsigned long long gen = ++q->gen;
+  q->plan_gen = gen;
+  hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
+                     q->plans, q->counts, q->gflags, gen);
+  int st = hip_status(hipGetLastError());
   uint32_t* np_h = reinterpret_cast<uint32_t*>(q->misc());
-  // the overflow flag first: the scan below adds it in as the last count
-  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(np_h + 1, q->counts + ntx, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  uint64_t* ovf_h = q->misc() + 5;
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(ovf_h, q->gflags, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  // (counts[ntx], the scan's last input, only ends it: base[ntx] = the total)
   if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
   if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(np_h, q->base + ntx, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
   if (st != NICGPU_OK) return st;
-  if (np_h[1] != 0u) return NICGPU_ERR_RANGE;
+  if (*ovf_h == gen) return NICGPU_ERR_RANGE;
   const uint64_t np = *np_h;
   st = qp_grow(q->piece_desc, q->c_pdesc, np ? np : 1);
-  if (st == NICGPU_OK) st = qp_grow(q->piece_csum, q->c_pcs, np ? 2 * np : 1);
+  if (st == NICGPU_OK) st = qp_grow(q->piece_csum, q->c_pcs, np ? np : 1);
+  if (st == NICGPU_OK) st = qp_grow(q->piece_cs4, q->c_pcs4, np ? np : 1);
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->base, q->piece_desc);
+                     q->plans, q->base, q->piece_desc, (uint64_t) q->c_pdesc, q->gflags, gen);
   st = hip_status(hipGetLastError());
   if (st == NICGPU_OK && sums_stream != plan_stream) {  // the sums read the pieces the fill wrote
     st = hip_status(hipEventRecord(q->planned, s));
     if (st == NICGPU_OK) st = hip_status(hipStreamWaitEvent(static_cast<hipStream_t>(sums_stream), q->planned, 0));
   }
   if (st == NICGPU_OK && np)
-    st = nicgpu_checksum_batch_split(mem, q->piece_desc, np, q->piece_csum, q->piece_csum + np, sums_stream);
+    st = nicgpu_checksum_batch_split(mem, q->piece_desc, np, q->piece_csum, q->piece_cs4, sums_stream);
   q->np = np;
   *npieces = np;
   qp_fill_view(q, view);
   return st;
+}
+
+int nicgpu_qp_plan_async(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_t ntx, uint64_t max_mtu,
+                         nicgpu_qp_view* view, void* plan_stream, void* sums_stream) {
+  if (!q || ntx > q->cap_tx) return NICGPU_ERR_INVALID;
+  if (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0)) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(plan_stream);
+  const uint64_t want = std::max<uint64_t>((uint64_t) ntx + ntx / 4 + 64, q->want_pieces);
+  int st = qp_grow(q->piece_desc, q->c_pdesc, want);
+  if (st == NICGPU_OK) st = qp_grow(q->piece_csum, q->c_pcs, want);
+  if (st == NICGPU_OK) st = qp_grow(q->piece_cs4, q->c_pcs4, want);
+  if (st != NICGPU_OK) return st;
+  const uint64_t cap = std::min(q->c_pdesc, std::min(q->c_pcs, q->c_pcs4));
+  const unsigned grid = qp_grid(q, ntx + 1);
+  const unsigned long long gen = ++q->gen;
+  q->plan_gen = gen;
+  q->np = 0;  // known once resolved (nicgpu_qp_piece_count)
+  hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
+                     q->plans, q->counts, q->gflags, gen);
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
+                     q->plans, q->base, q->piece_desc, cap, q->gflags, gen);
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK && sums_stream != plan_stream) {
+    st = hip_status(hipEventRecord(q->planned, s));
+    if (st == NICGPU_OK) st = hip_status(hipStreamWaitEvent(static_cast<hipStream_t>(sums_stream), q->planned, 0));
+  }
+  // the sums over the count the fill left on the device (g[4] <= cap)
+  if (st == NICGPU_OK)
+    st = checksum_split_count(mem, q->piece_desc, cap, reinterpret_cast<const uint64_t*>(q->gflags + 4), q->piece_csum,
+                              q->piece_cs4, sums_stream);
+  qp_fill_view(q, view);
+  return st;
+}
+
+int nicgpu_qp_piece_count(const nicgpu_qp* q, uint64_t* npieces) {
+  if (!q || !npieces) return NICGPU_ERR_INVALID;
+  *npieces = q->np;
+  return NICGPU_OK;
 }
 
 int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int* verdict, void* stream) {
@@ -1545,8 +1634,9 @@ int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int
   *verdict = -1;
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  int st = hip_status(hipMemsetAsync(q->scal, 0, 2 * sizeof(unsigned long long), s));
-  if (st == NICGPU_OK && nrx) {
+  const unsigned long long gen = ++q->gen;
+  int st = NICGPU_OK;
+  if (nrx) {
     hipcub::TransformInputIterator<uint64_t, QpRxEnd, const nicgpu_rx_descriptor*> ends(q->rx, QpRxEnd{mem_size});
     size_t tb = 0;
     if (hipcub::DeviceScan::InclusiveScan(nullptr, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s) != hipSuccess)
@@ -1559,14 +1649,14 @@ int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int
   const uint64_t n = ntx > nrx ? ntx : nrx;
   if (n) {
     hipLaunchKernelGGL(qp_check_kernel, dim3(qp_grid(q, n)), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, q->rx,
-                       (uint64_t) nrx, mem_size, q->end_max, q->scal);
+                       (uint64_t) nrx, mem_size, q->end_max, q->gflags + 1, gen);
     st = hip_status(hipGetLastError());
   }
   uint64_t* f = q->misc() + 1;
-  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(f, q->scal, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(f, q->gflags + 1, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
   if (st != NICGPU_OK) return st;
-  *verdict = f[0] ? -1 : (f[1] ? 0 : 1);
+  *verdict = f[0] == gen ? -1 : (f[1] == gen ? 0 : 1);
   return NICGPU_OK;
 }
 
@@ -1576,7 +1666,7 @@ int nicgpu_qp_resolve_start(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t 
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   q->res = nicgpu_qp::Pending{};
-  QpCtx C{queue_id, max_mtu, mem_size, q->plans, q->piece_csum, q->piece_csum + q->np, q->tx, q->rx, (uint64_t) nrx};
+  QpCtx C{queue_id, max_mtu, mem_size, q->plans, q->piece_csum, q->piece_cs4, q->tx, q->rx, (uint64_t) nrx};
   const unsigned grid = qp_grid(q, ntx + 1);
   uint64_t* tail = q->partials + (size_t) grid * kQpStats;
   // first guess: every packet pops what it needs (rx_need).  The final pass
@@ -1584,16 +1674,16 @@ int nicgpu_qp_resolve_start(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t 
   // otherwise; a batch that settles at once (uniform RX descriptors, no early
   // ends) needs no relaxation step and no host round trip before its DMA writes.
   hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, (uint64_t) ntx, q->need,
-                     reinterpret_cast<unsigned long long*>(tail + 1));
+                     reinterpret_cast<unsigned long long*>(tail + 1), q->gflags, q->plan_gen);
   int st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, (uint64_t) ntx, q->txc, q->rxc,
-                     q->writes, q->partials, q->need);
+                     q->writes, q->partials, q->need, q->gflags, q->plan_gen);
   st = hip_status(hipGetLastError());
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_reduce_kernel, dim3(1), dim3(kQpReduceThreads), 0, s, q->partials, grid, q->pos,
-                     (uint64_t) ntx, true);
+                     (uint64_t) ntx, true, q->gflags, q->plan_gen);
   st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->hp, tail, kQpTail * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   if (st == NICGPU_OK) st = hip_status(hipEventRecord(q->resolved, s));
@@ -1610,12 +1700,18 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
   DeviceGuard g(q->device);
   hipStream_t s = R.s;
   const uint64_t ntx = R.ntx;
-  QpCtx C{R.queue_id, R.max_mtu, R.mem_size, q->plans, q->piece_csum, q->piece_csum + q->np, q->tx, q->rx, R.nrx};
+  QpCtx C{R.queue_id, R.max_mtu, R.mem_size, q->plans, q->piece_csum, q->piece_cs4, q->tx, q->rx, R.nrx};
   const unsigned grid = R.grid;
   const uint64_t* part = q->hp;  // the tail, kQpTail words (page-locked)
   uint64_t* tail = q->partials + (size_t) grid * kQpStats;
   int st = hip_status(hipEventSynchronize(q->resolved));
   if (st != NICGPU_OK) return st;
+  q->np = part[20];
+  if (part[19] == 2u) return NICGPU_ERR_RANGE;  // a descriptor planned > 256 pieces: nothing resolved or settled
+  if (part[19]) {  // the async plan did not fit its buffers: the same
+    q->want_pieces = part[20] + part[20] / 4 + 64;
+    return NICGPU_ERR_AGAIN;
+  }
   uint64_t used = part[0];
   const unsigned long long first0 = (unsigned long long) part[1];
   const uint64_t settled = part[2];
@@ -1641,11 +1737,12 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
     }
     if (st == NICGPU_OK) {
       hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, lim, q->txc, q->rxc, q->writes,
-                         q->partials, static_cast<const uint32_t*>(nullptr));
+                         q->partials, static_cast<const uint32_t*>(nullptr), q->gflags, q->plan_gen);
       st = hip_status(hipGetLastError());
     }
     if (st == NICGPU_OK) {
-      hipLaunchKernelGGL(qp_reduce_kernel, dim3(1), dim3(kQpReduceThreads), 0, s, q->partials, grid, q->pos, ntx, false);
+      hipLaunchKernelGGL(qp_reduce_kernel, dim3(1), dim3(kQpReduceThreads), 0, s, q->partials, grid, q->pos, ntx, false,
+                         q->gflags, q->plan_gen);
       st = hip_status(hipGetLastError());
     }
     if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->hp, tail, kQpTail * sizeof(uint64_t), hipMemcpyDeviceToHost, s));

@@ -28,6 +28,11 @@ int blocks_per_cu(const void* kernel, int threads, uint32_t lds);
 
 inline int hip_status(hipError_t e) { return e == hipSuccess ? NICGPU_OK : NICGPU_ERR_HIP; }
 
+// nicgpu_checksum_batch_split over min(n_max, *n_dev) frames, the count read
+// on the device (rx.hip; the f1 stage's asynchronous plan)
+int checksum_split_count(const uint8_t* frames, const uint64_t* desc, size_t n_max, const uint64_t* n_dev,
+                         uint16_t* out_rest, uint16_t* out_head4, void* stream);
+
 // Makes `dev` current for the scope and restores the previous device.
 struct DeviceGuard {
   int prev = -1;

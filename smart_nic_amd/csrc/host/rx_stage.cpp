@@ -1583,19 +1583,21 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     out.timings.copy_us += sl.upload_us;
     check(nicgpu_stream_wait_event(ps, sl.ev_tx), "nicgpu_stream_wait_event");
   }
-  std::uint64_t np = 0;
-  const int pst = nicgpu_qp_plan_on(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx,
-                                    config_.max_mtu, &np, &v, ps, stream);
+  // the plan and the piece sums enqueued without a wait: the piece buffers are
+  // sized ahead (ntx + ntx / 4 pieces, or what an earlier batch needed); a
+  // plan that does not fit them, or a descriptor planning more pieces than
+  // 32-bit piece indices allow, makes the resolve settle nothing and its
+  // finish return NICGPU_ERR_RANGE — that batch then takes the host path
+  // (which refuses it if its total does not fit either), the next one fits
+  check(nicgpu_qp_plan_async(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu,
+                             &v, ps, stream),
+        "nicgpu_qp_plan_async");
   out.timings.sums_us += us_since(t);
   t = clock::now();
   if (sl.up) {
     sl.up->finish();
     sl.up.reset();
   }
-  // a descriptor planning more pieces than 32-bit piece indices allow: the
-  // host path (which refuses the batch if its total does not fit either)
-  if (pst == NICGPU_ERR_RANGE) return false;
-  check(pst, "nicgpu_qp_plan_on");
   if (!dev_desc) {
     check(nicgpu_stream_wait_event(ps, sl.ev_rx), "nicgpu_stream_wait_event");
     if (side) check(nicgpu_stream_wait_event(stream, sl.ev_rx), "nicgpu_stream_wait_event");
@@ -1649,7 +1651,13 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   t = clock::now();
   std::uint64_t done = 0, used = 0, settled = 0;
   nicgpu_qp_stats ds{};
-  check(nicgpu_qp_resolve_finish(sl.qp, &done, &used, &settled, &ds), "nicgpu_qp_resolve_finish");
+  const int rst = nicgpu_qp_resolve_finish(sl.qp, &done, &used, &settled, &ds);
+  if (rst == NICGPU_ERR_AGAIN || rst == NICGPU_ERR_RANGE) {  // the plan did not fit: nothing resolved, settled or written
+    out.timings.resolve_us += us_since(t);
+    if (rst == NICGPU_ERR_RANGE) return false;
+    return front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);  // grown buffers: this plan fits
+  }
+  check(rst, "nicgpu_qp_resolve_finish");
   sl.settled = settled;
   sl.relaxed = done < ntx || settled < used;  // completions rewritten after ev_resolved
   out.timings.resolve_us += us_since(t);
@@ -1674,6 +1682,8 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     const auto tail_rx = hrx.subspan(used);
     make_plan(config_, mem.size, tail_tx, S.host.plan, /*split4=*/true);
     std::uint32_t pb = 0;
+    std::uint64_t np = 0;
+    check(nicgpu_qp_piece_count(sl.qp, &np), "nicgpu_qp_piece_count");
     check(nicgpu_memcpy_async(&pb, v.piece_base + done, sizeof(pb), stream), "nicgpu_memcpy_async");
     check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
     if (np - pb != S.host.plan.pieces.size()) throw GpuError("process_batch: device and host plans differ", NICGPU_ERR_INVALID);
@@ -1681,7 +1691,7 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     const std::size_t m = np - pb;
     S.tail_cs.resize(2 * m);
     check(nicgpu_memcpy_async(S.tail_cs.data(), v.piece_csum + pb, m * 2, stream), "nicgpu_memcpy_async");
-    check(nicgpu_memcpy_async(S.tail_cs.data() + m, v.piece_csum + np + pb, m * 2, stream), "nicgpu_memcpy_async");
+    check(nicgpu_memcpy_async(S.tail_cs.data() + m, v.piece_cs4 + pb, m * 2, stream), "nicgpu_memcpy_async");
     check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
     RxBatchResult& part = S.host.part;
     resolve(quiet_, mem.size, S.host.plan, S.tail_cs, tail_tx, tail_rx, st, part, S.host.writes, S.host.write_of_rx);

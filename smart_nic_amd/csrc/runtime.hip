@@ -78,6 +78,7 @@ const char* nicgpu_strerror(int status) {
     case NICGPU_ERR_NO_DEVICE: return "no gfx950 device";
     case NICGPU_ERR_NOMEM: return "out of device memory";
     case NICGPU_ERR_RANGE: return "batch too large for 32-bit piece indices";
+    case NICGPU_ERR_AGAIN: return "plan outgrew its buffers: redo the batch";
     default: return "unknown status";
   }
 }

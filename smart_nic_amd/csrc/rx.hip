@@ -932,6 +932,19 @@ int nicgpu_checksum_batch(const uint8_t* frames, const uint64_t* desc, size_t n,
                            stream);
 }
 
+}  // extern "C"
+
+namespace nicgpu_detail {
+int checksum_split_count(const uint8_t* frames, const uint64_t* desc, size_t n_max, const uint64_t* n_dev,
+                         uint16_t* out_rest, uint16_t* out_head4, void* stream) {
+  if (!n_dev || (n_max && (!out_rest || !out_head4))) return NICGPU_ERR_INVALID;
+  return rx_offload_impl(0, nullptr, frames, desc, n_max, NICGPU_TUPLE_NONE, 0, 0, out_rest, nullptr, nullptr, nullptr,
+                         nullptr, stream, n_dev, out_head4);
+}
+}  // namespace nicgpu_detail
+
+extern "C" {
+
 int nicgpu_checksum_batch_split(const uint8_t* frames, const uint64_t* desc, size_t n, uint16_t* out_rest,
                                 uint16_t* out_head4, void* stream) {
   if (n && (!out_rest || !out_head4)) return NICGPU_ERR_INVALID;

@@ -17,6 +17,10 @@
 // c3: IMIX 64/576/1518 (7:4:1) frames, each balanced so the whole-frame
 //     checksum verifies; RX descriptors with Layer4 checksum offload, 2 KiB
 //     buffers; RSS over the delivered frames (MS key, table i%16).
+// The RX ring's buffers start on a 4-KiB boundary after the TX frames, as a
+// driver's page-backed ring does (env NIC_BENCH_RX_ALIGN=16: right after them,
+// 16-B aligned only — frames then start inside 64-B sectors, which costs the
+// delivery a read-modify-write per partial sector).
 // c5: 9000-B frames with TSO (H = 54, mss = 1448 -> 7 segments), RX verify on:
 //     random payloads fail on the first segment, so the batch exercises the
 //     reference's first-failure abort (queue_pair.cpp:361-364).
@@ -76,7 +80,10 @@ int main(int argc, char** argv) {
   const std::size_t rx_buf = wl == "c5" ? 1600 : 2048;
   const std::size_t segs = wl == "c5" ? 7 : 1;
   const std::size_t nrx = n * segs;
-  const std::size_t mem_size = tx_bytes + nrx * rx_buf;
+  const char* ra = std::getenv("NIC_BENCH_RX_ALIGN");
+  const std::size_t rx_align = ra ? std::max<std::size_t>(16, std::strtoull(ra, nullptr, 10)) : 4096;
+  const std::size_t rx_base = (tx_bytes + rx_align - 1) / rx_align * rx_align;
+  const std::size_t mem_size = rx_base + nrx * rx_buf;
   std::vector<std::uint8_t> tx_img(tx_bytes);
   std::vector<TxDescriptor> tx(n);
   std::size_t at = 0;
@@ -109,7 +116,7 @@ int main(int argc, char** argv) {
   }
   std::vector<RxDescriptor> rx(nrx);
   for (std::size_t j = 0; j < nrx; ++j) {
-    rx[j].buffer_address = tx_bytes + j * rx_buf;
+    rx[j].buffer_address = rx_base + j * rx_buf;
     rx[j].buffer_length = static_cast<std::uint32_t>(rx_buf);
     rx[j].descriptor_index = static_cast<std::uint16_t>(j);
     rx[j].checksum_offload = true;
@@ -224,10 +231,10 @@ int main(int argc, char** argv) {
   for (auto L : lens) frame_bytes += L;
   const auto& T = tot[tot.size() / 2].second;  // the median batch's phases
   std::printf(
-      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"mode\": \"%s\", \"results\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, "
+      "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"mode\": \"%s\", \"results\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, \"rx_align\": %zu, "
       "\"rx_success\": %zu, \"interrupts\": %s, \"irq_callbacks\": %llu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
       "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f}}\n",
-      wl.c_str(), T.device ? "device" : "host", desc_kind.c_str(), pipelined ? "pipelined" : "sync", cfg.results_on_device ? "device" : "host", cfg.host_threads, n, last.rx_completions.size(), ok,
+      wl.c_str(), T.device ? "device" : "host", desc_kind.c_str(), pipelined ? "pipelined" : "sync", cfg.results_on_device ? "device" : "host", cfg.host_threads, n, last.rx_completions.size(), rx_align, ok,
       irq ? "true" : "false", (unsigned long long) irq_count, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
       T.resolve_us, T.gather_us, T.rss_us, T.copy_us);
   nicgpu_free(mem);

@@ -46,6 +46,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--slot", type=int, default=2048)
     ap.add_argument("--modes", default="0,1,2,4,8,6,5,7,32")
+    ap.add_argument("--frames", choices=["udp", "random"], default="udp",
+                    help="udp: IPv4/UDP headers (pktgen); random: random bytes behind EtherType 0x0800, as "
+                         "tools/bench_rx_stage.cpp builds them (IHL random: most tuples end past the 48-B stage)")
+    ap.add_argument("--rx-base", choices=["page", "packed"], default="page",
+                    help="page: RX slots from the next 4-KiB boundary after the TX bytes; packed: right after them "
+                         "(16-B aligned only, as tools/bench_rx_stage.cpp lays them out)")
+    ap.add_argument("--rx-shift", type=int, default=0, help="bytes added to the RX slot base (a multiple of 16)")
     ap.add_argument("--lib", default=os.path.join(ROOT, "smart_nic_amd", "libnicgpu_tune.so"),
                     help="tuning library to time (an A/B build of libnicgpu_tune.so)")
     ap.add_argument("--patterns", action="store_true",
@@ -73,7 +80,12 @@ def main():
     lens = pktgen.imix_lengths(n, rng)
     frames, desc, _ = pktgen.make_batch(lens, seed=33, proto=17, corrupt_frac=0.0)
     off = (desc & np.uint64((1 << 40) - 1)).astype(np.uint64)
-    tx_bytes = (int(frames.size) + 4095) // 4096 * 4096
+    if args.frames == "random":
+        frames = rng.integers(0, 256, frames.size, dtype=np.uint8)
+        frames[off.astype(np.int64) + 12] = 0x08
+        frames[off.astype(np.int64) + 13] = 0x00
+    tx_bytes = (int(frames.size) + 4095) // 4096 * 4096 if args.rx_base == "page" else (int(frames.size) + 15) // 16 * 16
+    tx_bytes += args.rx_shift
     mem_size = tx_bytes + n * args.slot
     mem = torch.zeros(mem_size + 64, dtype=torch.uint8, device="cuda")
     mem[: frames.size].copy_(torch.from_numpy(frames))
@@ -145,7 +157,8 @@ def main():
     got = mem[tx_bytes: tx_bytes + k * args.slot].view(k, args.slot).cpu().numpy()
     ok = all(np.array_equal(got[i, : lens[i]], frames[int(off[i]): int(off[i]) + lens[i]]) for i in range(k))
     moved = 2 * int(lens.sum())
-    out = {"lib": os.path.basename(args.lib), "n": n, "slot": args.slot, "frame_bytes": int(lens.sum()), "moved_bytes": moved, "delivered_ok": bool(ok),
+    out = {"lib": os.path.basename(args.lib), "frames": args.frames, "rx_base": args.rx_base, "rx_base_mod128": tx_bytes % 128,
+           "n": n, "slot": args.slot, "frame_bytes": int(lens.sum()), "moved_bytes": moved, "delivered_ok": bool(ok),
            "success_count": int(cnt.item()), "us_median": {}, "tbps_rw": {}}
     for name, ts in times.items():
         med = float(np.median(ts))
