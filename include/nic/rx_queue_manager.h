@@ -136,6 +136,8 @@ public:
 private:
   struct Queue;
   std::vector<std::unique_ptr<Queue>> qps_;
+  struct Streams;  // a stream per queue pair, forked from and joined into the caller's
+  std::unique_ptr<Streams> streams_;
   std::vector<std::uint8_t> weights_;
   std::size_t index_{0}, credit_{0};
   std::uint64_t advances_{0}, skips_{0};

@@ -130,6 +130,34 @@ QueueSchedule schedule(std::span<const std::uint8_t> weights, std::span<const st
 }
 
 bool queues_disjoint(std::size_t mem_size, std::span<const QueueBatch> batches) {
+  // Fast path, O(n): each queue's TX and RX spans inside bounding boxes; when
+  // no queue's RX box meets another queue's TX or RX box no two spans can
+  // overlap (the usual layout: every queue's buffers in a region of its own).
+  // Otherwise the exact sweep below (a sort of every span).
+  {
+    struct Box {
+      std::uint64_t lo = ~0ull, hi = 0;
+      void add(std::uint64_t a, std::uint64_t b) {
+        lo = std::min(lo, a);
+        hi = std::max(hi, b);
+      }
+      bool meets(const Box& o) const { return lo < o.hi && o.lo < hi; }
+    };
+    std::vector<Box> tb(batches.size()), rb(batches.size());
+    for (std::size_t q = 0; q < batches.size(); ++q) {
+      for (const TxDescriptor& t : batches[q].tx)
+        if (t.length && t.buffer_address < mem_size)
+          tb[q].add(t.buffer_address, std::min<std::uint64_t>(t.buffer_address + t.length, mem_size));
+      for (const RxDescriptor& x : batches[q].rx)
+        if (x.buffer_length && x.buffer_address < mem_size)
+          rb[q].add(x.buffer_address, std::min<std::uint64_t>(x.buffer_address + x.buffer_length, mem_size));
+    }
+    bool apart = true;
+    for (std::size_t q = 0; q < batches.size() && apart; ++q)
+      for (std::size_t r = 0; r < batches.size() && apart; ++r)
+        if (q != r && (rb[q].meets(tb[r]) || rb[q].meets(rb[r]))) apart = false;
+    if (apart) return true;
+  }
   std::vector<Span> spans;
   auto add = [&](std::uint64_t a, std::uint64_t n, std::uint32_t q, bool rx) {
     if (n == 0 || a >= mem_size) return;  // nothing moved, or a DMA fault
@@ -174,7 +202,44 @@ struct BatchedQueueManager::Queue {
   }
 };
 
-BatchedQueueManager::BatchedQueueManager(BatchedQueueManagerConfig config) {
+// Every queue pair's batch runs on a stream of its own, forked from the
+// caller's stream by an event and joined back into it, so the queue pairs'
+// device work overlaps (one shared stream serialised 16 x 64 K batches).
+struct BatchedQueueManager::Streams {
+  int device = -1;
+  void* fork = nullptr;           // recorded on the caller's stream
+  std::vector<void*> s, joined;   // per queue pair: its stream and its end event
+  ~Streams() { release(); }
+  void release() {
+    for (void* x : s) (void) nicgpu_stream_destroy(x);
+    for (void* e : joined) (void) nicgpu_event_destroy(e);
+    if (fork) (void) nicgpu_event_destroy(fork);
+    s.clear();
+    joined.clear();
+    fork = nullptr;
+    device = -1;
+  }
+  void ensure(std::size_t q) {
+    int dev = 0;
+    if (nicgpu_get_device(&dev) != NICGPU_OK) throw GpuError("BatchedQueueManager: no device", NICGPU_ERR_NO_DEVICE);
+    if (dev != device) release();
+    device = dev;
+    auto ok = [](int st, const char* what) {
+      if (st != NICGPU_OK) throw GpuError(std::string("BatchedQueueManager: ") + what, st);
+    };
+    if (!fork) ok(nicgpu_event_create(&fork), "nicgpu_event_create");
+    while (s.size() < q) {
+      void* x = nullptr;
+      void* e = nullptr;
+      ok(nicgpu_stream_create(&x), "nicgpu_stream_create");
+      s.push_back(x);
+      ok(nicgpu_event_create(&e), "nicgpu_event_create");
+      joined.push_back(e);
+    }
+  }
+};
+
+BatchedQueueManager::BatchedQueueManager(BatchedQueueManagerConfig config) : streams_(std::make_unique<Streams>()) {
   for (BatchedQueuePairConfig& c : config.queue_configs) {
     if (c.weight == 0) c.weight = 1;  // queue_manager.cpp:14-16
     weights_.push_back(c.weight);
@@ -217,12 +282,19 @@ QueueSchedule BatchedQueueManager::process_batch(const DeviceHostMemory& mem, st
     if (!shared) {
       for (std::size_t q = 0; q < Q; ++q)  // contexts made on this thread before the jobs read them
         if (n[q] && qps_[q]->config.rss && qps_[q]->config.device_resolve) (void) qps_[q]->config.rss->device_context(stream);
+      Streams& T = *streams_;
+      T.ensure(Q);
+      auto ok = [](int st, const char* what) {
+        if (st != NICGPU_OK) throw GpuError(std::string("BatchedQueueManager: ") + what, st);
+      };
+      ok(nicgpu_event_record(T.fork, stream), "nicgpu_event_record");  // the caller's earlier work first
       std::vector<std::size_t> sent;
       std::exception_ptr err;
       for (std::size_t q = 0; q < Q && !err; ++q) {
         if (!n[q]) continue;
         try {
-          qps_[q]->stage.submit(mem, batches[q].tx, batches[q].rx, stream);
+          ok(nicgpu_stream_wait_event(T.s[q], T.fork), "nicgpu_stream_wait_event");
+          qps_[q]->stage.submit(mem, batches[q].tx, batches[q].rx, T.s[q]);
           sent.push_back(q);
         } catch (...) {
           err = std::current_exception();
@@ -231,6 +303,9 @@ QueueSchedule BatchedQueueManager::process_batch(const DeviceHostMemory& mem, st
       for (const std::size_t q : sent) {  // every submitted batch is collected, whatever throws
         try {
           qps_[q]->stage.collect(out[q]);
+          // the caller's stream continues after every queue pair's work
+          ok(nicgpu_event_record(T.joined[q], T.s[q]), "nicgpu_event_record");
+          ok(nicgpu_stream_wait_event(stream, T.joined[q]), "nicgpu_stream_wait_event");
         } catch (...) {
           if (!err) err = std::current_exception();
         }

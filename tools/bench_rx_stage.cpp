@@ -1,6 +1,6 @@
 // bench_rx_stage.cpp — nic::BatchedQueuePair throughput.
 //
-//   bench_rx_stage <workload: c3|c5> <tx_descriptors> <reps> [host_threads] [device|host] [pageable|pinned|device] [sync|pipelined] [host|device] [irq]
+//   bench_rx_stage <workload: c3|c5|qm16> <tx_descriptors> <reps> [host_threads] [device|host] [pageable|pinned|device] [sync|pipelined] [host|device] [irq]
 //   (device: BatchedQueuePair's device resolve, the default for disjoint
 //   buffers; host: the host resolve, BatchedQueuePairConfig::device_resolve off;
 //   pinned: the descriptor arrays in page-locked memory, as a descriptor ring
@@ -21,6 +21,8 @@
 // driver's page-backed ring does (env NIC_BENCH_RX_ALIGN=16: right after them,
 // 16-B aligned only — frames then start inside 64-B sectors, which costs the
 // delivery a read-modify-write per partial sector).
+// qm16: the c3 batch split over 16 queue pairs of a nic::BatchedQueueManager
+//     (one process_batch drains them all; host descriptors only).
 // c5: 9000-B frames with TSO (H = 54, mss = 1448 -> 7 segments), RX verify on:
 //     random payloads fail on the first segment, so the batch exercises the
 //     reference's first-failure abort (queue_pair.cpp:361-364).
@@ -29,6 +31,7 @@
 // JSON line: packets/s, frame bytes/s and the per-phase split.
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -38,6 +41,7 @@
 #include <vector>
 
 #include "nic/rss.h"
+#include "nic/rx_queue_manager.h"
 #include "nic/rx_stage.h"
 #include "nicgpu.h"
 
@@ -145,6 +149,7 @@ int main(int argc, char** argv) {
   std::uint64_t irq_count = 0, irq_sum = 0;
   if (irq) {
     cfg.enable_tx_interrupts = true;
+    cfg.enable_rx_interrupts = true;
     cfg.on_interrupt = [&irq_count, &irq_sum](std::uint16_t, const CompletionEntry& e) {
       ++irq_count;
       irq_sum += e.descriptor_index;
@@ -174,6 +179,53 @@ int main(int argc, char** argv) {
     check(nicgpu_memcpy_async(drx, rx.data(), nrx * sizeof(RxDescriptor), nullptr), "memcpy");
     check(nicgpu_stream_synchronize(nullptr), "sync");
     dd = {static_cast<const TxDescriptor*>(dtx), n, static_cast<const RxDescriptor*>(drx), nrx};
+  }
+  if (wl == "qm16") {
+    // nic::BatchedQueueManager over 16 queue pairs, n / 16 C3 descriptors and
+    // RX buffers each (weights 1, one RssEngine per queue pair): one
+    // process_batch drains every queue, all 16 stages in flight at once
+    constexpr std::size_t Q = 16;
+    const std::size_t per = n / Q;
+    std::vector<std::unique_ptr<RssEngine>> engines;
+    BatchedQueueManagerConfig qc;
+    for (std::size_t q = 0; q < Q; ++q) {
+      engines.push_back(std::make_unique<RssEngine>(RssConfig{ms_key, table}));
+      BatchedQueuePairConfig c = cfg;
+      c.queue_id = static_cast<std::uint16_t>(q);
+      c.rss = engines.back().get();
+      c.on_interrupt = nullptr;
+      c.enable_tx_interrupts = c.enable_rx_interrupts = false;
+      qc.queue_configs.push_back(c);
+    }
+    BatchedQueueManager qm{qc};
+    std::vector<QueueBatch> b(Q);
+    for (std::size_t q = 0; q < Q; ++q) b[q] = QueueBatch{txs.subspan(q * per, per), rxs.subspan(q * per, per)};
+    std::vector<RxBatchResult> outs;
+    std::vector<double> ts;
+    std::uint64_t ok_q = 0;
+    for (int r = 0; r < reps + 2; ++r) {
+      const auto t0 = std::chrono::steady_clock::now();
+      qm.process_batch(dm, b, outs);
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      if (r >= 2) ts.push_back(us);
+    }
+    for (const auto& o : outs) {
+      if (o.timings.device && cfg.results_on_device) ok_q += o.dev.nrx;
+      else for (const auto& c : o.rx_completions) ok_q += c.status == 0;
+    }
+    std::sort(ts.begin(), ts.end());
+    const double med = ts[ts.size() / 2];
+    std::size_t fb = 0;
+    for (std::size_t i = 0; i < per * Q; ++i) fb += lens[i];
+    std::printf("{\"row\": \"f1_queue_manager\", \"workload\": \"c3\", \"queue_pairs\": %zu, \"tx_per_queue\": %zu, "
+                "\"descriptors\": \"%s\", \"results\": \"%s\", \"rx_align\": %zu, \"rx_completions\": %llu, "
+                "\"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f}\n",
+                Q, per, desc_kind.c_str(), cfg.results_on_device ? "device" : "host", rx_align, (unsigned long long) ok_q, med,
+                per * Q / med, fb / med / 1e3);
+    nicgpu_free(mem);
+    if (ptx) nicgpu_host_free(ptx);
+    if (prx) nicgpu_host_free(prx);
+    return 0;
   }
   auto submit = [&] {
     if (dev_desc) qp.submit(dm, dd);
