@@ -148,6 +148,7 @@ struct RxParams {
   uint32_t xpf_chunks;  // XPF kernels: prefetch the next tile's first batch when it has at most this many chunks
   unsigned long long* stamps;  // tuning builds only: per wave {start, end, XCC_ID, HW_ID} (s_memrealtime, 100 MHz)
   const unsigned long long* n_dev;  // batch size read on the device (min(n, *n_dev)); null: n
+  uint32_t xcd_w_odd;   // SPLIT kernels: share of an odd blockIdx % 8 group relative to an even one (65536 = 1)
   unsigned long long* hits_rep;  // per-context histogram replicas (flush_hist), or null
   unsigned int* hits_done;       // their done ticket
 };

@@ -23,6 +23,8 @@
 #include "common.h"
 #include "host.h"
 
+#include <cstdlib>
+
 #include <mutex>
 #include <vector>
 
@@ -445,7 +447,13 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
 // ring of P.hold_r tiles and stored when it is full and at the end, so output
 // writes reach DRAM in bursts instead of interleaved with the read stream
 // (DESIGN.md §4.1).  Loads are nontemporal.
-template <int U, int WPB, int SST, int OCC = 4, bool XPF = true>
+// SPLIT 1: each wave takes one contiguous packet range instead of every
+// nwaves-th tile, the ranges of the blockIdx % 8 groups (one XCD each under
+// round-robin placement) weighted by P.xcd_w_odd so the odd XCDs, which end
+// ~4-8% later (profiles/r02_wave_stamps_c2.jsonl), get less.  The split is a
+// function of (blockIdx, wave) and the count only: every packet is covered
+// exactly once wherever the blocks land; placement only affects its speed.
+template <int U, int WPB, int SST, int OCC = 4, bool XPF = true, int SPLIT = 0>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void rx_offload_kernel(
     RxParams P) {
   extern __shared__ uint4 lds_dyn[];
@@ -505,7 +513,26 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   // packets in this launch: n, or a count another kernel left on the device
   // (the grid is sized for n; waves past the count have no tile)
   const uint64_t n_all = P.n_dev ? (*P.n_dev < P.n ? (uint64_t) *P.n_dev : P.n) : P.n;
-  const uint64_t first = gw * kWave, end = n_all, step = nwaves * kWave;
+  uint64_t first = gw * kWave, end = n_all, step = nwaves * kWave;
+  if constexpr (SPLIT == 1) {
+    // group v = blockIdx % 8 gets [g0, g1), its waves equal parts of it in
+    // (blockIdx / 8, wave) order; n_all * weight sums < 2^64 (the host keeps
+    // n below 2^34); adjacent ranges share their boundary's expression
+    const uint32_t G = gridDim.x, v = blockIdx.x & 7u;
+    uint64_t cum = 0, tot = 0, mine = 0;
+    for (uint32_t u = 0; u < 8u; ++u) {
+      const uint64_t c = (uint64_t) ((G + 7u - u) / 8u) * ((u & 1u) ? (uint64_t) P.xcd_w_odd : 65536ull);
+      if (u < v) cum += c;
+      if (u == v) mine = c;
+      tot += c;
+    }
+    const uint64_t g0 = n_all * cum / tot, g1 = cum + mine == tot ? n_all : n_all * (cum + mine) / tot;
+    const uint64_t nw = (uint64_t) ((G + 7u - v) / 8u) * WPB,
+                   rank = (uint64_t) (blockIdx.x >> 3) * WPB + (uint64_t) __builtin_amdgcn_readfirstlane(w);
+    first = g0 + (g1 - g0) * rank / nw;
+    end = rank + 1 == nw ? g1 : g0 + (g1 - g0) * (rank + 1) / nw;
+    step = kWave;
+  }
   auto nvalid_of = [&](uint64_t b) __attribute__((always_inline)) -> uint32_t {
     return b < end ? (uint32_t) (end - b < (uint64_t) kWave ? end - b : (uint64_t) kWave) : 0u;
   };
@@ -711,6 +738,10 @@ const RxVariant kRxVariants[] = {
     // slots of 8 waves) keep 4-wave blocks (profiles/r02y_tune_variants.json).
     {rx_offload_kernel<2, 8, 16>, 2, 8, "u2_w8_c_sc1_ring_xpf"},
 #ifdef NICGPU_TUNING
+    // contiguous XCD-weighted ranges (SPLIT 1; P.xcd_w_odd from NICGPU_RX_XCD_ODD)
+    {rx_offload_kernel<2, 4, 16, 4, true, 1>, 2, 4, "u2_w4_c_sc1_ring_xpf_xcd"},
+    {rx_offload_kernel<2, 4, 0, 4, true, 1>, 2, 4, "u2_w4_c_ring_xpf_xcd"},
+    {rx_offload_kernel<2, 8, 16, 4, true, 1>, 2, 8, "u2_w8_c_sc1_ring_xpf_xcd"},
     // candidates timed by tools/tune_rx.py (the rejected experiments of
     // DESIGN.md §7 — deferred stores, register-held results, non-contiguous
     // only, other load policies — are in git history before round 4)
@@ -878,6 +909,11 @@ int rx_offload_impl(int variant, const nicgpu_rss_ctx* ctx, const uint8_t* frame
   P.out_hits = reinterpret_cast<unsigned long long*>(out_hits);
   P.out_l34 = out_l34;
   P.out_cs4 = out_cs4;
+  static const uint32_t xcd_odd = [] {
+    const char* e = std::getenv("NICGPU_RX_XCD_ODD");  // tuning: odd groups' share x 65536
+    return e ? (uint32_t) std::strtoul(e, nullptr, 10) : 61500u;
+  }();
+  P.xcd_w_odd = xcd_odd ? xcd_odd : 1u;
   P.n_dev = reinterpret_cast<const unsigned long long*>(n_dev);
 #ifdef NICGPU_TUNING
   P.stamps = g_tune_stamps;
