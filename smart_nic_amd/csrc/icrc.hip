@@ -245,6 +245,222 @@ __global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
   }
 }
 
+// ---------------------------------------------- lane-cooperative ICRC --
+// Eight lanes per packet (a group; eight groups per wave), one 128-B line of
+// the packet per step: lane `sub` loads the line's 16-B chunk `sub` — the
+// group's loads cover whole lines, so a wave instruction reads eight lines
+// instead of the 64 scattered lines of the lane-per-packet walk (92% of that
+// kernel's time, profiles/r03_icrc_variants.jsonl).  CRC-32C is linear over
+// GF(2): with A the state map of 16 zero bytes, a line's state is
+//   S' = A^8 S ^ sum_sub A^(7 - sub) f(0, chunk_sub),
+// f(s, c) the slice-by-4 chain over c from s.  Lane 0 runs its chain from S
+// (f(S, c) = A S ^ f(0, c)), every lane shifts its result by A^(7 - sub)
+// (operator tables: four byte lookups per power), and the group xor-reduces
+// (three lane swaps).  Lines are aligned to the packet's END, so only the
+// first line is partial: the packet is front-padded with Z zero bytes
+// (chunks before the packet read as zeros, the chunk holding its first byte is
+// masked) and the chain enters from kCrcLead128[Z], the state Z zero bytes
+// take to 0xFFFFFFFF.
+struct CrcLead128 {
+  uint32_t s[128];
+};
+constexpr CrcLead128 make_crc_lead128() {
+  const Crc32cTables T = make_crc32c_tables();
+  uint32_t top_inv[256] = {};
+  for (uint32_t k = 0; k < 256; ++k) top_inv[T.t[0][k] >> 24] = k;
+  CrcLead128 R{};
+  uint32_t s = 0xFFFFFFFFu;
+  R.s[0] = s;
+  for (int n = 1; n < 128; ++n) {
+    const uint32_t k = top_inv[s >> 24];
+    s = ((s ^ T.t[0][k]) << 8) | k;
+    R.s[n] = s;
+  }
+  return R;
+}
+__constant__ CrcLead128 kCrcLead128 = make_crc_lead128();
+
+// op[m][j][v] = A^m applied to (v << 8j): A^m s = xor_j op[m][j][byte j of s]
+// (m = 1..4; A = 16 zero bytes: state = (state >> 8) ^ T0[state & 0xFF] per byte)
+struct CrcShiftOps {
+  uint32_t t[4][4][256];
+};
+constexpr CrcShiftOps make_crc_shift_ops() {
+  const Crc32cTables T = make_crc32c_tables();
+  CrcShiftOps O{};
+  for (int m = 1; m <= 4; ++m)
+    for (int j = 0; j < 4; ++j)
+      for (uint32_t v = 0; v < 256; ++v) {
+        uint32_t st = v << (8 * j);
+        for (int b = 0; b < 16 * m; ++b) st = (st >> 8) ^ T.t[0][st & 0xFFu];
+        O.t[m - 1][j][v] = st;
+      }
+  return O;
+}
+__constant__ CrcShiftOps kCrcShiftOps = make_crc_shift_ops();
+
+constexpr int kCoopRing = 128;
+#ifndef NICGPU_ICRC_LINES
+#define NICGPU_ICRC_LINES 4
+#endif
+constexpr int kCoopLines = NICGPU_ICRC_LINES;  // lines of a packet in flight per group
+constexpr uint32_t kOpsBytes = 4u * 4u * 256u * 4u;  // 16 KiB
+
+__device__ __forceinline__ uint32_t crc_shift(const uint32_t* __restrict__ ops, uint32_t m, uint32_t s) {
+  const uint32_t* o = ops + (m - 1u) * 1024u;
+  return xor3(o[s & 0xFFu], o[256u + ((s >> 8) & 0xFFu)], o[512u + ((s >> 16) & 0xFFu)]) ^ o[768u + (s >> 24)];
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kIcrcThreads) void icrc_coop_kernel(IcrcParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t Tb[kB4Bytes];
+  __shared__ uint32_t ops[kOpsBytes / 4u];
+  __shared__ uint64_t ring_all[kIcrcWpb][kCoopRing];
+  __shared__ uint4 lead_m[16];  // bytes >= p of a chunk kept
+  if (threadIdx.x < 16u) {
+    const int p = (int) threadIdx.x;
+    lead_m[p] = make_uint4(dword_keep(p, 16, 0), dword_keep(p, 16, 1), dword_keep(p, 16, 2), dword_keep(p, 16, 3));
+  }
+  for (uint32_t q = threadIdx.x; q < kB4Bytes / 16u; q += kIcrcThreads) {
+    const uint32_t o = q * 16u;
+    const uint32_t j = 2u * (o >> 16) + ((o >> 7) & 1u), v = (o >> 8) & 255u;
+    const uint32_t val = kCrc32c.t[3u - j][v];
+    reinterpret_cast<uint4*>(Tb)[q] = make_uint4(val, val, val, val);
+  }
+  for (uint32_t q = threadIdx.x; q < kOpsBytes / 4u; q += kIcrcThreads) ops[q] = (&kCrcShiftOps.t[0][0][0])[q];
+  __syncthreads();
+  const uint32_t lane = lane_id();
+  const uint32_t sub = lane & 7u;
+  const uint32_t cb = (lane & 31u) << 2;  // this lane's copy of the byte tables: bank lane % 32
+  const uint32_t cbr = cb | ((cb + 128u) << 8) | (1u << 24);
+  uint64_t* ring = ring_all[threadIdx.x / kWave];
+  const uint64_t nwaves = (uint64_t) gridDim.x * kIcrcWpb;
+  const uint64_t wave = (uint64_t) blockIdx.x * kIcrcWpb + threadIdx.x / kWave;
+  const uint64_t per = (P.n + nwaves - 1) / nwaves;
+  const uint64_t p0 = wave * per < P.n ? wave * per : P.n;
+  const uint64_t p1 = p0 + per < P.n ? p0 + per : P.n;
+
+  uint64_t loaded = p0;
+  auto refill = [&]() __attribute__((always_inline)) {
+    const uint64_t i = loaded + lane;
+    ring[i & (kCoopRing - 1)] = i < p1 ? P.desc[i] : 0ull;
+    loaded += kWave;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  };
+  refill();
+  refill();
+  uint64_t next = p0 + 8u;
+  uint64_t my = p0 + (lane >> 3);  // this group's packet
+  // the group's packet (every lane of the group holds the same values):
+  // span [off, end), T lines to go counting down, state S
+  uint64_t off = 0, end = 0;
+  uint32_t len = 0, tl = 0, S = 0xFFFFFFFFu;
+  auto setup = [&]() __attribute__((always_inline)) {
+    const uint64_t d = ring[my & (kCoopRing - 1)];
+    off = d & kOffMask;
+    len = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
+    const uint32_t span = P.verify ? (len >= 4u ? len - 4u : 0u) : len;
+    end = off + span;
+    tl = (span + 127u) >> 7;
+    S = kCrcLead128.s[(tl << 7) - span];
+  };
+  if (my < p1) setup();
+  for (;;) {
+    const bool active = my < p1;
+    if (__ballot(active) == 0ull) break;
+    if (active && tl != 0u) {
+      // up to kCoopLines of the packet's lines per iteration, every load
+      // issued before the first chain (a line's chunk `sub` ends
+      // 128 * (tl - k - 1) bytes before the packet's end)
+      const uint32_t nl = tl < (uint32_t) kCoopLines ? tl : (uint32_t) kCoopLines;
+      u32x4 v[kCoopLines];
+      int64_t av[kCoopLines];
+#pragma unroll
+      for (int k = 0; k < kCoopLines; ++k) {
+        const uint32_t tk = (uint32_t) k < nl ? tl - (uint32_t) k : tl;
+        const int64_t a = (int64_t) end - 128 * (int64_t) tk + 16 * (int64_t) sub;
+        av[k] = a;
+        const bool pad = a + 16 <= (int64_t) off;
+        const int64_t la = pad ? (int64_t) off : (a < 0 ? 0 : a);
+        __builtin_memcpy(&v[k], P.frames + la, 16);  // 16 B at any byte alignment
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < kCoopLines; ++k) {
+        if ((uint32_t) k >= nl) break;
+        const int64_t a = av[k];
+        const bool pad = a + 16 <= (int64_t) off;
+        u32x4 x = v[k];
+        if (a < 0 && !pad) {  // (the packet starts within the image's first 16 B) bytes shifted up by -a
+          const uint32_t d = (uint32_t) (-a) * 8u;
+          uint64_t lo = ((uint64_t) x.y << 32) | x.x, hi = ((uint64_t) x.w << 32) | x.z;
+          if (d < 64u) {
+            hi = (hi << d) | (lo >> (64u - d));
+            lo <<= d;
+          } else {
+            hi = lo << (d - 64u);
+            lo = 0;
+          }
+          x = (u32x4){(uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32)};
+        }
+        if (pad) {
+          x = (u32x4){0u, 0u, 0u, 0u};
+        } else if (a < (int64_t) off) {
+          const uint4 m = lead_m[(uint32_t) ((int64_t) off - a)];
+          x.x &= m.x;
+          x.y &= m.y;
+          x.z &= m.z;
+          x.w &= m.w;
+        }
+        uint32_t s = sub == 0u ? S : 0u;
+        if constexpr (MODE == 1) {
+          s ^= x.x ^ x.y ^ x.z ^ x.w;
+        } else {
+          s = b4_dword(Tb, cbr, s ^ x.x);
+          s = b4_dword(Tb, cbr, s ^ x.y);
+          s = b4_dword(Tb, cbr, s ^ x.z);
+          s = b4_dword(Tb, cbr, s ^ x.w);
+          // A^(7 - sub): A^4 when 7 - sub >= 4, then A^((7 - sub) & 3)
+          const uint32_t r = 7u - sub;
+          const uint32_t s4 = crc_shift(ops, 4u, s);
+          s = (r & 4u) ? s4 : s;
+          const uint32_t rr = r & 3u;
+          const uint32_t sr = crc_shift(ops, rr ? rr : 1u, s);
+          s = rr ? sr : s;
+        }
+        s ^= (uint32_t) __shfl_xor((int) s, 1);
+        s ^= (uint32_t) __shfl_xor((int) s, 2);
+        s ^= (uint32_t) __shfl_xor((int) s, 4);
+        S = s;
+      }
+      tl -= nl;
+    }
+    const bool finished = active && tl == 0u;
+    if (finished && sub == 0u) {
+      const uint32_t crc = S ^ 0xFFFFFFFFu;
+      if (P.out_crc) P.out_crc[my] = (P.verify && len < 4u) ? 0u : crc;
+      if (P.verify) {
+        uint32_t ok = 0;
+        if (len >= 4u) {
+          const uint8_t* t = P.frames + end;
+          const uint32_t stored = ((uint32_t) t[0] << 24) | ((uint32_t) t[1] << 16) | ((uint32_t) t[2] << 8) | t[3];
+          ok = stored == crc;
+        }
+        P.out_ok[my] = (uint8_t) ok;
+      }
+    }
+    // finished groups take the next packets of the wave's range in group order
+    const uint64_t m = __ballot(finished && sub == 0u);
+    const uint32_t gl = lane & ~7u;
+    const uint64_t below = gl ? (m & ((1ull << gl) - 1ull)) : 0ull;
+    if (finished) my = next + (uint64_t) __builtin_popcountll(below);
+    next += (uint64_t) __builtin_popcountll(m);
+    if (finished && my < p1) setup();
+    if (next + kWave > loaded && loaded < p1) refill();
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -265,17 +481,28 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
   // every resident wave slot busy (a wave's range is then >= 64 packets, one
   // work-queue refill); ranges of 8 packets per lane left 3/4 of the slots idle
   // NICGPU_ICRC=b4mem: timing only, the loads without the table work (results wrong)
+  // NICGPU_ICRC (tuning): b4 (default) the lane-per-packet kernel; coop the
+  // lane-cooperative one; b4mem / coopmem: timing only, their loads without
+  // the table work (results wrong)
+  // (the cooperative kernel, measured slower: C2 591 / IMIX 1145 us against
+  // 408 / 471 at 4 lines in flight per group, profiles/r04_icrc_coop.jsonl)
   static const int var = [] {
     const char* e = std::getenv("NICGPU_ICRC");
-    return e && std::strcmp(e, "b4mem") == 0 ? 1 : 0;
+    if (!e) return 0;
+    if (std::strcmp(e, "coop") == 0) return 2;
+    if (std::strcmp(e, "b4mem") == 0) return 1;
+    if (std::strcmp(e, "b4") == 0) return 0;
+    if (std::strcmp(e, "coopmem") == 0) return 3;
+    return 0;
   }();
   const uint64_t want = (n + kIcrcThreads - 1) / kIcrcThreads;
   const uint64_t cap = (uint64_t) di->cus * (uint64_t) blocks_per_cu(reinterpret_cast<const void*>(icrc_b4_kernel<8, 0>), kIcrcThreads, 0);
   const unsigned grid = (unsigned) (want < 1 ? 1 : (want < cap ? want : cap));
-  if (var == 1)
-    hipLaunchKernelGGL((icrc_b4_kernel<8, 1>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
-  else
-    hipLaunchKernelGGL((icrc_b4_kernel<8, 0>), dim3(grid), dim3(kIcrcThreads), 0, static_cast<hipStream_t>(stream), P);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (var == 1) hipLaunchKernelGGL((icrc_b4_kernel<8, 1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
+  else if (var == 0) hipLaunchKernelGGL((icrc_b4_kernel<8, 0>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
+  else if (var == 3) hipLaunchKernelGGL((icrc_coop_kernel<1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
+  else hipLaunchKernelGGL((icrc_coop_kernel<0>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
   return hip_status(hipGetLastError());
 }
 
