@@ -464,6 +464,31 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
                             unsigned flags, const nicgpu_rss_ctx* ctx, int tuple_mode, uint32_t raw_off,
                             uint32_t raw_len, uint64_t* hits_dev, void* stream);
 
+/* ---- RSS dispatch into per-queue completion rings (row f1) ----
+ * nq rings of ring_size entries on one device, one nic::CompletionQueue each
+ * (src/completion_queue.cpp:30-53; replaces its post_completion /
+ * poll_completion for the completions a batch dispatches by RSS queue).
+ * State per ring: producer, consumer, count (all < ring_size) and the entries
+ * a full ring refused. */
+typedef struct nicgpu_cq_set nicgpu_cq_set;
+int nicgpu_cq_create(nicgpu_cq_set** out, int device, size_t nq, size_t ring_size);
+int nicgpu_cq_destroy(nicgpu_cq_set* cq);
+/* Posts, for every queue q < nlists, the device completions
+ * rxc[which[start[q] .. end[q])] into ring q in that order, as
+ * CompletionQueue::post_completion would one by one: entry i of the list
+ * lands at (producer + i) % ring_size while the ring has room, the rest are
+ * refused (counted).  start / end are host arrays (nicgpu_qp_group's lists,
+ * RxBatchResult::dev.queue_start / queue_end), rxc and which device arrays.
+ * Synchronises `stream`. */
+int nicgpu_cq_post(nicgpu_cq_set* cq, const nicgpu_completion* rxc, const uint32_t* which, const uint32_t* start,
+                   const uint32_t* end, size_t nlists, void* stream);
+/* The rings' state into out_host[4 * nq]: producer[nq] | consumer[nq] |
+ * count[nq] | refused[nq].  Synchronises `stream`. */
+int nicgpu_cq_state(const nicgpu_cq_set* cq, uint32_t* out_host, void* stream);
+/* CompletionQueue::poll_completion up to max times on ring q: the entries
+ * into out_host, their number into *got.  Synchronises `stream`. */
+int nicgpu_cq_poll(nicgpu_cq_set* cq, uint32_t q, nicgpu_completion* out_host, size_t max, size_t* got, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

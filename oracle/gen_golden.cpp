@@ -18,12 +18,16 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <random>
 #include <fstream>
 #include <sstream>
 #include <string>
 #include <vector>
 
 #include "nic/checksum.h"
+#include "nic/completion_queue.h"
+#include "nic/doorbell.h"
 #include "nic/dma_engine.h"
 #include "nic/interrupt_dispatcher.h"
 #include "nic/msix.h"
@@ -1297,6 +1301,102 @@ void gen_tso_vlan() {
 }
 }  // namespace
 
+// ------------------------------------------- per-RSS-queue completion rings --
+// The batched stage's RSS dispatch posts every Success RX completion into the
+// CompletionQueue of its RSS queue (completion_queue.cpp:30-43, full rings
+// refuse) and a consumer polls them (:45-53).  Reference CompletionQueues,
+// one per queue (ring 64, doorbells recording every ring): three batches of
+// completions with skewed queue ids, polls between the batches, a full drain
+// at the end.  cq_rings.json.
+void gen_cq() {
+  constexpr std::size_t Q = 8, kRing = 64, kBatch = 300;
+  std::mt19937_64 rng(4242);
+  std::vector<std::vector<std::pair<std::uint32_t, std::uint32_t>>> rung(Q);  // per doorbell: (queue_id, data)
+  std::vector<Doorbell> bells(Q);
+  std::vector<std::unique_ptr<CompletionQueue>> cqs;
+  std::vector<std::pair<std::uint32_t, std::uint32_t>> ring_log;  // in ring order across queues
+  for (std::size_t q = 0; q < Q; ++q) {
+    bells[q].set_callback([&ring_log](const DoorbellPayload& p) { ring_log.push_back({p.queue_id, p.data}); });
+    cqs.push_back(std::make_unique<CompletionQueue>(
+        CompletionQueueConfig{kRing, static_cast<std::uint16_t>(100 + q)}, &bells[q]));
+  }
+  auto entry_json = [](const CompletionEntry& e) {
+    std::ostringstream o;
+    o << "[" << e.queue_id << "," << e.descriptor_index << "," << e.status << "," << e.segments_produced << ","
+      << e.vlan_tag << "," << (int) e.checksum_verified << "]";
+    return o.str();
+  };
+  std::ostringstream js;
+  js << "{\"ring_size\": " << kRing << ", \"queues\": " << Q << ", \"cq_queue_id_base\": 100, \"batches\": [";
+  for (int b = 0; b < 3; ++b) {
+    std::vector<std::uint32_t> status, queue, didx, qid, segs, vlan, ver, posted;
+    ring_log.clear();
+    for (std::size_t j = 0; j < kBatch; ++j) {
+      CompletionEntry e;
+      e.queue_id = static_cast<std::uint16_t>(rng() % 4);
+      e.descriptor_index = static_cast<std::uint16_t>(b * 1000 + j);
+      const auto r = rng() % 10;
+      e.status = r < 8 ? 0u : static_cast<std::uint32_t>(1 + rng() % 7);
+      e.segments_produced = static_cast<std::uint16_t>(1 + rng() % 3);
+      e.vlan_tag = static_cast<std::uint16_t>(rng() % 4096);
+      e.checksum_verified = (rng() & 1) != 0;
+      // skewed RSS queues: queue 0 and 1 take most (their rings fill)
+      const auto u = rng() % 16;
+      const std::uint32_t q = u < 6 ? 0u : (u < 10 ? 1u : static_cast<std::uint32_t>(2 + rng() % (Q - 2)));
+      bool ok = false;
+      if (e.status == 0) ok = cqs[q]->post_completion(e);
+      status.push_back(e.status);
+      queue.push_back(q);
+      didx.push_back(e.descriptor_index);
+      qid.push_back(e.queue_id);
+      segs.push_back(e.segments_produced);
+      vlan.push_back(e.vlan_tag);
+      ver.push_back(e.checksum_verified);
+      posted.push_back(ok);
+    }
+    std::vector<std::uint32_t> bq, bd;
+    for (const auto& [a, d] : ring_log) {
+      bq.push_back(a);
+      bd.push_back(d);
+    }
+    // the consumer polls some of every ring before the next batch
+    std::vector<std::uint32_t> polls(Q);
+    std::ostringstream polled;
+    polled << "[";
+    for (std::size_t q = 0; q < Q; ++q) {
+      polls[q] = static_cast<std::uint32_t>(rng() % 48);
+      polled << (q ? "," : "") << "[";
+      for (std::uint32_t k = 0; k < polls[q]; ++k) {
+        const auto e = cqs[q]->poll_completion();
+        if (!e) break;
+        polled << (k ? "," : "") << entry_json(*e);
+      }
+      polled << "]";
+    }
+    polled << "]";
+    js << (b ? "," : "") << "{\"status\": " << json_arr(status) << ", \"rss_queue\": " << json_arr(queue)
+       << ", \"descriptor_index\": " << json_arr(didx) << ", \"queue_id\": " << json_arr(qid)
+       << ", \"segments\": " << json_arr(segs) << ", \"vlan\": " << json_arr(vlan) << ", \"verified\": " << json_arr(ver)
+       << ", \"posted\": " << json_arr(posted) << ", \"doorbell_queue\": " << json_arr(bq)
+       << ", \"doorbell_data\": " << json_arr(bd) << ", \"polls\": " << json_arr(polls) << ", \"polled\": " << polled.str()
+       << "}";
+  }
+  js << "], \"available_end\": [";
+  for (std::size_t q = 0; q < Q; ++q) js << (q ? "," : "") << cqs[q]->available();
+  js << "], \"drain\": [";
+  for (std::size_t q = 0; q < Q; ++q) {
+    js << (q ? "," : "") << "[";
+    bool first = true;
+    while (auto e = cqs[q]->poll_completion()) {
+      js << (first ? "" : ",") << entry_json(*e);
+      first = false;
+    }
+    js << "]";
+  }
+  js << "]}";
+  std::ofstream(g_out + "/cq_rings.json") << js.str();
+}
+
 int main(int argc, char** argv) {
   if (argc > 1) g_out = argv[1];
   // Sanity: the reference reproduces the Microsoft verification vector.
@@ -1307,6 +1407,11 @@ int main(int argc, char** argv) {
     auto t = tuple12(ip(66, 9, 149, 187), ip(161, 142, 100, 80), 2794, 1766);
     if (e.hash(std::span<const std::uint8_t>(t)) != 0x51ccc178u) { std::fprintf(stderr, "MS vector mismatch\n"); return 1; }
     if (e.hash(std::span<const std::uint8_t>(t.data(), 8)) != 0x323e8fc2u) { std::fprintf(stderr, "MS vector mismatch\n"); return 1; }
+  }
+  if (argc > 2 && std::string(argv[2]) == "cq") {  // only the completion-ring fixture
+    gen_cq();
+    std::printf("cq fixture written to %s\n", g_out.c_str());
+    return 0;
   }
   if (argc > 2 && std::string(argv[2]) == "qm") {  // only the QueueManager fixtures
     gen_qm();
@@ -1322,6 +1427,7 @@ int main(int argc, char** argv) {
   gen_l34();
   gen_tso_vlan();
   gen_qm();
+  gen_cq();
   std::printf("golden fixtures written to %s\n", g_out.c_str());
   return 0;
 }

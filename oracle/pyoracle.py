@@ -188,3 +188,36 @@ def tso_segment(pkt: bytes, hdr_len: int, mss: int, flags: int, stride: int = 92
     if k <= 0:
         return k, [], []
     return k, [out[i * stride: i * stride + int(lens[i])].tobytes() for i in range(k)], [int(c) for c in cs[:k]]
+
+
+class CompletionRing:
+    """nic::CompletionQueue restated (src/completion_queue.cpp:10-53): a ring of
+    `ring_size` entries; post_completion refuses when full (:30-33), stores at
+    the producer index, advances it modulo the ring, counts, and rings the
+    doorbell with (queue_id, producer index after the post) (:34-41);
+    poll_completion returns the entry at the consumer index or None (:45-53)."""
+
+    def __init__(self, ring_size: int, queue_id: int, doorbell=None):
+        self.ring = ring_size
+        self.queue_id = queue_id
+        self.entries = [None] * ring_size
+        self.prod = self.cons = self.count = 0
+        self.doorbell = doorbell
+
+    def post_completion(self, entry) -> bool:
+        if self.count == self.ring:
+            return False
+        self.entries[self.prod] = entry
+        self.prod = (self.prod + 1) % self.ring
+        self.count += 1
+        if self.doorbell is not None:
+            self.doorbell(self.queue_id, self.prod)
+        return True
+
+    def poll_completion(self):
+        if self.count == 0:
+            return None
+        e = self.entries[self.cons]
+        self.cons = (self.cons + 1) % self.ring
+        self.count -= 1
+        return e

@@ -94,6 +94,11 @@ ABI_SYMBOLS = (
     "nicgpu_qp_deliver_range",
     "nicgpu_icrc_batch",
     "nicgpu_tso_segment",
+    "nicgpu_cq_create",
+    "nicgpu_cq_destroy",
+    "nicgpu_cq_post",
+    "nicgpu_cq_state",
+    "nicgpu_cq_poll",
 )
 
 _lib = None
@@ -151,6 +156,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_tso_segment": (i32, [vp, vp, vp, vp, vp, vp, sz, vp, ctypes.c_uint64, u32, vp, vp, vp]),
         "nicgpu_checksum_batch": (i32, [vp, vp, sz, vp, vp]),
         "nicgpu_checksum_batch_split": (i32, [vp, vp, sz, vp, vp, vp]),
+        "nicgpu_cq_create": (i32, [ctypes.POINTER(vp), i32, sz, sz]),
+        "nicgpu_cq_destroy": (i32, [vp]),
+        "nicgpu_cq_post": (i32, [vp, vp, vp, vp, vp, sz, vp]),
+        "nicgpu_cq_state": (i32, [vp, vp, vp]),
+        "nicgpu_cq_poll": (i32, [vp, ctypes.c_uint32, vp, sz, ctypes.POINTER(sz), vp]),
         "nicgpu_stream_create": (i32, [ctypes.POINTER(vp)]),
         "nicgpu_stream_destroy": (i32, [vp]),
         "nicgpu_event_create": (i32, [ctypes.POINTER(vp)]),

@@ -1,0 +1,92 @@
+// rss_rings.cpp — nic::RssCompletionRings (include/nic/rss_rings.h) over the
+// C-ABI's device rings (nicgpu_cq_*, csrc/cq.hip).
+#include "nic/rss_rings.h"
+
+#include <stdexcept>
+#include <string>
+
+#include "nic/gpu_batch.h"
+#include "nicgpu.h"
+
+namespace nic {
+
+namespace {
+void ok(int st, const char* what) {
+  if (st != NICGPU_OK) throw GpuError(std::string("RssCompletionRings: ") + what + ": " + nicgpu_strerror(st), st);
+}
+static_assert(sizeof(CompletionEntry) == sizeof(nicgpu_completion), "CompletionEntry is the C-ABI record");
+}  // namespace
+
+RssCompletionRings::RssCompletionRings(std::size_t queues, std::size_t ring_size, int device)
+    : nq_(queues), ring_(ring_size), device_(device) {
+  ok(nicgpu_cq_create(&cq_, device, queues, ring_size), "nicgpu_cq_create");
+}
+
+RssCompletionRings::~RssCompletionRings() {
+  if (up_rxc_) (void) nicgpu_free(up_rxc_);
+  if (up_which_) (void) nicgpu_free(up_which_);
+  if (cq_) (void) nicgpu_cq_destroy(cq_);
+}
+
+void RssCompletionRings::post(const RxBatchResult& r, void* stream) {
+  if (r.dev.rx_completions && r.dev.queue_which) {  // results in HBM: the device lists
+    const std::size_t nl = r.dev.queue_start.size();
+    if (nl > nq_) throw std::invalid_argument("RssCompletionRings::post: more RSS queues than rings");
+    ok(nicgpu_cq_post(cq_, reinterpret_cast<const nicgpu_completion*>(r.dev.rx_completions), r.dev.queue_which,
+                      r.dev.queue_start.data(), r.dev.queue_end.data(), nl, stream),
+       "nicgpu_cq_post");
+    return;
+  }
+  // host results: the lists and completions go up once
+  const std::size_t nl = r.queues.size();
+  if (nl > nq_) throw std::invalid_argument("RssCompletionRings::post: more RSS queues than rings");
+  std::vector<std::uint32_t> which, start(nl), end(nl);
+  for (std::size_t q = 0; q < nl; ++q) {
+    start[q] = static_cast<std::uint32_t>(which.size());
+    which.insert(which.end(), r.queues[q].begin(), r.queues[q].end());
+    end[q] = static_cast<std::uint32_t>(which.size());
+  }
+  const std::size_t n = r.rx_completions.size();
+  auto grow = [](void*& p, std::size_t& cap, std::size_t bytes) {
+    if (bytes <= cap) return;
+    if (p) (void) nicgpu_free(p);
+    p = nullptr;
+    cap = 0;
+    ok(nicgpu_malloc(&p, bytes), "nicgpu_malloc");
+    cap = bytes;
+  };
+  grow(up_rxc_, cap_rxc_, std::max<std::size_t>(n, 1) * sizeof(CompletionEntry));
+  grow(up_which_, cap_which_, std::max<std::size_t>(which.size(), 1) * sizeof(std::uint32_t));
+  if (n) ok(nicgpu_memcpy_async(up_rxc_, r.rx_completions.data(), n * sizeof(CompletionEntry), stream), "nicgpu_memcpy_async");
+  if (!which.empty())
+    ok(nicgpu_memcpy_async(up_which_, which.data(), which.size() * sizeof(std::uint32_t), stream), "nicgpu_memcpy_async");
+  ok(nicgpu_cq_post(cq_, static_cast<const nicgpu_completion*>(up_rxc_), static_cast<const std::uint32_t*>(up_which_),
+                    start.data(), end.data(), nl, stream),
+     "nicgpu_cq_post");
+}
+
+std::optional<CompletionEntry> RssCompletionRings::poll(std::size_t q) {
+  auto v = poll(q, 1);
+  if (v.empty()) return std::nullopt;
+  return v.front();
+}
+
+std::vector<CompletionEntry> RssCompletionRings::poll(std::size_t q, std::size_t max) {
+  if (q >= nq_) throw std::out_of_range("RssCompletionRings::poll: no such queue");
+  std::vector<CompletionEntry> out(std::min(max, ring_));
+  std::size_t got = 0;
+  ok(nicgpu_cq_poll(cq_, static_cast<std::uint32_t>(q), reinterpret_cast<nicgpu_completion*>(out.data()), out.size(), &got,
+                    nullptr),
+     "nicgpu_cq_poll");
+  out.resize(got);
+  return out;
+}
+
+RssCompletionRings::State RssCompletionRings::state(std::size_t q) const {
+  if (q >= nq_) throw std::out_of_range("RssCompletionRings::state: no such queue");
+  std::vector<std::uint32_t> s(4 * nq_);
+  ok(nicgpu_cq_state(cq_, s.data(), nullptr), "nicgpu_cq_state");
+  return State{s[q], s[nq_ + q], s[2 * nq_ + q], s[3 * nq_ + q]};
+}
+
+}  // namespace nic

@@ -33,6 +33,7 @@
 #include "cpu_backend.h"
 #include "nic/rss.h"
 #include "nic/rx_stage.h"
+#include "nic/rss_rings.h"
 #include "nicgpu.h"
 #include "oracle.h"
 
@@ -853,8 +854,122 @@ int run_edges() {
 
 }  // namespace
 
+// RSS dispatch into per-queue completion rings (nic::RssCompletionRings):
+// two C3 batches of 64 K descriptors with RSS, their Success completions
+// posted into 16 rings of 2048 entries (so the busy queues refuse), 1000
+// entries polled from every ring between the batches, then every ring drained
+// — from the device lists of a batch that kept its results in HBM and from
+// the host lists of the same batch with host results, against
+// nic::CompletionQueue's semantics restated here (src/completion_queue.cpp:30-53).
+int run_rings() {
+  const std::size_t n = 65536, Q = 16, kRing = 2048;
+  Rng r{909};
+  std::vector<std::size_t> lens(n);
+  for (auto& L : lens) {
+    const std::uint32_t k = r.below(12);
+    L = k < 7 ? 64 : (k < 11 ? 576 : 1518);
+  }
+  std::size_t tx_bytes = 0;
+  for (auto L : lens) tx_bytes += (L + 15) & ~std::size_t{15};
+  const std::size_t mem_size = tx_bytes + n * 2048;
+  std::vector<std::uint8_t> image(mem_size, 0);
+  std::vector<TxDescriptor> tx(n);
+  std::size_t at = 0;
+  for (std::size_t i = 0; i < n; ++i) {
+    std::uint8_t* p = image.data() + at;
+    for (std::size_t b = 0; b < lens[i]; ++b) p[b] = r.byte();
+    p[12] = 0x08;
+    p[13] = 0x00;
+    TxDescriptor& t = tx[i];
+    t.buffer_address = at;
+    t.length = static_cast<std::uint32_t>(lens[i]);
+    t.descriptor_index = static_cast<std::uint16_t>(i);
+    t.checksum_offload = true;
+    t.checksum = ChecksumMode::None;
+    at += (lens[i] + 15) & ~std::size_t{15};
+  }
+  std::vector<RxDescriptor> rx(n);
+  for (std::size_t j = 0; j < n; ++j) {
+    rx[j].buffer_address = tx_bytes + j * 2048;
+    rx[j].buffer_length = 2048;
+    rx[j].descriptor_index = static_cast<std::uint16_t>(j);
+    // a few short buffers: BufferTooSmall completions stay out of the rings
+    if (r.below(16) == 0) rx[j].buffer_length = 60;
+  }
+  std::vector<std::uint16_t> table(128);
+  for (int i = 0; i < 128; ++i) table[i] = static_cast<std::uint16_t>(i % Q);
+  RssEngine rss_a{RssConfig{kMsKey, table}}, rss_b{RssConfig{kMsKey, table}};
+  void* d = nullptr;
+  assert(nicgpu_malloc(&d, mem_size + 64) == NICGPU_OK);
+  assert(nicgpu_memcpy_async(d, image.data(), mem_size, nullptr) == NICGPU_OK);
+  const DeviceHostMemory dm{static_cast<std::byte*>(d), mem_size};
+  BatchedQueuePairConfig ca, cb;
+  ca.rss = &rss_a;
+  cb.rss = &rss_b;
+  cb.results_on_device = true;
+  BatchedQueuePair qa{ca}, qb{cb};
+  RssCompletionRings ring_host{Q, kRing}, ring_dev{Q, kRing};
+  // CompletionQueue restated: a ring per queue
+  struct Sim {
+    std::vector<CompletionEntry> e;
+    std::size_t prod = 0, cons = 0, count = 0, refused = 0;
+  };
+  std::vector<Sim> sim(Q);
+  for (auto& x : sim) x.e.resize(kRing);
+  bool ok = true;
+  auto same_entry = [](const CompletionEntry& a, const CompletionEntry& b) { return std::memcmp(&a, &b, sizeof(a)) == 0; };
+  std::size_t posted_total = 0, refused_total = 0;
+  for (int batch = 0; batch < 2 && ok; ++batch) {
+    RxBatchResult ra, rb;
+    qa.process_batch(dm, tx, rx, ra);
+    qb.process_batch(dm, tx, rx, rb);
+    ok = ok && ra.timings.device && rb.timings.device && rb.dev.queue_which != nullptr;
+    // expected: Success completions in posting order into their queue's ring
+    for (std::size_t j = 0; j < ra.rx_completions.size(); ++j) {
+      if (ra.rx_completions[j].status != 0) continue;
+      Sim& x = sim[ra.rx_queue[j]];
+      if (x.count == kRing) {
+        ++x.refused;
+        ++refused_total;
+        continue;
+      }
+      x.e[x.prod] = ra.rx_completions[j];
+      x.prod = (x.prod + 1) % kRing;
+      ++x.count;
+      ++posted_total;
+    }
+    ring_host.post(ra);
+    ring_dev.post(rb);
+    for (std::size_t q = 0; q < Q && ok; ++q) {
+      const auto sh = ring_host.state(q), sd = ring_dev.state(q);
+      ok = sh.producer == sim[q].prod && sh.count == sim[q].count && sh.refused == sim[q].refused &&
+           sd.producer == sh.producer && sd.consumer == sh.consumer && sd.count == sh.count && sd.refused == sh.refused;
+      if (!ok) std::fprintf(stderr, "rings: batch %d queue %zu state differs\n", batch, q);
+    }
+    // the consumer takes 1000 from every ring (all of them after the last batch)
+    for (std::size_t q = 0; q < Q && ok; ++q) {
+      const std::size_t k = batch == 0 ? 1000 : kRing;
+      const auto a = ring_host.poll(q, k), b = ring_dev.poll(q, k);
+      ok = a.size() == b.size() && a.size() == std::min(k, sim[q].count);
+      for (std::size_t i = 0; ok && i < a.size(); ++i) {
+        ok = same_entry(a[i], sim[q].e[(sim[q].cons + i) % kRing]) && same_entry(b[i], a[i]);
+      }
+      if (!ok) std::fprintf(stderr, "rings: batch %d queue %zu polled entries differ\n", batch, q);
+      sim[q].cons = (sim[q].cons + a.size()) % kRing;
+      sim[q].count -= a.size();
+    }
+  }
+  nicgpu_free(d);
+  if (!ok) return 1;
+  std::printf("rx_stage_gpu_fuzz rings: ok (%zu queues x %zu entries, %zu completions posted, %zu refused by full rings; "
+              "device lists and host lists equal the CompletionQueue semantics)\n",
+              Q, kRing, posted_total, refused_total);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   assert(gpu_device_count() >= 1);
+  if (argc > 1 && std::strcmp(argv[1], "rings") == 0) return run_rings();
   if (argc > 1 && std::strcmp(argv[1], "check") == 0) return run_check(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 400);
   if (argc > 1 && std::strcmp(argv[1], "edges") == 0) return run_edges();
   if (argc > 1 && std::strcmp(argv[1], "pipeline") == 0) {

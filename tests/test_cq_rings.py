@@ -1,0 +1,130 @@
+"""RSS dispatch into per-queue completion rings (row f1):
+every Success RX completion posted into the CompletionQueue of its RSS queue,
+as nic::CompletionQueue::post_completion / poll_completion
+(src/completion_queue.cpp:30-53).  Pinned by tests/golden/cq_rings.json,
+written by the compiled reference (oracle/gen_golden.cpp gen_cq: reference
+CompletionQueues with recording doorbells; three batches with skewed queues
+so rings fill and refuse, polls between them, a full drain at the end).
+
+CPU: the oracle restatement (oracle/pyoracle.py CompletionRing) reproduces the
+fixture.  GPU: the device rings (nicgpu_cq_*) reproduce it from the
+completions grouped by queue in posting order, as nicgpu_qp_group leaves them."""
+
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from oracle import pyoracle as po  # noqa: E402
+
+FIX = json.load(open(os.path.join(ROOT, "tests", "golden", "cq_rings.json")))
+COMPL_DT = np.dtype([("queue_id", "<u2"), ("descriptor_index", "<u2"), ("status", "<u4"), ("flags", "u1", 8),
+                     ("segments", "<u2"), ("vlan", "<u2")])
+
+
+def entry(b, j):
+    # the fields the fixture records: queue_id, descriptor_index, status, segments_produced, vlan_tag, checksum_verified
+    return [b["queue_id"][j], b["descriptor_index"][j], b["status"][j], b["segments"][j], b["vlan"][j], b["verified"][j]]
+
+
+def test_oracle_rings_match_reference_fixture():
+    Q, R, base = FIX["queues"], FIX["ring_size"], FIX["cq_queue_id_base"]
+    bells = []
+    rings = [po.CompletionRing(R, base + q, lambda qid, p: bells.append((qid, p))) for q in range(Q)]
+    for b in FIX["batches"]:
+        bells.clear()
+        posted = []
+        for j, st in enumerate(b["status"]):
+            ok = st == 0 and rings[b["rss_queue"][j]].post_completion(entry(b, j))
+            posted.append(int(ok))
+        assert posted == b["posted"]
+        assert [q for q, _ in bells] == b["doorbell_queue"] and [p for _, p in bells] == b["doorbell_data"]
+        for q in range(Q):
+            got = [rings[q].poll_completion() for _ in range(b["polls"][q])]
+            assert [e for e in got if e is not None] == b["polled"][q]
+    assert [r.count for r in rings] == FIX["available_end"]
+    for q in range(Q):
+        drained = []
+        while (e := rings[q].poll_completion()) is not None:
+            drained.append(e)
+        assert drained == FIX["drain"][q]
+
+
+def group_by_queue(b, Q):
+    """Success completions grouped by RSS queue in posting order (nicgpu_qp_group's lists)."""
+    which, start, end = [], [], []
+    for q in range(Q):
+        start.append(len(which))
+        which += [j for j, st in enumerate(b["status"]) if st == 0 and b["rss_queue"][j] == q]
+        end.append(len(which))
+    return np.array(which, np.uint32), np.array(start, np.uint32), np.array(end, np.uint32)
+
+
+@pytest.mark.gpu
+def test_device_rings_match_reference_fixture():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import smart_nic_amd as sna
+
+    lib = sna.load_library()
+    Q, R = FIX["queues"], FIX["ring_size"]
+    h = ctypes.c_void_p()
+    assert lib.nicgpu_cq_create(ctypes.byref(h), 0, Q, R) == 0
+    try:
+        stream = torch.cuda.current_stream().cuda_stream
+        state = np.zeros(4 * Q, np.uint32)
+        for b in FIX["batches"]:
+            n = len(b["status"])
+            rxc = np.zeros(n, COMPL_DT)
+            rxc["queue_id"], rxc["descriptor_index"], rxc["status"] = b["queue_id"], b["descriptor_index"], b["status"]
+            rxc["segments"], rxc["vlan"] = b["segments"], b["vlan"]
+            rxc["flags"][:, 1] = b["verified"]  # checksum_verified: the second flag byte
+            which, start, end = group_by_queue(b, Q)
+            d_rxc = torch.from_numpy(rxc.view(np.uint8)).cuda()
+            d_which = torch.from_numpy(which.view(np.int32) if which.size else np.zeros(1, np.int32)).cuda()
+            assert lib.nicgpu_cq_state(h, state.ctypes.data, stream) == 0
+            prod0, count0 = state[:Q].copy(), state[2 * Q:3 * Q].copy()
+            assert lib.nicgpu_cq_post(h, d_rxc.data_ptr(), d_which.data_ptr(), start.ctypes.data, end.ctypes.data, Q,
+                                      stream) == 0
+            assert lib.nicgpu_cq_state(h, state.ctypes.data, stream) == 0
+            # posted: a completion is taken iff its rank in its queue's list is below the room left
+            posted = np.zeros(n, np.int64)
+            for q in range(Q):
+                room = R - int(count0[q])
+                posted[which[start[q]:end[q]][:room]] = 1
+            assert posted.tolist() == b["posted"]
+            # doorbells: each post rings (queue id, producer after it), in posting order
+            bells = []
+            took = {q: 0 for q in range(Q)}
+            for j in range(n):
+                if posted[j]:
+                    q = b["rss_queue"][j]
+                    took[q] += 1
+                    bells.append((FIX["cq_queue_id_base"] + q, (int(prod0[q]) + took[q]) % R))
+            assert [q for q, _ in bells] == b["doorbell_queue"] and [p for _, p in bells] == b["doorbell_data"]
+            assert state[:Q].tolist() == [(int(prod0[q]) + took[q]) % R for q in range(Q)]
+            for q in range(Q):
+                out = np.zeros(max(b["polls"][q], 1), COMPL_DT)
+                got = ctypes.c_size_t()
+                assert lib.nicgpu_cq_poll(h, q, out.ctypes.data, b["polls"][q], ctypes.byref(got), stream) == 0
+                ents = [[int(e["queue_id"]), int(e["descriptor_index"]), int(e["status"]), int(e["segments"]),
+                         int(e["vlan"]), int(e["flags"][1])] for e in out[:got.value]]
+                assert ents == b["polled"][q]
+        assert lib.nicgpu_cq_state(h, state.ctypes.data, stream) == 0
+        assert state[2 * Q:3 * Q].tolist() == FIX["available_end"]
+        for q in range(Q):
+            out = np.zeros(R, COMPL_DT)
+            got = ctypes.c_size_t()
+            assert lib.nicgpu_cq_poll(h, q, out.ctypes.data, R, ctypes.byref(got), stream) == 0
+            ents = [[int(e["queue_id"]), int(e["descriptor_index"]), int(e["status"]), int(e["segments"]), int(e["vlan"]),
+                     int(e["flags"][1])] for e in out[:got.value]]
+            assert ents == FIX["drain"][q]
+    finally:
+        lib.nicgpu_cq_destroy(h)

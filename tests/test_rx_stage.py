@@ -148,3 +148,17 @@ def test_rx_stage_fuzz_vs_reference_queue_pair():
     run = subprocess.run([exe, "1", "2000"], capture_output=True, text=True, timeout=600)
     assert run.returncode == 0, run.stdout[-2000:] + run.stderr[-2000:]
     assert "rx_stage_fuzz: ok" in run.stdout
+
+
+@pytest.mark.gpu
+def test_rss_completion_rings_gpu(tmp_path):
+    """RSS dispatch into per-queue completion rings (nic::RssCompletionRings,
+    nicgpu_cq_*): two 64 K C3 batches with RSS posted into 16 rings of 2048
+    entries (busy queues refuse), polls between the batches, a full drain —
+    from the device lists of a batch kept in HBM and from the host lists,
+    against nic::CompletionQueue's semantics (completion_queue.cpp:30-53)."""
+    exe = _build(tmp_path, "rx_stage_gpu_fuzz")
+    r = subprocess.run([exe, "rings"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "rx_stage_gpu_fuzz rings: ok" in r.stdout
+    print(r.stdout.strip())
