@@ -3,6 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 PT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
+# the variants live in commit 9e1bbfe (reverted from production); check it out to rerun
 for tv in ${TESTVARS:-xl}; do
   NICGPU_ICRC=$tv timeout -k 10 300 $PT -m gpu -k icrc tests/ > gpurun_out/icrc_${tv}_pytest.log 2>&1
   rc=$?; tail -2 gpurun_out/icrc_${tv}_pytest.log; [ $rc -eq 0 ] || exit $rc

@@ -119,68 +119,10 @@ __device__ __forceinline__ uint32_t b4_dword(const uint8_t* __restrict__ Tb, uin
 // line walk, not the table work, bounds this kernel; 4-chunk windows, a
 // prefetch of the packet's next window, and 32-B windows loaded coalesced and
 // transposed back with ds_bpermute were all slower.
-// Coalesced step loads (XL): a group of 8 lanes loads each member's 128-B
-// line in turn, lane `sub` taking chunk `sub` (one line per group per load
-// instruction, 8 lines per wave instruction, where the lane walk touches 64),
-// and an 8 x 8 transpose of the 16-B chunks inside the group (three DPP
-// butterflies) hands every lane exactly the chunks the lane walk loads itself,
-// so the chain and its results are unchanged.  Butterfly masks 7, 2, 1 (gfx9
-// DPP has row_half_mirror = lane ^ 7 in 8, quad_perm for ^2 and ^1, no ^4):
-// an element sits at (lane i, slot s) and must end at (s, i), so d = i ^ s is
-// invariant and moves once along each basis vector whose coefficient in d is
-// 1 — coefficients of d = a*7 ^ b*2 ^ c*1: a = d2, b = d1 ^ d2, c = d0 ^ d2.
-template <int M>
-__device__ __forceinline__ uint32_t xl_partner(uint32_t v) {
-  constexpr int ctrl = M == 7 ? 0x141 : (M == 2 ? 0x4E : 0xB1);  // row_half_mirror | quad_perm(2,3,0,1) | (1,0,3,2)
-  return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, ctrl, 0xF, 0xF, false);
-}
-template <int M, int S>  // one butterfly on slots S and S ^ M; L: this lane's coefficient along M
-__device__ __forceinline__ void xl_swap(u32x4* x, bool L) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t t = L ? x[S][i] : x[S ^ M][i];
-    const uint32_t r = xl_partner<M>(t);
-    x[S][i] = L ? r : x[S][i];
-    x[S ^ M][i] = L ? x[S ^ M][i] : r;
-  }
-}
-__device__ __forceinline__ void xl_transpose(u32x4* x, uint32_t lane) {
-  const uint32_t i = lane & 7u;
-  const bool La = (i >> 2) & 1u, Lb = ((i >> 1) ^ (i >> 2)) & 1u, Lc = (i ^ (i >> 2)) & 1u;
-  xl_swap<7, 0>(x, La);
-  xl_swap<7, 1>(x, La);
-  xl_swap<7, 2>(x, La);
-  xl_swap<7, 3>(x, La);
-  xl_swap<2, 0>(x, Lb);
-  xl_swap<2, 1>(x, Lb);
-  xl_swap<2, 6>(x, Lb);
-  xl_swap<2, 7>(x, Lb);
-  xl_swap<1, 0>(x, Lc);
-  xl_swap<1, 2>(x, Lc);
-  xl_swap<1, 5>(x, Lc);
-  xl_swap<1, 7>(x, Lc);
-}
-// member k's (lo, hi) in every lane of its 8-lane group: ds_swizzle bit mode,
-// lane' = (lane & 0x18) | k within each 32
-template <int K>
-__device__ __forceinline__ uint32_t xl_bcast(uint32_t v) {
-  return (uint32_t) __builtin_amdgcn_ds_swizzle((int) v, 0x18 | (K << 5));
-}
-template <int K, int CH>  // CH 16: chunks sub and sub + 8 of a 256-B window
-__device__ __forceinline__ void xl_load(u32x4* x, const u32x4* f16, uint32_t lo, uint32_t hi, uint32_t sub) {
-  // unconditional (a member with no step carries a line of the wave's first
-  // stepping lane, nck 0): a predicated load's join would wait for it
-  const uint32_t lk = xl_bcast<K>(lo), hk = xl_bcast<K>(hi);
-  const uint32_t nck = (hk >> 8) & 15u;
-  const uint64_t c = (((uint64_t) (hk & 0xFFu) << 32) | lk);
-  x[K] = f16[c + (sub < nck ? sub : nck)];
-  if constexpr (CH == 16) x[K + 8] = f16[c + (sub + 8u < nck ? sub + 8u : nck)];
-}
-
-template <int CH, int MODE, bool XL = false, int WPB = kIcrcWpb>  // CH: chunks per step, to the end of the packet's aligned CH x 16-B window
-__global__ __launch_bounds__(WPB * kWave) void icrc_b4_kernel(IcrcParams P) {
+template <int CH, int MODE>  // CH: chunks per step, to the end of the packet's aligned CH x 16-B window
+__global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t Tb[kB4Bytes];
-  __shared__ uint64_t ring_all[WPB][kIcrcRing];
+  __shared__ uint64_t ring_all[kIcrcWpb][kIcrcRing];
   __shared__ uint4 lead_m[16];  // bytes >= p of a chunk kept
   __shared__ uint32_t lead_s[16];
   if (threadIdx.x < 16u) {
@@ -188,7 +130,7 @@ __global__ __launch_bounds__(WPB * kWave) void icrc_b4_kernel(IcrcParams P) {
     lead_s[p] = kCrcLead.s[p];
     lead_m[p] = make_uint4(dword_keep(p, 16, 0), dword_keep(p, 16, 1), dword_keep(p, 16, 2), dword_keep(p, 16, 3));
   }
-  for (uint32_t q = threadIdx.x; q < kB4Bytes / 16u; q += WPB * kWave) {
+  for (uint32_t q = threadIdx.x; q < kB4Bytes / 16u; q += kIcrcThreads) {
     const uint32_t o = q * 16u;
     const uint32_t j = 2u * (o >> 16) + ((o >> 7) & 1u), v = (o >> 8) & 255u;
     const uint32_t val = kCrc32c.t[3u - j][v];
@@ -199,8 +141,8 @@ __global__ __launch_bounds__(WPB * kWave) void icrc_b4_kernel(IcrcParams P) {
   const uint32_t cb = (lane & 31u) << 2;  // this lane's copy: bank lane % 32
   const uint32_t cbr = cb | ((cb + 128u) << 8) | (1u << 24);
   uint64_t* ring = ring_all[threadIdx.x / kWave];
-  const uint64_t nwaves = (uint64_t) gridDim.x * WPB;
-  const uint64_t wave = (uint64_t) blockIdx.x * WPB + threadIdx.x / kWave;
+  const uint64_t nwaves = (uint64_t) gridDim.x * kIcrcWpb;
+  const uint64_t wave = (uint64_t) blockIdx.x * kIcrcWpb + threadIdx.x / kWave;
   const uint64_t per = (P.n + nwaves - 1) / nwaves;
   const uint64_t p0 = wave * per < P.n ? wave * per : P.n;
   const uint64_t p1 = p0 + per < P.n ? p0 + per : P.n;
@@ -243,59 +185,7 @@ __global__ __launch_bounds__(WPB * kWave) void icrc_b4_kernel(IcrcParams P) {
   for (;;) {
     const bool active = my < p1;
     if (__ballot(active) == 0ull) break;
-    if constexpr (XL) {
-      static_assert(CH == 8 || CH == 16, "XL moves 128- or 256-B windows");
-      const bool stepping = active && cur < end4;
-      const uint64_t sm = __ballot(stepping);
-      if (sm) {  // the whole wave: swizzles and DPP read every lane of a group
-        uint32_t c0 = 0, cl = 0, lim = 0, lo = 0, hi = 0;
-        if (stepping) {
-          c0 = cur >> 4;
-          const uint32_t clast = (end4 - 1u) >> 4;
-          const uint32_t ce = ((lb + c0) | (uint32_t) (CH - 1)) - lb;
-          cl = ce < clast ? ce : clast;
-          lim = ((cl + 1u) << 4 < end4 ? (cl + 1u) << 4 : end4) - cur;
-          const uint64_t base = c16 + c0;  // chunk index < 2^36
-          lo = (uint32_t) base;
-          hi = (uint32_t) (base >> 32) | ((cl - c0) << 8);
-        }
-        {
-          const int first = __builtin_ctzll(sm);
-          const uint32_t flo = (uint32_t) __builtin_amdgcn_readlane((int) lo, first);
-          const uint32_t fhi = (uint32_t) __builtin_amdgcn_readlane((int) hi, first) & 0xFFu;
-          lo = stepping ? lo : flo;
-          hi = stepping ? hi : fhi;
-        }
-        const uint32_t sub = lane & 7u;
-        u32x4 v[CH];
-        xl_load<0, CH>(v, f16, lo, hi, sub);
-        xl_load<1, CH>(v, f16, lo, hi, sub);
-        xl_load<2, CH>(v, f16, lo, hi, sub);
-        xl_load<3, CH>(v, f16, lo, hi, sub);
-        xl_load<4, CH>(v, f16, lo, hi, sub);
-        xl_load<5, CH>(v, f16, lo, hi, sub);
-        xl_load<6, CH>(v, f16, lo, hi, sub);
-        xl_load<7, CH>(v, f16, lo, hi, sub);
-        xl_transpose(v, lane);
-        if constexpr (CH == 16) xl_transpose(v + 8, lane);
-        if (stepping) {
-          const uint4 m0 = lead_m[c0 == 0u ? pos : 0u];
-          v[0][0] &= m0.x;
-          v[0][1] &= m0.y;
-          v[0][2] &= m0.z;
-          v[0][3] &= m0.w;
-#pragma unroll
-          for (int u = 0; u < CH; ++u) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const uint32_t Sn = MODE == 1 ? S + v[u][i] : b4_dword(Tb, cbr, S ^ v[u][i]);
-              S = (uint32_t) (16 * u + 4 * i) < lim ? Sn : S;
-            }
-          }
-          cur = (cl + 1u) << 4;
-        }
-      }
-    } else if (active && cur < end4) {
+    if (active && cur < end4) {
       // up to the end of the current CH-chunk window; every chunk of the
       // step is processed (predicated on the dword being below lim), so all
       // CH loads issue before the first is used
@@ -603,15 +493,6 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
     if (std::strcmp(e, "b4mem") == 0) return 1;
     if (std::strcmp(e, "b4") == 0) return 0;
     if (std::strcmp(e, "coopmem") == 0) return 3;
-    if (std::strcmp(e, "xl") == 0) return 4;
-    if (std::strcmp(e, "xlmem") == 0) return 5;
-    if (std::strcmp(e, "xl12") == 0) return 6;
-    if (std::strcmp(e, "xl12mem") == 0) return 7;
-    if (std::strcmp(e, "xl16") == 0) return 8;
-    if (std::strcmp(e, "xl16mem") == 0) return 9;
-    if (std::strcmp(e, "xlw12") == 0) return 10;
-    if (std::strcmp(e, "xlw16") == 0) return 11;
-    if (std::strcmp(e, "xlw8") == 0) return 12;
     return 0;
   }();
   const uint64_t want = (n + kIcrcThreads - 1) / kIcrcThreads;
@@ -620,23 +501,6 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (var == 1) hipLaunchKernelGGL((icrc_b4_kernel<8, 1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
   else if (var == 0) hipLaunchKernelGGL((icrc_b4_kernel<8, 0>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
-  else if (var == 4) hipLaunchKernelGGL((icrc_b4_kernel<8, 0, true>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
-  else if (var == 5) hipLaunchKernelGGL((icrc_b4_kernel<8, 1, true>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
-  else if (var == 6 || var == 7) {  // 12 waves per block
-    const uint64_t w12 = (n + 12 * kWave - 1) / (12 * kWave);
-    const unsigned g12 = (unsigned) (w12 < 1 ? 1 : (w12 < (uint64_t) di->cus ? w12 : (uint64_t) di->cus));
-    if (var == 6) hipLaunchKernelGGL((icrc_b4_kernel<8, 0, true, 12>), dim3(g12), dim3(12 * kWave), 0, s, P);
-    else hipLaunchKernelGGL((icrc_b4_kernel<8, 1, true, 12>), dim3(g12), dim3(12 * kWave), 0, s, P);
-  } else if (var >= 8) {  // tuning: 16-wave blocks, 256-B windows
-    const int wpb = var == 10 ? 12 : (var == 12 ? 8 : 16);
-    const uint64_t wn = (n + wpb * kWave - 1) / (wpb * kWave);
-    const unsigned gn = (unsigned) (wn < 1 ? 1 : (wn < (uint64_t) di->cus ? wn : (uint64_t) di->cus));
-    if (var == 8) hipLaunchKernelGGL((icrc_b4_kernel<8, 0, true, 16>), dim3(gn), dim3(16 * kWave), 0, s, P);
-    else if (var == 9) hipLaunchKernelGGL((icrc_b4_kernel<8, 1, true, 16>), dim3(gn), dim3(16 * kWave), 0, s, P);
-    else if (var == 10) hipLaunchKernelGGL((icrc_b4_kernel<16, 0, true, 12>), dim3(gn), dim3(12 * kWave), 0, s, P);
-    else if (var == 11) hipLaunchKernelGGL((icrc_b4_kernel<16, 0, true, 16>), dim3(gn), dim3(16 * kWave), 0, s, P);
-    else hipLaunchKernelGGL((icrc_b4_kernel<16, 0, true, 8>), dim3(gn), dim3(8 * kWave), 0, s, P);
-  }
   else if (var == 3) hipLaunchKernelGGL((icrc_coop_kernel<1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
   else hipLaunchKernelGGL((icrc_coop_kernel<0>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
   return hip_status(hipGetLastError());
