@@ -100,6 +100,11 @@ int nicgpu_stream_synchronize(void* stream);
  * implicit ordering with the null stream), and completion events for ordering
  * one stream after another (copies beside compute). */
 int nicgpu_stream_create(void** stream);
+/* A stream at the device's least (low != 0) or greatest (low == 0) priority
+ * (hipDeviceGetStreamPriorityRange): the batched stage plans the next batch on
+ * a least-priority stream so that its kernels yield wave slots to the
+ * delivery running beside them. */
+int nicgpu_stream_create_priority(void** stream, int low);
 int nicgpu_stream_destroy(void* stream);
 int nicgpu_event_create(void** event);
 int nicgpu_event_destroy(void* event);

@@ -1,6 +1,7 @@
 # f1 batch A/B: the f1 GPU tests on the tree's library, then the C3 1 M
 # HBM-pipelined batch alternating between the tree's libnicgpu.so and the one
-# in ab_old/ (built from the previous commit), same box.
+# in ab_old/ (built from the previous commit; with libnic_host.so too when
+# the host side changed), same box.
 set -o pipefail
 mkdir -p gpurun_out
 PT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"

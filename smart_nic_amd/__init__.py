@@ -55,6 +55,7 @@ ABI_SYMBOLS = (
     "nicgpu_memcpy_async",
     "nicgpu_stream_synchronize",
     "nicgpu_stream_create",
+    "nicgpu_stream_create_priority",
     "nicgpu_stream_destroy",
     "nicgpu_event_create",
     "nicgpu_event_destroy",
@@ -162,6 +163,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_cq_state": (i32, [vp, vp, vp]),
         "nicgpu_cq_poll": (i32, [vp, ctypes.c_uint32, vp, sz, ctypes.POINTER(sz), vp]),
         "nicgpu_stream_create": (i32, [ctypes.POINTER(vp)]),
+        "nicgpu_stream_create_priority": (i32, [ctypes.POINTER(vp), i32]),
         "nicgpu_stream_destroy": (i32, [vp]),
         "nicgpu_event_create": (i32, [ctypes.POINTER(vp)]),
         "nicgpu_event_destroy": (i32, [vp]),

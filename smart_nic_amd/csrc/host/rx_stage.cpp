@@ -1111,7 +1111,7 @@ struct BatchedQueuePair::Scratch {
     release();
     check(nicgpu_stream_create(&side_up), "nicgpu_stream_create");
     check(nicgpu_stream_create(&side_down), "nicgpu_stream_create");
-    check(nicgpu_stream_create(&side_plan), "nicgpu_stream_create");
+    check(nicgpu_stream_create_priority(&side_plan, 1), "nicgpu_stream_create_priority");
     for (Slot& sl : slot) sl.create(dev);
     device = dev;
   }

@@ -146,6 +146,17 @@ int nicgpu_stream_create(void** stream) {
   return st;
 }
 
+int nicgpu_stream_create_priority(void** stream, int low) {
+  if (!stream) return NICGPU_ERR_INVALID;
+  *stream = nullptr;
+  int least = 0, greatest = 0;
+  int st = hip_status(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  hipStream_t s = nullptr;
+  if (st == NICGPU_OK) st = hip_status(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, low ? least : greatest));
+  if (st == NICGPU_OK) *stream = s;
+  return st;
+}
+
 int nicgpu_stream_destroy(void* stream) {
   if (!stream) return NICGPU_ERR_INVALID;
   return hip_status(hipStreamDestroy(static_cast<hipStream_t>(stream)));
