@@ -359,7 +359,7 @@ __device__ __forceinline__ uint32_t seg_copy_stage(uint8_t* out, uint64_t dst, u
       o.y = sh ? __builtin_amdgcn_alignbyte(w2, w1, sh) : w1;
       o.z = sh ? __builtin_amdgcn_alignbyte(w3, w2, sh) : w2;
       o.w = sh ? __builtin_amdgcn_alignbyte(w4, w3, sh) : w3;
-      *reinterpret_cast<u32x4*>(out + D16 + 16ull * j) = o;
+      __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + D16 + 16ull * j));  // nt: as the f1 delivery
       sum = add_halves(o.w, add_halves(o.z, add_halves(o.y, add_halves(o.x, sum))));
     }
   }
