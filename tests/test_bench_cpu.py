@@ -55,7 +55,7 @@ def test_committed_traffic_profiles_name_their_kernel_source():
 
     traffic, info = bench.load_traffic(os.path.join(ROOT, "profiles", "r04c_pmc_c2.json"))
     assert traffic and traffic > 1_600_000_000 and info["profile_kernel_source"]
-    rows = bench.load_rows_traffic(os.path.join(ROOT, "profiles", "r04c_rows_prof.json"))
+    rows = bench.load_rows_traffic(os.path.join(ROOT, "profiles", "r04d_rows_prof.json"))
     assert rows.get("error") is None and rows["profile_kernel_source"]
     for r in ("rx_c2", "rx_c3", "rx_u64", "icrc_c2", "tso_c5", "tso_seg_c5", "f1"):
         assert r in rows["rows"], r
