@@ -53,7 +53,7 @@ def test_committed_traffic_profiles_name_their_kernel_source():
     stale)."""
     import bench
 
-    traffic, info = bench.load_traffic(os.path.join(ROOT, "profiles", "r04c_pmc_c2.json"))
+    traffic, info = bench.load_traffic(os.path.join(ROOT, "profiles", "r04e_pmc_c2.json"))
     assert traffic and traffic > 1_600_000_000 and info["profile_kernel_source"]
     rows = bench.load_rows_traffic(os.path.join(ROOT, "profiles", "r04d_rows_prof.json"))
     assert rows.get("error") is None and rows["profile_kernel_source"]
