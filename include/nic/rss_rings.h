@@ -7,6 +7,11 @@
 // refuses the entry and counts it); poll() is CompletionQueue::poll_completion.
 // A batch whose results stayed in HBM (results_on_device) is posted from its
 // device lists without leaving the device.
+// No doorbell: the reference's post_completion rings Doorbell{queue_id,
+// producer} after every post (completion_queue.cpp:38-39); the device rings do
+// not.  A caller that needs the doorbell sequence derives it from the rings'
+// producers (state()): the last doorbell of a batch on queue q carries
+// state(q).producer.
 #pragma once
 #include <cstddef>
 #include <cstdint>

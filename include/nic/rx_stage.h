@@ -15,9 +15,14 @@
 // It adds RSS dispatch, which the reference lacks: every frame delivered with
 // RX status Success is hashed by an RssEngine and listed under its queue.
 //
-// Host memory is a device-resident image (DeviceHostMemory): host address a
-// is byte a of the image, and the bounds rule of SimpleHostMemory::translate_view
-// (simple_host_memory.cpp:85-93) decides DMA faults.  Descriptors arrive
+// Host memory is either a device-resident image (DeviceHostMemory): host
+// address a is byte a of the image; or the reference's own HostMemory
+// (host_memory.h:49-73; e.g. SimpleHostMemory, simple_host_memory.cpp:16,
+// 70-109): its flat window translate(0, size) is registered with the GPU and
+// mirrored in HBM, each batch stages only the TX bytes it reads up and writes
+// only the bytes it delivers back (see process_batch(HostMemory&, ...)).  In
+// both, the bounds rule of SimpleHostMemory::translate_view
+// (simple_host_memory.cpp:89-96) decides DMA faults.  Descriptors arrive
 // already popped from their rings (DescriptorRing owns ring/doorbell state;
 // the stage starts where pop_descriptor ends).
 //
@@ -44,7 +49,9 @@
 // them.  The results are the sequential reference's in every case.
 //
 // Not modelled: address translators / fault injectors of SimpleHostMemory
-// (only the plain bounds check).
+// (only the plain bounds check).  A HostMemory whose window is not flat (a
+// translator that moves addresses) is refused with GpuError before anything
+// is read or written.
 //
 // Failure: process_batch (or submit / collect) throws nic::GpuError on a HIP
 // failure.  stats() is then unchanged, but the memory image may hold some of
@@ -109,6 +116,50 @@ struct QueuePairStats {
   std::uint64_t rx_vlan_strips{0};
   std::uint64_t rx_checksum_verified{0};
   std::uint64_t rx_gro_aggregated{0};
+};
+}  // namespace nic
+#endif
+
+struct nicgpu_segment_write;  // nicgpu.h
+
+#if __has_include("nic/host_memory.h")
+#include "nic/host_memory.h"  // reference build: its HostMemory interface
+#else
+namespace nic {
+// Same declarations, in the same order (so the same vtable layout), as
+// include/nic/host_memory.h:9-73: a reference HostMemory (SimpleHostMemory)
+// compiled against that header is passed to this library as it is.
+using HostAddress = std::uint64_t;
+struct HostMemoryConfig {
+  std::size_t size_bytes{0};
+  std::size_t page_size{4096};
+  bool iommu_enabled{false};
+};
+enum class HostMemoryError : std::uint8_t { None, OutOfBounds, IommuFault, FaultInjected };
+struct HostMemoryResult {
+  HostMemoryError error{HostMemoryError::None};
+  std::size_t bytes_processed{0};
+  [[nodiscard]] bool ok() const noexcept { return error == HostMemoryError::None; }
+};
+struct HostMemoryView {
+  std::byte* data{nullptr};
+  std::size_t length{0};
+  HostAddress address{0};
+};
+struct ConstHostMemoryView {
+  const std::byte* data{nullptr};
+  std::size_t length{0};
+  HostAddress address{0};
+};
+class HostMemory {
+public:
+  virtual ~HostMemory() = default;
+  [[nodiscard]] virtual HostMemoryConfig config() const noexcept = 0;
+  [[nodiscard]] virtual HostMemoryResult translate(HostAddress address, std::size_t length, HostMemoryView& view) = 0;
+  [[nodiscard]] virtual HostMemoryResult translate_const(HostAddress address, std::size_t length,
+                                                         ConstHostMemoryView& view) const = 0;
+  [[nodiscard]] virtual HostMemoryResult read(HostAddress address, std::span<std::byte> buffer) const = 0;
+  [[nodiscard]] virtual HostMemoryResult write(HostAddress address, std::span<const std::byte> data) = 0;
 };
 }  // namespace nic
 #endif
@@ -213,8 +264,15 @@ struct RxBatchResult {
     double copy_us{0};   // device resolve: descriptors up, completions down
     bool device{false};     // resolved on the device
     bool host_tail{false};  // ... and the rest on the host (positions not settled in 8 relaxation steps)
+    bool host_image{false};  // run against a HostMemory: TX bytes staged up, delivered bytes written back
+    bool staged_whole{false};  // ... the TX bytes' span went up in one copy (dense), else per descriptor
+    unsigned replans{0};    // device plans redone because the first outgrew the piece buffers (at most 1)
   } timings;
 };
+
+namespace rx_stage_detail {
+struct SegmentWrite;
+}
 
 /// QueuePair::process_once over a batch (src/queue_pair.cpp:67-460).
 class BatchedQueuePair {
@@ -259,6 +317,35 @@ public:
   void process_batch(const DeviceHostMemory& mem, const DeviceDescriptors& d, RxBatchResult& out,
                      void* stream = nullptr);
   void submit(const DeviceHostMemory& mem, const DeviceDescriptors& d, void* stream = nullptr);
+
+  /// The same batch against the reference's HostMemory (host_memory.h:49-73),
+  /// which is where QueuePair's DMAEngine reads and writes (dma_engine.cpp:12-32;
+  /// queue_pair.cpp:86-92 reads each TX buffer, :416-426 writes each segment).
+  /// The memory's window translate(0, config().size_bytes) must be flat and
+  /// 16-B aligned (SimpleHostMemory without an address translator or fault
+  /// injector: its std::vector, simple_host_memory.cpp:16); GpuError
+  /// (NICGPU_ERR_INVALID) otherwise, before anything is read or written.  The
+  /// window is page-locked once (hipHostRegister, unregistered when the stage
+  /// binds another memory or is destroyed) and mirrored in HBM.  Per batch only
+  /// the TX buffers' bytes go up (one copy of their span when it is dense,
+  /// otherwise a gather of each buffer), the stage runs on the mirror, and
+  /// exactly the bytes its DMA writes deliver are written back into the
+  /// memory (a GPU kernel storing through the registered window); no other
+  /// byte of the memory is touched.  Results, statistics, interrupts and the
+  /// memory's bytes equal those of the reference QueuePair on the same memory.
+  /// The memory must not be written by anyone else while a batch is pending.
+  void process_batch(HostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+                     RxBatchResult& out, void* stream = nullptr);
+  RxBatchResult process_batch(HostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+                              void* stream = nullptr);
+  /// Pipelined: batch k's bytes are written back while batch k+1 is resolved
+  /// and batch k+2's TX bytes go up; a batch that reads (or delivers into)
+  /// bytes an earlier pending batch delivers into is ordered after that
+  /// batch's write-back.  collect() returns once the batch's bytes are in the
+  /// memory.  Mixing HostMemory and DeviceHostMemory batches in flight is not
+  /// supported (std::logic_error).
+  void submit(HostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+              void* stream = nullptr);
   [[nodiscard]] std::size_t pending() const noexcept;
 
   [[nodiscard]] const QueuePairStats& stats() const noexcept { return stats_; }
@@ -267,6 +354,7 @@ public:
 
   struct Scratch;  // device, pinned and host buffers reused across batches (grown, never shrunk)
   struct Slot;     // one batch in flight on the device: its context, events and landing buffers
+  struct HostImage;  // a registered HostMemory window and its HBM mirror
 
 private:
   // Device resolve of one batch in four steps: upload() sends the descriptors
@@ -278,19 +366,31 @@ private:
   void upload(Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx, bool rx_beside);
   bool front(Slot& sl, const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
              QueuePairStats& stats, RxBatchResult& out, void* stream, int& disjoint, double& check_us);
+  bool front_once(Slot& sl, const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
+                  std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out, void* stream,
+                  int& disjoint, double& check_us, int& again);
+  // host-image batches (process_batch / submit with a HostMemory)
+  HostImage& bind_image(HostMemory& mem);
+  void image_prepare(Slot& sl, HostImage& img, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx);
+  void image_host_path(Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+                       QueuePairStats& stats, RxBatchResult& out, void* stream, int disjoint, double& check_us);
+  void image_stage(Slot& sl, std::span<const TxDescriptor> tx, const void* tx_dev, void* stream);
+  void image_writeback(Slot& sl, const nicgpu_segment_write* writes_dev, std::size_t n, void* stream);
   void back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult& out, void* stream);
   void deliver(Slot& sl, const DeviceHostMemory& mem, std::size_t a, std::size_t b, unsigned flags,
                const nicgpu_rss_ctx* rctx, std::uint64_t* hits, void* stream);
   void finish(Slot& sl, RxBatchResult& out);
   void enqueue(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
-               const DeviceDescriptors* d, void* stream);
+               const DeviceDescriptors* d, void* stream, HostImage* img = nullptr);
   void check_rings_unwritten(Slot& sl, const DeviceHostMemory& mem, void* stream);
   void fire_interrupts(const RxBatchResult& r);  // config_.on_interrupt over r's completions
   std::pair<std::span<const TxDescriptor>, std::span<const RxDescriptor>> host_spans(
       Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx, void* stream);
   // the host path (buffers_disjoint unless `disjoint` is known, then run_batch)
+  // (applied: every DMA write made is appended — a host-image batch writes them back)
   void on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
-               QueuePairStats& stats, RxBatchResult& out, void* stream, int disjoint, double& check_us);
+               QueuePairStats& stats, RxBatchResult& out, void* stream, int disjoint, double& check_us,
+               std::vector<rx_stage_detail::SegmentWrite>* applied = nullptr);
   BatchedQueuePairConfig config_;
   BatchedQueuePairConfig quiet_;  // config_ without the interrupt callback (every resolve; replayed after)
   QueuePairStats stats_{};

@@ -38,7 +38,12 @@
 extern "C" {
 #endif
 
-#define NICGPU_ABI_VERSION 1
+/* 2: nicgpu_qp_view gained piece_cs4 (split piece sums: piece_csum covers each
+ *    piece past its first 4 bytes) and the plans of nicgpu_qp_plan* are split
+ *    (one piece per plain packet); host-image staging (nicgpu_host_register,
+ *    nicgpu_image_*, nicgpu_qp_writeback) added.  A caller built against 1
+ *    must not use this library: check nicgpu_abi_version() first. */
+#define NICGPU_ABI_VERSION 2
 
 #define NICGPU_OK 0
 #define NICGPU_ERR_INVALID (-1)    /* bad argument (null ctx, bad mode, size limits) */
@@ -373,8 +378,11 @@ int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int
  * nicgpu_qp_reserve returns the context to its own arrays. */
 int nicgpu_qp_bind(nicgpu_qp* q, const nicgpu_tx_descriptor* tx, size_t ntx, const nicgpu_rx_descriptor* rx,
                    size_t nrx, nicgpu_qp_view* view);
-/* The plan (qp_logic.h plan_packet) of view.tx[0, ntx) and the checksum of
- * every piece over the image mem[0, mem_size): *npieces on return
+/* The plan (qp_logic.h plan_packet, split form: one piece per plain packet below
+ * 64 KiB, PacketPlan kPlainSplit) of view.tx[0, ntx) and the split checksums
+ * of every piece over the image mem[0, mem_size) — view.piece_csum holds each
+ * piece's bytes past its first 4, view.piece_cs4 its first min(4, len) bytes;
+ * neither is compute_checksum of the whole piece: *npieces on return
  * (NICGPU_ERR_RANGE, nothing enqueued after the count, when a descriptor plans
  * more than 256 pieces: the total may then not fit 32 bits).  Waits for
  * `stream` once (the piece count sizes the piece buffers); the piece
@@ -469,6 +477,35 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
                             unsigned flags, const nicgpu_rss_ctx* ctx, int tuple_mode, uint32_t raw_off,
                             uint32_t raw_len, uint64_t* hits_dev, void* stream);
 
+/* ---- Host-image staging (row f1 on the reference's HostMemory) ----
+ * nic::BatchedQueuePair::process_batch(HostMemory&, ...) runs the stage on an
+ * HBM mirror of the memory's flat window (SimpleHostMemory's std::vector,
+ * src/simple_host_memory.cpp:16, 70-109): the TX buffers' bytes go up before a
+ * batch (QueuePair's DMA read, queue_pair.cpp:86-92) and exactly the bytes its
+ * DMA writes delivered come back (queue_pair.cpp:416-426). */
+/* Waits for the event's last record on the calling thread. */
+int nicgpu_event_synchronize(void* event);
+/* Page-locks host memory [host_ptr, host_ptr + bytes) (whole pages around it)
+ * and maps it for the device: *dev_alias = the device-visible address of
+ * host_ptr.  *owned = 1 when this call registered it (unregister it later),
+ * 0 when it was registered already (by the caller or hipHostMalloc). */
+int nicgpu_host_register(void* host_ptr, size_t bytes, void** dev_alias, int* owned);
+int nicgpu_host_unregister(void* host_ptr);
+/* image[a, a + len) <- host[a, a + len) for every TX descriptor tx[0, ntx)
+ * (device array) whose buffer is inside mem_size (a = buffer_address, len =
+ * length): byte-exact, no byte outside the buffers is written.  host is a
+ * device-visible alias (nicgpu_host_register) with 16-B alignment; image and
+ * host both hold mem_size bytes (readable up to the next 16-B boundary). */
+int nicgpu_image_stage(uint8_t* image, const uint8_t* host, uint64_t mem_size, const nicgpu_tx_descriptor* tx,
+                       size_t ntx, void* stream);
+/* host[d, d + len) <- image[d, d + len) for every write w of writes[0, n)
+ * (device array; d = w.dst, len = w.prefix_len + w.len_a + w.len_b, skipped
+ * when empty or outside mem_size): the bytes nicgpu_segment_gather /
+ * nicgpu_qp_deliver wrote, written back byte-exact (no other host byte is
+ * stored to).  Same alignment rules as nicgpu_image_stage. */
+int nicgpu_image_writeback(const uint8_t* image, uint8_t* host, uint64_t mem_size, const nicgpu_segment_write* writes,
+                           size_t n, void* stream);
+
 /* ---- RSS dispatch into per-queue completion rings (row f1) ----
  * nq rings of ring_size entries on one device, one nic::CompletionQueue each
  * (src/completion_queue.cpp:30-53; replaces its post_completion /
@@ -482,7 +519,9 @@ int nicgpu_cq_destroy(nicgpu_cq_set* cq);
  * rxc[which[start[q] .. end[q])] into ring q in that order, as
  * CompletionQueue::post_completion would one by one: entry i of the list
  * lands at (producer + i) % ring_size while the ring has room, the rest are
- * refused (counted).  start / end are host arrays (nicgpu_qp_group's lists,
+ * refused (counted).  No doorbell is rung (the reference rings
+ * Doorbell{queue_id, producer} per post, completion_queue.cpp:38-39): the
+ * producer nicgpu_cq_state reports is what the last one would carry.  start / end are host arrays (nicgpu_qp_group's lists,
  * RxBatchResult::dev.queue_start / queue_end), rxc and which device arrays.
  * Synchronises `stream`. */
 int nicgpu_cq_post(nicgpu_cq_set* cq, const nicgpu_completion* rxc, const uint32_t* which, const uint32_t* start,

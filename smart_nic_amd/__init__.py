@@ -39,6 +39,7 @@ L34_UDP_NOCSUM = 0x10
 RAW_MAX_END = 64
 MAX_PACKET = 65535
 DESC_OFFSET_BITS = 40
+ABI_VERSION = 2  # include/nicgpu.h NICGPU_ABI_VERSION
 
 # Every symbol include/nicgpu.h declares (tests check the library exports them).
 ABI_SYMBOLS = (
@@ -100,6 +101,11 @@ ABI_SYMBOLS = (
     "nicgpu_cq_post",
     "nicgpu_cq_state",
     "nicgpu_cq_poll",
+    "nicgpu_event_synchronize",
+    "nicgpu_host_register",
+    "nicgpu_host_unregister",
+    "nicgpu_image_stage",
+    "nicgpu_image_writeback",
 )
 
 _lib = None
@@ -170,11 +176,18 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_event_record": (i32, [vp, vp]),
         "nicgpu_stream_wait_event": (i32, [vp, vp]),
         "nicgpu_tso_checksum": (i32, [vp, vp, vp, vp, vp, sz, vp, vp]),
+        "nicgpu_event_synchronize": (i32, [vp]),
+        "nicgpu_host_register": (i32, [vp, sz, ctypes.POINTER(vp), ctypes.POINTER(i32)]),
+        "nicgpu_host_unregister": (i32, [vp]),
+        "nicgpu_image_stage": (i32, [vp, vp, ctypes.c_uint64, vp, sz, vp]),
+        "nicgpu_image_writeback": (i32, [vp, vp, ctypes.c_uint64, vp, sz, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.nicgpu_abi_version() != ABI_VERSION:
+        raise NicGpuError(f"{path}: ABI version {lib.nicgpu_abi_version()}, this package needs {ABI_VERSION}")
     _lib = lib
     return lib
 

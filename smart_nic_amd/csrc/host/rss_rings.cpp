@@ -15,6 +15,20 @@ void ok(int st, const char* what) {
   if (st != NICGPU_OK) throw GpuError(std::string("RssCompletionRings: ") + what + ": " + nicgpu_strerror(st), st);
 }
 static_assert(sizeof(CompletionEntry) == sizeof(nicgpu_completion), "CompletionEntry is the C-ABI record");
+
+// The rings' device current for a scope (the staging buffers of post() live
+// on it, whatever device the calling thread has selected).
+struct OnDevice {
+  int prev = -1;
+  explicit OnDevice(int dev) {
+    ok(nicgpu_get_device(&prev), "nicgpu_get_device");
+    if (prev != dev) ok(nicgpu_set_device(dev), "nicgpu_set_device");
+  }
+  ~OnDevice() {
+    int cur = -1;
+    if (prev >= 0 && nicgpu_get_device(&cur) == NICGPU_OK && cur != prev) (void) nicgpu_set_device(prev);
+  }
+};
 }  // namespace
 
 RssCompletionRings::RssCompletionRings(std::size_t queues, std::size_t ring_size, int device)
@@ -23,8 +37,12 @@ RssCompletionRings::RssCompletionRings(std::size_t queues, std::size_t ring_size
 }
 
 RssCompletionRings::~RssCompletionRings() {
+  int prev = -1;
+  const bool switched = (up_rxc_ || up_which_) && nicgpu_get_device(&prev) == NICGPU_OK && prev != device_ &&
+                        nicgpu_set_device(device_) == NICGPU_OK;
   if (up_rxc_) (void) nicgpu_free(up_rxc_);
   if (up_which_) (void) nicgpu_free(up_which_);
+  if (switched) (void) nicgpu_set_device(prev);
   if (cq_) (void) nicgpu_cq_destroy(cq_);
 }
 
@@ -37,7 +55,9 @@ void RssCompletionRings::post(const RxBatchResult& r, void* stream) {
        "nicgpu_cq_post");
     return;
   }
-  // host results: the lists and completions go up once
+  // host results: the lists and completions go up once, into staging buffers
+  // on the rings' device
+  const OnDevice on(device_);
   const std::size_t nl = r.queues.size();
   if (nl > nq_) throw std::invalid_argument("RssCompletionRings::post: more RSS queues than rings");
   std::vector<std::uint32_t> which, start(nl), end(nl);

@@ -1053,6 +1053,18 @@ struct BatchedQueuePair::Slot {
   bool on_device = false;
   std::promise<void> job_done;
   std::future<void> job;
+  // host-image batch (HostMemory): the TX bytes' span / the RX buffers' box in
+  // the memory, the earlier pending batches whose write-back the stage-in
+  // (dep_stage) or the delivery (dep_rx) must follow, and the writes a
+  // host-path batch made (written back from the device copy in wbuf)
+  HostImage* image = nullptr;
+  void* ev_staged = nullptr;  // the batch's TX bytes are in the mirror
+  void* ev_wb = nullptr;      // its delivered bytes are back in the host memory
+  bool staged = false, stage_deferred = false, wb = false, whole = false;
+  std::uint64_t tx_lo = 0, tx_hi = 0, tx_bytes = 0, rx_lo = 0, rx_hi = 0;
+  std::vector<Slot*> dep_stage, dep_rx;
+  std::vector<rx_stage_detail::SegmentWrite> applied;
+  DevBuf wbuf, stage_tx;
 
   void release_rss() {
     if (!rss_released) rss_recorded.set_value();
@@ -1068,17 +1080,48 @@ struct BatchedQueuePair::Slot {
     wait();
     up.reset();
     if (qp) (void) nicgpu_qp_destroy(qp);
-    for (void* e : {ev_tx, ev_rx, ev_resolved, ev_done, ev_submit})
+    if (wb) (void) nicgpu_event_synchronize(ev_wb);  // no write-back may outlive the slot's buffers
+    wb = false;
+    for (void* e : {ev_tx, ev_rx, ev_resolved, ev_done, ev_submit, ev_staged, ev_wb})
       if (e) (void) nicgpu_event_destroy(e);
     qp = nullptr;
-    ev_tx = ev_rx = ev_resolved = ev_done = ev_submit = nullptr;
+    ev_tx = ev_rx = ev_resolved = ev_done = ev_submit = ev_staged = ev_wb = nullptr;
   }
   void create(int dev) {
     check(nicgpu_qp_create(&qp, dev), "nicgpu_qp_create");
-    for (void** e : {&ev_tx, &ev_rx, &ev_resolved, &ev_done, &ev_submit})
+    for (void** e : {&ev_tx, &ev_rx, &ev_resolved, &ev_done, &ev_submit, &ev_staged, &ev_wb})
       check(nicgpu_event_create(e), "nicgpu_event_create");
   }
+  // the batch's bytes are in the host memory (host-image batches)
+  void wait_writeback() {
+    if (!wb) return;
+    wb = false;
+    check(nicgpu_event_synchronize(ev_wb), "nicgpu_event_synchronize");
+  }
   ~Slot() { release(); }
+};
+
+// A HostMemory's flat window, page-locked and mapped for the device, and its
+// mirror in HBM (the image every kernel of the stage works on).
+struct BatchedQueuePair::HostImage {
+  HostMemory* mem = nullptr;
+  std::byte* host = nullptr;      // translate(0, size).data
+  std::uint8_t* alias = nullptr;  // its device-visible address (nicgpu_host_register)
+  bool owned = false;             // registered by this stage
+  std::size_t size = 0;
+  int device = -1;
+  DevBuf mirror;
+  DeviceHostMemory view() const { return DeviceHostMemory{static_cast<std::byte*>(mirror.p), size}; }
+  void release() {
+    if (owned && host) (void) nicgpu_host_unregister(host);
+    mem = nullptr;
+    host = nullptr;
+    alias = nullptr;
+    owned = false;
+    size = 0;
+    device = -1;
+  }
+  ~HostImage() { release(); }
 };
 
 struct BatchedQueuePair::Scratch {
@@ -1093,6 +1136,8 @@ struct BatchedQueuePair::Scratch {
   void* side_up = nullptr;
   void* side_down = nullptr;
   void* side_plan = nullptr;  // plan and overlap check of a batch beside the earlier batch's writes
+  void* side_wb = nullptr;    // host-image write-backs, beside the next batches' work
+  HostImage img;              // the HostMemory the host-image batches run against
   SideWorker up_worker;  // process_batch: issues the RX descriptor uploads
   static constexpr unsigned kSlots = 3;
   Slot slot[kSlots];
@@ -1103,7 +1148,9 @@ struct BatchedQueuePair::Scratch {
     if (side_up) (void) nicgpu_stream_destroy(side_up);
     if (side_down) (void) nicgpu_stream_destroy(side_down);
     if (side_plan) (void) nicgpu_stream_destroy(side_plan);
-    side_up = side_down = side_plan = nullptr;
+    if (side_wb) (void) nicgpu_stream_destroy(side_wb);
+    side_up = side_down = side_plan = side_wb = nullptr;
+    img.release();
     device = -1;
   }
   void ensure(int dev) {
@@ -1112,6 +1159,7 @@ struct BatchedQueuePair::Scratch {
     check(nicgpu_stream_create(&side_up), "nicgpu_stream_create");
     check(nicgpu_stream_create(&side_down), "nicgpu_stream_create");
     check(nicgpu_stream_create_priority(&side_plan, 1), "nicgpu_stream_create_priority");
+    check(nicgpu_stream_create(&side_wb), "nicgpu_stream_create");
     for (Slot& sl : slot) sl.create(dev);
     device = dev;
   }
@@ -1158,8 +1206,8 @@ namespace {
 class GpuBackend final : public rx_stage_detail::Backend {
 public:
   GpuBackend(BatchedQueuePair::Scratch& s, const DeviceHostMemory& mem, const BatchedQueuePairConfig& config,
-             void* stream)
-      : S(s), mem_(mem), config_(config), stream_(stream) {}
+             void* stream, std::vector<rx_stage_detail::SegmentWrite>* applied = nullptr)
+      : S(s), mem_(mem), config_(config), stream_(stream), applied_(applied) {}
 
   std::span<const std::uint16_t> piece_sums(std::span<const rx_stage_detail::Piece> pieces) override {
     const std::size_t np = pieces.size();
@@ -1190,6 +1238,9 @@ public:
     const std::size_t nw = writes.size();
     if (nw == 0) return;
     if (from_copy && !have_copy_) throw GpuError("process_batch: gather from a copy that was never taken", NICGPU_ERR_INVALID);
+    if (applied_)
+      for (const auto& w : writes)
+        if (rx_stage_detail::write_len(w)) applied_->push_back(w);
     auto* hw = S.h_writes.get<rx_stage_detail::SegmentWrite>(nw);
     std::memcpy(hw, writes.data(), nw * sizeof(rx_stage_detail::SegmentWrite));
     void* d_w = S.writes.get(nw * sizeof(rx_stage_detail::SegmentWrite));
@@ -1225,6 +1276,7 @@ private:
   const DeviceHostMemory& mem_;
   const BatchedQueuePairConfig& config_;
   void* stream_;
+  std::vector<rx_stage_detail::SegmentWrite>* applied_;
   bool have_copy_ = false;
 };
 
@@ -1287,6 +1339,10 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
     Slot& sl = scratch_->slot[0];
     sl.tx_dev = nullptr;
     sl.rx_dev = nullptr;
+    sl.image = nullptr;
+    sl.staged = false;
+    sl.dep_stage.clear();
+    sl.dep_rx.clear();
     upload(sl, tx, rx, true);
     on_device = front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);
     if (on_device) {
@@ -1302,7 +1358,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
 
 void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out, void* stream,
-                               int disjoint, double& check_us) {
+                               int disjoint, double& check_us, std::vector<rx_stage_detail::SegmentWrite>* applied) {
   using clock = std::chrono::steady_clock;
   out.dev = RxBatchResult::DeviceResults{};
   if (disjoint < 0) {
@@ -1310,7 +1366,7 @@ void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDe
     disjoint = rx_stage_detail::buffers_disjoint(mem.size, tx, rx) ? 1 : 0;
     check_us += std::chrono::duration<double, std::micro>(clock::now() - t0).count();
   }
-  GpuBackend dev{*scratch_, mem, config_, stream};
+  GpuBackend dev{*scratch_, mem, config_, stream, applied};
   rx_stage_detail::run_batch(quiet_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint);
 }
 
@@ -1328,6 +1384,10 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDe
   sl.ntx_dev = d.ntx;
   sl.nrx_dev = d.nrx;
   sl.fetched = false;
+  sl.image = nullptr;
+  sl.staged = false;
+  sl.dep_stage.clear();
+  sl.dep_rx.clear();
   check(nicgpu_event_record(sl.ev_submit, stream), "nicgpu_event_record");  // a producer's writes before this call
   QueuePairStats st = stats_;
   int disjoint = -1;
@@ -1411,7 +1471,8 @@ void BatchedQueuePair::submit(const DeviceHostMemory& mem, const DeviceDescripto
 }
 
 void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
-                               std::span<const RxDescriptor> rx, const DeviceDescriptors* d, void* stream) {
+                               std::span<const RxDescriptor> rx, const DeviceDescriptors* d, void* stream,
+                               HostImage* img) {
   if (mem.base == nullptr && mem.size != 0) throw GpuError("submit: null host-memory image", NICGPU_ERR_INVALID);
   Scratch& S = *scratch_;
   if (S.pending == Scratch::kSlots) throw std::logic_error("submit: three batches pending; collect() one first");
@@ -1419,7 +1480,15 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
   check(nicgpu_get_device(&dev), "nicgpu_get_device");
   if (S.pending == 0) S.ensure(dev);
   else if (S.device != dev) throw std::logic_error("submit: batches pending on another device");
+  for (unsigned k = 0; k < S.pending; ++k)
+    if (S.slot[(S.head + k) % Scratch::kSlots].image != img)
+      throw std::logic_error("submit: HostMemory and DeviceHostMemory batches (or two memories) pending together");
   Slot& sl = S.slot[(S.head + S.pending) % Scratch::kSlots];
+  sl.image = nullptr;
+  sl.staged = false;
+  sl.dep_stage.clear();
+  sl.dep_rx.clear();
+  if (img) image_prepare(sl, *img, tx, rx);  // dependencies on the batches pending now
   sl.stats = QueuePairStats{};
   sl.on_device = false;
   sl.mem = mem;
@@ -1437,6 +1506,11 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
   // the rest runs in submission order on the job thread
   if (device && !d) upload(sl, tx, rx, false);
   if (device && d) check(nicgpu_event_record(sl.ev_submit, stream), "nicgpu_event_record");
+  // a host-image batch's TX bytes go up now, beside the earlier batches' work,
+  // unless they overlap bytes an earlier pending batch delivers: then its job
+  // stages them after that batch's write-back (recorded by the earlier job)
+  sl.stage_deferred = img && !sl.dep_stage.empty();
+  if (img && !sl.stage_deferred) image_stage(sl, tx, device ? sl.v.tx : nullptr, S.side_up);
   sl.job_done = std::promise<void>();
   sl.job = sl.job_done.get_future();
   auto run = [this, &sl, device, dev] {
@@ -1444,11 +1518,18 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
       check(nicgpu_set_device(dev), "nicgpu_set_device");  // the HIP device is per thread
       int disjoint = -1;
       double check_us = 0;
+      if (sl.stage_deferred) {
+        for (Slot* p : sl.dep_stage)
+          check(nicgpu_stream_wait_event(scratch_->side_up, p->ev_wb), "nicgpu_stream_wait_event");
+        image_stage(sl, sl.tx, device ? sl.v.tx : nullptr, scratch_->side_up);
+      }
       if (device) {
         sl.on_device = front(sl, sl.mem, sl.tx, sl.rx, sl.stats, sl.result, sl.stream, disjoint, check_us);
         if (sl.on_device) back(sl, sl.mem, sl.result, sl.stream);
       }
-      if (!sl.on_device) {
+      if (!sl.on_device && sl.image) {
+        image_host_path(sl, sl.tx, sl.rx, sl.stats, sl.result, sl.stream, disjoint, check_us);
+      } else if (!sl.on_device) {
         check_rings_unwritten(sl, sl.mem, sl.stream);
         const auto [htx, hrx] = host_spans(sl, sl.tx, sl.rx, sl.stream);
         on_host(sl.mem, htx, hrx, sl.stats, sl.result, sl.stream, disjoint, check_us);
@@ -1470,8 +1551,17 @@ bool BatchedQueuePair::collect(RxBatchResult& out) {
   // the slot is free again whatever the batch throws
   S.head = (S.head + 1) % Scratch::kSlots;
   --S.pending;
-  sl.job.get();  // the job's exception, if any
+  try {
+    sl.job.get();  // the job's exception, if any
+  } catch (...) {
+    try {
+      sl.wait_writeback();
+    } catch (...) {
+    }
+    throw;
+  }
   if (sl.on_device) finish(sl, sl.result);
+  else sl.wait_writeback();  // a host-path batch of a HostMemory: its bytes are back
   rx_stage_detail::add_stats(stats_, sl.stats);
   std::swap(out, sl.result);
   if (config_.on_interrupt) fire_interrupts(out);
@@ -1535,9 +1625,27 @@ void BatchedQueuePair::upload(Slot& sl, std::span<const TxDescriptor> tx, std::s
 // descriptor whose RX side ends it early (or where the ring runs short)
 // resolved here in order.  The host moves descriptors up; back() and finish()
 // do the rest.
+// A plan that outgrew the piece buffers (NICGPU_ERR_AGAIN: nothing resolved,
+// settled or written) is redone once with the buffers it asked for; a second
+// AGAIN would mean the sizing is broken, and is an error.
 bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                              std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out, void* stream,
                              int& disjoint, double& check_us) {
+  for (int attempt = 0;; ++attempt) {
+    int again = 0;
+    const bool r = front_once(sl, mem, tx, rx, st, out, stream, disjoint, check_us, again);
+    if (!again) {
+      out.timings.replans = static_cast<unsigned>(attempt);
+      return r;
+    }
+    if (attempt >= 1)
+      throw GpuError("process_batch: the device plan outgrew its piece buffers twice", NICGPU_ERR_AGAIN);
+  }
+}
+
+bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
+                                  std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out,
+                                  void* stream, int& disjoint, double& check_us, int& again) {
   using namespace rx_stage_detail;
   using clock = std::chrono::steady_clock;
   auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
@@ -1581,8 +1689,13 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
     }
   } else {
     out.timings.copy_us += sl.upload_us;
+    sl.upload_us = 0;  // counted once, also when the plan is redone
     check(nicgpu_stream_wait_event(ps, sl.ev_tx), "nicgpu_stream_wait_event");
   }
+  // a host-image batch: the piece sums read the TX bytes staged into the mirror
+  out.timings.host_image = sl.image != nullptr;
+  out.timings.staged_whole = sl.image != nullptr && sl.whole;
+  if (sl.staged) check(nicgpu_stream_wait_event(stream, sl.ev_staged), "nicgpu_stream_wait_event");
   // the plan and the piece sums enqueued without a wait: the piece buffers are
   // sized ahead (ntx + ntx / 4 pieces, or what an earlier batch needed); a
   // plan that does not fit them, or a descriptor planning more pieces than
@@ -1646,6 +1759,9 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   }
   out.timings.resolve_us += us_since(t);
   t = clock::now();
+  // host image: the delivery rewrites RX bytes an earlier pending batch may
+  // still be writing back from the mirror
+  for (Slot* p : sl.dep_rx) check(nicgpu_stream_wait_event(stream, p->ev_wb), "nicgpu_stream_wait_event");
   deliver(sl, mem, 0, nrx, NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_RESET_HITS, rctx, hits, stream);  // hits set, not added
   out.timings.gather_us += us_since(t);
   t = clock::now();
@@ -1655,7 +1771,8 @@ bool BatchedQueuePair::front(Slot& sl, const DeviceHostMemory& mem, std::span<co
   if (rst == NICGPU_ERR_AGAIN || rst == NICGPU_ERR_RANGE) {  // the plan did not fit: nothing resolved, settled or written
     out.timings.resolve_us += us_since(t);
     if (rst == NICGPU_ERR_RANGE) return false;
-    return front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);  // grown buffers: this plan fits
+    again = 1;  // grown buffers: the redone plan fits
+    return false;
   }
   check(rst, "nicgpu_qp_resolve_finish");
   sl.settled = settled;
@@ -1806,6 +1923,10 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
     out.timings.gather_us += us_since(t);
     t = clock::now();
     check(nicgpu_event_record(sl.ev_done, stream), "nicgpu_event_record");
+    if (sl.image) {  // the delivered bytes back into the host memory, beside the next batches' work
+      check(nicgpu_stream_wait_event(S.side_wb, sl.ev_done), "nicgpu_stream_wait_event");
+      image_writeback(sl, v.writes, nrx_total, S.side_wb);
+    }
   } catch (...) {
     sl.wait();  // the downloads must not outlive this batch's buffers
     throw;
@@ -1828,6 +1949,7 @@ void BatchedQueuePair::finish(Slot& sl, RxBatchResult& out) {
     ~Reset() { sl.down.reset(); }
   } reset{sl};
   sl.down->finish();
+  sl.wait_writeback();
   if (sl.rss) {
     const std::uint64_t m = sl.meta[0];
     config_.rss->account_batch(m, std::span<const std::uint64_t>(sl.meta + 1, sl.tn));
@@ -1843,6 +1965,242 @@ void BatchedQueuePair::finish(Slot& sl, RxBatchResult& out) {
     }
   }
   out.timings.copy_us += std::chrono::duration<double, std::micro>(clock::now() - t).count();
+}
+
+// ------------------------------------------------------------------------
+// The stage on the reference's HostMemory (host_memory.h:49-73): an HBM mirror
+// of its flat window.  Per batch the TX buffers' bytes go up (QueuePair's DMA
+// read, queue_pair.cpp:86-92), the stage runs on the mirror, and the bytes its
+// DMA writes delivered (:416-426) come back — nothing else of the memory is
+// read or written by the device.
+
+BatchedQueuePair::HostImage& BatchedQueuePair::bind_image(HostMemory& m) {
+  Scratch& S = *scratch_;
+  int dev = 0;
+  check(nicgpu_get_device(&dev), "nicgpu_get_device");
+  const std::size_t size = m.config().size_bytes;
+  std::byte* host = nullptr;
+  if (size) {
+    HostMemoryView v{};
+    const HostMemoryResult r = m.translate(0, size, v);
+    if (!r.ok() || v.data == nullptr || v.length != size)
+      throw GpuError("process_batch: HostMemory::translate(0, size) is not a view of the whole memory (an address "
+                     "translator or fault injector is not modelled)",
+                     NICGPU_ERR_INVALID);
+    host = v.data;
+    // flat: the last and a middle byte translate where the window puts them
+    for (const HostAddress a : {static_cast<HostAddress>(size - 1), static_cast<HostAddress>(size / 2)}) {
+      HostMemoryView p{};
+      if (!m.translate(a, 1, p).ok() || p.data != host + a)
+        throw GpuError("process_batch: HostMemory window is not flat (address translation is not modelled)",
+                       NICGPU_ERR_INVALID);
+    }
+    if (reinterpret_cast<std::uintptr_t>(host) & 15u)
+      throw GpuError("process_batch: HostMemory window is not 16-B aligned", NICGPU_ERR_INVALID);
+  }
+  HostImage& I = S.img;
+  if (I.mem == &m && I.host == host && I.size == size && I.device == dev) return I;
+  if (S.pending) throw std::logic_error("submit: another HostMemory while batches are pending");
+  I.release();
+  I.mem = &m;
+  I.host = host;
+  I.size = size;
+  I.device = dev;
+  if (size) {
+    void* alias = nullptr;
+    int owned = 0;
+    check(nicgpu_host_register(host, size, &alias, &owned), "nicgpu_host_register");
+    I.alias = static_cast<std::uint8_t*>(alias);
+    I.owned = owned != 0;
+    I.mirror.get((size + 15) / 16 * 16);
+  }
+  return I;
+}
+
+// The batch's TX span and bytes, its RX box, whether one copy of the span
+// stages it (dense: at most 1.5 x its bytes + 64 KiB), and the pending
+// batches it must follow: their RX boxes meet the span this batch stages
+// (its stage-in waits for their write-back) or its own RX box (its delivery
+// does).  Boxes are conservative: a wait that is not needed costs time, not
+// results.
+void BatchedQueuePair::image_prepare(Slot& sl, HostImage& img, std::span<const TxDescriptor> tx,
+                                     std::span<const RxDescriptor> rx) {
+  Scratch& S = *scratch_;
+  const std::uint64_t size = img.size;
+  struct Box {
+    std::uint64_t lo = ~0ull, hi = 0, bytes = 0;
+  };
+  const rx_stage_detail::Chunks ct(tx.size(), config_.host_threads ? config_.host_threads : 16, 1u << 17);
+  std::vector<Box> tb(ct.k), rb;
+  ct.run([&](std::size_t c, std::size_t b, std::size_t e) {
+    Box x;
+    for (std::size_t i = b; i < e; ++i) {
+      const std::uint64_t a = tx[i].buffer_address, n = tx[i].length;
+      if (n == 0 || !nicqp::dma_ok(size, a, n)) continue;
+      x.lo = std::min(x.lo, a);
+      x.hi = std::max(x.hi, a + n);
+      x.bytes += n;
+    }
+    tb[c] = x;
+  });
+  const rx_stage_detail::Chunks cr(rx.size(), config_.host_threads ? config_.host_threads : 16, 1u << 17);
+  rb.resize(cr.k);
+  cr.run([&](std::size_t c, std::size_t b, std::size_t e) {
+    Box x;
+    for (std::size_t j = b; j < e; ++j) {
+      const std::uint64_t a = rx[j].buffer_address;
+      if (rx[j].buffer_length == 0 || a >= size) continue;
+      x.lo = std::min(x.lo, a);
+      x.hi = std::max(x.hi, a + std::min<std::uint64_t>(rx[j].buffer_length, size - a));
+    }
+    rb[c] = x;
+  });
+  Box T, R;
+  for (const Box& x : tb) {
+    T.lo = std::min(T.lo, x.lo);
+    T.hi = std::max(T.hi, x.hi);
+    T.bytes += x.bytes;
+  }
+  for (const Box& x : rb) {
+    R.lo = std::min(R.lo, x.lo);
+    R.hi = std::max(R.hi, x.hi);
+  }
+  sl.image = &img;
+  sl.tx_lo = T.hi > T.lo ? T.lo : 0;
+  sl.tx_hi = T.hi > T.lo ? T.hi : 0;
+  sl.tx_bytes = T.bytes;
+  sl.rx_lo = R.hi > R.lo ? R.lo : 0;
+  sl.rx_hi = R.hi > R.lo ? R.hi : 0;
+  sl.whole = sl.tx_hi > sl.tx_lo && sl.tx_hi - sl.tx_lo <= T.bytes + T.bytes / 2 + (std::uint64_t{1} << 16);
+  sl.dep_stage.clear();
+  sl.dep_rx.clear();
+  for (unsigned k = 0; k < S.pending; ++k) {
+    Slot& p = S.slot[(S.head + k) % Scratch::kSlots];
+    if (&p == &sl || p.image != &img || p.rx_hi <= p.rx_lo) continue;
+    if (p.rx_lo < sl.tx_hi && sl.tx_lo < p.rx_hi) sl.dep_stage.push_back(&p);
+    if (p.rx_lo < sl.rx_hi && sl.rx_lo < p.rx_hi) sl.dep_rx.push_back(&p);
+  }
+}
+
+// The TX bytes into the mirror on `stream`: one copy of the span when dense
+// (the registered window goes up by DMA at the link's rate), else the gather
+// kernel over the TX descriptors (tx_dev: the batch's descriptors on the
+// device, in stream order; null: uploaded here).  Records ev_staged.
+void BatchedQueuePair::image_stage(Slot& sl, std::span<const TxDescriptor> tx, const void* tx_dev, void* stream) {
+  HostImage& I = *sl.image;
+  if (sl.tx_hi > sl.tx_lo) {
+    auto* mirror = static_cast<std::uint8_t*>(I.mirror.p);
+    if (sl.whole) {
+      check(nicgpu_memcpy_async(mirror + sl.tx_lo, I.host + sl.tx_lo, sl.tx_hi - sl.tx_lo, stream), "nicgpu_memcpy_async");
+    } else {
+      if (!tx_dev) {
+        tx_dev = sl.stage_tx.get(tx.size() * sizeof(TxDescriptor));
+        check(nicgpu_memcpy_async(const_cast<void*>(tx_dev), tx.data(), tx.size() * sizeof(TxDescriptor), stream),
+              "nicgpu_memcpy_async");
+      }
+      check(nicgpu_image_stage(mirror, I.alias, I.size, static_cast<const nicgpu_tx_descriptor*>(tx_dev), tx.size(),
+                               stream),
+            "nicgpu_image_stage");
+    }
+  }
+  check(nicgpu_event_record(sl.ev_staged, stream), "nicgpu_event_record");
+  sl.staged = true;
+}
+
+// The bytes of writes_dev[0, n) from the mirror back into the memory, on
+// `stream`; records ev_wb (finish() / collect() wait for it).
+void BatchedQueuePair::image_writeback(Slot& sl, const nicgpu_segment_write* writes_dev, std::size_t n, void* stream) {
+  HostImage& I = *sl.image;
+  if (n)
+    check(nicgpu_image_writeback(static_cast<const std::uint8_t*>(I.mirror.p), I.alias, I.size, writes_dev, n, stream),
+          "nicgpu_image_writeback");
+  check(nicgpu_event_record(sl.ev_wb, stream), "nicgpu_event_record");
+  sl.wb = true;
+}
+
+// Overlapping buffers or the host resolve, on a HostMemory: the host path over
+// the mirror (its piece sums after the stage-in, its writes after the
+// write-backs of earlier batches it rewrites), then every write it made back
+// into the memory, on `stream`.
+void BatchedQueuePair::image_host_path(Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+                                       QueuePairStats& st, RxBatchResult& out, void* stream, int disjoint,
+                                       double& check_us) {
+  if (!sl.staged) image_stage(sl, tx, nullptr, stream);
+  check(nicgpu_stream_wait_event(stream, sl.ev_staged), "nicgpu_stream_wait_event");
+  for (Slot* p : sl.dep_rx) check(nicgpu_stream_wait_event(stream, p->ev_wb), "nicgpu_stream_wait_event");
+  sl.applied.clear();
+  on_host(sl.image->view(), tx, rx, st, out, stream, disjoint, check_us, &sl.applied);
+  out.timings.host_image = true;
+  out.timings.staged_whole = sl.whole;
+  const std::size_t n = sl.applied.size();
+  void* d = sl.wbuf.get(std::max<std::size_t>(n, 1) * sizeof(rx_stage_detail::SegmentWrite));
+  if (n)
+    check(nicgpu_memcpy_async(d, sl.applied.data(), n * sizeof(rx_stage_detail::SegmentWrite), stream),
+          "nicgpu_memcpy_async");
+  image_writeback(sl, static_cast<const nicgpu_segment_write*>(d), n, stream);
+}
+
+RxBatchResult BatchedQueuePair::process_batch(HostMemory& mem, std::span<const TxDescriptor> tx,
+                                              std::span<const RxDescriptor> rx, void* stream) {
+  RxBatchResult out;
+  process_batch(mem, tx, rx, out, stream);
+  return out;
+}
+
+void BatchedQueuePair::process_batch(HostMemory& m, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+                                     RxBatchResult& out, void* stream) {
+  Scratch& S = *scratch_;
+  if (S.pending) throw std::logic_error("process_batch: collect() the submitted batches first");
+  int dev = 0;
+  check(nicgpu_get_device(&dev), "nicgpu_get_device");
+  S.ensure(dev);
+  HostImage& I = bind_image(m);
+  const DeviceHostMemory mem = I.view();
+  Slot& sl = S.slot[0];
+  sl.tx_dev = nullptr;
+  sl.rx_dev = nullptr;
+  image_prepare(sl, I, tx, rx);  // nothing pending: no dependencies
+  sl.staged = false;
+  QueuePairStats st = stats_;
+  int disjoint = -1;
+  double check_us = 0;
+  bool on_device = false;
+  try {
+    if (config_.device_resolve && device_fits(tx.size(), rx.size())) {
+      upload(sl, tx, rx, true);
+      image_stage(sl, tx, sl.v.tx, S.side_up);
+      on_device = front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);
+      if (on_device) {
+        back(sl, mem, out, stream);
+        finish(sl, out);
+      }
+    }
+    if (!on_device) {
+      image_host_path(sl, tx, rx, st, out, stream, disjoint, check_us);
+      sl.wait_writeback();
+    }
+  } catch (...) {
+    try {
+      sl.wait_writeback();
+    } catch (...) {
+    }
+    throw;
+  }
+  out.timings.check_us = check_us;
+  stats_ = st;
+  if (config_.on_interrupt) fire_interrupts(out);
+}
+
+void BatchedQueuePair::submit(HostMemory& m, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+                              void* stream) {
+  Scratch& S = *scratch_;
+  if (S.pending == Scratch::kSlots) throw std::logic_error("submit: three batches pending; collect() one first");
+  int dev = 0;
+  check(nicgpu_get_device(&dev), "nicgpu_get_device");
+  if (S.pending == 0) S.ensure(dev);
+  else if (S.device != dev) throw std::logic_error("submit: batches pending on another device");
+  HostImage& I = bind_image(m);
+  enqueue(I.view(), tx, rx, nullptr, stream, &I);
 }
 
 }  // namespace nic

@@ -1,0 +1,112 @@
+// image.hip — host-image staging for the batched QueuePair stage (SURVEY §8
+// row f1) on the reference's HostMemory (include/nic/host_memory.h:49-73):
+// the TX buffers' bytes from the registered host window into the HBM mirror
+// before a batch (QueuePair's DMA read, src/queue_pair.cpp:86-92), and the
+// bytes the batch's DMA writes delivered from the mirror back into the host
+// window after it (:416-426).  Both are byte-exact copies between two images
+// of the same memory at the same offsets: 16-B chunks aligned to the image
+// offsets, one 16-B load and store per whole chunk, byte stores for the bytes
+// of an edge chunk that lie inside the range, so no byte outside the range is
+// ever stored to (the host bytes past a frame are the application's).
+// One wave per range, a persistent grid walking the ranges; the host side is
+// PCIe-bound (≈ 50 GB/s each way), so the kernels only need enough bytes in
+// flight: every wave has one 1-KiB chunk step of its range outstanding.
+
+#include "common.h"
+#include "host.h"
+#include "qp_logic.h"
+
+using namespace nicgpu_detail;
+
+namespace {
+
+constexpr unsigned kImgWaves = 4;
+
+// dst[a, a + len) <- src[a, a + len), lanes over the 16-B chunks.
+__device__ __forceinline__ void copy_range(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t a,
+                                           uint64_t len, uint32_t lane) {
+  const uint64_t e = a + len;
+  const uint64_t c1 = (e + 15) & ~15ull;
+  for (uint64_t c = (a & ~15ull) + 16ull * lane; c < c1; c += 16ull * kWave) {
+    u32x4 v;
+    __builtin_memcpy(&v, src + c, 16);
+    if (c >= a && c + 16 <= e) {
+      __builtin_memcpy(dst + c, &v, 16);
+    } else {
+      uint8_t b[16];
+      __builtin_memcpy(b, &v, 16);
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (c + k >= a && c + k < e) dst[c + k] = b[k];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kWave * kImgWaves) void image_stage_kernel(uint8_t* image, const uint8_t* host,
+                                                                        uint64_t mem_size,
+                                                                        const nicgpu_tx_descriptor* __restrict__ tx,
+                                                                        uint64_t n) {
+  const uint32_t lane = lane_id();
+  // wave-uniform (scalar) index, so the descriptor loads are s_loads
+  const uint64_t w0 = (uint32_t) __builtin_amdgcn_readfirstlane(blockIdx.x * kImgWaves + threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t) gridDim.x * kImgWaves;
+  for (uint64_t i = w0; i < n; i += stride) {
+    const uint64_t a = tx[i].buffer_address, len = tx[i].length;
+    if (len == 0 || !nicqp::dma_ok(mem_size, a, len)) continue;  // a DMA read fault reads nothing (:86-92)
+    copy_range(image, host, a, len, lane);
+  }
+}
+
+__global__ __launch_bounds__(kWave * kImgWaves) void image_writeback_kernel(const uint8_t* image, uint8_t* host,
+                                                                            uint64_t mem_size,
+                                                                            const nicgpu_segment_write* __restrict__ w,
+                                                                            uint64_t n) {
+  const uint32_t lane = lane_id();
+  const uint64_t w0 = (uint32_t) __builtin_amdgcn_readfirstlane(blockIdx.x * kImgWaves + threadIdx.x / kWave);
+  const uint64_t stride = (uint64_t) gridDim.x * kImgWaves;
+  for (uint64_t j = w0; j < n; j += stride) {
+    const uint64_t d = w[j].dst;
+    const uint64_t len = (uint64_t) w[j].prefix_len + w[j].len_a + w[j].len_b;
+    if (len == 0 || !nicqp::dma_ok(mem_size, d, len)) continue;
+    copy_range(host, image, d, len, lane);
+  }
+}
+
+unsigned image_grid(uint64_t n, const DeviceInfo* di) {
+  const uint64_t want = (n + kImgWaves - 1) / kImgWaves;
+  const uint64_t cap = (uint64_t) di->cus * 8;
+  return (unsigned) (want < cap ? (want ? want : 1) : cap);
+}
+
+}  // namespace
+
+extern "C" {
+
+int nicgpu_image_stage(uint8_t* image, const uint8_t* host, uint64_t mem_size, const nicgpu_tx_descriptor* tx,
+                       size_t ntx, void* stream) {
+  if (ntx == 0 || mem_size == 0) return NICGPU_OK;
+  if (!image || !host || !tx || (reinterpret_cast<uintptr_t>(host) & 15u) || (reinterpret_cast<uintptr_t>(image) & 15u))
+    return NICGPU_ERR_INVALID;
+  const DeviceInfo* di = nullptr;
+  const int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(image_stage_kernel, dim3(image_grid(ntx, di)), dim3(kWave * kImgWaves), 0,
+                     static_cast<hipStream_t>(stream), image, host, mem_size, tx, (uint64_t) ntx);
+  return hip_status(hipGetLastError());
+}
+
+int nicgpu_image_writeback(const uint8_t* image, uint8_t* host, uint64_t mem_size, const nicgpu_segment_write* writes,
+                           size_t n, void* stream) {
+  if (n == 0 || mem_size == 0) return NICGPU_OK;
+  if (!image || !host || !writes || (reinterpret_cast<uintptr_t>(host) & 15u) ||
+      (reinterpret_cast<uintptr_t>(image) & 15u))
+    return NICGPU_ERR_INVALID;
+  const DeviceInfo* di = nullptr;
+  const int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(image_writeback_kernel, dim3(image_grid(n, di)), dim3(kWave * kImgWaves), 0,
+                     static_cast<hipStream_t>(stream), image, host, mem_size, writes, (uint64_t) n);
+  return hip_status(hipGetLastError());
+}
+
+}  // extern "C"

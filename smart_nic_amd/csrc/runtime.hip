@@ -186,4 +186,50 @@ int nicgpu_stream_wait_event(void* stream, void* event) {
   return hip_status(hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(event), 0));
 }
 
+int nicgpu_event_synchronize(void* event) {
+  if (!event) return NICGPU_ERR_INVALID;
+  return hip_status(hipEventSynchronize(static_cast<hipEvent_t>(event)));
+}
+
+// Whole pages around the range: hipHostRegister locks pages, and the staging
+// kernels read up to the next 16-B boundary past the last byte.
+namespace {
+constexpr uintptr_t kPage = 4096;
+void page_span(void* p, size_t n, void*& base, size_t& len) {
+  const auto a = reinterpret_cast<uintptr_t>(p);
+  const uintptr_t lo = a & ~(kPage - 1), hi = (a + n + 16 + kPage - 1) & ~(kPage - 1);
+  base = reinterpret_cast<void*>(lo);
+  len = hi - lo;
+}
+}  // namespace
+
+int nicgpu_host_register(void* host_ptr, size_t bytes, void** dev_alias, int* owned) {
+  if (!host_ptr || !dev_alias || !owned || bytes == 0) return NICGPU_ERR_INVALID;
+  *dev_alias = nullptr;
+  *owned = 0;
+  void* base = nullptr;
+  size_t len = 0;
+  page_span(host_ptr, bytes, base, len);
+  const hipError_t e = hipHostRegister(base, len, hipHostRegisterMapped);
+  if (e == hipSuccess) *owned = 1;
+  else if (e != hipErrorHostMemoryAlreadyRegistered) return NICGPU_ERR_HIP;
+  (void) hipGetLastError();  // clear the sticky "already registered"
+  void* dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) {
+    if (*owned) (void) hipHostUnregister(base);
+    *owned = 0;
+    return NICGPU_ERR_HIP;
+  }
+  *dev_alias = static_cast<uint8_t*>(dev) + (reinterpret_cast<uintptr_t>(host_ptr) - reinterpret_cast<uintptr_t>(base));
+  return NICGPU_OK;
+}
+
+int nicgpu_host_unregister(void* host_ptr) {
+  if (!host_ptr) return NICGPU_ERR_INVALID;
+  void* base = nullptr;
+  size_t len = 0;
+  page_span(host_ptr, 1, base, len);
+  return hip_status(hipHostUnregister(base));
+}
+
 }  // extern "C"

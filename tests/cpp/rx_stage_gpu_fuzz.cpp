@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "cpu_backend.h"
+#include "nic/flat_host_memory.h"
 #include "nic/rss.h"
 #include "nic/rx_stage.h"
 #include "nic/rss_rings.h"
@@ -74,6 +75,7 @@ const std::vector<std::uint8_t> kMsKey = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x
                                           0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
 
 std::size_t g_tail = 0, g_device = 0, g_short = 0, g_devdesc = 0;  // host tails, device batches, NoDescriptor, device descriptors
+std::size_t g_himg = 0, g_himg_sparse = 0;  // batches run on a HostMemory (and staged per descriptor)
 std::size_t g_irq = 0;  // interrupt callbacks compared
 
 // BatchedQueuePairConfig::results_on_device: copy RxBatchResult::dev into the
@@ -279,6 +281,39 @@ int run_case(std::uint64_t seed) {
                  ho.rx_consumed);
     return 1;
   }
+  // seeds with bit 2 set (host descriptors): the same batch once more on a
+  // HostMemory (the reference's interface, FlatHostMemory = SimpleHostMemory's
+  // bounds rule): TX bytes staged up, delivered bytes written back, everything
+  // equal to the host resolve's, the memory's bytes included
+  if (!dev_desc && ((seed >> 2) & 1)) {
+    FlatHostMemory hm(mem_size);
+    std::memcpy(hm.data(), image.data(), mem_size);
+    RssEngine hi_rss{rss_cfg};
+    cfg.rss = &hi_rss;
+    std::vector<CompletionEntry> fired_hi;
+    if (irq) cfg.on_interrupt = [&fired_hi](std::uint16_t, const CompletionEntry& e) { fired_hi.push_back(e); };
+    BatchedQueuePair hq{cfg};
+    RxBatchResult hio;
+    hq.process_batch(hm, tx, rx, hio);
+    if (keep && !materialize(hio)) return 1;
+    bool hok = hio.timings.host_image && hio.tx_completions.size() == ho.tx_completions.size() &&
+               hio.rx_completions.size() == ho.rx_completions.size();
+    for (std::size_t i = 0; hok && i < ho.tx_completions.size(); ++i) hok = same(hio.tx_completions[i], ho.tx_completions[i]);
+    for (std::size_t i = 0; hok && i < ho.rx_completions.size(); ++i) hok = same(hio.rx_completions[i], ho.rx_completions[i]);
+    hok = hok && std::memcmp(&hs, &hq.stats(), sizeof(hs)) == 0 && hio.rx_consumed == ho.rx_consumed;
+    const bool hmem = std::memcmp(hm.data(), host_img.data(), mem_size) == 0;
+    hok = hok && hmem && hio.rx_hash == ho.rx_hash && hio.rx_queue == ho.rx_queue && hio.queues == ho.queues;
+    hok = hok && hi_rss.stats().hashes == host_rss.stats().hashes && hi_rss.stats().queue_hits == host_rss.stats().queue_hits;
+    hok = hok && fired_hi.size() == fired_host.size();
+    for (std::size_t i = 0; hok && i < fired_host.size(); ++i) hok = same(fired_hi[i], fired_host[i]);
+    if (!hok) {
+      std::fprintf(stderr, "seed %llu: HostMemory batch differs (memory %d, device %d)\n", (unsigned long long) seed,
+                   int(hmem), int(hio.timings.device));
+      return 1;
+    }
+    g_himg += 1;
+    g_himg_sparse += !hio.timings.staged_whole;
+  }
   if (go.timings.host_tail) g_tail += 1;
   for (const auto& c : ho.tx_completions)
     if (c.status == static_cast<std::uint32_t>(CompletionCode::NoDescriptor)) {
@@ -418,7 +453,8 @@ int run_full(const char* wl, bool dev_desc, bool keep) {
 // ones wrote (TX buffers inside the RX ring), some batches overlap their own
 // buffers (host path) and the RX windows wrap the ring.  Results, statistics,
 // the image and the RSS engine's stats must all be equal.
-std::size_t g_pipe_batches = 0, g_pipe_host = 0, g_pipe_devdesc = 0;
+std::size_t g_pipe_batches = 0, g_pipe_host = 0, g_pipe_devdesc = 0, g_pipe_himg = 0;
+bool g_force_himg = false;  // `pipeline himg`: every sequence's pipelined side on a HostMemory
 
 int run_pipeline(std::uint64_t seed) {
   Rng r{seed * 7727 + 5};
@@ -489,6 +525,12 @@ int run_pipeline(std::uint64_t seed) {
   assert(nicgpu_memcpy_async(d_pipe, image.data(), mem_size, nullptr) == NICGPU_OK);
   assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
   const DeviceHostMemory m_seq{static_cast<std::byte*>(d_seq), mem_size}, m_pipe{static_cast<std::byte*>(d_pipe), mem_size};
+  // host descriptors with bit 2 set (every seed under `pipeline himg`): the
+  // pipelined side runs on a HostMemory — later batches read frames earlier
+  // pending ones deliver, rings wrap onto buffers still being written back
+  const bool himg = !(seed & 1) && (g_force_himg || ((seed >> 2) & 1));
+  FlatHostMemory hm(himg ? mem_size : 0);
+  if (himg) std::memcpy(hm.data(), image.data(), mem_size);
 
   RssEngine rss_seq{rss_cfg}, rss_pipe{rss_cfg};
   cfg.rss = &rss_seq;
@@ -555,7 +597,14 @@ int run_pipeline(std::uint64_t seed) {
       got.push_back(std::move(out));
       out = RxBatchResult{};
     }
-    if (!dev_desc) {
+    if (himg && pipe.pending() == 0 && r.below(4) == 0) {
+      pipe.process_batch(hm, txs[b], rxs[b], out);
+      if (keep) view_ok &= materialize(out);
+      got.push_back(std::move(out));
+      out = RxBatchResult{};
+    } else if (himg) {
+      pipe.submit(hm, txs[b], rxs[b]);
+    } else if (!dev_desc) {
       pipe.submit(m_pipe, txs[b], rxs[b]);
     } else if (pipe.pending() == 0 && r.below(3) == 0) {
       produce(b);
@@ -578,7 +627,8 @@ int run_pipeline(std::uint64_t seed) {
     const RxBatchResult &w = want[b], &g = got[b];
     ok = w.tx_completions.size() == g.tx_completions.size() && w.rx_completions.size() == g.rx_completions.size() &&
          w.rx_consumed == g.rx_consumed && w.tx_processed == g.tx_processed && w.rx_hash == g.rx_hash &&
-         w.rx_queue == g.rx_queue && w.queues == g.queues && w.timings.device == g.timings.device;
+         w.rx_queue == g.rx_queue && w.queues == g.queues && w.timings.device == g.timings.device &&
+         g.timings.host_image == himg;
     for (std::size_t i = 0; ok && i < w.tx_completions.size(); ++i) ok = same(w.tx_completions[i], g.tx_completions[i]);
     for (std::size_t i = 0; ok && i < w.rx_completions.size(); ++i) ok = same(w.rx_completions[i], g.rx_completions[i]);
     if (!ok) std::fprintf(stderr, "pipeline seed %llu: batch %d differs\n", (unsigned long long) seed, b);
@@ -586,6 +636,7 @@ int run_pipeline(std::uint64_t seed) {
   }
   g_pipe_batches += nb;
   if (dev_desc) g_pipe_devdesc += nb;
+  if (himg) g_pipe_himg += nb;
   ok = ok && std::memcmp(&seq.stats(), &pipe.stats(), sizeof(QueuePairStats)) == 0;
   bool irq_ok = irq_seq.size() == irq_pipe.size();
   for (std::size_t i = 0; irq_ok && i < irq_seq.size(); ++i) irq_ok = same(irq_seq[i], irq_pipe[i]);
@@ -596,6 +647,7 @@ int run_pipeline(std::uint64_t seed) {
   assert(nicgpu_memcpy_async(a.data(), d_seq, mem_size, nullptr) == NICGPU_OK);
   assert(nicgpu_memcpy_async(b.data(), d_pipe, mem_size, nullptr) == NICGPU_OK);
   assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+  if (himg) std::memcpy(b.data(), hm.data(), mem_size);  // the HostMemory itself, after every collect
   ok = ok && a == b;
   nicgpu_free(d_seq);
   nicgpu_free(d_pipe);
@@ -973,13 +1025,18 @@ int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "check") == 0) return run_check(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 400);
   if (argc > 1 && std::strcmp(argv[1], "edges") == 0) return run_edges();
   if (argc > 1 && std::strcmp(argv[1], "pipeline") == 0) {
-    const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 40;
+    int a = 2;
+    if (argc > a && std::strcmp(argv[a], "himg") == 0) {
+      g_force_himg = true;
+      ++a;
+    }
+    const std::uint64_t count = argc > a ? std::strtoull(argv[a], nullptr, 10) : 40;
     int bad = 0;
     for (std::uint64_t s = 1; s <= count; ++s) bad += run_pipeline(s);
     if (bad) return 1;
     std::printf("rx_stage_gpu_fuzz pipeline: ok (%llu sequences, %zu batches, %zu of them on the host path, %zu "
-                "with device descriptors, %zu results left on the device)\n",
-                (unsigned long long) count, g_pipe_batches, g_pipe_host, g_pipe_devdesc, g_keep);
+                "with device descriptors, %zu on a HostMemory, %zu results left on the device)\n",
+                (unsigned long long) count, g_pipe_batches, g_pipe_host, g_pipe_devdesc, g_pipe_himg, g_keep);
     return 0;
   }
   if (argc > 1 && std::strcmp(argv[1], "full") == 0) {
@@ -997,7 +1054,7 @@ int main(int argc, char** argv) {
   if (bad) return 1;
   std::printf("rx_stage_gpu_fuzz: ok (%llu batches, %zu resolved on the device, %zu of them with a host tail, %zu "
               "running out of RX descriptors, %zu with device descriptors, %zu with results left on the device, "
-              "%zu interrupt callbacks equal)\n",
-              (unsigned long long) count, g_device, g_tail, g_short, g_devdesc, g_keep, g_irq);
+              "%zu interrupt callbacks equal, %zu also on a HostMemory (%zu staged per descriptor))\n",
+              (unsigned long long) count, g_device, g_tail, g_short, g_devdesc, g_keep, g_irq, g_himg, g_himg_sparse);
   return 0;
 }

@@ -43,7 +43,7 @@ def test_host_library_exports_nic_api():
 
 def test_abi_version_and_errors_without_gpu():
     lib = sna.load_library()
-    assert lib.nicgpu_abi_version() == 1
+    assert lib.nicgpu_abi_version() == 2 == sna.ABI_VERSION
     assert lib.nicgpu_strerror(sna.ERR_NO_DEVICE) == b"no gfx950 device"
     # argument validation happens before any device access
     assert lib.nicgpu_rx_offload(None, None, None, 0, 7, 0, 0, None, None, None, None, None) == sna.ERR_INVALID

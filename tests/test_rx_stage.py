@@ -78,6 +78,60 @@ def test_rx_stage_gpu(tmp_path):
 
 
 @pytest.mark.gpu
+def test_rx_stage_host_memory_gpu(tmp_path):
+    """The product path on a HostMemory (the interface QueuePair's DMAEngine
+    reads and writes, include/nic/host_memory.h:49-73) instead of an HBM image:
+    TX bytes staged up, delivered bytes written back; the memory's bytes,
+    completions, stats and RSS must equal the reference's on every fixture
+    (device resolve, host resolve, submit/collect).  nic::FlatHostMemory."""
+    exe = _build(tmp_path, "rx_stage_test")
+    for n in CASES:
+        _run(exe, "host", n, tmp_path)
+
+
+REFMEM = os.path.join(ROOT, "oracle", "_ref", "rx_stage_test_refmem")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REFMEM), reason="oracle/_ref/rx_stage_test_refmem not built (make -C oracle ref)")
+def test_rx_stage_reference_simple_host_memory_gpu(tmp_path):
+    """The same through the reference's own SimpleHostMemory
+    (src/simple_host_memory.cpp compiled in place by oracle/Makefile into
+    oracle/_ref/rx_stage_test_refmem, which travels to the GPU box): the
+    stage drops in on the reference's memory object unchanged."""
+    for n in CASES:
+        _run(REFMEM, "host", n, tmp_path)
+
+
+def test_rx_stage_refmem_binary_builds():
+    """Where the reference exists, build() leaves the drop-in binary behind
+    (its GPU run is test_rx_stage_reference_simple_host_memory_gpu)."""
+    if not os.path.isdir("/root/reference/src"):
+        pytest.skip("needs /root/reference")
+    r = subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "_ref/rx_stage_test_refmem"], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    nm = subprocess.run(["nm", "-C", REFMEM], capture_output=True, text=True).stdout
+    assert "nic::SimpleHostMemory::translate_view" in nm  # the reference's memory object is compiled in
+    assert " U nic::BatchedQueuePair::process_batch(nic::HostMemory&" in nm  # and the stage comes from libnic_host.so
+
+
+@pytest.mark.gpu
+def test_rx_stage_pipelined_host_memory(tmp_path):
+    """submit/collect on a HostMemory against process_batch on an HBM image,
+    in order, over 40 sequences: later batches read frames earlier pending
+    batches deliver (their stage-in waits for that write-back), RX windows wrap
+    onto buffers still being written back (the delivery waits), some batches
+    overlap their own buffers (host path).  Results, stats, RSS stats and the
+    memory's bytes after every collect equal."""
+    exe = _build(tmp_path, "rx_stage_gpu_fuzz")
+    r = subprocess.run([exe, "pipeline", "himg", "40"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "rx_stage_gpu_fuzz pipeline: ok" in r.stdout
+    print(r.stdout.strip())
+
+
+@pytest.mark.gpu
 def test_rx_stage_device_resolve_vs_host_resolve(tmp_path):
     """Random batches with disjoint buffers: the device resolve (nicgpu_qp_*,
     process_batch's path for them) against the host resolve over the CPU

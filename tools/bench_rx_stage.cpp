@@ -12,7 +12,12 @@
 //   argument: results copied to the host vectors, or left in device memory
 //   (BatchedQueuePairConfig::results_on_device)); irq: RX and TX interrupt
 //   callbacks on (a counting callback, as an InterruptDispatcher delivers
-//   them: queue_pair.cpp:371-383), replayed from the completions
+//   them: queue_pair.cpp:371-383), replayed from the completions;
+//   hostmem: the memory is a HostMemory (nic::FlatHostMemory, the reference
+//   SimpleHostMemory's bounds rule) in host RAM, descriptors in page-locked
+//   arrays — every batch stages its TX bytes up and writes its delivered bytes
+//   back (process_batch(HostMemory&, ...)): the end-to-end rate from host
+//   memory, PCIe included
 //
 // c3: IMIX 64/576/1518 (7:4:1) frames, each balanced so the whole-frame
 //     checksum verifies; RX descriptors with Layer4 checksum offload, 2 KiB
@@ -40,6 +45,7 @@
 #include <string>
 #include <vector>
 
+#include "nic/flat_host_memory.h"
 #include "nic/rss.h"
 #include "nic/rx_queue_manager.h"
 #include "nic/rx_stage.h"
@@ -156,7 +162,13 @@ int main(int argc, char** argv) {
     };
   }
   const std::string desc_kind = argc > 6 ? argv[6] : "pageable";
-  const bool pinned = desc_kind == "pinned", dev_desc = desc_kind == "device";
+  const bool hostmem = desc_kind == "hostmem";
+  const bool pinned = desc_kind == "pinned" || hostmem, dev_desc = desc_kind == "device";
+  std::unique_ptr<FlatHostMemory> hm;
+  if (hostmem) {  // the same bytes in host RAM, behind the reference's HostMemory interface
+    hm = std::make_unique<FlatHostMemory>(mem_size);
+    std::memcpy(hm->data(), tx_img.data(), tx_bytes);
+  }
   BatchedQueuePair qp{cfg};
   const DeviceHostMemory dm{static_cast<std::byte*>(mem), mem_size};
   std::span<const TxDescriptor> txs{tx};
@@ -229,6 +241,7 @@ int main(int argc, char** argv) {
   }
   auto submit = [&] {
     if (dev_desc) qp.submit(dm, dd);
+    else if (hostmem) qp.submit(*hm, txs, rxs);
     else qp.submit(dm, txs, rxs);
   };
 
@@ -261,6 +274,7 @@ int main(int argc, char** argv) {
     const auto t0 = std::chrono::steady_clock::now();
     // one result object reused across batches
     if (dev_desc) qp.process_batch(dm, dd, last);
+    else if (hostmem) qp.process_batch(*hm, txs, rxs, last);
     else qp.process_batch(dm, txs, rxs, last);
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     if (r > 0) tot.emplace_back(us, last.timings);
@@ -281,13 +295,22 @@ int main(int argc, char** argv) {
   }
   for (const auto& c : last.rx_completions) ok += c.status == 0;
   for (auto L : lens) frame_bytes += L;
+  if (hostmem) {  // the last batch's frames are in the host memory, byte for byte
+    std::size_t bad = 0;
+    for (std::size_t j = 0; j < std::min<std::size_t>(n, nrx) && !wl.compare("c3"); ++j)
+      bad += std::memcmp(hm->data() + rx[j].buffer_address, tx_img.data() + tx[j].buffer_address, lens[j]) != 0;
+    if (bad) {
+      std::fprintf(stderr, "hostmem: %zu delivered frames differ in the host memory\n", bad);
+      return 1;
+    }
+  }
   const auto& T = tot[tot.size() / 2].second;  // the median batch's phases
   std::printf(
       "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"mode\": \"%s\", \"results\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, \"rx_align\": %zu, "
-      "\"rx_success\": %zu, \"interrupts\": %s, \"irq_callbacks\": %llu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
+      "\"rx_success\": %zu, \"host_memory\": %s, \"tx_staged_whole\": %s, \"interrupts\": %s, \"irq_callbacks\": %llu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
       "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f}}\n",
       wl.c_str(), T.device ? "device" : "host", desc_kind.c_str(), pipelined ? "pipelined" : "sync", cfg.results_on_device ? "device" : "host", cfg.host_threads, n, last.rx_completions.size(), rx_align, ok,
-      irq ? "true" : "false", (unsigned long long) irq_count, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
+      T.host_image ? "true" : "false", T.staged_whole ? "true" : "false", irq ? "true" : "false", (unsigned long long) irq_count, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
       T.resolve_us, T.gather_us, T.rss_us, T.copy_us);
   nicgpu_free(mem);
   if (ptx) nicgpu_host_free(ptx);
