@@ -17,8 +17,16 @@
 //     fails);
 //   * when no queue's RX buffer overlaps a byte another queue reads or writes,
 //     each queue pair's results are independent of the order the scheduler
-//     interleaves them in, so every queue's batch goes to its own
-//     BatchedQueuePair on the device, all in flight at once (submit/collect);
+//     interleaves them in, so the queue pairs' batches are resolved as ONE
+//     device batch: their TX batches and RX rings back to back, each queue
+//     pair a segment with its own queue id, MTU and ring (the scan of the
+//     ring positions restarted per segment), one plan / piece-sum / resolve /
+//     delivery chain, the results, statistics and RSS dispatch lists split per
+//     queue pair afterwards.  It needs the queue pairs' stage settings to agree
+//     (device resolve on, results_on_device alike, RSS engines of equal key,
+//     table and tuple — each engine still counts its own frames) and the
+//     batch's buffers to be disjoint and settle on the device; otherwise each
+//     queue's batch goes to its own BatchedQueuePair, all in flight at once;
 //   * otherwise the interleaving decides the bytes (a queue writes into
 //     another's TX buffer before or after it is read): the schedule is replayed
 //     run by run, each run of one queue's consecutive descriptors a host-path
@@ -82,6 +90,16 @@ struct QueueBatch {
   std::span<const RxDescriptor> rx;
 };
 
+/// The same with the descriptors already in device memory (a host-backed ring
+/// in the image, a device-side producer): device pointers, read in stream
+/// order after the caller's earlier work on the stream.
+struct DeviceQueueBatch {
+  const TxDescriptor* tx{nullptr};
+  std::size_t ntx{0};
+  const RxDescriptor* rx{nullptr};
+  std::size_t nrx{0};
+};
+
 /// How one drain served the queues: runs of consecutive descriptors of one
 /// queue, in order, and the scheduler counters it added.
 struct QueueSchedule {
@@ -114,6 +132,8 @@ public:
   [[nodiscard]] std::size_t queue_count() const noexcept { return qps_.size(); }
   /// The queue pair's stage (its config has no interrupt callback: the
   /// manager fires them, in the scheduler's order); nullptr past the end.
+  /// Its own stats() count only the batches that ran per queue pair; the
+  /// queue pair's statistics are queue_stats().
   [[nodiscard]] BatchedQueuePair* queue(std::size_t index) noexcept;
   [[nodiscard]] std::optional<QueuePairStats> queue_stats(std::size_t index) const noexcept;
 
@@ -126,6 +146,22 @@ public:
   /// exception propagates.
   QueueSchedule process_batch(const DeviceHostMemory& mem, std::span<const QueueBatch> batches,
                               std::vector<RxBatchResult>& out, void* stream = nullptr);
+  /// The same against the reference's HostMemory (host_memory.h:49-73), as
+  /// BatchedQueuePair::process_batch(HostMemory&, ...): one HBM mirror for all
+  /// queue pairs, every queue's TX bytes staged up, the delivered bytes written
+  /// back; when the fused batch does not apply, the queue pairs run one after
+  /// another on it.
+  QueueSchedule process_batch(HostMemory& mem, std::span<const QueueBatch> batches, std::vector<RxBatchResult>& out,
+                              void* stream = nullptr);
+  /// Descriptors in device memory: the fused batch when the device finds the
+  /// whole concatenated batch disjoint (every queue pair's buffers apart from
+  /// every other's); otherwise the descriptors come down once and the host
+  /// path of process_batch above decides.
+  QueueSchedule process_batch(const DeviceHostMemory& mem, std::span<const DeviceQueueBatch> batches,
+                              std::vector<RxBatchResult>& out, void* stream = nullptr);
+  /// How the last process_batch ran: 1 = one fused device batch, 0 = per
+  /// queue pair (device stages or the reference's interleaving on the host).
+  [[nodiscard]] int last_fused() const noexcept { return last_fused_; }
 
   /// Scheduler index/credit/counters and every queue pair's statistics
   /// (QueueManager::reset, :80-93; the rings are the caller's).
@@ -134,8 +170,14 @@ public:
   [[nodiscard]] std::string stats_summary() const;
 
 private:
+  QueueSchedule run(const DeviceHostMemory& dmem, HostMemory* hmem, std::span<const QueueBatch> batches,
+                    std::vector<RxBatchResult>& out, void* stream);
+  bool fusable() const;
+  void replay(const QueueSchedule& sched, const std::vector<RxBatchResult>& out, void* stream);
   struct Queue;
   std::vector<std::unique_ptr<Queue>> qps_;
+  std::unique_ptr<BatchedQueuePair> fused_;  // every queue pair's batch as one (queue 0's settings)
+  int last_fused_{0};
   struct Streams;  // a stream per queue pair, forked from and joined into the caller's
   std::unique_ptr<Streams> streams_;
   std::vector<std::uint8_t> weights_;

@@ -357,6 +357,26 @@ public:
   struct HostImage;  // a registered HostMemory window and its HBM mirror
 
 private:
+  friend class BatchedQueueManager;
+  // BatchedQueueManager's fused batch: the queue pairs' TX batches and RX
+  // rings resolved as ONE device batch (nicgpu_qp_set_segments: each queue
+  // pair's own queue id, MTU and ring), one plan / piece-sum / resolve /
+  // delivery chain, the results split per queue pair (out[q], stats[q]).
+  // `img` null: `mem` is the device image.  Returns false, having written
+  // nothing, when the batch does not fit the fused path (overlapping or
+  // unsorted buffers, positions that do not settle): the caller then runs the
+  // queue pairs one by one.  Interrupts are the caller's to replay.
+  // dev_desc: the spans point at device memory (copied in stream order after
+  // `stream`'s earlier work; needs whole_check and no img).  whole_check: the
+  // device checks the batch as one ring (the caller has not checked the queue
+  // pairs against each other).
+  bool process_queues(const DeviceHostMemory& mem, HostImage* img, std::span<const std::span<const TxDescriptor>> tx,
+                      std::span<const std::span<const RxDescriptor>> rx, std::span<const BatchedQueuePairConfig> configs,
+                      std::vector<RxBatchResult>& out, std::vector<QueuePairStats>& stats, void* stream,
+                      bool dev_desc = false, bool whole_check = false);
+  bool front_multi(Slot& sl, const DeviceHostMemory& mem, std::size_t ntx, std::size_t nrx, RxBatchResult& out,
+                   void* stream, int& again, bool whole_check);
+  void share_image(const BatchedQueuePair& owner);  // use owner's HostImage (one mirror per manager)
   // Device resolve of one batch in four steps: upload() sends the descriptors
   // up; front() plans and checks (false, nothing written, when the buffers
   // overlap), starts the resolve, enqueues the DMA writes and RSS of the
@@ -374,7 +394,7 @@ private:
   void image_prepare(Slot& sl, HostImage& img, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx);
   void image_host_path(Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                        QueuePairStats& stats, RxBatchResult& out, void* stream, int disjoint, double& check_us);
-  void image_stage(Slot& sl, std::span<const TxDescriptor> tx, const void* tx_dev, void* stream);
+  void image_stage(Slot& sl, std::size_t ntx, const TxDescriptor* tx_host, const void* tx_dev, void* stream);
   void image_writeback(Slot& sl, const nicgpu_segment_write* writes_dev, std::size_t n, void* stream);
   void back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult& out, void* stream);
   void deliver(Slot& sl, const DeviceHostMemory& mem, std::size_t a, std::size_t b, unsigned flags,

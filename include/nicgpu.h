@@ -52,6 +52,7 @@ extern "C" {
 #define NICGPU_ERR_NOMEM (-4)
 #define NICGPU_ERR_RANGE (-5)    /* a batch too large for 32-bit piece indices: split it */
 #define NICGPU_ERR_AGAIN (-6)    /* an asynchronous plan outgrew its buffers: redo the batch (the next plan fits) */
+#define NICGPU_ERR_UNSETTLED (-7) /* segmented resolve: positions did not settle; nothing written, resolve per queue pair */
 
 #define NICGPU_DESC_OFFSET_BITS 40
 /* Longest packet the kernels accept: 64 KiB - 1 (the TSO super-frame limit of
@@ -370,6 +371,12 @@ int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view
  * ascending and apart (the caller then sorts on the host).  Synchronises
  * `stream`. */
 int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int* verdict, void* stream);
+/* nicgpu_qp_check with flags: NICGPU_QP_CHECK_WHOLE checks a segmented batch
+ * as one ring (every RX span against every other and every TX span, across
+ * queue pairs too), not queue pair by queue pair. */
+#define NICGPU_QP_CHECK_WHOLE 1u
+int nicgpu_qp_check_flags(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, unsigned flags, int* verdict,
+                          void* stream);
 /* The kernels of the next plan/check/resolve read the caller's device arrays
  * tx[0, ntx) and rx[0, nrx) in place of view.tx / view.rx (no copy; view is
  * refreshed to point at them).  They must stay valid and unchanged until the
@@ -476,6 +483,57 @@ int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx,
 int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t rx_begin, size_t rx_end,
                             unsigned flags, const nicgpu_rss_ctx* ctx, int tuple_mode, uint32_t raw_off,
                             uint32_t raw_len, uint64_t* hits_dev, void* stream);
+
+/* ---- Several queue pairs in one batch (nic::BatchedQueueManager) ----
+ * QueueManager::process_once (src/queue_manager.cpp:54-78) serves several
+ * QueuePairs; when no queue's buffers meet another's, each queue pair's
+ * results are independent of the interleaving, so their batches can be
+ * resolved together: view.tx holds the queue pairs' TX batches back to back
+ * (segment s's are [tx_begin_s, tx_begin_{s+1}), the last ends at ntx) and
+ * view.rx their RX rings back to back (segment s's ring is
+ * [rx_begin_s, rx_begin_s + nrx_s), rx_begin ascending).  Every kernel of the
+ * next plans and resolves then runs segment s's packets with its own queue id
+ * and MTU against its own ring: ring positions are the scan of the pops
+ * restarted at every segment, a ring's end is its own.  Completions land at
+ * their absolute slots: segment s's TX completions at view.txc[tx_begin_s ..],
+ * its RX completions at view.rxc[rx_begin_s, + used_s); the ring slots it does
+ * not use hold an empty write and status NICGPU_QP_SLOT_UNUSED (no delivery,
+ * no RSS).  The resolve settles all of the batch or nothing:
+ * nicgpu_qp_resolve_finish returns NICGPU_ERR_UNSETTLED when some position
+ * is still unsettled after the relaxation steps (nothing was written; the
+ * caller resolves the queue pairs one by one) and otherwise *done = ntx,
+ * *rx_used = *rx_settled = the concatenated ring's length when the
+ * speculative pass settled everything (0 settled otherwise: deliver it all
+ * afterwards). */
+typedef struct nicgpu_qp_segment {
+  uint64_t tx_begin;
+  uint64_t rx_begin;
+  uint64_t nrx;
+  uint64_t max_mtu;
+  uint16_t queue_id;
+  uint16_t pad0, pad1, pad2;
+} nicgpu_qp_segment; /* 40 B */
+#define NICGPU_QP_SLOT_UNUSED 0xFFFFFFFFu
+#define NICGPU_QP_MAX_SEGMENTS 1024u
+/* Segments for the following plans/resolves of q (host array, copied; nseg 0:
+ * back to one queue pair).  ntx: the batch's TX descriptors (sizes the block
+ * map: each grid block serves one segment, blocks in proportion to its TX
+ * descriptors).  Enqueued on `stream`. */
+int nicgpu_qp_set_segments(nicgpu_qp* q, const nicgpu_qp_segment* seg, size_t nseg, size_t ntx, void* stream);
+/* After a segmented nicgpu_qp_resolve_finish: per segment, the RX descriptors
+ * its queue pair popped (used[nseg]) and its QueuePairStats (stats[nseg]). */
+int nicgpu_qp_segment_results(const nicgpu_qp* q, uint64_t* used, nicgpu_qp_stats* stats);
+/* After nicgpu_qp_group over a segmented batch's nrx slots with nq RSS queues:
+ * the dispatch lists split per segment — entries rewritten to indices relative
+ * to their segment's rx_begin, and split[s * nq + r] = the first entry of RSS
+ * queue r's list (view.queue_which[queue_start[r], queue_end[r])) that belongs
+ * to segment s or later, for s in [0, nseg] (split[nseg * nq + r] =
+ * queue_end[r]).  split_host: (nseg + 1) * nq words; synchronises `stream`. */
+int nicgpu_qp_segment_lists(nicgpu_qp* q, size_t nrx, size_t nq, uint32_t* split_host, void* stream);
+/* Per-segment RSS hits of the delivered frames (Success completions, hashed by
+ * the delivery): hits_dev[s * table_n + h % table_n] (u64, set, not added).
+ * For queue pairs that count into RssEngines of their own. */
+int nicgpu_qp_segment_hits(nicgpu_qp* q, size_t nrx, size_t table_n, uint64_t* hits_dev, void* stream);
 
 /* ---- Host-image staging (row f1 on the reference's HostMemory) ----
  * nic::BatchedQueuePair::process_batch(HostMemory&, ...) runs the stage on an

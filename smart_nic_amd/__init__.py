@@ -101,6 +101,11 @@ ABI_SYMBOLS = (
     "nicgpu_cq_post",
     "nicgpu_cq_state",
     "nicgpu_cq_poll",
+    "nicgpu_qp_check_flags",
+    "nicgpu_qp_set_segments",
+    "nicgpu_qp_segment_results",
+    "nicgpu_qp_segment_lists",
+    "nicgpu_qp_segment_hits",
     "nicgpu_event_synchronize",
     "nicgpu_host_register",
     "nicgpu_host_unregister",
@@ -176,6 +181,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_event_record": (i32, [vp, vp]),
         "nicgpu_stream_wait_event": (i32, [vp, vp]),
         "nicgpu_tso_checksum": (i32, [vp, vp, vp, vp, vp, sz, vp, vp]),
+        "nicgpu_qp_check_flags": (i32, [vp, ctypes.c_uint64, sz, sz, u32, vp, vp]),
+        "nicgpu_qp_set_segments": (i32, [vp, vp, sz, sz, vp]),
+        "nicgpu_qp_segment_results": (i32, [vp, vp, vp]),
+        "nicgpu_qp_segment_lists": (i32, [vp, sz, sz, vp, vp]),
+        "nicgpu_qp_segment_hits": (i32, [vp, sz, sz, vp, vp]),
         "nicgpu_event_synchronize": (i32, [vp]),
         "nicgpu_host_register": (i32, [vp, sz, ctypes.POINTER(vp), ctypes.POINTER(i32)]),
         "nicgpu_host_unregister": (i32, [vp]),

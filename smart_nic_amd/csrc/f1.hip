@@ -973,6 +973,56 @@ constexpr unsigned kQpStats = 16;
 constexpr unsigned kQpTail = 3 + 16 + 2;  // ... then [19] the plan overflowed (1 buffers, 2 pieces per descriptor), [20] its piece count
 constexpr int kQpRelaxSteps = 8;  // position relaxations before the host takes the rest
 
+// Segmented batches (several queue pairs, nicgpu_qp_set_segments): each grid
+// block serves one segment — blocks in proportion to its TX descriptors — so a
+// block's per-block statistics belong to one queue pair, and a packet's queue
+// id, MTU and ring come from its block's segment.  seg == null: one queue pair
+// (the context's), every block over all of [0, n).
+struct QpBlk {
+  uint32_t seg, rank, nb, pad;  // the block's segment, its rank among that segment's blocks, their number
+};
+struct QpSegs {
+  const nicgpu_qp_segment* seg;
+  const QpBlk* blk;
+  uint32_t nseg;
+};
+struct QpRange {
+  uint64_t i, end, step;
+  uint32_t s;
+};
+__device__ __forceinline__ uint64_t qp_seg_end(const QpSegs& S, uint32_t s, uint64_t n) {
+  return s + 1 < S.nseg ? S.seg[s + 1].tx_begin : n;
+}
+// the TX indices this thread visits
+__device__ __forceinline__ QpRange qp_range(const QpSegs& S, uint64_t n) {
+  if (!S.seg) return QpRange{(uint64_t) blockIdx.x * kQpBlock + threadIdx.x, n, (uint64_t) gridDim.x * kQpBlock, 0u};
+  const QpBlk b = S.blk[blockIdx.x];
+  const uint64_t hi = qp_seg_end(S, b.seg, n);
+  return QpRange{S.seg[b.seg].tx_begin + (uint64_t) b.rank * kQpBlock + threadIdx.x, hi < n ? hi : n,
+                 (uint64_t) b.nb * kQpBlock, b.seg};
+}
+// segment s's context: its queue id and MTU, its ring's end in the
+// concatenated ring (positions are absolute)
+__device__ __forceinline__ QpCtx qp_ctx_of(QpCtx C, const QpSegs& S, uint32_t s) {
+  if (S.seg) {
+    const nicgpu_qp_segment g = S.seg[s];
+    C.queue_id = g.queue_id;
+    C.max_mtu = g.max_mtu;
+    C.nrx = g.rx_begin + g.nrx;
+  }
+  return C;
+}
+// the absolute ring position of packet i of segment s: the scan restarted at
+// the segment's first packet, from its ring's first slot
+__device__ __forceinline__ uint64_t qp_abs(const uint32_t* __restrict__ pos, const QpSegs& S, uint32_t s, uint64_t i) {
+  if (!S.seg) return pos[i];
+  const nicgpu_qp_segment g = S.seg[s];
+  return g.rx_begin + (uint64_t) (uint32_t) (pos[i] - pos[g.tx_begin]);
+}
+__device__ __forceinline__ uint64_t qp_max_mtu(uint64_t max_mtu, const QpSegs& S, uint32_t s) {
+  return S.seg ? S.seg[s].max_mtu : max_mtu;
+}
+
 struct QpNullSink {
   __device__ void tx(const nicgpu_completion&, bool) {}
   __device__ void rx(const nicgpu_completion&, const nicgpu_segment_write*) {}
@@ -1004,11 +1054,13 @@ constexpr uint32_t kQpMaxPieces = 256;
 __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
                                                             uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
                                                             uint32_t* counts, unsigned long long* ovf,
-                                                            unsigned long long gen) {
-  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
+                                                            unsigned long long gen, QpSegs S) {
+  const QpRange R = qp_range(S, n);
+  const uint64_t mtu = qp_max_mtu(max_mtu, S, R.s);
+  for (uint64_t i = R.i; i < R.end; i += R.step) {
     QpPlan pp;
     const uint32_t c =
-        nicqp::plan_packet(max_mtu, mem_size, nicqp::desc_load(tx + i), pp, [](uint64_t, uint64_t) {}, /*split4=*/true);
+        nicqp::plan_packet(mtu, mem_size, nicqp::desc_load(tx + i), pp, [](uint64_t, uint64_t) {}, /*split4=*/true);
     counts[i] = c <= kQpMaxPieces ? c : 0u;
     if (c > kQpMaxPieces) *ovf = gen;
     plans[i] = pp;
@@ -1021,19 +1073,22 @@ __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_desc
 __global__ __launch_bounds__(kQpBlock) void qp_fill_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
                                                            uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
                                                            const uint32_t* __restrict__ base, uint64_t* desc,
-                                                           uint64_t cap, unsigned long long* g, unsigned long long gen) {
+                                                           uint64_t cap, unsigned long long* g, unsigned long long gen,
+                                                           QpSegs S) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const uint64_t np = base[n];
     g[5] = np;
     g[4] = np < cap ? np : cap;
     if (np > cap) g[3] = gen;
   }
-  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
+  const QpRange R = qp_range(S, n);
+  const uint64_t mtu = qp_max_mtu(max_mtu, S, R.s);
+  for (uint64_t i = R.i; i < R.end; i += R.step) {
     uint64_t at = base[i];
     plans[i].first_piece = (uint32_t) at;
     QpPlan pp;
     nicqp::plan_packet(
-        max_mtu, mem_size, nicqp::desc_load(tx + i), pp,
+        mtu, mem_size, nicqp::desc_load(tx + i), pp,
         [&](uint64_t a, uint64_t len) {
           if (at < cap) desc[at] = NICGPU_DESC(a, len);
           ++at;
@@ -1050,9 +1105,16 @@ __device__ __forceinline__ bool qp_plan_bad(const unsigned long long* g, unsigne
 
 __global__ __launch_bounds__(kQpBlock) void qp_need_kernel(QpCtx C, uint64_t n, uint32_t* need,
                                                            unsigned long long* first, const unsigned long long* g,
-                                                           unsigned long long gen) {
+                                                           unsigned long long gen, QpSegs S) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *first = n;  // the speculative final pass's "nothing differed"
   const bool bad = qp_plan_bad(g, gen);
+  if (S.seg) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) need[n] = 0u;
+    const QpRange R = qp_range(S, n);
+    const QpCtx Cs = qp_ctx_of(C, S, R.s);
+    for (uint64_t i = R.i; i < R.end; i += R.step) need[i] = !bad ? nicqp::rx_need(Cs, i) : 0u;
+    return;
+  }
   for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i <= n; i += (uint64_t) gridDim.x * kQpBlock)
     need[i] = i < n && !bad ? nicqp::rx_need(C, i) : 0u;
 }
@@ -1064,14 +1126,17 @@ __global__ __launch_bounds__(kQpBlock) void qp_need_kernel(QpCtx C, uint64_t n, 
 // are the fixed point, and each step makes at least one more packet exact:
 // pos[0] = 0 always is, so after k steps packets [0, k) are.
 __global__ __launch_bounds__(kQpBlock) void qp_relax_kernel(QpCtx C, uint32_t* pops, const uint32_t* __restrict__ pos,
-                                                            uint64_t n, unsigned long long* scal) {
-  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock) {
+                                                            uint64_t n, unsigned long long* scal, QpSegs S) {
+  const QpRange R = qp_range(S, n);
+  const QpCtx Cs = qp_ctx_of(C, S, R.s);
+  for (uint64_t i = R.i; i < R.end; i += R.step) {
     nicgpu_qp_stats st{};
     QpNullSink sink;
     // a guess past the ring's end is clamped to it (the sequential positions
     // never pass it; resolve_packet must not index past rx[nrx - 1])
-    const uint64_t rc = pos[i] < C.nrx ? (uint64_t) pos[i] : C.nrx;
-    const uint32_t popped = (uint32_t) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(C, i, rc, st, sink);
+    const uint64_t p = qp_abs(pos, S, R.s, i);
+    const uint64_t rc = p < Cs.nrx ? p : Cs.nrx;
+    const uint32_t popped = (uint32_t) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(Cs, i, rc, st, sink);
     if (popped != pops[i]) {
       atomicMin(&scal[0], (unsigned long long) i);
       pops[i] = popped;
@@ -1087,7 +1152,7 @@ __global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32
                                                            nicgpu_completion* txc, nicgpu_completion* rxc,
                                                            nicgpu_segment_write* writes, uint64_t* partials,
                                                            const uint32_t* __restrict__ guess, const unsigned long long* g,
-                                                           unsigned long long gen) {
+                                                           unsigned long long gen, QpSegs S) {
   __shared__ uint64_t red[kQpStats][kQpBlock / kWave];
   // after the per-block stats: [0] the RX descriptors used (pos[lim]), [1] the
   // first mismatch (seeded with n by qp_need_kernel) — one download for all
@@ -1096,13 +1161,16 @@ __global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32
   if (blockIdx.x == 0 && threadIdx.x == 0) tail[0] = pos[lim];
   nicgpu_qp_stats st{};
   if (qp_plan_bad(g, gen)) lim = 0;
-  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < lim; i += (uint64_t) gridDim.x * kQpBlock) {
-    if (pos[i] > C.nrx) {  // exact positions never pass the ring's end: a guess past it is wrong
+  const QpRange R = qp_range(S, lim);
+  const QpCtx Cs = qp_ctx_of(C, S, R.s);
+  for (uint64_t i = R.i; i < R.end; i += R.step) {
+    const uint64_t p = qp_abs(pos, S, R.s, i);
+    if (p > Cs.nrx) {  // exact positions never pass the ring's end: a guess past it is wrong
       if (guess) atomicMin(first, (unsigned long long) i);
       continue;
     }
-    QpDevSink sink{txc, rxc, writes, i, pos[i]};
-    const uint32_t popped = (uint32_t) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(C, i, pos[i], st, sink);
+    QpDevSink sink{txc, rxc, writes, i, p};
+    const uint32_t popped = (uint32_t) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(Cs, i, p, st, sink);
     if (guess && popped != guess[i]) atomicMin(first, (unsigned long long) i);
   }
   uint64_t v[kQpStats];
@@ -1154,6 +1222,109 @@ __global__ __launch_bounds__(kQpReduceThreads) void qp_reduce_kernel(const uint6
     }
     tail[19] = g[0] == gen ? 2u : (g[3] == gen ? 1u : 0u);
     tail[20] = g[5];
+  }
+}
+
+// Segmented batches, after a final pass and qp_reduce_kernel (one block per
+// segment): out[s * kQpSegOut ..] = segment s's 16 statistics summed over its
+// blocks' partials, then the RX descriptors its queue pair used (its pops'
+// scan across its packets); block 0 sets the settled count the delivery reads,
+// tail[2], to the whole concatenated ring when the speculative pass settled
+// every packet and to 0 otherwise (a segmented resolve settles all or nothing).
+constexpr unsigned kQpSegOut = kQpStats + 1;
+__global__ __launch_bounds__(kQpBlock) void qp_seg_reduce_kernel(const uint64_t* __restrict__ partials, QpSegs S,
+                                                                 const uint32_t* __restrict__ fb,
+                                                                 const uint32_t* __restrict__ pos, uint64_t ntx,
+                                                                 uint64_t* out, uint64_t* tail, uint64_t nrx_cat,
+                                                                 bool settle, const unsigned long long* g,
+                                                                 unsigned long long gen) {
+  __shared__ uint64_t red[kQpBlock];
+  const uint32_t s = blockIdx.x;
+  const uint32_t b0 = fb[s], nb = S.blk[b0].nb;
+  const unsigned k = threadIdx.x % kQpStats, r = threadIdx.x / kQpStats;
+  constexpr unsigned kRows = kQpBlock / kQpStats;
+  uint64_t x = 0;
+  for (unsigned b = r; b < nb; b += kRows) x += partials[(size_t) (b0 + b) * kQpStats + k];
+  red[threadIdx.x] = x;
+  __syncthreads();
+  for (unsigned h = kRows / 2; h > 0; h >>= 1) {
+    if (r < h) red[threadIdx.x] += red[threadIdx.x + h * kQpStats];
+    __syncthreads();
+  }
+  if (threadIdx.x < kQpStats) out[(size_t) s * kQpSegOut + threadIdx.x] = red[threadIdx.x];
+  if (threadIdx.x == 0) {
+    const uint64_t a = S.seg[s].tx_begin, e = qp_seg_end(S, s, ntx);
+    out[(size_t) s * kQpSegOut + kQpStats] = (uint32_t) (pos[e] - pos[a]);
+    if (s == 0 && settle) tail[2] = (!qp_plan_bad(g, gen) && tail[1] >= ntx) ? nrx_cat : 0u;
+  }
+}
+
+// the segment that RX slot j belongs to (rx_begin ascending)
+__device__ __forceinline__ uint32_t qp_seg_of_rx(const QpSegs& S, uint64_t j) {
+  uint32_t lo = 0, hi = S.nseg;  // largest s with rx_begin_s <= j
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (S.seg[mid].rx_begin <= j) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Ring slots a segment's queue pair did not use: an empty write and status
+// NICGPU_QP_SLOT_UNUSED, so the delivery writes nothing there and RSS skips
+// them.  Speculative (`first`): only when the speculative pass settled all.
+__global__ __launch_bounds__(kQpBlock) void qp_holes_kernel(QpSegs S, const uint64_t* __restrict__ segout,
+                                                            uint64_t nrx_cat, nicgpu_completion* rxc,
+                                                            nicgpu_segment_write* w, const unsigned long long* first,
+                                                            uint64_t ntx) {
+  if (first && *first < ntx) return;
+  for (uint64_t j = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; j < nrx_cat; j += (uint64_t) gridDim.x * kQpBlock) {
+    const uint32_t s = qp_seg_of_rx(S, j);
+    if (j - S.seg[s].rx_begin < segout[(size_t) s * kQpSegOut + kQpStats]) continue;
+    nicgpu_segment_write z{};
+    w[j] = z;
+    rxc[j].status = NICGPU_QP_SLOT_UNUSED;
+  }
+}
+
+// Dispatch lists of a segmented batch split per segment: split[s * nq + r] =
+// the first entry of RSS queue r's list at or past segment s's first slot
+// (lists hold absolute slots, ascending), split[nseg * nq + r] = its end.
+__global__ __launch_bounds__(kQpBlock) void qp_seg_split_kernel(QpSegs S, uint32_t nq, const uint32_t* __restrict__ which,
+                                                                const uint32_t* __restrict__ start,
+                                                                const uint32_t* __restrict__ end, uint32_t* split) {
+  const uint64_t t = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x;
+  if (t >= (uint64_t) (S.nseg + 1) * nq) return;
+  const uint32_t s = (uint32_t) (t / nq), r = (uint32_t) (t % nq);
+  uint32_t lo = start[r], hi = end[r];
+  if (s < S.nseg) {
+    const uint64_t v = S.seg[s].rx_begin;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (which[mid] < v) lo = mid + 1;
+      else hi = mid;
+    }
+  }
+  split[t] = s < S.nseg ? lo : end[r];
+}
+
+// the listed entries relative to their segment's first slot
+__global__ __launch_bounds__(kQpBlock) void qp_seg_rel_kernel(QpSegs S, uint32_t* which,
+                                                              const unsigned long long* __restrict__ count) {
+  const uint64_t m = *count;
+  for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < m; k += (uint64_t) gridDim.x * kQpBlock) {
+    const uint32_t e = which[k];
+    which[k] = e - (uint32_t) S.seg[qp_seg_of_rx(S, e)].rx_begin;
+  }
+}
+
+// per-segment RSS hits of the delivered frames
+__global__ __launch_bounds__(kQpBlock) void qp_seg_hits_kernel(QpSegs S, uint64_t nrx, const nicgpu_completion* __restrict__ rxc,
+                                                               const uint32_t* __restrict__ rx_hash, uint64_t tn,
+                                                               unsigned long long* hits) {
+  for (uint64_t j = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; j < nrx; j += (uint64_t) gridDim.x * kQpBlock) {
+    if (rxc[j].status != nicqp::kSuccess) continue;
+    atomicAdd(&hits[(uint64_t) qp_seg_of_rx(S, j) * tn + rx_hash[j] % tn], 1ull);
   }
 }
 
@@ -1301,23 +1472,63 @@ struct QpRxEnd {  // end of RX descriptor j's span; 0 when it receives nothing
 // (flag[0] stays 0); a TX span [a, b) then meets an RX span iff the first RX
 // descriptor whose running max passes a (its own end, so it has a span) starts
 // before b (flag[1]).  TX order does not matter.
+// Segmented (several queue pairs): the check is per queue pair — the spans of
+// another queue pair are the manager's business (qm_detail::queues_disjoint).
+// Each span end is keyed (segment << 48) | end, so the running max restarts at
+// every segment's first RX descriptor and a comparison across segments never
+// flags; a TX descriptor searches its own segment's ring.
+constexpr unsigned kQpSegShift = 48;
+__device__ __forceinline__ uint32_t qp_seg_of_tx(const QpSegs& S, uint64_t i) {
+  uint32_t lo = 0, hi = S.nseg;  // largest s with tx_begin_s <= i (empty segments share a tx_begin: the last)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (S.seg[mid].tx_begin <= i) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+struct QpRxEndSeg {  // QpRxEnd keyed by segment, for RX index k
+  const nicgpu_rx_descriptor* rx;
+  QpSegs S;
+  uint64_t mem_size;
+  __host__ __device__ uint64_t operator()(uint64_t k) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint64_t key = S.seg ? (uint64_t) qp_seg_of_rx(S, k) << kQpSegShift : 0u;
+    return key | QpRxEnd{mem_size}(rx[k]);
+#else
+    (void) k;
+    return 0;
+#endif
+  }
+};
+
 __global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t ntx,
                                                             const nicgpu_rx_descriptor* __restrict__ rx, uint64_t nrx,
                                                             uint64_t mem_size, const uint64_t* __restrict__ end_max,
-                                                            unsigned long long* flag, unsigned long long gen) {
+                                                            unsigned long long* flag, unsigned long long gen, QpSegs S) {
   const uint64_t n = ntx > nrx ? ntx : nrx;
   for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < n; k += (uint64_t) gridDim.x * kQpBlock) {
-    if (k < nrx && k > 0 && QpRxEnd{mem_size}(rx[k]) != 0 && rx[k].buffer_address < end_max[k - 1]) flag[0] = gen;
+    if (k < nrx && k > 0 && QpRxEnd{mem_size}(rx[k]) != 0) {
+      const uint64_t key = S.seg ? (uint64_t) qp_seg_of_rx(S, k) << kQpSegShift : 0u;
+      if ((key | rx[k].buffer_address) < end_max[k - 1]) flag[0] = gen;
+    }
     if (k < ntx) {
       const uint64_t a = tx[k].buffer_address, len = tx[k].length;
       if (len == 0 || !nicqp::dma_ok(mem_size, a, len)) continue;
-      uint64_t lo = 0, hi = nrx;
+      uint64_t lo = 0, hi = nrx, key = 0;
+      if (S.seg) {
+        const uint32_t s = qp_seg_of_tx(S, k);
+        lo = S.seg[s].rx_begin;
+        hi = lo + S.seg[s].nrx;
+        key = (uint64_t) s << kQpSegShift;
+      }
+      const uint64_t ring_end = hi;
       while (lo < hi) {
         const uint64_t mid = lo + (hi - lo) / 2;
-        if (end_max[mid] <= a) lo = mid + 1;
+        if (end_max[mid] <= (key | a)) lo = mid + 1;
         else hi = mid;
       }
-      if (lo < nrx && rx[lo].buffer_address < a + len) flag[1] = gen;
+      if (lo < ring_end && rx[lo].buffer_address < a + len) flag[1] = gen;
     }
   }
 }
@@ -1398,6 +1609,22 @@ struct nicgpu_qp {
     unsigned grid = 1;
   } res;
   bool delivered = false;  // the RSS results are per completion (nicgpu_qp_deliver), not compacted
+  // segmented batches (nicgpu_qp_set_segments): the segment table, the block
+  // map of the per-TX launches (seg_grid blocks), each segment's first block,
+  // the per-segment results (stats + RX used) on the device and page-locked
+  uint32_t nseg = 0;
+  unsigned seg_grid = 0;
+  uint64_t seg_ntx = 0, seg_nrx = 0;  // the batch the map was made for; the concatenated ring's length
+  nicgpu_qp_segment* d_seg = nullptr;
+  QpBlk* d_blk = nullptr;
+  uint32_t* d_fb = nullptr;
+  uint64_t* d_segout = nullptr;
+  uint32_t* d_split = nullptr;
+  size_t c_seg = 0, c_blk = 0, c_fb = 0, c_segout = 0, c_split = 0;
+  uint64_t* seg_hp = nullptr;  // page-locked: nseg * kQpSegOut
+  size_t c_seg_hp = 0;
+  void* seg_stage = nullptr;   // page-locked staging of the table and the map
+  size_t c_seg_stage = 0;
 };
 
 namespace {
@@ -1428,6 +1655,13 @@ unsigned qp_grid(const nicgpu_qp* q, uint64_t n) {
   return (unsigned) (want < q->grid ? (want ? want : 1) : q->grid);
 }
 
+QpSegs qp_segs(const nicgpu_qp* q) {
+  return q->nseg ? QpSegs{q->d_seg, q->d_blk, q->nseg} : QpSegs{nullptr, nullptr, 0u};
+}
+
+// the grid of a per-TX launch over n descriptors: the block map's when segmented
+unsigned qp_tx_grid(const nicgpu_qp* q, uint64_t n) { return q->nseg ? q->seg_grid : qp_grid(q, n); }
+
 // hipcub exclusive sum of in[0, n) into out[0, n) (n includes the trailing 0)
 int qp_scan(nicgpu_qp* q, const uint32_t* in, uint32_t* out, size_t n, hipStream_t s) {
   size_t tb = 0;
@@ -1435,6 +1669,28 @@ int qp_scan(nicgpu_qp* q, const uint32_t* in, uint32_t* out, size_t n, hipStream
   int st = qp_grow(q->tmp, q->c_tmp, tb);
   if (st != NICGPU_OK) return st;
   return hip_status(hipcub::DeviceScan::ExclusiveSum(q->tmp, tb, in, out, (int) n, s));
+}
+
+// After a segmented final pass and its qp_reduce_kernel: per-segment stats and
+// RX used (qp_seg_reduce_kernel), the unused ring slots marked (speculative:
+// only if everything settled), the results down into seg_hp.
+int qp_seg_finish(nicgpu_qp* q, uint64_t ntx, bool speculative, hipStream_t s) {
+  const QpSegs S = qp_segs(q);
+  uint64_t* tail = q->partials + (size_t) q->seg_grid * kQpStats;
+  hipLaunchKernelGGL(qp_seg_reduce_kernel, dim3(q->nseg), dim3(kQpBlock), 0, s, q->partials, S, q->d_fb, q->pos, ntx,
+                     q->d_segout, tail, q->seg_nrx, speculative, q->gflags, q->plan_gen);
+  int st = hip_status(hipGetLastError());
+  if (st != NICGPU_OK) return st;
+  if (q->seg_nrx) {
+    hipLaunchKernelGGL(qp_holes_kernel, dim3(qp_grid(q, q->seg_nrx)), dim3(kQpBlock), 0, s, S, q->d_segout, q->seg_nrx,
+                       q->rxc, q->writes, speculative ? reinterpret_cast<const unsigned long long*>(tail + 1) : nullptr,
+                       ntx);
+    st = hip_status(hipGetLastError());
+  }
+  if (st == NICGPU_OK)
+    st = hip_status(hipMemcpyAsync(q->seg_hp, q->d_segout, (size_t) q->nseg * kQpSegOut * sizeof(uint64_t),
+                                   hipMemcpyDeviceToHost, s));
+  return st;
 }
 
 }  // namespace
@@ -1483,10 +1739,13 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
   void* bufs[] = {q->tx_own, q->rx_own, q->tmp_chk, q->plans, q->counts, q->base, q->need, q->pos, q->piece_desc, q->piece_csum,
                   q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
                   q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sort_key, q->sorted_key, q->queue_which,
-                  q->queue_start, q->queue_end, q->end_max, q->dlv_acc, q->dlv_done, q->gflags, q->piece_cs4};
+                  q->queue_start, q->queue_end, q->end_max, q->dlv_acc, q->dlv_done, q->gflags, q->piece_cs4,
+                  q->d_seg, q->d_blk, q->d_fb, q->d_segout, q->d_split};
   for (void* b : bufs)
     if (b) (void) hipFree(b);
   if (q->hp) (void) hipHostFree(q->hp);
+  if (q->seg_hp) (void) hipHostFree(q->seg_hp);
+  if (q->seg_stage) (void) hipHostFree(q->seg_stage);
   if (q->planned) (void) hipEventDestroy(q->planned);
   if (q->resolved) (void) hipEventDestroy(q->resolved);
   delete q;
@@ -1552,11 +1811,12 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(plan_stream);
   *npieces = 0;
-  const unsigned grid = qp_grid(q, ntx + 1);
+  if (q->nseg && ntx != q->seg_ntx) return NICGPU_ERR_INVALID;  // the block map is the batch's
+  const unsigned grid = qp_tx_grid(q, ntx + 1);
   const unsigned long long gen = ++q->gen;
   q->plan_gen = gen;
   hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->counts, q->gflags, gen);
+                     q->plans, q->counts, q->gflags, gen, qp_segs(q));
   int st = hip_status(hipGetLastError());
   uint32_t* np_h = reinterpret_cast<uint32_t*>(q->misc());
   uint64_t* ovf_h = q->misc() + 5;
@@ -1573,7 +1833,7 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
   if (st == NICGPU_OK) st = qp_grow(q->piece_cs4, q->c_pcs4, np ? np : 1);
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->base, q->piece_desc, (uint64_t) q->c_pdesc, q->gflags, gen);
+                     q->plans, q->base, q->piece_desc, (uint64_t) q->c_pdesc, q->gflags, gen, qp_segs(q));
   st = hip_status(hipGetLastError());
   if (st == NICGPU_OK && sums_stream != plan_stream) {  // the sums read the pieces the fill wrote
     st = hip_status(hipEventRecord(q->planned, s));
@@ -1599,17 +1859,18 @@ int nicgpu_qp_plan_async(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, si
   if (st == NICGPU_OK) st = qp_grow(q->piece_cs4, q->c_pcs4, want);
   if (st != NICGPU_OK) return st;
   const uint64_t cap = std::min(q->c_pdesc, std::min(q->c_pcs, q->c_pcs4));
-  const unsigned grid = qp_grid(q, ntx + 1);
+  if (q->nseg && ntx != q->seg_ntx) return NICGPU_ERR_INVALID;  // the block map is the batch's
+  const unsigned grid = qp_tx_grid(q, ntx + 1);
   const unsigned long long gen = ++q->gen;
   q->plan_gen = gen;
   q->np = 0;  // known once resolved (nicgpu_qp_piece_count)
   hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->counts, q->gflags, gen);
+                     q->plans, q->counts, q->gflags, gen, qp_segs(q));
   st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_fill_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->base, q->piece_desc, cap, q->gflags, gen);
+                     q->plans, q->base, q->piece_desc, cap, q->gflags, gen, qp_segs(q));
   st = hip_status(hipGetLastError());
   if (st == NICGPU_OK && sums_stream != plan_stream) {
     st = hip_status(hipEventRecord(q->planned, s));
@@ -1630,13 +1891,29 @@ int nicgpu_qp_piece_count(const nicgpu_qp* q, uint64_t* npieces) {
 }
 
 int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int* verdict, void* stream) {
-  if (!q || !verdict || ntx > q->cap_tx || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  return nicgpu_qp_check_flags(q, mem_size, ntx, nrx, 0u, verdict, stream);
+}
+
+int nicgpu_qp_check_flags(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, unsigned flags, int* verdict,
+                          void* stream) {
+  if (!q || !verdict || ntx > q->cap_tx || nrx > q->cap_rx || (flags & ~NICGPU_QP_CHECK_WHOLE)) return NICGPU_ERR_INVALID;
+  const bool segmented = q->nseg && !(flags & NICGPU_QP_CHECK_WHOLE);
   *verdict = -1;
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned long long gen = ++q->gen;
   int st = NICGPU_OK;
-  if (nrx) {
+  if (segmented && (ntx != q->seg_ntx || nrx != q->seg_nrx)) return NICGPU_ERR_INVALID;
+  if (nrx && segmented) {  // per queue pair: ends keyed by segment
+    hipcub::TransformInputIterator<uint64_t, QpRxEndSeg, hipcub::CountingInputIterator<uint64_t>> ends(
+        hipcub::CountingInputIterator<uint64_t>(0), QpRxEndSeg{q->rx, qp_segs(q), mem_size});
+    size_t tb = 0;
+    if (hipcub::DeviceScan::InclusiveScan(nullptr, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s) != hipSuccess)
+      return NICGPU_ERR_HIP;
+    st = qp_grow(q->tmp_chk, q->c_tmp_chk, tb);
+    if (st == NICGPU_OK)
+      st = hip_status(hipcub::DeviceScan::InclusiveScan(q->tmp_chk, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s));
+  } else if (nrx) {
     hipcub::TransformInputIterator<uint64_t, QpRxEnd, const nicgpu_rx_descriptor*> ends(q->rx, QpRxEnd{mem_size});
     size_t tb = 0;
     if (hipcub::DeviceScan::InclusiveScan(nullptr, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s) != hipSuccess)
@@ -1649,7 +1926,8 @@ int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int
   const uint64_t n = ntx > nrx ? ntx : nrx;
   if (n) {
     hipLaunchKernelGGL(qp_check_kernel, dim3(qp_grid(q, n)), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, q->rx,
-                       (uint64_t) nrx, mem_size, q->end_max, q->gflags + 1, gen);
+                       (uint64_t) nrx, mem_size, q->end_max, q->gflags + 1, gen,
+                       segmented ? qp_segs(q) : QpSegs{nullptr, nullptr, 0u});
     st = hip_status(hipGetLastError());
   }
   uint64_t* f = q->misc() + 1;
@@ -1666,25 +1944,28 @@ int nicgpu_qp_resolve_start(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t 
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   q->res = nicgpu_qp::Pending{};
+  if (q->nseg && (ntx != q->seg_ntx || nrx != q->seg_nrx)) return NICGPU_ERR_INVALID;
   QpCtx C{queue_id, max_mtu, mem_size, q->plans, q->piece_csum, q->piece_cs4, q->tx, q->rx, (uint64_t) nrx};
-  const unsigned grid = qp_grid(q, ntx + 1);
+  const QpSegs S = qp_segs(q);
+  const unsigned grid = qp_tx_grid(q, ntx + 1);
   uint64_t* tail = q->partials + (size_t) grid * kQpStats;
   // first guess: every packet pops what it needs (rx_need).  The final pass
   // runs on it speculatively and reports the first packet that popped
   // otherwise; a batch that settles at once (uniform RX descriptors, no early
   // ends) needs no relaxation step and no host round trip before its DMA writes.
   hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, (uint64_t) ntx, q->need,
-                     reinterpret_cast<unsigned long long*>(tail + 1), q->gflags, q->plan_gen);
+                     reinterpret_cast<unsigned long long*>(tail + 1), q->gflags, q->plan_gen, S);
   int st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, (uint64_t) ntx, q->txc, q->rxc,
-                     q->writes, q->partials, q->need, q->gflags, q->plan_gen);
+                     q->writes, q->partials, q->need, q->gflags, q->plan_gen, S);
   st = hip_status(hipGetLastError());
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_reduce_kernel, dim3(1), dim3(kQpReduceThreads), 0, s, q->partials, grid, q->pos,
                      (uint64_t) ntx, true, q->gflags, q->plan_gen);
   st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK && q->nseg) st = qp_seg_finish(q, ntx, true, s);
   if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->hp, tail, kQpTail * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   if (st == NICGPU_OK) st = hip_status(hipEventRecord(q->resolved, s));
   if (st != NICGPU_OK) return st;
@@ -1701,6 +1982,7 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
   hipStream_t s = R.s;
   const uint64_t ntx = R.ntx;
   QpCtx C{R.queue_id, R.max_mtu, R.mem_size, q->plans, q->piece_csum, q->piece_cs4, q->tx, q->rx, R.nrx};
+  const QpSegs S = qp_segs(q);
   const unsigned grid = R.grid;
   const uint64_t* part = q->hp;  // the tail, kQpTail words (page-locked)
   uint64_t* tail = q->partials + (size_t) grid * kQpStats;
@@ -1725,7 +2007,7 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
       q->misc()[4] = ntx;  // page-locked source; the step below waits for the stream
       if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->scal, q->misc() + 4, sizeof(uint64_t), hipMemcpyHostToDevice, s));
       if (st != NICGPU_OK) break;
-      hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, ntx, q->scal);
+      hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, ntx, q->scal, S);
       st = hip_status(hipGetLastError());
       if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->misc() + 3, q->scal, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
       if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
@@ -1735,9 +2017,12 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
       lim = first < ntx ? (uint64_t) first : ntx;
       if (first >= ntx || it + 1 == kQpRelaxSteps) break;
     }
+    // a segmented batch settles all or nothing (nothing was delivered: the
+    // speculative pass's settled count was 0)
+    if (st == NICGPU_OK && q->nseg && lim < ntx) return NICGPU_ERR_UNSETTLED;
     if (st == NICGPU_OK) {
       hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, lim, q->txc, q->rxc, q->writes,
-                         q->partials, static_cast<const uint32_t*>(nullptr), q->gflags, q->plan_gen);
+                         q->partials, static_cast<const uint32_t*>(nullptr), q->gflags, q->plan_gen, S);
       st = hip_status(hipGetLastError());
     }
     if (st == NICGPU_OK) {
@@ -1745,12 +2030,14 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
                          q->gflags, q->plan_gen);
       st = hip_status(hipGetLastError());
     }
+    if (st == NICGPU_OK && q->nseg) st = qp_seg_finish(q, ntx, false, s);
     if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->hp, tail, kQpTail * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
     if (st != NICGPU_OK) return st;
     used = part[0];
   }
   std::memcpy(stats, part + 3, kQpStats * sizeof(uint64_t));
+  if (q->nseg) used = q->seg_nrx;  // every slot of the concatenated ring (the unused ones marked)
   *done = lim;
   *rx_used = used;
   if (rx_settled) *rx_settled = settled < used ? settled : used;
@@ -1926,6 +2213,124 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
 #endif
   }
   return launch_deliver<0>(P, rss, di->cus, s);
+}
+
+int nicgpu_qp_set_segments(nicgpu_qp* q, const nicgpu_qp_segment* seg, size_t nseg, size_t ntx, void* stream) {
+  if (!q || nseg > NICGPU_QP_MAX_SEGMENTS || (nseg && !seg)) return NICGPU_ERR_INVALID;
+  if (nseg == 0) {
+    q->nseg = 0;
+    return NICGPU_OK;
+  }
+  // the segments partition [0, ntx) and the concatenated ring, in order
+  uint64_t rx_end = 0;
+  for (size_t k = 0; k < nseg; ++k) {
+    if (seg[k].tx_begin > ntx || (k && seg[k].tx_begin < seg[k - 1].tx_begin) || seg[k].rx_begin != rx_end)
+      return NICGPU_ERR_INVALID;
+    rx_end += seg[k].nrx;
+  }
+  if (seg[0].tx_begin != 0 || ntx > q->cap_tx || rx_end > q->cap_rx) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // blocks in proportion to the segments' TX descriptors, at least one each
+  const uint64_t want = std::max<uint64_t>((ntx + kQpBlock - 1) / kQpBlock, nseg);
+  const uint64_t G = std::min<uint64_t>(std::max<uint64_t>(want, nseg), std::max<uint64_t>(q->grid, nseg));
+  if (G > q->grid) return NICGPU_ERR_INVALID;  // partials hold q->grid blocks
+  std::vector<QpBlk> blk;
+  std::vector<uint32_t> fb(nseg);
+  blk.reserve(G);
+  const uint64_t spare = G - nseg;
+  for (size_t k = 0; k < nseg; ++k) {
+    const uint64_t e = k + 1 < nseg ? seg[k + 1].tx_begin : ntx;
+    const uint64_t n = e - seg[k].tx_begin;
+    const uint64_t nb = 1 + (ntx ? spare * n / ntx : 0);
+    fb[k] = (uint32_t) blk.size();
+    for (uint64_t r = 0; r < nb; ++r) blk.push_back(QpBlk{(uint32_t) k, (uint32_t) r, (uint32_t) nb, 0u});
+  }
+  int st = qp_grow(q->d_seg, q->c_seg, nseg);
+  if (st == NICGPU_OK) st = qp_grow(q->d_blk, q->c_blk, blk.size());
+  if (st == NICGPU_OK) st = qp_grow(q->d_fb, q->c_fb, nseg);
+  if (st == NICGPU_OK) st = qp_grow(q->d_segout, q->c_segout, nseg * kQpSegOut);
+  if (st != NICGPU_OK) return st;
+  const size_t b_seg = nseg * sizeof(nicgpu_qp_segment), b_blk = blk.size() * sizeof(QpBlk), b_fb = nseg * 4;
+  const size_t need = b_seg + b_blk + b_fb;
+  if (need > q->c_seg_stage || nseg * kQpSegOut > q->c_seg_hp) {
+    // the previous batch's copies out of the staging may still be in flight
+    if (hipStreamSynchronize(s) != hipSuccess) return NICGPU_ERR_HIP;
+    if (need > q->c_seg_stage) {
+      if (q->seg_stage) (void) hipHostFree(q->seg_stage);
+      q->seg_stage = nullptr;
+      q->c_seg_stage = 0;
+      if (hipHostMalloc(&q->seg_stage, need * 2) != hipSuccess) return NICGPU_ERR_NOMEM;
+      q->c_seg_stage = need * 2;
+    }
+    if (nseg * kQpSegOut > q->c_seg_hp) {
+      if (q->seg_hp) (void) hipHostFree(q->seg_hp);
+      q->seg_hp = nullptr;
+      q->c_seg_hp = 0;
+      if (hipHostMalloc(reinterpret_cast<void**>(&q->seg_hp), nseg * kQpSegOut * sizeof(uint64_t)) != hipSuccess)
+        return NICGPU_ERR_NOMEM;
+      q->c_seg_hp = nseg * kQpSegOut;
+    }
+  } else if (hipStreamSynchronize(s) != hipSuccess) {  // the staging is reused: its last copies done
+    return NICGPU_ERR_HIP;
+  }
+  auto* st8 = static_cast<uint8_t*>(q->seg_stage);
+  std::memcpy(st8, seg, b_seg);
+  std::memcpy(st8 + b_seg, blk.data(), b_blk);
+  std::memcpy(st8 + b_seg + b_blk, fb.data(), b_fb);
+  st = hip_status(hipMemcpyAsync(q->d_seg, st8, b_seg, hipMemcpyHostToDevice, s));
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->d_blk, st8 + b_seg, b_blk, hipMemcpyHostToDevice, s));
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->d_fb, st8 + b_seg + b_blk, b_fb, hipMemcpyHostToDevice, s));
+  if (st != NICGPU_OK) return st;
+  q->nseg = (uint32_t) nseg;
+  q->seg_grid = (unsigned) blk.size();
+  q->seg_ntx = ntx;
+  q->seg_nrx = rx_end;
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_segment_results(const nicgpu_qp* q, uint64_t* used, nicgpu_qp_stats* stats) {
+  if (!q || !q->nseg || !used || !stats) return NICGPU_ERR_INVALID;
+  for (uint32_t k = 0; k < q->nseg; ++k) {
+    std::memcpy(&stats[k], q->seg_hp + (size_t) k * kQpSegOut, sizeof(nicgpu_qp_stats));
+    used[k] = q->seg_hp[(size_t) k * kQpSegOut + kQpStats];
+  }
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_segment_lists(nicgpu_qp* q, size_t nrx, size_t nq, uint32_t* split_host, void* stream) {
+  if (!q || !q->nseg || !split_host || nrx > q->cap_rx || nq > 65536) return NICGPU_ERR_INVALID;
+  const size_t ns = (size_t) (q->nseg + 1) * nq;
+  if (ns == 0) return NICGPU_OK;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int st = qp_grow(q->d_split, q->c_split, ns);
+  if (st != NICGPU_OK) return st;
+  const QpSegs S = qp_segs(q);
+  hipLaunchKernelGGL(qp_seg_split_kernel, dim3((unsigned) ((ns + kQpBlock - 1) / kQpBlock)), dim3(kQpBlock), 0, s, S,
+                     (uint32_t) nq, q->queue_which, q->queue_start, q->queue_end, q->d_split);
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK && nrx) {
+    hipLaunchKernelGGL(qp_seg_rel_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, S, q->queue_which,
+                       reinterpret_cast<const unsigned long long*>(q->scal + 3));
+    st = hip_status(hipGetLastError());
+  }
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(split_host, q->d_split, ns * 4, hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  return st;
+}
+
+int nicgpu_qp_segment_hits(nicgpu_qp* q, size_t nrx, size_t table_n, uint64_t* hits_dev, void* stream) {
+  if (!q || !q->nseg || !hits_dev || table_n == 0 || nrx > q->cap_rx) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int st = hip_status(hipMemsetAsync(hits_dev, 0, (size_t) q->nseg * table_n * sizeof(uint64_t), s));
+  if (st == NICGPU_OK && nrx) {
+    hipLaunchKernelGGL(qp_seg_hits_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, qp_segs(q), (uint64_t) nrx,
+                       q->rxc, q->rx_hash, (uint64_t) table_n, reinterpret_cast<unsigned long long*>(hits_dev));
+    st = hip_status(hipGetLastError());
+  }
+  return st;
 }
 
 }  // extern "C"

@@ -246,6 +246,34 @@ BatchedQueueManager::BatchedQueueManager(BatchedQueueManagerConfig config) : str
     qps_.push_back(std::make_unique<Queue>(c));
   }
   credit_ = weights_.empty() ? 0 : weights_.front();
+  if (!qps_.empty()) {
+    fused_ = std::make_unique<BatchedQueuePair>(Queue::quiet(qps_.front()->config));
+    for (auto& qp : qps_) qp->stage.share_image(*fused_);  // one HBM mirror of a HostMemory for all
+  }
+}
+
+// The fused batch needs the queue pairs' stage settings to agree: device
+// resolve on, results kept alike, RSS off everywhere or engines whose key,
+// table and tuple are equal (each still counts its own frames).
+bool BatchedQueueManager::fusable() const {
+  if (qps_.empty() || qps_.size() > NICGPU_QP_MAX_SEGMENTS) return false;
+  const BatchedQueuePairConfig& c0 = qps_.front()->config;
+  for (const auto& qp : qps_) {
+    const BatchedQueuePairConfig& c = qp->config;
+    if (!c.device_resolve || c.results_on_device != c0.results_on_device || (c.rss == nullptr) != (c0.rss == nullptr))
+      return false;
+    if (c.rss && c.rss != c0.rss) {
+      if (c.tuple.mode != c0.tuple.mode || c.tuple.raw_offset != c0.tuple.raw_offset ||
+          c.tuple.raw_length != c0.tuple.raw_length)
+        return false;
+      const RssConfig &a = c.rss->config(), &b = c0.rss->config();
+      if (a.key != b.key || a.table != b.table) return false;
+    } else if (c.rss && (c.tuple.mode != c0.tuple.mode || c.tuple.raw_offset != c0.tuple.raw_offset ||
+                         c.tuple.raw_length != c0.tuple.raw_length)) {
+      return false;
+    }
+  }
+  return true;
 }
 
 BatchedQueueManager::~BatchedQueueManager() = default;
@@ -261,6 +289,68 @@ std::optional<QueuePairStats> BatchedQueueManager::queue_stats(std::size_t index
 
 QueueSchedule BatchedQueueManager::process_batch(const DeviceHostMemory& mem, std::span<const QueueBatch> batches,
                                                  std::vector<RxBatchResult>& out, void* stream) {
+  return run(mem, nullptr, batches, out, stream);
+}
+
+QueueSchedule BatchedQueueManager::process_batch(HostMemory& mem, std::span<const QueueBatch> batches,
+                                                 std::vector<RxBatchResult>& out, void* stream) {
+  return run(DeviceHostMemory{}, &mem, batches, out, stream);
+}
+
+QueueSchedule BatchedQueueManager::process_batch(const DeviceHostMemory& mem, std::span<const DeviceQueueBatch> batches,
+                                                 std::vector<RxBatchResult>& out, void* stream) {
+  const std::size_t Q = qps_.size();
+  if (batches.size() != Q) throw std::invalid_argument("BatchedQueueManager::process_batch: one batch per queue pair");
+  for (const DeviceQueueBatch& b : batches)
+    if ((b.ntx && !b.tx) || (b.nrx && !b.rx)) throw GpuError("process_batch: null device descriptors", NICGPU_ERR_INVALID);
+  if (fusable()) {
+    std::vector<std::span<const TxDescriptor>> txs(Q);
+    std::vector<std::span<const RxDescriptor>> rxs(Q);
+    std::vector<BatchedQueuePairConfig> cfgs(Q);
+    std::vector<std::size_t> n(Q);
+    for (std::size_t q = 0; q < Q; ++q) {
+      txs[q] = {batches[q].tx, batches[q].ntx};
+      rxs[q] = {batches[q].rx, batches[q].nrx};
+      cfgs[q] = qps_[q]->config;
+      n[q] = batches[q].ntx;
+    }
+    for (RxBatchResult& r : out) clear_result(r);
+    std::vector<QueuePairStats> st;
+    if (fused_->process_queues(mem, nullptr, txs, rxs, cfgs, out, st, stream, /*dev_desc=*/true, /*whole_check=*/true)) {
+      for (std::size_t q = 0; q < Q; ++q) add_delta(qps_[q]->stats, st[q], QueuePairStats{});
+      std::size_t index = index_, credit = credit_;
+      QueueSchedule sched = qm_detail::schedule(weights_, n, index, credit);
+      index_ = index;
+      credit_ = credit;
+      advances_ += sched.advances;
+      skips_ += sched.skips;
+      last_fused_ = 1;
+      replay(sched, out, stream);
+      return sched;
+    }
+  }
+  // the host decides: the descriptors come down once
+  std::vector<std::vector<TxDescriptor>> htx(Q);
+  std::vector<std::vector<RxDescriptor>> hrx(Q);
+  std::vector<QueueBatch> hb(Q);
+  auto ok = [](int st, const char* what) {
+    if (st != NICGPU_OK) throw GpuError(std::string("BatchedQueueManager: ") + what, st);
+  };
+  for (std::size_t q = 0; q < Q; ++q) {
+    htx[q].resize(batches[q].ntx);
+    hrx[q].resize(batches[q].nrx);
+    if (batches[q].ntx)
+      ok(nicgpu_memcpy_async(htx[q].data(), batches[q].tx, batches[q].ntx * sizeof(TxDescriptor), stream), "nicgpu_memcpy_async");
+    if (batches[q].nrx)
+      ok(nicgpu_memcpy_async(hrx[q].data(), batches[q].rx, batches[q].nrx * sizeof(RxDescriptor), stream), "nicgpu_memcpy_async");
+  }
+  ok(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+  for (std::size_t q = 0; q < Q; ++q) hb[q] = QueueBatch{htx[q], hrx[q]};
+  return run(mem, nullptr, hb, out, stream);
+}
+
+QueueSchedule BatchedQueueManager::run(const DeviceHostMemory& dmem, HostMemory* hmem, std::span<const QueueBatch> batches,
+                                       std::vector<RxBatchResult>& out, void* stream) {
   const std::size_t Q = qps_.size();
   if (batches.size() != Q) throw std::invalid_argument("BatchedQueueManager::process_batch: one batch per queue pair");
   std::vector<std::size_t> n(Q);
@@ -269,7 +359,41 @@ QueueSchedule BatchedQueueManager::process_batch(const DeviceHostMemory& mem, st
   for (RxBatchResult& r : out) clear_result(r);
   std::size_t index = index_, credit = credit_;
   QueueSchedule sched = qm_detail::schedule(weights_, n, index, credit);
-  if (qm_detail::queues_disjoint(mem.size, batches)) {
+  // a HostMemory: the manager's one mirror of it (every stage shares it)
+  BatchedQueuePair::HostImage* img = hmem ? &fused_->bind_image(*hmem) : nullptr;
+  const std::size_t mem_size = hmem ? hmem->config().size_bytes : dmem.size;
+  last_fused_ = 0;
+  bool fused = false;
+  const bool disjoint = qm_detail::queues_disjoint(mem_size, batches);
+  if (disjoint && fusable()) {
+    std::vector<std::span<const TxDescriptor>> txs(Q);
+    std::vector<std::span<const RxDescriptor>> rxs(Q);
+    std::vector<BatchedQueuePairConfig> cfgs(Q);
+    for (std::size_t q = 0; q < Q; ++q) {
+      txs[q] = batches[q].tx;
+      rxs[q] = batches[q].rx;
+      cfgs[q] = qps_[q]->config;
+    }
+    std::vector<QueuePairStats> st;
+    fused = fused_->process_queues(dmem, img, txs, rxs, cfgs, out, st, stream);
+    if (fused) {
+      for (std::size_t q = 0; q < Q; ++q) add_delta(qps_[q]->stats, st[q], QueuePairStats{});
+      last_fused_ = 1;
+    }
+  }
+  if (fused) {
+    // done: scheduler state and interrupts below
+  } else if (disjoint && hmem) {
+    // one mirror: the queue pairs one after another (their buffers are apart,
+    // so the order does not matter)
+    for (std::size_t q = 0; q < Q; ++q) {
+      if (!n[q]) continue;
+      const QueuePairStats b = qps_[q]->stage.stats();
+      qps_[q]->stage.process_batch(*hmem, batches[q].tx, batches[q].rx, out[q], stream);
+      add_delta(qps_[q]->stats, qps_[q]->stage.stats(), b);
+    }
+  } else if (disjoint) {
+    const DeviceHostMemory& mem = dmem;
     // each queue pair's results do not depend on the interleaving: every
     // queue's batch on its own stage, all in flight at once — unless two share
     // an RssEngine (its statistics are not shared across job threads)
@@ -331,9 +455,11 @@ QueueSchedule BatchedQueueManager::process_batch(const DeviceHostMemory& mem, st
     for (const QueueSchedule::Run& run : sched.runs) {
       Queue& qp = *qps_[run.queue];
       BatchedQueuePair& h = qp.host_stage();
+      if (hmem) h.share_image(*fused_);
       const QueuePairStats b = h.stats();
       const QueueBatch& B = batches[run.queue];
-      h.process_batch(mem, B.tx.subspan(ti[run.queue], run.count), B.rx.subspan(ri[run.queue]), part, stream);
+      if (hmem) h.process_batch(*hmem, B.tx.subspan(ti[run.queue], run.count), B.rx.subspan(ri[run.queue]), part, stream);
+      else h.process_batch(dmem, B.tx.subspan(ti[run.queue], run.count), B.rx.subspan(ri[run.queue]), part, stream);
       add_delta(qp.stats, h.stats(), b);
       append_result(out[run.queue], part);
       ti[run.queue] += run.count;
@@ -344,7 +470,13 @@ QueueSchedule BatchedQueueManager::process_batch(const DeviceHostMemory& mem, st
   credit_ = credit;
   advances_ += sched.advances;
   skips_ += sched.skips;
-  // interrupts in the order the reference's dispatcher sees them: run by run
+  replay(sched, out, stream);
+  return sched;
+}
+
+// interrupts in the order the reference's dispatcher sees them: run by run
+void BatchedQueueManager::replay(const QueueSchedule& sched, const std::vector<RxBatchResult>& out, void* stream) {
+  const std::size_t Q = qps_.size();
   bool any = false;
   for (const auto& qp : qps_) any |= qp->config.on_interrupt && (qp->config.enable_tx_interrupts || qp->config.enable_rx_interrupts);
   if (any) {
@@ -371,7 +503,6 @@ QueueSchedule BatchedQueueManager::process_batch(const DeviceHostMemory& mem, st
     for (const QueueSchedule::Run& run : sched.runs)
       rx_stage_detail::replay_interrupts(qps_[run.queue]->config, txc[run.queue], rxc[run.queue], at[run.queue], run.count);
   }
-  return sched;
 }
 
 void BatchedQueueManager::reset() {

@@ -1065,6 +1065,13 @@ struct BatchedQueuePair::Slot {
   std::vector<Slot*> dep_stage, dep_rx;
   std::vector<rx_stage_detail::SegmentWrite> applied;
   DevBuf wbuf, stage_tx;
+  // a manager's fused batch (process_queues): nseg queue pairs; their RSS
+  // dispatch lists split per queue pair (split, (nseg + 1) x nq) and, when
+  // they count into RssEngines of their own, their hits (seg_hits, nseg x tn)
+  bool multi = false, seg_hits_on = false;
+  std::size_t nseg = 0;
+  HostBuf h_split, h_seg_hits;
+  DevBuf seg_hits;
 
   void release_rss() {
     if (!rss_released) rss_recorded.set_value();
@@ -1137,7 +1144,7 @@ struct BatchedQueuePair::Scratch {
   void* side_down = nullptr;
   void* side_plan = nullptr;  // plan and overlap check of a batch beside the earlier batch's writes
   void* side_wb = nullptr;    // host-image write-backs, beside the next batches' work
-  HostImage img;              // the HostMemory the host-image batches run against
+  std::shared_ptr<HostImage> img = std::make_shared<HostImage>();  // the HostMemory the host-image batches run against (shared by a manager's stages)
   SideWorker up_worker;  // process_batch: issues the RX descriptor uploads
   static constexpr unsigned kSlots = 3;
   Slot slot[kSlots];
@@ -1150,7 +1157,7 @@ struct BatchedQueuePair::Scratch {
     if (side_plan) (void) nicgpu_stream_destroy(side_plan);
     if (side_wb) (void) nicgpu_stream_destroy(side_wb);
     side_up = side_down = side_plan = side_wb = nullptr;
-    img.release();
+    if (img.use_count() == 1) img->release();  // a manager's shared image is released by its last stage
     device = -1;
   }
   void ensure(int dev) {
@@ -1341,6 +1348,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
     sl.rx_dev = nullptr;
     sl.image = nullptr;
     sl.staged = false;
+    sl.multi = false;
     sl.dep_stage.clear();
     sl.dep_rx.clear();
     upload(sl, tx, rx, true);
@@ -1386,6 +1394,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDe
   sl.fetched = false;
   sl.image = nullptr;
   sl.staged = false;
+  sl.multi = false;
   sl.dep_stage.clear();
   sl.dep_rx.clear();
   check(nicgpu_event_record(sl.ev_submit, stream), "nicgpu_event_record");  // a producer's writes before this call
@@ -1486,6 +1495,7 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
   Slot& sl = S.slot[(S.head + S.pending) % Scratch::kSlots];
   sl.image = nullptr;
   sl.staged = false;
+  sl.multi = false;
   sl.dep_stage.clear();
   sl.dep_rx.clear();
   if (img) image_prepare(sl, *img, tx, rx);  // dependencies on the batches pending now
@@ -1510,7 +1520,7 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
   // unless they overlap bytes an earlier pending batch delivers: then its job
   // stages them after that batch's write-back (recorded by the earlier job)
   sl.stage_deferred = img && !sl.dep_stage.empty();
-  if (img && !sl.stage_deferred) image_stage(sl, tx, device ? sl.v.tx : nullptr, S.side_up);
+  if (img && !sl.stage_deferred) image_stage(sl, tx.size(), tx.data(), device ? sl.v.tx : nullptr, S.side_up);
   sl.job_done = std::promise<void>();
   sl.job = sl.job_done.get_future();
   auto run = [this, &sl, device, dev] {
@@ -1521,7 +1531,7 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
       if (sl.stage_deferred) {
         for (Slot* p : sl.dep_stage)
           check(nicgpu_stream_wait_event(scratch_->side_up, p->ev_wb), "nicgpu_stream_wait_event");
-        image_stage(sl, sl.tx, device ? sl.v.tx : nullptr, scratch_->side_up);
+        image_stage(sl, sl.tx.size(), sl.tx.data(), device ? sl.v.tx : nullptr, scratch_->side_up);
       }
       if (device) {
         sl.on_device = front(sl, sl.mem, sl.tx, sl.rx, sl.stats, sl.result, sl.stream, disjoint, check_us);
@@ -1899,6 +1909,18 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
     rss_ready.wait();
     ok = ok && j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_done), "nicgpu_stream_wait_event");
     if (ok && rss) ok = j.ok(nicgpu_qp_group(sl.qp, nrx_total, nq, S.side_down), "nicgpu_qp_group");
+    // a fused batch: the lists split per queue pair (entries made relative to
+    // each queue pair's ring), and its per-queue-pair hits when it needs them
+    if (ok && rss && sl.multi)
+      ok = j.ok(nicgpu_qp_segment_lists(sl.qp, nrx_total, nq, sl.h_split.get<std::uint32_t>((sl.nseg + 1) * std::max<std::size_t>(nq, 1)),
+                                        S.side_down),
+                "nicgpu_qp_segment_lists");
+    if (ok && rss && sl.multi && sl.seg_hits_on) {
+      auto* sh = static_cast<std::uint64_t*>(sl.seg_hits.get(sl.nseg * tn * sizeof(std::uint64_t)));
+      ok = j.ok(nicgpu_qp_segment_hits(sl.qp, nrx_total, tn, sh, S.side_down), "nicgpu_qp_segment_hits") &&
+           j.ok(nicgpu_memcpy_async(sl.h_seg_hits.get<std::uint64_t>(sl.nseg * tn), sh, sl.nseg * tn * 8, S.side_down),
+                "nicgpu_memcpy_async");
+    }
     if (ok && rss)
       ok = j.ok(nicgpu_memcpy_async(sl.meta, v.rss_count, sizeof(std::uint64_t), S.side_down), "nicgpu_memcpy_async") &&
            j.ok(nicgpu_memcpy_async(sl.meta + 1, hits, tn * sizeof(std::uint64_t), S.side_down), "nicgpu_memcpy_async") &&
@@ -1950,7 +1972,7 @@ void BatchedQueuePair::finish(Slot& sl, RxBatchResult& out) {
   } reset{sl};
   sl.down->finish();
   sl.wait_writeback();
-  if (sl.rss) {
+  if (sl.rss && !sl.multi) {  // (a fused batch's accounting and lists are process_queues')
     const std::uint64_t m = sl.meta[0];
     config_.rss->account_batch(m, std::span<const std::uint64_t>(sl.meta + 1, sl.tn));
     std::size_t used_q = 0;  // largest queue with frames + 1
@@ -1998,7 +2020,7 @@ BatchedQueuePair::HostImage& BatchedQueuePair::bind_image(HostMemory& m) {
     if (reinterpret_cast<std::uintptr_t>(host) & 15u)
       throw GpuError("process_batch: HostMemory window is not 16-B aligned", NICGPU_ERR_INVALID);
   }
-  HostImage& I = S.img;
+  HostImage& I = *S.img;
   if (I.mem == &m && I.host == host && I.size == size && I.device == dev) return I;
   if (S.pending) throw std::logic_error("submit: another HostMemory while batches are pending");
   I.release();
@@ -2086,7 +2108,8 @@ void BatchedQueuePair::image_prepare(Slot& sl, HostImage& img, std::span<const T
 // (the registered window goes up by DMA at the link's rate), else the gather
 // kernel over the TX descriptors (tx_dev: the batch's descriptors on the
 // device, in stream order; null: uploaded here).  Records ev_staged.
-void BatchedQueuePair::image_stage(Slot& sl, std::span<const TxDescriptor> tx, const void* tx_dev, void* stream) {
+void BatchedQueuePair::image_stage(Slot& sl, std::size_t ntx, const TxDescriptor* tx_host, const void* tx_dev,
+                                   void* stream) {
   HostImage& I = *sl.image;
   if (sl.tx_hi > sl.tx_lo) {
     auto* mirror = static_cast<std::uint8_t*>(I.mirror.p);
@@ -2094,12 +2117,11 @@ void BatchedQueuePair::image_stage(Slot& sl, std::span<const TxDescriptor> tx, c
       check(nicgpu_memcpy_async(mirror + sl.tx_lo, I.host + sl.tx_lo, sl.tx_hi - sl.tx_lo, stream), "nicgpu_memcpy_async");
     } else {
       if (!tx_dev) {
-        tx_dev = sl.stage_tx.get(tx.size() * sizeof(TxDescriptor));
-        check(nicgpu_memcpy_async(const_cast<void*>(tx_dev), tx.data(), tx.size() * sizeof(TxDescriptor), stream),
+        tx_dev = sl.stage_tx.get(ntx * sizeof(TxDescriptor));
+        check(nicgpu_memcpy_async(const_cast<void*>(tx_dev), tx_host, ntx * sizeof(TxDescriptor), stream),
               "nicgpu_memcpy_async");
       }
-      check(nicgpu_image_stage(mirror, I.alias, I.size, static_cast<const nicgpu_tx_descriptor*>(tx_dev), tx.size(),
-                               stream),
+      check(nicgpu_image_stage(mirror, I.alias, I.size, static_cast<const nicgpu_tx_descriptor*>(tx_dev), ntx, stream),
             "nicgpu_image_stage");
     }
   }
@@ -2125,7 +2147,7 @@ void BatchedQueuePair::image_writeback(Slot& sl, const nicgpu_segment_write* wri
 void BatchedQueuePair::image_host_path(Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                                        QueuePairStats& st, RxBatchResult& out, void* stream, int disjoint,
                                        double& check_us) {
-  if (!sl.staged) image_stage(sl, tx, nullptr, stream);
+  if (!sl.staged) image_stage(sl, tx.size(), tx.data(), nullptr, stream);
   check(nicgpu_stream_wait_event(stream, sl.ev_staged), "nicgpu_stream_wait_event");
   for (Slot* p : sl.dep_rx) check(nicgpu_stream_wait_event(stream, p->ev_wb), "nicgpu_stream_wait_event");
   sl.applied.clear();
@@ -2159,6 +2181,7 @@ void BatchedQueuePair::process_batch(HostMemory& m, std::span<const TxDescriptor
   Slot& sl = S.slot[0];
   sl.tx_dev = nullptr;
   sl.rx_dev = nullptr;
+  sl.multi = false;
   image_prepare(sl, I, tx, rx);  // nothing pending: no dependencies
   sl.staged = false;
   QueuePairStats st = stats_;
@@ -2168,7 +2191,7 @@ void BatchedQueuePair::process_batch(HostMemory& m, std::span<const TxDescriptor
   try {
     if (config_.device_resolve && device_fits(tx.size(), rx.size())) {
       upload(sl, tx, rx, true);
-      image_stage(sl, tx, sl.v.tx, S.side_up);
+      image_stage(sl, tx.size(), tx.data(), sl.v.tx, S.side_up);
       on_device = front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);
       if (on_device) {
         back(sl, mem, out, stream);
@@ -2201,6 +2224,253 @@ void BatchedQueuePair::submit(HostMemory& m, std::span<const TxDescriptor> tx, s
   else if (S.device != dev) throw std::logic_error("submit: batches pending on another device");
   HostImage& I = bind_image(m);
   enqueue(I.view(), tx, rx, nullptr, stream, &I);
+}
+
+// ------------------------------------------------------------------------
+// BatchedQueueManager's fused batch (queue_manager.cpp:54-78 over queue pairs
+// whose buffers do not meet): every queue pair's TX batch and RX ring back to
+// back in one device context, resolved as one batch with per-queue-pair
+// segments (nicgpu_qp_set_segments), delivered in one launch.
+
+void BatchedQueuePair::share_image(const BatchedQueuePair& owner) { scratch_->img = owner.scratch_->img; }
+
+// front_once's device path for a segmented batch (sizes from the caller, no
+// host tail, no host sort): false = the batch does not fit the fused path.
+bool BatchedQueuePair::front_multi(Slot& sl, const DeviceHostMemory& mem, std::size_t ntx, std::size_t nrx,
+                                   RxBatchResult& out, void* stream, int& again, bool whole_check) {
+  using clock = std::chrono::steady_clock;
+  auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
+  Scratch& S = *scratch_;
+  nicgpu_qp_view& v = sl.v;
+  void* ps = S.side_plan;
+  auto t = clock::now();
+  check(nicgpu_stream_wait_event(ps, sl.ev_tx), "nicgpu_stream_wait_event");
+  if (sl.staged) check(nicgpu_stream_wait_event(stream, sl.ev_staged), "nicgpu_stream_wait_event");
+  check(nicgpu_qp_plan_async(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &v,
+                             ps, stream),
+        "nicgpu_qp_plan_async");
+  check(nicgpu_stream_wait_event(ps, sl.ev_rx), "nicgpu_stream_wait_event");
+  check(nicgpu_stream_wait_event(stream, sl.ev_rx), "nicgpu_stream_wait_event");
+  out.timings.sums_us += us_since(t);
+  t = clock::now();
+  check(nicgpu_qp_resolve_start(sl.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, stream),
+        "nicgpu_qp_resolve_start");
+  check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");
+  out.timings.resolve_us += us_since(t);
+  t = clock::now();
+  int verdict = -1;
+  check(nicgpu_qp_check_flags(sl.qp, mem.size, ntx, nrx, whole_check ? NICGPU_QP_CHECK_WHOLE : 0u, &verdict, ps),
+        "nicgpu_qp_check_flags");
+  out.timings.check_us += us_since(t);
+  if (verdict != 1) return false;  // overlapping, or a ring not in address order: per queue pair
+  t = clock::now();
+  sl.tn = sl.nq = 0;
+  const nicgpu_rss_ctx* rctx = nullptr;
+  std::uint64_t* hits = nullptr;
+  if (config_.rss != nullptr) {
+    const auto& table = config_.rss->config().table;
+    sl.tn = table.size();
+    for (const std::uint16_t q : table) sl.nq = std::max<std::size_t>(sl.nq, std::size_t{q} + 1);
+    rctx = config_.rss->device_context(stream);
+    hits = static_cast<std::uint64_t*>(sl.hits.get(std::max<std::size_t>(sl.tn, 1) * sizeof(std::uint64_t)));
+  }
+  deliver(sl, mem, 0, nrx, NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_RESET_HITS, rctx, hits, stream);
+  out.timings.gather_us += us_since(t);
+  t = clock::now();
+  std::uint64_t done = 0, used = 0, settled = 0;
+  nicgpu_qp_stats ds{};
+  const int rst = nicgpu_qp_resolve_finish(sl.qp, &done, &used, &settled, &ds);
+  out.timings.resolve_us += us_since(t);
+  if (rst == NICGPU_ERR_AGAIN) {
+    again = 1;
+    return false;
+  }
+  if (rst == NICGPU_ERR_RANGE || rst == NICGPU_ERR_UNSETTLED) return false;
+  check(rst, "nicgpu_qp_resolve_finish");
+  sl.settled = settled;
+  sl.relaxed = settled < used;
+  sl.ntx = ntx;
+  sl.nrx_total = used;
+  out.tx_processed = ntx;
+  out.rx_consumed = used;
+  if (config_.results_on_device) out.tx_completions.clear();
+  else out.tx_completions.resize(ntx);
+  return true;
+}
+
+bool BatchedQueuePair::process_queues(const DeviceHostMemory& mem_in, HostImage* img,
+                                      std::span<const std::span<const TxDescriptor>> tx,
+                                      std::span<const std::span<const RxDescriptor>> rx,
+                                      std::span<const BatchedQueuePairConfig> configs, std::vector<RxBatchResult>& out,
+                                      std::vector<QueuePairStats>& stats, void* stream, bool dev_desc,
+                                      bool whole_check) {
+  using clock = std::chrono::steady_clock;
+  Scratch& S = *scratch_;
+  if (S.pending) throw std::logic_error("process_queues: batches pending");
+  const std::size_t Q = tx.size();
+  if (Q == 0 || Q > NICGPU_QP_MAX_SEGMENTS || rx.size() != Q || configs.size() != Q) return false;
+  std::vector<nicgpu_qp_segment> seg(Q);
+  std::size_t ntx = 0, nrx = 0;
+  for (std::size_t q = 0; q < Q; ++q) {
+    seg[q] = nicgpu_qp_segment{ntx, nrx, rx[q].size(), configs[q].max_mtu, configs[q].queue_id, 0, 0, 0};
+    ntx += tx[q].size();
+    nrx += rx[q].size();
+  }
+  if (!device_fits(ntx, nrx) || ntx == 0 || (dev_desc && img)) return false;
+  int dev = 0;
+  check(nicgpu_get_device(&dev), "nicgpu_get_device");
+  S.ensure(dev);
+  const DeviceHostMemory mem = img ? img->view() : mem_in;
+  Slot& sl = S.slot[0];
+  sl.tx_dev = nullptr;
+  sl.rx_dev = nullptr;
+  sl.image = nullptr;
+  sl.staged = false;
+  sl.dep_stage.clear();
+  sl.dep_rx.clear();
+  sl.multi = true;
+  sl.nseg = Q;
+  RxBatchResult cat;
+  cat.timings = RxBatchResult::Timings{};
+  cat.timings.device = true;
+  const auto t0 = clock::now();
+  // descriptors up, queue pair by queue pair, into the concatenated arrays
+  // (device arrays: copied after what the caller enqueued before the call)
+  nicgpu_qp_view& v = sl.v;
+  check(nicgpu_qp_reserve(sl.qp, ntx, nrx, &v), "nicgpu_qp_reserve");
+  if (dev_desc) {
+    check(nicgpu_event_record(sl.ev_submit, stream), "nicgpu_event_record");
+    check(nicgpu_stream_wait_event(S.side_up, sl.ev_submit), "nicgpu_stream_wait_event");
+  }
+  for (std::size_t q = 0; q < Q; ++q)
+    check(nicgpu_memcpy_async(v.tx + seg[q].tx_begin, tx[q].data(), tx[q].size() * sizeof(TxDescriptor), S.side_up),
+          "nicgpu_memcpy_async");
+  check(nicgpu_event_record(sl.ev_tx, S.side_up), "nicgpu_event_record");
+  for (std::size_t q = 0; q < Q; ++q)
+    check(nicgpu_memcpy_async(v.rx + seg[q].rx_begin, rx[q].data(), rx[q].size() * sizeof(RxDescriptor), S.side_up),
+          "nicgpu_memcpy_async");
+  check(nicgpu_event_record(sl.ev_rx, S.side_up), "nicgpu_event_record");
+  if (img) {  // the TX bytes of every queue pair: their span, or a gather over the uploaded descriptors
+    sl.image = img;
+    std::uint64_t lo = ~0ull, hi = 0, bytes = 0, rlo = ~0ull, rhi = 0;
+    for (std::size_t q = 0; q < Q; ++q) {
+      for (const TxDescriptor& t : tx[q]) {
+        if (t.length == 0 || !nicqp::dma_ok(img->size, t.buffer_address, t.length)) continue;
+        lo = std::min<std::uint64_t>(lo, t.buffer_address);
+        hi = std::max<std::uint64_t>(hi, t.buffer_address + t.length);
+        bytes += t.length;
+      }
+      for (const RxDescriptor& x : rx[q]) {
+        if (x.buffer_length == 0 || x.buffer_address >= img->size) continue;
+        rlo = std::min<std::uint64_t>(rlo, x.buffer_address);
+        rhi = std::max<std::uint64_t>(rhi, x.buffer_address + std::min<std::uint64_t>(x.buffer_length, img->size - x.buffer_address));
+      }
+    }
+    sl.tx_lo = hi > lo ? lo : 0;
+    sl.tx_hi = hi > lo ? hi : 0;
+    sl.tx_bytes = bytes;
+    sl.rx_lo = rhi > rlo ? rlo : 0;
+    sl.rx_hi = rhi > rlo ? rhi : 0;
+    sl.whole = sl.tx_hi > sl.tx_lo && sl.tx_hi - sl.tx_lo <= bytes + bytes / 2 + (std::uint64_t{1} << 16);
+    image_stage(sl, ntx, nullptr, v.tx, S.side_up);
+  }
+  cat.timings.copy_us += std::chrono::duration<double, std::micro>(clock::now() - t0).count();
+  check(nicgpu_qp_set_segments(sl.qp, seg.data(), Q, ntx, S.side_plan), "nicgpu_qp_set_segments");
+  // RSS: the engines' configurations are equal (the manager checked): one
+  // context hashes every queue pair's frames; separate engines count their own
+  RssEngine* const rss0 = configs[0].rss;
+  bool own_engines = false;
+  for (std::size_t q = 1; q < Q; ++q) own_engines |= configs[q].rss != rss0;
+  sl.seg_hits_on = rss0 != nullptr && own_engines;
+  bool ok = false;
+  try {
+    for (int attempt = 0;; ++attempt) {
+      int again = 0;
+      ok = front_multi(sl, mem, ntx, nrx, cat, stream, again, whole_check);
+      if (!again) break;
+      if (attempt >= 1) throw GpuError("process_queues: the device plan outgrew its piece buffers twice", NICGPU_ERR_AGAIN);
+      cat.timings.replans += 1;
+    }
+    if (ok) {
+      back(sl, mem, cat, stream);
+      finish(sl, cat);
+    }
+  } catch (...) {
+    (void) nicgpu_qp_set_segments(sl.qp, nullptr, 0, 0, nullptr);
+    sl.multi = false;
+    try {
+      sl.wait_writeback();
+    } catch (...) {
+    }
+    throw;
+  }
+  if (!ok) {
+    check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");  // the wasted resolve is over
+    check(nicgpu_qp_set_segments(sl.qp, nullptr, 0, 0, nullptr), "nicgpu_qp_set_segments");
+    sl.multi = false;
+    return false;
+  }
+  // split per queue pair
+  std::vector<std::uint64_t> used(Q);
+  std::vector<nicgpu_qp_stats> ds(Q);
+  check(nicgpu_qp_segment_results(sl.qp, used.data(), ds.data()), "nicgpu_qp_segment_results");
+  out.resize(Q);
+  stats.assign(Q, QueuePairStats{});
+  const bool keep = config_.results_on_device;
+  const bool rss = sl.rss;
+  const std::size_t nq = sl.nq, tn = sl.tn;
+  const std::uint32_t* split = rss ? sl.h_split.get<std::uint32_t>((Q + 1) * std::max<std::size_t>(nq, 1)) : nullptr;
+  const std::uint64_t* seg_hits = sl.seg_hits_on ? sl.h_seg_hits.get<std::uint64_t>(Q * tn) : nullptr;
+  for (std::size_t q = 0; q < Q; ++q) {
+    RxBatchResult& o = out[q];
+    const std::size_t tb = seg[q].tx_begin, rb = seg[q].rx_begin, nt = tx[q].size(), nr = used[q];
+    static_assert(sizeof(QueuePairStats) == sizeof(nicgpu_qp_stats));
+    std::memcpy(static_cast<void*>(&stats[q]), &ds[q], sizeof(QueuePairStats));
+    o.tx_processed = nt;
+    o.rx_consumed = nr;
+    o.timings = cat.timings;
+    o.timings.host_image = img != nullptr;
+    o.timings.staged_whole = img != nullptr && sl.whole;
+    o.dev = RxBatchResult::DeviceResults{};
+    std::size_t used_q = 0;  // largest RSS queue with frames + 1
+    if (rss)
+      for (std::size_t r = 0; r < nq; ++r)
+        if (split[(q + 1) * nq + r] > split[q * nq + r]) used_q = r + 1;
+    if (keep) {
+      o.tx_completions.clear();
+      o.rx_completions.clear();
+      o.rx_hash.clear();
+      o.rx_queue.clear();
+      o.queues.clear();
+      RxBatchResult::DeviceResults& d = o.dev;
+      d.tx_completions = reinterpret_cast<const CompletionEntry*>(v.txc) + tb;
+      d.rx_completions = reinterpret_cast<const CompletionEntry*>(v.rxc) + rb;
+      d.ntx = nt;
+      d.nrx = nr;
+      d.rx_hash = rss ? v.rx_hash + rb : nullptr;
+      d.rx_queue = rss ? v.rx_queue + rb : nullptr;
+      d.queue_which = rss ? v.queue_which : nullptr;
+      if (rss) {
+        d.queue_start.assign(split + q * nq, split + q * nq + used_q);
+        d.queue_end.assign(split + (q + 1) * nq, split + (q + 1) * nq + used_q);
+      }
+    } else {
+      o.tx_completions.assign(cat.tx_completions.begin() + tb, cat.tx_completions.begin() + tb + nt);
+      o.rx_completions.assign(cat.rx_completions.begin() + rb, cat.rx_completions.begin() + rb + nr);
+      o.rx_hash.assign(cat.rx_hash.begin() + rb, cat.rx_hash.begin() + rb + nr);
+      o.rx_queue.assign(cat.rx_queue.begin() + rb, cat.rx_queue.begin() + rb + nr);
+      for (auto& l : o.queues) l.clear();
+      o.queues.resize(used_q);
+      for (std::size_t r = 0; r < used_q; ++r) o.queues[r].assign(sl.which + split[q * nq + r], sl.which + split[(q + 1) * nq + r]);
+    }
+    if (rss && seg_hits) {  // queue pair q's engine counts its own frames
+      std::uint64_t m = 0;
+      for (std::size_t k = 0; k < tn; ++k) m += seg_hits[q * tn + k];
+      configs[q].rss->account_batch(m, std::span<const std::uint64_t>(seg_hits + q * tn, tn));
+    }
+  }
+  if (rss && !seg_hits) rss0->account_batch(sl.meta[0], std::span<const std::uint64_t>(sl.meta + 1, sl.tn));
+  return true;
 }
 
 }  // namespace nic

@@ -79,6 +79,7 @@ const char* nicgpu_strerror(int status) {
     case NICGPU_ERR_NOMEM: return "out of device memory";
     case NICGPU_ERR_RANGE: return "batch too large for 32-bit piece indices";
     case NICGPU_ERR_AGAIN: return "plan outgrew its buffers: redo the batch";
+    case NICGPU_ERR_UNSETTLED: return "segmented resolve did not settle: resolve per queue pair";
     default: return "unknown status";
   }
 }

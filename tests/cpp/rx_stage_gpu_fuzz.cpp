@@ -22,7 +22,8 @@
 //   rx_stage_gpu_fuzz full c3|c5 [dev] [keep]
 //   rx_stage_gpu_fuzz check [count]
 //   rx_stage_gpu_fuzz edges             (piece-count limit, descriptor rings inside the image)
-//   rx_stage_gpu_fuzz pipeline [count]   (submit/collect vs process_batch in order)
+//   rx_stage_gpu_fuzz pipeline [himg] [count]   (submit/collect vs process_batch in order)
+//   rx_stage_gpu_fuzz qm [count]         (BatchedQueueManager's fused batch vs each queue pair alone)
 #undef NDEBUG
 #include <cassert>
 #include <cstdio>
@@ -33,6 +34,7 @@
 #include "cpu_backend.h"
 #include "nic/flat_host_memory.h"
 #include "nic/rss.h"
+#include "nic/rx_queue_manager.h"
 #include "nic/rx_stage.h"
 #include "nic/rss_rings.h"
 #include "nicgpu.h"
@@ -897,10 +899,67 @@ int run_edges() {
     if (!same_all) std::fprintf(stderr, "edges: the over-count batch differs from the host resolve\n");
     ok = ok && same_all;
   }
+  // a first batch whose device plan outgrows the piece buffers the stage sizes
+  // ahead (ntx + ntx / 4 + 64 pieces): TSO with a small mss, ~60 segments and
+  // 62 pieces per descriptor.  The resolve finishes with NICGPU_ERR_AGAIN, the
+  // stage redoes the batch once with the grown buffers (timings.replans == 1),
+  // and the result equals the host resolve; the next batch fits at once.
+  bool replanned = false;
+  {
+    const std::size_t ntx = 96, nrx = ntx * 64;
+    std::vector<TxDescriptor> ttx(ntx);
+    for (std::size_t i = 0; i < ntx; ++i) {
+      TxDescriptor& t = ttx[i];
+      t.buffer_address = big + (i % 8) * 2048;
+      t.length = 1518;
+      t.descriptor_index = static_cast<std::uint16_t>(i);
+      t.tso_enabled = true;
+      t.mss = static_cast<std::uint16_t>(24 + i % 3);
+      t.header_length = 54;
+      t.checksum_offload = true;
+    }
+    std::vector<RxDescriptor> trx(nrx);
+    // distinct 80-B RX buffers after the TX frames (segments are 54 + <= 26 B)
+    const std::size_t rx_base = big + 8 * 2048;
+    for (std::size_t j = 0; j < nrx; ++j) {
+      trx[j].buffer_address = rx_base + j * 80;
+      trx[j].buffer_length = 80;
+      trx[j].checksum = ChecksumMode::None;
+    }
+    assert(rx_base + nrx * 80 <= mem_size);
+    std::vector<std::uint8_t> timg = image;
+    test::CpuBackend tcpu{timg, nullptr, TupleSpec{}};
+    RxBatchResult th;
+    QueuePairStats ths{};
+    rx_stage_detail::BatchScratch tscratch;
+    rx_stage_detail::run_batch(cfg, mem_size, ttx, trx, ths, th, tscratch, tcpu);
+    assert(nicgpu_memcpy_async(d, image.data(), mem_size, nullptr) == NICGPU_OK);
+    BatchedQueuePair tqp{cfg};
+    RxBatchResult tg;
+    tqp.process_batch(DeviceHostMemory{static_cast<std::byte*>(d), mem_size}, ttx, trx, tg);
+    std::vector<std::uint8_t> tdev(mem_size);
+    assert(nicgpu_memcpy_async(tdev.data(), d, mem_size, nullptr) == NICGPU_OK);
+    assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+    replanned = tg.timings.device && tg.timings.replans == 1;
+    bool eq = replanned && tg.tx_completions.size() == th.tx_completions.size() &&
+              tg.rx_completions.size() == th.rx_completions.size() && tdev == timg &&
+              std::memcmp(&ths, &tqp.stats(), sizeof(ths)) == 0;
+    for (std::size_t i = 0; eq && i < th.tx_completions.size(); ++i) eq = same(tg.tx_completions[i], th.tx_completions[i]);
+    for (std::size_t i = 0; eq && i < th.rx_completions.size(); ++i) eq = same(tg.rx_completions[i], th.rx_completions[i]);
+    // the same stage again: its buffers now fit the plan
+    RxBatchResult tg2;
+    tqp.process_batch(DeviceHostMemory{static_cast<std::byte*>(d), mem_size}, ttx, trx, tg2);
+    eq = eq && tg2.timings.device && tg2.timings.replans == 0 && tg2.tx_completions.size() == th.tx_completions.size();
+    if (!eq)
+      std::fprintf(stderr, "edges: the outgrown plan (device %d, replans %u) differs from the host resolve\n",
+                   int(tg.timings.device), tg.timings.replans);
+    ok = ok && eq;
+  }
   nicgpu_free(d);
   if (ok)
     std::printf("rx_stage_gpu_fuzz edges: ok (over-range plan and over-count batch took the host path; ring "
-                "overwrite refused)\n");
+                "overwrite refused; an outgrown plan was redone once: %d)\n",
+                int(replanned));
   return ok ? 0 : 1;
 }
 
@@ -1019,11 +1078,174 @@ int run_rings() {
   return 0;
 }
 
+// BatchedQueueManager's fused batch (every queue pair's batch and ring in one
+// device batch, segments with their own queue id, MTU and ring) against each
+// queue pair's batch run alone through the host resolve (run_batch over the
+// CPU backend, which rx_stage_fuzz pins to the reference QueuePair): random
+// queue counts, per-queue MTUs, rings that run short or are empty, TSO, VLAN,
+// faults, every queue's buffers in a region of its own (queues disjoint).
+// RSS through one shared engine or one engine per queue pair (equal configs);
+// results on the host or left on the device; one sequence in three on a
+// HostMemory.  Two rounds per seed (ring leftovers carried over).
+std::size_t g_qm_fused = 0, g_qm_rounds = 0, g_qm_himg = 0;
+int run_qm(std::uint64_t seed) {
+  Rng r{seed * 6151 + 17};
+  const std::size_t Q = 1 + r.below(12);
+  const std::size_t region = 1u << 20;
+  const std::size_t mem_size = Q * region;
+  std::vector<std::uint8_t> image(mem_size);
+  for (auto& b : image) b = r.byte();
+  const bool shared_engine = r.below(2) == 0, rss_on = r.below(5) != 0, keep = r.below(3) == 0;
+  const bool himg = r.below(3) == 0;
+  std::vector<std::uint16_t> table(64 + r.below(100));
+  for (auto& t : table) t = static_cast<std::uint16_t>(r.below(24));
+  const RssConfig rss_cfg{kMsKey, table};
+  std::vector<std::unique_ptr<RssEngine>> dev_eng, ref_eng;
+  for (std::size_t q = 0; q < (shared_engine ? 1 : Q); ++q) {
+    dev_eng.push_back(std::make_unique<RssEngine>(rss_cfg));
+    ref_eng.push_back(std::make_unique<RssEngine>(rss_cfg));
+  }
+  std::vector<BatchedQueuePairConfig> cfg(Q);
+  const std::size_t mtus[] = {9000, 1500, 3000};
+  for (std::size_t q = 0; q < Q; ++q) {
+    cfg[q].queue_id = static_cast<std::uint16_t>(r.below(9));
+    cfg[q].max_mtu = mtus[r.below(3)];
+    cfg[q].weight = static_cast<std::uint8_t>(r.below(4));
+    cfg[q].results_on_device = keep;
+  }
+  std::vector<std::uint8_t> ref_img = image;
+  void* d = nullptr;
+  assert(nicgpu_malloc(&d, mem_size + 64) == NICGPU_OK);
+  assert(nicgpu_memcpy_async(d, image.data(), mem_size, nullptr) == NICGPU_OK);
+  assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+  FlatHostMemory hm(himg ? mem_size : 0);
+  if (himg) std::memcpy(hm.data(), image.data(), mem_size);
+  std::vector<BatchedQueuePairConfig> dcfg = cfg;
+  for (std::size_t q = 0; q < Q; ++q) dcfg[q].rss = rss_on ? dev_eng[shared_engine ? 0 : q].get() : nullptr;
+  BatchedQueueManager qm{BatchedQueueManagerConfig{dcfg}};
+  std::vector<QueuePairStats> ref_st(Q);
+  std::vector<std::vector<RxDescriptor>> ring(Q);
+  bool ok = true;
+  for (int round = 0; round < 2 && ok; ++round) {
+    std::vector<std::vector<TxDescriptor>> tx(Q);
+    for (std::size_t q = 0; q < Q; ++q) {
+      const std::size_t base = q * region;
+      const std::size_t ntx = r.below(5) == 0 ? 0 : 1 + r.below(r.below(4) == 0 ? 3000 : 200);
+      for (std::size_t i = 0; i < ntx; ++i) {
+        TxDescriptor t{};
+        const std::size_t L = r.below(8) == 0 ? r.below(60) : (r.below(3) ? 64 + r.below(1500) : 1518);
+        t.buffer_address = base + r.below(static_cast<std::uint32_t>(region / 2 - 2048));
+        if (r.below(80) == 0) t.buffer_address = mem_size + 1;  // a DMA read fault
+        t.length = static_cast<std::uint32_t>(L);
+        t.descriptor_index = static_cast<std::uint16_t>(i);
+        t.checksum = static_cast<ChecksumMode>(r.below(3));
+        t.checksum_offload = r.below(4) != 0;
+        t.checksum_value = static_cast<std::uint16_t>(r.below(65536));
+        if (r.below(8) == 0) {
+          t.tso_enabled = true;
+          t.mss = static_cast<std::uint16_t>(100 + r.below(1400));
+          t.header_length = static_cast<std::uint16_t>(14 + r.below(60));
+        }
+        if (r.below(8) == 0) {
+          t.vlan_insert = true;
+          t.vlan_tag = static_cast<std::uint16_t>(r.below(65536));
+        }
+        tx[q].push_back(t);
+      }
+      // the ring: leftovers first, then new descriptors in the upper half
+      const std::size_t add = r.below(4) == 0 ? r.below(static_cast<std::uint32_t>(ntx + 1)) : ntx + r.below(20);
+      const std::size_t at0 = base + region / 2 + (round ? region / 4 : 0);
+      for (std::size_t j = 0; j < add; ++j) {
+        RxDescriptor x{};
+        const std::size_t slot = (region / 4) / std::max<std::size_t>(add, 1);
+        x.buffer_address = at0 + j * std::min<std::size_t>(slot, 2048);
+        x.buffer_length = static_cast<std::uint32_t>(r.below(10) ? std::min<std::size_t>(slot, 2048) : r.below(200));
+        x.descriptor_index = static_cast<std::uint16_t>(j);
+        x.checksum = static_cast<ChecksumMode>(r.below(3));
+        x.checksum_offload = r.below(3) != 0;
+        x.vlan_strip = r.below(4) == 0;
+        x.vlan_present = r.below(4) == 0;
+        x.vlan_tag = static_cast<std::uint16_t>(r.below(65536));
+        x.gro_enabled = r.below(4) == 0;
+        ring[q].push_back(x);
+      }
+    }
+    // the reference: each queue pair alone, host resolve over the CPU backend
+    std::vector<RxBatchResult> want(Q);
+    for (std::size_t q = 0; q < Q; ++q) {
+      BatchedQueuePairConfig c = cfg[q];
+      c.rss = rss_on ? ref_eng[shared_engine ? 0 : q].get() : nullptr;
+      c.results_on_device = false;
+      test::CpuBackend cpu{ref_img, c.rss, TupleSpec{}};
+      rx_stage_detail::BatchScratch scratch;
+      rx_stage_detail::run_batch(c, mem_size, tx[q], ring[q], ref_st[q], want[q], scratch, cpu);
+    }
+    std::vector<QueueBatch> b(Q);
+    for (std::size_t q = 0; q < Q; ++q) b[q] = QueueBatch{tx[q], ring[q]};
+    std::vector<RxBatchResult> got;
+    if (himg) qm.process_batch(hm, b, got);
+    else qm.process_batch(DeviceHostMemory{static_cast<std::byte*>(d), mem_size}, b, got);
+    g_qm_fused += qm.last_fused();
+    g_qm_rounds += 1;
+    for (std::size_t q = 0; q < Q && ok; ++q) {
+      RxBatchResult& g = got[q];
+      if (keep && !materialize(g)) {
+        std::fprintf(stderr, "qm seed %llu: results on the device not as documented\n", (unsigned long long) seed);
+        ok = false;
+        break;
+      }
+      const RxBatchResult& w = want[q];
+      bool e = g.tx_completions.size() == w.tx_completions.size() && g.rx_completions.size() == w.rx_completions.size() &&
+               g.rx_consumed == w.rx_consumed;
+      for (std::size_t i = 0; e && i < w.tx_completions.size(); ++i) e = same(g.tx_completions[i], w.tx_completions[i]);
+      for (std::size_t i = 0; e && i < w.rx_completions.size(); ++i) e = same(g.rx_completions[i], w.rx_completions[i]);
+      const QueuePairStats gs = *qm.queue_stats(q);
+      e = e && std::memcmp(&ref_st[q], &gs, sizeof(QueuePairStats)) == 0;
+      if (rss_on) e = e && g.rx_hash == w.rx_hash && g.rx_queue == w.rx_queue && g.queues == w.queues;
+      if (!e) {
+        std::fprintf(stderr, "qm seed %llu round %d queue %zu/%zu differs (fused %d, tx %zu/%zu rx %zu/%zu)\n",
+                     (unsigned long long) seed, round, q, Q, qm.last_fused(), g.tx_completions.size(),
+                     w.tx_completions.size(), g.rx_completions.size(), w.rx_completions.size());
+        ok = false;
+      }
+    }
+    for (std::size_t q = 0; q < Q; ++q) ring[q].erase(ring[q].begin(), ring[q].begin() + want[q].rx_consumed);
+  }
+  if (ok && rss_on)
+    for (std::size_t k = 0; k < dev_eng.size(); ++k)
+      ok = ok && dev_eng[k]->stats().hashes == ref_eng[k]->stats().hashes &&
+           dev_eng[k]->stats().queue_hits == ref_eng[k]->stats().queue_hits;
+  std::vector<std::uint8_t> after(mem_size);
+  if (himg) {
+    std::memcpy(after.data(), hm.data(), mem_size);
+    g_qm_himg += 1;
+  } else {
+    assert(nicgpu_memcpy_async(after.data(), d, mem_size, nullptr) == NICGPU_OK);
+    assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+  }
+  if (ok && after != ref_img) {
+    std::fprintf(stderr, "qm seed %llu: memory differs\n", (unsigned long long) seed);
+    ok = false;
+  }
+  if (!ok && rss_on) std::fprintf(stderr, "qm seed %llu: (engines %s)\n", (unsigned long long) seed, shared_engine ? "shared" : "own");
+  nicgpu_free(d);
+  return ok ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
   assert(gpu_device_count() >= 1);
   if (argc > 1 && std::strcmp(argv[1], "rings") == 0) return run_rings();
   if (argc > 1 && std::strcmp(argv[1], "check") == 0) return run_check(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 400);
   if (argc > 1 && std::strcmp(argv[1], "edges") == 0) return run_edges();
+  if (argc > 1 && std::strcmp(argv[1], "qm") == 0) {
+    const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 60;
+    int bad = 0;
+    for (std::uint64_t s = 1; s <= count; ++s) bad += run_qm(s);
+    if (bad) return 1;
+    std::printf("rx_stage_gpu_fuzz qm: ok (%llu managers, %zu of %zu drains fused, %zu on a HostMemory)\n",
+                (unsigned long long) count, g_qm_fused, g_qm_rounds, g_qm_himg);
+    return 0;
+  }
   if (argc > 1 && std::strcmp(argv[1], "pipeline") == 0) {
     int a = 2;
     if (argc > a && std::strcmp(argv[a], "himg") == 0) {

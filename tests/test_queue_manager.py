@@ -89,3 +89,41 @@ def test_queue_manager_gpu(tmp_path):
     exe = _build(tmp_path, "qm_test")
     for name, disjoint in CASES.items():
         _run(exe, "gpu", name, tmp_path, () if disjoint else ("interleaved",))
+
+
+@pytest.mark.gpu
+def test_queue_manager_host_memory_gpu(tmp_path):
+    """The same fixtures on a HostMemory (nic::FlatHostMemory): one HBM mirror
+    for all queue pairs, the fused batch's TX bytes staged up and its delivered
+    bytes written back; the memory's bytes must be the reference's."""
+    exe = _build(tmp_path, "qm_test")
+    for name, disjoint in CASES.items():
+        _run(exe, "host", name, tmp_path, () if disjoint else ("interleaved",))
+
+
+QM_REFMEM = os.path.join(ROOT, "oracle", "_ref", "qm_test_refmem")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(QM_REFMEM), reason="oracle/_ref/qm_test_refmem not built (make -C oracle ref)")
+def test_queue_manager_reference_simple_host_memory_gpu(tmp_path):
+    """...and on the reference's own SimpleHostMemory (src/simple_host_memory.cpp
+    compiled in place by oracle/Makefile; the binary travels to the GPU box)."""
+    for name, disjoint in CASES.items():
+        _run(QM_REFMEM, "host", name, tmp_path, () if disjoint else ("interleaved",))
+
+
+@pytest.mark.gpu
+def test_queue_manager_fused_fuzz(tmp_path):
+    """BatchedQueueManager's fused batch (all queue pairs' batches and rings in
+    one device batch, per-queue-pair segments) against each queue pair alone
+    through the host resolve, on 60 random managers (1-12 queue pairs, mixed
+    MTUs and queue ids, short and empty rings, TSO, VLAN, faults; RSS through a
+    shared engine or one per queue pair; results on the host or the device;
+    one in three on a HostMemory), two drains each."""
+    from test_host_cpp import _build as build
+    exe = build(tmp_path, "rx_stage_gpu_fuzz")
+    r = subprocess.run([exe, "qm", "60"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "rx_stage_gpu_fuzz qm: ok" in r.stdout
+    print(r.stdout.strip())

@@ -212,14 +212,23 @@ int main(int argc, char** argv) {
     BatchedQueueManager qm{qc};
     std::vector<QueueBatch> b(Q);
     for (std::size_t q = 0; q < Q; ++q) b[q] = QueueBatch{txs.subspan(q * per, per), rxs.subspan(q * per, per)};
+    std::vector<DeviceQueueBatch> db(Q);  // descriptors in HBM
+    if (dev_desc)
+      for (std::size_t q = 0; q < Q; ++q)
+        db[q] = DeviceQueueBatch{static_cast<const TxDescriptor*>(dtx) + q * per, per,
+                                 static_cast<const RxDescriptor*>(drx) + q * per, per};
     std::vector<RxBatchResult> outs;
     std::vector<double> ts;
     std::uint64_t ok_q = 0;
+    int fused = 0;
     for (int r = 0; r < reps + 2; ++r) {
       const auto t0 = std::chrono::steady_clock::now();
-      qm.process_batch(dm, b, outs);
+      if (dev_desc) qm.process_batch(dm, db, outs);
+      else if (hostmem) qm.process_batch(*hm, b, outs);
+      else qm.process_batch(dm, b, outs);
       const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
       if (r >= 2) ts.push_back(us);
+      fused += r >= 2 ? qm.last_fused() : 0;
     }
     for (const auto& o : outs) {
       if (o.timings.device && cfg.results_on_device) ok_q += o.dev.nrx;
@@ -230,10 +239,10 @@ int main(int argc, char** argv) {
     std::size_t fb = 0;
     for (std::size_t i = 0; i < per * Q; ++i) fb += lens[i];
     std::printf("{\"row\": \"f1_queue_manager\", \"workload\": \"c3\", \"queue_pairs\": %zu, \"tx_per_queue\": %zu, "
-                "\"descriptors\": \"%s\", \"results\": \"%s\", \"rx_align\": %zu, \"rx_completions\": %llu, "
-                "\"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f}\n",
-                Q, per, desc_kind.c_str(), cfg.results_on_device ? "device" : "host", rx_align, (unsigned long long) ok_q, med,
-                per * Q / med, fb / med / 1e3);
+                "\"descriptors\": \"%s\", \"results\": \"%s\", \"host_memory\": %s, \"rx_align\": %zu, \"rx_completions\": %llu, "
+                "\"fused_drains\": %d, \"drains\": %d, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f}\n",
+                Q, per, desc_kind.c_str(), cfg.results_on_device ? "device" : "host", hostmem ? "true" : "false", rx_align,
+                (unsigned long long) ok_q, fused, reps, med, per * Q / med, fb / med / 1e3);
     nicgpu_free(mem);
     if (ptx) nicgpu_host_free(ptx);
     if (prx) nicgpu_host_free(prx);
