@@ -267,6 +267,8 @@ struct RxBatchResult {
     bool host_image{false};  // run against a HostMemory: TX bytes staged up, delivered bytes written back
     bool staged_whole{false};  // ... the TX bytes' span went up in one copy (dense), else per descriptor
     unsigned replans{0};    // device plans redone because the first outgrew the piece buffers (at most 1)
+    double irq_us{0};       // interrupt callbacks replayed (the whole replay, its waits included)
+    double irq_wait_us{0};  // ... of which waiting for completions still landing
   } timings;
 };
 
@@ -403,7 +405,7 @@ private:
   void enqueue(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                const DeviceDescriptors* d, void* stream, HostImage* img = nullptr);
   void check_rings_unwritten(Slot& sl, const DeviceHostMemory& mem, void* stream);
-  void fire_interrupts(const RxBatchResult& r);  // config_.on_interrupt over r's completions
+  void fire_interrupts(RxBatchResult& r, Slot* sl = nullptr);  // config_.on_interrupt over r's completions
   std::pair<std::span<const TxDescriptor>, std::span<const RxDescriptor>> host_spans(
       Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx, void* stream);
   // the host path (buffers_disjoint unless `disjoint` is known, then run_batch)
@@ -550,6 +552,15 @@ struct InterruptCursor {
 };
 void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> tx_completions,
                        std::span<const CompletionEntry> rx_completions, InterruptCursor& at, std::size_t n);
+
+/// The same over completions that are still landing, chunk by chunk:
+/// wait_chunk(0, c) is called before TX completion c * chunk_tx onwards is
+/// first read, wait_chunk(1, c) before RX completion c * chunk_rx onwards
+/// (each chunk once, in order) — so the callbacks start on the first chunk
+/// while the later ones are still on their way down.
+void replay_interrupts_chunked(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> tx_completions,
+                               std::span<const CompletionEntry> rx_completions, std::size_t chunk_tx,
+                               std::size_t chunk_rx, const std::function<void(int, std::size_t)>& wait_chunk);
 
 /// Order of the DMA writes of one resolved sub-batch for parallel gathers.
 /// Writes (RX completions j with write_of_rx[j] >= 0 and at least one byte) are

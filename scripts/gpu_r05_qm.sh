@@ -13,4 +13,9 @@ for kind in pinned device hostmem; do
   timeout -k 10 200 $B qm16 1048576 6 0 device $kind sync device > gpurun_out/r05_qm16_$kind.json 2> gpurun_out/r05_qm16_$kind.err || { tail gpurun_out/r05_qm16_$kind.err; exit 1; }
   cat gpurun_out/r05_qm16_$kind.json
 done
+# interrupts on, results in HBM: the chunked completion download beside the replay, and the callback floor
+timeout -k 10 200 $B c3 1048576 6 0 device device pipelined device irq > gpurun_out/r05_irq.json 2> gpurun_out/r05_irq.err || { tail gpurun_out/r05_irq.err; exit 1; }
+cat gpurun_out/r05_irq.json
+timeout -k 10 300 $PT tests/test_rx_stage.py -m gpu -k "pipelined or device_resolve" > gpurun_out/r05_irq_tests.log 2>&1
+rc=$?; tail -5 gpurun_out/r05_irq_tests.log; [ $rc -eq 0 ] || exit $rc
 echo done

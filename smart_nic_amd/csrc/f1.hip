@@ -1318,10 +1318,38 @@ __global__ __launch_bounds__(kQpBlock) void qp_seg_rel_kernel(QpSegs S, uint32_t
   }
 }
 
-// per-segment RSS hits of the delivered frames
+// per-segment RSS hits of the delivered frames.  Each block takes a
+// contiguous range of slots, which meets one or two segments: per segment an
+// LDS histogram, flushed once (its nonzero bins) with global atomics — one
+// atomic per slot on a few thousand addresses took 1.3 ms per 1 M slots.
+constexpr uint32_t kQpSegHitsLds = 8192;  // table entries histogrammed in LDS
 __global__ __launch_bounds__(kQpBlock) void qp_seg_hits_kernel(QpSegs S, uint64_t nrx, const nicgpu_completion* __restrict__ rxc,
                                                                const uint32_t* __restrict__ rx_hash, uint64_t tn,
                                                                unsigned long long* hits) {
+  __shared__ uint32_t h[kQpSegHitsLds];
+  const uint64_t per = (nrx + gridDim.x - 1) / gridDim.x;
+  const uint64_t lo = (uint64_t) blockIdx.x * per, hi = lo + per < nrx ? lo + per : nrx;
+  if (lo >= hi) return;
+  for (uint32_t s = qp_seg_of_rx(S, lo); s < S.nseg && S.seg[s].rx_begin < hi; ++s) {
+    const uint64_t a = S.seg[s].rx_begin > lo ? S.seg[s].rx_begin : lo;
+    const uint64_t e0 = S.seg[s].rx_begin + S.seg[s].nrx, e = e0 < hi ? e0 : hi;
+    if (a >= e) continue;
+    for (uint32_t k = threadIdx.x; k < tn; k += kQpBlock) h[k] = 0u;
+    __syncthreads();
+    for (uint64_t j = a + threadIdx.x; j < e; j += kQpBlock)
+      if (rxc[j].status == nicqp::kSuccess) atomicAdd(&h[rx_hash[j] % tn], 1u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < tn; k += kQpBlock)
+      if (h[k]) atomicAdd(&hits[(uint64_t) s * tn + k], (unsigned long long) h[k]);
+    __syncthreads();
+  }
+}
+
+// (tables above kQpSegHitsLds entries) one global atomic per delivered frame
+__global__ __launch_bounds__(kQpBlock) void qp_seg_hits_global_kernel(QpSegs S, uint64_t nrx,
+                                                                      const nicgpu_completion* __restrict__ rxc,
+                                                                      const uint32_t* __restrict__ rx_hash, uint64_t tn,
+                                                                      unsigned long long* hits) {
   for (uint64_t j = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; j < nrx; j += (uint64_t) gridDim.x * kQpBlock) {
     if (rxc[j].status != nicqp::kSuccess) continue;
     atomicAdd(&hits[(uint64_t) qp_seg_of_rx(S, j) * tn + rx_hash[j] % tn], 1ull);
@@ -2325,9 +2353,17 @@ int nicgpu_qp_segment_hits(nicgpu_qp* q, size_t nrx, size_t table_n, uint64_t* h
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   int st = hip_status(hipMemsetAsync(hits_dev, 0, (size_t) q->nseg * table_n * sizeof(uint64_t), s));
-  if (st == NICGPU_OK && nrx) {
-    hipLaunchKernelGGL(qp_seg_hits_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, qp_segs(q), (uint64_t) nrx,
-                       q->rxc, q->rx_hash, (uint64_t) table_n, reinterpret_cast<unsigned long long*>(hits_dev));
+  if (st == NICGPU_OK && nrx && table_n <= kQpSegHitsLds) {
+    // a few blocks of long ranges: ~1 K atomics of histogram bins per segment
+    const uint64_t want = (nrx + 8191) / 8192;
+    const unsigned grid = (unsigned) (want < 256 ? (want ? want : 1) : 256);
+    hipLaunchKernelGGL(qp_seg_hits_kernel, dim3(grid), dim3(kQpBlock), 0, s, qp_segs(q), (uint64_t) nrx, q->rxc,
+                       q->rx_hash, (uint64_t) table_n, reinterpret_cast<unsigned long long*>(hits_dev));
+    st = hip_status(hipGetLastError());
+  } else if (st == NICGPU_OK && nrx) {
+    hipLaunchKernelGGL(qp_seg_hits_global_kernel, dim3(qp_grid(q, nrx)), dim3(kQpBlock), 0, s, qp_segs(q),
+                       (uint64_t) nrx, q->rxc, q->rx_hash, (uint64_t) table_n,
+                       reinterpret_cast<unsigned long long*>(hits_dev));
     st = hip_status(hipGetLastError());
   }
   return st;

@@ -94,21 +94,49 @@ struct Top2 {
 namespace qm_detail {
 
 QueueSchedule schedule(std::span<const std::uint8_t> weights, std::span<const std::size_t> pending, std::size_t& index,
-                       std::size_t& credit) {
+                       std::size_t& credit, bool want_runs) {
   QueueSchedule out;
   const std::size_t Q = weights.size();
   if (Q == 0) return out;
   std::vector<std::size_t> left(pending.begin(), pending.end());
   left.resize(Q, 0);
   for (;;) {  // one process_once per iteration (a run of them while the turn holds)
+    // Without the runs, whole cycles are counted at once: from a fresh turn on
+    // a nonempty queue, one trip round the ring serves weights[q] from every
+    // nonempty queue and skips every empty one once, and comes back to the
+    // same turn — as long as every nonempty queue has weights[q] left, and
+    // more is served after it (the empty queues after the last serve are
+    // skipped by the final call instead): k - 1 of the k possible cycles.
+    if (!want_runs && left[index] > 0 && credit == weights[index]) {
+      std::size_t k = ~std::size_t{0}, served_per = 0, empty = 0;
+      for (std::size_t q = 0; q < Q; ++q) {
+        if (left[q] == 0) {
+          ++empty;
+          continue;
+        }
+        k = std::min(k, left[q] / weights[q]);
+        served_per += weights[q];
+      }
+      if (k > 1 && k != ~std::size_t{0}) {
+        k -= 1;
+        for (std::size_t q = 0; q < Q; ++q)
+          if (left[q]) left[q] -= k * weights[q];
+        out.advances += k * served_per;
+        out.skips += k * empty;
+      }
+    }
     bool served = false;
     for (std::size_t tries = 0; tries < Q; ++tries) {
       if (left[index] > 0) {
         // process_once returns true for every descriptor of the batch: the
         // turn serves min(credit, left) of them, then passes when the credit ends
         const std::size_t k = std::min(credit, left[index]);
-        if (!out.runs.empty() && out.runs.back().queue == index) out.runs.back().count += static_cast<std::uint32_t>(k);
-        else out.runs.push_back({static_cast<std::uint32_t>(index), static_cast<std::uint32_t>(k)});
+        if (!want_runs) {
+        } else if (!out.runs.empty() && out.runs.back().queue == index) {
+          out.runs.back().count += static_cast<std::uint32_t>(k);
+        } else {
+          out.runs.push_back({static_cast<std::uint32_t>(index), static_cast<std::uint32_t>(k)});
+        }
         left[index] -= k;
         out.advances += k;
         if (k == credit) {
@@ -319,7 +347,7 @@ QueueSchedule BatchedQueueManager::process_batch(const DeviceHostMemory& mem, st
     if (fused_->process_queues(mem, nullptr, txs, rxs, cfgs, out, st, stream, /*dev_desc=*/true, /*whole_check=*/true)) {
       for (std::size_t q = 0; q < Q; ++q) add_delta(qps_[q]->stats, st[q], QueuePairStats{});
       std::size_t index = index_, credit = credit_;
-      QueueSchedule sched = qm_detail::schedule(weights_, n, index, credit);
+      QueueSchedule sched = qm_detail::schedule(weights_, n, index, credit, interrupts());
       index_ = index;
       credit_ = credit;
       advances_ += sched.advances;
@@ -357,14 +385,16 @@ QueueSchedule BatchedQueueManager::run(const DeviceHostMemory& dmem, HostMemory*
   for (std::size_t q = 0; q < Q; ++q) n[q] = batches[q].tx.size();
   out.resize(Q);
   for (RxBatchResult& r : out) clear_result(r);
-  std::size_t index = index_, credit = credit_;
-  QueueSchedule sched = qm_detail::schedule(weights_, n, index, credit);
   // a HostMemory: the manager's one mirror of it (every stage shares it)
   BatchedQueuePair::HostImage* img = hmem ? &fused_->bind_image(*hmem) : nullptr;
   const std::size_t mem_size = hmem ? hmem->config().size_bytes : dmem.size;
   last_fused_ = 0;
   bool fused = false;
   const bool disjoint = qm_detail::queues_disjoint(mem_size, batches);
+  // the runs of the schedule: for the reference's interleaving on the host
+  // path and for the interrupts' order; the counters alone otherwise
+  std::size_t index = index_, credit = credit_;
+  QueueSchedule sched = qm_detail::schedule(weights_, n, index, credit, !disjoint || interrupts());
   if (disjoint && fusable()) {
     std::vector<std::span<const TxDescriptor>> txs(Q);
     std::vector<std::span<const RxDescriptor>> rxs(Q);
@@ -474,12 +504,16 @@ QueueSchedule BatchedQueueManager::run(const DeviceHostMemory& dmem, HostMemory*
   return sched;
 }
 
+bool BatchedQueueManager::interrupts() const {
+  for (const auto& qp : qps_)
+    if (qp->config.on_interrupt && (qp->config.enable_tx_interrupts || qp->config.enable_rx_interrupts)) return true;
+  return false;
+}
+
 // interrupts in the order the reference's dispatcher sees them: run by run
 void BatchedQueueManager::replay(const QueueSchedule& sched, const std::vector<RxBatchResult>& out, void* stream) {
   const std::size_t Q = qps_.size();
-  bool any = false;
-  for (const auto& qp : qps_) any |= qp->config.on_interrupt && (qp->config.enable_tx_interrupts || qp->config.enable_rx_interrupts);
-  if (any) {
+  if (interrupts()) {
     std::vector<std::vector<CompletionEntry>> htx(Q), hrx(Q);
     std::vector<std::span<const CompletionEntry>> txc(Q), rxc(Q);
     for (std::size_t q = 0; q < Q; ++q) {

@@ -131,8 +131,13 @@ void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const Com
   replay_interrupts(config, txc, rxc, at, txc.size());
 }
 
-void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> txc,
-                       std::span<const CompletionEntry> rxc, InterruptCursor& at, std::size_t n) {
+namespace {
+// The replay loop; ready_tx(i) / ready_rx(j) are called before TX completion i
+// / RX completion j is first read (completions still landing in chunks).
+template <class ReadyTx, class ReadyRx>
+void replay_core(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> txc,
+                 std::span<const CompletionEntry> rxc, InterruptCursor& at, std::size_t n, ReadyTx&& ready_tx,
+                 ReadyRx&& ready_rx) {
   constexpr auto kOk = static_cast<std::uint32_t>(CompletionCode::Success);
   constexpr auto kFault = static_cast<std::uint32_t>(CompletionCode::Fault);
   const bool any = config.on_interrupt && (config.enable_tx_interrupts || config.enable_rx_interrupts);
@@ -148,6 +153,7 @@ void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const Com
   const CompletionEntry* R = rxc.data();
   const std::size_t nr = rxc.size();
   for (std::size_t i = at.tx; i < end; ++i) {
+    ready_tx(i);
     const CompletionEntry& t = txc[i];
     // the packets that popped RX descriptors: Success (all delivered, or an
     // RX-side abort), and a DMA write fault after some segment (segments_produced > 0)
@@ -156,6 +162,7 @@ void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const Com
     if (popped) {
       fires = t.status == kOk;  // a faulted packet's TX completion fires none
       for (std::uint32_t k = 0; k < t.segments_produced && j < nr; ++k) {
+        ready_rx(j);
         const CompletionEntry& e = R[j++];
         if (rx_on) cb(q, e);
         if (e.status != kOk) {  // the packet ends here and its TX completion fires none
@@ -168,6 +175,34 @@ void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const Com
   }
   at.tx = end;
   at.rx = j;
+}
+}  // namespace
+
+void replay_interrupts(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> txc,
+                       std::span<const CompletionEntry> rxc, InterruptCursor& at, std::size_t n) {
+  replay_core(config, txc, rxc, at, n, [](std::size_t) {}, [](std::size_t) {});
+}
+
+void replay_interrupts_chunked(const BatchedQueuePairConfig& config, std::span<const CompletionEntry> txc,
+                               std::span<const CompletionEntry> rxc, std::size_t chunk_tx, std::size_t chunk_rx,
+                               const std::function<void(int, std::size_t)>& wait_chunk) {
+  if (!config.on_interrupt || (!config.enable_tx_interrupts && !config.enable_rx_interrupts)) return;
+  InterruptCursor at;
+  std::size_t next_tx = 0, next_rx = 0;  // first index not yet known to have landed
+  replay_core(
+      config, txc, rxc, at, txc.size(),
+      [&](std::size_t i) {
+        if (i >= next_tx) {
+          wait_chunk(0, i / chunk_tx);
+          next_tx = (i / chunk_tx + 1) * chunk_tx;
+        }
+      },
+      [&](std::size_t j) {
+        if (j >= next_rx) {
+          wait_chunk(1, j / chunk_rx);
+          next_rx = (j / chunk_rx + 1) * chunk_rx;
+        }
+      });
 }
 
 // Count pass, prefix over the chunks, fill pass (each chunk in its own thread).
@@ -1072,6 +1107,14 @@ struct BatchedQueuePair::Slot {
   std::size_t nseg = 0;
   HostBuf h_split, h_seg_hits;
   DevBuf seg_hits;
+  // interrupt callbacks of a batch whose results stay on the device: its
+  // completions come down in chunks into page-locked memory as soon as they
+  // are final (side_irq), and the replay starts on the first chunk
+  static constexpr int kIrqChunks = 16;
+  void* ev_irq[2][kIrqChunks] = {};
+  HostBuf h_itx, h_irx;
+  bool irq_pending = false;
+  std::size_t irq_ntx = 0, irq_nrx = 0;
 
   void release_rss() {
     if (!rss_released) rss_recorded.set_value();
@@ -1089,6 +1132,13 @@ struct BatchedQueuePair::Slot {
     if (qp) (void) nicgpu_qp_destroy(qp);
     if (wb) (void) nicgpu_event_synchronize(ev_wb);  // no write-back may outlive the slot's buffers
     wb = false;
+    for (auto& side : ev_irq)
+      for (void*& e : side) {
+        if (e && irq_pending) (void) nicgpu_event_synchronize(e);
+        if (e) (void) nicgpu_event_destroy(e);
+        e = nullptr;
+      }
+    irq_pending = false;
     for (void* e : {ev_tx, ev_rx, ev_resolved, ev_done, ev_submit, ev_staged, ev_wb})
       if (e) (void) nicgpu_event_destroy(e);
     qp = nullptr;
@@ -1098,6 +1148,8 @@ struct BatchedQueuePair::Slot {
     check(nicgpu_qp_create(&qp, dev), "nicgpu_qp_create");
     for (void** e : {&ev_tx, &ev_rx, &ev_resolved, &ev_done, &ev_submit, &ev_staged, &ev_wb})
       check(nicgpu_event_create(e), "nicgpu_event_create");
+    for (auto& side : ev_irq)
+      for (void*& e : side) check(nicgpu_event_create(&e), "nicgpu_event_create");
   }
   // the batch's bytes are in the host memory (host-image batches)
   void wait_writeback() {
@@ -1144,6 +1196,7 @@ struct BatchedQueuePair::Scratch {
   void* side_down = nullptr;
   void* side_plan = nullptr;  // plan and overlap check of a batch beside the earlier batch's writes
   void* side_wb = nullptr;    // host-image write-backs, beside the next batches' work
+  void* side_irq = nullptr;   // completions for the interrupt callbacks, as soon as they are final
   std::shared_ptr<HostImage> img = std::make_shared<HostImage>();  // the HostMemory the host-image batches run against (shared by a manager's stages)
   SideWorker up_worker;  // process_batch: issues the RX descriptor uploads
   static constexpr unsigned kSlots = 3;
@@ -1156,7 +1209,8 @@ struct BatchedQueuePair::Scratch {
     if (side_down) (void) nicgpu_stream_destroy(side_down);
     if (side_plan) (void) nicgpu_stream_destroy(side_plan);
     if (side_wb) (void) nicgpu_stream_destroy(side_wb);
-    side_up = side_down = side_plan = side_wb = nullptr;
+    if (side_irq) (void) nicgpu_stream_destroy(side_irq);
+    side_up = side_down = side_plan = side_wb = side_irq = nullptr;
     if (img.use_count() == 1) img->release();  // a manager's shared image is released by its last stage
     device = -1;
   }
@@ -1167,6 +1221,7 @@ struct BatchedQueuePair::Scratch {
     check(nicgpu_stream_create(&side_down), "nicgpu_stream_create");
     check(nicgpu_stream_create_priority(&side_plan, 1), "nicgpu_stream_create_priority");
     check(nicgpu_stream_create(&side_wb), "nicgpu_stream_create");
+    check(nicgpu_stream_create(&side_irq), "nicgpu_stream_create");
     for (Slot& sl : slot) sl.create(dev);
     device = dev;
   }
@@ -1361,7 +1416,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
   if (!on_device) on_host(mem, tx, rx, st, out, stream, disjoint, check_us);
   out.timings.check_us = check_us;
   stats_ = st;
-  if (config_.on_interrupt) fire_interrupts(out);
+  if (config_.on_interrupt) fire_interrupts(out, &scratch_->slot[0]);
 }
 
 void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
@@ -1416,7 +1471,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDe
   }
   out.timings.check_us = check_us;
   stats_ = st;
-  if (config_.on_interrupt) fire_interrupts(out);
+  if (config_.on_interrupt) fire_interrupts(out, &sl);
 }
 
 // Device descriptor arrays inside the image: no RX buffer of the batch may
@@ -1574,14 +1629,40 @@ bool BatchedQueuePair::collect(RxBatchResult& out) {
   else sl.wait_writeback();  // a host-path batch of a HostMemory: its bytes are back
   rx_stage_detail::add_stats(stats_, sl.stats);
   std::swap(out, sl.result);
-  if (config_.on_interrupt) fire_interrupts(out);
+  if (config_.on_interrupt) fire_interrupts(out, &sl);
   return true;
 }
 
-// Completions still on the device (results_on_device) are fetched first.
-void BatchedQueuePair::fire_interrupts(const RxBatchResult& r) {
+// Completions still on the device (results_on_device) come from the slot's
+// chunked page-locked copies (back()), the replay waiting for each chunk as it
+// reaches it; without them they are fetched first.
+void BatchedQueuePair::fire_interrupts(RxBatchResult& r, Slot* sl) {
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  struct Timed {
+    RxBatchResult& r;
+    clock::time_point t0;
+    ~Timed() { r.timings.irq_us = std::chrono::duration<double, std::micro>(clock::now() - t0).count(); }
+  } timed{r, t0};
   if (!r.timings.device || !config_.results_on_device) {
     rx_stage_detail::replay_interrupts(config_, r.tx_completions, r.rx_completions);
+    return;
+  }
+  if (sl && sl->irq_pending && sl->irq_ntx == r.dev.ntx && sl->irq_nrx == r.dev.nrx) {
+    sl->irq_pending = false;
+    const std::size_t ptx = std::max<std::size_t>(1, (sl->irq_ntx + Slot::kIrqChunks - 1) / Slot::kIrqChunks);
+    const std::size_t prx = std::max<std::size_t>(1, (sl->irq_nrx + Slot::kIrqChunks - 1) / Slot::kIrqChunks);
+    double wait_us = 0;
+    rx_stage_detail::replay_interrupts_chunked(
+        config_, std::span<const CompletionEntry>(sl->h_itx.get<CompletionEntry>(1), sl->irq_ntx),
+        std::span<const CompletionEntry>(sl->h_irx.get<CompletionEntry>(1), sl->irq_nrx), ptx, prx,
+        [sl, &wait_us](int side, std::size_t c) {
+          const auto w = clock::now();
+          check(nicgpu_event_synchronize(sl->ev_irq[side][std::min<std::size_t>(c, Slot::kIrqChunks - 1)]),
+                "nicgpu_event_synchronize");
+          wait_us += std::chrono::duration<double, std::micro>(clock::now() - w).count();
+        });
+    r.timings.irq_wait_us = wait_us;
     return;
   }
   Scratch& S = *scratch_;
@@ -1894,6 +1975,29 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   sl.rss_released = false;
   std::shared_future<void> rss_ready = sl.rss_recorded.get_future().share();
   if (sl.relaxed) check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");
+  sl.irq_pending = false;
+  if (keep && config_.on_interrupt && (config_.enable_tx_interrupts || config_.enable_rx_interrupts) && !sl.multi) {
+    // the completions for the callbacks, in chunks, page-locked, as soon as
+    // they are final: collect() replays chunk c while chunk c + 1 lands
+    check(nicgpu_stream_wait_event(S.side_irq, sl.ev_resolved), "nicgpu_stream_wait_event");
+    const std::size_t n2[2] = {ntx, nrx_total};
+    CompletionEntry* dst[2] = {sl.h_itx.get<CompletionEntry>(std::max<std::size_t>(ntx, 1)),
+                               sl.h_irx.get<CompletionEntry>(std::max<std::size_t>(nrx_total, 1))};
+    const nicgpu_completion* src[2] = {v.txc, v.rxc};
+    for (int side = 0; side < 2; ++side) {
+      const std::size_t per = std::max<std::size_t>(1, (n2[side] + Slot::kIrqChunks - 1) / Slot::kIrqChunks);
+      for (int c = 0; c < Slot::kIrqChunks; ++c) {
+        const std::size_t a = std::min(n2[side], c * per), b = std::min(n2[side], a + per);
+        if (b > a)
+          check(nicgpu_memcpy_async(dst[side] + a, src[side] + a, (b - a) * sizeof(CompletionEntry), S.side_irq),
+                "nicgpu_memcpy_async");
+        check(nicgpu_event_record(sl.ev_irq[side][c], S.side_irq), "nicgpu_event_record");
+      }
+    }
+    sl.irq_ntx = ntx;
+    sl.irq_nrx = nrx_total;
+    sl.irq_pending = true;
+  }
   sl.down.emplace(sl.worker);
   // the dispatch lists are made here too, on the download stream: they read
   // this slot's buffers only, so the next batch's piece sums need not queue
@@ -2211,7 +2315,7 @@ void BatchedQueuePair::process_batch(HostMemory& m, std::span<const TxDescriptor
   }
   out.timings.check_us = check_us;
   stats_ = st;
-  if (config_.on_interrupt) fire_interrupts(out);
+  if (config_.on_interrupt) fire_interrupts(out, &sl);
 }
 
 void BatchedQueuePair::submit(HostMemory& m, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,

@@ -78,6 +78,15 @@ def test_fixture_shape():
     assert skips > 0 and adv > 0 and 0 in weights and max(weights) > 2
 
 
+def test_schedule_counters_only_form(tmp_path):
+    """qm_detail::schedule without its runs (whole round-robin cycles counted
+    at once, the fused path's form) equals the run-by-run drain."""
+    exe = _build(tmp_path, "qm_test")
+    r = subprocess.run([exe, "schedule"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "counters-only form equals" in r.stdout
+
+
 def test_queue_manager_cpu(tmp_path):
     exe = _build(tmp_path, "qm_test")
     for name, disjoint in CASES.items():

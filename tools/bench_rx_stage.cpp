@@ -240,9 +240,12 @@ int main(int argc, char** argv) {
     for (std::size_t i = 0; i < per * Q; ++i) fb += lens[i];
     std::printf("{\"row\": \"f1_queue_manager\", \"workload\": \"c3\", \"queue_pairs\": %zu, \"tx_per_queue\": %zu, "
                 "\"descriptors\": \"%s\", \"results\": \"%s\", \"host_memory\": %s, \"rx_align\": %zu, \"rx_completions\": %llu, "
-                "\"fused_drains\": %d, \"drains\": %d, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f}\n",
+                "\"fused_drains\": %d, \"drains\": %d, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
+                "\"phases_us\": {\"check\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f}}\n",
                 Q, per, desc_kind.c_str(), cfg.results_on_device ? "device" : "host", hostmem ? "true" : "false", rx_align,
-                (unsigned long long) ok_q, fused, reps, med, per * Q / med, fb / med / 1e3);
+                (unsigned long long) ok_q, fused, reps, med, per * Q / med, fb / med / 1e3, outs[0].timings.check_us,
+                outs[0].timings.sums_us, outs[0].timings.resolve_us, outs[0].timings.gather_us, outs[0].timings.rss_us,
+                outs[0].timings.copy_us);
     nicgpu_free(mem);
     if (ptx) nicgpu_host_free(ptx);
     if (prx) nicgpu_host_free(prx);
@@ -302,6 +305,27 @@ int main(int argc, char** argv) {
           "memcpy");
     check(nicgpu_stream_synchronize(nullptr), "sync");
   }
+  // the interrupt callbacks' floor: the same replay over host arrays of the
+  // last batch's completions, no GPU (what the irq row cannot go below)
+  double floor_us = 0;
+  const std::uint64_t irq_batches = irq_count;  // callbacks of the measured batches (the floor replays add more)
+  if (irq) {
+    std::vector<CompletionEntry> htc = last.tx_completions;
+    if (last.timings.device && cfg.results_on_device) {
+      htc.resize(last.dev.ntx);
+      check(nicgpu_memcpy_async(htc.data(), last.dev.tx_completions, last.dev.ntx * sizeof(CompletionEntry), nullptr),
+            "memcpy");
+      check(nicgpu_stream_synchronize(nullptr), "sync");
+    }
+    std::vector<double> fl;
+    for (int k = 0; k < 5; ++k) {
+      const auto t0 = std::chrono::steady_clock::now();
+      rx_stage_detail::replay_interrupts(cfg, htc, last.rx_completions);
+      fl.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+    std::sort(fl.begin(), fl.end());
+    floor_us = fl[fl.size() / 2];
+  }
   for (const auto& c : last.rx_completions) ok += c.status == 0;
   for (auto L : lens) frame_bytes += L;
   if (hostmem) {  // the last batch's frames are in the host memory, byte for byte
@@ -316,11 +340,11 @@ int main(int argc, char** argv) {
   const auto& T = tot[tot.size() / 2].second;  // the median batch's phases
   std::printf(
       "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"mode\": \"%s\", \"results\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, \"rx_align\": %zu, "
-      "\"rx_success\": %zu, \"host_memory\": %s, \"tx_staged_whole\": %s, \"interrupts\": %s, \"irq_callbacks\": %llu, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
-      "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f}}\n",
+      "\"rx_success\": %zu, \"host_memory\": %s, \"tx_staged_whole\": %s, \"interrupts\": %s, \"irq_callbacks\": %llu, \"callback_floor_us\": %.1f, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
+      "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f, \"irq\": %.1f, \"irq_wait\": %.1f}}\n",
       wl.c_str(), T.device ? "device" : "host", desc_kind.c_str(), pipelined ? "pipelined" : "sync", cfg.results_on_device ? "device" : "host", cfg.host_threads, n, last.rx_completions.size(), rx_align, ok,
-      T.host_image ? "true" : "false", T.staged_whole ? "true" : "false", irq ? "true" : "false", (unsigned long long) irq_count, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
-      T.resolve_us, T.gather_us, T.rss_us, T.copy_us);
+      T.host_image ? "true" : "false", T.staged_whole ? "true" : "false", irq ? "true" : "false", (unsigned long long) irq_batches, floor_us, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
+      T.resolve_us, T.gather_us, T.rss_us, T.copy_us, T.irq_us, T.irq_wait_us);
   nicgpu_free(mem);
   if (ptx) nicgpu_host_free(ptx);
   if (prx) nicgpu_host_free(prx);
