@@ -245,189 +245,6 @@ __global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
   }
 }
 
-// ------------------------------------------- pipelined lane walk (round 5) --
-// icrc_b4_kernel waits one memory round trip per step: its step's loads go out,
-// then the chain consumes them.  Here every lane keeps TWO windows in flight:
-// the next window's loads (the same packet's next CH-chunk window, or — when
-// this window ends the packet — the first window of the packet the wave's
-// work queue hands it next, decided BEFORE this window's chain, since only
-// positions decide it) are issued before this window's chain, so the chain
-// and the next round trip overlap and a wave has twice the bytes in flight.
-// The packet's tail dword (1..3 bytes past its last whole dword) is loaded with
-// the next window too.  Same arithmetic as icrc_b4_kernel.
-struct IcrcWin {  // a lane's window: its packet, where the window lies, what the chain takes from it
-  uint64_t my, c16;
-  uint32_t pos, end4, wend, len, lb, cur, cl, lim;
-  bool active, last;
-};
-
-template <int CH>
-__device__ __forceinline__ void icrc_window(IcrcWin& w, uint32_t cur) {
-  w.cur = cur;
-  if (cur >= w.end4) {  // nothing (more) to chain: empty window, the packet's last
-    w.cl = 0;
-    w.lim = 0;
-    w.last = true;
-    return;
-  }
-  const uint32_t c0 = cur >> 4, clast = (w.end4 - 1u) >> 4;
-  const uint32_t ce = ((w.lb + c0) | (uint32_t) (CH - 1)) - w.lb;
-  w.cl = ce < clast ? ce : clast;
-  const uint32_t e = (w.cl + 1u) << 4;
-  w.lim = (e < w.end4 ? e : w.end4) - cur;
-  w.last = e >= w.end4;
-}
-
-// Every load of an iteration is unconditional (inactive lanes and empty
-// windows read chunk 0; a lane that needs no tail dword reads the image's
-// first one), so hipcc counts them exactly and the chain waits for this
-// window's loads only (vmcnt(k), not 0).  The descriptor ring is refilled the
-// same way: each iteration loads a 64-descriptor block (the same block again,
-// a cache hit, when no refill is due) and the next iteration writes it into
-// the 256-entry ring before it reads it — so that load, too, never drains the
-// window loads behind it.
-constexpr int kIcrcPipeRing = 256;
-
-template <int CH, int MODE>
-__global__ __launch_bounds__(kIcrcThreads) void icrc_pipe_kernel(IcrcParams P) {
-  __shared__ __attribute__((aligned(16))) uint8_t Tb[kB4Bytes];
-  __shared__ uint64_t ring_all[kIcrcWpb][kIcrcPipeRing];
-  __shared__ uint4 lead_m[16];  // bytes >= p of a chunk kept
-  __shared__ uint32_t lead_s[16];
-  if (threadIdx.x < 16u) {
-    const int p = (int) threadIdx.x;
-    lead_s[p] = kCrcLead.s[p];
-    lead_m[p] = make_uint4(dword_keep(p, 16, 0), dword_keep(p, 16, 1), dword_keep(p, 16, 2), dword_keep(p, 16, 3));
-  }
-  for (uint32_t q = threadIdx.x; q < kB4Bytes / 16u; q += kIcrcThreads) {
-    const uint32_t o = q * 16u;
-    const uint32_t j = 2u * (o >> 16) + ((o >> 7) & 1u), v = (o >> 8) & 255u;
-    const uint32_t val = kCrc32c.t[3u - j][v];
-    reinterpret_cast<uint4*>(Tb)[q] = make_uint4(val, val, val, val);
-  }
-  __syncthreads();
-  const uint32_t lane = lane_id();
-  const uint32_t cb = (lane & 31u) << 2;  // this lane's copy: bank lane % 32
-  const uint32_t cbr = cb | ((cb + 128u) << 8) | (1u << 24);
-  uint64_t* ring = ring_all[threadIdx.x / kWave];
-  const uint64_t nwaves = (uint64_t) gridDim.x * kIcrcWpb;
-  const uint64_t wave = (uint64_t) blockIdx.x * kIcrcWpb + threadIdx.x / kWave;
-  const uint64_t per = (P.n + nwaves - 1) / nwaves;
-  const uint64_t p0 = wave * per < P.n ? wave * per : P.n;
-  const uint64_t p1 = p0 + per < P.n ? p0 + per : P.n;
-  const u32x4* f16 = reinterpret_cast<const u32x4*>(P.frames);
-  const uint64_t dlast = p1 ? p1 - 1 : 0;  // a valid descriptor to re-read when nothing is due
-
-  uint64_t loaded = p0;
-  for (int k = 0; k < 2; ++k) {  // the first two blocks, before the loop
-    const uint64_t i = loaded + lane;
-    ring[i & (kIcrcPipeRing - 1)] = i < p1 ? P.desc[i] : 0ull;
-    loaded += kWave;
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  auto setup = [&](IcrcWin& w, uint64_t my) __attribute__((always_inline)) {
-    w.my = my;
-    w.active = my < p1;
-    const uint64_t d = w.active ? ring[my & (kIcrcPipeRing - 1)] : 0ull;
-    const uint64_t off = d & kOffMask;
-    w.len = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
-    const uint32_t span = P.verify ? (w.len >= 4u ? w.len - 4u : 0u) : w.len;
-    w.c16 = off >> 4;
-    w.lb = (uint32_t) w.c16 & (uint32_t) (CH - 1);
-    w.pos = (uint32_t) off & 15u;
-    const uint32_t end = w.pos + span;
-    w.wend = span ? end : 0u;
-    w.end4 = w.wend & ~3u;
-    icrc_window<CH>(w, 0u);
-  };
-  auto load = [&](const IcrcWin& w, u32x4* v) __attribute__((always_inline)) {
-    const uint32_t c0 = w.cur >> 4;
-    const uint64_t base = w.lim ? w.c16 : 0u;  // an empty window reads chunk 0
-#pragma unroll
-    for (int u = 0; u < CH; ++u) v[u] = f16[base + (c0 + (uint32_t) u <= w.cl ? c0 + (uint32_t) u : w.cl)];
-  };
-  uint64_t next = p0 + kWave;
-  IcrcWin A, B;
-  setup(A, p0 + lane);
-  u32x4 va[CH], vb[CH];
-  load(A, va);
-  uint32_t S = A.active && A.wend ? lead_s[A.pos] : 0xFFFFFFFFu;
-  uint64_t dreg = 0;
-  bool pending = false;
-  for (;;) {
-    if (pending) {  // the block the last iteration loaded: into the ring before any setup reads it
-      ring[(loaded + lane) & (kIcrcPipeRing - 1)] = loaded + lane < p1 ? dreg : 0ull;
-      loaded += kWave;
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    }
-    if (__ballot(A.active) == 0ull) break;
-    // the window after A: A's packet's next, or the next packet's first
-    const bool fin = A.active && A.last;
-    const uint64_t m = __ballot(fin);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
-    if (fin) {
-      setup(B, next + rank);
-    } else {
-      B = A;
-      if (A.active) icrc_window<CH>(B, (A.cl + 1u) << 4);
-    }
-    next += (uint64_t) __builtin_popcountll(m);
-    // this iteration's loads, all unconditional: the next descriptor block
-    // (a refill is due when fewer than two blocks are ahead of `next`), B's
-    // window, A's tail dword and (verify) A's stored ICRC
-    // (order: the small loads first, so that using them waits for nothing of
-    // B's window; each is consumed every iteration, branch-free, so no
-    // register of a load still in flight is reused by another instruction)
-    pending = loaded < p1 && next + 2 * kWave > loaded;
-    const uint64_t di = loaded + lane;
-    dreg = P.desc[di < p1 ? di : dlast];
-    const bool tail = fin && A.end4 < A.wend;
-    const uint32_t wv = *reinterpret_cast<const uint32_t*>(P.frames + (tail ? (A.c16 << 4) + A.end4 : 0u));
-    const bool chk = P.verify && fin && A.len >= 4u;
-    uint32_t stored;
-    __builtin_memcpy(&stored, P.frames + (chk ? (A.c16 << 4) + A.pos + (A.len - 4u) : 0u), 4);
-    load(B, vb);
-    __builtin_amdgcn_sched_barrier(0);  // B's loads in flight before A's chain
-    if (A.active && A.lim) {
-      const uint4 m0 = lead_m[A.cur == 0u ? A.pos : 0u];
-      va[0][0] &= m0.x;
-      va[0][1] &= m0.y;
-      va[0][2] &= m0.z;
-      va[0][3] &= m0.w;
-#pragma unroll
-      for (int u = 0; u < CH; ++u) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t Sn = MODE == 1 ? S + va[u][i] : b4_dword(Tb, cbr, S ^ va[u][i]);
-          S = (uint32_t) (16 * u + 4 * i) < A.lim ? Sn : S;
-        }
-      }
-    }
-    // 1..3 bytes past the last whole dword: byte steps on T0 (every lane,
-    // kept only where this window ends a packet with a tail)
-#pragma unroll
-    for (uint32_t b = 0; b < 3u; ++b) {
-      const uint32_t idx = A.end4 + b;
-      const uint32_t z = S ^ (idx < A.pos ? 0u : (wv >> (8u * b)) & 0xFFu);
-      const uint32_t Sn = b4_lookup(Tb, cbr, z, 0x0C070005u) ^ (S >> 8);
-      S = tail && idx < A.wend ? Sn : S;
-    }
-    const uint32_t crc = S ^ 0xFFFFFFFFu;
-    // the stored ICRC, read big-endian (memory order b0 b1 b2 b3 -> b0 << 24 ...)
-    const bool ok = chk && __builtin_bswap32(stored) == crc;
-    if (fin) {
-      if (P.out_crc) P.out_crc[A.my] = (P.verify && A.len < 4u) ? 0u : crc;
-      if (P.verify) P.out_ok[A.my] = (uint8_t) ok;
-      S = B.active && B.wend ? lead_s[B.pos] : 0xFFFFFFFFu;
-    }
-    A = B;
-#pragma unroll
-    for (int u = 0; u < CH; ++u) va[u] = vb[u];
-  }
-}
-
 // ---------------------------------------------- lane-cooperative ICRC --
 // Eight lanes per packet (a group; eight groups per wave), one 128-B line of
 // the packet per step: lane `sub` loads the line's 16-B chunk `sub` — the
@@ -668,7 +485,10 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
   // lane-cooperative one; b4mem / coopmem: timing only, their loads without
   // the table work (results wrong)
   // (the cooperative kernel, measured slower: C2 591 / IMIX 1145 us against
-  // 408 / 471 at 4 lines in flight per group, profiles/r04_icrc_coop.jsonl)
+  // 408 / 471 at 4 lines in flight per group, profiles/r04_icrc_coop.jsonl;
+  // round 5's pipelined lane walk — two windows in flight per lane, exact
+  // vmcnt waits — C2 437 / C3 515 us against 402 / 469, its loads alone 447 /
+  // 420: profiles/r05_icrc_pipe_rejected.jsonl, code in git history)
   static const int var = [] {
     const char* e = std::getenv("NICGPU_ICRC");
     if (!e) return 0;
@@ -676,19 +496,13 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
     if (std::strcmp(e, "b4mem") == 0) return 1;
     if (std::strcmp(e, "b4") == 0) return 0;
     if (std::strcmp(e, "coopmem") == 0) return 3;
-    if (std::strcmp(e, "pipe") == 0) return 4;
-    if (std::strcmp(e, "pipemem") == 0) return 5;
-    if (std::strcmp(e, "pipe4") == 0) return 6;
     return 0;
   }();
   const uint64_t want = (n + kIcrcThreads - 1) / kIcrcThreads;
   const uint64_t cap = (uint64_t) di->cus * (uint64_t) blocks_per_cu(reinterpret_cast<const void*>(icrc_b4_kernel<8, 0>), kIcrcThreads, 0);
   const unsigned grid = (unsigned) (want < 1 ? 1 : (want < cap ? want : cap));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (var == 4) hipLaunchKernelGGL((icrc_pipe_kernel<8, 0>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
-  else if (var == 5) hipLaunchKernelGGL((icrc_pipe_kernel<8, 1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
-  else if (var == 6) hipLaunchKernelGGL((icrc_pipe_kernel<4, 0>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
-  else if (var == 1) hipLaunchKernelGGL((icrc_b4_kernel<8, 1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
+  if (var == 1) hipLaunchKernelGGL((icrc_b4_kernel<8, 1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
   else if (var == 0) hipLaunchKernelGGL((icrc_b4_kernel<8, 0>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
   else if (var == 3) hipLaunchKernelGGL((icrc_coop_kernel<1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
   else hipLaunchKernelGGL((icrc_coop_kernel<0>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
