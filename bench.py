@@ -252,8 +252,10 @@ def gpu_rows():
     (tools/bench_rows.py: HIP events per launch, medians, algorithmic bytes
     and roofline fraction per row), RSS without checksums, and the batched
     QueuePair stage of row f1 on C3 and C5, one batch at a time and pipelined,
-    with host and with device-resident descriptors and results, with interrupt
-    callbacks, and BatchedQueueManager over 16 queue pairs
+    with host and with device-resident descriptors and results, on the
+    reference's HostMemory (host bytes staged to an HBM mirror and written
+    back), with interrupt callbacks, and BatchedQueueManager over 16 queue
+    pairs as one fused batch
     (tools/bin/bench_rx_stage, built by __graft_entry__.build()).  Errors are
     reported, never hidden."""
     import subprocess
@@ -277,8 +279,14 @@ def gpu_rows():
                  ["c3", "1048576", "12", "0", "device", "device", "pipelined", "device"],
                  # TX and RX interrupt callbacks on (2 M per batch, replayed in posting order)
                  ["c3", "1048576", "6", "0", "device", "device", "pipelined", "device", "irq"],
-                 # nic::BatchedQueueManager: 16 queue pairs x 64 K C3 descriptors, one drain
-                 ["qm16", "1048576", "6", "0", "device", "pinned", "sync", "device"]):
+                 # the reference's HostMemory interface: TX bytes staged into an HBM
+                 # mirror, delivered bytes written back over PCIe (FlatHostMemory)
+                 ["c3", "1048576", "8", "0", "device", "hostmem", "pipelined"],
+                 # nic::BatchedQueueManager: 16 queue pairs x 64 K C3 descriptors, one
+                 # drain as one fused device batch; host, HBM and HostMemory descriptors
+                 ["qm16", "1048576", "6", "0", "device", "pinned", "sync", "device"],
+                 ["qm16", "1048576", "6", "0", "device", "device", "sync", "device"],
+                 ["qm16", "1048576", "4", "0", "device", "hostmem", "sync", "device"]):
         try:
             r = subprocess.run([stage, *args], capture_output=True, text=True, timeout=180)
             rows += [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]

@@ -263,7 +263,8 @@ struct RxBatchResult {
     double plan_us{0}, sums_us{0}, resolve_us{0}, gather_us{0}, rss_us{0};
     double copy_us{0};   // device resolve: descriptors up, completions down
     bool device{false};     // resolved on the device
-    bool host_tail{false};  // ... and the rest on the host (positions not settled in 8 relaxation steps)
+    bool host_tail{false};  // ... and the rest on the host (positions settled neither by relaxation nor by the walk)
+    bool walked{false};     // ... positions made by the walk (8 relaxation steps did not settle them)
     bool host_image{false};  // run against a HostMemory: TX bytes staged up, delivered bytes written back
     bool staged_whole{false};  // ... the TX bytes' span went up in one copy (dense), else per descriptor
     unsigned replans{0};    // device plans redone because the first outgrew the piece buffers (at most 1)

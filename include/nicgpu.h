@@ -377,6 +377,11 @@ int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int
 #define NICGPU_QP_CHECK_WHOLE 1u
 int nicgpu_qp_check_flags(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, unsigned flags, int* verdict,
                           void* stream);
+/* nicgpu_qp_check_flags in two halves: _async enqueues the check on `stream`
+ * and returns; _wait waits for its verdict (one check pending per nicgpu_qp).
+ * The check may then run beside the plan and the speculative resolve. */
+int nicgpu_qp_check_async(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, unsigned flags, void* stream);
+int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict);
 /* The kernels of the next plan/check/resolve read the caller's device arrays
  * tx[0, ntx) and rx[0, nrx) in place of view.tx / view.rx (no copy; view is
  * refreshed to point at them).  They must stay valid and unchanged until the
@@ -424,9 +429,15 @@ int nicgpu_qp_piece_count(const nicgpu_qp* q, uint64_t* npieces);
  * step's pops (first guess: what it needs), which is exact for at least one
  * more packet per step and, when a packet's pops do not depend on where in the
  * ring it lands (a ring that runs short, failed segment checksums on uniform
- * RX descriptors), for all of them after two.  After 8 steps *done stops at
- * the first packet not yet exact and the caller resolves the rest in order
- * (piece checksums from view.piece_base[*done]).  Synchronises `stream`. */
+ * RX descriptors), for all of them after two.  When 8 steps have not settled
+ * every packet (a long chain of TSO/GSO packets each ending early on the RX
+ * side), the positions are walked instead: only a packet needing more than one
+ * RX descriptor can pop other than its need while the ring lasts, so one
+ * thread per queue pair resolves those in ring order at their exact positions
+ * and the ring's end is relaxed once more (nicgpu_qp_walks counts these).
+ * Should *done still stop short, it stops at the first packet not yet exact
+ * and the caller resolves the rest in order (piece checksums from
+ * view.piece_base[*done]).  Synchronises `stream`. */
 int nicgpu_qp_resolve(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, uint64_t max_mtu, uint16_t queue_id,
                       uint64_t* done, uint64_t* rx_used, nicgpu_qp_stats* stats, void* stream);
 /* nicgpu_qp_resolve in two halves (NICGPU_ERR_AGAIN / _RANGE from _finish:
@@ -444,6 +455,8 @@ int nicgpu_qp_resolve_start(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t 
                             uint16_t queue_id, void* stream);
 int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, uint64_t* rx_settled,
                              nicgpu_qp_stats* stats);
+/* The resolves of q whose positions the walk made, since q was created. */
+int nicgpu_qp_walks(const nicgpu_qp* q, uint64_t* walks);
 /* The frames of view.rxc[0, nrx) delivered with Success, as RSS descriptors
  * (view.rss_desc[0, m), lengths clipped to NICGPU_MAX_PACKET), m written to
  * the device scalar view.rss_count; view.rx_hash / rx_queue reset to 0 /
@@ -534,6 +547,17 @@ int nicgpu_qp_segment_lists(nicgpu_qp* q, size_t nrx, size_t nq, uint32_t* split
  * the delivery): hits_dev[s * table_n + h % table_n] (u64, set, not added).
  * For queue pairs that count into RssEngines of their own. */
 int nicgpu_qp_segment_hits(nicgpu_qp* q, size_t nrx, size_t table_n, uint64_t* hits_dev, void* stream);
+/* Gathers the queue pairs' device-resident descriptor arrays into the
+ * concatenated view.tx / view.rx in ONE launch: dst[i] <- src[i] (bytes[i]
+ * each) for i < n, all device-accessible, ranges not overlapping.  (The n
+ * separate copies cost a launch each — 2 per queue pair.)  n <= 64 per call. */
+typedef struct nicgpu_copy_range {
+  void* dst;
+  const void* src;
+  uint64_t bytes;
+} nicgpu_copy_range;
+#define NICGPU_COPY_BATCH_MAX 64u
+int nicgpu_memcpy_batch(const nicgpu_copy_range* ranges, size_t n, void* stream);
 
 /* ---- Host-image staging (row f1 on the reference's HostMemory) ----
  * nic::BatchedQueuePair::process_batch(HostMemory&, ...) runs the stage on an

@@ -37,6 +37,7 @@
 #include "nic/simple_host_memory.h"
 #include "nic/tx_rx.h"
 #include "oracle.h"
+#include "../tests/cpp/qm_scale_gen.h"
 
 using namespace nic;
 
@@ -1135,6 +1136,120 @@ void gen_qm() {
   gen_qm_case("qm_alias", 707, {2, 1, 3}, {{30, 25, 20}, {15, 15, 15}}, {{40, 40, 40}, {20, 20, 20}}, 1);
 }
 
+// QueueManager at scale: 16 queue pairs, ≈ 70 K TX descriptors over two rounds
+// (tests/cpp/qm_scale_gen.h makes the input from the seed on both sides; the
+// fixture holds the seed, the schedule counters and digests — see there).
+void gen_qm_scale(std::uint64_t seed) {
+  auto c = qm_scale::make_case<TxDescriptor, RxDescriptor>(seed, ChecksumMode::None, ChecksumMode::Layer3,
+                                                           ChecksumMode::Layer4);
+  const std::size_t Q = c.Q, mem_size = c.image.size();
+  HostMemoryConfig mc{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false};
+  SimpleHostMemory mem{mc};
+  assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(c.image))).ok());
+  DMAEngine dma{mem};
+  std::vector<std::uint16_t> fired;
+  MsixMapping mapping{Q, 0};
+  for (std::size_t q = 0; q < Q; ++q) mapping.set_queue_vector(q, static_cast<std::uint16_t>(q));
+  InterruptDispatcher irq{MsixTable{Q}, mapping, CoalesceConfig{1, 0},
+                          [&](std::uint16_t v, std::uint32_t) { fired.push_back(v); }};
+  QueueManagerConfig qmc;
+  for (std::size_t q = 0; q < Q; ++q) {
+    std::size_t tt = 0, tr = 0;
+    for (std::size_t k = 0; k < c.R; ++k) { tt += c.ntx[k][q]; tr += c.nrx[k][q]; }
+    const auto id = static_cast<std::uint16_t>(q);
+    QueuePairConfig qc{
+        .queue_id = id,
+        .tx_ring = {.descriptor_size = sizeof(TxDescriptor), .ring_size = tt + 1, .base_address = 0, .queue_id = id, .host_backed = false},
+        .rx_ring = {.descriptor_size = sizeof(RxDescriptor), .ring_size = tr + 1, .base_address = 0, .queue_id = id, .host_backed = false},
+        .tx_completion = {.ring_size = tt + 1, .queue_id = id},
+        .rx_completion = {.ring_size = 8 * tt + 1, .queue_id = id},
+    };
+    qc.interrupt_dispatcher = &irq;
+    qc.weight = c.weights[q];
+    qc.max_mtu = c.max_mtu;
+    qc.enable_tx_interrupts = c.etx(q);
+    qc.enable_rx_interrupts = c.erx(q);
+    qmc.queue_configs.push_back(qc);
+  }
+  QueueManager qm{qmc, dma};
+  std::ostringstream js;
+  js << "{\n \"source\": \"QueueManager::process_once drained per round (src/queue_manager.cpp:54-78), stats :119-139; "
+        "input made by tests/cpp/qm_scale_gen.h from the seed\",\n"
+     << " \"seed\": " << seed << ", \"queues\": " << Q << ", \"weights\": " << json_arr(c.weights)
+     << ", \"max_mtu\": " << c.max_mtu << ", \"mem_size\": " << mem_size << ",\n \"rounds\": [";
+  auto str_arr = [](const std::vector<std::string>& v) {
+    std::string o = "[";
+    for (std::size_t i = 0; i < v.size(); ++i) o += (i ? "," : "") + v[i];
+    return o + "]";
+  };
+  std::uint64_t adv0 = 0, skip0 = 0;
+  for (std::size_t k = 0; k < c.R; ++k) {
+    for (std::size_t q = 0; q < Q; ++q) {
+      QueuePair& qp = *qm.queue(q);
+      for (const TxDescriptor& t : c.tx[k][q]) {
+        std::vector<std::byte> b(sizeof(TxDescriptor));
+        std::memcpy(b.data(), &t, sizeof(t));
+        assert(qp.tx_ring().push_descriptor(b).ok());
+      }
+      for (const RxDescriptor& x : c.rx[k][q]) {
+        std::vector<std::byte> b(sizeof(RxDescriptor));
+        std::memcpy(b.data(), &x, sizeof(x));
+        assert(qp.rx_ring().push_descriptor(b).ok());
+      }
+    }
+    std::vector<std::size_t> avail0(Q);
+    for (std::size_t q = 0; q < Q; ++q) avail0[q] = qm.queue(q)->rx_ring().available();
+    fired.clear();
+    while (qm.process_once()) {
+    }
+    const QueueManagerStats ms = qm.stats();
+    std::vector<std::size_t> consumed(Q), ntc(Q), nrc(Q);
+    std::vector<std::string> ftx(Q), frx(Q);
+    for (std::size_t q = 0; q < Q; ++q) {
+      consumed[q] = avail0[q] - qm.queue(q)->rx_ring().available();
+      std::uint64_t h = qm_scale::kFnv0;
+      while (auto e = qm.queue(q)->tx_completion().poll_completion()) { h = qm_scale::fnv_completion(h, *e); ++ntc[q]; }
+      std::ostringstream o;
+      o << std::hex << h;
+      ftx[q] = "\"" + o.str() + "\"";
+      h = qm_scale::kFnv0;
+      while (auto e = qm.queue(q)->rx_completion().poll_completion()) { h = qm_scale::fnv_completion(h, *e); ++nrc[q]; }
+      o.str("");
+      o << std::hex << h;
+      frx[q] = "\"" + o.str() + "\"";
+    }
+    std::ostringstream fv;
+    fv << std::hex << qm_scale::fnv(qm_scale::kFnv0, fired.data(), fired.size() * sizeof(std::uint16_t));
+    js << (k ? "," : "") << "\n  {\"ntx\": " << json_arr(c.ntx[k]) << ", \"nrx\": " << json_arr(c.nrx[k])
+       << ", \"advances\": " << ms.scheduler_advances - adv0 << ", \"skips\": " << ms.scheduler_skips - skip0
+       << ", \"rx_consumed\": " << json_arr(consumed) << ",\n   \"irq_count\": " << fired.size() << ", \"irq_fnv\": \""
+       << fv.str() << "\",\n   \"tx_count\": " << json_arr(ntc) << ", \"rx_count\": " << json_arr(nrc)
+       << ",\n   \"tx_fnv\": " << str_arr(ftx) << ",\n   \"rx_fnv\": " << str_arr(frx) << "}";
+    adv0 = ms.scheduler_advances;
+    skip0 = ms.scheduler_skips;
+  }
+  js << "],\n \"stats\": [";
+  for (std::size_t q = 0; q < Q; ++q) {
+    const QueuePairStats st = *qm.queue_stats(q);
+    js << (q ? "," : "") << "\n  [" << st.tx_packets << "," << st.rx_packets << "," << st.tx_bytes << "," << st.rx_bytes
+       << "," << st.drops_checksum << "," << st.drops_no_rx_desc << "," << st.drops_buffer_small << ","
+       << st.drops_mtu_exceeded << "," << st.drops_invalid_mss << "," << st.drops_too_many_segments << ","
+       << st.tx_tso_segments << "," << st.tx_gso_segments << "," << st.tx_vlan_insertions << "," << st.rx_vlan_strips
+       << "," << st.rx_checksum_verified << "," << st.rx_gro_aggregated << "]";
+  }
+  const QueueManagerStats ms = qm.stats();
+  js << "],\n \"qm_stats\": [" << ms.total_tx_packets << "," << ms.total_rx_packets << "," << ms.total_tx_bytes << ","
+     << ms.total_rx_bytes << "," << ms.total_drops_checksum << "," << ms.total_drops_no_rx_desc << ","
+     << ms.total_drops_buffer_small << "," << ms.total_tx_tso_segments << "," << ms.total_tx_gso_segments << ","
+     << ms.total_tx_vlan_insertions << "," << ms.total_rx_vlan_strips << "," << ms.total_rx_checksum_verified << ","
+     << ms.total_rx_gro_aggregated << "," << ms.scheduler_advances << "," << ms.scheduler_skips << "],\n"
+     << " \"stats_summary\": \"" << qm.stats_summary() << "\",\n";
+  std::vector<std::byte> after(mem_size);
+  assert(mem.read(0, after).ok());
+  js << " \"mem_fnv\": \"" << std::hex << fnv1a(after.data(), mem_size) << std::dec << "\"\n}\n";
+  std::ofstream(g_out + "/qm16_scale.json") << js.str();
+}
+
 // ------------------------------------------------------ L3/L4 verification --
 // SURVEY §8 f3.  Frames from build_frame (valid IPv4 header and TCP/UDP
 // checksums), then mutated.  Expected flags use the reference's own
@@ -1415,6 +1530,7 @@ int main(int argc, char** argv) {
   }
   if (argc > 2 && std::string(argv[2]) == "qm") {  // only the QueueManager fixtures
     gen_qm();
+    gen_qm_scale(808);
     std::printf("qm fixtures written to %s\n", g_out.c_str());
     return 0;
   }
@@ -1427,6 +1543,7 @@ int main(int argc, char** argv) {
   gen_l34();
   gen_tso_vlan();
   gen_qm();
+  gen_qm_scale(808);
   gen_cq();
   std::printf("golden fixtures written to %s\n", g_out.c_str());
   return 0;

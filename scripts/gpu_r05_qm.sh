@@ -6,7 +6,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 PT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
-timeout -k 10 600 $PT tests/test_queue_manager.py "tests/test_rx_stage.py::test_rx_stage_device_limits" -m gpu > gpurun_out/r05_qm_tests.log 2>&1
+timeout -k 10 600 $PT tests/test_memcpy_batch.py tests/test_queue_manager.py "tests/test_rx_stage.py::test_rx_stage_device_limits" -m gpu > gpurun_out/r05_qm_tests.log 2>&1
 rc=$?; tail -12 gpurun_out/r05_qm_tests.log; [ $rc -eq 0 ] || exit $rc
 B=tools/bin/bench_rx_stage
 for kind in pinned device hostmem; do

@@ -106,6 +106,10 @@ ABI_SYMBOLS = (
     "nicgpu_qp_segment_results",
     "nicgpu_qp_segment_lists",
     "nicgpu_qp_segment_hits",
+    "nicgpu_memcpy_batch",
+    "nicgpu_qp_walks",
+    "nicgpu_qp_check_async",
+    "nicgpu_qp_check_wait",
     "nicgpu_event_synchronize",
     "nicgpu_host_register",
     "nicgpu_host_unregister",
@@ -186,6 +190,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_qp_segment_results": (i32, [vp, vp, vp]),
         "nicgpu_qp_segment_lists": (i32, [vp, sz, sz, vp, vp]),
         "nicgpu_qp_segment_hits": (i32, [vp, sz, sz, vp, vp]),
+        "nicgpu_memcpy_batch": (i32, [vp, sz, vp]),
+        "nicgpu_qp_walks": (i32, [vp, vp]),
+        "nicgpu_qp_check_async": (i32, [vp, ctypes.c_uint64, sz, sz, ctypes.c_uint, vp]),
+        "nicgpu_qp_check_wait": (i32, [vp, vp]),
         "nicgpu_event_synchronize": (i32, [vp]),
         "nicgpu_host_register": (i32, [vp, sz, ctypes.POINTER(vp), ctypes.POINTER(i32)]),
         "nicgpu_host_unregister": (i32, [vp]),

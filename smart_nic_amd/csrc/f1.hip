@@ -1144,6 +1144,50 @@ __global__ __launch_bounds__(kQpBlock) void qp_relax_kernel(QpCtx C, uint32_t* p
   }
 }
 
+// When the relaxation has not settled within kQpRelaxSteps (a long chain of
+// packets each shifting the ring under the next), the positions are made by a
+// walk instead.  Only a packet that needs more than one RX descriptor (a
+// TSO/GSO packet) can pop a count other than its need while the ring lasts — a
+// segment's RX check ends it early — and a packet with need 1 pops 1 until the
+// ring's end.  So with u_i = (scan of need)_i + delta_i, where delta_i adds
+// (pops - need) over the multi-descriptor packets before i, the exact position
+// is min(u_i, ring end): one thread per segment walks those packets in ring
+// order, resolving each at its exact position and carrying delta; the packets
+// that reach the ring's end are then settled by one relaxation step.
+__global__ __launch_bounds__(kQpBlock) void qp_multi_flag_kernel(const uint32_t* __restrict__ need, uint64_t n,
+                                                                 uint32_t* flag) {
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i <= n; i += (uint64_t) gridDim.x * kQpBlock)
+    flag[i] = i < n && need[i] >= 2u ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kQpBlock) void qp_multi_list_kernel(const uint32_t* __restrict__ flag,
+                                                                 const uint32_t* __restrict__ at, uint64_t n,
+                                                                 uint32_t* list) {
+  for (uint64_t i = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; i < n; i += (uint64_t) gridDim.x * kQpBlock)
+    if (flag[i]) list[at[i]] = (uint32_t) i;
+}
+
+// one block per segment (one for an unsegmented batch), its first thread walks
+__global__ __launch_bounds__(kWave) void qp_walk_kernel(QpCtx C, uint32_t* need, const uint32_t* __restrict__ pos,
+                                                        const uint32_t* __restrict__ list,
+                                                        const uint32_t* __restrict__ at, uint64_t n, QpSegs S) {
+  if (threadIdx.x != 0) return;
+  const uint32_t s = blockIdx.x;
+  const uint64_t tb = S.seg ? S.seg[s].tx_begin : 0, te = S.seg ? qp_seg_end(S, s, n) : n;
+  const QpCtx Cs = qp_ctx_of(C, S, s);
+  int64_t delta = 0;
+  for (uint32_t k = at[tb], ke = at[te]; k < ke; ++k) {
+    const uint64_t m = list[k];
+    const int64_t u = (int64_t) qp_abs(pos, S, s, m) + delta;
+    const uint64_t p = u < (int64_t) Cs.nrx ? (uint64_t) u : Cs.nrx;
+    nicgpu_qp_stats st{};
+    QpNullSink sink;
+    const uint32_t got = (uint32_t) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(Cs, m, p, st, sink);
+    delta += (int64_t) got - (int64_t) need[m];
+    need[m] = got;
+  }
+}
+
 // packets [0, lim) at their (exact) positions: completions, writes, per-block
 // stats.  With `guess` (the pops the positions were scanned from) the pass is
 // speculative: first[0] becomes the first packet that popped otherwise, and
@@ -1591,6 +1635,8 @@ struct nicgpu_qp {
   size_t c_tmp_chk = 0;
   QpPlan* plans = nullptr;
   uint32_t *counts = nullptr, *base = nullptr, *need = nullptr, *pos = nullptr;
+  uint32_t *mflag = nullptr, *mscan = nullptr, *mlist = nullptr;  // the position walk's (qp_walk)
+  size_t c_mflag = 0, c_mscan = 0, c_mlist = 0;
   uint64_t* piece_desc = nullptr;
   uint16_t* piece_csum = nullptr;  // split sums: each piece past its first 4 bytes ...
   uint16_t* piece_cs4 = nullptr;   // ... and its first min(4, len)
@@ -1626,8 +1672,12 @@ struct nicgpu_qp {
   uint64_t* hp = nullptr;
   uint64_t* misc() const { return hp + kQpTail; }
   unsigned grid = 1;
+  uint64_t walks = 0;  // resolves whose positions the walk made (qp_walk)
   hipEvent_t planned = nullptr;   // nicgpu_qp_plan_on: the piece descriptors are written
   hipEvent_t resolved = nullptr;  // nicgpu_qp_resolve_start: its partials are on the host
+  hipEvent_t checked = nullptr;   // nicgpu_qp_check_async: its flags are on the host
+  unsigned long long chk_gen = 0; // ... the generation they are compared with
+  bool chk_on = false;            // a check is pending (nicgpu_qp_check_wait not yet called)
   // the resolve between nicgpu_qp_resolve_start and _finish
   struct Pending {
     bool on = false;
@@ -1653,6 +1703,8 @@ struct nicgpu_qp {
   size_t c_seg_hp = 0;
   void* seg_stage = nullptr;   // page-locked staging of the table and the map
   size_t c_seg_stage = 0;
+  std::vector<nicgpu_qp_segment> seg_last;  // the table on the device (and its ntx)
+  size_t seg_last_ntx = 0;
 };
 
 namespace {
@@ -1721,6 +1773,33 @@ int qp_seg_finish(nicgpu_qp* q, uint64_t ntx, bool speculative, hipStream_t s) {
   return st;
 }
 
+// The position walk (qp_walk_kernel): need afresh, its scan, the
+// multi-descriptor packets listed, the walk; need then holds every such
+// packet's exact pops (the caller scans it and relaxes the ring's end).
+int qp_walk(nicgpu_qp* q, const QpCtx& C, const QpSegs& S, uint64_t ntx, unsigned grid, hipStream_t s) {
+  int st = qp_grow(q->mflag, q->c_mflag, ntx + 1);
+  if (st == NICGPU_OK) st = qp_grow(q->mscan, q->c_mscan, ntx + 1);
+  if (st == NICGPU_OK) st = qp_grow(q->mlist, q->c_mlist, ntx + 1);
+  if (st != NICGPU_OK) return st;
+  uint64_t* tail = q->partials + (size_t) grid * kQpStats;
+  hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, ntx, q->need,
+                     reinterpret_cast<unsigned long long*>(tail + 1), q->gflags, q->plan_gen, S);
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
+  if (st != NICGPU_OK) return st;
+  const unsigned g = qp_grid(q, ntx + 1);
+  hipLaunchKernelGGL(qp_multi_flag_kernel, dim3(g), dim3(kQpBlock), 0, s, q->need, ntx, q->mflag);
+  st = hip_status(hipGetLastError());
+  if (st == NICGPU_OK) st = qp_scan(q, q->mflag, q->mscan, ntx + 1, s);
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_multi_list_kernel, dim3(g), dim3(kQpBlock), 0, s, q->mflag, q->mscan, ntx, q->mlist);
+  st = hip_status(hipGetLastError());
+  if (st != NICGPU_OK) return st;
+  hipLaunchKernelGGL(qp_walk_kernel, dim3(S.seg ? S.nseg : 1u), dim3(kWave), 0, s, C, q->need, q->pos, q->mlist,
+                     q->mscan, ntx, S);
+  return hip_status(hipGetLastError());
+}
+
 }  // namespace
 
 extern "C" {
@@ -1753,7 +1832,8 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
     return NICGPU_ERR_NOMEM;
   }
   if (hipEventCreateWithFlags(&q->planned, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&q->resolved, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&q->resolved, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&q->checked, hipEventDisableTiming) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_HIP;
   }
@@ -1768,7 +1848,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
                   q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
                   q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sort_key, q->sorted_key, q->queue_which,
                   q->queue_start, q->queue_end, q->end_max, q->dlv_acc, q->dlv_done, q->gflags, q->piece_cs4,
-                  q->d_seg, q->d_blk, q->d_fb, q->d_segout, q->d_split};
+                  q->d_seg, q->d_blk, q->d_fb, q->d_segout, q->d_split, q->mflag, q->mscan, q->mlist};
   for (void* b : bufs)
     if (b) (void) hipFree(b);
   if (q->hp) (void) hipHostFree(q->hp);
@@ -1776,6 +1856,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
   if (q->seg_stage) (void) hipHostFree(q->seg_stage);
   if (q->planned) (void) hipEventDestroy(q->planned);
   if (q->resolved) (void) hipEventDestroy(q->resolved);
+  if (q->checked) (void) hipEventDestroy(q->checked);
   delete q;
   return NICGPU_OK;
 }
@@ -1924,10 +2005,31 @@ int nicgpu_qp_check(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, int
 
 int nicgpu_qp_check_flags(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, unsigned flags, int* verdict,
                           void* stream) {
-  if (!q || !verdict || ntx > q->cap_tx || nrx > q->cap_rx || (flags & ~NICGPU_QP_CHECK_WHOLE)) return NICGPU_ERR_INVALID;
-  const bool segmented = q->nseg && !(flags & NICGPU_QP_CHECK_WHOLE);
+  if (!verdict) return NICGPU_ERR_INVALID;
   *verdict = -1;
+  const int st = nicgpu_qp_check_async(q, mem_size, ntx, nrx, flags, stream);
+  return st == NICGPU_OK ? nicgpu_qp_check_wait(q, verdict) : st;
+}
+
+int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict) {
+  if (!q || !verdict || !q->chk_on) return NICGPU_ERR_INVALID;
+  q->chk_on = false;
   DeviceGuard g(q->device);
+  const int st = hip_status(hipEventSynchronize(q->checked));
+  if (st != NICGPU_OK) return st;
+  const uint64_t* f = q->misc() + 1;
+  *verdict = f[0] == q->chk_gen ? -1 : (f[1] == q->chk_gen ? 0 : 1);
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_check_async(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, unsigned flags, void* stream) {
+  if (!q || ntx > q->cap_tx || nrx > q->cap_rx || (flags & ~NICGPU_QP_CHECK_WHOLE)) return NICGPU_ERR_INVALID;
+  const bool segmented = q->nseg && !(flags & NICGPU_QP_CHECK_WHOLE);
+  DeviceGuard g(q->device);
+  if (q->chk_on) {  // an unwaited earlier check: its flags land before these are reused
+    q->chk_on = false;
+    if (hipEventSynchronize(q->checked) != hipSuccess) return NICGPU_ERR_HIP;
+  }
   hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned long long gen = ++q->gen;
   int st = NICGPU_OK;
@@ -1960,9 +2062,10 @@ int nicgpu_qp_check_flags(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nr
   }
   uint64_t* f = q->misc() + 1;
   if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(f, q->gflags + 1, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+  if (st == NICGPU_OK) st = hip_status(hipEventRecord(q->checked, s));
   if (st != NICGPU_OK) return st;
-  *verdict = f[0] == gen ? -1 : (f[1] == gen ? 0 : 1);
+  q->chk_gen = gen;
+  q->chk_on = true;
   return NICGPU_OK;
 }
 
@@ -2030,20 +2133,29 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
   if (first < ntx) {  // relax from the same guess (the speculative pass left `need` as it was)
     // everything from here waits on the stream, behind whatever was enqueued
     // after the start (a settled-prefix delivery reads none of what follows)
-    for (int it = 0; st == NICGPU_OK; ++it) {
-      if (it > 0) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
-      q->misc()[4] = ntx;  // page-locked source; the step below waits for the stream
-      if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->scal, q->misc() + 4, sizeof(uint64_t), hipMemcpyHostToDevice, s));
-      if (st != NICGPU_OK) break;
-      hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, ntx, q->scal, S);
-      st = hip_status(hipGetLastError());
-      if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->misc() + 3, q->scal, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-      if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
-      if (st != NICGPU_OK) break;
-      first = (unsigned long long) q->misc()[3];
-      // pos is exact up to and including `first` (pops before it agreed)
-      lim = first < ntx ? (uint64_t) first : ntx;
-      if (first >= ntx || it + 1 == kQpRelaxSteps) break;
+    auto relax = [&](bool scan_first) {
+      for (int it = 0; st == NICGPU_OK; ++it) {
+        if (it > 0 || scan_first) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
+        q->misc()[4] = ntx;  // page-locked source; the step below waits for the stream
+        if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->scal, q->misc() + 4, sizeof(uint64_t), hipMemcpyHostToDevice, s));
+        if (st != NICGPU_OK) break;
+        hipLaunchKernelGGL(qp_relax_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->need, q->pos, ntx, q->scal, S);
+        st = hip_status(hipGetLastError());
+        if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->misc() + 3, q->scal, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        if (st == NICGPU_OK) st = hip_status(hipStreamSynchronize(s));
+        if (st != NICGPU_OK) break;
+        first = (unsigned long long) q->misc()[3];
+        // pos is exact up to and including `first` (pops before it agreed)
+        lim = first < ntx ? (uint64_t) first : ntx;
+        if (first >= ntx || it + 1 == kQpRelaxSteps) break;
+      }
+    };
+    relax(false);
+    // not settled: the walk, then the ring's end relaxed
+    if (st == NICGPU_OK && lim < ntx) {
+      st = qp_walk(q, C, S, ntx, grid, s);
+      if (st == NICGPU_OK) relax(true);
+      if (st == NICGPU_OK) q->walks += 1;
     }
     // a segmented batch settles all or nothing (nothing was delivered: the
     // speculative pass's settled count was 0)
@@ -2069,6 +2181,12 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
   *done = lim;
   *rx_used = used;
   if (rx_settled) *rx_settled = settled < used ? settled : used;
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_walks(const nicgpu_qp* q, uint64_t* walks) {
+  if (!q || !walks) return NICGPU_ERR_INVALID;
+  *walks = q->walks;
   return NICGPU_OK;
 }
 
@@ -2257,6 +2375,16 @@ int nicgpu_qp_set_segments(nicgpu_qp* q, const nicgpu_qp_segment* seg, size_t ns
     rx_end += seg[k].nrx;
   }
   if (seg[0].tx_begin != 0 || ntx > q->cap_tx || rx_end > q->cap_rx) return NICGPU_ERR_INVALID;
+  // the table the device holds already (a manager drains the same queue
+  // layout again and again): nothing to upload
+  if (q->seg_last.size() == nseg && q->seg_last_ntx == ntx && q->seg_grid &&
+      std::memcmp(q->seg_last.data(), seg, nseg * sizeof(nicgpu_qp_segment)) == 0) {
+    q->nseg = (uint32_t) nseg;
+    q->seg_ntx = ntx;
+    q->seg_nrx = rx_end;
+    return NICGPU_OK;
+  }
+  q->seg_last.clear();
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   // blocks in proportion to the segments' TX descriptors, at least one each
@@ -2314,6 +2442,8 @@ int nicgpu_qp_set_segments(nicgpu_qp* q, const nicgpu_qp_segment* seg, size_t ns
   q->seg_grid = (unsigned) blk.size();
   q->seg_ntx = ntx;
   q->seg_nrx = rx_end;
+  q->seg_last.assign(seg, seg + nseg);
+  q->seg_last_ntx = ntx;
   return NICGPU_OK;
 }
 

@@ -390,12 +390,8 @@ QueueSchedule BatchedQueueManager::run(const DeviceHostMemory& dmem, HostMemory*
   const std::size_t mem_size = hmem ? hmem->config().size_bytes : dmem.size;
   last_fused_ = 0;
   bool fused = false;
-  const bool disjoint = qm_detail::queues_disjoint(mem_size, batches);
-  // the runs of the schedule: for the reference's interleaving on the host
-  // path and for the interrupts' order; the counters alone otherwise
-  std::size_t index = index_, credit = credit_;
-  QueueSchedule sched = qm_detail::schedule(weights_, n, index, credit, !disjoint || interrupts());
-  if (disjoint && fusable()) {
+  int disjoint = -1;  // the queues' buffers apart from each other's (-1: not looked at yet)
+  auto try_fused = [&](bool whole_check) {
     std::vector<std::span<const TxDescriptor>> txs(Q);
     std::vector<std::span<const RxDescriptor>> rxs(Q);
     std::vector<BatchedQueuePairConfig> cfgs(Q);
@@ -405,12 +401,26 @@ QueueSchedule BatchedQueueManager::run(const DeviceHostMemory& dmem, HostMemory*
       cfgs[q] = qps_[q]->config;
     }
     std::vector<QueuePairStats> st;
-    fused = fused_->process_queues(dmem, img, txs, rxs, cfgs, out, st, stream);
+    fused = fused_->process_queues(dmem, img, txs, rxs, cfgs, out, st, stream, false, whole_check);
     if (fused) {
       for (std::size_t q = 0; q < Q; ++q) add_delta(qps_[q]->stats, st[q], QueuePairStats{});
       last_fused_ = 1;
     }
+  };
+  // First the fused batch with the device checking the whole concatenation
+  // (every queue's buffers against every other's too): no host pass over the
+  // descriptors.  Rings laid out out of address order across queues fail that
+  // check; then the host decides whether the queues are apart, and the fused
+  // batch is tried once more, checked queue pair by queue pair.
+  if (fusable()) try_fused(true);
+  if (!fused) {
+    disjoint = qm_detail::queues_disjoint(mem_size, batches) ? 1 : 0;
+    if (disjoint && fusable()) try_fused(false);
   }
+  // the runs of the schedule: for the reference's interleaving on the host
+  // path and for the interrupts' order; the counters alone otherwise
+  std::size_t index = index_, credit = credit_;
+  QueueSchedule sched = qm_detail::schedule(weights_, n, index, credit, (!fused && !disjoint) || interrupts());
   if (fused) {
     // done: scheduler state and interrupts below
   } else if (disjoint && hmem) {

@@ -17,6 +17,7 @@
 #include "nic/rx_stage.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -927,9 +928,18 @@ public:
     if (!th_.joinable()) th_ = std::thread([this] { loop(); });
     job_ = std::move(f);
     done_ = false;
+    done_flag_.store(false, std::memory_order_relaxed);
     cv_.notify_all();
   }
+  // A job ends a batch the caller is waiting for: spin briefly before
+  // sleeping, so the caller does not pay a thread wake-up (tens of µs) on the
+  // batch's critical path.
   void wait() {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned i = 0; !done_flag_.load(std::memory_order_acquire); ++i) {
+      if ((i & 63u) == 63u && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(1500)) break;
+      std::this_thread::yield();
+    }
     std::unique_lock<std::mutex> lk(mu_);
     cv_.wait(lk, [this] { return done_; });
   }
@@ -946,6 +956,7 @@ private:
       f();
       lk.lock();
       done_ = true;
+      done_flag_.store(true, std::memory_order_release);  // under the lock: a new job's start() cannot interleave
       cv_.notify_all();
     }
   }
@@ -954,6 +965,7 @@ private:
   std::thread th_;
   std::function<void()> job_;
   bool done_ = true, stop_ = false;
+  std::atomic<bool> done_flag_{true};
 };
 
 // A pageable host<->device copy keeps the thread that issues it busy until the
@@ -1858,7 +1870,11 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
   t = clock::now();
   std::uint64_t done = 0, used = 0, settled = 0;
   nicgpu_qp_stats ds{};
+  std::uint64_t walks0 = 0, walks1 = 0;
+  check(nicgpu_qp_walks(sl.qp, &walks0), "nicgpu_qp_walks");
   const int rst = nicgpu_qp_resolve_finish(sl.qp, &done, &used, &settled, &ds);
+  check(nicgpu_qp_walks(sl.qp, &walks1), "nicgpu_qp_walks");
+  out.timings.walked = out.timings.walked || walks1 != walks0;
   if (rst == NICGPU_ERR_AGAIN || rst == NICGPU_ERR_RANGE) {  // the plan did not fit: nothing resolved, settled or written
     out.timings.resolve_us += us_since(t);
     if (rst == NICGPU_ERR_RANGE) return false;
@@ -2012,23 +2028,32 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
                 "nicgpu_memcpy_async");
     rss_ready.wait();
     ok = ok && j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_done), "nicgpu_stream_wait_event");
-    if (ok && rss) ok = j.ok(nicgpu_qp_group(sl.qp, nrx_total, nq, S.side_down), "nicgpu_qp_group");
     // a fused batch: the lists split per queue pair (entries made relative to
     // each queue pair's ring), and its per-queue-pair hits when it needs them
+    // (its per-queue-pair hits beside the lists, on the interrupt stream, which
+    // a fused batch does not use)
+    const bool seg_hits = ok && rss && sl.multi && sl.seg_hits_on;
+    if (seg_hits) {
+      auto* sh = static_cast<std::uint64_t*>(sl.seg_hits.get(sl.nseg * tn * sizeof(std::uint64_t)));
+      ok = j.ok(nicgpu_stream_wait_event(S.side_irq, sl.ev_done), "nicgpu_stream_wait_event") &&
+           j.ok(nicgpu_qp_segment_hits(sl.qp, nrx_total, tn, sh, S.side_irq), "nicgpu_qp_segment_hits") &&
+           j.ok(nicgpu_memcpy_async(sl.h_seg_hits.get<std::uint64_t>(sl.nseg * tn), sh, sl.nseg * tn * 8, S.side_irq),
+                "nicgpu_memcpy_async");
+    }
+    if (ok && rss)
+      ok = j.ok(nicgpu_qp_group(sl.qp, nrx_total, nq, S.side_down), "nicgpu_qp_group");
     if (ok && rss && sl.multi)
       ok = j.ok(nicgpu_qp_segment_lists(sl.qp, nrx_total, nq, sl.h_split.get<std::uint32_t>((sl.nseg + 1) * std::max<std::size_t>(nq, 1)),
                                         S.side_down),
                 "nicgpu_qp_segment_lists");
-    if (ok && rss && sl.multi && sl.seg_hits_on) {
-      auto* sh = static_cast<std::uint64_t*>(sl.seg_hits.get(sl.nseg * tn * sizeof(std::uint64_t)));
-      ok = j.ok(nicgpu_qp_segment_hits(sl.qp, nrx_total, tn, sh, S.side_down), "nicgpu_qp_segment_hits") &&
-           j.ok(nicgpu_memcpy_async(sl.h_seg_hits.get<std::uint64_t>(sl.nseg * tn), sh, sl.nseg * tn * 8, S.side_down),
-                "nicgpu_memcpy_async");
-    }
-    if (ok && rss)
+    if (seg_hits) ok = j.ok(nicgpu_stream_synchronize(S.side_irq), "nicgpu_stream_synchronize") && ok;
+    // (a fused batch's lists are the split's, so no list bounds; its totals
+    // only for one shared engine or for the dispatch list's download)
+    if (ok && rss && !(sl.multi && keep && sl.seg_hits_on))
       ok = j.ok(nicgpu_memcpy_async(sl.meta, v.rss_count, sizeof(std::uint64_t), S.side_down), "nicgpu_memcpy_async") &&
-           j.ok(nicgpu_memcpy_async(sl.meta + 1, hits, tn * sizeof(std::uint64_t), S.side_down), "nicgpu_memcpy_async") &&
-           j.ok(nicgpu_memcpy_async(sl.qs, v.queue_start, nq * 4, S.side_down), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(sl.meta + 1, hits, tn * sizeof(std::uint64_t), S.side_down), "nicgpu_memcpy_async");
+    if (ok && rss && !sl.multi)
+      ok = j.ok(nicgpu_memcpy_async(sl.qs, v.queue_start, nq * 4, S.side_down), "nicgpu_memcpy_async") &&
            j.ok(nicgpu_memcpy_async(sl.qe, v.queue_end, nq * 4, S.side_down), "nicgpu_memcpy_async");
     if (ok && rss && !keep)
       ok = j.ok(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, S.side_down), "nicgpu_memcpy_async") &&
@@ -2362,9 +2387,13 @@ bool BatchedQueuePair::front_multi(Slot& sl, const DeviceHostMemory& mem, std::s
   check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");
   out.timings.resolve_us += us_since(t);
   t = clock::now();
+  // the overlap check behind the plan on its stream, beside the piece sums and
+  // the speculative resolve (measured: run beside the plan instead, it slows
+  // the plan and the sums more than it gains)
   int verdict = -1;
-  check(nicgpu_qp_check_flags(sl.qp, mem.size, ntx, nrx, whole_check ? NICGPU_QP_CHECK_WHOLE : 0u, &verdict, ps),
-        "nicgpu_qp_check_flags");
+  check(nicgpu_qp_check_async(sl.qp, mem.size, ntx, nrx, whole_check ? NICGPU_QP_CHECK_WHOLE : 0u, ps),
+        "nicgpu_qp_check_async");
+  check(nicgpu_qp_check_wait(sl.qp, &verdict), "nicgpu_qp_check_wait");
   out.timings.check_us += us_since(t);
   if (verdict != 1) return false;  // overlapping, or a ring not in address order: per queue pair
   t = clock::now();
@@ -2383,7 +2412,11 @@ bool BatchedQueuePair::front_multi(Slot& sl, const DeviceHostMemory& mem, std::s
   t = clock::now();
   std::uint64_t done = 0, used = 0, settled = 0;
   nicgpu_qp_stats ds{};
+  std::uint64_t walks0 = 0, walks1 = 0;
+  check(nicgpu_qp_walks(sl.qp, &walks0), "nicgpu_qp_walks");
   const int rst = nicgpu_qp_resolve_finish(sl.qp, &done, &used, &settled, &ds);
+  check(nicgpu_qp_walks(sl.qp, &walks1), "nicgpu_qp_walks");
+  out.timings.walked = out.timings.walked || walks1 != walks0;
   out.timings.resolve_us += us_since(t);
   if (rst == NICGPU_ERR_AGAIN) {
     again = 1;
@@ -2446,14 +2479,28 @@ bool BatchedQueuePair::process_queues(const DeviceHostMemory& mem_in, HostImage*
     check(nicgpu_event_record(sl.ev_submit, stream), "nicgpu_event_record");
     check(nicgpu_stream_wait_event(S.side_up, sl.ev_submit), "nicgpu_stream_wait_event");
   }
-  for (std::size_t q = 0; q < Q; ++q)
-    check(nicgpu_memcpy_async(v.tx + seg[q].tx_begin, tx[q].data(), tx[q].size() * sizeof(TxDescriptor), S.side_up),
-          "nicgpu_memcpy_async");
-  check(nicgpu_event_record(sl.ev_tx, S.side_up), "nicgpu_event_record");
-  for (std::size_t q = 0; q < Q; ++q)
-    check(nicgpu_memcpy_async(v.rx + seg[q].rx_begin, rx[q].data(), rx[q].size() * sizeof(RxDescriptor), S.side_up),
-          "nicgpu_memcpy_async");
-  check(nicgpu_event_record(sl.ev_rx, S.side_up), "nicgpu_event_record");
+  if (dev_desc) {  // HBM to HBM: one gather launch per 64 arrays, not a copy per array
+    std::vector<nicgpu_copy_range> cr;
+    cr.reserve(2 * Q);
+    for (std::size_t q = 0; q < Q; ++q)
+      cr.push_back({v.tx + seg[q].tx_begin, tx[q].data(), tx[q].size() * sizeof(TxDescriptor)});
+    for (std::size_t q = 0; q < Q; ++q)
+      cr.push_back({v.rx + seg[q].rx_begin, rx[q].data(), rx[q].size() * sizeof(RxDescriptor)});
+    for (std::size_t i = 0; i < cr.size(); i += NICGPU_COPY_BATCH_MAX)
+      check(nicgpu_memcpy_batch(cr.data() + i, std::min<std::size_t>(NICGPU_COPY_BATCH_MAX, cr.size() - i), S.side_up),
+            "nicgpu_memcpy_batch");
+    check(nicgpu_event_record(sl.ev_tx, S.side_up), "nicgpu_event_record");
+    check(nicgpu_event_record(sl.ev_rx, S.side_up), "nicgpu_event_record");
+  } else {
+    for (std::size_t q = 0; q < Q; ++q)
+      check(nicgpu_memcpy_async(v.tx + seg[q].tx_begin, tx[q].data(), tx[q].size() * sizeof(TxDescriptor), S.side_up),
+            "nicgpu_memcpy_async");
+    check(nicgpu_event_record(sl.ev_tx, S.side_up), "nicgpu_event_record");
+    for (std::size_t q = 0; q < Q; ++q)
+      check(nicgpu_memcpy_async(v.rx + seg[q].rx_begin, rx[q].data(), rx[q].size() * sizeof(RxDescriptor), S.side_up),
+            "nicgpu_memcpy_async");
+    check(nicgpu_event_record(sl.ev_rx, S.side_up), "nicgpu_event_record");
+  }
   if (img) {  // the TX bytes of every queue pair: their span, or a gather over the uploaded descriptors
     sl.image = img;
     std::uint64_t lo = ~0ull, hi = 0, bytes = 0, rlo = ~0ull, rhi = 0;

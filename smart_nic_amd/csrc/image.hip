@@ -72,6 +72,55 @@ __global__ __launch_bounds__(kWave * kImgWaves) void image_writeback_kernel(cons
   }
 }
 
+// Batched device copy (nicgpu_memcpy_batch): the ranges split into tiles of
+// kCopyTile units (8 B when the range's pointers and size allow, else 1 B);
+// blocks walk the tiles grid-stride, the range found by a scalar binary search
+// over the tile prefix held in the kernel arguments.
+constexpr unsigned kCopyThreads = 256;
+constexpr unsigned kCopyTile = kCopyThreads * 4;
+
+struct CopyBatch {
+  uint64_t dst[NICGPU_COPY_BATCH_MAX];
+  uint64_t src[NICGPU_COPY_BATCH_MAX];
+  uint64_t units[NICGPU_COPY_BATCH_MAX];        // 8-B words (wide) or bytes
+  uint64_t tile0[NICGPU_COPY_BATCH_MAX + 1];    // first tile of each range; tile0[n] = all tiles
+  uint64_t wide;                                // bit i: range i moves 8-B words
+  uint32_t n;
+};
+
+__global__ __launch_bounds__(kCopyThreads) void copy_batch_kernel(const CopyBatch B) {
+  const uint64_t total = B.tile0[B.n];
+  for (uint64_t t = blockIdx.x; t < total; t += gridDim.x) {
+    uint32_t lo = 0, hi = B.n;  // the range holding tile t: tile0[lo] <= t < tile0[lo + 1]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (B.tile0[mid] <= t) lo = mid;
+      else hi = mid;
+    }
+    const uint64_t u0 = (t - B.tile0[lo]) * kCopyTile;
+    const uint64_t u1 = u0 + kCopyTile < B.units[lo] ? u0 + kCopyTile : B.units[lo];
+    if ((B.wide >> lo) & 1) {
+      uint64_t* d = reinterpret_cast<uint64_t*>(B.dst[lo]);
+      const uint64_t* s = reinterpret_cast<const uint64_t*>(B.src[lo]);
+      uint64_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t u = u0 + threadIdx.x + (uint64_t) k * kCopyThreads;
+        if (u < u1) v[k] = s[u];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t u = u0 + threadIdx.x + (uint64_t) k * kCopyThreads;
+        if (u < u1) d[u] = v[k];
+      }
+    } else {
+      uint8_t* d = reinterpret_cast<uint8_t*>(B.dst[lo]);
+      const uint8_t* s = reinterpret_cast<const uint8_t*>(B.src[lo]);
+      for (uint64_t u = u0 + threadIdx.x; u < u1; u += kCopyThreads) d[u] = s[u];
+    }
+  }
+}
+
 unsigned image_grid(uint64_t n, const DeviceInfo* di) {
   const uint64_t want = (n + kImgWaves - 1) / kImgWaves;
   const uint64_t cap = (uint64_t) di->cus * 8;
@@ -106,6 +155,33 @@ int nicgpu_image_writeback(const uint8_t* image, uint8_t* host, uint64_t mem_siz
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(image_writeback_kernel, dim3(image_grid(n, di)), dim3(kWave * kImgWaves), 0,
                      static_cast<hipStream_t>(stream), image, host, mem_size, writes, (uint64_t) n);
+  return hip_status(hipGetLastError());
+}
+
+int nicgpu_memcpy_batch(const nicgpu_copy_range* r, size_t n, void* stream) {
+  if (n == 0) return NICGPU_OK;
+  if (!r || n > NICGPU_COPY_BATCH_MAX) return NICGPU_ERR_INVALID;
+  CopyBatch B{};
+  uint64_t tiles = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (r[i].bytes && (!r[i].dst || !r[i].src)) return NICGPU_ERR_INVALID;
+    const bool wide = ((reinterpret_cast<uintptr_t>(r[i].dst) | reinterpret_cast<uintptr_t>(r[i].src) | r[i].bytes) & 7u) == 0;
+    B.dst[i] = reinterpret_cast<uint64_t>(r[i].dst);
+    B.src[i] = reinterpret_cast<uint64_t>(r[i].src);
+    B.units[i] = wide ? r[i].bytes / 8 : r[i].bytes;
+    B.wide |= (uint64_t) wide << i;
+    B.tile0[i] = tiles;
+    tiles += (B.units[i] + kCopyTile - 1) / kCopyTile;
+  }
+  B.tile0[n] = tiles;
+  B.n = (uint32_t) n;
+  if (tiles == 0) return NICGPU_OK;
+  const DeviceInfo* di = nullptr;
+  const int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  const uint64_t cap = (uint64_t) di->cus * 8;
+  hipLaunchKernelGGL(copy_batch_kernel, dim3((unsigned) (tiles < cap ? tiles : cap)), dim3(kCopyThreads), 0,
+                     static_cast<hipStream_t>(stream), B);
   return hip_status(hipGetLastError());
 }
 

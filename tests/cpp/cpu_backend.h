@@ -45,8 +45,21 @@ public:
 
   void gather(std::span<const rx_stage_detail::SegmentWrite> writes, bool from_copy) override {
     if (from_copy && copy_.size() != image_.size()) std::abort();
-    const std::vector<std::uint8_t> before = from_copy ? std::vector<std::uint8_t>() : image_;
-    const std::vector<std::uint8_t>& src = from_copy ? copy_ : before;
+    // the writes read the image as it was before any of them: a copy, unless
+    // no write's destination meets another's source (small batches checked
+    // pair by pair; the copy is the whole image)
+    bool meet = false;
+    if (!from_copy && writes.size() <= 256) {
+      for (const auto& w : writes) {
+        const std::uint64_t d0 = w.dst, d1 = w.dst + w.prefix_len + w.len_a + w.len_b;
+        for (const auto& u : writes)
+          meet |= (u.len_a && u.src_a < d1 && d0 < u.src_a + u.len_a) || (u.len_b && u.src_b < d1 && d0 < u.src_b + u.len_b);
+      }
+    } else {
+      meet = !from_copy;
+    }
+    const std::vector<std::uint8_t> before = meet ? image_ : std::vector<std::uint8_t>();
+    const std::vector<std::uint8_t>& src = from_copy ? copy_ : meet ? before : image_;
     for (std::size_t k = writes.size(); k-- > 0;) {
       const auto& w = writes[k];
       const std::uint64_t total = std::uint64_t{w.prefix_len} + w.len_a + w.len_b;

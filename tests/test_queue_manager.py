@@ -7,10 +7,13 @@ cpu: the weighted round-robin schedule (advances, skips, the index/credit a
      round leaves for the next), each run of it through the stage's driver over
      the CPU backend, and the interrupts replayed in the scheduler's order —
      completions, MSI-X vector order, stats and memory bytes as the reference's.
-gpu: the product path (every queue's batch on its own device stage, in flight
-     at once, when the queues' buffers are disjoint; the reference's
-     interleaving on the host path when qm_alias makes the order decide the
-     bytes), compared the same way plus QueueManagerStats and stats_summary().
+gpu: the product path (every queue pair's batch in ONE fused device batch when
+     the queues' buffers are disjoint; the reference's interleaving on the host
+     path when qm_alias makes the order decide the bytes), compared the same way
+     plus QueueManagerStats and stats_summary().
+scale: 16 queue pairs, ~70 K descriptors (tests/golden/qm16_scale.json; the
+     input made from its seed by tests/cpp/qm_scale_gen.h on both sides),
+     checked by digest on the CPU path, the fused GPU batch and HostMemory.
 """
 
 import json
@@ -59,6 +62,63 @@ def _run(exe, mode, name, tmp_path, extra=()):
     r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert f"qm_test {mode}: ok" in r.stdout
+
+
+def _flatten_scale(out_dir):
+    d = json.load(open(os.path.join(GOLDEN, "qm16_scale.json")))
+    Q = d["queues"]
+    lines = [f'{Q} {d["max_mtu"]} {d["mem_size"]} {len(d["rounds"])} {d["seed"]}',
+             " ".join(str(x) for x in d["weights"])]
+    for r in d["rounds"]:
+        for key in ("ntx", "nrx"):
+            lines.append(" ".join(str(x) for x in r[key]))
+        lines.append(f'{r["advances"]} {r["skips"]}')
+        lines.append(" ".join(str(x) for x in r["rx_consumed"]))
+        lines.append(f'{r["irq_count"]} {r["irq_fnv"]}')
+        for key in ("tx_count", "rx_count", "tx_fnv", "rx_fnv"):
+            lines.append(" ".join(str(x) for x in r[key]))
+    lines += [" ".join(str(x) for x in s) for s in d["stats"]]
+    lines.append(" ".join(str(x) for x in d["qm_stats"]))
+    lines.append(d["mem_fnv"])
+    lines.append(d["stats_summary"])
+    path = os.path.join(out_dir, "qm16_scale.expect.txt")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return path
+
+
+def _run_scale(exe, mode, tmp_path):
+    r = subprocess.run([exe, "scale", mode, _flatten_scale(str(tmp_path))], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "qm_test scale: ok" in r.stdout
+    print(r.stdout.strip())
+
+
+def test_scale_fixture_shape():
+    """The scale fixture: 16 queue pairs, >= 64 K TX descriptors, an idle queue
+    pair the scheduler skips, a ring that runs dry, TSO/GSO segments, checksum
+    drops, small buffers and interrupts on most queue pairs."""
+    d = json.load(open(os.path.join(GOLDEN, "qm16_scale.json")))
+    assert d["queues"] == 16 and sum(sum(r["ntx"]) for r in d["rounds"]) >= 65536
+    r0 = d["rounds"][0]
+    assert r0["ntx"][5] == 0 and r0["skips"] > 0 and r0["rx_consumed"][7] == r0["nrx"][7]
+    qs = d["qm_stats"]  # tx, rx, txb, rxb, drops csum, no_rx, small, tso, gso, vlan ins, strip, verified, gro, adv, skip
+    assert qs[4] > 0 and qs[5] > 0 and qs[6] > 0 and qs[7] > 0 and qs[8] > 0 and qs[13] == sum(sum(r["ntx"]) for r in d["rounds"])
+    assert all(r["irq_count"] > 0 for r in d["rounds"])
+
+
+def test_queue_manager_scale_cpu(tmp_path):
+    """The CPU path (schedule, run-by-run driver, interrupt replay) reproduces
+    the reference QueueManager's digests at 16 queue pairs x 4096."""
+    _run_scale(_build(tmp_path, "qm_test"), "cpu", tmp_path)
+
+
+@pytest.mark.gpu
+def test_queue_manager_scale_gpu(tmp_path):
+    """The fused device batch at scale, on an HBM image and on FlatHostMemory."""
+    exe = _build(tmp_path, "qm_test")
+    _run_scale(exe, "gpu", tmp_path)
+    _run_scale(exe, "host", tmp_path)
 
 
 def test_fixture_shape():
@@ -120,6 +180,7 @@ def test_queue_manager_reference_simple_host_memory_gpu(tmp_path):
     compiled in place by oracle/Makefile; the binary travels to the GPU box)."""
     for name, disjoint in CASES.items():
         _run(QM_REFMEM, "host", name, tmp_path, () if disjoint else ("interleaved",))
+    _run_scale(QM_REFMEM, "host", tmp_path)
 
 
 @pytest.mark.gpu
