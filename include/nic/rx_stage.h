@@ -224,6 +224,15 @@ struct BatchedQueuePairConfig {
   /// (RxBatchResult::dev) instead of copying them to the host vectors: for
   /// consumers that read completions, hashes and dispatch lists on the GPU.
   bool results_on_device{false};
+  /// submit/collect: a batch's piece sums and resolve run beside the earlier
+  /// pending batches' DMA writes (their own stream) when its TX frames lie
+  /// outside every byte those writes can touch (the overlap check's bounds);
+  /// otherwise — or when that is not known — they are redone after them.
+  /// Results are the same either way.  Off by default: measured on C3 1 M
+  ///  the resolve chain is as bandwidth-bound as the delivery
+  /// beside it, so the overlap gains nothing at the default CU reserve and
+  /// ≈ 4 % with 96 CUs kept free of delivery blocks.
+  bool overlap_resolve{false};
 };
 
 struct RxBatchResult {
@@ -265,6 +274,8 @@ struct RxBatchResult {
     bool device{false};     // resolved on the device
     bool host_tail{false};  // ... and the rest on the host (positions settled neither by relaxation nor by the walk)
     bool walked{false};     // ... positions made by the walk (8 relaxation steps did not settle them)
+    bool overlapped{false};  // submit/collect: sums and resolve ran beside the earlier batches' DMA writes
+    bool overlap_redone{false};  // ... but the frames lie where those write: redone after them
     bool host_image{false};  // run against a HostMemory: TX bytes staged up, delivered bytes written back
     bool staged_whole{false};  // ... the TX bytes' span went up in one copy (dense), else per descriptor
     unsigned replans{0};    // device plans redone because the first outgrew the piece buffers (at most 1)

@@ -382,6 +382,16 @@ int nicgpu_qp_check_flags(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nr
  * The check may then run beside the plan and the speculative resolve. */
 int nicgpu_qp_check_async(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, unsigned flags, void* stream);
 int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict);
+/* After an unsegmented check: bounds[0..1] = [min start, max end) of the TX
+ * spans, bounds[2..3] = [first start, max end) of the RX spans (all bytes the
+ * batch's DMA writes can touch when the verdict was 1); [~0, 0) when empty.
+ * A pipeline tells with them whether a batch's frames lie where an earlier
+ * batch still writes. */
+int nicgpu_qp_check_bounds(const nicgpu_qp* q, uint64_t* bounds);
+/* The piece sums of q's current plan again (nicgpu_qp_plan_async's sums), on
+ * `stream`: for frames an earlier batch's DMA writes changed after the first
+ * sums read them. */
+int nicgpu_qp_resum(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, void* stream);
 /* The kernels of the next plan/check/resolve read the caller's device arrays
  * tx[0, ntx) and rx[0, nrx) in place of view.tx / view.rx (no copy; view is
  * refreshed to point at them).  They must stay valid and unchanged until the

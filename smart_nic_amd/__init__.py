@@ -110,6 +110,8 @@ ABI_SYMBOLS = (
     "nicgpu_qp_walks",
     "nicgpu_qp_check_async",
     "nicgpu_qp_check_wait",
+    "nicgpu_qp_check_bounds",
+    "nicgpu_qp_resum",
     "nicgpu_event_synchronize",
     "nicgpu_host_register",
     "nicgpu_host_unregister",
@@ -194,6 +196,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_qp_walks": (i32, [vp, vp]),
         "nicgpu_qp_check_async": (i32, [vp, ctypes.c_uint64, sz, sz, ctypes.c_uint, vp]),
         "nicgpu_qp_check_wait": (i32, [vp, vp]),
+        "nicgpu_qp_check_bounds": (i32, [vp, vp]),
+        "nicgpu_qp_resum": (i32, [vp, vp, ctypes.c_uint64, vp]),
         "nicgpu_event_synchronize": (i32, [vp]),
         "nicgpu_host_register": (i32, [vp, sz, ctypes.POINTER(vp), ctypes.POINTER(i32)]),
         "nicgpu_host_unregister": (i32, [vp]),

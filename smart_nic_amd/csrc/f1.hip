@@ -972,6 +972,7 @@ constexpr unsigned kQpStats = 16;
 // batch's 16 stats totals — the one download a resolve needs
 constexpr unsigned kQpTail = 3 + 16 + 2;  // ... then [19] the plan overflowed (1 buffers, 2 pieces per descriptor), [20] its piece count
 constexpr int kQpRelaxSteps = 8;  // position relaxations before the host takes the rest
+constexpr unsigned kQpBoundsAt = 8;  // misc()[8..11]: the check's bounds, [12..15] their presets
 
 // Segmented batches (several queue pairs, nicgpu_qp_set_segments): each grid
 // block serves one segment — blocks in proportion to its TX descriptors — so a
@@ -1574,12 +1575,25 @@ struct QpRxEndSeg {  // QpRxEnd keyed by segment, for RX index k
   }
 };
 
+// Also the batch's bounds (unsegmented batches; bounds[0..3] preset to
+// ~0, 0, ~0, 0): the TX spans' [min start, max end) — per-block reduction, one
+// atomic pair per block — and the RX spans' [first start, running max end),
+// which bound every byte the batch's DMA writes can touch when the spans
+// ascend (the caller's pipelining reads them only then).
 __global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t ntx,
                                                             const nicgpu_rx_descriptor* __restrict__ rx, uint64_t nrx,
                                                             uint64_t mem_size, const uint64_t* __restrict__ end_max,
-                                                            unsigned long long* flag, unsigned long long gen, QpSegs S) {
+                                                            unsigned long long* flag, unsigned long long gen, QpSegs S,
+                                                            unsigned long long* bounds) {
+  __shared__ unsigned long long red_lo[kQpBlock / kWave], red_hi[kQpBlock / kWave];
   const uint64_t n = ntx > nrx ? ntx : nrx;
+  uint64_t tlo = ~0ull, thi = 0;
   for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < n; k += (uint64_t) gridDim.x * kQpBlock) {
+    if (bounds && k < nrx) {
+      const uint64_t e = QpRxEnd{mem_size}(rx[k]);
+      if (e != 0 && (k == 0 || end_max[k - 1] == 0)) bounds[2] = rx[k].buffer_address;  // the first span's start
+      if (k + 1 == nrx) bounds[3] = end_max[k];
+    }
     if (k < nrx && k > 0 && QpRxEnd{mem_size}(rx[k]) != 0) {
       const uint64_t key = S.seg ? (uint64_t) qp_seg_of_rx(S, k) << kQpSegShift : 0u;
       if ((key | rx[k].buffer_address) < end_max[k - 1]) flag[0] = gen;
@@ -1587,6 +1601,8 @@ __global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_desc
     if (k < ntx) {
       const uint64_t a = tx[k].buffer_address, len = tx[k].length;
       if (len == 0 || !nicqp::dma_ok(mem_size, a, len)) continue;
+      tlo = a < tlo ? a : tlo;
+      thi = a + len > thi ? a + len : thi;
       uint64_t lo = 0, hi = nrx, key = 0;
       if (S.seg) {
         const uint32_t s = qp_seg_of_tx(S, k);
@@ -1601,6 +1617,29 @@ __global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_desc
         else hi = mid;
       }
       if (lo < ring_end && rx[lo].buffer_address < a + len) flag[1] = gen;
+    }
+  }
+  if (!bounds) return;
+  // the block's TX bounds: wave minimum / maximum, then the block's waves
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    const uint64_t l2 = __shfl_xor(tlo, o), h2 = __shfl_xor(thi, o);
+    tlo = l2 < tlo ? l2 : tlo;
+    thi = h2 > thi ? h2 : thi;
+  }
+  const unsigned w = threadIdx.x / kWave;
+  if (lane_id() == 0) {
+    red_lo[w] = tlo;
+    red_hi[w] = thi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (unsigned i = 1; i < kQpBlock / kWave; ++i) {
+      tlo = red_lo[i] < tlo ? red_lo[i] : tlo;
+      thi = red_hi[i] > thi ? red_hi[i] : thi;
+    }
+    if (thi != 0) {
+      atomicMin(&bounds[0], (unsigned long long) tlo);
+      atomicMax(&bounds[1], (unsigned long long) thi);
     }
   }
 }
@@ -1654,6 +1693,7 @@ struct nicgpu_qp {
   uint32_t *queue_which = nullptr, *queue_start = nullptr, *queue_end = nullptr;
   size_t c_sk = 0, c_qw = 0, c_em = 0, c_key = 0;
   uint64_t* end_max = nullptr;  // [nrx] nicgpu_qp_check's running max of RX span ends
+  unsigned long long* bounds = nullptr;  // [4] the check's TX and RX bounds (nicgpu_qp_check_bounds)
   unsigned long long* scal = nullptr;
   unsigned long long* dlv_acc = nullptr;  // the delivery's accumulator (DeliverParams::acc), zero between launches
   size_t c_dlv_acc = 0;
@@ -1822,6 +1862,7 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
       hipMalloc(&q->dlv_done, sizeof(unsigned int)) != hipSuccess ||
       hipMemset(q->dlv_done, 0, sizeof(unsigned int)) != hipSuccess ||
       hipMalloc(&q->gflags, 6 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&q->bounds, 4 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(q->gflags, 0, 6 * sizeof(unsigned long long)) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
@@ -1848,7 +1889,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
                   q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
                   q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sort_key, q->sorted_key, q->queue_which,
                   q->queue_start, q->queue_end, q->end_max, q->dlv_acc, q->dlv_done, q->gflags, q->piece_cs4,
-                  q->d_seg, q->d_blk, q->d_fb, q->d_segout, q->d_split, q->mflag, q->mscan, q->mlist};
+                  q->d_seg, q->d_blk, q->d_fb, q->d_segout, q->d_split, q->mflag, q->mscan, q->mlist, q->bounds};
   for (void* b : bufs)
     if (b) (void) hipFree(b);
   if (q->hp) (void) hipHostFree(q->hp);
@@ -2011,6 +2052,20 @@ int nicgpu_qp_check_flags(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nr
   return st == NICGPU_OK ? nicgpu_qp_check_wait(q, verdict) : st;
 }
 
+int nicgpu_qp_check_bounds(const nicgpu_qp* q, uint64_t* bounds) {
+  if (!q || !bounds || q->chk_on || q->nseg) return NICGPU_ERR_INVALID;
+  std::memcpy(bounds, q->misc() + kQpBoundsAt, 4 * sizeof(uint64_t));
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_resum(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, void* stream) {
+  if (!q || (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0))) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  const uint64_t cap = std::min(q->c_pdesc, std::min(q->c_pcs, q->c_pcs4));
+  return checksum_split_count(mem, q->piece_desc, cap, reinterpret_cast<const uint64_t*>(q->gflags + 4), q->piece_csum,
+                              q->piece_cs4, stream);
+}
+
 int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict) {
   if (!q || !verdict || !q->chk_on) return NICGPU_ERR_INVALID;
   q->chk_on = false;
@@ -2034,6 +2089,15 @@ int nicgpu_qp_check_async(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nr
   const unsigned long long gen = ++q->gen;
   int st = NICGPU_OK;
   if (segmented && (ntx != q->seg_ntx || nrx != q->seg_nrx)) return NICGPU_ERR_INVALID;
+  // the bounds' presets (page-locked source, constant: no hazard with an
+  // earlier copy still reading it)
+  uint64_t* preset = q->misc() + kQpBoundsAt + 4;
+  preset[0] = ~0ull;
+  preset[1] = 0;
+  preset[2] = ~0ull;
+  preset[3] = 0;
+  st = hip_status(hipMemcpyAsync(q->bounds, preset, 4 * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  if (st != NICGPU_OK) return st;
   if (nrx && segmented) {  // per queue pair: ends keyed by segment
     hipcub::TransformInputIterator<uint64_t, QpRxEndSeg, hipcub::CountingInputIterator<uint64_t>> ends(
         hipcub::CountingInputIterator<uint64_t>(0), QpRxEndSeg{q->rx, qp_segs(q), mem_size});
@@ -2057,11 +2121,13 @@ int nicgpu_qp_check_async(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nr
   if (n) {
     hipLaunchKernelGGL(qp_check_kernel, dim3(qp_grid(q, n)), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, q->rx,
                        (uint64_t) nrx, mem_size, q->end_max, q->gflags + 1, gen,
-                       segmented ? qp_segs(q) : QpSegs{nullptr, nullptr, 0u});
+                       segmented ? qp_segs(q) : QpSegs{nullptr, nullptr, 0u}, q->nseg ? nullptr : q->bounds);
     st = hip_status(hipGetLastError());
   }
   uint64_t* f = q->misc() + 1;
   if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(f, q->gflags + 1, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK)
+    st = hip_status(hipMemcpyAsync(q->misc() + kQpBoundsAt, q->bounds, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   if (st == NICGPU_OK) st = hip_status(hipEventRecord(q->checked, s));
   if (st != NICGPU_OK) return st;
   q->chk_gen = gen;

@@ -20,6 +20,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -1064,7 +1065,14 @@ struct BatchedQueuePair::Slot {
   void* ev_rx = nullptr;     // RX descriptors uploaded
   void* ev_resolved = nullptr;  // completions final
   void* ev_done = nullptr;      // DMA writes and RSS done
-  void* ev_submit = nullptr;    // the caller's stream when device descriptors were handed over
+  void* ev_submit = nullptr;    // the caller's stream at submit (device descriptors handed over; frames produced)
+  void* ev_gate = nullptr;      // overlapped resolve: the caller's stream, for a batch whose frames earlier batches write
+  // overlapped resolve (submit/collect): the piece sums and the resolve on the
+  // resolve stream, beside the earlier batches' DMA writes; rx_lo/hi_w: the
+  // bytes this batch's DMA writes can touch ([0, ~0) unknown), for the later
+  // batches' hazard test
+  bool overlap = false;
+  std::uint64_t rx_lo_w = 0, rx_hi_w = ~0ull;
   DevBuf hits;               // per-table-index RSS hits of the batch
   HostBuf h_meta, h_lists;   // pinned landing space of the downloads
   SideWorker worker;         // issues the downloads
@@ -1151,14 +1159,14 @@ struct BatchedQueuePair::Slot {
         e = nullptr;
       }
     irq_pending = false;
-    for (void* e : {ev_tx, ev_rx, ev_resolved, ev_done, ev_submit, ev_staged, ev_wb})
+    for (void* e : {ev_tx, ev_rx, ev_resolved, ev_done, ev_submit, ev_staged, ev_wb, ev_gate})
       if (e) (void) nicgpu_event_destroy(e);
     qp = nullptr;
-    ev_tx = ev_rx = ev_resolved = ev_done = ev_submit = ev_staged = ev_wb = nullptr;
+    ev_tx = ev_rx = ev_resolved = ev_done = ev_submit = ev_staged = ev_wb = ev_gate = nullptr;
   }
   void create(int dev) {
     check(nicgpu_qp_create(&qp, dev), "nicgpu_qp_create");
-    for (void** e : {&ev_tx, &ev_rx, &ev_resolved, &ev_done, &ev_submit, &ev_staged, &ev_wb})
+    for (void** e : {&ev_tx, &ev_rx, &ev_resolved, &ev_done, &ev_submit, &ev_staged, &ev_wb, &ev_gate})
       check(nicgpu_event_create(e), "nicgpu_event_create");
     for (auto& side : ev_irq)
       for (void*& e : side) check(nicgpu_event_create(&e), "nicgpu_event_create");
@@ -1209,6 +1217,15 @@ struct BatchedQueuePair::Scratch {
   void* side_plan = nullptr;  // plan and overlap check of a batch beside the earlier batch's writes
   void* side_wb = nullptr;    // host-image write-backs, beside the next batches' work
   void* side_irq = nullptr;   // completions for the interrupt callbacks, as soon as they are final
+  void* side_res = nullptr;   // overlapped resolves: piece sums and resolve beside the earlier batches' DMA writes
+  // the job thread's record of the two batches before the current one (their
+  // DMA writes may still run): the bytes each can write, [0, ~0) unknown
+  struct WriteBox {
+    std::uint64_t lo = 0, hi = ~0ull;
+  };
+  WriteBox recent[2];
+  unsigned n_recent = 0;
+  std::uint64_t overlaps = 0, overlaps_redone = 0;
   std::shared_ptr<HostImage> img = std::make_shared<HostImage>();  // the HostMemory the host-image batches run against (shared by a manager's stages)
   SideWorker up_worker;  // process_batch: issues the RX descriptor uploads
   static constexpr unsigned kSlots = 3;
@@ -1222,7 +1239,8 @@ struct BatchedQueuePair::Scratch {
     if (side_plan) (void) nicgpu_stream_destroy(side_plan);
     if (side_wb) (void) nicgpu_stream_destroy(side_wb);
     if (side_irq) (void) nicgpu_stream_destroy(side_irq);
-    side_up = side_down = side_plan = side_wb = side_irq = nullptr;
+    if (side_res) (void) nicgpu_stream_destroy(side_res);
+    side_up = side_down = side_plan = side_wb = side_irq = side_res = nullptr;
     if (img.use_count() == 1) img->release();  // a manager's shared image is released by its last stage
     device = -1;
   }
@@ -1231,9 +1249,14 @@ struct BatchedQueuePair::Scratch {
     release();
     check(nicgpu_stream_create(&side_up), "nicgpu_stream_create");
     check(nicgpu_stream_create(&side_down), "nicgpu_stream_create");
-    check(nicgpu_stream_create_priority(&side_plan, 1), "nicgpu_stream_create_priority");
+    static const int plan_low = [] {  // tuning A/B: NIC_PLAN_PRIORITY=high
+      const char* e = std::getenv("NIC_PLAN_PRIORITY");
+      return e && std::strcmp(e, "high") == 0 ? 0 : 1;
+    }();
+    check(nicgpu_stream_create_priority(&side_plan, plan_low), "nicgpu_stream_create_priority");
     check(nicgpu_stream_create(&side_wb), "nicgpu_stream_create");
     check(nicgpu_stream_create(&side_irq), "nicgpu_stream_create");
+    check(nicgpu_stream_create_priority(&side_res, 0), "nicgpu_stream_create_priority");  // high: beside a DMA write
     for (Slot& sl : slot) sl.create(dev);
     device = dev;
   }
@@ -1416,6 +1439,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
     sl.image = nullptr;
     sl.staged = false;
     sl.multi = false;
+    sl.overlap = false;
     sl.dep_stage.clear();
     sl.dep_rx.clear();
     upload(sl, tx, rx, true);
@@ -1462,6 +1486,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDe
   sl.image = nullptr;
   sl.staged = false;
   sl.multi = false;
+  sl.overlap = false;
   sl.dep_stage.clear();
   sl.dep_rx.clear();
   check(nicgpu_event_record(sl.ev_submit, stream), "nicgpu_event_record");  // a producer's writes before this call
@@ -1563,6 +1588,7 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
   sl.image = nullptr;
   sl.staged = false;
   sl.multi = false;
+  sl.overlap = false;
   sl.dep_stage.clear();
   sl.dep_rx.clear();
   if (img) image_prepare(sl, *img, tx, rx);  // dependencies on the batches pending now
@@ -1582,7 +1608,13 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
   // device work (device descriptors are copied in the job, in stream order);
   // the rest runs in submission order on the job thread
   if (device && !d) upload(sl, tx, rx, false);
-  if (device && d) check(nicgpu_event_record(sl.ev_submit, stream), "nicgpu_event_record");
+  // what the caller enqueued before this call (descriptors, frames): the
+  // overlapped resolve waits for it, not for the earlier batches' DMA writes
+  if (device) check(nicgpu_event_record(sl.ev_submit, stream), "nicgpu_event_record");
+  sl.overlap = device && !img && config_.overlap_resolve;
+  sl.rx_lo_w = 0;
+  sl.rx_hi_w = ~0ull;
+  if (S.pending == 0) S.n_recent = 0;  // every earlier batch collected: their writes are done
   // a host-image batch's TX bytes go up now, beside the earlier batches' work,
   // unless they overlap bytes an earlier pending batch delivers: then its job
   // stages them after that batch's write-back (recorded by the earlier job)
@@ -1612,8 +1644,18 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
         on_host(sl.mem, htx, hrx, sl.stats, sl.result, sl.stream, disjoint, check_us);
       }
       sl.result.timings.check_us = check_us;
+      // this batch's writes, for the overlapped resolves of the next two
+      Scratch& SS = *scratch_;
+      const Scratch::WriteBox box{sl.on_device ? sl.rx_lo_w : 0, sl.on_device ? sl.rx_hi_w : ~0ull};
+      SS.recent[1] = SS.recent[0];
+      SS.recent[0] = box;
+      SS.n_recent = std::min(SS.n_recent + 1, 2u);
       sl.job_done.set_value();
     } catch (...) {
+      Scratch& SS = *scratch_;  // writes unknown
+      SS.recent[1] = SS.recent[0];
+      SS.recent[0] = Scratch::WriteBox{};
+      SS.n_recent = std::min(SS.n_recent + 1, 2u);
       sl.job_done.set_exception(std::current_exception());
     }
   };
@@ -1799,6 +1841,14 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
   out.timings.host_image = sl.image != nullptr;
   out.timings.staged_whole = sl.image != nullptr && sl.whole;
   if (sl.staged) check(nicgpu_stream_wait_event(stream, sl.ev_staged), "nicgpu_stream_wait_event");
+  // Overlapped resolve (submit/collect): the piece sums and the resolve on the
+  // resolve stream `rs`, after what the caller enqueued before submit, beside
+  // the earlier batches' DMA writes still on `stream`; the overlap check's
+  // bounds then tell whether this batch's frames lie where those write (then
+  // both are redone behind them).  The DMA writes stay on `stream`, in order.
+  const bool ov = sl.overlap && side && sl.image == nullptr;
+  void* rs = ov ? S.side_res : stream;
+  if (ov) check(nicgpu_stream_wait_event(rs, sl.ev_submit), "nicgpu_stream_wait_event");
   // the plan and the piece sums enqueued without a wait: the piece buffers are
   // sized ahead (ntx + ntx / 4 pieces, or what an earlier batch needed); a
   // plan that does not fit them, or a descriptor planning more pieces than
@@ -1806,7 +1856,7 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
   // finish return NICGPU_ERR_RANGE — that batch then takes the host path
   // (which refuses it if its total does not fit either), the next one fits
   check(nicgpu_qp_plan_async(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu,
-                             &v, ps, stream),
+                             &v, ps, rs),
         "nicgpu_qp_plan_async");
   out.timings.sums_us += us_since(t);
   t = clock::now();
@@ -1816,7 +1866,7 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
   }
   if (!dev_desc) {
     check(nicgpu_stream_wait_event(ps, sl.ev_rx), "nicgpu_stream_wait_event");
-    if (side) check(nicgpu_stream_wait_event(stream, sl.ev_rx), "nicgpu_stream_wait_event");
+    if (side) check(nicgpu_stream_wait_event(rs, sl.ev_rx), "nicgpu_stream_wait_event");
   }
   out.timings.copy_us += us_since(t);
   // the speculative resolve goes in behind the piece sums before the overlap
@@ -1827,9 +1877,9 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
   // batch, and the context's resolve state stays set until the next start.
   // Results are unaffected; disjoint rings are the common case.
   t = clock::now();
-  check(nicgpu_qp_resolve_start(sl.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, stream),
+  check(nicgpu_qp_resolve_start(sl.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, rs),
         "nicgpu_qp_resolve_start");
-  check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");  // final unless relaxed / tail below
+  check(nicgpu_event_record(sl.ev_resolved, rs), "nicgpu_event_record");  // final unless relaxed / tail below
   out.timings.resolve_us += us_since(t);
   // overlapping buffers go to the host path before anything is written; a
   // ring whose RX buffers are not in ascending address order is sorted there.
@@ -1837,13 +1887,45 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
   t = clock::now();
   int verdict = -1;
   check(nicgpu_qp_check(sl.qp, mem.size, ntx, nrx, &verdict, ps), "nicgpu_qp_check");
+  const bool ascending = verdict >= 0;  // the device decided: RX spans in address order
   if (verdict < 0) {
     const auto [htx, hrx] = host_spans(sl, tx, rx, stream);
     verdict = buffers_disjoint(mem.size, htx, hrx) ? 1 : 0;
   }
   disjoint = verdict;
   check_us += us_since(t);
+  if (ov) {
+    // the overlapped pass must be over before anything else touches this
+    // context's buffers, whatever happens next (the host path included)
+    check(nicgpu_stream_wait_event(stream, sl.ev_resolved), "nicgpu_stream_wait_event");
+  }
   if (!disjoint) return false;
+  if (ov) {
+    std::uint64_t bnd[4];
+    check(nicgpu_qp_check_bounds(sl.qp, bnd), "nicgpu_qp_check_bounds");
+    // this batch's writes stay inside its RX spans (ascending: the first
+    // span's start is their least; unsorted rings: unknown)
+    sl.rx_lo_w = !ascending ? 0 : bnd[3] > bnd[2] ? bnd[2] : 0;
+    sl.rx_hi_w = !ascending ? ~0ull : bnd[3] > bnd[2] ? bnd[3] : 0;
+    bool hazard = false;
+    if (bnd[1] > bnd[0])  // frames to read: do the earlier batches' writes reach them?
+      for (unsigned k = 0; k < S.n_recent; ++k) hazard |= S.recent[k].hi > bnd[0] && bnd[1] > S.recent[k].lo;
+    out.timings.overlapped = true;
+    ++S.overlaps;
+    if (hazard) {
+      // redo the sums and the resolve behind everything `stream` holds now
+      // (the earlier batches' DMA writes included)
+      out.timings.overlap_redone = true;
+      ++S.overlaps_redone;
+      check(nicgpu_event_record(sl.ev_gate, stream), "nicgpu_event_record");
+      check(nicgpu_stream_wait_event(rs, sl.ev_gate), "nicgpu_stream_wait_event");
+      check(nicgpu_qp_resum(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, rs), "nicgpu_qp_resum");
+      check(nicgpu_qp_resolve_start(sl.qp, mem.size, ntx, nrx, config_.max_mtu, config_.queue_id, rs),
+            "nicgpu_qp_resolve_start");
+      check(nicgpu_event_record(sl.ev_resolved, rs), "nicgpu_event_record");
+      check(nicgpu_stream_wait_event(stream, sl.ev_resolved), "nicgpu_stream_wait_event");
+    }
+  }
   t = clock::now();
   // the DMA writes and RSS of the completions the resolve settles (bounded on
   // the device) go in at once: the host waits for the resolve while they are
@@ -1882,6 +1964,10 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
     return false;
   }
   check(rst, "nicgpu_qp_resolve_finish");
+  if (ov) {  // the relaxation's rewrites (on rs) before the rest of this batch's work on `stream`
+    check(nicgpu_event_record(sl.ev_resolved, rs), "nicgpu_event_record");
+    check(nicgpu_stream_wait_event(stream, sl.ev_resolved), "nicgpu_stream_wait_event");
+  }
   sl.settled = settled;
   sl.relaxed = done < ntx || settled < used;  // completions rewritten after ev_resolved
   out.timings.resolve_us += us_since(t);
@@ -2311,6 +2397,7 @@ void BatchedQueuePair::process_batch(HostMemory& m, std::span<const TxDescriptor
   sl.tx_dev = nullptr;
   sl.rx_dev = nullptr;
   sl.multi = false;
+  sl.overlap = false;
   image_prepare(sl, I, tx, rx);  // nothing pending: no dependencies
   sl.staged = false;
   QueuePairStats st = stats_;
@@ -2466,6 +2553,7 @@ bool BatchedQueuePair::process_queues(const DeviceHostMemory& mem_in, HostImage*
   sl.dep_stage.clear();
   sl.dep_rx.clear();
   sl.multi = true;
+  sl.overlap = false;
   sl.nseg = Q;
   RxBatchResult cat;
   cat.timings = RxBatchResult::Timings{};

@@ -243,11 +243,24 @@ int run_case(std::uint64_t seed) {
     qp.process_batch(DeviceHostMemory{base, mem_size}, tx, rx, go);
   }
   bool irq_ok = fired_dev.size() == fired_host.size();
-  for (std::size_t i = 0; irq_ok && i < fired_host.size(); ++i) irq_ok = same(fired_dev[i], fired_host[i]);
+  std::size_t irq_at = 0;
+  for (; irq_ok && irq_at < fired_host.size(); ++irq_at) irq_ok = same(fired_dev[irq_at], fired_host[irq_at]);
   if (!irq_ok) {
-    std::fprintf(stderr, "seed %llu: interrupt callbacks differ (%zu device, %zu host)\n", (unsigned long long) seed,
-                 fired_dev.size(), fired_host.size());
-    return 1;
+    // the first difference and how the batch was resolved; the completions
+    // are compared below too, so the report says whether only the replay's
+    // copy of them differed
+    const auto& T = go.timings;
+    std::fprintf(stderr,
+                 "seed %llu: interrupt callbacks differ (%zu device, %zu host), first at %zu; device %s keep %d "
+                 "walked %d host_tail %d ntx %zu nrx %zu irq_wait %.1f us\n",
+                 (unsigned long long) seed, fired_dev.size(), fired_host.size(), irq_at ? irq_at - 1 : 0,
+                 T.device ? "yes" : "no", (int) keep, (int) T.walked, (int) T.host_tail, ntx, nrx, T.irq_wait_us);
+    if (irq_at && irq_at - 1 < fired_dev.size() && irq_at - 1 < fired_host.size()) {
+      const CompletionEntry &a = fired_dev[irq_at - 1], &b = fired_host[irq_at - 1];
+      std::fprintf(stderr, "  device: q %u idx %u status %u segs %u ver %u | host: q %u idx %u status %u segs %u ver %u\n",
+                   a.queue_id, a.descriptor_index, a.status, a.segments_produced, (unsigned) a.checksum_verified,
+                   b.queue_id, b.descriptor_index, b.status, b.segments_produced, (unsigned) b.checksum_verified);
+    }
   }
   g_irq += irq ? fired_dev.size() : 0;
   if (keep && !materialize(go)) {
@@ -267,6 +280,10 @@ int run_case(std::uint64_t seed) {
   for (std::size_t i = 0; ok && i < ho.tx_completions.size(); ++i) ok = same(go.tx_completions[i], ho.tx_completions[i]);
   for (std::size_t i = 0; ok && i < ho.rx_completions.size(); ++i) ok = same(go.rx_completions[i], ho.rx_completions[i]);
   const bool comp_ok = ok;
+  if (!irq_ok) {
+    std::fprintf(stderr, "  completions (materialized after the batch) %s the host's\n", comp_ok ? "equal" : "differ from");
+    return 1;
+  }
   ok = ok && std::memcmp(&hs, &qp.stats(), sizeof(hs)) == 0;
   const bool stats_ok = ok;
   ok = ok && go.rx_consumed == ho.rx_consumed && go.tx_processed == ho.tx_processed;
@@ -457,6 +474,7 @@ int run_full(const char* wl, bool dev_desc, bool keep) {
 // the image and the RSS engine's stats must all be equal.
 std::size_t g_pipe_batches = 0, g_pipe_host = 0, g_pipe_devdesc = 0, g_pipe_himg = 0;
 bool g_force_himg = false;  // `pipeline himg`: every sequence's pipelined side on a HostMemory
+std::size_t g_pipe_overlapped = 0, g_pipe_redone = 0;  // overlapped resolves that stood / were redone
 
 int run_pipeline(std::uint64_t seed) {
   Rng r{seed * 7727 + 5};
@@ -477,6 +495,10 @@ int run_pipeline(std::uint64_t seed) {
   std::vector<std::vector<TxDescriptor>> txs(nb);
   std::vector<std::vector<RxDescriptor>> rxs(nb);
   std::size_t ring_at = 0;
+  // one sequence in five reads no frame from the ring: every batch's
+  // overlapped resolve then stands (the others mostly redo it behind the
+  // earlier batches' writes)
+  const bool quiet = seed % 5 == 0;
   for (int b = 0; b < nb; ++b) {
     const std::size_t ntx = 1 + r.below(b % 3 == 0 ? 3000 : 300);
     const std::size_t nrx = std::min<std::size_t>(ring / 2, ntx * (1 + r.below(2)) + r.below(5));
@@ -484,7 +506,7 @@ int run_pipeline(std::uint64_t seed) {
     const bool own = r.below(4) == 0;
     for (std::size_t i = 0; i < ntx; ++i) {
       TxDescriptor t{};
-      if (r.below(6) == 0) {  // a frame an earlier batch delivered into the ring
+      if (r.below(6) == 0 && !quiet) {  // a frame an earlier batch delivered into the ring
         const std::size_t slot = own ? r.below(ring) : (ring_at + nrx + r.below(static_cast<std::uint32_t>(ring - nrx))) % ring;
         t.buffer_address = tx_region + slot * buf;
         t.length = 64 + r.below(1400);
@@ -544,6 +566,7 @@ int run_pipeline(std::uint64_t seed) {
   cfg.on_interrupt = [&irq_pipe](std::uint16_t, const CompletionEntry& e) { irq_pipe.push_back(e); };
   const bool keep = (seed >> 1) & 1;  // results_on_device on the pipelined side
   cfg.results_on_device = keep;
+  cfg.overlap_resolve = seed % 3 != 1;  // the overlapped resolve (opt-in) on two sequences in three
   BatchedQueuePair pipe{cfg};
   bool view_ok = true;
   std::vector<RxBatchResult> want(nb), got;
@@ -635,6 +658,8 @@ int run_pipeline(std::uint64_t seed) {
     for (std::size_t i = 0; ok && i < w.rx_completions.size(); ++i) ok = same(w.rx_completions[i], g.rx_completions[i]);
     if (!ok) std::fprintf(stderr, "pipeline seed %llu: batch %d differs\n", (unsigned long long) seed, b);
     g_pipe_host += !w.timings.device;
+    g_pipe_overlapped += g.timings.overlapped && !g.timings.overlap_redone;
+    g_pipe_redone += g.timings.overlap_redone;
   }
   g_pipe_batches += nb;
   if (dev_desc) g_pipe_devdesc += nb;
@@ -1256,9 +1281,17 @@ int main(int argc, char** argv) {
     int bad = 0;
     for (std::uint64_t s = 1; s <= count; ++s) bad += run_pipeline(s);
     if (bad) return 1;
+    // both kinds of overlapped resolve happened (unless every sequence ran on a HostMemory)
+    if (!g_force_himg && count >= 10 && (g_pipe_overlapped == 0 || g_pipe_redone == 0)) {
+      std::fprintf(stderr, "pipeline: %zu overlapped resolves stood, %zu redone: both paths expected\n",
+                   g_pipe_overlapped, g_pipe_redone);
+      return 1;
+    }
     std::printf("rx_stage_gpu_fuzz pipeline: ok (%llu sequences, %zu batches, %zu of them on the host path, %zu "
-                "with device descriptors, %zu on a HostMemory, %zu results left on the device)\n",
-                (unsigned long long) count, g_pipe_batches, g_pipe_host, g_pipe_devdesc, g_pipe_himg, g_keep);
+                "with device descriptors, %zu on a HostMemory, %zu results left on the device; overlapped "
+                "resolves: %zu stood, %zu redone behind earlier writes)\n",
+                (unsigned long long) count, g_pipe_batches, g_pipe_host, g_pipe_devdesc, g_pipe_himg, g_keep,
+                g_pipe_overlapped, g_pipe_redone);
     return 0;
   }
   if (argc > 1 && std::strcmp(argv[1], "full") == 0) {
