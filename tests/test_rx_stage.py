@@ -164,7 +164,8 @@ def test_rx_stage_device_overlap_check(tmp_path):
     buffers_disjoint on 600 random layouts (ascending rings with and without
     TX/RX and RX/RX overlaps or touching ends, shuffled rings, invalid and
     clipped descriptors): equal whenever the device decides, and it decides
-    every ascending ring."""
+    every ascending ring; the check's TX / RX bounds (nicgpu_qp_check_bounds)
+    equal the host's on every layout."""
     exe = _build(tmp_path, "rx_stage_gpu_fuzz")
     r = subprocess.run([exe, "check", "600"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -177,7 +178,11 @@ def test_rx_stage_device_limits(tmp_path):
     """The device path's limits: a descriptor planning more pieces than 32-bit
     piece indices allow makes nicgpu_qp_plan return NICGPU_ERR_RANGE and the
     batch takes the host path (equal to the host resolve); descriptor arrays
-    inside the image that an RX buffer of the batch overlaps are refused."""
+    inside the image that an RX buffer of the batch overlaps are refused; a
+    plan that outgrows the piece buffers is redone once; and a batch whose
+    ring positions 8 relaxation steps do not settle (400 TSO packets against
+    a ring of one-in-three too-small buffers) is walked on the device
+    (timings.walked, no host tail) and equals the host resolve."""
     exe = _build(tmp_path, "rx_stage_gpu_fuzz")
     r = subprocess.run([exe, "edges"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
