@@ -1712,6 +1712,8 @@ struct nicgpu_qp {
   uint64_t* hp = nullptr;
   uint64_t* misc() const { return hp + kQpTail; }
   unsigned grid = 1;
+  // blocks the partials hold: the grid, or one per segment of the largest table
+  unsigned part_blocks() const { return grid > NICGPU_QP_MAX_SEGMENTS ? grid : NICGPU_QP_MAX_SEGMENTS; }
   uint64_t walks = 0;  // resolves whose positions the walk made (qp_walk)
   hipEvent_t planned = nullptr;   // nicgpu_qp_plan_on: the piece descriptors are written
   hipEvent_t resolved = nullptr;  // nicgpu_qp_resolve_start: its partials are on the host
@@ -1854,9 +1856,18 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
   if (di.status != NICGPU_OK) return di.status;
   auto* q = new nicgpu_qp();
   q->device = device;
-  q->grid = (unsigned) di.cus * 8u;
+  // blocks per CU of the per-TX kernels (grid-stride loops): 4 measured best
+  // on C3 1 M — 8 → 4: one batch at a time 537 → 505 µs, pipelined 480 → 455,
+  // qm16 622 → 615; 16 slower, 1–3 no better (profiles/r05_qp_grid_ab.txt).
+  // Tuning A/B: NICGPU_QP_BLOCKS_PER_CU.
+  static const unsigned grid_per_cu = [] {
+    const char* e = std::getenv("NICGPU_QP_BLOCKS_PER_CU");
+    const int v = e ? std::atoi(e) : 4;
+    return (unsigned) (v >= 1 && v <= 64 ? v : 4);
+  }();
+  q->grid = (unsigned) di.cus * grid_per_cu;
   if (hipMalloc(&q->scal, 4 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc(&q->partials, ((size_t) q->grid * kQpStats + kQpTail) * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&q->partials, ((size_t) q->part_blocks() * kQpStats + kQpTail) * sizeof(uint64_t)) != hipSuccess ||
       hipMalloc(&q->queue_start, 65536 * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&q->queue_end, 65536 * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&q->dlv_done, sizeof(unsigned int)) != hipSuccess ||
@@ -2456,7 +2467,7 @@ int nicgpu_qp_set_segments(nicgpu_qp* q, const nicgpu_qp_segment* seg, size_t ns
   // blocks in proportion to the segments' TX descriptors, at least one each
   const uint64_t want = std::max<uint64_t>((ntx + kQpBlock - 1) / kQpBlock, nseg);
   const uint64_t G = std::min<uint64_t>(std::max<uint64_t>(want, nseg), std::max<uint64_t>(q->grid, nseg));
-  if (G > q->grid) return NICGPU_ERR_INVALID;  // partials hold q->grid blocks
+  if (G > q->part_blocks()) return NICGPU_ERR_INVALID;  // partials hold part_blocks() blocks
   std::vector<QpBlk> blk;
   std::vector<uint32_t> fb(nseg);
   blk.reserve(G);
