@@ -383,8 +383,9 @@ int nicgpu_qp_check_flags(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nr
 int nicgpu_qp_check_async(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, unsigned flags, void* stream);
 int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict);
 /* After an unsegmented check: bounds[0..1] = [min start, max end) of the TX
- * spans, bounds[2..3] = [first start, max end) of the RX spans (all bytes the
- * batch's DMA writes can touch when the verdict was 1); [~0, 0) when empty.
+ * spans; when the verdict was 0 or 1 (the RX spans ascend) bounds[2..3] =
+ * [least start, max end) of the RX spans, all bytes the batch's DMA writes can
+ * touch (undefined for a verdict of -1); [~0, 0) when empty.
  * A pipeline tells with them whether a batch's frames lie where an earlier
  * batch still writes. */
 int nicgpu_qp_check_bounds(const nicgpu_qp* q, uint64_t* bounds);

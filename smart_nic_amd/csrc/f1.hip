@@ -1580,6 +1580,11 @@ struct QpRxEndSeg {  // QpRxEnd keyed by segment, for RX index k
 // atomic pair per block — and the RX spans' [first start, running max end),
 // which bound every byte the batch's DMA writes can touch when the spans
 // ascend (the caller's pipelining reads them only then).
+// SIMPLE: no running-max scan beforehand — every RX span is taken to be
+// nonempty, so the ring ascends iff each span starts at or after the previous
+// one's end and the running max is the previous end itself; a span that
+// receives nothing sets bounds[4] = gen (the caller then runs the scan form).
+template <bool SIMPLE>
 __global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t ntx,
                                                             const nicgpu_rx_descriptor* __restrict__ rx, uint64_t nrx,
                                                             uint64_t mem_size, const uint64_t* __restrict__ end_max,
@@ -1588,15 +1593,27 @@ __global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_desc
   __shared__ unsigned long long red_lo[kQpBlock / kWave], red_hi[kQpBlock / kWave];
   const uint64_t n = ntx > nrx ? ntx : nrx;
   uint64_t tlo = ~0ull, thi = 0;
+  // key | end of RX span j: the scan's running max, or (SIMPLE) the span's own
+  auto end_at = [&](uint64_t j) __attribute__((always_inline)) -> uint64_t {
+    if constexpr (SIMPLE) {
+      const uint64_t key = S.seg ? (uint64_t) qp_seg_of_rx(S, j) << kQpSegShift : 0u;
+      return key | QpRxEnd{mem_size}(rx[j]);
+    } else {
+      return end_max[j];
+    }
+  };
   for (uint64_t k = (uint64_t) blockIdx.x * kQpBlock + threadIdx.x; k < n; k += (uint64_t) gridDim.x * kQpBlock) {
-    if (bounds && k < nrx) {
+    if constexpr (SIMPLE) {
+      if (k < nrx && QpRxEnd{mem_size}(rx[k]) == 0) bounds[4] = gen;  // not the simple form
+    }
+    if (k < nrx && bounds && !S.seg) {
       const uint64_t e = QpRxEnd{mem_size}(rx[k]);
-      if (e != 0 && (k == 0 || end_max[k - 1] == 0)) bounds[2] = rx[k].buffer_address;  // the first span's start
-      if (k + 1 == nrx) bounds[3] = end_max[k];
+      if (e != 0 && (k == 0 || end_at(k - 1) == 0)) bounds[2] = rx[k].buffer_address;  // the first span's start
+      if (k + 1 == nrx) bounds[3] = end_at(k);
     }
     if (k < nrx && k > 0 && QpRxEnd{mem_size}(rx[k]) != 0) {
       const uint64_t key = S.seg ? (uint64_t) qp_seg_of_rx(S, k) << kQpSegShift : 0u;
-      if ((key | rx[k].buffer_address) < end_max[k - 1]) flag[0] = gen;
+      if ((key | rx[k].buffer_address) < end_at(k - 1)) flag[0] = gen;
     }
     if (k < ntx) {
       const uint64_t a = tx[k].buffer_address, len = tx[k].length;
@@ -1613,13 +1630,13 @@ __global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_desc
       const uint64_t ring_end = hi;
       while (lo < hi) {
         const uint64_t mid = lo + (hi - lo) / 2;
-        if (end_max[mid] <= (key | a)) lo = mid + 1;
+        if (end_at(mid) <= (key | a)) lo = mid + 1;
         else hi = mid;
       }
       if (lo < ring_end && rx[lo].buffer_address < a + len) flag[1] = gen;
     }
   }
-  if (!bounds) return;
+  if (!bounds || S.seg) return;
   // the block's TX bounds: wave minimum / maximum, then the block's waves
   for (int o = kWave / 2; o > 0; o >>= 1) {
     const uint64_t l2 = __shfl_xor(tlo, o), h2 = __shfl_xor(thi, o);
@@ -1711,6 +1728,7 @@ struct nicgpu_qp {
   // flags, relax verdict
   uint64_t* hp = nullptr;
   uint64_t* misc() const { return hp + kQpTail; }
+  uint64_t* hp_simple = nullptr;  // page-locked: the simple check's "empty span" flag
   unsigned grid = 1;
   // blocks the partials hold: the grid, or one per segment of the largest table
   unsigned part_blocks() const { return grid > NICGPU_QP_MAX_SEGMENTS ? grid : NICGPU_QP_MAX_SEGMENTS; }
@@ -1720,6 +1738,12 @@ struct nicgpu_qp {
   hipEvent_t checked = nullptr;   // nicgpu_qp_check_async: its flags are on the host
   unsigned long long chk_gen = 0; // ... the generation they are compared with
   bool chk_on = false;            // a check is pending (nicgpu_qp_check_wait not yet called)
+  struct CheckArgs {              // the pending check's, for its scan form
+    uint64_t mem_size = 0, ntx = 0, nrx = 0;
+    bool segmented = false;
+    hipStream_t s = nullptr;
+  } chk_args;
+  uint64_t checks_scanned = 0;    // checks that needed the scan form (an RX span receiving nothing)
   // the resolve between nicgpu_qp_resolve_start and _finish
   struct Pending {
     bool on = false;
@@ -1842,6 +1866,60 @@ int qp_walk(nicgpu_qp* q, const QpCtx& C, const QpSegs& S, uint64_t ntx, unsigne
   return hip_status(hipGetLastError());
 }
 
+// The overlap check's launches on s: (simple) the scan-free kernel, or the
+// running-max scan then the kernel; the flags and the bounds come down into
+// misc() and q->checked is recorded.
+int qp_check_enqueue(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, bool segmented, bool simple,
+                     hipStream_t s, unsigned long long gen) {
+  // the bounds' presets (page-locked source, constant: no hazard with an
+  // earlier copy still reading it)
+  uint64_t* preset = q->misc() + kQpBoundsAt + 4;
+  preset[0] = ~0ull;
+  preset[1] = 0;
+  preset[2] = ~0ull;
+  preset[3] = 0;
+  int st = hip_status(hipMemcpyAsync(q->bounds, preset, 4 * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  if (st != NICGPU_OK) return st;
+  if (!simple && nrx && segmented) {  // per queue pair: ends keyed by segment
+    hipcub::TransformInputIterator<uint64_t, QpRxEndSeg, hipcub::CountingInputIterator<uint64_t>> ends(
+        hipcub::CountingInputIterator<uint64_t>(0), QpRxEndSeg{q->rx, qp_segs(q), mem_size});
+    size_t tb = 0;
+    if (hipcub::DeviceScan::InclusiveScan(nullptr, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s) != hipSuccess)
+      return NICGPU_ERR_HIP;
+    st = qp_grow(q->tmp_chk, q->c_tmp_chk, tb);
+    if (st == NICGPU_OK)
+      st = hip_status(hipcub::DeviceScan::InclusiveScan(q->tmp_chk, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s));
+  } else if (!simple && nrx) {
+    hipcub::TransformInputIterator<uint64_t, QpRxEnd, const nicgpu_rx_descriptor*> ends(q->rx, QpRxEnd{mem_size});
+    size_t tb = 0;
+    if (hipcub::DeviceScan::InclusiveScan(nullptr, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s) != hipSuccess)
+      return NICGPU_ERR_HIP;
+    st = qp_grow(q->tmp_chk, q->c_tmp_chk, tb);
+    if (st == NICGPU_OK)
+      st = hip_status(hipcub::DeviceScan::InclusiveScan(q->tmp_chk, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s));
+  }
+  if (st != NICGPU_OK) return st;
+  const uint64_t n = ntx > nrx ? ntx : nrx;
+  if (n) {
+    const QpSegs S = segmented ? qp_segs(q) : QpSegs{nullptr, nullptr, 0u};
+    if (simple)
+      hipLaunchKernelGGL(qp_check_kernel<true>, dim3(qp_grid(q, n)), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, q->rx,
+                         (uint64_t) nrx, mem_size, q->end_max, q->gflags + 1, gen, S, q->bounds);
+    else
+      hipLaunchKernelGGL(qp_check_kernel<false>, dim3(qp_grid(q, n)), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx,
+                         q->rx, (uint64_t) nrx, mem_size, q->end_max, q->gflags + 1, gen, S, q->bounds);
+    st = hip_status(hipGetLastError());
+  }
+  uint64_t* f = q->misc() + 1;
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(f, q->gflags + 1, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK)
+    st = hip_status(hipMemcpyAsync(q->misc() + kQpBoundsAt, q->bounds, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK)
+    st = hip_status(hipMemcpyAsync(&q->hp_simple[0], q->bounds + 4, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  if (st == NICGPU_OK) st = hip_status(hipEventRecord(q->checked, s));
+  return st;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1873,16 +1951,18 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
       hipMalloc(&q->dlv_done, sizeof(unsigned int)) != hipSuccess ||
       hipMemset(q->dlv_done, 0, sizeof(unsigned int)) != hipSuccess ||
       hipMalloc(&q->gflags, 6 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc(&q->bounds, 4 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&q->bounds, 8 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(q->bounds, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(q->gflags, 0, 6 * sizeof(unsigned long long)) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
   }
-  if (hipHostMalloc(reinterpret_cast<void**>(&q->hp), (kQpTail + 16) * sizeof(uint64_t)) !=
-      hipSuccess) {
+  if (hipHostMalloc(reinterpret_cast<void**>(&q->hp), (kQpTail + 16) * sizeof(uint64_t)) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&q->hp_simple), 8 * sizeof(uint64_t)) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
   }
+  std::memset(q->hp_simple, 0, 8 * sizeof(uint64_t));  // no generation is 0
   if (hipEventCreateWithFlags(&q->planned, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&q->resolved, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&q->checked, hipEventDisableTiming) != hipSuccess) {
@@ -1904,6 +1984,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
   for (void* b : bufs)
     if (b) (void) hipFree(b);
   if (q->hp) (void) hipHostFree(q->hp);
+  if (q->hp_simple) (void) hipHostFree(q->hp_simple);
   if (q->seg_hp) (void) hipHostFree(q->seg_hp);
   if (q->seg_stage) (void) hipHostFree(q->seg_stage);
   if (q->planned) (void) hipEventDestroy(q->planned);
@@ -2081,8 +2162,17 @@ int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict) {
   if (!q || !verdict || !q->chk_on) return NICGPU_ERR_INVALID;
   q->chk_on = false;
   DeviceGuard g(q->device);
-  const int st = hip_status(hipEventSynchronize(q->checked));
+  int st = hip_status(hipEventSynchronize(q->checked));
   if (st != NICGPU_OK) return st;
+  if (q->hp_simple[0] == q->chk_gen) {  // a span that receives nothing: the scan form
+    const nicgpu_qp::CheckArgs& A = q->chk_args;
+    const unsigned long long gen = ++q->gen;
+    st = qp_check_enqueue(q, A.mem_size, A.ntx, A.nrx, A.segmented, false, A.s, gen);
+    if (st == NICGPU_OK) st = hip_status(hipEventSynchronize(q->checked));
+    if (st != NICGPU_OK) return st;
+    q->chk_gen = gen;
+    ++q->checks_scanned;
+  }
   const uint64_t* f = q->misc() + 1;
   *verdict = f[0] == q->chk_gen ? -1 : (f[1] == q->chk_gen ? 0 : 1);
   return NICGPU_OK;
@@ -2097,52 +2187,15 @@ int nicgpu_qp_check_async(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nr
     if (hipEventSynchronize(q->checked) != hipSuccess) return NICGPU_ERR_HIP;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const unsigned long long gen = ++q->gen;
-  int st = NICGPU_OK;
   if (segmented && (ntx != q->seg_ntx || nrx != q->seg_nrx)) return NICGPU_ERR_INVALID;
-  // the bounds' presets (page-locked source, constant: no hazard with an
-  // earlier copy still reading it)
-  uint64_t* preset = q->misc() + kQpBoundsAt + 4;
-  preset[0] = ~0ull;
-  preset[1] = 0;
-  preset[2] = ~0ull;
-  preset[3] = 0;
-  st = hip_status(hipMemcpyAsync(q->bounds, preset, 4 * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  if (st != NICGPU_OK) return st;
-  if (nrx && segmented) {  // per queue pair: ends keyed by segment
-    hipcub::TransformInputIterator<uint64_t, QpRxEndSeg, hipcub::CountingInputIterator<uint64_t>> ends(
-        hipcub::CountingInputIterator<uint64_t>(0), QpRxEndSeg{q->rx, qp_segs(q), mem_size});
-    size_t tb = 0;
-    if (hipcub::DeviceScan::InclusiveScan(nullptr, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s) != hipSuccess)
-      return NICGPU_ERR_HIP;
-    st = qp_grow(q->tmp_chk, q->c_tmp_chk, tb);
-    if (st == NICGPU_OK)
-      st = hip_status(hipcub::DeviceScan::InclusiveScan(q->tmp_chk, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s));
-  } else if (nrx) {
-    hipcub::TransformInputIterator<uint64_t, QpRxEnd, const nicgpu_rx_descriptor*> ends(q->rx, QpRxEnd{mem_size});
-    size_t tb = 0;
-    if (hipcub::DeviceScan::InclusiveScan(nullptr, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s) != hipSuccess)
-      return NICGPU_ERR_HIP;
-    st = qp_grow(q->tmp_chk, q->c_tmp_chk, tb);
-    if (st == NICGPU_OK)
-      st = hip_status(hipcub::DeviceScan::InclusiveScan(q->tmp_chk, tb, ends, q->end_max, hipcub::Max(), (int) nrx, s));
-  }
-  if (st != NICGPU_OK) return st;
-  const uint64_t n = ntx > nrx ? ntx : nrx;
-  if (n) {
-    hipLaunchKernelGGL(qp_check_kernel, dim3(qp_grid(q, n)), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, q->rx,
-                       (uint64_t) nrx, mem_size, q->end_max, q->gflags + 1, gen,
-                       segmented ? qp_segs(q) : QpSegs{nullptr, nullptr, 0u}, q->nseg ? nullptr : q->bounds);
-    st = hip_status(hipGetLastError());
-  }
-  uint64_t* f = q->misc() + 1;
-  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(f, q->gflags + 1, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  if (st == NICGPU_OK)
-    st = hip_status(hipMemcpyAsync(q->misc() + kQpBoundsAt, q->bounds, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  if (st == NICGPU_OK) st = hip_status(hipEventRecord(q->checked, s));
+  const unsigned long long gen = ++q->gen;
+  // the simple form first (no scan: every RX span nonempty); a ring with an
+  // empty span makes nicgpu_qp_check_wait run the scan form behind it
+  const int st = qp_check_enqueue(q, mem_size, ntx, nrx, segmented, true, s, gen);
   if (st != NICGPU_OK) return st;
   q->chk_gen = gen;
   q->chk_on = true;
+  q->chk_args = nicgpu_qp::CheckArgs{mem_size, (uint64_t) ntx, (uint64_t) nrx, segmented, s};
   return NICGPU_OK;
 }
 
