@@ -233,6 +233,15 @@ struct BatchedQueuePairConfig {
   /// beside it, so the overlap gains nothing at the default CU reserve and
   /// ≈ 4 % with 96 CUs kept free of delivery blocks.
   bool overlap_resolve{false};
+  /// Device path: a batch in which no decision that moves ring positions reads
+  /// a checksum (no TX verify, queue_pair.cpp:94-105; one segment per packet)
+  /// skips its piece-sum pass over the TX frames; its RX verifies
+  /// (:434-447) are made by the delivery from the bytes it writes — the bytes
+  /// that verify covers — which patches any that fail into the reference's
+  /// ChecksumError completion, and the statistics are corrected when the batch
+  /// completes (nicgpu_qp_set_deferred_verify).  Results are the same either
+  /// way (tests/cpp/rx_stage_gpu_fuzz.cpp).  NIC_DEFER_VERIFY=0 turns it off.
+  bool defer_rx_verify{true};
 };
 
 struct RxBatchResult {
@@ -276,6 +285,7 @@ struct RxBatchResult {
     bool walked{false};     // ... positions made by the walk (8 relaxation steps did not settle them)
     bool overlapped{false};  // submit/collect: sums and resolve ran beside the earlier batches' DMA writes
     bool overlap_redone{false};  // ... but the frames lie where those write: redone after them
+    bool deferred{false};   // RX verifies made by the delivery (BatchedQueuePairConfig::defer_rx_verify)
     bool host_image{false};  // run against a HostMemory: TX bytes staged up, delivered bytes written back
     bool staged_whole{false};  // ... the TX bytes' span went up in one copy (dense), else per descriptor
     unsigned replans{0};    // device plans redone because the first outgrew the piece buffers (at most 1)
@@ -413,7 +423,7 @@ private:
   void back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult& out, void* stream);
   void deliver(Slot& sl, const DeviceHostMemory& mem, std::size_t a, std::size_t b, unsigned flags,
                const nicgpu_rss_ctx* rctx, std::uint64_t* hits, void* stream);
-  void finish(Slot& sl, RxBatchResult& out);
+  void finish(Slot& sl, RxBatchResult& out, QueuePairStats* st);
   void enqueue(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                const DeviceDescriptors* d, void* stream, HostImage* img = nullptr);
   void check_rings_unwritten(Slot& sl, const DeviceHostMemory& mem, void* stream);

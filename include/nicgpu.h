@@ -391,7 +391,7 @@ int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict);
 int nicgpu_qp_check_bounds(const nicgpu_qp* q, uint64_t* bounds);
 /* The piece sums of q's current plan again (nicgpu_qp_plan_async's sums), on
  * `stream`: for frames an earlier batch's DMA writes changed after the first
- * sums read them. */
+ * sums read them, or for a batch that skipped them (deferred RX verify). */
 int nicgpu_qp_resum(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, void* stream);
 /* The kernels of the next plan/check/resolve read the caller's device arrays
  * tx[0, ntx) and rx[0, nrx) in place of view.tx / view.rx (no copy; view is
@@ -468,6 +468,32 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
                              nicgpu_qp_stats* stats);
 /* The resolves of q whose positions the walk made, since q was created. */
 int nicgpu_qp_walks(const nicgpu_qp* q, uint64_t* walks);
+/* Deferred RX verify (off by default).  With it on, a batch planned by
+ * nicgpu_qp_plan_async in which no decision that moves ring positions reads a
+ * sum — no TX descriptor needs the TX verify (queue_pair.cpp:94-105) and none
+ * makes more than one segment — skips its piece sums: the resolve takes every
+ * RX verify (:434-447) to pass, and the delivery (nicgpu_qp_deliver_range)
+ * sums the bytes each such completion's write delivers, which are exactly the
+ * bytes that verify covers.  A completion whose sum fails gets the
+ * reference's ChecksumError completion there (status, no VLAN strip), RSS
+ * skips it, and the counts the resolve's statistics took for it as delivered
+ * are accumulated on the device for the caller to correct
+ * (nicgpu_qp_verify_fixups_async).  Completions and statistics of such a
+ * batch are therefore final only after its deliveries; nicgpu_qp_deferred
+ * tells, after nicgpu_qp_resolve_finish, whether the last batch deferred.
+ * Its host-resolved rest (*done < ntx) needs nicgpu_qp_resum first: the
+ * piece sums were skipped.  Unsegmented batches only; the synchronous
+ * nicgpu_qp_plan / _plan_on always sum. */
+int nicgpu_qp_set_deferred_verify(nicgpu_qp* q, int on);
+int nicgpu_qp_deferred(const nicgpu_qp* q, int* deferred);
+/* The deferred verifies' running corrections of q since it was created, on
+ * `stream` into out[NICGPU_QP_FIXUPS]: [0] verifies that failed (each a
+ * drops_checksum the statistics lack and an rx_packets and tx_packets they
+ * hold too many), then what they hold too many of: [1] rx_bytes, [2]
+ * rx_vlan_strips, [3] tx_bytes, [4] tx_vlan_insertions.  A caller keeps the
+ * last values and applies the difference. */
+#define NICGPU_QP_FIXUPS 5u
+int nicgpu_qp_verify_fixups_async(nicgpu_qp* q, uint64_t* out, void* stream);
 /* The frames of view.rxc[0, nrx) delivered with Success, as RSS descriptors
  * (view.rss_desc[0, m), lengths clipped to NICGPU_MAX_PACKET), m written to
  * the device scalar view.rss_count; view.rx_hash / rx_queue reset to 0 /

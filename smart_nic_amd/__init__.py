@@ -112,6 +112,9 @@ ABI_SYMBOLS = (
     "nicgpu_qp_check_wait",
     "nicgpu_qp_check_bounds",
     "nicgpu_qp_resum",
+    "nicgpu_qp_set_deferred_verify",
+    "nicgpu_qp_deferred",
+    "nicgpu_qp_verify_fixups_async",
     "nicgpu_event_synchronize",
     "nicgpu_host_register",
     "nicgpu_host_unregister",
@@ -198,6 +201,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_qp_check_wait": (i32, [vp, vp]),
         "nicgpu_qp_check_bounds": (i32, [vp, vp]),
         "nicgpu_qp_resum": (i32, [vp, vp, ctypes.c_uint64, vp]),
+        "nicgpu_qp_set_deferred_verify": (i32, [vp, i32]),
+        "nicgpu_qp_deferred": (i32, [vp, vp]),
+        "nicgpu_qp_verify_fixups_async": (i32, [vp, vp, vp]),
         "nicgpu_event_synchronize": (i32, [vp]),
         "nicgpu_host_register": (i32, [vp, sz, ctypes.POINTER(vp), ctypes.POINTER(i32)]),
         "nicgpu_host_unregister": (i32, [vp]),

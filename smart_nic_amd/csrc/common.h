@@ -151,7 +151,6 @@ struct RxParams {
   uint32_t xcd_w_odd;   // SPLIT kernels: share of an odd blockIdx % 8 group relative to an even one (65536 = 1)
   unsigned long long* hits_rep;  // per-context histogram replicas (flush_hist), or null
   unsigned int* hits_done;       // their done ticket
-  unsigned int* xcd_tickets;     // SPLIT 2 kernels (tuning): 8 per-XCD ticket counters, zero at launch
 };
 
 // s_waitcnt immediate for vmcnt(0) alone (gfx9 encoding: expcnt 7, lgkmcnt 15).

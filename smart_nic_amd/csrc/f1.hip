@@ -139,7 +139,7 @@ struct DeliverParams {
   uint8_t* mem;
   uint64_t mem_size;
   const nicgpu_segment_write* w;
-  const nicgpu_completion* rxc;  // statuses (RSS of Success completions)
+  nicgpu_completion* rxc;  // statuses (RSS of Success completions; a deferred verify's failure patched)
   uint64_t j0, n;                // completions [j0, n) ...
   const unsigned long long* n_dev;  // ... with n lowered to *n_dev (a speculative resolve's settled prefix)
   RxParams rss;                  // mode NICGPU_TUPLE_NONE: no RSS
@@ -155,6 +155,15 @@ struct DeliverParams {
   unsigned int* done;
   uint32_t add_count, add_hits;  // the last block adds (1) or stores (0)
   uint64_t alt_dst;  // tuning (kDlvPackedDst): destination = src_a + alt_dst
+  // deferred RX verify (nicgpu_qp_set_deferred_verify; the LATE kernels): the
+  // batch deferred when *lateflag != late_gen; completion j < late_n with
+  // late[j] & kLateDeferred is verified here from the bytes its write
+  // delivers; fix: the running corrections (nicgpu_qp_verify_fixups_async)
+  const uint8_t* late;
+  const unsigned long long* lateflag;
+  unsigned long long late_gen;
+  uint64_t late_n;
+  unsigned long long* fix;
 };
 
 // Tuning-only modes of deliver_kernel (libnicgpu_tune.so, tools/f1_deliver_bench.py;
@@ -325,15 +334,36 @@ struct DlvStep {
   u32x4 v[kDlvU];      // the source window (window items)
 };
 
-// marks | windows | metas; the RSS header stage takes the windows' place at
-// the tile end, once every lane holds its own three (it is no larger)
-template <bool WIDE>
+// marks | windows | metas (| LATE: the tile's 64 frame sums); the RSS header
+// stage takes the windows' place at the tile end, once every lane holds its
+// own three (it is no larger)
+template <bool WIDE, bool LATE = false>
 __host__ __device__ constexpr uint32_t dlv_wave_bytes() {
   static_assert(192u * sizeof(DlvWin<WIDE>) >= 64u * kHdrStride * 16u, "stage fits the windows");
-  return kDlvMarks + 192u * (uint32_t) sizeof(DlvWin<WIDE>) + 192u * 4u;
+  return kDlvMarks + 192u * (uint32_t) sizeof(DlvWin<WIDE>) + 192u * 4u + (LATE ? 64u * 4u : 0u);
 }
 
-template <bool RSS, int MODE, bool WIDE>
+// (LATE) The halfword sum, at absolute byte parities, of bytes [x0, x1) of a
+// 16-B window at destination address W: bytes kept, each dword rotated by a
+// byte when W is odd (so every byte lands in the half its address parity
+// gives), halves added — the RX kernel's convention, under which a frame's
+// sums compose whatever its alignment.
+__device__ __forceinline__ uint32_t dlv_window_sum(u32x4 v, uint32_t x0, uint32_t x1, uint32_t odd) {
+  if (x0 != 0u || x1 != 16u) {
+    v.x &= dword_keep((int) x0, (int) x1, 0);
+    v.y &= dword_keep((int) x0, (int) x1, 1);
+    v.z &= dword_keep((int) x0, (int) x1, 2);
+    v.w &= dword_keep((int) x0, (int) x1, 3);
+  }
+  const uint32_t r = odd ? 8u : 0u;
+  v.x = __builtin_amdgcn_alignbit(v.x, v.x, r);
+  v.y = __builtin_amdgcn_alignbit(v.y, v.y, r);
+  v.z = __builtin_amdgcn_alignbit(v.z, v.z, r);
+  v.w = __builtin_amdgcn_alignbit(v.w, v.w, r);
+  return add_halves(v.w, add_halves(v.z, add_halves(v.y, add_halves(v.x, 0u))));
+}
+
+template <bool RSS, int MODE, bool WIDE, bool LATE>
 __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   typedef typename DlvOff<WIDE>::T Off;
   typedef DlvWin<WIDE> Win;
@@ -353,10 +383,11 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   const uint32_t block_bytes = dlv_block_bytes(RSS, R.lut_words, hist_lds ? R.table_n : 0u,
                                                table_lds ? (R.table_n + 1u) / 2u : 0u);
   uint32_t* cnt_s = reinterpret_cast<uint32_t*>(base_b + block_bytes - 16u);
-  uint8_t* wave_b = base_b + block_bytes + w * dlv_wave_bytes<WIDE>();
+  uint8_t* wave_b = base_b + block_bytes + w * dlv_wave_bytes<WIDE, LATE>();
   uint8_t* marks = wave_b;
   Win* wins = reinterpret_cast<Win*>(wave_b + kDlvMarks);
   uint32_t* metas = reinterpret_cast<uint32_t*>(wins + 192);
+  uint32_t* sumc = metas + 192;  // (LATE) per frame of the tile: its running sum
   uint4* stage = reinterpret_cast<uint4*>(wins);  // at the tile end
   if (RSS) {
     for (uint32_t i = threadIdx.x; i < R.lut_words; i += kThreads) lut[i] = R.lut[i];
@@ -388,6 +419,8 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
   const __amdgpu_buffer_rsrc_t mrs =
       __builtin_amdgcn_make_buffer_rsrc(P.mem, (short) 0, (int) (uint32_t) (WIDE ? 0u : msize), 0x00020000);
   uint32_t my_count = 0;
+  // the batch deferred its RX verifies (wave-uniform)
+  const bool lateb = LATE && *P.lateflag != P.late_gen;
   for (uint64_t tile = (uint64_t) blockIdx.x * kDlvWpb + w; tile < ntiles; tile += nwaves) {
     // ---- this lane's write: its items and their stream entries
     const uint64_t j = P.j0 + tile * kWave + lane;
@@ -431,6 +464,7 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
       put(0, wr.dst, wr.prefix, plen, F);
       put(1, d1, wr.src_a, wr.len_a, F + c0);
       put(2, d2, wr.src_b, wr.len_b, F + c0 + c1);
+      if (LATE && lateb) sumc[lane] = 0u;
     }
     uint32_t carry = 0;  // item (id + 1) of the entry before the step being planned
     // ---- load phase of the step at stream position W
@@ -458,6 +492,12 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
         const Off Wn = D < I.lo ? I.lo : (D > I.hi ? I.hi : D);
         S.D[u] = win ? Wn : D;
         S.pk[u] = id | ((uint32_t) win << 8) | ((uint32_t) valid << 9);
+        if constexpr (LATE) {  // the chunk's own bytes within the window: [x0, x1)
+          const Off e = I.hi + (Off) 16u;
+          const Off a = D < I.lo ? I.lo : D;
+          const Off b = D + (Off) 16u > e ? e : D + (Off) 16u;
+          S.pk[u] |= ((uint32_t) (a - Wn) << 10) | ((uint32_t) (b - Wn) << 15);
+        }
         if constexpr ((MODE & kDlvNoLoad) != 0) {
           S.v[u] = (u32x4){(uint32_t) D, 1u, 2u, 3u};
         } else if constexpr (kBuf) {
@@ -474,9 +514,15 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
     // ---- store phase
     auto store = [&](const DlvStep<WIDE>& S) __attribute__((always_inline)) {
       bool slow = false;
+      uint32_t su[kDlvU];  // (LATE) each entry's sum
 #pragma unroll
       for (int u = 0; u < kDlvU; ++u) {
         const uint32_t pk = S.pk[u];
+        if constexpr (LATE) {
+          su[u] = 0u;
+          if (lateb && (pk & 256u))
+            su[u] = dlv_window_sum(S.v[u], (pk >> 10) & 31u, (pk >> 15) & 31u, (uint32_t) S.D[u] & 1u);
+        }
         if constexpr ((MODE & kDlvNoStore) != 0) {
           if ((pk & 256u) && (S.v[u].x ^ S.v[u].w) == 0x12345678u) P.mem[S.D[u]] = 0;  // keeps the loads
         } else if constexpr (kBuf) {
@@ -526,7 +572,27 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
               o[3] |= (b >> 2) == 3u ? z : 0u;
             }
           }
+          if constexpr (LATE) su[u] = add_halves(o[3], add_halves(o[2], add_halves(o[1], add_halves(o[0], 0u))));
           if constexpr ((MODE & kDlvNoStore) == 0) dlv_store_partial(P.mem, (uint64_t) D, x, y, o);
+        }
+      }
+      if constexpr (LATE) {
+        if (lateb) {
+          // each frame's entries are consecutive in the stream: a scan of the
+          // step's sums, the frame's last entry in the step adding its prefix
+          // and its first one taking away the prefix before it (one LDS add
+          // per frame and step)
+#pragma unroll
+          for (int u = 0; u < kDlvU; ++u) {
+            const uint32_t pk = S.pk[u];
+            const bool valid = (pk & 512u) != 0u;
+            const uint32_t q = valid ? (pk & 255u) / 3u : 0xFFu;
+            const uint32_t incl = wave_incl_scan(su[u]);
+            const uint32_t qp = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) q, 0x138, 0xf, 0xf, false);  // wave_shr:1
+            const uint32_t qn = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) q, 0x130, 0xf, 0xf, false);  // wave_shl:1
+            const bool first = lane == 0u || qp != q, last = lane == 63u || qn != q;
+            if (valid && (first || last)) atomicAdd(&sumc[q], (last ? incl : 0u) - (first ? incl - su[u] : 0u));
+          }
         }
       }
     };
@@ -554,6 +620,35 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
       }
       if (s < nsteps) store(A);
       if (s + 1 < nsteps) store(B);
+    }
+    if (LATE && lateb) {
+      // the deferred verifies (queue_pair.cpp:434-447) of the tile's frames
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const uint32_t sum = sumc[lane];
+      if (j < n && j < P.late_n) {
+        const uint32_t lb = P.late[j];
+        if (lb & nicqp::kLateDeferred) {
+          nicgpu_completion e = P.rxc[j];
+          if (e.status == nicqp::kSuccess && fold16(sum) != 0xFFFFu) {
+            // the reference's ChecksumError completion (no VLAN strip) and
+            // what the resolve counted for it as delivered
+            const Win I0 = wins[lane * 3u], I1 = wins[lane * 3u + 1u], I2 = wins[lane * 3u + 2u];
+            const uint64_t len_a = (uint32_t) (I1.hi + 16u - I1.lo), len_b = (uint32_t) (I2.hi + 16u - I2.lo);
+            const uint64_t size = (uint64_t) (uint32_t) (I0.hi + 16u - I0.lo) + len_a + len_b;
+            atomicAdd(&P.fix[0], 1ull);
+            atomicAdd(&P.fix[1], (unsigned long long) size);
+            if (e.vlan_stripped) atomicAdd(&P.fix[2], 1ull);
+            atomicAdd(&P.fix[3], (unsigned long long) (len_a + len_b + ((lb & nicqp::kLateStripBase) ? 4u : 0u)));
+            if (lb & nicqp::kLateVlanInsert) atomicAdd(&P.fix[4], 1ull);
+            e.status = nicqp::kChecksumError;
+            e.vlan_stripped = false;
+            e.vlan_tag = 0;
+            P.rxc[j] = e;
+            flag = false;
+          }
+        }
+      }
     }
     if (kHash) {
       // every lane reads its items before the stage overwrites them
@@ -637,9 +732,9 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
 #endif
 // waves per SIMD the delivery is compiled for (tuning: 6, 80 VGPRs, which
 // its LDS allows, spills the RSS variant and measured slower)
-template <bool RSS, int MODE = 0, bool WIDE = false>
+template <bool RSS, int MODE = 0, bool WIDE = false, bool LATE = false>
 __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu(NICGPU_DLV_OCC, 8))) void deliver_kernel(DeliverParams P) {
-  deliver_tiles<RSS, MODE, WIDE>(P);
+  deliver_tiles<RSS, MODE, WIDE, LATE>(P);
 }
 
 #ifdef NICGPU_TUNING
@@ -881,9 +976,9 @@ __global__ __launch_bounds__(kWave * kDlvWpb) __attribute__((amdgpu_waves_per_eu
 }
 #endif  // NICGPU_TUNING
 
-template <bool RSS>
+template <bool RSS, bool LATE = false>
 int dlv_blocks_per_cu(uint32_t lds) {
-  return blocks_per_cu(reinterpret_cast<const void*>(deliver_kernel<RSS>), kWave * kDlvWpb, lds);
+  return blocks_per_cu(reinterpret_cast<const void*>(deliver_kernel<RSS, 0, false, LATE>), kWave * kDlvWpb, lds);
 }
 
 template <int MODE>
@@ -891,9 +986,13 @@ int launch_deliver(const DeliverParams& P, bool rss, int cus_total, hipStream_t 
   const uint32_t hist_n = (rss && P.rss.table_n <= (uint32_t) kHistLds) ? P.rss.table_n : 0u;
   const uint32_t table_words = (rss && P.rss.table_n <= (uint32_t) kTableLds) ? (P.rss.table_n + 1u) / 2u : 0u;
   const bool wide = P.mem_size > 0xFFFFFFF0ull;  // 32-bit offsets for images below 4 GiB
-  const uint32_t wave_bytes = (MODE & kDlvV1) ? kDlvWaveBytes : (wide ? dlv_wave_bytes<true>() : dlv_wave_bytes<false>());
+  const bool late = MODE == 0 && P.late != nullptr;
+  const uint32_t wave_bytes = (MODE & kDlvV1) ? kDlvWaveBytes
+                              : late ? (wide ? dlv_wave_bytes<true, true>() : dlv_wave_bytes<false, true>())
+                                     : (wide ? dlv_wave_bytes<true>() : dlv_wave_bytes<false>());
   const uint32_t lds = dlv_block_bytes(rss, P.rss.lut_words, hist_n, table_words) + kDlvWpb * wave_bytes;
-  const int bpc = rss ? dlv_blocks_per_cu<true>(lds) : dlv_blocks_per_cu<false>(lds);
+  const int bpc = late ? (rss ? dlv_blocks_per_cu<true, true>(lds) : dlv_blocks_per_cu<false, true>(lds))
+                       : (rss ? dlv_blocks_per_cu<true>(lds) : dlv_blocks_per_cu<false>(lds));
   const uint64_t ntiles = (P.n - P.j0 + kWave - 1) / kWave;
   const uint64_t want = (ntiles + kDlvWpb - 1) / kDlvWpb;
   // CUs left without a delivery block, so the next batch's plan and check
@@ -912,6 +1011,15 @@ int launch_deliver(const DeliverParams& P, bool rss, int cus_total, hipStream_t 
     return hip_status(hipGetLastError());
   }
 #endif
+  if constexpr (MODE == 0) {
+    if (late) {
+      if (rss && !wide) hipLaunchKernelGGL((deliver_kernel<true, 0, false, true>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+      else if (rss) hipLaunchKernelGGL((deliver_kernel<true, 0, true, true>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+      else if (!wide) hipLaunchKernelGGL((deliver_kernel<false, 0, false, true>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+      else hipLaunchKernelGGL((deliver_kernel<false, 0, true, true>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
+      return hip_status(hipGetLastError());
+    }
+  }
   if (rss && !wide) hipLaunchKernelGGL((deliver_kernel<true, MODE, false>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
   else if (rss) hipLaunchKernelGGL((deliver_kernel<true, MODE, true>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
   else if (!wide) hipLaunchKernelGGL((deliver_kernel<false, MODE, false>), dim3(grid), dim3(kWave * kDlvWpb), lds, s, P);
@@ -970,7 +1078,7 @@ constexpr unsigned kQpBlock = 256;
 constexpr unsigned kQpStats = 16;
 // after the per-block stats: RX used, first mismatch, settled prefix, then the
 // batch's 16 stats totals — the one download a resolve needs
-constexpr unsigned kQpTail = 3 + 16 + 2;  // ... then [19] the plan overflowed (1 buffers, 2 pieces per descriptor), [20] its piece count
+constexpr unsigned kQpTail = 3 + 16 + 3;  // ... then [19] the plan overflowed (1 buffers, 2 pieces per descriptor), [20] its piece count, [21] RX verify deferred
 constexpr int kQpRelaxSteps = 8;  // position relaxations before the host takes the rest
 constexpr unsigned kQpBoundsAt = 8;  // misc()[8..11]: the check's bounds, [12..15] their presets
 
@@ -1034,8 +1142,15 @@ struct QpDevSink {
   nicgpu_completion* rxc;
   nicgpu_segment_write* w;
   uint64_t ti, rj;
+  uint8_t* late;  // a deferred-verify batch: every completion's bits (0: final)
+  uint64_t keep;  // completions [0, keep) are already delivered: not rewritten (a deferred verify may have patched them)
   __device__ void tx(const nicgpu_completion& e, bool) { txc[ti] = e; }
-  __device__ void rx(const nicgpu_completion& e, const nicgpu_segment_write* sw) {
+  __device__ void rx(const nicgpu_completion& e, const nicgpu_segment_write* sw) { rx_late(e, sw, 0u); }
+  __device__ void rx_late(const nicgpu_completion& e, const nicgpu_segment_write* sw, uint32_t bits) {
+    if (rj < keep) {
+      ++rj;
+      return;
+    }
     rxc[rj] = e;
     if (sw) {
       w[rj] = *sw;
@@ -1043,6 +1158,7 @@ struct QpDevSink {
       nicgpu_segment_write z{};
       w[rj] = z;
     }
+    if (late) late[rj] = (uint8_t) bits;
     ++rj;
   }
 };
@@ -1052,25 +1168,40 @@ struct QpDevSink {
 // reset before the launch), so the 32-bit scan of the counts (n <= 2^32 /
 // kQpMaxPieces) cannot wrap and the caller sees the flag.
 constexpr uint32_t kQpMaxPieces = 256;
+// Also whether the batch may defer its RX verifies (defer, unsegmented): g[7]
+// becomes the generation when it may not — a packet with a TX verify or more
+// than one segment, whose pops a sum can change (qp_logic.h Ctx::late).
 __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
                                                             uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
-                                                            uint32_t* counts, unsigned long long* ovf,
-                                                            unsigned long long gen, QpSegs S) {
+                                                            uint32_t* counts, unsigned long long* g,
+                                                            unsigned long long gen, QpSegs S, uint32_t defer) {
   const QpRange R = qp_range(S, n);
   const uint64_t mtu = qp_max_mtu(max_mtu, S, R.s);
+  const bool may = defer != 0u && !S.seg;
+  bool needs = false;
   for (uint64_t i = R.i; i < R.end; i += R.step) {
     QpPlan pp;
-    const uint32_t c =
-        nicqp::plan_packet(mtu, mem_size, nicqp::desc_load(tx + i), pp, [](uint64_t, uint64_t) {}, /*split4=*/true);
+    const nicgpu_tx_descriptor t = nicqp::desc_load(tx + i);
+    const uint32_t c = nicqp::plan_packet(mtu, mem_size, t, pp, [](uint64_t, uint64_t) {}, /*split4=*/true);
     counts[i] = c <= kQpMaxPieces ? c : 0u;
-    if (c > kQpMaxPieces) *ovf = gen;
+    if (c > kQpMaxPieces) g[0] = gen;
     plans[i] = pp;
+    if (may) needs = needs || nicqp::tx_verify_needed(t) || nicqp::decide_segments(t).nseg > 1u;
+  }
+  if (!may) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) g[7] = gen;
+  } else if (__ballot(needs) != 0ull && lane_id() == 0u) {
+    g[7] = gen;
   }
 }
 
+// the batch defers its RX verifies (after its count kernel)
+__device__ __forceinline__ bool qp_late(const unsigned long long* g, unsigned long long gen) { return g[7] != gen; }
+
 // Piece descriptors below `cap` only; the first thread leaves the piece count
-// in g[5], the count the sums run over, min(count, cap), in g[4], and the
-// generation in g[3] when the plan does not fit (nicgpu_qp_plan_async).
+// in g[5], min(count, cap) in g[6], the count the sums run over in g[4] (that,
+// or 0 when the batch defers its RX verifies), and the generation in g[3]
+// when the plan does not fit (nicgpu_qp_plan_async).
 __global__ __launch_bounds__(kQpBlock) void qp_fill_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
                                                            uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
                                                            const uint32_t* __restrict__ base, uint64_t* desc,
@@ -1079,7 +1210,8 @@ __global__ __launch_bounds__(kQpBlock) void qp_fill_kernel(const nicgpu_tx_descr
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     const uint64_t np = base[n];
     g[5] = np;
-    g[4] = np < cap ? np : cap;
+    g[6] = np < cap ? np : cap;
+    g[4] = qp_late(g, gen) ? 0u : g[6];  // a deferred-verify batch reads no piece sum
     if (np > cap) g[3] = gen;
   }
   const QpRange R = qp_range(S, n);
@@ -1197,7 +1329,8 @@ __global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32
                                                            nicgpu_completion* txc, nicgpu_completion* rxc,
                                                            nicgpu_segment_write* writes, uint64_t* partials,
                                                            const uint32_t* __restrict__ guess, const unsigned long long* g,
-                                                           unsigned long long gen, QpSegs S) {
+                                                           unsigned long long gen, QpSegs S, uint8_t* late,
+                                                           uint64_t keep) {
   __shared__ uint64_t red[kQpStats][kQpBlock / kWave];
   // after the per-block stats: [0] the RX descriptors used (pos[lim]), [1] the
   // first mismatch (seeded with n by qp_need_kernel) — one download for all
@@ -1207,14 +1340,15 @@ __global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32
   nicgpu_qp_stats st{};
   if (qp_plan_bad(g, gen)) lim = 0;
   const QpRange R = qp_range(S, lim);
-  const QpCtx Cs = qp_ctx_of(C, S, R.s);
+  QpCtx Cs = qp_ctx_of(C, S, R.s);
+  Cs.late = qp_late(g, gen);
   for (uint64_t i = R.i; i < R.end; i += R.step) {
     const uint64_t p = qp_abs(pos, S, R.s, i);
     if (p > Cs.nrx) {  // exact positions never pass the ring's end: a guess past it is wrong
       if (guess) atomicMin(first, (unsigned long long) i);
       continue;
     }
-    QpDevSink sink{txc, rxc, writes, i, p};
+    QpDevSink sink{txc, rxc, writes, i, p, Cs.late ? late : nullptr, keep};
     const uint32_t popped = (uint32_t) nicqp::resolve_packet<nicgpu_completion, nicgpu_segment_write>(Cs, i, p, st, sink);
     if (guess && popped != guess[i]) atomicMin(first, (unsigned long long) i);
   }
@@ -1267,6 +1401,7 @@ __global__ __launch_bounds__(kQpReduceThreads) void qp_reduce_kernel(const uint6
     }
     tail[19] = g[0] == gen ? 2u : (g[3] == gen ? 1u : 0u);
     tail[20] = g[5];
+    tail[21] = qp_late(g, gen) ? 1u : 0u;
   }
 }
 
@@ -1717,8 +1852,19 @@ struct nicgpu_qp {
   unsigned int* dlv_done = nullptr;       // its done ticket
   // zeroed once; flags are set to a call's generation: [0] a descriptor plans
   // > 256 pieces, [1..2] the check's, [3] the plan does not fit; then the
-  // device piece counts [4] min(count, capacity), [5] count
+  // device piece counts [4] the sums' (below), [5] count, [6] min(count,
+  // capacity); [7] the plan's batch may not defer its RX verifies
   unsigned long long* gflags = nullptr;
+  // deferred RX verify (nicgpu_qp_set_deferred_verify): per RX completion its
+  // bits (qp_logic.h kLate*), the delivery's running corrections [5] (failed
+  // verifies, then the rx bytes, rx VLAN strips, tx bytes and tx VLAN
+  // insertions they had counted), whether the last resolved batch deferred,
+  // and the RX completions its device resolve made (the rest: the host's)
+  uint8_t* late = nullptr;
+  size_t c_late = 0;
+  unsigned long long* fix = nullptr;
+  bool defer_verify = false, late_batch = false;
+  uint64_t late_used = 0;
   unsigned long long gen = 0;             // generation of the last plan / check call
   uint8_t* tmp = nullptr;
   uint64_t host_scal[4] = {0, 0, 0, 0};
@@ -1950,10 +2096,12 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
       hipMalloc(&q->queue_end, 65536 * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&q->dlv_done, sizeof(unsigned int)) != hipSuccess ||
       hipMemset(q->dlv_done, 0, sizeof(unsigned int)) != hipSuccess ||
-      hipMalloc(&q->gflags, 6 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&q->gflags, 8 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&q->fix, 8 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(q->fix, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&q->bounds, 8 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(q->bounds, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(q->gflags, 0, 6 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMemset(q->gflags, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
   }
@@ -1980,7 +2128,8 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
                   q->txc, q->rxc, q->writes, q->flags, q->at, q->which, q->rss_hash, q->rx_hash, q->rss_desc,
                   q->rss_queue, q->rx_queue, q->partials, q->scal, q->tmp, q->sort_key, q->sorted_key, q->queue_which,
                   q->queue_start, q->queue_end, q->end_max, q->dlv_acc, q->dlv_done, q->gflags, q->piece_cs4,
-                  q->d_seg, q->d_blk, q->d_fb, q->d_segout, q->d_split, q->mflag, q->mscan, q->mlist, q->bounds};
+                  q->d_seg, q->d_blk, q->d_fb, q->d_segout, q->d_split, q->mflag, q->mscan, q->mlist, q->bounds,
+                  q->late, q->fix};
   for (void* b : bufs)
     if (b) (void) hipFree(b);
   if (q->hp) (void) hipHostFree(q->hp);
@@ -2026,6 +2175,7 @@ int nicgpu_qp_reserve(nicgpu_qp* q, size_t ntx, size_t nrx, nicgpu_qp_view* view
   if (st == NICGPU_OK) st = qp_grow(q->sorted_key, q->c_sk, r1);
   if (st == NICGPU_OK) st = qp_grow(q->queue_which, q->c_qw, r1);
   if (st == NICGPU_OK) st = qp_grow(q->end_max, q->c_em, r1);
+  if (st == NICGPU_OK) st = qp_grow(q->late, q->c_late, r1);
   q->cap_tx = ntx;
   q->cap_rx = nrx;
   qp_fill_view(q, view);
@@ -2058,7 +2208,7 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
   const unsigned long long gen = ++q->gen;
   q->plan_gen = gen;
   hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->counts, q->gflags, gen, qp_segs(q));
+                     q->plans, q->counts, q->gflags, gen, qp_segs(q), 0u);  // (its sums always run)
   int st = hip_status(hipGetLastError());
   uint32_t* np_h = reinterpret_cast<uint32_t*>(q->misc());
   uint64_t* ovf_h = q->misc() + 5;
@@ -2107,7 +2257,7 @@ int nicgpu_qp_plan_async(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, si
   q->plan_gen = gen;
   q->np = 0;  // known once resolved (nicgpu_qp_piece_count)
   hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->counts, q->gflags, gen, qp_segs(q));
+                     q->plans, q->counts, q->gflags, gen, qp_segs(q), q->defer_verify ? 1u : 0u);
   st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
   if (st != NICGPU_OK) return st;
@@ -2118,7 +2268,8 @@ int nicgpu_qp_plan_async(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, si
     st = hip_status(hipEventRecord(q->planned, s));
     if (st == NICGPU_OK) st = hip_status(hipStreamWaitEvent(static_cast<hipStream_t>(sums_stream), q->planned, 0));
   }
-  // the sums over the count the fill left on the device (g[4] <= cap)
+  // the sums over the count the fill left on the device (g[4] <= cap; 0 when
+  // the batch defers its RX verifies)
   if (st == NICGPU_OK)
     st = checksum_split_count(mem, q->piece_desc, cap, reinterpret_cast<const uint64_t*>(q->gflags + 4), q->piece_csum,
                               q->piece_cs4, sums_stream);
@@ -2154,7 +2305,8 @@ int nicgpu_qp_resum(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, void* s
   if (!q || (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0))) return NICGPU_ERR_INVALID;
   DeviceGuard g(q->device);
   const uint64_t cap = std::min(q->c_pdesc, std::min(q->c_pcs, q->c_pcs4));
-  return checksum_split_count(mem, q->piece_desc, cap, reinterpret_cast<const uint64_t*>(q->gflags + 4), q->piece_csum,
+  // (every piece the plan holds, also of a batch that deferred its RX verifies)
+  return checksum_split_count(mem, q->piece_desc, cap, reinterpret_cast<const uint64_t*>(q->gflags + 6), q->piece_csum,
                               q->piece_cs4, stream);
 }
 
@@ -2220,7 +2372,7 @@ int nicgpu_qp_resolve_start(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t 
   if (st == NICGPU_OK) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, (uint64_t) ntx, q->txc, q->rxc,
-                     q->writes, q->partials, q->need, q->gflags, q->plan_gen, S);
+                     q->writes, q->partials, q->need, q->gflags, q->plan_gen, S, q->late, (uint64_t) 0);
   st = hip_status(hipGetLastError());
   if (st != NICGPU_OK) return st;
   hipLaunchKernelGGL(qp_reduce_kernel, dim3(1), dim3(kQpReduceThreads), 0, s, q->partials, grid, q->pos,
@@ -2250,6 +2402,9 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
   int st = hip_status(hipEventSynchronize(q->resolved));
   if (st != NICGPU_OK) return st;
   q->np = part[20];
+  q->late_batch = part[21] != 0u;
+  C.late = q->late_batch;  // (the relaxation's and the walk's resolves)
+  q->late_used = 0;
   if (part[19] == 2u) return NICGPU_ERR_RANGE;  // a descriptor planned > 256 pieces: nothing resolved or settled
   if (part[19]) {  // the async plan did not fit its buffers: the same
     q->want_pieces = part[20] + part[20] / 4 + 64;
@@ -2292,7 +2447,8 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
     if (st == NICGPU_OK && q->nseg && lim < ntx) return NICGPU_ERR_UNSETTLED;
     if (st == NICGPU_OK) {
       hipLaunchKernelGGL(qp_full_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, q->pos, lim, q->txc, q->rxc, q->writes,
-                         q->partials, static_cast<const uint32_t*>(nullptr), q->gflags, q->plan_gen, S);
+                         q->partials, static_cast<const uint32_t*>(nullptr), q->gflags, q->plan_gen, S, q->late,
+                         q->late_batch ? (uint64_t) settled : (uint64_t) 0);  // (the settled prefix is delivered: its patches stay)
       st = hip_status(hipGetLastError());
     }
     if (st == NICGPU_OK) {
@@ -2307,11 +2463,31 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
     used = part[0];
   }
   std::memcpy(stats, part + 3, kQpStats * sizeof(uint64_t));
+  q->late_used = used;  // the completions the device resolved (deferred ones among them)
   if (q->nseg) used = q->seg_nrx;  // every slot of the concatenated ring (the unused ones marked)
   *done = lim;
   *rx_used = used;
   if (rx_settled) *rx_settled = settled < used ? settled : used;
   return NICGPU_OK;
+}
+
+int nicgpu_qp_set_deferred_verify(nicgpu_qp* q, int on) {
+  if (!q) return NICGPU_ERR_INVALID;
+  q->defer_verify = on != 0;
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_deferred(const nicgpu_qp* q, int* deferred) {
+  if (!q || !deferred) return NICGPU_ERR_INVALID;
+  *deferred = q->late_batch ? 1 : 0;
+  return NICGPU_OK;
+}
+
+int nicgpu_qp_verify_fixups_async(nicgpu_qp* q, uint64_t* out, void* stream) {
+  if (!q || !out) return NICGPU_ERR_INVALID;
+  DeviceGuard g(q->device);
+  return hip_status(hipMemcpyAsync(out, q->fix, NICGPU_QP_FIXUPS * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                   static_cast<hipStream_t>(stream)));
 }
 
 int nicgpu_qp_walks(const nicgpu_qp* q, uint64_t* walks) {
@@ -2468,6 +2644,13 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
   P.rss.mode = tuple_mode;
   P.rss.raw_off = raw_off;
   P.rss.raw_len = raw_len;
+  if (q->defer_verify && q->nseg == 0) {  // (the kernel reads whether the plan deferred)
+    P.late = q->late;
+    P.lateflag = q->gflags + 7;
+    P.late_gen = q->plan_gen;
+    P.late_n = (flags & NICGPU_DELIVER_SETTLED) ? ~0ull : q->late_used;
+    P.fix = q->fix;
+  }
   if (rss) {
     P.rss.lut = ctx->d_lut;
     P.rss.table = ctx->d_table;
@@ -2646,7 +2829,7 @@ extern "C" int nicgpu_tune_deliver(int mode, uint8_t* mem, uint64_t mem_size, co
   P.mem = mem;
   P.mem_size = mem_size;
   P.w = w;
-  P.rxc = rxc;
+  P.rxc = const_cast<nicgpu_completion*>(rxc);  // (tuning modes never write it)
   P.j0 = 0;
   P.n = n;
   P.alt_dst = alt_dst;

@@ -864,9 +864,12 @@ void build_queue_lists(RxBatchResult& out) {
 
 namespace {
 
-void check(int st, const char* what) {
-  if (st != NICGPU_OK) throw GpuError(std::string(what) + ": " + nicgpu_strerror(st), st);
+void check_at(int st, const char* what, int line) {
+  if (st != NICGPU_OK)
+    throw GpuError(std::string(what) + " (rx_stage.cpp:" + std::to_string(line) + "): " + nicgpu_strerror(st), st);
 }
+// (the call site in the message: one failing HIP call among many alike)
+#define check(st, what) check_at((st), (what), __LINE__)
 
 // One growable device buffer.
 struct DevBuf {
@@ -1120,6 +1123,7 @@ struct BatchedQueuePair::Slot {
   std::vector<Slot*> dep_stage, dep_rx;
   std::vector<rx_stage_detail::SegmentWrite> applied;
   DevBuf wbuf, stage_tx;
+  HostBuf h_applied;
   // a manager's fused batch (process_queues): nseg queue pairs; their RSS
   // dispatch lists split per queue pair (split, (nseg + 1) x nq) and, when
   // they count into RssEngines of their own, their hits (seg_hits, nseg x tn)
@@ -1135,6 +1139,12 @@ struct BatchedQueuePair::Slot {
   HostBuf h_itx, h_irx;
   bool irq_pending = false;
   std::size_t irq_ntx = 0, irq_nrx = 0;
+  // deferred RX verify (nicgpu_qp_set_deferred_verify): the batch's completions
+  // and statistics are final after its deliveries; the context's running
+  // corrections come down into h_fix, fix_seen the last applied
+  bool late = false;
+  HostBuf h_fix;
+  std::uint64_t fix_seen[NICGPU_QP_FIXUPS] = {};
 
   void release_rss() {
     if (!rss_released) rss_recorded.set_value();
@@ -1166,6 +1176,7 @@ struct BatchedQueuePair::Slot {
   }
   void create(int dev) {
     check(nicgpu_qp_create(&qp, dev), "nicgpu_qp_create");
+    for (std::uint64_t& f : fix_seen) f = 0;  // a new context's corrections start at 0
     for (void** e : {&ev_tx, &ev_rx, &ev_resolved, &ev_done, &ev_submit, &ev_staged, &ev_wb, &ev_gate})
       check(nicgpu_event_create(e), "nicgpu_event_create");
     for (auto& side : ev_irq)
@@ -1446,7 +1457,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
     on_device = front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);
     if (on_device) {
       back(sl, mem, out, stream);
-      finish(sl, out);
+      finish(sl, out, &st);
     }
   }
   if (!on_device) on_host(mem, tx, rx, st, out, stream, disjoint, check_us);
@@ -1498,7 +1509,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDe
     on_device = front(sl, mem, {}, {}, st, out, stream, disjoint, check_us);
     if (on_device) {
       back(sl, mem, out, stream);
-      finish(sl, out);
+      finish(sl, out, &st);
     }
   }
   if (!on_device) {
@@ -1679,7 +1690,7 @@ bool BatchedQueuePair::collect(RxBatchResult& out) {
     }
     throw;
   }
-  if (sl.on_device) finish(sl, sl.result);
+  if (sl.on_device) finish(sl, sl.result, &sl.stats);
   else sl.wait_writeback();  // a host-path batch of a HostMemory: its bytes are back
   rx_stage_detail::add_stats(stats_, sl.stats);
   std::swap(out, sl.result);
@@ -1855,6 +1866,12 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
   // 32-bit piece indices allow, makes the resolve settle nothing and its
   // finish return NICGPU_ERR_RANGE — that batch then takes the host path
   // (which refuses it if its total does not fit either), the next one fits
+  static const bool defer_env = [] {  // tuning A/B: NIC_DEFER_VERIFY=0
+    const char* e = std::getenv("NIC_DEFER_VERIFY");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  check(nicgpu_qp_set_deferred_verify(sl.qp, config_.defer_rx_verify && defer_env ? 1 : 0),
+        "nicgpu_qp_set_deferred_verify");
   check(nicgpu_qp_plan_async(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu,
                              &v, ps, rs),
         "nicgpu_qp_plan_async");
@@ -1964,6 +1981,10 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
     return false;
   }
   check(rst, "nicgpu_qp_resolve_finish");
+  int late = 0;
+  check(nicgpu_qp_deferred(sl.qp, &late), "nicgpu_qp_deferred");
+  sl.late = late != 0;
+  out.timings.deferred = sl.late;
   if (ov) {  // the relaxation's rewrites (on rs) before the rest of this batch's work on `stream`
     check(nicgpu_event_record(sl.ev_resolved, rs), "nicgpu_event_record");
     check(nicgpu_stream_wait_event(stream, sl.ev_resolved), "nicgpu_stream_wait_event");
@@ -1997,6 +2018,9 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
     check(nicgpu_memcpy_async(&pb, v.piece_base + done, sizeof(pb), stream), "nicgpu_memcpy_async");
     check(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
     if (np - pb != S.host.plan.pieces.size()) throw GpuError("process_batch: device and host plans differ", NICGPU_ERR_INVALID);
+    // a batch that deferred its RX verifies skipped the piece sums
+    if (sl.late)
+      check(nicgpu_qp_resum(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, stream), "nicgpu_qp_resum");
     // the device's split sums of those pieces: rests, then first-4 parts
     const std::size_t m = np - pb;
     S.tail_cs.resize(2 * m);
@@ -2078,10 +2102,13 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   std::shared_future<void> rss_ready = sl.rss_recorded.get_future().share();
   if (sl.relaxed) check(nicgpu_event_record(sl.ev_resolved, stream), "nicgpu_event_record");
   sl.irq_pending = false;
-  if (keep && config_.on_interrupt && (config_.enable_tx_interrupts || config_.enable_rx_interrupts) && !sl.multi) {
-    // the completions for the callbacks, in chunks, page-locked, as soon as
-    // they are final: collect() replays chunk c while chunk c + 1 lands
-    check(nicgpu_stream_wait_event(S.side_irq, sl.ev_resolved), "nicgpu_stream_wait_event");
+  const bool irq_down =
+      keep && config_.on_interrupt && (config_.enable_tx_interrupts || config_.enable_rx_interrupts) && !sl.multi;
+  // the completions for the callbacks, in chunks, page-locked, as soon as they
+  // are final (ev_resolved; a deferred-verify batch's after its deliveries,
+  // ev_done): collect() replays chunk c while chunk c + 1 lands
+  auto irq_download = [&](void* final_ev) {
+    check(nicgpu_stream_wait_event(S.side_irq, final_ev), "nicgpu_stream_wait_event");
     const std::size_t n2[2] = {ntx, nrx_total};
     CompletionEntry* dst[2] = {sl.h_itx.get<CompletionEntry>(std::max<std::size_t>(ntx, 1)),
                                sl.h_irx.get<CompletionEntry>(std::max<std::size_t>(nrx_total, 1))};
@@ -2099,7 +2126,8 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
     sl.irq_ntx = ntx;
     sl.irq_nrx = nrx_total;
     sl.irq_pending = true;
-  }
+  };
+  if (irq_down && !sl.late) irq_download(sl.ev_resolved);
   sl.down.emplace(sl.worker);
   // the dispatch lists are made here too, on the download stream: they read
   // this slot's buffers only, so the next batch's piece sums need not queue
@@ -2107,13 +2135,21 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   sl.down->start([&sl, &S, &out, &v, ntx, nrx_total, tn, nq, rss, keep, hits, rss_ready](SideJob& j) {
     bool ok = j.ok(nicgpu_set_device(S.device), "nicgpu_set_device") &&
               j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_resolved), "nicgpu_stream_wait_event");
-    if (ok && !keep)
+    auto completions_down = [&] {
       ok = j.ok(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), S.side_down),
                 "nicgpu_memcpy_async") &&
            j.ok(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry), S.side_down),
                 "nicgpu_memcpy_async");
+    };
+    if (ok && !keep && !sl.late) completions_down();
     rss_ready.wait();
     ok = ok && j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_done), "nicgpu_stream_wait_event");
+    // a deferred-verify batch: its completions are final now, and its
+    // statistics' corrections come down with them
+    if (ok && !keep && sl.late) completions_down();
+    if (ok && sl.late)
+      ok = j.ok(nicgpu_qp_verify_fixups_async(sl.qp, sl.h_fix.get<std::uint64_t>(NICGPU_QP_FIXUPS), S.side_down),
+                "nicgpu_qp_verify_fixups_async");
     // a fused batch: the lists split per queue pair (entries made relative to
     // each queue pair's ring), and its per-queue-pair hits when it needs them
     // (its per-queue-pair hits beside the lists, on the interrupt stream, which
@@ -2160,6 +2196,7 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
     out.timings.gather_us += us_since(t);
     t = clock::now();
     check(nicgpu_event_record(sl.ev_done, stream), "nicgpu_event_record");
+    if (irq_down && sl.late) irq_download(sl.ev_done);
     if (sl.image) {  // the delivered bytes back into the host memory, beside the next batches' work
       check(nicgpu_stream_wait_event(S.side_wb, sl.ev_done), "nicgpu_stream_wait_event");
       image_writeback(sl, v.writes, nrx_total, S.side_wb);
@@ -2178,7 +2215,7 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
 
 // The downloads waited for everything the batch did on the caller's stream,
 // so the image holds its writes once they are done.
-void BatchedQueuePair::finish(Slot& sl, RxBatchResult& out) {
+void BatchedQueuePair::finish(Slot& sl, RxBatchResult& out, QueuePairStats* st) {
   using clock = std::chrono::steady_clock;
   const auto t = clock::now();
   struct Reset {  // the slot's job is over whatever finish() throws
@@ -2187,6 +2224,25 @@ void BatchedQueuePair::finish(Slot& sl, RxBatchResult& out) {
   } reset{sl};
   sl.down->finish();
   sl.wait_writeback();
+  if (sl.late) {
+    // the deferred verifies that failed since the last batch of this context:
+    // the statistics took them as delivered (queue_pair.cpp:434-447 counts a
+    // drop instead, and neither the RX nor the finalized TX counters)
+    if (!st) throw std::logic_error("finish: a deferred-verify batch without its statistics");
+    const std::uint64_t* f = static_cast<const std::uint64_t*>(sl.h_fix.p);
+    std::uint64_t d[NICGPU_QP_FIXUPS];
+    for (unsigned k = 0; k < NICGPU_QP_FIXUPS; ++k) {
+      d[k] = f[k] - sl.fix_seen[k];
+      sl.fix_seen[k] = f[k];
+    }
+    st->drops_checksum += d[0];
+    st->rx_packets -= d[0];
+    st->tx_packets -= d[0];
+    st->rx_bytes -= d[1];
+    st->rx_vlan_strips -= d[2];
+    st->tx_bytes -= d[3];
+    st->tx_vlan_insertions -= d[4];
+  }
   if (sl.rss && !sl.multi) {  // (a fused batch's accounting and lists are process_queues')
     const std::uint64_t m = sl.meta[0];
     config_.rss->account_batch(m, std::span<const std::uint64_t>(sl.meta + 1, sl.tn));
@@ -2371,9 +2427,14 @@ void BatchedQueuePair::image_host_path(Slot& sl, std::span<const TxDescriptor> t
   out.timings.staged_whole = sl.whole;
   const std::size_t n = sl.applied.size();
   void* d = sl.wbuf.get(std::max<std::size_t>(n, 1) * sizeof(rx_stage_detail::SegmentWrite));
-  if (n)
-    check(nicgpu_memcpy_async(d, sl.applied.data(), n * sizeof(rx_stage_detail::SegmentWrite), stream),
-          "nicgpu_memcpy_async");
+  if (n) {
+    // staged through page-locked memory: the registered window's pages (a
+    // HostMemory buffer need not be page-aligned) may hold part of a heap
+    // vector, and a copy from one straddling them fails
+    auto* h = sl.h_applied.get<rx_stage_detail::SegmentWrite>(n);
+    std::memcpy(h, sl.applied.data(), n * sizeof(rx_stage_detail::SegmentWrite));
+    check(nicgpu_memcpy_async(d, h, n * sizeof(rx_stage_detail::SegmentWrite), stream), "nicgpu_memcpy_async");
+  }
   image_writeback(sl, static_cast<const nicgpu_segment_write*>(d), n, stream);
 }
 
@@ -2411,7 +2472,7 @@ void BatchedQueuePair::process_batch(HostMemory& m, std::span<const TxDescriptor
       on_device = front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);
       if (on_device) {
         back(sl, mem, out, stream);
-        finish(sl, out);
+        finish(sl, out, &st);
       }
     }
     if (!on_device) {
@@ -2505,6 +2566,7 @@ bool BatchedQueuePair::front_multi(Slot& sl, const DeviceHostMemory& mem, std::s
   check(nicgpu_qp_walks(sl.qp, &walks1), "nicgpu_qp_walks");
   out.timings.walked = out.timings.walked || walks1 != walks0;
   out.timings.resolve_us += us_since(t);
+  sl.late = false;  // (segmented batches never defer their RX verifies)
   if (rst == NICGPU_ERR_AGAIN) {
     again = 1;
     return false;
@@ -2632,7 +2694,7 @@ bool BatchedQueuePair::process_queues(const DeviceHostMemory& mem_in, HostImage*
     }
     if (ok) {
       back(sl, mem, cat, stream);
-      finish(sl, cat);
+      finish(sl, cat, nullptr);
     }
   } catch (...) {
     (void) nicgpu_qp_set_segments(sl.qp, nullptr, 0, 0, nullptr);

@@ -274,7 +274,27 @@ struct Ctx {
   const Tx* tx;
   const Rx* rx;
   uint64_t nrx;
+  // deferred RX verify (the device's f1 path, batches where no decision that
+  // moves ring positions reads a sum: no TX verify, one segment per packet):
+  // the :434-447 check is taken to pass and the completion marked for the
+  // delivery, which sums the bytes it writes and patches the failures
+  bool late = false;
 };
+
+// A deferred completion's bits (the delivery's stats correction on a failure)
+enum : uint32_t { kLateDeferred = 1, kLateStripBase = 2, kLateVlanInsert = 4 };
+
+// sink.rx_late(e, w, bits) for a sink that records deferred completions, else
+// sink.rx(e, w)
+template <class Sink, class Comp, class Write>
+NICQP_HD auto sink_rx_late(Sink& s, const Comp& e, const Write* w, uint32_t bits, int)
+    -> decltype(s.rx_late(e, w, bits), void()) {
+  s.rx_late(e, w, bits);
+}
+template <class Sink, class Comp, class Write>
+NICQP_HD void sink_rx_late(Sink& s, const Comp& e, const Write* w, uint32_t, long) {
+  s.rx(e, w);
+}
 
 template <class Comp>
 NICQP_HD Comp make_completion(uint16_t qid, uint16_t idx, uint32_t st) {  // :150-158
@@ -446,7 +466,13 @@ NICQP_HD uint64_t resolve_packet(const Ctx<Tx, Rx, Plan>& C, uint64_t i, uint64_
     e.gro_aggregated = xr.gro_enabled;
     if (e.gro_aggregated) stats.rx_gro_aggregated += 1;
     // :434-447 RX checksum verify of the delivered bytes
-    if (xr.checksum_offload && (uint32_t) xr.checksum != 0u) {
+    bool deferred = false;
+    if (xr.checksum_offload && (uint32_t) xr.checksum != 0u && C.late) {
+      // (its sum is that of the bytes w writes: the delivery's)
+      e.checksum_verified = true;
+      stats.rx_checksum_verified += 1;
+      deferred = true;
+    } else if (xr.checksum_offload && (uint32_t) xr.checksum != 0u) {
       e.checksum_verified = true;
       stats.rx_checksum_verified += 1;
       uint32_t first4, rest;
@@ -466,7 +492,11 @@ NICQP_HD uint64_t resolve_packet(const Ctx<Tx, Rx, Plan>& C, uint64_t i, uint64_
       e.vlan_tag = t.vlan_insert ? t.vlan_tag : xr.vlan_tag;
       stats.rx_vlan_strips += 1;
     }
-    sink.rx(e, &w);
+    if (deferred)
+      sink_rx_late(sink, e, &w,
+                   kLateDeferred | (strip_base ? kLateStripBase : 0u) | (t.vlan_insert ? kLateVlanInsert : 0u), 0);
+    else
+      sink.rx(e, &w);
     stats.rx_packets += 1;
     stats.rx_bytes += size;
   }

@@ -4,6 +4,7 @@
 
 #include "host.h"
 
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -128,9 +129,53 @@ int nicgpu_memset_async(void* dev_ptr, int value, size_t bytes, void* stream) {
   return hip_status(hipMemsetAsync(dev_ptr, value, bytes, static_cast<hipStream_t>(stream)));
 }
 
+}  // extern "C"
+
+// Whole pages around the range: hipHostRegister locks pages, and the staging
+// kernels read up to the next 16-B boundary past the last byte.  The page
+// ranges this library registered, for nicgpu_memcpy_async.
+namespace {
+constexpr uintptr_t kPage = 4096;
+void page_span(void* p, size_t n, void*& base, size_t& len) {
+  const auto a = reinterpret_cast<uintptr_t>(p);
+  const uintptr_t lo = a & ~(kPage - 1), hi = (a + n + 16 + kPage - 1) & ~(kPage - 1);
+  base = reinterpret_cast<void*>(lo);
+  len = hi - lo;
+}
+std::mutex g_reg_mu;
+std::vector<std::pair<uintptr_t, uintptr_t>> g_reg;  // [base, end)
+std::atomic<size_t> g_nreg{0};
+// bytes of [p, p + n) before the end of a registered range p starts inside,
+// when the range ends first; 0 otherwise
+size_t registered_cut1(const void* p, size_t n) {
+  const auto a = reinterpret_cast<uintptr_t>(p);
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  for (const auto& r : g_reg)
+    if (a >= r.first && a < r.second && a + n > r.second) return r.second - a;
+  return 0;
+}
+size_t registered_cut(const void* dst, const void* src, size_t n) {
+  if (g_nreg.load(std::memory_order_relaxed) == 0) return 0;
+  const size_t a = registered_cut1(dst, n), b = registered_cut1(src, n);
+  return a && b ? (a < b ? a : b) : (a ? a : b);
+}
+}  // namespace
+
+extern "C" {
+
 int nicgpu_memcpy_async(void* dst, const void* src, size_t bytes, void* stream) {
   if (bytes == 0) return NICGPU_OK;
   if (!dst || !src) return NICGPU_ERR_INVALID;
+  // A host range that starts inside pages nicgpu_host_register locked and runs
+  // past them (a heap neighbour of a HostMemory buffer that is not page
+  // aligned) is not one allocation to the runtime: the copy is cut there.
+  for (size_t cut; (cut = registered_cut(dst, src, bytes)) != 0 && cut < bytes;) {
+    const int st = hip_status(hipMemcpyAsync(dst, src, cut, hipMemcpyDefault, static_cast<hipStream_t>(stream)));
+    if (st != NICGPU_OK) return st;
+    dst = static_cast<uint8_t*>(dst) + cut;
+    src = static_cast<const uint8_t*>(src) + cut;
+    bytes -= cut;
+  }
   return hip_status(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, static_cast<hipStream_t>(stream)));
 }
 
@@ -192,17 +237,7 @@ int nicgpu_event_synchronize(void* event) {
   return hip_status(hipEventSynchronize(static_cast<hipEvent_t>(event)));
 }
 
-// Whole pages around the range: hipHostRegister locks pages, and the staging
-// kernels read up to the next 16-B boundary past the last byte.
-namespace {
-constexpr uintptr_t kPage = 4096;
-void page_span(void* p, size_t n, void*& base, size_t& len) {
-  const auto a = reinterpret_cast<uintptr_t>(p);
-  const uintptr_t lo = a & ~(kPage - 1), hi = (a + n + 16 + kPage - 1) & ~(kPage - 1);
-  base = reinterpret_cast<void*>(lo);
-  len = hi - lo;
-}
-}  // namespace
+
 
 int nicgpu_host_register(void* host_ptr, size_t bytes, void** dev_alias, int* owned) {
   if (!host_ptr || !dev_alias || !owned || bytes == 0) return NICGPU_ERR_INVALID;
@@ -212,7 +247,12 @@ int nicgpu_host_register(void* host_ptr, size_t bytes, void** dev_alias, int* ow
   size_t len = 0;
   page_span(host_ptr, bytes, base, len);
   const hipError_t e = hipHostRegister(base, len, hipHostRegisterMapped);
-  if (e == hipSuccess) *owned = 1;
+  if (e == hipSuccess) {
+    *owned = 1;
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    g_reg.emplace_back(reinterpret_cast<uintptr_t>(base), reinterpret_cast<uintptr_t>(base) + len);
+    g_nreg.store(g_reg.size());
+  }
   else if (e != hipErrorHostMemoryAlreadyRegistered) return NICGPU_ERR_HIP;
   (void) hipGetLastError();  // clear the sticky "already registered"
   void* dev = nullptr;
@@ -230,6 +270,15 @@ int nicgpu_host_unregister(void* host_ptr) {
   void* base = nullptr;
   size_t len = 0;
   page_span(host_ptr, 1, base, len);
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    for (size_t i = 0; i < g_reg.size(); ++i)
+      if (g_reg[i].first == reinterpret_cast<uintptr_t>(base)) {
+        g_reg.erase(g_reg.begin() + (long) i);
+        break;
+      }
+    g_nreg.store(g_reg.size());
+  }
   return hip_status(hipHostUnregister(base));
 }
 

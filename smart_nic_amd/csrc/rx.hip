@@ -453,11 +453,7 @@ __device__ __forceinline__ void run_general_tile(const RxParams& P, const RxLdsP
 // ~4-8% later (profiles/r02_wave_stamps_c2.jsonl), get less.  The split is a
 // function of (blockIdx, wave) and the count only: every packet is covered
 // exactly once wherever the blocks land; placement only affects its speed.
-// XPF2 (with XPF): a next tile of at most two batches (64-B packets, short
-// IMIX tiles) gets BOTH batches issued before this tile's epilogue, so a wave
-// keeps a whole small tile in flight across it; such a tile is then processed
-// without further loads.
-template <int U, int WPB, int SST, int OCC = 4, bool XPF = true, int SPLIT = 0, bool XPF2 = false>
+template <int U, int WPB, int SST, int OCC = 4, bool XPF = true, int SPLIT = 0>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void rx_offload_kernel(
     RxParams P) {
   extern __shared__ uint4 lds_dyn[];
@@ -506,27 +502,6 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   if (L.table_lds) {
     for (uint32_t i = threadIdx.x; i < P.table_n; i += kWave * WPB) L.table_s[i] = P.table[i];
   }
-  // SPLIT 2: one ticket per block from the counter of the XCD it really runs
-  // on (XCC_ID), or, that one spent, from the next XCD's; tickets = blocks, so
-  // every block gets one whatever the placement
-  __shared__ uint32_t xcc_ticket[2];
-  if constexpr (SPLIT == 2) {
-    if (threadIdx.x == 0) {
-      const uint32_t G = gridDim.x, x0 = (uint32_t) __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
-      uint32_t grp = 0, tk = 0;
-      for (uint32_t k = 0; k < 8u; ++k) {
-        const uint32_t c = (x0 + k) & 7u;
-        const uint32_t t = atomicAdd(&P.xcd_tickets[c], 1u);
-        if (t < (G + 7u - c) / 8u) {
-          grp = c;
-          tk = t;
-          break;
-        }
-      }
-      xcc_ticket[0] = grp;
-      xcc_ticket[1] = tk;
-    }
-  }
   __syncthreads();
 #ifdef NICGPU_TUNING
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
@@ -539,13 +514,11 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
   // (the grid is sized for n; waves past the count have no tile)
   const uint64_t n_all = P.n_dev ? (*P.n_dev < P.n ? (uint64_t) *P.n_dev : P.n) : P.n;
   uint64_t first = gw * kWave, end = n_all, step = nwaves * kWave;
-  if constexpr (SPLIT != 0) {
-    // group v = blockIdx % 8 (SPLIT 2: the block's ticket group) gets
-    // [g0, g1), its waves equal parts of it in (blockIdx / 8 or ticket, wave)
-    // order; n_all * weight sums < 2^64 (the host keeps n below 2^34);
-    // adjacent ranges share their boundary's expression
-    const uint32_t G = gridDim.x, v = SPLIT == 2 ? xcc_ticket[0] : blockIdx.x & 7u;
-    const uint32_t bslot = SPLIT == 2 ? xcc_ticket[1] : blockIdx.x >> 3;
+  if constexpr (SPLIT == 1) {
+    // group v = blockIdx % 8 gets [g0, g1), its waves equal parts of it in
+    // (blockIdx / 8, wave) order; n_all * weight sums < 2^64 (the host keeps
+    // n below 2^34); adjacent ranges share their boundary's expression
+    const uint32_t G = gridDim.x, v = blockIdx.x & 7u;
     uint64_t cum = 0, tot = 0, mine = 0;
     for (uint32_t u = 0; u < 8u; ++u) {
       const uint64_t c = (uint64_t) ((G + 7u - u) / 8u) * ((u & 1u) ? (uint64_t) P.xcd_w_odd : 65536ull);
@@ -555,7 +528,7 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
     }
     const uint64_t g0 = n_all * cum / tot, g1 = cum + mine == tot ? n_all : n_all * (cum + mine) / tot;
     const uint64_t nw = (uint64_t) ((G + 7u - v) / 8u) * WPB,
-                   rank = (uint64_t) bslot * WPB + (uint64_t) __builtin_amdgcn_readfirstlane(w);
+                   rank = (uint64_t) (blockIdx.x >> 3) * WPB + (uint64_t) __builtin_amdgcn_readfirstlane(w);
     first = g0 + (g1 - g0) * rank / nw;
     end = rank + 1 == nw ? g1 : g0 + (g1 - g0) * (rank + 1) / nw;
     step = kWave;
@@ -589,16 +562,10 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
     __builtin_amdgcn_wave_barrier();
     plan_contig<U, kLoadNt>(A, L.slotsA, 0, lane, t.start, t.nch, t.info, r);
   };
-  bool pre = false;   // (XPF) A already holds cur's first batch
-  bool pre2 = false;  // (XPF2) ... and B its second, the last
+  bool pre = false;  // (XPF) A already holds cur's first batch
   __amdgpu_buffer_rsrc_t rsrc_pre = tile_rsrc(cur);
   while (cur.nvalid != 0u) {
-    if (XPF2 && pre2) {
-      // a small tile wholly in flight since the previous epilogue
-      uint32_t run = process_contig<U>(A, L.slotsA, L.masks, 0u, L.E, L.hdr, L.stage, lane);
-      run = process_contig<U>(B, L.slotsB, L.masks, run, L.E, L.hdr, L.stage, lane);
-      (void) run;
-    } else if (cur.contig && cur.total != 0u) {
+    if (cur.contig && cur.total != 0u) {
       // Contiguous tile: chunk c is absolute chunk D + c.  Ping-pong: batch
       // i+1's loads are in flight while batch i is reduced; every plan is
       // unconditional (positions past the end read zeros through the buffer
@@ -626,14 +593,9 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(OCC
     const uint64_t nb = cur.base + step;
     const Tile nxt = make_tile(nb, nvalid_of(nb), d_next);
     pre = false;
-    pre2 = false;
     if (XPF && nxt.contig && nxt.total != 0u && nxt.total <= P.xpf_chunks) {
       rsrc_pre = tile_rsrc(nxt);
       tile_first(nxt, rsrc_pre);
-      if (XPF2 && nxt.total > kStep && nxt.total <= 2u * kStep) {
-        plan_contig<U, kLoadNt>(B, L.slotsB, kStep, lane, nxt.start, nxt.nch, nxt.info, rsrc_pre);
-        pre2 = true;
-      }
       __builtin_amdgcn_sched_barrier(0);  // the next tile's loads go out before this tile's epilogue
       pre = true;
     }
@@ -756,7 +718,6 @@ struct RxVariant {
   int wpb;
   const char* name;
   bool xpf = true;  // cross-tile prefetch (P.xpf_chunks)
-  bool tickets = false;  // SPLIT 2: per-XCD ticket counters zeroed before the launch
 };
 
 const RxVariant kRxVariants[] = {
@@ -781,9 +742,6 @@ const RxVariant kRxVariants[] = {
     {rx_offload_kernel<2, 4, 16, 4, true, 1>, 2, 4, "u2_w4_c_sc1_ring_xpf_xcd"},
     {rx_offload_kernel<2, 4, 0, 4, true, 1>, 2, 4, "u2_w4_c_ring_xpf_xcd"},
     {rx_offload_kernel<2, 8, 16, 4, true, 1>, 2, 8, "u2_w8_c_sc1_ring_xpf_xcd"},
-    // round 5: the same ranges dealt by the block's real XCC id (SPLIT 2)
-    {rx_offload_kernel<2, 4, 16, 4, true, 2>, 2, 4, "u2_w4_c_sc1_ring_xpf_xcc", true, true},
-    {rx_offload_kernel<2, 4, 0, 4, true, 2>, 2, 4, "u2_w4_c_ring_xpf_xcc", true, true},
     // candidates timed by tools/tune_rx.py (the rejected experiments of
     // DESIGN.md §7 — deferred stores, register-held results, non-contiguous
     // only, other load policies — are in git history before round 4)
@@ -794,10 +752,6 @@ const RxVariant kRxVariants[] = {
     {rx_offload_kernel<2, 4, 0, 1, false>, 2, 4, "u2_nt1_w4_c_ring", false},
     // bigger blocks still: 256 same-address atomics per bin
     {rx_offload_kernel<2, 16, 16, 1>, 2, 16, "u2_w16_c_sc1_ring_xpf"},
-    // round 5: both batches of a small next tile before the epilogue (XPF2)
-    {rx_offload_kernel<2, 8, 16, 4, true, 0, true>, 2, 8, "u2_w8_c_sc1_ring_xpf2"},
-    {rx_offload_kernel<2, 4, 16, 4, true, 0, true>, 2, 4, "u2_w4_c_sc1_ring_xpf2"},
-    {rx_offload_kernel<2, 4, 0, 4, true, 0, true>, 2, 4, "u2_w4_c_ring_xpf2"},
 #endif
 };
 constexpr int kNumRxVariants = (int) (sizeof(kRxVariants) / sizeof(kRxVariants[0]));
@@ -912,18 +866,6 @@ int launch_rx(const RxParams& P, const DeviceInfo& di, int variant, hipStream_t 
 #endif
   const uint64_t cap = (uint64_t) di.cus * (uint64_t) bpc;
   const unsigned grid = (unsigned) (want < cap ? want : cap);
-#ifdef NICGPU_TUNING
-  if (v.tickets) {
-    static unsigned int* tickets = [] {
-      void* p = nullptr;
-      return hipMalloc(&p, 8 * sizeof(unsigned int)) == hipSuccess ? static_cast<unsigned int*>(p) : nullptr;
-    }();
-    if (!tickets) return NICGPU_ERR_NOMEM;
-    Pl.xcd_tickets = tickets;
-    int st = hip_status(hipMemsetAsync(tickets, 0, 8 * sizeof(unsigned int), stream));
-    if (st != NICGPU_OK) return st;
-  }
-#endif
   hipLaunchKernelGGL(v.kernel, dim3(grid), dim3(kWave * v.wpb), lds_launch, stream, Pl);
   return hip_status(hipGetLastError());
 }

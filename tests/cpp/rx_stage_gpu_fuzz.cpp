@@ -77,6 +77,7 @@ const std::vector<std::uint8_t> kMsKey = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x
                                           0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
 
 std::size_t g_tail = 0, g_device = 0, g_short = 0, g_devdesc = 0;  // host tails, device batches, NoDescriptor, device descriptors
+std::size_t g_late = 0, g_late_fail = 0;  // batches whose RX verifies the delivery made; ChecksumError completions in them
 std::size_t g_himg = 0, g_himg_sparse = 0;  // batches run on a HostMemory (and staged per descriptor)
 std::size_t g_irq = 0;  // interrupt callbacks compared
 
@@ -125,6 +126,10 @@ int run_case(std::uint64_t seed) {
   const std::size_t mtus[] = {9000, 1500, 3000, 65535};
   const std::size_t max_mtu = mtus[r.below(4)];
   const bool tso_heavy = r.below(4) == 0;
+  // one seed in three: a batch the device resolves with its RX verifies
+  // deferred to the delivery (no TX verify, one segment per packet; a quarter
+  // of the frames unbalanced, so many of those verifies fail)
+  const bool late_case = seed % 3 == 2;
   std::vector<TxDescriptor> tx(ntx);
   std::vector<std::uint8_t> image;
   std::size_t at = 0;
@@ -133,6 +138,7 @@ int run_case(std::uint64_t seed) {
     const std::uint32_t pick = r.below(16);
     std::size_t L = pick < 4 ? r.below(70) : (pick < 10 ? 60 + r.below(1500) : (pick < 15 ? 9000 : 9000 + r.below(70000)));
     if (large && L > 9000) L = 1518;
+    if (late_case && L > 9000) L = 9000;
     std::vector<std::uint8_t> p(L);
     const bool zero = r.below(40) == 0;
     for (auto& b : p) b = zero ? 0 : r.byte();
@@ -157,6 +163,13 @@ int run_case(std::uint64_t seed) {
     if (r.below(5) == 0) {
       t.vlan_insert = true;
       t.vlan_tag = static_cast<std::uint16_t>(r.below(65536));
+    }
+    if (late_case) {
+      t.checksum_offload = true;
+      // TSO/GSO of at most one segment (header || one chunk when the mss is
+      // at least the payload: the segmented write form)
+      if ((t.tso_enabled || t.gso_enabled) && t.mss && L > t.header_length)
+        t.mss = static_cast<std::uint16_t>(std::min<std::size_t>(9000, L - t.header_length + r.below(3)));
     }
     pkts.emplace_back(at, std::move(p));
     at += L;
@@ -276,6 +289,10 @@ int run_case(std::uint64_t seed) {
     return 1;
   }
   g_device += 1;
+  if (go.timings.deferred) {
+    g_late += 1;
+    for (const CompletionEntry& e : ho.rx_completions) g_late_fail += e.status == static_cast<std::uint32_t>(CompletionCode::ChecksumError);
+  }
   bool ok = go.tx_completions.size() == ho.tx_completions.size() && go.rx_completions.size() == ho.rx_completions.size();
   for (std::size_t i = 0; ok && i < ho.tx_completions.size(); ++i) ok = same(go.tx_completions[i], ho.tx_completions[i]);
   for (std::size_t i = 0; ok && i < ho.rx_completions.size(); ++i) ok = same(go.rx_completions[i], ho.rx_completions[i]);
@@ -472,7 +489,7 @@ int run_full(const char* wl, bool dev_desc, bool keep) {
 // ones wrote (TX buffers inside the RX ring), some batches overlap their own
 // buffers (host path) and the RX windows wrap the ring.  Results, statistics,
 // the image and the RSS engine's stats must all be equal.
-std::size_t g_pipe_batches = 0, g_pipe_host = 0, g_pipe_devdesc = 0, g_pipe_himg = 0;
+std::size_t g_pipe_batches = 0, g_pipe_host = 0, g_pipe_devdesc = 0, g_pipe_himg = 0, g_pipe_late = 0;
 bool g_force_himg = false;  // `pipeline himg`: every sequence's pipelined side on a HostMemory
 std::size_t g_pipe_overlapped = 0, g_pipe_redone = 0;  // overlapped resolves that stood / were redone
 
@@ -499,6 +516,9 @@ int run_pipeline(std::uint64_t seed) {
   // overlapped resolve then stands (the others mostly redo it behind the
   // earlier batches' writes)
   const bool quiet = seed % 5 == 0;
+  // one sequence in four: batches the device resolves with their RX verifies
+  // deferred to the delivery (the process_batch side sums them eagerly)
+  const bool late_case = seed % 4 == 1;
   for (int b = 0; b < nb; ++b) {
     const std::size_t ntx = 1 + r.below(b % 3 == 0 ? 3000 : 300);
     const std::size_t nrx = std::min<std::size_t>(ring / 2, ntx * (1 + r.below(2)) + r.below(5));
@@ -516,8 +536,8 @@ int run_pipeline(std::uint64_t seed) {
       }
       t.descriptor_index = static_cast<std::uint16_t>(i);
       t.checksum = static_cast<ChecksumMode>(r.below(3));
-      t.checksum_offload = r.below(4) != 0;
-      if (r.below(8) == 0) {
+      t.checksum_offload = late_case || r.below(4) != 0;
+      if (r.below(8) == 0 && !late_case) {
         t.tso_enabled = true;
         t.mss = static_cast<std::uint16_t>(200 + r.below(1200));
         t.header_length = 54;
@@ -558,6 +578,7 @@ int run_pipeline(std::uint64_t seed) {
 
   RssEngine rss_seq{rss_cfg}, rss_pipe{rss_cfg};
   cfg.rss = &rss_seq;
+  cfg.defer_rx_verify = false;  // the reference side: every batch's piece sums before its resolve
   cfg.enable_tx_interrupts = r.below(2);
   std::vector<CompletionEntry> irq_seq, irq_pipe;
   cfg.on_interrupt = [&irq_seq](std::uint16_t, const CompletionEntry& e) { irq_seq.push_back(e); };
@@ -567,6 +588,7 @@ int run_pipeline(std::uint64_t seed) {
   const bool keep = (seed >> 1) & 1;  // results_on_device on the pipelined side
   cfg.results_on_device = keep;
   cfg.overlap_resolve = seed % 3 != 1;  // the overlapped resolve (opt-in) on two sequences in three
+  cfg.defer_rx_verify = true;
   BatchedQueuePair pipe{cfg};
   bool view_ok = true;
   std::vector<RxBatchResult> want(nb), got;
@@ -656,15 +678,43 @@ int run_pipeline(std::uint64_t seed) {
          g.timings.host_image == himg;
     for (std::size_t i = 0; ok && i < w.tx_completions.size(); ++i) ok = same(w.tx_completions[i], g.tx_completions[i]);
     for (std::size_t i = 0; ok && i < w.rx_completions.size(); ++i) ok = same(w.rx_completions[i], g.rx_completions[i]);
-    if (!ok) std::fprintf(stderr, "pipeline seed %llu: batch %d differs\n", (unsigned long long) seed, b);
+    if (!ok) {
+      std::fprintf(stderr, "pipeline seed %llu: batch %d differs (deferred %d, device %d/%d, tx %zu/%zu rx %zu/%zu)\n",
+                   (unsigned long long) seed, b, (int) g.timings.deferred, (int) w.timings.device,
+                   (int) g.timings.device, w.tx_completions.size(), g.tx_completions.size(), w.rx_completions.size(),
+                   g.rx_completions.size());
+      for (std::size_t i = 0; i < std::min(w.rx_completions.size(), g.rx_completions.size()); ++i)
+        if (!same(w.rx_completions[i], g.rx_completions[i])) {
+          const CompletionEntry &x = w.rx_completions[i], &y = g.rx_completions[i];
+          std::fprintf(stderr, "  rx %zu: in order status %u strip %u tag %u ver %u | pipelined status %u strip %u tag %u ver %u\n",
+                       i, x.status, (unsigned) x.vlan_stripped, x.vlan_tag, (unsigned) x.checksum_verified, y.status,
+                       (unsigned) y.vlan_stripped, y.vlan_tag, (unsigned) y.checksum_verified);
+          break;
+        }
+      for (std::size_t i = 0; i < std::min(w.tx_completions.size(), g.tx_completions.size()); ++i)
+        if (!same(w.tx_completions[i], g.tx_completions[i])) {
+          std::fprintf(stderr, "  tx %zu: status %u / %u\n", i, w.tx_completions[i].status, g.tx_completions[i].status);
+          break;
+        }
+      if (w.rx_hash != g.rx_hash || w.rx_queue != g.rx_queue) std::fprintf(stderr, "  RSS results differ\n");
+    }
     g_pipe_host += !w.timings.device;
     g_pipe_overlapped += g.timings.overlapped && !g.timings.overlap_redone;
     g_pipe_redone += g.timings.overlap_redone;
+    g_pipe_late += g.timings.deferred;
   }
   g_pipe_batches += nb;
   if (dev_desc) g_pipe_devdesc += nb;
   if (himg) g_pipe_himg += nb;
-  ok = ok && std::memcmp(&seq.stats(), &pipe.stats(), sizeof(QueuePairStats)) == 0;
+  if (std::memcmp(&seq.stats(), &pipe.stats(), sizeof(QueuePairStats)) != 0) {
+    const auto* x = reinterpret_cast<const std::uint64_t*>(&seq.stats());
+    const auto* y = reinterpret_cast<const std::uint64_t*>(&pipe.stats());
+    std::fprintf(stderr, "pipeline seed %llu: stats differ:", (unsigned long long) seed);
+    for (std::size_t k = 0; k < sizeof(QueuePairStats) / 8; ++k)
+      if (x[k] != y[k]) std::fprintf(stderr, " [%zu] %llu/%llu", k, (unsigned long long) x[k], (unsigned long long) y[k]);
+    std::fprintf(stderr, "\n");
+    ok = false;
+  }
   bool irq_ok = irq_seq.size() == irq_pipe.size();
   for (std::size_t i = 0; irq_ok && i < irq_seq.size(); ++i) irq_ok = same(irq_seq[i], irq_pipe[i]);
   if (!irq_ok) std::fprintf(stderr, "pipeline seed %llu: interrupt callbacks differ\n", (unsigned long long) seed);
@@ -1370,11 +1420,15 @@ int main(int argc, char** argv) {
                    g_pipe_overlapped, g_pipe_redone);
       return 1;
     }
+    if (count >= 10 && g_pipe_late == 0) {
+      std::fprintf(stderr, "pipeline: no batch deferred its RX verifies\n");
+      return 1;
+    }
     std::printf("rx_stage_gpu_fuzz pipeline: ok (%llu sequences, %zu batches, %zu of them on the host path, %zu "
                 "with device descriptors, %zu on a HostMemory, %zu results left on the device; overlapped "
-                "resolves: %zu stood, %zu redone behind earlier writes)\n",
+                "resolves: %zu stood, %zu redone behind earlier writes; %zu with the RX verifies deferred)\n",
                 (unsigned long long) count, g_pipe_batches, g_pipe_host, g_pipe_devdesc, g_pipe_himg, g_keep,
-                g_pipe_overlapped, g_pipe_redone);
+                g_pipe_overlapped, g_pipe_redone, g_pipe_late);
     return 0;
   }
   if (argc > 1 && std::strcmp(argv[1], "full") == 0) {
@@ -1390,9 +1444,15 @@ int main(int argc, char** argv) {
   int bad = 0;
   for (std::uint64_t s = first; s < first + count; ++s) bad += run_case(s);
   if (bad) return 1;
+  if (count >= 30 && (g_late == 0 || g_late_fail == 0)) {
+    std::fprintf(stderr, "fuzz: %zu batches deferred their RX verifies (%zu failed): both expected\n", g_late, g_late_fail);
+    return 1;
+  }
   std::printf("rx_stage_gpu_fuzz: ok (%llu batches, %zu resolved on the device, %zu of them with a host tail, %zu "
               "running out of RX descriptors, %zu with device descriptors, %zu with results left on the device, "
-              "%zu interrupt callbacks equal, %zu also on a HostMemory (%zu staged per descriptor))\n",
-              (unsigned long long) count, g_device, g_tail, g_short, g_devdesc, g_keep, g_irq, g_himg, g_himg_sparse);
+              "%zu interrupt callbacks equal, %zu also on a HostMemory (%zu staged per descriptor); %zu with the RX "
+              "verifies deferred to the delivery, %zu of those failing)\n",
+              (unsigned long long) count, g_device, g_tail, g_short, g_devdesc, g_keep, g_irq, g_himg, g_himg_sparse,
+              g_late, g_late_fail);
   return 0;
 }

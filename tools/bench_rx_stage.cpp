@@ -341,11 +341,11 @@ int main(int argc, char** argv) {
   const auto& T = tot[tot.size() / 2].second;  // the median batch's phases
   std::printf(
       "{\"row\": \"f1_rx_stage\", \"workload\": \"%s\", \"resolve\": \"%s\", \"descriptors\": \"%s\", \"mode\": \"%s\", \"results\": \"%s\", \"host_threads\": %u, \"tx_descriptors\": %zu, \"rx_completions\": %zu, \"rx_align\": %zu, "
-      "\"rx_success\": %zu, \"host_memory\": %s, \"tx_staged_whole\": %s, \"overlapped_resolve\": %s, \"overlap_redone\": %s, \"interrupts\": %s, \"irq_callbacks\": %llu, \"callback_floor_us\": %.1f, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
+      "\"rx_success\": %zu, \"host_memory\": %s, \"tx_staged_whole\": %s, \"overlapped_resolve\": %s, \"overlap_redone\": %s, \"deferred\": %s, \"interrupts\": %s, \"irq_callbacks\": %llu, \"callback_floor_us\": %.1f, \"us_median\": %.1f, \"mpkt_s\": %.3f, \"frame_GBps\": %.2f, "
       "\"phases_us\": {\"check\": %.1f, \"plan\": %.1f, \"gpu_sums\": %.1f, \"resolve\": %.1f, \"gpu_gather\": %.1f, \"gpu_rss\": %.1f, \"copy\": %.1f, \"irq\": %.1f, \"irq_wait\": %.1f}}\n",
       wl.c_str(), T.device ? "device" : "host", desc_kind.c_str(), pipelined ? "pipelined" : "sync", cfg.results_on_device ? "device" : "host", cfg.host_threads, n, last.rx_completions.size(), rx_align, ok,
       T.host_image ? "true" : "false", T.staged_whole ? "true" : "false", T.overlapped ? "true" : "false",
-      T.overlap_redone ? "true" : "false", irq ? "true" : "false", (unsigned long long) irq_batches, floor_us, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
+      T.overlap_redone ? "true" : "false", T.deferred ? "true" : "false", irq ? "true" : "false", (unsigned long long) irq_batches, floor_us, med, n / med, frame_bytes / med / 1e3, T.check_us, T.plan_us, T.sums_us,
       T.resolve_us, T.gather_us, T.rss_us, T.copy_us, T.irq_us, T.irq_wait_us);
   nicgpu_free(mem);
   if (ptx) nicgpu_host_free(ptx);
