@@ -424,6 +424,7 @@ private:
   void deliver(Slot& sl, const DeviceHostMemory& mem, std::size_t a, std::size_t b, unsigned flags,
                const nicgpu_rss_ctx* rctx, std::uint64_t* hits, void* stream);
   void finish(Slot& sl, RxBatchResult& out, QueuePairStats* st);
+  static void apply_fixups(Slot& sl, std::size_t s, QueuePairStats& st);
   void enqueue(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                const DeviceDescriptors* d, void* stream, HostImage* img = nullptr);
   void check_rings_unwritten(Slot& sl, const DeviceHostMemory& mem, void* stream);
@@ -437,6 +438,7 @@ private:
                std::vector<rx_stage_detail::SegmentWrite>* applied = nullptr);
   BatchedQueuePairConfig config_;
   BatchedQueuePairConfig quiet_;  // config_ without the interrupt callback (every resolve; replayed after)
+  bool defer_multi_ = false;      // process_queues: this fused batch may defer its RX verifies
   QueuePairStats stats_{};
   std::unique_ptr<Scratch> scratch_;
 };

@@ -482,18 +482,19 @@ int nicgpu_qp_walks(const nicgpu_qp* q, uint64_t* walks);
  * batch are therefore final only after its deliveries; nicgpu_qp_deferred
  * tells, after nicgpu_qp_resolve_finish, whether the last batch deferred.
  * Its host-resolved rest (*done < ntx) needs nicgpu_qp_resum first: the
- * piece sums were skipped.  Unsegmented batches only; the synchronous
- * nicgpu_qp_plan / _plan_on always sum. */
+ * piece sums were skipped.  Segmented batches too (each segment's
+ * corrections apart).  The synchronous nicgpu_qp_plan / _plan_on always sum. */
 int nicgpu_qp_set_deferred_verify(nicgpu_qp* q, int on);
 int nicgpu_qp_deferred(const nicgpu_qp* q, int* deferred);
 /* The deferred verifies' running corrections of q since it was created, on
- * `stream` into out[NICGPU_QP_FIXUPS]: [0] verifies that failed (each a
+ * `stream` into out[nseg][NICGPU_QP_FIXUPS] (nseg: 1, or the segments of a
+ * segmented batch, each its queue pair's): [0] verifies that failed (each a
  * drops_checksum the statistics lack and an rx_packets and tx_packets they
  * hold too many), then what they hold too many of: [1] rx_bytes, [2]
- * rx_vlan_strips, [3] tx_bytes, [4] tx_vlan_insertions.  A caller keeps the
- * last values and applies the difference. */
-#define NICGPU_QP_FIXUPS 5u
-int nicgpu_qp_verify_fixups_async(nicgpu_qp* q, uint64_t* out, void* stream);
+ * rx_vlan_strips, [3] tx_bytes, [4] tx_vlan_insertions; [5..7] 0.  A caller
+ * keeps the last values and applies the difference. */
+#define NICGPU_QP_FIXUPS 8u
+int nicgpu_qp_verify_fixups_async(nicgpu_qp* q, uint64_t* out, size_t nseg, void* stream);
 /* The frames of view.rxc[0, nrx) delivered with Success, as RSS descriptors
  * (view.rss_desc[0, m), lengths clipped to NICGPU_MAX_PACKET), m written to
  * the device scalar view.rss_count; view.rx_hash / rx_queue reset to 0 /

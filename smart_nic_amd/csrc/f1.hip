@@ -163,7 +163,9 @@ struct DeliverParams {
   const unsigned long long* lateflag;
   unsigned long long late_gen;
   uint64_t late_n;
-  unsigned long long* fix;
+  unsigned long long* fix;  // [segment][NICGPU_QP_FIXUPS]
+  const nicgpu_qp_segment* seg;  // a segmented batch's table (its completion's segment), or null
+  uint32_t nseg;
 };
 
 // Tuning-only modes of deliver_kernel (libnicgpu_tune.so, tools/f1_deliver_bench.py;
@@ -636,11 +638,21 @@ __device__ __forceinline__ void deliver_tiles(const DeliverParams& P) {
             const Win I0 = wins[lane * 3u], I1 = wins[lane * 3u + 1u], I2 = wins[lane * 3u + 2u];
             const uint64_t len_a = (uint32_t) (I1.hi + 16u - I1.lo), len_b = (uint32_t) (I2.hi + 16u - I2.lo);
             const uint64_t size = (uint64_t) (uint32_t) (I0.hi + 16u - I0.lo) + len_a + len_b;
-            atomicAdd(&P.fix[0], 1ull);
-            atomicAdd(&P.fix[1], (unsigned long long) size);
-            if (e.vlan_stripped) atomicAdd(&P.fix[2], 1ull);
-            atomicAdd(&P.fix[3], (unsigned long long) (len_a + len_b + ((lb & nicqp::kLateStripBase) ? 4u : 0u)));
-            if (lb & nicqp::kLateVlanInsert) atomicAdd(&P.fix[4], 1ull);
+            uint32_t sg = 0;  // the completion's segment: the last whose ring starts at or before j
+            if (P.seg) {
+              uint32_t hi = P.nseg;
+              while (hi - sg > 1u) {
+                const uint32_t mid = (sg + hi) / 2u;
+                if (P.seg[mid].rx_begin <= j) sg = mid;
+                else hi = mid;
+              }
+            }
+            unsigned long long* fx = P.fix + (uint64_t) sg * NICGPU_QP_FIXUPS;
+            atomicAdd(&fx[0], 1ull);
+            atomicAdd(&fx[1], (unsigned long long) size);
+            if (e.vlan_stripped) atomicAdd(&fx[2], 1ull);
+            atomicAdd(&fx[3], (unsigned long long) (len_a + len_b + ((lb & nicqp::kLateStripBase) ? 4u : 0u)));
+            if (lb & nicqp::kLateVlanInsert) atomicAdd(&fx[4], 1ull);
             e.status = nicqp::kChecksumError;
             e.vlan_stripped = false;
             e.vlan_tag = 0;
@@ -1168,7 +1180,7 @@ struct QpDevSink {
 // reset before the launch), so the 32-bit scan of the counts (n <= 2^32 /
 // kQpMaxPieces) cannot wrap and the caller sees the flag.
 constexpr uint32_t kQpMaxPieces = 256;
-// Also whether the batch may defer its RX verifies (defer, unsegmented): g[7]
+// Also whether the batch may defer its RX verifies (defer): g[7]
 // becomes the generation when it may not — a packet with a TX verify or more
 // than one segment, whose pops a sum can change (qp_logic.h Ctx::late).
 __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
@@ -1177,7 +1189,7 @@ __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_desc
                                                             unsigned long long gen, QpSegs S, uint32_t defer) {
   const QpRange R = qp_range(S, n);
   const uint64_t mtu = qp_max_mtu(max_mtu, S, R.s);
-  const bool may = defer != 0u && !S.seg;
+  const bool may = defer != 0u;
   bool needs = false;
   for (uint64_t i = R.i; i < R.end; i += R.step) {
     QpPlan pp;
@@ -2097,8 +2109,8 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
       hipMalloc(&q->dlv_done, sizeof(unsigned int)) != hipSuccess ||
       hipMemset(q->dlv_done, 0, sizeof(unsigned int)) != hipSuccess ||
       hipMalloc(&q->gflags, 8 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc(&q->fix, 8 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMemset(q->fix, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&q->fix, (size_t) NICGPU_QP_MAX_SEGMENTS * NICGPU_QP_FIXUPS * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(q->fix, 0, (size_t) NICGPU_QP_MAX_SEGMENTS * NICGPU_QP_FIXUPS * sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&q->bounds, 8 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(q->bounds, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(q->gflags, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
@@ -2463,8 +2475,8 @@ int nicgpu_qp_resolve_finish(nicgpu_qp* q, uint64_t* done, uint64_t* rx_used, ui
     used = part[0];
   }
   std::memcpy(stats, part + 3, kQpStats * sizeof(uint64_t));
-  q->late_used = used;  // the completions the device resolved (deferred ones among them)
-  if (q->nseg) used = q->seg_nrx;  // every slot of the concatenated ring (the unused ones marked)
+  if (q->nseg) used = q->seg_nrx;
+  q->late_used = used;  // the completions the device resolved (deferred ones among them)  // every slot of the concatenated ring (the unused ones marked)
   *done = lim;
   *rx_used = used;
   if (rx_settled) *rx_settled = settled < used ? settled : used;
@@ -2483,10 +2495,10 @@ int nicgpu_qp_deferred(const nicgpu_qp* q, int* deferred) {
   return NICGPU_OK;
 }
 
-int nicgpu_qp_verify_fixups_async(nicgpu_qp* q, uint64_t* out, void* stream) {
-  if (!q || !out) return NICGPU_ERR_INVALID;
+int nicgpu_qp_verify_fixups_async(nicgpu_qp* q, uint64_t* out, size_t nseg, void* stream) {
+  if (!q || !out || nseg == 0 || nseg > NICGPU_QP_MAX_SEGMENTS) return NICGPU_ERR_INVALID;
   DeviceGuard g(q->device);
-  return hip_status(hipMemcpyAsync(out, q->fix, NICGPU_QP_FIXUPS * sizeof(uint64_t), hipMemcpyDeviceToHost,
+  return hip_status(hipMemcpyAsync(out, q->fix, nseg * NICGPU_QP_FIXUPS * sizeof(uint64_t), hipMemcpyDeviceToHost,
                                    static_cast<hipStream_t>(stream)));
 }
 
@@ -2644,12 +2656,14 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
   P.rss.mode = tuple_mode;
   P.rss.raw_off = raw_off;
   P.rss.raw_len = raw_len;
-  if (q->defer_verify && q->nseg == 0) {  // (the kernel reads whether the plan deferred)
+  if (q->defer_verify) {  // (the kernel reads whether the plan deferred)
     P.late = q->late;
     P.lateflag = q->gflags + 7;
     P.late_gen = q->plan_gen;
     P.late_n = (flags & NICGPU_DELIVER_SETTLED) ? ~0ull : q->late_used;
     P.fix = q->fix;
+    P.seg = q->nseg ? q->d_seg : nullptr;
+    P.nseg = q->nseg;
   }
   if (rss) {
     P.rss.lut = ctx->d_lut;

@@ -871,6 +871,15 @@ void check_at(int st, const char* what, int line) {
 // (the call site in the message: one failing HIP call among many alike)
 #define check(st, what) check_at((st), (what), __LINE__)
 
+// BatchedQueuePairConfig::defer_rx_verify unless NIC_DEFER_VERIFY=0 (tuning A/B)
+bool defer_env() {
+  static const bool on = [] {
+    const char* e = std::getenv("NIC_DEFER_VERIFY");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 // One growable device buffer.
 struct DevBuf {
   void* p = nullptr;
@@ -1141,10 +1150,20 @@ struct BatchedQueuePair::Slot {
   std::size_t irq_ntx = 0, irq_nrx = 0;
   // deferred RX verify (nicgpu_qp_set_deferred_verify): the batch's completions
   // and statistics are final after its deliveries; the context's running
-  // corrections come down into h_fix, fix_seen the last applied
+  // corrections (per segment of a fused batch) come down into h_fix, fix_seen
+  // the last applied
   bool late = false;
   HostBuf h_fix;
-  std::uint64_t fix_seen[NICGPU_QP_FIXUPS] = {};
+  std::vector<std::uint64_t> fix_seen;
+  // this batch's corrections (a segment's row: s * NICGPU_QP_FIXUPS), the
+  // seen values moved on
+  std::uint64_t fix_delta(std::size_t s, unsigned k) {
+    const std::size_t i = s * NICGPU_QP_FIXUPS + k;
+    if (fix_seen.size() <= i) fix_seen.resize(i + 1, 0);
+    const std::uint64_t now = static_cast<const std::uint64_t*>(h_fix.p)[i], d = now - fix_seen[i];
+    fix_seen[i] = now;
+    return d;
+  }
 
   void release_rss() {
     if (!rss_released) rss_recorded.set_value();
@@ -1176,7 +1195,7 @@ struct BatchedQueuePair::Slot {
   }
   void create(int dev) {
     check(nicgpu_qp_create(&qp, dev), "nicgpu_qp_create");
-    for (std::uint64_t& f : fix_seen) f = 0;  // a new context's corrections start at 0
+    fix_seen.clear();  // a new context's corrections start at 0
     for (void** e : {&ev_tx, &ev_rx, &ev_resolved, &ev_done, &ev_submit, &ev_staged, &ev_wb, &ev_gate})
       check(nicgpu_event_create(e), "nicgpu_event_create");
     for (auto& side : ev_irq)
@@ -1866,11 +1885,7 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
   // 32-bit piece indices allow, makes the resolve settle nothing and its
   // finish return NICGPU_ERR_RANGE — that batch then takes the host path
   // (which refuses it if its total does not fit either), the next one fits
-  static const bool defer_env = [] {  // tuning A/B: NIC_DEFER_VERIFY=0
-    const char* e = std::getenv("NIC_DEFER_VERIFY");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  check(nicgpu_qp_set_deferred_verify(sl.qp, config_.defer_rx_verify && defer_env ? 1 : 0),
+  check(nicgpu_qp_set_deferred_verify(sl.qp, config_.defer_rx_verify && defer_env() ? 1 : 0),
         "nicgpu_qp_set_deferred_verify");
   check(nicgpu_qp_plan_async(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu,
                              &v, ps, rs),
@@ -2147,9 +2162,11 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
     // a deferred-verify batch: its completions are final now, and its
     // statistics' corrections come down with them
     if (ok && !keep && sl.late) completions_down();
-    if (ok && sl.late)
-      ok = j.ok(nicgpu_qp_verify_fixups_async(sl.qp, sl.h_fix.get<std::uint64_t>(NICGPU_QP_FIXUPS), S.side_down),
+    if (ok && sl.late) {
+      const std::size_t ns = sl.multi ? sl.nseg : 1;
+      ok = j.ok(nicgpu_qp_verify_fixups_async(sl.qp, sl.h_fix.get<std::uint64_t>(ns * NICGPU_QP_FIXUPS), ns, S.side_down),
                 "nicgpu_qp_verify_fixups_async");
+    }
     // a fused batch: the lists split per queue pair (entries made relative to
     // each queue pair's ring), and its per-queue-pair hits when it needs them
     // (its per-queue-pair hits beside the lists, on the interrupt stream, which
@@ -2213,6 +2230,20 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
   }
 }
 
+// The deferred verifies of segment s that failed in the batch just finished:
+// its statistics took them as delivered (queue_pair.cpp:434-447 counts a drop
+// instead, and neither the RX nor the finalized TX counters).
+void BatchedQueuePair::apply_fixups(Slot& sl, std::size_t s, QueuePairStats& st) {
+  const std::uint64_t failed = sl.fix_delta(s, 0);
+  st.drops_checksum += failed;
+  st.rx_packets -= failed;
+  st.tx_packets -= failed;
+  st.rx_bytes -= sl.fix_delta(s, 1);
+  st.rx_vlan_strips -= sl.fix_delta(s, 2);
+  st.tx_bytes -= sl.fix_delta(s, 3);
+  st.tx_vlan_insertions -= sl.fix_delta(s, 4);
+}
+
 // The downloads waited for everything the batch did on the caller's stream,
 // so the image holds its writes once they are done.
 void BatchedQueuePair::finish(Slot& sl, RxBatchResult& out, QueuePairStats* st) {
@@ -2224,24 +2255,9 @@ void BatchedQueuePair::finish(Slot& sl, RxBatchResult& out, QueuePairStats* st) 
   } reset{sl};
   sl.down->finish();
   sl.wait_writeback();
-  if (sl.late) {
-    // the deferred verifies that failed since the last batch of this context:
-    // the statistics took them as delivered (queue_pair.cpp:434-447 counts a
-    // drop instead, and neither the RX nor the finalized TX counters)
+  if (sl.late && !sl.multi) {  // (a fused batch's, per queue pair, are process_queues')
     if (!st) throw std::logic_error("finish: a deferred-verify batch without its statistics");
-    const std::uint64_t* f = static_cast<const std::uint64_t*>(sl.h_fix.p);
-    std::uint64_t d[NICGPU_QP_FIXUPS];
-    for (unsigned k = 0; k < NICGPU_QP_FIXUPS; ++k) {
-      d[k] = f[k] - sl.fix_seen[k];
-      sl.fix_seen[k] = f[k];
-    }
-    st->drops_checksum += d[0];
-    st->rx_packets -= d[0];
-    st->tx_packets -= d[0];
-    st->rx_bytes -= d[1];
-    st->rx_vlan_strips -= d[2];
-    st->tx_bytes -= d[3];
-    st->tx_vlan_insertions -= d[4];
+    apply_fixups(sl, 0, *st);
   }
   if (sl.rss && !sl.multi) {  // (a fused batch's accounting and lists are process_queues')
     const std::uint64_t m = sl.meta[0];
@@ -2523,6 +2539,7 @@ bool BatchedQueuePair::front_multi(Slot& sl, const DeviceHostMemory& mem, std::s
   auto t = clock::now();
   check(nicgpu_stream_wait_event(ps, sl.ev_tx), "nicgpu_stream_wait_event");
   if (sl.staged) check(nicgpu_stream_wait_event(stream, sl.ev_staged), "nicgpu_stream_wait_event");
+  check(nicgpu_qp_set_deferred_verify(sl.qp, defer_multi_ ? 1 : 0), "nicgpu_qp_set_deferred_verify");
   check(nicgpu_qp_plan_async(sl.qp, reinterpret_cast<const std::uint8_t*>(mem.base), mem.size, ntx, config_.max_mtu, &v,
                              ps, stream),
         "nicgpu_qp_plan_async");
@@ -2566,7 +2583,10 @@ bool BatchedQueuePair::front_multi(Slot& sl, const DeviceHostMemory& mem, std::s
   check(nicgpu_qp_walks(sl.qp, &walks1), "nicgpu_qp_walks");
   out.timings.walked = out.timings.walked || walks1 != walks0;
   out.timings.resolve_us += us_since(t);
-  sl.late = false;  // (segmented batches never defer their RX verifies)
+  int late = 0;
+  check(nicgpu_qp_deferred(sl.qp, &late), "nicgpu_qp_deferred");
+  sl.late = rst == NICGPU_OK && late != 0;
+  out.timings.deferred = sl.late;
   if (rst == NICGPU_ERR_AGAIN) {
     again = 1;
     return false;
@@ -2683,6 +2703,9 @@ bool BatchedQueuePair::process_queues(const DeviceHostMemory& mem_in, HostImage*
   bool own_engines = false;
   for (std::size_t q = 1; q < Q; ++q) own_engines |= configs[q].rss != rss0;
   sl.seg_hits_on = rss0 != nullptr && own_engines;
+  // deferred RX verify when this stage and every queue pair's configuration allow it
+  defer_multi_ = config_.defer_rx_verify && defer_env();
+  for (std::size_t q = 0; q < Q; ++q) defer_multi_ = defer_multi_ && configs[q].defer_rx_verify;
   bool ok = false;
   try {
     for (int attempt = 0;; ++attempt) {
@@ -2727,6 +2750,7 @@ bool BatchedQueuePair::process_queues(const DeviceHostMemory& mem_in, HostImage*
     const std::size_t tb = seg[q].tx_begin, rb = seg[q].rx_begin, nt = tx[q].size(), nr = used[q];
     static_assert(sizeof(QueuePairStats) == sizeof(nicgpu_qp_stats));
     std::memcpy(static_cast<void*>(&stats[q]), &ds[q], sizeof(QueuePairStats));
+    if (sl.late) apply_fixups(sl, q, stats[q]);
     o.tx_processed = nt;
     o.rx_consumed = nr;
     o.timings = cat.timings;

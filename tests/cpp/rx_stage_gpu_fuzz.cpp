@@ -1245,7 +1245,7 @@ int run_rings() {
 // RSS through one shared engine or one engine per queue pair (equal configs);
 // results on the host or left on the device; one sequence in three on a
 // HostMemory.  Two rounds per seed (ring leftovers carried over).
-std::size_t g_qm_fused = 0, g_qm_rounds = 0, g_qm_himg = 0;
+std::size_t g_qm_fused = 0, g_qm_rounds = 0, g_qm_himg = 0, g_qm_late = 0;
 int run_qm(std::uint64_t seed) {
   Rng r{seed * 6151 + 17};
   const std::size_t Q = 1 + r.below(12);
@@ -1255,6 +1255,9 @@ int run_qm(std::uint64_t seed) {
   for (auto& b : image) b = r.byte();
   const bool shared_engine = r.below(2) == 0, rss_on = r.below(5) != 0, keep = r.below(3) == 0;
   const bool himg = r.below(3) == 0;
+  // one manager in three: drains the fused batch resolves with its RX
+  // verifies deferred to the delivery (no TX verify, no TSO)
+  const bool late_case = seed % 3 == 2;
   std::vector<std::uint16_t> table(64 + r.below(100));
   for (auto& t : table) t = static_cast<std::uint16_t>(r.below(24));
   const RssConfig rss_cfg{kMsKey, table};
@@ -1297,9 +1300,9 @@ int run_qm(std::uint64_t seed) {
         t.length = static_cast<std::uint32_t>(L);
         t.descriptor_index = static_cast<std::uint16_t>(i);
         t.checksum = static_cast<ChecksumMode>(r.below(3));
-        t.checksum_offload = r.below(4) != 0;
+        t.checksum_offload = late_case || r.below(4) != 0;
         t.checksum_value = static_cast<std::uint16_t>(r.below(65536));
-        if (r.below(8) == 0) {
+        if (r.below(8) == 0 && !late_case) {
           t.tso_enabled = true;
           t.mss = static_cast<std::uint16_t>(100 + r.below(1400));
           t.header_length = static_cast<std::uint16_t>(14 + r.below(60));
@@ -1345,6 +1348,7 @@ int run_qm(std::uint64_t seed) {
     else qm.process_batch(DeviceHostMemory{static_cast<std::byte*>(d), mem_size}, b, got);
     g_qm_fused += qm.last_fused();
     g_qm_rounds += 1;
+    if (qm.last_fused() && !got.empty() && got[0].timings.deferred) g_qm_late += 1;
     for (std::size_t q = 0; q < Q && ok; ++q) {
       RxBatchResult& g = got[q];
       if (keep && !materialize(g)) {
@@ -1400,8 +1404,13 @@ int main(int argc, char** argv) {
     int bad = 0;
     for (std::uint64_t s = 1; s <= count; ++s) bad += run_qm(s);
     if (bad) return 1;
-    std::printf("rx_stage_gpu_fuzz qm: ok (%llu managers, %zu of %zu drains fused, %zu on a HostMemory)\n",
-                (unsigned long long) count, g_qm_fused, g_qm_rounds, g_qm_himg);
+    if (count >= 20 && g_qm_late == 0) {
+      std::fprintf(stderr, "qm: no fused drain deferred its RX verifies\n");
+      return 1;
+    }
+    std::printf("rx_stage_gpu_fuzz qm: ok (%llu managers, %zu of %zu drains fused, %zu on a HostMemory, %zu fused "
+                "drains with the RX verifies deferred)\n",
+                (unsigned long long) count, g_qm_fused, g_qm_rounds, g_qm_himg, g_qm_late);
     return 0;
   }
   if (argc > 1 && std::strcmp(argv[1], "pipeline") == 0) {
