@@ -4,6 +4,8 @@
 # descriptors).  No tests (run them on the tree first).
 #   /usr/local/graft/bin/gpurun --timeout 600 -- 'bash scripts/gpu_r05_ab.sh'
 set -o pipefail
+# (ab_old/ must travel: a missing directory would silently load the tree's libraries through the rpath)
+[ -f ab_old/libnicgpu.so ] && [ -f ab_old/libnic_host.so ] || { echo "ab_old/ missing on the box"; exit 1; }
 mkdir -p gpurun_out/ab
 : > gpurun_out/ab/ab.txt
 for rep in 1 2 3; do

@@ -1092,7 +1092,7 @@ constexpr unsigned kQpStats = 16;
 // batch's 16 stats totals — the one download a resolve needs
 constexpr unsigned kQpTail = 3 + 16 + 3;  // ... then [19] the plan overflowed (1 buffers, 2 pieces per descriptor), [20] its piece count, [21] RX verify deferred
 constexpr int kQpRelaxSteps = 8;  // position relaxations before the host takes the rest
-constexpr unsigned kQpBoundsAt = 8;  // misc()[8..11]: the check's bounds, [12..15] their presets
+constexpr unsigned kQpBoundsAt = 8;  // misc()[12..15]: the check's bounds' presets
 
 // Segmented batches (several queue pairs, nicgpu_qp_set_segments): each grid
 // block serves one segment — blocks in proportion to its TX descriptors — so a
@@ -1775,6 +1775,12 @@ __global__ __launch_bounds__(kQpBlock) void qp_check_kernel(const nicgpu_tx_desc
         key = (uint64_t) s << kQpSegShift;
       }
       const uint64_t ring_end = hi;
+      if constexpr (SIMPLE) {
+        // every span nonempty and (when the verdict stands) ascending: a TX
+        // span before the range's first RX span or past its last meets none —
+        // two reads instead of a search (a TX region apart from the ring)
+        if (lo < hi && (a + len <= rx[lo].buffer_address || (key | a) >= end_at(hi - 1))) continue;
+      }
       while (lo < hi) {
         const uint64_t mid = lo + (hi - lo) / 2;
         if (end_at(mid) <= (key | a)) lo = mid + 1;
@@ -1857,13 +1863,13 @@ struct nicgpu_qp {
   uint32_t *queue_which = nullptr, *queue_start = nullptr, *queue_end = nullptr;
   size_t c_sk = 0, c_qw = 0, c_em = 0, c_key = 0;
   uint64_t* end_max = nullptr;  // [nrx] nicgpu_qp_check's running max of RX span ends
-  unsigned long long* bounds = nullptr;  // [4] the check's TX and RX bounds (nicgpu_qp_check_bounds)
+  unsigned long long* bounds = nullptr;  // [8] the check's TX and RX bounds (nicgpu_qp_check_bounds), [4] empty-span flag, [5..6] its two flags
   unsigned long long* scal = nullptr;
   unsigned long long* dlv_acc = nullptr;  // the delivery's accumulator (DeliverParams::acc), zero between launches
   size_t c_dlv_acc = 0;
   unsigned int* dlv_done = nullptr;       // its done ticket
   // zeroed once; flags are set to a call's generation: [0] a descriptor plans
-  // > 256 pieces, [1..2] the check's, [3] the plan does not fit; then the
+  // > 256 pieces, [1..2] unused, [3] the plan does not fit; then the
   // device piece counts [4] the sums' (below), [5] count, [6] min(count,
   // capacity); [7] the plan's batch may not defer its RX verifies
   unsigned long long* gflags = nullptr;
@@ -1886,7 +1892,9 @@ struct nicgpu_qp {
   // flags, relax verdict
   uint64_t* hp = nullptr;
   uint64_t* misc() const { return hp + kQpTail; }
-  uint64_t* hp_simple = nullptr;  // page-locked: the simple check's "empty span" flag
+  // page-locked: the check's download — bounds[0..3], the simple form's
+  // "empty span" flag, the unsorted-ring and TX-meets-RX flags (bounds[4..6])
+  uint64_t* hp_chk = nullptr;
   unsigned grid = 1;
   // blocks the partials hold: the grid, or one per segment of the largest table
   unsigned part_blocks() const { return grid > NICGPU_QP_MAX_SEGMENTS ? grid : NICGPU_QP_MAX_SEGMENTS; }
@@ -2025,8 +2033,8 @@ int qp_walk(nicgpu_qp* q, const QpCtx& C, const QpSegs& S, uint64_t ntx, unsigne
 }
 
 // The overlap check's launches on s: (simple) the scan-free kernel, or the
-// running-max scan then the kernel; the flags and the bounds come down into
-// misc() and q->checked is recorded.
+// running-max scan then the kernel; bounds and flags (bounds[0..6]) come down
+// into hp_chk and q->checked is recorded.
 int qp_check_enqueue(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, bool segmented, bool simple,
                      hipStream_t s, unsigned long long gen) {
   // the bounds' presets (page-locked source, constant: no hazard with an
@@ -2062,18 +2070,14 @@ int qp_check_enqueue(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, bo
     const QpSegs S = segmented ? qp_segs(q) : QpSegs{nullptr, nullptr, 0u};
     if (simple)
       hipLaunchKernelGGL(qp_check_kernel<true>, dim3(qp_grid(q, n)), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, q->rx,
-                         (uint64_t) nrx, mem_size, q->end_max, q->gflags + 1, gen, S, q->bounds);
+                         (uint64_t) nrx, mem_size, q->end_max, q->bounds + 5, gen, S, q->bounds);
     else
       hipLaunchKernelGGL(qp_check_kernel<false>, dim3(qp_grid(q, n)), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx,
-                         q->rx, (uint64_t) nrx, mem_size, q->end_max, q->gflags + 1, gen, S, q->bounds);
+                         q->rx, (uint64_t) nrx, mem_size, q->end_max, q->bounds + 5, gen, S, q->bounds);
     st = hip_status(hipGetLastError());
   }
-  uint64_t* f = q->misc() + 1;
-  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(f, q->gflags + 1, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  if (st == NICGPU_OK)
-    st = hip_status(hipMemcpyAsync(q->misc() + kQpBoundsAt, q->bounds, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  if (st == NICGPU_OK)
-    st = hip_status(hipMemcpyAsync(&q->hp_simple[0], q->bounds + 4, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  // one download: bounds, the simple form's empty-span flag, the two flags
+  if (st == NICGPU_OK) st = hip_status(hipMemcpyAsync(q->hp_chk, q->bounds, 7 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   if (st == NICGPU_OK) st = hip_status(hipEventRecord(q->checked, s));
   return st;
 }
@@ -2118,11 +2122,11 @@ int nicgpu_qp_create(nicgpu_qp** out, int device) {
     return NICGPU_ERR_NOMEM;
   }
   if (hipHostMalloc(reinterpret_cast<void**>(&q->hp), (kQpTail + 16) * sizeof(uint64_t)) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&q->hp_simple), 8 * sizeof(uint64_t)) != hipSuccess) {
+      hipHostMalloc(reinterpret_cast<void**>(&q->hp_chk), 8 * sizeof(uint64_t)) != hipSuccess) {
     nicgpu_qp_destroy(q);
     return NICGPU_ERR_NOMEM;
   }
-  std::memset(q->hp_simple, 0, 8 * sizeof(uint64_t));  // no generation is 0
+  std::memset(q->hp_chk, 0, 8 * sizeof(uint64_t));  // no generation is 0
   if (hipEventCreateWithFlags(&q->planned, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&q->resolved, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&q->checked, hipEventDisableTiming) != hipSuccess) {
@@ -2145,7 +2149,7 @@ int nicgpu_qp_destroy(nicgpu_qp* q) {
   for (void* b : bufs)
     if (b) (void) hipFree(b);
   if (q->hp) (void) hipHostFree(q->hp);
-  if (q->hp_simple) (void) hipHostFree(q->hp_simple);
+  if (q->hp_chk) (void) hipHostFree(q->hp_chk);
   if (q->seg_hp) (void) hipHostFree(q->seg_hp);
   if (q->seg_stage) (void) hipHostFree(q->seg_stage);
   if (q->planned) (void) hipEventDestroy(q->planned);
@@ -2309,7 +2313,7 @@ int nicgpu_qp_check_flags(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nr
 
 int nicgpu_qp_check_bounds(const nicgpu_qp* q, uint64_t* bounds) {
   if (!q || !bounds || q->chk_on || q->nseg) return NICGPU_ERR_INVALID;
-  std::memcpy(bounds, q->misc() + kQpBoundsAt, 4 * sizeof(uint64_t));
+  std::memcpy(bounds, q->hp_chk, 4 * sizeof(uint64_t));
   return NICGPU_OK;
 }
 
@@ -2328,7 +2332,7 @@ int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict) {
   DeviceGuard g(q->device);
   int st = hip_status(hipEventSynchronize(q->checked));
   if (st != NICGPU_OK) return st;
-  if (q->hp_simple[0] == q->chk_gen) {  // a span that receives nothing: the scan form
+  if (q->hp_chk[4] == q->chk_gen) {  // a span that receives nothing: the scan form
     const nicgpu_qp::CheckArgs& A = q->chk_args;
     const unsigned long long gen = ++q->gen;
     st = qp_check_enqueue(q, A.mem_size, A.ntx, A.nrx, A.segmented, false, A.s, gen);
@@ -2337,7 +2341,7 @@ int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict) {
     q->chk_gen = gen;
     ++q->checks_scanned;
   }
-  const uint64_t* f = q->misc() + 1;
+  const uint64_t* f = q->hp_chk + 5;
   *verdict = f[0] == q->chk_gen ? -1 : (f[1] == q->chk_gen ? 0 : 1);
   return NICGPU_OK;
 }
