@@ -485,6 +485,11 @@ int nicgpu_qp_walks(const nicgpu_qp* q, uint64_t* walks);
  * piece sums were skipped.  Segmented batches too (each segment's
  * corrections apart).  The synchronous nicgpu_qp_plan / _plan_on always sum. */
 int nicgpu_qp_set_deferred_verify(nicgpu_qp* q, int on);
+/* CUs the next deliveries of q leave without a delivery block (< 0: the
+ * default, 0 unless NICGPU_DLV_RESERVE_CUS says otherwise): a pipeline whose
+ * next batch plans and checks beside this delivery gives those kernels wave
+ * slots this way (nic::BatchedQueuePair: 32 while another batch is submitted). */
+int nicgpu_qp_set_delivery_reserve(nicgpu_qp* q, int cus);
 int nicgpu_qp_deferred(const nicgpu_qp* q, int* deferred);
 /* The deferred verifies' running corrections of q since it was created, on
  * `stream` into out[nseg][NICGPU_QP_FIXUPS] (nseg: 1, or the segments of a

@@ -113,6 +113,7 @@ ABI_SYMBOLS = (
     "nicgpu_qp_check_bounds",
     "nicgpu_qp_resum",
     "nicgpu_qp_set_deferred_verify",
+    "nicgpu_qp_set_delivery_reserve",
     "nicgpu_qp_deferred",
     "nicgpu_qp_verify_fixups_async",
     "nicgpu_event_synchronize",
@@ -202,6 +203,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_qp_check_bounds": (i32, [vp, vp]),
         "nicgpu_qp_resum": (i32, [vp, vp, ctypes.c_uint64, vp]),
         "nicgpu_qp_set_deferred_verify": (i32, [vp, i32]),
+        "nicgpu_qp_set_delivery_reserve": (i32, [vp, i32]),
         "nicgpu_qp_deferred": (i32, [vp, vp]),
         "nicgpu_qp_verify_fixups_async": (i32, [vp, vp, vp]),
         "nicgpu_event_synchronize": (i32, [vp]),

@@ -166,6 +166,7 @@ struct DeliverParams {
   unsigned long long* fix;  // [segment][NICGPU_QP_FIXUPS]
   const nicgpu_qp_segment* seg;  // a segmented batch's table (its completion's segment), or null
   uint32_t nseg;
+  int reserve;  // (host side) CUs left without a delivery block; < 0: NICGPU_DLV_RESERVE_CUS / the build default
 };
 
 // Tuning-only modes of deliver_kernel (libnicgpu_tune.so, tools/f1_deliver_bench.py;
@@ -1009,10 +1010,11 @@ int launch_deliver(const DeliverParams& P, bool rss, int cus_total, hipStream_t 
   const uint64_t want = (ntiles + kDlvWpb - 1) / kDlvWpb;
   // CUs left without a delivery block, so the next batch's plan and check
   // (small launches on a side stream) find wave slots while this one runs
-  static const int reserve = [] {
+  static const int reserve_default = [] {
     const char* e = std::getenv("NICGPU_DLV_RESERVE_CUS");
     return e ? std::atoi(e) : kDlvReserveCus;
   }();
+  const int reserve = P.reserve >= 0 ? P.reserve : reserve_default;
   const uint64_t cus = (uint64_t) (cus_total > reserve + 8 ? cus_total - reserve : cus_total);
   const uint64_t cap = cus * (uint64_t) bpc;
   const unsigned grid = (unsigned) (want < cap ? want : cap);
@@ -1883,6 +1885,7 @@ struct nicgpu_qp {
   unsigned long long* fix = nullptr;
   bool defer_verify = false, late_batch = false;
   uint64_t late_used = 0;
+  int dlv_reserve = -1;  // nicgpu_qp_set_delivery_reserve (< 0: the default)
   unsigned long long gen = 0;             // generation of the last plan / check call
   uint8_t* tmp = nullptr;
   uint64_t host_scal[4] = {0, 0, 0, 0};
@@ -2493,6 +2496,12 @@ int nicgpu_qp_set_deferred_verify(nicgpu_qp* q, int on) {
   return NICGPU_OK;
 }
 
+int nicgpu_qp_set_delivery_reserve(nicgpu_qp* q, int cus) {
+  if (!q) return NICGPU_ERR_INVALID;
+  q->dlv_reserve = cus;
+  return NICGPU_OK;
+}
+
 int nicgpu_qp_deferred(const nicgpu_qp* q, int* deferred) {
   if (!q || !deferred) return NICGPU_ERR_INVALID;
   *deferred = q->late_batch ? 1 : 0;
@@ -2649,6 +2658,7 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
   st = current_device_info(&di);
   if (st != NICGPU_OK) return st;
   DeliverParams P{};
+  P.reserve = q->dlv_reserve;
   P.mem = mem;
   P.mem_size = mem_size;
   P.w = q->writes;
@@ -2844,6 +2854,7 @@ extern "C" int nicgpu_tune_deliver(int mode, uint8_t* mem, uint64_t mem_size, co
   int st = current_device_info(&di);
   if (st != NICGPU_OK) return st;
   DeliverParams P{};
+  P.reserve = -1;
   P.mem = mem;
   P.mem_size = mem_size;
   P.w = w;

@@ -1261,6 +1261,7 @@ struct BatchedQueuePair::Scratch {
   static constexpr unsigned kSlots = 3;
   Slot slot[kSlots];
   unsigned head = 0, pending = 0;  // submit(): oldest pending slot, batches pending
+  std::atomic<unsigned> inflight{0};  // pending, as the job thread reads it (a later batch submitted?)
   JobQueue jobs;                   // submit(): plans, resolves and enqueues the batches in order
   void release() {
     for (Slot& sl : slot) sl.release();
@@ -1690,6 +1691,7 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
     }
   };
   ++S.pending;
+  S.inflight.fetch_add(1);
   S.jobs.push(run);  // interrupt callbacks fire in collect(), on the caller's thread
 }
 
@@ -1700,6 +1702,7 @@ bool BatchedQueuePair::collect(RxBatchResult& out) {
   // the slot is free again whatever the batch throws
   S.head = (S.head + 1) % Scratch::kSlots;
   --S.pending;
+  S.inflight.fetch_sub(1);
   try {
     sl.job.get();  // the job's exception, if any
   } catch (...) {
@@ -2070,6 +2073,15 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
 // lowered on the device to the pending resolve's settled prefix).
 void BatchedQueuePair::deliver(Slot& sl, const DeviceHostMemory& mem, std::size_t a, std::size_t b, unsigned flags,
                                const nicgpu_rss_ctx* rctx, std::uint64_t* hits, void* stream) {
+  // a later batch already submitted plans and checks beside this delivery:
+  // CUs left to it (f1 C3 1 M pipelined 371 -> 353 us with 32; one batch at a
+  // time is fastest with none, profiles/r05_dlv_reserve.txt, r05_dlv_reserve_ab.txt)
+  static const int pipe_reserve = [] {
+    const char* e = std::getenv("NIC_DLV_RESERVE_PIPE");
+    return e ? std::atoi(e) : 32;
+  }();
+  check(nicgpu_qp_set_delivery_reserve(sl.qp, scratch_->inflight.load() > 1 ? pipe_reserve : -1),
+        "nicgpu_qp_set_delivery_reserve");
   check(nicgpu_qp_deliver_range(sl.qp, reinterpret_cast<std::uint8_t*>(mem.base), mem.size, a, b, flags, rctx,
                                 rctx ? static_cast<int>(config_.tuple.mode) : NICGPU_TUPLE_NONE, config_.tuple.raw_offset,
                                 config_.tuple.raw_length, rctx ? hits : nullptr, stream),
