@@ -1188,7 +1188,8 @@ constexpr uint32_t kQpMaxPieces = 256;
 __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_descriptor* __restrict__ tx, uint64_t n,
                                                             uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
                                                             uint32_t* counts, unsigned long long* g,
-                                                            unsigned long long gen, QpSegs S, uint32_t defer) {
+                                                            unsigned long long gen, QpSegs S, uint32_t defer,
+                                                            uint32_t* need) {
   const QpRange R = qp_range(S, n);
   const uint64_t mtu = qp_max_mtu(max_mtu, S, R.s);
   const bool may = defer != 0u;
@@ -1200,7 +1201,13 @@ __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_desc
     counts[i] = c <= kQpMaxPieces ? c : 0u;
     if (c > kQpMaxPieces) g[0] = gen;
     plans[i] = pp;
-    if (may) needs = needs || nicqp::tx_verify_needed(t) || nicqp::decide_segments(t).nseg > 1u;
+    if (may) {
+      needs = needs || nicqp::tx_verify_needed(t) || nicqp::decide_segments(t).nseg > 1u;
+      // a deferring batch's need, final: no packet of it has a TX verify
+      // (qp_need_kernel then writes only the seed; any other batch's need it
+      // recomputes)
+      need[i] = nicqp::rx_need_unverified(t, mem_size, mtu);
+    }
   }
   if (!may) {
     if (blockIdx.x == 0 && threadIdx.x == 0) g[7] = gen;
@@ -1255,6 +1262,10 @@ __global__ __launch_bounds__(kQpBlock) void qp_need_kernel(QpCtx C, uint64_t n, 
                                                            unsigned long long gen, QpSegs S) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *first = n;  // the speculative final pass's "nothing differed"
   const bool bad = qp_plan_bad(g, gen);
+  if (!bad && qp_late(g, gen)) {  // the count kernel wrote every need: only the scan's end
+    if (blockIdx.x == 0 && threadIdx.x == 0) need[n] = 0u;
+    return;
+  }
   if (S.seg) {
     if (blockIdx.x == 0 && threadIdx.x == 0) need[n] = 0u;
     const QpRange R = qp_range(S, n);
@@ -2227,7 +2238,7 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
   const unsigned long long gen = ++q->gen;
   q->plan_gen = gen;
   hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->counts, q->gflags, gen, qp_segs(q), 0u);  // (its sums always run)
+                     q->plans, q->counts, q->gflags, gen, qp_segs(q), 0u, q->need);  // (its sums always run)
   int st = hip_status(hipGetLastError());
   uint32_t* np_h = reinterpret_cast<uint32_t*>(q->misc());
   uint64_t* ovf_h = q->misc() + 5;
@@ -2276,7 +2287,7 @@ int nicgpu_qp_plan_async(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, si
   q->plan_gen = gen;
   q->np = 0;  // known once resolved (nicgpu_qp_piece_count)
   hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->counts, q->gflags, gen, qp_segs(q), q->defer_verify ? 1u : 0u);
+                     q->plans, q->counts, q->gflags, gen, qp_segs(q), q->defer_verify ? 1u : 0u, q->need);
   st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
   if (st != NICGPU_OK) return st;

@@ -331,6 +331,18 @@ NICQP_HD Comp make_tx(uint16_t qid, const Tx& t, uint32_t st, uint64_t segs, boo
 // RX descriptors TX descriptor i pops when the ring has enough of them and no
 // RX-side check aborts it early: 0 when it is dropped before the RX stage
 // (read fault, TX checksum, MTU, invalid mss, too many segments).
+// rx_need of a packet that needs no TX verify (or passed it): the MTU and
+// segmentation checks only
+template <class Tx>
+NICQP_HD uint32_t rx_need_unverified(const Tx& t, uint64_t mem_size, uint64_t max_mtu) {
+  const uint64_t L = t.length;
+  if (!dma_ok(mem_size, t.buffer_address, L)) return 0;
+  if (L > max_mtu) return 0;
+  const SegDecision d = decide_segments(t);
+  if (d.invalid_mss || d.too_many) return 0;
+  return d.nseg;
+}
+
 template <class Tx, class Rx, class Plan>
 NICQP_HD uint32_t rx_need(const Ctx<Tx, Rx, Plan>& C, uint64_t i) {
   const Tx t = desc_load(C.tx + i);
@@ -340,10 +352,7 @@ NICQP_HD uint32_t rx_need(const Ctx<Tx, Rx, Plan>& C, uint64_t i) {
     const PacketSums<Plan> ps{&C.plans[i], C.cs, C.cs4, L};
     if ((uint16_t) (~ps.whole() & 0xFFFFu) != t.checksum_value) return 0;
   }
-  if (L > C.max_mtu) return 0;
-  const SegDecision d = decide_segments(t);
-  if (d.invalid_mss || d.too_many) return 0;
-  return d.nseg;
+  return rx_need_unverified(t, C.mem_size, C.max_mtu);
 }
 
 // QueuePair::process_once (queue_pair.cpp:67-460) for TX descriptor i with
