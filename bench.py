@@ -383,7 +383,7 @@ def main():
                     help="take the multi-rank path (RCCL init, key/table broadcast, barriers, max-reduce) even at "
                          "world size 1, to exercise it on a one-GPU box")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05d_pmc_c2.json"))
-    ap.add_argument("--rows-prof-json", default=os.path.join(ROOT, "profiles", "r05d_rows_prof.json"))
+    ap.add_argument("--rows-prof-json", default=os.path.join(ROOT, "profiles", "r05e_rows_prof.json"))
     args = ap.parse_args()
 
     import torch
