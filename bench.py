@@ -382,7 +382,7 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="take the multi-rank path (RCCL init, key/table broadcast, barriers, max-reduce) even at "
                          "world size 1, to exercise it on a one-GPU box")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05d_pmc_c2.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05f_pmc_c2.json"))
     ap.add_argument("--rows-prof-json", default=os.path.join(ROOT, "profiles", "r05e_rows_prof.json"))
     args = ap.parse_args()
 
