@@ -366,6 +366,91 @@ WORKLOAD_TEXT = {
 }
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run the same
+    command as N rank processes under a torch.distributed.run CHILD process
+    (one process per GPU, LOCAL_RANK = GPU index, RCCL over xGMI; gloo for
+    --dry-run) and exit with its status.  Nothing here touches the GPU: the
+    process is never exec'd into another one and device_count() does not
+    initialise HIP on this image.  Rank 0 prints the one JSON line to the
+    inherited stdout; a failing rank makes torch.distributed.run stop the
+    others and return non-zero, which this process returns."""
+    import subprocess
+
+    if not args.dry_run:
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            log(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) are visible")
+            return 2
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    log(f"bench.py: launching {args.gpus} ranks: {' '.join(cmd)}")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args):
+    """The multi-rank path without a GPU (gloo on the CPU): rank setup, the
+    shard plan, the key/table broadcast from rank 0 (the other ranks start
+    from zeros), barriers around an empty timed loop, the max over ranks and
+    the job-wide queue_hits reduction, then rank 0's line with n_gpus = world.
+    No packet is processed (the step is empty, so `value` is null): it exists
+    so a CPU test can run the launcher end to end (tests/test_bench_launch.py)."""
+    import hashlib
+
+    import torch
+
+    from smart_nic_amd import dist as sdist
+
+    if "WORLD_SIZE" not in os.environ:  # --gpus 1 --dry-run: a one-rank group
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(_free_port()))
+    ranks = sdist.init_ranks(force=True, backend="gloo")
+    rank, world = ranks.rank, ranks.world
+    shard = sdist.plan_shard(args.workload, ranks, args.packets)
+    table = (np.arange(128) % shard.queues).astype(np.uint16)
+    key_t, tab_t = sdist.setup_rss(ranks, MS_KEY if rank == 0 else bytes(len(MS_KEY)),
+                                   table if rank == 0 else np.zeros_like(table))
+    got = hashlib.sha256(bytes(key_t.numpy()) + tab_t.numpy().tobytes()).hexdigest()[:16]
+    want = hashlib.sha256(MS_KEY + table.astype(np.int16).tobytes()).hexdigest()[:16]
+    sdist.barrier(ranks)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    sdist.barrier(ranks)
+    t_max = sdist.max_over_ranks(time.perf_counter() - t0, ranks.dist)
+    per = sdist.gather_over_ranks([shard.hi - shard.lo, got == want], ranks.dist)
+    hits = torch.zeros(128, dtype=torch.int64)
+    job_hits, _, hits_ok = sdist.job_queue_hits(ranks, hits)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC_TEXT[args.workload], "value": None, "unit": "Mpkt/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_max / max(args.steps, 1) * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "dry run (gloo, no GPU, no packets processed)", "dry_run": True,
+            "config": {"workload": WORKLOAD_TEXT[args.workload], "job_packets": shard.job_packets,
+                       "parallelism": f"replicas x{world} (gloo dry run)"},
+            "per_rank": [{"rank": r, "packets": int(p[0]), "rss_config_broadcast_ok": bool(p[1])}
+                         for r, p in enumerate(per)],
+            "rss_config_sha": got, "job_queue_hits_ok": bool(hits_ok and int(job_hits.sum()) == 0),
+        }), flush=True)
+    sdist.finish(ranks)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -384,7 +469,22 @@ def main():
                          "world size 1, to exercise it on a one-GPU box")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05f_pmc_c2.json"))
     ap.add_argument("--rows-prof-json", default=os.path.join(ROOT, "profiles", "r05e_rows_prof.json"))
+    ap.add_argument("--dry-run", action="store_true",
+                    help="run the rank machinery on gloo/CPU without a GPU or packets (launcher test)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher around us: start the N ranks ourselves (child process)
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        log(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}: refusing to report a mislabelled run")
+        sys.exit(2)
+    if args.dry_run:
+        dry_run(args)
+        return
 
     import torch
 
@@ -457,6 +557,8 @@ def main():
     ceiling = read_ceiling(torch, f_dev) if (rank == 0 and world == 1 and not args.no_ceiling) else None
 
     t_max = sdist.max_over_ranks(t_wall, ranks.dist, dev)
+    # per-rank [local GPU index, packets, wall s, kernel avg s, kernel median s]
+    per_rank = sdist.gather_over_ranks([ranks.local, n, t_wall, kern_avg_s, kern_med_s], ranks.dist, dev)
 
     # one more launch with the histogram zeroed: the job-wide RssStats of one
     # batch (all-reduce of the per-table-index hits), checked against the
@@ -529,6 +631,10 @@ def main():
                 "ceiling_measured": ceiling,
                 "frac_of_ceiling": (round(achieved_gbs / ceiling["gbs"], 4) if ceiling else None),
             },
+            "per_rank": [{"rank": r, "gpu": int(p[0]), "packets": int(p[1]), "ms_per_step": round(p[2] / args.steps * 1e3, 4),
+                          "kernel_us_avg": round(p[3] * 1e6, 2), "kernel_us_median": round(p[4] * 1e6, 2)}
+                         for r, p in enumerate(per_rank)],
+            "kernel_us_avg_max_over_ranks": round(max(p[3] for p in per_rank) * 1e6, 2),
             "checks": dict(checks, all_ranks_ok=checks_all == world, job_queue_hits_ok=job_hits_ok),
             "rss_stats_job": {"hashes": int(job_hits.sum()), "queue_hits_nonzero": int((job_hits > 0).sum()),
                               "queue_hits_per_rank_sum": [int(h.sum()) for h in per_rank_hits]},

@@ -193,6 +193,18 @@ def max_over_ranks(value: float, dist, device=None) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(values, dist, device=None) -> list:
+    """Every rank's list of floats (same length on every rank), in rank order."""
+    import torch
+
+    if dist is None:
+        return [[float(v) for v in values]]
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [p.cpu().tolist() for p in parts]
+
+
 def sum_over_ranks(value: int, dist, device=None) -> int:
     import torch
 
