@@ -349,8 +349,10 @@ public:
   /// 16-B aligned (SimpleHostMemory without an address translator or fault
   /// injector: its std::vector, simple_host_memory.cpp:16); GpuError
   /// (NICGPU_ERR_INVALID) otherwise, before anything is read or written.  The
-  /// window is page-locked once (hipHostRegister, unregistered when the stage
-  /// binds another memory or is destroyed) and mirrored in HBM.  Per batch only
+  /// window — exactly its bytes, so heap neighbours on its pages stay ordinary
+  /// memory — is page-locked once (nicgpu_host_register, reference counted:
+  /// stages bound to one memory share it; released when the stage binds
+  /// another memory or is destroyed) and mirrored in HBM.  Per batch only
   /// the TX buffers' bytes go up (one copy of their span when it is dense,
   /// otherwise a gather of each buffer), the stage runs on the mirror, and
   /// exactly the bytes its DMA writes deliver are written back into the
@@ -372,6 +374,10 @@ public:
               void* stream = nullptr);
   [[nodiscard]] std::size_t pending() const noexcept;
 
+  /// The batches processed or collected so far, counter by counter as the
+  /// reference counts them; a submitted batch is added when it is collected
+  /// (pending batches, whose deferred RX verifies may still correct their
+  /// counts, are not in it).
   [[nodiscard]] const QueuePairStats& stats() const noexcept { return stats_; }
   void reset_stats() noexcept { stats_ = QueuePairStats{}; }
   [[nodiscard]] const BatchedQueuePairConfig& config() const noexcept { return config_; }

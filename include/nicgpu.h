@@ -491,13 +491,15 @@ int nicgpu_qp_set_deferred_verify(nicgpu_qp* q, int on);
  * slots this way (nic::BatchedQueuePair: 32 while another batch is submitted). */
 int nicgpu_qp_set_delivery_reserve(nicgpu_qp* q, int cus);
 int nicgpu_qp_deferred(const nicgpu_qp* q, int* deferred);
-/* The deferred verifies' running corrections of q since it was created, on
- * `stream` into out[nseg][NICGPU_QP_FIXUPS] (nseg: 1, or the segments of a
+/* The deferred verifies' corrections of q's last planned batch (the plan's
+ * count kernel zeroes them, in stream order, before the batch's deliveries),
+ * on `stream` into out[nseg][NICGPU_QP_FIXUPS] (nseg: 1, or the segments of a
  * segmented batch, each its queue pair's): [0] verifies that failed (each a
  * drops_checksum the statistics lack and an rx_packets and tx_packets they
  * hold too many), then what they hold too many of: [1] rx_bytes, [2]
- * rx_vlan_strips, [3] tx_bytes, [4] tx_vlan_insertions; [5..7] 0.  A caller
- * keeps the last values and applies the difference. */
+ * rx_vlan_strips, [3] tx_bytes, [4] tx_vlan_insertions; [5..7] 0.  Per batch,
+ * so a batch that failed after its deliveries leaves nothing behind for the
+ * next one. */
 #define NICGPU_QP_FIXUPS 8u
 int nicgpu_qp_verify_fixups_async(nicgpu_qp* q, uint64_t* out, size_t nseg, void* stream);
 /* The frames of view.rxc[0, nrx) delivered with Success, as RSS descriptors
@@ -610,17 +612,23 @@ int nicgpu_memcpy_batch(const nicgpu_copy_range* ranges, size_t n, void* stream)
  * DMA writes delivered come back (queue_pair.cpp:416-426). */
 /* Waits for the event's last record on the calling thread. */
 int nicgpu_event_synchronize(void* event);
-/* Page-locks host memory [host_ptr, host_ptr + bytes) (whole pages around it)
- * and maps it for the device: *dev_alias = the device-visible address of
- * host_ptr.  *owned = 1 when this call registered it (unregister it later),
- * 0 when it was registered already (by the caller or hipHostMalloc). */
+/* Page-locks exactly host memory [host_ptr, host_ptr + bytes) (hipHostRegister
+ * of that range, no page extension: heap neighbours sharing its pages stay
+ * ordinary pageable memory for every other copy) and maps it for the device:
+ * *dev_alias = the device-visible address of host_ptr.  Registrations are
+ * reference counted: a range inside one this library registered shares it,
+ * and each successful call (*owned = 1) is released by one
+ * nicgpu_host_unregister of the same host_ptr; the last release unregisters.
+ * A range registered by someone else (hipHostMalloc, the application) is
+ * refused with NICGPU_ERR_INVALID: its lifetime is not this library's.
+ * Kernels reading through the alias never read past host_ptr + bytes. */
 int nicgpu_host_register(void* host_ptr, size_t bytes, void** dev_alias, int* owned);
 int nicgpu_host_unregister(void* host_ptr);
 /* image[a, a + len) <- host[a, a + len) for every TX descriptor tx[0, ntx)
  * (device array) whose buffer is inside mem_size (a = buffer_address, len =
  * length): byte-exact, no byte outside the buffers is written.  host is a
  * device-visible alias (nicgpu_host_register) with 16-B alignment; image and
- * host both hold mem_size bytes (readable up to the next 16-B boundary). */
+ * host both hold mem_size bytes; no byte past mem_size is read. */
 int nicgpu_image_stage(uint8_t* image, const uint8_t* host, uint64_t mem_size, const nicgpu_tx_descriptor* tx,
                        size_t ntx, void* stream);
 /* host[d, d + len) <- image[d, d + len) for every write w of writes[0, n)

@@ -140,8 +140,22 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
         )
     lib = ctypes.CDLL(path)
+    for name, (res, args) in signatures().items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.nicgpu_abi_version() != ABI_VERSION:
+        raise NicGpuError(f"{path}: ABI version {lib.nicgpu_abi_version()}, this package needs {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def signatures() -> dict:
+    """ctypes (restype, argtypes) of the C-ABI entry points this package calls,
+    one per prototype of include/nicgpu.h (tests/test_abi.py checks the
+    argument counts against the header)."""
     vp, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
-    sig = {
+    return {
         "nicgpu_abi_version": (i32, []),
         "nicgpu_strerror": (ctypes.c_char_p, [i32]),
         "nicgpu_device_count": (i32, []),
@@ -205,21 +219,13 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "nicgpu_qp_set_deferred_verify": (i32, [vp, i32]),
         "nicgpu_qp_set_delivery_reserve": (i32, [vp, i32]),
         "nicgpu_qp_deferred": (i32, [vp, vp]),
-        "nicgpu_qp_verify_fixups_async": (i32, [vp, vp, vp]),
+        "nicgpu_qp_verify_fixups_async": (i32, [vp, vp, sz, vp]),
         "nicgpu_event_synchronize": (i32, [vp]),
         "nicgpu_host_register": (i32, [vp, sz, ctypes.POINTER(vp), ctypes.POINTER(i32)]),
         "nicgpu_host_unregister": (i32, [vp]),
         "nicgpu_image_stage": (i32, [vp, vp, ctypes.c_uint64, vp, sz, vp]),
         "nicgpu_image_writeback": (i32, [vp, vp, ctypes.c_uint64, vp, sz, vp]),
     }
-    for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
-        fn.restype = res
-        fn.argtypes = args
-    if lib.nicgpu_abi_version() != ABI_VERSION:
-        raise NicGpuError(f"{path}: ABI version {lib.nicgpu_abi_version()}, this package needs {ABI_VERSION}")
-    _lib = lib
-    return lib
 
 
 def _check(status: int, what: str) -> None:

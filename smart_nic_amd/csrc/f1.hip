@@ -1189,7 +1189,9 @@ __global__ __launch_bounds__(kQpBlock) void qp_count_kernel(const nicgpu_tx_desc
                                                             uint64_t mem_size, uint64_t max_mtu, QpPlan* plans,
                                                             uint32_t* counts, unsigned long long* g,
                                                             unsigned long long gen, QpSegs S, uint32_t defer,
-                                                            uint32_t* need) {
+                                                            uint32_t* need, unsigned long long* fix, uint32_t nfix) {
+  // this batch's deferred-verify corrections start at 0 (its deliveries follow)
+  for (uint32_t k = blockIdx.x * kQpBlock + threadIdx.x; k < nfix; k += gridDim.x * kQpBlock) fix[k] = 0ull;
   const QpRange R = qp_range(S, n);
   const uint64_t mtu = qp_max_mtu(max_mtu, S, R.s);
   const bool may = defer != 0u;
@@ -1257,12 +1259,16 @@ __device__ __forceinline__ bool qp_plan_bad(const unsigned long long* g, unsigne
   return g[0] == gen || g[3] == gen;
 }
 
+// fresh (the position walk): need recomputed for every batch — after the
+// relaxation a deferring batch's need[] holds the last step's pops, not the
+// count kernel's needs (rx_need of a deferring batch is rx_need_unverified:
+// none of its packets has a TX verify).
 __global__ __launch_bounds__(kQpBlock) void qp_need_kernel(QpCtx C, uint64_t n, uint32_t* need,
                                                            unsigned long long* first, const unsigned long long* g,
-                                                           unsigned long long gen, QpSegs S) {
+                                                           unsigned long long gen, QpSegs S, uint32_t fresh) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *first = n;  // the speculative final pass's "nothing differed"
   const bool bad = qp_plan_bad(g, gen);
-  if (!bad && qp_late(g, gen)) {  // the count kernel wrote every need: only the scan's end
+  if (!bad && !fresh && qp_late(g, gen)) {  // the count kernel wrote every need: only the scan's end
     if (blockIdx.x == 0 && threadIdx.x == 0) need[n] = 0u;
     return;
   }
@@ -2029,7 +2035,7 @@ int qp_walk(nicgpu_qp* q, const QpCtx& C, const QpSegs& S, uint64_t ntx, unsigne
   if (st != NICGPU_OK) return st;
   uint64_t* tail = q->partials + (size_t) grid * kQpStats;
   hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, ntx, q->need,
-                     reinterpret_cast<unsigned long long*>(tail + 1), q->gflags, q->plan_gen, S);
+                     reinterpret_cast<unsigned long long*>(tail + 1), q->gflags, q->plan_gen, S, 1u);
   st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
   if (st != NICGPU_OK) return st;
@@ -2238,7 +2244,8 @@ int nicgpu_qp_plan_on(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, size_
   const unsigned long long gen = ++q->gen;
   q->plan_gen = gen;
   hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->counts, q->gflags, gen, qp_segs(q), 0u, q->need);  // (its sums always run)
+                     q->plans, q->counts, q->gflags, gen, qp_segs(q), 0u, q->need, q->fix,
+                     (q->nseg ? q->nseg : 1u) * NICGPU_QP_FIXUPS);  // (its sums always run)
   int st = hip_status(hipGetLastError());
   uint32_t* np_h = reinterpret_cast<uint32_t*>(q->misc());
   uint64_t* ovf_h = q->misc() + 5;
@@ -2287,7 +2294,8 @@ int nicgpu_qp_plan_async(nicgpu_qp* q, const uint8_t* mem, uint64_t mem_size, si
   q->plan_gen = gen;
   q->np = 0;  // known once resolved (nicgpu_qp_piece_count)
   hipLaunchKernelGGL(qp_count_kernel, dim3(grid), dim3(kQpBlock), 0, s, q->tx, (uint64_t) ntx, mem_size, max_mtu,
-                     q->plans, q->counts, q->gflags, gen, qp_segs(q), q->defer_verify ? 1u : 0u, q->need);
+                     q->plans, q->counts, q->gflags, gen, qp_segs(q), q->defer_verify ? 1u : 0u, q->need, q->fix,
+                     (q->nseg ? q->nseg : 1u) * NICGPU_QP_FIXUPS);
   st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->counts, q->base, ntx + 1, s);
   if (st != NICGPU_OK) return st;
@@ -2397,7 +2405,7 @@ int nicgpu_qp_resolve_start(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t 
   // otherwise; a batch that settles at once (uniform RX descriptors, no early
   // ends) needs no relaxation step and no host round trip before its DMA writes.
   hipLaunchKernelGGL(qp_need_kernel, dim3(grid), dim3(kQpBlock), 0, s, C, (uint64_t) ntx, q->need,
-                     reinterpret_cast<unsigned long long*>(tail + 1), q->gflags, q->plan_gen, S);
+                     reinterpret_cast<unsigned long long*>(tail + 1), q->gflags, q->plan_gen, S, 0u);
   int st = hip_status(hipGetLastError());
   if (st == NICGPU_OK) st = qp_scan(q, q->need, q->pos, ntx + 1, s);
   if (st != NICGPU_OK) return st;

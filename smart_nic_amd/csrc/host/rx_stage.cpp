@@ -1149,20 +1149,15 @@ struct BatchedQueuePair::Slot {
   bool irq_pending = false;
   std::size_t irq_ntx = 0, irq_nrx = 0;
   // deferred RX verify (nicgpu_qp_set_deferred_verify): the batch's completions
-  // and statistics are final after its deliveries; the context's running
-  // corrections (per segment of a fused batch) come down into h_fix, fix_seen
-  // the last applied
+  // and statistics are final after its deliveries; its corrections (per
+  // segment of a fused batch; the plan zeroes them on the device, so a batch
+  // that failed after its deliveries leaves nothing for the next) come down
+  // into h_fix
   bool late = false;
   HostBuf h_fix;
-  std::vector<std::uint64_t> fix_seen;
-  // this batch's corrections (a segment's row: s * NICGPU_QP_FIXUPS), the
-  // seen values moved on
-  std::uint64_t fix_delta(std::size_t s, unsigned k) {
-    const std::size_t i = s * NICGPU_QP_FIXUPS + k;
-    if (fix_seen.size() <= i) fix_seen.resize(i + 1, 0);
-    const std::uint64_t now = static_cast<const std::uint64_t*>(h_fix.p)[i], d = now - fix_seen[i];
-    fix_seen[i] = now;
-    return d;
+  // this batch's correction k of segment s
+  std::uint64_t fix_delta(std::size_t s, unsigned k) const {
+    return static_cast<const std::uint64_t*>(h_fix.p)[s * NICGPU_QP_FIXUPS + k];
   }
 
   void release_rss() {
@@ -1195,7 +1190,6 @@ struct BatchedQueuePair::Slot {
   }
   void create(int dev) {
     check(nicgpu_qp_create(&qp, dev), "nicgpu_qp_create");
-    fix_seen.clear();  // a new context's corrections start at 0
     for (void** e : {&ev_tx, &ev_rx, &ev_resolved, &ev_done, &ev_submit, &ev_staged, &ev_wb, &ev_gate})
       check(nicgpu_event_create(e), "nicgpu_event_create");
     for (auto& side : ev_irq)
@@ -2456,9 +2450,7 @@ void BatchedQueuePair::image_host_path(Slot& sl, std::span<const TxDescriptor> t
   const std::size_t n = sl.applied.size();
   void* d = sl.wbuf.get(std::max<std::size_t>(n, 1) * sizeof(rx_stage_detail::SegmentWrite));
   if (n) {
-    // staged through page-locked memory: the registered window's pages (a
-    // HostMemory buffer need not be page-aligned) may hold part of a heap
-    // vector, and a copy from one straddling them fails
+    // staged through page-locked memory (a full-rate copy of the write list)
     auto* h = sl.h_applied.get<rx_stage_detail::SegmentWrite>(n);
     std::memcpy(h, sl.applied.data(), n * sizeof(rx_stage_detail::SegmentWrite));
     check(nicgpu_memcpy_async(d, h, n * sizeof(rx_stage_detail::SegmentWrite), stream), "nicgpu_memcpy_async");

@@ -22,14 +22,24 @@ namespace {
 
 constexpr unsigned kImgWaves = 4;
 
-// dst[a, a + len) <- src[a, a + len), lanes over the 16-B chunks.
+// dst[a, a + len) <- src[a, a + len), lanes over the 16-B chunks; no byte of
+// src at or past `limit` (the window's size) is read: the chunk holding the
+// window's end is read byte by byte (a registered host window ends exactly
+// there, and the bytes after it are other heap blocks').
 __device__ __forceinline__ void copy_range(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t a,
-                                           uint64_t len, uint32_t lane) {
+                                           uint64_t len, uint64_t limit, uint32_t lane) {
   const uint64_t e = a + len;
   const uint64_t c1 = (e + 15) & ~15ull;
   for (uint64_t c = (a & ~15ull) + 16ull * lane; c < c1; c += 16ull * kWave) {
     u32x4 v;
-    __builtin_memcpy(&v, src + c, 16);
+    if (c + 16 <= limit) {
+      __builtin_memcpy(&v, src + c, 16);
+    } else {
+      uint8_t t[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) t[k] = c + k < limit ? src[c + k] : (uint8_t) 0;
+      __builtin_memcpy(&v, t, 16);
+    }
     if (c >= a && c + 16 <= e) {
       __builtin_memcpy(dst + c, &v, 16);
     } else {
@@ -53,7 +63,7 @@ __global__ __launch_bounds__(kWave * kImgWaves) void image_stage_kernel(uint8_t*
   for (uint64_t i = w0; i < n; i += stride) {
     const uint64_t a = tx[i].buffer_address, len = tx[i].length;
     if (len == 0 || !nicqp::dma_ok(mem_size, a, len)) continue;  // a DMA read fault reads nothing (:86-92)
-    copy_range(image, host, a, len, lane);
+    copy_range(image, host, a, len, mem_size, lane);
   }
 }
 
@@ -68,7 +78,7 @@ __global__ __launch_bounds__(kWave * kImgWaves) void image_writeback_kernel(cons
     const uint64_t d = w[j].dst;
     const uint64_t len = (uint64_t) w[j].prefix_len + w[j].len_a + w[j].len_b;
     if (len == 0 || !nicqp::dma_ok(mem_size, d, len)) continue;
-    copy_range(host, image, d, len, lane);
+    copy_range(host, image, d, len, mem_size, lane);
   }
 }
 

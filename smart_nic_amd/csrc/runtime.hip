@@ -4,7 +4,6 @@
 
 #include "host.h"
 
-#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -131,34 +130,19 @@ int nicgpu_memset_async(void* dev_ptr, int value, size_t bytes, void* stream) {
 
 }  // extern "C"
 
-// Whole pages around the range: hipHostRegister locks pages, and the staging
-// kernels read up to the next 16-B boundary past the last byte.  The page
-// ranges this library registered, for nicgpu_memcpy_async.
+// Host windows this library registered (nicgpu_host_register): exactly the
+// caller's range (no page extension: the runtime then keeps treating heap
+// neighbours on the same pages as ordinary pageable memory), with a reference
+// count so that several stages binding one HostMemory share one registration
+// and only the last release unregisters it.
 namespace {
-constexpr uintptr_t kPage = 4096;
-void page_span(void* p, size_t n, void*& base, size_t& len) {
-  const auto a = reinterpret_cast<uintptr_t>(p);
-  const uintptr_t lo = a & ~(kPage - 1), hi = (a + n + 16 + kPage - 1) & ~(kPage - 1);
-  base = reinterpret_cast<void*>(lo);
-  len = hi - lo;
-}
+struct Registration {
+  uintptr_t lo, hi;  // [lo, hi) as registered
+  uint8_t* alias;    // device address of lo
+  unsigned refs;
+};
 std::mutex g_reg_mu;
-std::vector<std::pair<uintptr_t, uintptr_t>> g_reg;  // [base, end)
-std::atomic<size_t> g_nreg{0};
-// bytes of [p, p + n) before the end of a registered range p starts inside,
-// when the range ends first; 0 otherwise
-size_t registered_cut1(const void* p, size_t n) {
-  const auto a = reinterpret_cast<uintptr_t>(p);
-  std::lock_guard<std::mutex> g(g_reg_mu);
-  for (const auto& r : g_reg)
-    if (a >= r.first && a < r.second && a + n > r.second) return r.second - a;
-  return 0;
-}
-size_t registered_cut(const void* dst, const void* src, size_t n) {
-  if (g_nreg.load(std::memory_order_relaxed) == 0) return 0;
-  const size_t a = registered_cut1(dst, n), b = registered_cut1(src, n);
-  return a && b ? (a < b ? a : b) : (a ? a : b);
-}
+std::vector<Registration> g_reg;
 }  // namespace
 
 extern "C" {
@@ -166,16 +150,6 @@ extern "C" {
 int nicgpu_memcpy_async(void* dst, const void* src, size_t bytes, void* stream) {
   if (bytes == 0) return NICGPU_OK;
   if (!dst || !src) return NICGPU_ERR_INVALID;
-  // A host range that starts inside pages nicgpu_host_register locked and runs
-  // past them (a heap neighbour of a HostMemory buffer that is not page
-  // aligned) is not one allocation to the runtime: the copy is cut there.
-  for (size_t cut; (cut = registered_cut(dst, src, bytes)) != 0 && cut < bytes;) {
-    const int st = hip_status(hipMemcpyAsync(dst, src, cut, hipMemcpyDefault, static_cast<hipStream_t>(stream)));
-    if (st != NICGPU_OK) return st;
-    dst = static_cast<uint8_t*>(dst) + cut;
-    src = static_cast<const uint8_t*>(src) + cut;
-    bytes -= cut;
-  }
   return hip_status(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, static_cast<hipStream_t>(stream)));
 }
 
@@ -243,42 +217,49 @@ int nicgpu_host_register(void* host_ptr, size_t bytes, void** dev_alias, int* ow
   if (!host_ptr || !dev_alias || !owned || bytes == 0) return NICGPU_ERR_INVALID;
   *dev_alias = nullptr;
   *owned = 0;
-  void* base = nullptr;
-  size_t len = 0;
-  page_span(host_ptr, bytes, base, len);
-  const hipError_t e = hipHostRegister(base, len, hipHostRegisterMapped);
-  if (e == hipSuccess) {
-    *owned = 1;
-    std::lock_guard<std::mutex> g(g_reg_mu);
-    g_reg.emplace_back(reinterpret_cast<uintptr_t>(base), reinterpret_cast<uintptr_t>(base) + len);
-    g_nreg.store(g_reg.size());
+  const auto lo = reinterpret_cast<uintptr_t>(host_ptr), hi = lo + bytes;
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  // inside a window this library registered: one more reference to it
+  for (Registration& r : g_reg)
+    if (lo >= r.lo && hi <= r.hi) {
+      ++r.refs;
+      *dev_alias = r.alias + (lo - r.lo);
+      *owned = 1;
+      return NICGPU_OK;
+    }
+  const hipError_t e = hipHostRegister(host_ptr, bytes, hipHostRegisterMapped);
+  if (e != hipSuccess) {
+    (void) hipGetLastError();  // not sticky for the caller's next call
+    // registered by someone else (or overlapping a window of ours): its
+    // lifetime is not ours to hold, so it is refused rather than adopted
+    return e == hipErrorHostMemoryAlreadyRegistered ? NICGPU_ERR_INVALID : NICGPU_ERR_HIP;
   }
-  else if (e != hipErrorHostMemoryAlreadyRegistered) return NICGPU_ERR_HIP;
-  (void) hipGetLastError();  // clear the sticky "already registered"
   void* dev = nullptr;
-  if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) {
-    if (*owned) (void) hipHostUnregister(base);
-    *owned = 0;
+  if (hipHostGetDevicePointer(&dev, host_ptr, 0) != hipSuccess || dev == nullptr) {
+    (void) hipGetLastError();
+    (void) hipHostUnregister(host_ptr);
     return NICGPU_ERR_HIP;
   }
-  *dev_alias = static_cast<uint8_t*>(dev) + (reinterpret_cast<uintptr_t>(host_ptr) - reinterpret_cast<uintptr_t>(base));
+  g_reg.push_back({lo, hi, static_cast<uint8_t*>(dev), 1u});
+  *dev_alias = dev;
+  *owned = 1;
   return NICGPU_OK;
 }
 
 int nicgpu_host_unregister(void* host_ptr) {
   if (!host_ptr) return NICGPU_ERR_INVALID;
-  void* base = nullptr;
-  size_t len = 0;
-  page_span(host_ptr, 1, base, len);
-  {
-    std::lock_guard<std::mutex> g(g_reg_mu);
-    for (size_t i = 0; i < g_reg.size(); ++i)
-      if (g_reg[i].first == reinterpret_cast<uintptr_t>(base)) {
-        g_reg.erase(g_reg.begin() + (long) i);
-        break;
-      }
-    g_nreg.store(g_reg.size());
-  }
+  const auto a = reinterpret_cast<uintptr_t>(host_ptr);
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  // the registration starting at host_ptr, else the one holding it
+  size_t k = g_reg.size();
+  for (size_t i = 0; i < g_reg.size() && k == g_reg.size(); ++i)
+    if (g_reg[i].lo == a) k = i;
+  for (size_t i = 0; i < g_reg.size() && k == g_reg.size(); ++i)
+    if (a >= g_reg[i].lo && a < g_reg[i].hi) k = i;
+  if (k == g_reg.size()) return NICGPU_ERR_INVALID;  // not registered by this library
+  if (--g_reg[k].refs != 0) return NICGPU_OK;
+  void* base = reinterpret_cast<void*>(g_reg[k].lo);
+  g_reg.erase(g_reg.begin() + (long) k);
   return hip_status(hipHostUnregister(base));
 }
 

@@ -22,6 +22,28 @@ def test_header_symbols_match_binding_list():
     assert _declared("nicgpu.h") == sorted(sna.ABI_SYMBOLS)
 
 
+def _prototypes(header):
+    """{name: argument count} of every nicgpu_* prototype in the header."""
+    text = open(os.path.join(ROOT, "include", header)).read()
+    text = re.sub(r"//[^\n]*", "", text)
+    out = {}
+    for name, args in re.findall(r"(?:int|const char\*)\s+(nicgpu_\w+)\s*\(([^;{]*?)\)\s*;", text, re.S):
+        args = args.strip()
+        out[name] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_ctypes_signatures_match_header_prototypes():
+    """Every ctypes signature the package binds has the header's argument
+    count (nicgpu_qp_verify_fixups_async was bound with three)."""
+    protos = _prototypes("nicgpu.h")
+    sigs = sna.signatures()
+    assert set(sigs) <= set(protos), sorted(set(sigs) - set(protos))
+    bad = {n: (len(a), protos[n]) for n, (_, a) in sigs.items() if len(a) != protos[n]}
+    assert not bad, bad
+    assert len(sigs) >= 60  # (nearly every entry point is bound)
+
+
 def test_library_exports_every_declared_symbol():
     lib = sna.load_library()
     for name in _declared("nicgpu.h"):

@@ -103,6 +103,20 @@ def test_rx_stage_reference_simple_host_memory_gpu(tmp_path):
         _run(REFMEM, "host", n, tmp_path)
 
 
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REFMEM), reason="oracle/_ref/rx_stage_test_refmem not built (make -C oracle ref)")
+def test_host_window_registration_on_heap_blocks():
+    """The verdict's r05 registration hazard, on the reference's
+    SimpleHostMemory of 3000 B (a heap block, not page aligned, with live heap
+    neighbours): exactly the window is registered, so copies of the
+    neighbours through the runtime succeed while stages are bound; two stages
+    share one registration (reference counted) and the one left keeps working
+    after the other is destroyed; a second small memory beside it binds too."""
+    r = subprocess.run([REFMEM, "heap"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "rx_stage_test heap: ok" in r.stdout
+
+
 def test_rx_stage_refmem_binary_builds():
     """Where the reference exists, build() leaves the drop-in binary behind
     (its GPU run is test_rx_stage_reference_simple_host_memory_gpu)."""
