@@ -48,10 +48,15 @@
 // layer's delivered frames are hashed before the next layer can overwrite
 // them.  The results are the sequential reference's in every case.
 //
-// Not modelled: address translators / fault injectors of SimpleHostMemory
-// (only the plain bounds check).  A HostMemory whose window is not flat (a
-// translator that moves addresses) is refused with GpuError before anything
-// is read or written.
+// Faults of a HostMemory beyond the bounds rule (SimpleHostMemory's
+// FaultInjector and AddressTranslator, simple_host_memory.cpp:76-87): by
+// default the caller asserts the window is flat — no injector, no translator;
+// bind_image probes translate() at three addresses and refuses a window it
+// sees moved, but it cannot prove flatness.  With
+// BatchedQueuePairConfig::host_memory_faults every DMA access goes through the
+// memory's own translate_const / translate, so injected faults and IOMMU
+// faults post the reference's Fault completions (queue_pair.cpp:96-103,
+// 416-426); see that flag for what it requires.
 //
 // Failure: process_batch (or submit / collect) throws nic::GpuError on a HIP
 // failure.  stats() is then unchanged, but the memory image may hold some of
@@ -242,6 +247,22 @@ struct BatchedQueuePairConfig {
   /// completes (nicgpu_qp_set_deferred_verify).  Results are the same either
   /// way (tests/cpp/rx_stage_gpu_fuzz.cpp).  NIC_DEFER_VERIFY=0 turns it off.
   bool defer_rx_verify{true};
+  /// HostMemory batches: model the memory's own DMA faults.  Every TX read is
+  /// the memory's translate_const(buffer_address, length) and every RX write
+  /// its translate(buffer_address, size) — what DMAEngine::read / write reach
+  /// (dma_engine.cpp:12-32) — so a FaultInjector or an IOMMU AddressTranslator
+  /// that refuses an access makes the reference's Fault completion there
+  /// (queue_pair.cpp:96-103, 416-426) and the ring positions that follow from
+  /// it.  The reads are asked once per TX descriptor before the batch, the
+  /// writes in posting order by the host resolve (the batch is resolved on the
+  /// host; piece sums, DMA writes and RSS stay on the GPU).  Requires what
+  /// every reference test's injector and translator are: functions of
+  /// (address, length), and translators that map each access they allow onto
+  /// itself (an IOMMU that grants or denies); a translation that moves an
+  /// address throws GpuError (NICGPU_ERR_INVALID) — before anything is written
+  /// when it is a TX read's.  Off: the caller asserts the memory is flat (no
+  /// injector, no translator) and the bounds rule alone decides faults.
+  bool host_memory_faults{false};
 };
 
 struct RxBatchResult {
@@ -296,6 +317,7 @@ struct RxBatchResult {
 
 namespace rx_stage_detail {
 struct SegmentWrite;
+struct DmaWriteCheck;
 }
 
 /// QueuePair::process_once over a batch (src/queue_pair.cpp:67-460).
@@ -420,7 +442,11 @@ private:
                   std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out, void* stream,
                   int& disjoint, double& check_us, int& again);
   // host-image batches (process_batch / submit with a HostMemory)
-  HostImage& bind_image(HostMemory& mem);
+  HostImage& bind_image(HostMemory& mem, bool checked = false, std::byte* window = nullptr);
+  // host_memory_faults: the batch's descriptors with refused reads moved out of
+  // bounds (kept in the slot until collected) and the write verdicts
+  std::span<const TxDescriptor> checked_tx(Slot& sl, HostMemory& mem, std::span<const TxDescriptor> tx,
+                                           std::byte*& window);
   void image_prepare(Slot& sl, HostImage& img, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx);
   void image_host_path(Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                        QueuePairStats& stats, RxBatchResult& out, void* stream, int disjoint, double& check_us);
@@ -441,7 +467,8 @@ private:
   // (applied: every DMA write made is appended — a host-image batch writes them back)
   void on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                QueuePairStats& stats, RxBatchResult& out, void* stream, int disjoint, double& check_us,
-               std::vector<rx_stage_detail::SegmentWrite>* applied = nullptr);
+               std::vector<rx_stage_detail::SegmentWrite>* applied = nullptr,
+               const rx_stage_detail::DmaWriteCheck* wcheck = nullptr);
   BatchedQueuePairConfig config_;
   BatchedQueuePairConfig quiet_;  // config_ without the interrupt callback (every resolve; replayed after)
   bool defer_multi_ = false;      // process_queues: this fused batch may defer its RX verifies
@@ -452,6 +479,14 @@ private:
 // Building blocks of process_batch, public so that the host logic can be
 // tested without a GPU (the piece sums then come from a CPU checker).
 namespace rx_stage_detail {
+
+/// A HostMemory's own verdict on each DMA write (host_memory_faults): true
+/// when translate(address, length) allows it.  Asked by the host resolve in
+/// posting order, once per write the bounds rule allows.
+struct DmaWriteCheck {
+  virtual ~DmaWriteCheck() = default;
+  virtual bool write_ok(std::uint64_t address, std::uint64_t length) const = 0;
+};
 
 /// A byte range of host memory whose ones'-complement sum the GPU computes.
 struct Piece {
@@ -534,7 +569,8 @@ void make_plan(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
 void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
              std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
              std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
-             std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx, unsigned max_threads = 0);
+             std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx, unsigned max_threads = 0,
+             const DmaWriteCheck* wcheck = nullptr);
 
 /// The sequential resolve, stopped before the first TX descriptor whose
 /// pieces read bytes that an earlier descriptor of this call writes (that
@@ -544,7 +580,8 @@ void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const P
 std::size_t resolve_prefix(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
                            std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
                            std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
-                           std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx);
+                           std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx,
+                           const DmaWriteCheck* wcheck = nullptr);
 
 /// The device resolve's algorithm (nicgpu_qp_resolve) on the host, for the
 /// tests: ring positions by relaxation — every packet resolved at the
@@ -643,10 +680,20 @@ struct BatchScratch {
 void build_queue_lists(RxBatchResult& out);
 
 /// disjoint: buffers_disjoint(mem_size, tx, rx) when the caller knows it (-1:
-/// computed here).
+/// computed here).  wcheck: the memory's verdict on each DMA write (the
+/// resolve then runs sequentially, on the calling thread).
 void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
                std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out, BatchScratch& scratch,
-               Backend& backend, int disjoint = -1);
+               Backend& backend, int disjoint = -1, const DmaWriteCheck* wcheck = nullptr);
+
+/// host_memory_faults' TX reads: tx with every descriptor whose read
+/// m.translate_const(buffer_address, length) refuses moved out of bounds
+/// (mem_size + 1: the bounds rule then faults it exactly as the reference's
+/// read does).  Returns the window's address (data - address of any read it
+/// allows; null when none does).  Throws GpuError (NICGPU_ERR_INVALID) when a
+/// read is translated to another address or the allowed reads disagree on
+/// the window.
+std::byte* checked_reads(const HostMemory& m, std::span<const TxDescriptor> tx, std::vector<TxDescriptor>& out);
 
 }  // namespace rx_stage_detail
 

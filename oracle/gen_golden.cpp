@@ -38,6 +38,7 @@
 #include "nic/tx_rx.h"
 #include "oracle.h"
 #include "../tests/cpp/qm_scale_gen.h"
+#include "../tests/cpp/fault_model.h"
 
 using namespace nic;
 
@@ -690,7 +691,9 @@ std::string completion_json(const CompletionEntry& e) {
 // delivered frame's bytes as written, before any later write lands on them.
 class RecordingMemory final : public HostMemory {
 public:
-  explicit RecordingMemory(HostMemoryConfig c) : mem_(c) {}
+  explicit RecordingMemory(HostMemoryConfig c, SimpleHostMemory::AddressTranslator tr = {},
+                           SimpleHostMemory::FaultInjector fi = {})
+      : mem_(c, std::move(tr), std::move(fi)) {}
   HostMemoryConfig config() const noexcept override { return mem_.config(); }
   HostMemoryResult translate(HostAddress a, std::size_t n, HostMemoryView& v) override { return mem_.translate(a, n, v); }
   HostMemoryResult translate_const(HostAddress a, std::size_t n, ConstHostMemoryView& v) const override {
@@ -715,7 +718,11 @@ private:
 // flavour 0: mixed sizes; 1: 9000 B TSO/GSO; 2: mixed sizes with overlapping
 // buffers (recycled RX buffers, RX buffers straddling the previous one or
 // lying inside TX buffers), where the reference's in-order writes decide.
-void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t ntx, std::size_t nrx, int flavour) {
+// faults (faultfx::Kind): the memory's own DMA faults (tests/cpp/fault_model.h)
+// through SimpleHostMemory's FaultInjector / AddressTranslator, armed once the
+// memory is loaded and disarmed before it is read back.
+void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t ntx, std::size_t nrx, int flavour,
+                       int faults = faultfx::kNone) {
   Rng r{seed};
   // TX region, then the RX buffers, then a guard tail; a few descriptors point
   // past the end (DMA fault).
@@ -818,13 +825,16 @@ void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t 
   for (std::size_t j = 0; j < nrx; ++j)
     if (r.below(80) == 0) rxs[j].buffer_address = mem_size + 1 + j;
 
-  HostMemoryConfig mc{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false};
-  RecordingMemory mem{mc};
+  HostMemoryConfig mc{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = faults == faultfx::kIommu};
+  faultfx::Model fm;
+  fm.kind = static_cast<faultfx::Kind>(faults);
+  RecordingMemory mem = faults ? RecordingMemory{mc, fm.translator(), fm.injector()} : RecordingMemory{mc};
   std::vector<std::uint8_t> image(mem_size);
   for (std::size_t a = 0; a < tx_end; ++a) image[a] = r.byte();  // RX region starts zeroed
   for (std::size_t i = 0; i < ntx; ++i) std::memcpy(image.data() + tx_addr[i], pkts[i].data(), pkts[i].size());
   assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(image))).ok());
   mem.recording = true;
+  *fm.armed = true;
   DMAEngine dma{mem};
   QueuePairConfig qc{
       .queue_id = 5,
@@ -884,6 +894,7 @@ void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t 
     rx_queue[j] = *rss_eng.select_queue(std::span<const std::uint8_t>(t, tl));
   }
   assert(wk == mem.writes.size());
+  *fm.armed = false;  // read back whole
   const auto& st = qp.stats();
   js << "],\n \"stats\": [" << st.tx_packets << "," << st.rx_packets << "," << st.tx_bytes << "," << st.rx_bytes << ","
      << st.drops_checksum << "," << st.drops_no_rx_desc << "," << st.drops_buffer_small << "," << st.drops_mtu_exceeded
@@ -898,6 +909,7 @@ void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t 
     js << (j ? "," : "") << "\"" << std::hex << fnv1a(after.data() + a, n) << std::dec << "\"";
   }
   js << "],\n \"mem_fnv\": \"" << std::hex << fnv1a(after.data(), mem_size) << std::dec << "\"";
+  js << ",\n \"faults\": " << faults;
   js << ",\n \"rss\": \"RssEngine{MS 40-B key, table i % 16 of 128}::select_queue on oracle_extract_tuple(AUTO) of each Success frame as written\"";
   js << ",\n \"rx_hash\": [";
   for (std::size_t j = 0; j < rx_hash.size(); ++j) js << (j ? "," : "") << rx_hash[j];
@@ -920,6 +932,10 @@ void gen_qp_batch() {
   gen_qp_batch_case("qp_mix_b", 202, 400, 700, 0);    // ample RX descriptors
   gen_qp_batch_case("qp_tso", 303, 40, 300, 1);       // 9000 B TSO/GSO, odd mss, tiny headers
   gen_qp_batch_case("qp_alias", 404, 300, 400, 2);    // overlapping RX/RX and RX/TX buffers
+  // the memory's own faults (SimpleHostMemory's injector / IOMMU translator)
+  gen_qp_batch_case("qp_fault_inj", 505, 400, 700, 0, faultfx::kInjector);
+  gen_qp_batch_case("qp_fault_iommu", 606, 400, 700, 0, faultfx::kIommu);
+  gen_qp_batch_case("qp_fault_tso", 707, 40, 300, 1, faultfx::kInjector);
 }
 
 // ------------------------------------------------------------ QueueManager --

@@ -290,6 +290,7 @@ bool BatchedQueueManager::fusable() const {
     const BatchedQueuePairConfig& c = qp->config;
     if (!c.device_resolve || c.results_on_device != c0.results_on_device || (c.rss == nullptr) != (c0.rss == nullptr))
       return false;
+    if (c.host_memory_faults) return false;  // the memory decides each access: per queue pair, on the host
     if (c.rss && c.rss != c0.rss) {
       if (c.tuple.mode != c0.tuple.mode || c.tuple.raw_offset != c0.tuple.raw_offset ||
           c.tuple.raw_length != c0.tuple.raw_length)
@@ -385,8 +386,16 @@ QueueSchedule BatchedQueueManager::run(const DeviceHostMemory& dmem, HostMemory*
   for (std::size_t q = 0; q < Q; ++q) n[q] = batches[q].tx.size();
   out.resize(Q);
   for (RxBatchResult& r : out) clear_result(r);
-  // a HostMemory: the manager's one mirror of it (every stage shares it)
-  BatchedQueuePair::HostImage* img = hmem ? &fused_->bind_image(*hmem) : nullptr;
+  // a HostMemory: the manager's one mirror of it (every stage shares it); with
+  // host_memory_faults its window comes from the reads the memory allows
+  bool checked = false;
+  for (const auto& qp : qps_) checked = checked || qp->config.host_memory_faults;
+  std::byte* window = nullptr;
+  if (hmem && checked) {
+    std::vector<TxDescriptor> scratch;
+    for (std::size_t q = 0; q < Q && !window; ++q) window = rx_stage_detail::checked_reads(*hmem, batches[q].tx, scratch);
+  }
+  BatchedQueuePair::HostImage* img = hmem ? &fused_->bind_image(*hmem, checked, window) : nullptr;
   const std::size_t mem_size = hmem ? hmem->config().size_bytes : dmem.size;
   last_fused_ = 0;
   bool fused = false;

@@ -263,12 +263,22 @@ void add_stats(QueuePairStats& a, const QueuePairStats& b) {
   a.rx_gro_aggregated += b.rx_gro_aggregated;
 }
 
+bool write_check_thunk(const void* w, std::uint64_t a, std::uint64_t n) {
+  return static_cast<const DmaWriteCheck*>(w)->write_ok(a, n);
+}
+
 Ctx make_ctx(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
-             std::span<const std::uint16_t> cs, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx) {
+             std::span<const std::uint16_t> cs, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
+             const DmaWriteCheck* wcheck = nullptr) {
   const std::size_t np = plan.pieces.size();
   if (cs.size() < (plan.split4 ? 2 * np : np)) throw std::invalid_argument("resolve: fewer piece sums than the plan's pieces");
-  return Ctx{config.queue_id, config.max_mtu, mem_size,  plan.packets.data(), cs.data(),
-             plan.split4 ? cs.data() + np : nullptr,   tx.data(), rx.data(), rx.size()};
+  Ctx C{config.queue_id, config.max_mtu, mem_size,  plan.packets.data(), cs.data(),
+        plan.split4 ? cs.data() + np : nullptr,   tx.data(), rx.data(), rx.size()};
+  if (wcheck) {
+    C.wcheck = wcheck;
+    C.wcheck_fn = &write_check_thunk;
+  }
+  return C;
 }
 
 std::size_t rx_need(const Ctx& C, std::size_t i) { return nicqp::rx_need(C, i); }
@@ -319,11 +329,13 @@ struct PlaceSink {
 void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
              std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
              std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
-             std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx, unsigned max_threads) {
-  const Ctx C = make_ctx(config, mem_size, plan, piece_csum, tx, rx);
+             std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx, unsigned max_threads,
+             const DmaWriteCheck* wcheck) {
+  const Ctx C = make_ctx(config, mem_size, plan, piece_csum, tx, rx, wcheck);
   const std::size_t n = tx.size();
   const std::size_t want = max_threads ? max_threads : (config.host_threads ? config.host_threads : 16);
-  const Chunks ch(n, config.on_interrupt ? 1 : want, max_threads ? 1 : 32768);
+  // (the memory's write verdicts are asked in posting order, on this thread)
+  const Chunks ch(n, (config.on_interrupt || wcheck) ? 1 : want, max_threads ? 1 : 32768);
   std::size_t from = 0, rc = 0;  // first TX descriptor the sequential pass resolves, and its ring position
   std::size_t nmulti = 0;         // packets of more than one segment (only they can abort early)
   static thread_local std::vector<std::uint32_t> need_tl;
@@ -635,8 +647,9 @@ bool buffers_disjoint(std::size_t mem_size, std::span<const TxDescriptor> tx, st
 std::size_t resolve_prefix(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
                            std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
                            std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
-                           std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx) {
-  const Ctx C = make_ctx(config, mem_size, plan, piece_csum, tx, rx);
+                           std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx,
+                           const DmaWriteCheck* wcheck) {
+  const Ctx C = make_ctx(config, mem_size, plan, piece_csum, tx, rx, wcheck);
   out.tx_completions.clear();
   out.rx_completions.clear();
   writes.clear();
@@ -660,6 +673,27 @@ std::size_t resolve_prefix(const BatchedQueuePairConfig& config, std::size_t mem
   out.tx_processed = i;
   out.rx_consumed = rc;
   return i;
+}
+
+std::byte* checked_reads(const HostMemory& m, std::span<const TxDescriptor> tx, std::vector<TxDescriptor>& out) {
+  const std::uint64_t size = m.config().size_bytes;
+  out.assign(tx.begin(), tx.end());
+  const std::byte* window = nullptr;
+  for (TxDescriptor& t : out) {
+    // DMAEngine::read -> HostMemory::read -> translate_const (dma_engine.cpp:12-21)
+    ConstHostMemoryView v{};
+    if (!m.translate_const(t.buffer_address, t.length, v).ok()) {
+      t.buffer_address = size + 1;  // refused: a read fault (queue_pair.cpp:96-103)
+      continue;
+    }
+    if (v.address != t.buffer_address)
+      throw GpuError("host_memory_faults: a TX read is translated to another address (not modelled)", NICGPU_ERR_INVALID);
+    const std::byte* w = v.data - t.buffer_address;
+    if (window && w != window)
+      throw GpuError("host_memory_faults: the memory's reads do not share one flat window", NICGPU_ERR_INVALID);
+    window = w;
+  }
+  return const_cast<std::byte*>(window);
 }
 
 void schedule_writes(std::span<const SegmentWrite> writes, std::span<const std::int64_t> write_of_rx,
@@ -723,7 +757,7 @@ void schedule_writes(std::span<const SegmentWrite> writes, std::span<const std::
 
 void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
                std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out, BatchScratch& S,
-               Backend& dev, int disjoint_hint) {
+               Backend& dev, int disjoint_hint, const DmaWriteCheck* wcheck) {
   using clock = std::chrono::steady_clock;
   auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
   constexpr auto kSuccess = static_cast<std::uint32_t>(CompletionCode::Success);
@@ -775,10 +809,10 @@ void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
     t = clock::now();
     std::size_t k;
     if (disjoint) {
-      resolve(config, mem_size, S.plan, cs, txs, rxs, stats, part, S.writes, S.write_of_rx);
+      resolve(config, mem_size, S.plan, cs, txs, rxs, stats, part, S.writes, S.write_of_rx, 0, wcheck);
       k = txs.size();
     } else {
-      k = resolve_prefix(config, mem_size, S.plan, cs, txs, rxs, stats, part, S.writes, S.write_of_rx);
+      k = resolve_prefix(config, mem_size, S.plan, cs, txs, rxs, stats, part, S.writes, S.write_of_rx, wcheck);
     }
     out.timings.resolve_us += us_since(t);
     const std::size_t nrx = part.rx_completions.size();
@@ -1071,6 +1105,26 @@ private:
 // cycles through all of them, so batch k's buffers stay untouched while its
 // results come down, batch k+1 is planned and resolved and batch k+2's
 // descriptors go up.
+namespace {
+// host_memory_faults: a HostMemory's verdict on each DMA write, as
+// DMAEngine::write reaches it (HostMemory::write -> translate,
+// dma_engine.cpp:23-32, simple_host_memory.cpp:58-68): refused -> the
+// reference's Fault completion; allowed -> the write lands where the window
+// puts it (a translation elsewhere is not modelled).
+struct MemWriteCheck final : rx_stage_detail::DmaWriteCheck {
+  HostMemory* mem = nullptr;
+  std::byte* window = nullptr;  // host address 0 (the registered window)
+  bool write_ok(std::uint64_t a, std::uint64_t n) const override {
+    HostMemoryView v{};
+    if (!mem->translate(a, n, v).ok()) return false;
+    if (v.address != a || window == nullptr || v.data != window + a)
+      throw GpuError("host_memory_faults: an RX write is translated to another address (not modelled)",
+                     NICGPU_ERR_INVALID);
+    return true;
+  }
+};
+}  // namespace
+
 struct BatchedQueuePair::Slot {
   nicgpu_qp* qp = nullptr;   // device resolve context (same device as the Scratch streams)
   void* ev_tx = nullptr;     // TX descriptors uploaded
@@ -1131,6 +1185,11 @@ struct BatchedQueuePair::Slot {
   std::uint64_t tx_lo = 0, tx_hi = 0, tx_bytes = 0, rx_lo = 0, rx_hi = 0;
   std::vector<Slot*> dep_stage, dep_rx;
   std::vector<rx_stage_detail::SegmentWrite> applied;
+  // host_memory_faults: the TX descriptors with refused reads moved out of
+  // bounds (the batch runs on these), and the memory's write verdicts
+  std::vector<TxDescriptor> checked_tx;
+  MemWriteCheck mem_writes;
+  const rx_stage_detail::DmaWriteCheck* wcheck = nullptr;
   DevBuf wbuf, stage_tx;
   HostBuf h_applied;
   // a manager's fused batch (process_queues): nseg queue pairs; their RSS
@@ -1482,7 +1541,8 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
 
 void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out, void* stream,
-                               int disjoint, double& check_us, std::vector<rx_stage_detail::SegmentWrite>* applied) {
+                               int disjoint, double& check_us, std::vector<rx_stage_detail::SegmentWrite>* applied,
+                               const rx_stage_detail::DmaWriteCheck* wcheck) {
   using clock = std::chrono::steady_clock;
   out.dev = RxBatchResult::DeviceResults{};
   if (disjoint < 0) {
@@ -1491,7 +1551,7 @@ void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDe
     check_us += std::chrono::duration<double, std::micro>(clock::now() - t0).count();
   }
   GpuBackend dev{*scratch_, mem, config_, stream, applied};
-  rx_stage_detail::run_batch(quiet_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint);
+  rx_stage_detail::run_batch(quiet_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint, wcheck);
 }
 
 void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDescriptors& d, RxBatchResult& out,
@@ -1628,7 +1688,12 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
   sl.ntx_dev = d ? d->ntx : 0;
   sl.nrx_dev = d ? d->nrx : 0;
   sl.fetched = false;
-  const bool device = config_.device_resolve && (d ? device_fits(d->ntx, d->nrx) : device_fits(tx.size(), rx.size()));
+  // host_memory_faults (checked image batches): the host resolve asks the
+  // memory for every write's verdict (submit set the slot's descriptors)
+  const bool checked = img && config_.host_memory_faults;
+  sl.wcheck = checked ? &sl.mem_writes : nullptr;
+  const bool device = !checked && config_.device_resolve &&
+                      (d ? device_fits(d->ntx, d->nrx) : device_fits(tx.size(), rx.size()));
   // host descriptors go up now, on this thread, beside the earlier batches'
   // device work (device descriptors are copied in the job, in stream order);
   // the rest runs in submission order on the job thread
@@ -2289,13 +2354,26 @@ void BatchedQueuePair::finish(Slot& sl, RxBatchResult& out, QueuePairStats* st) 
 // DMA writes delivered (:416-426) come back — nothing else of the memory is
 // read or written by the device.
 
-BatchedQueuePair::HostImage& BatchedQueuePair::bind_image(HostMemory& m) {
+BatchedQueuePair::HostImage& BatchedQueuePair::bind_image(HostMemory& m, bool checked, std::byte* window) {
   Scratch& S = *scratch_;
   int dev = 0;
   check(nicgpu_get_device(&dev), "nicgpu_get_device");
   const std::size_t size = m.config().size_bytes;
   std::byte* host = nullptr;
-  if (size) {
+  if (checked) {
+    // host_memory_faults: the window the batch's allowed reads showed, else the
+    // whole memory's translation when it is allowed; none when every access
+    // so far is refused (then no byte is read, and none written)
+    host = window;
+    if (!host && size) {
+      HostMemoryView v{};
+      if (m.translate(0, size, v).ok() && v.address == 0 && v.length == size) host = v.data;
+    }
+    HostImage& I = *S.img;
+    if (!host && I.mem == &m && I.size == size && I.device == dev) return I;  // keep the known window
+    if (reinterpret_cast<std::uintptr_t>(host) & 15u)
+      throw GpuError("process_batch: HostMemory window is not 16-B aligned", NICGPU_ERR_INVALID);
+  } else if (size) {
     HostMemoryView v{};
     const HostMemoryResult r = m.translate(0, size, v);
     if (!r.ok() || v.data == nullptr || v.length != size)
@@ -2322,11 +2400,13 @@ BatchedQueuePair::HostImage& BatchedQueuePair::bind_image(HostMemory& m) {
   I.size = size;
   I.device = dev;
   if (size) {
-    void* alias = nullptr;
-    int owned = 0;
-    check(nicgpu_host_register(host, size, &alias, &owned), "nicgpu_host_register");
-    I.alias = static_cast<std::uint8_t*>(alias);
-    I.owned = owned != 0;
+    if (host) {
+      void* alias = nullptr;
+      int owned = 0;
+      check(nicgpu_host_register(host, size, &alias, &owned), "nicgpu_host_register");
+      I.alias = static_cast<std::uint8_t*>(alias);
+      I.owned = owned != 0;
+    }
     I.mirror.get((size + 15) / 16 * 16);
   }
   return I;
@@ -2444,7 +2524,7 @@ void BatchedQueuePair::image_host_path(Slot& sl, std::span<const TxDescriptor> t
   check(nicgpu_stream_wait_event(stream, sl.ev_staged), "nicgpu_stream_wait_event");
   for (Slot* p : sl.dep_rx) check(nicgpu_stream_wait_event(stream, p->ev_wb), "nicgpu_stream_wait_event");
   sl.applied.clear();
-  on_host(sl.image->view(), tx, rx, st, out, stream, disjoint, check_us, &sl.applied);
+  on_host(sl.image->view(), tx, rx, st, out, stream, disjoint, check_us, &sl.applied, sl.wcheck);
   out.timings.host_image = true;
   out.timings.staged_whole = sl.whole;
   const std::size_t n = sl.applied.size();
@@ -2472,9 +2552,15 @@ void BatchedQueuePair::process_batch(HostMemory& m, std::span<const TxDescriptor
   int dev = 0;
   check(nicgpu_get_device(&dev), "nicgpu_get_device");
   S.ensure(dev);
-  HostImage& I = bind_image(m);
-  const DeviceHostMemory mem = I.view();
   Slot& sl = S.slot[0];
+  const bool checked = config_.host_memory_faults;
+  std::byte* window = nullptr;
+  if (checked) tx = checked_tx(sl, m, tx, window);  // the reads' verdicts, before anything is written
+  HostImage& I = bind_image(m, checked, window);
+  sl.mem_writes.mem = &m;
+  sl.mem_writes.window = I.host;
+  sl.wcheck = checked ? &sl.mem_writes : nullptr;
+  const DeviceHostMemory mem = I.view();
   sl.tx_dev = nullptr;
   sl.rx_dev = nullptr;
   sl.multi = false;
@@ -2486,7 +2572,7 @@ void BatchedQueuePair::process_batch(HostMemory& m, std::span<const TxDescriptor
   double check_us = 0;
   bool on_device = false;
   try {
-    if (config_.device_resolve && device_fits(tx.size(), rx.size())) {
+    if (!checked && config_.device_resolve && device_fits(tx.size(), rx.size())) {
       upload(sl, tx, rx, true);
       image_stage(sl, tx.size(), tx.data(), sl.v.tx, S.side_up);
       on_device = front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);
@@ -2519,8 +2605,20 @@ void BatchedQueuePair::submit(HostMemory& m, std::span<const TxDescriptor> tx, s
   check(nicgpu_get_device(&dev), "nicgpu_get_device");
   if (S.pending == 0) S.ensure(dev);
   else if (S.device != dev) throw std::logic_error("submit: batches pending on another device");
-  HostImage& I = bind_image(m);
+  Slot& sl = S.slot[(S.head + S.pending) % Scratch::kSlots];
+  const bool checked = config_.host_memory_faults;
+  std::byte* window = nullptr;
+  if (checked) tx = checked_tx(sl, m, tx, window);  // kept in the slot until collected
+  HostImage& I = bind_image(m, checked, window);
+  sl.mem_writes.mem = &m;
+  sl.mem_writes.window = I.host;
   enqueue(I.view(), tx, rx, nullptr, stream, &I);
+}
+
+std::span<const TxDescriptor> BatchedQueuePair::checked_tx(Slot& sl, HostMemory& m, std::span<const TxDescriptor> tx,
+                                                           std::byte*& window) {
+  window = rx_stage_detail::checked_reads(m, tx, sl.checked_tx);
+  return sl.checked_tx;
 }
 
 // ------------------------------------------------------------------------
@@ -2635,6 +2733,7 @@ bool BatchedQueuePair::process_queues(const DeviceHostMemory& mem_in, HostImage*
   sl.tx_dev = nullptr;
   sl.rx_dev = nullptr;
   sl.image = nullptr;
+  sl.wcheck = nullptr;
   sl.staged = false;
   sl.dep_stage.clear();
   sl.dep_rx.clear();

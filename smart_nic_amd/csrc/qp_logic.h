@@ -279,7 +279,26 @@ struct Ctx {
   // the :434-447 check is taken to pass and the completion marked for the
   // delivery, which sums the bytes it writes and patches the failures
   bool late = false;
+  // host resolve on a HostMemory with faults modelled (host_memory_faults):
+  // each DMA write's verdict is the memory's own translate(address, length)
+  // (DMAEngine::write, dma_engine.cpp:23-32), asked here in posting order;
+  // null: the bounds rule alone.  Never set on the device.
+  const void* wcheck = nullptr;
+  bool (*wcheck_fn)(const void*, uint64_t, uint64_t) = nullptr;
 };
+
+// The memory's verdict on a DMA write the bounds rule allows (Ctx::wcheck).
+template <class C_>
+NICQP_HD bool write_allowed(const C_& C, uint64_t addr, uint64_t len) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  (void) C;
+  (void) addr;
+  (void) len;
+  return true;
+#else
+  return C.wcheck_fn == nullptr || C.wcheck_fn(C.wcheck, addr, len);
+#endif
+}
 
 // A deferred completion's bits (the delivery's stats correction on a failure)
 enum : uint32_t { kLateDeferred = 1, kLateStripBase = 2, kLateVlanInsert = 4 };
@@ -445,7 +464,7 @@ NICQP_HD uint64_t resolve_packet(const Ctx<Tx, Rx, Plan>& C, uint64_t i, uint64_
       return rc - rc0;
     }
     // :416-426 DMA write
-    if (!dma_ok(C.mem_size, xr.buffer_address, size)) {
+    if (!dma_ok(C.mem_size, xr.buffer_address, size) || !write_allowed(C, xr.buffer_address, size)) {
       sink.tx(make_tx<Comp>(qid, t, kFault, total, tso, gso), false);
       sink.rx(make_completion<Comp>(qid, xr.descriptor_index, kFault), (const Write*) nullptr);
       return rc - rc0;

@@ -27,6 +27,7 @@
 #include "nic/rx_stage.h"
 #include "nic/simple_host_memory.h"
 #include "cpu_backend.h"
+#include "fault_model.h"
 #include "oracle.h"
 
 using namespace nic;
@@ -34,6 +35,7 @@ using namespace nic;
 namespace {
 
 std::size_t g_overlapping = 0, g_split = 0, g_snap = 0;  // batches that took each careful step
+std::size_t g_faulty = 0;  // batches on a memory with its own DMA faults
 int g_steps_max = 0;                                        // most relaxation steps a batch needed
 std::size_t g_split_pieces_saved = 0;                       // pieces the split plans did without
 
@@ -63,7 +65,9 @@ bool same(const QueuePairStats& a, const QueuePairStats& b) { return std::memcmp
 // writes of QueuePair::handle_rx_segment, :416-426) in order.
 class RecordingMemory final : public HostMemory {
 public:
-  explicit RecordingMemory(HostMemoryConfig c) : mem_(c) {}
+  explicit RecordingMemory(HostMemoryConfig c, SimpleHostMemory::AddressTranslator tr = {},
+                           SimpleHostMemory::FaultInjector fi = {})
+      : mem_(c, std::move(tr), std::move(fi)) {}
   HostMemoryConfig config() const noexcept override { return mem_.config(); }
   HostMemoryResult translate(HostAddress a, std::size_t n, HostMemoryView& v) override { return mem_.translate(a, n, v); }
   HostMemoryResult translate_const(HostAddress a, std::size_t n, ConstHostMemoryView& v) const override {
@@ -268,10 +272,19 @@ int run_case(std::uint64_t seed) {
   for (auto& q : rss_table) q = static_cast<std::uint16_t>(r.below(16));
   const RssConfig rss_cfg{r.below(2) ? ms_key : std::vector<std::uint8_t>{}, rss_table};
 
+  // the memory's own DMA faults in a third of the cases (tests/cpp/fault_model.h:
+  // SimpleHostMemory's FaultInjector or an IOMMU translator), which the stage
+  // models with host_memory_faults' verdicts (checked_reads, DmaWriteCheck)
+  faultfx::Model fm;
+  fm.kind = r.below(3) == 0 ? static_cast<faultfx::Kind>(1 + r.below(2)) : faultfx::kNone;
+  if (fm.kind != faultfx::kNone) g_faulty += 1;
+
   // ---- reference
-  RecordingMemory mem{HostMemoryConfig{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false}};
+  const HostMemoryConfig hmc{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = fm.kind == faultfx::kIommu};
+  RecordingMemory mem = fm.kind ? RecordingMemory{hmc, fm.translator(), fm.injector()} : RecordingMemory{hmc};
   assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(image))).ok());
   mem.recording = true;
+  *fm.armed = true;
   DMAEngine dma{mem};
   std::size_t ref_irq = 0;
   MsixTable table(8);
@@ -304,6 +317,7 @@ int run_case(std::uint64_t seed) {
   std::vector<CompletionEntry> ref_tx, ref_rx;
   while (auto c = qp.tx_completion().poll_completion()) ref_tx.push_back(*c);
   while (auto c = qp.rx_completion().poll_completion()) ref_rx.push_back(*c);
+  *fm.armed = false;
   std::vector<std::byte> ref_after(mem_size);
   assert(mem.read(0, ref_after).ok());
 
@@ -328,7 +342,25 @@ int run_case(std::uint64_t seed) {
   RxBatchResult out;
   QueuePairStats st{};
   BatchScratch scratch;
-  run_batch(cfg, mem_size, tx, rx, st, out, scratch, dev);
+  if (fm.kind != faultfx::kNone) {
+    // the verdicts of a memory with the same faults (its bytes do not matter)
+    SimpleHostMemory verdicts{hmc, fm.translator(), fm.injector()};
+    *fm.armed = true;
+    struct Writes final : DmaWriteCheck {
+      HostMemory* m;
+      bool write_ok(std::uint64_t a, std::uint64_t n) const override {
+        HostMemoryView v{};
+        return m->translate(a, n, v).ok();
+      }
+    } wv;
+    wv.m = &verdicts;
+    std::vector<TxDescriptor> ctx;
+    checked_reads(verdicts, tx, ctx);
+    run_batch(cfg, mem_size, ctx, rx, st, out, scratch, dev, -1, &wv);
+    *fm.armed = false;
+  } else {
+    run_batch(cfg, mem_size, tx, rx, st, out, scratch, dev);
+  }
   if (buffers_disjoint(mem_size, tx, rx) != disjoint_brute(mem_size, tx, rx)) {
     std::fprintf(stderr, "seed %llu: buffers_disjoint differs from the pairwise check\n", (unsigned long long) seed);
     return 1;
@@ -505,7 +537,8 @@ int main(int argc, char** argv) {
   for (std::uint64_t s = first; s < first + count; ++s) bad += run_case(s);
   if (bad) return 1;
   std::printf("rx_stage_fuzz: ok (%llu batches; %zu with overlapping buffers, %zu split into sub-batches, %zu gathered "
-              "from a copy; relaxation settled every batch in <= %d steps; split plans equal, %zu pieces fewer)\n",
-              (unsigned long long) count, g_overlapping, g_split, g_snap, g_steps_max, g_split_pieces_saved);
+              "from a copy; %zu on a memory with its own DMA faults; relaxation settled every batch in <= %d steps; split "
+              "plans equal, %zu pieces fewer)\n",
+              (unsigned long long) count, g_overlapping, g_split, g_snap, g_faulty, g_steps_max, g_split_pieces_saved);
   return 0;
 }

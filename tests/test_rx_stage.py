@@ -24,6 +24,9 @@ from test_host_cpp import _build
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 CASES = ["qp_mix_a", "qp_mix_b", "qp_tso", "qp_alias"]
+# the memory's own DMA faults: SimpleHostMemory's FaultInjector / IOMMU
+# translator (tests/cpp/fault_model.h), generated through the reference QueuePair
+FAULT_CASES = ["qp_fault_inj", "qp_fault_iommu", "qp_fault_tso"]
 
 
 def _flatten(name, out_dir):
@@ -47,6 +50,9 @@ def _flatten(name, out_dir):
 def _run(exe, mode, name, tmp_path):
     exp = _flatten(name, str(tmp_path))
     args = [exe, mode, exp] + [os.path.join(GOLDEN, f"{name}.{k}.bin") for k in ("mem", "tx", "rx")]
+    faults = json.load(open(os.path.join(GOLDEN, name + ".json"))).get("faults", 0)
+    if faults:
+        args.append(str(faults))
     r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert f"rx_stage_test {mode}: ok" in r.stdout
@@ -68,6 +74,37 @@ def test_rx_stage_host_logic(tmp_path):
     exe = _build(tmp_path, "rx_stage_test")
     for n in CASES:
         _run(exe, "cpu", n, tmp_path)
+
+
+def test_fault_fixture_coverage():
+    """The fault fixtures post the reference's Fault completions on both sides
+    (refused TX reads and refused RX writes) besides every other status."""
+    for n in FAULT_CASES:
+        d = json.load(open(os.path.join(GOLDEN, n + ".json")))
+        assert d["faults"] in (1, 2)
+        assert sum(c[2] == 4 for c in d["tx_completions"]) >= 10
+        assert sum(c[2] == 4 for c in d["rx_completions"]) >= 5
+        assert sum(c[2] == 0 for c in d["rx_completions"]) >= 40
+
+
+def test_rx_stage_fault_host_logic(tmp_path):
+    """The host resolve with the memory's own verdicts (checked_reads + a
+    DmaWriteCheck) over the CPU backend equals the reference on every fault
+    fixture."""
+    exe = _build(tmp_path, "rx_stage_test")
+    for n in FAULT_CASES:
+        _run(exe, "cpu", n, tmp_path)
+
+
+@pytest.mark.gpu
+def test_rx_stage_faults_host_memory_gpu(tmp_path):
+    """The product path with host_memory_faults on a faulty HostMemory (the
+    fixture's injector / IOMMU over a FlatHostMemory, in SimpleHostMemory's
+    order): completions, stats, RSS and the memory's bytes equal the
+    reference's; process_batch and submit/collect."""
+    exe = _build(tmp_path, "rx_stage_test")
+    for n in FAULT_CASES:
+        _run(exe, "host", n, tmp_path)
 
 
 @pytest.mark.gpu
@@ -100,6 +137,9 @@ def test_rx_stage_reference_simple_host_memory_gpu(tmp_path):
     oracle/_ref/rx_stage_test_refmem, which travels to the GPU box): the
     stage drops in on the reference's memory object unchanged."""
     for n in CASES:
+        _run(REFMEM, "host", n, tmp_path)
+    # and with the reference SimpleHostMemory's own FaultInjector / translator
+    for n in FAULT_CASES:
         _run(REFMEM, "host", n, tmp_path)
 
 
