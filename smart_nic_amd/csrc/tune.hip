@@ -262,3 +262,63 @@ extern "C" int nicgpu_tune_unaligned_copy(const uint8_t* src, uint8_t* dst, uint
                      dst, n, soff, doff);
   return hip_status(hipGetLastError());
 }
+
+// ---- segmentation copy ceiling ----------------------
+// The write pattern of nicgpu_tso_segment on C5 without its work: frame f's
+// segment k (k < nseg) is the seg_k = hlen + (k < nseg - 1 ? mss : last)
+// bytes at frame offset k * mss (the header's re-read included) copied to slot
+// f * nseg + k of `stride` bytes; consecutive lanes on consecutive 16-B chunks
+// (16-B loads at the source's alignment, 16-B stores), the segment's last
+// chunk stored in part (byte stores: a partial-line write, as segmentation
+// must leave the slot's tail alone) unless PAD (the whole chunk written).
+namespace {
+template <bool NT, bool PAD>
+__global__ __launch_bounds__(256) void seg_copy_kernel(const uint8_t* __restrict__ frames, uint32_t nframes,
+                                                       uint32_t fstride, uint8_t* __restrict__ out, uint32_t stride,
+                                                       uint32_t hlen, uint32_t mss, uint32_t nseg, uint32_t last) {
+  const uint32_t segF = hlen + mss, segL = hlen + last;
+  const uint32_t nchF = (segF + 15u) / 16u, nchL = (segL + 15u) / 16u;
+  const uint32_t per = (nseg - 1u) * nchF + nchL;
+  const uint64_t total = (uint64_t) nframes * per;
+  const uint64_t step = (uint64_t) gridDim.x * blockDim.x;
+  for (uint64_t c = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; c < total; c += step) {
+    const uint32_t f = (uint32_t) (c / per), r = (uint32_t) (c - (uint64_t) f * per);
+    uint32_t k = r / nchF;
+    if (k > nseg - 1u) k = nseg - 1u;
+    const uint32_t ch = r - k * nchF;
+    const uint32_t seg = k + 1u < nseg ? segF : segL;
+    const uint8_t* s = frames + (uint64_t) f * fstride + (uint64_t) k * mss + 16u * ch;
+    uint8_t* d = out + ((uint64_t) f * nseg + k) * stride + 16u * ch;
+    u32x4 v;
+    __builtin_memcpy(&v, s, 16);
+    const uint32_t rem = seg - 16u * ch;
+    if (PAD || rem >= 16u) {
+      if (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(d));
+      else *reinterpret_cast<u32x4*>(d) = v;
+    } else {
+      uint8_t b[16];
+      __builtin_memcpy(b, &v, 16);
+      for (uint32_t i = 0; i < rem; ++i) d[i] = b[i];
+    }
+  }
+}
+}  // namespace
+
+extern "C" int nicgpu_tune_seg_copy(const uint8_t* frames, uint32_t nframes, uint32_t fstride, uint8_t* out,
+                                    uint32_t stride, uint32_t hlen, uint32_t mss, uint32_t nseg, uint32_t last,
+                                    int blocks_per_cu, int flags, void* stream) {
+  const DeviceInfo* di = nullptr;
+  int st = current_device_info(&di);
+  if (st != NICGPU_OK) return st;
+  if (!frames || !out || nseg == 0 || mss == 0 || (stride & 15u) || stride < ((hlen + mss + 15u) & ~15u) ||
+      ((uint64_t) nframes * ((nseg * (hlen + mss)) / 16u + nseg) >= (1ull << 32)))
+    return NICGPU_ERR_INVALID;
+  const unsigned grid = (unsigned) (di->cus * (blocks_per_cu > 0 ? blocks_per_cu : 8));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool nt = flags & 1, pad = flags & 2;
+  if (nt && pad) hipLaunchKernelGGL((seg_copy_kernel<true, true>), dim3(grid), dim3(256), 0, s, frames, nframes, fstride, out, stride, hlen, mss, nseg, last);
+  else if (nt) hipLaunchKernelGGL((seg_copy_kernel<true, false>), dim3(grid), dim3(256), 0, s, frames, nframes, fstride, out, stride, hlen, mss, nseg, last);
+  else if (pad) hipLaunchKernelGGL((seg_copy_kernel<false, true>), dim3(grid), dim3(256), 0, s, frames, nframes, fstride, out, stride, hlen, mss, nseg, last);
+  else hipLaunchKernelGGL((seg_copy_kernel<false, false>), dim3(grid), dim3(256), 0, s, frames, nframes, fstride, out, stride, hlen, mss, nseg, last);
+  return hip_status(hipGetLastError());
+}

@@ -204,6 +204,40 @@ def main():
             # read frames once + write the segments + 8 B desc, 12 B per-frame params, 6 B per segment out
             report(row, "c5", n, fb, fb + written + 20 * n + 6 * total, region, med,
                    {"segments": total, "bytes_written": written})
+        elif row == "seg_copy_c5":
+            # the segmentation row's ceiling: a plain copy
+            # with tso_seg_c5's write pattern (libnicgpu_tune.so
+            # nicgpu_tune_seg_copy: each 1506-B segment at the slot stride,
+            # its last chunk written in part), best of a small sweep; and the
+            # same copy with whole last chunks (pad) for the partial-line cost
+            import ctypes
+
+            n, fb, f, d = batch("c5")
+            H, MSS, STRIDE = 54, 1448, 1536
+            nseg, last = 7, 9000 - 54 - 6 * 1448
+            tl = ctypes.CDLL(os.path.join(ROOT, "smart_nic_amd", "libnicgpu_tune.so"))
+            vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+            tl.nicgpu_tune_seg_copy.restype = i32
+            tl.nicgpu_tune_seg_copy.argtypes = [vp, u32, u32, vp, u32, u32, u32, u32, u32, i32, i32, vp]
+            fstride = (9000 + 15) // 16 * 16
+            out = torch.empty(n * nseg * STRIDE, dtype=torch.uint8, device=dev)
+            sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            written = int(n * nseg * (H + 4) + n * (9000 - H))
+            sweep = {}
+            for flags in (0, 1, 2, 3):
+                for bpc in (4, 8, 16):
+                    def fn(flags=flags, bpc=bpc):
+                        rc = tl.nicgpu_tune_seg_copy(f.data_ptr(), n, fstride, out.data_ptr(), STRIDE, H + 4, MSS, nseg,
+                                                     last, bpc, flags, sp)
+                        assert rc == 0, rc
+                    sweep[(flags, bpc)] = timed(torch, fn, args.steps, args.warmup)
+            best = min((v[1], k) for k, v in sweep.items() if not k[0] & 2)
+            best_pad = min((v[1], k) for k, v in sweep.items() if k[0] & 2)
+            region = sweep[best[1]][0]
+            report(row, "c5", n, fb, fb + written + 20 * n + 6 * n * nseg, region, best[0],
+                   {"segments": n * nseg, "bytes_written": written, "best": {"nt": best[1][0] & 1, "blocks_per_cu": best[1][1]},
+                    "pad_best_us": round(best_pad[0], 2),
+                    "sweep_median_us": {f"nt{k[0] & 1}_pad{k[0] >> 1}_bpc{k[1]}": round(v[1], 2) for k, v in sweep.items()}})
         else:
             raise SystemExit(f"unknown row {row}")
 
