@@ -7,15 +7,19 @@
 // refuses the entry and counts it); poll() is CompletionQueue::poll_completion.
 // A batch whose results stayed in HBM (results_on_device) is posted from its
 // device lists without leaving the device.
-// No doorbell: the reference's post_completion rings Doorbell{queue_id,
-// producer} after every post (completion_queue.cpp:38-39); the device rings do
-// not.  A caller that needs the doorbell sequence derives it from the rings'
-// producers (state()): the last doorbell of a batch on queue q carries
-// state(q).producer.
+// Doorbells: the reference's post_completion rings Doorbell{queue_id,
+// producer} after every post it accepts (completion_queue.cpp:30-41).  The
+// device rings place a batch's entries in parallel; with set_doorbell() post()
+// then rings the same sequence through a callback — one call per accepted
+// entry, in the batch's posting order across queues, each with its queue's
+// CompletionQueueConfig::queue_id and the producer index that post left.
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <optional>
+#include <span>
+#include <utility>
 #include <vector>
 
 #include "nic/rx_stage.h"
@@ -44,8 +48,16 @@ public:
   std::optional<CompletionEntry> poll(std::size_t q);
   std::vector<CompletionEntry> poll(std::size_t q, std::size_t max);
   [[nodiscard]] State state(std::size_t q) const;
+  /// What Doorbell::ring receives per accepted post (DoorbellPayload{queue_id,
+  /// data = producer}); queue_ids[q] is ring q's CompletionQueueConfig::queue_id
+  /// (default q).  With a doorbell, post() synchronises `stream`.  An empty
+  /// function turns it off.
+  using DoorbellFn = std::function<void(std::uint16_t queue_id, std::uint32_t producer)>;
+  void set_doorbell(DoorbellFn ring, std::vector<std::uint16_t> queue_ids = {});
 
 private:
+  DoorbellFn bell_;
+  std::vector<std::uint16_t> bell_ids_;
   nicgpu_cq_set* cq_{nullptr};
   std::size_t nq_{0}, ring_{0};
   int device_{0};
@@ -53,5 +65,20 @@ private:
   void* up_which_{nullptr};
   std::size_t cap_rxc_{0}, cap_which_{0};
 };
+
+namespace rss_rings_detail {
+/// The doorbells one post rings: which[start[q] .. end[q]) are queue q's
+/// completion indices in posting order (< n); before[q] its ring's state
+/// before the post.  Entry k of list q is accepted while k < ring_size -
+/// before[q].count and then rings (queue_ids[q], (before[q].producer + k + 1)
+/// % ring_size); the doorbells come out in posting order (completion index),
+/// as the reference's one-by-one posts ring them.
+std::vector<std::pair<std::uint16_t, std::uint32_t>> doorbells(std::span<const std::uint32_t> which,
+                                                               std::span<const std::uint32_t> start,
+                                                               std::span<const std::uint32_t> end,
+                                                               std::span<const RssCompletionRings::State> before,
+                                                               std::size_t ring_size,
+                                                               std::span<const std::uint16_t> queue_ids, std::size_t n);
+}  // namespace rss_rings_detail
 
 }  // namespace nic

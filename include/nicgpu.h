@@ -652,9 +652,10 @@ int nicgpu_cq_destroy(nicgpu_cq_set* cq);
  * rxc[which[start[q] .. end[q])] into ring q in that order, as
  * CompletionQueue::post_completion would one by one: entry i of the list
  * lands at (producer + i) % ring_size while the ring has room, the rest are
- * refused (counted).  No doorbell is rung (the reference rings
- * Doorbell{queue_id, producer} per post, completion_queue.cpp:38-39): the
- * producer nicgpu_cq_state reports is what the last one would carry.  start / end are host arrays (nicgpu_qp_group's lists,
+ * refused (counted).  No doorbell is rung here (the reference rings
+ * Doorbell{queue_id, producer} per post, completion_queue.cpp:38-39):
+ * nic::RssCompletionRings::set_doorbell rings that sequence on the host from
+ * the lists and the state before the post.  start / end are host arrays (nicgpu_qp_group's lists,
  * RxBatchResult::dev.queue_start / queue_end), rxc and which device arrays.
  * Synchronises `stream`. */
 int nicgpu_cq_post(nicgpu_cq_set* cq, const nicgpu_completion* rxc, const uint32_t* which, const uint32_t* start,

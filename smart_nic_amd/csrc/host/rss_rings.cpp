@@ -2,6 +2,7 @@
 // C-ABI's device rings (nicgpu_cq_*, csrc/cq.hip).
 #include "nic/rss_rings.h"
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -46,13 +47,72 @@ RssCompletionRings::~RssCompletionRings() {
   if (cq_) (void) nicgpu_cq_destroy(cq_);
 }
 
+namespace rss_rings_detail {
+std::vector<std::pair<std::uint16_t, std::uint32_t>> doorbells(std::span<const std::uint32_t> which,
+                                                               std::span<const std::uint32_t> start,
+                                                               std::span<const std::uint32_t> end,
+                                                               std::span<const RssCompletionRings::State> before,
+                                                               std::size_t ring_size,
+                                                               std::span<const std::uint16_t> queue_ids, std::size_t n) {
+  // at[j] = the doorbell completion j rings (queue + 1, producer), 0: none
+  std::vector<std::pair<std::uint32_t, std::uint32_t>> at(n, {0u, 0u});
+  std::size_t rung = 0;
+  for (std::size_t q = 0; q < start.size(); ++q) {
+    const std::size_t room = ring_size > before[q].count ? ring_size - before[q].count : 0;
+    const std::size_t m = std::min<std::size_t>(end[q] - start[q], room);
+    for (std::size_t k = 0; k < m; ++k) {
+      const std::uint32_t j = which[start[q] + k];
+      if (j >= n) throw std::out_of_range("doorbells: completion index past the batch");
+      at[j] = {static_cast<std::uint32_t>(q) + 1u, static_cast<std::uint32_t>((before[q].producer + k + 1) % ring_size)};
+    }
+    rung += m;
+  }
+  std::vector<std::pair<std::uint16_t, std::uint32_t>> out;
+  out.reserve(rung);
+  for (const auto& [q1, p] : at)
+    if (q1) out.emplace_back(q1 - 1 < queue_ids.size() ? queue_ids[q1 - 1] : static_cast<std::uint16_t>(q1 - 1), p);
+  return out;
+}
+}  // namespace rss_rings_detail
+
+void RssCompletionRings::set_doorbell(DoorbellFn ring, std::vector<std::uint16_t> queue_ids) {
+  if (!queue_ids.empty() && queue_ids.size() != nq_)
+    throw std::invalid_argument("RssCompletionRings::set_doorbell: one queue id per ring");
+  bell_ = std::move(ring);
+  bell_ids_ = std::move(queue_ids);
+}
+
 void RssCompletionRings::post(const RxBatchResult& r, void* stream) {
+  // with a doorbell: the rings' state before, then the accepted posts rung in
+  // the batch's posting order once the entries are placed
+  std::vector<State> before;
+  if (bell_) {
+    std::vector<std::uint32_t> s(4 * nq_);
+    ok(nicgpu_cq_state(cq_, s.data(), stream), "nicgpu_cq_state");
+    before.resize(nq_);
+    for (std::size_t q = 0; q < nq_; ++q) before[q] = State{s[q], s[nq_ + q], s[2 * nq_ + q], s[3 * nq_ + q]};
+  }
+  auto ring_bells = [&](std::span<const std::uint32_t> which, std::span<const std::uint32_t> start,
+                        std::span<const std::uint32_t> end, std::size_t n) {
+    if (!bell_) return;
+    for (const auto& [qid, p] : rss_rings_detail::doorbells(which, start, end, before, ring_, bell_ids_, n)) bell_(qid, p);
+  };
   if (r.dev.rx_completions && r.dev.queue_which) {  // results in HBM: the device lists
     const std::size_t nl = r.dev.queue_start.size();
     if (nl > nq_) throw std::invalid_argument("RssCompletionRings::post: more RSS queues than rings");
     ok(nicgpu_cq_post(cq_, reinterpret_cast<const nicgpu_completion*>(r.dev.rx_completions), r.dev.queue_which,
                       r.dev.queue_start.data(), r.dev.queue_end.data(), nl, stream),
        "nicgpu_cq_post");
+    if (bell_) {  // the lists come down for the order
+      std::size_t m = 0;
+      for (std::size_t q = 0; q < nl; ++q) m = std::max<std::size_t>(m, r.dev.queue_end[q]);
+      std::vector<std::uint32_t> which(m);
+      if (m) {
+        ok(nicgpu_memcpy_async(which.data(), r.dev.queue_which, m * sizeof(std::uint32_t), stream), "nicgpu_memcpy_async");
+        ok(nicgpu_stream_synchronize(stream), "nicgpu_stream_synchronize");
+      }
+      ring_bells(which, r.dev.queue_start, r.dev.queue_end, r.dev.nrx);
+    }
     return;
   }
   // host results: the lists and completions go up once, into staging buffers
@@ -83,6 +143,7 @@ void RssCompletionRings::post(const RxBatchResult& r, void* stream) {
   ok(nicgpu_cq_post(cq_, static_cast<const nicgpu_completion*>(up_rxc_), static_cast<const std::uint32_t*>(up_which_),
                     start.data(), end.data(), nl, stream),
      "nicgpu_cq_post");
+  ring_bells(which, start, end, n);
 }
 
 std::optional<CompletionEntry> RssCompletionRings::poll(std::size_t q) {
