@@ -914,6 +914,16 @@ bool defer_env() {
   return on;
 }
 
+// NIC_IRQ_TOUCH=1: the chunked interrupt replay's completions read once by a
+// helper thread as they land (tuning A/B; off by default)
+bool irq_touch_env() {
+  static const bool on = [] {
+    const char* e = std::getenv("NIC_IRQ_TOUCH");
+    return e && std::strcmp(e, "1") == 0;
+  }();
+  return on;
+}
+
 // One growable device buffer.
 struct DevBuf {
   void* p = nullptr;
@@ -1799,10 +1809,58 @@ void BatchedQueuePair::fire_interrupts(RxBatchResult& r, Slot* sl) {
     const std::size_t ptx = std::max<std::size_t>(1, (sl->irq_ntx + Slot::kIrqChunks - 1) / Slot::kIrqChunks);
     const std::size_t prx = std::max<std::size_t>(1, (sl->irq_nrx + Slot::kIrqChunks - 1) / Slot::kIrqChunks);
     double wait_us = 0;
+    const CompletionEntry* itx = sl->h_itx.get<CompletionEntry>(1);
+    const CompletionEntry* irx = sl->h_irx.get<CompletionEntry>(1);
+    if (irq_touch_env()) {
+      // (opt-in, NIC_IRQ_TOUCH=1) a helper on the next CPU waits for each chunk
+      // and reads it once (a load per 64-B line), so the replay finds the
+      // DMA-written completions in the shared cache instead of DRAM
+      std::atomic<int> ready[2] = {-1, -1};
+      std::atomic<bool> failed{false}, stop{false};
+      const std::vector<int> cpus = rx_stage_detail::near_cpus(2);
+      std::thread helper([&] {
+        rx_stage_detail::pin_to(cpus, 1);
+        std::uint32_t sink = 0;
+        for (int c = 0; c < Slot::kIrqChunks && !stop.load(std::memory_order_relaxed); ++c)
+          for (int side = 0; side < 2; ++side) {
+            if (nicgpu_event_synchronize(sl->ev_irq[side][c]) != NICGPU_OK) {
+              failed.store(true);
+              ready[0].store(Slot::kIrqChunks);
+              ready[1].store(Slot::kIrqChunks);
+              return;
+            }
+            const std::size_t per = side ? prx : ptx, n = side ? sl->irq_nrx : sl->irq_ntx;
+            const auto* b = reinterpret_cast<const volatile std::uint8_t*>(side ? irx : itx);
+            const std::size_t lo = std::min(n, per * c) * sizeof(CompletionEntry);
+            const std::size_t hi = (c + 1 == Slot::kIrqChunks ? n : std::min(n, per * (c + 1))) * sizeof(CompletionEntry);
+            for (std::size_t o = lo; o < hi; o += 64) sink += b[o];
+            ready[side].store(c, std::memory_order_release);
+          }
+        (void) sink;
+      });
+      struct Join {
+        std::thread& t;
+        std::atomic<bool>& stop;
+        ~Join() {
+          stop.store(true);
+          t.join();
+        }
+      } join{helper, stop};
+      rx_stage_detail::replay_interrupts_chunked(
+          config_, std::span<const CompletionEntry>(itx, sl->irq_ntx), std::span<const CompletionEntry>(irx, sl->irq_nrx),
+          ptx, prx, [&](int side, std::size_t c) {
+            const int want = static_cast<int>(std::min<std::size_t>(c, Slot::kIrqChunks - 1));
+            const auto w = clock::now();
+            while (ready[side].load(std::memory_order_acquire) < want) std::this_thread::yield();
+            if (failed.load()) check(NICGPU_ERR_HIP, "nicgpu_event_synchronize");
+            wait_us += std::chrono::duration<double, std::micro>(clock::now() - w).count();
+          });
+      r.timings.irq_wait_us = wait_us;
+      return;
+    }
     rx_stage_detail::replay_interrupts_chunked(
-        config_, std::span<const CompletionEntry>(sl->h_itx.get<CompletionEntry>(1), sl->irq_ntx),
-        std::span<const CompletionEntry>(sl->h_irx.get<CompletionEntry>(1), sl->irq_nrx), ptx, prx,
-        [sl, &wait_us](int side, std::size_t c) {
+        config_, std::span<const CompletionEntry>(itx, sl->irq_ntx), std::span<const CompletionEntry>(irx, sl->irq_nrx),
+        ptx, prx, [sl, &wait_us](int side, std::size_t c) {
           const auto w = clock::now();
           check(nicgpu_event_synchronize(sl->ev_irq[side][std::min<std::size_t>(c, Slot::kIrqChunks - 1)]),
                 "nicgpu_event_synchronize");
