@@ -184,12 +184,17 @@ struct DeviceHostMemory {
 /// descriptors live in the image itself (mem.base + the ring's address).  The
 /// stage copies them in stream order (no PCIe upload) and fetches host copies
 /// only when a host step needs them (a ring whose RX buffers are not in
-/// address order, a host tail, overlapping buffers).  The descriptors are read
-/// once, at the start of the batch; the reference DMA-reads each slot when it
-/// pops it (descriptor_ring.cpp:97-106), so an RX buffer of the batch that
-/// overlaps the descriptor arrays (inside the image) would change a later
-/// descriptor there.  That case is not modelled: process_batch / submit throw
-/// GpuError (NICGPU_ERR_INVALID) for it before anything is written.
+/// address order, a host tail, overlapping buffers).  The reference DMA-reads
+/// each ring slot when it pops it (descriptor_ring.cpp:97-106), so an RX
+/// buffer of the batch that overlaps the descriptor arrays inside the image
+/// changes the descriptors popped after its write: such a batch runs on the
+/// host path in sub-batches, each ending before the first TX descriptor whose
+/// slot, or an RX slot it may pop, an earlier write touched, and the rest of
+/// the descriptors are read again from the image (rx_stage_detail::RingSlots).
+/// One case stays refused with GpuError (NICGPU_ERR_INVALID), found while
+/// resolving, possibly after earlier sub-batches were written: a segment's
+/// write that lands on an RX slot a later segment of the same TX descriptor
+/// pops.
 struct DeviceDescriptors {
   const TxDescriptor* tx{nullptr};
   std::size_t ntx{0};
@@ -318,6 +323,7 @@ struct RxBatchResult {
 namespace rx_stage_detail {
 struct SegmentWrite;
 struct DmaWriteCheck;
+struct RingSlots;
 }
 
 /// QueuePair::process_once over a batch (src/queue_pair.cpp:67-460).
@@ -459,7 +465,9 @@ private:
   static void apply_fixups(Slot& sl, std::size_t s, QueuePairStats& st);
   void enqueue(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                const DeviceDescriptors* d, void* stream, HostImage* img = nullptr);
-  void check_rings_unwritten(Slot& sl, const DeviceHostMemory& mem, void* stream);
+  // true when a DMA write of the batch can land on its descriptor arrays inside
+  // the image (then *slots their image offsets: the host path re-reads them)
+  bool rings_written(Slot& sl, const DeviceHostMemory& mem, void* stream, rx_stage_detail::RingSlots* slots);
   void fire_interrupts(RxBatchResult& r, Slot* sl = nullptr);  // config_.on_interrupt over r's completions
   std::pair<std::span<const TxDescriptor>, std::span<const RxDescriptor>> host_spans(
       Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx, void* stream);
@@ -468,7 +476,7 @@ private:
   void on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                QueuePairStats& stats, RxBatchResult& out, void* stream, int disjoint, double& check_us,
                std::vector<rx_stage_detail::SegmentWrite>* applied = nullptr,
-               const rx_stage_detail::DmaWriteCheck* wcheck = nullptr);
+               const rx_stage_detail::DmaWriteCheck* wcheck = nullptr, const rx_stage_detail::RingSlots* slots = nullptr);
   BatchedQueuePairConfig config_;
   BatchedQueuePairConfig quiet_;  // config_ without the interrupt callback (every resolve; replayed after)
   bool defer_multi_ = false;      // process_queues: this fused batch may defer its RX verifies
@@ -575,13 +583,15 @@ void resolve(const BatchedQueuePairConfig& config, std::size_t mem_size, const P
 /// The sequential resolve, stopped before the first TX descriptor whose
 /// pieces read bytes that an earlier descriptor of this call writes (that
 /// descriptor must see the written bytes, so its sums are taken again after the
-/// writes).  Same outputs as resolve for the descriptors it covers; returns
+/// writes) — and, with slots (the offsets of tx[0] / rx[0] in the image),
+/// before the first whose own slot or an RX slot it may pop such a write
+/// touched.  Same outputs as resolve for the descriptors it covers; returns
 /// their number (at least 1 when tx is not empty).
 std::size_t resolve_prefix(const BatchedQueuePairConfig& config, std::size_t mem_size, const Plan& plan,
                            std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
                            std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
                            std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx,
-                           const DmaWriteCheck* wcheck = nullptr);
+                           const DmaWriteCheck* wcheck = nullptr, const RingSlots* slots = nullptr);
 
 /// The device resolve's algorithm (nicgpu_qp_resolve) on the host, for the
 /// tests: ring positions by relaxation — every packet resolved at the
@@ -642,11 +652,26 @@ struct WriteSchedule {
 void schedule_writes(std::span<const SegmentWrite> writes, std::span<const std::int64_t> write_of_rx,
                      WriteSchedule& schedule);
 
+/// Descriptor arrays that live in the memory image itself (DeviceDescriptors
+/// inside it): the image offsets of tx[0] and rx[0], ~0 when an array is not
+/// in the image.  The reference pops each ring slot by a DMA read when it
+/// reaches it (descriptor_ring.cpp:97-106), after the writes of the packets
+/// before; run_batch reproduces that (see DeviceDescriptors).
+struct RingSlots {
+  std::uint64_t tx_at{~0ull};
+  std::uint64_t rx_at{~0ull};
+  [[nodiscard]] bool any() const noexcept { return tx_at != ~0ull || rx_at != ~0ull; }
+};
+
 /// Device work of run_batch: nicgpu_* launches in BatchedQueuePair; tests run
 /// the same driver with a CPU implementation (tests/cpp/cpu_backend.h).
 class Backend {
 public:
   virtual ~Backend() = default;
+  /// The descriptors at image offsets tx_at / rx_at (~0: none) as the image
+  /// holds them now, into tx / rx (run_batch with RingSlots).
+  virtual void descriptors(std::uint64_t tx_at, std::span<TxDescriptor> tx, std::uint64_t rx_at,
+                           std::span<RxDescriptor> rx);
   /// compute_checksum of every piece over the image as it is now; the span
   /// stays valid until the next call.
   virtual std::span<const std::uint16_t> piece_sums(std::span<const Piece> pieces) = 0;
@@ -666,6 +691,8 @@ public:
 /// Host state run_batch reuses across batches.
 struct BatchScratch {
   Plan plan;
+  std::vector<TxDescriptor> ring_tx;  // run_batch with RingSlots: the descriptors as last read
+  std::vector<RxDescriptor> ring_rx;
   std::vector<SegmentWrite> writes, layer;
   std::vector<std::int64_t> write_of_rx;
   std::vector<std::uint32_t> which;
@@ -684,7 +711,8 @@ void build_queue_lists(RxBatchResult& out);
 /// resolve then runs sequentially, on the calling thread).
 void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
                std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out, BatchScratch& scratch,
-               Backend& backend, int disjoint = -1, const DmaWriteCheck* wcheck = nullptr);
+               Backend& backend, int disjoint = -1, const DmaWriteCheck* wcheck = nullptr,
+               const RingSlots* slots = nullptr);
 
 /// host_memory_faults' TX reads: tx with every descriptor whose read
 /// m.translate_const(buffer_address, length) refuses moved out of bounds

@@ -715,6 +715,126 @@ private:
   SimpleHostMemory mem_;
 };
 
+// The reference QueuePair over one batch and the fixture it leaves (shared by
+// the plain, fault and ring cases).  ring_tx_at / ring_rx_at (not ~0): the
+// rings are host-backed at those addresses (DescriptorRing pushes and pops by
+// DMA, descriptor_ring.cpp:48-110) and the saved image holds them as pushed.
+void emit_qp_case(const std::string& name, const std::vector<TxDescriptor>& txs,
+                  const std::vector<RxDescriptor>& rxs, std::vector<std::uint8_t> image, std::size_t mem_size,
+                  std::size_t tx_end, int faults, std::uint64_t ring_tx_at = ~0ull, std::uint64_t ring_rx_at = ~0ull) {
+  const std::size_t ntx = txs.size(), nrx = rxs.size();
+  const bool rings = ring_tx_at != ~0ull;
+  HostMemoryConfig mc{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = faults == faultfx::kIommu};
+  faultfx::Model fm;
+  fm.kind = static_cast<faultfx::Kind>(faults);
+  RecordingMemory mem = faults ? RecordingMemory{mc, fm.translator(), fm.injector()} : RecordingMemory{mc};
+  (void) tx_end;
+  assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(image))).ok());
+  mem.recording = true;
+  *fm.armed = true;
+  DMAEngine dma{mem};
+  QueuePairConfig qc{
+      .queue_id = 5,
+      .tx_ring = {.descriptor_size = sizeof(TxDescriptor), .ring_size = ntx + 1, .base_address = rings ? ring_tx_at : 0,
+                  .queue_id = 5, .host_backed = rings},
+      .rx_ring = {.descriptor_size = sizeof(RxDescriptor), .ring_size = nrx + 1, .base_address = rings ? ring_rx_at : 0,
+                  .queue_id = 5, .host_backed = rings},
+      .tx_completion = {.ring_size = ntx + 1, .queue_id = 5},
+      .rx_completion = {.ring_size = 70 * ntx + 1, .queue_id = 5},
+  };
+  QueuePair qp{qc, dma};
+  for (auto& t : txs) {
+    std::vector<std::byte> b(sizeof(TxDescriptor));
+    std::memcpy(b.data(), &t, sizeof(t));
+    assert(qp.tx_ring().push_descriptor(b).ok());
+  }
+  for (auto& x : rxs) {
+    std::vector<std::byte> b(sizeof(RxDescriptor));
+    std::memcpy(b.data(), &x, sizeof(x));
+    assert(qp.rx_ring().push_descriptor(b).ok());
+  }
+  if (rings) {  // the image the batch starts from holds the pushed rings
+    mem.recording = false;
+    std::vector<std::byte> pushed(mem_size);
+    assert(mem.read(0, pushed).ok());
+    std::memcpy(image.data(), pushed.data(), mem_size);
+    mem.writes.clear();  // (the pushes' DMA writes are not RX deliveries)
+    mem.recording = true;
+  }
+  while (qp.process_once()) {
+  }
+  const std::size_t rx_consumed = nrx - qp.rx_ring().available();
+  std::ostringstream js;
+  js << "{\n \"source\": \"QueuePair::process_once over a batch (src/queue_pair.cpp:67-460)\",\n"
+     << " \"queue_id\": 5, \"max_mtu\": 9000, \"mem_size\": " << mem_size << ", \"ntx\": " << ntx << ", \"nrx\": " << nrx
+     << ", \"rx_consumed\": " << rx_consumed << ",\n \"tx_completions\": [";
+  bool first = true;
+  while (auto c = qp.tx_completion().poll_completion()) { js << (first ? "" : ",") << "\n  " << completion_json(*c); first = false; }
+  js << "],\n \"rx_completions\": [";
+  first = true;
+  std::vector<CompletionEntry> rxc;
+  while (auto c = qp.rx_completion().poll_completion()) {
+    js << (first ? "" : ",") << "\n  " << completion_json(*c);
+    first = false;
+    rxc.push_back(*c);
+  }
+  // RSS of every frame delivered with Success (the reference RssEngine, MS
+  // 40-B key, 128-entry table i % 16, on oracle_extract_tuple AUTO of the
+  // bytes written for it); writes pair with the RX completions that carry one
+  // (Success and ChecksumError: handle_rx_segment writes, then verifies)
+  const std::vector<std::uint8_t>& ms_key = kMsKey;
+  std::vector<std::uint16_t> rss_table(128);
+  for (int i = 0; i < 128; ++i) rss_table[i] = static_cast<std::uint16_t>(i % 16);
+  RssEngine rss_eng{RssConfig{ms_key, rss_table}};
+  std::vector<std::uint32_t> rx_hash(rxc.size(), 0);
+  std::vector<std::uint32_t> rx_queue(rxc.size(), 0xFFFFu);
+  std::size_t wk = 0;
+  for (std::size_t j = 0; j < rxc.size(); ++j) {
+    const auto status = static_cast<CompletionCode>(rxc[j].status);
+    if (status != CompletionCode::Success && status != CompletionCode::ChecksumError) continue;
+    assert(wk < mem.writes.size());
+    const std::vector<std::uint8_t>& bytes = mem.writes[wk++];
+    if (status != CompletionCode::Success) continue;
+    std::uint8_t t[64];
+    const std::size_t tl = oracle_extract_tuple(bytes.data(), bytes.size(), ORACLE_TUPLE_AUTO, 0, 0, t);
+    rx_hash[j] = RssEngine{RssConfig{ms_key, rss_table}}.hash(std::span<const std::uint8_t>(t, tl));
+    rx_queue[j] = *rss_eng.select_queue(std::span<const std::uint8_t>(t, tl));
+  }
+  assert(wk == mem.writes.size());
+  *fm.armed = false;  // read back whole
+  const auto& st = qp.stats();
+  js << "],\n \"stats\": [" << st.tx_packets << "," << st.rx_packets << "," << st.tx_bytes << "," << st.rx_bytes << ","
+     << st.drops_checksum << "," << st.drops_no_rx_desc << "," << st.drops_buffer_small << "," << st.drops_mtu_exceeded
+     << "," << st.drops_invalid_mss << "," << st.drops_too_many_segments << "," << st.tx_tso_segments << ","
+     << st.tx_gso_segments << "," << st.tx_vlan_insertions << "," << st.rx_vlan_strips << "," << st.rx_checksum_verified
+     << "," << st.rx_gro_aggregated << "],\n \"rx_region_fnv\": [";
+  std::vector<std::byte> after(mem_size);
+  assert(mem.read(0, after).ok());
+  for (std::size_t j = 0; j < nrx; ++j) {
+    const std::size_t a = std::min<std::size_t>(rxs[j].buffer_address, mem_size);
+    const std::size_t n = std::min<std::size_t>(rxs[j].buffer_length, mem_size - a);
+    js << (j ? "," : "") << "\"" << std::hex << fnv1a(after.data() + a, n) << std::dec << "\"";
+  }
+  js << "],\n \"mem_fnv\": \"" << std::hex << fnv1a(after.data(), mem_size) << std::dec << "\"";
+  js << ",\n \"faults\": " << faults;
+  if (rings) js << ",\n \"tx_ring_at\": " << ring_tx_at << ", \"rx_ring_at\": " << ring_rx_at;
+  js << ",\n \"rss\": \"RssEngine{MS 40-B key, table i % 16 of 128}::select_queue on oracle_extract_tuple(AUTO) of each Success frame as written\"";
+  js << ",\n \"rx_hash\": [";
+  for (std::size_t j = 0; j < rx_hash.size(); ++j) js << (j ? "," : "") << rx_hash[j];
+  js << "],\n \"rx_queue\": [";
+  for (std::size_t j = 0; j < rx_queue.size(); ++j) js << (j ? "," : "") << rx_queue[j];
+  js << "],\n \"rss_hashes\": " << rss_eng.stats().hashes << ",\n \"rss_queue_hits\": [";
+  for (std::size_t i = 0; i < rss_eng.stats().queue_hits.size(); ++i) js << (i ? "," : "") << rss_eng.stats().queue_hits[i];
+  js << "]\n}\n";
+  std::ofstream(g_out + "/" + name + ".json") << js.str();
+  write_bin(name + ".mem.bin", image);
+  std::vector<std::uint8_t> tb(txs.size() * sizeof(TxDescriptor)), rb(rxs.size() * sizeof(RxDescriptor));
+  std::memcpy(tb.data(), txs.data(), tb.size());
+  std::memcpy(rb.data(), rxs.data(), rb.size());
+  write_bin(name + ".tx.bin", tb);
+  write_bin(name + ".rx.bin", rb);
+}
+
 // flavour 0: mixed sizes; 1: 9000 B TSO/GSO; 2: mixed sizes with overlapping
 // buffers (recycled RX buffers, RX buffers straddling the previous one or
 // lying inside TX buffers), where the reference's in-order writes decide.
@@ -825,106 +945,102 @@ void gen_qp_batch_case(const std::string& name, std::uint64_t seed, std::size_t 
   for (std::size_t j = 0; j < nrx; ++j)
     if (r.below(80) == 0) rxs[j].buffer_address = mem_size + 1 + j;
 
-  HostMemoryConfig mc{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = faults == faultfx::kIommu};
-  faultfx::Model fm;
-  fm.kind = static_cast<faultfx::Kind>(faults);
-  RecordingMemory mem = faults ? RecordingMemory{mc, fm.translator(), fm.injector()} : RecordingMemory{mc};
   std::vector<std::uint8_t> image(mem_size);
   for (std::size_t a = 0; a < tx_end; ++a) image[a] = r.byte();  // RX region starts zeroed
   for (std::size_t i = 0; i < ntx; ++i) std::memcpy(image.data() + tx_addr[i], pkts[i].data(), pkts[i].size());
-  assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(image))).ok());
-  mem.recording = true;
-  *fm.armed = true;
-  DMAEngine dma{mem};
-  QueuePairConfig qc{
-      .queue_id = 5,
-      .tx_ring = {.descriptor_size = sizeof(TxDescriptor), .ring_size = ntx + 1, .base_address = 0, .queue_id = 5, .host_backed = false},
-      .rx_ring = {.descriptor_size = sizeof(RxDescriptor), .ring_size = nrx + 1, .base_address = 0, .queue_id = 5, .host_backed = false},
-      .tx_completion = {.ring_size = ntx + 1, .queue_id = 5},
-      .rx_completion = {.ring_size = 70 * ntx + 1, .queue_id = 5},
+  emit_qp_case(name, txs, rxs, std::move(image), mem_size, tx_end, faults);
+}
+
+
+// Host-backed rings that the batch's own DMA writes land on: some RX buffers
+// are exactly a later TX or RX ring slot (buffer_length 32 / 24), so a frame
+// of at most that size delivered there becomes the descriptor the reference
+// pops from that slot later (descriptor_ring.cpp:97-106).  Every frame starts
+// with a 32-byte head that reads as a sane TxDescriptor and RxDescriptor
+// (bools 0/1, no checksum, no TSO, no VLAN, lengths <= 1600, buffers below the
+// rings), a third of the frames are that head alone (24..32 B), and no
+// original descriptor inserts or strips a VLAN tag (a shifted head would not
+// read as one).
+void gen_qp_ring_case(const std::string& name, std::uint64_t seed, std::size_t ntx, std::size_t nrx) {
+  Rng r{seed};
+  const std::size_t rx_len = 2048;
+  // layout: TX frames | RX buffers | TX ring | RX ring | guard
+  std::vector<std::size_t> lens(ntx);
+  std::size_t tx_end = 0;
+  std::vector<std::uint64_t> tx_addr(ntx);
+  for (std::size_t i = 0; i < ntx; ++i) {
+    const std::uint32_t pick = r.below(3);
+    lens[i] = pick == 0 ? 16 + r.below(17) : (pick == 1 ? 64 + r.below(500) : 600 + r.below(1000));
+    tx_addr[i] = tx_end;
+    tx_end += lens[i] + r.below(8);
+  }
+  tx_end = (tx_end + 63) & ~std::size_t{63};
+  const std::size_t rx_base = tx_end;
+  const std::size_t ring_tx_at = rx_base + nrx * rx_len;
+  const std::size_t ring_rx_at = ring_tx_at + ntx * sizeof(TxDescriptor);
+  const std::size_t rings_start = ring_tx_at;
+  const std::size_t mem_size = ring_rx_at + nrx * sizeof(RxDescriptor) + 256;
+  auto head = [&](std::uint8_t* h) {  // 32 bytes, a sane TxDescriptor and RxDescriptor
+    std::memset(h, 0, 32);
+    const std::uint64_t a = r.below(static_cast<std::uint32_t>(rings_start - 2048));
+    std::memcpy(h, &a, 8);                                       // buffer_address
+    const std::uint32_t len = r.below(1601);
+    std::memcpy(h + 8, &len, 4);                                 // length / buffer_length
+    h[14] = r.byte();                                            // descriptor_index
+    h[15] = r.byte();
+    h[16] = static_cast<std::uint8_t>(r.below(2));               // TX checksum_value lo | RX checksum_offload
+    h[18] = static_cast<std::uint8_t>(r.below(2));               // TX checksum_offload | RX vlan_present
+    h[22] = static_cast<std::uint8_t>(r.below(2));               // TX mss lo | RX gro_enabled
+    h[23] = r.byte();                                            // TX mss hi
+    h[24] = r.byte();                                            // TX header_length
+    h[25] = r.byte();
+    h[28] = r.byte();                                            // TX vlan_tag | (past the RX descriptor)
+    h[29] = r.byte();
   };
-  QueuePair qp{qc, dma};
-  for (auto& t : txs) {
-    std::vector<std::byte> b(sizeof(TxDescriptor));
-    std::memcpy(b.data(), &t, sizeof(t));
-    assert(qp.tx_ring().push_descriptor(b).ok());
+  std::vector<std::uint8_t> image(mem_size, 0);
+  for (std::size_t a = 0; a < tx_end; ++a) image[a] = r.byte();
+  std::vector<TxDescriptor> txs(ntx);
+  for (std::size_t i = 0; i < ntx; ++i) {
+    std::uint8_t* f = image.data() + tx_addr[i];
+    std::uint8_t h[32];
+    head(h);
+    std::memcpy(f, h, std::min<std::size_t>(32, lens[i]));
+    TxDescriptor& t = txs[i];
+    t.buffer_address = tx_addr[i];
+    t.length = static_cast<std::uint32_t>(lens[i]);
+    t.descriptor_index = static_cast<std::uint16_t>(i);
+    const std::uint32_t cm = r.below(6);
+    t.checksum = cm < 4 ? ChecksumMode::None : ChecksumMode::Layer4;
+    t.checksum_offload = r.below(3) != 0;
+    const std::uint16_t good = ref_csum(f, lens[i]);
+    t.checksum_value = r.below(5) == 0 ? static_cast<std::uint16_t>(good ^ 1u) : good;
+    if (lens[i] > 400 && r.below(4) == 0) {  // segmentation, headers of at least 32 bytes
+      (r.below(2) ? t.tso_enabled : t.gso_enabled) = true;
+      t.mss = static_cast<std::uint16_t>(100 + r.below(400));
+      t.header_length = static_cast<std::uint16_t>(32 + r.below(40));
+    }
   }
-  for (auto& x : rxs) {
-    std::vector<std::byte> b(sizeof(RxDescriptor));
-    std::memcpy(b.data(), &x, sizeof(x));
-    assert(qp.rx_ring().push_descriptor(b).ok());
-  }
-  while (qp.process_once()) {
-  }
-  const std::size_t rx_consumed = nrx - qp.rx_ring().available();
-  std::ostringstream js;
-  js << "{\n \"source\": \"QueuePair::process_once over a batch (src/queue_pair.cpp:67-460)\",\n"
-     << " \"queue_id\": 5, \"max_mtu\": 9000, \"mem_size\": " << mem_size << ", \"ntx\": " << ntx << ", \"nrx\": " << nrx
-     << ", \"rx_consumed\": " << rx_consumed << ",\n \"tx_completions\": [";
-  bool first = true;
-  while (auto c = qp.tx_completion().poll_completion()) { js << (first ? "" : ",") << "\n  " << completion_json(*c); first = false; }
-  js << "],\n \"rx_completions\": [";
-  first = true;
-  std::vector<CompletionEntry> rxc;
-  while (auto c = qp.rx_completion().poll_completion()) {
-    js << (first ? "" : ",") << "\n  " << completion_json(*c);
-    first = false;
-    rxc.push_back(*c);
-  }
-  // RSS of every frame delivered with Success (the reference RssEngine, MS
-  // 40-B key, 128-entry table i % 16, on oracle_extract_tuple AUTO of the
-  // bytes written for it); writes pair with the RX completions that carry one
-  // (Success and ChecksumError: handle_rx_segment writes, then verifies)
-  const std::vector<std::uint8_t>& ms_key = kMsKey;
-  std::vector<std::uint16_t> rss_table(128);
-  for (int i = 0; i < 128; ++i) rss_table[i] = static_cast<std::uint16_t>(i % 16);
-  RssEngine rss_eng{RssConfig{ms_key, rss_table}};
-  std::vector<std::uint32_t> rx_hash(rxc.size(), 0);
-  std::vector<std::uint32_t> rx_queue(rxc.size(), 0xFFFFu);
-  std::size_t wk = 0;
-  for (std::size_t j = 0; j < rxc.size(); ++j) {
-    const auto status = static_cast<CompletionCode>(rxc[j].status);
-    if (status != CompletionCode::Success && status != CompletionCode::ChecksumError) continue;
-    assert(wk < mem.writes.size());
-    const std::vector<std::uint8_t>& bytes = mem.writes[wk++];
-    if (status != CompletionCode::Success) continue;
-    std::uint8_t t[64];
-    const std::size_t tl = oracle_extract_tuple(bytes.data(), bytes.size(), ORACLE_TUPLE_AUTO, 0, 0, t);
-    rx_hash[j] = RssEngine{RssConfig{ms_key, rss_table}}.hash(std::span<const std::uint8_t>(t, tl));
-    rx_queue[j] = *rss_eng.select_queue(std::span<const std::uint8_t>(t, tl));
-  }
-  assert(wk == mem.writes.size());
-  *fm.armed = false;  // read back whole
-  const auto& st = qp.stats();
-  js << "],\n \"stats\": [" << st.tx_packets << "," << st.rx_packets << "," << st.tx_bytes << "," << st.rx_bytes << ","
-     << st.drops_checksum << "," << st.drops_no_rx_desc << "," << st.drops_buffer_small << "," << st.drops_mtu_exceeded
-     << "," << st.drops_invalid_mss << "," << st.drops_too_many_segments << "," << st.tx_tso_segments << ","
-     << st.tx_gso_segments << "," << st.tx_vlan_insertions << "," << st.rx_vlan_strips << "," << st.rx_checksum_verified
-     << "," << st.rx_gro_aggregated << "],\n \"rx_region_fnv\": [";
-  std::vector<std::byte> after(mem_size);
-  assert(mem.read(0, after).ok());
+  std::vector<RxDescriptor> rxs(nrx);
   for (std::size_t j = 0; j < nrx; ++j) {
-    const std::size_t a = std::min<std::size_t>(rxs[j].buffer_address, mem_size);
-    const std::size_t n = std::min<std::size_t>(rxs[j].buffer_length, mem_size - a);
-    js << (j ? "," : "") << "\"" << std::hex << fnv1a(after.data() + a, n) << std::dec << "\"";
+    RxDescriptor& x = rxs[j];
+    x.buffer_address = rx_base + j * rx_len;
+    x.buffer_length = static_cast<std::uint32_t>(rx_len);
+    x.descriptor_index = static_cast<std::uint16_t>(1000 + j);
+    x.checksum_offload = r.below(2) != 0;
+    x.checksum = r.below(3) == 0 ? ChecksumMode::None : ChecksumMode::Layer4;
+    x.vlan_present = r.below(4) == 0;
+    x.gro_enabled = r.below(4) == 0;
+    const std::uint32_t k = r.below(8);
+    if (k == 0 && j + 100 < nrx) {  // a later RX ring slot (beyond the pops of any one packet)
+      x.buffer_address = ring_rx_at + (j + 80 + r.below(static_cast<std::uint32_t>(std::min<std::size_t>(60, nrx - j - 80)))) *
+                                          sizeof(RxDescriptor);
+      x.buffer_length = sizeof(RxDescriptor);
+    } else if (k == 1 && j + 40 < ntx) {  // a later TX ring slot
+      x.buffer_address = ring_tx_at + (j + 10 + r.below(30)) * sizeof(TxDescriptor);
+      x.buffer_length = sizeof(TxDescriptor);
+    }
   }
-  js << "],\n \"mem_fnv\": \"" << std::hex << fnv1a(after.data(), mem_size) << std::dec << "\"";
-  js << ",\n \"faults\": " << faults;
-  js << ",\n \"rss\": \"RssEngine{MS 40-B key, table i % 16 of 128}::select_queue on oracle_extract_tuple(AUTO) of each Success frame as written\"";
-  js << ",\n \"rx_hash\": [";
-  for (std::size_t j = 0; j < rx_hash.size(); ++j) js << (j ? "," : "") << rx_hash[j];
-  js << "],\n \"rx_queue\": [";
-  for (std::size_t j = 0; j < rx_queue.size(); ++j) js << (j ? "," : "") << rx_queue[j];
-  js << "],\n \"rss_hashes\": " << rss_eng.stats().hashes << ",\n \"rss_queue_hits\": [";
-  for (std::size_t i = 0; i < rss_eng.stats().queue_hits.size(); ++i) js << (i ? "," : "") << rss_eng.stats().queue_hits[i];
-  js << "]\n}\n";
-  std::ofstream(g_out + "/" + name + ".json") << js.str();
-  write_bin(name + ".mem.bin", image);
-  std::vector<std::uint8_t> tb(txs.size() * sizeof(TxDescriptor)), rb(rxs.size() * sizeof(RxDescriptor));
-  std::memcpy(tb.data(), txs.data(), tb.size());
-  std::memcpy(rb.data(), rxs.data(), rb.size());
-  write_bin(name + ".tx.bin", tb);
-  write_bin(name + ".rx.bin", rb);
+  emit_qp_case(name, txs, rxs, std::move(image), mem_size, tx_end, faultfx::kNone, ring_tx_at, ring_rx_at);
 }
 
 void gen_qp_batch() {
@@ -936,6 +1052,8 @@ void gen_qp_batch() {
   gen_qp_batch_case("qp_fault_inj", 505, 400, 700, 0, faultfx::kInjector);
   gen_qp_batch_case("qp_fault_iommu", 606, 400, 700, 0, faultfx::kIommu);
   gen_qp_batch_case("qp_fault_tso", 707, 40, 300, 1, faultfx::kInjector);
+  // host-backed rings written over by the batch's own DMA writes
+  gen_qp_ring_case("qp_ring", 808, 400, 600);
 }
 
 // ------------------------------------------------------------ QueueManager --

@@ -648,8 +648,10 @@ std::size_t resolve_prefix(const BatchedQueuePairConfig& config, std::size_t mem
                            std::span<const std::uint16_t> piece_csum, std::span<const TxDescriptor> tx,
                            std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out,
                            std::vector<SegmentWrite>& writes, std::vector<std::int64_t>& write_of_rx,
-                           const DmaWriteCheck* wcheck) {
+                           const DmaWriteCheck* wcheck, const RingSlots* slots) {
   const Ctx C = make_ctx(config, mem_size, plan, piece_csum, tx, rx, wcheck);
+  constexpr std::uint64_t kTxSlot = sizeof(TxDescriptor), kRxSlot = sizeof(RxDescriptor), kNone = ~0ull;
+  const bool tx_ring = slots && slots->tx_at != kNone, rx_ring = slots && slots->rx_at != kNone;
   out.tx_completions.clear();
   out.rx_completions.clear();
   writes.clear();
@@ -665,8 +667,28 @@ std::size_t resolve_prefix(const BatchedQueuePairConfig& config, std::size_t mem
       reads_written = written.overlaps(q.addr, q.addr + q.len);
     }
     if (reads_written) break;
+    // ring slots in the image: the reference pops TX slot i, and the RX slots
+    // from rc on, by DMA reads after the writes before (descriptor_ring.cpp:
+    // 97-106) — a slot an earlier write touched is read again after it
+    if (tx_ring && written.overlaps(slots->tx_at + kTxSlot * i, slots->tx_at + kTxSlot * (i + 1))) break;
+    if (rx_ring && rc < rx.size()) {
+      const std::uint64_t pops = std::min<std::uint64_t>(nicqp::decide_segments(tx[i]).nseg, rx.size() - rc);
+      if (pops && written.overlaps(slots->rx_at + kRxSlot * rc, slots->rx_at + kRxSlot * (rc + pops))) break;
+    }
     const std::size_t w0 = writes.size();
+    const std::size_t rc0 = rc;
     rc += resolve_packet(C, i, rc, stats, sink);
+    if (rx_ring)  // a segment's write over an RX slot a later segment of the same packet pops
+      for (std::size_t k = 1; k < rc - rc0; ++k) {
+        const std::uint64_t a = slots->rx_at + kRxSlot * (rc0 + k);
+        for (std::size_t j = w0; j < w0 + k; ++j) {
+          const std::uint64_t d = writes[j].dst, n = write_len(writes[j]);
+          if (write_of_rx[j] >= 0 && n && d < a + kRxSlot && a < d + n)
+            throw GpuError("process_batch: a segment's DMA write lands on an RX descriptor slot a later segment of the same "
+                           "TX descriptor pops (not modelled)",
+                           NICGPU_ERR_INVALID);
+        }
+      }
     for (std::size_t j = w0; j < writes.size(); ++j)
       if (write_of_rx[j] >= 0) written.add(writes[j].dst, writes[j].dst + write_len(writes[j]));
   }
@@ -757,7 +779,7 @@ void schedule_writes(std::span<const SegmentWrite> writes, std::span<const std::
 
 void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::span<const TxDescriptor> tx,
                std::span<const RxDescriptor> rx, QueuePairStats& stats, RxBatchResult& out, BatchScratch& S,
-               Backend& dev, int disjoint_hint, const DmaWriteCheck* wcheck) {
+               Backend& dev, int disjoint_hint, const DmaWriteCheck* wcheck, const RingSlots* slots) {
   using clock = std::chrono::steady_clock;
   auto us_since = [](clock::time_point t) { return std::chrono::duration<double, std::micro>(clock::now() - t).count(); };
   constexpr auto kSuccess = static_cast<std::uint32_t>(CompletionCode::Success);
@@ -772,7 +794,16 @@ void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
   out.timings = RxBatchResult::Timings{};
 
   auto t0 = clock::now();
-  const bool disjoint = disjoint_hint >= 0 ? disjoint_hint != 0 : buffers_disjoint(mem_size, tx, rx);
+  // descriptor arrays in the image that a write may land on: the sub-batch
+  // path, over copies of the descriptors read again between sub-batches
+  const bool rings = slots != nullptr && slots->any();
+  if (rings) {
+    S.ring_tx.assign(tx.begin(), tx.end());
+    S.ring_rx.assign(rx.begin(), rx.end());
+    tx = S.ring_tx;
+    rx = S.ring_rx;
+  }
+  const bool disjoint = !rings && (disjoint_hint >= 0 ? disjoint_hint != 0 : buffers_disjoint(mem_size, tx, rx));
   out.timings.check_us = us_since(t0);
   // RSS of the frames part.rx_completions[which[..]] delivered with Success,
   // from the image as it is now.  The tuple lies in the first 82 bytes, so a
@@ -812,7 +843,13 @@ void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
       resolve(config, mem_size, S.plan, cs, txs, rxs, stats, part, S.writes, S.write_of_rx, 0, wcheck);
       k = txs.size();
     } else {
-      k = resolve_prefix(config, mem_size, S.plan, cs, txs, rxs, stats, part, S.writes, S.write_of_rx, wcheck);
+      RingSlots sub;  // the offsets of txs[0] / rxs[0]
+      if (rings) {
+        sub.tx_at = slots->tx_at == ~0ull ? ~0ull : slots->tx_at + sizeof(TxDescriptor) * s;
+        sub.rx_at = slots->rx_at == ~0ull ? ~0ull : slots->rx_at + sizeof(RxDescriptor) * r;
+      }
+      k = resolve_prefix(config, mem_size, S.plan, cs, txs, rxs, stats, part, S.writes, S.write_of_rx, wcheck,
+                         rings ? &sub : nullptr);
     }
     out.timings.resolve_us += us_since(t);
     const std::size_t nrx = part.rx_completions.size();
@@ -867,6 +904,14 @@ void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
     }
     s += k;
     r += part.rx_consumed;
+    if (rings && s < tx.size()) {  // the descriptors not yet popped, as the writes left them
+      auto t = clock::now();
+      dev.descriptors(slots->tx_at == ~0ull ? ~0ull : slots->tx_at + sizeof(TxDescriptor) * s,
+                      std::span<TxDescriptor>(S.ring_tx).subspan(s),
+                      slots->rx_at == ~0ull ? ~0ull : slots->rx_at + sizeof(RxDescriptor) * r,
+                      std::span<RxDescriptor>(S.ring_rx).subspan(r));
+      out.timings.copy_us += us_since(t);
+    }
   } while (s < tx.size());
   out.tx_processed = tx.size();
   out.rx_consumed = r;
@@ -876,6 +921,10 @@ void run_batch(const BatchedQueuePairConfig& config, std::size_t mem_size, std::
     build_queue_lists(out);
     out.timings.rss_us += us_since(t);
   }
+}
+
+void Backend::descriptors(std::uint64_t, std::span<TxDescriptor>, std::uint64_t, std::span<RxDescriptor>) {
+  throw std::logic_error("run_batch: this backend cannot read descriptors from the image (RingSlots)");
 }
 
 void build_queue_lists(RxBatchResult& out) {
@@ -1444,6 +1493,15 @@ public:
 
   std::uint64_t* frame_desc(std::size_t n) override { return S.h_rss_desc.get<std::uint64_t>(std::max<std::size_t>(n, 1)); }
 
+  void descriptors(std::uint64_t tx_at, std::span<TxDescriptor> tx, std::uint64_t rx_at,
+                   std::span<RxDescriptor> rx) override {
+    if (tx_at != ~0ull && !tx.empty())
+      check(nicgpu_memcpy_async(tx.data(), image() + tx_at, tx.size_bytes(), stream_), "nicgpu_memcpy_async");
+    if (rx_at != ~0ull && !rx.empty())
+      check(nicgpu_memcpy_async(rx.data(), image() + rx_at, rx.size_bytes(), stream_), "nicgpu_memcpy_async");
+    check(nicgpu_stream_synchronize(stream_), "nicgpu_stream_synchronize");
+  }
+
   void rss(std::size_t m, const std::uint32_t*& hash, const std::uint16_t*& queue) override {
     void* d_desc = S.rss_desc.get(m * 8);
     void* d_h = S.rss_hash.get(m * 4);
@@ -1552,7 +1610,7 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, std::span<cons
 void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDescriptor> tx,
                                std::span<const RxDescriptor> rx, QueuePairStats& st, RxBatchResult& out, void* stream,
                                int disjoint, double& check_us, std::vector<rx_stage_detail::SegmentWrite>* applied,
-                               const rx_stage_detail::DmaWriteCheck* wcheck) {
+                               const rx_stage_detail::DmaWriteCheck* wcheck, const rx_stage_detail::RingSlots* slots) {
   using clock = std::chrono::steady_clock;
   out.dev = RxBatchResult::DeviceResults{};
   if (disjoint < 0) {
@@ -1561,7 +1619,7 @@ void BatchedQueuePair::on_host(const DeviceHostMemory& mem, std::span<const TxDe
     check_us += std::chrono::duration<double, std::micro>(clock::now() - t0).count();
   }
   GpuBackend dev{*scratch_, mem, config_, stream, applied};
-  rx_stage_detail::run_batch(quiet_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint, wcheck);
+  rx_stage_detail::run_batch(quiet_, mem.size, tx, rx, st, out, scratch_->host, dev, disjoint, wcheck, slots);
 }
 
 void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDescriptors& d, RxBatchResult& out,
@@ -1597,43 +1655,68 @@ void BatchedQueuePair::process_batch(const DeviceHostMemory& mem, const DeviceDe
     }
   }
   if (!on_device) {
-    check_rings_unwritten(sl, mem, stream);
+    rx_stage_detail::RingSlots rs;
+    const bool rw = rings_written(sl, mem, stream, &rs);
     const auto [htx, hrx] = host_spans(sl, {}, {}, stream);
-    on_host(mem, htx, hrx, st, out, stream, disjoint, check_us);
+    on_host(mem, htx, hrx, st, out, stream, disjoint, check_us, nullptr, nullptr, rw ? &rs : nullptr);
   }
   out.timings.check_us = check_us;
   stats_ = st;
   if (config_.on_interrupt) fire_interrupts(out, &sl);
 }
 
-// Device descriptor arrays inside the image: no RX buffer of the batch may
-// overlap them (an RX write there would change a descriptor the reference pops
-// later, descriptor_ring.cpp:97-106; the stage reads them once).  Throws
-// before anything is written.
-void BatchedQueuePair::check_rings_unwritten(Slot& sl, const DeviceHostMemory& mem, void* stream) {
-  if (!sl.tx_dev && !sl.rx_dev) return;
+// Device descriptor arrays inside the image that an RX buffer of the batch
+// overlaps: a DMA write there changes descriptors the reference pops later
+// (descriptor_ring.cpp:97-106), so the batch goes to the host path with the
+// arrays' image offsets in *slots, which re-reads them between sub-batches.
+// An array that only partly lies in the image is refused (GpuError, before
+// anything is written) when a buffer overlaps it.
+bool BatchedQueuePair::rings_written(Slot& sl, const DeviceHostMemory& mem, void* stream,
+                                     rx_stage_detail::RingSlots* slots) {
+  if (!sl.tx_dev && !sl.rx_dev) return false;
   const auto b = reinterpret_cast<std::uintptr_t>(mem.base);
-  struct Span { std::uint64_t lo, hi; };
+  struct Span {
+    std::uint64_t lo, hi;
+    bool whole;
+  };
   Span rings[2];
+  std::uint64_t* at[2] = {nullptr, nullptr};
   int nr = 0;
-  auto add = [&](const void* p, std::size_t bytes) {
+  rx_stage_detail::RingSlots rs;
+  auto add = [&](const void* p, std::size_t bytes, std::uint64_t* where) {
     const auto a = reinterpret_cast<std::uintptr_t>(p);
     if (!bytes || a >= b + mem.size || a + bytes <= b) return;
     const std::uint64_t lo = a > b ? a - b : 0, hi = std::min<std::uint64_t>(a + bytes - b, mem.size);
-    rings[nr++] = Span{lo, hi};
+    const bool whole = a >= b && a + bytes <= b + mem.size;
+    at[nr] = where;
+    rings[nr++] = Span{lo, hi, whole};
   };
-  add(sl.tx_dev, sl.ntx_dev * sizeof(TxDescriptor));
-  add(sl.rx_dev, sl.nrx_dev * sizeof(RxDescriptor));
-  if (nr == 0) return;
+  add(sl.tx_dev, sl.ntx_dev * sizeof(TxDescriptor), &rs.tx_at);
+  add(sl.rx_dev, sl.nrx_dev * sizeof(RxDescriptor), &rs.rx_at);
+  if (nr == 0) return false;
   const auto hrx = host_spans(sl, {}, {}, stream).second;
+  bool hit[2] = {false, false};
   for (const RxDescriptor& d : hrx) {
     if (d.buffer_length == 0 || d.buffer_address >= mem.size) continue;
     const std::uint64_t lo = d.buffer_address, hi = std::min<std::uint64_t>(lo + d.buffer_length, mem.size);
-    for (int k = 0; k < nr; ++k)
-      if (lo < rings[k].hi && rings[k].lo < hi)
-        throw GpuError("process_batch: an RX buffer overlaps the descriptor arrays inside the image (not modelled)",
-                       NICGPU_ERR_INVALID);
+    for (int k = 0; k < nr; ++k) hit[k] = hit[k] || (lo < rings[k].hi && rings[k].lo < hi);
   }
+  bool any = false;
+  for (int k = 0; k < nr; ++k) {
+    if (!hit[k]) continue;
+    if (!rings[k].whole)
+      throw GpuError("process_batch: an RX buffer overlaps a descriptor array that lies only partly in the image",
+                     NICGPU_ERR_INVALID);
+    *at[k] = rings[k].lo;
+    any = true;
+  }
+  if (any && slots) {
+    // (both arrays' offsets when both lie in the image: a write may land on either)
+    for (int k = 0; k < nr; ++k)
+      if (rings[k].whole) *at[k] = rings[k].lo;
+    *slots = rs;
+  }
+  return any;
 }
 
 // The batch's descriptors on the host: the caller's spans, or (device
@@ -1739,9 +1822,10 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
       if (!sl.on_device && sl.image) {
         image_host_path(sl, sl.tx, sl.rx, sl.stats, sl.result, sl.stream, disjoint, check_us);
       } else if (!sl.on_device) {
-        check_rings_unwritten(sl, sl.mem, sl.stream);
+        rx_stage_detail::RingSlots rs;
+        const bool rw = rings_written(sl, sl.mem, sl.stream, &rs);
         const auto [htx, hrx] = host_spans(sl, sl.tx, sl.rx, sl.stream);
-        on_host(sl.mem, htx, hrx, sl.stats, sl.result, sl.stream, disjoint, check_us);
+        on_host(sl.mem, htx, hrx, sl.stats, sl.result, sl.stream, disjoint, check_us, nullptr, nullptr, rw ? &rs : nullptr);
       }
       sl.result.timings.check_us = check_us;
       // this batch's writes, for the overlapped resolves of the next two
@@ -1966,7 +2050,9 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
   };
   const bool side = !dev_desc || (!inside(sl.tx_dev, ntx * sizeof(TxDescriptor)) &&
                                   !inside(sl.rx_dev, nrx * sizeof(RxDescriptor)));
-  if (!side) check_rings_unwritten(sl, mem, stream);
+  // descriptor arrays in the image that a write of the batch lands on: the
+  // host path, which pops them as the reference does (nothing written yet)
+  if (!side && rings_written(sl, mem, stream, nullptr)) return false;
   void* ps = side ? S.side_plan : stream;
   if (dev_desc) {
     check(nicgpu_qp_reserve(sl.qp, ntx, nrx, &v), "nicgpu_qp_reserve");

@@ -72,6 +72,13 @@ public:
     ++gathers;
   }
 
+  void descriptors(std::uint64_t tx_at, std::span<TxDescriptor> tx, std::uint64_t rx_at,
+                   std::span<RxDescriptor> rx) override {
+    if (tx_at != ~0ull && !tx.empty()) std::memcpy(static_cast<void*>(tx.data()), image_.data() + tx_at, tx.size_bytes());
+    if (rx_at != ~0ull && !rx.empty()) std::memcpy(static_cast<void*>(rx.data()), image_.data() + rx_at, rx.size_bytes());
+    ++refetches;
+  }
+
   std::uint64_t* frame_desc(std::size_t n) override {
     desc_.resize(n);
     return desc_.data();
@@ -96,7 +103,7 @@ public:
     ++rss_calls;
   }
 
-  std::size_t sum_calls = 0, snapshots = 0, gathers = 0, rss_calls = 0;
+  std::size_t sum_calls = 0, snapshots = 0, gathers = 0, rss_calls = 0, refetches = 0;
 
 private:
   std::vector<std::uint8_t>& image_;

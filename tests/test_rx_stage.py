@@ -50,9 +50,12 @@ def _flatten(name, out_dir):
 def _run(exe, mode, name, tmp_path):
     exp = _flatten(name, str(tmp_path))
     args = [exe, mode, exp] + [os.path.join(GOLDEN, f"{name}.{k}.bin") for k in ("mem", "tx", "rx")]
-    faults = json.load(open(os.path.join(GOLDEN, name + ".json"))).get("faults", 0)
-    if faults:
+    fx = json.load(open(os.path.join(GOLDEN, name + ".json")))
+    faults = fx.get("faults", 0)
+    if faults or "tx_ring_at" in fx:
         args.append(str(faults))
+    if "tx_ring_at" in fx:
+        args.append(f'{fx["tx_ring_at"]}:{fx["rx_ring_at"]}')
     r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert f"rx_stage_test {mode}: ok" in r.stdout
@@ -94,6 +97,31 @@ def test_rx_stage_fault_host_logic(tmp_path):
     exe = _build(tmp_path, "rx_stage_test")
     for n in FAULT_CASES:
         _run(exe, "cpu", n, tmp_path)
+
+
+def test_ring_fixture_rereads_slots():
+    """qp_ring (oracle/gen_golden.cpp gen_qp_ring_case): the reference popped
+    descriptors that the batch's own writes had put into later ring slots."""
+    d = json.load(open(os.path.join(GOLDEN, "qp_ring.json")))
+    assert sum(c[1] >= d["ntx"] for c in d["tx_completions"]) >= 5  # TX slots rewritten before their pop
+    assert sum(not (1000 <= c[1] < 1000 + d["nrx"]) for c in d["rx_completions"]) >= 3  # RX slots likewise
+
+
+def test_rx_stage_ring_rereads_host_logic(tmp_path):
+    """The driver with RingSlots over the CPU backend: sub-batches end before
+    a descriptor whose slot was written, the rest is read again from the image;
+    completions, stats, bytes and RSS equal the reference's."""
+    exe = _build(tmp_path, "rx_stage_test")
+    _run(exe, "cpu", "qp_ring", tmp_path)
+
+
+@pytest.mark.gpu
+def test_rx_stage_ring_rereads_gpu(tmp_path):
+    """The same through the product path: DeviceDescriptors inside the device
+    image whose slots the batch's writes land on go to the host path and pop
+    each slot as the reference does (process_batch and submit/collect)."""
+    exe = _build(tmp_path, "rx_stage_test")
+    _run(exe, "gpu", "qp_ring", tmp_path)
 
 
 @pytest.mark.gpu
