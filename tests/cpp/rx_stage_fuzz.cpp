@@ -528,6 +528,142 @@ int run_case(std::uint64_t seed) {
   return 0;
 }
 
+
+// Host-backed rings that the batch's own DMA writes land on (the reference
+// pops each slot by a DMA read, descriptor_ring.cpp:97-106): RX buffers that
+// are exactly a later TX or RX ring slot, frames whose first 32 bytes read as
+// sane descriptors (bools 0/1, no checksum, no TSO, no VLAN, small lengths,
+// buffers below the rings).  The reference QueuePair with host-backed rings
+// against run_batch with RingSlots.
+std::size_t g_ring_rereads = 0, g_ring_batches = 0;
+
+int run_ring_case(std::uint64_t seed) {
+  Rng r{seed * 104729 + 7};
+  const std::size_t ntx = 1 + r.below(90), nrx = 1 + r.below(160);
+  const std::size_t rx_len = 1600;
+  std::vector<std::size_t> lens(ntx);
+  std::vector<std::uint64_t> addr(ntx);
+  std::size_t at = 0;
+  for (std::size_t i = 0; i < ntx; ++i) {
+    const std::uint32_t pick = r.below(3);
+    lens[i] = pick == 0 ? 8 + r.below(25) : (pick == 1 ? 33 + r.below(300) : 400 + r.below(1100));
+    addr[i] = at;
+    at += lens[i] + r.below(4);
+  }
+  at = (at + 15) & ~std::size_t{15};
+  const std::size_t rx_base = at;
+  const std::size_t tx_at = rx_base + nrx * rx_len, rx_at = tx_at + ntx * sizeof(TxDescriptor);
+  const std::size_t mem_size = rx_at + nrx * sizeof(RxDescriptor) + 64;
+  std::vector<std::uint8_t> image(mem_size, 0);
+  for (std::size_t a = 0; a < rx_base; ++a) image[a] = r.byte();
+  std::vector<TxDescriptor> tx(ntx);
+  for (std::size_t i = 0; i < ntx; ++i) {
+    std::uint8_t* f = image.data() + addr[i];
+    std::uint8_t h[32] = {};
+    const std::uint64_t ba = r.below(static_cast<std::uint32_t>(std::max<std::size_t>(tx_at, 2048) - 1600));
+    std::memcpy(h, &ba, 8);
+    const std::uint32_t bl = r.below(1601);
+    std::memcpy(h + 8, &bl, 4);
+    h[14] = r.byte();
+    h[15] = r.byte();
+    h[16] = static_cast<std::uint8_t>(r.below(2));
+    h[18] = static_cast<std::uint8_t>(r.below(2));
+    h[22] = static_cast<std::uint8_t>(r.below(2));
+    h[23] = r.byte();
+    h[24] = r.byte();
+    h[28] = r.byte();
+    std::memcpy(f, h, std::min<std::size_t>(32, lens[i]));
+    TxDescriptor& t = tx[i];
+    t.buffer_address = addr[i];
+    t.length = static_cast<std::uint32_t>(lens[i]);
+    t.descriptor_index = static_cast<std::uint16_t>(i);
+    t.checksum = r.below(4) == 0 ? ChecksumMode::Layer4 : ChecksumMode::None;
+    t.checksum_offload = r.below(2);
+    const std::uint16_t good = oracle_compute_checksum(f, lens[i]);
+    t.checksum_value = r.below(4) == 0 ? static_cast<std::uint16_t>(good ^ 1u) : good;
+    if (lens[i] > 300 && r.below(3) == 0) {
+      (r.below(2) ? t.tso_enabled : t.gso_enabled) = true;
+      t.mss = static_cast<std::uint16_t>(60 + r.below(300));
+      t.header_length = static_cast<std::uint16_t>(32 + r.below(30));
+    }
+  }
+  std::vector<RxDescriptor> rx(nrx);
+  for (std::size_t j = 0; j < nrx; ++j) {
+    RxDescriptor& x = rx[j];
+    x.buffer_address = rx_base + j * rx_len;
+    x.buffer_length = static_cast<std::uint32_t>(rx_len);
+    x.descriptor_index = static_cast<std::uint16_t>(1000 + j);
+    x.checksum_offload = r.below(2);
+    x.checksum = r.below(3) == 0 ? ChecksumMode::None : ChecksumMode::Layer4;
+    x.vlan_present = r.below(4) == 0;
+    x.gro_enabled = r.below(4) == 0;
+    const std::uint32_t k = r.below(5);
+    if (k == 0 && j + 66 < nrx) {  // a later RX slot, past any one packet's pops
+      x.buffer_address = rx_at + (j + 65 + r.below(static_cast<std::uint32_t>(nrx - j - 65))) * sizeof(RxDescriptor);
+      x.buffer_length = sizeof(RxDescriptor);
+    } else if (k == 1 && j + 2 < ntx) {  // a later TX slot
+      x.buffer_address = tx_at + (j + 1 + r.below(static_cast<std::uint32_t>(ntx - j - 1))) * sizeof(TxDescriptor);
+      x.buffer_length = sizeof(TxDescriptor);
+    }
+  }
+  const std::uint16_t qid = static_cast<std::uint16_t>(r.below(8));
+  // ---- reference, host-backed rings
+  RecordingMemory mem{HostMemoryConfig{.size_bytes = mem_size, .page_size = 4096, .iommu_enabled = false}};
+  assert(mem.write(0, std::as_bytes(std::span<const std::uint8_t>(image))).ok());
+  DMAEngine dma{mem};
+  QueuePairConfig qc{
+      .queue_id = qid,
+      .tx_ring = {.descriptor_size = sizeof(TxDescriptor), .ring_size = ntx + 1, .base_address = tx_at, .queue_id = qid, .host_backed = true},
+      .rx_ring = {.descriptor_size = sizeof(RxDescriptor), .ring_size = nrx + 1, .base_address = rx_at, .queue_id = qid, .host_backed = true},
+      .tx_completion = {.ring_size = ntx + 1, .queue_id = qid},
+      .rx_completion = {.ring_size = 70 * ntx + 1, .queue_id = qid},
+  };
+  QueuePair qp{qc, dma};
+  for (auto& t : tx) {
+    std::vector<std::byte> b(sizeof(TxDescriptor));
+    std::memcpy(b.data(), &t, sizeof(t));
+    assert(qp.tx_ring().push_descriptor(b).ok());
+  }
+  for (auto& x : rx) {
+    std::vector<std::byte> b(sizeof(RxDescriptor));
+    std::memcpy(b.data(), &x, sizeof(x));
+    assert(qp.rx_ring().push_descriptor(b).ok());
+  }
+  std::vector<std::byte> pushed(mem_size);
+  assert(mem.read(0, pushed).ok());
+  std::vector<std::uint8_t> ours(mem_size);
+  std::memcpy(ours.data(), pushed.data(), mem_size);
+  while (qp.process_once()) {
+  }
+  std::vector<CompletionEntry> ref_tx, ref_rx;
+  while (auto c = qp.tx_completion().poll_completion()) ref_tx.push_back(*c);
+  while (auto c = qp.rx_completion().poll_completion()) ref_rx.push_back(*c);
+  std::vector<std::byte> ref_after(mem_size);
+  assert(mem.read(0, ref_after).ok());
+  // ---- the driver with the rings' offsets
+  using namespace rx_stage_detail;
+  BatchedQueuePairConfig cfg;
+  cfg.queue_id = qid;
+  test::CpuBackend dev{ours, nullptr, TupleSpec{}};
+  RxBatchResult out;
+  QueuePairStats st{};
+  BatchScratch scratch;
+  const RingSlots slots{tx_at, rx_at};
+  run_batch(cfg, mem_size, tx, rx, st, out, scratch, dev, -1, nullptr, &slots);
+  g_ring_batches += 1;
+  g_ring_rereads += dev.refetches;
+  bool ok = out.tx_completions.size() == ref_tx.size() && out.rx_completions.size() == ref_rx.size();
+  for (std::size_t i = 0; ok && i < ref_tx.size(); ++i) ok = same(out.tx_completions[i], ref_tx[i]);
+  for (std::size_t i = 0; ok && i < ref_rx.size(); ++i) ok = same(out.rx_completions[i], ref_rx[i]);
+  ok = ok && same(st, qp.stats());
+  ok = ok && std::memcmp(ours.data(), ref_after.data(), mem_size) == 0;
+  if (!ok) {
+    std::fprintf(stderr, "ring seed %llu: mismatch (tx %zu/%zu rx %zu/%zu)\n", (unsigned long long) seed,
+                 out.tx_completions.size(), ref_tx.size(), out.rx_completions.size(), ref_rx.size());
+    return 1;
+  }
+  return 0;
+}
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -535,10 +671,12 @@ int main(int argc, char** argv) {
   const std::uint64_t count = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 200;
   int bad = check_disjoint_large();
   for (std::uint64_t s = first; s < first + count; ++s) bad += run_case(s);
+  for (std::uint64_t s = first; s < first + count / 4; ++s) bad += run_ring_case(s);
   if (bad) return 1;
   std::printf("rx_stage_fuzz: ok (%llu batches; %zu with overlapping buffers, %zu split into sub-batches, %zu gathered "
               "from a copy; %zu on a memory with its own DMA faults; relaxation settled every batch in <= %d steps; split "
-              "plans equal, %zu pieces fewer)\n",
-              (unsigned long long) count, g_overlapping, g_split, g_snap, g_faulty, g_steps_max, g_split_pieces_saved);
+              "plans equal, %zu pieces fewer; %zu batches on host-backed rings their own writes land on, %zu re-reads)\n",
+              (unsigned long long) count, g_overlapping, g_split, g_snap, g_faulty, g_steps_max, g_split_pieces_saved,
+              g_ring_batches, g_ring_rereads);
   return 0;
 }
