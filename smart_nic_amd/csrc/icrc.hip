@@ -5,10 +5,8 @@
 #include "common.h"
 #include "host.h"
 
-#include <algorithm>
 #include <cstdlib>
 #include <cstring>
-#include <vector>
 
 using namespace nicgpu_detail;
 
@@ -121,18 +119,7 @@ __device__ __forceinline__ uint32_t b4_dword(const uint8_t* __restrict__ Tb, uin
 // line walk, not the table work, bounds this kernel; 4-chunk windows, a
 // prefetch of the packet's next window, and 32-B windows loaded coalesced and
 // transposed back with ds_bpermute were all slower.
-// POL (tuning, NICGPU_ICRC=b4nt / b4sc1): the frame loads' cache policy — 0
-// plain, 1 nt, 2 sc1 (L2-served, bypassing the CU's 32 KiB L1, which the
-// 64 lines of a wave-step overrun: every 16-B load then refetches its line).
-template <int POL>
-__device__ __forceinline__ u32x4 icrc_load(const u32x4* f16, __amdgpu_buffer_rsrc_t rsrc, uint64_t c) {
-  if constexpr (POL == 1) return __builtin_nontemporal_load(f16 + c);
-  else if constexpr (POL == 2)
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int) (uint32_t) (c * 16u), 0, 16));
-  else return f16[c];
-}
-
-template <int CH, int MODE, int POL = 0>  // CH: chunks per step, to the end of the packet's aligned CH x 16-B window
+template <int CH, int MODE>  // CH: chunks per step, to the end of the packet's aligned CH x 16-B window
 __global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t Tb[kB4Bytes];
   __shared__ uint64_t ring_all[kIcrcWpb][kIcrcRing];
@@ -160,9 +147,6 @@ __global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
   const uint64_t p0 = wave * per < P.n ? wave * per : P.n;
   const uint64_t p1 = p0 + per < P.n ? p0 + per : P.n;
   const u32x4* f16 = reinterpret_cast<const u32x4*>(P.frames);
-  // (POL 2: frames below 4 GiB, the launcher checks)
-  const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(P.frames), (short) 0, 0x7FFFFFF0, 0x00020000);
 
   uint64_t loaded = p0;
   auto refill = [&]() __attribute__((always_inline)) {
@@ -211,7 +195,7 @@ __global__ __launch_bounds__(kIcrcThreads) void icrc_b4_kernel(IcrcParams P) {
       const uint32_t lim = ((cl + 1u) << 4 < end4 ? (cl + 1u) << 4 : end4) - cur;  // dwords [0, lim) of the step
       u32x4 v[CH];
 #pragma unroll
-      for (int u = 0; u < CH; ++u) v[u] = icrc_load<POL>(f16, rsrc, c16 + (c0 + (uint32_t) u <= cl ? c0 + (uint32_t) u : cl));
+      for (int u = 0; u < CH; ++u) v[u] = f16[c16 + (c0 + (uint32_t) u <= cl ? c0 + (uint32_t) u : cl)];
       __builtin_amdgcn_sched_barrier(0);  // every load of the step in flight before the chain starts
       const uint4 m0 = lead_m[c0 == 0u ? pos : 0u];
       v[0][0] &= m0.x;
@@ -478,225 +462,6 @@ __global__ __launch_bounds__(kIcrcThreads) void icrc_coop_kernel(IcrcParams P) {
 }
 
 
-// ------------------------------------------- LDS-staged line walk (lds) --
-// The lane-per-packet walk of icrc_b4_kernel, fed from LDS.  Its own loads —
-// every lane a 16-B piece of its own packet's 128-B line, 64 lines per wave
-// instruction — overrun the CU's 32 KiB L1 (8 waves x 64 lines x 128 B), so
-// each piece refetched its line from L2.  Here a wave loads its 64 lanes'
-// current lines COOPERATIVELY: instruction u moves lines 8u..8u+7 whole (lane l
-// the piece l % 8 of lane 8u + l / 8's line) straight into LDS
-// (global_load_lds_dwordx4: 1 KiB per instruction, 8 lines per instruction),
-// and each lane reads its own line back with eight ds_read_b128.  The next
-// step's lines are issued right after that, so they land while the chain runs
-// on the registers.
-//   * Line image: lane T's line at stage + 128 T, chunk g of it in slot
-//     g ^ ((T >> 1) & 7) (the swizzle goes on the source address; the eight
-//     reads of a 16-lane group then cover all 64 banks).
-//   * Chunks of the line outside the packet are loaded from a zero chunk
-//     instead (no read past a packet's last chunk, and the leading ones read
-//     as the zeros the lead state expects); the packet's first chunk, when its
-//     first byte is not the chunk's, is masked in LDS by its own lane.
-//   * The chain enters at the line's first byte from kCrcLead128[off % 128]
-//     (the state those zero bytes take to 0xFFFFFFFF) and runs to the last
-//     whole dword; 0..3 tail bytes as in icrc_b4_kernel.
-//   * Byte tables in 16 copies (64 KiB; lanes l and l + 16 share a copy:
-//     2-way conflicts), so 8 waves' 8 KiB line images fit beside them.
-__device__ u32x4 kIcrcZero16[1] = {{0u, 0u, 0u, 0u}};
-
-constexpr uint32_t kL16Bytes = 256u * 256u;  // row v: T0..T3[v] x 16 copies
-
-__device__ __forceinline__ uint32_t l16_lookup(const uint8_t* __restrict__ Tb, uint32_t cbr, uint32_t s, uint32_t sel) {
-  return *reinterpret_cast<const uint32_t*>(Tb + __builtin_amdgcn_perm(cbr, s, sel));
-}
-
-__device__ __forceinline__ uint32_t l16_dword(const uint8_t* __restrict__ Tb, uint32_t cbr, uint32_t s) {
-  const uint32_t t0 = l16_lookup(Tb, cbr, s, 0x0C0C0007u);  // T3[s.b0]
-  const uint32_t t1 = l16_lookup(Tb, cbr, s, 0x0C0C0106u);  // T2[s.b1]
-  const uint32_t t2 = l16_lookup(Tb, cbr, s, 0x0C0C0205u);  // T1[s.b2]
-  const uint32_t t3 = l16_lookup(Tb, cbr, s, 0x0C0C0304u);  // T0[s.b3]
-  return xor3(t0, t1, t2) ^ t3;
-}
-
-template <int MODE>
-__global__ __launch_bounds__(kIcrcThreads) void icrc_lds_kernel(IcrcParams P) {
-  __shared__ __attribute__((aligned(16))) uint8_t Tb[kL16Bytes];
-  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kIcrcWpb][kWave * 128];
-  __shared__ uint64_t ring_all[kIcrcWpb][kIcrcRing];
-  __shared__ uint4 lead_m[16];  // bytes >= p of a chunk kept
-  __shared__ uint32_t lead_s[128];
-  if (threadIdx.x < 16u) {
-    const int p = (int) threadIdx.x;
-    lead_m[p] = make_uint4(dword_keep(p, 16, 0), dword_keep(p, 16, 1), dword_keep(p, 16, 2), dword_keep(p, 16, 3));
-  }
-  if (threadIdx.x < 128u) lead_s[threadIdx.x] = kCrcLead128.s[threadIdx.x];
-  for (uint32_t q = threadIdx.x; q < kL16Bytes / 16u; q += kIcrcThreads) {
-    const uint32_t v = q >> 4, t = (q >> 2) & 3u;  // 16-B piece q: row v, table t, copies 4 (q & 3) ..
-    const uint32_t val = kCrc32c.t[t][v];
-    reinterpret_cast<uint4*>(Tb)[q] = make_uint4(val, val, val, val);
-  }
-  __syncthreads();
-  const uint32_t lane = lane_id();
-  const uint32_t c4 = (lane & 15u) << 2;  // this lane's copy: bank (16 t + lane % 16) mod 32
-  const uint32_t cbr = c4 | ((c4 + 64u) << 8) | ((c4 + 128u) << 16) | ((c4 + 192u) << 24);
-  const uint32_t wv = threadIdx.x / kWave;
-  uint64_t* ring = ring_all[wv];
-  uint8_t* stage = stage_all[wv];
-  const uint32_t swz = (lane >> 1) & 7u;
-  const uint64_t nwaves = (uint64_t) gridDim.x * kIcrcWpb;
-  const uint64_t wave = (uint64_t) blockIdx.x * kIcrcWpb + wv;
-  const uint64_t per = (P.n + nwaves - 1) / nwaves;
-  const uint64_t p0 = wave * per < P.n ? wave * per : P.n;
-  const uint64_t p1 = p0 + per < P.n ? p0 + per : P.n;
-
-  uint64_t loaded = p0;
-  auto refill = [&]() __attribute__((always_inline)) {
-    const uint64_t i = loaded + lane;
-    ring[i & (kIcrcRing - 1)] = i < p1 ? P.desc[i] : 0ull;
-    loaded += kWave;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  };
-  refill();
-  refill();
-  uint64_t next = p0 + kWave;
-  uint64_t my = p0 + lane;
-  // the packet: span [off, off + span); its lines from line0 = off >> 7; byte
-  // positions below relative to line0 * 128: Z = off % 128 the first byte,
-  // wend = Z + span the end (0: empty span), end4 = wend & ~3; nl lines, il
-  // the next to process
-  uint64_t line0 = 0;
-  uint32_t Z = 0, wend = 0, end4 = 0, nl = 0, il = 0, len = 0, S = 0xFFFFFFFFu;
-  auto setup = [&](uint64_t k) __attribute__((always_inline)) {
-    const uint64_t d = ring[k & (kIcrcRing - 1)];
-    const uint64_t off = d & kOffMask;
-    len = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
-    const uint32_t span = P.verify ? (len >= 4u ? len - 4u : 0u) : len;
-    line0 = off >> 7;
-    Z = (uint32_t) off & 127u;
-    wend = span ? Z + span : 0u;
-    end4 = wend & ~3u;
-    nl = (wend + 127u) >> 7;
-    il = 0;
-    S = span ? lead_s[Z] : 0xFFFFFFFFu;
-  };
-  if (my < p1) setup(my);
-  // this lane's line for the loads of a step: its index and the slots
-  // [lo, hi] of it that hold packet chunks (lo > hi: none)
-  auto line_of = [&](bool act, uint32_t& lo, uint32_t& hi) __attribute__((always_inline)) -> uint64_t {
-    if (!act || il >= nl) {
-      lo = 1u;
-      hi = 0u;
-      return 0;
-    }
-    lo = il == 0u ? (Z >> 4) : 0u;
-    const uint32_t last = (wend - 1u) >> 4;  // the packet's last chunk (relative)
-    hi = last >= 8u * il + 7u ? 7u : last - 8u * il;
-    return line0 + il;
-  };
-  // the cooperative loads of every lane's line into the stage
-  auto issue = [&](uint64_t ln, uint32_t lo, uint32_t hi) __attribute__((always_inline)) {
-    const uint32_t ln_lo = (uint32_t) ln, ln_hi = (uint32_t) (ln >> 32), lh = lo | (hi << 4);
-    const uint32_t sub = lane & 7u;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const uint32_t T = 8u * (uint32_t) u + (lane >> 3);
-      const uint32_t tlo = (uint32_t) __builtin_amdgcn_ds_bpermute((int) (T << 2), (int) ln_lo);
-      const uint32_t thi = (uint32_t) __builtin_amdgcn_ds_bpermute((int) (T << 2), (int) ln_hi);
-      const uint32_t tlh = (uint32_t) __builtin_amdgcn_ds_bpermute((int) (T << 2), (int) lh);
-      const uint32_t g = sub ^ ((T >> 1) & 7u);  // the chunk this piece of T's line holds
-      const bool in = g >= (tlh & 15u) && g <= (tlh >> 4);
-      const uint64_t tl = ((uint64_t) thi << 32) | tlo;
-      const void* src = in ? static_cast<const void*>(P.frames + tl * 128u + 16u * g)
-                           : static_cast<const void*>(&kIcrcZero16[0]);
-      __builtin_amdgcn_global_load_lds(src, stage + u * 1024, 16, 0, 0);
-    }
-  };
-  uint32_t lo = 0, hi = 0;
-  uint64_t ln = line_of(my < p1, lo, hi);
-  issue(ln, lo, hi);
-  for (;;) {
-    const bool active = my < p1;
-    if (__ballot(active) == 0ull) break;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const bool has = active && il < nl;
-    // the packet's first chunk, where its first byte is not the chunk's: the
-    // bytes before it zeroed in place
-    if (has && il == 0u && (Z & 15u) != 0u) {
-      uint4* c = reinterpret_cast<uint4*>(stage + lane * 128u + 16u * ((Z >> 4) ^ swz));
-      const uint4 m = lead_m[Z & 15u];
-      uint4 x = *c;
-      x.x &= m.x;
-      x.y &= m.y;
-      x.z &= m.z;
-      x.w &= m.w;
-      *c = x;
-    }
-    __builtin_amdgcn_wave_barrier();
-    u32x4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      v[u] = *reinterpret_cast<const u32x4*>(stage + lane * 128u + 16u * ((uint32_t) u ^ swz));
-    // dwords of this line to chain: [0, lim)
-    const uint32_t lim = has ? (end4 > 128u * il ? (end4 - 128u * il < 128u ? (end4 - 128u * il) >> 2 : 32u) : 0u) : 0u;
-    // finishing lanes (this line is their packet's last, or it has none) take
-    // the next packets of the wave's range now, so that every lane's next line
-    // can be loaded before the chain
-    const bool finished = active && il + 1u >= nl;
-    const uint64_t m = __ballot(finished);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
-    const uint64_t my_next = finished ? next + rank : my;
-    next += (uint64_t) __builtin_popcountll(m);
-    // this packet's state, kept for the chain and the finish
-    const uint64_t c_line0 = line0;
-    const uint32_t c_Z = Z, c_wend = wend, c_end4 = end4, c_len = len;
-    uint32_t Sc = S;
-    if (finished && my_next < p1) setup(my_next);
-    else if (!finished && active) ++il;
-    // (after the setups, which read ring entries a refill may overwrite; and
-    // before the line loads, so its own load's wait drains nothing of them)
-    if (next + kWave > loaded && loaded < p1) refill();
-    ln = line_of(finished ? my_next < p1 : active, lo, hi);
-    __builtin_amdgcn_sched_barrier(0);
-    issue(ln, lo, hi);  // the next step's lines, in flight during the chain
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t Sn = MODE == 1 ? Sc + v[u][i] : l16_dword(Tb, cbr, Sc ^ v[u][i]);
-        Sc = (uint32_t) (4 * u + i) < lim ? Sn : Sc;
-      }
-    }
-    if (finished) {
-      if (c_end4 < c_wend) {  // 1..3 bytes past the last whole dword: byte steps on T0
-        const uint32_t tw = *reinterpret_cast<const uint32_t*>(P.frames + c_line0 * 128u + c_end4);
-#pragma unroll
-        for (uint32_t b = 0; b < 3u; ++b) {
-          const uint32_t idx = c_end4 + b;
-          const uint32_t z = Sc ^ (idx < c_Z ? 0u : (tw >> (8u * b)) & 0xFFu);
-          const uint32_t Sn = l16_lookup(Tb, cbr, z, 0x0C0C0004u) ^ (Sc >> 8);
-          Sc = idx < c_wend ? Sn : Sc;
-        }
-      }
-      const uint32_t crc = Sc ^ 0xFFFFFFFFu;
-      if (P.out_crc) P.out_crc[my] = (P.verify && c_len < 4u) ? 0u : crc;
-      if (P.verify) {
-        uint32_t ok = 0;
-        if (c_len >= 4u) {
-          const uint8_t* t = P.frames + c_line0 * 128u + c_Z + (c_len - 4u);
-          const uint32_t stored = ((uint32_t) t[0] << 24) | ((uint32_t) t[1] << 16) | ((uint32_t) t[2] << 8) | t[3];
-          ok = stored == crc;
-        }
-        P.out_ok[my] = (uint8_t) ok;
-      }
-      my = my_next;
-    } else {
-      S = Sc;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the wave
-}
 }  // namespace
 
 extern "C" {
@@ -724,7 +489,12 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
   // 408 / 471 at 4 lines in flight per group, profiles/r04_icrc_coop.jsonl;
   // round 5's pipelined lane walk — two windows in flight per lane, exact
   // vmcnt waits — C2 437 / C3 515 us against 402 / 469, its loads alone 447 /
-  // 420: profiles/r05_icrc_pipe_rejected.jsonl, code in git history)
+  // 420: profiles/r05_icrc_pipe_rejected.jsonl, code in git history; round 6's
+  // LDS-staged line walk — whole lines moved into LDS by cooperative
+  // global_load_lds, 16-copy tables — C2 / C3 442 / 547 against 404 / 477, its
+  // loads alone 324 / 386 against 388 / 384, and the lane walk's loads with
+  // sc1 / nt policies 604 / 689 and 1006 / 1036: profiles/r06_icrc_variants.jsonl,
+  // code in git history, commit 5777fdb)
   static const int var = [] {
     const char* e = std::getenv("NICGPU_ICRC");
     if (!e) return 0;
@@ -732,38 +502,14 @@ int nicgpu_icrc_batch(const uint8_t* frames, const uint64_t* desc, size_t n, int
     if (std::strcmp(e, "b4mem") == 0) return 1;
     if (std::strcmp(e, "b4") == 0) return 0;
     if (std::strcmp(e, "coopmem") == 0) return 3;
-    if (std::strcmp(e, "b4nt") == 0) return 4;
-    if (std::strcmp(e, "b4sc1") == 0) return 5;
-    if (std::strcmp(e, "lds") == 0) return 6;
-    if (std::strcmp(e, "ldsmem") == 0) return 7;
     return 0;
   }();
   const uint64_t want = (n + kIcrcThreads - 1) / kIcrcThreads;
   const uint64_t cap = (uint64_t) di->cus * (uint64_t) blocks_per_cu(reinterpret_cast<const void*>(icrc_b4_kernel<8, 0>), kIcrcThreads, 0);
   const unsigned grid = (unsigned) (want < 1 ? 1 : (want < cap ? want : cap));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // bytes the descriptors can address (b4sc1's 32-bit buffer offsets; checked
-  // only for it, once per descriptor array: the tuning A/B's warm-up pays it)
-  static const uint64_t* span_desc = nullptr;
-  static size_t span_n = 0;
-  static uint64_t span = 0;
-  if (var == 5 && (span_desc != desc || span_n != n)) {
-    std::vector<uint64_t> h(n);
-    if (hipMemcpy(h.data(), desc, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return NICGPU_ERR_HIP;
-    span = 0;
-    for (uint64_t d : h) span = std::max<uint64_t>(span, (d & kOffMask) + (d >> NICGPU_DESC_OFFSET_BITS) + 16);
-    span_desc = desc;
-    span_n = n;
-  }
-  const int v = var == 5 && span >= 0x7FFFFFF0ull ? 0 : var;
-  if (v == 6 || v == 7) {
-    const uint64_t capl = (uint64_t) di->cus * (uint64_t) blocks_per_cu(reinterpret_cast<const void*>(icrc_lds_kernel<0>), kIcrcThreads, 0);
-    const unsigned gl = (unsigned) (want < 1 ? 1 : (want < capl ? want : capl));
-    if (v == 6) hipLaunchKernelGGL(icrc_lds_kernel<0>, dim3(gl), dim3(kIcrcThreads), 0, s, P);
-    else hipLaunchKernelGGL(icrc_lds_kernel<1>, dim3(gl), dim3(kIcrcThreads), 0, s, P);
-  } else if (v == 5) hipLaunchKernelGGL((icrc_b4_kernel<8, 0, 2>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
-  else if (v == 4) hipLaunchKernelGGL((icrc_b4_kernel<8, 0, 1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
-  else if (v == 1) hipLaunchKernelGGL((icrc_b4_kernel<8, 1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
+  const int v = var;
+  if (v == 1) hipLaunchKernelGGL((icrc_b4_kernel<8, 1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
   else if (v == 0) hipLaunchKernelGGL((icrc_b4_kernel<8, 0>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
   else if (v == 3) hipLaunchKernelGGL((icrc_coop_kernel<1>), dim3(grid), dim3(kIcrcThreads), 0, s, P);
   else hipLaunchKernelGGL((icrc_coop_kernel<0>), dim3(grid), dim3(kIcrcThreads), 0, s, P);

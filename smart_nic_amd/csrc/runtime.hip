@@ -227,6 +227,13 @@ int nicgpu_host_register(void* host_ptr, size_t bytes, void** dev_alias, int* ow
       *owned = 1;
       return NICGPU_OK;
     }
+  // registered or allocated page-locked by someone else: hipHostRegister would
+  // succeed again on an identical range (it does not count registrations), and
+  // this library's release would then unregister the owner's
+  hipPointerAttribute_t pa{};
+  const hipError_t q = hipPointerGetAttributes(&pa, host_ptr);
+  (void) hipGetLastError();
+  if (q == hipSuccess && pa.type == hipMemoryTypeHost) return NICGPU_ERR_INVALID;
   const hipError_t e = hipHostRegister(host_ptr, bytes, hipHostRegisterMapped);
   if (e != hipSuccess) {
     (void) hipGetLastError();  // not sticky for the caller's next call
