@@ -945,14 +945,32 @@ int run_edges() {
     assert(nicgpu_memcpy_async(base + ring_at + 4096, rx2.data(), rx2.size() * sizeof(RxDescriptor), nullptr) ==
            NICGPU_OK);
     assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
-    bool threw = false;
-    try {
-      qp2.process_batch(DeviceHostMemory{base, mem_size}, dd, o2);
-    } catch (const GpuError& e) {
-      threw = e.status() == NICGPU_ERR_INVALID;
-    }
-    if (!threw) std::fprintf(stderr, "edges: an RX buffer over the descriptor ring was not refused\n");
-    ok = ok && threw;
+    // popped as the reference pops host-backed rings (descriptor_ring.cpp:
+    // 97-106): the product path against the driver with RingSlots on the CPU
+    // backend over a copy of the same image
+    std::vector<std::uint8_t> host(mem_size), after(mem_size);
+    assert(nicgpu_memcpy_async(host.data(), base, mem_size, nullptr) == NICGPU_OK);
+    assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+    BatchedQueuePairConfig ccfg = cfg;
+    ccfg.rss = nullptr;
+    ccfg.on_interrupt = nullptr;
+    test::CpuBackend cpu{host, nullptr, TupleSpec{}};
+    RxBatchResult co;
+    QueuePairStats cst{};
+    rx_stage_detail::BatchScratch cs;
+    const rx_stage_detail::RingSlots slots{ring_at, ring_at + 4096};
+    rx_stage_detail::run_batch(ccfg, mem_size, tx, rx2, cst, co, cs, cpu, -1, nullptr, &slots);
+    BatchedQueuePair qp3{cfg};
+    qp3.process_batch(DeviceHostMemory{base, mem_size}, dd, o2);
+    assert(nicgpu_memcpy_async(after.data(), base, mem_size, nullptr) == NICGPU_OK);
+    assert(nicgpu_stream_synchronize(nullptr) == NICGPU_OK);
+    bool eq = !o2.timings.device && o2.tx_completions.size() == co.tx_completions.size() &&
+              o2.rx_completions.size() == co.rx_completions.size() &&
+              std::memcmp(&qp3.stats(), &cst, sizeof(cst)) == 0 && after == host;
+    for (std::size_t i = 0; eq && i < co.tx_completions.size(); ++i) eq = same(o2.tx_completions[i], co.tx_completions[i]);
+    for (std::size_t i = 0; eq && i < co.rx_completions.size(); ++i) eq = same(o2.rx_completions[i], co.rx_completions[i]);
+    if (!eq) std::fprintf(stderr, "edges: an RX buffer over the descriptor ring: the product path differs from the driver\n");
+    ok = ok && eq;
   }
   // a batch of more TX descriptors than the device context's 32-bit piece
   // indices allow (NICGPU_QP_MAX_TX): refused by nicgpu_qp_reserve, so the

@@ -260,7 +260,8 @@ def test_rx_stage_device_limits(tmp_path):
     """The device path's limits: a descriptor planning more pieces than 32-bit
     piece indices allow makes nicgpu_qp_plan return NICGPU_ERR_RANGE and the
     batch takes the host path (equal to the host resolve); descriptor arrays
-    inside the image that an RX buffer of the batch overlaps are refused; a
+    inside the image that an RX buffer of the batch overlaps are popped again
+    after the write (equal to the driver with RingSlots on the CPU backend); a
     plan that outgrows the piece buffers is redone once; and a batch whose
     ring positions 8 relaxation steps do not settle (400 TSO packets against
     a ring of one-in-three too-small buffers) is walked on the device
