@@ -963,14 +963,14 @@ bool defer_env() {
   return on;
 }
 
-// NIC_IRQ_TOUCH=1: the chunked interrupt replay's completions read once by a
-// helper thread as they land (tuning A/B; off by default)
-bool irq_touch_env() {
-  static const bool on = [] {
-    const char* e = std::getenv("NIC_IRQ_TOUCH");
-    return e && std::strcmp(e, "1") == 0;
+// HostMemory mirrors in HBM for pipelined batches: 2, or NIC_IMAGE_MIRRORS=1
+// (tuning A/B)
+unsigned image_mirrors_env() {
+  static const unsigned n = [] {
+    const char* e = std::getenv("NIC_IMAGE_MIRRORS");
+    return e && std::strcmp(e, "1") == 0 ? 1u : 2u;
   }();
-  return on;
+  return n;
 }
 
 // One growable device buffer.
@@ -1238,6 +1238,7 @@ struct BatchedQueuePair::Slot {
   // (dep_stage) or the delivery (dep_rx) must follow, and the writes a
   // host-path batch made (written back from the device copy in wbuf)
   HostImage* image = nullptr;
+  unsigned mirror = 0;        // which of the image's HBM mirrors the batch runs on
   void* ev_staged = nullptr;  // the batch's TX bytes are in the mirror
   void* ev_wb = nullptr;      // its delivered bytes are back in the host memory
   bool staged = false, stage_deferred = false, wb = false, whole = false;
@@ -1331,8 +1332,13 @@ struct BatchedQueuePair::HostImage {
   bool owned = false;             // registered by this stage
   std::size_t size = 0;
   int device = -1;
-  DevBuf mirror;
-  DeviceHostMemory view() const { return DeviceHostMemory{static_cast<std::byte*>(mirror.p), size}; }
+  // two mirrors: pipelined batches alternate between them, so a batch's
+  // delivery need not wait for the previous batch's write-back out of the
+  // same bytes (the second is allocated by the first pipelined submit)
+  DevBuf mirror[2];
+  DeviceHostMemory view(unsigned m = 0) const {
+    return DeviceHostMemory{static_cast<std::byte*>(mirror[m].p), size};
+  }
   void release() {
     if (owned && host) (void) nicgpu_host_unregister(host);
     mem = nullptr;
@@ -1895,53 +1901,6 @@ void BatchedQueuePair::fire_interrupts(RxBatchResult& r, Slot* sl) {
     double wait_us = 0;
     const CompletionEntry* itx = sl->h_itx.get<CompletionEntry>(1);
     const CompletionEntry* irx = sl->h_irx.get<CompletionEntry>(1);
-    if (irq_touch_env()) {
-      // (opt-in, NIC_IRQ_TOUCH=1) a helper on the next CPU waits for each chunk
-      // and reads it once (a load per 64-B line), so the replay finds the
-      // DMA-written completions in the shared cache instead of DRAM
-      std::atomic<int> ready[2] = {-1, -1};
-      std::atomic<bool> failed{false}, stop{false};
-      const std::vector<int> cpus = rx_stage_detail::near_cpus(2);
-      std::thread helper([&] {
-        rx_stage_detail::pin_to(cpus, 1);
-        std::uint32_t sink = 0;
-        for (int c = 0; c < Slot::kIrqChunks && !stop.load(std::memory_order_relaxed); ++c)
-          for (int side = 0; side < 2; ++side) {
-            if (nicgpu_event_synchronize(sl->ev_irq[side][c]) != NICGPU_OK) {
-              failed.store(true);
-              ready[0].store(Slot::kIrqChunks);
-              ready[1].store(Slot::kIrqChunks);
-              return;
-            }
-            const std::size_t per = side ? prx : ptx, n = side ? sl->irq_nrx : sl->irq_ntx;
-            const auto* b = reinterpret_cast<const volatile std::uint8_t*>(side ? irx : itx);
-            const std::size_t lo = std::min(n, per * c) * sizeof(CompletionEntry);
-            const std::size_t hi = (c + 1 == Slot::kIrqChunks ? n : std::min(n, per * (c + 1))) * sizeof(CompletionEntry);
-            for (std::size_t o = lo; o < hi; o += 64) sink += b[o];
-            ready[side].store(c, std::memory_order_release);
-          }
-        (void) sink;
-      });
-      struct Join {
-        std::thread& t;
-        std::atomic<bool>& stop;
-        ~Join() {
-          stop.store(true);
-          t.join();
-        }
-      } join{helper, stop};
-      rx_stage_detail::replay_interrupts_chunked(
-          config_, std::span<const CompletionEntry>(itx, sl->irq_ntx), std::span<const CompletionEntry>(irx, sl->irq_nrx),
-          ptx, prx, [&](int side, std::size_t c) {
-            const int want = static_cast<int>(std::min<std::size_t>(c, Slot::kIrqChunks - 1));
-            const auto w = clock::now();
-            while (ready[side].load(std::memory_order_acquire) < want) std::this_thread::yield();
-            if (failed.load()) check(NICGPU_ERR_HIP, "nicgpu_event_synchronize");
-            wait_us += std::chrono::duration<double, std::micro>(clock::now() - w).count();
-          });
-      r.timings.irq_wait_us = wait_us;
-      return;
-    }
     rx_stage_detail::replay_interrupts_chunked(
         config_, std::span<const CompletionEntry>(itx, sl->irq_ntx), std::span<const CompletionEntry>(irx, sl->irq_nrx),
         ptx, prx, [sl, &wait_us](int side, std::size_t c) {
@@ -2551,7 +2510,7 @@ BatchedQueuePair::HostImage& BatchedQueuePair::bind_image(HostMemory& m, bool ch
       I.alias = static_cast<std::uint8_t*>(alias);
       I.owned = owned != 0;
     }
-    I.mirror.get((size + 15) / 16 * 16);
+    I.mirror[0].get((size + 15) / 16 * 16);
   }
   return I;
 }
@@ -2617,7 +2576,8 @@ void BatchedQueuePair::image_prepare(Slot& sl, HostImage& img, std::span<const T
     Slot& p = S.slot[(S.head + k) % Scratch::kSlots];
     if (&p == &sl || p.image != &img || p.rx_hi <= p.rx_lo) continue;
     if (p.rx_lo < sl.tx_hi && sl.tx_lo < p.rx_hi) sl.dep_stage.push_back(&p);
-    if (p.rx_lo < sl.rx_hi && sl.rx_lo < p.rx_hi) sl.dep_rx.push_back(&p);
+    // the delivery may not overwrite bytes a write-back still reads
+    if (p.mirror == sl.mirror && p.rx_lo < sl.rx_hi && sl.rx_lo < p.rx_hi) sl.dep_rx.push_back(&p);
   }
 }
 
@@ -2629,7 +2589,7 @@ void BatchedQueuePair::image_stage(Slot& sl, std::size_t ntx, const TxDescriptor
                                    void* stream) {
   HostImage& I = *sl.image;
   if (sl.tx_hi > sl.tx_lo) {
-    auto* mirror = static_cast<std::uint8_t*>(I.mirror.p);
+    auto* mirror = static_cast<std::uint8_t*>(I.mirror[sl.mirror].p);
     if (sl.whole) {
       check(nicgpu_memcpy_async(mirror + sl.tx_lo, I.host + sl.tx_lo, sl.tx_hi - sl.tx_lo, stream), "nicgpu_memcpy_async");
     } else {
@@ -2651,7 +2611,7 @@ void BatchedQueuePair::image_stage(Slot& sl, std::size_t ntx, const TxDescriptor
 void BatchedQueuePair::image_writeback(Slot& sl, const nicgpu_segment_write* writes_dev, std::size_t n, void* stream) {
   HostImage& I = *sl.image;
   if (n)
-    check(nicgpu_image_writeback(static_cast<const std::uint8_t*>(I.mirror.p), I.alias, I.size, writes_dev, n, stream),
+    check(nicgpu_image_writeback(static_cast<const std::uint8_t*>(I.mirror[sl.mirror].p), I.alias, I.size, writes_dev, n, stream),
           "nicgpu_image_writeback");
   check(nicgpu_event_record(sl.ev_wb, stream), "nicgpu_event_record");
   sl.wb = true;
@@ -2668,7 +2628,7 @@ void BatchedQueuePair::image_host_path(Slot& sl, std::span<const TxDescriptor> t
   check(nicgpu_stream_wait_event(stream, sl.ev_staged), "nicgpu_stream_wait_event");
   for (Slot* p : sl.dep_rx) check(nicgpu_stream_wait_event(stream, p->ev_wb), "nicgpu_stream_wait_event");
   sl.applied.clear();
-  on_host(sl.image->view(), tx, rx, st, out, stream, disjoint, check_us, &sl.applied, sl.wcheck);
+  on_host(sl.image->view(sl.mirror), tx, rx, st, out, stream, disjoint, check_us, &sl.applied, sl.wcheck);
   out.timings.host_image = true;
   out.timings.staged_whole = sl.whole;
   const std::size_t n = sl.applied.size();
@@ -2704,6 +2664,7 @@ void BatchedQueuePair::process_batch(HostMemory& m, std::span<const TxDescriptor
   sl.mem_writes.mem = &m;
   sl.mem_writes.window = I.host;
   sl.wcheck = checked ? &sl.mem_writes : nullptr;
+  sl.mirror = 0;
   const DeviceHostMemory mem = I.view();
   sl.tx_dev = nullptr;
   sl.rx_dev = nullptr;
@@ -2756,7 +2717,13 @@ void BatchedQueuePair::submit(HostMemory& m, std::span<const TxDescriptor> tx, s
   HostImage& I = bind_image(m, checked, window);
   sl.mem_writes.mem = &m;
   sl.mem_writes.window = I.host;
-  enqueue(I.view(), tx, rx, nullptr, stream, &I);
+  // alternate mirrors while batches are pending (NIC_IMAGE_MIRRORS=1: one, A/B)
+  sl.mirror = 0;
+  if (S.pending && image_mirrors_env() > 1 && I.size) {
+    sl.mirror = 1u - S.slot[(S.head + S.pending - 1) % Scratch::kSlots].mirror;
+    I.mirror[sl.mirror].get((I.size + 15) / 16 * 16);
+  }
+  enqueue(I.view(sl.mirror), tx, rx, nullptr, stream, &I);
 }
 
 std::span<const TxDescriptor> BatchedQueuePair::checked_tx(Slot& sl, HostMemory& m, std::span<const TxDescriptor> tx,
@@ -2874,6 +2841,7 @@ bool BatchedQueuePair::process_queues(const DeviceHostMemory& mem_in, HostImage*
   S.ensure(dev);
   const DeviceHostMemory mem = img ? img->view() : mem_in;
   Slot& sl = S.slot[0];
+  sl.mirror = 0;
   sl.tx_dev = nullptr;
   sl.rx_dev = nullptr;
   sl.image = nullptr;

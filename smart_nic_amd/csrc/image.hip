@@ -12,6 +12,7 @@
 // PCIe-bound (≈ 50 GB/s each way), so the kernels only need enough bytes in
 // flight: every wave has one 1-KiB chunk step of its range outstanding.
 
+#include <cstdlib>
 #include "common.h"
 #include "host.h"
 #include "qp_logic.h"
@@ -131,9 +132,20 @@ __global__ __launch_bounds__(kCopyThreads) void copy_batch_kernel(const CopyBatc
   }
 }
 
+// Workgroups per CU the image kernels may take: 8, or NICGPU_IMG_BLOCKS_PER_CU
+// (1..64; tuning A/B — a write-back beside the next batch's kernels shares the CUs)
+uint64_t image_blocks_per_cu() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("NICGPU_IMG_BLOCKS_PER_CU");
+    const long x = e ? std::strtol(e, nullptr, 10) : 0;
+    return x >= 1 && x <= 64 ? (uint64_t) x : uint64_t{8};
+  }();
+  return v;
+}
+
 unsigned image_grid(uint64_t n, const DeviceInfo* di) {
   const uint64_t want = (n + kImgWaves - 1) / kImgWaves;
-  const uint64_t cap = (uint64_t) di->cus * 8;
+  const uint64_t cap = (uint64_t) di->cus * image_blocks_per_cu();
   return (unsigned) (want < cap ? (want ? want : 1) : cap);
 }
 
