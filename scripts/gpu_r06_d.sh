@@ -1,8 +1,6 @@
 # Round 6, fourth GPU call: the HostMemory tests after the double mirror, then
 # the f1 C3 1 M HostMemory rows A/B — one mirror vs two (NIC_IMAGE_MIRRORS),
-# and the image kernels' workgroups per CU (NICGPU_IMG_BLOCKS_PER_CU); the
-# segmentation kernel with and without the next frame's loads in flight
-# beside the stores (NICGPU_TSO_PREFETCH).
+# and the image kernels' workgroups per CU (NICGPU_IMG_BLOCKS_PER_CU).
 set -o pipefail
 O=gpurun_out/r06d
 mkdir -p $O
@@ -10,14 +8,6 @@ S=tools/bin/bench_rx_stage
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
   tests/test_rx_stage.py tests/test_queue_manager.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -3 $O/tests.log
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu -k "tso or seg" tests > $O/tests_tso.log 2>&1 || { tail -30 $O/tests_tso.log; exit 1; }
-tail -3 $O/tests_tso.log
-for rep in 1 2; do
-  for p in 0 1; do
-    NICGPU_TSO_PREFETCH=$p timeout -k 10 200 python tools/bench_rows.py --rows tso_seg_c5 > $O/tso_p${p}_$rep.jsonl 2> $O/tso_p${p}_$rep.err || { tail -5 $O/tso_p${p}_$rep.err; exit 1; }
-    echo "tso prefetch=$p: $(python -c "import json; d=json.loads(open('$O/tso_p${p}_$rep.jsonl').read().strip().splitlines()[-1]); print(d['us_median'], d['roofline_frac'])")"
-  done
-done
 row() {  # name env... -- args
   local n=$1; shift
   env "$@" > $O/$n.json 2> $O/$n.err || { tail -5 $O/$n.err; return 1; }

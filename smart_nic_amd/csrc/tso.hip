@@ -3,7 +3,6 @@
 // verify, src/queue_pair.cpp:212-278, 434-447) and the materialised
 // segmentation with VLAN insert/strip (tso_segment_kernel).  DESIGN.md §4.2, §4.5.
 
-#include <cstdlib>
 #include "common.h"
 #include "host.h"
 
@@ -379,10 +378,6 @@ __device__ __forceinline__ uint32_t seg_copy_stage(uint8_t* out, uint64_t dst, u
   return sum;
 }
 
-// Pre: frame t+1's loads are issued as soon as frame t is in LDS, so they are
-// in flight beside frame t's segment stores (without it a wave alternates
-// load latency and store bursts; NICGPU_TSO_PREFETCH=0 selects that for A/B).
-template <bool Pre>
 __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
   __shared__ uint4 stage_s[kWavesPerBlock][kSegStageChunks + 1];  // +1: stage_u32's second dword
   const int w = __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
@@ -408,30 +403,9 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
     // consume the loads here, once: otherwise the wait-count pass keeps them
     // pending around the frame loop and drains vmcnt at every frame
     asm volatile("" : "+v"(d_lo), "+v"(d_hi), "+v"(fl_v), "+v"(mh_v), "+v"(sb_v));
-    auto frame_of = [&](uint32_t t) __attribute__((always_inline)) {
-      return ((uint64_t) (uint32_t) __builtin_amdgcn_readlane((int) d_hi, (int) t) << 32) |
-             (uint32_t) __builtin_amdgcn_readlane((int) d_lo, (int) t);
-    };
-    // frame d's first kSegStage bytes from its 16-B chunk, 9 loads of 16 B per
-    // lane (bounded to the frame's chunks); false: too long to stage
-    u32x4 v[kTsoSteps];
-    auto fetch = [&](uint64_t d) __attribute__((always_inline)) {
-      const uint64_t off = d & kOffMask;
-      const uint32_t L = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
-      const uint32_t fo = (uint32_t) (off & 15u);
-      if (fo + L > kSegStage) return;
-      const uint64_t ab = reinterpret_cast<uint64_t>(P.frames) + (off & ~15ull);
-      const uint32_t nb = (fo + L + 15u) & ~15u;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          reinterpret_cast<void*>(uniform64(ab)), (short) 0, __builtin_amdgcn_readfirstlane((int) nb), 0x00020000);
-#pragma unroll
-      for (int c = 0; c < kTsoSteps; ++c)
-        v[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int) (lane * 16u),
-                                                                                (int) ((uint32_t) c * 1024u), 2));
-    };
-    if (Pre && cnt) fetch(frame_of(0));
   for (uint32_t t = 0; t < cnt; ++t) {
-    const uint64_t d = frame_of(t);
+    const uint64_t d = ((uint64_t) (uint32_t) __builtin_amdgcn_readlane((int) d_hi, (int) t) << 32) |
+                       (uint32_t) __builtin_amdgcn_readlane((int) d_lo, (int) t);
     const uint64_t off = d & kOffMask;
     const uint32_t L = (uint32_t) (d >> NICGPU_DESC_OFFSET_BITS);
     const uint32_t fl = (uint32_t) __builtin_amdgcn_readlane((int) fl_v, (int) t);
@@ -440,19 +414,6 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
     const uint32_t mss = mh & 0xFFFFu;
     uint32_t H = mh >> 16;
     const uint32_t seg_base = (uint32_t) __builtin_amdgcn_readlane((int) sb_v, (int) t);
-    const uint64_t a0 = off & ~15ull;
-    const uint32_t fo = (uint32_t) (off & 15u);
-    const bool staged = fo + L <= kSegStage;
-    if (staged) {
-      if (!Pre) fetch(d);
-      __builtin_amdgcn_wave_barrier();  // the previous frame's stage reads are done
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#pragma unroll
-      for (int c = 0; c < kTsoSteps; ++c) stage[c * kWave + (int) lane] = make_uint4(v[c].x, v[c].y, v[c].z, v[c].w);
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    }
-    if (Pre && t + 1 < cnt) fetch(frame_of(t + 1));
     // build_segments (:212-278)
     uint32_t nseg = 1;
     bool seg = (fl & NICGPU_SEG_TSO) && mss > 0 && L > mss;
@@ -468,6 +429,26 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
     if (!seg) H = L;
     const bool insert = fl & NICGPU_SEG_VLAN_INSERT;
     const bool has_vlan = insert || (fl & NICGPU_SEG_VLAN_PRESENT);
+    const uint64_t a0 = off & ~15ull;
+    const uint32_t fo = (uint32_t) (off & 15u);
+    const bool staged = fo + L <= kSegStage;
+    if (staged) {
+      const uint64_t ab = reinterpret_cast<uint64_t>(P.frames) + a0;
+      const uint32_t nb = (fo + L + 15u) & ~15u;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<void*>(uniform64(ab)), (short) 0, __builtin_amdgcn_readfirstlane((int) nb), 0x00020000);
+      u32x4 v[kTsoSteps];
+#pragma unroll
+      for (int c = 0; c < kTsoSteps; ++c)
+        v[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int) (lane * 16u),
+                                                                                (int) ((uint32_t) c * 1024u), 2));
+      __builtin_amdgcn_wave_barrier();  // the previous frame's stage reads are done
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+      for (int c = 0; c < kTsoSteps; ++c) stage[c * kWave + (int) lane] = make_uint4(v[c].x, v[c].y, v[c].z, v[c].w);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
     for (uint32_t k = 0; k < nseg; ++k) {
       const uint32_t clen = seg ? min(mss, L - H - k * mss) : 0u;
       const uint64_t base_len = (uint64_t) H + clen;
@@ -513,14 +494,6 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
   }
 }
 
-bool tso_prefetch() {
-  static const bool on = [] {
-    const char* e = std::getenv("NICGPU_TSO_PREFETCH");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 }  // namespace
 
 extern "C" {
@@ -552,14 +525,9 @@ int nicgpu_tso_segment(const uint8_t* frames, const uint64_t* desc, const uint16
   if (st != NICGPU_OK) return st;
   TsoSegParams P{frames, desc, hdr_len, mss, seg_base, flags, n, out, out_size, stride, out_len, out_csum};
   const uint64_t want = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-  const void* fn = tso_prefetch() ? reinterpret_cast<const void*>(tso_segment_kernel<true>)
-                                  : reinterpret_cast<const void*>(tso_segment_kernel<false>);
-  const uint64_t cap = (uint64_t) di->cus * (uint64_t) blocks_per_cu(fn, kBlock, 0);
+  const uint64_t cap = (uint64_t) di->cus * (uint64_t) blocks_per_cu(reinterpret_cast<const void*>(tso_segment_kernel), kBlock, 0);
   const unsigned grid = (unsigned) (want < cap ? want : cap);
-  if (tso_prefetch())
-    hipLaunchKernelGGL(tso_segment_kernel<true>, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
-  else
-    hipLaunchKernelGGL(tso_segment_kernel<false>, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
+  hipLaunchKernelGGL(tso_segment_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), P);
   return hip_status(hipGetLastError());
 }
 
