@@ -457,6 +457,7 @@ private:
   void image_host_path(Slot& sl, std::span<const TxDescriptor> tx, std::span<const RxDescriptor> rx,
                        QueuePairStats& stats, RxBatchResult& out, void* stream, int disjoint, double& check_us);
   void image_stage(Slot& sl, std::size_t ntx, const TxDescriptor* tx_host, const void* tx_dev, void* stream);
+  void* stage_stream() const;  // the stream host-image staging runs on
   void image_writeback(Slot& sl, const nicgpu_segment_write* writes_dev, std::size_t n, void* stream);
   void back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult& out, void* stream);
   void deliver(Slot& sl, const DeviceHostMemory& mem, std::size_t a, std::size_t b, unsigned flags,

@@ -963,6 +963,17 @@ bool defer_env() {
   return on;
 }
 
+// Host-image TX staging on its own stream (measured, profiles/r06_hostmem_ab.txt:
+// behind the descriptor uploads on side_up, each batch's span copy started
+// 1-2 ms late), or NIC_STAGE_STREAM=0: on side_up (tuning A/B)
+bool stage_stream_env() {
+  static const bool on = [] {
+    const char* e = std::getenv("NIC_STAGE_STREAM");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 // HostMemory mirrors in HBM for pipelined batches: 2, or NIC_IMAGE_MIRRORS=1
 // (tuning A/B)
 unsigned image_mirrors_env() {
@@ -1366,6 +1377,7 @@ struct BatchedQueuePair::Scratch {
   void* side_wb = nullptr;    // host-image write-backs, beside the next batches' work
   void* side_irq = nullptr;   // completions for the interrupt callbacks, as soon as they are final
   void* side_res = nullptr;   // overlapped resolves: piece sums and resolve beside the earlier batches' DMA writes
+  void* side_stage = nullptr; // host-image TX staging, apart from the descriptor uploads (see stage_stream)
   // the job thread's record of the two batches before the current one (their
   // DMA writes may still run): the bytes each can write, [0, ~0) unknown
   struct WriteBox {
@@ -1389,7 +1401,8 @@ struct BatchedQueuePair::Scratch {
     if (side_wb) (void) nicgpu_stream_destroy(side_wb);
     if (side_irq) (void) nicgpu_stream_destroy(side_irq);
     if (side_res) (void) nicgpu_stream_destroy(side_res);
-    side_up = side_down = side_plan = side_wb = side_irq = side_res = nullptr;
+    if (side_stage) (void) nicgpu_stream_destroy(side_stage);
+    side_up = side_down = side_plan = side_wb = side_irq = side_res = side_stage = nullptr;
     if (img.use_count() == 1) img->release();  // a manager's shared image is released by its last stage
     device = -1;
   }
@@ -1406,6 +1419,7 @@ struct BatchedQueuePair::Scratch {
     check(nicgpu_stream_create(&side_wb), "nicgpu_stream_create");
     check(nicgpu_stream_create(&side_irq), "nicgpu_stream_create");
     check(nicgpu_stream_create_priority(&side_res, 0), "nicgpu_stream_create_priority");  // high: beside a DMA write
+    check(nicgpu_stream_create(&side_stage), "nicgpu_stream_create");
     for (Slot& sl : slot) sl.create(dev);
     device = dev;
   }
@@ -1808,7 +1822,7 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
   // unless they overlap bytes an earlier pending batch delivers: then its job
   // stages them after that batch's write-back (recorded by the earlier job)
   sl.stage_deferred = img && !sl.dep_stage.empty();
-  if (img && !sl.stage_deferred) image_stage(sl, tx.size(), tx.data(), device ? sl.v.tx : nullptr, S.side_up);
+  if (img && !sl.stage_deferred) image_stage(sl, tx.size(), tx.data(), device ? sl.v.tx : nullptr, stage_stream());
   sl.job_done = std::promise<void>();
   sl.job = sl.job_done.get_future();
   auto run = [this, &sl, device, dev] {
@@ -1817,9 +1831,8 @@ void BatchedQueuePair::enqueue(const DeviceHostMemory& mem, std::span<const TxDe
       int disjoint = -1;
       double check_us = 0;
       if (sl.stage_deferred) {
-        for (Slot* p : sl.dep_stage)
-          check(nicgpu_stream_wait_event(scratch_->side_up, p->ev_wb), "nicgpu_stream_wait_event");
-        image_stage(sl, sl.tx.size(), sl.tx.data(), device ? sl.v.tx : nullptr, scratch_->side_up);
+        for (Slot* p : sl.dep_stage) check(nicgpu_stream_wait_event(stage_stream(), p->ev_wb), "nicgpu_stream_wait_event");
+        image_stage(sl, sl.tx.size(), sl.tx.data(), device ? sl.v.tx : nullptr, stage_stream());
       }
       if (device) {
         sl.on_device = front(sl, sl.mem, sl.tx, sl.rx, sl.stats, sl.result, sl.stream, disjoint, check_us);
@@ -2581,6 +2594,10 @@ void BatchedQueuePair::image_prepare(Slot& sl, HostImage& img, std::span<const T
   }
 }
 
+void* BatchedQueuePair::stage_stream() const {
+  return stage_stream_env() ? scratch_->side_stage : scratch_->side_up;
+}
+
 // The TX bytes into the mirror on `stream`: one copy of the span when dense
 // (the registered window goes up by DMA at the link's rate), else the gather
 // kernel over the TX descriptors (tx_dev: the batch's descriptors on the
@@ -2588,11 +2605,14 @@ void BatchedQueuePair::image_prepare(Slot& sl, HostImage& img, std::span<const T
 void BatchedQueuePair::image_stage(Slot& sl, std::size_t ntx, const TxDescriptor* tx_host, const void* tx_dev,
                                    void* stream) {
   HostImage& I = *sl.image;
+  Scratch& S = *scratch_;
   if (sl.tx_hi > sl.tx_lo) {
     auto* mirror = static_cast<std::uint8_t*>(I.mirror[sl.mirror].p);
     if (sl.whole) {
       check(nicgpu_memcpy_async(mirror + sl.tx_lo, I.host + sl.tx_lo, sl.tx_hi - sl.tx_lo, stream), "nicgpu_memcpy_async");
     } else {
+      // descriptors uploaded on side_up (ev_tx) unless uploaded here
+      if (tx_dev && stream != S.side_up) check(nicgpu_stream_wait_event(stream, sl.ev_tx), "nicgpu_stream_wait_event");
       if (!tx_dev) {
         tx_dev = sl.stage_tx.get(ntx * sizeof(TxDescriptor));
         check(nicgpu_memcpy_async(const_cast<void*>(tx_dev), tx_host, ntx * sizeof(TxDescriptor), stream),
@@ -2679,7 +2699,7 @@ void BatchedQueuePair::process_batch(HostMemory& m, std::span<const TxDescriptor
   try {
     if (!checked && config_.device_resolve && device_fits(tx.size(), rx.size())) {
       upload(sl, tx, rx, true);
-      image_stage(sl, tx.size(), tx.data(), sl.v.tx, S.side_up);
+      image_stage(sl, tx.size(), tx.data(), sl.v.tx, stage_stream());
       on_device = front(sl, mem, tx, rx, st, out, stream, disjoint, check_us);
       if (on_device) {
         back(sl, mem, out, stream);
@@ -2908,7 +2928,7 @@ bool BatchedQueuePair::process_queues(const DeviceHostMemory& mem_in, HostImage*
     sl.rx_lo = rhi > rlo ? rlo : 0;
     sl.rx_hi = rhi > rlo ? rhi : 0;
     sl.whole = sl.tx_hi > sl.tx_lo && sl.tx_hi - sl.tx_lo <= bytes + bytes / 2 + (std::uint64_t{1} << 16);
-    image_stage(sl, ntx, nullptr, v.tx, S.side_up);
+    image_stage(sl, ntx, nullptr, v.tx, stage_stream());
   }
   cat.timings.copy_us += std::chrono::duration<double, std::micro>(clock::now() - t0).count();
   check(nicgpu_qp_set_segments(sl.qp, seg.data(), Q, ntx, S.side_plan), "nicgpu_qp_set_segments");
