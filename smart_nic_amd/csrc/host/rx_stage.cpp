@@ -974,6 +974,17 @@ bool stage_stream_env() {
   return on;
 }
 
+// NIC_STAGE_GATHER=1: TX bytes staged by the gather kernel over the mapped
+// window even when one copy of their span would do (tuning A/B: the copy
+// engines then carry only the descriptors and the results)
+bool stage_gather_env() {
+  static const bool on = [] {
+    const char* e = std::getenv("NIC_STAGE_GATHER");
+    return e && std::strcmp(e, "1") == 0;
+  }();
+  return on;
+}
+
 // HostMemory mirrors in HBM for pipelined batches: 2, or NIC_IMAGE_MIRRORS=1
 // (tuning A/B)
 unsigned image_mirrors_env() {
@@ -2582,7 +2593,8 @@ void BatchedQueuePair::image_prepare(Slot& sl, HostImage& img, std::span<const T
   sl.tx_bytes = T.bytes;
   sl.rx_lo = R.hi > R.lo ? R.lo : 0;
   sl.rx_hi = R.hi > R.lo ? R.hi : 0;
-  sl.whole = sl.tx_hi > sl.tx_lo && sl.tx_hi - sl.tx_lo <= T.bytes + T.bytes / 2 + (std::uint64_t{1} << 16);
+  sl.whole = sl.tx_hi > sl.tx_lo && sl.tx_hi - sl.tx_lo <= T.bytes + T.bytes / 2 + (std::uint64_t{1} << 16) &&
+             !stage_gather_env();
   sl.dep_stage.clear();
   sl.dep_rx.clear();
   for (unsigned k = 0; k < S.pending; ++k) {
