@@ -963,6 +963,16 @@ bool defer_env() {
   return on;
 }
 
+// NIC_CHECK_EARLY=1: the single-batch overlap check launched before the
+// resolve on a normal-priority stream of its own (tuning A/B)
+bool check_early_env() {
+  static const bool on = [] {
+    const char* e = std::getenv("NIC_CHECK_EARLY");
+    return e && std::strcmp(e, "1") == 0;
+  }();
+  return on;
+}
+
 // Host-image TX staging on its own stream (measured, profiles/r06_hostmem_ab.txt:
 // behind the descriptor uploads on side_up, each batch's span copy started
 // 1-2 ms late), or NIC_STAGE_STREAM=0: on side_up (tuning A/B)
@@ -1389,6 +1399,7 @@ struct BatchedQueuePair::Scratch {
   void* side_irq = nullptr;   // completions for the interrupt callbacks, as soon as they are final
   void* side_res = nullptr;   // overlapped resolves: piece sums and resolve beside the earlier batches' DMA writes
   void* side_stage = nullptr; // host-image TX staging, apart from the descriptor uploads (see stage_stream)
+  void* side_chk = nullptr;   // the overlap check launched early (check_early_env), at normal priority
   // the job thread's record of the two batches before the current one (their
   // DMA writes may still run): the bytes each can write, [0, ~0) unknown
   struct WriteBox {
@@ -1413,7 +1424,8 @@ struct BatchedQueuePair::Scratch {
     if (side_irq) (void) nicgpu_stream_destroy(side_irq);
     if (side_res) (void) nicgpu_stream_destroy(side_res);
     if (side_stage) (void) nicgpu_stream_destroy(side_stage);
-    side_up = side_down = side_plan = side_wb = side_irq = side_res = side_stage = nullptr;
+    if (side_chk) (void) nicgpu_stream_destroy(side_chk);
+    side_up = side_down = side_plan = side_wb = side_irq = side_res = side_stage = side_chk = nullptr;
     if (img.use_count() == 1) img->release();  // a manager's shared image is released by its last stage
     device = -1;
   }
@@ -1431,6 +1443,7 @@ struct BatchedQueuePair::Scratch {
     check(nicgpu_stream_create(&side_irq), "nicgpu_stream_create");
     check(nicgpu_stream_create_priority(&side_res, 0), "nicgpu_stream_create_priority");  // high: beside a DMA write
     check(nicgpu_stream_create(&side_stage), "nicgpu_stream_create");
+    check(nicgpu_stream_create(&side_chk), "nicgpu_stream_create");
     for (Slot& sl : slot) sl.create(dev);
     device = dev;
   }
@@ -2090,6 +2103,19 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
     if (side) check(nicgpu_stream_wait_event(rs, sl.ev_rx), "nicgpu_stream_wait_event");
   }
   out.timings.copy_us += us_since(t);
+  // (NIC_CHECK_EARLY=1) the overlap check on its own normal-priority stream as
+  // soon as the descriptors are in place — beside the earlier batch's
+  // delivery — instead of behind the plan on the least-priority stream, where
+  // it waits for wave slots until the resolve is over
+  const bool early = side && check_early_env();
+  if (early) {
+    if (dev_desc) check(nicgpu_stream_wait_event(S.side_chk, sl.ev_submit), "nicgpu_stream_wait_event");
+    else {
+      check(nicgpu_stream_wait_event(S.side_chk, sl.ev_tx), "nicgpu_stream_wait_event");
+      check(nicgpu_stream_wait_event(S.side_chk, sl.ev_rx), "nicgpu_stream_wait_event");
+    }
+    check(nicgpu_qp_check_async(sl.qp, mem.size, ntx, nrx, 0u, S.side_chk), "nicgpu_qp_check_async");
+  }
   // the speculative resolve goes in behind the piece sums before the overlap
   // check's verdict (it writes only the context's completions and writes),
   // so the stream does not wait for this thread's round trip on the check.
@@ -2107,7 +2133,8 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
   // The check synchronises `ps`: the descriptors are then in place for `stream`.
   t = clock::now();
   int verdict = -1;
-  check(nicgpu_qp_check(sl.qp, mem.size, ntx, nrx, &verdict, ps), "nicgpu_qp_check");
+  if (early) check(nicgpu_qp_check_wait(sl.qp, &verdict), "nicgpu_qp_check_wait");
+  else check(nicgpu_qp_check(sl.qp, mem.size, ntx, nrx, &verdict, ps), "nicgpu_qp_check");
   const bool ascending = verdict >= 0;  // the device decided: RX spans in address order
   if (verdict < 0) {
     const auto [htx, hrx] = host_spans(sl, tx, rx, stream);
