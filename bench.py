@@ -282,6 +282,9 @@ def gpu_rows():
                  # the reference's HostMemory interface: TX bytes staged into an HBM
                  # mirror, delivered bytes written back over PCIe (FlatHostMemory)
                  ["c3", "1048576", "8", "0", "device", "hostmem", "pipelined"],
+                 # the same with the results kept in HBM (no 38 MB of pageable result
+                 # downloads sharing the link with the write-backs: profiles/r06_hostmem_ab.txt)
+                 ["c3", "1048576", "8", "0", "device", "hostmem", "pipelined", "device"],
                  # nic::BatchedQueueManager: 16 queue pairs x 64 K C3 descriptors, one
                  # drain as one fused device batch; host, HBM and HostMemory descriptors
                  ["qm16", "1048576", "6", "0", "device", "pinned", "sync", "device"],

@@ -987,37 +987,6 @@ bool stage_stream_env() {
   return on;
 }
 
-// NIC_RESULT_LANDING=1: host results written by a copy kernel into page-locked
-// landing space through its mapping, then copied into the result's vectors by
-// the download worker; default: downloaded straight into the vectors (tuning A/B)
-bool landing_env() {
-  static const bool on = [] {
-    const char* e = std::getenv("NIC_RESULT_LANDING");
-    return e && std::strcmp(e, "1") == 0;
-  }();
-  return on;
-}
-
-// dst <- src for each part, the bytes split over up to 4 threads
-struct Span {
-  void* dst;
-  const void* src;
-  std::size_t bytes;
-};
-void copy_spans(const Span (&parts)[4]) {
-  std::size_t total = 0;
-  for (const Span& p : parts) total += p.bytes;
-  const rx_stage_detail::Chunks ch(total, 4, std::size_t{1} << 22);
-  ch.run([&](std::size_t, std::size_t b, std::size_t e) {
-    std::size_t at = 0;
-    for (const Span& p : parts) {
-      const std::size_t lo = std::max(b, at), hi = std::min(e, at + p.bytes);
-      if (hi > lo) std::memcpy(static_cast<char*>(p.dst) + (lo - at), static_cast<const char*>(p.src) + (lo - at), hi - lo);
-      at += p.bytes;
-    }
-  });
-}
-
 // HostMemory mirrors in HBM for pipelined batches: 2, or NIC_IMAGE_MIRRORS=1
 // (tuning A/B)
 unsigned image_mirrors_env() {
@@ -1320,10 +1289,6 @@ struct BatchedQueuePair::Slot {
   static constexpr int kIrqChunks = 16;
   void* ev_irq[2][kIrqChunks] = {};
   HostBuf h_itx, h_irx;
-  // results on the host: completions, hashes and queues land here first
-  // (page-locked: a DMA at the link's rate, no staged copy holding the
-  // runtime) and are copied into the result's vectors by the download worker
-  HostBuf h_rtx, h_rrx, h_rhash, h_rqueue;
   bool irq_pending = false;
   std::size_t irq_ntx = 0, irq_nrx = 0;
   // deferred RX verify (nicgpu_qp_set_deferred_verify): the batch's completions
@@ -2395,48 +2360,18 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
     sl.irq_pending = true;
   };
   if (irq_down && !sl.late) irq_download(sl.ev_resolved);
-  // host results: page-locked landing space (NIC_RESULT_LANDING=0: straight
-  // into the vectors, tuning A/B)
-  struct Landing {
-    CompletionEntry *tx = nullptr, *rx = nullptr;
-    std::uint32_t* hash = nullptr;
-    std::uint16_t* queue = nullptr;
-  } land;
-  if (!keep && landing_env()) {
-    land.tx = sl.h_rtx.get<CompletionEntry>(std::max<std::size_t>(ntx, 1));
-    land.rx = sl.h_rrx.get<CompletionEntry>(std::max<std::size_t>(nrx_total, 1));
-    if (rss) {
-      land.hash = sl.h_rhash.get<std::uint32_t>(std::max<std::size_t>(nrx_total, 1));
-      land.queue = sl.h_rqueue.get<std::uint16_t>(std::max<std::size_t>(nrx_total, 1));
-    }
-  }
   sl.down.emplace(sl.worker);
   // the dispatch lists are made here too, on the download stream: they read
   // this slot's buffers only, so the next batch's piece sums need not queue
   // behind them on `stream`
-  sl.down->start([&sl, &S, &out, &v, ntx, nrx_total, tn, nq, rss, keep, hits, rss_ready, land](SideJob& j) {
+  sl.down->start([&sl, &S, &out, &v, ntx, nrx_total, tn, nq, rss, keep, hits, rss_ready](SideJob& j) {
     bool ok = j.ok(nicgpu_set_device(S.device), "nicgpu_set_device") &&
               j.ok(nicgpu_stream_wait_event(S.side_down, sl.ev_resolved), "nicgpu_stream_wait_event");
     auto completions_down = [&] {
-      if (land.tx) {  // one copy kernel writing the landing space through its mapping
-        const nicgpu_copy_range r[2] = {{land.tx, v.txc, ntx * sizeof(CompletionEntry)},
-                                        {land.rx, v.rxc, nrx_total * sizeof(CompletionEntry)}};
-        ok = j.ok(nicgpu_memcpy_batch(r, 2, S.side_down), "nicgpu_memcpy_batch");
-        return;
-      }
       ok = j.ok(nicgpu_memcpy_async(out.tx_completions.data(), v.txc, ntx * sizeof(CompletionEntry), S.side_down),
                 "nicgpu_memcpy_async") &&
            j.ok(nicgpu_memcpy_async(out.rx_completions.data(), v.rxc, nrx_total * sizeof(CompletionEntry), S.side_down),
                 "nicgpu_memcpy_async");
-    };
-    // hashes and queues: into the landing space by the copy kernel too
-    auto hash_down = [&] {
-      if (land.hash) {
-        const nicgpu_copy_range r[2] = {{land.hash, v.rx_hash, nrx_total * 4}, {land.queue, v.rx_queue, nrx_total * 2}};
-        return j.ok(nicgpu_memcpy_batch(r, 2, S.side_down), "nicgpu_memcpy_batch");
-      }
-      return j.ok(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, S.side_down), "nicgpu_memcpy_async") &&
-             j.ok(nicgpu_memcpy_async(out.rx_queue.data(), v.rx_queue, nrx_total * 2, S.side_down), "nicgpu_memcpy_async");
     };
     if (ok && !keep && !sl.late) completions_down();
     rss_ready.wait();
@@ -2477,18 +2412,12 @@ void BatchedQueuePair::back(Slot& sl, const DeviceHostMemory& mem, RxBatchResult
       ok = j.ok(nicgpu_memcpy_async(sl.qs, v.queue_start, nq * 4, S.side_down), "nicgpu_memcpy_async") &&
            j.ok(nicgpu_memcpy_async(sl.qe, v.queue_end, nq * 4, S.side_down), "nicgpu_memcpy_async");
     if (ok && rss && !keep)
-      ok = hash_down() &&
+      ok = j.ok(nicgpu_memcpy_async(out.rx_hash.data(), v.rx_hash, nrx_total * 4, S.side_down), "nicgpu_memcpy_async") &&
+           j.ok(nicgpu_memcpy_async(out.rx_queue.data(), v.rx_queue, nrx_total * 2, S.side_down), "nicgpu_memcpy_async") &&
            j.ok(nicgpu_stream_synchronize(S.side_down), "nicgpu_stream_synchronize") &&
            j.ok(nicgpu_memcpy_async(sl.which, v.queue_which, sl.meta[0] * 4, S.side_down), "nicgpu_memcpy_async");
     // (with the results kept on the device this is where the batch is known done)
     ok = ok && j.ok(nicgpu_stream_synchronize(S.side_down), "nicgpu_stream_synchronize");
-    if (ok && land.tx) {  // landed: into the result's vectors, a few threads
-      const Span parts[4] = {{out.tx_completions.data(), land.tx, ntx * sizeof(CompletionEntry)},
-                             {out.rx_completions.data(), land.rx, nrx_total * sizeof(CompletionEntry)},
-                             {land.hash ? out.rx_hash.data() : nullptr, land.hash, land.hash ? nrx_total * 4 : 0},
-                             {land.queue ? out.rx_queue.data() : nullptr, land.queue, land.queue ? nrx_total * 2 : 0}};
-      copy_spans(parts);
-    }
   });
   try {
     out.timings.copy_us += us_since(t);
