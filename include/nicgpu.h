@@ -382,19 +382,6 @@ int nicgpu_qp_check_flags(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nr
  * The check may then run beside the plan and the speculative resolve. */
 int nicgpu_qp_check_async(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t nrx, unsigned flags, void* stream);
 int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict);
-/* A delivery that need not wait for the host to read the check's verdict:
- * enqueues on `stream`, after the pending check (nicgpu_qp_check_async) and
- * the pending resolve (nicgpu_qp_resolve_start, unsegmented), a one-wave
- * kernel that leaves the resolve's settled prefix for
- * nicgpu_qp_deliver_range(NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_GATED) when
- * the check's simple form finds the buffers disjoint and the ring ascending,
- * and 0 otherwise (that delivery then writes nothing, and its counts and hits
- * are those of an empty range).  After nicgpu_qp_check_wait,
- * nicgpu_qp_gate_passed says which: a verdict of 1 with *passed == 0 (the
- * check needed its scan form) means the settled prefix is still to be
- * delivered, without GATED. */
-int nicgpu_qp_gate_settled(nicgpu_qp* q, void* stream);
-int nicgpu_qp_gate_passed(const nicgpu_qp* q, int* passed);
 /* After an unsegmented check: bounds[0..1] = [min start, max end) of the TX
  * spans; when the verdict was 0 or 1 (the RX spans ascend) bounds[2..3] =
  * [least start, max end) of the RX spans, all bytes the batch's DMA writes can
@@ -546,7 +533,6 @@ int nicgpu_qp_deliver(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_t nrx,
 #define NICGPU_DELIVER_SETTLED 1u /* end at the settled prefix of the pending nicgpu_qp_resolve_start */
 #define NICGPU_DELIVER_APPEND 2u  /* add to *view.rss_count instead of resetting it (a later range) */
 #define NICGPU_DELIVER_RESET_HITS 4u /* set hits_dev to this range's hits instead of adding (no memset first) */
-#define NICGPU_DELIVER_GATED 8u      /* with SETTLED: end at the prefix nicgpu_qp_gate_settled left (0 unless disjoint) */
 /* nicgpu_qp_deliver over completions [rx_begin, rx_end) (bounded on the device
  * with NICGPU_DELIVER_SETTLED).  Ranges of one batch may be delivered in any
  * order when the batch's buffers are disjoint (nicgpu_qp_check verdict 1): the

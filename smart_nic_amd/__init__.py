@@ -110,8 +110,6 @@ ABI_SYMBOLS = (
     "nicgpu_qp_walks",
     "nicgpu_qp_check_async",
     "nicgpu_qp_check_wait",
-    "nicgpu_qp_gate_settled",
-    "nicgpu_qp_gate_passed",
     "nicgpu_qp_check_bounds",
     "nicgpu_qp_resum",
     "nicgpu_qp_set_deferred_verify",
@@ -216,8 +214,6 @@ def signatures() -> dict:
         "nicgpu_qp_walks": (i32, [vp, vp]),
         "nicgpu_qp_check_async": (i32, [vp, ctypes.c_uint64, sz, sz, ctypes.c_uint, vp]),
         "nicgpu_qp_check_wait": (i32, [vp, vp]),
-        "nicgpu_qp_gate_settled": (i32, [vp, vp]),
-        "nicgpu_qp_gate_passed": (i32, [vp, vp]),
         "nicgpu_qp_check_bounds": (i32, [vp, vp]),
         "nicgpu_qp_resum": (i32, [vp, vp, ctypes.c_uint64, vp]),
         "nicgpu_qp_set_deferred_verify": (i32, [vp, i32]),

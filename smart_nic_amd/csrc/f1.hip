@@ -1406,17 +1406,6 @@ __global__ __launch_bounds__(kQpBlock) void qp_full_kernel(QpCtx C, const uint32
 // the packets before the first mismatch, [0, pos[first]), or all `used` when
 // nothing differed.  nicgpu_qp_deliver_range(NICGPU_DELIVER_SETTLED) reads it
 // on the device, so the DMA writes start before the host has seen the resolve.
-// nicgpu_qp_gate_settled: the settled prefix a gated delivery ends at —
-// the resolve's (settled[0]) when the pending check's simple form found the
-// buffers disjoint and the ring ascending (no flag of its generation set),
-// else 0 (the delivery then writes nothing and the host decides).
-__global__ void qp_gate_kernel(unsigned long long* bounds, unsigned long long gen, const uint64_t* settled) {
-  if (threadIdx.x == 0) {
-    const bool ok = bounds[4] != gen && bounds[5] != gen && bounds[6] != gen;
-    bounds[7] = ok ? (unsigned long long) settled[0] : 0ull;
-  }
-}
-
 constexpr unsigned kQpReduceThreads = 1024;
 __global__ __launch_bounds__(kQpReduceThreads) void qp_reduce_kernel(const uint64_t* __restrict__ partials,
                                                                      unsigned nblocks, const uint32_t* __restrict__ pos,
@@ -1941,8 +1930,6 @@ struct nicgpu_qp {
     hipStream_t s = nullptr;
   } chk_args;
   uint64_t checks_scanned = 0;    // checks that needed the scan form (an RX span receiving nothing)
-  bool simple_ok = false;         // the last waited check's simple form said disjoint (nicgpu_qp_gate_passed)
-  bool gate_on = false;           // nicgpu_qp_gate_settled enqueued for the pending resolve
   // the resolve between nicgpu_qp_resolve_start and _finish
   struct Pending {
     bool on = false;
@@ -2367,8 +2354,6 @@ int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict) {
   DeviceGuard g(q->device);
   int st = hip_status(hipEventSynchronize(q->checked));
   if (st != NICGPU_OK) return st;
-  // what a delivery gated on this check saw (nicgpu_qp_gate_settled)
-  q->simple_ok = q->hp_chk[4] != q->chk_gen && q->hp_chk[5] != q->chk_gen && q->hp_chk[6] != q->chk_gen;
   if (q->hp_chk[4] == q->chk_gen) {  // a span that receives nothing: the scan form
     const nicgpu_qp::CheckArgs& A = q->chk_args;
     const unsigned long long gen = ++q->gen;
@@ -2380,25 +2365,6 @@ int nicgpu_qp_check_wait(nicgpu_qp* q, int* verdict) {
   }
   const uint64_t* f = q->hp_chk + 5;
   *verdict = f[0] == q->chk_gen ? -1 : (f[1] == q->chk_gen ? 0 : 1);
-  return NICGPU_OK;
-}
-
-int nicgpu_qp_gate_settled(nicgpu_qp* q, void* stream) {
-  if (!q || !q->chk_on || !q->res.on || q->nseg) return NICGPU_ERR_INVALID;
-  DeviceGuard g(q->device);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  int st = hip_status(hipStreamWaitEvent(s, q->checked, 0));
-  if (st != NICGPU_OK) return st;
-  hipLaunchKernelGGL(qp_gate_kernel, dim3(1), dim3(kWave), 0, s, q->bounds, q->chk_gen,
-                     q->partials + (size_t) q->res.grid * kQpStats + 2);
-  st = hip_status(hipGetLastError());
-  q->gate_on = st == NICGPU_OK;
-  return st;
-}
-
-int nicgpu_qp_gate_passed(const nicgpu_qp* q, int* passed) {
-  if (!q || !passed || q->chk_on) return NICGPU_ERR_INVALID;
-  *passed = q->simple_ok ? 1 : 0;
   return NICGPU_OK;
 }
 
@@ -2429,7 +2395,6 @@ int nicgpu_qp_resolve_start(nicgpu_qp* q, uint64_t mem_size, size_t ntx, size_t 
   DeviceGuard g(q->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   q->res = nicgpu_qp::Pending{};
-  q->gate_on = false;
   if (q->nseg && (ntx != q->seg_ntx || nrx != q->seg_nrx)) return NICGPU_ERR_INVALID;
   QpCtx C{queue_id, max_mtu, mem_size, q->plans, q->piece_csum, q->piece_cs4, q->tx, q->rx, (uint64_t) nrx};
   const QpSegs S = qp_segs(q);
@@ -2677,10 +2642,8 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
                             unsigned flags, const nicgpu_rss_ctx* ctx, int tuple_mode, uint32_t raw_off,
                             uint32_t raw_len, uint64_t* hits_dev, void* stream) {
   if (!q || rx_end > q->cap_rx || rx_begin > rx_end) return NICGPU_ERR_INVALID;
-  if (flags & ~(unsigned) (NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_APPEND | NICGPU_DELIVER_RESET_HITS |
-                           NICGPU_DELIVER_GATED))
+  if (flags & ~(unsigned) (NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_APPEND | NICGPU_DELIVER_RESET_HITS))
     return NICGPU_ERR_INVALID;
-  if ((flags & NICGPU_DELIVER_GATED) && (!(flags & NICGPU_DELIVER_SETTLED) || !q->gate_on)) return NICGPU_ERR_INVALID;
   // the settled prefix of the resolve started last (its grid places the tail)
   if ((flags & NICGPU_DELIVER_SETTLED) && !q->res.on) return NICGPU_ERR_INVALID;
   if (mem_size && (!mem || (reinterpret_cast<uintptr_t>(mem) & 15u) != 0)) return NICGPU_ERR_INVALID;
@@ -2722,9 +2685,7 @@ int nicgpu_qp_deliver_range(nicgpu_qp* q, uint8_t* mem, uint64_t mem_size, size_
   P.j0 = rx_begin;
   P.n = rx_end;
   if (flags & NICGPU_DELIVER_SETTLED)
-    P.n_dev = (flags & NICGPU_DELIVER_GATED)
-                  ? q->bounds + 7
-                  : reinterpret_cast<const unsigned long long*>(q->partials + (size_t) q->res.grid * kQpStats + 2);
+    P.n_dev = reinterpret_cast<const unsigned long long*>(q->partials + (size_t) q->res.grid * kQpStats + 2);
   P.rss.mode = tuple_mode;
   P.rss.raw_off = raw_off;
   P.rss.raw_len = raw_len;

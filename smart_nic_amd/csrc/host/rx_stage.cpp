@@ -963,17 +963,6 @@ bool defer_env() {
   return on;
 }
 
-// A batch whose overlap check runs behind the plan delivers its settled prefix
-// gated on the check's device flags (nicgpu_qp_gate_settled), or
-// NIC_DLV_GATE=0: after this thread read the verdict (tuning A/B)
-bool gate_env() {
-  static const bool on = [] {
-    const char* e = std::getenv("NIC_DLV_GATE");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  return on;
-}
-
 // The overlap check of a batch with no other in flight launched before the
 // resolve on a normal-priority stream of its own (measured: one at a time
 // 421-427 -> 413-415 us; with batches pending it only competes with the
@@ -2131,46 +2120,12 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
         "nicgpu_qp_resolve_start");
   check(nicgpu_event_record(sl.ev_resolved, rs), "nicgpu_event_record");  // final unless relaxed / tail below
   out.timings.resolve_us += us_since(t);
-  // the DMA writes and RSS of the completions the resolve settles (bounded on
-  // the device) go in at once: the host waits for the resolve while they are
-  // already queued, so the stream does not idle on this thread's round trip
-  sl.tn = sl.nq = 0;
-  const nicgpu_rss_ctx* rctx = nullptr;
-  std::uint64_t* hits = nullptr;
-  auto deliver_settled = [&](unsigned gate) {
-    t = clock::now();
-    if (config_.rss != nullptr && rctx == nullptr) {
-      if (config_.tuple.mode == TupleMode::None)
-        throw GpuError("process_batch: TupleMode::None cannot produce hashes", NICGPU_ERR_INVALID);
-      const auto& table = config_.rss->config().table;
-      sl.tn = table.size();
-      for (const std::uint16_t q : table) sl.nq = std::max<std::size_t>(sl.nq, std::size_t{q} + 1);
-      rctx = config_.rss->device_context(stream);
-      hits = static_cast<std::uint64_t*>(sl.hits.get(std::max<std::size_t>(sl.tn, 1) * sizeof(std::uint64_t)));
-    }
-    // host image: the delivery rewrites RX bytes an earlier pending batch may
-    // still be writing back from the mirror
-    for (Slot* p : sl.dep_rx) check(nicgpu_stream_wait_event(stream, p->ev_wb), "nicgpu_stream_wait_event");
-    if (gate) check(nicgpu_qp_gate_settled(sl.qp, stream), "nicgpu_qp_gate_settled");
-    deliver(sl, mem, 0, nrx, NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_RESET_HITS | gate, rctx, hits,
-            stream);  // hits set, not added
-    out.timings.gather_us += us_since(t);
-  };
   // overlapping buffers go to the host path before anything is written; a
   // ring whose RX buffers are not in ascending address order is sorted there.
   // The check synchronises `ps`: the descriptors are then in place for `stream`.
-  // Gated (a batch whose check runs behind the plan, NIC_DLV_GATE=0 to turn
-  // off): the settled prefix is delivered behind the check on the device,
-  // empty unless the check's simple form found the batch disjoint, so the
-  // stream does not wait for this thread to read the verdict.
-  const bool gated = side && !ov && !early && gate_env();
-  if (gated) {
-    check(nicgpu_qp_check_async(sl.qp, mem.size, ntx, nrx, 0u, ps), "nicgpu_qp_check_async");
-    deliver_settled(NICGPU_DELIVER_GATED);
-  }
   t = clock::now();
   int verdict = -1;
-  if (early || gated) check(nicgpu_qp_check_wait(sl.qp, &verdict), "nicgpu_qp_check_wait");
+  if (early) check(nicgpu_qp_check_wait(sl.qp, &verdict), "nicgpu_qp_check_wait");
   else check(nicgpu_qp_check(sl.qp, mem.size, ntx, nrx, &verdict, ps), "nicgpu_qp_check");
   const bool ascending = verdict >= 0;  // the device decided: RX spans in address order
   if (verdict < 0) {
@@ -2211,11 +2166,29 @@ bool BatchedQueuePair::front_once(Slot& sl, const DeviceHostMemory& mem, std::sp
       check(nicgpu_stream_wait_event(stream, sl.ev_resolved), "nicgpu_stream_wait_event");
     }
   }
-  // gated: delivered already unless the check needed its scan form (or the
-  // host found an unsorted ring disjoint)
-  int passed = 0;
-  if (gated) check(nicgpu_qp_gate_passed(sl.qp, &passed), "nicgpu_qp_gate_passed");
-  if (!passed) deliver_settled(0u);
+  t = clock::now();
+  // the DMA writes and RSS of the completions the resolve settles (bounded on
+  // the device) go in at once: the host waits for the resolve while they are
+  // already queued, so the stream does not idle on this thread's round trip
+  sl.tn = sl.nq = 0;
+  const nicgpu_rss_ctx* rctx = nullptr;
+  std::uint64_t* hits = nullptr;
+  if (config_.rss != nullptr) {
+    if (config_.tuple.mode == TupleMode::None)
+      throw GpuError("process_batch: TupleMode::None cannot produce hashes", NICGPU_ERR_INVALID);
+    const auto& table = config_.rss->config().table;
+    sl.tn = table.size();
+    for (const std::uint16_t q : table) sl.nq = std::max<std::size_t>(sl.nq, std::size_t{q} + 1);
+    rctx = config_.rss->device_context(stream);
+    hits = static_cast<std::uint64_t*>(sl.hits.get(std::max<std::size_t>(sl.tn, 1) * sizeof(std::uint64_t)));
+  }
+  out.timings.resolve_us += us_since(t);
+  t = clock::now();
+  // host image: the delivery rewrites RX bytes an earlier pending batch may
+  // still be writing back from the mirror
+  for (Slot* p : sl.dep_rx) check(nicgpu_stream_wait_event(stream, p->ev_wb), "nicgpu_stream_wait_event");
+  deliver(sl, mem, 0, nrx, NICGPU_DELIVER_SETTLED | NICGPU_DELIVER_RESET_HITS, rctx, hits, stream);  // hits set, not added
+  out.timings.gather_us += us_since(t);
   t = clock::now();
   std::uint64_t done = 0, used = 0, settled = 0;
   nicgpu_qp_stats ds{};
