@@ -297,29 +297,30 @@ constexpr uint32_t kSegStageChunks = (uint32_t) kTsoSteps * kWave;
 constexpr uint32_t kSegStage = kSegStageChunks * 16u;  // 9216 B
 
 
-// One dword of a segment at absolute address A (4-aligned), any overlap with
-// the segment: bytes from the prefix / part A / part B, byte stores at the
-// segment's ends.  Returns its halfword sum (absolute positions).
-__device__ __forceinline__ uint32_t seg_dword_bytes(uint8_t* out, uint64_t A, uint64_t dst, int sz, int pa, int pb,
-                                                    uint32_t tag, const uint8_t* st_b, uint32_t a, uint32_t b) {
-  const int r0 = (int) ((int64_t) A - (int64_t) dst);
-  uint32_t o = 0, keep = 0;
+// One dword of a segment at offset r0 from its start (4-aligned in memory),
+// any overlap with the segment: bytes from the prefix / part A / part B,
+// chosen with selects from unconditional LDS byte reads, and stored through a
+// buffer resource over the segment's own bytes (`seg` = out + dst,
+// num_records = size), so a byte outside the segment — or every byte of a
+// lane with no edge dword (`on` false) — is an out-of-range store the
+// hardware drops.  Returns its halfword sum (absolute positions).  (Round 5's
+// form branched per byte: most of the kernel's scalar instructions,
+// profiles/r06_tso_pmc.json.)
+__device__ __forceinline__ uint32_t seg_dword_select(__amdgpu_buffer_rsrc_t seg, bool on, int r0, int sz, int pa, int pb,
+                                                     uint32_t tag, const uint8_t* st_b, uint32_t a, uint32_t b) {
+  // the prefix (81 00 tag-hi tag-lo) as a little-endian dword: byte r of it
+  const uint32_t pfx = 0x81u | (((tag >> 8) & 0xFFu) << 16) | ((tag & 0xFFu) << 24);
+  uint32_t o = 0;
+#pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int r = r0 + q;
-    if (r < 0 || r >= sz) continue;
-    uint32_t val;
-    if (r < pa) val = r == 0 ? 0x81u : (r == 1 ? 0u : (r == 2 ? (tag >> 8) & 0xFFu : tag & 0xFFu));
-    else if (r < pb) val = st_b[a + (uint32_t) (r - pa)];
-    else val = st_b[b + (uint32_t) (r - pb)];
-    o |= val << (8 * q);
-    keep |= 0xFFu << (8 * q);
-  }
-  uint8_t* p = out + A;
-  if (keep == 0xFFFFFFFFu) {
-    *reinterpret_cast<uint32_t*>(p) = o;
-  } else {
-    for (int q = 0; q < 4; ++q)
-      if ((keep >> (8 * q)) & 0xFFu) p[q] = (uint8_t) (o >> (8 * q));
+    const bool in = on && r >= 0 && r < sz;
+    const uint32_t idx = r >= pb ? b + (uint32_t) (r - pb) : a + (uint32_t) (r - pa);
+    const uint32_t lb = st_b[in && r >= pa ? idx : 0u];
+    const uint32_t pv = (pfx >> (8u * ((uint32_t) r & 3u))) & 0xFFu;
+    const uint32_t v = in ? (r < pa ? pv : lb) : 0u;
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t) v, seg, in ? r : -1, 0, 0);
+    o |= v << (8 * q);
   }
   return (o & 0xFFFFu) + (o >> 16);
 }
@@ -372,8 +373,10 @@ __device__ __forceinline__ uint32_t seg_copy_stage(uint8_t* out, uint64_t dst, u
     for (uint32_t q = 0; q < g; ++q) dup |= blk[q] == B;
     const bool pass1 = B >= D16 && B < E16 && inside16((int) ((int64_t) B - (int64_t) dst));
     const uint64_t A = B + 4ull * (lane & 3u);
-    if (size != 0 && !dup && !pass1 && A + 4 > dst && A < E)
-      sum += seg_dword_bytes(out, A, dst, sz, pa, pb, tag, st_b, a, b);
+    const bool on = size != 0 && !dup && !pass1 && A + 4 > dst && A < E;
+    const __amdgpu_buffer_rsrc_t seg =
+        __builtin_amdgcn_make_buffer_rsrc(out + dst, (short) 0, (int) size, 0x00020000);
+    sum += seg_dword_select(seg, on, (int) ((int64_t) A - (int64_t) dst), sz, pa, pb, tag, st_b, a, b);
   }
   return sum;
 }
