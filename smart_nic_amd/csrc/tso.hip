@@ -347,22 +347,32 @@ __device__ __forceinline__ uint32_t seg_copy_stage(uint8_t* out, uint64_t dst, u
     return (r0 >= pb && r0 + 16 <= sz) || (r0 >= pa && r0 + 16 <= pb);
   };
   uint32_t sum = 0;
-  for (uint32_t j = lane; j < nblk; j += kWave) {
+  // a uniform trip count, and no branch per block: a block outside part A /
+  // part B (or past nblk) reads the stage's first dwords and stores at an
+  // out-of-range offset of the blocks' buffer resource, which the hardware
+  // drops; alignbyte by 0 is the low dword, so no select on the shift
+  const __amdgpu_buffer_rsrc_t blks =
+      __builtin_amdgcn_make_buffer_rsrc(out + D16, (short) 0, (int) (nblk * 16u), 0x00020000);
+  const uint32_t iters = (nblk + kWave - 1) / kWave;
+  for (uint32_t it = 0; it < iters; ++it) {
+    const uint32_t j = it * kWave + lane;
     const int r0 = (int) (D16 - dst) + 16 * (int) j;
     const bool inB = r0 >= pb && r0 + 16 <= sz;
     const bool inA = r0 >= pa && r0 + 16 <= pb;
-    if (inA || inB) {
-      const uint32_t src = inB ? b + (uint32_t) (r0 - pb) : a + (uint32_t) (r0 - pa);
-      const uint32_t k = src >> 2, sh = src & 3u;
-      const uint32_t w0 = st[k], w1 = st[k + 1], w2 = st[k + 2], w3 = st[k + 3], w4 = st[k + 4];
-      u32x4 o;
-      o.x = sh ? __builtin_amdgcn_alignbyte(w1, w0, sh) : w0;
-      o.y = sh ? __builtin_amdgcn_alignbyte(w2, w1, sh) : w1;
-      o.z = sh ? __builtin_amdgcn_alignbyte(w3, w2, sh) : w2;
-      o.w = sh ? __builtin_amdgcn_alignbyte(w4, w3, sh) : w3;
-      __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out + D16 + 16ull * j));  // nt: as the f1 delivery
-      sum = add_halves(o.w, add_halves(o.z, add_halves(o.y, add_halves(o.x, sum))));
-    }
+    const uint32_t okm = -(uint32_t) ((inA || inB) && j < nblk);  // all ones for a block to write
+    // (masks, not selects: the compiler turned the selects into branches)
+    const uint32_t srcA = a + (uint32_t) (r0 - pa), srcB = b + (uint32_t) (r0 - pb);
+    const uint32_t src = (srcA ^ ((srcA ^ srcB) & -(uint32_t) inB)) & okm;
+    const uint32_t k = src >> 2, sh = src & 3u;
+    const uint32_t w0 = st[k], w1 = st[k + 1], w2 = st[k + 2], w3 = st[k + 3], w4 = st[k + 4];
+    u32x4 o;
+    o.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    o.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    o.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+    o.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+    __builtin_amdgcn_raw_buffer_store_b128(o, blks, (int) ((16u * j) | ~okm), 0, 2);  // nt: as the f1 delivery
+    const uint32_t s4 = add_halves(o.w, add_halves(o.z, add_halves(o.y, add_halves(o.x, 0u))));
+    sum += s4 & okm;
   }
   if (lane < 16u) {
     const uint64_t blk[4] = {dst & ~15ull, (dst + (uint64_t) pa) & ~15ull, (dst + (uint64_t) pb) & ~15ull,
