@@ -391,12 +391,71 @@ __device__ __forceinline__ uint32_t seg_copy_stage(uint8_t* out, uint64_t dst, u
   return sum;
 }
 
+// A segment whose prefix and part A together fit 64 B is first made one
+// contiguous run in the stage: [prefix | part A] is written right before its
+// part B (over bytes of the previous segment's payload, already stored, or —
+// for the first segment — A over itself and the prefix into the pad before
+// the frame), so the copy has one source and edges only at the segment's
+// ends (seg_copy_one).  The pad: 64 B before the stage.
+constexpr uint32_t kSegPadChunks = 4;
+
+// Segment bytes out[dst, +size) = stage[s0, +size), one source: pass 1 as in
+// seg_copy_stage over the 16-B blocks inside the segment, pass 2 the (at most
+// two) partial blocks at its ends, byte-selected as in seg_dword_select.
+__device__ __forceinline__ uint32_t seg_copy_one(uint8_t* out, uint64_t dst, uint32_t size, const uint8_t* st_b,
+                                                 int s0, uint32_t lane) {
+  const uint32_t* st = reinterpret_cast<const uint32_t*>(st_b);
+  const uint64_t E = dst + size;
+  const uint64_t D16 = (dst + 15) & ~15ull, E16 = E & ~15ull;
+  const uint32_t nblk = E16 > D16 ? (uint32_t) ((E16 - D16) >> 4) : 0u;
+  const __amdgpu_buffer_rsrc_t blks =
+      __builtin_amdgcn_make_buffer_rsrc(out + D16, (short) 0, (int) (nblk * 16u), 0x00020000);
+  const uint32_t iters = (nblk + kWave - 1) / kWave;
+  const uint32_t base = (uint32_t) (s0 + (int) (D16 - dst));  // stage byte of block 0
+  uint32_t sum = 0;
+  for (uint32_t it = 0; it < iters; ++it) {
+    const uint32_t j = it * kWave + lane;
+    const uint32_t okm = -(uint32_t) (j < nblk);
+    const uint32_t src = (base + 16u * j) & okm;
+    const uint32_t k = src >> 2, sh = src & 3u;
+    const uint32_t w0 = st[k], w1 = st[k + 1], w2 = st[k + 2], w3 = st[k + 3], w4 = st[k + 4];
+    u32x4 o;
+    o.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    o.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    o.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+    o.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+    __builtin_amdgcn_raw_buffer_store_b128(o, blks, (int) ((16u * j) | ~okm), 0, 2);  // nt: as the f1 delivery
+    sum += add_halves(o.w, add_halves(o.z, add_halves(o.y, add_halves(o.x, 0u)))) & okm;
+  }
+  if (lane < 8u) {  // the first and the last block, when partial: 4 dwords each
+    const uint64_t B = (lane < 4u ? dst : E - 1) & ~15ull;
+    const bool dup = lane >= 4u && B == (dst & ~15ull);
+    const bool full = B >= D16 && B < E16;
+    const uint64_t A = B + 4ull * (lane & 3u);
+    const bool on = size != 0 && !dup && !full && A + 4 > dst && A < E;
+    const __amdgpu_buffer_rsrc_t seg = __builtin_amdgcn_make_buffer_rsrc(out + dst, (short) 0, (int) size, 0x00020000);
+    const int r0 = (int) ((int64_t) A - (int64_t) dst);
+    uint32_t o = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = r0 + q;
+      const bool in = on && r >= 0 && r < (int) size;
+      const uint32_t v = in ? (uint32_t) st_b[s0 + r] : 0u;
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t) v, seg, in ? r : -1, 0, 0);
+      o |= v << (8 * q);
+    }
+    sum += (o & 0xFFFFu) + (o >> 16);
+  }
+  return sum;
+}
+
 __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
-  __shared__ uint4 stage_s[kWavesPerBlock][kSegStageChunks + 1];  // +1: stage_u32's second dword
+  // +1: stage_u32's second dword; the pad before it: seg_copy_one's prefixes
+  __shared__ uint4 stage_s[kWavesPerBlock][kSegPadChunks + kSegStageChunks + 1];
   const int w = __builtin_amdgcn_readfirstlane((int) (threadIdx.x / kWave));
   const uint32_t lane = lane_id();
   const uint64_t nwaves = (uint64_t) gridDim.x * kWavesPerBlock;
-  uint4* stage = stage_s[w];
+  uint4* stage = stage_s[w] + kSegPadChunks;
   // The wave's frames are f0 + t * nwaves.  Their parameters are fetched 64 at
   // a time, one frame per lane, and broadcast with readlane: a per-frame
   // global load would make hipcc wait on vmcnt(0) — i.e. for the previous
@@ -484,8 +543,37 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
       uint32_t sum = 0;
       const uint64_t pl = prefix ? 4 : 0;
       if (staged) {
-        sum = seg_copy_stage(P.out, dst, (uint32_t) size, (uint32_t) pl, tag, reinterpret_cast<const uint8_t*>(stage),
-                             (uint32_t) (src_a - a0), (uint32_t) len_a, (uint32_t) (src_b - a0), lane);
+        // stage bytes indexed from the pad's start, so no index is negative
+        uint8_t* st_b = reinterpret_cast<uint8_t*>(stage - kSegPadChunks);
+        const int a = (int) (src_a - a0 + 16u * kSegPadChunks), b = (int) (src_b - a0 + 16u * kSegPadChunks);
+        const int hb = (int) (pl + len_a);
+        // [prefix | A] before B: the first segment's B follows A; a later
+        // one's run must not reach back into A
+        const bool one = hb <= 64 && (k == 0 ? b == a + (int) len_a : b - hb >= a + (int) len_a);
+        if (one) {
+          if (lane < 16u) {
+            const uint32_t pfx = 0x81u | (((tag >> 8) & 0xFFu) << 16) | ((tag & 0xFFu) << 24);
+            uint32_t v4[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // read every byte first: the first segment writes A over itself
+              const int i = (int) (4u * lane) + q;
+              const uint32_t lb = st_b[a + (i < hb ? i : 0) - (int) pl];
+              v4[q] = i < (int) pl ? (pfx >> (8 * i)) & 0xFFu : lb;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int i = (int) (4u * lane) + q;
+              if (i < hb) st_b[b - hb + i] = (uint8_t) v4[q];
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          sum = seg_copy_one(P.out, dst, (uint32_t) size, st_b, b - hb, lane);
+        } else {
+          sum = seg_copy_stage(P.out, dst, (uint32_t) size, (uint32_t) pl, tag, st_b, (uint32_t) a, (uint32_t) len_a,
+                               (uint32_t) b, lane);
+        }
       } else {
         if (lane < pl) {
           const uint32_t b = lane == 0 ? 0x81u : (lane == 1 ? 0x00u : (lane == 2 ? (tag >> 8) : (tag & 0xFFu)));
