@@ -558,12 +558,14 @@ __global__ __launch_bounds__(kBlock) void tso_segment_kernel(TsoSegParams P) {
             for (int q = 0; q < 4; ++q) {  // read every byte first: the first segment writes A over itself
               const int i = (int) (4u * lane) + q;
               const uint32_t lb = st_b[a + (i < hb ? i : 0) - (int) pl];
-              v4[q] = i < (int) pl ? (pfx >> (8 * i)) & 0xFFu : lb;
+              v4[q] = i < (int) pl ? (pfx >> (8 * (i & 3))) & 0xFFu : lb;
             }
+            // bytes past the blob go to byte 0 of the pad (never read: a
+            // prefix reaches back at most 4 bytes before the frame, at >= 60)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int i = (int) (4u * lane) + q;
-              if (i < hb) st_b[b - hb + i] = (uint8_t) v4[q];
+              st_b[i < hb ? b - hb + i : 0] = (uint8_t) v4[q];
             }
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
