@@ -471,7 +471,7 @@ def main():
                     help="take the multi-rank path (RCCL init, key/table broadcast, barriers, max-reduce) even at "
                          "world size 1, to exercise it on a one-GPU box")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r06w_pmc_c2.json"))
-    ap.add_argument("--rows-prof-json", default=os.path.join(ROOT, "profiles", "r06y_rows_prof.json"))
+    ap.add_argument("--rows-prof-json", default=os.path.join(ROOT, "profiles", "r06x_rows_prof.json"))
     ap.add_argument("--dry-run", action="store_true",
                     help="run the rank machinery on gloo/CPU without a GPU or packets (launcher test)")
     args = ap.parse_args()
