@@ -646,6 +646,60 @@ def test_tso_segment_random_vs_oracle():
         assert oc[g: g + max(k, 0)].tolist() == cs
 
 
+def test_tso_segment_contiguous_run_boundaries():
+    """The kernel's one-source path (a segment whose VLAN prefix plus header fit
+    64 B is made one contiguous run in its LDS stage) at its edges: prefix +
+    header of 63 / 64 / 65 / 68 B (the last two take the two-part copy), mss
+    just above, at and below the blob (a later segment's run must not reach
+    back into the header), frames starting at every offset 0..15 in their 16-B
+    chunk (a first segment's prefix lands before the frame), strip / insert /
+    both / neither, slot strides 1506 (segment ends on no 16-B boundary), 1536
+    and 1531, random slot fill; every segment vs the oracle, tails untouched."""
+    rng = np.random.default_rng(64)
+    cases = []
+    for hb_target in (63, 64, 65, 68):
+        for mode in (sna.SEG_VLAN_INSERT, sna.SEG_VLAN_STRIP | sna.SEG_VLAN_PRESENT,
+                     sna.SEG_VLAN_INSERT | sna.SEG_VLAN_STRIP, 0):
+            pl = 4 if mode == sna.SEG_VLAN_INSERT else 0
+            H = hb_target - pl
+            for mss in (hb_target + 1, hb_target, hb_target - 1, 200, 1448):
+                for fo in (0, 1, 3, 4, 15):
+                    L = int(min(9000, H + 3 * mss + int(rng.integers(0, mss))))
+                    cases.append((fo, L, H, mss, sna.SEG_TSO | mode | int(rng.integers(0, 65536))))
+    n = len(cases)
+    offs = np.zeros(n, np.int64)
+    pos = 0
+    for i, (fo, L, H, mss, fl) in enumerate(cases):
+        pos = (pos + 15) // 16 * 16 + fo
+        offs[i] = pos
+        pos += L
+    frames = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    lens = np.array([c[1] for c in cases], np.int64)
+    hdr = np.array([c[2] for c in cases], np.int64)
+    mss = np.array([c[3] for c in cases], np.int64)
+    fl = np.array([c[4] for c in cases], np.int64)
+    segs_seen = 0
+    for stride, fill_seed in ((1506, 9), (1536, None), (1531, 11)):
+        s_mss = np.minimum(mss, stride - 80)  # every segment fits its slot
+        cnt, base, out, ol, oc = gpu_tso_segment(frames, sna.desc_pack(offs, lens), hdr, s_mss, fl, stride, fill_seed)
+        fill = (np.zeros(out.size, np.uint8) if fill_seed is None
+                else np.random.default_rng(fill_seed).integers(0, 256, out.size, dtype=np.uint8))
+        for i in range(n):
+            k, segs, cs = po.tso_segment(frames[offs[i]: offs[i] + lens[i]].tobytes(), int(hdr[i]), int(s_mss[i]),
+                                         int(fl[i]), stride)
+            assert max(k, 0) == cnt[i], (stride, i, k, int(cnt[i]))
+            g = int(base[i])
+            for j in range(max(k, 0)):
+                assert ol[g + j] == len(segs[j])
+                slot = out[(g + j) * stride: (g + j + 1) * stride]
+                assert slot[: len(segs[j])].tobytes() == segs[j], (stride, i, j)
+                assert np.array_equal(slot[len(segs[j]):],
+                                      fill[(g + j) * stride + len(segs[j]): (g + j + 1) * stride]), (stride, i, j)
+            assert oc[g: g + max(k, 0)].tolist() == cs
+            segs_seen += max(k, 0)
+    assert segs_seen > 3 * n
+
+
 @pytest.mark.parametrize("stride,fill_seed", [(1600, None), (1531, 5)])
 def test_tso_segment_several_frames_per_wave(stride, fill_seed):
     """16384 frames, so each of the kernel's waves (at most 4096) walks about
